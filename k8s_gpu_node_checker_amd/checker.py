@@ -1,0 +1,233 @@
+"""Check orchestration: scan -> MI355X health gate -> Slack -> report.
+
+Reference ``one_shot`` (``check-gpu-node.py:252-293``) runs strictly in
+sequence: LIST, then Slack (including up to 3 x ``retry_delay`` of sleeps),
+then output.  Here the Slack POST runs on a worker thread while the report is
+rendered, and the report is written in one ``write`` once Slack has finished,
+so the stream order of Appendix A / SURVEY §5.1 is unchanged (the Slack
+success line still precedes the summary on stdout).
+
+:func:`run_check` is the library entry point (used by the CLI, the bench and
+the node agent's self-test); :func:`one_shot` adds the printing.
+"""
+
+from __future__ import annotations
+
+import sys
+import threading
+from typing import Any, Callable, Dict, List, Optional, TextIO
+
+from . import report
+from .kube.client import KubeClient
+from .kube.config import ClusterConnection
+from .models import health as H
+from .models.node import ScanResult, primary_gpu_count
+from .models.resources import GPU_RESOURCE_KEYS, PRIMARY_GPU_KEY
+from .utils.timing import NullTracer, Tracer
+
+
+class CheckOptions:
+    """All knobs of one check; defaults reproduce the reference exactly."""
+
+    def __init__(self, **kw: Any):
+        self.json = False
+        self.json_extended = False
+        self.slack_webhook: Optional[str] = None
+        self.slack_username = "k8s-gpu-checker"
+        self.slack_only_on_error = False
+        self.slack_retry_count = 3
+        self.slack_retry_delay = 30
+        self.slack_retry_policy = "backoff"
+        self.kube_timeout = 30.0
+        self.kube_retries = 2
+        self.page_size = 500
+        self.label_selector: Optional[str] = None
+        self.resource_version: Optional[str] = None
+        self.gpu_source = "capacity"
+        self.health_policy = "auto"
+        self.probe_max_age = 900.0
+        self.probe_unknown = "allow"
+        self.xgmi_links = H.XGMI_LINKS_EXPECTED
+        self.probe_endpoint: Optional[str] = None
+        self.probe_concurrency = 64
+        self.probe_timeout = 2.0
+        self.trace = False
+        self.slack_gate: Optional[Callable[["CheckResult"], bool]] = None
+        for k, v in kw.items():
+            if not hasattr(self, k):
+                raise TypeError(f"unknown check option {k!r}")
+            setattr(self, k, v)
+
+    @classmethod
+    def from_args(cls, args: Any) -> "CheckOptions":
+        o = cls()
+        for k in list(vars(o)):
+            if hasattr(args, k):
+                setattr(o, k, getattr(args, k))
+        return o
+
+    @property
+    def needs_extras(self) -> bool:
+        return self.health_policy != "off" or self.json_extended
+
+
+class CheckResult:
+    def __init__(self, scan: ScanResult, verdicts: List[Optional[H.Verdict]], tracer: Tracer):
+        self.scan = scan
+        self.verdicts = verdicts
+        self.tracer = tracer
+        self.slack_sent: Optional[bool] = None
+
+    @property
+    def gpu_nodes(self) -> List[Dict[str, Any]]:
+        return self.scan.gpu_nodes
+
+    @property
+    def ready_gpu_nodes(self) -> List[Dict[str, Any]]:
+        return self.scan.ready_gpu_nodes
+
+    @property
+    def exit_code(self) -> int:
+        return self.scan.exit_code()
+
+    def extended_fields(self) -> Dict[str, Any]:
+        nodes = []
+        for i, n in enumerate(self.scan.gpu_nodes):
+            ex = self.scan.extras[i] if i < len(self.scan.extras) else None
+            v = self.verdicts[i] if i < len(self.verdicts) else None
+            entry: Dict[str, Any] = {"name": n["name"], "ready": n["ready"]}
+            if ex is not None:
+                entry.update(ex.to_dict())
+            entry["health"] = v.to_dict() if v is not None else None
+            nodes.append(entry)
+        return {
+            "mi355x": {
+                "health_summary": H.summarize(self.verdicts) if self.verdicts else None,
+                "nodes": nodes,
+            },
+            "timings_ms": self.tracer.as_ms(),
+            "items_seen": self.scan.items_seen,
+        }
+
+
+def scan_cluster(cluster: ClusterConnection, opts: CheckOptions, tracer: Tracer) -> ScanResult:
+    client = KubeClient(cluster, timeout=opts.kube_timeout, retries=opts.kube_retries, tracer=tracer)
+    try:
+        with tracer.span("list"):
+            return client.scan_nodes(limit=opts.page_size, keys=GPU_RESOURCE_KEYS, gpu_source=opts.gpu_source,
+                                     want_extras=opts.needs_extras, label_selector=opts.label_selector,
+                                     resource_version=opts.resource_version)
+    finally:
+        client.close()
+
+
+def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer) -> List[Optional[H.Verdict]]:
+    """Evaluate MI355X probe reports and gate ``ready`` (no-op when no node carries one)."""
+    if opts.health_policy == "off" or not scan.gpu_nodes:
+        return []
+    with tracer.span("health"):
+        exp = H.HealthExpectations(xgmi_links=opts.xgmi_links, max_age_s=opts.probe_max_age)
+        reports: List[Optional[Dict[str, Any]]]
+        if opts.probe_endpoint:
+            from .parallel.fanout import fetch_probe_reports
+            reports = fetch_probe_reports(scan, opts.probe_endpoint, opts.probe_concurrency, opts.probe_timeout)
+        else:
+            reports = [H.parse_annotation(ex.health_annotation) for ex in scan.extras]
+        verdicts: List[Optional[H.Verdict]] = []
+        changed = False
+        unknown_ok = opts.probe_unknown == "allow"
+        for node, ex, rep in zip(scan.gpu_nodes, scan.extras, reports):
+            is_amd = PRIMARY_GPU_KEY in node["gpu_breakdown"] or PRIMARY_GPU_KEY in ex.allocatable
+            if rep is None and opts.health_policy != "require":
+                verdicts.append(None)
+                continue
+            v = H.evaluate_report(rep, primary_gpu_count(ex, opts.gpu_source), exp)
+            verdicts.append(v)
+            gated = H.gate_ready(ex.ready_condition, v, opts.health_policy, is_amd, unknown_ok)
+            if gated != node["ready"]:
+                node["ready"] = gated
+                changed = True
+        if changed:
+            scan.recompute_ready()
+        if not any(verdicts):
+            return []
+        return verdicts
+
+
+def run_check(cluster: ClusterConnection, opts: CheckOptions, tracer: Optional[Tracer] = None) -> CheckResult:
+    tracer = tracer or (Tracer() if (opts.trace or opts.json_extended) else NullTracer())
+    scan = scan_cluster(cluster, opts, tracer)
+    verdicts = apply_health(scan, opts, tracer)
+    return CheckResult(scan, verdicts, tracer)
+
+
+def _health_notes(result: CheckResult) -> Optional[List[Optional[str]]]:
+    if not result.verdicts:
+        return None
+    return [v.short() if v is not None else None for v in result.verdicts]
+
+
+def one_shot(cluster: ClusterConnection, opts: CheckOptions, out: Optional[TextIO] = None,
+             err: Optional[TextIO] = None, tracer: Optional[Tracer] = None) -> int:
+    """Reference ``one_shot`` (``:252-293``): prints the report, returns the exit code."""
+    return check_and_report(cluster, opts, out, err, tracer).exit_code
+
+
+def check_and_report(cluster: ClusterConnection, opts: CheckOptions, out: Optional[TextIO] = None,
+                     err: Optional[TextIO] = None, tracer: Optional[Tracer] = None) -> CheckResult:
+    from .notify import slack
+    out = out if out is not None else sys.stdout
+    err = err if err is not None else sys.stderr
+    result = run_check(cluster, opts, tracer)
+    tr = result.tracer
+    gpu_nodes, ready = result.gpu_nodes, result.ready_gpu_nodes
+
+    url = slack.get_slack_webhook_url(opts.slack_webhook)
+    worker: Optional[threading.Thread] = None
+    box: Dict[str, bool] = {}
+    if slack.should_send(url, opts.slack_only_on_error, len(ready)) and (
+            opts.slack_gate is None or opts.slack_gate(result)):
+        text = report.format_slack_message(gpu_nodes, ready, _health_notes(result))
+        delay = opts.slack_retry_delay
+        if delay < 0:
+            print(f"경고: --slack-retry-delay {delay} 는 음수이므로 0으로 처리합니다.", file=err)
+            delay = 0
+
+        def _send() -> None:
+            with tr.span("slack"):
+                box["ok"] = slack.send_slack_message(url, text, opts.slack_username, opts.slack_retry_count,
+                                                     delay, policy=opts.slack_retry_policy, err=err)
+        worker = threading.Thread(target=_send, name="slack", daemon=True)
+        worker.start()
+
+    json_mode = opts.json or opts.json_extended
+    with tr.span("render"):
+        if json_mode:
+            extra = None
+            if opts.json_extended:
+                tr.finish()
+                extra = result.extended_fields()
+            body = report.render_json(report.json_payload(gpu_nodes, ready, extra))
+        else:
+            body = report.render_text(gpu_nodes, ready)
+
+    prefix = ""
+    if worker is not None:
+        worker.join()
+        result.slack_sent = box.get("ok", False)
+        if not json_mode:
+            if result.slack_sent:
+                prefix = report.SLACK_SENT + "\n"
+            else:
+                print(report.SLACK_FAILED, file=err)
+    out.write(prefix + body)
+    out.flush()
+    if opts.trace:
+        tr.finish()
+        print(f"[trace] {tr.format()} backend={_backend()}", file=err)
+    return result
+
+
+def _backend() -> str:
+    from .ops import fastpath
+    return fastpath.backend()

@@ -1,0 +1,157 @@
+"""Command line: ``check-gpu-node``.
+
+``--help`` is byte-identical to the reference: the
+reference's seven flags, the same Korean help strings, the same ``슬랙 알림``
+group.  The MI355X extensions are real flags but hidden from ``--help``;
+``--help-all`` lists them.
+
+Exit codes (reference ``:289-293``, ``:319-327``): 0 = at least one Ready GPU
+node, 3 = GPU nodes but none Ready, 2 = no GPU nodes (and argparse usage
+errors, as in the reference), 1 = any exception (kubeconfig, API, transport).
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+from typing import List, Optional
+
+HIDE = argparse.SUPPRESS
+
+
+def build_parser(show_all: bool = False, prog: Optional[str] = None) -> argparse.ArgumentParser:
+    if prog is None:
+        base = os.path.basename(sys.argv[0]) if sys.argv and sys.argv[0] else "check-gpu-node"
+        prog = "check-gpu-node" if base in ("__main__.py", "-c", "") else base
+    p = argparse.ArgumentParser(prog=prog, description="Kubernetes GPU 노드 점검 스크립트")
+    p.add_argument("--kubeconfig", help="kubeconfig 경로 직접 지정")
+    p.add_argument("--json", action="store_true", help="JSON 형태로만 출력(머신 판독용)")
+
+    g = p.add_argument_group("슬랙 알림", "슬랙으로 메시지를 전송하는 옵션들")
+    g.add_argument("--slack-webhook", help="슬랙 웹훅 URL (환경변수 SLACK_WEBHOOK_URL로도 설정 가능)")
+    g.add_argument("--slack-username", default="k8s-gpu-checker", help="슬랙 봇 사용자명 (기본: k8s-gpu-checker)")
+    g.add_argument("--slack-only-on-error", action="store_true",
+                   help="GPU 노드가 없거나 Ready 상태가 아닐 때만 슬랙 메시지 전송")
+    g.add_argument("--slack-retry-count", type=int, default=3, help="슬랙 메시지 전송 실패시 최대 재시도 횟수 (기본: 3)")
+    g.add_argument("--slack-retry-delay", type=int, default=30, help="슬랙 메시지 재시도 간격(초) (기본: 30)")
+
+    def h(text: str) -> str:
+        return text if show_all else HIDE
+
+    x = p.add_argument_group("MI355X / 확장 옵션", "reference 에 없는 옵션들 (--help-all 에서만 표시)") if show_all else p
+    x.add_argument("--help-all", action="store_true", help=h("모든 옵션(확장 포함) 도움말"))
+    g.add_argument("--slack-retry-policy", choices=("backoff", "reference"), default="backoff",
+                   help=h("5xx/429 재시도 정책: backoff(지수 백오프, 기본) | reference(즉시 재시도)"))
+    g.add_argument("--slack-on-change", action="store_true",
+                   help=h("--state-file 과 함께: 상태가 바뀌었을 때만 전송 (복구 알림 포함)"))
+    x.add_argument("--context", help=h("kubeconfig context (기본: current-context)"))
+    x.add_argument("--in-cluster", action="store_true", help=h("Pod ServiceAccount 로 접속"))
+    x.add_argument("--kube-timeout", type=float, default=30.0, help=h("kube-apiserver 요청 타임아웃(초) (기본: 30)"))
+    x.add_argument("--kube-retries", type=int, default=2, help=h("LIST 재시도 횟수 (429/5xx/연결 오류, 기본: 2)"))
+    x.add_argument("--page-size", type=int, default=500, help=h("LIST 페이지 크기 (0 = 한 번에, 기본: 500)"))
+    x.add_argument("--label-selector", help=h("노드 labelSelector"))
+    x.add_argument("--resource-version", help=h("LIST resourceVersion (예: 0 = watch cache)"))
+    x.add_argument("--gpu-source", choices=("capacity", "allocatable"), default="capacity",
+                   help=h("GPU 수를 읽을 status 필드 (기본: capacity = reference)"))
+    x.add_argument("--health-policy", choices=("off", "auto", "require"), default="auto",
+                   help=h("MI355X 헬스 게이트: off | auto(리포트가 있으면 반영, 기본) | require"))
+    x.add_argument("--probe-max-age", type=float, default=900.0, help=h("프로브 리포트 최대 나이(초) (기본: 900)"))
+    x.add_argument("--probe-unknown", choices=("allow", "deny"), default="allow",
+                   help=h("프로브 상태 unknown(만료/실패) 노드 처리 (기본: allow)"))
+    x.add_argument("--xgmi-links", type=int, default=7, help=h("GPU 당 기대 xGMI 링크 수 (0 = 검사 안 함, 기본: 7)"))
+    x.add_argument("--probe-endpoint", help=h("노드별 프로브 URL 템플릿, 예: http://{ip}:9464/probe"))
+    x.add_argument("--probe-concurrency", type=int, default=64, help=h("프로브 fan-out 동시성 (기본: 64)"))
+    x.add_argument("--probe-timeout", type=float, default=2.0, help=h("노드별 프로브 타임아웃(초) (기본: 2)"))
+    x.add_argument("--mi355x", action="store_true",
+                   help=h("MI355X 프리셋: --gpu-source allocatable --health-policy require"))
+    x.add_argument("--json-extended", action="store_true", help=h("JSON 에 MI355X 헬스/타이밍 필드 추가"))
+    x.add_argument("--trace", action="store_true", help=h("단계별 소요 시간을 stderr 로 출력"))
+    x.add_argument("--prometheus-textfile", help=h("node-exporter textfile 메트릭 경로"))
+    x.add_argument("--state-file", help=h("직전 결과 저장 파일 (알림 중복 제거)"))
+    x.add_argument("--watch", type=float, default=0.0, help=h("N초마다 반복 점검 (0 = 한 번, 기본)"))
+    return p
+
+
+def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
+    argv = sys.argv[1:] if argv is None else argv
+    if "--help-all" in argv:
+        build_parser(show_all=True).print_help()
+        sys.exit(0)
+    args = build_parser().parse_args(argv)
+    if args.mi355x:
+        args.gpu_source = "allocatable"
+        args.health_policy = "require"
+    if args.json_extended:
+        args.json = True
+    return args
+
+
+def _load_cluster(args: argparse.Namespace):
+    from .kube.config import incluster_connection, load_kube_config
+    from .kube.errors import ConfigException
+    if args.in_cluster:
+        conn = incluster_connection()
+        if conn is None:
+            raise ConfigException("Service host/port is not set.")
+        return conn
+    return load_kube_config(args.kubeconfig, args.context)
+
+
+def _run_once(args: argparse.Namespace) -> int:
+    """Reference ``main`` body (``:316-327``) for one iteration."""
+    import json
+    try:
+        from .checker import CheckOptions, check_and_report
+        from .utils import statefile
+        cluster = _load_cluster(args)
+        opts = CheckOptions.from_args(args)
+        prev = statefile.load(args.state_file) if args.state_file else None
+        if args.state_file and args.slack_on_change:
+            opts.slack_webhook = statefile.gate_webhook(prev, opts, cluster)
+        result = check_and_report(cluster, opts)
+        if args.state_file:
+            statefile.save(args.state_file, result, prev)
+        if args.prometheus_textfile:
+            from .utils.prom import write_textfile
+            write_textfile(args.prometheus_textfile, result)
+        return result.exit_code
+    except Exception as e:
+        if getattr(args, "json", False):
+            print(json.dumps({"error": str(e)}, ensure_ascii=False))
+        else:
+            import traceback
+            print(f"에러: {e}", file=sys.stderr)
+            traceback.print_exc()
+        if args.prometheus_textfile:
+            try:
+                from .utils.prom import write_error_textfile
+                write_error_textfile(args.prometheus_textfile, str(e))
+            except Exception:
+                pass
+        return 1
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    args = parse_args(argv)
+    if args.watch and args.watch > 0:
+        import time
+        code = 0
+        while True:
+            started = time.monotonic()
+            code = _run_once(args)
+            sys.stdout.flush()
+            time.sleep(max(0.0, args.watch - (time.monotonic() - started)))
+        return code  # pragma: no cover
+    return _run_once(args)
+
+
+def entry() -> None:
+    """Console-script entry: load ``.env`` (reference ``:331``) then exit with ``main()``."""
+    from .utils.dotenv import load_dotenv
+    load_dotenv()
+    sys.exit(main())
+
+
+if __name__ == "__main__":
+    entry()

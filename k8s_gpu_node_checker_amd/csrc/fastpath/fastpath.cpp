@@ -1,0 +1,1020 @@
+// Native CPU hot path of the checker (CPython extension `_fastpath`).
+//
+// scan_nodelist(buf, result, keys, use_allocatable, want_extras, health_key, NodeExtras)
+//   One pass over a kube-apiserver NodeList JSON page.  Only the fields the
+//   checker consumes are materialised as Python objects (metadata.name,
+//   metadata.labels, one annotation, spec.taints, spec.unschedulable,
+//   status.capacity / status.allocatable GPU keys, status.conditions Ready);
+//   everything else (images, managedFields, nodeInfo, addresses, ...) is
+//   skipped at byte level.  Semantics are those of the pure-Python path
+//   (models/node.py), which reproduces reference check-gpu-node.py:172-226:
+//   capacity values go through str() and Python int() (zeros kept, "1k"
+//   dropped), Ready = a condition with type "Ready" and status "True",
+//   duplicate JSON keys: last one wins (as json.loads).  Any shape this code
+//   does not model raises FallbackError *before* `result` is touched, and
+//   the caller re-scans the page with json.loads.
+//
+// dumps_indent2(obj)
+//   Byte-identical json.dumps(obj, ensure_ascii=False, indent=2) for
+//   dict/list/tuple/str/int/bool/None/float trees.  CPython's indent encoder
+//   is the pure-Python _make_iterencode, the dominant render cost at 1000
+//   nodes (reference check-gpu-node.py:279).
+//
+// Known, documented divergence: bytes inside *skipped* string values are not
+// UTF-8-validated (json.loads would reject invalid UTF-8 anywhere).
+
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+PyObject* g_fallback = nullptr;  // FallbackError
+PyObject *k_name, *k_ready, *k_gpus, *k_breakdown, *k_labels, *k_taints, *k_key, *k_value, *k_effect;
+PyObject *a_gpu_nodes, *a_ready_gpu_nodes, *a_extras, *a_items_seen;
+
+struct Fallback {
+  const char* why;
+};
+
+// ---------------------------------------------------------------- scanning --
+struct Cursor {
+  const char* p;
+  const char* end;
+
+  void ws() {
+    while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  }
+  char peek() {
+    ws();
+    if (p >= end) throw Fallback{"unexpected end"};
+    return *p;
+  }
+  void expect(char c) {
+    if (peek() != c) throw Fallback{"unexpected character"};
+    ++p;
+  }
+  bool consume(char c) {
+    if (peek() == c) {
+      ++p;
+      return true;
+    }
+    return false;
+  }
+};
+
+// A raw JSON string token: [b, e) excludes the quotes; `esc` if it has backslashes.
+struct RawStr {
+  const char* b;
+  const char* e;
+  bool esc;
+};
+
+RawStr read_raw_string(Cursor& c) {
+  c.expect('"');
+  const char* b = c.p;
+  bool esc = false;
+  const char* p = c.p;
+  const char* end = c.end;
+  for (;;) {
+    const void* q = memchr(p, '"', end - p);
+    if (!q) throw Fallback{"unterminated string"};
+    const char* qq = static_cast<const char*>(q);
+    // count preceding backslashes to see whether the quote is escaped
+    const char* s = qq;
+    while (s > b && s[-1] == '\\') --s;
+    if (s != qq) esc = true;
+    if (((qq - s) & 1) == 0) {
+      if (!esc && memchr(b, '\\', qq - b)) esc = true;
+      c.p = qq + 1;
+      return RawStr{b, qq, esc};
+    }
+    p = qq + 1;
+  }
+}
+
+void append_utf8(std::string& out, uint32_t cp) {
+  if (cp < 0x80) {
+    out.push_back(static_cast<char>(cp));
+  } else if (cp < 0x800) {
+    out.push_back(static_cast<char>(0xC0 | (cp >> 6)));
+    out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else if (cp < 0x10000) {
+    out.push_back(static_cast<char>(0xE0 | (cp >> 12)));
+    out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else {
+    out.push_back(static_cast<char>(0xF0 | (cp >> 18)));
+    out.push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+    out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  }
+}
+
+int hexval(char ch) {
+  if (ch >= '0' && ch <= '9') return ch - '0';
+  if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+  if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
+  return -1;
+}
+
+uint32_t read_u4(const char*& p, const char* e) {
+  if (e - p < 4) throw Fallback{"short \\u escape"};
+  uint32_t v = 0;
+  for (int i = 0; i < 4; ++i) {
+    int h = hexval(p[i]);
+    if (h < 0) throw Fallback{"bad \\u escape"};
+    v = (v << 4) | static_cast<uint32_t>(h);
+  }
+  p += 4;
+  return v;
+}
+
+// Decoded UTF-8 bytes of a JSON string token.
+void decode_into(const RawStr& s, std::string& out) {
+  out.clear();
+  if (!s.esc) {
+    out.assign(s.b, s.e);
+    return;
+  }
+  const char* p = s.b;
+  while (p < s.e) {
+    char ch = *p++;
+    if (ch != '\\') {
+      out.push_back(ch);
+      continue;
+    }
+    if (p >= s.e) throw Fallback{"dangling escape"};
+    char x = *p++;
+    switch (x) {
+      case '"': out.push_back('"'); break;
+      case '\\': out.push_back('\\'); break;
+      case '/': out.push_back('/'); break;
+      case 'b': out.push_back('\b'); break;
+      case 'f': out.push_back('\f'); break;
+      case 'n': out.push_back('\n'); break;
+      case 'r': out.push_back('\r'); break;
+      case 't': out.push_back('\t'); break;
+      case 'u': {
+        uint32_t cp = read_u4(p, s.e);
+        if (cp >= 0xD800 && cp <= 0xDBFF) {
+          if (s.e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+            const char* q = p + 2;
+            uint32_t lo = read_u4(q, s.e);
+            if (lo >= 0xDC00 && lo <= 0xDFFF) {
+              p = q;
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            } else {
+              throw Fallback{"lone surrogate"};
+            }
+          } else {
+            throw Fallback{"lone surrogate"};
+          }
+        } else if (cp >= 0xDC00 && cp <= 0xDFFF) {
+          throw Fallback{"lone surrogate"};
+        }
+        append_utf8(out, cp);
+        break;
+      }
+      default:
+        throw Fallback{"bad escape"};
+    }
+  }
+}
+
+bool raw_equals(const RawStr& s, const char* lit, std::string& scratch) {
+  size_t n = strlen(lit);
+  if (!s.esc) return static_cast<size_t>(s.e - s.b) == n && memcmp(s.b, lit, n) == 0;
+  decode_into(s, scratch);
+  return scratch.size() == n && memcmp(scratch.data(), lit, n) == 0;
+}
+
+PyObject* make_str(const RawStr& s, std::string& scratch) {
+  PyObject* o;
+  if (!s.esc) {
+    o = PyUnicode_DecodeUTF8(s.b, s.e - s.b, "strict");
+  } else {
+    decode_into(s, scratch);
+    o = PyUnicode_DecodeUTF8(scratch.data(), static_cast<Py_ssize_t>(scratch.size()), "strict");
+  }
+  if (!o) {
+    PyErr_Clear();
+    throw Fallback{"invalid utf-8"};
+  }
+  return o;
+}
+
+void skip_value(Cursor& c);
+
+void skip_number(Cursor& c) {
+  const char* p = c.p;
+  const char* e = c.end;
+  if (p < e && *p == '-') ++p;
+  if (e - p >= 8 && memcmp(p, "Infinity", 8) == 0) {
+    c.p = p + 8;
+    return;
+  }
+  const char* start = p;
+  while (p < e && ((*p >= '0' && *p <= '9') || *p == '.' || *p == 'e' || *p == 'E' || *p == '+' || *p == '-')) ++p;
+  if (p == start) throw Fallback{"bad number"};
+  c.p = p;
+}
+
+void skip_literal(Cursor& c) {
+  const char* p = c.p;
+  size_t left = static_cast<size_t>(c.end - p);
+  if (left >= 4 && (memcmp(p, "true", 4) == 0 || memcmp(p, "null", 4) == 0)) {
+    c.p += 4;
+  } else if (left >= 5 && memcmp(p, "false", 5) == 0) {
+    c.p += 5;
+  } else if (left >= 3 && memcmp(p, "NaN", 3) == 0) {
+    c.p += 3;
+  } else {
+    throw Fallback{"bad literal"};
+  }
+}
+
+// Skip a whole object/array with a flat bracket counter (string-aware).
+void skip_container(Cursor& c) {
+  const char* p = c.p;
+  const char* e = c.end;
+  int depth = 0;
+  while (p < e) {
+    char ch = *p;
+    if (ch == '"') {
+      Cursor t{p, e};
+      read_raw_string(t);
+      p = t.p;
+      continue;
+    }
+    if (ch == '{' || ch == '[') {
+      ++depth;
+    } else if (ch == '}' || ch == ']') {
+      if (--depth == 0) {
+        c.p = p + 1;
+        return;
+      }
+    }
+    ++p;
+  }
+  throw Fallback{"unterminated container"};
+}
+
+void skip_value(Cursor& c) {
+  char ch = c.peek();
+  if (ch == '"') {
+    read_raw_string(c);
+  } else if (ch == '{' || ch == '[') {
+    skip_container(c);
+  } else if (ch == '-' || (ch >= '0' && ch <= '9')) {
+    skip_number(c);
+  } else {
+    skip_literal(c);
+  }
+}
+
+// Iterate the members of an object; `fn(key, cursor)` must consume the value.
+template <class F>
+void for_members(Cursor& c, F&& fn) {
+  c.expect('{');
+  if (c.consume('}')) return;
+  for (;;) {
+    if (c.peek() != '"') throw Fallback{"expected key"};
+    RawStr k = read_raw_string(c);
+    c.expect(':');
+    fn(k, c);
+    if (c.consume(',')) continue;
+    c.expect('}');
+    return;
+  }
+}
+
+template <class F>
+void for_elements(Cursor& c, F&& fn) {
+  c.expect('[');
+  if (c.consume(']')) return;
+  for (;;) {
+    fn(c);
+    if (c.consume(',')) continue;
+    c.expect(']');
+    return;
+  }
+}
+
+bool is_null(Cursor& c) {
+  if (c.peek() == 'n') {
+    skip_literal(c);
+    return true;
+  }
+  return false;
+}
+
+// RAII holder for an owned PyObject*.
+struct Ref {
+  PyObject* o = nullptr;
+  Ref() = default;
+  explicit Ref(PyObject* x) : o(x) {}
+  Ref(const Ref&) = delete;
+  Ref& operator=(const Ref&) = delete;
+  Ref(Ref&& r) noexcept : o(r.o) { r.o = nullptr; }
+  Ref& operator=(Ref&& r) noexcept {
+    if (this != &r) {
+      Py_XDECREF(o);
+      o = r.o;
+      r.o = nullptr;
+    }
+    return *this;
+  }
+  ~Ref() { Py_XDECREF(o); }
+  void reset(PyObject* x) {
+    Py_XDECREF(o);
+    o = x;
+  }
+  PyObject* release() {
+    PyObject* x = o;
+    o = nullptr;
+    return x;
+  }
+};
+
+struct KeySpec {
+  std::vector<std::string> keys;  // registry order
+  std::vector<PyObject*> pykeys;  // borrowed from the keys tuple
+};
+
+// Value of a capacity entry -> (present, parsed ok, value) with str()+int() semantics.
+struct Qty {
+  bool set = false;   // key present with a non-null value (last one wins)
+  bool ok = false;    // int() succeeded
+  Ref value;          // PyLong
+};
+
+PyObject* parse_int_text(const char* b, size_t n, std::string& scratch, bool is_json_string) {
+  // Fast path: optional sign + ASCII digits, nothing else.
+  const char* p = b;
+  const char* e = b + n;
+  if (is_json_string) {
+    if (n == 0) return nullptr;  // "" -> skipped, handled by caller
+  }
+  const char* q = p;
+  if (q < e && (*q == '+' || *q == '-')) ++q;
+  bool simple = q < e && (e - q) <= 18;
+  for (const char* r = q; simple && r < e; ++r)
+    if (*r < '0' || *r > '9') simple = false;
+  if (simple) {
+    long long v = 0;
+    for (const char* r = q; r < e; ++r) v = v * 10 + (*r - '0');
+    if (*p == '-') v = -v;
+    return PyLong_FromLongLong(v);
+  }
+  // Exact Python int(str) semantics (whitespace, '_' separators, unicode digits).
+  scratch.assign(b, n);
+  PyObject* s = PyUnicode_DecodeUTF8(scratch.data(), static_cast<Py_ssize_t>(scratch.size()), "strict");
+  if (!s) {
+    PyErr_Clear();
+    throw Fallback{"invalid utf-8 in quantity"};
+  }
+  PyObject* v = PyLong_FromUnicodeObject(s, 10);
+  Py_DECREF(s);
+  if (!v) {
+    if (PyErr_ExceptionMatches(PyExc_ValueError)) {
+      PyErr_Clear();
+      return nullptr;  // dropped, as the reference's `except Exception: pass`
+    }
+    PyErr_Clear();
+    throw Fallback{"int() raised"};
+  }
+  return v;
+}
+
+void parse_quantity(Cursor& c, Qty& q, std::string& scratch) {
+  char ch = c.peek();
+  q.ok = false;
+  q.value.reset(nullptr);
+  if (ch == 'n') {  // null -> key treated as missing
+    skip_literal(c);
+    q.set = false;
+    return;
+  }
+  q.set = true;
+  if (ch == '"') {
+    RawStr s = read_raw_string(c);
+    std::string dec;
+    const char* b = s.b;
+    size_t n = static_cast<size_t>(s.e - s.b);
+    if (s.esc) {
+      decode_into(s, dec);
+      b = dec.data();
+      n = dec.size();
+    }
+    if (n == 0) {  // `if not val: continue`
+      q.set = false;
+      return;
+    }
+    PyObject* v = parse_int_text(b, n, scratch, true);
+    if (v) {
+      q.ok = true;
+      q.value.reset(v);
+    }
+    return;
+  }
+  if (ch == '-' || (ch >= '0' && ch <= '9')) {
+    const char* b = c.p;
+    skip_number(c);
+    size_t n = static_cast<size_t>(c.p - b);
+    bool integral = true;
+    for (size_t i = 0; i < n; ++i)
+      if (b[i] == '.' || b[i] == 'e' || b[i] == 'E' || b[i] == 'I') integral = false;
+    if (!integral) return;  // str(float) is never int()-parsable
+    PyObject* v = parse_int_text(b, n, scratch, false);
+    if (v) {
+      q.ok = true;
+      q.value.reset(v);
+    }
+    return;
+  }
+  skip_value(c);  // bools, objects, arrays: str() of them never parses as int
+}
+
+// capacity / allocatable object -> per-registry-key Qty
+void parse_resource_map(Cursor& c, const KeySpec& ks, std::vector<Qty>& out, std::string& scratch) {
+  for (auto& q : out) {
+    q.set = false;
+    q.ok = false;
+    q.value.reset(nullptr);
+  }
+  if (c.peek() != '{') {
+    skip_value(c);
+    return;
+  }
+  std::string kd;
+  for_members(c, [&](const RawStr& k, Cursor& cc) {
+    const char* kb = k.b;
+    size_t kn = static_cast<size_t>(k.e - k.b);
+    if (k.esc) {
+      decode_into(k, kd);
+      kb = kd.data();
+      kn = kd.size();
+    }
+    for (size_t i = 0; i < ks.keys.size(); ++i) {
+      if (ks.keys[i].size() == kn && memcmp(ks.keys[i].data(), kb, kn) == 0) {
+        parse_quantity(cc, out[i], scratch);
+        return;
+      }
+    }
+    skip_value(cc);
+  });
+}
+
+PyObject* breakdown_dict(const KeySpec& ks, const std::vector<Qty>& q, long long* total) {
+  PyObject* d = PyDict_New();
+  if (!d) throw Fallback{"oom"};
+  long long sum = 0;
+  bool overflow = false;
+  for (size_t i = 0; i < ks.keys.size(); ++i) {
+    if (q[i].set && q[i].ok) {
+      if (PyDict_SetItem(d, ks.pykeys[i], q[i].value.o) < 0) {
+        Py_DECREF(d);
+        throw Fallback{"dict"};
+      }
+      int of = 0;
+      long long v = PyLong_AsLongLongAndOverflow(q[i].value.o, &of);
+      if (of) overflow = true;
+      sum += v;
+    }
+  }
+  if (overflow) {
+    Py_DECREF(d);
+    throw Fallback{"huge quantity"};
+  }
+  if (total) *total = sum;
+  return d;
+}
+
+struct NodeScan {
+  bool meta_obj = false;     // metadata is a JSON object
+  Ref name;                  // str or None
+  Ref labels;                // dict (possibly empty) or null
+  Ref health;                // str or nullptr
+  Ref taints;                // list
+  bool unschedulable = false;
+  bool ready = false;
+  std::vector<Qty> cap, alloc;
+};
+
+void parse_labels(Cursor& c, NodeScan& ns, std::string& scratch) {
+  if (is_null(c)) {
+    ns.labels.reset(nullptr);
+    return;
+  }
+  if (c.peek() != '{') throw Fallback{"labels not an object"};
+  PyObject* d = PyDict_New();
+  if (!d) throw Fallback{"oom"};
+  Ref hold(d);
+  for_members(c, [&](const RawStr& k, Cursor& cc) {
+    Ref key(make_str(k, scratch));
+    if (cc.peek() != '"') throw Fallback{"label value not a string"};
+    Ref val(make_str(read_raw_string(cc), scratch));
+    if (PyDict_SetItem(d, key.o, val.o) < 0) throw Fallback{"dict"};
+  });
+  ns.labels.reset(hold.release());
+}
+
+void parse_metadata(Cursor& c, NodeScan& ns, const std::string& health_key, std::string& scratch) {
+  ns.name.reset(nullptr);
+  ns.labels.reset(nullptr);
+  ns.health.reset(nullptr);
+  ns.meta_obj = false;
+  if (c.peek() != '{') {
+    skip_value(c);  // null or a non-object: name "" / labels {} (models/node.py)
+    return;
+  }
+  ns.meta_obj = true;
+  for_members(c, [&](const RawStr& k, Cursor& cc) {
+    if (raw_equals(k, "name", scratch)) {
+      if (is_null(cc)) {
+        ns.name.reset(nullptr);
+      } else if (cc.peek() == '"') {
+        ns.name.reset(make_str(read_raw_string(cc), scratch));
+      } else {
+        throw Fallback{"name not a string"};
+      }
+    } else if (raw_equals(k, "labels", scratch)) {
+      parse_labels(cc, ns, scratch);
+    } else if (raw_equals(k, "annotations", scratch)) {
+      ns.health.reset(nullptr);
+      if (cc.peek() != '{') {
+        skip_value(cc);
+        return;
+      }
+      for_members(cc, [&](const RawStr& ak, Cursor& c3) {
+        if (!health_key.empty() && raw_equals(ak, health_key.c_str(), scratch) && c3.peek() == '"') {
+          ns.health.reset(make_str(read_raw_string(c3), scratch));
+        } else {
+          if (!health_key.empty() && raw_equals(ak, health_key.c_str(), scratch)) ns.health.reset(nullptr);
+          skip_value(c3);
+        }
+      });
+    } else {
+      skip_value(cc);
+    }
+  });
+}
+
+PyObject* taint_field(Cursor& c, std::string& scratch) {
+  if (is_null(c)) Py_RETURN_NONE;
+  if (c.peek() != '"') throw Fallback{"taint field not a string"};
+  return make_str(read_raw_string(c), scratch);
+}
+
+void parse_spec(Cursor& c, NodeScan& ns, std::string& scratch) {
+  ns.taints.reset(PyList_New(0));
+  ns.unschedulable = false;
+  if (!ns.taints.o) throw Fallback{"oom"};
+  if (c.peek() != '{') {
+    skip_value(c);
+    return;
+  }
+  for_members(c, [&](const RawStr& k, Cursor& cc) {
+    if (raw_equals(k, "taints", scratch)) {
+      ns.taints.reset(PyList_New(0));
+      if (!ns.taints.o) throw Fallback{"oom"};
+      if (cc.peek() != '[') {
+        skip_value(cc);
+        return;
+      }
+      for_elements(cc, [&](Cursor& c3) {
+        if (c3.peek() != '{') {
+          skip_value(c3);
+          return;
+        }
+        Ref tk(Py_NewRef(Py_None)), tv(Py_NewRef(Py_None)), te(Py_NewRef(Py_None));
+        for_members(c3, [&](const RawStr& fk, Cursor& c4) {
+          if (raw_equals(fk, "key", scratch)) tk.reset(taint_field(c4, scratch));
+          else if (raw_equals(fk, "value", scratch)) tv.reset(taint_field(c4, scratch));
+          else if (raw_equals(fk, "effect", scratch)) te.reset(taint_field(c4, scratch));
+          else skip_value(c4);
+        });
+        PyObject* d = PyDict_New();
+        if (!d) throw Fallback{"oom"};
+        Ref hd(d);
+        if (PyDict_SetItem(d, k_key, tk.o) < 0 || PyDict_SetItem(d, k_value, tv.o) < 0 ||
+            PyDict_SetItem(d, k_effect, te.o) < 0 || PyList_Append(ns.taints.o, d) < 0)
+          throw Fallback{"dict"};
+      });
+    } else if (raw_equals(k, "unschedulable", scratch)) {
+      char ch = cc.peek();
+      if (ch == 't') {
+        skip_literal(cc);
+        ns.unschedulable = true;
+      } else if (ch == 'f' || ch == 'n') {
+        skip_literal(cc);
+        ns.unschedulable = false;
+      } else {
+        throw Fallback{"unschedulable not a bool"};
+      }
+    } else {
+      skip_value(cc);
+    }
+  });
+}
+
+void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scratch) {
+  for (auto* v : {&ns.cap, &ns.alloc})
+    for (auto& q : *v) {
+      q.set = false;
+      q.ok = false;
+      q.value.reset(nullptr);
+    }
+  ns.ready = false;
+  if (c.peek() != '{') {
+    skip_value(c);
+    return;
+  }
+  for_members(c, [&](const RawStr& k, Cursor& cc) {
+    if (raw_equals(k, "capacity", scratch)) {
+      parse_resource_map(cc, ks, ns.cap, scratch);
+    } else if (raw_equals(k, "allocatable", scratch)) {
+      parse_resource_map(cc, ks, ns.alloc, scratch);
+    } else if (raw_equals(k, "conditions", scratch)) {
+      ns.ready = false;
+      if (cc.peek() != '[') {
+        skip_value(cc);
+        return;
+      }
+      for_elements(cc, [&](Cursor& c3) {
+        if (c3.peek() != '{') {
+          skip_value(c3);
+          return;
+        }
+        bool type_ready = false, status_true = false;
+        for_members(c3, [&](const RawStr& fk, Cursor& c4) {
+          bool is_type = raw_equals(fk, "type", scratch);
+          bool is_status = !is_type && raw_equals(fk, "status", scratch);
+          if ((is_type || is_status) && c4.peek() == '"') {
+            RawStr v = read_raw_string(c4);
+            bool eq = raw_equals(v, is_type ? "Ready" : "True", scratch);
+            if (is_type) type_ready = eq;
+            else status_true = eq;
+          } else {
+            if (is_type) type_ready = false;
+            if (is_status) status_true = false;
+            skip_value(c4);
+          }
+        });
+        if (type_ready && status_true) ns.ready = true;
+      });
+    } else {
+      skip_value(cc);
+    }
+  });
+}
+
+struct PageOut {
+  Ref gpu_nodes{PyList_New(0)};
+  Ref ready_nodes{PyList_New(0)};
+  Ref extras{PyList_New(0)};
+  Ref cont;  // str or nullptr
+  Py_ssize_t items = 0;
+};
+
+void emit_node(NodeScan& ns, const KeySpec& ks, bool use_alloc, bool want_extras, PyObject* extras_cls,
+               PageOut& out) {
+  long long total = 0;
+  Ref bd(breakdown_dict(ks, use_alloc ? ns.alloc : ns.cap, &total));
+  if (total <= 0) return;  // not a GPU node (reference :222)
+  PyObject* info = PyDict_New();
+  if (!info) throw Fallback{"oom"};
+  Ref hi(info);
+  PyObject* name = ns.meta_obj ? (ns.name.o ? ns.name.o : Py_None) : nullptr;
+  Ref empty_name;
+  if (!name) {
+    empty_name.reset(PyUnicode_FromStringAndSize("", 0));
+    name = empty_name.o;
+  }
+  Ref labels;
+  PyObject* lab = ns.labels.o;
+  if (!lab || PyDict_GET_SIZE(lab) == 0) {
+    labels.reset(PyDict_New());
+    lab = labels.o;
+  }
+  Ref taints;
+  PyObject* tl = ns.taints.o;
+  if (!tl) {
+    taints.reset(PyList_New(0));
+    tl = taints.o;
+  }
+  Ref gpus(PyLong_FromLongLong(total));
+  if (PyDict_SetItem(info, k_name, name) < 0 || PyDict_SetItem(info, k_ready, ns.ready ? Py_True : Py_False) < 0 ||
+      PyDict_SetItem(info, k_gpus, gpus.o) < 0 || PyDict_SetItem(info, k_breakdown, bd.o) < 0 ||
+      PyDict_SetItem(info, k_labels, lab) < 0 || PyDict_SetItem(info, k_taints, tl) < 0)
+    throw Fallback{"dict"};
+  if (PyList_Append(out.gpu_nodes.o, info) < 0) throw Fallback{"list"};
+  if (ns.ready && PyList_Append(out.ready_nodes.o, info) < 0) throw Fallback{"list"};
+  if (want_extras) {
+    Ref capd(breakdown_dict(ks, ns.cap, nullptr));
+    Ref allocd(breakdown_dict(ks, ns.alloc, nullptr));
+    PyObject* health = ns.health.o ? ns.health.o : Py_None;
+    Ref ex(PyObject_CallFunctionObjArgs(extras_cls, ns.ready ? Py_True : Py_False, capd.o, allocd.o,
+                                        ns.unschedulable ? Py_True : Py_False, health, nullptr));
+    if (!ex.o) {
+      PyErr_Clear();
+      throw Fallback{"NodeExtras()"};
+    }
+    if (PyList_Append(out.extras.o, ex.o) < 0) throw Fallback{"list"};
+  }
+}
+
+void parse_item(Cursor& c, const KeySpec& ks, bool use_alloc, bool want_extras, PyObject* extras_cls,
+                const std::string& health_key, PageOut& out, std::string& scratch) {
+  out.items++;
+  if (c.peek() != '{') {
+    skip_value(c);  // non-object item: never a GPU node
+    return;
+  }
+  NodeScan ns;
+  ns.cap.resize(ks.keys.size());
+  ns.alloc.resize(ks.keys.size());
+  for_members(c, [&](const RawStr& k, Cursor& cc) {
+    if (raw_equals(k, "metadata", scratch)) parse_metadata(cc, ns, health_key, scratch);
+    else if (raw_equals(k, "spec", scratch)) parse_spec(cc, ns, scratch);
+    else if (raw_equals(k, "status", scratch)) parse_status(cc, ns, ks, scratch);
+    else skip_value(cc);
+  });
+  emit_node(ns, ks, use_alloc, want_extras, extras_cls, out);
+}
+
+int append_all(PyObject* result, PyObject* attr, PyObject* items) {
+  PyObject* lst = PyObject_GetAttr(result, attr);
+  if (!lst) return -1;
+  Py_ssize_t n = PyList_GET_SIZE(items);
+  int rc = 0;
+  if (PyList_Check(lst)) {
+    rc = PyList_SetSlice(lst, PyList_GET_SIZE(lst), PyList_GET_SIZE(lst), items);
+  } else {
+    for (Py_ssize_t i = 0; i < n && rc == 0; ++i) {
+      PyObject* r = PyObject_CallMethod(lst, "append", "O", PyList_GET_ITEM(items, i));
+      if (!r) rc = -1;
+      Py_XDECREF(r);
+    }
+  }
+  Py_DECREF(lst);
+  return rc;
+}
+
+PyObject* scan_nodelist(PyObject*, PyObject* args) {
+  Py_buffer view;
+  PyObject *result, *keys, *extras_cls;
+  int use_alloc, want_extras;
+  const char* health_key_c;
+  if (!PyArg_ParseTuple(args, "y*OO!ppsO", &view, &result, &PyTuple_Type, &keys, &use_alloc, &want_extras,
+                        &health_key_c, &extras_cls))
+    return nullptr;
+  KeySpec ks;
+  for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(keys); ++i) {
+    PyObject* k = PyTuple_GET_ITEM(keys, i);
+    Py_ssize_t n;
+    const char* s = PyUnicode_AsUTF8AndSize(k, &n);
+    if (!s) {
+      PyBuffer_Release(&view);
+      return nullptr;
+    }
+    ks.keys.emplace_back(s, static_cast<size_t>(n));
+    ks.pykeys.push_back(k);
+  }
+  std::string health_key(health_key_c);
+  std::string scratch;
+  PageOut out;
+  const char* why = nullptr;
+  try {
+    if (!out.gpu_nodes.o || !out.ready_nodes.o || !out.extras.o) throw Fallback{"oom"};
+    Cursor c{static_cast<const char*>(view.buf), static_cast<const char*>(view.buf) + view.len};
+    if (c.peek() != '{') throw Fallback{"top level is not an object"};
+    bool items_seen = false;
+    for_members(c, [&](const RawStr& k, Cursor& cc) {
+      if (raw_equals(k, "items", scratch)) {
+        if (items_seen) throw Fallback{"duplicate items"};
+        items_seen = true;
+        if (is_null(cc)) return;
+        if (cc.peek() != '[') throw Fallback{"items not a list"};
+        for_elements(cc, [&](Cursor& c3) {
+          parse_item(c3, ks, use_alloc, want_extras, extras_cls, health_key, out, scratch);
+        });
+      } else if (raw_equals(k, "metadata", scratch)) {
+        out.cont.reset(nullptr);
+        if (cc.peek() != '{') {
+          skip_value(cc);
+          return;
+        }
+        for_members(cc, [&](const RawStr& mk, Cursor& c3) {
+          if (raw_equals(mk, "continue", scratch)) {
+            if (c3.peek() == '"') {
+              RawStr v = read_raw_string(c3);
+              if (v.e > v.b) out.cont.reset(make_str(v, scratch));
+              else out.cont.reset(nullptr);
+            } else {
+              out.cont.reset(nullptr);
+              skip_value(c3);
+            }
+          } else {
+            skip_value(c3);
+          }
+        });
+      } else {
+        skip_value(cc);
+      }
+    });
+    c.ws();
+    if (c.p != c.end) throw Fallback{"trailing data"};
+  } catch (const Fallback& f) {
+    why = f.why;
+  }
+  PyBuffer_Release(&view);
+  if (why) {
+    if (!PyErr_Occurred()) PyErr_SetString(g_fallback, why);
+    return nullptr;
+  }
+  // commit: nothing above touched `result`
+  if (append_all(result, a_gpu_nodes, out.gpu_nodes.o) < 0 ||
+      append_all(result, a_ready_gpu_nodes, out.ready_nodes.o) < 0 ||
+      (want_extras && append_all(result, a_extras, out.extras.o) < 0))
+    return nullptr;
+  PyObject* seen = PyObject_GetAttr(result, a_items_seen);
+  if (!seen) return nullptr;
+  PyObject* n = PyLong_FromSsize_t(out.items);
+  PyObject* tot = n ? PyNumber_Add(seen, n) : nullptr;
+  Py_DECREF(seen);
+  Py_XDECREF(n);
+  if (!tot) return nullptr;
+  int rc = PyObject_SetAttr(result, a_items_seen, tot);
+  Py_DECREF(tot);
+  if (rc < 0) return nullptr;
+  PyObject* cont = out.cont.o ? out.cont.o : Py_None;
+  return Py_BuildValue("(On)", cont, out.items);
+}
+
+// ---------------------------------------------------------------- emitting --
+void emit_string(std::string& out, PyObject* s) {
+  Py_ssize_t n;
+  const char* u = PyUnicode_AsUTF8AndSize(s, &n);
+  if (!u) {
+    PyErr_Clear();
+    throw Fallback{"unencodable string"};
+  }
+  out.push_back('"');
+  const char* p = u;
+  const char* e = u + n;
+  const char* run = p;
+  static const char hex[] = "0123456789abcdef";
+  for (; p < e; ++p) {
+    unsigned char ch = static_cast<unsigned char>(*p);
+    if (ch >= 0x20 && ch != '"' && ch != '\\') continue;
+    out.append(run, p - run);
+    switch (ch) {
+      case '"': out.append("\\\""); break;
+      case '\\': out.append("\\\\"); break;
+      case '\n': out.append("\\n"); break;
+      case '\r': out.append("\\r"); break;
+      case '\t': out.append("\\t"); break;
+      case '\b': out.append("\\b"); break;
+      case '\f': out.append("\\f"); break;
+      default: {
+        char buf[7] = {'\\', 'u', '0', '0', hex[ch >> 4], hex[ch & 15], 0};
+        out.append(buf, 6);
+      }
+    }
+    run = p + 1;
+  }
+  out.append(run, e - run);
+  out.push_back('"');
+}
+
+void emit_indent(std::string& out, int level) {
+  out.push_back('\n');
+  out.append(static_cast<size_t>(level) * 2, ' ');
+}
+
+void emit_float(std::string& out, PyObject* o) {
+  double d = PyFloat_AS_DOUBLE(o);
+  if (std::isnan(d)) {
+    out.append("NaN");
+  } else if (std::isinf(d)) {
+    out.append(d > 0 ? "Infinity" : "-Infinity");
+  } else {
+    PyObject* r = PyObject_Repr(o);
+    if (!r) throw Fallback{"repr"};
+    Py_ssize_t n;
+    const char* u = PyUnicode_AsUTF8AndSize(r, &n);
+    out.append(u, static_cast<size_t>(n));
+    Py_DECREF(r);
+  }
+}
+
+void emit_value(std::string& out, PyObject* o, int level) {
+  if (level > 200) throw Fallback{"too deep"};
+  if (o == Py_None) {
+    out.append("null");
+  } else if (o == Py_True) {
+    out.append("true");
+  } else if (o == Py_False) {
+    out.append("false");
+  } else if (PyUnicode_CheckExact(o)) {
+    emit_string(out, o);
+  } else if (PyLong_CheckExact(o)) {
+    PyObject* r = PyObject_Str(o);
+    if (!r) throw Fallback{"str"};
+    Py_ssize_t n;
+    const char* u = PyUnicode_AsUTF8AndSize(r, &n);
+    out.append(u, static_cast<size_t>(n));
+    Py_DECREF(r);
+  } else if (PyFloat_CheckExact(o)) {
+    emit_float(out, o);
+  } else if (PyDict_CheckExact(o)) {
+    if (PyDict_GET_SIZE(o) == 0) {
+      out.append("{}");
+      return;
+    }
+    out.push_back('{');
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    bool first = true;
+    while (PyDict_Next(o, &pos, &k, &v)) {
+      if (!PyUnicode_CheckExact(k)) throw Fallback{"non-str key"};
+      if (!first) out.push_back(',');
+      first = false;
+      emit_indent(out, level + 1);
+      emit_string(out, k);
+      out.append(": ");
+      emit_value(out, v, level + 1);
+    }
+    emit_indent(out, level);
+    out.push_back('}');
+  } else if (PyList_CheckExact(o) || PyTuple_CheckExact(o)) {
+    PyObject* seq = o;
+    Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    if (n == 0) {
+      out.append("[]");
+      return;
+    }
+    out.push_back('[');
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (i) out.push_back(',');
+      emit_indent(out, level + 1);
+      emit_value(out, PySequence_Fast_GET_ITEM(seq, i), level + 1);
+    }
+    emit_indent(out, level);
+    out.push_back(']');
+  } else {
+    throw Fallback{"unsupported type"};
+  }
+}
+
+PyObject* dumps_indent2(PyObject*, PyObject* obj) {
+  std::string out;
+  out.reserve(4096);
+  try {
+    emit_value(out, obj, 0);
+  } catch (const Fallback& f) {
+    if (!PyErr_Occurred()) PyErr_SetString(g_fallback, f.why);
+    return nullptr;
+  }
+  return PyUnicode_DecodeUTF8(out.data(), static_cast<Py_ssize_t>(out.size()), "surrogatepass");
+}
+
+PyMethodDef methods[] = {
+    {"scan_nodelist", scan_nodelist, METH_VARARGS, "Scan one NodeList page into a ScanResult."},
+    {"dumps_indent2", dumps_indent2, METH_O, "json.dumps(obj, ensure_ascii=False, indent=2), natively."},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_fastpath", "Native CPU hot path (NodeList scan, JSON emit).", -1,
+                      methods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__fastpath(void) {
+  PyObject* m = PyModule_Create(&moddef);
+  if (!m) return nullptr;
+  g_fallback = PyErr_NewException("_fastpath.FallbackError", PyExc_ValueError, nullptr);
+  Py_INCREF(g_fallback);
+  PyModule_AddObject(m, "FallbackError", g_fallback);
+  k_name = PyUnicode_InternFromString("name");
+  k_ready = PyUnicode_InternFromString("ready");
+  k_gpus = PyUnicode_InternFromString("gpus");
+  k_breakdown = PyUnicode_InternFromString("gpu_breakdown");
+  k_labels = PyUnicode_InternFromString("labels");
+  k_taints = PyUnicode_InternFromString("taints");
+  k_key = PyUnicode_InternFromString("key");
+  k_value = PyUnicode_InternFromString("value");
+  k_effect = PyUnicode_InternFromString("effect");
+  a_gpu_nodes = PyUnicode_InternFromString("gpu_nodes");
+  a_ready_gpu_nodes = PyUnicode_InternFromString("ready_gpu_nodes");
+  a_extras = PyUnicode_InternFromString("extras");
+  a_items_seen = PyUnicode_InternFromString("items_seen");
+  PyModule_AddStringConstant(m, "BUILD", "gfx950-host/x86_64");
+  return m;
+}

@@ -1,0 +1,151 @@
+"""kube-apiserver client: paginated node LIST, node GET/PATCH (SURVEY §7.2 layer 2).
+
+Replaces ``CoreV1Api().list_node()`` (reference ``check-gpu-node.py:217``),
+which is one unpaginated GET with no timeout and no retry.  Here:
+
+* ``GET /api/v1/nodes?limit=<page>`` then ``&continue=<token>`` on one
+  keep-alive connection; pages are scanned as they arrive (the native scanner
+  never holds more than one page), so memory is bounded by the page size.
+* an expired ``continue`` token (HTTP 410) falls back to one full LIST, as
+  client-go's pager does.
+* every request has a timeout; idempotent requests are retried on connection
+  errors, 429 and 5xx with jittered exponential backoff honouring
+  ``Retry-After``.
+* ``Accept-Encoding: gzip`` is sent to non-loopback servers (a 1000-node
+  NodeList shrinks ~15x on the wire); loopback skips the inflate cost.
+* failures raise :class:`ApiException` / :class:`TransportError` whose
+  ``str()`` matches what the reference would have printed.
+"""
+
+from __future__ import annotations
+
+import json
+import time
+from typing import Any, Dict, Optional, Sequence
+from urllib.parse import quote
+
+from ..models.node import ScanResult
+from ..models.resources import GPU_RESOURCE_KEYS
+from ..utils.backoff import Backoff
+from ..utils.http import Connection, HTTPError, Response
+from .config import ClusterConnection
+from .errors import ApiException, TransportError
+
+USER_AGENT = "k8s-gpu-node-checker-amd/0.1 (MI355X)"
+_RETRY_STATUS = frozenset((429, 500, 502, 503, 504))
+_LOOPBACK = ("127.", "localhost", "::1", "[::1]")
+
+
+class KubeClient:
+    def __init__(self, cluster: ClusterConnection, timeout: float = 30.0, retries: int = 2,
+                 backoff: Optional[Backoff] = None, gzip: Optional[bool] = None,
+                 sleep=time.sleep, tracer=None):
+        self.cluster = cluster
+        self.timeout = timeout
+        self.retries = max(0, retries)
+        self.backoff = backoff or Backoff(base=0.2, cap=5.0)
+        self.sleep = sleep
+        self.tracer = tracer
+        self._conn: Optional[Connection] = None
+        host = cluster.server.split("://", 1)[-1]
+        self.gzip = (not host.startswith(_LOOPBACK)) if gzip is None else gzip
+        self.requests_made = 0
+
+    # -- plumbing -------------------------------------------------------------
+    def _connection(self) -> Connection:
+        if self._conn is None:
+            ctx = self.cluster.ssl_context() if self.cluster.server.startswith("https") else None
+            self._conn = Connection(self.cluster.server, timeout=self.timeout, ssl_context=ctx,
+                                    server_hostname=self.cluster.tls_server_name,
+                                    proxy_url=self.cluster.proxy_url)
+        return self._conn
+
+    def close(self) -> None:
+        if self._conn is not None:
+            self._conn.close()
+            self._conn = None
+
+    def __enter__(self) -> "KubeClient":
+        return self
+
+    def __exit__(self, *exc: Any) -> None:
+        self.close()
+
+    def request(self, method: str, path: str, body: Optional[bytes] = None,
+                content_type: Optional[str] = None, idempotent: bool = True) -> Response:
+        headers = {"Accept": "application/json", "User-Agent": USER_AGENT}
+        headers.update(self.cluster.auth_headers())
+        if self.gzip:
+            headers["Accept-Encoding"] = "gzip"
+        if content_type:
+            headers["Content-Type"] = content_type
+        attempt = 0
+        while True:
+            conn = self._connection()
+            self.requests_made += 1
+            try:
+                resp = conn.request(method, path, headers, body)
+            except HTTPError as e:
+                if idempotent and attempt < self.retries and e.kind != "tls":
+                    self.sleep(self.backoff.delay(attempt))
+                    attempt += 1
+                    continue
+                raise TransportError(conn.scheme, conn.host, conn.port, path, e) from e
+            if 200 <= resp.status < 300:
+                return resp
+            if idempotent and resp.status in _RETRY_STATUS and attempt < self.retries:
+                self.sleep(self.backoff.delay(attempt, resp.header("Retry-After")))
+                attempt += 1
+                continue
+            raise ApiException(resp.status, resp.reason, resp.header_dict(), resp.text)
+
+    # -- nodes ----------------------------------------------------------------
+    def _list_path(self, limit: int, cont: Optional[str], label_selector: Optional[str],
+                   resource_version: Optional[str]) -> str:
+        q = []
+        if limit > 0:
+            q.append(f"limit={limit}")
+        if cont:
+            q.append("continue=" + quote(cont, safe=""))
+        if label_selector:
+            q.append("labelSelector=" + quote(label_selector, safe=""))
+        if resource_version is not None and not cont:
+            q.append("resourceVersion=" + quote(resource_version, safe=""))
+        return "/api/v1/nodes" + ("?" + "&".join(q) if q else "")
+
+    def scan_nodes(self, limit: int = 500, keys: Sequence[str] = GPU_RESOURCE_KEYS,
+                   gpu_source: str = "capacity", want_extras: bool = False,
+                   label_selector: Optional[str] = None,
+                   resource_version: Optional[str] = None) -> ScanResult:
+        """LIST all nodes (paginated) and classify them (reference ``list_gpu_nodes``, ``:215-226``)."""
+        from ..ops import fastpath
+        result = ScanResult()
+        cont: Optional[str] = None
+        while True:
+            path = self._list_path(limit, cont, label_selector, resource_version)
+            try:
+                resp = self.request("GET", path)
+            except ApiException as e:
+                if e.status == 410 and cont:
+                    # continue token expired mid-list: restart as one consistent full LIST
+                    result = ScanResult()
+                    resp = self.request("GET", self._list_path(0, None, label_selector, None))
+                    fastpath.scan_page(resp.body, result, keys, gpu_source, want_extras)
+                    return result
+                raise
+            t0 = time.perf_counter()
+            cont, _ = fastpath.scan_page(resp.body, result, keys, gpu_source, want_extras)
+            if self.tracer is not None:
+                self.tracer.add("parse", time.perf_counter() - t0)
+            if not cont or limit <= 0:
+                return result
+
+    def get_node(self, name: str) -> Dict[str, Any]:
+        return json.loads(self.request("GET", "/api/v1/nodes/" + quote(name, safe="")).body)
+
+    def patch_node_annotations(self, name: str, annotations: Dict[str, Optional[str]]) -> Dict[str, Any]:
+        """JSON merge-patch ``metadata.annotations`` (needs RBAC ``nodes: patch``)."""
+        body = json.dumps({"metadata": {"annotations": annotations}}).encode()
+        resp = self.request("PATCH", "/api/v1/nodes/" + quote(name, safe=""), body,
+                            content_type="application/merge-patch+json", idempotent=True)
+        return json.loads(resp.body) if resp.body else {}

@@ -1,0 +1,224 @@
+"""MI355X health model: probe-report schema, verdicts and the Ready gate.
+
+The reference's only failure signal is NodeCondition ``Ready`` plus "GPU
+capacity > 0" (``check-gpu-node.py:172-196``).  It cannot see a node whose
+kubelet is fine but whose accelerators are not: a GPU that fell off the bus,
+uncorrectable HBM ECC errors, a downed xGMI link, a partition-mode change
+that halves the visible VRAM.  The MI355X node agent (``agent/``) runs the
+native amd-smi probe (``csrc/probe``) and publishes a compact report as the
+node annotation ``amd.com/mi355x-health``; the checker evaluates it here.
+
+Expectations, measured on a real MI355X via ``gpurun`` (amd-smi 26.2.1,
+``profiles/amdsmi_mi355x.json``): ``target_graphics_version=gfx950``,
+``market_name="AMD Instinct MI355 OAM"``, ``vram_type=5`` (HBM3E),
+``vram_size=294896`` MB in SPX/NPS1, xGMI ``status=["X","U"x7]`` (7 of 8
+ports Up, one disabled), 256 CUs.
+
+Verdicts: ``healthy`` / ``degraded`` (warnings only, still schedulable) /
+``unhealthy`` / ``unknown`` (no report, stale report, or the probe could not
+run: driver not loaded, no permission).
+"""
+
+from __future__ import annotations
+
+import json
+import time
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+SCHEMA = "mi355x-health/v1"
+
+# --- MI355X / gfx950 expectations (CDNA4) ------------------------------------
+GFX_TARGET = "gfx950"
+PRODUCT_TOKENS = ("MI355", "MI350")          # market_name / vbios name on gfx950 parts
+HBM3E_VRAM_TYPE = 5                           # amdsmi.h AMDSMI_VRAM_TYPE_HBM3E
+VRAM_MB_FULL = 294896                         # measured vram_size, SPX/NPS1 (288 GB class)
+VRAM_MIN_FRACTION = 0.97
+XGMI_LINKS_EXPECTED = 7                       # 8-GPU hive: 7 peers per GPU
+NUM_CUS = 256
+HOTSPOT_WARN_C = 100
+
+HEALTHY, DEGRADED, UNHEALTHY, UNKNOWN = "healthy", "degraded", "unhealthy", "unknown"
+_OK_STATES = (HEALTHY, DEGRADED)
+
+
+class HealthExpectations:
+    """Tunable thresholds (CLI flags map onto these)."""
+
+    def __init__(self, xgmi_links: int = XGMI_LINKS_EXPECTED, max_age_s: float = 900.0,
+                 require_product: bool = True, vram_min_fraction: float = VRAM_MIN_FRACTION,
+                 bad_page_limit: int = 64, correctable_warn: int = 1000):
+        self.xgmi_links = xgmi_links
+        self.max_age_s = max_age_s
+        self.require_product = require_product
+        self.vram_min_fraction = vram_min_fraction
+        self.bad_page_limit = bad_page_limit
+        self.correctable_warn = correctable_warn
+
+
+class Verdict:
+    __slots__ = ("state", "reasons", "warnings", "gpus_ok", "gpus_seen", "age_s")
+
+    def __init__(self, state: str, reasons: Optional[List[str]] = None, warnings: Optional[List[str]] = None,
+                 gpus_ok: int = 0, gpus_seen: int = 0, age_s: Optional[float] = None):
+        self.state = state
+        self.reasons = reasons or []
+        self.warnings = warnings or []
+        self.gpus_ok = gpus_ok
+        self.gpus_seen = gpus_seen
+        self.age_s = age_s
+
+    @property
+    def ok(self) -> bool:
+        return self.state in _OK_STATES
+
+    def short(self) -> str:
+        if self.state == HEALTHY:
+            return f"MI355X {self.gpus_ok}/{self.gpus_seen} healthy"
+        detail = "; ".join(self.reasons or self.warnings)
+        return f"MI355X {self.state}" + (f": {detail}" if detail else "")
+
+    def to_dict(self) -> Dict[str, Any]:
+        d: Dict[str, Any] = {"state": self.state, "gpus_ok": self.gpus_ok, "gpus_seen": self.gpus_seen}
+        if self.reasons:
+            d["reasons"] = self.reasons
+        if self.warnings:
+            d["warnings"] = self.warnings
+        if self.age_s is not None:
+            d["age_s"] = round(self.age_s, 1)
+        return d
+
+
+def _nps(mem_partition: Any) -> int:
+    if isinstance(mem_partition, str) and mem_partition.upper().startswith("NPS"):
+        try:
+            return max(1, int(mem_partition[3:]))
+        except ValueError:
+            return 1
+    return 1
+
+
+def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str], List[str]]:
+    """Return ``(failures, warnings)`` for one GPU entry of a probe report."""
+    fail: List[str] = []
+    warn: List[str] = []
+    idx = g.get("index", "?")
+    if g.get("error"):
+        fail.append(f"gpu{idx}: probe error {g['error']}")
+        return fail, warn
+    gfx = g.get("gfx")
+    if gfx != GFX_TARGET:
+        fail.append(f"gpu{idx}: target {gfx!r} is not {GFX_TARGET}")
+    name = f"{g.get('market_name') or ''} {g.get('vbios_name') or ''}"
+    if exp.require_product and not any(t in name for t in PRODUCT_TOKENS):
+        fail.append(f"gpu{idx}: product {g.get('market_name')!r} is not MI355X/MI350X")
+    vt = g.get("vram_type")
+    if vt is not None and vt != HBM3E_VRAM_TYPE and vt != "HBM3E":
+        fail.append(f"gpu{idx}: VRAM type {vt} is not HBM3E")
+    vram = g.get("vram_mb")
+    if isinstance(vram, (int, float)):
+        need = VRAM_MB_FULL / _nps(g.get("memory_partition")) * exp.vram_min_fraction
+        if vram < need:
+            fail.append(f"gpu{idx}: VRAM {vram} MB < {need:.0f} MB expected")
+    ue = g.get("ecc_uncorrectable")
+    if isinstance(ue, int) and ue > 0:
+        fail.append(f"gpu{idx}: {ue} uncorrectable ECC errors")
+    de = g.get("ecc_deferred")
+    if isinstance(de, int) and de > 0:
+        warn.append(f"gpu{idx}: {de} deferred ECC errors")
+    ce = g.get("ecc_correctable")
+    if isinstance(ce, int) and ce > exp.correctable_warn:
+        warn.append(f"gpu{idx}: {ce} correctable ECC errors")
+    bp = g.get("bad_pages")
+    if isinstance(bp, int):
+        if bp > exp.bad_page_limit:
+            fail.append(f"gpu{idx}: {bp} retired pages > {exp.bad_page_limit}")
+        elif bp > 0:
+            warn.append(f"gpu{idx}: {bp} retired pages")
+    links = g.get("xgmi")
+    if isinstance(links, str) and exp.xgmi_links > 0:
+        up, down = links.count("U"), links.count("D")
+        if down:
+            fail.append(f"gpu{idx}: {down} xGMI link(s) down ({links})")
+        elif up < exp.xgmi_links:
+            fail.append(f"gpu{idx}: {up}/{exp.xgmi_links} xGMI links up ({links})")
+    if g.get("kfd") is False:
+        fail.append(f"gpu{idx}: no KFD node (not usable by ROCm)")
+    cus = g.get("cus")
+    if isinstance(cus, int) and g.get("compute_partition", "SPX") == "SPX" and 0 < cus < NUM_CUS:
+        fail.append(f"gpu{idx}: {cus} CUs < {NUM_CUS}")
+    t = g.get("hotspot_c")
+    if isinstance(t, (int, float)) and t >= HOTSPOT_WARN_C:
+        warn.append(f"gpu{idx}: hotspot {t} C")
+    diag = g.get("diag")
+    if isinstance(diag, dict):
+        for test, res in diag.items():
+            if isinstance(res, dict) and res.get("pass") is False:
+                fail.append(f"gpu{idx}: diag {test} failed ({res.get('detail', '')})".rstrip(" ()"))
+    return fail, warn
+
+
+def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
+                    exp: Optional[HealthExpectations] = None, now: Optional[float] = None) -> Verdict:
+    exp = exp or HealthExpectations()
+    if not report:
+        return Verdict(UNKNOWN, ["no probe report"])
+    if report.get("schema") != SCHEMA:
+        return Verdict(UNKNOWN, [f"unsupported probe schema {report.get('schema')!r}"])
+    now = time.time() if now is None else now
+    ts = report.get("ts")
+    age = (now - float(ts)) if isinstance(ts, (int, float)) else None
+    if age is None or age > exp.max_age_s:
+        return Verdict(UNKNOWN, ["stale probe report" if age is not None else "probe report has no timestamp"],
+                       age_s=age)
+    if report.get("error"):
+        return Verdict(UNKNOWN, [f"probe failed: {report['error']}"], age_s=age)
+    gpus = report.get("gpus") or []
+    fails: List[str] = []
+    warns: List[str] = []
+    ok = 0
+    for g in gpus:
+        if not isinstance(g, dict):
+            continue
+        f, w = evaluate_gpu(g, exp)
+        fails += f
+        warns += w
+        ok += 0 if f else 1
+    if expected_gpus and len(gpus) < expected_gpus:
+        fails.append(f"{len(gpus)} of {expected_gpus} GPUs visible to amd-smi")
+    state = UNHEALTHY if fails else (DEGRADED if warns else HEALTHY)
+    return Verdict(state, fails, warns, gpus_ok=ok, gpus_seen=len(gpus), age_s=age)
+
+
+def parse_annotation(raw: Optional[str]) -> Optional[Dict[str, Any]]:
+    if not raw:
+        return None
+    try:
+        doc = json.loads(raw)
+    except ValueError:
+        return {"schema": SCHEMA, "error": "annotation is not JSON", "ts": time.time()}
+    return doc if isinstance(doc, dict) else None
+
+
+def gate_ready(ready_condition: bool, verdict: Optional[Verdict], policy: str, is_amd: bool,
+               unknown_ok: bool = True) -> bool:
+    """Combine NodeCondition Ready with the MI355X verdict.
+
+    ``off``     -> Ready condition only (the reference).
+    ``auto``    -> nodes that carry a probe report must also be healthy;
+                   nodes without one keep the reference semantics.
+    ``require`` -> every ``amd.com/gpu`` node needs a healthy, fresh report.
+    """
+    if not ready_condition or policy == "off" or not is_amd:
+        return ready_condition
+    if verdict is None:
+        return policy != "require"
+    if verdict.state == UNKNOWN:
+        return unknown_ok and policy != "require"
+    return verdict.ok
+
+
+def summarize(verdicts: Sequence[Optional[Verdict]]) -> Dict[str, int]:
+    out = {HEALTHY: 0, DEGRADED: 0, UNHEALTHY: 0, UNKNOWN: 0}
+    for v in verdicts:
+        out[v.state if v else UNKNOWN] += 1
+    return out

@@ -1,0 +1,161 @@
+"""Node projection and GPU-node classification.
+
+The reference deserialises every ``V1Node`` through the OpenAPI client and
+then projects it (``check-gpu-node.py:172-226``).  Here the raw JSON *is* the
+model: a ``NodeList`` page is decoded once (``json.loads`` or the native
+scanner in :mod:`k8s_gpu_node_checker_amd.ops.fastpath`) and each item is
+projected straight into the report dict, so there is no per-node object
+graph to build and no ``isinstance(cond, V1NodeCondition)`` trap (``:176``).
+
+Report dict schema (reference ``:202-212``)::
+
+    {"name": str, "ready": bool, "gpus": int, "gpu_breakdown": {key: int},
+     "labels": {str: str}, "taints": [{"key", "value", "effect"}]}
+"""
+
+from __future__ import annotations
+
+from typing import Any, Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
+
+from .resources import GPU_RESOURCE_KEYS, PRIMARY_GPU_KEY, gpu_breakdown
+
+#: Annotation written by the MI355X node agent (see ``agent/``).
+HEALTH_ANNOTATION = "amd.com/mi355x-health"
+
+
+def _get(obj: Any, key: str) -> Any:
+    return obj.get(key) if isinstance(obj, Mapping) else None
+
+
+def is_ready(node: Mapping[str, Any]) -> bool:
+    """NodeCondition ``Ready`` with status ``"True"`` (reference ``:172-178``)."""
+    conds = _get(_get(node, "status"), "conditions")
+    if not conds or not isinstance(conds, list):
+        return False
+    for cond in conds:
+        if isinstance(cond, Mapping) and cond.get("type") == "Ready" and cond.get("status") == "True":
+            return True
+    return False
+
+
+def _taints(spec: Any) -> List[Dict[str, Any]]:
+    taints = _get(spec, "taints")
+    if not taints or not isinstance(taints, list):
+        return []
+    out = []
+    for t in taints:
+        if isinstance(t, Mapping):
+            out.append({"key": t.get("key"), "value": t.get("value"), "effect": t.get("effect")})
+    return out
+
+
+def project_node(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS,
+                 gpu_source: str = "capacity") -> Dict[str, Any]:
+    """Project one raw ``Node`` into the report dict (reference ``extract_node_info``, ``:199-212``).
+
+    ``gpu_source`` selects which status map the GPU counts come from.  The
+    reference reads ``capacity`` only (default, byte parity); the MI355X
+    preset reads ``allocatable``, i.e. what the ROCm device plugin reports as
+    usable after its own health checks.
+    """
+    meta = _get(node, "metadata")
+    status = _get(node, "status")
+    caps = gpu_breakdown(_get(status, gpu_source), keys)
+    labels = _get(meta, "labels") if meta else None
+    return {
+        "name": meta.get("name") if isinstance(meta, Mapping) else "",
+        "ready": is_ready(node),
+        "gpus": sum(caps.values()) if caps else 0,
+        "gpu_breakdown": caps,
+        "labels": labels if labels else {},
+        "taints": _taints(_get(node, "spec")),
+    }
+
+
+class NodeExtras:
+    """Side information the default report does not show but the health gate uses."""
+
+    __slots__ = ("ready_condition", "capacity", "allocatable", "unschedulable", "health_annotation")
+
+    def __init__(self, ready_condition: bool, capacity: Dict[str, int], allocatable: Dict[str, int],
+                 unschedulable: bool, health_annotation: Optional[str]):
+        self.ready_condition = ready_condition
+        self.capacity = capacity
+        self.allocatable = allocatable
+        self.unschedulable = unschedulable
+        self.health_annotation = health_annotation
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {
+            "ready_condition": self.ready_condition,
+            "capacity": self.capacity,
+            "allocatable": self.allocatable,
+            "unschedulable": self.unschedulable,
+        }
+
+
+def node_extras(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS) -> NodeExtras:
+    meta = _get(node, "metadata")
+    status = _get(node, "status")
+    ann = _get(meta, "annotations")
+    raw = ann.get(HEALTH_ANNOTATION) if isinstance(ann, Mapping) else None
+    return NodeExtras(
+        ready_condition=is_ready(node),
+        capacity=gpu_breakdown(_get(status, "capacity"), keys),
+        allocatable=gpu_breakdown(_get(status, "allocatable"), keys),
+        unschedulable=bool(_get(_get(node, "spec"), "unschedulable")),
+        health_annotation=raw if isinstance(raw, str) else None,
+    )
+
+
+class ScanResult:
+    """Outcome of one cluster scan (reference ``list_gpu_nodes`` return value, ``:215-226``).
+
+    ``gpu_nodes`` keeps API order; ``ready_gpu_nodes`` is the Ready subset.
+    ``extras`` is parallel to ``gpu_nodes`` and only filled when a consumer
+    (health gate, extended JSON) asked for it.
+    """
+
+    __slots__ = ("gpu_nodes", "ready_gpu_nodes", "extras", "items_seen")
+
+    def __init__(self) -> None:
+        self.gpu_nodes: List[Dict[str, Any]] = []
+        self.ready_gpu_nodes: List[Dict[str, Any]] = []
+        self.extras: List[NodeExtras] = []
+        self.items_seen = 0
+
+    def add(self, info: Dict[str, Any], extras: Optional[NodeExtras] = None) -> None:
+        self.items_seen += 1
+        if info["gpus"] > 0:
+            self.gpu_nodes.append(info)
+            if extras is not None:
+                self.extras.append(extras)
+            if info["ready"]:
+                self.ready_gpu_nodes.append(info)
+
+    def recompute_ready(self) -> None:
+        self.ready_gpu_nodes = [n for n in self.gpu_nodes if n["ready"]]
+
+    def exit_code(self) -> int:
+        """Reference exit-code contract (``:289-293``): 0 ready, 3 none ready, 2 no GPU nodes."""
+        if self.ready_gpu_nodes:
+            return 0
+        if self.gpu_nodes:
+            return 3
+        return 2
+
+
+def scan_items(items: Iterable[Mapping[str, Any]], result: Optional[ScanResult] = None,
+               keys: Sequence[str] = GPU_RESOURCE_KEYS, gpu_source: str = "capacity",
+               want_extras: bool = False) -> ScanResult:
+    """Pure-Python scan of decoded ``NodeList.items`` (reference ``:217-225``)."""
+    res = result if result is not None else ScanResult()
+    for n in items or ():
+        info = project_node(n, keys, gpu_source)
+        res.add(info, node_extras(n, keys) if want_extras else None)
+    return res
+
+
+def primary_gpu_count(extras: NodeExtras, source: str = "capacity") -> int:
+    table = extras.capacity if source == "capacity" else extras.allocatable
+    return table.get(PRIMARY_GPU_KEY, 0)

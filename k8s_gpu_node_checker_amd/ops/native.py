@@ -1,0 +1,74 @@
+"""Locate and load the in-tree native libraries built by :mod:`k8s_gpu_node_checker_amd.build`.
+
+All artefacts live in ``k8s_gpu_node_checker_amd/_native/`` (git-ignored,
+but shipped with the source tree to the GPU box).  Nothing is JIT-compiled
+into a user cache.
+
+* ``_fastpath*.so``      CPython extension: NodeList scanner + JSON emitter (CPU hot path)
+* ``libmi355x_probe.so`` C ABI over ``libamd_smi``: passive MI355X health probe
+* ``libmi355x_diag.so``  HIP/gfx950 kernels: active diagnostics (MFMA, HBM, memtest)
+"""
+
+from __future__ import annotations
+
+import ctypes
+import importlib.machinery
+import importlib.util
+import os
+import sys
+from typing import Dict, Optional
+
+NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
+
+_cache: Dict[str, object] = {}
+
+
+class NativeUnavailable(RuntimeError):
+    """Raised when a required native library is missing or fails to load."""
+
+
+def native_path(filename: str) -> str:
+    return os.path.join(NATIVE_DIR, filename)
+
+
+def load_extension(name: str):
+    """Import a CPython extension module from ``_native`` (returns ``None`` if absent)."""
+    key = "ext:" + name
+    if key in _cache:
+        return _cache[key]
+    mod = None
+    if os.environ.get("K8SGPU_DISABLE_NATIVE") != "1":
+        for suffix in importlib.machinery.EXTENSION_SUFFIXES:
+            path = os.path.join(NATIVE_DIR, name + suffix)
+            if os.path.exists(path):
+                spec = importlib.util.spec_from_file_location(name, path)
+                if spec is not None and spec.loader is not None:
+                    mod = importlib.util.module_from_spec(spec)
+                    spec.loader.exec_module(mod)  # type: ignore[union-attr]
+                    sys.modules.setdefault(name, mod)
+                break
+    _cache[key] = mod
+    return mod
+
+
+def load_cdll(filename: str, required: bool = False) -> Optional[ctypes.CDLL]:
+    """Load a C-ABI shared library from ``_native``; raise loudly when ``required``."""
+    key = "dll:" + filename
+    if key in _cache and _cache[key] is not None:
+        return _cache[key]  # type: ignore[return-value]
+    path = native_path(filename)
+    lib = None
+    err = None
+    if os.path.exists(path):
+        try:
+            lib = ctypes.CDLL(path, mode=getattr(os, "RTLD_NOW", 2) | ctypes.RTLD_GLOBAL)
+        except OSError as e:  # missing ROCm runtime, wrong arch, ...
+            err = e
+    else:
+        err = FileNotFoundError(path)
+    if lib is None and required:
+        raise NativeUnavailable(
+            f"native library {filename} not available ({err}); build it with "
+            f"`python -m k8s_gpu_node_checker_amd.build`")
+    _cache[key] = lib
+    return lib

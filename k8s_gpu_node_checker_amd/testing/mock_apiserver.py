@@ -1,0 +1,308 @@
+"""Mock kube-apiserver: ``GET/PATCH /api/v1/nodes`` over HTTP/1.1.
+
+The single ``list_node()`` call is the reference's only cluster seam
+(``check-gpu-node.py:217``); anything that serves a ``NodeList`` at
+``/api/v1/nodes`` is a complete fake cluster.  Features:
+
+* ``limit`` / ``continue`` pagination (pages pre-serialised and cached, so
+  the server's own JSON encoding does not pollute client-side timings)
+* ``GET /api/v1/nodes/{name}``, JSON merge-``PATCH`` of a node (the node
+  agent's annotation write)
+* bearer-token auth (401 on mismatch), TLS (given a cert/key)
+* fault injection: fixed status (``403``/``500``), ``fail_first`` transient
+  errors with ``Retry-After``, an expired-``continue`` 410, response delay,
+  connection reset
+* request log for assertions
+
+Run standalone (used by ``bench.py`` in its own process, so the client under
+test does not share a GIL with the server)::
+
+    python -m k8s_gpu_node_checker_amd.testing.mock_apiserver --nodes 8 --kind amd --port 0
+"""
+
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import socket
+import struct
+import sys
+import threading
+import time
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Any, Dict, List, Optional
+from urllib.parse import parse_qs, unquote, urlsplit
+
+from . import fixtures
+
+
+class ClusterState:
+    def __init__(self, nodes: List[Dict[str, Any]]):
+        self.lock = threading.Lock()
+        self.nodes = nodes
+        self.rv = 1000
+        self._cache: Dict[Any, bytes] = {}
+
+    def set_nodes(self, nodes: List[Dict[str, Any]]) -> None:
+        with self.lock:
+            self.nodes = nodes
+            self.rv += 1
+            self._cache.clear()
+
+    def page(self, limit: int, start: int) -> bytes:
+        key = (limit, start, self.rv)
+        with self.lock:
+            body = self._cache.get(key)
+            if body is None:
+                items = self.nodes[start:start + limit] if limit > 0 else self.nodes[start:]
+                nxt = start + len(items)
+                cont = f"c{nxt}.{self.rv}" if (limit > 0 and nxt < len(self.nodes)) else None
+                body = json.dumps(fixtures.node_list(items, cont, str(self.rv)), separators=(",", ":")).encode()
+                self._cache[key] = body
+            return body
+
+    def find(self, name: str) -> Optional[Dict[str, Any]]:
+        for n in self.nodes:
+            if (n.get("metadata") or {}).get("name") == name:
+                return n
+        return None
+
+    def patch(self, name: str, patch: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+        with self.lock:
+            node = self.find(name)
+            if node is None:
+                return None
+            _merge_patch(node, patch)
+            self.rv += 1
+            self._cache.clear()
+            return copy.deepcopy(node)
+
+
+def _merge_patch(target: Dict[str, Any], patch: Dict[str, Any]) -> None:
+    for k, v in patch.items():
+        if v is None:
+            target.pop(k, None)
+        elif isinstance(v, dict) and isinstance(target.get(k), dict):
+            _merge_patch(target[k], v)
+        else:
+            target[k] = copy.deepcopy(v)
+
+
+class MockConfig:
+    def __init__(self, token: Optional[str] = None, status: Optional[int] = None, fail_first: int = 0,
+                 fail_status: int = 503, retry_after: Optional[str] = None, delay: float = 0.0,
+                 expire_continue: bool = False, reset: bool = False):
+        self.token = token
+        self.status = status
+        self.fail_first = fail_first
+        self.fail_status = fail_status
+        self.retry_after = retry_after
+        self.delay = delay
+        self.expire_continue = expire_continue
+        self.reset = reset
+
+
+class _Handler(BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+    server: "MockApiServer"  # type: ignore[assignment]
+
+    def log_message(self, fmt: str, *args: Any) -> None:  # quiet
+        pass
+
+    def _send(self, status: int, body: bytes, extra: Optional[Dict[str, str]] = None,
+              reason: Optional[str] = None) -> None:
+        self.send_response(status, reason)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(body)))
+        self.send_header("Audit-Id", "00000000-0000-0000-0000-000000000000")
+        for k, v in (extra or {}).items():
+            self.send_header(k, v)
+        self.end_headers()
+        self.wfile.write(body)
+
+    def _status_body(self, code: int, reason: str, message: str) -> bytes:
+        return json.dumps({"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Failure",
+                           "message": message, "reason": reason, "code": code}).encode()
+
+    def _pre(self) -> bool:
+        srv = self.server
+        cfg = srv.cfg
+        srv.log.append({"method": self.command, "path": self.path,
+                        "auth": self.headers.get("Authorization"), "ts": time.time()})
+        if cfg.delay:
+            time.sleep(cfg.delay)
+        if cfg.reset:
+            self.connection.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+            self.close_connection = True
+            self.connection.close()
+            return False
+        if cfg.token is not None and self.headers.get("Authorization") != f"Bearer {cfg.token}":
+            self._send(401, self._status_body(401, "Unauthorized", "Unauthorized"), reason="Unauthorized")
+            return False
+        if cfg.status is not None:
+            msg = 'nodes is forbidden: User "system:anonymous" cannot list resource "nodes" in API group "" at the cluster scope' \
+                if cfg.status == 403 else "internal error"
+            reason = {403: "Forbidden", 500: "Internal Server Error", 404: "Not Found"}.get(cfg.status, "Error")
+            self._send(cfg.status, self._status_body(cfg.status, reason.replace(" ", ""), msg), reason=reason)
+            return False
+        with srv.lock:
+            failing = srv.failures_left > 0
+            if failing:
+                srv.failures_left -= 1
+        if failing:
+            extra = {"Retry-After": cfg.retry_after} if cfg.retry_after else None
+            self._send(cfg.fail_status, self._status_body(cfg.fail_status, "ServiceUnavailable", "try again"), extra)
+            return False
+        return True
+
+    def do_GET(self) -> None:  # noqa: N802
+        if not self._pre():
+            return
+        parts = urlsplit(self.path)
+        path = parts.path
+        if path == "/api/v1/nodes":
+            q = parse_qs(parts.query)
+            limit = int(q.get("limit", ["0"])[0] or 0)
+            cont = q.get("continue", [None])[0]
+            start = 0
+            if cont:
+                if self.server.cfg.expire_continue:
+                    self._send(410, self._status_body(410, "Expired", "The provided continue parameter is too old"),
+                               reason="Gone")
+                    return
+                try:
+                    start = int(cont[1:].split(".")[0])
+                except ValueError:
+                    self._send(400, self._status_body(400, "BadRequest", "invalid continue token"))
+                    return
+            self._send(200, self.server.state.page(limit, start))
+            return
+        if path.startswith("/api/v1/nodes/"):
+            node = self.server.state.find(unquote(path[len("/api/v1/nodes/"):]))
+            if node is None:
+                self._send(404, self._status_body(404, "NotFound", "node not found"), reason="Not Found")
+            else:
+                self._send(200, json.dumps(node).encode())
+            return
+        if path in ("/healthz", "/readyz", "/livez"):
+            self._send(200, b"ok")
+            return
+        self._send(404, self._status_body(404, "NotFound", "not found"), reason="Not Found")
+
+    def do_PATCH(self) -> None:  # noqa: N802
+        length = int(self.headers.get("Content-Length") or 0)
+        body = self.rfile.read(length) if length else b""
+        if not self._pre():
+            return
+        path = urlsplit(self.path).path
+        if not path.startswith("/api/v1/nodes/"):
+            self._send(404, self._status_body(404, "NotFound", "not found"), reason="Not Found")
+            return
+        try:
+            patch = json.loads(body or b"{}")
+        except ValueError:
+            self._send(400, self._status_body(400, "BadRequest", "invalid patch"))
+            return
+        node = self.server.state.patch(unquote(path[len("/api/v1/nodes/"):]), patch)
+        if node is None:
+            self._send(404, self._status_body(404, "NotFound", "node not found"), reason="Not Found")
+        else:
+            self._send(200, json.dumps(node).encode())
+
+
+class MockApiServer(ThreadingHTTPServer):
+    daemon_threads = True
+    allow_reuse_address = True
+    request_queue_size = 256
+
+    def __init__(self, nodes: List[Dict[str, Any]], host: str = "127.0.0.1", port: int = 0,
+                 cfg: Optional[MockConfig] = None, certfile: Optional[str] = None, keyfile: Optional[str] = None):
+        super().__init__((host, port), _Handler)
+        self.state = ClusterState(nodes)
+        self.cfg = cfg or MockConfig()
+        self.lock = threading.Lock()
+        self.failures_left = self.cfg.fail_first
+        self.log: List[Dict[str, Any]] = []
+        self.scheme = "http"
+        if certfile:
+            import ssl
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(certfile, keyfile)
+            self.socket = ctx.wrap_socket(self.socket, server_side=True)
+            self.scheme = "https"
+        self._thread: Optional[threading.Thread] = None
+
+    @property
+    def url(self) -> str:
+        host, port = self.server_address[:2]
+        return f"{self.scheme}://{host}:{port}"
+
+    def start(self) -> "MockApiServer":
+        self._thread = threading.Thread(target=self.serve_forever, kwargs={"poll_interval": 0.05}, daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self.shutdown()
+        self.server_close()
+
+    def __enter__(self) -> "MockApiServer":
+        return self.start()
+
+    def __exit__(self, *exc: Any) -> None:
+        self.stop()
+
+    def kubeconfig(self, path: str, token: Optional[str] = None, extra_cluster: Optional[Dict[str, Any]] = None) -> str:
+        return write_kubeconfig(path, self.url, token if token is not None else self.cfg.token, extra_cluster)
+
+
+def write_kubeconfig(path: str, server: str, token: Optional[str] = None,
+                     extra_cluster: Optional[Dict[str, Any]] = None, fmt: str = "yaml") -> str:
+    cluster: Dict[str, Any] = {"server": server}
+    if extra_cluster:
+        cluster.update(extra_cluster)
+    user: Dict[str, Any] = {"token": token} if token else {}
+    cfg = {"apiVersion": "v1", "kind": "Config", "current-context": "mock",
+           "clusters": [{"name": "mock", "cluster": cluster}],
+           "contexts": [{"name": "mock", "context": {"cluster": "mock", "user": "mock-user"}}],
+           "users": [{"name": "mock-user", "user": user}]}
+    with open(path, "w", encoding="utf-8") as f:
+        if fmt == "json":
+            json.dump(cfg, f)
+        else:
+            import yaml
+            yaml.safe_dump(cfg, f)
+    return path
+
+
+def build_nodes(n: int, kind: str, not_ready: int = 0, with_health: bool = False,
+                gpus_per_node: int = 8) -> List[Dict[str, Any]]:
+    return fixtures.cluster(n, kind, not_ready=range(not_ready), with_health=with_health, gpus_per_node=gpus_per_node)
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    ap = argparse.ArgumentParser(description="mock kube-apiserver for k8s-gpu-node-checker-amd")
+    ap.add_argument("--nodes", type=int, default=8)
+    ap.add_argument("--kind", default="amd", choices=("amd", "nvidia", "mixed", "cpu"))
+    ap.add_argument("--not-ready", type=int, default=0)
+    ap.add_argument("--gpus-per-node", type=int, default=8)
+    ap.add_argument("--with-health", action="store_true")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--token")
+    ap.add_argument("--golden", help="serve a golden fixture instead of a generated cluster")
+    args = ap.parse_args(argv)
+    nodes = fixtures.golden(args.golden) if args.golden else build_nodes(
+        args.nodes, args.kind, args.not_ready, args.with_health, args.gpus_per_node)
+    srv = MockApiServer(nodes, args.host, args.port, MockConfig(token=args.token))
+    print(json.dumps({"url": srv.url, "port": srv.server_address[1], "nodes": len(nodes)}), flush=True)
+    try:
+        srv.serve_forever(poll_interval=0.2)
+    except KeyboardInterrupt:
+        pass
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,134 @@
+"""Slack-webhook sink with fault injection.
+
+The URL path selects the behaviour, so one sink serves every test:
+
+==============  =============================================================
+``/200``        ``200 ok``
+``/500``        ``500 server_error``
+``/204``        ``204`` (not a success for the reference, ``:79``)
+``/404``        ``404 no_service`` (revoked webhook)
+``/429``        ``429 rate_limited`` with ``Retry-After: 1``
+``/flakyN``     ``500`` N times (per sink), then ``200``
+``/reset``      TCP RST on every attempt (``SO_LINGER {1,0}``)
+``/resetflaky`` RST once, then ``200``
+``/slow``       sleep ``slow_s`` (default 11 s) before answering ``200``
+``/close``      close without a response ("Remote end closed connection")
+==============  =============================================================
+
+Every request is logged (path, headers, body) for assertions.
+"""
+
+from __future__ import annotations
+
+import json
+import socket
+import socketserver
+import struct
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+
+class _SinkHandler(socketserver.BaseRequestHandler):
+    server: "WebhookSink"  # type: ignore[assignment]
+
+    def _read_request(self) -> Optional[Dict[str, Any]]:
+        sock: socket.socket = self.request
+        data = b""
+        while b"\r\n\r\n" not in data:
+            chunk = sock.recv(65536)
+            if not chunk:
+                return None
+            data += chunk
+        head, _, rest = data.partition(b"\r\n\r\n")
+        lines = head.decode("latin-1").split("\r\n")
+        method, path, _ = lines[0].split(" ", 2)
+        headers = {}
+        for line in lines[1:]:
+            k, _, v = line.partition(":")
+            headers[k.strip()] = v.strip()
+        n = int(headers.get("Content-Length", "0") or 0)
+        while len(rest) < n:
+            chunk = sock.recv(65536)
+            if not chunk:
+                break
+            rest += chunk
+        return {"method": method, "path": path, "headers": headers, "body": rest[:n], "ts": time.time()}
+
+    def _respond(self, status: int, reason: str, body: bytes, extra: str = "") -> None:
+        msg = (f"HTTP/1.1 {status} {reason}\r\nContent-Type: text/plain\r\nContent-Length: {len(body)}\r\n"
+               f"{extra}Connection: close\r\n\r\n").encode() + body
+        self.request.sendall(msg)
+
+    def handle(self) -> None:
+        req = self._read_request()
+        if req is None:
+            return
+        srv = self.server
+        with srv.lock:
+            srv.requests.append(req)
+            count = srv.counts.get(req["path"], 0) + 1
+            srv.counts[req["path"]] = count
+        path = req["path"].split("?", 1)[0]
+        if path == "/reset" or (path == "/resetflaky" and count == 1):
+            self.request.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+            self.request.close()
+            return
+        if path == "/close":
+            self.request.close()
+            return
+        if path == "/slow":
+            time.sleep(srv.slow_s)
+        if path.startswith("/flaky"):
+            n = int(path[6:] or 2)
+            if count <= n:
+                self._respond(500, "Internal Server Error", b"server_error")
+                return
+            self._respond(200, "OK", b"ok")
+            return
+        table = {"/200": (200, "OK", b"ok", ""), "/500": (500, "Internal Server Error", b"server_error", ""),
+                 "/204": (204, "No Content", b"", ""), "/404": (404, "Not Found", b"no_service", ""),
+                 "/429": (429, "Too Many Requests", b"rate_limited", "Retry-After: 1\r\n"),
+                 "/slow": (200, "OK", b"ok", ""), "/resetflaky": (200, "OK", b"ok", "")}
+        status, reason, body, extra = table.get(path, (404, "Not Found", b"no_such_mode", ""))
+        if status == 204:
+            self.request.sendall(f"HTTP/1.1 204 No Content\r\n{extra}Connection: close\r\n\r\n".encode())
+            return
+        self._respond(status, reason, body, extra)
+
+
+class WebhookSink(socketserver.ThreadingTCPServer):
+    daemon_threads = True
+    allow_reuse_address = True
+
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, slow_s: float = 11.0):
+        super().__init__((host, port), _SinkHandler)
+        self.lock = threading.Lock()
+        self.requests: List[Dict[str, Any]] = []
+        self.counts: Dict[str, int] = {}
+        self.slow_s = slow_s
+
+    @property
+    def base_url(self) -> str:
+        host, port = self.server_address[:2]
+        return f"http://{host}:{port}"
+
+    def url(self, mode: str) -> str:
+        return f"{self.base_url}/{mode.lstrip('/')}"
+
+    def payloads(self) -> List[Dict[str, Any]]:
+        return [json.loads(r["body"]) for r in self.requests if r["body"]]
+
+    def start(self) -> "WebhookSink":
+        threading.Thread(target=self.serve_forever, kwargs={"poll_interval": 0.05}, daemon=True).start()
+        return self
+
+    def stop(self) -> None:
+        self.shutdown()
+        self.server_close()
+
+    def __enter__(self) -> "WebhookSink":
+        return self.start()
+
+    def __exit__(self, *exc: Any) -> None:
+        self.stop()

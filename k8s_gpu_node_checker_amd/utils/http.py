@@ -1,0 +1,327 @@
+"""Minimal HTTP/1.1 client on raw sockets (+ ``ssl``): the checker's only transport.
+
+Why not ``requests``/``urllib3``/``aiohttp``: at 1-16 nodes the reference's
+process wall clock is ~95 % interpreter + import cost (``import
+requests`` 138 ms, ``aiohttp`` 310 ms).  This module imports only ``socket``
+(and ``ssl`` for https, ``zlib`` for gzip) and reads bodies with
+``recv_into`` a pre-sized buffer, so a 5.9 MB NodeList is one allocation.
+
+Features: keep-alive connection reuse, ``Content-Length`` / chunked /
+close-delimited bodies, ``gzip`` content coding, connect/read timeouts, an
+HTTP ``CONNECT`` proxy for https and absolute-form requests for http proxies.
+
+Errors are :class:`HTTPError` with a ``kind`` (``refused``, ``reset``,
+``aborted``, ``timeout``, ``connect_timeout``, ``dns``, ``tls``,
+``protocol``) and a message shaped like the one ``requests`` prints for the
+same failure, because the reference's Slack retry policy keys on that text
+(``check-gpu-node.py:88``).
+"""
+
+from __future__ import annotations
+
+import errno
+import socket
+from typing import Dict, List, Optional, Tuple
+from urllib.parse import urlsplit
+
+_DEFAULT_PORTS = {"http": 80, "https": 443}
+
+
+class HTTPError(Exception):
+    def __init__(self, kind: str, message: str, cause: Optional[BaseException] = None):
+        super().__init__(message)
+        self.kind = kind
+        self.cause = cause
+
+    @property
+    def retryable_reset(self) -> bool:
+        """Matches the reference's "Connection reset by peer" / "Connection aborted" test."""
+        return self.kind in ("reset", "aborted")
+
+
+class Response:
+    __slots__ = ("status", "reason", "headers", "body")
+
+    def __init__(self, status: int, reason: str, headers: List[Tuple[str, str]], body: bytes):
+        self.status = status
+        self.reason = reason
+        self.headers = headers
+        self.body = body
+
+    def header(self, name: str, default: Optional[str] = None) -> Optional[str]:
+        name = name.lower()
+        for k, v in self.headers:
+            if k.lower() == name:
+                return v
+        return default
+
+    def header_dict(self) -> Dict[str, str]:
+        return {k: v for k, v in self.headers}
+
+    @property
+    def text(self) -> str:
+        return self.body.decode("utf-8", "replace")
+
+
+def _pool_name(scheme: str, host: str, port: int) -> str:
+    pool = "HTTPSConnectionPool" if scheme == "https" else "HTTPConnectionPool"
+    return f"{pool}(host='{host}', port={port})"
+
+
+class Connection:
+    """One persistent HTTP/1.1 connection to ``scheme://host:port``."""
+
+    def __init__(self, url: str, timeout: float = 30.0, ssl_context=None, server_hostname: Optional[str] = None,
+                 proxy_url: Optional[str] = None):
+        parts = urlsplit(url)
+        self.scheme = parts.scheme or "http"
+        self.host = parts.hostname or "localhost"
+        self.port = parts.port or _DEFAULT_PORTS.get(self.scheme, 80)
+        self.base_path = parts.path.rstrip("/")
+        self.timeout = timeout
+        self.ssl_context = ssl_context
+        self.server_hostname = server_hostname or self.host
+        self.proxy = urlsplit(proxy_url) if proxy_url else None
+        self.sock: Optional[socket.socket] = None
+        self._buf = bytearray()
+        host_hdr = self.host if ":" not in self.host else f"[{self.host}]"
+        if self.port != _DEFAULT_PORTS.get(self.scheme):
+            host_hdr += f":{self.port}"
+        self.host_header = host_hdr
+
+    # -- connection management ------------------------------------------------
+    def _fail(self, kind: str, url: str, e: BaseException) -> HTTPError:
+        pool = _pool_name(self.scheme, self.host, self.port)
+        if kind in ("reset", "aborted"):
+            msg = f"('Connection aborted.', {e!r})"
+        elif kind == "timeout":
+            msg = f"{pool}: Read timed out. (read timeout={self.timeout:g})"
+        elif kind == "connect_timeout":
+            msg = (f"{pool}: Max retries exceeded with url: {url} (Caused by ConnectTimeoutError("
+                   f"'Connection to {self.host} timed out. (connect timeout={self.timeout:g})'))")
+        elif kind in ("refused", "dns"):
+            msg = (f"{pool}: Max retries exceeded with url: {url} (Caused by NewConnectionError("
+                   f"'Failed to establish a new connection: {e}'))")
+        elif kind == "tls":
+            msg = f"{pool}: Max retries exceeded with url: {url} (Caused by SSLError({e!r}))"
+        else:
+            msg = f"{pool}: {e}"
+        return HTTPError(kind, msg, e)
+
+    def connect(self, url: str = "/") -> None:
+        if self.sock is not None:
+            return
+        target = (self.proxy.hostname, self.proxy.port or 80) if self.proxy else (self.host, self.port)
+        try:
+            sock = socket.create_connection(target, timeout=self.timeout)
+        except socket.timeout as e:
+            raise self._fail("connect_timeout", url, e)
+        except socket.gaierror as e:
+            raise self._fail("dns", url, e)
+        except ConnectionRefusedError as e:
+            raise self._fail("refused", url, e)
+        except OSError as e:
+            raise self._fail("refused" if e.errno in (errno.ECONNREFUSED, errno.EHOSTUNREACH,
+                                                      errno.ENETUNREACH) else "aborted", url, e)
+        sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        try:
+            if self.proxy and self.scheme == "https":
+                self._tunnel(sock)
+            if self.scheme == "https":
+                ctx = self.ssl_context
+                if ctx is None:
+                    import ssl
+                    ctx = ssl.create_default_context()
+                sock = ctx.wrap_socket(sock, server_hostname=self.server_hostname)
+        except HTTPError:
+            sock.close()
+            raise
+        except OSError as e:
+            sock.close()
+            raise self._fail("tls", url, e)
+        self.sock = sock
+        self._buf = bytearray()
+
+    def _tunnel(self, sock: socket.socket) -> None:
+        req = (f"CONNECT {self.host}:{self.port} HTTP/1.1\r\nHost: {self.host}:{self.port}\r\n\r\n").encode()
+        sock.sendall(req)
+        data = b""
+        while b"\r\n\r\n" not in data:
+            chunk = sock.recv(4096)
+            if not chunk:
+                raise HTTPError("protocol", "proxy closed the CONNECT tunnel")
+            data += chunk
+        first = data.split(b"\r\n", 1)[0]
+        status = first.split()
+        if len(status) < 2 or status[1] != b"200":
+            raise HTTPError("protocol", "proxy CONNECT failed: " + first.decode(errors="replace"))
+
+    def close(self) -> None:
+        if self.sock is not None:
+            try:
+                self.sock.close()
+            except OSError:
+                pass
+            self.sock = None
+
+    # -- request/response -----------------------------------------------------
+    def _recv_more(self) -> bool:
+        assert self.sock is not None
+        chunk = self.sock.recv(262144)
+        if not chunk:
+            return False
+        self._buf += chunk
+        return True
+
+    def _read_exact(self, n: int):
+        buf = self._buf
+        if len(buf) >= n:
+            out = bytes(buf[:n])
+            del buf[:n]
+            return out
+        out = bytearray(n)
+        view = memoryview(out)
+        have = len(buf)
+        view[:have] = buf
+        self._buf = bytearray()
+        sock = self.sock
+        assert sock is not None
+        while have < n:
+            got = sock.recv_into(view[have:], n - have)
+            if not got:
+                raise HTTPError("aborted", "('Connection aborted.', RemoteDisconnected("
+                                           "'Remote end closed connection without response'))")
+            have += got
+        return out  # bytearray: json.loads and the native scanner take it without a copy
+
+    def _read_line(self) -> bytes:
+        while True:
+            i = self._buf.find(b"\r\n")
+            if i >= 0:
+                line = bytes(self._buf[:i])
+                del self._buf[:i + 2]
+                return line
+            if not self._recv_more():
+                raise HTTPError("aborted", "('Connection aborted.', RemoteDisconnected("
+                                           "'Remote end closed connection without response'))")
+
+    def request(self, method: str, path: str, headers: Optional[Dict[str, str]] = None,
+                body: Optional[bytes] = None) -> Response:
+        url = path
+        req_target = self.base_path + path
+        if self.proxy and self.scheme == "http":
+            req_target = f"http://{self.host_header}{req_target}"
+        lines = [f"{method} {req_target} HTTP/1.1", f"Host: {self.host_header}"]
+        hdrs = headers or {}
+        for k, v in hdrs.items():
+            lines.append(f"{k}: {v}")
+        if body is not None:
+            lines.append(f"Content-Length: {len(body)}")
+        raw = ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
+        if body:
+            raw += body
+        reused = self.sock is not None
+        try:
+            self.connect(url)
+            assert self.sock is not None
+            self.sock.sendall(raw)
+            return self._read_response(method)
+        except HTTPError as e:
+            self.close()
+            if reused and e.kind in ("aborted", "reset"):
+                # stale keep-alive socket: one transparent reconnect (idempotent callers only)
+                self.connect(url)
+                assert self.sock is not None
+                self.sock.sendall(raw)
+                return self._read_response(method)
+            raise
+        except socket.timeout as e:
+            self.close()
+            raise self._fail("timeout", url, e)
+        except ConnectionResetError as e:
+            self.close()
+            raise self._fail("reset", url, e)
+        except (BrokenPipeError, ConnectionAbortedError) as e:
+            self.close()
+            raise self._fail("aborted", url, e)
+        except OSError as e:
+            self.close()
+            if e.__class__.__name__.startswith("SSL"):
+                raise self._fail("tls", url, e)
+            raise self._fail("aborted", url, e)
+
+    def _read_response(self, method: str) -> Response:
+        while True:
+            status_line = self._read_line()
+            parts = status_line.split(None, 2)
+            if len(parts) < 2 or not parts[0].startswith(b"HTTP/"):
+                raise HTTPError("protocol", f"bad status line {status_line[:80]!r}")
+            status = int(parts[1])
+            reason = parts[2].decode("latin-1") if len(parts) > 2 else ""
+            headers: List[Tuple[str, str]] = []
+            while True:
+                line = self._read_line()
+                if not line:
+                    break
+                k, _, v = line.partition(b":")
+                headers.append((k.decode("latin-1").strip(), v.decode("latin-1").strip()))
+            if 100 <= status < 200 and status != 101:
+                continue  # 100-continue / 103 early hints: read the real response
+            break
+        hmap = {k.lower(): v for k, v in headers}
+        if method == "HEAD" or status in (204, 304):
+            body = b""
+        elif "chunked" in hmap.get("transfer-encoding", "").lower():
+            body = self._read_chunked()
+        elif "content-length" in hmap:
+            body = self._read_exact(int(hmap["content-length"]))
+        else:
+            chunks = [bytes(self._buf)]
+            self._buf = bytearray()
+            assert self.sock is not None
+            while True:
+                c = self.sock.recv(262144)
+                if not c:
+                    break
+                chunks.append(c)
+            body = b"".join(chunks)
+            self.close()
+        if hmap.get("content-encoding", "").lower() == "gzip" and body:
+            import zlib
+            body = zlib.decompress(body, 16 + zlib.MAX_WBITS)
+        if hmap.get("connection", "").lower() == "close":
+            self.close()
+        return Response(status, reason, headers, body)
+
+    def _read_chunked(self) -> bytes:
+        out = []
+        while True:
+            size_line = self._read_line()
+            size = int(size_line.split(b";", 1)[0].strip() or b"0", 16)
+            if size == 0:
+                while self._read_line():  # trailers
+                    pass
+                return b"".join(out)
+            out.append(self._read_exact(size))
+            self._read_line()
+
+
+def request(url: str, method: str = "GET", headers: Optional[Dict[str, str]] = None, body: Optional[bytes] = None,
+            timeout: float = 30.0, ssl_context=None) -> Response:
+    """One-shot request on a fresh connection."""
+    parts = urlsplit(url)
+    if parts.scheme not in ("http", "https"):
+        if not parts.scheme:
+            raise HTTPError("invalid_url", f"Invalid URL '{url}': No scheme supplied. Perhaps you meant https://{url}?")
+        raise HTTPError("invalid_url", f"No connection adapters were found for '{url}'")
+    if not parts.hostname:
+        raise HTTPError("invalid_url", f"Invalid URL '{url}': No host supplied")
+    base = f"{parts.scheme}://{parts.netloc}"
+    path = parts.path or "/"
+    if parts.query:
+        path += "?" + parts.query
+    conn = Connection(base, timeout=timeout, ssl_context=ssl_context)
+    try:
+        return conn.request(method, path, headers, body)
+    finally:
+        conn.close()

@@ -1,0 +1,84 @@
+"""Alert de-duplication state (SURVEY §5 "Checkpoint / resume": the reference is stateless).
+
+Under cron (reference ``README.md:188-189``) every failing run re-alerts and a
+recovery is never announced.  With ``--state-file PATH --slack-on-change`` the
+checker remembers the previous outcome and only notifies when it changes:
+
+* a different exit code or a different set of (node, ready) pairs -> send;
+* with ``--slack-only-on-error``: send on a change *into* an error state, and
+  once more on the recovery back to exit 0.
+
+Without ``--slack-on-change`` the file is still written (last outcome, for
+dashboards) and Slack behaves exactly like the reference.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import tempfile
+import time
+from typing import Any, Dict, Optional
+
+
+def fingerprint(result: Any) -> str:
+    h = hashlib.sha256()
+    h.update(str(result.exit_code).encode())
+    for n in result.gpu_nodes:
+        h.update(f"\0{n['name']}\0{n['ready']}\0{n['gpus']}".encode())
+    return h.hexdigest()[:16]
+
+
+def load(path: str) -> Optional[Dict[str, Any]]:
+    try:
+        with open(path, encoding="utf-8") as f:
+            doc = json.load(f)
+        return doc if isinstance(doc, dict) else None
+    except (OSError, ValueError):
+        return None
+
+
+def save(path: str, result: Any, prev: Optional[Dict[str, Any]] = None) -> None:
+    doc = {
+        "version": 1,
+        "ts": time.time(),
+        "exit_code": result.exit_code,
+        "fingerprint": fingerprint(result),
+        "total_nodes": len(result.gpu_nodes),
+        "ready_nodes": len(result.ready_gpu_nodes),
+        "not_ready": [n["name"] for n in result.gpu_nodes if not n["ready"]],
+        "slack_sent": result.slack_sent,
+        "runs": (prev or {}).get("runs", 0) + 1,
+    }
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(prefix=".state-", dir=d)
+    with os.fdopen(fd, "w", encoding="utf-8") as f:
+        json.dump(doc, f, ensure_ascii=False, indent=2)
+    os.replace(tmp, path)
+
+
+def should_notify(prev: Optional[Dict[str, Any]], result: Any, only_on_error: bool) -> bool:
+    fp = fingerprint(result)
+    if prev is not None and prev.get("fingerprint") == fp:
+        return False
+    if not only_on_error:
+        return True
+    if result.exit_code != 0:
+        return True
+    return prev is not None and prev.get("exit_code", 0) != 0  # recovery
+
+
+def gate_webhook(prev: Optional[Dict[str, Any]], opts: Any, cluster: Any) -> Optional[str]:
+    """Install a de-dup gate on ``opts``; returns the (unchanged) webhook flag value."""
+    only = opts.slack_only_on_error
+
+    def gate(result: Any) -> bool:
+        return should_notify(prev, result, only)
+
+    opts.slack_gate = gate
+    if only:
+        # the gate decides (recoveries must be able to send although Ready > 0)
+        opts.slack_only_on_error = False
+    return opts.slack_webhook
