@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Headline benchmark: end-to-end GPU-node check latency + nodes/s against a mock kube-apiserver.
+
+Metric of record (BASELINE.json): "end-to-end check latency (ms) + nodes/sec,
+mock kube-API at 1/2/4/8 GPU nodes".  One rank per GPU; GPU ``r`` *is* cluster
+node ``mi355x-node-r`` (``amd.com/gpu: 1``), so the cluster grows with the
+job (weak scaling: fixed work per GPU).
+
+Setup (untimed)
+  * rank 0 starts the mock kube-apiserver in its own process (before any GPU
+    work) serving N realistic ~5.9 KB Node objects;
+  * every rank runs the MI355X node agent on its own GPU: native amd-smi probe
+    (``libmi355x_probe.so``) + level-1 HIP diagnostics (``libmi355x_diag.so``:
+    MFMA bf16 GEMM with fp32-reference check, HBM bandwidth) and PATCHes the
+    ``amd.com/mi355x-health`` annotation of its node over HTTP.
+
+Timed step (rank 0, identical to ``check-gpu-node --json``; other ranks wait at
+the closing barrier):  fresh TCP connection -> paginated ``GET
+/api/v1/nodes`` -> native NodeList scan -> MI355X health gate on every node's
+annotation -> JSON report rendered -> exit code.  Nothing is cached between
+steps.  ``--mode sweep`` additionally re-probes every GPU and re-PATCHes its
+annotation inside each step.
+
+Prints ONE JSON line (rank 0): value = nodes/s over the whole job.
+"""
+
+from __future__ import annotations
+
+import argparse
+import io
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# reference in-process one_shot median (ms, no Slack) at N GPU nodes
+REF_MS = {1: 2.17, 2: 1.68, 4: 1.74, 8: 2.30, 16: 2.23, 1000: 92.7}
+REF_MS_SLACK = {1: 4.43, 2: 4.02, 4: 3.08, 8: 3.08, 16: 3.57, 1000: 86.1}
+
+
+def _spawn(module: str, *args: str) -> "tuple[subprocess.Popen, dict]":
+    env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    proc = subprocess.Popen([sys.executable, "-m", module, *args], stdout=subprocess.PIPE, env=env, text=True)
+    assert proc.stdout is not None
+    line = proc.stdout.readline()
+    if not line:
+        raise RuntimeError(f"{module} failed to start")
+    return proc, json.loads(line)
+
+
+def _pctl(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    i = min(len(xs) - 1, max(0, int(round(q * (len(xs) - 1)))))
+    return xs[i]
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--nodes", type=int, default=0, help="cluster size override (default: one node per GPU)")
+    ap.add_argument("--mode", choices=("check", "sweep"), default="check")
+    ap.add_argument("--diag-level", type=int, default=1, choices=(0, 1, 2))
+    ap.add_argument("--slack", action="store_true", help="also POST the Slack report to a local sink each step")
+    ap.add_argument("--page-size", type=int, default=500)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = world if world > 1 else args.gpus
+    n_nodes = args.nodes or n_gpus
+
+    # --- control-plane processes first: nothing below has touched the GPU yet
+    procs = []
+    ctrl = {}
+    if rank == 0:
+        p, info = _spawn("k8s_gpu_node_checker_amd.testing.mock_apiserver", "--nodes", str(n_nodes), "--kind", "amd",
+                         "--gpus-per-node", "1")
+        procs.append(p)
+        ctrl["api"] = info["url"]
+        if args.slack:
+            p, sinfo = _spawn("k8s_gpu_node_checker_amd.testing.webhook_sink")
+            procs.append(p)
+            ctrl["slack"] = sinfo["url"] + "/200"
+    try:
+        return _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl)
+    finally:
+        for p in procs:
+            p.terminate()
+            try:
+                p.wait(timeout=5)
+            except subprocess.TimeoutExpired:
+                p.kill()
+
+
+def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
+    import torch
+    import torch.distributed as dist
+
+    from k8s_gpu_node_checker_amd.agent.agent import Agent
+    from k8s_gpu_node_checker_amd.checker import CheckOptions, check_and_report
+    from k8s_gpu_node_checker_amd.kube.client import KubeClient
+    from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+    from k8s_gpu_node_checker_amd.ops import fastpath
+    from k8s_gpu_node_checker_amd.testing import fixtures
+
+    cuda = torch.cuda.is_available()
+    if cuda:
+        torch.cuda.set_device(local_rank)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl" if cuda else "gloo")
+        group = dist.new_group(backend="gloo")  # control-plane objects (URLs, reports)
+        box = [ctrl]
+        dist.broadcast_object_list(box, src=0, group=group)
+        ctrl = box[0]
+
+    def barrier():
+        if world > 1:
+            if cuda:
+                dist.barrier(device_ids=[local_rank])
+            else:
+                dist.barrier()
+        if cuda:
+            torch.cuda.synchronize()
+
+    cluster = ClusterConnection(ctrl["api"])
+    node = f"mi355x-node-{rank:04d}"
+
+    # --- node agent on this rank's GPU: probe (+ diagnostics), publish annotation
+    agent = Agent(node, source="auto", diag_level=args.diag_level if cuda else 0,
+                  devices=[local_rank] if cuda else [])
+    t0 = time.perf_counter()
+    rep = agent.probe_once()
+    probe_source = rep.get("probe")
+    if rep.get("error") or not rep.get("gpus"):
+        # no amdgpu driver (CPU CI): publish a recorded MI355X report instead, and say so
+        rep = fixtures.mi355x_probe_report(node, gpus=1)
+        probe_source = "fixture"
+    else:
+        gpus = rep["gpus"]
+        if len(gpus) > 1:  # amd-smi sees every GPU of the host: keep this rank's
+            rep["gpus"] = [g for g in gpus if g.get("index") == local_rank] or gpus[:1]
+            rep["gpus"][0]["index"] = 0
+    probe_ms = (time.perf_counter() - t0) * 1e3
+    with KubeClient(cluster) as kc:
+        agent.publish_annotation(kc, rep)
+        if rank == 0 and n_nodes > n_gpus:  # --nodes > GPUs: the extra nodes get a copy of rank 0's report
+            for i in range(n_gpus, n_nodes):
+                r2 = dict(rep, node=f"mi355x-node-{i:04d}")
+                kc.patch_node_annotations(f"mi355x-node-{i:04d}", agent.annotation(r2))
+    diag = {}
+    for g in rep.get("gpus") or []:
+        diag = g.get("diag") or {}
+    barrier()
+
+    opts = CheckOptions(json=True, page_size=args.page_size, health_policy="auto",
+                        slack_webhook=ctrl.get("slack"), slack_retry_policy="backoff")
+    sink_out, sink_err = io.StringIO(), io.StringIO()
+
+    def step():
+        if args.mode == "sweep":
+            r = agent.probe_once() if probe_source != "fixture" else fixtures.mi355x_probe_report(node, gpus=1)
+            if len(r.get("gpus") or []) > 1:
+                r["gpus"] = [g for g in r["gpus"] if g.get("index") == local_rank] or r["gpus"][:1]
+            with KubeClient(cluster) as kc2:
+                agent.publish_annotation(kc2, r)
+            barrier()
+        if rank == 0:
+            sink_out.seek(0)
+            sink_out.truncate()
+            res = check_and_report(cluster, opts, out=sink_out, err=sink_err)
+            return res
+        return None
+
+    last = None
+    for _ in range(args.warmup):
+        last = step()
+    barrier()
+    lat = []
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        s = time.perf_counter()
+        last = step()
+        lat.append(time.perf_counter() - s)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+
+    if world > 1:
+        import torch as _t
+        t = _t.tensor([elapsed], dtype=_t.float64, device=f"cuda:{local_rank}" if cuda else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        ok = last is not None and last.exit_code == 0 and len(last.ready_gpu_nodes) == n_nodes
+        verdicts = [v.state for v in (last.verdicts or []) if v is not None] if last else []
+        ms = elapsed / max(args.steps, 1) * 1e3
+        value = n_nodes * args.steps / elapsed
+        ref = (REF_MS_SLACK if args.slack else REF_MS).get(n_nodes)
+        vs = round(value / (n_nodes / (ref / 1e3)), 3) if ref else None
+        node_bytes = len(json.dumps(fixtures.realistic_node("x", "amd.com/gpu", 1), separators=(",", ":")))
+        out = {
+            "metric": "end-to-end GPU-node check throughput (nodes/s) against a mock kube-apiserver; "
+                      "ms_per_step = check latency",
+            "value": round(value, 2),
+            "unit": "nodes/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": vs,
+            "dtype": "n/a (control plane; agent diagnostics bf16 MFMA)",
+            "data": "synthetic: mock kube-apiserver, realistic Node objects, live MI355X probe annotations"
+                    if probe_source != "fixture" else "synthetic: mock kube-apiserver, fixture probe annotations (no GPU)",
+            "config": {"model": f"{n_nodes}-node MI355X mock cluster (amd.com/gpu:1 per node = 1 GPU per rank)",
+                       "global_batch": n_nodes, "seq_len": node_bytes,
+                       "parallelism": f"dp{n_gpus}" if n_gpus > 1 else "single",
+                       "mode": args.mode, "slack": bool(args.slack), "page_size": args.page_size},
+            "latency_ms": {"p50": round(_pctl(lat, 0.5) * 1e3, 4), "p90": round(_pctl(lat, 0.9) * 1e3, 4),
+                           "p99": round(_pctl(lat, 0.99) * 1e3, 4), "min": round(min(lat) * 1e3, 4)},
+            "baseline_ms": ref,
+            "check_ok": ok,
+            "exit_code": last.exit_code if last else None,
+            "health": {s: verdicts.count(s) for s in sorted(set(verdicts))},
+            "backend": fastpath.backend(),
+            "probe": {"source": probe_source, "setup_ms": round(probe_ms, 1), "diag": diag},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier(group=group)
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,175 @@
+"""MI355X node agent (DaemonSet): probe -> publish (SURVEY §7.2 layer 5 source (a)/(b)).
+
+Every ``--interval`` seconds the agent runs the passive amd-smi probe
+(``ops/amdsmi_probe.py``, native library) and, every ``--diag-interval``
+seconds, the active HIP diagnostics (``ops/diag.py``: MFMA GEMM + numerics,
+HBM bandwidth, memtest) at ``--diag-level``.  The merged report is published
+
+* as the node annotation ``amd.com/mi355x-health`` (JSON merge-PATCH; the
+  checker reads it from the LIST it already does -- zero extra API calls), and/or
+* over HTTP at ``/probe`` (JSON) and ``/metrics`` (Prometheus) for the
+  checker's ``--probe-endpoint`` fan-out, and/or
+* on stdout (``--publish stdout``, one JSON line per probe).
+
+RBAC: ``nodes: get, patch`` for the annotation path (``deploy/daemonset.yaml``).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import threading
+import time
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Any, Dict, List, Optional
+
+from ..models.health import HealthExpectations, evaluate_report
+from ..models.node import HEALTH_ANNOTATION
+
+
+class Agent:
+    def __init__(self, node: str, source: str = "auto", fixture: Optional[str] = None, diag_level: int = 0,
+                 diag_interval: float = 3600.0, devices: Optional[List[int]] = None):
+        self.node = node
+        self.source = source
+        self.fixture = fixture
+        self.diag_level = diag_level
+        self.diag_interval = diag_interval
+        self.devices = devices
+        self._diag_cache: Dict[int, Dict[str, Any]] = {}
+        self._diag_ts = 0.0
+        self.last: Optional[Dict[str, Any]] = None
+        self.lock = threading.Lock()
+
+    def _diagnostics(self, n_gpus: int) -> Dict[int, Dict[str, Any]]:
+        if self.diag_level <= 0:
+            return {}
+        now = time.time()
+        if self._diag_cache and now - self._diag_ts < self.diag_interval:
+            return self._diag_cache
+        from ..ops import diag
+        devices = self.devices if self.devices is not None else list(range(min(n_gpus, diag.device_count())))
+        self._diag_cache = {d: diag.run(self.diag_level, d) for d in devices}
+        self._diag_ts = now
+        return self._diag_cache
+
+    def probe_once(self) -> Dict[str, Any]:
+        from ..ops.amdsmi_probe import probe
+        rep = probe(self.node, self.source, self.fixture)
+        diags = self._diagnostics(len(rep.get("gpus") or []))
+        for g in rep.get("gpus") or []:
+            d = diags.get(g.get("index"))
+            if d:
+                g["diag"] = d
+        verdict = evaluate_report(rep, 0, HealthExpectations())
+        rep["state"] = verdict.state
+        with self.lock:
+            self.last = rep
+        return rep
+
+    def annotation(self, rep: Dict[str, Any]) -> Dict[str, str]:
+        return {HEALTH_ANNOTATION: json.dumps(rep, separators=(",", ":"))}
+
+    def publish_annotation(self, client: Any, rep: Dict[str, Any]) -> None:
+        client.patch_node_annotations(self.node, self.annotation(rep))
+
+
+def _metrics(rep: Optional[Dict[str, Any]]) -> str:
+    if not rep:
+        return "# no probe yet\n"
+    lines = ["# TYPE mi355x_agent_probe_timestamp_seconds gauge", f"mi355x_agent_probe_timestamp_seconds {rep.get('ts', 0)}",
+             "# TYPE mi355x_gpu_ecc_uncorrectable gauge", "# TYPE mi355x_gpu_xgmi_links_up gauge",
+             "# TYPE mi355x_gpu_hotspot_celsius gauge"]
+    for g in rep.get("gpus") or []:
+        lbl = f'gpu="{g.get("index")}",bdf="{g.get("bdf", "")}"'
+        if isinstance(g.get("ecc_uncorrectable"), int):
+            lines.append(f"mi355x_gpu_ecc_uncorrectable{{{lbl}}} {g['ecc_uncorrectable']}")
+        if isinstance(g.get("xgmi"), str):
+            lines.append(f"mi355x_gpu_xgmi_links_up{{{lbl}}} {g['xgmi'].count('U')}")
+        if isinstance(g.get("hotspot_c"), (int, float)):
+            lines.append(f"mi355x_gpu_hotspot_celsius{{{lbl}}} {g['hotspot_c']}")
+        for test, res in (g.get("diag") or {}).items():
+            for k in ("tflops", "copy_tbs", "errors"):
+                if k in res:
+                    lines.append(f'mi355x_gpu_diag_{k}{{{lbl},test="{test}"}} {res[k]}')
+    return "\n".join(lines) + "\n"
+
+
+def serve(agent: Agent, host: str, port: int) -> ThreadingHTTPServer:
+    class H(BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def log_message(self, *a: Any) -> None:
+            pass
+
+        def do_GET(self) -> None:  # noqa: N802
+            with agent.lock:
+                rep = agent.last
+            if self.path.startswith("/probe"):
+                body = json.dumps(rep or {"schema": "mi355x-health/v1", "error": "no probe yet"}).encode()
+                ctype = "application/json"
+            elif self.path.startswith("/metrics"):
+                body = _metrics(rep).encode()
+                ctype = "text/plain; version=0.0.4"
+            elif self.path.startswith("/healthz"):
+                body, ctype = b"ok", "text/plain"
+            else:
+                self.send_response(404)
+                self.send_header("Content-Length", "0")
+                self.end_headers()
+                return
+            self.send_response(200)
+            self.send_header("Content-Type", ctype)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+    srv = ThreadingHTTPServer((host, port), H)
+    srv.daemon_threads = True
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    return srv
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    ap = argparse.ArgumentParser(prog="k8s-gpu-node-agent", description="MI355X node agent (probe + publish)")
+    ap.add_argument("--node", default=os.environ.get("NODE_NAME") or socket.gethostname())
+    ap.add_argument("--source", choices=("auto", "native", "python", "fixture"), default="auto")
+    ap.add_argument("--fixture", help="recorded probe report (source=fixture)")
+    ap.add_argument("--interval", type=float, default=60.0)
+    ap.add_argument("--diag-level", type=int, default=0, choices=(0, 1, 2))
+    ap.add_argument("--diag-interval", type=float, default=3600.0)
+    ap.add_argument("--publish", default="annotation", help="comma list of annotation,http,stdout")
+    ap.add_argument("--listen", default="0.0.0.0:9464")
+    ap.add_argument("--kubeconfig")
+    ap.add_argument("--once", action="store_true")
+    args = ap.parse_args(argv)
+    pubs = set(args.publish.split(","))
+    agent = Agent(args.node, args.source, args.fixture, args.diag_level, args.diag_interval)
+    client = None
+    if "annotation" in pubs:
+        from ..kube.client import KubeClient
+        from ..kube.config import load_kube_config
+        client = KubeClient(load_kube_config(args.kubeconfig), timeout=10.0)
+    if "http" in pubs:
+        host, _, port = args.listen.rpartition(":")
+        serve(agent, host or "0.0.0.0", int(port))
+    while True:
+        started = time.monotonic()
+        rep = agent.probe_once()
+        if "stdout" in pubs:
+            print(json.dumps(rep, separators=(",", ":")), flush=True)
+        if client is not None:
+            try:
+                agent.publish_annotation(client, rep)
+            except Exception as e:
+                print(f"annotation publish failed: {e}", file=sys.stderr, flush=True)
+        if args.once:
+            return 0
+        time.sleep(max(0.0, args.interval - (time.monotonic() - started)))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,469 @@
+// Active MI355X diagnostics (gfx950 / CDNA4 only): the "deep" health checks the
+// node agent can run besides the passive amd-smi probe.  A node can be
+// Ready=True with clean ECC counters and still have a GPU that computes wrong
+// results, runs at a fraction of its matrix rate (stuck clocks, throttling) or
+// has a weak HBM stack; these kernels measure exactly that.
+//
+//   gemm_bf16   C[M,N] = A[M,K] . Bt[N,K]^T, bf16 in / fp32 out on MFMA
+//               (v_mfma_f32_16x16x32_bf16), 128x128x64 tiles, 4 waves (2x2) of
+//               64x64, XOR-swizzled LDS (conflict-free ds_read_b128 fragment
+//               loads), register-staged double buffer, XCD-aware tile order.
+//               Verified against an fp32 reference kernel on sampled outputs.
+//   hbm_copy / hbm_read / hbm_write
+//               float4 streams, 4 loads in flight per thread, grid sized to
+//               fill 256 CUs; reported in TB/s against the 8 TB/s HBM3E spec.
+//   memtest     address-hash patterns written and verified (plus the
+//               bit-inverted pass), mismatches counted with one atomic per
+//               failing 16-byte word.
+//
+// C ABI (ctypes, ops/diag.py).  Every HIP call is checked; on failure the
+// function returns a negative code and diag_last_error() says what failed.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+#define DIAG_CHECK(expr)                                                                  \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      g_err = std::string(#expr) + ": " + hipGetErrorString(e_);                          \
+      return -1;                                                                          \
+    }                                                                                     \
+  } while (0)
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native 16-byte vector (SROA-friendly, unlike uint4)
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int THREADS = 256;
+constexpr int CHUNKS_PER_ROW = BK / 8;                 // 16-byte chunks per 64-wide bf16 row
+constexpr int TILE_CHUNKS = BM * CHUNKS_PER_ROW;       // 1024 chunks per operand tile
+constexpr int LOADS_PER_THREAD = TILE_CHUNKS / THREADS;  // 4
+
+// LDS image: [row][8 chunks of 16 B], chunk c of row r stored at c ^ ((r >> 1) & 7).
+// For the 16x16x32 fragment read (lane l: row l&15, chunk (l>>4)+4s) this puts
+// every ds_read_b128 lane group on 16 distinct 16-byte slots (all 64 banks).
+__device__ __forceinline__ int swz(int r, int c) { return r * CHUNKS_PER_ROW + (c ^ ((r >> 1) & 7)); }
+
+__device__ __forceinline__ void gemm_gload(u32x4 (&ra)[LOADS_PER_THREAD], u32x4 (&rb)[LOADS_PER_THREAD],
+                                           const u32x4* __restrict__ Ablk, const u32x4* __restrict__ Bblk,
+                                           const int (&g_off)[LOADS_PER_THREAD], int kt) {
+#pragma unroll
+  for (int i = 0; i < LOADS_PER_THREAD; ++i) {
+    ra[i] = Ablk[g_off[i] + kt * CHUNKS_PER_ROW];
+    rb[i] = Bblk[g_off[i] + kt * CHUNKS_PER_ROW];
+  }
+}
+
+__device__ __forceinline__ void gemm_lstore(u32x4 (&buf)[2][TILE_CHUNKS], const u32x4 (&ra)[LOADS_PER_THREAD],
+                                            const u32x4 (&rb)[LOADS_PER_THREAD], const int (&l_off)[LOADS_PER_THREAD]) {
+#pragma unroll
+  for (int i = 0; i < LOADS_PER_THREAD; ++i) {
+    buf[0][l_off[i]] = ra[i];
+    buf[1][l_off[i]] = rb[i];
+  }
+}
+
+// One BK=64 step: 2 x (4 A-fragments, 4 B-fragments, 16 MFMA 16x16x32).
+__device__ __forceinline__ void gemm_compute(floatx4 (&acc)[4][4], const u32x4 (&buf)[2][TILE_CHUNKS], int wr, int wc,
+                                             int frow, int fq) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) af[m] = __builtin_bit_cast(bf16x8, buf[0][swz(wr * 64 + m * 16 + frow, fq + 4 * s)]);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = __builtin_bit_cast(bf16x8, buf[1][swz(wc * 64 + n * 16 + frow, fq + 4 * s)]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(THREADS, 2)
+gemm_bf16_kernel(const u32x4* __restrict__ A, const u32x4* __restrict__ Bt, float* __restrict__ C, int M, int N,
+                 int K) {
+  __shared__ u32x4 lds[2][2][TILE_CHUNKS];  // [buffer][A|B][chunk]  = 64 KiB
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+
+  // XCD-aware, grouped tile order: consecutive blocks land on different XCDs
+  // (round-robin dispatch), so regroup ids so one XCD walks a compact 2D patch.
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % (GROUP_M * tiles_n)) % gsize;
+  const int tn = (bid % (GROUP_M * tiles_n)) / gsize;
+
+  const int kchunks = K / 8;  // 16-byte chunks per row of A / Bt
+  const u32x4* Ablk = A + static_cast<size_t>(tm) * BM * kchunks;
+  const u32x4* Bblk = Bt + static_cast<size_t>(tn) * BN * kchunks;
+
+  u32x4 ra[LOADS_PER_THREAD], rb[LOADS_PER_THREAD];
+  // per-thread chunk coordinates are loop invariant
+  int g_off[LOADS_PER_THREAD], l_off[LOADS_PER_THREAD];
+#pragma unroll
+  for (int i = 0; i < LOADS_PER_THREAD; ++i) {
+    const int ch = tid + i * THREADS;
+    const int r = ch / CHUNKS_PER_ROW, c = ch % CHUNKS_PER_ROW;
+    g_off[i] = r * kchunks + c;
+    l_off[i] = swz(r, c);
+  }
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = K / BK;
+  const int frow = lane & 15, fq = lane >> 4;
+  gemm_gload(ra, rb, Ablk, Bblk, g_off, 0);
+  gemm_lstore(lds[0], ra, rb, l_off);
+  __syncthreads();
+  // two K-steps per trip so the LDS buffer index is a compile-time constant
+  for (int kt = 0; kt < KT; kt += 2) {
+    const bool more1 = kt + 1 < KT;
+    if (more1) gemm_gload(ra, rb, Ablk, Bblk, g_off, kt + 1);
+    gemm_compute(acc, lds[0], wr, wc, frow, fq);
+    if (more1) gemm_lstore(lds[1], ra, rb, l_off);
+    __syncthreads();
+    if (!more1) break;
+    const bool more2 = kt + 2 < KT;
+    if (more2) gemm_gload(ra, rb, Ablk, Bblk, g_off, kt + 2);
+    gemm_compute(acc, lds[1], wr, wc, frow, fq);
+    if (more2) gemm_lstore(lds[0], ra, rb, l_off);
+    __syncthreads();
+  }
+  // C/D layout of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + reg
+  const int row0 = tm * BM + wr * 64, col0 = tn * BN + wc * 64;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        C[static_cast<size_t>(row0 + m * 16 + fq * 4 + j) * N + col0 + n * 16 + frow] = acc[m][n][j];
+}
+
+// fp32 reference for sampled outputs: one thread per (row, col) sample.
+__global__ void gemm_ref_kernel(const __bf16* A, const __bf16* Bt, const int* rows, const int* cols, float* out,
+                                int nsamp, int K) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsamp) return;
+  const __bf16* a = A + static_cast<size_t>(rows[i]) * K;
+  const __bf16* b = Bt + static_cast<size_t>(cols[i]) * K;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += static_cast<float>(a[k]) * static_cast<float>(b[k]);
+  out[i] = s;
+}
+
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return static_cast<uint32_t>(x);
+}
+
+// Deterministic pseudo-random bf16 in [-1, 1).
+__global__ void fill_bf16_kernel(__bf16* p, size_t n, uint64_t seed) {
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const uint32_t h = mix32(i * 0x9E3779B97F4A7C15ULL + seed);
+    p[i] = static_cast<__bf16>((h >> 8) * (2.0f / 16777216.0f) - 1.0f);
+  }
+}
+
+// ---------------------------------------------------------------- HBM streams
+__global__ void __launch_bounds__(256) copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) read_kernel(const float4* __restrict__ src, size_t n, float* sink) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  float acc = 0.f;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    acc += (a.x + b.y) + (c.z + d.w);
+  }
+  for (; i < n; i += stride) acc += src[i].x;
+  if (acc == 1234.5678f) *sink = acc;  // keeps the loads alive, practically never stores
+}
+
+__global__ void __launch_bounds__(256) write_kernel(float4* __restrict__ dst, size_t n, float v) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const float4 x = make_float4(v, v, v, v);
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride) dst[i] = x;
+}
+
+// ---------------------------------------------------------------- memtest
+__device__ __forceinline__ uint4 pattern(size_t i, uint64_t seed, bool invert) {
+  uint4 v;
+  v.x = mix32(4 * i + seed);
+  v.y = mix32(4 * i + 1 + seed);
+  v.z = mix32(4 * i + 2 + seed);
+  v.w = mix32(4 * i + 3 + seed);
+  if (invert) {
+    v.x = ~v.x;
+    v.y = ~v.y;
+    v.z = ~v.z;
+    v.w = ~v.w;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(256) mt_write_kernel(uint4* p, size_t n, uint64_t seed, int invert) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride)
+    p[i] = pattern(i, seed, invert != 0);
+}
+
+__global__ void __launch_bounds__(256) mt_verify_kernel(const uint4* p, size_t n, uint64_t seed, int invert,
+                                                        unsigned long long* errors, unsigned long long* first_bad) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
+    const uint4 v = p[i];
+    const uint4 e = pattern(i, seed, invert != 0);
+    if (v.x != e.x || v.y != e.y || v.z != e.z || v.w != e.w) {
+      atomicAdd(errors, 1ULL);
+      atomicMin(first_bad, static_cast<unsigned long long>(i));
+    }
+  }
+}
+
+int grid_for(int device, int blocks_per_cu) {
+  int cus = 256;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  return cus * blocks_per_cu;
+}
+
+float elapsed_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, a, b);
+  return ms;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* diag_last_error(void) { return g_err.c_str(); }
+
+int diag_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// Device name / arch string ("gfx950:sramecc+:xnack-") into buf.
+int diag_device_arch(int device, char* buf, int len) {
+  hipDeviceProp_t prop;
+  DIAG_CHECK(hipGetDeviceProperties(&prop, device));
+  snprintf(buf, static_cast<size_t>(len), "%s|%s|%d|%zu", prop.gcnArchName, prop.name, prop.multiProcessorCount,
+           static_cast<size_t>(prop.totalGlobalMem));
+  return 0;
+}
+
+// Raw kernel on caller-owned device pointers (used by the numerics tests with
+// torch tensors).  M, N multiples of 128; K multiple of 64.
+int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N, int K, void* stream) {
+  if (M % BM || N % BN || K % BK || M <= 0 || N <= 0 || K <= 0) {
+    g_err = "gemm_bf16: M, N must be multiples of 128 and K a multiple of 64";
+    return -2;
+  }
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(gemm_bf16_kernel, dim3(nwg), dim3(THREADS), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const u32x4*>(A), static_cast<const u32x4*>(Bt), C, M, N, K);
+  DIAG_CHECK(hipGetLastError());
+  return 0;
+}
+
+// Self-contained MFMA burn-in: allocate, fill, run `iters` GEMMs, time them,
+// verify `nsamp` sampled outputs against the fp32 reference kernel.
+int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int nsamp, double* tflops,
+                   double* max_rel_err, double* ms_per_iter) {
+  if (M % BM || N % BN || K % BK) {
+    g_err = "gemm_bf16: M, N must be multiples of 128 and K a multiple of 64";
+    return -2;
+  }
+  DIAG_CHECK(hipSetDevice(device));
+  __bf16 *A = nullptr, *Bt = nullptr;
+  float *C = nullptr, *ref = nullptr;
+  int *rows = nullptr, *cols = nullptr;
+  hipEvent_t e0, e1;
+  DIAG_CHECK(hipMalloc(&A, sizeof(__bf16) * static_cast<size_t>(M) * K));
+  DIAG_CHECK(hipMalloc(&Bt, sizeof(__bf16) * static_cast<size_t>(N) * K));
+  DIAG_CHECK(hipMalloc(&C, sizeof(float) * static_cast<size_t>(M) * N));
+  DIAG_CHECK(hipMalloc(&ref, sizeof(float) * nsamp));
+  DIAG_CHECK(hipMalloc(&rows, sizeof(int) * nsamp));
+  DIAG_CHECK(hipMalloc(&cols, sizeof(int) * nsamp));
+  hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, A, static_cast<size_t>(M) * K, 0x1234ULL);
+  hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, Bt, static_cast<size_t>(N) * K, 0xBEEFULL);
+  DIAG_CHECK(hipGetLastError());
+  std::vector<int> hr(nsamp), hc(nsamp);
+  uint64_t x = 0x243F6A8885A308D3ULL;
+  for (int i = 0; i < nsamp; ++i) {
+    x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+    hr[i] = static_cast<int>((x >> 33) % static_cast<uint64_t>(M));
+    x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+    hc[i] = static_cast<int>((x >> 33) % static_cast<uint64_t>(N));
+  }
+  DIAG_CHECK(hipMemcpy(rows, hr.data(), sizeof(int) * nsamp, hipMemcpyHostToDevice));
+  DIAG_CHECK(hipMemcpy(cols, hc.data(), sizeof(int) * nsamp, hipMemcpyHostToDevice));
+  DIAG_CHECK(hipEventCreate(&e0));
+  DIAG_CHECK(hipEventCreate(&e1));
+  for (int i = 0; i < warmup; ++i)
+    if (diag_gemm_bf16_launch(A, Bt, C, M, N, K, nullptr)) return -1;
+  DIAG_CHECK(hipEventRecord(e0, nullptr));
+  for (int i = 0; i < iters; ++i)
+    if (diag_gemm_bf16_launch(A, Bt, C, M, N, K, nullptr)) return -1;
+  DIAG_CHECK(hipEventRecord(e1, nullptr));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  const double ms = elapsed_ms(e0, e1) / std::max(iters, 1);
+  hipLaunchKernelGGL(gemm_ref_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, A, Bt, rows, cols, ref,
+                     nsamp, K);
+  DIAG_CHECK(hipGetLastError());
+  std::vector<float> href(nsamp), hC(nsamp);
+  DIAG_CHECK(hipMemcpy(href.data(), ref, sizeof(float) * nsamp, hipMemcpyDeviceToHost));
+  for (int i = 0; i < nsamp; ++i)
+    DIAG_CHECK(hipMemcpy(&hC[i], C + static_cast<size_t>(hr[i]) * N + hc[i], sizeof(float), hipMemcpyDeviceToHost));
+  double worst = 0.0;
+  for (int i = 0; i < nsamp; ++i) {
+    const double denom = std::max(1.0, std::fabs(static_cast<double>(href[i])));
+    worst = std::max(worst, std::fabs(static_cast<double>(hC[i]) - href[i]) / denom);
+  }
+  *max_rel_err = worst;
+  *ms_per_iter = ms;
+  *tflops = 2.0 * M * N * static_cast<double>(K) / (ms * 1e-3) / 1e12;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(A);
+  hipFree(Bt);
+  hipFree(C);
+  hipFree(ref);
+  hipFree(rows);
+  hipFree(cols);
+  return 0;
+}
+
+// HBM streams over `bytes` per buffer: copy (read+write), read-only, write-only, in TB/s.
+int diag_hbm_bandwidth(int device, size_t bytes, int iters, double* copy_tbs, double* read_tbs, double* write_tbs) {
+  DIAG_CHECK(hipSetDevice(device));
+  const size_t n = bytes / sizeof(float4);
+  float4 *a = nullptr, *b = nullptr;
+  float* sink = nullptr;
+  DIAG_CHECK(hipMalloc(&a, n * sizeof(float4)));
+  DIAG_CHECK(hipMalloc(&b, n * sizeof(float4)));
+  DIAG_CHECK(hipMalloc(&sink, sizeof(float)));
+  const int grid = grid_for(device, 8);
+  hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, a, n, 1.0f);
+  hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, b, n, 2.0f);
+  DIAG_CHECK(hipGetLastError());
+  hipEvent_t e0, e1;
+  DIAG_CHECK(hipEventCreate(&e0));
+  DIAG_CHECK(hipEventCreate(&e1));
+  const size_t nb = n * sizeof(float4);
+  // copy
+  hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, nullptr, a, b, n);
+  DIAG_CHECK(hipEventRecord(e0, nullptr));
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, nullptr, a, b, n);
+  DIAG_CHECK(hipEventRecord(e1, nullptr));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  *copy_tbs = 2.0 * nb * iters / (elapsed_ms(e0, e1) * 1e-3) / 1e12;
+  // read
+  hipLaunchKernelGGL(read_kernel, dim3(grid), dim3(256), 0, nullptr, a, n, sink);
+  DIAG_CHECK(hipEventRecord(e0, nullptr));
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(read_kernel, dim3(grid), dim3(256), 0, nullptr, a, n, sink);
+  DIAG_CHECK(hipEventRecord(e1, nullptr));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  *read_tbs = 1.0 * nb * iters / (elapsed_ms(e0, e1) * 1e-3) / 1e12;
+  // write
+  hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, b, n, 3.0f);
+  DIAG_CHECK(hipEventRecord(e0, nullptr));
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, b, n, 3.0f);
+  DIAG_CHECK(hipEventRecord(e1, nullptr));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  *write_tbs = 1.0 * nb * iters / (elapsed_ms(e0, e1) * 1e-3) / 1e12;
+  DIAG_CHECK(hipGetLastError());
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(a);
+  hipFree(b);
+  hipFree(sink);
+  return 0;
+}
+
+// Pattern test over `bytes` of HBM; `passes` x (pattern, inverted pattern).
+int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned long long* errors,
+                 unsigned long long* first_bad_byte, double* gbps) {
+  DIAG_CHECK(hipSetDevice(device));
+  const size_t n = bytes / sizeof(uint4);
+  uint4* p = nullptr;
+  unsigned long long* dev = nullptr;
+  DIAG_CHECK(hipMalloc(&p, n * sizeof(uint4)));
+  DIAG_CHECK(hipMalloc(&dev, 2 * sizeof(unsigned long long)));
+  const unsigned long long init[2] = {0ULL, ~0ULL};
+  DIAG_CHECK(hipMemcpy(dev, init, sizeof init, hipMemcpyHostToDevice));
+  const int grid = grid_for(device, 8);
+  hipEvent_t e0, e1;
+  DIAG_CHECK(hipEventCreate(&e0));
+  DIAG_CHECK(hipEventCreate(&e1));
+  DIAG_CHECK(hipEventRecord(e0, nullptr));
+  for (int pass = 0; pass < passes; ++pass) {
+    for (int inv = 0; inv < 2; ++inv) {
+      const uint64_t s = seed + static_cast<uint64_t>(pass) * 0x9E3779B97F4A7C15ULL;
+      hipLaunchKernelGGL(mt_write_kernel, dim3(grid), dim3(256), 0, nullptr, p, n, s, inv);
+      hipLaunchKernelGGL(mt_verify_kernel, dim3(grid), dim3(256), 0, nullptr, p, n, s, inv, dev, dev + 1);
+    }
+  }
+  DIAG_CHECK(hipEventRecord(e1, nullptr));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  DIAG_CHECK(hipGetLastError());
+  unsigned long long h[2];
+  DIAG_CHECK(hipMemcpy(h, dev, sizeof h, hipMemcpyDeviceToHost));
+  *errors = h[0];
+  *first_bad_byte = h[0] ? h[1] * sizeof(uint4) : ~0ULL;
+  *gbps = 4.0 * passes * static_cast<double>(n * sizeof(uint4)) / (elapsed_ms(e0, e1) * 1e-3) / 1e9;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(p);
+  hipFree(dev);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,271 @@
+// MI355X passive health probe: libamd_smi -> "mi355x-health/v1" JSON (see probe.h).
+//
+// Checks what SURVEY §7.1 lists (ASIC/gfx950, HBM3E VRAM size, ECC, xGMI links,
+// KFD node) plus bad pages, partition modes and hotspot temperature.  Every
+// amd-smi status other than success is recorded, never thrown: a node whose
+// driver is not loaded (AMDSMI_STATUS_DRIVER_NOT_LOADED) or that denies access
+// (AMDSMI_STATUS_NO_PERM) yields a report with "error" set, which the checker
+// maps to verdict "unknown" (models/health.py), not to a crash.
+#include "probe.h"
+
+#include <amd_smi/amdsmi.h>
+
+#include <chrono>
+#include <cinttypes>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+std::mutex g_mu;
+bool g_open = false;
+int g_gpus = -1;
+std::vector<amdsmi_processor_handle> g_handles;
+
+void jstr(std::string& o, const char* s) {
+  o.push_back('"');
+  for (const unsigned char* p = reinterpret_cast<const unsigned char*>(s); *p; ++p) {
+    unsigned char c = *p;
+    if (c == '"' || c == '\\') {
+      o.push_back('\\');
+      o.push_back(static_cast<char>(c));
+    } else if (c < 0x20) {
+      char buf[8];
+      snprintf(buf, sizeof buf, "\\u%04x", c);
+      o += buf;
+    } else {
+      o.push_back(static_cast<char>(c));
+    }
+  }
+  o.push_back('"');
+}
+
+void key(std::string& o, const char* k) {
+  if (o.back() != '{') o.push_back(',');
+  jstr(o, k);
+  o.push_back(':');
+}
+
+void kv_str(std::string& o, const char* k, const char* v) {
+  key(o, k);
+  jstr(o, v);
+}
+
+void kv_u64(std::string& o, const char* k, uint64_t v) {
+  key(o, k);
+  o += std::to_string(v);
+}
+
+void kv_i64(std::string& o, const char* k, int64_t v) {
+  key(o, k);
+  o += std::to_string(v);
+}
+
+void kv_null(std::string& o, const char* k) {
+  key(o, k);
+  o += "null";
+}
+
+const char* status_name(amdsmi_status_t st) {
+  const char* s = nullptr;
+  if (amdsmi_status_code_to_string(st, &s) == AMDSMI_STATUS_SUCCESS && s) return s;
+  return "AMDSMI_STATUS_UNKNOWN";
+}
+
+int open_locked() {
+  if (g_open) return 0;
+  amdsmi_status_t st = amdsmi_init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) return static_cast<int>(st);
+  uint32_t nsock = 0;
+  st = amdsmi_get_socket_handles(&nsock, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS) {
+    amdsmi_shut_down();
+    return static_cast<int>(st);
+  }
+  std::vector<amdsmi_socket_handle> socks(nsock);
+  st = amdsmi_get_socket_handles(&nsock, socks.data());
+  g_handles.clear();
+  for (uint32_t s = 0; st == AMDSMI_STATUS_SUCCESS && s < nsock; ++s) {
+    uint32_t n = 0;
+    if (amdsmi_get_processor_handles(socks[s], &n, nullptr) != AMDSMI_STATUS_SUCCESS) continue;
+    std::vector<amdsmi_processor_handle> hs(n);
+    if (amdsmi_get_processor_handles(socks[s], &n, hs.data()) != AMDSMI_STATUS_SUCCESS) continue;
+    for (uint32_t i = 0; i < n; ++i) {
+      processor_type_t t;
+      if (amdsmi_get_processor_type(hs[i], &t) == AMDSMI_STATUS_SUCCESS && t == AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+        g_handles.push_back(hs[i]);
+    }
+  }
+  g_open = true;
+  g_gpus = static_cast<int>(g_handles.size());
+  return 0;
+}
+
+void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
+  auto t0 = std::chrono::steady_clock::now();
+  o.push_back('{');
+  kv_i64(o, "index", index);
+  amdsmi_bdf_t bdf;
+  if (amdsmi_get_gpu_device_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS) {
+    char buf[32];
+    snprintf(buf, sizeof buf, "%04" PRIx64 ":%02x:%02x.%x", static_cast<uint64_t>(bdf.domain_number),
+             static_cast<unsigned>(bdf.bus_number), static_cast<unsigned>(bdf.device_number),
+             static_cast<unsigned>(bdf.function_number));
+    kv_str(o, "bdf", buf);
+  }
+  char uuid[AMDSMI_GPU_UUID_SIZE + 2] = {0};
+  unsigned int ulen = sizeof uuid;
+  if (amdsmi_get_gpu_device_uuid(h, &ulen, uuid) == AMDSMI_STATUS_SUCCESS) kv_str(o, "uuid", uuid);
+
+  amdsmi_asic_info_t asic;
+  memset(&asic, 0, sizeof asic);
+  amdsmi_status_t st = amdsmi_get_gpu_asic_info(h, &asic);
+  if (st != AMDSMI_STATUS_SUCCESS) {
+    kv_str(o, "error", status_name(st));
+    o.push_back('}');
+    return;
+  }
+  if (asic.target_graphics_version != UINT64_MAX) {
+    char buf[32];
+    snprintf(buf, sizeof buf, "gfx%" PRIx64, asic.target_graphics_version);
+    kv_str(o, "gfx", buf);
+  } else {
+    kv_null(o, "gfx");
+  }
+  kv_str(o, "market_name", asic.market_name);
+  {
+    char buf[24];
+    snprintf(buf, sizeof buf, "0x%04" PRIx64, asic.device_id);
+    kv_str(o, "device_id", buf);
+  }
+  if (asic.num_of_compute_units != UINT32_MAX) kv_u64(o, "cus", asic.num_of_compute_units);
+  amdsmi_vbios_info_t vb;
+  memset(&vb, 0, sizeof vb);
+  if (amdsmi_get_gpu_vbios_info(h, &vb) == AMDSMI_STATUS_SUCCESS) kv_str(o, "vbios_name", vb.name);
+
+  amdsmi_vram_info_t vram;
+  memset(&vram, 0, sizeof vram);
+  if (amdsmi_get_gpu_vram_info(h, &vram) == AMDSMI_STATUS_SUCCESS) {
+    kv_i64(o, "vram_type", static_cast<int64_t>(vram.vram_type));
+    kv_u64(o, "vram_mb", vram.vram_size);
+  }
+  amdsmi_error_count_t ec;
+  memset(&ec, 0, sizeof ec);
+  if (amdsmi_get_gpu_total_ecc_count(h, &ec) == AMDSMI_STATUS_SUCCESS) {
+    kv_u64(o, "ecc_correctable", ec.correctable_count);
+    kv_u64(o, "ecc_uncorrectable", ec.uncorrectable_count);
+    kv_u64(o, "ecc_deferred", ec.deferred_count);
+  } else {
+    kv_null(o, "ecc_uncorrectable");
+  }
+  uint32_t pages = 0;
+  if (amdsmi_get_gpu_bad_page_info(h, &pages, nullptr) == AMDSMI_STATUS_SUCCESS) kv_u64(o, "bad_pages", pages);
+
+  amdsmi_xgmi_link_status_t xs;
+  memset(&xs, 0, sizeof xs);
+  if (amdsmi_get_gpu_xgmi_link_status(h, &xs) == AMDSMI_STATUS_SUCCESS) {
+    std::string links;
+    for (uint32_t i = 0; i < xs.total_links && i < AMDSMI_MAX_NUM_XGMI_LINKS; ++i) {
+      switch (xs.status[i]) {
+        case AMDSMI_XGMI_LINK_UP: links.push_back('U'); break;
+        case AMDSMI_XGMI_LINK_DOWN: links.push_back('D'); break;
+        case AMDSMI_XGMI_LINK_DISABLE: links.push_back('X'); break;
+        default: links.push_back('N');
+      }
+    }
+    kv_str(o, "xgmi", links.c_str());
+  } else {
+    kv_null(o, "xgmi");
+  }
+  amdsmi_kfd_info_t kfd;
+  memset(&kfd, 0, sizeof kfd);
+  bool kfd_ok = amdsmi_get_gpu_kfd_info(h, &kfd) == AMDSMI_STATUS_SUCCESS && kfd.kfd_id != UINT64_MAX &&
+                kfd.node_id != UINT32_MAX;
+  key(o, "kfd");
+  o += kfd_ok ? "true" : "false";
+  if (kfd_ok) kv_u64(o, "kfd_node", kfd.node_id);
+  char part[64] = {0};
+  if (amdsmi_get_gpu_compute_partition(h, part, sizeof part) == AMDSMI_STATUS_SUCCESS) kv_str(o, "compute_partition", part);
+  memset(part, 0, sizeof part);
+  if (amdsmi_get_gpu_memory_partition(h, part, sizeof part) == AMDSMI_STATUS_SUCCESS) kv_str(o, "memory_partition", part);
+  int64_t temp = 0;
+  if (amdsmi_get_temp_metric(h, AMDSMI_TEMPERATURE_TYPE_HOTSPOT, AMDSMI_TEMP_CURRENT, &temp) == AMDSMI_STATUS_SUCCESS)
+    kv_i64(o, "hotspot_c", temp);
+  double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  key(o, "probe_us");
+  o += std::to_string(static_cast<int64_t>(us));
+  o.push_back('}');
+}
+
+char* dup(const std::string& s) {
+  char* p = static_cast<char*>(malloc(s.size() + 1));
+  if (p) memcpy(p, s.c_str(), s.size() + 1);
+  return p;
+}
+
+}  // namespace
+
+extern "C" int mi355x_probe_open(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return open_locked();
+}
+
+extern "C" int mi355x_probe_gpu_count(void) { return g_gpus; }
+
+extern "C" char* mi355x_probe_json(const char* node_name) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto t0 = std::chrono::steady_clock::now();
+  double now = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+  std::string o = "{";
+  kv_str(o, "schema", "mi355x-health/v1");
+  kv_str(o, "node", node_name ? node_name : "");
+  {
+    char buf[40];
+    snprintf(buf, sizeof buf, "%.3f", now);
+    key(o, "ts");
+    o += buf;
+  }
+  kv_str(o, "probe", "native");
+  amdsmi_version_t ver;
+  if (amdsmi_get_lib_version(&ver) == AMDSMI_STATUS_SUCCESS) {
+    char buf[64];
+    snprintf(buf, sizeof buf, "%u.%u.%u", ver.major, ver.minor, ver.release);
+    kv_str(o, "amdsmi", buf);
+  }
+  int st = open_locked();
+  if (st != 0) {
+    kv_str(o, "error", status_name(static_cast<amdsmi_status_t>(st)));
+    key(o, "gpus");
+    o += "[]}";
+    return dup(o);
+  }
+  key(o, "gpus");
+  o.push_back('[');
+  for (size_t i = 0; i < g_handles.size(); ++i) {
+    if (i) o.push_back(',');
+    probe_gpu(o, static_cast<int>(i), g_handles[i]);
+  }
+  o.push_back(']');
+  double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  char buf[40];
+  snprintf(buf, sizeof buf, "%.3f", ms);
+  key(o, "probe_ms");
+  o += buf;
+  o.push_back('}');
+  return dup(o);
+}
+
+extern "C" void mi355x_probe_free(char* doc) { free(doc); }
+
+extern "C" void mi355x_probe_close(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_open) {
+    amdsmi_shut_down();
+    g_open = false;
+    g_handles.clear();
+  }
+}

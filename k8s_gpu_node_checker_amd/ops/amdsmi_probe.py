@@ -1,0 +1,137 @@
+"""Passive MI355X probe front-end (SURVEY §7.1, §7.2 layer 4).
+
+Sources, in order of preference:
+
+``native``   ``libmi355x_probe.so`` (``csrc/probe/probe.cpp``) over libamd_smi:
+             amd-smi initialised once per process, ~1-2 ms per GPU per probe.
+``python``   the ``amdsmi`` Python binding (same library, ~50 ms import).
+``fixture``  a recorded report (CI / hosts without the amdgpu driver).
+
+All return a ``mi355x-health/v1`` dict (:mod:`models.health`).  Driver or
+permission problems come back as ``{"error": ...}`` (verdict ``unknown``),
+never as an exception.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import json
+import socket
+import time
+from typing import Any, Dict, Optional
+
+from ..models.health import SCHEMA
+from .native import load_cdll
+
+_lib = None
+
+
+def _native():
+    global _lib
+    if _lib is None:
+        L = load_cdll("libmi355x_probe.so")
+        if L is None:
+            return None
+        L.mi355x_probe_open.restype = ctypes.c_int
+        L.mi355x_probe_json.restype = ctypes.c_void_p
+        L.mi355x_probe_json.argtypes = [ctypes.c_char_p]
+        L.mi355x_probe_free.argtypes = [ctypes.c_void_p]
+        L.mi355x_probe_gpu_count.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def native_available() -> bool:
+    return _native() is not None
+
+
+def probe_native(node: str) -> Dict[str, Any]:
+    L = _native()
+    if L is None:
+        raise RuntimeError("libmi355x_probe.so is not built (python -m k8s_gpu_node_checker_amd.build)")
+    ptr = L.mi355x_probe_json(node.encode())
+    try:
+        return json.loads(ctypes.string_at(ptr).decode())
+    finally:
+        L.mi355x_probe_free(ptr)
+
+
+def _xgmi_string(status) -> Optional[str]:
+    if not isinstance(status, dict):
+        return None
+    m = {"U": "U", "D": "D", "X": "X"}
+    return "".join(m.get(s, "N") for s in status.get("status", []))
+
+
+def probe_python(node: str) -> Dict[str, Any]:
+    rep: Dict[str, Any] = {"schema": SCHEMA, "node": node, "ts": time.time(), "probe": "python", "gpus": []}
+    t0 = time.perf_counter()
+    try:
+        import amdsmi as A
+        A.amdsmi_init()
+    except Exception as e:
+        rep["error"] = f"amdsmi init: {e}"
+        return rep
+    try:
+        for i, h in enumerate(A.amdsmi_get_processor_handles()):
+            g: Dict[str, Any] = {"index": i}
+
+            def q(fn, *a):
+                try:
+                    return fn(h, *a)
+                except Exception:
+                    return None
+            asic = q(A.amdsmi_get_gpu_asic_info)
+            if not asic:
+                g["error"] = "asic info unavailable"
+                rep["gpus"].append(g)
+                continue
+            g.update({"bdf": q(A.amdsmi_get_gpu_device_bdf), "uuid": q(A.amdsmi_get_gpu_device_uuid),
+                      "gfx": asic.get("target_graphics_version"), "market_name": asic.get("market_name"),
+                      "device_id": asic.get("device_id"), "cus": asic.get("num_compute_units")})
+            vb = q(A.amdsmi_get_gpu_vbios_info) or {}
+            g["vbios_name"] = vb.get("name")
+            vram = q(A.amdsmi_get_gpu_vram_info) or {}
+            g["vram_type"], g["vram_mb"] = vram.get("vram_type"), vram.get("vram_size")
+            ecc = q(A.amdsmi_get_gpu_total_ecc_count)
+            if ecc:
+                g.update({"ecc_correctable": ecc.get("correctable_count"),
+                          "ecc_uncorrectable": ecc.get("uncorrectable_count"),
+                          "ecc_deferred": ecc.get("deferred_count")})
+            bp = q(A.amdsmi_get_gpu_bad_page_info)
+            g["bad_pages"] = len(bp) if isinstance(bp, list) else None
+            g["xgmi"] = _xgmi_string(q(A.amdsmi_get_gpu_xgmi_link_status))
+            kfd = q(A.amdsmi_get_gpu_kfd_info) or {}
+            g["kfd"] = bool(kfd.get("kfd_id") not in (None, "N/A"))
+            g["compute_partition"] = q(A.amdsmi_get_gpu_compute_partition)
+            g["memory_partition"] = q(A.amdsmi_get_gpu_memory_partition)
+            try:
+                g["hotspot_c"] = A.amdsmi_get_temp_metric(h, A.AmdSmiTemperatureType.HOTSPOT,
+                                                          A.AmdSmiTemperatureMetric.CURRENT)
+            except Exception:
+                pass
+            rep["gpus"].append({k: v for k, v in g.items() if v is not None})
+    finally:
+        rep["probe_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    return rep
+
+
+def probe_fixture(path: str, node: str) -> Dict[str, Any]:
+    with open(path, encoding="utf-8") as f:
+        rep = json.load(f)
+    rep["node"] = node
+    rep["ts"] = time.time()
+    rep.setdefault("schema", SCHEMA)
+    rep["probe"] = "fixture"
+    return rep
+
+
+def probe(node: Optional[str] = None, source: str = "auto", fixture: Optional[str] = None) -> Dict[str, Any]:
+    node = node or socket.gethostname()
+    if source == "fixture" or (source == "auto" and fixture):
+        if not fixture:
+            raise ValueError("fixture source needs a path")
+        return probe_fixture(fixture, node)
+    if source == "native" or (source == "auto" and native_available()):
+        return probe_native(node)
+    return probe_python(node)

@@ -1,0 +1,138 @@
+"""Active MI355X diagnostics: ctypes front-end of ``libmi355x_diag.so`` (``csrc/diag/diag.hip``).
+
+Each test returns a dict that the node agent folds into its probe report
+under ``gpus[i].diag.<test>`` and that :func:`models.health.evaluate_gpu`
+turns into a failure when ``pass`` is false.
+
+Thresholds are deliberately conservative fractions of what a healthy MI355X
+delivers (numbers in ``profiles/``): they flag a GPU that is broken or badly
+throttled, not one that is a few percent off.
+
+The library is *required* on a GPU box: a missing build raises
+:class:`~k8s_gpu_node_checker_amd.ops.native.NativeUnavailable` instead of
+silently skipping the diagnostic.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import time
+from typing import Any, Dict, Optional
+
+from .native import NativeUnavailable, load_cdll
+
+# Pass thresholds (healthy MI355X: see profiles/diag_mi355x.json)
+GEMM_MIN_TFLOPS = 400.0       # bf16 MFMA GEMM 8192^3
+GEMM_MAX_REL_ERR = 2e-3       # vs fp32 reference, K = 8192 accumulation
+HBM_MIN_COPY_TBS = 3.5        # float4 copy (read + write bytes)
+MEMTEST_MAX_ERRORS = 0
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        L = load_cdll("libmi355x_diag.so", required=True)
+        assert L is not None
+        L.diag_last_error.restype = ctypes.c_char_p
+        L.diag_device_count.restype = ctypes.c_int
+        L.diag_device_arch.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.diag_gemm_bf16_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.diag_gemm_bf16.argtypes = [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_double)] * 3
+        L.diag_hbm_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int] + \
+            [ctypes.POINTER(ctypes.c_double)] * 3
+        L.diag_memtest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong),
+                                   ctypes.POINTER(ctypes.c_double)]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise RuntimeError(f"mi355x diag failed ({rc}): {lib().diag_last_error().decode(errors='replace')}")
+
+
+def device_count() -> int:
+    return int(lib().diag_device_count())
+
+
+def device_info(device: int = 0) -> Dict[str, Any]:
+    buf = ctypes.create_string_buffer(512)
+    _check(lib().diag_device_arch(device, buf, len(buf)))
+    arch, name, cus, mem = buf.value.decode().split("|")
+    return {"arch": arch, "name": name, "cus": int(cus), "mem_bytes": int(mem)}
+
+
+def gemm_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int, stream: int = 0) -> None:
+    """Launch the MFMA GEMM on caller-owned device memory: ``C = A @ Bt.T`` (bf16 in, fp32 out)."""
+    if m % 128 or n % 128 or k % 64:
+        raise ValueError("gemm: M, N must be multiples of 128 and K a multiple of 64")
+    _check(lib().diag_gemm_bf16_launch(a_ptr, bt_ptr, c_ptr, m, n, k, stream))
+
+
+def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, samples: int = 4096) -> Dict[str, Any]:
+    tf, err, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    t0 = time.perf_counter()
+    _check(lib().diag_gemm_bf16(device, size, size, size, warmup, iters, samples, ctypes.byref(tf),
+                                ctypes.byref(err), ctypes.byref(ms)))
+    ok = tf.value >= GEMM_MIN_TFLOPS and err.value <= GEMM_MAX_REL_ERR
+    return {"pass": ok, "tflops": round(tf.value, 1), "max_rel_err": err.value, "ms_per_gemm": round(ms.value, 4),
+            "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3),
+            "detail": "" if ok else f"{tf.value:.0f} TFLOP/s, rel err {err.value:.2e}"}
+
+
+def hbm(device: int = 0, gib: float = 4.0, iters: int = 10) -> Dict[str, Any]:
+    c, r, w = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    t0 = time.perf_counter()
+    _check(lib().diag_hbm_bandwidth(device, int(gib * (1 << 30)), iters, ctypes.byref(c), ctypes.byref(r),
+                                    ctypes.byref(w)))
+    ok = c.value >= HBM_MIN_COPY_TBS
+    return {"pass": ok, "copy_tbs": round(c.value, 3), "read_tbs": round(r.value, 3), "write_tbs": round(w.value, 3),
+            "gib": gib, "wall_s": round(time.perf_counter() - t0, 3),
+            "detail": "" if ok else f"copy {c.value:.2f} TB/s"}
+
+
+def memtest(device: int = 0, gib: float = 8.0, passes: int = 1, seed: int = 0x5EED) -> Dict[str, Any]:
+    errs, first, gbps = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_double()
+    t0 = time.perf_counter()
+    _check(lib().diag_memtest(device, int(gib * (1 << 30)), seed, passes, ctypes.byref(errs), ctypes.byref(first),
+                              ctypes.byref(gbps)))
+    ok = errs.value <= MEMTEST_MAX_ERRORS
+    res: Dict[str, Any] = {"pass": ok, "errors": errs.value, "gib": gib, "passes": passes,
+                           "gbps": round(gbps.value, 1), "wall_s": round(time.perf_counter() - t0, 3),
+                           "detail": "" if ok else f"{errs.value} bad 16-byte words"}
+    if errs.value:
+        res["first_bad_byte"] = first.value
+    return res
+
+
+LEVELS = {
+    0: (),
+    1: ("gemm_quick", "hbm_quick"),
+    2: ("gemm", "hbm", "memtest"),
+}
+
+
+def run(level: int = 1, device: int = 0) -> Dict[str, Dict[str, Any]]:
+    """Run the diagnostics of ``level`` on ``device`` (1 = ~1 s quick check, 2 = deep)."""
+    out: Dict[str, Dict[str, Any]] = {}
+    for test in LEVELS.get(level, ()):
+        try:
+            if test == "gemm_quick":
+                out["gemm"] = gemm(device, size=4096, warmup=2, iters=10, samples=1024)
+            elif test == "hbm_quick":
+                out["hbm"] = hbm(device, gib=2.0, iters=5)
+            elif test == "gemm":
+                out["gemm"] = gemm(device)
+            elif test == "hbm":
+                out["hbm"] = hbm(device)
+            elif test == "memtest":
+                out["memtest"] = memtest(device)
+        except NativeUnavailable:
+            raise
+        except Exception as e:  # a failing diagnostic is a verdict, not a crash
+            out[test.replace("_quick", "")] = {"pass": False, "detail": str(e)[:200]}
+    return out

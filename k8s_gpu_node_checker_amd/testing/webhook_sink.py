@@ -132,3 +132,23 @@ class WebhookSink(socketserver.ThreadingTCPServer):
 
     def __exit__(self, *exc: Any) -> None:
         self.stop()
+
+
+def main() -> int:
+    import argparse
+    ap = argparse.ArgumentParser(description="Slack webhook sink with fault injection")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--slow-s", type=float, default=11.0)
+    args = ap.parse_args()
+    sink = WebhookSink(args.host, args.port, args.slow_s)
+    print(json.dumps({"url": sink.base_url}), flush=True)
+    try:
+        sink.serve_forever(poll_interval=0.2)
+    except KeyboardInterrupt:
+        pass
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,148 @@
+"""MI355X-only tests (``pytest -m gpu`` on a gfx950 box via gpurun).
+
+Numerics of the HIP MFMA GEMM are checked against a plain PyTorch fp32
+reference of the same op; the probe is checked against what amd-smi reported
+on a real MI355X (profiles/amdsmi_mi355x.json).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def test_native_libraries_present(dev):
+    from k8s_gpu_node_checker_amd.ops import amdsmi_probe, diag, fastpath
+    assert fastpath.backend() == "native"
+    assert amdsmi_probe.native_available()
+    assert diag.device_count() >= 1
+    info = diag.device_info(0)
+    assert info["arch"].startswith("gfx950"), info
+    assert info["cus"] == 256, info
+
+
+def test_native_probe_reports_healthy_mi355x(dev):
+    from k8s_gpu_node_checker_amd.models.health import HEALTHY, HealthExpectations, evaluate_report
+    from k8s_gpu_node_checker_amd.ops.amdsmi_probe import probe_native
+    rep = probe_native("test-node")
+    assert not rep.get("error"), rep
+    g = rep["gpus"][0]
+    assert g["gfx"] == "gfx950"
+    assert "MI355" in g["market_name"] or "MI350" in g["market_name"]
+    assert g["vram_type"] == 5  # HBM3E
+    assert g["vram_mb"] > 280000
+    assert g["ecc_uncorrectable"] == 0
+    assert g["kfd"] is True
+    assert set(g["xgmi"]) <= set("UXDN")
+    v = evaluate_report(rep, len(rep["gpus"]), HealthExpectations(xgmi_links=g["xgmi"].count("U")))
+    assert v.state == HEALTHY, v.to_dict()
+    # amd-smi stays initialised: a second probe is fast
+    rep2 = probe_native("test-node")
+    assert rep2["probe_ms"] < 200, rep2["probe_ms"]
+
+
+def test_python_probe_agrees_with_native(dev):
+    pytest.importorskip("amdsmi")
+    from k8s_gpu_node_checker_amd.ops.amdsmi_probe import probe_native, probe_python
+    a = probe_native("n")["gpus"][0]
+    b = probe_python("n")["gpus"][0]
+    for k in ("gfx", "market_name", "vram_type", "vram_mb", "ecc_uncorrectable", "xgmi", "compute_partition",
+              "memory_partition", "cus"):
+        assert a.get(k) == b.get(k), (k, a.get(k), b.get(k))
+
+
+@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (256, 384, 192), (1024, 1024, 1024), (512, 2048, 4096),
+                                   (2048, 1024, 256)])
+def test_mfma_gemm_matches_fp32_reference(dev, m, n, k):
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m * 7 + n * 3 + k)
+    a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
+    bt = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
+    c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+    diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = a.float() @ bt.float().t()
+    assert not torch.isnan(c).any()
+    rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
+    assert rel < 1e-4 * max(1, k / 512), rel
+
+
+def test_mfma_gemm_identity_asymmetric(dev):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    m = n = k = 128
+    a = torch.eye(m, k, device=dev).to(torch.bfloat16)
+    idx = torch.arange(n * k, device=dev, dtype=torch.float32).reshape(n, k)
+    bt = (idx % 251).to(torch.bfloat16)  # exact in bf16, asymmetric
+    c = torch.empty(m, n, device=dev, dtype=torch.float32)
+    diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(c, bt.float().t())
+
+
+def test_gemm_rejects_bad_shapes():
+    from k8s_gpu_node_checker_amd.ops import diag
+    with pytest.raises(ValueError):
+        diag.gemm_launch(0, 0, 0, 100, 128, 64)
+
+
+def test_diag_gemm_burn_in(dev):
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.gemm(0, size=4096, warmup=2, iters=10, samples=512)
+    print(json.dumps(r))
+    assert r["max_rel_err"] < diag.GEMM_MAX_REL_ERR
+    assert r["pass"], r
+
+
+def test_diag_hbm_bandwidth(dev):
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.hbm(0, gib=2.0, iters=5)
+    print(json.dumps(r))
+    assert r["pass"], r
+    assert r["copy_tbs"] < 8.5  # cannot beat the 8 TB/s HBM3E spec (sanity of the timing)
+
+
+def test_diag_memtest_clean(dev):
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.memtest(0, gib=1.0, passes=1)
+    print(json.dumps(r))
+    assert r["errors"] == 0 and r["pass"], r
+
+
+def test_agent_with_diagnostics_is_healthy(dev):
+    from k8s_gpu_node_checker_amd.agent.agent import Agent
+    from k8s_gpu_node_checker_amd.models.health import HealthExpectations, evaluate_report
+    ag = Agent("gpu-node", source="native", diag_level=1, devices=[0])
+    rep = ag.probe_once()
+    g = rep["gpus"][0]
+    assert g["diag"]["gemm"]["pass"] and g["diag"]["hbm"]["pass"], g["diag"]
+    v = evaluate_report(rep, len(rep["gpus"]), HealthExpectations(xgmi_links=g["xgmi"].count("U")))
+    assert v.ok, v.to_dict()
+
+
+def test_smoke(dev):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import __graft_entry__
+    __graft_entry__.smoke()
+
+
+def test_bench_contract_on_gpu(repo):
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--steps", "50", "--warmup", "5"],
+                       capture_output=True, text=True, timeout=600, cwd=repo)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["check_ok"] and d["n_gpus"] == 1 and d["value"] > 0
+    assert d["probe"]["source"] == "native", d["probe"]
