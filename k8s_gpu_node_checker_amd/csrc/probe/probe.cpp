@@ -143,6 +143,11 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
     kv_str(o, "device_id", buf);
   }
   if (asic.num_of_compute_units != UINT32_MAX) kv_u64(o, "cus", asic.num_of_compute_units);
+  amdsmi_board_info_t board;
+  memset(&board, 0, sizeof board);
+  // FRU product name does not depend on libdrm's amdgpu.ids (market_name does:
+  // inside a process that loaded another libdrm it degrades to "AMD Radeon Graphics")
+  if (amdsmi_get_gpu_board_info(h, &board) == AMDSMI_STATUS_SUCCESS) kv_str(o, "product_name", board.product_name);
   amdsmi_vbios_info_t vb;
   memset(&vb, 0, sizeof vb);
   if (amdsmi_get_gpu_vbios_info(h, &vb) == AMDSMI_STATUS_SUCCESS) kv_str(o, "vbios_name", vb.name);

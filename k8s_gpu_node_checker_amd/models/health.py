@@ -29,7 +29,8 @@ SCHEMA = "mi355x-health/v1"
 
 # --- MI355X / gfx950 expectations (CDNA4) ------------------------------------
 GFX_TARGET = "gfx950"
-PRODUCT_TOKENS = ("MI355", "MI350")          # market_name / vbios name on gfx950 parts
+PRODUCT_TOKENS = ("MI355", "MI350")          # product / market / vbios names on gfx950 parts
+MI35X_DEVICE_IDS = frozenset(("0x75a3",))     # measured: MI355X OAM (amd-smi DEVICE_ID)
 HBM3E_VRAM_TYPE = 5                           # amdsmi.h AMDSMI_VRAM_TYPE_HBM3E
 VRAM_MB_FULL = 294896                         # measured vram_size, SPX/NPS1 (288 GB class)
 VRAM_MIN_FRACTION = 0.97
@@ -88,6 +89,19 @@ class Verdict:
         return d
 
 
+def is_mi35x(g: Dict[str, Any]) -> bool:
+    """Identify an MI355X/MI350X from any of the names amd-smi reports, or its PCI device id.
+
+    ``market_name`` comes from libdrm's ``amdgpu.ids`` and degrades to "AMD
+    Radeon Graphics" when another libdrm copy (e.g. PyTorch's) is loaded first;
+    the FRU ``product_name`` and the VBIOS name do not.
+    """
+    names = " ".join(str(g.get(k) or "") for k in ("product_name", "market_name", "vbios_name"))
+    if any(t in names for t in PRODUCT_TOKENS):
+        return True
+    return str(g.get("device_id", "")).lower() in MI35X_DEVICE_IDS
+
+
 def _nps(mem_partition: Any) -> int:
     if isinstance(mem_partition, str) and mem_partition.upper().startswith("NPS"):
         try:
@@ -108,9 +122,8 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str],
     gfx = g.get("gfx")
     if gfx != GFX_TARGET:
         fail.append(f"gpu{idx}: target {gfx!r} is not {GFX_TARGET}")
-    name = f"{g.get('market_name') or ''} {g.get('vbios_name') or ''}"
-    if exp.require_product and not any(t in name for t in PRODUCT_TOKENS):
-        fail.append(f"gpu{idx}: product {g.get('market_name')!r} is not MI355X/MI350X")
+    if exp.require_product and not is_mi35x(g):
+        fail.append(f"gpu{idx}: product {g.get('product_name') or g.get('market_name')!r} is not MI355X/MI350X")
     vt = g.get("vram_type")
     if vt is not None and vt != HBM3E_VRAM_TYPE and vt != "HBM3E":
         fail.append(f"gpu{idx}: VRAM type {vt} is not HBM3E")

@@ -89,6 +89,8 @@ def probe_python(node: str) -> Dict[str, Any]:
             g.update({"bdf": q(A.amdsmi_get_gpu_device_bdf), "uuid": q(A.amdsmi_get_gpu_device_uuid),
                       "gfx": asic.get("target_graphics_version"), "market_name": asic.get("market_name"),
                       "device_id": asic.get("device_id"), "cus": asic.get("num_compute_units")})
+            board = q(A.amdsmi_get_gpu_board_info) or {}
+            g["product_name"] = board.get("product_name")
             vb = q(A.amdsmi_get_gpu_vbios_info) or {}
             g["vbios_name"] = vb.get("name")
             vram = q(A.amdsmi_get_gpu_vram_info) or {}

@@ -105,7 +105,8 @@ def mi355x_probe_report(node: str, gpus: int = 8, ts: Optional[float] = None, **
     entries = []
     for i in range(gpus):
         g = {"index": i, "bdf": f"0000:{0x05 + 0x10 * i:02x}:00.0", "gfx": "gfx950",
-             "market_name": "AMD Instinct MI355 OAM", "vbios_name": "AMD MI355X", "device_id": "0x75a3",
+             "market_name": "AMD Instinct MI355 OAM", "product_name": "AMD Instinct MI355 OAM",
+             "vbios_name": "AMD MI355X", "device_id": "0x75a3",
              "cus": 256, "vram_type": 5, "vram_mb": 294896, "ecc_correctable": 0, "ecc_uncorrectable": 0,
              "ecc_deferred": 0, "bad_pages": 0, "xgmi": "XUUUUUUU", "kfd": True,
              "compute_partition": "SPX", "memory_partition": "NPS1", "hotspot_c": 45}
