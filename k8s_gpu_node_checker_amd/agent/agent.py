@@ -127,8 +127,11 @@ def serve(agent: Agent, host: str, port: int) -> ThreadingHTTPServer:
             self.end_headers()
             self.wfile.write(body)
 
-    srv = ThreadingHTTPServer((host, port), H)
-    srv.daemon_threads = True
+    class Srv(ThreadingHTTPServer):
+        daemon_threads = True
+        request_queue_size = 128  # the checker's fan-out connects in bursts
+
+    srv = Srv((host, port), H)
     threading.Thread(target=srv.serve_forever, daemon=True).start()
     return srv
 

@@ -502,6 +502,7 @@ struct NodeScan {
   Ref labels;                // dict (possibly empty) or null
   Ref health;                // str or nullptr
   Ref taints;                // list
+  Ref internal_ip;           // str or nullptr (first InternalIP of status.addresses)
   bool unschedulable = false;
   bool ready = false;
   std::vector<Qty> cap, alloc;
@@ -632,6 +633,7 @@ void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scrat
       q.value.reset(nullptr);
     }
   ns.ready = false;
+  ns.internal_ip.reset(nullptr);
   if (c.peek() != '{') {
     skip_value(c);
     return;
@@ -641,6 +643,32 @@ void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scrat
       parse_resource_map(cc, ks, ns.cap, scratch);
     } else if (raw_equals(k, "allocatable", scratch)) {
       parse_resource_map(cc, ks, ns.alloc, scratch);
+    } else if (raw_equals(k, "addresses", scratch)) {
+      ns.internal_ip.reset(nullptr);
+      if (cc.peek() != '[') {
+        skip_value(cc);
+        return;
+      }
+      for_elements(cc, [&](Cursor& c3) {
+        if (c3.peek() != '{') {
+          skip_value(c3);
+          return;
+        }
+        bool internal = false;
+        Ref addr;
+        for_members(c3, [&](const RawStr& fk, Cursor& c4) {
+          if (raw_equals(fk, "type", scratch) && c4.peek() == '"') {
+            internal = raw_equals(read_raw_string(c4), "InternalIP", scratch);
+          } else if (raw_equals(fk, "address", scratch) && c4.peek() == '"') {
+            addr.reset(make_str(read_raw_string(c4), scratch));
+          } else {
+            if (raw_equals(fk, "type", scratch)) internal = false;
+            if (raw_equals(fk, "address", scratch)) addr.reset(nullptr);
+            skip_value(c4);
+          }
+        });
+        if (internal && addr.o && !ns.internal_ip.o) ns.internal_ip.reset(addr.release());
+      });
     } else if (raw_equals(k, "conditions", scratch)) {
       ns.ready = false;
       if (cc.peek() != '[') {
@@ -720,8 +748,9 @@ void emit_node(NodeScan& ns, const KeySpec& ks, bool use_alloc, bool want_extras
     Ref capd(breakdown_dict(ks, ns.cap, nullptr));
     Ref allocd(breakdown_dict(ks, ns.alloc, nullptr));
     PyObject* health = ns.health.o ? ns.health.o : Py_None;
+    PyObject* ip = ns.internal_ip.o ? ns.internal_ip.o : Py_None;
     Ref ex(PyObject_CallFunctionObjArgs(extras_cls, ns.ready ? Py_True : Py_False, capd.o, allocd.o,
-                                        ns.unschedulable ? Py_True : Py_False, health, nullptr));
+                                        ns.unschedulable ? Py_True : Py_False, health, ip, nullptr));
     if (!ex.o) {
       PyErr_Clear();
       throw Fallback{"NodeExtras()"};

@@ -294,7 +294,8 @@ def connection_from_config(cfg: Dict[str, Any], context: Optional[str] = None) -
     return conn
 
 
-def incluster_connection(sa_dir: str = SA_DIR) -> Optional[ClusterConnection]:
+def incluster_connection(sa_dir: Optional[str] = None) -> Optional[ClusterConnection]:
+    sa_dir = sa_dir or SA_DIR
     host = os.environ.get("KUBERNETES_SERVICE_HOST")
     port = os.environ.get("KUBERNETES_SERVICE_PORT")
     token_path = os.path.join(sa_dir, "token")

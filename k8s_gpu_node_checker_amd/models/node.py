@@ -75,15 +75,16 @@ def project_node(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEY
 class NodeExtras:
     """Side information the default report does not show but the health gate uses."""
 
-    __slots__ = ("ready_condition", "capacity", "allocatable", "unschedulable", "health_annotation")
+    __slots__ = ("ready_condition", "capacity", "allocatable", "unschedulable", "health_annotation", "internal_ip")
 
     def __init__(self, ready_condition: bool, capacity: Dict[str, int], allocatable: Dict[str, int],
-                 unschedulable: bool, health_annotation: Optional[str]):
+                 unschedulable: bool, health_annotation: Optional[str], internal_ip: Optional[str] = None):
         self.ready_condition = ready_condition
         self.capacity = capacity
         self.allocatable = allocatable
         self.unschedulable = unschedulable
         self.health_annotation = health_annotation
+        self.internal_ip = internal_ip
 
     def to_dict(self) -> Dict[str, Any]:
         return {
@@ -91,6 +92,7 @@ class NodeExtras:
             "capacity": self.capacity,
             "allocatable": self.allocatable,
             "unschedulable": self.unschedulable,
+            "internal_ip": self.internal_ip,
         }
 
 
@@ -99,12 +101,20 @@ def node_extras(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS
     status = _get(node, "status")
     ann = _get(meta, "annotations")
     raw = ann.get(HEALTH_ANNOTATION) if isinstance(ann, Mapping) else None
+    ip = None
+    addrs = _get(status, "addresses")
+    if isinstance(addrs, list):
+        for a in addrs:
+            if isinstance(a, Mapping) and a.get("type") == "InternalIP" and isinstance(a.get("address"), str):
+                ip = a["address"]
+                break
     return NodeExtras(
         ready_condition=is_ready(node),
         capacity=gpu_breakdown(_get(status, "capacity"), keys),
         allocatable=gpu_breakdown(_get(status, "allocatable"), keys),
         unschedulable=bool(_get(_get(node, "spec"), "unschedulable")),
         health_annotation=raw if isinstance(raw, str) else None,
+        internal_ip=ip,
     )
 
 

@@ -92,7 +92,8 @@ def _merge_patch(target: Dict[str, Any], patch: Dict[str, Any]) -> None:
 class MockConfig:
     def __init__(self, token: Optional[str] = None, status: Optional[int] = None, fail_first: int = 0,
                  fail_status: int = 503, retry_after: Optional[str] = None, delay: float = 0.0,
-                 expire_continue: bool = False, reset: bool = False):
+                 expire_continue: bool = False, reset: bool = False, gzip: bool = False,
+                 chunked: bool = False):
         self.token = token
         self.status = status
         self.fail_first = fail_first
@@ -101,6 +102,8 @@ class MockConfig:
         self.delay = delay
         self.expire_continue = expire_continue
         self.reset = reset
+        self.gzip = gzip
+        self.chunked = chunked
 
 
 class _Handler(BaseHTTPRequestHandler):
@@ -112,6 +115,10 @@ class _Handler(BaseHTTPRequestHandler):
 
     def _send(self, status: int, body: bytes, extra: Optional[Dict[str, str]] = None,
               reason: Optional[str] = None) -> None:
+        if self.server.cfg.gzip and "gzip" in (self.headers.get("Accept-Encoding") or ""):
+            import gzip
+            body = gzip.compress(body, compresslevel=1)
+            extra = dict(extra or {}, **{"Content-Encoding": "gzip"})
         self.send_response(status, reason)
         self.send_header("Content-Type", "application/json")
         self.send_header("Content-Length", str(len(body)))
@@ -176,7 +183,18 @@ class _Handler(BaseHTTPRequestHandler):
                 except ValueError:
                     self._send(400, self._status_body(400, "BadRequest", "invalid continue token"))
                     return
-            self._send(200, self.server.state.page(limit, start))
+            body = self.server.state.page(limit, start)
+            if self.server.cfg.chunked:
+                self.send_response(200)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Transfer-Encoding", "chunked")
+                self.end_headers()
+                for i in range(0, len(body), 4096):
+                    piece = body[i:i + 4096]
+                    self.wfile.write(b"%x\r\n" % len(piece) + piece + b"\r\n")
+                self.wfile.write(b"0\r\n\r\n")
+                return
+            self._send(200, body)
             return
         if path.startswith("/api/v1/nodes/"):
             node = self.server.state.find(unquote(path[len("/api/v1/nodes/"):]))

@@ -1,0 +1,122 @@
+"""Node agent (fixture probe) -> annotation / HTTP, and the checker's async probe fan-out."""
+import json
+
+import pytest
+
+from k8s_gpu_node_checker_amd.agent import agent as A
+from k8s_gpu_node_checker_amd.kube.client import KubeClient
+from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+from k8s_gpu_node_checker_amd.testing import fixtures
+from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+
+
+@pytest.fixture
+def fixture_report(tmp_path):
+    p = tmp_path / "probe.json"
+    p.write_text(json.dumps(fixtures.mi355x_probe_report("x", gpus=8)))
+    return str(p)
+
+
+def test_agent_fixture_probe_and_annotation(mock_cluster, fixture_report):
+    srv = mock_cluster(fixtures.cluster(2, "amd"))
+    ag = A.Agent("mi355x-node-0001", source="fixture", fixture=fixture_report)
+    rep = ag.probe_once()
+    assert rep["state"] == "healthy" and rep["node"] == "mi355x-node-0001"
+    with KubeClient(ClusterConnection(srv.url)) as c:
+        ag.publish_annotation(c, rep)
+        node = c.get_node("mi355x-node-0001")
+    assert json.loads(node["metadata"]["annotations"]["amd.com/mi355x-health"])["state"] == "healthy"
+
+
+def test_agent_main_once(mock_cluster, fixture_report, tmp_path, capsys):
+    srv = mock_cluster(fixtures.cluster(1, "amd"))
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    rc = A.main(["--node", "mi355x-node-0000", "--source", "fixture", "--fixture", fixture_report, "--once",
+                 "--publish", "annotation,stdout", "--kubeconfig", kc])
+    assert rc == 0
+    assert json.loads(capsys.readouterr().out)["schema"] == "mi355x-health/v1"
+    assert srv.log[-1]["method"] == "PATCH"
+
+
+def test_agent_http_endpoint(fixture_report):
+    from k8s_gpu_node_checker_amd.utils.http import request
+    ag = A.Agent("n", source="fixture", fixture=fixture_report)
+    srv = A.serve(ag, "127.0.0.1", 0)
+    base = f"http://127.0.0.1:{srv.server_address[1]}"
+    try:
+        assert "no probe yet" in request(base + "/probe").text
+        ag.probe_once()
+        assert json.loads(request(base + "/probe").body)["state"] == "healthy"
+        m = request(base + "/metrics").text
+        assert 'mi355x_gpu_xgmi_links_up{gpu="0",bdf="0000:05:00.0"} 7' in m
+        assert request(base + "/nope").status == 404
+    finally:
+        srv.shutdown()
+
+
+def test_checker_probe_endpoint_fanout(run_cli, mock_cluster, tmp_path, fixture_report):
+    # three nodes whose InternalIPs are 127.0.0.x; agents for two of them, one of them unhealthy
+    good = A.Agent("a", source="fixture", fixture=fixture_report)
+    good.probe_once()
+    bad = A.Agent("b", source="fixture", fixture=fixture_report)
+    r = bad.probe_once()
+    r["gpus"][0]["ecc_uncorrectable"] = 3
+    srv_a = A.serve(good, "127.0.0.1", 0)
+    port = srv_a.server_address[1]
+    srv_b = A.serve(bad, "127.0.0.2", port)
+    try:
+        nodes = []
+        for i, name in enumerate(["a", "b", "c"]):
+            n = fixtures.realistic_node(name, index=i)
+            n["status"]["addresses"][0]["address"] = f"127.0.0.{i + 1}"
+            nodes.append(n)
+        srv = mock_cluster(nodes)
+        kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+        p = run_cli(["--kubeconfig", kc, "--json-extended", "--probe-endpoint", f"http://{{ip}}:{port}/probe",
+                     "--probe-timeout", "1", "--probe-unknown", "deny"])
+        doc = json.loads(p.stdout)
+        states = [n["health"]["state"] for n in doc["mi355x"]["nodes"]]
+        assert states == ["healthy", "unhealthy", "unknown"]
+        assert [n["ready"] for n in doc["nodes"]] == [True, False, False]
+        assert p.returncode == 0
+    finally:
+        srv_a.shutdown()
+        srv_b.shutdown()
+
+
+def test_fanout_is_concurrent(fixture_report):
+    import asyncio
+    import time
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+    import threading
+    from k8s_gpu_node_checker_amd.parallel import fanout
+
+    class Slow(BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            time.sleep(0.3)
+            body = b'{"schema": "mi355x-health/v1"}'
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+    class Srv(ThreadingHTTPServer):
+        request_queue_size = 64  # default backlog of 5 would serialise the burst of connects
+
+    s = Srv(("127.0.0.1", 0), Slow)
+    s.daemon_threads = True
+    threading.Thread(target=s.serve_forever, daemon=True).start()
+    try:
+        url = f"http://127.0.0.1:{s.server_address[1]}/probe"
+        t = time.time()
+        out = asyncio.run(fanout.fetch_all([{"name": str(i), "url": url} for i in range(16)], concurrency=16))
+        assert time.time() - t < 1.5  # 16 x 0.3 s serially would be 4.8 s
+        assert all(o == {"schema": "mi355x-health/v1"} for o in out)
+        t = time.time()
+        out = asyncio.run(fanout.fetch_all([{"name": "x", "url": url}], timeout=0.05))
+        assert out[0]["error"].startswith("timeout") and time.time() - t < 1
+    finally:
+        s.shutdown()

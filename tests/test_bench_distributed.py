@@ -1,0 +1,85 @@
+"""bench.py contract (single process and torchrun world_size=2 on gloo) and the RCCL/xGMI
+collective diagnostic's logic on gloo (the GPU run uses backend nccl = RCCL)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def env():
+    e = dict(os.environ)
+    e["CUDA_VISIBLE_DEVICES"] = ""  # CPU path even if torch sees a device
+    e["HIP_VISIBLE_DEVICES"] = ""
+    return e
+
+
+def last_json(out):
+    lines = [x for x in out.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_single_process_contract():
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "30", "--warmup", "3"],
+                       capture_output=True, text=True, timeout=300, env=env(), cwd=REPO)
+    assert p.returncode == 0, p.stderr
+    d = last_json(p.stdout)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 30 and d["warmup"] == 3 and d["scaling"] == "weak"
+    assert d["higher_is_better"] is True and d["check_ok"] is True
+    assert d["value"] == pytest.approx(1 * 30 / (d["ms_per_step"] * 30 / 1e3), rel=0.01)
+    assert d["vs_baseline"] == pytest.approx(d["value"] / (1 / 2.17e-3), rel=0.01)
+    assert d["config"]["global_batch"] == 1 and d["backend"] == "native"
+
+
+def test_bench_torchrun_two_ranks_gloo():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2",
+           "--steps", "20", "--warmup", "2"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env(), cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = last_json(p.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["check_ok"] and d["health"] == {"healthy": 2}
+
+
+def test_bench_sweep_mode_and_slack():
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "10", "--warmup", "2", "--mode",
+                        "sweep", "--slack", "--nodes", "4"], capture_output=True, text=True, timeout=300, env=env(),
+                       cwd=REPO)
+    assert p.returncode == 0, p.stderr
+    d = last_json(p.stdout)
+    assert d["config"]["mode"] == "sweep" and d["config"]["slack"] and d["check_ok"]
+    assert d["config"]["global_batch"] == 4
+
+
+def test_collectives_gloo_two_ranks():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "-m", "k8s_gpu_node_checker_amd.parallel.collectives",
+           "--sizes", "4K,1M", "--iters", "3", "--warmup", "1", "--backend", "gloo"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env(), cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = last_json(p.stdout)
+    assert d["backend"] == "gloo" and d["world"] == 2 and d["pass"]
+    assert all(r["correct"] for r in d["rows"]) and d["rows"][1]["busbw_gbps"] > 0
+
+
+def test_collective_verdict_logic():
+    from k8s_gpu_node_checker_amd.parallel.collectives import parse_size, verdict
+    assert parse_size("256M") == 256 << 20 and parse_size("1.5K") == 1536
+    rows = [{"bytes": 1 << 30, "busbw_gbps": 50.0, "correct": True}]
+    assert not verdict(rows, 8)["pass"] and verdict(rows, 8, min_busbw=40)["pass"]
+    assert not verdict([dict(rows[0], correct=False)], 8, 1)["pass"]

@@ -1,0 +1,101 @@
+"""R7 .env loading, alert de-dup state file, Prometheus textfile output."""
+import json
+import os
+
+import pytest
+
+from k8s_gpu_node_checker_amd.utils import dotenv, prom, statefile
+
+
+def test_dotenv_parsing(tmp_path, monkeypatch):
+    p = tmp_path / ".env"
+    p.write_text("# comment\nSLACK_WEBHOOK_URL=https://hooks/x # trailing\nexport A='lit ${B}'\nB=\"two\\nlines\"\n"
+                 "C=${B}-${MISSING:-dflt}\nNOVAL\nEXISTING=file\n")
+    monkeypatch.setenv("EXISTING", "env")
+    vals = dotenv.dotenv_values(str(p))
+    assert vals["SLACK_WEBHOOK_URL"] == "https://hooks/x"
+    assert vals["A"] == "lit ${B}"
+    assert vals["B"] == "two\nlines"
+    assert vals["C"] == "two\nlines-dflt"
+    assert vals["NOVAL"] is None
+    for k in ("SLACK_WEBHOOK_URL", "A", "B", "C"):
+        monkeypatch.delenv(k, raising=False)
+    assert dotenv.load_dotenv(str(p))
+    assert os.environ["EXISTING"] == "env"  # real env wins (override=False)
+    assert os.environ["SLACK_WEBHOOK_URL"] == "https://hooks/x"
+
+
+def test_find_dotenv_walks_up(tmp_path):
+    (tmp_path / ".env").write_text("X=1\n")
+    deep = tmp_path / "a" / "b"
+    deep.mkdir(parents=True)
+    assert dotenv.find_dotenv(start=str(deep)) == str(tmp_path / ".env")
+
+
+class R:
+    def __init__(self, code, nodes, slack=None):
+        self.exit_code = code
+        self.gpu_nodes = nodes
+        self.ready_gpu_nodes = [n for n in nodes if n["ready"]]
+        self.slack_sent = slack
+        self.verdicts = []
+        self.tracer = None
+
+
+def node(name, ready):
+    return {"name": name, "ready": ready, "gpus": 8, "gpu_breakdown": {"amd.com/gpu": 8}}
+
+
+def test_state_dedup_and_recovery(tmp_path):
+    path = str(tmp_path / "state.json")
+    bad = R(3, [node("a", False)])
+    good = R(0, [node("a", True)])
+    assert statefile.should_notify(None, bad, only_on_error=True)
+    statefile.save(path, bad)
+    prev = statefile.load(path)
+    assert prev["exit_code"] == 3 and prev["not_ready"] == ["a"] and prev["runs"] == 1
+    assert not statefile.should_notify(prev, bad, only_on_error=True)  # unchanged: no re-alert
+    assert statefile.should_notify(prev, good, only_on_error=True)  # recovery
+    statefile.save(path, good, prev)
+    prev = statefile.load(path)
+    assert not statefile.should_notify(prev, good, only_on_error=True)
+    assert statefile.load(str(tmp_path / "missing")) is None
+
+
+def test_cli_slack_on_change(run_cli, mock_cluster, sink, tmp_path):
+    from k8s_gpu_node_checker_amd.testing import fixtures
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+    srv = mock_cluster(fixtures.golden("notready"))
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    args = ["--kubeconfig", kc, "--slack-webhook", sink.url("200"), "--slack-only-on-error",
+            "--state-file", str(tmp_path / "st.json"), "--slack-on-change"]
+    for _ in range(3):
+        assert run_cli(args).returncode == 3
+    assert len(sink.requests) == 1  # first failure only
+    srv.state.set_nodes(fixtures.golden("readme"))
+    assert run_cli(args).returncode == 0
+    assert len(sink.requests) == 2  # recovery announced
+    assert run_cli(args).returncode == 0
+    assert len(sink.requests) == 2
+
+
+def test_prometheus_textfile(run_cli, mock_cluster, tmp_path):
+    from k8s_gpu_node_checker_amd.testing import fixtures
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+    srv = mock_cluster(fixtures.cluster(2, "amd", not_ready=[1], with_health=True))
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    out = tmp_path / "m" / "gpu.prom"
+    p = run_cli(["--kubeconfig", kc, "--prometheus-textfile", str(out)])
+    assert p.returncode == 0
+    text = out.read_text()
+    assert "k8s_gpu_checker_gpu_nodes 2" in text and "k8s_gpu_checker_ready_gpu_nodes 1" in text
+    assert 'k8s_gpu_checker_node_ready{node="mi355x-node-0001"} 0' in text
+    assert 'k8s_gpu_checker_mi355x_health{node="mi355x-node-0000",state="healthy"} 1' in text
+    p = run_cli(["--kubeconfig", str(tmp_path / "missing"), "--prometheus-textfile", str(out)])
+    assert p.returncode == 1 and "k8s_gpu_checker_exit_code 1" in out.read_text()
+
+
+def test_prom_escaping():
+    r = R(0, [node('we"ird\\name', True)])
+    lines = prom.render(r)
+    assert 'k8s_gpu_checker_node_ready{node="we\\"ird\\\\name"} 1' in lines

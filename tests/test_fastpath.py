@@ -1,0 +1,154 @@
+"""Native NodeList scanner / JSON emitter == the pure-Python reference semantics (byte for byte)."""
+import json
+
+import pytest
+from hypothesis import HealthCheck, given, settings, strategies as st
+
+from k8s_gpu_node_checker_amd.models.node import HEALTH_ANNOTATION, NodeExtras, ScanResult, scan_items
+from k8s_gpu_node_checker_amd.models.resources import GPU_RESOURCE_KEYS
+from k8s_gpu_node_checker_amd.ops import fastpath
+from k8s_gpu_node_checker_amd.testing import fixtures
+
+ext = fastpath.ext()
+pytestmark = pytest.mark.skipif(ext is None, reason="native fast path not built")
+
+
+def native_scan(body, src="capacity", extras=True):
+    r = ScanResult()
+    tok = ext.scan_nodelist(body, r, GPU_RESOURCE_KEYS, src == "allocatable", extras, HEALTH_ANNOTATION, NodeExtras)
+    return r, tok
+
+
+def py_scan(body, src="capacity", extras=True):
+    doc = json.loads(body)
+    r = scan_items(doc.get("items") or [], None, GPU_RESOURCE_KEYS, src, extras)
+    tok = (doc.get("metadata") or {}).get("continue") or None
+    return r, (tok, r.items_seen)
+
+
+def canon(r):
+    ex = [dict(e.to_dict(), h=e.health_annotation) for e in r.extras]
+    return json.dumps([r.gpu_nodes, r.ready_gpu_nodes, ex, r.items_seen], ensure_ascii=False)
+
+
+def assert_same(body, src="capacity"):
+    try:
+        a, ta = native_scan(body, src)
+    except ext.FallbackError:
+        return "fallback"
+    b, tb = py_scan(body, src)
+    assert canon(a) == canon(b)
+    assert ta == tb
+    return "native"
+
+
+@pytest.mark.parametrize("g", fixtures.GOLDEN)
+@pytest.mark.parametrize("src", ["capacity", "allocatable"])
+def test_golden(g, src):
+    assert assert_same(json.dumps(fixtures.node_list(fixtures.golden(g), "tok")).encode(), src) == "native"
+
+
+def test_realistic_cluster_with_health_and_addresses():
+    body = json.dumps(fixtures.node_list(fixtures.cluster(50, "mixed", not_ready=[3], with_health=True))).encode()
+    assert assert_same(body) == "native"
+    r, _ = native_scan(body)
+    assert r.extras[0].internal_ip == "10.0.0.0" and r.extras[0].health_annotation.startswith("{")
+
+
+EDGE_BODIES = [
+    b'{"items": null}',
+    b'{"items": []}',
+    b'{"metadata": {"continue": ""}, "items": []}',
+    b'{"items": [{"metadata": {"name": "a"}, "status": {"capacity": {"amd.com/gpu": 8},'
+    b' "conditions": [{"type": "Ready", "status": "True"}]}}]}',
+    b'{"items": [{"metadata": {"name": "a"}, "status": {"capacity": {"amd.com/gpu": "8", "amd.com/gpu": "2"}}}]}',
+    b'{"items": [{"metadata": {"name": "a"}, "status": {"capacity": {"amd.com/gpu": " 8 "}}}]}',
+    b'{"items": [{"metadata": {"name": "a"}, "status": {"capacity": {"amd.com/gpu": "1_0"}}}]}',
+    b'{"items": [{"metadata": {"name": "a"}, "status": {"capacity": {"amd.com/gpu": 8.0, "nvidia.com/gpu": true}}}]}',
+    b'{"items": [{"metadata": {"name": "a"}, "status": {"capacity": {"amd.com/gpu": null, "nvidia.com/gpu": "-1"}}}]}',
+    b'{"items": [{"metadata": {"name": "a\\u00e9\\ud83d\\ude00", "labels": {"k\\"q": "v\\n"}},'
+    b' "status": {"capacity": {"amd\\u002ecom/gpu": "3"}, "conditions": [{"type": "Re\\u0061dy", "status": "True"}]}}]}',
+    b'{"items": [{"metadata": null, "spec": null, "status": {"capacity": {"amd.com/gpu": "1"}}}]}',
+    b'{"items": [{"metadata": {}, "status": {"capacity": {"amd.com/gpu": "1"}}}]}',
+    b'{"items": [{"metadata": {"name": "a"}, "spec": {"taints": [{"key": "k"}, 5, {"effect": "NoSchedule", "value": null}]},'
+    b' "status": {"capacity": {"amd.com/gpu": "1"}}}]}',
+    b'{"items": [{"metadata": {"name": "a"}, "status": {"capacity": {"amd.com/gpu": "1"},'
+    b' "conditions": [{"type": "Ready", "status": "True", "status": "False"}]}}]}',
+    b'{"items": [{"status": {"capacity": {"amd.com/gpu": "1"}}, "status": {"capacity": {"nvidia.com/gpu": "2"}}}]}',
+    b'{"items": [5, "x", null, {"metadata": {"name": "b"}, "status": {"capacity": {"amd.com/gpu": "99999999999999999999"}}}]}',
+    b'{"items": [{"metadata": {"name": "a", "labels": {}}, "status": {"capacity": {"amd.com/gpu": "1"},'
+    b' "extra": [1, 2.5e3, -0.1, NaN, true, {"x": [[]]}]}}]}',
+    b'  \n{"kind":"NodeList","items":[{"metadata":{"name":"w"},"status":{"capacity":{"amd.com/gpu":"4"}}}]}\n',
+]
+
+
+@pytest.mark.parametrize("body", EDGE_BODIES)
+def test_edge_shapes(body):
+    assert_same(body)
+
+
+@pytest.mark.parametrize("body", [b"[]", b'{"items": {}}', b'{"items": [', b"", b'{"items": [{"metadata": {"name": 5}}]}',
+                                  b'{"items": [{"metadata": {"labels": ["x"]}}]}', b'{"a": 1} x'])
+def test_unmodelled_or_malformed_falls_back_without_side_effects(body):
+    r = ScanResult()
+    with pytest.raises(ext.FallbackError):
+        ext.scan_nodelist(body, r, GPU_RESOURCE_KEYS, False, True, HEALTH_ANNOTATION, NodeExtras)
+    assert r.gpu_nodes == [] and r.items_seen == 0
+
+
+def test_scan_page_wrapper_falls_back_to_python():
+    r = ScanResult()
+    tok, n = fastpath.scan_page(b'{"items": [{"metadata": {"name": 5}, "status": {"capacity": {"amd.com/gpu": "1"}}}]}', r)
+    assert n == 1 and r.gpu_nodes[0]["name"] == 5
+    with pytest.raises(ValueError):
+        fastpath.scan_page(b"[1]", ScanResult())
+
+
+scalar = st.one_of(st.none(), st.booleans(), st.integers(-5, 10), st.text(max_size=6),
+                   st.sampled_from(["0", "8", "1k", " 3", "+2", "", "Ready", "True", "False"]))
+cap = st.dictionaries(st.sampled_from(list(GPU_RESOURCE_KEYS) + ["cpu"]), scalar, max_size=5)
+cond = st.fixed_dictionaries({}, optional={"type": st.sampled_from(["Ready", "Other", 1]),
+                                           "status": st.sampled_from(["True", "False", True])})
+node = st.fixed_dictionaries({}, optional={
+    "metadata": st.one_of(st.none(), st.fixed_dictionaries({}, optional={
+        "name": st.one_of(st.none(), st.text(max_size=8)),
+        "labels": st.one_of(st.none(), st.dictionaries(st.text(max_size=4), st.text(max_size=4), max_size=3)),
+        "annotations": st.dictionaries(st.sampled_from([HEALTH_ANNOTATION, "x"]), st.text(max_size=5), max_size=2)})),
+    "spec": st.one_of(st.none(), st.fixed_dictionaries({}, optional={
+        "taints": st.lists(st.fixed_dictionaries({}, optional={"key": st.text(max_size=3),
+                                                              "value": st.one_of(st.none(), st.text(max_size=3)),
+                                                              "effect": st.text(max_size=3)}), max_size=2),
+        "unschedulable": st.booleans()})),
+    "status": st.fixed_dictionaries({}, optional={"capacity": cap, "allocatable": cap,
+                                                  "conditions": st.lists(cond, max_size=3)}),
+})
+
+
+@settings(max_examples=300, suppress_health_check=[HealthCheck.too_slow])
+@given(st.lists(node, max_size=6), st.sampled_from(["capacity", "allocatable"]), st.booleans())
+def test_fuzz_equivalence(items, src, ascii_only):
+    body = json.dumps({"items": items}, ensure_ascii=ascii_only).encode()
+    assert_same(body, src)
+
+
+json_tree = st.recursive(
+    st.one_of(st.none(), st.booleans(), st.integers(), st.floats(allow_nan=True), st.text()),
+    lambda ch: st.one_of(st.lists(ch, max_size=4), st.dictionaries(st.text(max_size=5), ch, max_size=4)),
+    max_leaves=30)
+
+
+@settings(max_examples=400)
+@given(json_tree)
+def test_dumps_indent2_byte_identical(tree):
+    try:
+        got = ext.dumps_indent2(tree)
+    except ext.FallbackError:
+        return
+    assert got == json.dumps(tree, ensure_ascii=False, indent=2)
+
+
+def test_dumps_control_chars_and_unicode():
+    s = "".join(chr(i) for i in range(0, 0x30)) + " é😀\x7f\"\\"
+    obj = {"k": [s, {"": None}, [], {}, 1.5, -0.0, 10 ** 30, True]}
+    assert ext.dumps_indent2(obj) == json.dumps(obj, ensure_ascii=False, indent=2)
+    assert fastpath.dumps_indent2({1: 2}) == json.dumps({1: 2}, ensure_ascii=False, indent=2)  # fallback path

@@ -1,0 +1,148 @@
+"""MI355X health model + Ready gate + CLI integration (SURVEY §5 failure detection, §7.1)."""
+import json
+import time
+
+import pytest
+
+from k8s_gpu_node_checker_amd.models import health as H
+from k8s_gpu_node_checker_amd.testing import fixtures
+from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+
+
+def rep(**kw):
+    return fixtures.mi355x_probe_report("n", gpus=8, **kw)
+
+
+def test_measured_mi355x_report_is_healthy():
+    v = H.evaluate_report(rep(), 8)
+    assert v.state == H.HEALTHY and v.gpus_ok == 8 and v.ok
+    assert v.short() == "MI355X 8/8 healthy"
+
+
+@pytest.mark.parametrize("override,needle", [
+    ({"gfx": "gfx942"}, "not gfx950"),
+    ({"vram_type": 3}, "not HBM3E"),
+    ({"vram_mb": 196000}, "VRAM"),
+    ({"ecc_uncorrectable": 2}, "uncorrectable ECC"),
+    ({"xgmi": "XUUUUUDU"}, "xGMI link(s) down"),
+    ({"xgmi": "XUUUUUXX"}, "5/7 xGMI links up"),
+    ({"kfd": False}, "no KFD node"),
+    ({"cus": 240}, "240 CUs"),
+    ({"bad_pages": 100}, "retired pages"),
+    ({"error": "AMDSMI_STATUS_NO_PERM"}, "probe error"),
+    ({"diag": {"gemm": {"pass": False, "detail": "120 TFLOP/s"}}}, "diag gemm failed"),
+    ({"market_name": "AMD Radeon Graphics", "product_name": "Other", "vbios_name": "x", "device_id": "0x1234"},
+     "not MI355X"),
+])
+def test_failures(override, needle):
+    v = H.evaluate_report(rep(gpu3=override), 8)
+    assert v.state == H.UNHEALTHY
+    assert any(needle in r for r in v.reasons), v.reasons
+    assert v.gpus_ok == 7
+
+
+def test_identity_survives_generic_market_name():
+    g = dict(rep()["gpus"][0], market_name="AMD Radeon Graphics")
+    assert H.is_mi35x(g)
+    g.update(product_name="", vbios_name="")
+    assert H.is_mi35x(g)  # device id 0x75a3
+
+
+@pytest.mark.parametrize("override,needle", [({"ecc_deferred": 1}, "deferred"), ({"ecc_correctable": 5000}, "correctable"),
+                                            ({"bad_pages": 3}, "retired pages"), ({"hotspot_c": 104}, "hotspot")])
+def test_warnings_degrade_but_stay_ok(override, needle):
+    v = H.evaluate_report(rep(gpu0=override), 8)
+    assert v.state == H.DEGRADED and v.ok
+    assert any(needle in w for w in v.warnings)
+
+
+def test_partition_modes_scale_vram_expectation():
+    v = H.evaluate_report(rep(gpu0={"vram_mb": 147448, "memory_partition": "NPS2"}), 8)
+    assert v.state == H.HEALTHY
+    assert H.evaluate_report(rep(gpu0={"vram_mb": 147448}), 8).state == H.UNHEALTHY
+
+
+def test_missing_gpus_vs_capacity():
+    v = H.evaluate_report(fixtures.mi355x_probe_report("n", gpus=7), 8)
+    assert v.state == H.UNHEALTHY and "7 of 8 GPUs visible" in v.reasons[-1]
+
+
+def test_unknown_states():
+    assert H.evaluate_report(None, 8).state == H.UNKNOWN
+    assert H.evaluate_report(rep(ts=time.time() - 10000), 8).state == H.UNKNOWN
+    assert H.evaluate_report(rep(error="AMDSMI_STATUS_DRIVER_NOT_LOADED"), 8).state == H.UNKNOWN
+    assert H.evaluate_report({"schema": "other/v9"}, 8).state == H.UNKNOWN
+    assert H.parse_annotation("{not json")["error"] == "annotation is not JSON"
+
+
+def test_xgmi_check_can_be_disabled():
+    exp = H.HealthExpectations(xgmi_links=0)
+    assert H.evaluate_report(rep(gpu0={"xgmi": "XXXXXXXX"}), 8, exp).state == H.HEALTHY
+
+
+def test_gate_policies():
+    bad = H.Verdict(H.UNHEALTHY)
+    unk = H.Verdict(H.UNKNOWN)
+    good = H.Verdict(H.HEALTHY)
+    assert H.gate_ready(True, bad, "off", True) is True
+    assert H.gate_ready(True, bad, "auto", True) is False
+    assert H.gate_ready(True, good, "auto", True) is True
+    assert H.gate_ready(True, None, "auto", True) is True
+    assert H.gate_ready(True, None, "require", True) is False
+    assert H.gate_ready(True, unk, "auto", True, unknown_ok=True) is True
+    assert H.gate_ready(True, unk, "auto", True, unknown_ok=False) is False
+    assert H.gate_ready(False, good, "auto", True) is False
+    assert H.gate_ready(True, bad, "require", False) is True  # non-AMD GPU nodes are not gated
+
+
+def _cluster(mock_cluster, tmp_path, nodes):
+    srv = mock_cluster(nodes)
+    return write_kubeconfig(str(tmp_path / "kc"), srv.url)
+
+
+def test_cli_without_annotations_is_reference_behaviour(run_cli, mock_cluster, tmp_path):
+    kc = _cluster(mock_cluster, tmp_path, fixtures.cluster(3, "amd"))
+    for policy in ("off", "auto"):
+        p = run_cli(["--kubeconfig", kc, "--json", "--health-policy", policy])
+        assert p.returncode == 0 and json.loads(p.stdout)["ready_nodes"] == 3
+
+
+def test_cli_unhealthy_annotation_flips_ready_and_exit_code(run_cli, mock_cluster, tmp_path):
+    bad = fixtures.mi355x_probe_report("mi355x-node-0000", gpus=8, gpu2={"ecc_uncorrectable": 7})
+    nodes = [fixtures.realistic_node("mi355x-node-0000", annotations=fixtures.health_annotation(bad))]
+    kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc, "--json"])
+    assert p.returncode == 3
+    doc = json.loads(p.stdout)
+    assert doc["ready_nodes"] == 0 and doc["nodes"][0]["ready"] is False
+    assert set(doc) == {"total_nodes", "ready_nodes", "nodes"}  # schema unchanged
+    p = run_cli(["--kubeconfig", kc, "--json", "--health-policy", "off"])
+    assert p.returncode == 0
+
+
+def test_cli_require_policy_and_mi355x_preset(run_cli, mock_cluster, tmp_path):
+    good = fixtures.mi355x_probe_report("a", gpus=8)
+    nodes = [fixtures.realistic_node("a", annotations=fixtures.health_annotation(good), index=0),
+             fixtures.realistic_node("b", index=1),  # no probe report
+             fixtures.realistic_node("c", index=2, allocatable_gpus=0,
+                                     annotations=fixtures.health_annotation(fixtures.mi355x_probe_report("c")))]
+    kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc, "--json", "--health-policy", "require"])
+    doc = json.loads(p.stdout)
+    assert [n["ready"] for n in doc["nodes"]] == [True, False, True]
+    p = run_cli(["--kubeconfig", kc, "--json", "--mi355x"])  # allocatable-based + require
+    doc = json.loads(p.stdout)
+    assert [n["name"] for n in doc["nodes"]] == ["a", "b"]  # c has 0 allocatable GPUs
+    assert [n["ready"] for n in doc["nodes"]] == [True, False]
+
+
+def test_cli_health_in_slack_and_extended_json(run_cli, mock_cluster, sink, tmp_path):
+    bad = fixtures.mi355x_probe_report("mi355x-node-0000", gpus=8, gpu0={"xgmi": "XUUUDUUU"})
+    nodes = [fixtures.realistic_node("mi355x-node-0000", annotations=fixtures.health_annotation(bad))]
+    kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc, "--json-extended", "--slack-webhook", sink.url("200")])
+    doc = json.loads(p.stdout)
+    h = doc["mi355x"]["nodes"][0]["health"]
+    assert h["state"] == "unhealthy" and "xGMI" in h["reasons"][0]
+    text = sink.payloads()[-1]["text"]
+    assert "❌ Not Ready" in text and "[MI355X unhealthy: gpu0: 1 xGMI link(s) down (XUUUDUUU)]" in text

@@ -1,0 +1,176 @@
+"""kube-apiserver client: pagination, retries/backoff, errors, gzip, chunked, TLS (SURVEY §7.2 layer 2)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from k8s_gpu_node_checker_amd.kube.client import KubeClient
+from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+from k8s_gpu_node_checker_amd.kube.errors import ApiException, TransportError
+from k8s_gpu_node_checker_amd.models.node import scan_items
+from k8s_gpu_node_checker_amd.testing import fixtures
+from k8s_gpu_node_checker_amd.testing.mock_apiserver import MockApiServer, MockConfig
+
+
+def names(res):
+    return [n["name"] for n in res.gpu_nodes]
+
+
+def client(srv, **kw):
+    kw.setdefault("sleep", lambda s: None)
+    return KubeClient(ClusterConnection(srv.url), **kw)
+
+
+def test_pagination_preserves_order_and_uses_one_connection(mock_cluster):
+    nodes = fixtures.cluster(23, "mixed", not_ready=[4])
+    srv = mock_cluster(nodes)
+    with client(srv) as c:
+        res = c.scan_nodes(limit=5)
+    assert names(res) == names(scan_items(nodes))
+    assert res.items_seen == 23
+    assert [e["path"] for e in srv.log][:2] == ["/api/v1/nodes?limit=5", "/api/v1/nodes?limit=5&continue=c5.1000"]
+    assert len(srv.log) == 5
+
+
+def test_unpaginated(mock_cluster):
+    srv = mock_cluster(fixtures.cluster(7, "amd"))
+    with client(srv) as c:
+        res = c.scan_nodes(limit=0)
+    assert len(res.gpu_nodes) == 7 and srv.log[0]["path"] == "/api/v1/nodes"
+
+
+def test_expired_continue_falls_back_to_full_list(mock_cluster):
+    nodes = fixtures.cluster(12, "amd")
+    srv = mock_cluster(nodes, expire_continue=True)
+    with client(srv) as c:
+        res = c.scan_nodes(limit=5)
+    assert names(res) == names(scan_items(nodes))  # no duplicates from the partial first page
+    assert srv.log[-1]["path"] == "/api/v1/nodes"
+
+
+def test_transient_503_is_retried_honouring_retry_after(mock_cluster):
+    srv = mock_cluster(fixtures.cluster(2, "amd"), fail_first=2, retry_after="0.5")
+    slept = []
+    with KubeClient(ClusterConnection(srv.url), retries=2, sleep=slept.append) as c:
+        res = c.scan_nodes()
+    assert len(res.gpu_nodes) == 2 and slept == [0.5, 0.5]
+
+
+def test_retries_exhausted_raises_api_exception(mock_cluster):
+    srv = mock_cluster(fixtures.cluster(2, "amd"), fail_first=10)
+    with client(srv, retries=1) as c:
+        with pytest.raises(ApiException) as e:
+            c.scan_nodes()
+    assert e.value.status == 503
+    assert str(e.value).startswith("(503)\nReason: Service Unavailable\n")
+
+
+def test_403_not_retried(mock_cluster):
+    srv = mock_cluster(fixtures.cluster(2, "amd"), status=403)
+    with client(srv, retries=3) as c:
+        with pytest.raises(ApiException) as e:
+            c.scan_nodes()
+    assert len(srv.log) == 1
+    s = str(e.value)
+    assert s.startswith("(403)\nReason: Forbidden\nHTTP response headers: HTTPHeaderDict({")
+    assert "HTTP response body: " in s and "forbidden" in s
+
+
+def test_connection_refused_message():
+    c = KubeClient(ClusterConnection("http://127.0.0.1:9"), retries=1, sleep=lambda s: None)
+    with pytest.raises(TransportError) as e:
+        c.scan_nodes()
+    msg = str(e.value)
+    assert msg.startswith("HTTPConnectionPool(host='127.0.0.1', port=9): Max retries exceeded with url: /api/v1/nodes")
+
+
+def test_read_timeout(mock_cluster):
+    srv = mock_cluster(fixtures.cluster(1, "amd"), delay=1.0)
+    c = KubeClient(ClusterConnection(srv.url), timeout=0.2, retries=0)
+    with pytest.raises(TransportError) as e:
+        c.scan_nodes()
+    assert "Read timed out. (read timeout=0.2)" in str(e.value)
+
+
+def test_reset_by_server(mock_cluster):
+    srv = mock_cluster(fixtures.cluster(1, "amd"), reset=True)
+    c = KubeClient(ClusterConnection(srv.url), retries=0)
+    with pytest.raises(TransportError) as e:
+        c.scan_nodes()
+    assert "Connection aborted" in str(e.value) or "Connection reset" in str(e.value)
+
+
+def test_gzip_and_chunked(mock_cluster):
+    nodes = fixtures.cluster(9, "amd")
+    for cfg in ({"gzip": True}, {"chunked": True}):
+        srv = mock_cluster(nodes, **cfg)
+        with KubeClient(ClusterConnection(srv.url), gzip=True) as c:
+            res = c.scan_nodes(limit=4)
+        assert len(res.gpu_nodes) == 9
+
+
+def test_gzip_off_for_loopback_on_for_remote():
+    assert KubeClient(ClusterConnection("http://127.0.0.1:1")).gzip is False
+    assert KubeClient(ClusterConnection("https://api.example.com")).gzip is True
+
+
+def test_label_selector_and_resource_version(mock_cluster):
+    srv = mock_cluster(fixtures.cluster(2, "amd"))
+    with client(srv) as c:
+        c.scan_nodes(limit=0, label_selector="pool=training,amd.com/gpu.family=MI355X", resource_version="0")
+    assert srv.log[0]["path"] == "/api/v1/nodes?labelSelector=pool%3Dtraining%2Camd.com%2Fgpu.family%3DMI355X&resourceVersion=0"
+
+
+def test_patch_annotations_and_get(mock_cluster):
+    srv = mock_cluster(fixtures.cluster(2, "amd"))
+    with client(srv) as c:
+        c.patch_node_annotations("mi355x-node-0001", {"amd.com/x": "1"})
+        node = c.get_node("mi355x-node-0001")
+    assert node["metadata"]["annotations"]["amd.com/x"] == "1"
+    assert srv.log[0]["method"] == "PATCH"
+
+
+@pytest.fixture(scope="module")
+def certs(tmp_path_factory):
+    d = tmp_path_factory.mktemp("pki")
+    key, crt = d / "srv.key", d / "srv.crt"
+    r = subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
+                        "-days", "1", "-subj", "/CN=mock-apiserver", "-addext", "subjectAltName=IP:127.0.0.1,DNS:localhost"],
+                       capture_output=True)
+    if r.returncode != 0:
+        pytest.skip("openssl unavailable")
+    return str(crt), str(key)
+
+
+def test_tls_with_ca_file_and_sni(certs):
+    crt, key = certs
+    with MockApiServer(fixtures.cluster(3, "amd"), certfile=crt, keyfile=key) as srv:
+        conn = ClusterConnection(srv.url)
+        conn.ca_file = crt
+        with KubeClient(conn) as c:
+            assert len(c.scan_nodes().gpu_nodes) == 3
+        conn2 = ClusterConnection(srv.url.replace("127.0.0.1", "localhost"))
+        conn2.ca_data = open(crt, "rb").read()
+        conn2.tls_server_name = "localhost"
+        with KubeClient(conn2) as c:
+            assert len(c.scan_nodes().gpu_nodes) == 3
+
+
+def test_tls_verification_failure_is_not_retried(certs):
+    crt, key = certs
+    with MockApiServer(fixtures.cluster(1, "amd"), certfile=crt, keyfile=key) as srv:
+        c = KubeClient(ClusterConnection(srv.url), retries=3, sleep=lambda s: None)  # system CAs: untrusted
+        with pytest.raises(TransportError) as e:
+            c.scan_nodes()
+        assert "SSLError" in str(e.value) or "CERTIFICATE_VERIFY_FAILED" in str(e.value)
+        assert len(srv.log) == 0
+
+
+def test_tls_insecure_skip_verify(certs):
+    crt, key = certs
+    with MockApiServer(fixtures.cluster(2, "amd"), certfile=crt, keyfile=key) as srv:
+        conn = ClusterConnection(srv.url)
+        conn.insecure = True
+        with KubeClient(conn) as c:
+            assert len(c.scan_nodes().gpu_nodes) == 2

@@ -1,0 +1,141 @@
+"""Contract parity: the UNMODIFIED reference script (with test stand-ins for `kubernetes`/`dotenv`,
+tests/refstub) and this CLI run against the same mock apiserver / webhook sink; stdout, stderr
+classes, exit codes and Slack requests must match (SURVEY §4.3 "contract/parity").
+
+Skipped when /root/reference is not mounted (e.g. on the GPU box).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from k8s_gpu_node_checker_amd.testing import fixtures
+from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+
+REF = os.environ.get("K8SGPU_REFERENCE", "/root/reference/check-gpu-node.py")
+STUBS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "refstub")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = [pytest.mark.reference,
+              pytest.mark.skipif(not os.path.exists(REF), reason="reference script not mounted")]
+
+
+def _env(extra=None):
+    e = {k: v for k, v in os.environ.items() if k not in ("SLACK_WEBHOOK_URL", "KUBECONFIG", "PYTHONPATH")}
+    e["COLUMNS"] = "80"
+    if extra:
+        e.update(extra)
+    return e
+
+
+def run_ref(args, env=None, cwd=None):
+    e = _env(env)
+    e["PYTHONPATH"] = STUBS
+    return subprocess.run([sys.executable, REF] + args, capture_output=True, text=True, env=e, timeout=120, cwd=cwd)
+
+
+def run_new(args, env=None, cwd=None):
+    return subprocess.run([sys.executable, os.path.join(REPO, "check-gpu-node.py")] + args, capture_output=True,
+                          text=True, env=_env(env), timeout=120, cwd=cwd)
+
+
+@pytest.fixture
+def cluster(tmp_path, mock_cluster):
+    def make(nodes):
+        srv = mock_cluster(nodes)
+        return write_kubeconfig(str(tmp_path / "kc.yaml"), srv.url)
+    return make
+
+
+CLUSTERS = {**{g: (lambda g=g: fixtures.golden(g)) for g in fixtures.GOLDEN},
+            "amd8": lambda: fixtures.cluster(8, "amd"),
+            "amd8-2notready": lambda: fixtures.cluster(8, "amd", not_ready=[1, 5]),
+            "cpu16": lambda: fixtures.cluster(16, "cpu"),
+            "mixed40": lambda: fixtures.cluster(40, "mixed", not_ready=[3])}
+
+
+@pytest.mark.parametrize("name", sorted(CLUSTERS))
+@pytest.mark.parametrize("flags", [[], ["--json"]])
+def test_same_output_same_exit_code(cluster, name, flags):
+    kc = cluster(CLUSTERS[name]())
+    a = run_ref(["--kubeconfig", kc] + flags)
+    b = run_new(["--kubeconfig", kc] + flags)
+    assert a.returncode == b.returncode, (a.stderr, b.stderr)
+    assert a.stdout == b.stdout
+    assert a.stderr == b.stderr == ""
+
+
+def test_help_and_usage_error_identical():
+    a, b = run_ref(["--help"]), run_new(["--help"])
+    assert (a.returncode, a.stdout) == (b.returncode, b.stdout)
+    a, b = run_ref(["--bogus"]), run_new(["--bogus"])
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+
+
+def test_missing_kubeconfig_identical(tmp_path):
+    a = run_ref(["--json", "--kubeconfig", str(tmp_path / "missing")])
+    b = run_new(["--json", "--kubeconfig", str(tmp_path / "missing")])
+    assert (a.returncode, a.stdout) == (b.returncode, b.stdout) == (1, '{"error": "Invalid kube-config file. No configuration found."}\n')
+
+
+def _slack_case(cluster, sink, mode, extra_flags, nodes):
+    kc = cluster(nodes)
+    url = sink.url(mode)
+    flags = ["--kubeconfig", kc, "--slack-webhook", url, "--slack-retry-delay", "0"] + extra_flags
+    before = len(sink.requests)
+    a = run_ref(flags)
+    mid = len(sink.requests)
+    sink.counts.clear()
+    b = run_new(flags + ["--slack-retry-policy", "reference"])
+    after = len(sink.requests)
+    return a, b, sink.requests[before:mid], sink.requests[mid:after]
+
+
+@pytest.mark.parametrize("mode", ["200", "500", "204", "flaky2", "resetflaky", "reset"])
+def test_slack_behaviour_matches(cluster, sink, mode):
+    a, b, ra, rb = _slack_case(cluster, sink, mode, [], fixtures.golden("readme"))
+    assert a.returncode == b.returncode
+    assert a.stdout == b.stdout
+    assert len(ra) == len(rb), (mode, a.stderr, b.stderr)
+    assert [json.loads(r["body"]) for r in ra] == [json.loads(r["body"]) for r in rb]
+    assert ra[0]["headers"]["Content-Length"] == rb[0]["headers"]["Content-Length"]
+    assert ra[0]["headers"]["Content-Type"] == rb[0]["headers"]["Content-Type"] == "application/json"
+    # stderr: same lines, except the exception repr inside a reset message (requests vs our transport)
+    la, lb = a.stderr.splitlines(), b.stderr.splitlines()
+    assert len(la) == len(lb), (a.stderr, b.stderr)
+    for x, y in zip(la, lb):
+        if "Connection aborted" in x or "Connection reset" in x:
+            assert x.split(":")[0] == y.split(":")[0] and "Connection aborted" in y
+        else:
+            assert x == y
+
+
+def test_slack_only_on_error_gating_matches(cluster, sink):
+    for nodes, expect in ((fixtures.golden("readme"), 0), (fixtures.golden("notready"), 1), (fixtures.golden("nogpu"), 1)):
+        a, b, ra, rb = _slack_case(cluster, sink, "200", ["--slack-only-on-error"], nodes)
+        assert len(ra) == len(rb) == expect
+        assert a.stdout == b.stdout and a.returncode == b.returncode
+
+
+def test_slack_json_mode_suppresses_final_lines(cluster, sink):
+    a, b, ra, rb = _slack_case(cluster, sink, "500", ["--json"], fixtures.golden("readme"))
+    assert a.stdout == b.stdout
+    assert a.stderr == b.stderr
+    assert len(ra) == len(rb) == 4
+
+
+def test_retry_count_zero_and_negative(cluster, sink):
+    for n, posts in (("0", 1), ("-1", 0)):
+        a, b, ra, rb = _slack_case(cluster, sink, "500", ["--slack-retry-count", n], fixtures.golden("readme"))
+        assert len(ra) == len(rb) == posts
+        assert a.stderr == b.stderr and a.stdout == b.stdout
+
+
+def test_env_webhook_and_empty_flag_fallback(cluster, sink):
+    kc = cluster(fixtures.golden("readme"))
+    env = {"SLACK_WEBHOOK_URL": sink.url("200")}
+    a = run_ref(["--kubeconfig", kc, "--slack-webhook", ""], env=env)
+    b = run_new(["--kubeconfig", kc, "--slack-webhook", ""], env=env)
+    assert a.stdout == b.stdout and a.stdout.startswith("✅ 슬랙 메시지를 성공적으로 전송했습니다.")
