@@ -152,11 +152,12 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
             rep["gpus"][0]["index"] = 0
     probe_ms = (time.perf_counter() - t0) * 1e3
     with KubeClient(cluster) as kc:
-        agent.publish_annotation(kc, rep)
+        agent.publish(kc, rep)  # AMDGPUHealthy NodeCondition + full report annotation
         if rank == 0 and n_nodes > n_gpus:  # --nodes > GPUs: the extra nodes get a copy of rank 0's report
             for i in range(n_gpus, n_nodes):
                 r2 = dict(rep, node=f"mi355x-node-{i:04d}")
                 kc.patch_node_annotations(f"mi355x-node-{i:04d}", agent.annotation(r2))
+                kc.patch_node_condition(f"mi355x-node-{i:04d}", agent.condition(r2))
     diag = {}
     for g in rep.get("gpus") or []:
         diag = g.get("diag") or {}
@@ -172,7 +173,7 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
             if len(r.get("gpus") or []) > 1:
                 r["gpus"] = [g for g in r["gpus"] if g.get("index") == local_rank] or r["gpus"][:1]
             with KubeClient(cluster) as kc2:
-                agent.publish_annotation(kc2, r)
+                agent.publish(kc2, r)
             barrier()
         if rank == 0:
             sink_out.seek(0)

@@ -5,13 +5,16 @@ Every ``--interval`` seconds the agent runs the passive amd-smi probe
 seconds, the active HIP diagnostics (``ops/diag.py``: MFMA GEMM + numerics,
 HBM bandwidth, memtest) at ``--diag-level``.  The merged report is published
 
-* as the node annotation ``amd.com/mi355x-health`` (JSON merge-PATCH; the
-  checker reads it from the LIST it already does -- zero extra API calls), and/or
+* as the NodeCondition ``AMDGPUHealthy`` (strategic-merge PATCH of
+  ``nodes/status``, node-problem-detector style: the checker reads the
+  verdict from the LIST it already does, zero extra API calls, no JSON to
+  parse per node) plus the full report as the annotation
+  ``amd.com/mi355x-health`` (``--json-extended`` details, ``--health-reeval``), and/or
 * over HTTP at ``/probe`` (JSON) and ``/metrics`` (Prometheus) for the
   checker's ``--probe-endpoint`` fan-out, and/or
 * on stdout (``--publish stdout``, one JSON line per probe).
 
-RBAC: ``nodes: get, patch`` for the annotation path (``deploy/daemonset.yaml``).
+RBAC: ``nodes: get, patch`` and ``nodes/status: patch`` (``deploy/daemonset.yaml``).
 """
 
 from __future__ import annotations
@@ -26,7 +29,7 @@ import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional
 
-from ..models.health import HealthExpectations, evaluate_report
+from ..models.health import HealthExpectations, condition_for, evaluate_report
 from ..models.node import HEALTH_ANNOTATION
 
 
@@ -42,6 +45,7 @@ class Agent:
         self._diag_cache: Dict[int, Dict[str, Any]] = {}
         self._diag_ts = 0.0
         self.last: Optional[Dict[str, Any]] = None
+        self._last_condition: Optional[Dict[str, Any]] = None
         self.lock = threading.Lock()
 
     def _diagnostics(self, n_gpus: int) -> Dict[int, Dict[str, Any]]:
@@ -73,8 +77,19 @@ class Agent:
     def annotation(self, rep: Dict[str, Any]) -> Dict[str, str]:
         return {HEALTH_ANNOTATION: json.dumps(rep, separators=(",", ":"))}
 
+    def condition(self, rep: Dict[str, Any]) -> Dict[str, Any]:
+        v = evaluate_report(rep, 0, HealthExpectations())
+        cond = condition_for(v, previous=self._last_condition)
+        self._last_condition = cond
+        return cond
+
     def publish_annotation(self, client: Any, rep: Dict[str, Any]) -> None:
         client.patch_node_annotations(self.node, self.annotation(rep))
+
+    def publish(self, client: Any, rep: Dict[str, Any]) -> None:
+        """Full report as annotation + verdict as the ``AMDGPUHealthy`` NodeCondition."""
+        client.patch_node_annotations(self.node, self.annotation(rep))
+        client.patch_node_condition(self.node, self.condition(rep))
 
 
 def _metrics(rep: Optional[Dict[str, Any]]) -> str:
@@ -166,9 +181,9 @@ def main(argv: Optional[List[str]] = None) -> int:
             print(json.dumps(rep, separators=(",", ":")), flush=True)
         if client is not None:
             try:
-                agent.publish_annotation(client, rep)
+                agent.publish(client, rep)
             except Exception as e:
-                print(f"annotation publish failed: {e}", file=sys.stderr, flush=True)
+                print(f"node status publish failed: {e}", file=sys.stderr, flush=True)
         if args.once:
             return 0
         time.sleep(max(0.0, args.interval - (time.monotonic() - started)))

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import sys
 import threading
+import time
 from typing import Any, Callable, Dict, List, Optional, TextIO
 
 from . import report
@@ -51,6 +52,7 @@ class CheckOptions:
         self.probe_endpoint: Optional[str] = None
         self.probe_concurrency = 64
         self.probe_timeout = 2.0
+        self.health_reeval = False
         self.trace = False
         self.slack_gate: Optional[Callable[["CheckResult"], bool]] = None
         for k, v in kw.items():
@@ -127,21 +129,28 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer) -> List[O
         return []
     with tracer.span("health"):
         exp = H.HealthExpectations(xgmi_links=opts.xgmi_links, max_age_s=opts.probe_max_age)
-        reports: List[Optional[Dict[str, Any]]]
+        reports: List[Optional[Dict[str, Any]]] = [None] * len(scan.gpu_nodes)
         if opts.probe_endpoint:
             from .parallel.fanout import fetch_probe_reports
             reports = fetch_probe_reports(scan, opts.probe_endpoint, opts.probe_concurrency, opts.probe_timeout)
-        else:
-            reports = [H.parse_annotation(ex.health_annotation) for ex in scan.extras]
         verdicts: List[Optional[H.Verdict]] = []
         changed = False
         unknown_ok = opts.probe_unknown == "allow"
+        now = time.time()
         for node, ex, rep in zip(scan.gpu_nodes, scan.extras, reports):
             is_amd = PRIMARY_GPU_KEY in node["gpu_breakdown"] or PRIMARY_GPU_KEY in ex.allocatable
-            if rep is None and opts.health_policy != "require":
+            v: Optional[H.Verdict] = None
+            if rep is None and ex.health_condition is not None and not opts.health_reeval:
+                # cheap path: the agent's verdict is a NodeCondition already parsed by the scan
+                v = H.verdict_from_condition(ex.health_condition, opts.probe_max_age, now)
+            else:
+                if rep is None:
+                    rep = H.parse_annotation(ex.health_annotation)
+                if rep is not None or opts.health_policy == "require":
+                    v = H.evaluate_report(rep, primary_gpu_count(ex, opts.gpu_source), exp, now)
+            if v is None:
                 verdicts.append(None)
                 continue
-            v = H.evaluate_report(rep, primary_gpu_count(ex, opts.gpu_source), exp)
             verdicts.append(v)
             gated = H.gate_ready(ex.ready_condition, v, opts.health_policy, is_amd, unknown_ok)
             if gated != node["ready"]:

@@ -60,6 +60,8 @@ def build_parser(show_all: bool = False, prog: Optional[str] = None) -> argparse
     x.add_argument("--probe-unknown", choices=("allow", "deny"), default="allow",
                    help=h("프로브 상태 unknown(만료/실패) 노드 처리 (기본: allow)"))
     x.add_argument("--xgmi-links", type=int, default=7, help=h("GPU 당 기대 xGMI 링크 수 (0 = 검사 안 함, 기본: 7)"))
+    x.add_argument("--health-reeval", action="store_true",
+                   help=h("AMDGPUHealthy 조건 대신 프로브 리포트(annotation)를 이 임계값으로 재평가"))
     x.add_argument("--probe-endpoint", help=h("노드별 프로브 URL 템플릿, 예: http://{ip}:9464/probe"))
     x.add_argument("--probe-concurrency", type=int, default=64, help=h("프로브 fan-out 동시성 (기본: 64)"))
     x.add_argument("--probe-timeout", type=float, default=2.0, help=h("노드별 프로브 타임아웃(초) (기본: 2)"))

@@ -503,6 +503,7 @@ struct NodeScan {
   Ref health;                // str or nullptr
   Ref taints;                // list
   Ref internal_ip;           // str or nullptr (first InternalIP of status.addresses)
+  Ref health_cond;           // (status, reason, message, heartbeat) tuple of the health condition, or nullptr
   bool unschedulable = false;
   bool ready = false;
   std::vector<Qty> cap, alloc;
@@ -625,7 +626,41 @@ void parse_spec(Cursor& c, NodeScan& ns, std::string& scratch) {
   });
 }
 
-void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scratch) {
+// "YYYY-MM-DDTHH:MM:SSZ" -> epoch seconds (the apiserver's RFC 3339 form); other shapes fall back.
+double parse_k8s_time(const RawStr& s) {
+  if (s.esc || s.e - s.b != 20) throw Fallback{"unusual timestamp"};
+  const char* p = s.b;
+  auto num = [&](int off, int n) {
+    int v = 0;
+    for (int i = 0; i < n; ++i) {
+      char ch = p[off + i];
+      if (ch < '0' || ch > '9') throw Fallback{"unusual timestamp"};
+      v = v * 10 + (ch - '0');
+    }
+    return v;
+  };
+  if (p[4] != '-' || p[7] != '-' || p[10] != 'T' || p[13] != ':' || p[16] != ':' || p[19] != 'Z')
+    throw Fallback{"unusual timestamp"};
+  int y = num(0, 4), m = num(5, 2), d = num(8, 2), hh = num(11, 2), mm = num(14, 2), ss = num(17, 2);
+  if (m < 1 || m > 12 || d < 1 || d > 31 || hh > 23 || mm > 59 || ss > 59) throw Fallback{"unusual timestamp"};
+  // days_from_civil (Howard Hinnant)
+  y -= m <= 2;
+  const long era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = static_cast<unsigned>(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  const long days = era * 146097 + static_cast<long>(doe) - 719468;
+  return static_cast<double>(days) * 86400.0 + hh * 3600.0 + mm * 60.0 + ss;
+}
+
+PyObject* cond_str_field(Cursor& c, std::string& scratch) {
+  if (is_null(c)) Py_RETURN_NONE;
+  if (c.peek() != '"') throw Fallback{"condition field not a string"};
+  return make_str(read_raw_string(c), scratch);
+}
+
+void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scratch,
+                  const std::string& health_cond) {
   for (auto* v : {&ns.cap, &ns.alloc})
     for (auto& q : *v) {
       q.set = false;
@@ -634,6 +669,7 @@ void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scrat
     }
   ns.ready = false;
   ns.internal_ip.reset(nullptr);
+  ns.health_cond.reset(nullptr);
   if (c.peek() != '{') {
     skip_value(c);
     return;
@@ -671,6 +707,7 @@ void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scrat
       });
     } else if (raw_equals(k, "conditions", scratch)) {
       ns.ready = false;
+      ns.health_cond.reset(nullptr);
       if (cc.peek() != '[') {
         skip_value(cc);
         return;
@@ -680,22 +717,58 @@ void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scrat
           skip_value(c3);
           return;
         }
-        bool type_ready = false, status_true = false;
+        bool type_ready = false, status_true = false, type_health = false;
+        Ref st(Py_NewRef(Py_None)), reason(Py_NewRef(Py_None)), message(Py_NewRef(Py_None));
+        bool have_hb = false;
+        double hb = 0.0;
         for_members(c3, [&](const RawStr& fk, Cursor& c4) {
           bool is_type = raw_equals(fk, "type", scratch);
           bool is_status = !is_type && raw_equals(fk, "status", scratch);
-          if ((is_type || is_status) && c4.peek() == '"') {
-            RawStr v = read_raw_string(c4);
-            bool eq = raw_equals(v, is_type ? "Ready" : "True", scratch);
-            if (is_type) type_ready = eq;
-            else status_true = eq;
+          if (is_type) {
+            type_ready = type_health = false;
+            if (c4.peek() == '"') {
+              RawStr v = read_raw_string(c4);
+              type_ready = raw_equals(v, "Ready", scratch);
+              type_health = !health_cond.empty() && raw_equals(v, health_cond.c_str(), scratch);
+            } else {
+              skip_value(c4);
+            }
+          } else if (is_status) {
+            status_true = false;
+            if (c4.peek() == '"') {
+              RawStr v = read_raw_string(c4);
+              status_true = raw_equals(v, "True", scratch);
+              st.reset(make_str(v, scratch));
+            } else if (is_null(c4)) {
+              st.reset(Py_NewRef(Py_None));
+            } else {
+              st.reset(nullptr);  // non-string status: only matters for the health condition
+              skip_value(c4);
+            }
+          } else if (raw_equals(fk, "reason", scratch)) {
+            reason.reset(cond_str_field(c4, scratch));
+          } else if (raw_equals(fk, "message", scratch)) {
+            message.reset(cond_str_field(c4, scratch));
+          } else if (raw_equals(fk, "lastHeartbeatTime", scratch)) {
+            have_hb = false;
+            if (c4.peek() == '"') {
+              hb = parse_k8s_time(read_raw_string(c4));
+              have_hb = true;
+            } else {
+              skip_value(c4);
+            }
           } else {
-            if (is_type) type_ready = false;
-            if (is_status) status_true = false;
             skip_value(c4);
           }
         });
         if (type_ready && status_true) ns.ready = true;
+        if (type_health) {
+          if (!st.o) throw Fallback{"health condition status not a string"};
+          Ref hbo(have_hb ? PyFloat_FromDouble(hb) : Py_NewRef(Py_None));
+          PyObject* t = PyTuple_Pack(4, st.o, reason.o, message.o, hbo.o);
+          if (!t) throw Fallback{"oom"};
+          ns.health_cond.reset(t);
+        }
       });
     } else {
       skip_value(cc);
@@ -749,8 +822,9 @@ void emit_node(NodeScan& ns, const KeySpec& ks, bool use_alloc, bool want_extras
     Ref allocd(breakdown_dict(ks, ns.alloc, nullptr));
     PyObject* health = ns.health.o ? ns.health.o : Py_None;
     PyObject* ip = ns.internal_ip.o ? ns.internal_ip.o : Py_None;
+    PyObject* hc = ns.health_cond.o ? ns.health_cond.o : Py_None;
     Ref ex(PyObject_CallFunctionObjArgs(extras_cls, ns.ready ? Py_True : Py_False, capd.o, allocd.o,
-                                        ns.unschedulable ? Py_True : Py_False, health, ip, nullptr));
+                                        ns.unschedulable ? Py_True : Py_False, health, ip, hc, nullptr));
     if (!ex.o) {
       PyErr_Clear();
       throw Fallback{"NodeExtras()"};
@@ -760,7 +834,8 @@ void emit_node(NodeScan& ns, const KeySpec& ks, bool use_alloc, bool want_extras
 }
 
 void parse_item(Cursor& c, const KeySpec& ks, bool use_alloc, bool want_extras, PyObject* extras_cls,
-                const std::string& health_key, PageOut& out, std::string& scratch) {
+                const std::string& health_key, const std::string& health_cond, PageOut& out,
+                std::string& scratch) {
   out.items++;
   if (c.peek() != '{') {
     skip_value(c);  // non-object item: never a GPU node
@@ -772,7 +847,7 @@ void parse_item(Cursor& c, const KeySpec& ks, bool use_alloc, bool want_extras, 
   for_members(c, [&](const RawStr& k, Cursor& cc) {
     if (raw_equals(k, "metadata", scratch)) parse_metadata(cc, ns, health_key, scratch);
     else if (raw_equals(k, "spec", scratch)) parse_spec(cc, ns, scratch);
-    else if (raw_equals(k, "status", scratch)) parse_status(cc, ns, ks, scratch);
+    else if (raw_equals(k, "status", scratch)) parse_status(cc, ns, ks, scratch, health_cond);
     else skip_value(cc);
   });
   emit_node(ns, ks, use_alloc, want_extras, extras_cls, out);
@@ -801,8 +876,9 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
   PyObject *result, *keys, *extras_cls;
   int use_alloc, want_extras;
   const char* health_key_c;
-  if (!PyArg_ParseTuple(args, "y*OO!ppsO", &view, &result, &PyTuple_Type, &keys, &use_alloc, &want_extras,
-                        &health_key_c, &extras_cls))
+  const char* health_cond_c = "";
+  if (!PyArg_ParseTuple(args, "y*OO!ppsO|s", &view, &result, &PyTuple_Type, &keys, &use_alloc, &want_extras,
+                        &health_key_c, &extras_cls, &health_cond_c))
     return nullptr;
   KeySpec ks;
   for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(keys); ++i) {
@@ -817,6 +893,7 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
     ks.pykeys.push_back(k);
   }
   std::string health_key(health_key_c);
+  std::string health_cond(health_cond_c);
   std::string scratch;
   PageOut out;
   const char* why = nullptr;
@@ -832,7 +909,7 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
         if (is_null(cc)) return;
         if (cc.peek() != '[') throw Fallback{"items not a list"};
         for_elements(cc, [&](Cursor& c3) {
-          parse_item(c3, ks, use_alloc, want_extras, extras_cls, health_key, out, scratch);
+          parse_item(c3, ks, use_alloc, want_extras, extras_cls, health_key, health_cond, out, scratch);
         });
       } else if (raw_equals(k, "metadata", scratch)) {
         out.cont.reset(nullptr);

@@ -143,6 +143,17 @@ class KubeClient:
     def get_node(self, name: str) -> Dict[str, Any]:
         return json.loads(self.request("GET", "/api/v1/nodes/" + quote(name, safe="")).body)
 
+    def patch_node_condition(self, name: str, condition: Dict[str, Any]) -> Dict[str, Any]:
+        """Upsert one ``status.conditions`` entry (strategic merge by ``type``; RBAC ``nodes/status: patch``).
+
+        This is how node-problem-detector publishes custom node conditions; the
+        kubelet preserves condition types it does not own.
+        """
+        body = json.dumps({"status": {"conditions": [condition]}}).encode()
+        resp = self.request("PATCH", "/api/v1/nodes/" + quote(name, safe="") + "/status", body,
+                            content_type="application/strategic-merge-patch+json", idempotent=True)
+        return json.loads(resp.body) if resp.body else {}
+
     def patch_node_annotations(self, name: str, annotations: Dict[str, Optional[str]]) -> Dict[str, Any]:
         """JSON merge-patch ``metadata.annotations`` (needs RBAC ``nodes: patch``)."""
         body = json.dumps({"metadata": {"annotations": annotations}}).encode()

@@ -74,7 +74,7 @@ class Verdict:
 
     def short(self) -> str:
         if self.state == HEALTHY:
-            return f"MI355X {self.gpus_ok}/{self.gpus_seen} healthy"
+            return f"MI355X {self.gpus_ok}/{self.gpus_seen} healthy" if self.gpus_seen else "MI355X healthy"
         detail = "; ".join(self.reasons or self.warnings)
         return f"MI355X {self.state}" + (f": {detail}" if detail else "")
 
@@ -200,6 +200,69 @@ def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
         fails.append(f"{len(gpus)} of {expected_gpus} GPUs visible to amd-smi")
     state = UNHEALTHY if fails else (DEGRADED if warns else HEALTHY)
     return Verdict(state, fails, warns, gpus_ok=ok, gpus_seen=len(gpus), age_s=age)
+
+
+# --- NodeCondition path (node-problem-detector style) -------------------------
+#: Node condition the agent maintains via PATCH /api/v1/nodes/{name}/status.
+from .node import HEALTH_CONDITION  # noqa: E402  (single definition)
+_REASON = {HEALTHY: "MI355XHealthy", DEGRADED: "MI355XDegraded", UNHEALTHY: "MI355XUnhealthy",
+           UNKNOWN: "MI355XProbeFailed"}
+_STATE_OF_REASON = {v: k for k, v in _REASON.items()}
+
+
+def parse_k8s_time(ts: Optional[str]) -> Optional[float]:
+    """RFC 3339 ``2025-10-10T00:00:00Z`` (what the apiserver emits) -> epoch seconds."""
+    if not ts or not isinstance(ts, str):
+        return None
+    try:
+        from datetime import datetime
+        return datetime.fromisoformat(ts.replace("Z", "+00:00")).timestamp()
+    except ValueError:
+        return None
+
+
+def format_k8s_time(epoch: float) -> str:
+    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(epoch))
+
+
+def condition_for(verdict: Verdict, now: Optional[float] = None,
+                  previous: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+    """The ``AMDGPUHealthy`` NodeCondition the agent publishes for ``verdict``."""
+    now = time.time() if now is None else now
+    status = "True" if verdict.ok else ("Unknown" if verdict.state == UNKNOWN else "False")
+    if verdict.state == HEALTHY:
+        msg = f"{verdict.gpus_ok}/{verdict.gpus_seen} MI355X GPUs healthy"
+    else:
+        msg = "; ".join(verdict.reasons or verdict.warnings)
+    ts = format_k8s_time(now)
+    transition = ts
+    if previous and previous.get("status") == status and previous.get("lastTransitionTime"):
+        transition = previous["lastTransitionTime"]
+    return {"type": HEALTH_CONDITION, "status": status, "reason": _REASON[verdict.state], "message": msg[:1024],
+            "lastHeartbeatTime": ts, "lastTransitionTime": transition}
+
+
+def verdict_from_condition(cond: Tuple[Optional[str], Optional[str], Optional[str], Optional[float]],
+                           max_age_s: float, now: Optional[float] = None) -> Verdict:
+    """``(status, reason, message, heartbeat_epoch)`` of an ``AMDGPUHealthy`` condition -> Verdict.
+
+    The cheap path: no annotation JSON to parse, the apiserver already carries
+    the agent's verdict in ``status.conditions`` (parsed by the NodeList scan).
+    """
+    status, reason, message, hb = cond
+    now = time.time() if now is None else now
+    age = (now - hb) if hb is not None else None
+    if age is None or age > max_age_s:
+        return Verdict(UNKNOWN, ["stale AMDGPUHealthy condition" if age is not None
+                                 else "AMDGPUHealthy condition has no heartbeat"], age_s=age)
+    msg = [message] if message else []
+    if status == "True":
+        state = _STATE_OF_REASON.get(reason or "", HEALTHY)
+        state = state if state in _OK_STATES else HEALTHY
+        return Verdict(state, warnings=msg if state == DEGRADED else [], age_s=age)
+    if status == "False":
+        return Verdict(UNHEALTHY, msg or ["AMDGPUHealthy=False"], age_s=age)
+    return Verdict(UNKNOWN, msg or ["AMDGPUHealthy=Unknown"], age_s=age)
 
 
 def parse_annotation(raw: Optional[str]) -> Optional[Dict[str, Any]]:

@@ -19,8 +19,28 @@ from typing import Any, Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
 
 from .resources import GPU_RESOURCE_KEYS, PRIMARY_GPU_KEY, gpu_breakdown
 
-#: Annotation written by the MI355X node agent (see ``agent/``).
+#: Annotation written by the MI355X node agent (see ``agent/``): the full probe report.
 HEALTH_ANNOTATION = "amd.com/mi355x-health"
+#: NodeCondition the agent maintains (its verdict; cheap to read from the LIST).
+HEALTH_CONDITION = "AMDGPUHealthy"
+
+
+def _k8s_time(ts: Any) -> Optional[float]:
+    if not isinstance(ts, str):
+        return None
+    from .health import parse_k8s_time
+    return parse_k8s_time(ts)
+
+
+def health_condition(node: Mapping[str, Any]) -> Optional[Tuple[Any, Any, Any, Optional[float]]]:
+    conds = _get(_get(node, "status"), "conditions")
+    if not isinstance(conds, list):
+        return None
+    found = None
+    for c in conds:
+        if isinstance(c, Mapping) and c.get("type") == HEALTH_CONDITION:
+            found = (c.get("status"), c.get("reason"), c.get("message"), _k8s_time(c.get("lastHeartbeatTime")))
+    return found
 
 
 def _get(obj: Any, key: str) -> Any:
@@ -75,16 +95,20 @@ def project_node(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEY
 class NodeExtras:
     """Side information the default report does not show but the health gate uses."""
 
-    __slots__ = ("ready_condition", "capacity", "allocatable", "unschedulable", "health_annotation", "internal_ip")
+    __slots__ = ("ready_condition", "capacity", "allocatable", "unschedulable", "health_annotation", "internal_ip",
+                 "health_condition")
 
     def __init__(self, ready_condition: bool, capacity: Dict[str, int], allocatable: Dict[str, int],
-                 unschedulable: bool, health_annotation: Optional[str], internal_ip: Optional[str] = None):
+                 unschedulable: bool, health_annotation: Optional[str], internal_ip: Optional[str] = None,
+                 health_condition: Optional[Tuple[Any, Any, Any, Optional[float]]] = None):
         self.ready_condition = ready_condition
         self.capacity = capacity
         self.allocatable = allocatable
         self.unschedulable = unschedulable
         self.health_annotation = health_annotation
         self.internal_ip = internal_ip
+        #: ``(status, reason, message, lastHeartbeatTime epoch)`` of the AMDGPUHealthy condition
+        self.health_condition = health_condition
 
     def to_dict(self) -> Dict[str, Any]:
         return {
@@ -93,6 +117,7 @@ class NodeExtras:
             "allocatable": self.allocatable,
             "unschedulable": self.unschedulable,
             "internal_ip": self.internal_ip,
+            "health_condition": list(self.health_condition) if self.health_condition else None,
         }
 
 
@@ -115,6 +140,7 @@ def node_extras(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS
         unschedulable=bool(_get(_get(node, "spec"), "unschedulable")),
         health_annotation=raw if isinstance(raw, str) else None,
         internal_ip=ip,
+        health_condition=health_condition(node),
     )
 
 

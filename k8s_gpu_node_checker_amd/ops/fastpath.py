@@ -23,7 +23,7 @@ import json
 import os
 from typing import Any, Dict, Optional, Sequence, Tuple
 
-from ..models.node import HEALTH_ANNOTATION, NodeExtras, ScanResult, scan_items
+from ..models.node import HEALTH_ANNOTATION, HEALTH_CONDITION, NodeExtras, ScanResult, scan_items
 from ..models.resources import GPU_RESOURCE_KEYS
 from .native import load_extension
 
@@ -54,7 +54,7 @@ def scan_page(body: bytes, result: ScanResult, keys: Sequence[str] = GPU_RESOURC
     if mod is not None:
         try:
             return mod.scan_nodelist(body, result, tuple(keys), gpu_source == "allocatable",
-                                     want_extras, HEALTH_ANNOTATION, NodeExtras)
+                                     want_extras, HEALTH_ANNOTATION, NodeExtras, HEALTH_CONDITION)
         except mod.FallbackError:
             pass  # unusual shape: let the reference-semantics Python path decide
     doc = json.loads(body)

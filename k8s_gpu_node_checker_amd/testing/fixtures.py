@@ -29,7 +29,8 @@ def _cond(ctype: str, status: str, reason: str, message: str) -> Dict[str, Any]:
 def realistic_node(name: str, gpu_key: Optional[str] = "amd.com/gpu", gpu_count: int = 8, ready: bool = True,
                    index: int = 0, annotations: Optional[Dict[str, str]] = None,
                    taints: Optional[List[Dict[str, Any]]] = None, allocatable_gpus: Optional[int] = None,
-                   instance_type: str = "mi355x.8x") -> Dict[str, Any]:
+                   instance_type: str = "mi355x.8x",
+                   extra_conditions: Optional[List[Dict[str, Any]]] = None) -> Dict[str, Any]:
     h = hashlib.sha1(name.encode()).hexdigest()
     ip = f"10.{(index >> 16) & 255}.{(index >> 8) & 255}.{index & 255}"
     labels = {
@@ -75,7 +76,7 @@ def realistic_node(name: str, gpu_key: Optional[str] = "amd.com/gpu", gpu_count:
         _cond("NetworkUnavailable", "False", "CalicoIsUp", "Calico is running on this node"),
         _cond("Ready", "True" if ready else "False", "KubeletReady" if ready else "KubeletNotReady",
               "kubelet is posting ready status" if ready else "container runtime network not ready"),
-    ]
+    ] + list(extra_conditions or [])
     node = {
         "metadata": {
             "name": name, "uid": f"{h[:8]}-{h[8:12]}-{h[12:16]}-{h[16:20]}-{h[20:32]}",
@@ -124,6 +125,12 @@ def health_annotation(report: Dict[str, Any]) -> Dict[str, str]:
     return {HEALTH_ANNOTATION: json.dumps(report, separators=(",", ":"))}
 
 
+def health_condition(report: Dict[str, Any], expected_gpus: int = 0) -> Dict[str, Any]:
+    """The ``AMDGPUHealthy`` NodeCondition an agent would publish for ``report``."""
+    from ..models.health import condition_for, evaluate_report
+    return condition_for(evaluate_report(report, expected_gpus))
+
+
 def cluster(n: int, kind: str = "amd", not_ready: Sequence[int] = (), gpus_per_node: int = 8,
             with_health: bool = False, prefix: str = "mi355x-node") -> List[Dict[str, Any]]:
     """``kind``: ``amd`` | ``nvidia`` | ``mixed`` (alternating, as the survey's 1000-node run) | ``cpu``."""
@@ -138,8 +145,12 @@ def cluster(n: int, kind: str = "amd", not_ready: Sequence[int] = (), gpus_per_n
         else:
             key = "amd.com/gpu"
         name = f"{prefix}-{i:04d}" if kind != "cpu" else f"cpu-node-{i:04d}"
-        ann = health_annotation(mi355x_probe_report(name, gpus_per_node)) if (with_health and key == "amd.com/gpu") else None
-        nodes.append(realistic_node(name, key, gpus_per_node, ready=i not in not_ready, index=i, annotations=ann))
+        ann, conds = None, None
+        if with_health and key == "amd.com/gpu":
+            rep = mi355x_probe_report(name, gpus_per_node)
+            ann, conds = health_annotation(rep), [health_condition(rep, gpus_per_node)]
+        nodes.append(realistic_node(name, key, gpus_per_node, ready=i not in not_ready, index=i, annotations=ann,
+                                    extra_conditions=conds))
     return nodes
 
 

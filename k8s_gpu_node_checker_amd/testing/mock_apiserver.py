@@ -68,11 +68,24 @@ class ClusterState:
                 return n
         return None
 
-    def patch(self, name: str, patch: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+    def patch(self, name: str, patch: Dict[str, Any], strategic: bool = False) -> Optional[Dict[str, Any]]:
         with self.lock:
             node = self.find(name)
             if node is None:
                 return None
+            conds = (patch.get("status") or {}).get("conditions") if strategic else None
+            if conds is not None:
+                # strategic merge: status.conditions is a list merged by its `type` key
+                patch = copy.deepcopy(patch)
+                patch["status"].pop("conditions")
+                have = node.setdefault("status", {}).setdefault("conditions", [])
+                for c in conds:
+                    for i, old in enumerate(have):
+                        if old.get("type") == c.get("type"):
+                            have[i] = dict(old, **c)
+                            break
+                    else:
+                        have.append(c)
             _merge_patch(node, patch)
             self.rv += 1
             self._cache.clear()
@@ -222,7 +235,12 @@ class _Handler(BaseHTTPRequestHandler):
         except ValueError:
             self._send(400, self._status_body(400, "BadRequest", "invalid patch"))
             return
-        node = self.server.state.patch(unquote(path[len("/api/v1/nodes/"):]), patch)
+        name = unquote(path[len("/api/v1/nodes/"):])
+        strategic = "strategic-merge-patch" in (self.headers.get("Content-Type") or "")
+        if name.endswith("/status"):
+            name = name[:-len("/status")]
+            patch = {"status": patch.get("status") or {}}  # the status subresource ignores other fields
+        node = self.server.state.patch(name, patch, strategic)
         if node is None:
             self._send(404, self._status_body(404, "NotFound", "node not found"), reason="Not Found")
         else:

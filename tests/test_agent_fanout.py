@@ -23,9 +23,17 @@ def test_agent_fixture_probe_and_annotation(mock_cluster, fixture_report):
     rep = ag.probe_once()
     assert rep["state"] == "healthy" and rep["node"] == "mi355x-node-0001"
     with KubeClient(ClusterConnection(srv.url)) as c:
-        ag.publish_annotation(c, rep)
+        ag.publish(c, rep)
         node = c.get_node("mi355x-node-0001")
-    assert json.loads(node["metadata"]["annotations"]["amd.com/mi355x-health"])["state"] == "healthy"
+        assert json.loads(node["metadata"]["annotations"]["amd.com/mi355x-health"])["state"] == "healthy"
+        conds = {c_["type"]: c_ for c_ in node["status"]["conditions"]}
+        assert conds["AMDGPUHealthy"]["status"] == "True" and conds["Ready"]["status"] == "True"
+        t0 = conds["AMDGPUHealthy"]["lastTransitionTime"]
+        ag.publish(c, ag.probe_once())  # heartbeat refresh keeps the transition time, replaces by type
+        node = c.get_node("mi355x-node-0001")
+        hc = [c_ for c_ in node["status"]["conditions"] if c_["type"] == "AMDGPUHealthy"]
+        assert len(hc) == 1 and hc[0]["lastTransitionTime"] == t0
+    assert [e["path"] for e in srv.log if e["method"] == "PATCH"][1] == "/api/v1/nodes/mi355x-node-0001/status"
 
 
 def test_agent_main_once(mock_cluster, fixture_report, tmp_path, capsys):

@@ -4,7 +4,7 @@ import json
 import pytest
 from hypothesis import HealthCheck, given, settings, strategies as st
 
-from k8s_gpu_node_checker_amd.models.node import HEALTH_ANNOTATION, NodeExtras, ScanResult, scan_items
+from k8s_gpu_node_checker_amd.models.node import HEALTH_ANNOTATION, HEALTH_CONDITION, NodeExtras, ScanResult, scan_items
 from k8s_gpu_node_checker_amd.models.resources import GPU_RESOURCE_KEYS
 from k8s_gpu_node_checker_amd.ops import fastpath
 from k8s_gpu_node_checker_amd.testing import fixtures
@@ -15,7 +15,8 @@ pytestmark = pytest.mark.skipif(ext is None, reason="native fast path not built"
 
 def native_scan(body, src="capacity", extras=True):
     r = ScanResult()
-    tok = ext.scan_nodelist(body, r, GPU_RESOURCE_KEYS, src == "allocatable", extras, HEALTH_ANNOTATION, NodeExtras)
+    tok = ext.scan_nodelist(body, r, GPU_RESOURCE_KEYS, src == "allocatable", extras, HEALTH_ANNOTATION, NodeExtras,
+                            HEALTH_CONDITION)
     return r, tok
 
 
@@ -107,8 +108,12 @@ def test_scan_page_wrapper_falls_back_to_python():
 scalar = st.one_of(st.none(), st.booleans(), st.integers(-5, 10), st.text(max_size=6),
                    st.sampled_from(["0", "8", "1k", " 3", "+2", "", "Ready", "True", "False"]))
 cap = st.dictionaries(st.sampled_from(list(GPU_RESOURCE_KEYS) + ["cpu"]), scalar, max_size=5)
-cond = st.fixed_dictionaries({}, optional={"type": st.sampled_from(["Ready", "Other", 1]),
-                                           "status": st.sampled_from(["True", "False", True])})
+cond = st.fixed_dictionaries({}, optional={"type": st.sampled_from(["Ready", "Other", 1, "AMDGPUHealthy"]),
+                                           "status": st.sampled_from(["True", "False", "Unknown", None]),
+                                           "reason": st.one_of(st.none(), st.sampled_from(["MI355XDegraded", "x"])),
+                                           "message": st.text(max_size=5),
+                                           "lastHeartbeatTime": st.sampled_from(["2025-10-10T00:00:00Z",
+                                                                                 "2026-02-28T23:59:59Z", None])})
 node = st.fixed_dictionaries({}, optional={
     "metadata": st.one_of(st.none(), st.fixed_dictionaries({}, optional={
         "name": st.one_of(st.none(), st.text(max_size=8)),

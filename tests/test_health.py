@@ -146,3 +146,46 @@ def test_cli_health_in_slack_and_extended_json(run_cli, mock_cluster, sink, tmp_
     assert h["state"] == "unhealthy" and "xGMI" in h["reasons"][0]
     text = sink.payloads()[-1]["text"]
     assert "❌ Not Ready" in text and "[MI355X unhealthy: gpu0: 1 xGMI link(s) down (XUUUDUUU)]" in text
+
+
+def test_condition_roundtrip():
+    now = 1_800_000_000.0
+    good = H.evaluate_report(rep(ts=now), 8, now=now)
+    c = H.condition_for(good, now=now)
+    assert c["type"] == "AMDGPUHealthy" and c["status"] == "True" and c["reason"] == "MI355XHealthy"
+    assert c["lastHeartbeatTime"] == "2027-01-15T08:00:00Z" and H.parse_k8s_time(c["lastHeartbeatTime"]) == now
+    v = H.verdict_from_condition((c["status"], c["reason"], c["message"], now), 900, now + 10)
+    assert v.state == H.HEALTHY and v.ok
+    bad = H.evaluate_report(rep(ts=now, gpu1={"ecc_uncorrectable": 1}), 8, now=now)
+    c2 = H.condition_for(bad, now=now + 60, previous=c)
+    assert c2["status"] == "False" and c2["lastTransitionTime"] == "2027-01-15T08:01:00Z"
+    v = H.verdict_from_condition((c2["status"], c2["reason"], c2["message"], now + 60), 900, now + 70)
+    assert v.state == H.UNHEALTHY and "uncorrectable" in v.reasons[0]
+    c3 = H.condition_for(good, now=now + 120, previous=H.condition_for(good, now=now))
+    assert c3["lastTransitionTime"] == c["lastTransitionTime"]  # unchanged status keeps the transition
+    deg = H.evaluate_report(rep(ts=now, gpu0={"ecc_deferred": 2}), 8, now=now)
+    v = H.verdict_from_condition(tuple(H.condition_for(deg, now=now)[k] for k in ("status", "reason", "message")) + (now,),
+                                 900, now)
+    assert v.state == H.DEGRADED and v.ok
+    assert H.verdict_from_condition(("True", "MI355XHealthy", "", now - 5000), 900, now).state == H.UNKNOWN
+    assert H.verdict_from_condition(("Unknown", "MI355XProbeFailed", "no driver", now), 900, now).state == H.UNKNOWN
+
+
+def test_cli_condition_path_and_reeval(run_cli, mock_cluster, tmp_path):
+    # condition says healthy, but the report would fail a stricter --xgmi-links 8 re-evaluation
+    rep8 = fixtures.mi355x_probe_report("a", gpus=8)
+    cond = fixtures.health_condition(rep8, 8)
+    nodes = [fixtures.realistic_node("a", annotations=fixtures.health_annotation(rep8), extra_conditions=[cond])]
+    kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc, "--json", "--xgmi-links", "8"])
+    assert p.returncode == 0  # condition path: the agent's verdict
+    p = run_cli(["--kubeconfig", kc, "--json", "--xgmi-links", "8", "--health-reeval"])
+    assert p.returncode == 3  # re-evaluated with the checker's thresholds
+
+
+def test_cli_unhealthy_condition_without_annotation(run_cli, mock_cluster, tmp_path):
+    bad = H.condition_for(H.Verdict(H.UNHEALTHY, ["gpu3: 2 uncorrectable ECC errors"]))
+    nodes = [fixtures.realistic_node("a", extra_conditions=[bad]), fixtures.realistic_node("b", index=1)]
+    kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc, "--json"])
+    assert [n["ready"] for n in json.loads(p.stdout)["nodes"]] == [False, True] and p.returncode == 0
