@@ -118,7 +118,8 @@ def scan_cluster(cluster: ClusterConnection, opts: CheckOptions, tracer: Tracer)
         with tracer.span("list"):
             return client.scan_nodes(limit=opts.page_size, keys=GPU_RESOURCE_KEYS, gpu_source=opts.gpu_source,
                                      want_extras=opts.needs_extras, label_selector=opts.label_selector,
-                                     resource_version=opts.resource_version)
+                                     resource_version=opts.resource_version,
+                                     annotation_mode=2 if (opts.health_reeval or opts.json_extended) else 1)
     finally:
         client.close()
 

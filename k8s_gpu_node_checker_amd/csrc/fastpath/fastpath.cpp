@@ -1,6 +1,7 @@
 // Native CPU hot path of the checker (CPython extension `_fastpath`).
 //
-// scan_nodelist(buf, result, keys, use_allocatable, want_extras, health_key, NodeExtras)
+// scan_nodelist(buf, result, keys, use_allocatable, want_extras, health_key, NodeExtras,
+//               health_condition="", annotation_mode=2)
 //   One pass over a kube-apiserver NodeList JSON page.  Only the fields the
 //   checker consumes are materialised as Python objects (metadata.name,
 //   metadata.labels, one annotation, spec.taints, spec.unschedulable,
@@ -25,6 +26,8 @@
 
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+
+#include <emmintrin.h>
 
 #include <cmath>
 #include <cstdint>
@@ -75,26 +78,33 @@ struct RawStr {
   bool esc;
 };
 
+// First '"' or '\\' at or after p (SSE2, 16 bytes per step); e if none.
+inline const char* find_quote_or_backslash(const char* p, const char* e) {
+  const __m128i q = _mm_set1_epi8('"'), b = _mm_set1_epi8('\\');
+  while (e - p >= 16) {
+    __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+    unsigned m = static_cast<unsigned>(_mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(v, q), _mm_cmpeq_epi8(v, b))));
+    if (m) return p + __builtin_ctz(m);
+    p += 16;
+  }
+  while (p < e && *p != '"' && *p != '\\') ++p;
+  return p;
+}
+
 RawStr read_raw_string(Cursor& c) {
   c.expect('"');
   const char* b = c.p;
+  const char* p = b;
   bool esc = false;
-  const char* p = c.p;
-  const char* end = c.end;
   for (;;) {
-    const void* q = memchr(p, '"', end - p);
-    if (!q) throw Fallback{"unterminated string"};
-    const char* qq = static_cast<const char*>(q);
-    // count preceding backslashes to see whether the quote is escaped
-    const char* s = qq;
-    while (s > b && s[-1] == '\\') --s;
-    if (s != qq) esc = true;
-    if (((qq - s) & 1) == 0) {
-      if (!esc && memchr(b, '\\', qq - b)) esc = true;
-      c.p = qq + 1;
-      return RawStr{b, qq, esc};
+    p = find_quote_or_backslash(p, c.end);
+    if (p >= c.end) throw Fallback{"unterminated string"};
+    if (*p == '"') {
+      c.p = p + 1;
+      return RawStr{b, p, esc};
     }
-    p = qq + 1;
+    esc = true;  // backslash: skip it and the escaped character
+    p += 2;
   }
 }
 
@@ -239,28 +249,46 @@ void skip_literal(Cursor& c) {
   }
 }
 
-// Skip a whole object/array with a flat bracket counter (string-aware).
+// Skip a whole object/array with a flat bracket counter (string-aware), 16 bytes per step:
+// only '"', '{', '}', '[' and ']' stop the vector scan; strings are jumped over whole.
 void skip_container(Cursor& c) {
   const char* p = c.p;
   const char* e = c.end;
   int depth = 0;
+  const __m128i vq = _mm_set1_epi8('"'), vo = _mm_set1_epi8('{'), vc = _mm_set1_epi8('}');
+  const __m128i vl = _mm_set1_epi8('['), vr = _mm_set1_epi8(']');
   while (p < e) {
-    char ch = *p;
+    const char* hit;
+    if (e - p >= 16) {
+      __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+      __m128i m = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, vq), _mm_cmpeq_epi8(v, vo)),
+                               _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, vc), _mm_cmpeq_epi8(v, vl)),
+                                            _mm_cmpeq_epi8(v, vr)));
+      unsigned bits = static_cast<unsigned>(_mm_movemask_epi8(m));
+      if (!bits) {
+        p += 16;
+        continue;
+      }
+      hit = p + __builtin_ctz(bits);
+    } else {
+      hit = p;
+      while (hit < e && *hit != '"' && *hit != '{' && *hit != '}' && *hit != '[' && *hit != ']') ++hit;
+      if (hit >= e) break;
+    }
+    const char ch = *hit;
     if (ch == '"') {
-      Cursor t{p, e};
+      Cursor t{hit, e};
       read_raw_string(t);
       p = t.p;
       continue;
     }
     if (ch == '{' || ch == '[') {
       ++depth;
-    } else if (ch == '}' || ch == ']') {
-      if (--depth == 0) {
-        c.p = p + 1;
-        return;
-      }
+    } else if (--depth == 0) {
+      c.p = hit + 1;
+      return;
     }
-    ++p;
+    p = hit + 1;
   }
   throw Fallback{"unterminated container"};
 }
@@ -500,7 +528,8 @@ struct NodeScan {
   bool meta_obj = false;     // metadata is a JSON object
   Ref name;                  // str or None
   Ref labels;                // dict (possibly empty) or null
-  Ref health;                // str or nullptr
+  RawStr health_raw{nullptr, nullptr, false};  // annotation value, decoded only if needed
+  bool have_health = false;
   Ref taints;                // list
   Ref internal_ip;           // str or nullptr (first InternalIP of status.addresses)
   Ref health_cond;           // (status, reason, message, heartbeat) tuple of the health condition, or nullptr
@@ -530,7 +559,7 @@ void parse_labels(Cursor& c, NodeScan& ns, std::string& scratch) {
 void parse_metadata(Cursor& c, NodeScan& ns, const std::string& health_key, std::string& scratch) {
   ns.name.reset(nullptr);
   ns.labels.reset(nullptr);
-  ns.health.reset(nullptr);
+  ns.have_health = false;
   ns.meta_obj = false;
   if (c.peek() != '{') {
     skip_value(c);  // null or a non-object: name "" / labels {} (models/node.py)
@@ -549,16 +578,17 @@ void parse_metadata(Cursor& c, NodeScan& ns, const std::string& health_key, std:
     } else if (raw_equals(k, "labels", scratch)) {
       parse_labels(cc, ns, scratch);
     } else if (raw_equals(k, "annotations", scratch)) {
-      ns.health.reset(nullptr);
+      ns.have_health = false;
       if (cc.peek() != '{') {
         skip_value(cc);
         return;
       }
       for_members(cc, [&](const RawStr& ak, Cursor& c3) {
-        if (!health_key.empty() && raw_equals(ak, health_key.c_str(), scratch) && c3.peek() == '"') {
-          ns.health.reset(make_str(read_raw_string(c3), scratch));
+        if (!health_key.empty() && raw_equals(ak, health_key.c_str(), scratch)) {
+          ns.have_health = c3.peek() == '"';
+          if (ns.have_health) ns.health_raw = read_raw_string(c3);
+          else skip_value(c3);
         } else {
-          if (!health_key.empty() && raw_equals(ak, health_key.c_str(), scratch)) ns.health.reset(nullptr);
           skip_value(c3);
         }
       });
@@ -785,7 +815,7 @@ struct PageOut {
 };
 
 void emit_node(NodeScan& ns, const KeySpec& ks, bool use_alloc, bool want_extras, PyObject* extras_cls,
-               PageOut& out) {
+               int annot_mode, PageOut& out, std::string& scratch) {
   long long total = 0;
   Ref bd(breakdown_dict(ks, use_alloc ? ns.alloc : ns.cap, &total));
   if (total <= 0) return;  // not a GPU node (reference :222)
@@ -820,7 +850,12 @@ void emit_node(NodeScan& ns, const KeySpec& ks, bool use_alloc, bool want_extras
   if (want_extras) {
     Ref capd(breakdown_dict(ks, ns.cap, nullptr));
     Ref allocd(breakdown_dict(ks, ns.alloc, nullptr));
-    PyObject* health = ns.health.o ? ns.health.o : Py_None;
+    // the annotation (full probe report, KBs of escaped JSON) is only materialised when the
+    // caller will read it: always (mode 2) or for nodes without the AMDGPUHealthy condition (mode 1)
+    Ref health_str;
+    if (ns.have_health && (annot_mode == 2 || (annot_mode == 1 && !ns.health_cond.o)))
+      health_str.reset(make_str(ns.health_raw, scratch));
+    PyObject* health = health_str.o ? health_str.o : Py_None;
     PyObject* ip = ns.internal_ip.o ? ns.internal_ip.o : Py_None;
     PyObject* hc = ns.health_cond.o ? ns.health_cond.o : Py_None;
     Ref ex(PyObject_CallFunctionObjArgs(extras_cls, ns.ready ? Py_True : Py_False, capd.o, allocd.o,
@@ -834,7 +869,7 @@ void emit_node(NodeScan& ns, const KeySpec& ks, bool use_alloc, bool want_extras
 }
 
 void parse_item(Cursor& c, const KeySpec& ks, bool use_alloc, bool want_extras, PyObject* extras_cls,
-                const std::string& health_key, const std::string& health_cond, PageOut& out,
+                const std::string& health_key, const std::string& health_cond, int annot_mode, PageOut& out,
                 std::string& scratch) {
   out.items++;
   if (c.peek() != '{') {
@@ -850,7 +885,7 @@ void parse_item(Cursor& c, const KeySpec& ks, bool use_alloc, bool want_extras, 
     else if (raw_equals(k, "status", scratch)) parse_status(cc, ns, ks, scratch, health_cond);
     else skip_value(cc);
   });
-  emit_node(ns, ks, use_alloc, want_extras, extras_cls, out);
+  emit_node(ns, ks, use_alloc, want_extras, extras_cls, annot_mode, out, scratch);
 }
 
 int append_all(PyObject* result, PyObject* attr, PyObject* items) {
@@ -877,8 +912,9 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
   int use_alloc, want_extras;
   const char* health_key_c;
   const char* health_cond_c = "";
-  if (!PyArg_ParseTuple(args, "y*OO!ppsO|s", &view, &result, &PyTuple_Type, &keys, &use_alloc, &want_extras,
-                        &health_key_c, &extras_cls, &health_cond_c))
+  int annot_mode = 2;
+  if (!PyArg_ParseTuple(args, "y*OO!ppsO|si", &view, &result, &PyTuple_Type, &keys, &use_alloc, &want_extras,
+                        &health_key_c, &extras_cls, &health_cond_c, &annot_mode))
     return nullptr;
   KeySpec ks;
   for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(keys); ++i) {
@@ -909,7 +945,7 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
         if (is_null(cc)) return;
         if (cc.peek() != '[') throw Fallback{"items not a list"};
         for_elements(cc, [&](Cursor& c3) {
-          parse_item(c3, ks, use_alloc, want_extras, extras_cls, health_key, health_cond, out, scratch);
+          parse_item(c3, ks, use_alloc, want_extras, extras_cls, health_key, health_cond, annot_mode, out, scratch);
         });
       } else if (raw_equals(k, "metadata", scratch)) {
         out.cont.reset(nullptr);

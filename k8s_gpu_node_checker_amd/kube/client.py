@@ -116,7 +116,7 @@ class KubeClient:
     def scan_nodes(self, limit: int = 500, keys: Sequence[str] = GPU_RESOURCE_KEYS,
                    gpu_source: str = "capacity", want_extras: bool = False,
                    label_selector: Optional[str] = None,
-                   resource_version: Optional[str] = None) -> ScanResult:
+                   resource_version: Optional[str] = None, annotation_mode: int = 2) -> ScanResult:
         """LIST all nodes (paginated) and classify them (reference ``list_gpu_nodes``, ``:215-226``)."""
         from ..ops import fastpath
         result = ScanResult()
@@ -130,11 +130,11 @@ class KubeClient:
                     # continue token expired mid-list: restart as one consistent full LIST
                     result = ScanResult()
                     resp = self.request("GET", self._list_path(0, None, label_selector, None))
-                    fastpath.scan_page(resp.body, result, keys, gpu_source, want_extras)
+                    fastpath.scan_page(resp.body, result, keys, gpu_source, want_extras, annotation_mode)
                     return result
                 raise
             t0 = time.perf_counter()
-            cont, _ = fastpath.scan_page(resp.body, result, keys, gpu_source, want_extras)
+            cont, _ = fastpath.scan_page(resp.body, result, keys, gpu_source, want_extras, annotation_mode)
             if self.tracer is not None:
                 self.tracer.add("parse", time.perf_counter() - t0)
             if not cont or limit <= 0:

@@ -121,7 +121,10 @@ class NodeExtras:
         }
 
 
-def node_extras(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS) -> NodeExtras:
+def node_extras(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS,
+                annotation_mode: int = 2) -> NodeExtras:
+    """``annotation_mode``: 2 = always keep the probe-report annotation, 1 = only for nodes
+    without the ``AMDGPUHealthy`` condition (the checker's default: the condition is the verdict)."""
     meta = _get(node, "metadata")
     status = _get(node, "status")
     ann = _get(meta, "annotations")
@@ -133,6 +136,9 @@ def node_extras(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS
             if isinstance(a, Mapping) and a.get("type") == "InternalIP" and isinstance(a.get("address"), str):
                 ip = a["address"]
                 break
+    hc = health_condition(node)
+    if annotation_mode == 0 or (annotation_mode == 1 and hc is not None):
+        raw = None
     return NodeExtras(
         ready_condition=is_ready(node),
         capacity=gpu_breakdown(_get(status, "capacity"), keys),
@@ -140,7 +146,7 @@ def node_extras(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS
         unschedulable=bool(_get(_get(node, "spec"), "unschedulable")),
         health_annotation=raw if isinstance(raw, str) else None,
         internal_ip=ip,
-        health_condition=health_condition(node),
+        health_condition=hc,
     )
 
 
@@ -183,12 +189,12 @@ class ScanResult:
 
 def scan_items(items: Iterable[Mapping[str, Any]], result: Optional[ScanResult] = None,
                keys: Sequence[str] = GPU_RESOURCE_KEYS, gpu_source: str = "capacity",
-               want_extras: bool = False) -> ScanResult:
+               want_extras: bool = False, annotation_mode: int = 2) -> ScanResult:
     """Pure-Python scan of decoded ``NodeList.items`` (reference ``:217-225``)."""
     res = result if result is not None else ScanResult()
     for n in items or ():
         info = project_node(n, keys, gpu_source)
-        res.add(info, node_extras(n, keys) if want_extras else None)
+        res.add(info, node_extras(n, keys, annotation_mode) if want_extras else None)
     return res
 
 

@@ -44,7 +44,8 @@ def backend() -> str:
 
 
 def scan_page(body: bytes, result: ScanResult, keys: Sequence[str] = GPU_RESOURCE_KEYS,
-              gpu_source: str = "capacity", want_extras: bool = False) -> Tuple[Optional[str], int]:
+              gpu_source: str = "capacity", want_extras: bool = False,
+              annotation_mode: int = 2) -> Tuple[Optional[str], int]:
     """Scan one ``NodeList`` page into ``result``.
 
     Returns ``(continue_token, item_count)``.  Raises ``ValueError`` on a body
@@ -54,7 +55,8 @@ def scan_page(body: bytes, result: ScanResult, keys: Sequence[str] = GPU_RESOURC
     if mod is not None:
         try:
             return mod.scan_nodelist(body, result, tuple(keys), gpu_source == "allocatable",
-                                     want_extras, HEALTH_ANNOTATION, NodeExtras, HEALTH_CONDITION)
+                                     want_extras, HEALTH_ANNOTATION, NodeExtras, HEALTH_CONDITION,
+                                     annotation_mode)
         except mod.FallbackError:
             pass  # unusual shape: let the reference-semantics Python path decide
     doc = json.loads(body)
@@ -62,7 +64,7 @@ def scan_page(body: bytes, result: ScanResult, keys: Sequence[str] = GPU_RESOURC
         raise ValueError("NodeList response is not a JSON object")
     items = doc.get("items") or []
     before = result.items_seen
-    scan_items(items, result, keys, gpu_source, want_extras)
+    scan_items(items, result, keys, gpu_source, want_extras, annotation_mode)
     meta = doc.get("metadata") or {}
     token = meta.get("continue") if isinstance(meta, dict) else None
     return (token or None), result.items_seen - before

@@ -13,16 +13,16 @@ ext = fastpath.ext()
 pytestmark = pytest.mark.skipif(ext is None, reason="native fast path not built")
 
 
-def native_scan(body, src="capacity", extras=True):
+def native_scan(body, src="capacity", extras=True, mode=2):
     r = ScanResult()
     tok = ext.scan_nodelist(body, r, GPU_RESOURCE_KEYS, src == "allocatable", extras, HEALTH_ANNOTATION, NodeExtras,
-                            HEALTH_CONDITION)
+                            HEALTH_CONDITION, mode)
     return r, tok
 
 
-def py_scan(body, src="capacity", extras=True):
+def py_scan(body, src="capacity", extras=True, mode=2):
     doc = json.loads(body)
-    r = scan_items(doc.get("items") or [], None, GPU_RESOURCE_KEYS, src, extras)
+    r = scan_items(doc.get("items") or [], None, GPU_RESOURCE_KEYS, src, extras, mode)
     tok = (doc.get("metadata") or {}).get("continue") or None
     return r, (tok, r.items_seen)
 
@@ -32,12 +32,12 @@ def canon(r):
     return json.dumps([r.gpu_nodes, r.ready_gpu_nodes, ex, r.items_seen], ensure_ascii=False)
 
 
-def assert_same(body, src="capacity"):
+def assert_same(body, src="capacity", mode=2):
     try:
-        a, ta = native_scan(body, src)
+        a, ta = native_scan(body, src, mode=mode)
     except ext.FallbackError:
         return "fallback"
-    b, tb = py_scan(body, src)
+    b, tb = py_scan(body, src, mode=mode)
     assert canon(a) == canon(b)
     assert ta == tb
     return "native"
@@ -51,12 +51,18 @@ def test_golden(g, src):
 
 def test_realistic_cluster_with_health_and_addresses():
     body = json.dumps(fixtures.node_list(fixtures.cluster(50, "mixed", not_ready=[3], with_health=True))).encode()
-    assert assert_same(body) == "native"
+    for mode in (0, 1, 2):
+        assert assert_same(body, mode=mode) == "native"
+    r1, _ = native_scan(body, mode=1)
+    assert r1.extras[0].health_annotation is None and r1.extras[0].health_condition[0] == "True"
     r, _ = native_scan(body)
     assert r.extras[0].internal_ip == "10.0.0.0" and r.extras[0].health_annotation.startswith("{")
 
 
 EDGE_BODIES = [
+    b'{"items": [{"metadata": {"name": "e\\\\", "labels": {"a\\\\\\"b": "\\\\\\\\"}}, "status": {"capacity": {"amd.com/gpu": "1"}}}]}',
+    b'{"items": [{"metadata": {"name": "long-' + b"x" * 70 + b'\\"q"}, "status": {"capacity": {"amd.com/gpu": "1"},'
+    b' "images": [{"names": ["' + b"y" * 40 + b'\\\\", "z\\"{[]}"]}]}}]}',
     b'{"items": null}',
     b'{"items": []}',
     b'{"metadata": {"continue": ""}, "items": []}',
@@ -130,10 +136,11 @@ node = st.fixed_dictionaries({}, optional={
 
 
 @settings(max_examples=300, suppress_health_check=[HealthCheck.too_slow])
-@given(st.lists(node, max_size=6), st.sampled_from(["capacity", "allocatable"]), st.booleans())
-def test_fuzz_equivalence(items, src, ascii_only):
+@given(st.lists(node, max_size=6), st.sampled_from(["capacity", "allocatable"]), st.booleans(),
+       st.sampled_from([0, 1, 2]))
+def test_fuzz_equivalence(items, src, ascii_only, mode):
     body = json.dumps({"items": items}, ensure_ascii=ascii_only).encode()
-    assert_same(body, src)
+    assert_same(body, src, mode)
 
 
 json_tree = st.recursive(
