@@ -32,6 +32,7 @@
 namespace {
 
 thread_local std::string g_err;
+int g_gemm_variant = 0;
 
 #define DIAG_CHECK(expr)                                                                  \
   do {                                                                                    \
@@ -169,6 +170,102 @@ gemm_bf16_kernel(const u32x4* __restrict__ A, const u32x4* __restrict__ Bt, floa
         C[static_cast<size_t>(row0 + m * 16 + fq * 4 + j) * N + col0 + n * 16 + frow] = acc[m][n][j];
 }
 
+// ---------------------------------------------------------------------------
+// gemm v2: 256x256x64 block tile, 8 waves (2 M x 4 N, 128x64 each), operands
+// streamed global -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging,
+// 8 per thread per stage), two LDS stages of 64 KiB (1 block per CU), the same
+// XOR swizzle as v1 applied on the *global source* address because an LDS-DMA
+// wave instruction writes 1 KiB lane-linearly (8 rows of 128 B).
+constexpr int V2_BM = 256, V2_BN = 256, V2_THREADS = 512;
+constexpr int V2_ROWS_PER_WAVE = 32;                   // rows of each operand one wave fills per stage
+constexpr int V2_STAGE_BYTES = 2 * V2_BM * BK * 2;     // A + B, bf16 = 64 KiB
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ void v2_fill(unsigned char* lds_stage, const __bf16* __restrict__ A,
+                                        const __bf16* __restrict__ Bt, int K, int kt, int wid, int lane) {
+  // lane -> (row within an 8-row group, physical chunk); logical chunk = phys ^ swizzle(row)
+  const int rsub = lane >> 3, phys = lane & 7;
+#pragma unroll
+  for (int op = 0; op < 2; ++op) {
+    const __bf16* src = op == 0 ? A : Bt;
+#pragma unroll
+    for (int j = 0; j < V2_ROWS_PER_WAVE / 8; ++j) {
+      const int row = wid * V2_ROWS_PER_WAVE + j * 8 + rsub;
+      const int c = phys ^ ((row >> 1) & 7);
+      const __bf16* g = src + static_cast<size_t>(row) * K + kt * BK + c * 8;
+      unsigned char* l = lds_stage + op * (V2_BM * BK * 2) + (wid * V2_ROWS_PER_WAVE + j * 8) * (BK * 2);
+      __builtin_amdgcn_global_load_lds(g, (lds_void_t*)l, 16, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ void v2_compute(floatx4 (&acc)[8][4], const u32x4* __restrict__ a_img,
+                                           const u32x4* __restrict__ b_img, int wr, int wc, int frow, int fq) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 bfr[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = __builtin_bit_cast(bf16x8, b_img[swz(wc * 64 + n * 16 + frow, fq + 4 * s)]);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const bf16x8 af = __builtin_bit_cast(bf16x8, a_img[swz(wr * 128 + m * 16 + frow, fq + 4 * s)]);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[n], acc[m][n], 0, 0, 0);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(V2_THREADS, 1)
+gemm_bf16_v2_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
+                    int K) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages x 64 KiB (dynamic)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int tiles_m = M / V2_BM, tiles_n = N / V2_BN, nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  constexpr int GROUP_M = 4;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % (GROUP_M * tiles_n)) % gsize;
+  const int tn = (bid % (GROUP_M * tiles_n)) / gsize;
+  const __bf16* Ab = A + static_cast<size_t>(tm) * V2_BM * K;
+  const __bf16* Bb = Bt + static_cast<size_t>(tn) * V2_BN * K;
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = K / BK;
+  const int frow = lane & 15, fq = lane >> 4;
+  v2_fill(smem, Ab, Bb, K, 0, wid, lane);
+  __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0) (gfx9 encoding: vmcnt[3:0]=0, vmcnt[15:14]=0)
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    unsigned char* cur = smem + (kt & 1) * V2_STAGE_BYTES;
+    if (kt + 1 < KT) v2_fill(smem + ((kt + 1) & 1) * V2_STAGE_BYTES, Ab, Bb, K, kt + 1, wid, lane);
+    v2_compute(acc, reinterpret_cast<const u32x4*>(cur), reinterpret_cast<const u32x4*>(cur + V2_BM * BK * 2), wr, wc,
+               frow, fq);
+    __builtin_amdgcn_s_waitcnt(0x3f70);  // this wave's LDS-DMA for stage kt+1 has landed
+    __syncthreads();                     // ... and everyone's; stage kt is free for kt+2
+  }
+  const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 64;
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        C[static_cast<size_t>(row0 + m * 16 + fq * 4 + j) * N + col0 + n * 16 + frow] = acc[m][n][j];
+}
+
 // fp32 reference for sampled outputs: one thread per (row, col) sample.
 __global__ void gemm_ref_kernel(const __bf16* A, const __bf16* Bt, const int* rows, const int* cols, float* out,
                                 int nsamp, int K) {
@@ -200,34 +297,44 @@ __global__ void fill_bf16_kernel(__bf16* p, size_t n, uint64_t seed) {
 }
 
 // ---------------------------------------------------------------- HBM streams
-__global__ void __launch_bounds__(256) copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
+// Forms picked by the sweep in tools/hbm_explore.hip on MI355X (profiles/hbm_explore_mi355x.json):
+// copy 8-deep nontemporal 5.29 TB/s, read 8-deep nontemporal 6.78 TB/s, plain write 5.16 TB/s,
+// all at 32 blocks of 256 threads per CU (vs 4.5 / 5.5 / 4.6 TB/s for the first 4-deep, 8/CU form).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int HBM_UNROLL = 8;
+constexpr int HBM_BLOCKS_PER_CU = 32;
+
+__global__ void __launch_bounds__(256) copy_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst, size_t n) {
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
+  for (; i + (HBM_UNROLL - 1) * stride < n; i += HBM_UNROLL * stride) {
+    f32x4 v[HBM_UNROLL];
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
   }
   for (; i < n; i += stride) dst[i] = src[i];
 }
 
-__global__ void __launch_bounds__(256) read_kernel(const float4* __restrict__ src, size_t n, float* sink) {
+__global__ void __launch_bounds__(256) read_kernel(const f32x4* __restrict__ src, size_t n, float* sink) {
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
   float acc = 0.f;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    acc += (a.x + b.y) + (c.z + d.w);
+  for (; i + (HBM_UNROLL - 1) * stride < n; i += HBM_UNROLL * stride) {
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) {
+      const f32x4 v = __builtin_nontemporal_load(src + i + u * stride);
+      acc += v[0] + v[3];
+    }
   }
-  for (; i < n; i += stride) acc += src[i].x;
+  for (; i < n; i += stride) acc += src[i][0];
   if (acc == 1234.5678f) *sink = acc;  // keeps the loads alive, practically never stores
 }
 
-__global__ void __launch_bounds__(256) write_kernel(float4* __restrict__ dst, size_t n, float v) {
+__global__ void __launch_bounds__(256) write_kernel(f32x4* __restrict__ dst, size_t n, float v) {
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  const float4 x = make_float4(v, v, v, v);
+  const f32x4 x = {v, v, v, v};
   for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride) dst[i] = x;
 }
 
@@ -284,6 +391,10 @@ extern "C" {
 
 const char* diag_last_error(void) { return g_err.c_str(); }
 
+// 0 = auto (v2 256x256 LDS-DMA tiles when M, N are multiples of 256 and the grid fills the chip),
+// 1 = force v1 (128x128 register-staged), 2 = force v2
+void diag_set_gemm_variant(int v) { g_gemm_variant = v; }
+
 int diag_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -306,9 +417,29 @@ int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N,
     g_err = "gemm_bf16: M, N must be multiples of 128 and K a multiple of 64";
     return -2;
   }
-  const int nwg = (M / BM) * (N / BN);
-  hipLaunchKernelGGL(gemm_bf16_kernel, dim3(nwg), dim3(THREADS), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const u32x4*>(A), static_cast<const u32x4*>(Bt), C, M, N, K);
+  // v2 needs 256-multiples and enough 256x256 tiles to occupy the 256 CUs (one block per CU);
+  // below that the 128x128 kernel's 4x larger grid wins (measured: 2048^3 v1 543 vs v2 321 TFLOP/s)
+  const bool v2_ok = M % V2_BM == 0 && N % V2_BN == 0 && (M / V2_BM) * (N / V2_BN) >= 256;
+  if (g_gemm_variant == 2 || (g_gemm_variant == 0 && v2_ok)) {
+    if (M % V2_BM || N % V2_BN) {
+      g_err = "gemm_bf16 v2: M, N must be multiples of 256";
+      return -2;
+    }
+    static bool attr_set = false;
+    if (!attr_set) {
+      DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_v2_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+      attr_set = true;
+    }
+    const int nwg = (M / V2_BM) * (N / V2_BN);
+    hipLaunchKernelGGL(gemm_bf16_v2_kernel, dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
+                       static_cast<hipStream_t>(stream), static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt),
+                       C, M, N, K);
+  } else {
+    const int nwg = (M / BM) * (N / BN);
+    hipLaunchKernelGGL(gemm_bf16_kernel, dim3(nwg), dim3(THREADS), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const u32x4*>(A), static_cast<const u32x4*>(Bt), C, M, N, K);
+  }
   DIAG_CHECK(hipGetLastError());
   return 0;
 }
@@ -384,20 +515,20 @@ int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int n
 // HBM streams over `bytes` per buffer: copy (read+write), read-only, write-only, in TB/s.
 int diag_hbm_bandwidth(int device, size_t bytes, int iters, double* copy_tbs, double* read_tbs, double* write_tbs) {
   DIAG_CHECK(hipSetDevice(device));
-  const size_t n = bytes / sizeof(float4);
-  float4 *a = nullptr, *b = nullptr;
+  const size_t n = bytes / sizeof(f32x4);
+  f32x4 *a = nullptr, *b = nullptr;
   float* sink = nullptr;
-  DIAG_CHECK(hipMalloc(&a, n * sizeof(float4)));
-  DIAG_CHECK(hipMalloc(&b, n * sizeof(float4)));
+  DIAG_CHECK(hipMalloc(&a, n * sizeof(f32x4)));
+  DIAG_CHECK(hipMalloc(&b, n * sizeof(f32x4)));
   DIAG_CHECK(hipMalloc(&sink, sizeof(float)));
-  const int grid = grid_for(device, 8);
+  const int grid = grid_for(device, HBM_BLOCKS_PER_CU);
   hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, a, n, 1.0f);
   hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, b, n, 2.0f);
   DIAG_CHECK(hipGetLastError());
   hipEvent_t e0, e1;
   DIAG_CHECK(hipEventCreate(&e0));
   DIAG_CHECK(hipEventCreate(&e1));
-  const size_t nb = n * sizeof(float4);
+  const size_t nb = n * sizeof(f32x4);
   // copy
   hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, nullptr, a, b, n);
   DIAG_CHECK(hipEventRecord(e0, nullptr));
