@@ -5,13 +5,14 @@
 // has a weak HBM stack; these kernels measure exactly that.
 //
 //   gemm_bf16   C[M,N] = A[M,K] . Bt[N,K]^T, bf16 in / fp32 out on MFMA
-//               (v_mfma_f32_16x16x32_bf16), 128x128x64 tiles, 4 waves (2x2) of
-//               64x64, XOR-swizzled LDS (conflict-free ds_read_b128 fragment
-//               loads), register-staged double buffer, XCD-aware tile order.
+//               (v_mfma_f32_16x16x32_bf16), XOR-swizzled LDS (conflict-free
+//               ds_read_b128 fragment loads), XCD-aware tile order.
+//               v2: 256x256x64 tiles, 8 waves, LDS-DMA double buffer (large GEMMs);
+//               v1: 128x128x64 tiles, 4 waves, register-staged (small grids).
 //               Verified against an fp32 reference kernel on sampled outputs.
 //   hbm_copy / hbm_read / hbm_write
-//               float4 streams, 4 loads in flight per thread, grid sized to
-//               fill 256 CUs; reported in TB/s against the 8 TB/s HBM3E spec.
+//               16-byte nontemporal streams, 8 loads in flight per thread,
+//               32 blocks per CU; TB/s against the 8 TB/s HBM3E spec.
 //   memtest     address-hash patterns written and verified (plus the
 //               bit-inverted pass), mismatches counted with one atomic per
 //               failing 16-byte word.
