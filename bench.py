@@ -82,8 +82,10 @@ def main() -> int:
     procs = []
     ctrl = {}
     if rank == 0:
+        # nodes beyond the GPU count start with a recorded MI355X probe (condition + annotation); the
+        # ranks' own nodes get their live probe PATCHed below
         p, info = _spawn("k8s_gpu_node_checker_amd.testing.mock_apiserver", "--nodes", str(n_nodes), "--kind", "amd",
-                         "--gpus-per-node", "1")
+                         "--gpus-per-node", "1", *(["--with-health"] if n_nodes > n_gpus else []))
         procs.append(p)
         ctrl["api"] = info["url"]
         if args.slack:
@@ -153,11 +155,6 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
     probe_ms = (time.perf_counter() - t0) * 1e3
     with KubeClient(cluster) as kc:
         agent.publish(kc, rep)  # AMDGPUHealthy NodeCondition + full report annotation
-        if rank == 0 and n_nodes > n_gpus:  # --nodes > GPUs: the extra nodes get a copy of rank 0's report
-            for i in range(n_gpus, n_nodes):
-                r2 = dict(rep, node=f"mi355x-node-{i:04d}")
-                kc.patch_node_annotations(f"mi355x-node-{i:04d}", agent.annotation(r2))
-                kc.patch_node_condition(f"mi355x-node-{i:04d}", agent.condition(r2))
     diag = {}
     for g in rep.get("gpus") or []:
         diag = g.get("diag") or {}

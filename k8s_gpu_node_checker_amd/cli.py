@@ -105,12 +105,14 @@ def _run_once(args: argparse.Namespace) -> int:
     import json
     try:
         from .checker import CheckOptions, check_and_report
-        from .utils import statefile
         cluster = _load_cluster(args)
         opts = CheckOptions.from_args(args)
-        prev = statefile.load(args.state_file) if args.state_file else None
-        if args.state_file and args.slack_on_change:
-            opts.slack_webhook = statefile.gate_webhook(prev, opts, cluster)
+        prev = None
+        if args.state_file:
+            from .utils import statefile
+            prev = statefile.load(args.state_file)
+            if args.slack_on_change:
+                opts.slack_webhook = statefile.gate_webhook(prev, opts, cluster)
         result = check_and_report(cluster, opts)
         if args.state_file:
             statefile.save(args.state_file, result, prev)

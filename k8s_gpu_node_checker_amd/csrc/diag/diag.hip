@@ -279,6 +279,11 @@ __global__ void gemm_ref_kernel(const __bf16* A, const __bf16* Bt, const int* ro
   out[i] = s;
 }
 
+__global__ void gather_kernel(const float* C, const int* rows, const int* cols, float* out, int nsamp, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nsamp) out[i] = C[static_cast<size_t>(rows[i]) * N + cols[i]];
+}
+
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {
   x ^= x >> 33;
   x *= 0xff51afd7ed558ccdULL;
@@ -490,10 +495,15 @@ int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int n
   hipLaunchKernelGGL(gemm_ref_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, A, Bt, rows, cols, ref,
                      nsamp, K);
   DIAG_CHECK(hipGetLastError());
+  // gather the sampled outputs on the device: one copy instead of nsamp tiny ones
+  float* got = nullptr;
+  DIAG_CHECK(hipMalloc(&got, sizeof(float) * nsamp));
+  hipLaunchKernelGGL(gather_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, C, rows, cols, got, nsamp, N);
+  DIAG_CHECK(hipGetLastError());
   std::vector<float> href(nsamp), hC(nsamp);
   DIAG_CHECK(hipMemcpy(href.data(), ref, sizeof(float) * nsamp, hipMemcpyDeviceToHost));
-  for (int i = 0; i < nsamp; ++i)
-    DIAG_CHECK(hipMemcpy(&hC[i], C + static_cast<size_t>(hr[i]) * N + hc[i], sizeof(float), hipMemcpyDeviceToHost));
+  DIAG_CHECK(hipMemcpy(hC.data(), got, sizeof(float) * nsamp, hipMemcpyDeviceToHost));
+  hipFree(got);
   double worst = 0.0;
   for (int i = 0; i < nsamp; ++i) {
     const double denom = std::max(1.0, std::fabs(static_cast<double>(href[i])));

@@ -30,7 +30,6 @@ from __future__ import annotations
 import base64
 import json
 import os
-import tempfile
 import time
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -53,7 +52,15 @@ def _load_yaml(path: str) -> Any:
             return json.loads(raw)
         except ValueError:
             pass
-    import yaml  # lazy: ~11 ms import, only paid when a YAML kubeconfig is read
+    try:  # the kubeconfig YAML subset, without the ~10 ms PyYAML import
+        from ..utils.miniyaml import Unsupported, loads
+        try:
+            return loads(raw.decode("utf-8"))
+        except (Unsupported, UnicodeDecodeError):
+            pass
+    except ImportError:  # pragma: no cover
+        pass
+    import yaml  # full YAML (anchors, block scalars, ...)
     loader = getattr(yaml, "CSafeLoader", yaml.SafeLoader)
     return yaml.load(raw, Loader=loader)
 
@@ -200,6 +207,7 @@ class ClusterConnection:
             ctx.load_cert_chain(self.cert_file, self.key_file)
             return
         # ssl.load_cert_chain only takes paths: stage *-data in a private 0700 dir
+        import tempfile
         d = tempfile.mkdtemp(prefix="k8sgpu-")
         try:
             cert = os.path.join(d, "client.crt")

@@ -15,12 +15,10 @@ supports the syntax the ``.env-template`` needs and the common extras:
 from __future__ import annotations
 
 import os
-import re
 import sys
-from typing import Dict, Iterator, Optional, Tuple
+from typing import Callable, Dict, Iterator, Optional, Tuple
 
-_LINE = re.compile(r"^\s*(?:export\s+)?([A-Za-z_][A-Za-z0-9_.\-]*)\s*(?:=\s*(.*))?$")
-_EXPAND = re.compile(r"\$\{([A-Za-z_][A-Za-z0-9_]*)(?::-([^}]*))?\}")
+_KEY_CHARS = frozenset("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789_.-")
 _DQ_ESC = {"n": "\n", "t": "\t", "r": "\r", '"': '"', "\\": "\\", "'": "'", "$": "$"}
 
 
@@ -44,10 +42,43 @@ def _unquote(raw: str) -> Tuple[str, bool]:
             out.append(c)
             i += 1
         return "".join(out), True
-    m = re.search(r"\s#", raw)
-    if m:
-        raw = raw[:m.start()]
+    for i in range(1, len(raw)):
+        if raw[i] == "#" and raw[i - 1] in " \t":
+            raw = raw[:i]
+            break
     return raw.strip(), True
+
+
+def _split_line(line: str) -> Optional[Tuple[str, Optional[str]]]:
+    s = line.strip()
+    if s.startswith("export ") or s.startswith("export\t"):
+        s = s[7:].lstrip()
+    eq = s.find("=")
+    key = (s if eq < 0 else s[:eq]).rstrip()
+    if not key or not (key[0].isalpha() or key[0] == "_") or not all(c in _KEY_CHARS for c in key):
+        return None
+    return key, (None if eq < 0 else s[eq + 1:].lstrip())
+
+
+def _expand(val: str, lookup: Callable[[str], Optional[str]]) -> str:
+    """``${VAR}`` / ``${VAR:-default}`` expansion."""
+    out = []
+    i = 0
+    while i < len(val):
+        j = val.find("${", i)
+        k = val.find("}", j + 2) if j >= 0 else -1
+        if j < 0 or k < 0:
+            out.append(val[i:])
+            break
+        out.append(val[i:j])
+        name, _, default = val[j + 2:k].partition(":-")
+        if name and (name[0].isalpha() or name[0] == "_") and all(c.isalnum() or c == "_" for c in name):
+            got = lookup(name)
+            out.append(got if got else default)
+        else:
+            out.append(val[j:k + 1])
+        i = k + 1
+    return "".join(out)
 
 
 def parse_dotenv(text: str) -> Iterator[Tuple[str, Optional[str], bool]]:
@@ -55,10 +86,10 @@ def parse_dotenv(text: str) -> Iterator[Tuple[str, Optional[str], bool]]:
         s = line.strip()
         if not s or s.startswith("#"):
             continue
-        m = _LINE.match(line)
-        if not m:
+        kv = _split_line(line)
+        if kv is None:
             continue
-        key, rhs = m.group(1), m.group(2)
+        key, rhs = kv
         if rhs is None:
             yield key, None, False
             continue
@@ -76,15 +107,7 @@ def dotenv_values(path: str, environ: Optional[Dict[str, str]] = None) -> Dict[s
     values: Dict[str, Optional[str]] = {}
     for key, val, expand in parse_dotenv(text):
         if val is not None and expand and "${" in val:
-            def sub(m: "re.Match[str]") -> str:
-                name = m.group(1)
-                got = env.get(name)
-                if got is None:
-                    got = values.get(name)
-                if got is None or got == "":
-                    return m.group(2) or ""
-                return got
-            val = _EXPAND.sub(sub, val)
+            val = _expand(val, lambda name: env.get(name) if env.get(name) is not None else values.get(name))
         values[key] = val
     return values
 
