@@ -8,18 +8,27 @@ server sent ``Retry-After`` (seconds or an HTTP date), which wins (capped).
 
 from __future__ import annotations
 
-import random
 import time
-from typing import Optional
+from typing import TYPE_CHECKING, Optional
+
+if TYPE_CHECKING:  # `random` costs a few ms of import time; only a real backoff needs it
+    import random
 
 
 class Backoff:
     def __init__(self, base: float = 0.25, cap: float = 30.0, jitter: float = 0.5,
-                 rng: Optional[random.Random] = None):
+                 rng: "Optional[random.Random]" = None):
         self.base = max(0.0, base)
         self.cap = max(0.0, cap)
         self.jitter = min(max(jitter, 0.0), 1.0)
-        self.rng = rng or random.Random()
+        self._rng = rng  # seeded lazily: os.urandom seeding costs ~30 us and most checks never back off
+
+    @property
+    def rng(self) -> "random.Random":
+        if self._rng is None:
+            import random
+            self._rng = random.Random()
+        return self._rng
 
     def delay(self, attempt: int, retry_after: Optional[str] = None) -> float:
         ra = parse_retry_after(retry_after)

@@ -68,6 +68,21 @@ def _pool_name(scheme: str, host: str, port: int) -> str:
     return f"{pool}(host='{host}', port={port})"
 
 
+def _connect(target: Tuple[Optional[str], int], timeout: float) -> socket.socket:
+    """``socket.create_connection`` without the ``getaddrinfo`` round for IPv4 literals."""
+    host, port = target
+    if host and host.count(".") == 3 and host.replace(".", "").isdigit():
+        sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        try:
+            sock.settimeout(timeout)
+            sock.connect((host, port))
+            return sock
+        except BaseException:
+            sock.close()
+            raise
+    return socket.create_connection((host, port), timeout=timeout)
+
+
 class Connection:
     """One persistent HTTP/1.1 connection to ``scheme://host:port``."""
 
@@ -113,7 +128,7 @@ class Connection:
             return
         target = (self.proxy.hostname, self.proxy.port or 80) if self.proxy else (self.host, self.port)
         try:
-            sock = socket.create_connection(target, timeout=self.timeout)
+            sock = _connect(target, self.timeout)
         except socket.timeout as e:
             raise self._fail("connect_timeout", url, e)
         except socket.gaierror as e:
