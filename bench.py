@@ -52,6 +52,20 @@ def _spawn(module: str, *args: str) -> "tuple[subprocess.Popen, dict]":
     return proc, json.loads(line)
 
 
+def _own_gpu(gpus, local_rank, cuda):
+    """amd-smi sees every GPU of the host; keep the one this rank drives (matched by PCI address)."""
+    if len(gpus) <= 1:
+        return gpus
+    mine = []
+    if cuda:
+        from k8s_gpu_node_checker_amd.ops import diag
+        bdf = diag.device_info(local_rank)["bdf"].lower()
+        mine = [g for g in gpus if str(g.get("bdf", "")).lower() == bdf]
+    mine = mine or [g for g in gpus if g.get("index") == local_rank] or gpus[:1]
+    mine = [dict(mine[0], index=0)]
+    return mine
+
+
 def _pctl(xs, q):
     xs = sorted(xs)
     if not xs:
@@ -148,10 +162,7 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
         rep = fixtures.mi355x_probe_report(node, gpus=1)
         probe_source = "fixture"
     else:
-        gpus = rep["gpus"]
-        if len(gpus) > 1:  # amd-smi sees every GPU of the host: keep this rank's
-            rep["gpus"] = [g for g in gpus if g.get("index") == local_rank] or gpus[:1]
-            rep["gpus"][0]["index"] = 0
+        rep["gpus"] = _own_gpu(rep["gpus"], local_rank, cuda)
     probe_ms = (time.perf_counter() - t0) * 1e3
     with KubeClient(cluster) as kc:
         agent.publish(kc, rep)  # AMDGPUHealthy NodeCondition + full report annotation
@@ -167,8 +178,8 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
     def step():
         if args.mode == "sweep":
             r = agent.probe_once() if probe_source != "fixture" else fixtures.mi355x_probe_report(node, gpus=1)
-            if len(r.get("gpus") or []) > 1:
-                r["gpus"] = [g for g in r["gpus"] if g.get("index") == local_rank] or r["gpus"][:1]
+            if probe_source != "fixture":
+                r["gpus"] = _own_gpu(r["gpus"], local_rank, cuda)
             with KubeClient(cluster) as kc2:
                 agent.publish(kc2, r)
             barrier()

@@ -56,7 +56,18 @@ class Agent:
             return self._diag_cache
         from ..ops import diag
         devices = self.devices if self.devices is not None else list(range(min(n_gpus, diag.device_count())))
-        self._diag_cache = {d: diag.run(self.diag_level, d) for d in devices}
+        # one host thread per GPU: each diagnostic is a ctypes call that releases the GIL and drives its
+        # own device, so an 8-GPU node is checked in the time of one GPU instead of eight
+        results: Dict[int, Dict[str, Any]] = {}
+
+        def work(d: int) -> None:
+            results[d] = diag.run(self.diag_level, d)
+        threads = [threading.Thread(target=work, args=(d,), name=f"diag-gpu{d}") for d in devices]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        self._diag_cache = {d: results[d] for d in devices if d in results}
         self._diag_ts = now
         return self._diag_cache
 
@@ -64,10 +75,19 @@ class Agent:
         from ..ops.amdsmi_probe import probe
         rep = probe(self.node, self.source, self.fixture)
         diags = self._diagnostics(len(rep.get("gpus") or []))
-        for g in rep.get("gpus") or []:
-            d = diags.get(g.get("index"))
-            if d:
-                g["diag"] = d
+        if diags:
+            # amd-smi and HIP enumerate independently: match by PCI address, fall back to the index
+            from ..ops import diag
+            by_bdf = {}
+            for d in diags:
+                try:
+                    by_bdf[diag.device_info(d)["bdf"].lower()] = d
+                except Exception:
+                    pass
+            for g in rep.get("gpus") or []:
+                d = by_bdf.get(str(g.get("bdf", "")).lower(), g.get("index") if not by_bdf else None)
+                if d is not None and diags.get(d):
+                    g["diag"] = diags[d]
         verdict = evaluate_report(rep, 0, HealthExpectations())
         rep["state"] = verdict.state
         with self.lock:

@@ -407,12 +407,13 @@ int diag_device_count(void) {
   return n;
 }
 
-// Device name / arch string ("gfx950:sramecc+:xnack-") into buf.
+// "arch|name|CUs|bytes|PCI BDF" of a HIP device (arch e.g. "gfx950:sramecc+:xnack-").
 int diag_device_arch(int device, char* buf, int len) {
   hipDeviceProp_t prop;
   DIAG_CHECK(hipGetDeviceProperties(&prop, device));
-  snprintf(buf, static_cast<size_t>(len), "%s|%s|%d|%zu", prop.gcnArchName, prop.name, prop.multiProcessorCount,
-           static_cast<size_t>(prop.totalGlobalMem));
+  snprintf(buf, static_cast<size_t>(len), "%s|%s|%d|%zu|%04x:%02x:%02x.0", prop.gcnArchName, prop.name,
+           prop.multiProcessorCount, static_cast<size_t>(prop.totalGlobalMem), prop.pciDomainID, prop.pciBusID,
+           prop.pciDeviceID);
   return 0;
 }
 

@@ -65,8 +65,8 @@ def device_count() -> int:
 def device_info(device: int = 0) -> Dict[str, Any]:
     buf = ctypes.create_string_buffer(512)
     _check(lib().diag_device_arch(device, buf, len(buf)))
-    arch, name, cus, mem = buf.value.decode().split("|")
-    return {"arch": arch, "name": name, "cus": int(cus), "mem_bytes": int(mem)}
+    arch, name, cus, mem, bdf = buf.value.decode().split("|")
+    return {"arch": arch, "name": name, "cus": int(cus), "mem_bytes": int(mem), "bdf": bdf}
 
 
 def gemm_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int, stream: int = 0) -> None:

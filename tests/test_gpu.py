@@ -147,3 +147,28 @@ def test_bench_contract_on_gpu(repo):
     d = json.loads(line)
     assert d["check_ok"] and d["n_gpus"] == 1 and d["value"] > 0
     assert d["probe"]["source"] == "native", d["probe"]
+
+
+def test_rccl_collective_single_rank(repo):
+    """The RCCL (backend nccl) path of the xGMI diagnostic runs end to end on the GPU (world size 1 here;
+    the 8-GPU hive runs it with --nproc-per-node 8)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "-m", "k8s_gpu_node_checker_amd.parallel.collectives",
+           "--sizes", "1M,64M", "--iters", "5", "--warmup", "2"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["backend"] == "nccl" and d["pass"] and all(r["correct"] for r in d["rows"])
+
+
+def test_agent_diagnostics_threads_per_device(dev):
+    from k8s_gpu_node_checker_amd.agent.agent import Agent
+    from k8s_gpu_node_checker_amd.ops import diag
+    ag = Agent("n", source="native", diag_level=1)
+    rep = ag.probe_once()
+    assert len(rep["gpus"]) >= 1
+    assert all("diag" in g for g in rep["gpus"][: diag.device_count()])
