@@ -32,6 +32,28 @@ from .config import ClusterConnection
 from .errors import ApiException, TransportError
 
 USER_AGENT = "k8s-gpu-node-checker-amd/0.1 (MI355X)"
+
+
+def _continue_from_prefix(prefix: bytes) -> Optional[str]:
+    """``metadata.continue`` from the head of a NodeList body, if it precedes ``items``.
+
+    Only the unescaped form apiservers emit is accepted (opaque base64 tokens);
+    anything else returns ``None`` and pagination simply is not pipelined.
+    """
+    i = prefix.find(b'"continue"')
+    if i < 0:
+        return None
+    items = prefix.find(b'"items"')
+    if 0 <= items < i:
+        return None
+    j = prefix.find(b'"', prefix.find(b":", i + 10) + 1)
+    if j < 0:
+        return None
+    k = prefix.find(b'"', j + 1)
+    if k < 0 or b"\\" in prefix[j:k]:
+        return None
+    tok = prefix[j + 1:k]
+    return tok.decode("ascii", "strict") if tok and tok.isascii() else None
 _RETRY_STATUS = frozenset((429, 500, 502, 503, 504))
 _LOOPBACK = ("127.", "localhost", "::1", "[::1]")
 
@@ -39,7 +61,7 @@ _LOOPBACK = ("127.", "localhost", "::1", "[::1]")
 class KubeClient:
     def __init__(self, cluster: ClusterConnection, timeout: float = 30.0, retries: int = 2,
                  backoff: Optional[Backoff] = None, gzip: Optional[bool] = None,
-                 sleep=time.sleep, tracer=None):
+                 sleep=time.sleep, tracer=None, pipeline: bool = True):
         self.cluster = cluster
         self.timeout = timeout
         self.retries = max(0, retries)
@@ -47,6 +69,8 @@ class KubeClient:
         self.sleep = sleep
         self.tracer = tracer
         self._conn: Optional[Connection] = None
+        self._conn2: Optional[Connection] = None
+        self.pipeline = pipeline
         host = cluster.server.split("://", 1)[-1]
         self.gzip = (not host.startswith(_LOOPBACK)) if gzip is None else gzip
         self.requests_made = 0
@@ -61,9 +85,10 @@ class KubeClient:
         return self._conn
 
     def close(self) -> None:
-        if self._conn is not None:
-            self._conn.close()
-            self._conn = None
+        for c in (self._conn, self._conn2):
+            if c is not None:
+                c.close()
+        self._conn = self._conn2 = None
 
     def __enter__(self) -> "KubeClient":
         return self
@@ -71,20 +96,24 @@ class KubeClient:
     def __exit__(self, *exc: Any) -> None:
         self.close()
 
-    def request(self, method: str, path: str, body: Optional[bytes] = None,
-                content_type: Optional[str] = None, idempotent: bool = True) -> Response:
+    def _headers(self, content_type: Optional[str] = None) -> Dict[str, str]:
         headers = {"Accept": "application/json", "User-Agent": USER_AGENT}
         headers.update(self.cluster.auth_headers())
         if self.gzip:
             headers["Accept-Encoding"] = "gzip"
         if content_type:
             headers["Content-Type"] = content_type
+        return headers
+
+    def request(self, method: str, path: str, body: Optional[bytes] = None,
+                content_type: Optional[str] = None, idempotent: bool = True, peek=None) -> Response:
+        headers = self._headers(content_type)
         attempt = 0
         while True:
             conn = self._connection()
             self.requests_made += 1
             try:
-                resp = conn.request(method, path, headers, body)
+                resp = conn.request(method, path, headers, body, peek)
             except HTTPError as e:
                 if idempotent and attempt < self.retries and e.kind != "tls":
                     self.sleep(self.backoff.delay(attempt))
@@ -121,10 +150,31 @@ class KubeClient:
         from ..ops import fastpath
         result = ScanResult()
         cont: Optional[str] = None
+        prefetched: Dict[str, Connection] = {}  # next-page path -> connection its request was sent on
+
+        def peek(prefix: bytes) -> None:
+            # NodeList JSON carries metadata.continue *before* items: as soon as the head of page k
+            # arrives, request page k+1 on a second connection, so the server produces (and the
+            # kernel buffers) it while page k is still being received and scanned
+            if not self.pipeline or prefetched:
+                return
+            token = _continue_from_prefix(prefix)
+            if token is None:
+                return
+            nxt = self._list_path(limit, token, label_selector, resource_version)
+            conn2 = self._spare_connection()
+            try:
+                conn2.send_only("GET", nxt, self._headers())
+            except HTTPError:
+                return
+            prefetched[nxt] = conn2
+
         while True:
             path = self._list_path(limit, cont, label_selector, resource_version)
             try:
-                resp = self.request("GET", path)
+                resp = self._take_prefetched(prefetched, path)
+                if resp is None:
+                    resp = self.request("GET", path, peek=peek if limit > 0 else None)
             except ApiException as e:
                 if e.status == 410 and cont:
                     # continue token expired mid-list: restart as one consistent full LIST
@@ -139,6 +189,33 @@ class KubeClient:
                 self.tracer.add("parse", time.perf_counter() - t0)
             if not cont or limit <= 0:
                 return result
+
+    # -- pipelined pagination helpers ------------------------------------------
+    def _spare_connection(self) -> Connection:
+        if self._conn2 is None:
+            ctx = self.cluster.ssl_context() if self.cluster.server.startswith("https") else None
+            self._conn2 = Connection(self.cluster.server, timeout=self.timeout, ssl_context=ctx,
+                                     server_hostname=self.cluster.tls_server_name, proxy_url=self.cluster.proxy_url)
+        return self._conn2
+
+    def _take_prefetched(self, prefetched: Dict[str, Connection], path: str) -> Optional[Response]:
+        """Read the already-sent request for ``path``; swap it in as the primary connection."""
+        conn2 = prefetched.pop(path, None)
+        prefetched.clear()
+        if conn2 is None:
+            return None
+        self.requests_made += 1
+        try:
+            resp = conn2.read_pending("GET", path)
+        except HTTPError:
+            return None  # fall back to a normal (retried) request
+        # alternate: the connection that just answered becomes primary, the old primary the spare
+        self._conn, self._conn2 = conn2, self._conn
+        if 200 <= resp.status < 300:
+            return resp
+        if resp.status in _RETRY_STATUS:
+            return None  # retried through request() with backoff
+        raise ApiException(resp.status, resp.reason, resp.header_dict(), resp.text)
 
     def get_node(self, name: str) -> Dict[str, Any]:
         return json.loads(self.request("GET", "/api/v1/nodes/" + quote(name, safe="")).body)

@@ -18,7 +18,8 @@ import os
 import sys
 from typing import Dict, Optional
 
-NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
+NATIVE_DIR = os.environ.get("K8SGPU_NATIVE_DIR") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
 
 _cache: Dict[str, object] = {}
 

@@ -220,27 +220,57 @@ class Connection:
                 raise HTTPError("aborted", "('Connection aborted.', RemoteDisconnected("
                                            "'Remote end closed connection without response'))")
 
-    def request(self, method: str, path: str, headers: Optional[Dict[str, str]] = None,
-                body: Optional[bytes] = None) -> Response:
-        url = path
+    def _encode(self, method: str, path: str, headers: Optional[Dict[str, str]], body: Optional[bytes]) -> bytes:
         req_target = self.base_path + path
         if self.proxy and self.scheme == "http":
             req_target = f"http://{self.host_header}{req_target}"
         lines = [f"{method} {req_target} HTTP/1.1", f"Host: {self.host_header}"]
-        hdrs = headers or {}
-        for k, v in hdrs.items():
+        for k, v in (headers or {}).items():
             lines.append(f"{k}: {v}")
         if body is not None:
             lines.append(f"Content-Length: {len(body)}")
         raw = ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
-        if body:
-            raw += body
+        return raw + body if body else raw
+
+    def send_only(self, method: str, path: str, headers: Optional[Dict[str, str]] = None,
+                  body: Optional[bytes] = None) -> None:
+        """Send a request now and read its response later with :meth:`read_pending` (pipelining)."""
+        try:
+            self.connect(path)
+            assert self.sock is not None
+            self.sock.sendall(self._encode(method, path, headers, body))
+        except HTTPError:
+            self.close()
+            raise
+        except OSError as e:
+            self.close()
+            raise self._fail("aborted", path, e)
+
+    def read_pending(self, method: str = "GET", path: str = "/", peek=None) -> Response:
+        try:
+            return self._read_response(method, peek)
+        except HTTPError:
+            self.close()
+            raise
+        except socket.timeout as e:
+            self.close()
+            raise self._fail("timeout", path, e)
+        except OSError as e:
+            self.close()
+            raise self._fail("reset" if isinstance(e, ConnectionResetError) else "aborted", path, e)
+
+    def request(self, method: str, path: str, headers: Optional[Dict[str, str]] = None,
+                body: Optional[bytes] = None, peek=None) -> Response:
+        """Send and read one request.  ``peek(prefix)`` is called once with the first bytes of the
+        (decoded) body before the rest is read -- the kube client uses it to pipeline pagination."""
+        url = path
+        raw = self._encode(method, path, headers, body)
         reused = self.sock is not None
         try:
             self.connect(url)
             assert self.sock is not None
             self.sock.sendall(raw)
-            return self._read_response(method)
+            return self._read_response(method, peek)
         except HTTPError as e:
             self.close()
             if reused and e.kind in ("aborted", "reset"):
@@ -248,7 +278,7 @@ class Connection:
                 self.connect(url)
                 assert self.sock is not None
                 self.sock.sendall(raw)
-                return self._read_response(method)
+                return self._read_response(method, peek)
             raise
         except socket.timeout as e:
             self.close()
@@ -265,7 +295,20 @@ class Connection:
                 raise self._fail("tls", url, e)
             raise self._fail("aborted", url, e)
 
-    def _read_response(self, method: str) -> Response:
+    def _peek_prefix(self, want: int, gz: bool, peek) -> None:
+        """Buffer up to ``want`` body bytes (Content-Length bodies) and hand them to ``peek``."""
+        while len(self._buf) < want and self._recv_more():
+            pass
+        prefix = bytes(self._buf[:want])
+        if gz:
+            import zlib
+            try:
+                prefix = zlib.decompressobj(16 + zlib.MAX_WBITS).decompress(prefix, 65536)
+            except zlib.error:
+                return
+        peek(prefix)
+
+    def _read_response(self, method: str, peek=None) -> Response:
         while True:
             status_line = self._read_line()
             parts = status_line.split(None, 2)
@@ -287,9 +330,13 @@ class Connection:
         if method == "HEAD" or status in (204, 304):
             body = b""
         elif "chunked" in hmap.get("transfer-encoding", "").lower():
-            body = self._read_chunked()
+            body = self._read_chunked(peek if 200 <= status < 300 else None,
+                                      hmap.get("content-encoding", "").lower() == "gzip")
         elif "content-length" in hmap:
-            body = self._read_exact(int(hmap["content-length"]))
+            n = int(hmap["content-length"])
+            if peek is not None and 200 <= status < 300 and n > 0:
+                self._peek_prefix(min(n, 4096), hmap.get("content-encoding", "").lower() == "gzip", peek)
+            body = self._read_exact(n)
         else:
             chunks = [bytes(self._buf)]
             self._buf = bytearray()
@@ -308,17 +355,32 @@ class Connection:
             self.close()
         return Response(status, reason, headers, body)
 
-    def _read_chunked(self) -> bytes:
+    def _read_chunked(self, peek=None, gz: bool = False) -> bytes:
         out = []
+        have = 0
         while True:
             size_line = self._read_line()
             size = int(size_line.split(b";", 1)[0].strip() or b"0", 16)
             if size == 0:
                 while self._read_line():  # trailers
                     pass
+                if peek is not None and out:
+                    peek(b"".join(out)[:4096] if not gz else b"")
                 return b"".join(out)
             out.append(self._read_exact(size))
+            have += size
             self._read_line()
+            if peek is not None and have >= 4096:
+                prefix = b"".join(out)[:65536]
+                if gz:
+                    import zlib
+                    try:
+                        prefix = zlib.decompressobj(16 + zlib.MAX_WBITS).decompress(prefix, 65536)
+                    except zlib.error:
+                        prefix = b""
+                if prefix:
+                    peek(prefix)
+                peek = None
 
 
 def request(url: str, method: str = "GET", headers: Optional[Dict[str, str]] = None, body: Optional[bytes] = None,

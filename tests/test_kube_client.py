@@ -174,3 +174,109 @@ def test_tls_insecure_skip_verify(certs):
         conn.insecure = True
         with KubeClient(conn) as c:
             assert len(c.scan_nodes().gpu_nodes) == 2
+
+
+@pytest.fixture(scope="module")
+def mtls(tmp_path_factory):
+    """A CA, a server cert and a client cert (openssl CLI)."""
+    d = tmp_path_factory.mktemp("mtls")
+
+    def run(*a):
+        r = subprocess.run(["openssl", *a], capture_output=True, cwd=str(d))
+        if r.returncode != 0:
+            pytest.skip("openssl failed: " + r.stderr.decode()[-200:])
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "ca.key", "-out", "ca.crt", "-days", "1",
+        "-subj", "/CN=test-ca")
+    for name, ext in (("srv", "subjectAltName=IP:127.0.0.1"), ("cli", "extendedKeyUsage=clientAuth")):
+        run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", f"{name}.key", "-out", f"{name}.csr", "-subj",
+            f"/CN={name}")
+        (d / f"{name}.ext").write_text(ext + "\n")
+        run("x509", "-req", "-in", f"{name}.csr", "-CA", "ca.crt", "-CAkey", "ca.key", "-CAcreateserial", "-out",
+            f"{name}.crt", "-days", "1", "-extfile", f"{name}.ext")
+    return d
+
+
+def test_mutual_tls_client_certificate_data(mtls, tmp_path):
+    """kubeconfig client-certificate-data/client-key-data + certificate-authority-data against an mTLS server."""
+    import base64
+    import ssl
+    import yaml
+    from k8s_gpu_node_checker_amd.kube.config import load_kube_config
+    srv = MockApiServer(fixtures.cluster(2, "amd"), certfile=str(mtls / "srv.crt"), keyfile=str(mtls / "srv.key"))
+    ctx = srv.socket.context
+    ctx.verify_mode = ssl.CERT_REQUIRED
+    ctx.load_verify_locations(str(mtls / "ca.crt"))
+    with srv:
+        b64 = lambda f: base64.b64encode((mtls / f).read_bytes()).decode()
+        cfg = {"apiVersion": "v1", "kind": "Config", "current-context": "m",
+               "clusters": [{"name": "m", "cluster": {"server": srv.url, "certificate-authority-data": b64("ca.crt")}}],
+               "contexts": [{"name": "m", "context": {"cluster": "m", "user": "u"}}],
+               "users": [{"name": "u", "user": {"client-certificate-data": b64("cli.crt"),
+                                                "client-key-data": b64("cli.key")}}]}
+        kc = tmp_path / "kc.yaml"
+        kc.write_text(yaml.safe_dump(cfg))
+        with KubeClient(load_kube_config(str(kc))) as c:
+            assert len(c.scan_nodes().gpu_nodes) == 2
+        cfg["users"][0]["user"] = {}  # no client cert: the handshake must fail
+        kc.write_text(yaml.safe_dump(cfg))
+        with pytest.raises(TransportError):
+            KubeClient(load_kube_config(str(kc)), retries=0).scan_nodes()
+
+
+def test_https_through_connect_proxy(certs, tmp_path):
+    """cluster.proxy-url: HTTPS to the apiserver tunnelled through an HTTP CONNECT proxy."""
+    import select
+    import socket
+    import socketserver
+    import threading
+    seen = []
+
+    class Proxy(socketserver.BaseRequestHandler):
+        def handle(self):
+            data = b""
+            while b"\r\n\r\n" not in data:
+                data += self.request.recv(4096)
+            line = data.split(b"\r\n", 1)[0].decode()
+            seen.append(line)
+            host, port = line.split()[1].rsplit(":", 1)
+            up = socket.create_connection((host, int(port)))
+            self.request.sendall(b"HTTP/1.1 200 Connection established\r\n\r\n")
+            socks = [self.request, up]
+            while True:
+                r, _, _ = select.select(socks, [], [], 5)
+                if not r:
+                    break
+                for s in r:
+                    chunk = s.recv(65536)
+                    if not chunk:
+                        up.close()
+                        return
+                    (up if s is self.request else self.request).sendall(chunk)
+
+    class PS(socketserver.ThreadingTCPServer):
+        daemon_threads = True
+        allow_reuse_address = True
+    proxy = PS(("127.0.0.1", 0), Proxy)
+    threading.Thread(target=proxy.serve_forever, daemon=True).start()
+    crt, key = certs
+    try:
+        with MockApiServer(fixtures.cluster(3, "amd"), certfile=crt, keyfile=key) as srv:
+            conn = ClusterConnection(srv.url)
+            conn.ca_file = crt
+            conn.proxy_url = f"http://127.0.0.1:{proxy.server_address[1]}"
+            with KubeClient(conn) as c:
+                assert len(c.scan_nodes().gpu_nodes) == 3
+        assert seen and seen[0].startswith("CONNECT 127.0.0.1:")
+    finally:
+        proxy.shutdown()
+
+
+def test_pipelined_pagination_uses_two_connections(mock_cluster):
+    nodes = fixtures.cluster(30, "mixed", not_ready=[7])
+    srv = mock_cluster(nodes)
+    with client(srv) as c:
+        res = c.scan_nodes(limit=4)
+        assert c._conn2 is not None  # the next page was requested while the previous one was read
+    assert names(res) == names(scan_items(nodes)) and res.items_seen == 30
+    with KubeClient(ClusterConnection(srv.url), pipeline=False) as c:
+        assert names(c.scan_nodes(limit=4)) == names(res) and c._conn2 is None
