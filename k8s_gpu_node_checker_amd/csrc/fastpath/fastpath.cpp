@@ -27,12 +27,13 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
-#include <emmintrin.h>
+#include <immintrin.h>
 
 #include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <new>
 #include <vector>
 
 namespace {
@@ -251,9 +252,7 @@ void skip_literal(Cursor& c) {
 
 // Skip a whole object/array with a flat bracket counter (string-aware), 16 bytes per step:
 // only '"', '{', '}', '[' and ']' stop the vector scan; strings are jumped over whole.
-void skip_container(Cursor& c) {
-  const char* p = c.p;
-  const char* e = c.end;
+const char* skip_container_sse2(const char* p, const char* e) {
   int depth = 0;
   const __m128i vq = _mm_set1_epi8('"'), vo = _mm_set1_epi8('{'), vc = _mm_set1_epi8('}');
   const __m128i vl = _mm_set1_epi8('['), vr = _mm_set1_epi8(']');
@@ -285,12 +284,83 @@ void skip_container(Cursor& c) {
     if (ch == '{' || ch == '[') {
       ++depth;
     } else if (--depth == 0) {
-      c.p = hit + 1;
-      return;
+      return hit + 1;
     }
     p = hit + 1;
   }
-  throw Fallback{"unterminated container"};
+  return nullptr;
+}
+
+// 64 bytes per step, branch-free string tracking (the simdjson stage-1 idea, written for this
+// scanner): backslash runs -> escaped characters, unescaped quotes -> in-string mask via a carry-less
+// prefix XOR, then only brackets outside strings are counted.  AVX2 + PCLMUL (runtime-dispatched).
+__attribute__((target("avx2,pclmul,popcnt,bmi")))
+inline uint64_t eq_mask64(const __m256i lo, const __m256i hi, char ch) {
+  const __m256i v = _mm256_set1_epi8(ch);
+  const uint32_t a = static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(lo, v)));
+  const uint32_t b = static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(hi, v)));
+  return static_cast<uint64_t>(a) | (static_cast<uint64_t>(b) << 32);
+}
+
+__attribute__((target("avx2,pclmul,popcnt,bmi")))
+const char* skip_container_avx2(const char* p, const char* e) {
+  int64_t depth = 0;
+  uint64_t prev_escaped = 0, prev_in_string = 0;
+  const uint64_t even = 0x5555555555555555ULL;
+  alignas(32) char tail[64];
+  for (const char* base = p; base < e; base += 64) {
+    const char* src = base;
+    if (e - base < 64) {
+      memset(tail, ' ', sizeof tail);
+      memcpy(tail, base, static_cast<size_t>(e - base));
+      src = tail;
+    }
+    const __m256i lo = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src));
+    const __m256i hi = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 32));
+    uint64_t bs = eq_mask64(lo, hi, '\\');
+    uint64_t quotes = eq_mask64(lo, hi, '"');
+    // characters escaped by an odd-length backslash run
+    bs &= ~prev_escaped;
+    const uint64_t follows = (bs << 1) | prev_escaped;
+    const uint64_t odd_starts = bs & ~even & ~follows;
+    uint64_t even_starts;
+    prev_escaped = __builtin_add_overflow(odd_starts, bs, &even_starts) ? 1 : 0;
+    const uint64_t escaped = (even ^ (even_starts << 1)) & follows;
+    quotes &= ~escaped;
+    const uint64_t in_str =
+        static_cast<uint64_t>(_mm_cvtsi128_si64(_mm_clmulepi64_si128(_mm_set_epi64x(0, static_cast<long long>(quotes)),
+                                                                     _mm_set1_epi8(static_cast<char>(0xFF)), 0))) ^
+        prev_in_string;
+    prev_in_string = static_cast<uint64_t>(static_cast<int64_t>(in_str) >> 63);
+    const uint64_t opens = (eq_mask64(lo, hi, '{') | eq_mask64(lo, hi, '[')) & ~in_str;
+    const uint64_t closes = (eq_mask64(lo, hi, '}') | eq_mask64(lo, hi, ']')) & ~in_str;
+    const int nc = __builtin_popcountll(closes);
+    if (depth > nc) {  // cannot reach depth 0 inside this block
+      depth += __builtin_popcountll(opens) - nc;
+      continue;
+    }
+    uint64_t st = opens | closes;
+    while (st) {
+      const int i = __builtin_ctzll(st);
+      if ((opens >> i) & 1) {
+        ++depth;
+      } else if (--depth == 0) {
+        const char* hit = base + i;
+        return hit < e ? hit + 1 : nullptr;
+      }
+      st &= st - 1;
+    }
+  }
+  return nullptr;
+}
+
+const bool g_have_avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("pclmul") &&
+                         __builtin_cpu_supports("popcnt") && __builtin_cpu_supports("bmi");
+
+void skip_container(Cursor& c) {
+  const char* end = g_have_avx2 ? skip_container_avx2(c.p, c.end) : skip_container_sse2(c.p, c.end);
+  if (!end) throw Fallback{"unterminated container"};
+  c.p = end;
 }
 
 void skip_value(Cursor& c) {
@@ -370,112 +440,64 @@ struct Ref {
   }
 };
 
-struct KeySpec {
-  std::vector<std::string> keys;  // registry order
-  std::vector<PyObject*> pykeys;  // borrowed from the keys tuple
+// ---------------------------------------------------------------------------
+// Two passes per page:
+//   pass 1 (GIL released): walk the bytes, validate the shapes this code models,
+//          record spans of the fields the checker needs (NodeRec) -- no Python objects;
+//   pass 2 (GIL held): for GPU nodes only, materialise dicts/strings/ints from the spans.
+// Pass 1 is most of the byte work, so another thread (the kube client's reader of the
+// next page) runs concurrently with it.
+
+enum class QKind : uint8_t { Unset, Str, Num, Other };
+
+// One capacity / allocatable entry as it appeared last (json.loads: last duplicate wins).
+struct QRaw {
+  QKind kind = QKind::Unset;
+  RawStr s{nullptr, nullptr, false};  // Str: the string token; Num: the number text
 };
 
-// Value of a capacity entry -> (present, parsed ok, value) with str()+int() semantics.
-struct Qty {
-  bool set = false;   // key present with a non-null value (last one wins)
-  bool ok = false;    // int() succeeded
-  Ref value;          // PyLong
+enum class VKind : uint8_t { Absent, Null, Str };
+struct SRaw {  // an optional string-or-null field
+  VKind kind = VKind::Absent;
+  RawStr s{nullptr, nullptr, false};
 };
 
-PyObject* parse_int_text(const char* b, size_t n, std::string& scratch, bool is_json_string) {
-  // Fast path: optional sign + ASCII digits, nothing else.
-  const char* p = b;
-  const char* e = b + n;
-  if (is_json_string) {
-    if (n == 0) return nullptr;  // "" -> skipped, handled by caller
-  }
-  const char* q = p;
-  if (q < e && (*q == '+' || *q == '-')) ++q;
-  bool simple = q < e && (e - q) <= 18;
-  for (const char* r = q; simple && r < e; ++r)
-    if (*r < '0' || *r > '9') simple = false;
-  if (simple) {
-    long long v = 0;
-    for (const char* r = q; r < e; ++r) v = v * 10 + (*r - '0');
-    if (*p == '-') v = -v;
-    return PyLong_FromLongLong(v);
-  }
-  // Exact Python int(str) semantics (whitespace, '_' separators, unicode digits).
-  scratch.assign(b, n);
-  PyObject* s = PyUnicode_DecodeUTF8(scratch.data(), static_cast<Py_ssize_t>(scratch.size()), "strict");
-  if (!s) {
-    PyErr_Clear();
-    throw Fallback{"invalid utf-8 in quantity"};
-  }
-  PyObject* v = PyLong_FromUnicodeObject(s, 10);
-  Py_DECREF(s);
-  if (!v) {
-    if (PyErr_ExceptionMatches(PyExc_ValueError)) {
-      PyErr_Clear();
-      return nullptr;  // dropped, as the reference's `except Exception: pass`
-    }
-    PyErr_Clear();
-    throw Fallback{"int() raised"};
-  }
-  return v;
-}
+struct Span {
+  const char* b = nullptr;
+  const char* e = nullptr;
+};
 
-void parse_quantity(Cursor& c, Qty& q, std::string& scratch) {
-  char ch = c.peek();
-  q.ok = false;
-  q.value.reset(nullptr);
-  if (ch == 'n') {  // null -> key treated as missing
-    skip_literal(c);
-    q.set = false;
-    return;
-  }
-  q.set = true;
-  if (ch == '"') {
-    RawStr s = read_raw_string(c);
-    std::string dec;
-    const char* b = s.b;
-    size_t n = static_cast<size_t>(s.e - s.b);
-    if (s.esc) {
-      decode_into(s, dec);
-      b = dec.data();
-      n = dec.size();
-    }
-    if (n == 0) {  // `if not val: continue`
-      q.set = false;
-      return;
-    }
-    PyObject* v = parse_int_text(b, n, scratch, true);
-    if (v) {
-      q.ok = true;
-      q.value.reset(v);
-    }
-    return;
-  }
-  if (ch == '-' || (ch >= '0' && ch <= '9')) {
-    const char* b = c.p;
-    skip_number(c);
-    size_t n = static_cast<size_t>(c.p - b);
-    bool integral = true;
-    for (size_t i = 0; i < n; ++i)
-      if (b[i] == '.' || b[i] == 'e' || b[i] == 'E' || b[i] == 'I') integral = false;
-    if (!integral) return;  // str(float) is never int()-parsable
-    PyObject* v = parse_int_text(b, n, scratch, false);
-    if (v) {
-      q.ok = true;
-      q.value.reset(v);
-    }
-    return;
-  }
-  skip_value(c);  // bools, objects, arrays: str() of them never parses as int
-}
+struct NodeRec {
+  bool is_obj = false;
+  bool meta_obj = false;
+  SRaw name;
+  bool labels_obj = false;  // labels present as an object (possibly empty)
+  Span labels;
+  bool have_health = false;
+  RawStr health_raw{nullptr, nullptr, false};
+  bool taints_list = false;
+  Span taints;
+  bool unschedulable = false;
+  bool ready = false;
+  bool have_ip = false;
+  RawStr ip{nullptr, nullptr, false};
+  bool have_hc = false;  // AMDGPUHealthy condition
+  SRaw hc_status, hc_reason, hc_message;
+  bool hc_have_hb = false;
+  double hc_hb = 0.0;
+  std::vector<QRaw> cap, alloc;
+};
 
-// capacity / allocatable object -> per-registry-key Qty
-void parse_resource_map(Cursor& c, const KeySpec& ks, std::vector<Qty>& out, std::string& scratch) {
-  for (auto& q : out) {
-    q.set = false;
-    q.ok = false;
-    q.value.reset(nullptr);
-  }
+struct Pass1Ctx {
+  size_t nkeys;
+  const std::vector<std::string>* keys;
+  const std::string* health_key;
+  const std::string* health_cond;
+  std::string scratch;
+};
+
+void p1_resource_map(Cursor& c, Pass1Ctx& x, std::vector<QRaw>& out) {
+  for (auto& q : out) q = QRaw{};
   if (c.peek() != '{') {
     skip_value(c);
     return;
@@ -489,9 +511,26 @@ void parse_resource_map(Cursor& c, const KeySpec& ks, std::vector<Qty>& out, std
       kb = kd.data();
       kn = kd.size();
     }
-    for (size_t i = 0; i < ks.keys.size(); ++i) {
-      if (ks.keys[i].size() == kn && memcmp(ks.keys[i].data(), kb, kn) == 0) {
-        parse_quantity(cc, out[i], scratch);
+    for (size_t i = 0; i < x.nkeys; ++i) {
+      const std::string& key = (*x.keys)[i];
+      if (key.size() == kn && memcmp(key.data(), kb, kn) == 0) {
+        QRaw& q = out[i];
+        char ch = cc.peek();
+        if (ch == 'n') {  // null -> key treated as missing
+          skip_literal(cc);
+          q = QRaw{};
+        } else if (ch == '"') {
+          q.kind = QKind::Str;
+          q.s = read_raw_string(cc);
+        } else if (ch == '-' || (ch >= '0' && ch <= '9')) {
+          q.kind = QKind::Num;
+          const char* b = cc.p;
+          skip_number(cc);
+          q.s = RawStr{b, cc.p, false};
+        } else {
+          q.kind = QKind::Other;  // bools, objects, arrays: str() of them never parses as int
+          skip_value(cc);
+        }
         return;
       }
     }
@@ -499,94 +538,61 @@ void parse_resource_map(Cursor& c, const KeySpec& ks, std::vector<Qty>& out, std
   });
 }
 
-PyObject* breakdown_dict(const KeySpec& ks, const std::vector<Qty>& q, long long* total) {
-  PyObject* d = PyDict_New();
-  if (!d) throw Fallback{"oom"};
-  long long sum = 0;
-  bool overflow = false;
-  for (size_t i = 0; i < ks.keys.size(); ++i) {
-    if (q[i].set && q[i].ok) {
-      if (PyDict_SetItem(d, ks.pykeys[i], q[i].value.o) < 0) {
-        Py_DECREF(d);
-        throw Fallback{"dict"};
-      }
-      int of = 0;
-      long long v = PyLong_AsLongLongAndOverflow(q[i].value.o, &of);
-      if (of) overflow = true;
-      sum += v;
-    }
-  }
-  if (overflow) {
-    Py_DECREF(d);
-    throw Fallback{"huge quantity"};
-  }
-  if (total) *total = sum;
-  return d;
-}
-
-struct NodeScan {
-  bool meta_obj = false;     // metadata is a JSON object
-  Ref name;                  // str or None
-  Ref labels;                // dict (possibly empty) or null
-  RawStr health_raw{nullptr, nullptr, false};  // annotation value, decoded only if needed
-  bool have_health = false;
-  Ref taints;                // list
-  Ref internal_ip;           // str or nullptr (first InternalIP of status.addresses)
-  Ref health_cond;           // (status, reason, message, heartbeat) tuple of the health condition, or nullptr
-  bool unschedulable = false;
-  bool ready = false;
-  std::vector<Qty> cap, alloc;
-};
-
-void parse_labels(Cursor& c, NodeScan& ns, std::string& scratch) {
+// validate a labels object: string keys -> string values (else the Python path decides)
+void p1_labels(Cursor& c, NodeRec& r) {
   if (is_null(c)) {
-    ns.labels.reset(nullptr);
+    r.labels_obj = false;
     return;
   }
   if (c.peek() != '{') throw Fallback{"labels not an object"};
-  PyObject* d = PyDict_New();
-  if (!d) throw Fallback{"oom"};
-  Ref hold(d);
-  for_members(c, [&](const RawStr& k, Cursor& cc) {
-    Ref key(make_str(k, scratch));
+  const char* b = c.p;
+  for_members(c, [&](const RawStr&, Cursor& cc) {
     if (cc.peek() != '"') throw Fallback{"label value not a string"};
-    Ref val(make_str(read_raw_string(cc), scratch));
-    if (PyDict_SetItem(d, key.o, val.o) < 0) throw Fallback{"dict"};
+    read_raw_string(cc);
   });
-  ns.labels.reset(hold.release());
+  r.labels_obj = true;
+  r.labels = Span{b, c.p};
 }
 
-void parse_metadata(Cursor& c, NodeScan& ns, const std::string& health_key, std::string& scratch) {
-  ns.name.reset(nullptr);
-  ns.labels.reset(nullptr);
-  ns.have_health = false;
-  ns.meta_obj = false;
+SRaw p1_str_or_null(Cursor& c, const char* what) {
+  SRaw v;
+  if (is_null(c)) {
+    v.kind = VKind::Null;
+  } else if (c.peek() == '"') {
+    v.kind = VKind::Str;
+    v.s = read_raw_string(c);
+  } else {
+    throw Fallback{what};
+  }
+  return v;
+}
+
+void p1_metadata(Cursor& c, Pass1Ctx& x, NodeRec& r) {
+  r.name = SRaw{};
+  r.labels_obj = false;
+  r.have_health = false;
+  r.meta_obj = false;
   if (c.peek() != '{') {
     skip_value(c);  // null or a non-object: name "" / labels {} (models/node.py)
     return;
   }
-  ns.meta_obj = true;
+  r.meta_obj = true;
+  std::string& scratch = x.scratch;
   for_members(c, [&](const RawStr& k, Cursor& cc) {
     if (raw_equals(k, "name", scratch)) {
-      if (is_null(cc)) {
-        ns.name.reset(nullptr);
-      } else if (cc.peek() == '"') {
-        ns.name.reset(make_str(read_raw_string(cc), scratch));
-      } else {
-        throw Fallback{"name not a string"};
-      }
+      r.name = p1_str_or_null(cc, "name not a string");
     } else if (raw_equals(k, "labels", scratch)) {
-      parse_labels(cc, ns, scratch);
+      p1_labels(cc, r);
     } else if (raw_equals(k, "annotations", scratch)) {
-      ns.have_health = false;
+      r.have_health = false;
       if (cc.peek() != '{') {
         skip_value(cc);
         return;
       }
       for_members(cc, [&](const RawStr& ak, Cursor& c3) {
-        if (!health_key.empty() && raw_equals(ak, health_key.c_str(), scratch)) {
-          ns.have_health = c3.peek() == '"';
-          if (ns.have_health) ns.health_raw = read_raw_string(c3);
+        if (!x.health_key->empty() && raw_equals(ak, x.health_key->c_str(), scratch)) {
+          r.have_health = c3.peek() == '"';
+          if (r.have_health) r.health_raw = read_raw_string(c3);
           else skip_value(c3);
         } else {
           skip_value(c3);
@@ -598,55 +604,44 @@ void parse_metadata(Cursor& c, NodeScan& ns, const std::string& health_key, std:
   });
 }
 
-PyObject* taint_field(Cursor& c, std::string& scratch) {
-  if (is_null(c)) Py_RETURN_NONE;
-  if (c.peek() != '"') throw Fallback{"taint field not a string"};
-  return make_str(read_raw_string(c), scratch);
-}
-
-void parse_spec(Cursor& c, NodeScan& ns, std::string& scratch) {
-  ns.taints.reset(PyList_New(0));
-  ns.unschedulable = false;
-  if (!ns.taints.o) throw Fallback{"oom"};
+void p1_spec(Cursor& c, Pass1Ctx& x, NodeRec& r) {
+  r.taints_list = false;
+  r.unschedulable = false;
   if (c.peek() != '{') {
     skip_value(c);
     return;
   }
+  std::string& scratch = x.scratch;
   for_members(c, [&](const RawStr& k, Cursor& cc) {
     if (raw_equals(k, "taints", scratch)) {
-      ns.taints.reset(PyList_New(0));
-      if (!ns.taints.o) throw Fallback{"oom"};
+      r.taints_list = false;
       if (cc.peek() != '[') {
         skip_value(cc);
         return;
       }
+      const char* b = cc.p;
       for_elements(cc, [&](Cursor& c3) {
         if (c3.peek() != '{') {
           skip_value(c3);
           return;
         }
-        Ref tk(Py_NewRef(Py_None)), tv(Py_NewRef(Py_None)), te(Py_NewRef(Py_None));
         for_members(c3, [&](const RawStr& fk, Cursor& c4) {
-          if (raw_equals(fk, "key", scratch)) tk.reset(taint_field(c4, scratch));
-          else if (raw_equals(fk, "value", scratch)) tv.reset(taint_field(c4, scratch));
-          else if (raw_equals(fk, "effect", scratch)) te.reset(taint_field(c4, scratch));
-          else skip_value(c4);
+          if (raw_equals(fk, "key", scratch) || raw_equals(fk, "value", scratch) || raw_equals(fk, "effect", scratch))
+            p1_str_or_null(c4, "taint field not a string");
+          else
+            skip_value(c4);
         });
-        PyObject* d = PyDict_New();
-        if (!d) throw Fallback{"oom"};
-        Ref hd(d);
-        if (PyDict_SetItem(d, k_key, tk.o) < 0 || PyDict_SetItem(d, k_value, tv.o) < 0 ||
-            PyDict_SetItem(d, k_effect, te.o) < 0 || PyList_Append(ns.taints.o, d) < 0)
-          throw Fallback{"dict"};
       });
+      r.taints_list = true;
+      r.taints = Span{b, cc.p};
     } else if (raw_equals(k, "unschedulable", scratch)) {
       char ch = cc.peek();
       if (ch == 't') {
         skip_literal(cc);
-        ns.unschedulable = true;
+        r.unschedulable = true;
       } else if (ch == 'f' || ch == 'n') {
         skip_literal(cc);
-        ns.unschedulable = false;
+        r.unschedulable = false;
       } else {
         throw Fallback{"unschedulable not a bool"};
       }
@@ -683,34 +678,24 @@ double parse_k8s_time(const RawStr& s) {
   return static_cast<double>(days) * 86400.0 + hh * 3600.0 + mm * 60.0 + ss;
 }
 
-PyObject* cond_str_field(Cursor& c, std::string& scratch) {
-  if (is_null(c)) Py_RETURN_NONE;
-  if (c.peek() != '"') throw Fallback{"condition field not a string"};
-  return make_str(read_raw_string(c), scratch);
-}
-
-void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scratch,
-                  const std::string& health_cond) {
-  for (auto* v : {&ns.cap, &ns.alloc})
-    for (auto& q : *v) {
-      q.set = false;
-      q.ok = false;
-      q.value.reset(nullptr);
-    }
-  ns.ready = false;
-  ns.internal_ip.reset(nullptr);
-  ns.health_cond.reset(nullptr);
+void p1_status(Cursor& c, Pass1Ctx& x, NodeRec& r) {
+  for (auto* v : {&r.cap, &r.alloc})
+    for (auto& q : *v) q = QRaw{};
+  r.ready = false;
+  r.have_ip = false;
+  r.have_hc = false;
   if (c.peek() != '{') {
     skip_value(c);
     return;
   }
+  std::string& scratch = x.scratch;
   for_members(c, [&](const RawStr& k, Cursor& cc) {
     if (raw_equals(k, "capacity", scratch)) {
-      parse_resource_map(cc, ks, ns.cap, scratch);
+      p1_resource_map(cc, x, r.cap);
     } else if (raw_equals(k, "allocatable", scratch)) {
-      parse_resource_map(cc, ks, ns.alloc, scratch);
+      p1_resource_map(cc, x, r.alloc);
     } else if (raw_equals(k, "addresses", scratch)) {
-      ns.internal_ip.reset(nullptr);
+      r.have_ip = false;
       if (cc.peek() != '[') {
         skip_value(cc);
         return;
@@ -720,24 +705,28 @@ void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scrat
           skip_value(c3);
           return;
         }
-        bool internal = false;
-        Ref addr;
+        bool internal = false, have_addr = false;
+        RawStr addr{nullptr, nullptr, false};
         for_members(c3, [&](const RawStr& fk, Cursor& c4) {
           if (raw_equals(fk, "type", scratch) && c4.peek() == '"') {
             internal = raw_equals(read_raw_string(c4), "InternalIP", scratch);
           } else if (raw_equals(fk, "address", scratch) && c4.peek() == '"') {
-            addr.reset(make_str(read_raw_string(c4), scratch));
+            addr = read_raw_string(c4);
+            have_addr = true;
           } else {
             if (raw_equals(fk, "type", scratch)) internal = false;
-            if (raw_equals(fk, "address", scratch)) addr.reset(nullptr);
+            if (raw_equals(fk, "address", scratch)) have_addr = false;
             skip_value(c4);
           }
         });
-        if (internal && addr.o && !ns.internal_ip.o) ns.internal_ip.reset(addr.release());
+        if (internal && have_addr && !r.have_ip) {
+          r.have_ip = true;
+          r.ip = addr;
+        }
       });
     } else if (raw_equals(k, "conditions", scratch)) {
-      ns.ready = false;
-      ns.health_cond.reset(nullptr);
+      r.ready = false;
+      r.have_hc = false;
       if (cc.peek() != '[') {
         skip_value(cc);
         return;
@@ -747,8 +736,11 @@ void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scrat
           skip_value(c3);
           return;
         }
-        bool type_ready = false, status_true = false, type_health = false;
-        Ref st(Py_NewRef(Py_None)), reason(Py_NewRef(Py_None)), message(Py_NewRef(Py_None));
+        bool type_ready = false, status_true = false, type_health = false, status_bad = false;
+        SRaw st, reason, message;
+        st.kind = VKind::Null;
+        reason.kind = VKind::Null;
+        message.kind = VKind::Null;
         bool have_hb = false;
         double hb = 0.0;
         for_members(c3, [&](const RawStr& fk, Cursor& c4) {
@@ -759,26 +751,28 @@ void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scrat
             if (c4.peek() == '"') {
               RawStr v = read_raw_string(c4);
               type_ready = raw_equals(v, "Ready", scratch);
-              type_health = !health_cond.empty() && raw_equals(v, health_cond.c_str(), scratch);
+              type_health = !x.health_cond->empty() && raw_equals(v, x.health_cond->c_str(), scratch);
             } else {
               skip_value(c4);
             }
           } else if (is_status) {
             status_true = false;
+            status_bad = false;
             if (c4.peek() == '"') {
               RawStr v = read_raw_string(c4);
               status_true = raw_equals(v, "True", scratch);
-              st.reset(make_str(v, scratch));
+              st.kind = VKind::Str;
+              st.s = v;
             } else if (is_null(c4)) {
-              st.reset(Py_NewRef(Py_None));
+              st.kind = VKind::Null;
             } else {
-              st.reset(nullptr);  // non-string status: only matters for the health condition
+              status_bad = true;  // non-string status: only matters for the health condition
               skip_value(c4);
             }
           } else if (raw_equals(fk, "reason", scratch)) {
-            reason.reset(cond_str_field(c4, scratch));
+            reason = p1_str_or_null(c4, "condition field not a string");
           } else if (raw_equals(fk, "message", scratch)) {
-            message.reset(cond_str_field(c4, scratch));
+            message = p1_str_or_null(c4, "condition field not a string");
           } else if (raw_equals(fk, "lastHeartbeatTime", scratch)) {
             have_hb = false;
             if (c4.peek() == '"') {
@@ -791,19 +785,217 @@ void parse_status(Cursor& c, NodeScan& ns, const KeySpec& ks, std::string& scrat
             skip_value(c4);
           }
         });
-        if (type_ready && status_true) ns.ready = true;
+        if (type_ready && status_true) r.ready = true;
         if (type_health) {
-          if (!st.o) throw Fallback{"health condition status not a string"};
-          Ref hbo(have_hb ? PyFloat_FromDouble(hb) : Py_NewRef(Py_None));
-          PyObject* t = PyTuple_Pack(4, st.o, reason.o, message.o, hbo.o);
-          if (!t) throw Fallback{"oom"};
-          ns.health_cond.reset(t);
+          if (status_bad) throw Fallback{"health condition status not a string"};
+          r.have_hc = true;
+          r.hc_status = st;
+          r.hc_reason = reason;
+          r.hc_message = message;
+          r.hc_have_hb = have_hb;
+          r.hc_hb = hb;
         }
       });
     } else {
       skip_value(cc);
     }
   });
+}
+
+void p1_item(Cursor& c, Pass1Ctx& x, NodeRec& r) {
+  r.cap.assign(x.nkeys, QRaw{});
+  r.alloc.assign(x.nkeys, QRaw{});
+  if (c.peek() != '{') {
+    skip_value(c);  // non-object item: never a GPU node
+    r.is_obj = false;
+    return;
+  }
+  r.is_obj = true;
+  std::string& scratch = x.scratch;
+  for_members(c, [&](const RawStr& k, Cursor& cc) {
+    if (raw_equals(k, "metadata", scratch)) p1_metadata(cc, x, r);
+    else if (raw_equals(k, "spec", scratch)) p1_spec(cc, x, r);
+    else if (raw_equals(k, "status", scratch)) p1_status(cc, x, r);
+    else skip_value(cc);
+  });
+}
+
+struct Pass1Out {
+  std::vector<NodeRec> items;
+  bool have_cont = false;
+  RawStr cont{nullptr, nullptr, false};
+};
+
+// The whole page, no Python API calls (runs with the GIL released).
+void pass1(const char* b, const char* e, Pass1Ctx& x, Pass1Out& out) {
+  Cursor c{b, e};
+  if (c.peek() != '{') throw Fallback{"top level is not an object"};
+  bool items_seen = false;
+  std::string& scratch = x.scratch;
+  for_members(c, [&](const RawStr& k, Cursor& cc) {
+    if (raw_equals(k, "items", scratch)) {
+      if (items_seen) throw Fallback{"duplicate items"};
+      items_seen = true;
+      if (is_null(cc)) return;
+      if (cc.peek() != '[') throw Fallback{"items not a list"};
+      for_elements(cc, [&](Cursor& c3) {
+        out.items.emplace_back();
+        p1_item(c3, x, out.items.back());
+      });
+    } else if (raw_equals(k, "metadata", scratch)) {
+      out.have_cont = false;
+      if (cc.peek() != '{') {
+        skip_value(cc);
+        return;
+      }
+      for_members(cc, [&](const RawStr& mk, Cursor& c3) {
+        if (raw_equals(mk, "continue", scratch)) {
+          out.have_cont = false;
+          if (c3.peek() == '"') {
+            RawStr v = read_raw_string(c3);
+            if (v.e > v.b) {
+              out.have_cont = true;
+              out.cont = v;
+            }
+          } else {
+            skip_value(c3);
+          }
+        } else {
+          skip_value(c3);
+        }
+      });
+    } else {
+      skip_value(cc);
+    }
+  });
+  c.ws();
+  if (c.p != c.end) throw Fallback{"trailing data"};
+}
+
+// ------------------------------------------------------------ pass 2 (GIL) --
+PyObject* parse_int_text(const char* b, size_t n, std::string& scratch) {
+  // Fast path: optional sign + ASCII digits, nothing else.
+  const char* p = b;
+  const char* e = b + n;
+  const char* q = p;
+  if (q < e && (*q == '+' || *q == '-')) ++q;
+  bool simple = q < e && (e - q) <= 18;
+  for (const char* r = q; simple && r < e; ++r)
+    if (*r < '0' || *r > '9') simple = false;
+  if (simple) {
+    long long v = 0;
+    for (const char* r = q; r < e; ++r) v = v * 10 + (*r - '0');
+    if (*p == '-') v = -v;
+    return PyLong_FromLongLong(v);
+  }
+  // Exact Python int(str) semantics (whitespace, '_' separators, unicode digits).
+  scratch.assign(b, n);
+  PyObject* s = PyUnicode_DecodeUTF8(scratch.data(), static_cast<Py_ssize_t>(scratch.size()), "strict");
+  if (!s) {
+    PyErr_Clear();
+    throw Fallback{"invalid utf-8 in quantity"};
+  }
+  PyObject* v = PyLong_FromUnicodeObject(s, 10);
+  Py_DECREF(s);
+  if (!v) {
+    if (PyErr_ExceptionMatches(PyExc_ValueError)) {
+      PyErr_Clear();
+      return nullptr;  // dropped, as the reference's `except Exception: pass`
+    }
+    PyErr_Clear();
+    throw Fallback{"int() raised"};
+  }
+  return v;
+}
+
+// str()+int() semantics of one QRaw; nullptr = not in the breakdown
+PyObject* quantity_value(const QRaw& q, std::string& scratch) {
+  if (q.kind == QKind::Unset || q.kind == QKind::Other) return nullptr;
+  if (q.kind == QKind::Num) {
+    size_t n = static_cast<size_t>(q.s.e - q.s.b);
+    for (size_t i = 0; i < n; ++i) {
+      char ch = q.s.b[i];
+      if (ch == '.' || ch == 'e' || ch == 'E' || ch == 'I') return nullptr;  // str(float): never int()-parsable
+    }
+    return parse_int_text(q.s.b, n, scratch);
+  }
+  const char* b = q.s.b;
+  size_t n = static_cast<size_t>(q.s.e - q.s.b);
+  std::string dec;
+  if (q.s.esc) {
+    decode_into(q.s, dec);
+    b = dec.data();
+    n = dec.size();
+  }
+  if (n == 0) return nullptr;  // `if not val: continue`
+  return parse_int_text(b, n, scratch);
+}
+
+PyObject* breakdown(const std::vector<PyObject*>& pykeys, const std::vector<QRaw>& qs, long long* total,
+                    std::string& scratch) {
+  PyObject* d = PyDict_New();
+  if (!d) throw Fallback{"oom"};
+  Ref hold(d);
+  long long sum = 0;
+  for (size_t i = 0; i < pykeys.size(); ++i) {
+    PyObject* v = quantity_value(qs[i], scratch);
+    if (!v) continue;
+    Ref hv(v);
+    if (PyDict_SetItem(d, pykeys[i], v) < 0) throw Fallback{"dict"};
+    int of = 0;
+    long long x = PyLong_AsLongLongAndOverflow(v, &of);
+    if (of) throw Fallback{"huge quantity"};
+    sum += x;
+  }
+  if (total) *total = sum;
+  return hold.release();
+}
+
+PyObject* sraw_obj(const SRaw& v, std::string& scratch) {
+  if (v.kind != VKind::Str) Py_RETURN_NONE;
+  return make_str(v.s, scratch);
+}
+
+PyObject* labels_dict(const NodeRec& r, std::string& scratch) {
+  PyObject* d = PyDict_New();
+  if (!d) throw Fallback{"oom"};
+  Ref hold(d);
+  if (!r.labels_obj) return hold.release();
+  Cursor c{r.labels.b, r.labels.e};
+  for_members(c, [&](const RawStr& k, Cursor& cc) {
+    Ref key(make_str(k, scratch));
+    Ref val(make_str(read_raw_string(cc), scratch));
+    if (PyDict_SetItem(d, key.o, val.o) < 0) throw Fallback{"dict"};
+  });
+  return hold.release();
+}
+
+PyObject* taints_list(const NodeRec& r, std::string& scratch) {
+  PyObject* lst = PyList_New(0);
+  if (!lst) throw Fallback{"oom"};
+  Ref hold(lst);
+  if (!r.taints_list) return hold.release();
+  Cursor c{r.taints.b, r.taints.e};
+  for_elements(c, [&](Cursor& c3) {
+    if (c3.peek() != '{') {
+      skip_value(c3);
+      return;
+    }
+    Ref tk(Py_NewRef(Py_None)), tv(Py_NewRef(Py_None)), te(Py_NewRef(Py_None));
+    for_members(c3, [&](const RawStr& fk, Cursor& c4) {
+      if (raw_equals(fk, "key", scratch)) tk.reset(sraw_obj(p1_str_or_null(c4, "taint"), scratch));
+      else if (raw_equals(fk, "value", scratch)) tv.reset(sraw_obj(p1_str_or_null(c4, "taint"), scratch));
+      else if (raw_equals(fk, "effect", scratch)) te.reset(sraw_obj(p1_str_or_null(c4, "taint"), scratch));
+      else skip_value(c4);
+    });
+    PyObject* d = PyDict_New();
+    if (!d) throw Fallback{"oom"};
+    Ref hd(d);
+    if (PyDict_SetItem(d, k_key, tk.o) < 0 || PyDict_SetItem(d, k_value, tv.o) < 0 ||
+        PyDict_SetItem(d, k_effect, te.o) < 0 || PyList_Append(lst, d) < 0)
+      throw Fallback{"dict"};
+  });
+  return hold.release();
 }
 
 struct PageOut {
@@ -814,78 +1006,51 @@ struct PageOut {
   Py_ssize_t items = 0;
 };
 
-void emit_node(NodeScan& ns, const KeySpec& ks, bool use_alloc, bool want_extras, PyObject* extras_cls,
-               int annot_mode, PageOut& out, std::string& scratch) {
+void emit_node(const NodeRec& r, const std::vector<PyObject*>& pykeys, bool use_alloc, bool want_extras,
+               PyObject* extras_cls, int annot_mode, PageOut& out, std::string& scratch) {
+  if (!r.is_obj) return;
   long long total = 0;
-  Ref bd(breakdown_dict(ks, use_alloc ? ns.alloc : ns.cap, &total));
+  Ref bd(breakdown(pykeys, use_alloc ? r.alloc : r.cap, &total, scratch));
   if (total <= 0) return;  // not a GPU node (reference :222)
   PyObject* info = PyDict_New();
   if (!info) throw Fallback{"oom"};
   Ref hi(info);
-  PyObject* name = ns.meta_obj ? (ns.name.o ? ns.name.o : Py_None) : nullptr;
-  Ref empty_name;
-  if (!name) {
-    empty_name.reset(PyUnicode_FromStringAndSize("", 0));
-    name = empty_name.o;
-  }
-  Ref labels;
-  PyObject* lab = ns.labels.o;
-  if (!lab || PyDict_GET_SIZE(lab) == 0) {
-    labels.reset(PyDict_New());
-    lab = labels.o;
-  }
-  Ref taints;
-  PyObject* tl = ns.taints.o;
-  if (!tl) {
-    taints.reset(PyList_New(0));
-    tl = taints.o;
-  }
+  Ref name(r.meta_obj ? sraw_obj(r.name, scratch) : PyUnicode_FromStringAndSize("", 0));
+  Ref labels(labels_dict(r, scratch));
+  Ref taints(taints_list(r, scratch));
   Ref gpus(PyLong_FromLongLong(total));
-  if (PyDict_SetItem(info, k_name, name) < 0 || PyDict_SetItem(info, k_ready, ns.ready ? Py_True : Py_False) < 0 ||
+  if (!name.o || !gpus.o) throw Fallback{"oom"};
+  if (PyDict_SetItem(info, k_name, name.o) < 0 || PyDict_SetItem(info, k_ready, r.ready ? Py_True : Py_False) < 0 ||
       PyDict_SetItem(info, k_gpus, gpus.o) < 0 || PyDict_SetItem(info, k_breakdown, bd.o) < 0 ||
-      PyDict_SetItem(info, k_labels, lab) < 0 || PyDict_SetItem(info, k_taints, tl) < 0)
+      PyDict_SetItem(info, k_labels, labels.o) < 0 || PyDict_SetItem(info, k_taints, taints.o) < 0)
     throw Fallback{"dict"};
   if (PyList_Append(out.gpu_nodes.o, info) < 0) throw Fallback{"list"};
-  if (ns.ready && PyList_Append(out.ready_nodes.o, info) < 0) throw Fallback{"list"};
-  if (want_extras) {
-    Ref capd(breakdown_dict(ks, ns.cap, nullptr));
-    Ref allocd(breakdown_dict(ks, ns.alloc, nullptr));
-    // the annotation (full probe report, KBs of escaped JSON) is only materialised when the
-    // caller will read it: always (mode 2) or for nodes without the AMDGPUHealthy condition (mode 1)
-    Ref health_str;
-    if (ns.have_health && (annot_mode == 2 || (annot_mode == 1 && !ns.health_cond.o)))
-      health_str.reset(make_str(ns.health_raw, scratch));
-    PyObject* health = health_str.o ? health_str.o : Py_None;
-    PyObject* ip = ns.internal_ip.o ? ns.internal_ip.o : Py_None;
-    PyObject* hc = ns.health_cond.o ? ns.health_cond.o : Py_None;
-    Ref ex(PyObject_CallFunctionObjArgs(extras_cls, ns.ready ? Py_True : Py_False, capd.o, allocd.o,
-                                        ns.unschedulable ? Py_True : Py_False, health, ip, hc, nullptr));
-    if (!ex.o) {
-      PyErr_Clear();
-      throw Fallback{"NodeExtras()"};
-    }
-    if (PyList_Append(out.extras.o, ex.o) < 0) throw Fallback{"list"};
+  if (r.ready && PyList_Append(out.ready_nodes.o, info) < 0) throw Fallback{"list"};
+  if (!want_extras) return;
+  Ref capd(breakdown(pykeys, r.cap, nullptr, scratch));
+  Ref allocd(breakdown(pykeys, r.alloc, nullptr, scratch));
+  Ref hc;
+  if (r.have_hc) {
+    Ref st(sraw_obj(r.hc_status, scratch)), rs(sraw_obj(r.hc_reason, scratch)), ms(sraw_obj(r.hc_message, scratch));
+    Ref hb(r.hc_have_hb ? PyFloat_FromDouble(r.hc_hb) : Py_NewRef(Py_None));
+    hc.reset(PyTuple_Pack(4, st.o, rs.o, ms.o, hb.o));
+    if (!hc.o) throw Fallback{"oom"};
   }
-}
-
-void parse_item(Cursor& c, const KeySpec& ks, bool use_alloc, bool want_extras, PyObject* extras_cls,
-                const std::string& health_key, const std::string& health_cond, int annot_mode, PageOut& out,
-                std::string& scratch) {
-  out.items++;
-  if (c.peek() != '{') {
-    skip_value(c);  // non-object item: never a GPU node
-    return;
+  // the annotation (full probe report, KBs of escaped JSON) is only materialised when the
+  // caller will read it: always (mode 2) or for nodes without the AMDGPUHealthy condition (mode 1)
+  Ref health_str;
+  if (r.have_health && (annot_mode == 2 || (annot_mode == 1 && !r.have_hc)))
+    health_str.reset(make_str(r.health_raw, scratch));
+  Ref ip;
+  if (r.have_ip) ip.reset(make_str(r.ip, scratch));
+  Ref ex(PyObject_CallFunctionObjArgs(extras_cls, r.ready ? Py_True : Py_False, capd.o, allocd.o,
+                                      r.unschedulable ? Py_True : Py_False, health_str.o ? health_str.o : Py_None,
+                                      ip.o ? ip.o : Py_None, hc.o ? hc.o : Py_None, nullptr));
+  if (!ex.o) {
+    PyErr_Clear();
+    throw Fallback{"NodeExtras()"};
   }
-  NodeScan ns;
-  ns.cap.resize(ks.keys.size());
-  ns.alloc.resize(ks.keys.size());
-  for_members(c, [&](const RawStr& k, Cursor& cc) {
-    if (raw_equals(k, "metadata", scratch)) parse_metadata(cc, ns, health_key, scratch);
-    else if (raw_equals(k, "spec", scratch)) parse_spec(cc, ns, scratch);
-    else if (raw_equals(k, "status", scratch)) parse_status(cc, ns, ks, scratch, health_cond);
-    else skip_value(cc);
-  });
-  emit_node(ns, ks, use_alloc, want_extras, extras_cls, annot_mode, out, scratch);
+  if (PyList_Append(out.extras.o, ex.o) < 0) throw Fallback{"list"};
 }
 
 int append_all(PyObject* result, PyObject* attr, PyObject* items) {
@@ -916,7 +1081,8 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
   if (!PyArg_ParseTuple(args, "y*OO!ppsO|si", &view, &result, &PyTuple_Type, &keys, &use_alloc, &want_extras,
                         &health_key_c, &extras_cls, &health_cond_c, &annot_mode))
     return nullptr;
-  KeySpec ks;
+  std::vector<std::string> kstr;
+  std::vector<PyObject*> pykeys;
   for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(keys); ++i) {
     PyObject* k = PyTuple_GET_ITEM(keys, i);
     Py_ssize_t n;
@@ -925,56 +1091,36 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
       PyBuffer_Release(&view);
       return nullptr;
     }
-    ks.keys.emplace_back(s, static_cast<size_t>(n));
-    ks.pykeys.push_back(k);
+    kstr.emplace_back(s, static_cast<size_t>(n));
+    pykeys.push_back(k);
   }
-  std::string health_key(health_key_c);
-  std::string health_cond(health_cond_c);
-  std::string scratch;
-  PageOut out;
+  std::string health_key(health_key_c), health_cond(health_cond_c);
+  Pass1Ctx ctx{kstr.size(), &kstr, &health_key, &health_cond, {}};
+  Pass1Out p1;
   const char* why = nullptr;
+  const char* b = static_cast<const char*>(view.buf);
+  // pass 1 without the GIL: the buffer is held by `view` (a bytearray cannot be resized while exported)
+  Py_BEGIN_ALLOW_THREADS
   try {
-    if (!out.gpu_nodes.o || !out.ready_nodes.o || !out.extras.o) throw Fallback{"oom"};
-    Cursor c{static_cast<const char*>(view.buf), static_cast<const char*>(view.buf) + view.len};
-    if (c.peek() != '{') throw Fallback{"top level is not an object"};
-    bool items_seen = false;
-    for_members(c, [&](const RawStr& k, Cursor& cc) {
-      if (raw_equals(k, "items", scratch)) {
-        if (items_seen) throw Fallback{"duplicate items"};
-        items_seen = true;
-        if (is_null(cc)) return;
-        if (cc.peek() != '[') throw Fallback{"items not a list"};
-        for_elements(cc, [&](Cursor& c3) {
-          parse_item(c3, ks, use_alloc, want_extras, extras_cls, health_key, health_cond, annot_mode, out, scratch);
-        });
-      } else if (raw_equals(k, "metadata", scratch)) {
-        out.cont.reset(nullptr);
-        if (cc.peek() != '{') {
-          skip_value(cc);
-          return;
-        }
-        for_members(cc, [&](const RawStr& mk, Cursor& c3) {
-          if (raw_equals(mk, "continue", scratch)) {
-            if (c3.peek() == '"') {
-              RawStr v = read_raw_string(c3);
-              if (v.e > v.b) out.cont.reset(make_str(v, scratch));
-              else out.cont.reset(nullptr);
-            } else {
-              out.cont.reset(nullptr);
-              skip_value(c3);
-            }
-          } else {
-            skip_value(c3);
-          }
-        });
-      } else {
-        skip_value(cc);
-      }
-    });
-    c.ws();
-    if (c.p != c.end) throw Fallback{"trailing data"};
+    pass1(b, b + view.len, ctx, p1);
   } catch (const Fallback& f) {
     why = f.why;
+  } catch (const std::bad_alloc&) {
+    why = "out of memory";
+  }
+  Py_END_ALLOW_THREADS
+  PageOut out;
+  if (!why) {
+    try {
+      if (!out.gpu_nodes.o || !out.ready_nodes.o || !out.extras.o) throw Fallback{"oom"};
+      std::string& scratch = ctx.scratch;
+      for (const NodeRec& r : p1.items)
+        emit_node(r, pykeys, use_alloc, want_extras, extras_cls, annot_mode, out, scratch);
+      out.items = static_cast<Py_ssize_t>(p1.items.size());
+      if (p1.have_cont) out.cont.reset(make_str(p1.cont, scratch));
+    } catch (const Fallback& f) {
+      why = f.why;
+    }
   }
   PyBuffer_Release(&view);
   if (why) {

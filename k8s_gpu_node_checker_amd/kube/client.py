@@ -58,6 +58,32 @@ _RETRY_STATUS = frozenset((429, 500, 502, 503, 504))
 _LOOPBACK = ("127.", "localhost", "::1", "[::1]")
 
 
+class _PageReader:
+    """Receives one pipelined LIST page on its own thread.
+
+    Socket reads release the GIL, and so does pass 1 of the native NodeList
+    scan, so page k+1 streams in while page k is being scanned.
+    """
+
+    def __init__(self, conn: Connection, path: str):
+        import threading
+        self.conn = conn
+        self.path = path
+        self.resp: Optional[Response] = None
+        self.thread = threading.Thread(target=self._run, name="list-prefetch", daemon=True)
+        self.thread.start()
+
+    def _run(self) -> None:
+        try:
+            self.resp = self.conn.read_pending("GET", self.path)
+        except Exception:  # transport trouble: the caller re-requests the page normally
+            self.resp = None
+
+    def join(self) -> Optional[Response]:
+        self.thread.join()
+        return self.resp
+
+
 class KubeClient:
     def __init__(self, cluster: ClusterConnection, timeout: float = 30.0, retries: int = 2,
                  backoff: Optional[Backoff] = None, gzip: Optional[bool] = None,
@@ -150,7 +176,7 @@ class KubeClient:
         from ..ops import fastpath
         result = ScanResult()
         cont: Optional[str] = None
-        prefetched: Dict[str, Connection] = {}  # next-page path -> connection its request was sent on
+        prefetched: Dict[str, _PageReader] = {}  # next-page path -> reader of the request already sent
 
         def peek(prefix: bytes) -> None:
             # NodeList JSON carries metadata.continue *before* items: as soon as the head of page k
@@ -167,7 +193,7 @@ class KubeClient:
                 conn2.send_only("GET", nxt, self._headers())
             except HTTPError:
                 return
-            prefetched[nxt] = conn2
+            prefetched[nxt] = _PageReader(conn2, nxt)
 
         while True:
             path = self._list_path(limit, cont, label_selector, resource_version)
@@ -198,16 +224,18 @@ class KubeClient:
                                      server_hostname=self.cluster.tls_server_name, proxy_url=self.cluster.proxy_url)
         return self._conn2
 
-    def _take_prefetched(self, prefetched: Dict[str, Connection], path: str) -> Optional[Response]:
-        """Read the already-sent request for ``path``; swap it in as the primary connection."""
-        conn2 = prefetched.pop(path, None)
+    def _take_prefetched(self, prefetched: Dict[str, "_PageReader"], path: str) -> Optional[Response]:
+        """Collect the already-sent request for ``path``; swap its connection in as the primary."""
+        reader = prefetched.pop(path, None)
+        for other in prefetched.values():
+            other.join()
         prefetched.clear()
-        if conn2 is None:
+        if reader is None:
             return None
         self.requests_made += 1
-        try:
-            resp = conn2.read_pending("GET", path)
-        except HTTPError:
+        conn2 = reader.conn
+        resp = reader.join()
+        if resp is None:
             return None  # fall back to a normal (retried) request
         # alternate: the connection that just answered becomes primary, the old primary the spare
         self._conn, self._conn2 = conn2, self._conn

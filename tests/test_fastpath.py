@@ -164,3 +164,20 @@ def test_dumps_control_chars_and_unicode():
     obj = {"k": [s, {"": None}, [], {}, 1.5, -0.0, 10 ** 30, True]}
     assert ext.dumps_indent2(obj) == json.dumps(obj, ensure_ascii=False, indent=2)
     assert fastpath.dumps_indent2({1: 2}) == json.dumps({1: 2}, ensure_ascii=False, indent=2)  # fallback path
+
+
+@settings(max_examples=300, suppress_health_check=[HealthCheck.too_slow])
+@given(json_tree, st.integers(0, 70), st.booleans())
+def test_skipped_subtrees_with_escapes(junk, pad, ascii_only):
+    """Arbitrary JSON (quotes, backslash runs, brackets inside strings) in skipped fields, at every
+    alignment relative to the 64-byte SIMD blocks, must not change the scan."""
+    node = {"metadata": {"name": "n" * pad, "annotations": {"x": json.dumps(junk)}},
+            "spec": {"providerID": "\\\\\"[{" * (pad % 7)},
+            "status": {"images": [junk, {"names": ["\\" * pad + '"]}']}],
+                       "capacity": {"amd.com/gpu": "8"},
+                       "nodeInfo": junk,
+                       "conditions": [{"type": "Ready", "status": "True"}]}}
+    body = json.dumps({"kind": "NodeList", "pad": "x" * pad, "items": [node, junk, node]}, ensure_ascii=ascii_only)
+    assert assert_same(body.encode()) in ("native", "fallback")
+    r, _ = native_scan(body.encode())
+    assert len(r.gpu_nodes) == 2
