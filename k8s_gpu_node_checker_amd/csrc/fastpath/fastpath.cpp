@@ -245,6 +245,8 @@ void skip_literal(Cursor& c) {
     c.p += 5;
   } else if (left >= 3 && memcmp(p, "NaN", 3) == 0) {
     c.p += 3;
+  } else if (left >= 8 && memcmp(p, "Infinity", 8) == 0) {  // json.loads accepts it too
+    c.p += 8;
   } else {
     throw Fallback{"bad literal"};
   }
