@@ -13,7 +13,7 @@ timeout -k 10 300 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/
 cat gpurun_out/bench_default.json
 for n in 8 1000; do
   step bench-nodes-$n
-  timeout -k 10 300 python bench.py --nodes $n --steps $([ $n = 1000 ] && echo 50 || echo 500) --warmup 10 > gpurun_out/bench_nodes$n.json 2> gpurun_out/bench_nodes$n.err || { echo "bench $n failed"; tail -20 gpurun_out/bench_nodes$n.err; exit 1; }
+  timeout -k 10 300 python bench.py --nodes $n --steps $([ $n = 1000 ] && echo 100 || echo 500) --warmup 20 > gpurun_out/bench_nodes$n.json 2> gpurun_out/bench_nodes$n.err || { echo "bench $n failed"; tail -20 gpurun_out/bench_nodes$n.err; exit 1; }
   cat gpurun_out/bench_nodes$n.json
 done
 step bench-slack
