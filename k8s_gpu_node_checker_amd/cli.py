@@ -72,6 +72,8 @@ def build_parser(show_all: bool = False, prog: Optional[str] = None) -> argparse
     x.add_argument("--prometheus-textfile", help=h("node-exporter textfile 메트릭 경로"))
     x.add_argument("--state-file", help=h("직전 결과 저장 파일 (알림 중복 제거)"))
     x.add_argument("--watch", type=float, default=0.0, help=h("N초마다 반복 점검 (0 = 한 번, 기본)"))
+    x.add_argument("--watch-count", type=int, default=0,
+                   help=h("--watch 반복 횟수 (0 = 무제한, 기본); 종료 코드는 마지막 점검의 것"))
     return p
 
 
@@ -139,15 +141,35 @@ def _run_once(args: argparse.Namespace) -> int:
 def main(argv: Optional[List[str]] = None) -> int:
     args = parse_args(argv)
     if args.watch and args.watch > 0:
-        import time
-        code = 0
-        while True:
-            started = time.monotonic()
-            code = _run_once(args)
-            sys.stdout.flush()
-            time.sleep(max(0.0, args.watch - (time.monotonic() - started)))
-        return code  # pragma: no cover
+        return _watch(args)
     return _run_once(args)
+
+
+def _watch(args: argparse.Namespace) -> int:
+    """Repeat the check every ``--watch`` seconds (fixed cadence, not fixed sleep).
+
+    Ends after ``--watch-count`` checks (0 = forever) or on Ctrl-C, with the
+    exit code of the last completed check.  Combine with ``--state-file
+    --slack-on-change`` for de-duplicated alerts from a long-running Pod.
+    """
+    import time
+    code = 0
+    n = 0
+    next_at = time.monotonic()
+    try:
+        while True:
+            code = _run_once(args)
+            n += 1
+            sys.stdout.flush()
+            if args.watch_count > 0 and n >= args.watch_count:
+                return code
+            next_at += args.watch
+            now = time.monotonic()
+            if next_at < now:  # a check overran the period: skip the missed slots
+                next_at = now
+            time.sleep(next_at - now)
+    except KeyboardInterrupt:
+        return code
 
 
 def entry() -> None:

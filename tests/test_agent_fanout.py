@@ -128,3 +128,58 @@ def test_fanout_is_concurrent(fixture_report):
         assert out[0]["error"].startswith("timeout") and time.time() - t < 1
     finally:
         s.shutdown()
+
+
+def test_fanout_asyncio_debug_mode_clean(fixture_report):
+    """SURVEY §5 race detection: the fan-out under asyncio debug mode (never-awaited coroutines,
+    unclosed transports, slow callbacks) against a mix of good, refused and garbage endpoints."""
+    import asyncio
+    import gc
+    import socket
+    import threading
+    import warnings
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+    from k8s_gpu_node_checker_amd.parallel import fanout
+
+    class H(BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            body = b'{"ok": 1}' if self.path == "/good" else b"not json"
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+    s = ThreadingHTTPServer(("127.0.0.1", 0), H)
+    s.daemon_threads = True
+    threading.Thread(target=s.serve_forever, daemon=True).start()
+    free = socket.socket()
+    free.bind(("127.0.0.1", 0))
+    dead_port = free.getsockname()[1]
+    free.close()
+    base = f"http://127.0.0.1:{s.server_address[1]}"
+    targets = ([{"name": f"g{i}", "url": base + "/good"} for i in range(8)]
+               + [{"name": "bad", "url": base + "/bad"}, {"name": "dead", "url": f"http://127.0.0.1:{dead_port}/"}])
+    try:
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            loop = asyncio.new_event_loop()
+            loop.set_debug(True)
+            loop.slow_callback_duration = 0.25
+            errors = []
+            loop.set_exception_handler(lambda lp, ctx: errors.append(ctx.get("message")))
+            try:
+                out = loop.run_until_complete(fanout.fetch_all(targets, concurrency=4, timeout=2.0, retries=1))
+                loop.run_until_complete(loop.shutdown_asyncgens())
+            finally:
+                loop.close()
+            gc.collect()
+        assert [o.get("ok") for o in out[:8]] == [1] * 8
+        assert "error" in out[8] and "error" in out[9]
+        assert not errors, errors
+        leaks = [str(w.message) for w in caught if issubclass(w.category, (ResourceWarning, RuntimeWarning))]
+        assert not leaks, leaks
+    finally:
+        s.shutdown()

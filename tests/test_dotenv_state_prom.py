@@ -99,3 +99,32 @@ def test_prom_escaping():
     r = R(0, [node('we"ird\\name', True)])
     lines = prom.render(r)
     assert 'k8s_gpu_checker_node_ready{node="we\\"ird\\\\name"} 1' in lines
+
+
+def test_cli_watch_bounded(run_cli, mock_cluster, sink, tmp_path):
+    """``--watch P --watch-count N``: N checks on a fixed cadence, exit code of the last one; with
+    ``--state-file --slack-on-change`` a long-running watcher alerts once per state change."""
+    import json
+    import time
+    from k8s_gpu_node_checker_amd.testing import fixtures
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+    srv = mock_cluster(fixtures.golden("readme"))
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    t = time.monotonic()
+    p = run_cli(["--kubeconfig", kc, "--json", "--watch", "0.3", "--watch-count", "3"])
+    elapsed = time.monotonic() - t
+    assert p.returncode == 0, p.stderr
+    docs = []
+    dec = json.JSONDecoder()
+    text = p.stdout.strip()
+    while text:
+        d, i = dec.raw_decode(text)
+        docs.append(d)
+        text = text[i:].strip()
+    assert len(docs) == 3 and all(d["ready_nodes"] == 2 for d in docs)
+    assert elapsed >= 0.6  # two full periods between three checks
+    args = ["--kubeconfig", kc, "--slack-webhook", sink.url("200"), "--slack-only-on-error",
+            "--state-file", str(tmp_path / "st.json"), "--slack-on-change", "--watch", "0.05", "--watch-count", "4"]
+    srv.state.set_nodes(fixtures.golden("notready"))
+    assert run_cli(args).returncode == 3
+    assert len(sink.requests) == 1  # four failing checks, one alert
