@@ -7,7 +7,9 @@
 //   gemm_bf16   C[M,N] = A[M,K] . Bt[N,K]^T, bf16 in / fp32 out on MFMA
 //               (v_mfma_f32_16x16x32_bf16), XOR-swizzled LDS (conflict-free
 //               ds_read_b128 fragment loads), XCD-aware tile order.
-//               v2: 256x256x64 tiles, 8 waves, LDS-DMA double buffer (large GEMMs);
+//               v3: 256x256x64 tiles, 8 waves in two barrier-staggered groups, LDS-DMA
+//                   restaged region by region (large GEMMs, default);
+//               v2: the same tile, one barrier per K-tile (kept for A/B);
 //               v1: 128x128x64 tiles, 4 waves, register-staged (small grids).
 //               Verified against an fp32 reference kernel on sampled outputs.
 //   hbm_copy / hbm_read / hbm_write
@@ -267,6 +269,174 @@ gemm_bf16_v2_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
         C[static_cast<size_t>(row0 + m * 16 + fq * 4 + j) * N + col0 + n * 16 + frow] = acc[m][n][j];
 }
 
+// ---------------------------------------------------------------------------
+// gemm v3: the v2 tile and LDS image on a staggered 4-phase schedule (tools/gemm_lab.hip "v5";
+// +5-7 % over v2 at 4096^3/8192^3 on MI355X, profiles/gemm_lab_*.jsonl).
+// Waves 0-3 and 4-7 form two groups (one wave of each per SIMD); group 1 runs one s_barrier behind
+// group 0, so on every SIMD one wave's MFMA slot covers the other's load slot and barrier wait.
+// Each K-tile is 4 phases, one 64x32 quadrant of the wave's 128x64 output each (16 MFMA):
+//   load slot: this quadrant's ds_reads (+ LDS-DMA restaging) -> s_barrier -> lgkmcnt(0) ->
+//   MFMA slot -> s_barrier.
+// Quadrant order (m0,n0) (m0,n1) (m1,n1) (m1,n0): phase 0 reads A(m0)+B(n0), phase 1 B(n1), phase 2
+// A(m1), phase 3 reuses B(n0) from registers.  A stage is restaged region by region (16 KiB each):
+// R0 = A rows of m0, R1 = B rows of n0, R2 = B rows of n1, R3 = A rows of m1.  Reads retire after
+// the barrier that closes their load slot, so a region read in phase p is free two phases later:
+// R0/R1 of tile t+2 go out in phase 2 of tile t, R2 in phase 3, and R3 of tile t+1 (other buffer,
+// last read in phase 2 of tile t-1) in phase 0.  Tile t+1 is retired at phase 3 of tile t with a
+// counted vmcnt(6) (tile t+2's R0-R2 may stay in flight); raw s_barrier only -- __syncthreads()
+// would drain the in-flight LDS-DMA with vmcnt(0).
+#define STG_BARRIER()                  \
+  do {                                 \
+    __builtin_amdgcn_sched_barrier(0); \
+    __builtin_amdgcn_s_barrier();      \
+    __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
+// One 16 KiB region of a stage: 16 LDS-DMA wave-instructions of 8 rows, 2 per wave.
+__device__ __forceinline__ void stg_region(unsigned char* lds_stage, const __bf16* __restrict__ A,
+                                           const __bf16* __restrict__ Bt, int K, int kt, int region, int i, int wid,
+                                           int lane) {
+  const int rsub = lane >> 3, phys = lane & 7;
+  const int g = wid * 2 + i;
+  const bool is_a = region == 0 || region == 3;
+  const int row0 = is_a ? (g >> 3) * 128 + (region == 0 ? 0 : 64) + (g & 7) * 8
+                        : (g >> 2) * 64 + (region == 1 ? 0 : 32) + (g & 3) * 8;
+  const int row = row0 + rsub;
+  const int c = phys ^ ((row >> 1) & 7);
+  const __bf16* gp = (is_a ? A : Bt) + static_cast<size_t>(row) * K + kt * BK + c * 8;
+  unsigned char* l = lds_stage + (is_a ? 0 : V2_BM * BK * 2) + row0 * (BK * 2);
+  __builtin_amdgcn_global_load_lds(gp, (lds_void_t*)l, 16, 0, 0);
+}
+
+__device__ __forceinline__ void stg_mfma(floatx4 (&acc)[8][4], const bf16x8 (&af)[4][2], const bf16x8 (&bf)[2][2],
+                                         int m0, int n0) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        acc[m0 + m][n0 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][s], bf[n][s], acc[m0 + m][n0 + n], 0, 0, 0);
+  // MFMAs are not memory operations, so IR passes may sink them past the next s_barrier into the
+  // other group's slot; an empty volatile asm that reads and writes each result pins them here.
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[m0 + m][n0 + n]));
+}
+
+__global__ void __launch_bounds__(V2_THREADS, 1)
+gemm_bf16_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
+                    int K) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int tiles_m = M / V2_BM, tiles_n = N / V2_BN, nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  constexpr int GROUP_M = 4;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % (GROUP_M * tiles_n)) % gsize;
+  const int tn = (bid % (GROUP_M * tiles_n)) / gsize;
+  const __bf16* Ab = A + static_cast<size_t>(tm) * V2_BM * K;
+  const __bf16* Bb = Bt + static_cast<size_t>(tn) * V2_BN * K;
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int KT = K / BK;
+  const int frow = lane & 15, fq = lane >> 4;
+
+  v2_fill(smem, Ab, Bb, K, 0, wid, lane);
+  if (KT > 1) {
+    v2_fill(smem + V2_STAGE_BYTES, Ab, Bb, K, 1, wid, lane);
+    __builtin_amdgcn_s_waitcnt(0x3f78);  // vmcnt(8): tile 0 landed, tile 1 may be in flight
+  } else {
+    __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
+  }
+  STG_BARRIER();
+  if (wr == 1) STG_BARRIER();  // the stagger
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  for (int kt = 0; kt < KT; ++kt) {
+    unsigned char* cur = smem + (kt & 1) * V2_STAGE_BYTES;
+    unsigned char* nxt = smem + ((kt + 1) & 1) * V2_STAGE_BYTES;
+    const u32x4* a_img = reinterpret_cast<const u32x4*>(cur);
+    const u32x4* b_img = reinterpret_cast<const u32x4*>(cur + V2_BM * BK * 2);
+    const bool pre = kt + 2 < KT;
+    // phase 0: A(m0), B(n0); R3 of tile kt+1 (tile 1 came whole with the prologue)
+    if (kt >= 1 && kt + 1 < KT) {
+      stg_region(nxt, Ab, Bb, K, kt + 1, 3, 0, wid, lane);
+      stg_region(nxt, Ab, Bb, K, kt + 1, 3, 1, wid, lane);
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) b0[n][s] = __builtin_bit_cast(bf16x8, b_img[swz(wc * 64 + n * 16 + frow, fq + 4 * s)]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) af[m][s] = __builtin_bit_cast(bf16x8, a_img[swz(wr * 128 + m * 16 + frow, fq + 4 * s)]);
+    STG_BARRIER();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    stg_mfma(acc, af, b0, 0, 0);
+    STG_BARRIER();
+    // phase 1: B(n1)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        b1[n][s] = __builtin_bit_cast(bf16x8, b_img[swz(wc * 64 + (n + 2) * 16 + frow, fq + 4 * s)]);
+    STG_BARRIER();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    stg_mfma(acc, af, b1, 0, 2);
+    STG_BARRIER();
+    // phase 2: A(m1); restage R0, R1 with tile kt+2
+    if (pre) {
+      stg_region(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
+      stg_region(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
+      stg_region(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
+      stg_region(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        af[m][s] = __builtin_bit_cast(bf16x8, a_img[swz(wr * 128 + (m + 4) * 16 + frow, fq + 4 * s)]);
+    STG_BARRIER();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    stg_mfma(acc, af, b1, 4, 2);
+    STG_BARRIER();
+    // phase 3: no LDS reads; restage R2, retire tile kt+1
+    if (pre) {
+      stg_region(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
+      stg_region(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
+      __builtin_amdgcn_s_waitcnt(0x3f76);  // vmcnt(6)
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
+    }
+    STG_BARRIER();
+    stg_mfma(acc, af, b0, 4, 0);
+    STG_BARRIER();
+  }
+  if (wr == 0) STG_BARRIER();  // balance the stagger
+  const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 64;
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        C[static_cast<size_t>(row0 + m * 16 + fq * 4 + j) * N + col0 + n * 16 + frow] = acc[m][n][j];
+}
+
 // fp32 reference for sampled outputs: one thread per (row, col) sample.
 __global__ void gemm_ref_kernel(const __bf16* A, const __bf16* Bt, const int* rows, const int* cols, float* out,
                                 int nsamp, int K) {
@@ -397,8 +567,8 @@ extern "C" {
 
 const char* diag_last_error(void) { return g_err.c_str(); }
 
-// 0 = auto (v2 256x256 LDS-DMA tiles when M, N are multiples of 256 and the grid fills the chip),
-// 1 = force v1 (128x128 register-staged), 2 = force v2
+// 0 = auto (v3 staggered 256x256 LDS-DMA tiles when M, N are multiples of 256 and the grid fills the
+// chip, else v1), 1 = force v1 (128x128 register-staged), 2 = force v2, 3 = force v3
 void diag_set_gemm_variant(int v) { g_gemm_variant = v; }
 
 int diag_device_count(void) {
@@ -426,22 +596,29 @@ int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N,
   }
   // v2 needs 256-multiples and enough 256x256 tiles to occupy the 256 CUs (one block per CU);
   // below that the 128x128 kernel's 4x larger grid wins (measured: 2048^3 v1 543 vs v2 321 TFLOP/s)
-  const bool v2_ok = M % V2_BM == 0 && N % V2_BN == 0 && (M / V2_BM) * (N / V2_BN) >= 256;
-  if (g_gemm_variant == 2 || (g_gemm_variant == 0 && v2_ok)) {
+  const bool big_ok = M % V2_BM == 0 && N % V2_BN == 0 && (M / V2_BM) * (N / V2_BN) >= 256;
+  const int variant = g_gemm_variant == 0 ? (big_ok ? 3 : 1) : g_gemm_variant;
+  if (variant == 2 || variant == 3) {
     if (M % V2_BM || N % V2_BN) {
-      g_err = "gemm_bf16 v2: M, N must be multiples of 256";
+      g_err = "gemm_bf16 v2/v3: M, N must be multiples of 256";
       return -2;
     }
-    static bool attr_set = false;
-    if (!attr_set) {
-      DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_v2_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
-      attr_set = true;
+    static bool attr_set[2] = {false, false};
+    const void* fn = variant == 2 ? reinterpret_cast<const void*>(gemm_bf16_v2_kernel)
+                                  : reinterpret_cast<const void*>(gemm_bf16_v3_kernel);
+    if (!attr_set[variant - 2]) {
+      DIAG_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+      attr_set[variant - 2] = true;
     }
     const int nwg = (M / V2_BM) * (N / V2_BN);
-    hipLaunchKernelGGL(gemm_bf16_v2_kernel, dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
-                       static_cast<hipStream_t>(stream), static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt),
-                       C, M, N, K);
+    if (variant == 2)
+      hipLaunchKernelGGL(gemm_bf16_v2_kernel, dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
+                         static_cast<hipStream_t>(stream), static_cast<const __bf16*>(A),
+                         static_cast<const __bf16*>(Bt), C, M, N, K);
+    else
+      hipLaunchKernelGGL(gemm_bf16_v3_kernel, dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
+                         static_cast<hipStream_t>(stream), static_cast<const __bf16*>(A),
+                         static_cast<const __bf16*>(Bt), C, M, N, K);
   } else {
     const int nwg = (M / BM) * (N / BN);
     hipLaunchKernelGGL(gemm_bf16_kernel, dim3(nwg), dim3(THREADS), 0, static_cast<hipStream_t>(stream),

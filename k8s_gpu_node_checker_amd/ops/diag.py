@@ -39,6 +39,7 @@ def lib() -> ctypes.CDLL:
         L = load_cdll("libmi355x_diag.so", required=True)
         assert L is not None
         L.diag_last_error.restype = ctypes.c_char_p
+        L.diag_set_gemm_variant.argtypes = [ctypes.c_int]
         L.diag_device_count.restype = ctypes.c_int
         L.diag_device_arch.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.diag_gemm_bf16_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -67,6 +68,16 @@ def device_info(device: int = 0) -> Dict[str, Any]:
     _check(lib().diag_device_arch(device, buf, len(buf)))
     arch, name, cus, mem, bdf = buf.value.decode().split("|")
     return {"arch": arch, "name": name, "cus": int(cus), "mem_bytes": int(mem), "bdf": bdf}
+
+
+GEMM_VARIANTS = {"auto": 0, "v1": 1, "v2": 2, "v3": 3}
+
+
+def set_gemm_variant(variant: str = "auto") -> None:
+    """Select the GEMM kernel: ``auto`` (v3 for 256-multiples that fill the chip, else v1),
+    ``v1`` 128x128 register-staged, ``v2`` 256x256 LDS-DMA, ``v3`` 256x256 staggered LDS-DMA.
+    v2/v3 need M, N multiples of 256."""
+    lib().diag_set_gemm_variant(GEMM_VARIANTS[variant])
 
 
 def gemm_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int, stream: int = 0) -> None:

@@ -80,6 +80,45 @@ def test_mfma_gemm_matches_fp32_reference(dev, m, n, k):
     assert rel < 1e-4 * max(1, k / 512), rel
 
 
+@pytest.mark.parametrize("variant", ["v1", "v2", "v3"])
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (768, 512, 256),
+                                   (1024, 768, 4096)])
+def test_mfma_gemm_variants_match_fp32_reference(dev, variant, m, n, k):
+    """Every kernel variant on shapes that exercise 1, 2, 3, 4 and 64 K-tiles (prologue/epilogue
+    paths of the staggered v3 pipeline) and non-square grids."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + 5 * n + 11 * k)
+    a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
+    bt = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
+    c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+    diag.set_gemm_variant(variant)
+    try:
+        diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        diag.set_gemm_variant("auto")
+    ref = a.float() @ bt.float().t()
+    assert not torch.isnan(c).any()
+    rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
+    assert rel < 1e-4 * max(1, k / 512), rel
+
+
+def test_mfma_gemm_large_auto_uses_v3_and_matches(dev):
+    """4096^3 in auto mode runs the staggered v3 kernel; compare every output with a bf16-input,
+    fp32-accumulate torch reference."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    m = n = k = 4096
+    g = torch.Generator(device=dev).manual_seed(4096)
+    a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
+    bt = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
+    c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+    diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = a.float() @ bt.float().t()
+    rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
+    assert rel < 1e-4 * (k / 512), rel
+
+
 def test_mfma_gemm_identity_asymmetric(dev):
     """A = I with an asymmetric B catches a transposed C write (guide §3)."""
     from k8s_gpu_node_checker_amd.ops import diag
