@@ -220,6 +220,59 @@ PyObject* make_str(const RawStr& s, std::string& scratch) {
   return o;
 }
 
+// Per-page cache of the Python str objects made from short, escape-free tokens.  Label keys and most
+// label values repeat on every node of a cluster ("kubernetes.io/arch": "amd64", ...): the first node
+// creates them, the others share them (one INCREF instead of UTF-8 decode + allocation, and dict
+// insertion reuses the cached hash).  Keys point into the page buffer, alive for the whole call.
+class StrCache {
+ public:
+  StrCache() : slots_(kSlots) {}
+  StrCache(const StrCache&) = delete;
+  StrCache& operator=(const StrCache&) = delete;
+  ~StrCache() {
+    for (Slot& e : slots_) Py_XDECREF(e.obj);
+  }
+  // new reference
+  PyObject* get(const RawStr& s, std::string& scratch) {
+    const size_t n = static_cast<size_t>(s.e - s.b);
+    if (s.esc || n > kMaxLen) return make_str(s, scratch);
+    uint64_t h = 1469598103934665603ULL;  // FNV-1a
+    for (size_t i = 0; i < n; ++i) h = (h ^ static_cast<unsigned char>(s.b[i])) * 1099511628211ULL;
+    size_t i = static_cast<size_t>(h) & (kSlots - 1);
+    for (;;) {
+      Slot& e = slots_[i];
+      if (!e.obj) break;
+      if (e.hash == h && e.len == n && memcmp(e.b, s.b, n) == 0) {
+        Py_INCREF(e.obj);
+        return e.obj;
+      }
+      i = (i + 1) & (kSlots - 1);
+    }
+    PyObject* o = make_str(s, scratch);
+    if (used_ < kSlots / 2) {
+      Slot& e = slots_[i];
+      e.hash = h;
+      e.b = s.b;
+      e.len = n;
+      e.obj = o;
+      Py_INCREF(o);
+      ++used_;
+    }
+    return o;
+  }
+
+ private:
+  static constexpr size_t kSlots = 2048, kMaxLen = 96;
+  struct Slot {
+    uint64_t hash = 0;
+    const char* b = nullptr;
+    size_t len = 0;
+    PyObject* obj = nullptr;
+  };
+  std::vector<Slot> slots_;
+  size_t used_ = 0;
+};
+
 void skip_value(Cursor& c);
 
 void skip_number(Cursor& c) {
@@ -958,21 +1011,26 @@ PyObject* sraw_obj(const SRaw& v, std::string& scratch) {
   return make_str(v.s, scratch);
 }
 
-PyObject* labels_dict(const NodeRec& r, std::string& scratch) {
+PyObject* sraw_cached(const SRaw& v, StrCache& cache, std::string& scratch) {
+  if (v.kind != VKind::Str) Py_RETURN_NONE;
+  return cache.get(v.s, scratch);
+}
+
+PyObject* labels_dict(const NodeRec& r, StrCache& cache, std::string& scratch) {
   PyObject* d = PyDict_New();
   if (!d) throw Fallback{"oom"};
   Ref hold(d);
   if (!r.labels_obj) return hold.release();
   Cursor c{r.labels.b, r.labels.e};
   for_members(c, [&](const RawStr& k, Cursor& cc) {
-    Ref key(make_str(k, scratch));
-    Ref val(make_str(read_raw_string(cc), scratch));
+    Ref key(cache.get(k, scratch));
+    Ref val(cache.get(read_raw_string(cc), scratch));
     if (PyDict_SetItem(d, key.o, val.o) < 0) throw Fallback{"dict"};
   });
   return hold.release();
 }
 
-PyObject* taints_list(const NodeRec& r, std::string& scratch) {
+PyObject* taints_list(const NodeRec& r, StrCache& cache, std::string& scratch) {
   PyObject* lst = PyList_New(0);
   if (!lst) throw Fallback{"oom"};
   Ref hold(lst);
@@ -985,9 +1043,9 @@ PyObject* taints_list(const NodeRec& r, std::string& scratch) {
     }
     Ref tk(Py_NewRef(Py_None)), tv(Py_NewRef(Py_None)), te(Py_NewRef(Py_None));
     for_members(c3, [&](const RawStr& fk, Cursor& c4) {
-      if (raw_equals(fk, "key", scratch)) tk.reset(sraw_obj(p1_str_or_null(c4, "taint"), scratch));
-      else if (raw_equals(fk, "value", scratch)) tv.reset(sraw_obj(p1_str_or_null(c4, "taint"), scratch));
-      else if (raw_equals(fk, "effect", scratch)) te.reset(sraw_obj(p1_str_or_null(c4, "taint"), scratch));
+      if (raw_equals(fk, "key", scratch)) tk.reset(sraw_cached(p1_str_or_null(c4, "taint"), cache, scratch));
+      else if (raw_equals(fk, "value", scratch)) tv.reset(sraw_cached(p1_str_or_null(c4, "taint"), cache, scratch));
+      else if (raw_equals(fk, "effect", scratch)) te.reset(sraw_cached(p1_str_or_null(c4, "taint"), cache, scratch));
       else skip_value(c4);
     });
     PyObject* d = PyDict_New();
@@ -1008,8 +1066,57 @@ struct PageOut {
   Py_ssize_t items = 0;
 };
 
+// NodeExtras (models/node.py: a __slots__ class) built without running its Python __init__: the
+// instance is allocated by the type and each slot set through its member descriptor, in __init__'s
+// order.  Resolved once per page; anything unexpected (not a type, missing or non-member slot)
+// keeps the plain constructor call.
+struct ExtrasMaker {
+  static constexpr int kN = 7;
+  PyObject* cls = nullptr;
+  PyObject* descr[kN] = {};
+  bool direct = false;
+
+  explicit ExtrasMaker(PyObject* c) : cls(c) {
+    static const char* names[kN] = {"ready_condition", "capacity",         "allocatable",     "unschedulable",
+                                    "health_annotation", "internal_ip", "health_condition"};
+    if (!PyType_Check(c)) return;
+    PyTypeObject* t = reinterpret_cast<PyTypeObject*>(c);
+    if (t->tp_init == nullptr || t->tp_alloc == nullptr) return;
+    for (int i = 0; i < kN; ++i) {
+      PyObject* d = PyObject_GetAttrString(c, names[i]);
+      if (!d) {
+        PyErr_Clear();
+        return;
+      }
+      descr[i] = d;
+      if (strcmp(Py_TYPE(d)->tp_name, "member_descriptor") != 0 || Py_TYPE(d)->tp_descr_set == nullptr) return;
+    }
+    direct = true;
+  }
+  ExtrasMaker(const ExtrasMaker&) = delete;
+  ExtrasMaker& operator=(const ExtrasMaker&) = delete;
+  ~ExtrasMaker() {
+    for (PyObject* d : descr) Py_XDECREF(d);
+  }
+  // new reference or nullptr (Python error set)
+  PyObject* make(PyObject* const (&vals)[kN]) {
+    if (!direct)
+      return PyObject_CallFunctionObjArgs(cls, vals[0], vals[1], vals[2], vals[3], vals[4], vals[5], vals[6], nullptr);
+    PyTypeObject* t = reinterpret_cast<PyTypeObject*>(cls);
+    PyObject* o = t->tp_alloc(t, 0);
+    if (!o) return nullptr;
+    for (int i = 0; i < kN; ++i) {
+      if (Py_TYPE(descr[i])->tp_descr_set(descr[i], o, vals[i]) < 0) {
+        Py_DECREF(o);
+        return nullptr;
+      }
+    }
+    return o;
+  }
+};
+
 void emit_node(const NodeRec& r, const std::vector<PyObject*>& pykeys, bool use_alloc, bool want_extras,
-               PyObject* extras_cls, int annot_mode, PageOut& out, std::string& scratch) {
+               ExtrasMaker& extras, int annot_mode, PageOut& out, StrCache& cache, std::string& scratch) {
   if (!r.is_obj) return;
   long long total = 0;
   Ref bd(breakdown(pykeys, use_alloc ? r.alloc : r.cap, &total, scratch));
@@ -1018,8 +1125,8 @@ void emit_node(const NodeRec& r, const std::vector<PyObject*>& pykeys, bool use_
   if (!info) throw Fallback{"oom"};
   Ref hi(info);
   Ref name(r.meta_obj ? sraw_obj(r.name, scratch) : PyUnicode_FromStringAndSize("", 0));
-  Ref labels(labels_dict(r, scratch));
-  Ref taints(taints_list(r, scratch));
+  Ref labels(labels_dict(r, cache, scratch));
+  Ref taints(taints_list(r, cache, scratch));
   Ref gpus(PyLong_FromLongLong(total));
   if (!name.o || !gpus.o) throw Fallback{"oom"};
   if (PyDict_SetItem(info, k_name, name.o) < 0 || PyDict_SetItem(info, k_ready, r.ready ? Py_True : Py_False) < 0 ||
@@ -1045,9 +1152,14 @@ void emit_node(const NodeRec& r, const std::vector<PyObject*>& pykeys, bool use_
     health_str.reset(make_str(r.health_raw, scratch));
   Ref ip;
   if (r.have_ip) ip.reset(make_str(r.ip, scratch));
-  Ref ex(PyObject_CallFunctionObjArgs(extras_cls, r.ready ? Py_True : Py_False, capd.o, allocd.o,
-                                      r.unschedulable ? Py_True : Py_False, health_str.o ? health_str.o : Py_None,
-                                      ip.o ? ip.o : Py_None, hc.o ? hc.o : Py_None, nullptr));
+  PyObject* const vals[ExtrasMaker::kN] = {r.ready ? Py_True : Py_False,
+                                            capd.o,
+                                            allocd.o,
+                                            r.unschedulable ? Py_True : Py_False,
+                                            health_str.o ? health_str.o : Py_None,
+                                            ip.o ? ip.o : Py_None,
+                                            hc.o ? hc.o : Py_None};
+  Ref ex(extras.make(vals));
   if (!ex.o) {
     PyErr_Clear();
     throw Fallback{"NodeExtras()"};
@@ -1116,8 +1228,10 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
     try {
       if (!out.gpu_nodes.o || !out.ready_nodes.o || !out.extras.o) throw Fallback{"oom"};
       std::string& scratch = ctx.scratch;
+      StrCache cache;
+      ExtrasMaker maker(extras_cls);
       for (const NodeRec& r : p1.items)
-        emit_node(r, pykeys, use_alloc, want_extras, extras_cls, annot_mode, out, scratch);
+        emit_node(r, pykeys, use_alloc, want_extras, maker, annot_mode, out, cache, scratch);
       out.items = static_cast<Py_ssize_t>(p1.items.size());
       if (p1.have_cont) out.cont.reset(make_str(p1.cont, scratch));
     } catch (const Fallback& f) {

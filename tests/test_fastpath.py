@@ -181,3 +181,43 @@ def test_skipped_subtrees_with_escapes(junk, pad, ascii_only):
     if assert_same(body.encode()) == "native":
         r, _ = native_scan(body.encode())
         assert len(r.gpu_nodes) == 2
+
+
+def test_string_cache_overflow_escapes_and_long_values():
+    """Pass 2 shares repeated short label/taint strings through a per-page cache: a page with more
+    distinct strings than the cache holds, escaped and long (uncached) strings, and repeats of each,
+    must still equal the Python path."""
+    items = []
+    for i in range(700):
+        labels = {f"k{i}": f"v{i}", "shared/key": "shared-value", "esc\\u00e9\"q": "a\\nb",
+                  "long": "x" * (90 + i % 20), f"dup{i % 3}": "é" * (i % 4)}
+        node = fixtures.realistic_node(f"n{i}", gpu_count=1 + i % 2, ready=i % 5 != 0)
+        node["metadata"]["labels"] = labels
+        node["spec"]["taints"] = [{"key": "amd.com/gpu", "value": None if i % 2 else f"t{i}", "effect": "NoSchedule"}]
+        items.append(node)
+    for ascii_only in (True, False):
+        body = json.dumps({"kind": "NodeList", "metadata": {"continue": "tok"}, "items": items},
+                          ensure_ascii=ascii_only).encode()
+        assert assert_same(body) != "fallback"
+    a, _ = native_scan(body)
+    # shared strings really are shared objects, distinct ones stay distinct
+    l0, l1 = a.gpu_nodes[1]["labels"], a.gpu_nodes[2]["labels"]
+    k0 = [k for k in l0 if k == "shared/key"][0]
+    k1 = [k for k in l1 if k == "shared/key"][0]
+    assert k0 is k1 and l0["k1"] == "v1" and l1["k2"] == "v2"
+
+
+def test_node_extras_built_without_init_has_every_slot():
+    body = json.dumps({"items": [fixtures.realistic_node("a", gpu_count=2)]}).encode()
+    a, _ = native_scan(body)
+    ex = a.extras[0]
+    assert type(ex) is NodeExtras
+    for slot in NodeExtras.__slots__:
+        getattr(ex, slot)  # AttributeError if a slot was left unset
+
+    class Custom:  # not a __slots__ type with member descriptors: the constructor path is used
+        def __init__(self, *args):
+            self.args = args
+    r = ScanResult()
+    ext.scan_nodelist(body, r, GPU_RESOURCE_KEYS, False, True, HEALTH_ANNOTATION, Custom, HEALTH_CONDITION, 2)
+    assert isinstance(r.extras[0], Custom) and len(r.extras[0].args) == 7
