@@ -226,7 +226,13 @@ PyObject* make_str(const RawStr& s, std::string& scratch) {
 // insertion reuses the cached hash).  Keys point into the page buffer, alive for the whole call.
 class StrCache {
  public:
-  StrCache() : slots_(kSlots) {}
+  // sized for the page: ~30 shared strings plus a few unique ones per node, at most half full
+  explicit StrCache(size_t items) {
+    size_t want = 2 * (32 + 4 * items), n = 64;
+    while (n < want && n < kMaxSlots) n <<= 1;
+    mask_ = n - 1;
+    slots_.resize(n);
+  }
   StrCache(const StrCache&) = delete;
   StrCache& operator=(const StrCache&) = delete;
   ~StrCache() {
@@ -238,7 +244,7 @@ class StrCache {
     if (s.esc || n > kMaxLen) return make_str(s, scratch);
     uint64_t h = 1469598103934665603ULL;  // FNV-1a
     for (size_t i = 0; i < n; ++i) h = (h ^ static_cast<unsigned char>(s.b[i])) * 1099511628211ULL;
-    size_t i = static_cast<size_t>(h) & (kSlots - 1);
+    size_t i = static_cast<size_t>(h) & mask_;
     for (;;) {
       Slot& e = slots_[i];
       if (!e.obj) break;
@@ -246,10 +252,10 @@ class StrCache {
         Py_INCREF(e.obj);
         return e.obj;
       }
-      i = (i + 1) & (kSlots - 1);
+      i = (i + 1) & mask_;
     }
     PyObject* o = make_str(s, scratch);
-    if (used_ < kSlots / 2) {
+    if (used_ < (mask_ + 1) / 2) {
       Slot& e = slots_[i];
       e.hash = h;
       e.b = s.b;
@@ -262,7 +268,7 @@ class StrCache {
   }
 
  private:
-  static constexpr size_t kSlots = 2048, kMaxLen = 96;
+  static constexpr size_t kMaxSlots = 4096, kMaxLen = 96;
   struct Slot {
     uint64_t hash = 0;
     const char* b = nullptr;
@@ -270,6 +276,7 @@ class StrCache {
     PyObject* obj = nullptr;
   };
   std::vector<Slot> slots_;
+  size_t mask_ = 0;
   size_t used_ = 0;
 };
 
@@ -1228,7 +1235,7 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
     try {
       if (!out.gpu_nodes.o || !out.ready_nodes.o || !out.extras.o) throw Fallback{"oom"};
       std::string& scratch = ctx.scratch;
-      StrCache cache;
+      StrCache cache(p1.items.size());
       ExtrasMaker maker(extras_cls);
       for (const NodeRec& r : p1.items)
         emit_node(r, pykeys, use_alloc, want_extras, maker, annot_mode, out, cache, scratch);
