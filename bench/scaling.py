@@ -79,11 +79,11 @@ def main():
             from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
             write_kubeconfig(kc, url)
             reps = args.reps if n < 1000 else max(7, args.reps // 5)
-            row = {"nodes": n, "ours_ms": round(ours(url, reps, 5, 500), 3),
-                   "ours_unpaginated_ms": round(ours(url, reps, 5, 0), 3) if n >= 1000 else None}
+            row = {"nodes": n, "ours_ms": round(ours(url, reps, 20, 500), 3),
+                   "ours_unpaginated_ms": round(ours(url, reps, 20, 0), 3) if n >= 1000 else None}
             if os.path.exists(REF):
                 code = REF_TIMER.format(stubs=os.path.join(REPO, "tests", "refstub"), ref=REF, kc=kc, reps=reps,
-                                        warm=3)
+                                        warm=20)
                 p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=900)
                 row["reference_ms"] = round(json.loads(p.stdout.strip().splitlines()[-1])["median_ms"], 3) \
                     if p.returncode == 0 else None
