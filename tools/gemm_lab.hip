@@ -270,25 +270,6 @@ __device__ __forceinline__ void v4_piece(unsigned char* lds_stage, const __bf16*
   __builtin_amdgcn_global_load_lds(gp, (lds_void_t*)l, 16, 0, 0);
 }
 
-// ablation helper: the same global reads as v4_piece, into a throw-away VGPR quad instead of LDS
-// `sink` must stay live (and is only read after vmcnt(0)): the load returns asynchronously into it.
-__device__ __forceinline__ void v4_piece_reg(u32x4& sink, const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                                             int K, int kt, int region, int i, int wid, int lane) {
-  const int rsub = lane >> 3, phys = lane & 7;
-  const int g = wid * 2 + i;
-  int row0;
-  if (region == 0 || region == 3) {
-    row0 = (g >> 3) * 128 + (region == 0 ? 0 : 64) + (g & 7) * 8;
-  } else {
-    row0 = (g >> 2) * 64 + (region == 1 ? 0 : 32) + (g & 3) * 8;
-  }
-  const int row = row0 + rsub;
-  const int c = phys ^ ((row >> 1) & 7);
-  const bool is_a = region == 0 || region == 3;
-  const __bf16* gp = (is_a ? A : Bt) + static_cast<size_t>(row) * K + kt * BK + c * 8;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(sink) : "v"(gp) : "memory");
-}
-
 template <bool PRIO>
 __global__ void __launch_bounds__(V2_THREADS, 1)
 gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N, int K) {
@@ -409,7 +390,7 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
 // tile t+2's R0 R1 R2 pieces (6) were issued after tile t+1's last one -> vmcnt(6).
 // ABL (timing ablations, wrong results): bit 0 = no LDS-DMA in the loop, bit 1 = no barriers in the loop,
 // bit 2 = no vmcnt waits in the loop
-template <bool PRIO, int ABL = 0>
+template <bool PRIO, int ABL = 0, int GM = 4>
 __global__ void __launch_bounds__(V2_THREADS, 1)
 gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -421,7 +402,7 @@ gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
   }
-  constexpr int GROUP_M = 4;
+  constexpr int GROUP_M = GM;
   const int group = bid / (GROUP_M * tiles_n);
   const int first_m = group * GROUP_M;
   const int gsize = min(tiles_m - first_m, GROUP_M);
@@ -449,7 +430,6 @@ gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
   if (wr == 1) SLOT_BARRIER();
 
   bf16x8 af[4][2], b0[2][2], b1[2][2];
-  u32x4 sink = {0u, 0u, 0u, 0u};
   for (int kt = 0; kt < KT; ++kt) {
     unsigned char* cur = smem + (kt & 1) * V2_STAGE_BYTES;
     unsigned char* nxt = smem + ((kt + 1) & 1) * V2_STAGE_BYTES;
@@ -458,13 +438,8 @@ gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     const bool pre = kt + 2 < KT;
     // phase 0 (+ tile kt+1's R3 into the other buffer; tile 1 came whole with the prologue)
     if (!(ABL & 1) && kt >= 1 && kt + 1 < KT) {
-      if (ABL & 8) {
-        v4_piece_reg(sink, Ab, Bb, K, kt + 1, 3, 0, wid, lane);
-        v4_piece_reg(sink, Ab, Bb, K, kt + 1, 3, 1, wid, lane);
-      } else {
-        v4_piece(nxt, Ab, Bb, K, kt + 1, 3, 0, wid, lane);
-        v4_piece(nxt, Ab, Bb, K, kt + 1, 3, 1, wid, lane);
-      }
+      v4_piece(nxt, Ab, Bb, K, kt + 1, 3, 0, wid, lane);
+      v4_piece(nxt, Ab, Bb, K, kt + 1, 3, 1, wid, lane);
     }
 #pragma unroll
     for (int n = 0; n < 2; ++n)
@@ -490,17 +465,10 @@ gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     if (!(ABL & 2)) SLOT_BARRIER();
     // phase 2: restage R0, R1 of this buffer with tile kt+2
     if (!(ABL & 1) && pre) {
-      if (ABL & 8) {
-        v4_piece_reg(sink, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
-        v4_piece_reg(sink, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
-        v4_piece_reg(sink, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
-        v4_piece_reg(sink, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
-      } else {
-        v4_piece(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
-        v4_piece(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
-        v4_piece(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
-        v4_piece(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
-      }
+      v4_piece(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
+      v4_piece(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
+      v4_piece(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
+      v4_piece(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -513,13 +481,8 @@ gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     if (!(ABL & 2)) SLOT_BARRIER();
     // phase 3: restage R2; retire tile kt+1
     if (!(ABL & 1) && pre) {
-      if (ABL & 8) {
-        v4_piece_reg(sink, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
-        v4_piece_reg(sink, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
-      } else {
-        v4_piece(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
-        v4_piece(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
-      }
+      v4_piece(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
+      v4_piece(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
       if (!(ABL & 4)) __builtin_amdgcn_s_waitcnt(0x3f76);  // vmcnt(6)
     } else {
       if (!(ABL & 4)) __builtin_amdgcn_s_waitcnt(0x3f70);
@@ -529,10 +492,6 @@ gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     if (!(ABL & 2)) SLOT_BARRIER();
   }
   if (wr == 0) SLOT_BARRIER();
-  if (ABL & 8) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if ((sink.x ^ sink.y ^ sink.z ^ sink.w) == 0x9e3779b9u) acc[0][0][0] += 1.0f;  // keeps `sink` live
-  }
   const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 64;
 #pragma unroll
   for (int m = 0; m < 8; ++m)
@@ -761,9 +720,18 @@ int main(int argc, char** argv) {
     check("v6", ms);
     ms = time_ms([&] { hipLaunchKernelGGL(gemm_v6_kernel<true>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("v6+prio", ms);
-    CK(hipFuncSetAttribute((const void*)gemm_v5_kernel<false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
-    ms = time_ms([&] { hipLaunchKernelGGL((gemm_v5_kernel<false, 8>), dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
-    check("v5-ablation-reg-loads", ms);
+    CK(hipFuncSetAttribute((const void*)gemm_v5_kernel<false, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    CK(hipFuncSetAttribute((const void*)gemm_v5_kernel<false, 0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    CK(hipFuncSetAttribute((const void*)gemm_v5_kernel<false, 0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    CK(hipFuncSetAttribute((const void*)gemm_v5_kernel<false, 0, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    ms = time_ms([&] { hipLaunchKernelGGL((gemm_v5_kernel<false, 0, 1>), dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
+    check("v5-groupm1", ms);
+    ms = time_ms([&] { hipLaunchKernelGGL((gemm_v5_kernel<false, 0, 2>), dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
+    check("v5-groupm2", ms);
+    ms = time_ms([&] { hipLaunchKernelGGL((gemm_v5_kernel<false, 0, 8>), dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
+    check("v5-groupm8", ms);
+    ms = time_ms([&] { hipLaunchKernelGGL((gemm_v5_kernel<false, 0, 16>), dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
+    check("v5-groupm16", ms);
     CK(hipFuncSetAttribute((const void*)gemm_v5_kernel<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     ms = time_ms([&] { hipLaunchKernelGGL((gemm_v5_kernel<false, 4>), dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("v5-ablation-no-vmcnt", ms);
