@@ -66,6 +66,20 @@ def _own_gpu(gpus, local_rank, cuda):
     return mine
 
 
+def _fabric_check(world, local_rank, cuda):
+    """Untimed: all-reduce bus bandwidth + correctness over the job's process group (RCCL over xGMI
+    on GPUs, gloo on CPU) -- the node-fabric health the passive probe can only infer from link state."""
+    from k8s_gpu_node_checker_amd.parallel import collectives
+    import torch
+    sizes = [64 << 20, 256 << 20] if cuda else [1 << 20]
+    try:
+        rows = collectives.allreduce_bench(sizes, iters=10, warmup=3,
+                                           device=torch.device(f"cuda:{local_rank}") if cuda else None)
+        return {"backend": "nccl(rccl)" if cuda else "gloo", "rows": rows, **collectives.verdict(rows, world)}
+    except Exception as e:  # report, never lose the benchmark line over the fabric check
+        return {"backend": "nccl(rccl)" if cuda else "gloo", "pass": False, "detail": f"{type(e).__name__}: {e}"}
+
+
 def _pctl(xs, q):
     xs = sorted(xs)
     if not xs:
@@ -84,6 +98,8 @@ def main() -> int:
     ap.add_argument("--diag-level", type=int, default=1, choices=(0, 1, 2))
     ap.add_argument("--slack", action="store_true", help="also POST the Slack report to a local sink each step")
     ap.add_argument("--page-size", type=int, default=500)
+    ap.add_argument("--no-fabric-check", dest="fabric_check", action="store_false",
+                    help="skip the untimed all-reduce fabric check (world > 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,6 +185,7 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
     diag = {}
     for g in rep.get("gpus") or []:
         diag = g.get("diag") or {}
+    fabric = _fabric_check(world, local_rank, cuda) if world > 1 and args.fabric_check else None
     barrier()
 
     opts = CheckOptions(json=True, page_size=args.page_size, health_policy="auto",
@@ -244,6 +261,7 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
             "health": {s: verdicts.count(s) for s in sorted(set(verdicts))},
             "backend": fastpath.backend(),
             "probe": {"source": probe_source, "setup_ms": round(probe_ms, 1), "diag": diag},
+            "fabric": fabric,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

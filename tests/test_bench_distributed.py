@@ -54,6 +54,9 @@ def test_bench_torchrun_two_ranks_gloo():
     d = last_json(p.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["check_ok"] and d["health"] == {"healthy": 2}
+    fab = d["fabric"]  # untimed all-reduce check over the job's process group (gloo here, RCCL on GPUs)
+    assert fab["pass"] and fab["world"] == 2 and fab["backend"] == "gloo"
+    assert all(r["correct"] for r in fab["rows"])
 
 
 def test_bench_sweep_mode_and_slack():
