@@ -20,8 +20,7 @@ SURVEY §6 takeaway 2: at 1000 nodes (5.9 MB NodeList) parse + projection is
 from __future__ import annotations
 
 import json
-import os
-from typing import Any, Dict, Optional, Sequence, Tuple
+from typing import Any, Optional, Sequence, Tuple
 
 from ..models.node import HEALTH_ANNOTATION, HEALTH_CONDITION, NodeExtras, ScanResult, scan_items
 from ..models.resources import GPU_RESOURCE_KEYS

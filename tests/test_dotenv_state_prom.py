@@ -2,7 +2,6 @@
 import json
 import os
 
-import pytest
 
 from k8s_gpu_node_checker_amd.utils import dotenv, prom, statefile
 

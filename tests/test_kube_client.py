@@ -1,5 +1,4 @@
 """kube-apiserver client: pagination, retries/backoff, errors, gzip, chunked, TLS (SURVEY §7.2 layer 2)."""
-import json
 import os
 import subprocess
 
@@ -10,7 +9,7 @@ from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
 from k8s_gpu_node_checker_amd.kube.errors import ApiException, TransportError
 from k8s_gpu_node_checker_amd.models.node import scan_items
 from k8s_gpu_node_checker_amd.testing import fixtures
-from k8s_gpu_node_checker_amd.testing.mock_apiserver import MockApiServer, MockConfig
+from k8s_gpu_node_checker_amd.testing.mock_apiserver import MockApiServer
 
 
 def names(res):

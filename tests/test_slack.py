@@ -3,7 +3,6 @@ import io
 import json
 import time
 
-import pytest
 
 from k8s_gpu_node_checker_amd.notify import slack
 from k8s_gpu_node_checker_amd.utils.backoff import Backoff, parse_retry_after
