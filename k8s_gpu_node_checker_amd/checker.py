@@ -200,10 +200,18 @@ def check_and_report(cluster: ClusterConnection, opts: CheckOptions, out: Option
 
 def _check_and_report(cluster: ClusterConnection, opts: CheckOptions, out: Optional[TextIO],
                       err: Optional[TextIO], tracer: Optional[Tracer]) -> CheckResult:
+    result = run_check(cluster, opts, tracer)
+    emit_report(result, opts, out, err)
+    return result
+
+
+def emit_report(result: CheckResult, opts: CheckOptions, out: Optional[TextIO] = None,
+                err: Optional[TextIO] = None) -> None:
+    """Slack (on a worker thread) + JSON/text report of a finished check, in the reference's stream
+    order (``:262-287``); shared by one-shot checks and the event-driven watcher (``kube/watch.py``)."""
     from .notify import slack
     out = out if out is not None else sys.stdout
     err = err if err is not None else sys.stderr
-    result = run_check(cluster, opts, tracer)
     tr = result.tracer
     gpu_nodes, ready = result.gpu_nodes, result.ready_gpu_nodes
 
@@ -250,7 +258,6 @@ def _check_and_report(cluster: ClusterConnection, opts: CheckOptions, out: Optio
     if opts.trace:
         tr.finish()
         print(f"[trace] {tr.format()} backend={_backend()}", file=err)
-    return result
 
 
 def _backend() -> str:

@@ -73,7 +73,13 @@ def build_parser(show_all: bool = False, prog: Optional[str] = None) -> argparse
     x.add_argument("--state-file", help=h("직전 결과 저장 파일 (알림 중복 제거)"))
     x.add_argument("--watch", type=float, default=0.0, help=h("N초마다 반복 점검 (0 = 한 번, 기본)"))
     x.add_argument("--watch-count", type=int, default=0,
-                   help=h("--watch 반복 횟수 (0 = 무제한, 기본); 종료 코드는 마지막 점검의 것"))
+                   help=h("--watch 반복 횟수 / --watch-events 보고 횟수 (0 = 무제한, 기본); 종료 코드는 마지막 점검의 것"))
+    x.add_argument("--watch-events", action="store_true",
+                   help=h("이벤트 기반 감시: LIST 한 번 후 watch 스트림을 따라가며 상태가 바뀔 때만 보고"))
+    x.add_argument("--watch-debounce", type=float, default=0.2,
+                   help=h("--watch-events: 이 시간(초) 안에 도착한 이벤트를 한 번에 평가 (기본: 0.2)"))
+    x.add_argument("--watch-duration", type=float, default=0.0,
+                   help=h("--watch-events: N초 후 종료 (0 = 무제한, 기본)"))
     return p
 
 
@@ -104,7 +110,6 @@ def _load_cluster(args: argparse.Namespace):
 
 def _run_once(args: argparse.Namespace) -> int:
     """Reference ``main`` body (``:316-327``) for one iteration."""
-    import json
     try:
         from .checker import CheckOptions, check_and_report
         cluster = _load_cluster(args)
@@ -123,26 +128,79 @@ def _run_once(args: argparse.Namespace) -> int:
             write_textfile(args.prometheus_textfile, result)
         return result.exit_code
     except Exception as e:
-        if getattr(args, "json", False):
-            print(json.dumps({"error": str(e)}, ensure_ascii=False))
-        else:
-            import traceback
-            print(f"에러: {e}", file=sys.stderr)
-            traceback.print_exc()
-        if args.prometheus_textfile:
-            try:
-                from .utils.prom import write_error_textfile
-                write_error_textfile(args.prometheus_textfile, str(e))
-            except Exception:
-                pass
-        return 1
+        return _report_error(args, e)
+
+
+def _report_error(args: argparse.Namespace, e: BaseException) -> int:
+    """Reference error reporter (``:319-327``): JSON one-liner on stdout or message + traceback."""
+    import json
+    if getattr(args, "json", False):
+        print(json.dumps({"error": str(e)}, ensure_ascii=False))
+    else:
+        import traceback
+        print(f"에러: {e}", file=sys.stderr)
+        traceback.print_exc()
+    if args.prometheus_textfile:
+        try:
+            from .utils.prom import write_error_textfile
+            write_error_textfile(args.prometheus_textfile, str(e))
+        except Exception:
+            pass
+    return 1
 
 
 def main(argv: Optional[List[str]] = None) -> int:
     args = parse_args(argv)
+    if args.watch_events:
+        return _watch_events(args)
     if args.watch and args.watch > 0:
         return _watch(args)
     return _run_once(args)
+
+
+def _watch_events(args: argparse.Namespace) -> int:
+    """``--watch-events``: LIST once, follow the watch stream, report each change of outcome.
+
+    Every report is a complete one-shot report (same JSON/text, same exit-code rule); Slack goes
+    through the ``--slack-on-change`` de-dup gate (first report, changes, one recovery notice under
+    ``--slack-only-on-error``).  Ends after ``--watch-count`` reports, ``--watch-duration`` seconds
+    or Ctrl-C, with the exit code of the last report.
+    """
+    last = {"code": 0}
+    try:
+        from .checker import CheckOptions, CheckResult, apply_health, emit_report
+        from .kube.watch import NodeWatcher
+        from .utils import statefile
+        from .utils.timing import NullTracer, Tracer
+        cluster = _load_cluster(args)
+        opts = CheckOptions.from_args(args)
+        prev = statefile.load(args.state_file) if args.state_file else None
+        memo = {"prev": prev}
+        only = opts.slack_only_on_error
+        opts.slack_gate = lambda result: statefile.should_notify(memo["prev"], result, only)
+        opts.slack_only_on_error = False  # the gate decides (a recovery must be able to send)
+
+        def evaluate(scan):
+            tr = Tracer() if (opts.trace or opts.json_extended) else NullTracer()
+            return CheckResult(scan, apply_health(scan, opts, tr), tr)
+
+        def report(result) -> None:
+            emit_report(result, opts)
+            memo["prev"] = {"fingerprint": statefile.fingerprint(result), "exit_code": result.exit_code}
+            if args.state_file:
+                statefile.save(args.state_file, result, prev)
+            if args.prometheus_textfile:
+                from .utils.prom import write_textfile
+                write_textfile(args.prometheus_textfile, result)
+            last["code"] = result.exit_code
+
+        NodeWatcher(cluster, opts, debounce=args.watch_debounce).run(
+            evaluate, report, max_reports=args.watch_count, duration=args.watch_duration)
+        return last["code"]
+    except KeyboardInterrupt:
+        return last["code"]
+    except Exception as e:
+        return _report_error(args, e)
 
 
 def _watch(args: argparse.Namespace) -> int:

@@ -12,6 +12,10 @@ The single ``list_node()`` call is the reference's only cluster seam
 * fault injection: fixed status (``403``/``500``), ``fail_first`` transient
   errors with ``Retry-After``, an expired-``continue`` 410, response delay,
   connection reset
+* ``?watch=1`` event streams (chunked, one JSON event per line): ADDED /
+  MODIFIED / DELETED from every change (``set_nodes``, PATCH, ``add_node``,
+  ``delete_node``), BOOKMARKs with ``allowWatchBookmarks``, ``timeoutSeconds``,
+  and the 410 ``ERROR`` event for a ``resourceVersion`` older than the log
 * request log for assertions
 
 Run standalone (used by ``bench.py`` in its own process, so the client under
@@ -37,18 +41,74 @@ from urllib.parse import parse_qs, unquote, urlsplit
 from . import fixtures
 
 
+def _name(node: Dict[str, Any]) -> Optional[str]:
+    return (node.get("metadata") or {}).get("name")
+
+
 class ClusterState:
+    EVENT_LOG = 10000  # events kept for watchers; older resourceVersions get 410 Gone
+
     def __init__(self, nodes: List[Dict[str, Any]]):
         self.lock = threading.Lock()
+        self.changed = threading.Condition(self.lock)
         self.nodes = nodes
         self.rv = 1000
         self._cache: Dict[Any, bytes] = {}
+        self.events: List[Any] = []  # (rv, type, node snapshot)
+        self.closed = False
+
+    def _event(self, kind: str, node: Dict[str, Any]) -> None:
+        """Record one change (lock held): bump the resourceVersion, stamp it on the node, wake watchers."""
+        self.rv += 1
+        if isinstance(node.get("metadata"), dict):
+            node["metadata"]["resourceVersion"] = str(self.rv)
+        self.events.append((self.rv, kind, copy.deepcopy(node)))
+        if len(self.events) > self.EVENT_LOG:
+            del self.events[:len(self.events) - self.EVENT_LOG]
+        self._cache.clear()
+        self.changed.notify_all()
 
     def set_nodes(self, nodes: List[Dict[str, Any]]) -> None:
+        """Replace the cluster; watchers see the difference as DELETED / ADDED / MODIFIED events."""
         with self.lock:
+            old = {_name(n): n for n in self.nodes}
+            new = {_name(n): n for n in nodes}
+            for name, n in old.items():
+                if name not in new:
+                    self._event("DELETED", n)
+            for name, n in new.items():
+                if name not in old:
+                    self._event("ADDED", n)
+                elif json.dumps(n, sort_keys=True) != json.dumps(old[name], sort_keys=True):
+                    self._event("MODIFIED", n)
             self.nodes = nodes
             self.rv += 1
             self._cache.clear()
+
+    def add_node(self, node: Dict[str, Any]) -> None:
+        with self.lock:
+            self.nodes.append(node)
+            self._event("ADDED", node)
+
+    def delete_node(self, name: str) -> bool:
+        with self.lock:
+            for i, n in enumerate(self.nodes):
+                if _name(n) == name:
+                    del self.nodes[i]
+                    self._event("DELETED", n)
+                    return True
+            return False
+
+    def events_after(self, rv: int) -> Optional[List[Any]]:
+        """Events newer than ``rv`` (lock held); ``None`` if ``rv`` is older than the log."""
+        if self.events and rv < self.events[0][0] - 1:
+            return None
+        return [e for e in self.events if e[0] > rv]
+
+    def close(self) -> None:
+        with self.lock:
+            self.closed = True
+            self.changed.notify_all()
 
     def page(self, limit: int, start: int) -> bytes:
         key = (limit, start, self.rv)
@@ -87,8 +147,7 @@ class ClusterState:
                     else:
                         have.append(c)
             _merge_patch(node, patch)
-            self.rv += 1
-            self._cache.clear()
+            self._event("MODIFIED", node)
             return copy.deepcopy(node)
 
 
@@ -106,7 +165,7 @@ class MockConfig:
     def __init__(self, token: Optional[str] = None, status: Optional[int] = None, fail_first: int = 0,
                  fail_status: int = 503, retry_after: Optional[str] = None, delay: float = 0.0,
                  expire_continue: bool = False, reset: bool = False, gzip: bool = False,
-                 chunked: bool = False):
+                 chunked: bool = False, bookmark_interval: float = 1.0):
         self.token = token
         self.status = status
         self.fail_first = fail_first
@@ -117,6 +176,7 @@ class MockConfig:
         self.reset = reset
         self.gzip = gzip
         self.chunked = chunked
+        self.bookmark_interval = bookmark_interval
 
 
 class _Handler(BaseHTTPRequestHandler):
@@ -183,6 +243,9 @@ class _Handler(BaseHTTPRequestHandler):
         path = parts.path
         if path == "/api/v1/nodes":
             q = parse_qs(parts.query)
+            if q.get("watch", ["0"])[0] in ("1", "true"):
+                self._watch(q)
+                return
             limit = int(q.get("limit", ["0"])[0] or 0)
             cont = q.get("continue", [None])[0]
             start = 0
@@ -220,6 +283,73 @@ class _Handler(BaseHTTPRequestHandler):
             self._send(200, b"ok")
             return
         self._send(404, self._status_body(404, "NotFound", "not found"), reason="Not Found")
+
+    def _watch(self, q: Dict[str, List[str]]) -> None:
+        """Stream node events (chunked, one JSON object per line) like the apiserver's watch."""
+        st = self.server.state
+        timeout = float(q.get("timeoutSeconds", ["30"])[0] or 30)
+        bookmarks = q.get("allowWatchBookmarks", ["false"])[0] in ("1", "true")
+        rv_param = q.get("resourceVersion", [""])[0]
+        self.send_response(200)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Transfer-Encoding", "chunked")
+        self.end_headers()
+
+        def send(ev: Dict[str, Any]) -> None:
+            line = json.dumps(ev, separators=(",", ":")).encode() + b"\n"
+            self.wfile.write(b"%x\r\n" % len(line) + line + b"\r\n")
+            self.wfile.flush()
+
+        with st.lock:
+            if rv_param in ("", "0"):  # "any": synthetic ADDED for the current state, then follow
+                initial = [("ADDED", copy.deepcopy(n)) for n in st.nodes]
+                last = st.rv
+            else:
+                initial = []
+                last = int(rv_param)
+                if st.events_after(last) is None:
+                    initial = None
+        try:
+            if initial is None:
+                send({"type": "ERROR", "object": {"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                                  "message": f"too old resource version: {rv_param}",
+                                                  "reason": "Expired", "code": 410}})
+            else:
+                for kind, node in initial:
+                    send({"type": kind, "object": node})
+                deadline = time.monotonic() + timeout
+                next_bookmark = time.monotonic() + self.server.cfg.bookmark_interval
+                while True:
+                    now = time.monotonic()
+                    if now >= deadline:
+                        break
+                    with st.lock:
+                        evs = st.events_after(last)
+                        if evs == [] and not st.closed:
+                            st.changed.wait(min(deadline, next_bookmark if bookmarks else deadline) - now)
+                            evs = st.events_after(last)
+                        closed = st.closed
+                        cur = st.rv
+                    if closed:
+                        break
+                    if evs is None:
+                        send({"type": "ERROR", "object": {"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                                          "message": "too old resource version", "reason": "Expired",
+                                                          "code": 410}})
+                        break
+                    for rv, kind, node in evs:
+                        send({"type": kind, "object": node})
+                        last = rv
+                    if bookmarks and time.monotonic() >= next_bookmark:
+                        send({"type": "BOOKMARK", "object": {"kind": "Node", "apiVersion": "v1",
+                                                             "metadata": {"resourceVersion": str(max(cur, last))}}})
+                        last = max(cur, last)
+                        next_bookmark = time.monotonic() + self.server.cfg.bookmark_interval
+            self.wfile.write(b"0\r\n\r\n")
+            self.wfile.flush()
+        except OSError:
+            pass
+        self.close_connection = True
 
     def do_PATCH(self) -> None:  # noqa: N802
         length = int(self.headers.get("Content-Length") or 0)
@@ -280,6 +410,7 @@ class MockApiServer(ThreadingHTTPServer):
         return self
 
     def stop(self) -> None:
+        self.state.close()  # end open watch streams
         self.shutdown()
         self.server_close()
 

@@ -308,7 +308,7 @@ class Connection:
                 return
         peek(prefix)
 
-    def _read_response(self, method: str, peek=None) -> Response:
+    def _read_head(self) -> Tuple[int, str, List[Tuple[str, str]], Dict[str, str]]:
         while True:
             status_line = self._read_line()
             parts = status_line.split(None, 2)
@@ -325,8 +325,41 @@ class Connection:
                 headers.append((k.decode("latin-1").strip(), v.decode("latin-1").strip()))
             if 100 <= status < 200 and status != 101:
                 continue  # 100-continue / 103 early hints: read the real response
-            break
-        hmap = {k.lower(): v for k, v in headers}
+            return status, reason, headers, {k.lower(): v for k, v in headers}
+
+    def open_stream(self, method: str, path: str, headers: Optional[Dict[str, str]] = None,
+                    read_timeout: Optional[float] = None) -> "Response | LineStream":
+        """Send a request whose 2xx body is a stream of newline-delimited records (a kube watch).
+
+        Returns a :class:`LineStream` for 2xx responses, else the complete :class:`Response`.
+        ``read_timeout`` replaces the connection timeout for the stream's reads.
+        """
+        try:
+            self.connect(path)
+            assert self.sock is not None
+            self.sock.sendall(self._encode(method, path, headers, None))
+            status, reason, hdrs, hmap = self._read_head()
+            if not 200 <= status < 300:
+                return self._finish_body(method, status, reason, hdrs, hmap, None)
+        except HTTPError:
+            self.close()
+            raise
+        except socket.timeout as e:
+            self.close()
+            raise self._fail("timeout", path, e)
+        except OSError as e:
+            self.close()
+            raise self._fail("reset" if isinstance(e, ConnectionResetError) else "aborted", path, e)
+        if read_timeout is not None:
+            self.sock.settimeout(read_timeout)
+        return LineStream(self, status, reason, hdrs, hmap, path)
+
+    def _read_response(self, method: str, peek=None) -> Response:
+        status, reason, headers, hmap = self._read_head()
+        return self._finish_body(method, status, reason, headers, hmap, peek)
+
+    def _finish_body(self, method: str, status: int, reason: str, headers: List[Tuple[str, str]],
+                     hmap: Dict[str, str], peek) -> Response:
         if method == "HEAD" or status in (204, 304):
             body = b""
         elif "chunked" in hmap.get("transfer-encoding", "").lower():
@@ -381,6 +414,108 @@ class Connection:
                 if prefix:
                     peek(prefix)
                 peek = None
+
+
+class LineStream:
+    """The body of a streaming 2xx response, read record by record (``\n``-terminated lines).
+
+    Handles chunked, ``Content-Length`` and close-delimited bodies and gzip.  :meth:`next_line`
+    returns ``None`` when nothing arrived within the read timeout (the stream stays usable: the
+    decoder state lives in buffers, nothing is lost) and raises ``EOFError`` at the end.
+    """
+
+    def __init__(self, conn: Connection, status: int, reason: str, headers: List[Tuple[str, str]],
+                 hmap: Dict[str, str], path: str):
+        self.conn = conn
+        self.status = status
+        self.reason = reason
+        self.headers = headers
+        self.path = path
+        self._chunked = "chunked" in hmap.get("transfer-encoding", "").lower()
+        self._left = int(hmap["content-length"]) if (not self._chunked and "content-length" in hmap) else -1
+        self._chunk_left = 0       # bytes of the current chunk still to take from the wire buffer
+        self._need_size = True     # chunked: expecting a size line next
+        self._done = False
+        self._body = bytearray()   # decoded body bytes not yet returned as lines
+        self._inflate = None
+        if hmap.get("content-encoding", "").lower() == "gzip":
+            import zlib
+            self._inflate = zlib.decompressobj(16 + zlib.MAX_WBITS)
+
+    def _feed(self, data: bytes) -> None:
+        self._body += self._inflate.decompress(data) if self._inflate is not None else data
+
+    def _drain_wire(self) -> None:
+        """Move every complete piece of the wire buffer into the decoded body buffer."""
+        buf = self.conn._buf
+        if not self._chunked:
+            take = len(buf) if self._left < 0 else min(len(buf), self._left)
+            if take:
+                self._feed(bytes(buf[:take]))
+                del buf[:take]
+                if self._left >= 0:
+                    self._left -= take
+            if self._left == 0:
+                self._done = True
+            return
+        while not self._done:
+            if self._need_size:
+                i = buf.find(b"\r\n")
+                if i < 0:
+                    return
+                size = int(bytes(buf[:i]).split(b";", 1)[0].strip() or b"0", 16)
+                del buf[:i + 2]
+                if size == 0:
+                    self._done = True  # trailers (if any) are left unread; the stream is closed after
+                    return
+                self._chunk_left = size
+                self._need_size = False
+            take = min(len(buf), self._chunk_left)
+            if take:
+                self._feed(bytes(buf[:take]))
+                del buf[:take]
+                self._chunk_left -= take
+            if self._chunk_left:
+                return
+            if len(buf) < 2:
+                return
+            del buf[:2]  # CRLF after the chunk
+            self._need_size = True
+
+    def next_line(self) -> Optional[bytes]:
+        while True:
+            i = self._body.find(b"\n")
+            if i >= 0:
+                line = bytes(self._body[:i])
+                del self._body[:i + 1]
+                if line.strip():
+                    return line
+                continue
+            if self._done:
+                if self._body.strip():
+                    line = bytes(self._body)
+                    self._body = bytearray()
+                    return line
+                raise EOFError
+            self._drain_wire()
+            if self._body.find(b"\n") >= 0 or self._done:
+                continue
+            try:
+                got = self.conn._recv_more()
+            except socket.timeout:
+                return None
+            except OSError as e:
+                self.conn.close()
+                raise self.conn._fail("reset" if isinstance(e, ConnectionResetError) else "aborted", self.path, e)
+            if not got:
+                if self._chunked or self._left > 0:
+                    self.conn.close()
+                    raise HTTPError("aborted", "('Connection aborted.', RemoteDisconnected("
+                                               "'Remote end closed connection without response'))")
+                self._done = True
+
+    def close(self) -> None:
+        self.conn.close()
 
 
 def request(url: str, method: str = "GET", headers: Optional[Dict[str, str]] = None, body: Optional[bytes] = None,
