@@ -171,7 +171,7 @@ def serve(agent: Agent, host: str, port: int) -> ThreadingHTTPServer:
     return srv
 
 
-def main(argv: Optional[List[str]] = None) -> int:
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="k8s-gpu-node-agent", description="MI355X node agent (probe + publish)")
     ap.add_argument("--node", default=os.environ.get("NODE_NAME") or socket.gethostname())
     ap.add_argument("--source", choices=("auto", "native", "python", "fixture"), default="auto")
@@ -183,7 +183,11 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--listen", default="0.0.0.0:9464")
     ap.add_argument("--kubeconfig")
     ap.add_argument("--once", action="store_true")
-    args = ap.parse_args(argv)
+    return ap
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    args = build_parser().parse_args(argv)
     pubs = set(args.publish.split(","))
     agent = Agent(args.node, args.source, args.fixture, args.diag_level, args.diag_interval)
     client = None
