@@ -43,6 +43,7 @@ class Agent:
         self.diag_interval = diag_interval
         self.devices = devices
         self._diag_cache: Dict[int, Dict[str, Any]] = {}
+        self._fabric: Optional[Dict[str, Any]] = None
         self._diag_ts = 0.0
         self.last: Optional[Dict[str, Any]] = None
         self._last_condition: Optional[Dict[str, Any]] = None
@@ -68,6 +69,13 @@ class Agent:
         for t in threads:
             t.join()
         self._diag_cache = {d: results[d] for d in devices if d in results}
+        if self.diag_level >= 2 and self.devices is None and len(devices) >= 2:
+            # node-level: every ordered GPU pair over xGMI (after the per-GPU tests, so no contention)
+            try:
+                m = diag.p2p_matrix(devices)
+                self._fabric = {"p2p": {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s")}}
+            except Exception as e:
+                self._fabric = {"p2p": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
         self._diag_ts = now
         return self._diag_cache
 
@@ -88,6 +96,8 @@ class Agent:
                 d = by_bdf.get(str(g.get("bdf", "")).lower(), g.get("index") if not by_bdf else None)
                 if d is not None and diags.get(d):
                     g["diag"] = diags[d]
+            if self._fabric:
+                rep["fabric"] = self._fabric
         verdict = evaluate_report(rep, 0, HealthExpectations())
         rep["state"] = verdict.state
         with self.lock:

@@ -18,6 +18,8 @@
 //   memtest     address-hash patterns written and verified (plus the
 //               bit-inverted pass), mismatches counted with one atomic per
 //               failing 16-byte word.
+//   p2p_copy    xGMI pair check: peer copies between two GPUs of the node,
+//               timed, and the received pattern verified on the destination.
 //
 // C ABI (ctypes, ops/diag.py).  Every HIP call is checked; on failure the
 // function returns a negative code and diag_last_error() says what failed.
@@ -561,6 +563,40 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// Device allocation owned by its device (frees with that device current), for the multi-GPU test.
+struct DevBuf {
+  int device = -1;
+  void* ptr = nullptr;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  hipError_t alloc(int dev, size_t bytes) {
+    device = dev;
+    hipError_t e = hipSetDevice(dev);
+    return e != hipSuccess ? e : hipMalloc(&ptr, bytes);
+  }
+  ~DevBuf() {
+    if (ptr) {
+      int cur = 0;
+      if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(device) == hipSuccess) {
+        (void)hipFree(ptr);
+        (void)hipSetDevice(cur);
+      }
+    }
+  }
+};
+
+hipError_t enable_peer(int from, int to) {
+  hipError_t e = hipSetDevice(from);
+  if (e != hipSuccess) return e;
+  e = hipDeviceEnablePeerAccess(to, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();  // sticky-free: clear it
+    return hipSuccess;
+  }
+  return e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -783,6 +819,77 @@ int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned l
   hipEventDestroy(e1);
   hipFree(p);
   hipFree(dev);
+  return 0;
+}
+
+// xGMI point-to-point check between two GPUs of the node: `iters` copies of `bytes` from `src` to
+// `dst` (hipMemcpyPeerAsync on a src-device stream, peer access enabled both ways when the pair
+// supports it -- on an MI355X hive every pair is one xGMI hop), timed with events; the received
+// buffer is then verified against the address-hash pattern on `dst`.  *peer = 1 if direct peer
+// access was available.  A slow pair (a link trained down or retrying) shows up as an outlier
+// against the node's other pairs; a corrupting one as errors.
+int diag_p2p_copy(int src, int dst, size_t bytes, int iters, double* gbps, unsigned long long* errors, int* peer) {
+  int n = 0;
+  DIAG_CHECK(hipGetDeviceCount(&n));
+  if (src < 0 || dst < 0 || src >= n || dst >= n || src == dst || iters < 1 || bytes < 16) {
+    g_err = "p2p: need two distinct devices, iters >= 1, bytes >= 16";
+    return -2;
+  }
+  int cur = 0;
+  DIAG_CHECK(hipGetDevice(&cur));
+  int can_sd = 0, can_ds = 0;
+  DIAG_CHECK(hipDeviceCanAccessPeer(&can_sd, src, dst));
+  DIAG_CHECK(hipDeviceCanAccessPeer(&can_ds, dst, src));
+  *peer = can_sd && can_ds;
+  if (*peer) {
+    DIAG_CHECK(enable_peer(src, dst));
+    DIAG_CHECK(enable_peer(dst, src));
+  }
+  const size_t nvec = bytes / sizeof(uint4);
+  const size_t nbytes = nvec * sizeof(uint4);
+  DevBuf a, b, cnt;
+  DIAG_CHECK(a.alloc(src, nbytes));
+  DIAG_CHECK(b.alloc(dst, nbytes));
+  DIAG_CHECK(cnt.alloc(dst, 2 * sizeof(unsigned long long)));
+  const uint64_t seed = 0xC0FFEEULL + static_cast<uint64_t>(src) * 131 + static_cast<uint64_t>(dst);
+  // pattern on src, junk on dst
+  DIAG_CHECK(hipSetDevice(src));
+  hipLaunchKernelGGL(mt_write_kernel, dim3(grid_for(src, 4)), dim3(256), 0, nullptr, static_cast<uint4*>(a.ptr), nvec,
+                     seed, 0);
+  DIAG_CHECK(hipGetLastError());
+  DIAG_CHECK(hipDeviceSynchronize());
+  DIAG_CHECK(hipSetDevice(dst));
+  DIAG_CHECK(hipMemset(b.ptr, 0xA5, nbytes));
+  const unsigned long long init[2] = {0ULL, ~0ULL};
+  DIAG_CHECK(hipMemcpy(cnt.ptr, init, sizeof init, hipMemcpyHostToDevice));
+  DIAG_CHECK(hipDeviceSynchronize());
+  // timed copies on a stream of the source device
+  DIAG_CHECK(hipSetDevice(src));
+  hipStream_t st;
+  DIAG_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  DIAG_CHECK(hipEventCreate(&e0));
+  DIAG_CHECK(hipEventCreate(&e1));
+  DIAG_CHECK(hipMemcpyPeerAsync(b.ptr, dst, a.ptr, src, nbytes, st));  // warm-up (maps, engine)
+  DIAG_CHECK(hipEventRecord(e0, st));
+  for (int i = 0; i < iters; ++i) DIAG_CHECK(hipMemcpyPeerAsync(b.ptr, dst, a.ptr, src, nbytes, st));
+  DIAG_CHECK(hipEventRecord(e1, st));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  const float ms = elapsed_ms(e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(st);
+  *gbps = ms > 0.f ? static_cast<double>(iters) * static_cast<double>(nbytes) / (ms * 1e-3) / 1e9 : 0.0;
+  // verify what arrived
+  DIAG_CHECK(hipSetDevice(dst));
+  unsigned long long* c = static_cast<unsigned long long*>(cnt.ptr);
+  hipLaunchKernelGGL(mt_verify_kernel, dim3(grid_for(dst, 4)), dim3(256), 0, nullptr,
+                     static_cast<const uint4*>(b.ptr), nvec, seed, 0, c, c + 1);
+  DIAG_CHECK(hipGetLastError());
+  unsigned long long h[2];
+  DIAG_CHECK(hipMemcpy(h, cnt.ptr, sizeof h, hipMemcpyDeviceToHost));
+  *errors = h[0];
+  DIAG_CHECK(hipSetDevice(cur));
   return 0;
 }
 

@@ -166,7 +166,8 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str],
     if isinstance(diag, dict):
         for test, res in diag.items():
             if isinstance(res, dict) and res.get("pass") is False:
-                fail.append(f"gpu{idx}: diag {test} failed ({res.get('detail', '')})".rstrip(" ()"))
+                detail = res.get("detail") or ""
+                fail.append(f"gpu{idx}: diag {test} failed" + (f" ({detail})" if detail else ""))
     return fail, warn
 
 
@@ -198,6 +199,12 @@ def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
         ok += 0 if f else 1
     if expected_gpus and len(gpus) < expected_gpus:
         fails.append(f"{len(gpus)} of {expected_gpus} GPUs visible to amd-smi")
+    fabric = report.get("fabric")
+    if isinstance(fabric, dict):
+        for test, res in fabric.items():  # node-level: the xGMI pair matrix (ops/diag.p2p_matrix)
+            if isinstance(res, dict) and res.get("pass") is False:
+                detail = res.get("detail") or ""
+                fails.append(f"xGMI {test} failed" + (f" ({detail})" if detail else ""))
     state = UNHEALTHY if fails else (DEGRADED if warns else HEALTHY)
     return Verdict(state, fails, warns, gpus_ok=ok, gpus_seen=len(gpus), age_s=age)
 

@@ -29,6 +29,7 @@ GEMM_MAX_REL_ERR = 2e-3       # vs fp32 reference; bf16 inputs are exact in fp32
 HBM_MIN_COPY_TBS = 4.0        # 16-byte copy (read + write bytes counted)
 HBM_MIN_READ_TBS = 4.5
 MEMTEST_MAX_ERRORS = 0
+P2P_MIN_FRACTION_OF_MEDIAN = 0.5  # a GPU pair slower than half the node's median pair: suspect link
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -50,6 +51,9 @@ def lib() -> ctypes.CDLL:
         L.diag_memtest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong),
                                    ctypes.POINTER(ctypes.c_double)]
+        L.diag_p2p_copy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
+                                    ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -123,6 +127,38 @@ def memtest(device: int = 0, gib: float = 8.0, passes: int = 1, seed: int = 0x5E
     return res
 
 
+def p2p_copy(src: int, dst: int, mib: int = 256, iters: int = 5) -> Dict[str, Any]:
+    """One ordered GPU pair: copy bandwidth over xGMI (GB/s) and pattern errors on arrival."""
+    gbps, errs, peer = ctypes.c_double(), ctypes.c_ulonglong(), ctypes.c_int()
+    _check(lib().diag_p2p_copy(src, dst, mib << 20, iters, ctypes.byref(gbps), ctypes.byref(errs),
+                               ctypes.byref(peer)))
+    return {"src": src, "dst": dst, "gbps": round(gbps.value, 1), "errors": errs.value, "peer": bool(peer.value)}
+
+
+def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5) -> Dict[str, Any]:
+    """Every ordered pair of ``devices`` (default: all): the node's xGMI fabric, link by link.
+
+    Pass: every pair has direct peer access, delivers its bytes intact, and runs at no less than
+    ``P2P_MIN_FRACTION_OF_MEDIAN`` of the median pair (relative, so it holds for any hive size,
+    partition mode or firmware; an absolute floor would need per-platform numbers).
+    """
+    devs = list(range(device_count())) if devices is None else list(devices)
+    t0 = time.perf_counter()
+    if len(devs) < 2:
+        return {"pass": True, "skipped": f"{len(devs)} GPU(s): no pairs", "pairs": [], "detail": ""}
+    pairs = [p2p_copy(a, b, mib, iters) for a in devs for b in devs if a != b]
+    rates = sorted(p["gbps"] for p in pairs)
+    median = rates[len(rates) // 2]
+    slow = [p for p in pairs if p["gbps"] < P2P_MIN_FRACTION_OF_MEDIAN * median]
+    bad = [p for p in pairs if p["errors"]]
+    nopeer = [p for p in pairs if not p["peer"]]
+    problems = ([f"{p['src']}->{p['dst']} {p['gbps']} GB/s" for p in slow]
+                + [f"{p['src']}->{p['dst']} {p['errors']} bad words" for p in bad]
+                + [f"{p['src']}->{p['dst']} no peer access" for p in nopeer])
+    return {"pass": not problems, "pairs": pairs, "median_gbps": median, "min_gbps": rates[0],
+            "wall_s": round(time.perf_counter() - t0, 3), "detail": "; ".join(problems[:8])}
+
+
 LEVELS = {
     0: (),
     1: ("gemm_quick", "hbm_quick"),
@@ -159,10 +195,15 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="mi355x-diag", description="MI355X active diagnostics (HIP, gfx950)")
     ap.add_argument("--level", type=int, default=1, choices=(1, 2))
     ap.add_argument("--device", type=int, action="append", help="GPU index (repeatable; default: all)")
+    ap.add_argument("--no-p2p", dest="p2p", action="store_false", help="skip the level-2 xGMI pair matrix")
     args = ap.parse_args(argv)
     devices = args.device if args.device else list(range(device_count()))
-    out = {"devices": {d: {"info": device_info(d), "tests": run(args.level, d)} for d in devices}}
-    out["pass"] = all(t.get("pass") for d in out["devices"].values() for t in d["tests"].values())
+    out: Dict[str, Any] = {"devices": {d: {"info": device_info(d), "tests": run(args.level, d)} for d in devices}}
+    ok = all(t.get("pass") for d in out["devices"].values() for t in d["tests"].values())
+    if args.level >= 2 and args.p2p:
+        out["fabric"] = {"p2p": p2p_matrix(devices)}
+        ok = ok and out["fabric"]["p2p"]["pass"]
+    out["pass"] = ok
     print(json.dumps(out, indent=1))
     return 0 if out["pass"] else 1
 

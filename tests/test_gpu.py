@@ -211,3 +211,17 @@ def test_agent_diagnostics_threads_per_device(dev):
     rep = ag.probe_once()
     assert len(rep["gpus"]) >= 1
     assert all("diag" in g for g in rep["gpus"][: diag.device_count()])
+
+
+def test_p2p_diag_on_this_box(dev):
+    """The pair matrix is a node-level xGMI test: with one visible GPU it is skipped, and the C ABI
+    rejects a pair that is not two distinct devices instead of faulting."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    n = diag.device_count()
+    if n < 2:
+        assert diag.p2p_matrix()["skipped"]
+        with pytest.raises(RuntimeError, match="two distinct devices"):
+            diag.p2p_copy(0, 0)
+    else:
+        m = diag.p2p_matrix([0, 1], mib=64, iters=3)
+        assert all(p["errors"] == 0 for p in m["pairs"]) and m["min_gbps"] > 1.0, m

@@ -189,3 +189,32 @@ def test_cli_unhealthy_condition_without_annotation(run_cli, mock_cluster, tmp_p
     kc = _cluster(mock_cluster, tmp_path, nodes)
     p = run_cli(["--kubeconfig", kc, "--json"])
     assert [n["ready"] for n in json.loads(p.stdout)["nodes"]] == [False, True] and p.returncode == 0
+
+
+def test_fabric_failure_makes_the_node_unhealthy():
+    from k8s_gpu_node_checker_amd.models import health as H
+    from k8s_gpu_node_checker_amd.testing import fixtures
+    rep = fixtures.mi355x_probe_report("n", gpus=8)
+    rep["fabric"] = {"p2p": {"pass": True, "median_gbps": 48.0, "min_gbps": 45.1, "detail": ""}}
+    assert H.evaluate_report(rep, 8).state == H.HEALTHY
+    rep["fabric"]["p2p"] = {"pass": False, "detail": "3->5 11.2 GB/s"}
+    v = H.evaluate_report(rep, 8)
+    assert v.state == H.UNHEALTHY and v.reasons == ["xGMI p2p failed (3->5 11.2 GB/s)"]
+
+
+def test_p2p_matrix_flags_slow_corrupting_and_non_peer_pairs(monkeypatch):
+    from k8s_gpu_node_checker_amd.ops import diag
+    fake = {(0, 1): (50.0, 0, True), (1, 0): (49.0, 0, True), (0, 2): (51.0, 0, True),
+            (2, 0): (12.0, 0, True), (1, 2): (50.5, 7, True), (2, 1): (48.0, 0, False)}
+
+    def p2p_copy(a, b, mib=256, iters=5):
+        g, e, p = fake[(a, b)]
+        return {"src": a, "dst": b, "gbps": g, "errors": e, "peer": p}
+    monkeypatch.setattr(diag, "p2p_copy", p2p_copy)
+    m = diag.p2p_matrix([0, 1, 2])
+    assert not m["pass"] and len(m["pairs"]) == 6 and m["median_gbps"] == 50.0 and m["min_gbps"] == 12.0
+    assert "2->0 12.0 GB/s" in m["detail"] and "1->2 7 bad words" in m["detail"] and "2->1 no peer access" in m["detail"]
+    for k in list(fake):
+        fake[k] = (50.0, 0, True)
+    assert diag.p2p_matrix([0, 1, 2])["pass"]
+    assert diag.p2p_matrix([0])["skipped"] and diag.p2p_matrix([0])["pass"]
