@@ -20,6 +20,8 @@
 //               failing 16-byte word.
 //   p2p_copy    xGMI pair check: peer copies between two GPUs of the node,
 //               timed, and the received pattern verified on the destination.
+//   mfma_burn   matrix-core datapath burn-in per precision (bf16, fp8, MX-fp8,
+//               MX-fp4), register-resident, every lane's exact result checked.
 //
 // C ABI (ctypes, ops/diag.py).  Every HIP call is checked; on failure the
 // function returns a negative code and diag_last_error() says what failed.
@@ -563,6 +565,57 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// ---------------------------------------------------------------------------
+// Matrix-core datapath burn-in, one kernel per precision the MI355X computes in (operand lane layouts
+// measured by tools/mfma_lab.hip: lane l holds A[l&15][k = (K/4)(l>>4) + e] and B[k][l&15] in element
+// e, fp4 low nibble first):
+//   0 bf16  v_mfma_f32_16x16x32_bf16          2 MX-fp8 (E4M3)  v_mfma_scale_f32_16x16x128_f8f6f4
+//   1 fp8   v_mfma_f32_16x16x32_fp8_fp8       3 MX-fp4 (E2M1)  v_mfma_scale_f32_16x16x128_f8f6f4
+// Register-resident (no memory traffic), 4 independent accumulators per wave, 2 waves per SIMD on every
+// CU.  Operands are {-1, 0, +1}: every product and partial sum is an integer below 2^24, so the fp32
+// result is exact and each lane's final sum must equal the host-computed value bit for bit -- a SIMD
+// whose matrix core miscomputes is counted, not averaged away.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+template <int KIND>
+__device__ __forceinline__ floatx4 burn_mfma(const i32x8& a, const i32x8& b, floatx4 c) {
+  if constexpr (KIND == 0) {
+    bf16x8 av, bv;
+    __builtin_memcpy(&av, &a, 16);
+    __builtin_memcpy(&bv, &b, 16);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c, 0, 0, 0);
+  } else if constexpr (KIND == 1) {
+    long av, bv;
+    __builtin_memcpy(&av, &a, 8);
+    __builtin_memcpy(&bv, &b, 8);
+    return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av, bv, c, 0, 0, 0);
+  } else if constexpr (KIND == 2) {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);  // E4M3, scales 2^0
+  } else {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);  // E2M1, scales 2^0
+  }
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(256) mfma_burn_kernel(const i32x8* __restrict__ fa, const i32x8* __restrict__ fb,
+                                                        const float* __restrict__ expect, int iters,
+                                                        unsigned long long* errors) {
+  const int lane = threadIdx.x & 63;
+  const i32x8 a = fa[lane], b = fb[lane];
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc0 = burn_mfma<KIND>(a, b, acc0);
+      acc1 = burn_mfma<KIND>(b, a, acc1);
+      acc2 = burn_mfma<KIND>(a, a, acc2);
+      acc3 = burn_mfma<KIND>(b, b, acc3);
+    }
+  }
+  const floatx4 s = acc0 + acc1 + acc2 + acc3;
+  if (s[0] + s[1] + s[2] + s[3] != expect[lane]) atomicAdd(errors, 1ULL);
+}
+
 // Device allocation owned by its device (frees with that device current), for the multi-GPU test.
 struct DevBuf {
   int device = -1;
@@ -890,6 +943,108 @@ int diag_p2p_copy(int src, int dst, size_t bytes, int iters, double* gbps, unsig
   DIAG_CHECK(hipMemcpy(h, cnt.ptr, sizeof h, hipMemcpyDeviceToHost));
   *errors = h[0];
   DIAG_CHECK(hipSetDevice(cur));
+  return 0;
+}
+
+// Matrix-core burn-in of one precision (`kind` as mfma_burn_kernel): `reps` launches of `iters`
+// iterations on every CU; *tflops = dense rate, *errors = wave-lanes whose exact result differed.
+int diag_mfma_burn(int device, int kind, int iters, int reps, double* tflops, unsigned long long* errors) {
+  if (kind < 0 || kind > 3 || iters < 1 || iters > 65536 || reps < 1) {
+    g_err = "mfma_burn: kind 0..3, 1 <= iters <= 65536, reps >= 1";
+    return -2;
+  }
+  DIAG_CHECK(hipSetDevice(device));
+  static const int kK[4] = {32, 32, 128, 128};
+  const int K = kK[kind], per = K / 4;
+  // a lane's final sum is bounded by 16 outputs * K * 4 MFMA per accumulator-iteration * iters
+  if (16.0 * K * 4 * iters >= 16777216.0) {
+    g_err = "mfma_burn: iters too large for an exact fp32 check (< 2048 at K=128, < 8192 at K=32)";
+    return -2;
+  }
+  // operands in {-1, 0, +1}, per lane (the same in every wave, so every wave has the same answer)
+  uint64_t st = 0x9E3779B97F4A7C15ULL ^ static_cast<uint64_t>(kind);
+  auto rnd3 = [&st]() {
+    st ^= st << 13;
+    st ^= st >> 7;
+    st ^= st << 17;
+    return static_cast<int>(st % 3) - 1;
+  };
+  std::vector<int> va(64 * per), vb(64 * per);
+  for (int& x : va) x = rnd3();
+  for (int& x : vb) x = rnd3();
+  std::vector<uint8_t> fa(64 * 32, 0), fb(64 * 32, 0);
+  auto encode = [&](std::vector<uint8_t>& f, const std::vector<int>& v) {
+    for (int l = 0; l < 64; ++l)
+      for (int e = 0; e < per; ++e) {
+        const int x = v[l * per + e];
+        if (kind == 0) {
+          const uint16_t bits = x == 0 ? 0 : (x > 0 ? 0x3F80 : 0xBF80);
+          memcpy(&f[l * 32 + 2 * e], &bits, 2);
+        } else if (kind == 3) {
+          const uint8_t nib = x == 0 ? 0 : (x > 0 ? 0x2 : 0xA);
+          f[l * 32 + e / 2] |= static_cast<uint8_t>(nib << ((e & 1) ? 4 : 0));
+        } else {
+          f[l * 32 + e] = x == 0 ? 0 : (x > 0 ? 0x38 : 0xB8);
+        }
+      }
+  };
+  encode(fa, va);
+  encode(fb, vb);
+  // host reference: C_xy[i][j] = sum_k x(lane i + 16(k/per), k%per) * y(lane j + 16(k/per), k%per)
+  auto prod = [&](const std::vector<int>& x, const std::vector<int>& y, int i, int j) {
+    long acc = 0;
+    for (int k = 0; k < K; ++k) acc += static_cast<long>(x[(i + 16 * (k / per)) * per + k % per]) *
+                                       y[(j + 16 * (k / per)) * per + k % per];
+    return acc;
+  };
+  std::vector<float> expect(64);
+  for (int l = 0; l < 64; ++l) {
+    long tot = 0;
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * (l >> 4) + r, col = l & 15;
+      tot += prod(va, vb, row, col) + prod(vb, va, row, col) + prod(va, va, row, col) + prod(vb, vb, row, col);
+    }
+    expect[l] = static_cast<float>(tot * 4L * iters);  // exact: bounded below 2^24 by the check above
+  }
+  DevBuf dfa, dfb, dex, dcnt;
+  DIAG_CHECK(dfa.alloc(device, fa.size()));
+  DIAG_CHECK(dfb.alloc(device, fb.size()));
+  DIAG_CHECK(dex.alloc(device, expect.size() * sizeof(float)));
+  DIAG_CHECK(dcnt.alloc(device, sizeof(unsigned long long)));
+  DIAG_CHECK(hipMemcpy(dfa.ptr, fa.data(), fa.size(), hipMemcpyHostToDevice));
+  DIAG_CHECK(hipMemcpy(dfb.ptr, fb.data(), fb.size(), hipMemcpyHostToDevice));
+  DIAG_CHECK(hipMemcpy(dex.ptr, expect.data(), expect.size() * sizeof(float), hipMemcpyHostToDevice));
+  DIAG_CHECK(hipMemset(dcnt.ptr, 0, sizeof(unsigned long long)));
+  const int blocks = grid_for(device, 2);  // 8 waves per CU = 2 per SIMD
+  auto launch = [&]() {
+    const i32x8* a = static_cast<const i32x8*>(dfa.ptr);
+    const i32x8* b = static_cast<const i32x8*>(dfb.ptr);
+    const float* ex = static_cast<const float*>(dex.ptr);
+    unsigned long long* c = static_cast<unsigned long long*>(dcnt.ptr);
+    switch (kind) {
+      case 0: hipLaunchKernelGGL(mfma_burn_kernel<0>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c); break;
+      case 1: hipLaunchKernelGGL(mfma_burn_kernel<1>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c); break;
+      case 2: hipLaunchKernelGGL(mfma_burn_kernel<2>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c); break;
+      default: hipLaunchKernelGGL(mfma_burn_kernel<3>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c);
+    }
+  };
+  launch();  // warm-up (also checked)
+  DIAG_CHECK(hipGetLastError());
+  DIAG_CHECK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  DIAG_CHECK(hipEventCreate(&e0));
+  DIAG_CHECK(hipEventCreate(&e1));
+  DIAG_CHECK(hipEventRecord(e0, nullptr));
+  for (int r = 0; r < reps; ++r) launch();
+  DIAG_CHECK(hipEventRecord(e1, nullptr));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  DIAG_CHECK(hipGetLastError());
+  const float ms = elapsed_ms(e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  DIAG_CHECK(hipMemcpy(errors, dcnt.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  const double flop = static_cast<double>(blocks) * 4 /*waves*/ * iters * 16 /*MFMA per iter*/ * 2.0 * 16 * 16 * K;
+  *tflops = ms > 0.f ? flop * reps / (ms * 1e-3) / 1e12 : 0.0;
   return 0;
 }
 

@@ -29,6 +29,10 @@ GEMM_MAX_REL_ERR = 2e-3       # vs fp32 reference; bf16 inputs are exact in fp32
 HBM_MIN_COPY_TBS = 4.0        # 16-byte copy (read + write bytes counted)
 HBM_MIN_READ_TBS = 4.5
 MEMTEST_MAX_ERRORS = 0
+# Matrix-core burn-in (register-resident MFMA loops, random {-1,0,1} operands; measured
+# profiles/mfma_lab_mi355x.jsonl: bf16 1687, fp8 1803, MX-fp8 4027, MX-fp4 7171 TFLOP/s dense)
+MFMA_KINDS = ("bf16", "fp8", "mxfp8", "mxfp4")
+MFMA_MIN_TFLOPS = {"bf16": 1000.0, "fp8": 1000.0, "mxfp8": 2400.0, "mxfp4": 4300.0}
 P2P_MIN_FRACTION_OF_MEDIAN = 0.5  # a GPU pair slower than half the node's median pair: suspect link
 
 _lib: Optional[ctypes.CDLL] = None
@@ -51,6 +55,8 @@ def lib() -> ctypes.CDLL:
         L.diag_memtest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong),
                                    ctypes.POINTER(ctypes.c_double)]
+        L.diag_mfma_burn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong)]
         L.diag_p2p_copy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                     ctypes.POINTER(ctypes.c_int)]
@@ -127,6 +133,23 @@ def memtest(device: int = 0, gib: float = 8.0, passes: int = 1, seed: int = 0x5E
     return res
 
 
+def mfma_burn(device: int = 0, kinds=MFMA_KINDS, iters: int = 2000, reps: int = 5) -> Dict[str, Any]:
+    """Every matrix-core precision of the MI355X: dense TFLOP/s and exact-result errors per kind."""
+    t0 = time.perf_counter()
+    rows: Dict[str, Any] = {}
+    problems = []
+    for kind in kinds:
+        tf, errs = ctypes.c_double(), ctypes.c_ulonglong()
+        _check(lib().diag_mfma_burn(device, MFMA_KINDS.index(kind), iters, reps, ctypes.byref(tf), ctypes.byref(errs)))
+        rows[kind] = {"tflops": round(tf.value, 1), "errors": errs.value}
+        if errs.value:
+            problems.append(f"{kind}: {errs.value} wrong results")
+        if tf.value < MFMA_MIN_TFLOPS[kind]:
+            problems.append(f"{kind}: {tf.value:.0f} TFLOP/s")
+    return {"pass": not problems, "kinds": rows, "wall_s": round(time.perf_counter() - t0, 3),
+            "detail": "; ".join(problems)}
+
+
 def p2p_copy(src: int, dst: int, mib: int = 256, iters: int = 5) -> Dict[str, Any]:
     """One ordered GPU pair: copy bandwidth over xGMI (GB/s) and pattern errors on arrival."""
     gbps, errs, peer = ctypes.c_double(), ctypes.c_ulonglong(), ctypes.c_int()
@@ -161,8 +184,8 @@ def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5) -
 
 LEVELS = {
     0: (),
-    1: ("gemm_quick", "hbm_quick"),
-    2: ("gemm", "hbm", "memtest"),
+    1: ("gemm_quick", "hbm_quick", "mfma"),
+    2: ("gemm", "hbm", "memtest", "mfma"),
 }
 
 
@@ -181,6 +204,8 @@ def run(level: int = 1, device: int = 0) -> Dict[str, Dict[str, Any]]:
                 out["hbm"] = hbm(device)
             elif test == "memtest":
                 out["memtest"] = memtest(device)
+            elif test == "mfma":
+                out["mfma"] = mfma_burn(device)
         except NativeUnavailable:
             raise
         except Exception as e:  # a failing diagnostic is a verdict, not a crash

@@ -225,3 +225,19 @@ def test_p2p_diag_on_this_box(dev):
     else:
         m = diag.p2p_matrix([0, 1], mib=64, iters=3)
         assert all(p["errors"] == 0 for p in m["pairs"]) and m["min_gbps"] > 1.0, m
+
+
+def test_mfma_burn_every_precision(dev):
+    """bf16 / fp8 / MX-fp8 / MX-fp4 matrix cores: exact results on every wave, rates above the floors."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.mfma_burn(0)
+    assert r["pass"], r
+    k = r["kinds"]
+    assert all(v["errors"] == 0 for v in k.values())
+    assert k["mxfp8"]["tflops"] > 1.5 * k["bf16"]["tflops"] and k["mxfp4"]["tflops"] > 1.5 * k["mxfp8"]["tflops"]
+
+
+def test_mfma_burn_rejects_inexact_iteration_counts():
+    from k8s_gpu_node_checker_amd.ops import diag
+    with pytest.raises(RuntimeError, match="exact fp32"):
+        diag.mfma_burn(0, kinds=("mxfp4",), iters=4096, reps=1)
