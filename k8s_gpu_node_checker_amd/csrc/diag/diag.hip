@@ -40,6 +40,8 @@ namespace {
 
 thread_local std::string g_err;
 int g_gemm_variant = 0;
+int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3 kernels;
+                          // measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
 
 #define DIAG_CHECK(expr)                                                                  \
   do {                                                                                    \
@@ -53,6 +55,7 @@ int g_gemm_variant = 0;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native 16-byte vector (SROA-friendly, unlike uint4)
+typedef int i32x8 __attribute__((ext_vector_type(8)));            // 32 fp8 / 64 fp4 operand bytes
 
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int THREADS = 256;
@@ -64,6 +67,15 @@ constexpr int LOADS_PER_THREAD = TILE_CHUNKS / THREADS;  // 4
 // For the 16x16x32 fragment read (lane l: row l&15, chunk (l>>4)+4s) this puts
 // every ds_read_b128 lane group on 16 distinct 16-byte slots (all 64 banks).
 __device__ __forceinline__ int swz(int r, int c) { return r * CHUNKS_PER_ROW + (c ^ ((r >> 1) & 7)); }
+
+// The fp8 16x16x128 fragment (lane l: row l&15, 32 bytes = chunks 2(l>>4), 2(l>>4)+1) needs another
+// XOR: f8(r) = 3*r[3] ^ 4*r[1] puts each ds_read_b128 lane group of both chunk reads on 16 distinct
+// 16-byte slots (searched exhaustively over GF(2)-linear swizzles; it is conflict-free for the bf16
+// fragment pattern too).
+__device__ __forceinline__ int swz_row_xor(int r, bool fp8) {
+  return fp8 ? ((((r >> 3) & 1) * 3) ^ (((r >> 1) & 1) << 2)) : ((r >> 1) & 7);
+}
+__device__ __forceinline__ int swz8(int r, int c) { return r * CHUNKS_PER_ROW + (c ^ swz_row_xor(r, true)); }
 
 __device__ __forceinline__ void gemm_gload(u32x4 (&ra)[LOADS_PER_THREAD], u32x4 (&rb)[LOADS_PER_THREAD],
                                            const u32x4* __restrict__ Ablk, const u32x4* __restrict__ Bblk,
@@ -189,6 +201,7 @@ constexpr int V2_STAGE_BYTES = 2 * V2_BM * BK * 2;     // A + B, bf16 = 64 KiB
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+template <bool FP8 = false>
 __device__ __forceinline__ void v2_fill(unsigned char* lds_stage, const __bf16* __restrict__ A,
                                         const __bf16* __restrict__ Bt, int K, int kt, int wid, int lane) {
   // lane -> (row within an 8-row group, physical chunk); logical chunk = phys ^ swizzle(row)
@@ -199,7 +212,7 @@ __device__ __forceinline__ void v2_fill(unsigned char* lds_stage, const __bf16* 
 #pragma unroll
     for (int j = 0; j < V2_ROWS_PER_WAVE / 8; ++j) {
       const int row = wid * V2_ROWS_PER_WAVE + j * 8 + rsub;
-      const int c = phys ^ ((row >> 1) & 7);
+      const int c = phys ^ swz_row_xor(row, FP8);
       const __bf16* g = src + static_cast<size_t>(row) * K + kt * BK + c * 8;
       unsigned char* l = lds_stage + op * (V2_BM * BK * 2) + (wid * V2_ROWS_PER_WAVE + j * 8) * (BK * 2);
       __builtin_amdgcn_global_load_lds(g, (lds_void_t*)l, 16, 0, 0);
@@ -297,6 +310,7 @@ gemm_bf16_v2_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   } while (0)
 
 // One 16 KiB region of a stage: 16 LDS-DMA wave-instructions of 8 rows, 2 per wave.
+template <bool FP8>
 __device__ __forceinline__ void stg_region(unsigned char* lds_stage, const __bf16* __restrict__ A,
                                            const __bf16* __restrict__ Bt, int K, int kt, int region, int i, int wid,
                                            int lane) {
@@ -306,7 +320,7 @@ __device__ __forceinline__ void stg_region(unsigned char* lds_stage, const __bf1
   const int row0 = is_a ? (g >> 3) * 128 + (region == 0 ? 0 : 64) + (g & 7) * 8
                         : (g >> 2) * 64 + (region == 1 ? 0 : 32) + (g & 3) * 8;
   const int row = row0 + rsub;
-  const int c = phys ^ ((row >> 1) & 7);
+  const int c = phys ^ swz_row_xor(row, FP8);
   const __bf16* gp = (is_a ? A : Bt) + static_cast<size_t>(row) * K + kt * BK + c * 8;
   unsigned char* l = lds_stage + (is_a ? 0 : V2_BM * BK * 2) + row0 * (BK * 2);
   __builtin_amdgcn_global_load_lds(gp, (lds_void_t*)l, 16, 0, 0);
@@ -329,9 +343,49 @@ __device__ __forceinline__ void stg_mfma(floatx4 (&acc)[8][4], const bf16x8 (&af
     for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[m0 + m][n0 + n]));
 }
 
+// MX-fp8 (E4M3, unit E8M0 scales): one v_mfma_scale_f32_16x16x128_f8f6f4 covers the K-tile's 128 bytes.
+__device__ __forceinline__ void stg_mfma(floatx4 (&acc)[8][4], const i32x8 (&af)[4], const i32x8 (&bf)[2], int m0,
+                                         int n0) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+      acc[m0 + m][n0 + n] =
+          __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bf[n], acc[m0 + m][n0 + n], 0, 0, 0, 127, 0, 127);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[m0 + m][n0 + n]));
+}
+
+// Fragment of one 16-row block: bf16 = two K=32 steps (chunks fq, fq+4); fp8 = the lane's 32
+// contiguous bytes of K (chunks 2fq, 2fq+1; lane layout measured by tools/mfma_lab.hip).
+__device__ __forceinline__ void stg_load(bf16x8 (&f)[2], const u32x4* img, int row, int fq) {
+  f[0] = __builtin_bit_cast(bf16x8, img[swz(row, fq)]);
+  f[1] = __builtin_bit_cast(bf16x8, img[swz(row, fq + 4)]);
+}
+__device__ __forceinline__ void stg_load(i32x8& f, const u32x4* img, int row, int fq) {
+  const u32x4 lo = img[swz8(row, 2 * fq)], hi = img[swz8(row, 2 * fq + 1)];
+  f = i32x8{static_cast<int>(lo.x), static_cast<int>(lo.y), static_cast<int>(lo.z), static_cast<int>(lo.w),
+            static_cast<int>(hi.x), static_cast<int>(hi.y), static_cast<int>(hi.z), static_cast<int>(hi.w)};
+}
+
+template <bool FP8>
+struct StgFrags {
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+};
+template <>
+struct StgFrags<true> {
+  i32x8 a[4], b0[2], b1[2];
+};
+
+// FP8 = false: bf16 A[M][K] . Bt[N][K]^T.  FP8 = true: MX-fp8 operands of K8 bytes per row, passed as
+// K = K8 / 2 "bf16 columns" so the byte-identical LDS-DMA staging is shared (a 64-column bf16 K-tile
+// is a 128-byte fp8 K-tile); only the swizzle, the fragment reads and the MFMA differ.
+template <bool FP8, bool EPI_LDS = false>
 __global__ void __launch_bounds__(V2_THREADS, 1)
-gemm_bf16_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
-                    int K) {
+gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
+               int K) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
@@ -358,9 +412,9 @@ gemm_bf16_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   const int KT = K / BK;
   const int frow = lane & 15, fq = lane >> 4;
 
-  v2_fill(smem, Ab, Bb, K, 0, wid, lane);
+  v2_fill<FP8>(smem, Ab, Bb, K, 0, wid, lane);
   if (KT > 1) {
-    v2_fill(smem + V2_STAGE_BYTES, Ab, Bb, K, 1, wid, lane);
+    v2_fill<FP8>(smem + V2_STAGE_BYTES, Ab, Bb, K, 1, wid, lane);
     __builtin_amdgcn_s_waitcnt(0x3f78);  // vmcnt(8): tile 0 landed, tile 1 may be in flight
   } else {
     __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
@@ -368,7 +422,7 @@ gemm_bf16_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   STG_BARRIER();
   if (wr == 1) STG_BARRIER();  // the stagger
 
-  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  StgFrags<FP8> f;
   for (int kt = 0; kt < KT; ++kt) {
     unsigned char* cur = smem + (kt & 1) * V2_STAGE_BYTES;
     unsigned char* nxt = smem + ((kt + 1) & 1) * V2_STAGE_BYTES;
@@ -377,68 +431,80 @@ gemm_bf16_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
     const bool pre = kt + 2 < KT;
     // phase 0: A(m0), B(n0); R3 of tile kt+1 (tile 1 came whole with the prologue)
     if (kt >= 1 && kt + 1 < KT) {
-      stg_region(nxt, Ab, Bb, K, kt + 1, 3, 0, wid, lane);
-      stg_region(nxt, Ab, Bb, K, kt + 1, 3, 1, wid, lane);
+      stg_region<FP8>(nxt, Ab, Bb, K, kt + 1, 3, 0, wid, lane);
+      stg_region<FP8>(nxt, Ab, Bb, K, kt + 1, 3, 1, wid, lane);
     }
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < 2; ++n) stg_load(f.b0[n], b_img, wc * 64 + n * 16 + frow, fq);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) b0[n][s] = __builtin_bit_cast(bf16x8, b_img[swz(wc * 64 + n * 16 + frow, fq + 4 * s)]);
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) af[m][s] = __builtin_bit_cast(bf16x8, a_img[swz(wr * 128 + m * 16 + frow, fq + 4 * s)]);
+    for (int m = 0; m < 4; ++m) stg_load(f.a[m], a_img, wr * 128 + m * 16 + frow, fq);
     STG_BARRIER();
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    stg_mfma(acc, af, b0, 0, 0);
+    stg_mfma(acc, f.a, f.b0, 0, 0);
     STG_BARRIER();
     // phase 1: B(n1)
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        b1[n][s] = __builtin_bit_cast(bf16x8, b_img[swz(wc * 64 + (n + 2) * 16 + frow, fq + 4 * s)]);
+    for (int n = 0; n < 2; ++n) stg_load(f.b1[n], b_img, wc * 64 + (n + 2) * 16 + frow, fq);
     STG_BARRIER();
     __builtin_amdgcn_s_waitcnt(0xc07f);
-    stg_mfma(acc, af, b1, 0, 2);
+    stg_mfma(acc, f.a, f.b1, 0, 2);
     STG_BARRIER();
     // phase 2: A(m1); restage R0, R1 with tile kt+2
     if (pre) {
-      stg_region(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
-      stg_region(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
-      stg_region(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
-      stg_region(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
+      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
+      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
+      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
+      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
     }
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        af[m][s] = __builtin_bit_cast(bf16x8, a_img[swz(wr * 128 + (m + 4) * 16 + frow, fq + 4 * s)]);
+    for (int m = 0; m < 4; ++m) stg_load(f.a[m], a_img, wr * 128 + (m + 4) * 16 + frow, fq);
     STG_BARRIER();
     __builtin_amdgcn_s_waitcnt(0xc07f);
-    stg_mfma(acc, af, b1, 4, 2);
+    stg_mfma(acc, f.a, f.b1, 4, 2);
     STG_BARRIER();
     // phase 3: no LDS reads; restage R2, retire tile kt+1
     if (pre) {
-      stg_region(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
-      stg_region(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
+      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
+      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
       __builtin_amdgcn_s_waitcnt(0x3f76);  // vmcnt(6)
     } else {
       __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
     }
     STG_BARRIER();
-    stg_mfma(acc, af, b0, 4, 0);
+    stg_mfma(acc, f.a, f.b0, 4, 0);
     STG_BARRIER();
   }
   if (wr == 0) STG_BARRIER();  // balance the stagger
   const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 64;
+  if constexpr (EPI_LDS) {
+    // Each 16x64 fp32 slice goes through the wave's own LDS patch (no DMA is in flight and every
+    // fragment read retired before the last barrier), then leaves as 16-byte row pieces: one store
+    // instruction covers 4 rows x 256 contiguous bytes instead of 4 rows x 64.
+    constexpr int LD = 64 + 4;
+    __builtin_amdgcn_s_barrier();
+    float* patch = reinterpret_cast<float*>(smem) + wid * (16 * LD);
 #pragma unroll
-  for (int m = 0; m < 8; ++m)
+    for (int m = 0; m < 8; ++m) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+      for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        C[static_cast<size_t>(row0 + m * 16 + fq * 4 + j) * N + col0 + n * 16 + frow] = acc[m][n][j];
+        for (int j = 0; j < 4; ++j) patch[(fq * 4 + j) * LD + n * 16 + frow] = acc[m][n][j];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = q * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+        const floatx4 v = *reinterpret_cast<const floatx4*>(patch + r * LD + c4);
+        *reinterpret_cast<floatx4*>(C + static_cast<size_t>(row0 + m * 16 + r) * N + col0 + c4) = v;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          C[static_cast<size_t>(row0 + m * 16 + fq * 4 + j) * N + col0 + n * 16 + frow] = acc[m][n][j];
+  }
 }
 
 // fp32 reference for sampled outputs: one thread per (row, col) sample.
@@ -474,6 +540,42 @@ __global__ void fill_bf16_kernel(__bf16* p, size_t n, uint64_t seed) {
     const uint32_t h = mix32(i * 0x9E3779B97F4A7C15ULL + seed);
     p[i] = static_cast<__bf16>((h >> 8) * (2.0f / 16777216.0f) - 1.0f);
   }
+}
+
+// Finite OCP E4M3 bytes (exponent field <= 8, so |x| < 4 and no NaN encoding), hashed from the index.
+__global__ void fill_fp8_kernel(uint8_t* p, size_t n, uint64_t seed) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
+    uint64_t h = (i + 1) * 0x9E3779B97F4A7C15ULL ^ seed;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ULL;
+    h ^= h >> 29;
+    const uint32_t e = static_cast<uint32_t>(h % 9), m = static_cast<uint32_t>((h >> 8) & 7), s = (h >> 12) & 1;
+    p[i] = static_cast<uint8_t>((s << 7) | (e << 3) | m);
+  }
+}
+
+__device__ __forceinline__ double e4m3_value(uint8_t b) {
+  const int e = (b >> 3) & 15, m = b & 7;
+  const double v = e == 0 ? m / 8.0 * 0.015625 : (1.0 + m / 8.0) * ldexp(1.0, e - 7);
+  return (b & 0x80) ? -v : v;
+}
+
+// fp64 reference of sampled fp8 outputs, plus sum |a*b| (the scale of the MX MFMA's accumulation error)
+__global__ void gemm_ref_fp8_kernel(const uint8_t* A, const uint8_t* Bt, const int* rows, const int* cols,
+                                    double* out, double* mag, int nsamp, int K) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsamp) return;
+  const uint8_t* a = A + static_cast<size_t>(rows[i]) * K;
+  const uint8_t* b = Bt + static_cast<size_t>(cols[i]) * K;
+  double acc = 0.0, m = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double p = e4m3_value(a[k]) * e4m3_value(b[k]);
+    acc += p;
+    m += fabs(p);
+  }
+  out[i] = acc;
+  mag[i] = m;
 }
 
 // ---------------------------------------------------------------- HBM streams
@@ -575,8 +677,6 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b) {
 // CU.  Operands are {-1, 0, +1}: every product and partial sum is an integer below 2^24, so the fp32
 // result is exact and each lane's final sum must equal the host-computed value bit for bit -- a SIMD
 // whose matrix core miscomputes is counted, not averaged away.
-typedef int i32x8 __attribute__((ext_vector_type(8)));
-
 template <int KIND>
 __device__ __forceinline__ floatx4 burn_mfma(const i32x8& a, const i32x8& b, floatx4 c) {
   if constexpr (KIND == 0) {
@@ -650,6 +750,27 @@ hipError_t enable_peer(int from, int to) {
   return e;
 }
 
+template <bool FP8, bool EPI>
+int launch_v3_inst(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v3_kernel<FP8, EPI>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    attr_set = true;
+  }
+  const int nwg = (M / V2_BM) * (N / V2_BN);
+  hipLaunchKernelGGL((gemm_v3_kernel<FP8, EPI>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, stream,
+                     static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, M, N, Kcols);
+  return 0;
+}
+
+// v3 launch (M, N multiples of 256; Kcols = bf16 columns, K8 / 2 for fp8), epilogue per g_gemm_epilogue
+template <bool FP8>
+int launch_v3(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
+  return g_gemm_epilogue ? launch_v3_inst<FP8, true>(A, Bt, C, M, N, Kcols, stream)
+                         : launch_v3_inst<FP8, false>(A, Bt, C, M, N, Kcols, stream);
+}
+
 }  // namespace
 
 extern "C" {
@@ -659,6 +780,7 @@ const char* diag_last_error(void) { return g_err.c_str(); }
 // 0 = auto (v3 staggered 256x256 LDS-DMA tiles when M, N are multiples of 256 and the grid fills the
 // chip, else v1), 1 = force v1 (128x128 register-staged), 2 = force v2, 3 = force v3
 void diag_set_gemm_variant(int v) { g_gemm_variant = v; }
+void diag_set_gemm_epilogue(int e) { g_gemm_epilogue = e; }
 
 int diag_device_count(void) {
   int n = 0;
@@ -692,27 +814,37 @@ int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N,
       g_err = "gemm_bf16 v2/v3: M, N must be multiples of 256";
       return -2;
     }
-    static bool attr_set[2] = {false, false};
-    const void* fn = variant == 2 ? reinterpret_cast<const void*>(gemm_bf16_v2_kernel)
-                                  : reinterpret_cast<const void*>(gemm_bf16_v3_kernel);
-    if (!attr_set[variant - 2]) {
-      DIAG_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
-      attr_set[variant - 2] = true;
-    }
-    const int nwg = (M / V2_BM) * (N / V2_BN);
-    if (variant == 2)
+    if (variant == 2) {
+      static bool attr_set = false;
+      if (!attr_set) {
+        DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_v2_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+        attr_set = true;
+      }
+      const int nwg = (M / V2_BM) * (N / V2_BN);
       hipLaunchKernelGGL(gemm_bf16_v2_kernel, dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
                          static_cast<hipStream_t>(stream), static_cast<const __bf16*>(A),
                          static_cast<const __bf16*>(Bt), C, M, N, K);
-    else
-      hipLaunchKernelGGL(gemm_bf16_v3_kernel, dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
-                         static_cast<hipStream_t>(stream), static_cast<const __bf16*>(A),
-                         static_cast<const __bf16*>(Bt), C, M, N, K);
+    } else if (launch_v3<false>(A, Bt, C, M, N, K, static_cast<hipStream_t>(stream)) != 0) {
+      return -1;
+    }
   } else {
     const int nwg = (M / BM) * (N / BN);
     hipLaunchKernelGGL(gemm_bf16_kernel, dim3(nwg), dim3(THREADS), 0, static_cast<hipStream_t>(stream),
                        static_cast<const u32x4*>(A), static_cast<const u32x4*>(Bt), C, M, N, K);
   }
+  DIAG_CHECK(hipGetLastError());
+  return 0;
+}
+
+// MX-fp8 GEMM on caller-owned device pointers: C[M,N] (fp32) = A[M,K] . Bt[N,K]^T with OCP E4M3
+// operands (one byte each) and unit block scales.  M, N multiples of 256; K a multiple of 128.
+int diag_gemm_fp8_launch(const void* A, const void* Bt, float* C, int M, int N, int K, void* stream) {
+  if (M % V2_BM || N % V2_BN || K % 128 || M <= 0 || N <= 0 || K <= 0) {
+    g_err = "gemm_fp8: M, N must be multiples of 256 and K a multiple of 128";
+    return -2;
+  }
+  if (launch_v3<true>(A, Bt, C, M, N, K / 2, static_cast<hipStream_t>(stream)) != 0) return -1;
   DIAG_CHECK(hipGetLastError());
   return 0;
 }
@@ -787,6 +919,74 @@ int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int n
   hipFree(ref);
   hipFree(rows);
   hipFree(cols);
+  return 0;
+}
+
+// MX-fp8 counterpart of diag_gemm_bf16: *max_err = max |C - ref| / sum|a*b| over the samples.
+int diag_gemm_fp8(int device, int M, int N, int K, int warmup, int iters, int nsamp, double* tflops,
+                  double* max_err, double* ms_per_iter) {
+  if (M % V2_BM || N % V2_BN || K % 128 || nsamp < 1) {
+    g_err = "gemm_fp8: M, N must be multiples of 256, K a multiple of 128";
+    return -2;
+  }
+  DIAG_CHECK(hipSetDevice(device));
+  DevBuf A, Bt, C, ref, mag, rows, cols, got;
+  DIAG_CHECK(A.alloc(device, static_cast<size_t>(M) * K));
+  DIAG_CHECK(Bt.alloc(device, static_cast<size_t>(N) * K));
+  DIAG_CHECK(C.alloc(device, sizeof(float) * static_cast<size_t>(M) * N));
+  DIAG_CHECK(ref.alloc(device, sizeof(double) * nsamp));
+  DIAG_CHECK(mag.alloc(device, sizeof(double) * nsamp));
+  DIAG_CHECK(rows.alloc(device, sizeof(int) * nsamp));
+  DIAG_CHECK(cols.alloc(device, sizeof(int) * nsamp));
+  DIAG_CHECK(got.alloc(device, sizeof(float) * nsamp));
+  hipLaunchKernelGGL(fill_fp8_kernel, dim3(2048), dim3(256), 0, nullptr, static_cast<uint8_t*>(A.ptr),
+                     static_cast<size_t>(M) * K, 0x5151ULL);
+  hipLaunchKernelGGL(fill_fp8_kernel, dim3(2048), dim3(256), 0, nullptr, static_cast<uint8_t*>(Bt.ptr),
+                     static_cast<size_t>(N) * K, 0xA7A7ULL);
+  DIAG_CHECK(hipGetLastError());
+  std::vector<int> hr(nsamp), hc(nsamp);
+  uint64_t x = 0x13198A2E03707344ULL;
+  for (int i = 0; i < nsamp; ++i) {
+    x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+    hr[i] = static_cast<int>((x >> 33) % static_cast<uint64_t>(M));
+    x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+    hc[i] = static_cast<int>((x >> 33) % static_cast<uint64_t>(N));
+  }
+  DIAG_CHECK(hipMemcpy(rows.ptr, hr.data(), sizeof(int) * nsamp, hipMemcpyHostToDevice));
+  DIAG_CHECK(hipMemcpy(cols.ptr, hc.data(), sizeof(int) * nsamp, hipMemcpyHostToDevice));
+  float* c = static_cast<float*>(C.ptr);
+  for (int i = 0; i < warmup; ++i)
+    if (diag_gemm_fp8_launch(A.ptr, Bt.ptr, c, M, N, K, nullptr)) return -1;
+  hipEvent_t e0, e1;
+  DIAG_CHECK(hipEventCreate(&e0));
+  DIAG_CHECK(hipEventCreate(&e1));
+  DIAG_CHECK(hipEventRecord(e0, nullptr));
+  for (int i = 0; i < iters; ++i)
+    if (diag_gemm_fp8_launch(A.ptr, Bt.ptr, c, M, N, K, nullptr)) return -1;
+  DIAG_CHECK(hipEventRecord(e1, nullptr));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  const double ms = elapsed_ms(e0, e1) / std::max(iters, 1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  const int* r = static_cast<const int*>(rows.ptr);
+  const int* cl = static_cast<const int*>(cols.ptr);
+  hipLaunchKernelGGL(gemm_ref_fp8_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr,
+                     static_cast<const uint8_t*>(A.ptr), static_cast<const uint8_t*>(Bt.ptr), r, cl,
+                     static_cast<double*>(ref.ptr), static_cast<double*>(mag.ptr), nsamp, K);
+  hipLaunchKernelGGL(gather_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, c, r, cl,
+                     static_cast<float*>(got.ptr), nsamp, N);
+  DIAG_CHECK(hipGetLastError());
+  std::vector<double> href(nsamp), hmag(nsamp);
+  std::vector<float> hC(nsamp);
+  DIAG_CHECK(hipMemcpy(href.data(), ref.ptr, sizeof(double) * nsamp, hipMemcpyDeviceToHost));
+  DIAG_CHECK(hipMemcpy(hmag.data(), mag.ptr, sizeof(double) * nsamp, hipMemcpyDeviceToHost));
+  DIAG_CHECK(hipMemcpy(hC.data(), got.ptr, sizeof(float) * nsamp, hipMemcpyDeviceToHost));
+  double worst = 0.0;
+  for (int i = 0; i < nsamp; ++i)
+    worst = std::max(worst, std::fabs(static_cast<double>(hC[i]) - href[i]) / std::max(hmag[i], 1e-30));
+  *max_err = worst;
+  *ms_per_iter = ms;
+  *tflops = 2.0 * M * N * static_cast<double>(K) / (ms * 1e-3) / 1e12;
   return 0;
 }
 

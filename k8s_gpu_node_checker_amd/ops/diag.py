@@ -26,6 +26,8 @@ from .native import NativeUnavailable, load_cdll
 # read ~6.8 TB/s.  Device-to-device DVFS spread is ~10 %; these flag broken or badly throttled parts.
 GEMM_MIN_TFLOPS = 600.0       # bf16 MFMA GEMM (4096^3 quick / 8192^3 deep)
 GEMM_MAX_REL_ERR = 2e-3       # vs fp32 reference; bf16 inputs are exact in fp32, so ~1e-5 is typical
+GEMM_FP8_MIN_TFLOPS = 1200.0  # MX-fp8 GEMM (measured 2100 @4096^3, 2590 @8192^3, profiles/gemm_fp8_mi355x.jsonl)
+GEMM_FP8_MAX_ERR = 4e-5       # |C - ref| / sum|a*b|: the MX MFMA's own accumulation error is <= 1.6e-5
 HBM_MIN_COPY_TBS = 4.0        # 16-byte copy (read + write bytes counted)
 HBM_MIN_READ_TBS = 4.5
 MEMTEST_MAX_ERRORS = 0
@@ -45,11 +47,15 @@ def lib() -> ctypes.CDLL:
         assert L is not None
         L.diag_last_error.restype = ctypes.c_char_p
         L.diag_set_gemm_variant.argtypes = [ctypes.c_int]
+        L.diag_set_gemm_epilogue.argtypes = [ctypes.c_int]
         L.diag_device_count.restype = ctypes.c_int
         L.diag_device_arch.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.diag_gemm_bf16_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_gemm_bf16.argtypes = [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_double)] * 3
+        L.diag_gemm_fp8.argtypes = [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_double)] * 3
+        L.diag_gemm_fp8_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_hbm_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int] + \
             [ctypes.POINTER(ctypes.c_double)] * 3
         L.diag_memtest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
@@ -90,11 +96,25 @@ def set_gemm_variant(variant: str = "auto") -> None:
     lib().diag_set_gemm_variant(GEMM_VARIANTS[variant])
 
 
+def set_gemm_epilogue(lds_staged: bool) -> None:
+    """v3 kernels: write C with 4-byte stores straight from the MFMA layout (False) or staged
+    through LDS as 16-byte row pieces (True)."""
+    lib().diag_set_gemm_epilogue(1 if lds_staged else 0)
+
+
 def gemm_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int, stream: int = 0) -> None:
     """Launch the MFMA GEMM on caller-owned device memory: ``C = A @ Bt.T`` (bf16 in, fp32 out)."""
     if m % 128 or n % 128 or k % 64:
         raise ValueError("gemm: M, N must be multiples of 128 and K a multiple of 64")
     _check(lib().diag_gemm_bf16_launch(a_ptr, bt_ptr, c_ptr, m, n, k, stream))
+
+
+def gemm_fp8_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int, stream: int = 0) -> None:
+    """MX-fp8 GEMM on caller-owned memory: ``C = A @ Bt.T`` with OCP E4M3 operands (1 byte each,
+    unit block scales) and fp32 output, on ``v_mfma_scale_f32_16x16x128_f8f6f4``."""
+    if m % 256 or n % 256 or k % 128:
+        raise ValueError("gemm_fp8: M, N must be multiples of 256 and K a multiple of 128")
+    _check(lib().diag_gemm_fp8_launch(a_ptr, bt_ptr, c_ptr, m, n, k, stream))
 
 
 def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, samples: int = 4096) -> Dict[str, Any]:
@@ -106,6 +126,19 @@ def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, sa
     return {"pass": ok, "tflops": round(tf.value, 1), "max_rel_err": err.value, "ms_per_gemm": round(ms.value, 4),
             "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3),
             "detail": "" if ok else f"{tf.value:.0f} TFLOP/s, rel err {err.value:.2e}"}
+
+
+def gemm_fp8(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20,
+             samples: int = 4096) -> Dict[str, Any]:
+    """MX-fp8 GEMM burn-in: rate and sampled fp64-reference error (normalised by sum|a*b|)."""
+    tf, err, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    t0 = time.perf_counter()
+    _check(lib().diag_gemm_fp8(device, size, size, size, warmup, iters, samples, ctypes.byref(tf),
+                               ctypes.byref(err), ctypes.byref(ms)))
+    ok = tf.value >= GEMM_FP8_MIN_TFLOPS and err.value <= GEMM_FP8_MAX_ERR
+    return {"pass": ok, "tflops": round(tf.value, 1), "max_err_over_mag": err.value, "ms_per_gemm": round(ms.value, 4),
+            "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3),
+            "detail": "" if ok else f"{tf.value:.0f} TFLOP/s, err {err.value:.2e}"}
 
 
 def hbm(device: int = 0, gib: float = 4.0, iters: int = 10) -> Dict[str, Any]:
@@ -184,8 +217,8 @@ def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5) -
 
 LEVELS = {
     0: (),
-    1: ("gemm_quick", "hbm_quick", "mfma"),
-    2: ("gemm", "hbm", "memtest", "mfma"),
+    1: ("gemm_quick", "gemm_fp8_quick", "hbm_quick", "mfma"),
+    2: ("gemm", "gemm_fp8", "hbm", "memtest", "mfma"),
 }
 
 
@@ -196,6 +229,10 @@ def run(level: int = 1, device: int = 0) -> Dict[str, Dict[str, Any]]:
         try:
             if test == "gemm_quick":
                 out["gemm"] = gemm(device, size=4096, warmup=2, iters=10, samples=1024)
+            elif test == "gemm_fp8_quick":
+                out["gemm_fp8"] = gemm_fp8(device, size=4096, warmup=2, iters=10, samples=1024)
+            elif test == "gemm_fp8":
+                out["gemm_fp8"] = gemm_fp8(device)
             elif test == "hbm_quick":
                 out["hbm"] = hbm(device, gib=2.0, iters=5)
             elif test == "gemm":

@@ -80,7 +80,7 @@ def test_mfma_gemm_matches_fp32_reference(dev, m, n, k):
     assert rel < 1e-4 * max(1, k / 512), rel
 
 
-@pytest.mark.parametrize("variant", ["v1", "v2", "v3"])
+@pytest.mark.parametrize("variant", ["v1", "v2", "v3", "v3-lds-epilogue"])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (768, 512, 256),
                                    (1024, 768, 4096)])
 def test_mfma_gemm_variants_match_fp32_reference(dev, variant, m, n, k):
@@ -91,12 +91,14 @@ def test_mfma_gemm_variants_match_fp32_reference(dev, variant, m, n, k):
     a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
     bt = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
     c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
-    diag.set_gemm_variant(variant)
+    diag.set_gemm_variant(variant.split("-")[0])
+    diag.set_gemm_epilogue(variant.endswith("lds-epilogue"))
     try:
         diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
     finally:
         diag.set_gemm_variant("auto")
+        diag.set_gemm_epilogue(False)
     ref = a.float() @ bt.float().t()
     assert not torch.isnan(c).any()
     rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
@@ -241,3 +243,49 @@ def test_mfma_burn_rejects_inexact_iteration_counts():
     from k8s_gpu_node_checker_amd.ops import diag
     with pytest.raises(RuntimeError, match="exact fp32"):
         diag.mfma_burn(0, kinds=("mxfp4",), iters=4096, reps=1)
+
+
+@pytest.mark.parametrize("lds_epilogue", [False, True])
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (256, 512, 256), (512, 256, 384), (768, 512, 512),
+                                   (1024, 768, 8192), (4096, 4096, 4096)])
+def test_mxfp8_gemm_matches_fp32_reference(dev, m, n, k, lds_epilogue):
+    """MX-fp8 (E4M3) GEMM on the staggered v3 pipeline vs torch on the same fp8 values in fp32."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    diag.set_gemm_epilogue(lds_epilogue)
+    g = torch.Generator(device=dev).manual_seed(m + 3 * n + 7 * k)
+    a = torch.randn(m, k, device=dev, generator=g).to(torch.float8_e4m3fn)
+    bt = torch.randn(n, k, device=dev, generator=g).to(torch.float8_e4m3fn)
+    c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+    try:
+        diag.gemm_fp8_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k,
+                             torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        diag.set_gemm_epilogue(False)
+    ref = a.double() @ bt.double().t()
+    mag = a.double().abs() @ bt.double().abs().t()
+    assert not torch.isnan(c).any()
+    # The MX MFMA does not accumulate a 128-long block in exact fp32: hipBLASLt's fp8 GEMM
+    # (torch._scaled_mm) shows the identical error, <= 1.6e-5 of sum|a*b| (tools/fp8_numerics.py,
+    # profiles/fp8_numerics_mi355x.jsonl); a layout or staging bug is off by O(1).
+    worst = ((c.double() - ref).abs() / mag.clamp_min(1e-30)).max().item()
+    assert worst < 4e-5, worst
+
+
+def test_mxfp8_gemm_identity_asymmetric(dev):
+    from k8s_gpu_node_checker_amd.ops import diag
+    m = n = 256
+    k = 256
+    a = torch.eye(m, k, device=dev).to(torch.float8_e4m3fn)
+    bt = ((torch.arange(n * k, device=dev, dtype=torch.float32).reshape(n, k) % 13) - 6).to(torch.float8_e4m3fn)
+    c = torch.empty(m, n, device=dev, dtype=torch.float32)
+    diag.gemm_fp8_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(c, bt.float().t()[:m, :n])
+
+
+def test_diag_gemm_fp8_burn_in(dev):
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.gemm_fp8(0, size=4096, warmup=2, iters=5, samples=512)
+    assert r["pass"], r
+    assert r["max_err_over_mag"] < 4e-5 and r["tflops"] > 1200

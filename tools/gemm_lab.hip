@@ -143,7 +143,7 @@ __device__ __forceinline__ void v3_mfma(floatx4 (&acc)[8][4], const bf16x8 (&af)
 
 template <bool PRIO>
 __global__ void __launch_bounds__(V2_THREADS, 1)
-gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N, int K) {
+lab_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
@@ -678,8 +678,8 @@ int main(int argc, char** argv) {
     CK(hipFuncSetAttribute((const void*)gemm_bf16_v2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     CK(hipFuncSetAttribute((const void*)gemm_vp_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     CK(hipFuncSetAttribute((const void*)gemm_vp_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
-    CK(hipFuncSetAttribute((const void*)gemm_v3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
-    CK(hipFuncSetAttribute((const void*)gemm_v3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    CK(hipFuncSetAttribute((const void*)lab_v3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    CK(hipFuncSetAttribute((const void*)lab_v3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     CK(hipFuncSetAttribute((const void*)gemm_v4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     CK(hipFuncSetAttribute((const void*)gemm_v4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     CK(hipFuncSetAttribute((const void*)gemm_v5_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
@@ -702,9 +702,9 @@ int main(int argc, char** argv) {
     check("vP", ms);
     ms = time_ms([&] { hipLaunchKernelGGL(gemm_vp_kernel<true>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("vP+prio", ms);
-    ms = time_ms([&] { hipLaunchKernelGGL(gemm_v3_kernel<false>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
+    ms = time_ms([&] { hipLaunchKernelGGL(lab_v3_kernel<false>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("v3", ms);
-    ms = time_ms([&] { hipLaunchKernelGGL(gemm_v3_kernel<true>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
+    ms = time_ms([&] { hipLaunchKernelGGL(lab_v3_kernel<true>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("v3+prio", ms);
     ms = time_ms([&] { hipLaunchKernelGGL(gemm_v4_kernel<false>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("v4", ms);
