@@ -370,19 +370,55 @@ __device__ __forceinline__ void stg_load(i32x8& f, const u32x4* img, int row, in
             static_cast<int>(hi.x), static_cast<int>(hi.y), static_cast<int>(hi.z), static_cast<int>(hi.w)};
 }
 
-template <bool FP8>
+// MX-fp4 (E2M1): a 16-byte chunk is 32 values = one lane's share of a 16x16x128 MFMA, so the fp4
+// fragments are read exactly like the bf16 ones (chunks fq, fq + 4) and feed two MFMAs per K-tile.
+__device__ __forceinline__ void stg_load(u32x4 (&f)[2], const u32x4* img, int row, int fq) {
+  f[0] = img[swz(row, fq)];
+  f[1] = img[swz(row, fq + 4)];
+}
+
+__device__ __forceinline__ void stg_mfma(floatx4 (&acc)[8][4], const u32x4 (&af)[4][2], const u32x4 (&bf)[2][2],
+                                         int m0, int n0) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const u32x4 a = af[m][s], b = bf[n][s];
+        const i32x8 a8 = {static_cast<int>(a.x), static_cast<int>(a.y), static_cast<int>(a.z), static_cast<int>(a.w),
+                          0, 0, 0, 0};
+        const i32x8 b8 = {static_cast<int>(b.x), static_cast<int>(b.y), static_cast<int>(b.z), static_cast<int>(b.w),
+                          0, 0, 0, 0};
+        acc[m0 + m][n0 + n] =
+            __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, acc[m0 + m][n0 + n], 4, 4, 0, 127, 0, 127);
+      }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[m0 + m][n0 + n]));
+}
+
+enum GemmDtype { DT_BF16 = 0, DT_FP8 = 1, DT_FP4 = 2 };
+
+template <int DT>
 struct StgFrags {
   bf16x8 a[4][2], b0[2][2], b1[2][2];
 };
 template <>
-struct StgFrags<true> {
+struct StgFrags<DT_FP8> {
   i32x8 a[4], b0[2], b1[2];
 };
+template <>
+struct StgFrags<DT_FP4> {
+  u32x4 a[4][2], b0[2][2], b1[2][2];
+};
 
-// FP8 = false: bf16 A[M][K] . Bt[N][K]^T.  FP8 = true: MX-fp8 operands of K8 bytes per row, passed as
-// K = K8 / 2 "bf16 columns" so the byte-identical LDS-DMA staging is shared (a 64-column bf16 K-tile
-// is a 128-byte fp8 K-tile); only the swizzle, the fragment reads and the MFMA differ.
-template <bool FP8, bool EPI_LDS = false>
+// DT_BF16: bf16 A[M][K] . Bt[N][K]^T.  DT_FP8 / DT_FP4: MX operands (E4M3 bytes / packed E2M1 pairs,
+// unit scales) passed as K = row bytes / 2 "bf16 columns", so the byte-identical LDS-DMA staging is
+// shared (a 64-column bf16 K-tile is a 128-byte fp8 or fp4 K-tile); only the swizzle (fp8), the
+// fragment reads and the MFMA differ.
+template <int DT, bool EPI_LDS = false>
 __global__ void __launch_bounds__(V2_THREADS, 1)
 gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
                int K) {
@@ -412,6 +448,7 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
   const int KT = K / BK;
   const int frow = lane & 15, fq = lane >> 4;
 
+  constexpr bool FP8 = DT == DT_FP8;
   v2_fill<FP8>(smem, Ab, Bb, K, 0, wid, lane);
   if (KT > 1) {
     v2_fill<FP8>(smem + V2_STAGE_BYTES, Ab, Bb, K, 1, wid, lane);
@@ -422,7 +459,7 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
   STG_BARRIER();
   if (wr == 1) STG_BARRIER();  // the stagger
 
-  StgFrags<FP8> f;
+  StgFrags<DT> f;
   for (int kt = 0; kt < KT; ++kt) {
     unsigned char* cur = smem + (kt & 1) * V2_STAGE_BYTES;
     unsigned char* nxt = smem + ((kt + 1) & 1) * V2_STAGE_BYTES;
@@ -750,25 +787,25 @@ hipError_t enable_peer(int from, int to) {
   return e;
 }
 
-template <bool FP8, bool EPI>
+template <int DT, bool EPI>
 int launch_v3_inst(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v3_kernel<FP8, EPI>),
+    DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     attr_set = true;
   }
   const int nwg = (M / V2_BM) * (N / V2_BN);
-  hipLaunchKernelGGL((gemm_v3_kernel<FP8, EPI>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, stream,
+  hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, stream,
                      static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, M, N, Kcols);
   return 0;
 }
 
 // v3 launch (M, N multiples of 256; Kcols = bf16 columns, K8 / 2 for fp8), epilogue per g_gemm_epilogue
-template <bool FP8>
+template <int DT>
 int launch_v3(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
-  return g_gemm_epilogue ? launch_v3_inst<FP8, true>(A, Bt, C, M, N, Kcols, stream)
-                         : launch_v3_inst<FP8, false>(A, Bt, C, M, N, Kcols, stream);
+  return g_gemm_epilogue ? launch_v3_inst<DT, true>(A, Bt, C, M, N, Kcols, stream)
+                         : launch_v3_inst<DT, false>(A, Bt, C, M, N, Kcols, stream);
 }
 
 }  // namespace
@@ -825,7 +862,7 @@ int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N,
       hipLaunchKernelGGL(gemm_bf16_v2_kernel, dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
                          static_cast<hipStream_t>(stream), static_cast<const __bf16*>(A),
                          static_cast<const __bf16*>(Bt), C, M, N, K);
-    } else if (launch_v3<false>(A, Bt, C, M, N, K, static_cast<hipStream_t>(stream)) != 0) {
+    } else if (launch_v3<DT_BF16>(A, Bt, C, M, N, K, static_cast<hipStream_t>(stream)) != 0) {
       return -1;
     }
   } else {
@@ -844,7 +881,19 @@ int diag_gemm_fp8_launch(const void* A, const void* Bt, float* C, int M, int N, 
     g_err = "gemm_fp8: M, N must be multiples of 256 and K a multiple of 128";
     return -2;
   }
-  if (launch_v3<true>(A, Bt, C, M, N, K / 2, static_cast<hipStream_t>(stream)) != 0) return -1;
+  if (launch_v3<DT_FP8>(A, Bt, C, M, N, K / 2, static_cast<hipStream_t>(stream)) != 0) return -1;
+  DIAG_CHECK(hipGetLastError());
+  return 0;
+}
+
+// MX-fp4 GEMM: OCP E2M1 operands packed two per byte (element 2i in the low nibble), unit block
+// scales, fp32 C.  M, N multiples of 256; K (elements) a multiple of 256.
+int diag_gemm_fp4_launch(const void* A, const void* Bt, float* C, int M, int N, int K, void* stream) {
+  if (M % V2_BM || N % V2_BN || K % 256 || M <= 0 || N <= 0 || K <= 0) {
+    g_err = "gemm_fp4: M, N must be multiples of 256 and K a multiple of 256";
+    return -2;
+  }
+  if (launch_v3<DT_FP4>(A, Bt, C, M, N, K / 4, static_cast<hipStream_t>(stream)) != 0) return -1;
   DIAG_CHECK(hipGetLastError());
   return 0;
 }

@@ -54,6 +54,8 @@ def lib() -> ctypes.CDLL:
                                             ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_gemm_bf16.argtypes = [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_double)] * 3
         L.diag_gemm_fp8.argtypes = [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_double)] * 3
+        L.diag_gemm_fp4_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_gemm_fp8_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_hbm_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int] + \
@@ -115,6 +117,14 @@ def gemm_fp8_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int,
     if m % 256 or n % 256 or k % 128:
         raise ValueError("gemm_fp8: M, N must be multiples of 256 and K a multiple of 128")
     _check(lib().diag_gemm_fp8_launch(a_ptr, bt_ptr, c_ptr, m, n, k, stream))
+
+
+def gemm_fp4_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int, stream: int = 0) -> None:
+    """MX-fp4 GEMM on caller-owned memory: OCP E2M1 operands packed two per byte (element 2i in the
+    low nibble), unit block scales, fp32 ``C = A @ Bt.T``; ``k`` counts elements."""
+    if m % 256 or n % 256 or k % 256:
+        raise ValueError("gemm_fp4: M, N must be multiples of 256 and K a multiple of 256")
+    _check(lib().diag_gemm_fp4_launch(a_ptr, bt_ptr, c_ptr, m, n, k, stream))
 
 
 def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, samples: int = 4096) -> Dict[str, Any]:

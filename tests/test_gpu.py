@@ -289,3 +289,30 @@ def test_diag_gemm_fp8_burn_in(dev):
     r = diag.gemm_fp8(0, size=4096, warmup=2, iters=5, samples=512)
     assert r["pass"], r
     assert r["max_err_over_mag"] < 4e-5 and r["tflops"] > 1200
+
+
+FP4_VALUES = [0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0, -0.0, -0.5, -1.0, -1.5, -2.0, -3.0, -4.0, -6.0]
+
+
+def _fp4_operand(rows, k, gen, dev):
+    """Random E2M1 codes -> (packed bytes [rows, k/2], decoded float32 values [rows, k])."""
+    codes = torch.randint(0, 16, (rows, k), generator=gen, device=dev, dtype=torch.int32)
+    table = torch.tensor(FP4_VALUES, device=dev)
+    packed = (codes[:, 0::2] | (codes[:, 1::2] << 4)).to(torch.uint8)
+    return packed.contiguous(), table[codes]
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 256, 768), (768, 512, 1024), (1024, 1024, 8192)])
+def test_mxfp4_gemm_matches_fp64_reference(dev, m, n, k):
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + n + k)
+    a, av = _fp4_operand(m, k, g, dev)
+    bt, bv = _fp4_operand(n, k, g, dev)
+    c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+    diag.gemm_fp4_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = av.double() @ bv.double().t()
+    mag = av.double().abs() @ bv.double().abs().t()
+    assert not torch.isnan(c).any()
+    worst = ((c.double() - ref).abs() / mag.clamp_min(1e-30)).max().item()
+    assert worst < 4e-5, worst

@@ -1,4 +1,4 @@
-"""MX-fp8 GEMM (diag v3 pipeline) vs bf16 v3 vs torch (hipBLASLt) at 4096^3 / 8192^3, TFLOP/s."""
+"""MX-fp8 / MX-fp4 GEMM (diag v3 pipeline) vs bf16 v3 vs torch (hipBLASLt) at 4096^3 / 8192^3, TFLOP/s."""
 import json
 import os
 import sys
@@ -43,7 +43,13 @@ def main():
             errs["mxfp8_v3" + tag] = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
             rows["bf16_v3" + tag] = timeit(
                 lambda: diag.gemm_launch(a16.data_ptr(), b16.data_ptr(), c.data_ptr(), n, n, n, st), it)
-        diag.set_gemm_epilogue(False)
+        diag.set_gemm_epilogue(True)
+        codes_a = torch.randint(0, 16, (n, n), device="cuda", dtype=torch.int32)
+        codes_b = torch.randint(0, 16, (n, n), device="cuda", dtype=torch.int32)
+        a4 = (codes_a[:, 0::2] | (codes_a[:, 1::2] << 4)).to(torch.uint8).contiguous()
+        b4 = (codes_b[:, 0::2] | (codes_b[:, 1::2] << 4)).to(torch.uint8).contiguous()
+        rows["mxfp4_v3_lds_epilogue"] = timeit(
+            lambda: diag.gemm_fp4_launch(a4.data_ptr(), b4.data_ptr(), c.data_ptr(), n, n, n, st), it)
         rows["torch_bf16"] = timeit(lambda: a16 @ b16.t(), it)
         try:
             one = torch.ones((), device="cuda")
