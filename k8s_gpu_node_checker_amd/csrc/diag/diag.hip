@@ -20,6 +20,7 @@
 //               failing 16-byte word.
 //   p2p_copy    xGMI pair check: peer copies between two GPUs of the node,
 //               timed, and the received pattern verified on the destination.
+//   host_link   pinned host <-> device copy bandwidth over the PCIe link.
 //   mfma_burn   matrix-core datapath burn-in per precision (bf16, fp8, MX-fp8,
 //               MX-fp4), register-resident, every lane's exact result checked.
 //
@@ -1294,6 +1295,48 @@ int diag_mfma_burn(int device, int kind, int iters, int reps, double* tflops, un
   DIAG_CHECK(hipMemcpy(errors, dcnt.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   const double flop = static_cast<double>(blocks) * 4 /*waves*/ * iters * 16 /*MFMA per iter*/ * 2.0 * 16 * 16 * K;
   *tflops = ms > 0.f ? flop * reps / (ms * 1e-3) / 1e12 : 0.0;
+  return 0;
+}
+
+// Host link check: pinned host <-> device copies of `bytes`, `iters` each way (SDMA over PCIe),
+// timed with events.  A slot trained down to x8 / an older generation shows up here at half rate.
+int diag_host_link(int device, size_t bytes, int iters, double* h2d_gbps, double* d2h_gbps) {
+  if (bytes < 4096 || iters < 1) {
+    g_err = "host_link: bytes >= 4096 and iters >= 1";
+    return -2;
+  }
+  DIAG_CHECK(hipSetDevice(device));
+  void* host = nullptr;
+  DIAG_CHECK(hipHostMalloc(&host, bytes, hipHostMallocDefault));
+  struct HostFree {
+    void* p;
+    ~HostFree() { (void)hipHostFree(p); }
+  } hf{host};
+  memset(host, 0x5A, bytes);
+  DevBuf dev;
+  DIAG_CHECK(dev.alloc(device, bytes));
+  hipStream_t st;
+  DIAG_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  DIAG_CHECK(hipEventCreate(&e0));
+  DIAG_CHECK(hipEventCreate(&e1));
+  for (int dir = 0; dir < 2; ++dir) {
+    auto copy = [&]() {
+      return dir == 0 ? hipMemcpyAsync(dev.ptr, host, bytes, hipMemcpyHostToDevice, st)
+                      : hipMemcpyAsync(host, dev.ptr, bytes, hipMemcpyDeviceToHost, st);
+    };
+    DIAG_CHECK(copy());  // warm-up
+    DIAG_CHECK(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i) DIAG_CHECK(copy());
+    DIAG_CHECK(hipEventRecord(e1, st));
+    DIAG_CHECK(hipEventSynchronize(e1));
+    const float ms = elapsed_ms(e0, e1);
+    const double gbps = ms > 0.f ? static_cast<double>(iters) * static_cast<double>(bytes) / (ms * 1e-3) / 1e9 : 0.0;
+    *(dir == 0 ? h2d_gbps : d2h_gbps) = gbps;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(st);
   return 0;
 }
 

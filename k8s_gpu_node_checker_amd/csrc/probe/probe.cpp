@@ -200,6 +200,19 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
   int64_t temp = 0;
   if (amdsmi_get_temp_metric(h, AMDSMI_TEMPERATURE_TYPE_HOTSPOT, AMDSMI_TEMP_CURRENT, &temp) == AMDSMI_STATUS_SUCCESS)
     kv_i64(o, "hotspot_c", temp);
+  // PCIe host link: a slot trained down (x8, Gen4) halves host<->GPU bandwidth without any error;
+  // the current speed may drop at idle (link power management), the width does not.
+  amdsmi_pcie_info_t pcie;
+  memset(&pcie, 0, sizeof pcie);
+  if (amdsmi_get_pcie_info(h, &pcie) == AMDSMI_STATUS_SUCCESS) {
+    kv_u64(o, "pcie_width", pcie.pcie_metric.pcie_width);
+    kv_u64(o, "pcie_max_width", pcie.pcie_static.max_pcie_width);
+    kv_u64(o, "pcie_speed_mts", pcie.pcie_metric.pcie_speed);
+    kv_u64(o, "pcie_max_speed_mts", pcie.pcie_static.max_pcie_speed);  // header says GT/s; MI355X reports 32000
+    if (pcie.pcie_metric.pcie_replay_count != UINT64_MAX) kv_u64(o, "pcie_replays", pcie.pcie_metric.pcie_replay_count);
+    if (pcie.pcie_metric.pcie_l0_to_recovery_count != UINT64_MAX)
+      kv_u64(o, "pcie_recoveries", pcie.pcie_metric.pcie_l0_to_recovery_count);
+  }
   double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
   key(o, "probe_us");
   o += std::to_string(static_cast<int64_t>(us));

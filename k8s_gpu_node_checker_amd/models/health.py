@@ -37,6 +37,7 @@ VRAM_MIN_FRACTION = 0.97
 XGMI_LINKS_EXPECTED = 7                       # 8-GPU hive: 7 peers per GPU
 NUM_CUS = 256
 HOTSPOT_WARN_C = 100
+PCIE_REPLAY_WARN = 10000                      # link-level retries since boot: a marginal slot or riser
 
 HEALTHY, DEGRADED, UNHEALTHY, UNKNOWN = "healthy", "degraded", "unhealthy", "unknown"
 _OK_STATES = (HEALTHY, DEGRADED)
@@ -162,6 +163,12 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str],
     t = g.get("hotspot_c")
     if isinstance(t, (int, float)) and t >= HOTSPOT_WARN_C:
         warn.append(f"gpu{idx}: hotspot {t} C")
+    w, mw = g.get("pcie_width"), g.get("pcie_max_width")
+    if isinstance(w, int) and isinstance(mw, int) and 0 < w < mw:
+        warn.append(f"gpu{idx}: PCIe link x{w} of x{mw}")
+    rp = g.get("pcie_replays")
+    if isinstance(rp, int) and rp >= PCIE_REPLAY_WARN:
+        warn.append(f"gpu{idx}: {rp} PCIe replays")
     diag = g.get("diag")
     if isinstance(diag, dict):
         for test, res in diag.items():

@@ -112,6 +112,15 @@ def probe_python(node: str) -> Dict[str, Any]:
                                                           A.AmdSmiTemperatureMetric.CURRENT)
             except Exception:
                 pass
+            pcie = q(A.amdsmi_get_pcie_info) or {}
+            pst, pmt = pcie.get("pcie_static") or {}, pcie.get("pcie_metric") or {}
+            for out_key, src, key in (("pcie_width", pmt, "pcie_width"), ("pcie_max_width", pst, "max_pcie_width"),
+                                      ("pcie_speed_mts", pmt, "pcie_speed"),
+                                      ("pcie_max_speed_mts", pst, "max_pcie_speed"),
+                                      ("pcie_replays", pmt, "pcie_replay_count"),
+                                      ("pcie_recoveries", pmt, "pcie_l0_to_recovery_count")):
+                if isinstance(src.get(key), int):
+                    g[out_key] = src[key]
             rep["gpus"].append({k: v for k, v in g.items() if v is not None})
     finally:
         rep["probe_ms"] = round((time.perf_counter() - t0) * 1e3, 3)

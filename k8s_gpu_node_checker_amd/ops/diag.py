@@ -35,7 +35,9 @@ MEMTEST_MAX_ERRORS = 0
 # profiles/mfma_lab_mi355x.jsonl: bf16 1687, fp8 1803, MX-fp8 4027, MX-fp4 7171 TFLOP/s dense)
 MFMA_KINDS = ("bf16", "fp8", "mxfp8", "mxfp4")
 MFMA_MIN_TFLOPS = {"bf16": 1000.0, "fp8": 1000.0, "mxfp8": 2400.0, "mxfp4": 4300.0}
-P2P_MIN_FRACTION_OF_MEDIAN = 0.5  # a GPU pair slower than half the node's median pair: suspect link
+P2P_MIN_FRACTION_OF_MEDIAN = 0.5
+HOST_LINK_MIN_GBPS = 28.0     # PCIe Gen5 x16 host link, pinned copies: measured 56.8 / 56.7 GB/s h2d / d2h
+                              # (profiles/diag_mi355x.json); a Gen4 or x8 link lands at about half  # a GPU pair slower than half the node's median pair: suspect link
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -65,6 +67,8 @@ def lib() -> ctypes.CDLL:
                                    ctypes.POINTER(ctypes.c_double)]
         L.diag_mfma_burn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong)]
+        L.diag_host_link.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double)]
         L.diag_p2p_copy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                     ctypes.POINTER(ctypes.c_int)]
@@ -193,6 +197,17 @@ def mfma_burn(device: int = 0, kinds=MFMA_KINDS, iters: int = 2000, reps: int = 
             "detail": "; ".join(problems)}
 
 
+def host_link(device: int = 0, mib: int = 256, iters: int = 5) -> Dict[str, Any]:
+    """Pinned host <-> device bandwidth over the GPU's PCIe link (GB/s each way)."""
+    h2d, d2h = ctypes.c_double(), ctypes.c_double()
+    t0 = time.perf_counter()
+    _check(lib().diag_host_link(device, mib << 20, iters, ctypes.byref(h2d), ctypes.byref(d2h)))
+    ok = h2d.value >= HOST_LINK_MIN_GBPS and d2h.value >= HOST_LINK_MIN_GBPS
+    return {"pass": ok, "h2d_gbps": round(h2d.value, 1), "d2h_gbps": round(d2h.value, 1),
+            "wall_s": round(time.perf_counter() - t0, 3),
+            "detail": "" if ok else f"h2d {h2d.value:.1f} GB/s, d2h {d2h.value:.1f} GB/s"}
+
+
 def p2p_copy(src: int, dst: int, mib: int = 256, iters: int = 5) -> Dict[str, Any]:
     """One ordered GPU pair: copy bandwidth over xGMI (GB/s) and pattern errors on arrival."""
     gbps, errs, peer = ctypes.c_double(), ctypes.c_ulonglong(), ctypes.c_int()
@@ -228,7 +243,7 @@ def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5) -
 LEVELS = {
     0: (),
     1: ("gemm_quick", "gemm_fp8_quick", "hbm_quick", "mfma"),
-    2: ("gemm", "gemm_fp8", "hbm", "memtest", "mfma"),
+    2: ("gemm", "gemm_fp8", "hbm", "memtest", "mfma", "host_link"),
 }
 
 
@@ -253,6 +268,8 @@ def run(level: int = 1, device: int = 0) -> Dict[str, Dict[str, Any]]:
                 out["memtest"] = memtest(device)
             elif test == "mfma":
                 out["mfma"] = mfma_burn(device)
+            elif test == "host_link":
+                out["host_link"] = host_link(device)
         except NativeUnavailable:
             raise
         except Exception as e:  # a failing diagnostic is a verdict, not a crash

@@ -316,3 +316,12 @@ def test_mxfp4_gemm_matches_fp64_reference(dev, m, n, k):
     assert not torch.isnan(c).any()
     worst = ((c.double() - ref).abs() / mag.clamp_min(1e-30)).max().item()
     assert worst < 4e-5, worst
+
+
+def test_host_link_bandwidth_and_pcie_fields(dev):
+    from k8s_gpu_node_checker_amd.ops import amdsmi_probe, diag
+    r = diag.host_link(0, mib=128, iters=3)
+    print(json.dumps(r))
+    assert r["h2d_gbps"] > 1.0 and r["d2h_gbps"] > 1.0
+    g = amdsmi_probe.probe_native("n")["gpus"][0]
+    assert g.get("pcie_max_width", 0) >= 1 and g.get("pcie_width", 0) >= 1, g

@@ -49,7 +49,9 @@ def test_identity_survives_generic_market_name():
 
 
 @pytest.mark.parametrize("override,needle", [({"ecc_deferred": 1}, "deferred"), ({"ecc_correctable": 5000}, "correctable"),
-                                            ({"bad_pages": 3}, "retired pages"), ({"hotspot_c": 104}, "hotspot")])
+                                            ({"bad_pages": 3}, "retired pages"), ({"hotspot_c": 104}, "hotspot"),
+                                            ({"pcie_width": 8, "pcie_max_width": 16}, "PCIe link x8 of x16"),
+                                            ({"pcie_replays": 20000}, "PCIe replays")])
 def test_warnings_degrade_but_stay_ok(override, needle):
     v = H.evaluate_report(rep(gpu0=override), 8)
     assert v.state == H.DEGRADED and v.ok
@@ -218,3 +220,10 @@ def test_p2p_matrix_flags_slow_corrupting_and_non_peer_pairs(monkeypatch):
         fake[k] = (50.0, 0, True)
     assert diag.p2p_matrix([0, 1, 2])["pass"]
     assert diag.p2p_matrix([0])["skipped"] and diag.p2p_matrix([0])["pass"]
+
+
+def test_pcie_full_width_and_idle_speed_are_healthy():
+    # the link may idle at a lower speed (power management); only a narrower width is a finding
+    v = H.evaluate_report(rep(gpu0={"pcie_width": 16, "pcie_max_width": 16, "pcie_speed_mts": 2500,
+                                    "pcie_max_speed_mts": 32000, "pcie_replays": 3}), 8)
+    assert v.state == H.HEALTHY, v.warnings
