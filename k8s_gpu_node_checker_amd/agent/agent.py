@@ -127,7 +127,8 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
         return "# no probe yet\n"
     lines = ["# TYPE mi355x_agent_probe_timestamp_seconds gauge", f"mi355x_agent_probe_timestamp_seconds {rep.get('ts', 0)}",
              "# TYPE mi355x_gpu_ecc_uncorrectable gauge", "# TYPE mi355x_gpu_xgmi_links_up gauge",
-             "# TYPE mi355x_gpu_hotspot_celsius gauge"]
+             "# TYPE mi355x_gpu_hotspot_celsius gauge", "# TYPE mi355x_gpu_pcie_width gauge",
+             "# TYPE mi355x_gpu_pcie_replays counter"]
     for g in rep.get("gpus") or []:
         lbl = f'gpu="{g.get("index")}",bdf="{g.get("bdf", "")}"'
         if isinstance(g.get("ecc_uncorrectable"), int):
@@ -136,10 +137,21 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
             lines.append(f"mi355x_gpu_xgmi_links_up{{{lbl}}} {g['xgmi'].count('U')}")
         if isinstance(g.get("hotspot_c"), (int, float)):
             lines.append(f"mi355x_gpu_hotspot_celsius{{{lbl}}} {g['hotspot_c']}")
+        if isinstance(g.get("pcie_width"), int):
+            lines.append(f"mi355x_gpu_pcie_width{{{lbl}}} {g['pcie_width']}")
+        if isinstance(g.get("pcie_replays"), int):
+            lines.append(f"mi355x_gpu_pcie_replays{{{lbl}}} {g['pcie_replays']}")
         for test, res in (g.get("diag") or {}).items():
-            for k in ("tflops", "copy_tbs", "errors"):
-                if k in res:
+            for k in ("tflops", "copy_tbs", "read_tbs", "errors", "h2d_gbps", "d2h_gbps"):
+                if isinstance(res.get(k), (int, float)):
                     lines.append(f'mi355x_gpu_diag_{k}{{{lbl},test="{test}"}} {res[k]}')
+            for kind, row in ((res.get("kinds") or {}) if isinstance(res.get("kinds"), dict) else {}).items():
+                lines.append(f'mi355x_gpu_diag_tflops{{{lbl},test="{test}",dtype="{kind}"}} {row.get("tflops", 0)}')
+    fabric = (rep.get("fabric") or {}).get("p2p")
+    if isinstance(fabric, dict) and isinstance(fabric.get("median_gbps"), (int, float)):
+        lines.append("# TYPE mi355x_node_xgmi_p2p_gbps gauge")
+        lines.append(f'mi355x_node_xgmi_p2p_gbps{{stat="median"}} {fabric["median_gbps"]}')
+        lines.append(f'mi355x_node_xgmi_p2p_gbps{{stat="min"}} {fabric.get("min_gbps", 0)}')
     return "\n".join(lines) + "\n"
 
 

@@ -110,7 +110,9 @@ def mi355x_probe_report(node: str, gpus: int = 8, ts: Optional[float] = None, **
              "vbios_name": "AMD MI355X", "device_id": "0x75a3",
              "cus": 256, "vram_type": 5, "vram_mb": 294896, "ecc_correctable": 0, "ecc_uncorrectable": 0,
              "ecc_deferred": 0, "bad_pages": 0, "xgmi": "XUUUUUUU", "kfd": True,
-             "compute_partition": "SPX", "memory_partition": "NPS1", "hotspot_c": 45}
+             "compute_partition": "SPX", "memory_partition": "NPS1", "hotspot_c": 45,
+             "pcie_width": 16, "pcie_max_width": 16, "pcie_speed_mts": 32000, "pcie_max_speed_mts": 32000,
+             "pcie_replays": 0, "pcie_recoveries": 0}
         g.update(overrides.get(f"gpu{i}", {}))
         entries.append(g)
     rep = {"schema": "mi355x-health/v1", "node": node, "ts": time.time() if ts is None else ts,

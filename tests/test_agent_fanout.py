@@ -57,6 +57,7 @@ def test_agent_http_endpoint(fixture_report):
         assert json.loads(request(base + "/probe").body)["state"] == "healthy"
         m = request(base + "/metrics").text
         assert 'mi355x_gpu_xgmi_links_up{gpu="0",bdf="0000:05:00.0"} 7' in m
+        assert 'mi355x_gpu_pcie_width{gpu="0",bdf="0000:05:00.0"} 16' in m
         assert request(base + "/nope").status == 404
     finally:
         srv.shutdown()
@@ -183,3 +184,14 @@ def test_fanout_asyncio_debug_mode_clean(fixture_report):
         assert not leaks, leaks
     finally:
         s.shutdown()
+
+
+def test_agent_metrics_cover_diag_kinds_and_fabric():
+    rep = fixtures.mi355x_probe_report("n", gpus=1)
+    rep["gpus"][0]["diag"] = {"mfma": {"pass": True, "kinds": {"mxfp4": {"tflops": 7600.0, "errors": 0}}},
+                              "host_link": {"pass": True, "h2d_gbps": 56.8, "d2h_gbps": 56.7}}
+    rep["fabric"] = {"p2p": {"pass": True, "median_gbps": 48.0, "min_gbps": 45.0}}
+    m = A._metrics(rep)
+    assert 'mi355x_gpu_diag_tflops{gpu="0",bdf="0000:05:00.0",test="mfma",dtype="mxfp4"} 7600.0' in m
+    assert 'mi355x_gpu_diag_h2d_gbps{gpu="0",bdf="0000:05:00.0",test="host_link"} 56.8' in m
+    assert 'mi355x_node_xgmi_p2p_gbps{stat="min"} 45.0' in m
