@@ -67,14 +67,15 @@ def _own_gpu(gpus, local_rank, cuda):
 
 
 def _fabric_check(world, local_rank, cuda):
-    """Untimed: all-reduce bus bandwidth + correctness over the job's process group (RCCL over xGMI
-    on GPUs, gloo on CPU) -- the node-fabric health the passive probe can only infer from link state."""
+    """Untimed: bus bandwidth + correctness of all-reduce / reduce-scatter / all-gather / all-to-all over
+    the job's process group (RCCL over xGMI on GPUs, gloo on CPU) -- the node-fabric health the passive
+    probe can only infer from link state."""
     from k8s_gpu_node_checker_amd.parallel import collectives
     import torch
     sizes = [64 << 20, 256 << 20] if cuda else [1 << 20]
     try:
-        rows = collectives.allreduce_bench(sizes, iters=10, warmup=3,
-                                           device=torch.device(f"cuda:{local_rank}") if cuda else None)
+        rows = collectives.collective_bench(sizes, iters=10, warmup=3,
+                                            device=torch.device(f"cuda:{local_rank}") if cuda else None)
         return {"backend": "nccl(rccl)" if cuda else "gloo", "rows": rows, **collectives.verdict(rows, world)}
     except Exception as e:  # report, never lose the benchmark line over the fabric check
         return {"backend": "nccl(rccl)" if cuda else "gloo", "pass": False, "detail": f"{type(e).__name__}: {e}"}

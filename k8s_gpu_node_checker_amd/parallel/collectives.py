@@ -1,20 +1,25 @@
-"""xGMI / RCCL collective diagnostic: all-reduce bus bandwidth across a node's MI355X GPUs.
+"""xGMI / RCCL collective diagnostic: bus bandwidth of every collective across a node's MI355X GPUs.
 
 The passive probe only sees that every xGMI link reports "Up"; this measures
 what the fabric actually delivers.  One process per GPU, ``torch.distributed``
 with backend ``"nccl"`` (= RCCL on ROCm) over the 7 point-to-point xGMI links
-of each MI355X.  For each message size it times ``iters`` all-reduces and
-reports
+of each MI355X.  The four collectives data/tensor/sequence/expert parallelism
+lean on take different RCCL algorithms (rings for all-reduce / reduce-scatter /
+all-gather, direct peer exchanges for all-to-all), so each is checked.  For each
+op and message size it times ``iters`` calls and reports
 
-* ``algbw = bytes / t`` and ``busbw = algbw * 2 (n-1) / n`` (ring-equivalent
-  bytes each GPU moves, the nccl-tests convention), and
-* a correctness check: every rank contributes ``rank + 1``; the result must be
-  ``n (n + 1) / 2`` everywhere (a broken link or a bad GPU corrupts it).
+* ``algbw = bytes / t`` and ``busbw`` in the nccl-tests convention:
+  ``algbw * 2 (n-1) / n`` for all-reduce, ``algbw * (n-1) / n`` for the others
+  (``bytes`` = the larger of the per-rank input and output), and
+* a correctness check with rank-coded data: all-reduce of ``rank + 1`` must be
+  ``n (n + 1) / 2``; reduce-scatter likewise per chunk; all-gather chunk ``i``
+  must be ``i + 1``; all-to-all chunk ``i`` received by rank ``r`` must be
+  ``i * n + r`` (a broken link, a wrong route or a bad GPU corrupts it).
 
 Run on a node (the agent's level-3 check, or by hand)::
 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
-        -m k8s_gpu_node_checker_amd.parallel.collectives --sizes 64M,256M,1G
+        -m k8s_gpu_node_checker_amd.parallel.collectives --sizes 64M,256M,1G [--ops all_reduce,all_to_all]
 
 Size choice for xGMI: ring all-reduce is per-link bound, so the bandwidth
 plateau needs messages of hundreds of MB per GPU; 288 GB of HBM per GPU makes
@@ -45,9 +50,70 @@ def parse_size(s: str) -> int:
     return int(float(s) * mult)
 
 
-def allreduce_bench(sizes: Sequence[int], iters: int = 20, warmup: int = 5, device: Optional[Any] = None,
-                    group: Any = None) -> List[Dict[str, Any]]:
-    """Time all-reduce at each byte size on the current process group; returns per-size rows (rank-local)."""
+OPS = ("all_reduce", "reduce_scatter", "all_gather", "all_to_all")
+
+
+def _op_buffers(op: str, nbytes: int, world: int, rank: int, dev: Any):
+    """(call, check) for one op: ``call()`` runs it once, ``check()`` re-seeds, runs and verifies."""
+    import torch
+    import torch.distributed as dist
+
+    chunk = max(1, nbytes // 4 // world)
+    n = chunk * world
+    if op == "all_reduce":
+        x = torch.full((n,), float(rank + 1), dtype=torch.float32, device=dev)
+
+        def call(group=None):
+            dist.all_reduce(x, group=group)
+
+        def check(group=None):
+            x.fill_(float(rank + 1))
+            call(group)
+            return bool(torch.all(x == world * (world + 1) / 2).item())
+    elif op == "reduce_scatter":
+        x = torch.full((n,), float(rank + 1), dtype=torch.float32, device=dev)
+        y = torch.empty((chunk,), dtype=torch.float32, device=dev)
+
+        def call(group=None):
+            dist.reduce_scatter_tensor(y, x, group=group)
+
+        def check(group=None):
+            y.fill_(-1.0)
+            call(group)
+            return bool(torch.all(y == world * (world + 1) / 2).item())
+    elif op == "all_gather":
+        x = torch.full((chunk,), float(rank + 1), dtype=torch.float32, device=dev)
+        y = torch.empty((n,), dtype=torch.float32, device=dev)
+        want = torch.arange(1, world + 1, dtype=torch.float32, device=dev).repeat_interleave(chunk)
+
+        def call(group=None):
+            dist.all_gather_into_tensor(y, x, group=group)
+
+        def check(group=None):
+            y.fill_(-1.0)
+            call(group)
+            return bool(torch.equal(y, want))
+    elif op == "all_to_all":
+        # chunk j of rank r's input goes to rank j; value r * world + j identifies (source, destination)
+        x = (rank * world + torch.arange(world, dtype=torch.float32, device=dev)).repeat_interleave(chunk)
+        y = torch.empty((n,), dtype=torch.float32, device=dev)
+        want = (torch.arange(world, dtype=torch.float32, device=dev) * world + rank).repeat_interleave(chunk)
+
+        def call(group=None):
+            dist.all_to_all_single(y, x, group=group)
+
+        def check(group=None):
+            y.fill_(-1.0)
+            call(group)
+            return bool(torch.equal(y, want))
+    else:
+        raise ValueError(f"unknown collective {op!r}")
+    return n * 4, call, check
+
+
+def collective_bench(sizes: Sequence[int], ops: Sequence[str] = OPS, iters: int = 20, warmup: int = 5,
+                     device: Optional[Any] = None, group: Any = None) -> List[Dict[str, Any]]:
+    """Time each collective at each byte size on the current process group; rank-local rows."""
     import torch
     import torch.distributed as dist
 
@@ -55,45 +121,55 @@ def allreduce_bench(sizes: Sequence[int], iters: int = 20, warmup: int = 5, devi
     rank = dist.get_rank(group)
     dev = device if device is not None else torch.device("cpu")
     rows = []
-    for nbytes in sizes:
-        n = max(1, nbytes // 4)
-        x = torch.full((n,), float(rank + 1), dtype=torch.float32, device=dev)
-        expect = world * (world + 1) / 2
-        for _ in range(warmup):
-            dist.all_reduce(x, group=group)
-            x.fill_(float(rank + 1))
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        dist.barrier(group=group)
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            dist.all_reduce(x, group=group)
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        dt = (time.perf_counter() - t0) / iters
-        # after `iters` in-place reductions the value is expect * world**(iters-1); check the last one only
-        x.fill_(float(rank + 1))
-        dist.all_reduce(x, group=group)
-        ok = bool(torch.all(x == expect).item())
-        algbw = n * 4 / dt / 1e9
-        rows.append({"bytes": n * 4, "ms": round(dt * 1e3, 4), "algbw_gbps": round(algbw, 2),
-                     "busbw_gbps": round(algbw * 2 * (world - 1) / world, 2) if world > 1 else None,
-                     "correct": ok})
+    for op in ops:
+        factor = 2 * (world - 1) / world if op == "all_reduce" else (world - 1) / world
+        for nbytes in sizes:
+            nb, call, check = _op_buffers(op, nbytes, world, rank, dev)
+            for _ in range(warmup):
+                call(group)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            dist.barrier(group=group)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                call(group)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            dt = (time.perf_counter() - t0) / iters
+            ok = check(group)
+            algbw = nb / dt / 1e9
+            rows.append({"op": op, "bytes": nb, "ms": round(dt * 1e3, 4), "algbw_gbps": round(algbw, 2),
+                         "busbw_gbps": round(algbw * factor, 2) if world > 1 else None, "correct": ok})
     return rows
 
 
+def allreduce_bench(sizes: Sequence[int], iters: int = 20, warmup: int = 5, device: Optional[Any] = None,
+                    group: Any = None) -> List[Dict[str, Any]]:
+    """All-reduce rows only (the historical entry point)."""
+    return collective_bench(sizes, ("all_reduce",), iters, warmup, device, group)
+
+
 def verdict(rows: List[Dict[str, Any]], world: int, min_busbw: float = MIN_BUSBW_GBPS) -> Dict[str, Any]:
-    big = [r for r in rows if r["bytes"] >= 256 << 20 and r["busbw_gbps"] is not None]
+    """Pass: every op returned the right data, and on a full 8-GPU hive the best >= 256 MiB all-reduce
+    busbw clears ``min_busbw`` (the other ops are reported, not thresholded)."""
+    big = [r for r in rows if r["bytes"] >= 256 << 20 and r["busbw_gbps"] is not None
+           and r.get("op", "all_reduce") == "all_reduce"]
     best = max((r["busbw_gbps"] for r in big), default=None)
-    correct = all(r["correct"] for r in rows)
-    ok = correct and (best is None or world < 8 or best >= min_busbw)
-    detail = "" if ok else ("all-reduce result mismatch" if not correct else f"busbw {best} GB/s < {min_busbw}")
-    return {"pass": ok, "world": world, "best_busbw_gbps": best, "detail": detail}
+    wrong = sorted({r.get("op", "all_reduce") for r in rows if not r["correct"]})
+    ok = not wrong and (best is None or world < 8 or best >= min_busbw)
+    detail = "" if ok else (f"result mismatch: {', '.join(wrong)}" if wrong else f"busbw {best} GB/s < {min_busbw}")
+    per_op = {}
+    for r in rows:
+        op = r.get("op", "all_reduce")
+        if r["busbw_gbps"] is not None:
+            per_op[op] = max(per_op.get(op, 0.0), r["busbw_gbps"])
+    return {"pass": ok, "world": world, "best_busbw_gbps": best, "best_busbw_by_op": per_op, "detail": detail}
 
 
 def main(argv: Optional[List[str]] = None) -> int:
     ap = argparse.ArgumentParser(description="RCCL/xGMI all-reduce bus-bandwidth diagnostic")
     ap.add_argument("--sizes", default="1M,16M,64M,256M,1G")
+    ap.add_argument("--ops", default=",".join(OPS), help="comma list of " + ", ".join(OPS))
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--backend", default=None, help="nccl (RCCL, default with GPUs) or gloo")
@@ -109,7 +185,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         torch.cuda.set_device(local_rank)
     dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local_rank}") if cuda else torch.device("cpu")
-    rows = allreduce_bench([parse_size(s) for s in args.sizes.split(",")], args.iters, args.warmup, dev)
+    rows = collective_bench([parse_size(s) for s in args.sizes.split(",")], args.ops.split(","), args.iters,
+                            args.warmup, dev)
     world = dist.get_world_size()
     if dist.get_rank() == 0:
         print(json.dumps({"backend": backend, "rows": rows, **verdict(rows, world, args.min_busbw)}), flush=True)

@@ -56,7 +56,7 @@ def test_bench_torchrun_two_ranks_gloo():
     assert d["check_ok"] and d["health"] == {"healthy": 2}
     fab = d["fabric"]  # untimed all-reduce check over the job's process group (gloo here, RCCL on GPUs)
     assert fab["pass"] and fab["world"] == 2 and fab["backend"] == "gloo"
-    assert all(r["correct"] for r in fab["rows"])
+    assert all(r["correct"] for r in fab["rows"]) and len({r["op"] for r in fab["rows"]}) == 4
 
 
 def test_bench_sweep_mode_and_slack():
@@ -78,6 +78,8 @@ def test_collectives_gloo_two_ranks():
     d = last_json(p.stdout)
     assert d["backend"] == "gloo" and d["world"] == 2 and d["pass"]
     assert all(r["correct"] for r in d["rows"]) and d["rows"][1]["busbw_gbps"] > 0
+    assert {r["op"] for r in d["rows"]} == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all"}
+    assert set(d["best_busbw_by_op"]) == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all"}
 
 
 def test_collective_verdict_logic():
@@ -86,3 +88,5 @@ def test_collective_verdict_logic():
     rows = [{"bytes": 1 << 30, "busbw_gbps": 50.0, "correct": True}]
     assert not verdict(rows, 8)["pass"] and verdict(rows, 8, min_busbw=40)["pass"]
     assert not verdict([dict(rows[0], correct=False)], 8, 1)["pass"]
+    bad = verdict(rows + [{"op": "all_to_all", "bytes": 1 << 20, "busbw_gbps": 9.0, "correct": False}], 8, 40)
+    assert not bad["pass"] and bad["detail"] == "result mismatch: all_to_all"
