@@ -150,7 +150,10 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
         torch.cuda.set_device(local_rank)
     group = None
     if world > 1:
-        dist.init_process_group("nccl" if cuda else "gloo")
+        if cuda:  # device_id binds the group to this rank's GPU (eager RCCL init, no device guessing)
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        else:
+            dist.init_process_group("gloo")
         group = dist.new_group(backend="gloo")  # control-plane objects (URLs, reports)
         box = [ctrl]
         dist.broadcast_object_list(box, src=0, group=group)

@@ -183,7 +183,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     backend = args.backend or ("nccl" if cuda else "gloo")
     if cuda:
         torch.cuda.set_device(local_rank)
-    dist.init_process_group(backend)
+    if backend == "nccl" and cuda:
+        dist.init_process_group(backend, device_id=torch.device(f"cuda:{local_rank}"))
+    else:
+        dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local_rank}") if cuda else torch.device("cpu")
     rows = collective_bench([parse_size(s) for s in args.sizes.split(",")], args.ops.split(","), args.iters,
                             args.warmup, dev)
