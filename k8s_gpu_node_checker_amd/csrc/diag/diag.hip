@@ -617,46 +617,32 @@ __global__ void gemm_ref_fp8_kernel(const uint8_t* A, const uint8_t* Bt, const i
 }
 
 // ---------------------------------------------------------------- HBM streams
-// Forms picked by the sweep in tools/hbm_explore.hip on MI355X (profiles/hbm_explore_mi355x.json):
-// copy 8-deep nontemporal 5.29 TB/s, read 8-deep nontemporal 6.78 TB/s, plain write 5.16 TB/s,
-// all at 32 blocks of 256 threads per CU (vs 4.5 / 5.5 / 4.6 TB/s for the first 4-deep, 8/CU form).
+// Forms picked by the sweeps in tools/hbm_explore.hip on MI355X (profiles/hbm_explore_mi355x.json):
+// one 16-byte element per thread and a grid over the whole buffer (no grid-stride loop), nontemporal
+// loads/stores for copy and read, plain stores for write: copy 6.59, read 6.97, write 6.87 TB/s,
+// vs 5.29 / 6.78 / 5.16 for the best persistent form (8-deep unrolled, 32 blocks of 256 per CU).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int HBM_UNROLL = 8;
-constexpr int HBM_BLOCKS_PER_CU = 32;
 
 __global__ void __launch_bounds__(256) copy_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst, size_t n) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
-  for (; i + (HBM_UNROLL - 1) * stride < n; i += HBM_UNROLL * stride) {
-    f32x4 v[HBM_UNROLL];
-#pragma unroll
-    for (int u = 0; u < HBM_UNROLL; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
-#pragma unroll
-    for (int u = 0; u < HBM_UNROLL; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
-  }
-  for (; i < n; i += stride) dst[i] = src[i];
+  const size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 __global__ void __launch_bounds__(256) read_kernel(const f32x4* __restrict__ src, size_t n, float* sink) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
-  float acc = 0.f;
-  for (; i + (HBM_UNROLL - 1) * stride < n; i += HBM_UNROLL * stride) {
-#pragma unroll
-    for (int u = 0; u < HBM_UNROLL; ++u) {
-      const f32x4 v = __builtin_nontemporal_load(src + i + u * stride);
-      acc += v[0] + v[3];
-    }
+  const size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i < n) {
+    const f32x4 v = __builtin_nontemporal_load(src + i);
+    if (v[0] + v[3] == 1234.5678f) *sink = v[1];  // keeps the load alive, practically never stores
   }
-  for (; i < n; i += stride) acc += src[i][0];
-  if (acc == 1234.5678f) *sink = acc;  // keeps the loads alive, practically never stores
 }
 
 __global__ void __launch_bounds__(256) write_kernel(f32x4* __restrict__ dst, size_t n, float v) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  const f32x4 x = {v, v, v, v};
-  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride) dst[i] = x;
+  const size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i < n) dst[i] = f32x4{v, v, v, v};
 }
+
+// one thread per 16-byte element (grid-stride kernels launched with it run their loop once)
+unsigned flat_grid(size_t n) { return static_cast<unsigned>(std::min<size_t>((n + 255) / 256, 0x7FFFFFFFu)); }
 
 // ---------------------------------------------------------------- memtest
 __device__ __forceinline__ uint4 pattern(size_t i, uint64_t seed, bool invert) {
@@ -1049,7 +1035,7 @@ int diag_hbm_bandwidth(int device, size_t bytes, int iters, double* copy_tbs, do
   DIAG_CHECK(hipMalloc(&a, n * sizeof(f32x4)));
   DIAG_CHECK(hipMalloc(&b, n * sizeof(f32x4)));
   DIAG_CHECK(hipMalloc(&sink, sizeof(float)));
-  const int grid = grid_for(device, HBM_BLOCKS_PER_CU);
+  const unsigned grid = flat_grid(n);
   hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, a, n, 1.0f);
   hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, b, n, 2.0f);
   DIAG_CHECK(hipGetLastError());
@@ -1098,7 +1084,7 @@ int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned l
   DIAG_CHECK(hipMalloc(&dev, 2 * sizeof(unsigned long long)));
   const unsigned long long init[2] = {0ULL, ~0ULL};
   DIAG_CHECK(hipMemcpy(dev, init, sizeof init, hipMemcpyHostToDevice));
-  const int grid = grid_for(device, 8);
+  const unsigned grid = flat_grid(n);
   hipEvent_t e0, e1;
   DIAG_CHECK(hipEventCreate(&e0));
   DIAG_CHECK(hipEventCreate(&e1));

@@ -22,8 +22,8 @@ from typing import Any, Dict, Optional
 from .native import NativeUnavailable, load_cdll
 
 # Pass thresholds vs a healthy MI355X (measured: profiles/gemm_explore_mi355x.json,
-# profiles/hbm_explore_mi355x.json): GEMM 4096^3 ~1070 / 8192^3 ~1140 TFLOP/s bf16, HBM copy ~5.3 TB/s,
-# read ~6.8 TB/s.  Device-to-device DVFS spread is ~10 %; these flag broken or badly throttled parts.
+# profiles/hbm_explore_mi355x.json): GEMM 4096^3 ~1200 / 8192^3 ~1370 TFLOP/s bf16, HBM copy ~6.6 TB/s,
+# read ~7.0 TB/s.  Device-to-device DVFS spread is ~10 %; these flag broken or badly throttled parts.
 GEMM_MIN_TFLOPS = 600.0       # bf16 MFMA GEMM (4096^3 quick / 8192^3 deep)
 GEMM_MAX_REL_ERR = 2e-3       # vs fp32 reference; bf16 inputs are exact in fp32, so ~1e-5 is typical
 GEMM_FP8_MIN_TFLOPS = 1200.0  # MX-fp8 GEMM (measured 2100 @4096^3, 2590 @8192^3, profiles/gemm_fp8_mi355x.jsonl)
