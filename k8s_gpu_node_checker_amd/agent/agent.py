@@ -33,9 +33,30 @@ from ..models.health import HealthExpectations, condition_for, evaluate_report
 from ..models.node import HEALTH_ANNOTATION
 
 
+# Report fields that change on every probe without saying anything about health; ignored when deciding
+# whether the annotation must be rewritten.
+_VOLATILE = frozenset(("ts", "probe_ms", "probe_us", "hotspot_c", "wall_s", "ms_per_gemm", "setup_ms"))
+
+
+def report_digest(rep: Dict[str, Any]) -> str:
+    """Stable digest of a report minus its volatile fields (timestamps, timings, temperature)."""
+    import hashlib
+
+    def strip(x: Any) -> Any:
+        if isinstance(x, dict):
+            return {k: strip(v) for k, v in x.items() if k not in _VOLATILE}
+        if isinstance(x, list):
+            return [strip(v) for v in x]
+        if isinstance(x, float):
+            return round(x, 0)  # measured rates: only a real change (>= 1 unit) counts
+        return x
+    return hashlib.sha256(json.dumps(strip(rep), sort_keys=True).encode()).hexdigest()
+
+
 class Agent:
     def __init__(self, node: str, source: str = "auto", fixture: Optional[str] = None, diag_level: int = 0,
-                 diag_interval: float = 3600.0, devices: Optional[List[int]] = None):
+                 diag_interval: float = 3600.0, devices: Optional[List[int]] = None,
+                 annotation_refresh: float = 900.0):
         self.node = node
         self.source = source
         self.fixture = fixture
@@ -47,6 +68,11 @@ class Agent:
         self._diag_ts = 0.0
         self.last: Optional[Dict[str, Any]] = None
         self._last_condition: Optional[Dict[str, Any]] = None
+        # the annotation (KBs per node, a new object revision per write) is rewritten only when the
+        # report changed or every `annotation_refresh` s; the condition heartbeat goes out every probe
+        self.annotation_refresh = annotation_refresh
+        self._annotated: Optional[str] = None
+        self._annotated_at = 0.0
         self.lock = threading.Lock()
 
     def _diagnostics(self, n_gpus: int) -> Dict[int, Dict[str, Any]]:
@@ -116,10 +142,17 @@ class Agent:
     def publish_annotation(self, client: Any, rep: Dict[str, Any]) -> None:
         client.patch_node_annotations(self.node, self.annotation(rep))
 
-    def publish(self, client: Any, rep: Dict[str, Any]) -> None:
-        """Full report as annotation + verdict as the ``AMDGPUHealthy`` NodeCondition."""
-        client.patch_node_annotations(self.node, self.annotation(rep))
+    def publish(self, client: Any, rep: Dict[str, Any], force: bool = False) -> bool:
+        """Verdict as the ``AMDGPUHealthy`` NodeCondition (always: it carries the heartbeat) + the full
+        report as annotation when it changed.  Returns whether the annotation was written."""
+        digest = report_digest(rep)
+        now = time.monotonic()
+        write = force or digest != self._annotated or now - self._annotated_at >= self.annotation_refresh
+        if write:
+            client.patch_node_annotations(self.node, self.annotation(rep))
+            self._annotated, self._annotated_at = digest, now
         client.patch_node_condition(self.node, self.condition(rep))
+        return write
 
 
 def _metrics(rep: Optional[Dict[str, Any]]) -> str:
@@ -205,13 +238,17 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--listen", default="0.0.0.0:9464")
     ap.add_argument("--kubeconfig")
     ap.add_argument("--once", action="store_true")
+    ap.add_argument("--annotation-refresh", type=float, default=900.0,
+                    help="rewrite an unchanged report annotation at most this often (s); the condition "
+                         "heartbeat is published every interval")
     return ap
 
 
 def main(argv: Optional[List[str]] = None) -> int:
     args = build_parser().parse_args(argv)
     pubs = set(args.publish.split(","))
-    agent = Agent(args.node, args.source, args.fixture, args.diag_level, args.diag_interval)
+    agent = Agent(args.node, args.source, args.fixture, args.diag_level, args.diag_interval,
+                  annotation_refresh=args.annotation_refresh)
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient

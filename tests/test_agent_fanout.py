@@ -195,3 +195,22 @@ def test_agent_metrics_cover_diag_kinds_and_fabric():
     assert 'mi355x_gpu_diag_tflops{gpu="0",bdf="0000:05:00.0",test="mfma",dtype="mxfp4"} 7600.0' in m
     assert 'mi355x_gpu_diag_h2d_gbps{gpu="0",bdf="0000:05:00.0",test="host_link"} 56.8' in m
     assert 'mi355x_node_xgmi_p2p_gbps{stat="min"} 45.0' in m
+
+
+def test_agent_rewrites_the_annotation_only_on_change(mock_cluster, fixture_report):
+    srv = mock_cluster([fixtures.realistic_node("n")])
+    ag = A.Agent("n", source="fixture", fixture=fixture_report)
+    with KubeClient(ClusterConnection(srv.url)) as kc:
+        r1 = ag.probe_once()
+        assert ag.publish(kc, r1) is True
+        r2 = ag.probe_once()  # same GPUs, new timestamp / timings
+        r2["gpus"][0]["hotspot_c"] = 61
+        assert ag.publish(kc, r2) is False
+        r3 = ag.probe_once()
+        r3["gpus"][0]["ecc_uncorrectable"] = 2  # a real change
+        assert ag.publish(kc, r3) is True
+        ag.annotation_refresh = 0.0
+        assert ag.publish(kc, r3) is True  # refresh interval elapsed
+    patches = [e["path"] for e in srv.log if e["method"] == "PATCH"]
+    assert sum(p.endswith("/status") for p in patches) == 4  # a heartbeat every publish
+    assert sum(not p.endswith("/status") for p in patches) == 3
