@@ -56,7 +56,7 @@ def report_digest(rep: Dict[str, Any]) -> str:
 class Agent:
     def __init__(self, node: str, source: str = "auto", fixture: Optional[str] = None, diag_level: int = 0,
                  diag_interval: float = 3600.0, devices: Optional[List[int]] = None,
-                 annotation_refresh: float = 900.0):
+                 annotation_refresh: float = 900.0, heartbeat_interval: float = 300.0):
         self.node = node
         self.source = source
         self.fixture = fixture
@@ -73,6 +73,12 @@ class Agent:
         self.annotation_refresh = annotation_refresh
         self._annotated: Optional[str] = None
         self._annotated_at = 0.0
+        # the condition is re-sent on a verdict change at once, else every `heartbeat_interval` s (the
+        # kubelet's own node-status report cadence is 5 min); the checker's --probe-max-age (15 min
+        # default) must stay above it
+        self.heartbeat_interval = heartbeat_interval
+        self._cond_key: Optional[tuple] = None
+        self._cond_at = 0.0
         self.lock = threading.Lock()
 
     def _diagnostics(self, n_gpus: int) -> Dict[int, Dict[str, Any]]:
@@ -142,17 +148,24 @@ class Agent:
     def publish_annotation(self, client: Any, rep: Dict[str, Any]) -> None:
         client.patch_node_annotations(self.node, self.annotation(rep))
 
-    def publish(self, client: Any, rep: Dict[str, Any], force: bool = False) -> bool:
-        """Verdict as the ``AMDGPUHealthy`` NodeCondition (always: it carries the heartbeat) + the full
-        report as annotation when it changed.  Returns whether the annotation was written."""
+    def publish(self, client: Any, rep: Dict[str, Any], force: bool = False) -> Dict[str, bool]:
+        """Full report as annotation when it changed (or every ``annotation_refresh`` s), verdict as the
+        ``AMDGPUHealthy`` NodeCondition when it changed (or every ``heartbeat_interval`` s).
+        Returns which of the two were written."""
         digest = report_digest(rep)
         now = time.monotonic()
-        write = force or digest != self._annotated or now - self._annotated_at >= self.annotation_refresh
-        if write:
+        wrote = {"annotation": False, "condition": False}
+        if force or digest != self._annotated or now - self._annotated_at >= self.annotation_refresh:
             client.patch_node_annotations(self.node, self.annotation(rep))
             self._annotated, self._annotated_at = digest, now
-        client.patch_node_condition(self.node, self.condition(rep))
-        return write
+            wrote["annotation"] = True
+        cond = self.condition(rep)
+        key = (cond.get("status"), cond.get("reason"), cond.get("message"))
+        if force or key != self._cond_key or now - self._cond_at >= self.heartbeat_interval:
+            client.patch_node_condition(self.node, cond)
+            self._cond_key, self._cond_at = key, now
+            wrote["condition"] = True
+        return wrote
 
 
 def _metrics(rep: Optional[Dict[str, Any]]) -> str:
@@ -239,8 +252,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--kubeconfig")
     ap.add_argument("--once", action="store_true")
     ap.add_argument("--annotation-refresh", type=float, default=900.0,
-                    help="rewrite an unchanged report annotation at most this often (s); the condition "
-                         "heartbeat is published every interval")
+                    help="rewrite an unchanged report annotation at most this often (s)")
+    ap.add_argument("--heartbeat-interval", type=float, default=300.0,
+                    help="re-send an unchanged AMDGPUHealthy condition this often (s); keep it below the "
+                         "checker's --probe-max-age")
     return ap
 
 
@@ -248,7 +263,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     args = build_parser().parse_args(argv)
     pubs = set(args.publish.split(","))
     agent = Agent(args.node, args.source, args.fixture, args.diag_level, args.diag_interval,
-                  annotation_refresh=args.annotation_refresh)
+                  annotation_refresh=args.annotation_refresh, heartbeat_interval=args.heartbeat_interval)
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient

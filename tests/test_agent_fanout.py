@@ -29,7 +29,7 @@ def test_agent_fixture_probe_and_annotation(mock_cluster, fixture_report):
         conds = {c_["type"]: c_ for c_ in node["status"]["conditions"]}
         assert conds["AMDGPUHealthy"]["status"] == "True" and conds["Ready"]["status"] == "True"
         t0 = conds["AMDGPUHealthy"]["lastTransitionTime"]
-        ag.publish(c, ag.probe_once())  # heartbeat refresh keeps the transition time, replaces by type
+        ag.publish(c, ag.probe_once(), force=True)  # heartbeat refresh keeps the transition time, replaces by type
         node = c.get_node("mi355x-node-0001")
         hc = [c_ for c_ in node["status"]["conditions"] if c_["type"] == "AMDGPUHealthy"]
         assert len(hc) == 1 and hc[0]["lastTransitionTime"] == t0
@@ -197,20 +197,24 @@ def test_agent_metrics_cover_diag_kinds_and_fabric():
     assert 'mi355x_node_xgmi_p2p_gbps{stat="min"} 45.0' in m
 
 
-def test_agent_rewrites_the_annotation_only_on_change(mock_cluster, fixture_report):
+def test_agent_writes_only_changes_plus_heartbeats(mock_cluster, fixture_report):
     srv = mock_cluster([fixtures.realistic_node("n")])
     ag = A.Agent("n", source="fixture", fixture=fixture_report)
+    both = {"annotation": True, "condition": True}
     with KubeClient(ClusterConnection(srv.url)) as kc:
         r1 = ag.probe_once()
-        assert ag.publish(kc, r1) is True
-        r2 = ag.probe_once()  # same GPUs, new timestamp / timings
+        assert ag.publish(kc, r1) == both
+        r2 = ag.probe_once()  # same GPUs, new timestamp / timings / temperature: nothing to write
         r2["gpus"][0]["hotspot_c"] = 61
-        assert ag.publish(kc, r2) is False
+        assert ag.publish(kc, r2) == {"annotation": False, "condition": False}
         r3 = ag.probe_once()
-        r3["gpus"][0]["ecc_uncorrectable"] = 2  # a real change
-        assert ag.publish(kc, r3) is True
-        ag.annotation_refresh = 0.0
-        assert ag.publish(kc, r3) is True  # refresh interval elapsed
+        r3["gpus"][0]["ecc_uncorrectable"] = 2  # a real change: new report, new verdict
+        assert ag.publish(kc, r3) == both
+        ag.annotation_refresh = ag.heartbeat_interval = 0.0
+        assert ag.publish(kc, r3) == both  # refresh / heartbeat intervals elapsed
+        cond = kc.get_node("n")["status"]["conditions"]
     patches = [e["path"] for e in srv.log if e["method"] == "PATCH"]
-    assert sum(p.endswith("/status") for p in patches) == 4  # a heartbeat every publish
+    assert sum(p.endswith("/status") for p in patches) == 3
     assert sum(not p.endswith("/status") for p in patches) == 3
+    hc = [c for c in cond if c["type"] == "AMDGPUHealthy"][0]
+    assert hc["status"] == "False"
