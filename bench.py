@@ -185,7 +185,7 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
         rep["gpus"] = _own_gpu(rep["gpus"], local_rank, cuda)
     probe_ms = (time.perf_counter() - t0) * 1e3
     with KubeClient(cluster) as kc:
-        agent.publish(kc, rep)  # AMDGPUHealthy NodeCondition + full report annotation
+        agent.publish(kc, rep, force=True)  # AMDGPUHealthy NodeCondition + full report annotation
     diag = {}
     for g in rep.get("gpus") or []:
         diag = g.get("diag") or {}
@@ -202,7 +202,7 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
             if probe_source != "fixture":
                 r["gpus"] = _own_gpu(r["gpus"], local_rank, cuda)
             with KubeClient(cluster) as kc2:
-                agent.publish(kc2, r)
+                agent.publish(kc2, r, force=True)  # the full write cycle (a live agent skips unchanged writes)
             barrier()
         if rank == 0:
             sink_out.seek(0)
