@@ -135,6 +135,7 @@ class KubeClient:
                 content_type: Optional[str] = None, idempotent: bool = True, peek=None) -> Response:
         headers = self._headers(content_type)
         attempt = 0
+        reauth = False
         while True:
             conn = self._connection()
             self.requests_made += 1
@@ -148,6 +149,11 @@ class KubeClient:
                 raise TransportError(conn.scheme, conn.host, conn.port, path, e) from e
             if 200 <= resp.status < 300:
                 return resp
+            if resp.status == 401 and not reauth and self.cluster.invalidate_credentials():
+                # rotated service-account token / expired exec credential: fetch fresh ones once
+                reauth = True
+                headers = self._headers(content_type)
+                continue
             if idempotent and resp.status in _RETRY_STATUS and attempt < self.retries:
                 self.sleep(self.backoff.delay(attempt, resp.header("Retry-After")))
                 attempt += 1

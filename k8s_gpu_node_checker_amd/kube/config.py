@@ -157,6 +157,12 @@ class ClusterConnection:
         self._exec_cache = (status, expiry)
         return status
 
+    def invalidate_credentials(self) -> bool:
+        """Drop cached exec-plugin credentials (after a 401); True if the next request can present
+        different credentials (exec plugin re-run or a re-read tokenFile), as client-go does."""
+        self._exec_cache = None
+        return self.exec_spec is not None or bool(self.token_file)
+
     def auth_headers(self) -> Dict[str, str]:
         token = self.token
         if self.token_file:

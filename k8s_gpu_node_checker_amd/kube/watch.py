@@ -163,6 +163,8 @@ class NodeWatcher:
         resp = conn.open_stream("GET", path, client._headers(), read_timeout=self.debounce or None)
         if not isinstance(resp, LineStream):
             client.close()
+            if resp.status == 401:
+                self.cluster.invalidate_credentials()
             if resp.status == 410:
                 self.rv = None
                 raise _Relist()
@@ -239,8 +241,8 @@ class NodeWatcher:
                 failures += 1
                 if failures > 3:
                     self.rv = None  # persistent trouble: start over from a LIST
-                if isinstance(e, ApiException) and e.status in (401, 403):
-                    raise
+                if isinstance(e, ApiException) and (e.status == 403 or (e.status == 401 and failures > 3)):
+                    raise  # RBAC denies it / credentials stay rejected after re-reads: not transient
                 self.sleep(self.backoff.delay(min(failures, 6)))
             finally:
                 client.close()

@@ -279,3 +279,42 @@ def test_pipelined_pagination_uses_two_connections(mock_cluster):
     assert names(res) == names(scan_items(nodes)) and res.items_seen == 30
     with KubeClient(ClusterConnection(srv.url), pipeline=False) as c:
         assert names(c.scan_nodes(limit=4)) == names(res) and c._conn2 is None
+
+
+def test_401_refetches_rotated_credentials_once(tmp_path, mock_cluster):
+    """A token rejected with 401 (rotated service-account token, expired exec credential) is fetched
+    again once -- the exec plugin re-runs even though its credential had no expiry -- then the
+    request is repeated; a second 401 is final."""
+    import sys as _sys
+    from k8s_gpu_node_checker_amd.kube.config import load_kube_config
+    srv = mock_cluster(fixtures.cluster(1, "amd"), token="fresh")
+    counter = tmp_path / "n"
+    plugin = tmp_path / "plugin.py"
+    plugin.write_text(
+        "import json, pathlib\n"
+        f"p = pathlib.Path({str(counter)!r})\n"
+        "n = int(p.read_text()) if p.exists() else 0\n"
+        "p.write_text(str(n + 1))\n"
+        "tok = 'stale' if n == 0 else 'fresh'\n"
+        "print(json.dumps({'apiVersion': 'client.authentication.k8s.io/v1', 'kind': 'ExecCredential',"
+        " 'status': {'token': tok}}))\n")
+    import yaml as _yaml
+    cfg = {"apiVersion": "v1", "kind": "Config", "current-context": "c",
+           "clusters": [{"name": "c", "cluster": {"server": srv.url}}],
+           "contexts": [{"name": "c", "context": {"cluster": "c", "user": "u"}}],
+           "users": [{"name": "u", "user": {"exec": {"apiVersion": "client.authentication.k8s.io/v1",
+                                                     "command": _sys.executable, "args": [str(plugin)]}}}]}
+    kc = tmp_path / "kc"
+    kc.write_text(_yaml.safe_dump(cfg))
+    cluster = load_kube_config(str(kc))
+    with KubeClient(cluster) as c:
+        assert c.scan_nodes().gpu_nodes
+    assert counter.read_text() == "2"
+    auths = [e["auth"] for e in srv.log]
+    assert auths == ["Bearer stale", "Bearer fresh"]
+    # a credential that stays wrong: one re-fetch, then the 401 surfaces
+    srv.cfg.token = "other"
+    with KubeClient(cluster) as c:
+        with pytest.raises(ApiException) as ei:
+            c.scan_nodes()
+    assert ei.value.status == 401
