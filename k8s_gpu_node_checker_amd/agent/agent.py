@@ -29,13 +29,15 @@ import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional
 
-from ..models.health import HealthExpectations, condition_for, evaluate_report
+from ..models.health import HealthExpectations, condition_for, evaluate_report, throttle_window
 from ..models.node import HEALTH_ANNOTATION
 
 
 # Report fields that change on every probe without saying anything about health; ignored when deciding
 # whether the annotation must be rewritten.
-_VOLATILE = frozenset(("ts", "probe_ms", "probe_us", "hotspot_c", "wall_s", "ms_per_gemm", "setup_ms"))
+_VOLATILE = frozenset(("ts", "probe_ms", "probe_us", "hotspot_c", "wall_s", "ms_per_gemm", "setup_ms",
+                       "power_w", "hbm_temp_c", "gfxclk_mhz", "vram_used_mb", "processes", "throttle_acc",
+                       "throttle"))
 
 
 def report_digest(rep: Dict[str, Any]) -> str:
@@ -79,6 +81,8 @@ class Agent:
         self.heartbeat_interval = heartbeat_interval
         self._cond_key: Optional[tuple] = None
         self._cond_at = 0.0
+        # previous throttle-residency sample per GPU (bdf or index) -> (monotonic time, accumulators)
+        self._acc_prev: Dict[str, Any] = {}
         self.lock = threading.Lock()
 
     def _diagnostics(self, n_gpus: int) -> Dict[int, Dict[str, Any]]:
@@ -114,6 +118,7 @@ class Agent:
     def probe_once(self) -> Dict[str, Any]:
         from ..ops.amdsmi_probe import probe
         rep = probe(self.node, self.source, self.fixture)
+        self._throttle_windows(rep)
         diags = self._diagnostics(len(rep.get("gpus") or []))
         if diags:
             # amd-smi and HIP enumerate independently: match by PCI address, fall back to the index
@@ -135,6 +140,22 @@ class Agent:
         with self.lock:
             self.last = rep
         return rep
+
+    def _throttle_windows(self, rep: Dict[str, Any]) -> None:
+        """Turn the firmware's since-boot throttle accumulators into the share of the time since the
+        previous probe spent throttled (``gpus[i].throttle``; models/health.throttle_window)."""
+        now = time.monotonic()
+        for g in rep.get("gpus") or []:
+            acc = g.get("throttle_acc")
+            if not isinstance(acc, dict):
+                continue
+            key = str(g.get("bdf") or g.get("index"))
+            prev = self._acc_prev.get(key)
+            if prev is not None:
+                win = throttle_window(prev[1], acc, now - prev[0])
+                if win is not None:
+                    g["throttle"] = win
+            self._acc_prev[key] = (now, acc)
 
     def annotation(self, rep: Dict[str, Any]) -> Dict[str, str]:
         return {HEALTH_ANNOTATION: json.dumps(rep, separators=(",", ":"))}
@@ -174,7 +195,10 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
     lines = ["# TYPE mi355x_agent_probe_timestamp_seconds gauge", f"mi355x_agent_probe_timestamp_seconds {rep.get('ts', 0)}",
              "# TYPE mi355x_gpu_ecc_uncorrectable gauge", "# TYPE mi355x_gpu_xgmi_links_up gauge",
              "# TYPE mi355x_gpu_hotspot_celsius gauge", "# TYPE mi355x_gpu_pcie_width gauge",
-             "# TYPE mi355x_gpu_pcie_replays counter"]
+             "# TYPE mi355x_gpu_pcie_replays counter", "# TYPE mi355x_gpu_power_watts gauge",
+             "# TYPE mi355x_gpu_power_cap_watts gauge", "# TYPE mi355x_gpu_hbm_celsius gauge",
+             "# TYPE mi355x_gpu_gfxclk_mhz gauge", "# TYPE mi355x_gpu_vram_used_megabytes gauge",
+             "# TYPE mi355x_gpu_throttle_percent gauge"]
     for g in rep.get("gpus") or []:
         lbl = f'gpu="{g.get("index")}",bdf="{g.get("bdf", "")}"'
         if isinstance(g.get("ecc_uncorrectable"), int):
@@ -187,6 +211,15 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
             lines.append(f"mi355x_gpu_pcie_width{{{lbl}}} {g['pcie_width']}")
         if isinstance(g.get("pcie_replays"), int):
             lines.append(f"mi355x_gpu_pcie_replays{{{lbl}}} {g['pcie_replays']}")
+        for key, metric in (("power_w", "power_watts"), ("power_cap_w", "power_cap_watts"),
+                            ("hbm_temp_c", "hbm_celsius"), ("gfxclk_mhz", "gfxclk_mhz"),
+                            ("vram_used_mb", "vram_used_megabytes")):
+            if isinstance(g.get(key), (int, float)):
+                lines.append(f"mi355x_gpu_{metric}{{{lbl}}} {g[key]}")
+        for kind in ("thermal", "power", "prochot"):
+            v = (g.get("throttle") or {}).get(f"{kind}_pct")
+            if isinstance(v, (int, float)):
+                lines.append(f'mi355x_gpu_throttle_percent{{{lbl},kind="{kind}"}} {v}')
         for test, res in (g.get("diag") or {}).items():
             for k in ("tflops", "copy_tbs", "read_tbs", "errors", "h2d_gbps", "d2h_gbps"):
                 if isinstance(res.get(k), (int, float)):

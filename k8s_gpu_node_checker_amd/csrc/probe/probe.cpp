@@ -1,7 +1,8 @@
 // MI355X passive health probe: libamd_smi -> "mi355x-health/v1" JSON (see probe.h).
 //
 // Checks what SURVEY §7.1 lists (ASIC/gfx950, HBM3E VRAM size, ECC, xGMI links,
-// KFD node) plus bad pages, partition modes and hotspot temperature.  Every
+// KFD node) plus bad pages, partition modes, hotspot temperature, the PCIe link
+// and operating telemetry (power, HBM temperature, clock, throttle residency).  Every
 // amd-smi status other than success is recorded, never thrown: a node whose
 // driver is not loaded (AMDSMI_STATUS_DRIVER_NOT_LOADED) or that denies access
 // (AMDSMI_STATUS_NO_PERM) yields a report with "error" set, which the checker
@@ -103,6 +104,77 @@ int open_locked() {
   g_open = true;
   g_gpus = static_cast<int>(g_handles.size());
   return 0;
+}
+
+// Operating state, not identity: power against its cap, HBM stack temperature, clock, VRAM in use,
+// processes holding the device, and the firmware's throttle-residency accumulators.
+// The accumulators count since driver load; the agent turns two consecutive probes into the share
+// of the interval spent throttled (PVIOL / TVIOL in amd-smi terms).  A field the firmware does not
+// report (all-ones sentinel) is left out.
+void probe_telemetry(std::string& o, amdsmi_processor_handle h) {
+  amdsmi_power_info_t pw;
+  memset(&pw, 0, sizeof pw);
+  if (amdsmi_get_power_info(h, &pw) == AMDSMI_STATUS_SUCCESS && pw.current_socket_power != UINT32_MAX &&
+      pw.current_socket_power != UINT16_MAX)
+    kv_u64(o, "power_w", pw.current_socket_power);
+  // the cap in uW on bare-metal Linux (power_info's power_limit is documented in W but reads in uW too)
+  amdsmi_power_cap_info_t cap;
+  memset(&cap, 0, sizeof cap);
+  if (amdsmi_get_power_cap_info(h, 0, &cap) == AMDSMI_STATUS_SUCCESS && cap.power_cap != UINT64_MAX &&
+      cap.power_cap > 0) {
+    kv_u64(o, "power_cap_w", cap.power_cap / 1000000);
+    if (cap.default_power_cap != UINT64_MAX && cap.default_power_cap > 0)
+      kv_u64(o, "power_cap_default_w", cap.default_power_cap / 1000000);
+  }
+  // HBM stacks: per-stack sensors, then the VRAM sensor; the hottest one counts
+  int64_t hbm = -1;
+  for (amdsmi_temperature_type_t t : {AMDSMI_TEMPERATURE_TYPE_HBM_0, AMDSMI_TEMPERATURE_TYPE_HBM_1,
+                                      AMDSMI_TEMPERATURE_TYPE_HBM_2, AMDSMI_TEMPERATURE_TYPE_HBM_3,
+                                      AMDSMI_TEMPERATURE_TYPE_VRAM}) {
+    int64_t v = 0;
+    if (amdsmi_get_temp_metric(h, t, AMDSMI_TEMP_CURRENT, &v) == AMDSMI_STATUS_SUCCESS && v > 0 && v < 200 &&
+        v > hbm)
+      hbm = v;
+  }
+  amdsmi_vram_usage_t vu;
+  memset(&vu, 0, sizeof vu);
+  if (amdsmi_get_gpu_vram_usage(h, &vu) == AMDSMI_STATUS_SUCCESS && vu.vram_used != UINT32_MAX)
+    kv_u64(o, "vram_used_mb", vu.vram_used);
+  uint32_t nproc = 0;
+  if (amdsmi_get_gpu_process_list(h, &nproc, nullptr) == AMDSMI_STATUS_SUCCESS) kv_u64(o, "processes", nproc);
+  // all-ones first: whatever the library does not fill reads as the not-reported sentinel
+  amdsmi_gpu_metrics_t m;
+  memset(&m, 0xFF, sizeof m);
+  const bool have_m = amdsmi_get_gpu_metrics_info(h, &m) == AMDSMI_STATUS_SUCCESS;
+  for (int i = 0; have_m && i < AMDSMI_NUM_HBM_INSTANCES; ++i) {
+    const uint16_t t = m.temperature_hbm[i];
+    if (t != UINT16_MAX && t > 0 && t < 200 && static_cast<int64_t>(t) > hbm) hbm = t;
+  }
+  if (hbm > 0) kv_i64(o, "hbm_temp_c", hbm);
+  if (!have_m) return;
+  uint64_t clk_sum = 0, clk_n = 0;
+  for (int i = 0; i < AMDSMI_MAX_NUM_GFX_CLKS; ++i) {
+    const uint16_t c = m.current_gfxclks[i];
+    if (c != UINT16_MAX && c > 0) {
+      clk_sum += c;
+      ++clk_n;
+    }
+  }
+  if (clk_n) kv_u64(o, "gfxclk_mhz", clk_sum / clk_n);
+  if (m.accumulation_counter != UINT64_MAX && m.accumulation_counter != 0) {
+    key(o, "throttle_acc");
+    o.push_back('{');
+    kv_u64(o, "n", m.accumulation_counter);
+    const struct {
+      const char* k;
+      uint64_t v;
+    } acc[] = {{"prochot", m.prochot_residency_acc},       {"ppt", m.ppt_residency_acc},
+               {"socket_thm", m.socket_thm_residency_acc}, {"vr_thm", m.vr_thm_residency_acc},
+               {"hbm_thm", m.hbm_thm_residency_acc}};
+    for (const auto& a : acc)
+      if (a.v != UINT64_MAX) kv_u64(o, a.k, a.v);
+    o.push_back('}');
+  }
 }
 
 void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
@@ -213,6 +285,7 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
     if (pcie.pcie_metric.pcie_l0_to_recovery_count != UINT64_MAX)
       kv_u64(o, "pcie_recoveries", pcie.pcie_metric.pcie_l0_to_recovery_count);
   }
+  probe_telemetry(o, h);
   double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
   key(o, "probe_us");
   o += std::to_string(static_cast<int64_t>(us));

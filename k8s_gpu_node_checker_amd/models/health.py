@@ -37,7 +37,11 @@ VRAM_MIN_FRACTION = 0.97
 XGMI_LINKS_EXPECTED = 7                       # 8-GPU hive: 7 peers per GPU
 NUM_CUS = 256
 HOTSPOT_WARN_C = 100
+HBM_TEMP_WARN_C = 95                          # HBM3E stacks throttle in the 95-105 C band
 PCIE_REPLAY_WARN = 10000                      # link-level retries since boot: a marginal slot or riser
+POWER_CAP_MIN_FRACTION = 0.9                  # a cap set below 90 % of the board default
+THERMAL_THROTTLE_WARN_PCT = 10.0              # share of a probe interval spent thermally throttled
+PROCHOT_WARN_PCT = 1.0                        # PROCHOT is an emergency throttle: any sustained share counts
 
 HEALTHY, DEGRADED, UNHEALTHY, UNKNOWN = "healthy", "degraded", "unhealthy", "unknown"
 _OK_STATES = (HEALTHY, DEGRADED)
@@ -112,6 +116,45 @@ def _nps(mem_partition: Any) -> int:
     return 1
 
 
+def _num(x: Any) -> float:
+    return float(x) if isinstance(x, (int, float)) and not isinstance(x, bool) else 0.0
+
+
+def throttle_window(prev: Optional[Dict[str, Any]], cur: Optional[Dict[str, Any]],
+                    seconds: float) -> Optional[Dict[str, Any]]:
+    """Share of the interval between two probes spent throttled, from the firmware's residency
+    accumulators (``throttle_acc`` of two consecutive reports; amd-smi's PVIOL / TVIOL formula:
+    delta residency * 100 / delta accumulation counter).
+
+    ``thermal_pct`` is the largest of the socket, voltage-regulator and HBM thermal throttlers;
+    ``power_pct`` is package-power tracking, the normal operating point of an MI355X under full
+    MFMA load (reported, never a warning); ``prochot_pct`` is the emergency throttle.  ``None``
+    when either sample is missing or the counters went backwards (driver reload).
+    """
+    if not isinstance(prev, dict) or not isinstance(cur, dict):
+        return None
+    dn = _num(cur.get("n")) - _num(prev.get("n"))
+    if dn <= 0:
+        return None
+
+    def pct(*keys: str) -> Optional[float]:
+        vals = []
+        for k in keys:
+            if isinstance(cur.get(k), int) and isinstance(prev.get(k), int):
+                d = cur[k] - prev[k]
+                if d < 0:
+                    return None
+                vals.append(min(100.0, d * 100.0 / dn))
+        return round(max(vals), 2) if vals else None
+    out: Dict[str, Any] = {"s": round(seconds, 1)}
+    for name, keys in (("thermal_pct", ("socket_thm", "vr_thm", "hbm_thm")), ("power_pct", ("ppt",)),
+                       ("prochot_pct", ("prochot",))):
+        v = pct(*keys)
+        if v is not None:
+            out[name] = v
+    return out if len(out) > 1 else None
+
+
 def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str], List[str]]:
     """Return ``(failures, warnings)`` for one GPU entry of a probe report."""
     fail: List[str] = []
@@ -163,6 +206,19 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str],
     t = g.get("hotspot_c")
     if isinstance(t, (int, float)) and t >= HOTSPOT_WARN_C:
         warn.append(f"gpu{idx}: hotspot {t} C")
+    t = g.get("hbm_temp_c")
+    if isinstance(t, (int, float)) and t >= HBM_TEMP_WARN_C:
+        warn.append(f"gpu{idx}: HBM {t} C")
+    cap, dflt = g.get("power_cap_w"), g.get("power_cap_default_w")
+    if isinstance(cap, int) and isinstance(dflt, int) and 0 < cap < POWER_CAP_MIN_FRACTION * dflt:
+        warn.append(f"gpu{idx}: power cap {cap} W of {dflt} W default")
+    tw = g.get("throttle")
+    if isinstance(tw, dict):
+        # numbers stay out of the text: the condition message must not change with every probe
+        if _num(tw.get("thermal_pct")) >= THERMAL_THROTTLE_WARN_PCT:
+            warn.append(f"gpu{idx}: thermally throttled >= {THERMAL_THROTTLE_WARN_PCT:g}% of the last probe interval")
+        if _num(tw.get("prochot_pct")) >= PROCHOT_WARN_PCT:
+            warn.append(f"gpu{idx}: PROCHOT asserted >= {PROCHOT_WARN_PCT:g}% of the last probe interval")
     w, mw = g.get("pcie_width"), g.get("pcie_max_width")
     if isinstance(w, int) and isinstance(mw, int) and 0 < w < mw:
         warn.append(f"gpu{idx}: PCIe link x{w} of x{mw}")

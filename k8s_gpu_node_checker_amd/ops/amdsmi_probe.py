@@ -63,6 +63,57 @@ def _xgmi_string(status) -> Optional[str]:
     return "".join(m.get(s, "N") for s in status.get("status", []))
 
 
+def _int(v: Any) -> Optional[int]:
+    """amd-smi's Python binding reports unsupported fields as "N/A" or all-ones sentinels."""
+    if isinstance(v, bool) or not isinstance(v, int) or v < 0 or v in (0xFFFF, 0xFFFFFFFF, 0xFFFFFFFFFFFFFFFF):
+        return None
+    return v
+
+
+def _telemetry_python(A: Any, h: Any, q: Any) -> Dict[str, Any]:
+    """The native probe's ``probe_telemetry`` fields (csrc/probe/probe.cpp) from the Python binding."""
+    t: Dict[str, Any] = {}
+    pw = q(A.amdsmi_get_power_info) or {}
+    t["power_w"] = _int(pw.get("current_socket_power"))
+    cap = q(A.amdsmi_get_power_cap_info) or {}
+    for out_key, key in (("power_cap_w", "power_cap"), ("power_cap_default_w", "default_power_cap")):
+        v = _int(cap.get(key))
+        if v:  # uW on bare-metal Linux (probe.cpp); a binding that already converted gives W
+            t[out_key] = v // 1000000 if v > 100000 else v
+    hbm = []
+    for name in ("HBM_0", "HBM_1", "HBM_2", "HBM_3", "VRAM"):
+        try:
+            v = A.amdsmi_get_temp_metric(h, getattr(A.AmdSmiTemperatureType, name),
+                                         A.AmdSmiTemperatureMetric.CURRENT)
+        except Exception:
+            continue
+        v = _int(v)
+        if v and v < 200:
+            hbm.append(v)
+    vu = q(A.amdsmi_get_gpu_vram_usage) or {}
+    t["vram_used_mb"] = _int(vu.get("vram_used"))
+    procs = q(A.amdsmi_get_gpu_process_list)
+    t["processes"] = len(procs) if isinstance(procs, list) else None
+    m = q(A.amdsmi_get_gpu_metrics_info) or {}
+    th = m.get("temperature_hbm")
+    hbm += [x for x in (_int(v) for v in th) if x and x < 200] if isinstance(th, list) else []
+    t["hbm_temp_c"] = max(hbm) if hbm else None
+    clks = m.get("current_gfxclks")
+    clks = [x for x in (_int(v) for v in clks) if x] if isinstance(clks, list) else []
+    t["gfxclk_mhz"] = sum(clks) // len(clks) if clks else None
+    n = _int(m.get("accumulation_counter"))
+    if n:
+        acc = {"n": n}
+        for k, src in (("prochot", "prochot_residency_acc"), ("ppt", "ppt_residency_acc"),
+                       ("socket_thm", "socket_thm_residency_acc"), ("vr_thm", "vr_thm_residency_acc"),
+                       ("hbm_thm", "hbm_thm_residency_acc")):
+            v = _int(m.get(src))
+            if v is not None:
+                acc[k] = v
+        t["throttle_acc"] = acc
+    return {k: v for k, v in t.items() if v is not None}
+
+
 def probe_python(node: str) -> Dict[str, Any]:
     rep: Dict[str, Any] = {"schema": SCHEMA, "node": node, "ts": time.time(), "probe": "python", "gpus": []}
     t0 = time.perf_counter()
@@ -121,6 +172,7 @@ def probe_python(node: str) -> Dict[str, Any]:
                                       ("pcie_recoveries", pmt, "pcie_l0_to_recovery_count")):
                 if isinstance(src.get(key), int):
                     g[out_key] = src[key]
+            g.update(_telemetry_python(A, h, q))
             rep["gpus"].append({k: v for k, v in g.items() if v is not None})
     finally:
         rep["probe_ms"] = round((time.perf_counter() - t0) * 1e3, 3)

@@ -112,7 +112,10 @@ def mi355x_probe_report(node: str, gpus: int = 8, ts: Optional[float] = None, **
              "ecc_deferred": 0, "bad_pages": 0, "xgmi": "XUUUUUUU", "kfd": True,
              "compute_partition": "SPX", "memory_partition": "NPS1", "hotspot_c": 45,
              "pcie_width": 16, "pcie_max_width": 16, "pcie_speed_mts": 32000, "pcie_max_speed_mts": 32000,
-             "pcie_replays": 0, "pcie_recoveries": 0}
+             "pcie_replays": 0, "pcie_recoveries": 0, "power_w": 260, "power_cap_w": 1400,
+             "power_cap_default_w": 1400, "hbm_temp_c": 34, "gfxclk_mhz": 157, "vram_used_mb": 283,
+             "processes": 0, "throttle_acc": {"n": 499923464, "prochot": 0, "ppt": 1486216, "socket_thm": 0,
+                                              "vr_thm": 0, "hbm_thm": 0}}
         g.update(overrides.get(f"gpu{i}", {}))
         entries.append(g)
     rep = {"schema": "mi355x-health/v1", "node": node, "ts": time.time() if ts is None else ts,

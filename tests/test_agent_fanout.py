@@ -218,3 +218,36 @@ def test_agent_writes_only_changes_plus_heartbeats(mock_cluster, fixture_report)
     assert sum(not p.endswith("/status") for p in patches) == 3
     hc = [c for c in cond if c["type"] == "AMDGPUHealthy"][0]
     assert hc["status"] == "False"
+
+
+def test_agent_throttle_windows_and_telemetry_metrics(monkeypatch):
+    from k8s_gpu_node_checker_amd.ops import amdsmi_probe
+    samples = iter([{"n": 1000, "prochot": 0, "ppt": 0, "socket_thm": 0, "vr_thm": 0, "hbm_thm": 0},
+                    {"n": 3000, "prochot": 0, "ppt": 400, "socket_thm": 600, "vr_thm": 0, "hbm_thm": 0}])
+
+    def fake_probe(node, source, fixture):
+        r = fixtures.mi355x_probe_report(node, gpus=1)
+        r["gpus"][0]["throttle_acc"] = next(samples)
+        return r
+    monkeypatch.setattr(amdsmi_probe, "probe", fake_probe)
+    ag = A.Agent("n", source="fixture")
+    r1 = ag.probe_once()
+    assert "throttle" not in r1["gpus"][0]  # one sample: no window yet
+    r2 = ag.probe_once()
+    w = r2["gpus"][0]["throttle"]
+    assert (w["thermal_pct"], w["power_pct"], w["prochot_pct"]) == (30.0, 20.0, 0.0)
+    assert r2["state"] == "degraded"
+    m = A._metrics(r2)
+    assert 'mi355x_gpu_throttle_percent{gpu="0",bdf="0000:05:00.0",kind="thermal"} 30.0' in m
+    assert 'mi355x_gpu_power_cap_watts{gpu="0",bdf="0000:05:00.0"} 1400' in m
+    assert 'mi355x_gpu_hbm_celsius{gpu="0",bdf="0000:05:00.0"} 34' in m
+
+
+def test_report_digest_ignores_telemetry():
+    a = fixtures.mi355x_probe_report("n", gpus=1)
+    b = json.loads(json.dumps(a))
+    b["gpus"][0].update(power_w=900, gfxclk_mhz=2400, hbm_temp_c=60, vram_used_mb=200000, processes=3,
+                        throttle={"s": 60.0, "power_pct": 40.0}, throttle_acc={"n": 5})
+    assert A.report_digest(a) == A.report_digest(b)
+    b["gpus"][0]["power_cap_w"] = 1000  # configuration, not telemetry
+    assert A.report_digest(a) != A.report_digest(b)

@@ -60,8 +60,24 @@ def test_python_probe_agrees_with_native(dev):
     a = probe_native("n")["gpus"][0]
     b = probe_python("n")["gpus"][0]
     for k in ("gfx", "vram_type", "vram_mb", "ecc_uncorrectable", "xgmi", "compute_partition",
-              "memory_partition", "cus"):
+              "memory_partition", "cus", "power_cap_w", "power_cap_default_w"):
         assert a.get(k) == b.get(k), (k, a.get(k), b.get(k))
+    assert set(a.get("throttle_acc") or {}) == set(b.get("throttle_acc") or {})
+
+
+def test_native_probe_telemetry_and_throttle_window(dev):
+    from k8s_gpu_node_checker_amd.agent.agent import Agent
+    from k8s_gpu_node_checker_amd.ops import diag
+    ag = Agent("n", source="native")
+    g = ag.probe_once()["gpus"][0]
+    print(json.dumps({k: g.get(k) for k in ("power_w", "power_cap_w", "hbm_temp_c", "gfxclk_mhz", "throttle_acc")}))
+    assert 0 < g["power_w"] <= g["power_cap_w"] + 200 and 500 <= g["power_cap_w"] <= 2000, g
+    assert 0 < g["hbm_temp_c"] < 110 and g["gfxclk_mhz"] > 0, g
+    assert g["throttle_acc"]["n"] > 0 and "ppt" in g["throttle_acc"], g
+    diag.run(1, 0)  # some load between the two samples
+    g2 = ag.probe_once()["gpus"][0]
+    w = g2["throttle"]
+    assert w["s"] > 0 and all(0.0 <= w[k] <= 100.0 for k in ("thermal_pct", "power_pct", "prochot_pct")), w
 
 
 @pytest.mark.parametrize("m,n,k", [(128, 128, 64), (256, 384, 192), (1024, 1024, 1024), (512, 2048, 4096),

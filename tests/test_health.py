@@ -227,3 +227,34 @@ def test_pcie_full_width_and_idle_speed_are_healthy():
     v = H.evaluate_report(rep(gpu0={"pcie_width": 16, "pcie_max_width": 16, "pcie_speed_mts": 2500,
                                     "pcie_max_speed_mts": 32000, "pcie_replays": 3}), 8)
     assert v.state == H.HEALTHY, v.warnings
+
+
+@pytest.mark.parametrize("override,needle", [
+    ({"hbm_temp_c": 97}, "HBM 97 C"),
+    ({"power_cap_w": 1000, "power_cap_default_w": 1400}, "power cap 1000 W of 1400 W default"),
+    ({"throttle": {"s": 60.0, "thermal_pct": 25.0, "power_pct": 0.0, "prochot_pct": 0.0}}, "thermally throttled"),
+    ({"throttle": {"s": 60.0, "thermal_pct": 0.0, "power_pct": 0.0, "prochot_pct": 3.0}}, "PROCHOT"),
+])
+def test_telemetry_warnings(override, needle):
+    v = H.evaluate_report(rep(gpu2=override), 8)
+    assert v.state == H.DEGRADED and v.ok
+    assert any(needle in w for w in v.warnings), v.warnings
+
+
+def test_power_throttling_alone_is_the_normal_operating_point():
+    # package-power tracking under MFMA load is how an MI355X runs (profiles/telemetry_mi355x.json: 6.5 %
+    # of a level-2 diagnostic burst); it is reported, never a warning
+    v = H.evaluate_report(rep(gpu0={"throttle": {"s": 60.0, "thermal_pct": 0.0, "power_pct": 80.0,
+                                                 "prochot_pct": 0.0}}), 8)
+    assert v.state == H.HEALTHY
+
+
+def test_throttle_window_from_accumulators():
+    a = {"n": 1000, "prochot": 0, "ppt": 50, "socket_thm": 10, "vr_thm": 30, "hbm_thm": 0}
+    b = {"n": 2000, "prochot": 5, "ppt": 350, "socket_thm": 60, "vr_thm": 230, "hbm_thm": 0}
+    w = H.throttle_window(a, b, 12.34)
+    assert w == {"s": 12.3, "thermal_pct": 20.0, "power_pct": 30.0, "prochot_pct": 0.5}
+    assert H.throttle_window(None, b, 1.0) is None
+    assert H.throttle_window(b, a, 1.0) is None            # counter went backwards: driver reload
+    assert H.throttle_window(a, dict(b, ppt=10), 1.0).get("power_pct") is None
+    assert H.throttle_window({"n": 1}, {"n": 5}, 1.0) is None  # no residency fields at all

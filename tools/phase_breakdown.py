@@ -32,6 +32,9 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--page-size", type=int, default=500)
+    ap.add_argument("--kind", default="amd", help="amd | nvidia | mixed | cpu (mock_apiserver --kind)")
+    ap.add_argument("--gpus-per-node", type=int, default=1)
+    ap.add_argument("--no-health", action="store_true", help="serve nodes without MI355X health data")
     args = ap.parse_args()
 
     from k8s_gpu_node_checker_amd.checker import CheckOptions, check_and_report
@@ -41,7 +44,8 @@ def main() -> int:
 
     env = dict(os.environ, PYTHONPATH=REPO)
     srv = subprocess.Popen([sys.executable, "-m", "k8s_gpu_node_checker_amd.testing.mock_apiserver", "--nodes",
-                            str(args.nodes), "--kind", "amd", "--gpus-per-node", "1", "--with-health"],
+                            str(args.nodes), "--kind", args.kind, "--gpus-per-node", str(args.gpus_per_node)]
+                           + ([] if args.no_health else ["--with-health"]),
                            stdout=subprocess.PIPE, text=True, env=env)
     try:
         info = json.loads(srv.stdout.readline())
