@@ -14,7 +14,12 @@ HBM bandwidth, memtest) at ``--diag-level``.  The merged report is published
   checker's ``--probe-endpoint`` fan-out, and/or
 * on stdout (``--publish stdout``, one JSON line per probe).
 
-RBAC: ``nodes: get, patch`` and ``nodes/status: patch`` (``deploy/daemonset.yaml``).
+Each verdict change is also posted as a Kubernetes Event on the node (``Warning MI355XUnhealthy``,
+``Normal MI355XHealthy ... (was unhealthy)``), and with ``--taint-unhealthy`` the node carries
+``amd.com/gpu-unhealthy=true:NoSchedule`` while it is unhealthy (read-modify-write under the node's
+``resourceVersion``, so a concurrent ``kubectl taint`` is never lost).
+
+RBAC: ``nodes: get, patch``, ``nodes/status: patch`` and ``events: create`` (``deploy/rbac.yaml``).
 """
 
 from __future__ import annotations
@@ -29,7 +34,8 @@ import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional
 
-from ..models.health import HealthExpectations, condition_for, evaluate_report, throttle_window
+from ..models.health import (HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, HealthExpectations, Verdict,
+                              condition_for, condition_reason, evaluate_report, format_k8s_time, throttle_window)
 from ..models.node import HEALTH_ANNOTATION
 
 
@@ -55,10 +61,32 @@ def report_digest(rep: Dict[str, Any]) -> str:
     return hashlib.sha256(json.dumps(strip(rep), sort_keys=True).encode()).hexdigest()
 
 
+def node_event(node: str, verdict: Verdict, previous: Optional[str], namespace: str = "default",
+               now: Optional[float] = None) -> Dict[str, Any]:
+    """A core/v1 Event on the Node for one verdict change -- what ``kubectl describe node`` and event
+    exporters show.  Node events live in a namespace (``default``, as the kubelet's) with
+    ``involvedObject.uid`` = the node name, the kubelet's convention that ``kubectl describe node``
+    searches for besides the real UID."""
+    ts = format_k8s_time(time.time() if now is None else now)
+    if verdict.state == HEALTHY:
+        msg = f"{verdict.gpus_ok}/{verdict.gpus_seen} MI355X GPUs healthy" + (f" (was {previous})" if previous else "")
+    else:
+        msg = "; ".join(verdict.reasons or verdict.warnings) or verdict.state
+    return {"apiVersion": "v1", "kind": "Event",
+            "metadata": {"generateName": f"{node}.mi355x-", "namespace": namespace},
+            "involvedObject": {"apiVersion": "v1", "kind": "Node", "name": node, "uid": node},
+            "reason": condition_reason(verdict.state), "message": msg[:1024],
+            "type": "Normal" if verdict.state == HEALTHY else "Warning",
+            "source": {"component": "mi355x-node-agent", "host": node},
+            "reportingComponent": "mi355x-node-agent", "reportingInstance": node,
+            "firstTimestamp": ts, "lastTimestamp": ts, "count": 1}
+
+
 class Agent:
     def __init__(self, node: str, source: str = "auto", fixture: Optional[str] = None, diag_level: int = 0,
                  diag_interval: float = 3600.0, devices: Optional[List[int]] = None,
-                 annotation_refresh: float = 900.0, heartbeat_interval: float = 300.0):
+                 annotation_refresh: float = 900.0, heartbeat_interval: float = 300.0,
+                 events: bool = True, event_namespace: str = "default", taint_unhealthy: bool = False):
         self.node = node
         self.source = source
         self.fixture = fixture
@@ -83,6 +111,14 @@ class Agent:
         self._cond_at = 0.0
         # previous throttle-residency sample per GPU (bdf or index) -> (monotonic time, accumulators)
         self._acc_prev: Dict[str, Any] = {}
+        # remediation signals, both driven by verdict *changes*: an Event per change (advisory, never
+        # repeated) and, opt-in, the UNHEALTHY_TAINT while unhealthy (retried until written)
+        self.events = events
+        self.event_namespace = event_namespace
+        self.taint_unhealthy = taint_unhealthy
+        self._verdict: Optional[Verdict] = None
+        self._event_state: Optional[str] = None
+        self._taint_state: Optional[str] = None
         self.lock = threading.Lock()
 
     def _diagnostics(self, n_gpus: int) -> Dict[int, Dict[str, Any]]:
@@ -164,6 +200,7 @@ class Agent:
         v = evaluate_report(rep, 0, HealthExpectations())
         cond = condition_for(v, previous=self._last_condition)
         self._last_condition = cond
+        self._verdict = v
         return cond
 
     def publish_annotation(self, client: Any, rep: Dict[str, Any]) -> None:
@@ -171,11 +208,11 @@ class Agent:
 
     def publish(self, client: Any, rep: Dict[str, Any], force: bool = False) -> Dict[str, bool]:
         """Full report as annotation when it changed (or every ``annotation_refresh`` s), verdict as the
-        ``AMDGPUHealthy`` NodeCondition when it changed (or every ``heartbeat_interval`` s).
-        Returns which of the two were written."""
+        ``AMDGPUHealthy`` NodeCondition when it changed (or every ``heartbeat_interval`` s), and on a
+        verdict change an Event and (``taint_unhealthy``) the taint.  Returns what was written."""
         digest = report_digest(rep)
         now = time.monotonic()
-        wrote = {"annotation": False, "condition": False}
+        wrote = {"annotation": False, "condition": False, "event": False, "taint": False}
         if force or digest != self._annotated or now - self._annotated_at >= self.annotation_refresh:
             client.patch_node_annotations(self.node, self.annotation(rep))
             self._annotated, self._annotated_at = digest, now
@@ -186,7 +223,38 @@ class Agent:
             client.patch_node_condition(self.node, cond)
             self._cond_key, self._cond_at = key, now
             wrote["condition"] = True
+        v = self._verdict
+        if v is None:
+            return wrote
+        if self.events and v.state != self._event_state:
+            prev, self._event_state = self._event_state, v.state
+            if prev is not None or v.state != HEALTHY:  # an agent (re)starting on a healthy node is no news
+                wrote["event"] = self._post_event(client, v, prev)
+        # UNKNOWN (probe failed) leaves the taint as it is: a flaky probe must not flap scheduling
+        if self.taint_unhealthy and v.state != UNKNOWN and v.state != self._taint_state:
+            wrote["taint"] = self._sync_taint(client, v.state == UNHEALTHY)  # raises -> retried next publish
+            self._taint_state = v.state
         return wrote
+
+    def _post_event(self, client: Any, verdict: Verdict, previous: Optional[str]) -> bool:
+        try:
+            client.create_event(self.event_namespace,
+                                node_event(self.node, verdict, previous, self.event_namespace))
+            return True
+        except Exception as e:  # advisory: a missing RBAC rule must not stop the condition heartbeat
+            print(f"node event post failed: {e}", file=sys.stderr, flush=True)
+            return False
+
+    def _sync_taint(self, client: Any, want: bool) -> bool:
+        """Add (``want``) or remove UNHEALTHY_TAINT, keeping every other taint; True if a write happened.
+        On the first publish this also clears a taint left behind by a previous agent instance."""
+        key = UNHEALTHY_TAINT["key"]
+
+        def edit(taints: List[Dict[str, Any]]) -> Optional[List[Dict[str, Any]]]:
+            if any(t.get("key") == key for t in taints) == want:
+                return None
+            return taints + [dict(UNHEALTHY_TAINT)] if want else [t for t in taints if t.get("key") != key]
+        return client.update_node_taints(self.node, edit) is not None
 
 
 def _metrics(rep: Optional[Dict[str, Any]]) -> str:
@@ -289,6 +357,12 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--heartbeat-interval", type=float, default=300.0,
                     help="re-send an unchanged AMDGPUHealthy condition this often (s); keep it below the "
                          "checker's --probe-max-age")
+    ap.add_argument("--no-events", dest="events", action="store_false",
+                    help="do not post a Kubernetes Event on the node when its verdict changes")
+    ap.add_argument("--event-namespace", default="default", help="namespace of the node Events (default: default)")
+    ap.add_argument("--taint-unhealthy", action="store_true",
+                    help=f"keep the taint {UNHEALTHY_TAINT['key']}={UNHEALTHY_TAINT['value']}:"
+                         f"{UNHEALTHY_TAINT['effect']} on the node while it is unhealthy (removed on recovery)")
     return ap
 
 
@@ -296,7 +370,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     args = build_parser().parse_args(argv)
     pubs = set(args.publish.split(","))
     agent = Agent(args.node, args.source, args.fixture, args.diag_level, args.diag_interval,
-                  annotation_refresh=args.annotation_refresh, heartbeat_interval=args.heartbeat_interval)
+                  annotation_refresh=args.annotation_refresh, heartbeat_interval=args.heartbeat_interval,
+                  events=args.events, event_namespace=args.event_namespace, taint_unhealthy=args.taint_unhealthy)
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient

@@ -53,6 +53,7 @@ class CheckOptions:
         self.probe_concurrency = 64
         self.probe_timeout = 2.0
         self.health_reeval = False
+        self.require_schedulable = False
         self.trace = False
         self.slack_gate: Optional[Callable[["CheckResult"], bool]] = None
         for k, v in kw.items():
@@ -70,7 +71,7 @@ class CheckOptions:
 
     @property
     def needs_extras(self) -> bool:
-        return self.health_policy != "off" or self.json_extended
+        return self.health_policy != "off" or self.json_extended or self.require_schedulable
 
 
 class CheckResult:
@@ -164,10 +165,29 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer) -> List[O
         return verdicts
 
 
+def apply_schedulability(scan: ScanResult, opts: CheckOptions) -> None:
+    """``--require-schedulable``: a GPU node that takes no new pods -- cordoned (``spec.unschedulable``)
+    or tainted ``amd.com/gpu-unhealthy`` by the node agent -- does not count as Ready.
+
+    Off by default: the reference counts cordoned and tainted nodes as Ready (``check-gpu-node.py:172-178``
+    reads conditions only; SURVEY §2.2 "not consumed")."""
+    if not opts.require_schedulable:
+        return
+    changed = False
+    for node, ex in zip(scan.gpu_nodes, scan.extras):
+        if node["ready"] and (ex.unschedulable or any(t.get("key") == H.UNHEALTHY_TAINT["key"]
+                                                      for t in node["taints"])):
+            node["ready"] = False
+            changed = True
+    if changed:
+        scan.recompute_ready()
+
+
 def run_check(cluster: ClusterConnection, opts: CheckOptions, tracer: Optional[Tracer] = None) -> CheckResult:
     tracer = tracer or (Tracer() if (opts.trace or opts.json_extended) else NullTracer())
     scan = scan_cluster(cluster, opts, tracer)
     verdicts = apply_health(scan, opts, tracer)
+    apply_schedulability(scan, opts)
     return CheckResult(scan, verdicts, tracer)
 
 

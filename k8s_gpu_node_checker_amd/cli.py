@@ -65,8 +65,11 @@ def build_parser(show_all: bool = False, prog: Optional[str] = None) -> argparse
     x.add_argument("--probe-endpoint", help=h("노드별 프로브 URL 템플릿, 예: http://{ip}:9464/probe"))
     x.add_argument("--probe-concurrency", type=int, default=64, help=h("프로브 fan-out 동시성 (기본: 64)"))
     x.add_argument("--probe-timeout", type=float, default=2.0, help=h("노드별 프로브 타임아웃(초) (기본: 2)"))
+    x.add_argument("--require-schedulable", action="store_true",
+                   help=h("cordon(spec.unschedulable) 되었거나 amd.com/gpu-unhealthy taint 가 있는 GPU 노드는 "
+                          "Ready 로 세지 않음"))
     x.add_argument("--mi355x", action="store_true",
-                   help=h("MI355X 프리셋: --gpu-source allocatable --health-policy require"))
+                   help=h("MI355X 프리셋: --gpu-source allocatable --health-policy require --require-schedulable"))
     x.add_argument("--json-extended", action="store_true", help=h("JSON 에 MI355X 헬스/타이밍 필드 추가"))
     x.add_argument("--trace", action="store_true", help=h("단계별 소요 시간을 stderr 로 출력"))
     x.add_argument("--prometheus-textfile", help=h("node-exporter textfile 메트릭 경로"))
@@ -92,6 +95,7 @@ def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
     if args.mi355x:
         args.gpu_source = "allocatable"
         args.health_policy = "require"
+        args.require_schedulable = True
     if args.json_extended:
         args.json = True
     return args
@@ -168,7 +172,7 @@ def _watch_events(args: argparse.Namespace) -> int:
     """
     last = {"code": 0}
     try:
-        from .checker import CheckOptions, CheckResult, apply_health, emit_report
+        from .checker import CheckOptions, CheckResult, apply_health, apply_schedulability, emit_report
         from .kube.watch import NodeWatcher
         from .utils import statefile
         from .utils.timing import NullTracer, Tracer
@@ -182,7 +186,9 @@ def _watch_events(args: argparse.Namespace) -> int:
 
         def evaluate(scan):
             tr = Tracer() if (opts.trace or opts.json_extended) else NullTracer()
-            return CheckResult(scan, apply_health(scan, opts, tr), tr)
+            result = CheckResult(scan, apply_health(scan, opts, tr), tr)
+            apply_schedulability(scan, opts)
+            return result
 
         def report(result) -> None:
             emit_report(result, opts)

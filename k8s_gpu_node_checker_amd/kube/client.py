@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import json
 import time
-from typing import Any, Dict, Optional, Sequence
+from typing import Any, Callable, Dict, List, Optional, Sequence
 from urllib.parse import quote
 
 from ..models.node import ScanResult
@@ -270,4 +270,42 @@ class KubeClient:
         body = json.dumps({"metadata": {"annotations": annotations}}).encode()
         resp = self.request("PATCH", "/api/v1/nodes/" + quote(name, safe=""), body,
                             content_type="application/merge-patch+json", idempotent=True)
+        return json.loads(resp.body) if resp.body else {}
+
+    def update_node_taints(self, name: str,
+                           edit: Callable[[List[Dict[str, Any]]], Optional[List[Dict[str, Any]]]],
+                           attempts: int = 5) -> Optional[List[Dict[str, Any]]]:
+        """Read-modify-write of ``spec.taints`` under optimistic concurrency (client-go ``RetryOnConflict``).
+
+        ``edit(taints)`` returns the new list, or ``None`` when nothing has to change.  A merge-patch
+        replaces the whole list, so it carries the ``resourceVersion`` that was read: if anyone wrote the
+        node in between (kubelet, node controller, an operator's ``kubectl taint``) the apiserver answers
+        409 Conflict instead of dropping their change, and the cycle is redone on a fresh read.
+        Returns the list written, or ``None`` if no write was needed.
+        """
+        path = "/api/v1/nodes/" + quote(name, safe="")
+        attempts = max(1, attempts)
+        for attempt in range(attempts):
+            node = self.get_node(name)
+            new = edit(list((node.get("spec") or {}).get("taints") or []))
+            if new is None:
+                return None
+            patch: Dict[str, Any] = {"spec": {"taints": new}}
+            rv = (node.get("metadata") or {}).get("resourceVersion")
+            if rv:
+                patch["metadata"] = {"resourceVersion": rv}
+            try:
+                self.request("PATCH", path, json.dumps(patch).encode(), content_type="application/merge-patch+json")
+                return new
+            except ApiException as e:
+                if e.status != 409 or attempt + 1 >= attempts:
+                    raise
+                self.sleep(self.backoff.delay(attempt))
+        return None
+
+    def create_event(self, namespace: str, event: Dict[str, Any]) -> Dict[str, Any]:
+        """``POST /api/v1/namespaces/{ns}/events`` (RBAC ``events: create``).  Not retried: a retry after
+        a lost response would post the event twice."""
+        resp = self.request("POST", f"/api/v1/namespaces/{quote(namespace, safe='')}/events",
+                            json.dumps(event).encode(), content_type="application/json", idempotent=False)
         return json.loads(resp.body) if resp.body else {}

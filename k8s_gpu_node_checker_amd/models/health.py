@@ -279,6 +279,16 @@ _REASON = {HEALTHY: "MI355XHealthy", DEGRADED: "MI355XDegraded", UNHEALTHY: "MI3
            UNKNOWN: "MI355XProbeFailed"}
 _STATE_OF_REASON = {v: k for k, v in _REASON.items()}
 
+#: Taint the agent keeps on its node while the verdict is unhealthy (``--taint-unhealthy``) and removes on
+#: recovery: the scheduler stops placing new pods there.  NoSchedule only -- running jobs are left alone,
+#: evicting them is an operator's decision.  The checker's ``--require-schedulable`` reads it back.
+UNHEALTHY_TAINT = {"key": "amd.com/gpu-unhealthy", "value": "true", "effect": "NoSchedule"}
+
+
+def condition_reason(state: str) -> str:
+    """NodeCondition / Event reason of a verdict state (``MI355XHealthy``, ``MI355XUnhealthy``, ...)."""
+    return _REASON[state]
+
 
 def parse_k8s_time(ts: Optional[str]) -> Optional[float]:
     """RFC 3339 ``2025-10-10T00:00:00Z`` (what the apiserver emits) -> epoch seconds."""

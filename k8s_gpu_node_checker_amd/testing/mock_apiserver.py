@@ -7,7 +7,9 @@ The single ``list_node()`` call is the reference's only cluster seam
 * ``limit`` / ``continue`` pagination (pages pre-serialised and cached, so
   the server's own JSON encoding does not pollute client-side timings)
 * ``GET /api/v1/nodes/{name}``, JSON merge-``PATCH`` of a node (the node
-  agent's annotation write)
+  agent's annotation write) with ``metadata.resourceVersion`` preconditions
+  (409 Conflict on a stale version, ``conflict_first`` injected conflicts),
+  ``POST /api/v1/namespaces/{ns}/events`` (kept in ``k8s_events``)
 * bearer-token auth (401 on mismatch), TLS (given a cert/key)
 * fault injection: fixed status (``403``/``500``), ``fail_first`` transient
   errors with ``Retry-After``, an expired-``continue`` 410, response delay,
@@ -165,7 +167,7 @@ class MockConfig:
     def __init__(self, token: Optional[str] = None, status: Optional[int] = None, fail_first: int = 0,
                  fail_status: int = 503, retry_after: Optional[str] = None, delay: float = 0.0,
                  expire_continue: bool = False, reset: bool = False, gzip: bool = False,
-                 chunked: bool = False, bookmark_interval: float = 1.0):
+                 chunked: bool = False, bookmark_interval: float = 1.0, conflict_first: int = 0):
         self.token = token
         self.status = status
         self.fail_first = fail_first
@@ -177,6 +179,7 @@ class MockConfig:
         self.gzip = gzip
         self.chunked = chunked
         self.bookmark_interval = bookmark_interval
+        self.conflict_first = conflict_first  # 409 for the first N PATCHes that carry a resourceVersion
 
 
 class _Handler(BaseHTTPRequestHandler):
@@ -366,6 +369,22 @@ class _Handler(BaseHTTPRequestHandler):
             self._send(400, self._status_body(400, "BadRequest", "invalid patch"))
             return
         name = unquote(path[len("/api/v1/nodes/"):])
+        meta = patch.get("metadata") if isinstance(patch, dict) else None
+        want_rv = meta.pop("resourceVersion", None) if isinstance(meta, dict) else None
+        if want_rv is not None:
+            # optimistic concurrency: the write only applies to the object version it was computed from
+            srv = self.server
+            with srv.lock:
+                inject = srv.conflicts_left > 0
+                if inject:
+                    srv.conflicts_left -= 1
+            cur = srv.state.find(name[:-len("/status")] if name.endswith("/status") else name)
+            have = ((cur or {}).get("metadata") or {}).get("resourceVersion")
+            if inject or (have is not None and str(want_rv) != str(have)):
+                self._send(409, self._status_body(
+                    409, "Conflict", f'Operation cannot be fulfilled on nodes "{name}": the object has been '
+                    "modified; please apply your changes to the latest version and try again"), reason="Conflict")
+                return
         strategic = "strategic-merge-patch" in (self.headers.get("Content-Type") or "")
         if name.endswith("/status"):
             name = name[:-len("/status")]
@@ -375,6 +394,34 @@ class _Handler(BaseHTTPRequestHandler):
             self._send(404, self._status_body(404, "NotFound", "node not found"), reason="Not Found")
         else:
             self._send(200, json.dumps(node).encode())
+
+    def do_POST(self) -> None:  # noqa: N802
+        """``POST /api/v1/namespaces/{ns}/events``: stored in ``server.k8s_events`` (``generateName`` honoured)."""
+        length = int(self.headers.get("Content-Length") or 0)
+        body = self.rfile.read(length) if length else b""
+        if not self._pre():
+            return
+        parts = urlsplit(self.path).path.strip("/").split("/")
+        if len(parts) != 5 or parts[:3] != ["api", "v1", "namespaces"] or parts[4] != "events":
+            self._send(404, self._status_body(404, "NotFound", "not found"), reason="Not Found")
+            return
+        try:
+            ev = json.loads(body or b"{}")
+        except ValueError:
+            ev = None
+        if not isinstance(ev, dict):
+            self._send(400, self._status_body(400, "BadRequest", "invalid event"))
+            return
+        srv = self.server
+        with srv.lock:
+            srv.event_seq += 1
+            meta = ev.get("metadata") if isinstance(ev.get("metadata"), dict) else {}
+            ev["metadata"] = meta
+            meta["namespace"] = unquote(parts[3])
+            if not meta.get("name"):
+                meta["name"] = (meta.get("generateName") or "event.") + f"{srv.event_seq:08x}"
+            srv.k8s_events.append(ev)
+        self._send(201, json.dumps(ev).encode(), reason="Created")
 
 
 class MockApiServer(ThreadingHTTPServer):
@@ -389,7 +436,10 @@ class MockApiServer(ThreadingHTTPServer):
         self.cfg = cfg or MockConfig()
         self.lock = threading.Lock()
         self.failures_left = self.cfg.fail_first
+        self.conflicts_left = self.cfg.conflict_first
         self.log: List[Dict[str, Any]] = []
+        self.k8s_events: List[Dict[str, Any]] = []  # core/v1 Events POSTed by clients
+        self.event_seq = 0
         self.scheme = "http"
         if certfile:
             import ssl

@@ -201,17 +201,21 @@ def test_agent_writes_only_changes_plus_heartbeats(mock_cluster, fixture_report)
     srv = mock_cluster([fixtures.realistic_node("n")])
     ag = A.Agent("n", source="fixture", fixture=fixture_report)
     both = {"annotation": True, "condition": True}
+
+    def publish(rep):
+        w = ag.publish(kc, rep)
+        return {k: w[k] for k in both}
     with KubeClient(ClusterConnection(srv.url)) as kc:
         r1 = ag.probe_once()
-        assert ag.publish(kc, r1) == both
+        assert publish(r1) == both
         r2 = ag.probe_once()  # same GPUs, new timestamp / timings / temperature: nothing to write
         r2["gpus"][0]["hotspot_c"] = 61
-        assert ag.publish(kc, r2) == {"annotation": False, "condition": False}
+        assert publish(r2) == {"annotation": False, "condition": False}
         r3 = ag.probe_once()
         r3["gpus"][0]["ecc_uncorrectable"] = 2  # a real change: new report, new verdict
-        assert ag.publish(kc, r3) == both
+        assert publish(r3) == both
         ag.annotation_refresh = ag.heartbeat_interval = 0.0
-        assert ag.publish(kc, r3) == both  # refresh / heartbeat intervals elapsed
+        assert publish(r3) == both  # refresh / heartbeat intervals elapsed
         cond = kc.get_node("n")["status"]["conditions"]
     patches = [e["path"] for e in srv.log if e["method"] == "PATCH"]
     assert sum(p.endswith("/status") for p in patches) == 3

@@ -44,4 +44,5 @@ def test_rbac_matches_what_the_code_calls():
                                                 for v in rule["verbs"]}
     assert verbs["gpu-node-checker"] == {("nodes", "get"), ("nodes", "list")}  # the reference's contract
     assert ("nodes/status", "patch") in verbs["mi355x-node-agent"] and ("nodes", "patch") in verbs["mi355x-node-agent"]
+    assert {("nodes", "get"), ("events", "create")} <= verbs["mi355x-node-agent"]  # taint read-modify-write, events
     assert ("nodes", "watch") in verbs["gpu-node-watcher"]
