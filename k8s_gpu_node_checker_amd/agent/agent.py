@@ -148,6 +148,14 @@ class Agent:
                 self._fabric = {"p2p": {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s")}}
             except Exception as e:
                 self._fabric = {"p2p": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
+            # the collectives the node's jobs run, over the same links: RCCL in this process (ops/fabric.py)
+            try:
+                from ..ops import fabric
+                r = fabric.collective_suite(devices)
+                self._fabric["rccl"] = {k: r.get(k) for k in ("pass", "best_busbw_gbps", "best_busbw_by_op",
+                                                              "detail", "wall_s", "rccl")}
+            except Exception as e:
+                self._fabric["rccl"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
         self._diag_ts = now
         return self._diag_cache
 
@@ -299,6 +307,11 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
         lines.append("# TYPE mi355x_node_xgmi_p2p_gbps gauge")
         lines.append(f'mi355x_node_xgmi_p2p_gbps{{stat="median"}} {fabric["median_gbps"]}')
         lines.append(f'mi355x_node_xgmi_p2p_gbps{{stat="min"}} {fabric.get("min_gbps", 0)}')
+    rccl = (rep.get("fabric") or {}).get("rccl")
+    if isinstance(rccl, dict) and isinstance(rccl.get("best_busbw_by_op"), dict):
+        lines.append("# TYPE mi355x_node_rccl_busbw_gbps gauge")
+        for op, bw in sorted(rccl["best_busbw_by_op"].items()):
+            lines.append(f'mi355x_node_rccl_busbw_gbps{{op="{op}"}} {bw}')
     return "\n".join(lines) + "\n"
 
 

@@ -9,6 +9,7 @@ artefact               source                                              toolc
 ``libmi355x_probe.so`` ``csrc/probe/probe.cpp`` (C ABI over libamd_smi)     g++ + /opt/rocm/lib/libamd_smi
 ``mi355x-probe``       ``csrc/probe/probe_main.cpp`` (standalone CLI)       g++ + libamd_smi
 ``libmi355x_diag.so``  ``csrc/diag/diag.hip`` (HIP kernels, gfx950 only)    hipcc --offload-arch=gfx950
+``libmi355x_fabric.so`` ``csrc/fabric/fabric.hip`` (RCCL over xGMI)         hipcc + /opt/rocm/lib/librccl
 =====================  ==================================================  ==========================
 
 Outputs are rebuilt only when a source is newer (``--force`` to override).
@@ -69,6 +70,14 @@ def _targets() -> Dict[str, Dict[str, object]]:
             "out": os.path.join(OUT, "libmi355x_diag.so"),
             "cmd": [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
                     "-Wall", "-Wno-unused-result"],
+            "requires": hipcc,
+        },
+        "fabric": {
+            "sources": [os.path.join(CSRC, "fabric", "fabric.hip")],
+            "out": os.path.join(OUT, "libmi355x_fabric.so"),
+            "cmd": [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+                    "-Wall", "-Wno-unused-result"],
+            "post": ["-L", os.path.join(ROCM, "lib"), "-lrccl", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"],
             "requires": hipcc,
         },
     }

@@ -1,0 +1,282 @@
+// Node-level xGMI fabric check with RCCL, in one process (no torchrun, no torch): the node agent's
+// level-2 collective test.  ncclCommInitAll gives one communicator per local MI355X; every collective
+// is issued for all GPUs inside one ncclGroupStart/End from this thread, the way a multi-GPU-per-process
+// nccl-tests run drives them.  The four collectives cover RCCL's two algorithm families on the 7
+// point-to-point xGMI links of each GPU: rings (all-reduce, reduce-scatter, all-gather) and direct peer
+// exchanges (all-to-all).
+//
+// Every op runs on rank-coded fp32 data whose result is exact (sums of small integers), and every
+// received element is compared on the GPU:
+//   all_reduce      in_r = r+1                      -> out = n(n+1)/2
+//   reduce_scatter  in_r chunk c = (r+1)(c+1)       -> out_r = (r+1) n(n+1)/2
+//   all_gather      in_r = r+1                      -> out chunk c = c+1
+//   all_to_all      in_r chunk c = r*n + c          -> out_r chunk c = c*n + r
+// Bandwidth follows the nccl-tests convention: bytes = the larger of the per-rank input and output,
+// algbw = bytes / t, busbw = algbw * 2(n-1)/n (all-reduce) or algbw * (n-1)/n (the others).
+//
+// C ABI (ctypes, ops/fabric.py):  fabric_open -> fabric_run (any number) -> fabric_close.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+#define HIP_OK(expr)                                                          \
+  do {                                                                        \
+    hipError_t e_ = (expr);                                                   \
+    if (e_ != hipSuccess) {                                                   \
+      g_err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+      return -1;                                                              \
+    }                                                                         \
+  } while (0)
+
+#define NCCL_OK(expr)                                                         \
+  do {                                                                        \
+    ncclResult_t r_ = (expr);                                                 \
+    if (r_ != ncclSuccess) {                                                  \
+      g_err = std::string(#expr) + ": " + ncclGetErrorString(r_);             \
+      return -2;                                                              \
+    }                                                                         \
+  } while (0)
+
+enum Op { ALL_REDUCE = 0, REDUCE_SCATTER = 1, ALL_GATHER = 2, ALL_TO_ALL = 3 };
+
+// value of element i of a buffer made of chunks of `chunk` elements: a * (i / chunk) + b
+__global__ void __launch_bounds__(256) fill_kernel(float* p, size_t n, size_t chunk, float a, float b) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride)
+    p[i] = a * static_cast<float>(i / chunk) + b;
+}
+
+__global__ void __launch_bounds__(256) verify_kernel(const float* p, size_t n, size_t chunk, float a, float b,
+                                                     unsigned long long* errors) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  unsigned long long bad = 0;
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride)
+    bad += p[i] != a * static_cast<float>(i / chunk) + b;
+  if (bad) atomicAdd(errors, bad);
+}
+
+struct Dev {
+  int device = -1;
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;
+  float* in = nullptr;
+  float* out = nullptr;
+  unsigned long long* errors = nullptr;
+  size_t cap = 0;  // bytes of `in` and of `out`
+};
+
+struct Ctx {
+  std::vector<Dev> devs;
+};
+
+unsigned grid_for(size_t n) { return static_cast<unsigned>(std::min<size_t>((n + 255) / 256, 4096)); }
+
+int ensure_buffers(Dev& d, size_t bytes) {
+  if (d.cap >= bytes) return 0;
+  HIP_OK(hipSetDevice(d.device));
+  if (d.in) HIP_OK(hipFree(d.in));
+  if (d.out) HIP_OK(hipFree(d.out));
+  d.in = d.out = nullptr;
+  d.cap = 0;
+  HIP_OK(hipMalloc(&d.in, bytes));
+  HIP_OK(hipMalloc(&d.out, bytes));
+  d.cap = bytes;
+  return 0;
+}
+
+// in/out element counts per rank for op, given `count` = elements of the larger buffer
+void shapes(int op, size_t count, int n, size_t* in_n, size_t* out_n, size_t* per_rank) {
+  switch (op) {
+    case REDUCE_SCATTER: *in_n = count; *out_n = count / n; *per_rank = count / n; break;
+    case ALL_GATHER: *in_n = count / n; *out_n = count; *per_rank = count / n; break;
+    case ALL_TO_ALL: *in_n = count; *out_n = count; *per_rank = count / n; break;
+    default: *in_n = count; *out_n = count; *per_rank = count; break;
+  }
+}
+
+int issue(Ctx& c, int op, size_t count) {
+  const int n = static_cast<int>(c.devs.size());
+  size_t in_n, out_n, per;
+  shapes(op, count, n, &in_n, &out_n, &per);
+  NCCL_OK(ncclGroupStart());
+  for (Dev& d : c.devs) {
+    switch (op) {
+      case ALL_REDUCE: NCCL_OK(ncclAllReduce(d.in, d.out, per, ncclFloat32, ncclSum, d.comm, d.stream)); break;
+      case REDUCE_SCATTER:
+        NCCL_OK(ncclReduceScatter(d.in, d.out, per, ncclFloat32, ncclSum, d.comm, d.stream));
+        break;
+      case ALL_GATHER: NCCL_OK(ncclAllGather(d.in, d.out, per, ncclFloat32, d.comm, d.stream)); break;
+      default: NCCL_OK(ncclAllToAll(d.in, d.out, per, ncclFloat32, d.comm, d.stream)); break;
+    }
+  }
+  NCCL_OK(ncclGroupEnd());
+  return 0;
+}
+
+int sync_all(Ctx& c) {
+  for (Dev& d : c.devs) {
+    HIP_OK(hipSetDevice(d.device));
+    HIP_OK(hipStreamSynchronize(d.stream));
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fabric_last_error(void) { return g_err.c_str(); }
+
+int fabric_rccl_version(void) {
+  int v = 0;
+  return ncclGetVersion(&v) == ncclSuccess ? v : -1;
+}
+
+// One communicator, stream and error counter per device (devices = HIP ordinals, n >= 1).
+void* fabric_open(const int* devices, int n) {
+  if (n < 1 || n > 64) {
+    g_err = "fabric_open: 1..64 devices";
+    return nullptr;
+  }
+  Ctx* c = new Ctx();
+  c->devs.resize(static_cast<size_t>(n));
+  std::vector<ncclComm_t> comms(static_cast<size_t>(n));
+  auto fail = [&]() -> void* {
+    for (Dev& d : c->devs) {
+      if (d.device < 0) continue;
+      (void)hipSetDevice(d.device);
+      if (d.stream) (void)hipStreamDestroy(d.stream);
+      if (d.errors) (void)hipFree(d.errors);
+    }
+    delete c;
+    return nullptr;
+  };
+  for (int i = 0; i < n; ++i) {
+    Dev& d = c->devs[static_cast<size_t>(i)];
+    d.device = devices[i];
+    hipError_t e = hipSetDevice(d.device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&d.errors, sizeof(unsigned long long));
+    if (e != hipSuccess) {
+      g_err = std::string("device setup: ") + hipGetErrorString(e);
+      return fail();
+    }
+  }
+  ncclResult_t r = ncclCommInitAll(comms.data(), n, devices);
+  if (r != ncclSuccess) {
+    g_err = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+    return fail();
+  }
+  for (int i = 0; i < n; ++i) c->devs[static_cast<size_t>(i)].comm = comms[static_cast<size_t>(i)];
+  return c;
+}
+
+// Run `op` on `bytes` per rank (rounded down to a whole number of fp32 chunks): `warmup` untimed calls,
+// `iters` timed calls (host wall clock from the first issue to the last stream's completion), then one
+// verified call.  out[0] = ms per call, out[1] = algbw GB/s, out[2] = busbw GB/s, out[3] = bad elements
+// summed over every GPU.
+int fabric_run(void* ctx, int op, size_t bytes, int iters, int warmup, double* out) {
+  if (!ctx || op < 0 || op > 3 || iters < 1 || warmup < 0) {
+    g_err = "fabric_run: bad arguments";
+    return -3;
+  }
+  Ctx& c = *static_cast<Ctx*>(ctx);
+  const int n = static_cast<int>(c.devs.size());
+  size_t count = bytes / sizeof(float);
+  count -= count % static_cast<size_t>(n);
+  if (count == 0) {
+    g_err = "fabric_run: message smaller than one element per rank";
+    return -3;
+  }
+  size_t in_n, out_n, per;
+  shapes(op, count, n, &in_n, &out_n, &per);
+  for (Dev& d : c.devs)
+    if (ensure_buffers(d, count * sizeof(float)) != 0) return -1;
+
+  for (int r = 0; r < n; ++r) {  // rank-coded inputs (see the header)
+    Dev& d = c.devs[static_cast<size_t>(r)];
+    HIP_OK(hipSetDevice(d.device));
+    float a = 0.f, b = static_cast<float>(r + 1);
+    size_t chunk = in_n;
+    if (op == REDUCE_SCATTER) { a = static_cast<float>(r + 1); b = static_cast<float>(r + 1); chunk = per; }
+    if (op == ALL_TO_ALL) { a = 1.f; b = static_cast<float>(r * n); chunk = per; }
+    hipLaunchKernelGGL(fill_kernel, dim3(grid_for(in_n)), dim3(256), 0, d.stream, d.in, in_n, chunk, a, b);
+    HIP_OK(hipGetLastError());
+  }
+  if (sync_all(c) != 0) return -1;
+
+  for (int i = 0; i < warmup; ++i)
+    if (issue(c, op, count) != 0) return -2;
+  if (sync_all(c) != 0) return -1;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < iters; ++i)
+    if (issue(c, op, count) != 0) return -2;
+  if (sync_all(c) != 0) return -1;
+  const double ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / iters;
+
+  // one more call on freshly zeroed outputs, then every element checked on its GPU
+  for (Dev& d : c.devs) {
+    HIP_OK(hipSetDevice(d.device));
+    HIP_OK(hipMemsetAsync(d.out, 0, out_n * sizeof(float), d.stream));
+    HIP_OK(hipMemsetAsync(d.errors, 0, sizeof(unsigned long long), d.stream));
+  }
+  if (issue(c, op, count) != 0) return -2;
+  const float tri = static_cast<float>(n) * static_cast<float>(n + 1) / 2.f;
+  for (int r = 0; r < n; ++r) {
+    Dev& d = c.devs[static_cast<size_t>(r)];
+    HIP_OK(hipSetDevice(d.device));
+    float a = 0.f, b = tri;
+    size_t chunk = out_n;
+    if (op == REDUCE_SCATTER) b = static_cast<float>(r + 1) * tri;
+    if (op == ALL_GATHER) { a = 1.f; b = 1.f; chunk = per; }
+    if (op == ALL_TO_ALL) { a = static_cast<float>(n); b = static_cast<float>(r); chunk = per; }
+    hipLaunchKernelGGL(verify_kernel, dim3(grid_for(out_n)), dim3(256), 0, d.stream, d.out, out_n, chunk, a, b,
+                       d.errors);
+    HIP_OK(hipGetLastError());
+  }
+  if (sync_all(c) != 0) return -1;
+  unsigned long long bad = 0;
+  for (Dev& d : c.devs) {
+    unsigned long long e = 0;
+    HIP_OK(hipSetDevice(d.device));
+    HIP_OK(hipMemcpy(&e, d.errors, sizeof(e), hipMemcpyDeviceToHost));
+    bad += e;
+  }
+  const double moved = static_cast<double>(count * sizeof(float));  // the larger per-rank buffer
+  const double algbw = moved / (ms * 1e-3) / 1e9;
+  const double factor = op == ALL_REDUCE ? 2.0 * (n - 1) / n : static_cast<double>(n - 1) / n;
+  out[0] = ms;
+  out[1] = algbw;
+  out[2] = algbw * factor;
+  out[3] = static_cast<double>(bad);
+  return 0;
+}
+
+void fabric_close(void* ctx) {
+  if (!ctx) return;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  for (Dev& d : c->devs) {
+    if (d.device < 0) continue;
+    (void)hipSetDevice(d.device);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    if (d.comm) (void)ncclCommDestroy(d.comm);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+    if (d.in) (void)hipFree(d.in);
+    if (d.out) (void)hipFree(d.out);
+    if (d.errors) (void)hipFree(d.errors);
+  }
+  delete c;
+}
+
+}  // extern "C"

@@ -35,9 +35,9 @@ MEMTEST_MAX_ERRORS = 0
 # profiles/mfma_lab_mi355x.jsonl: bf16 1687, fp8 1803, MX-fp8 4027, MX-fp4 7171 TFLOP/s dense)
 MFMA_KINDS = ("bf16", "fp8", "mxfp8", "mxfp4")
 MFMA_MIN_TFLOPS = {"bf16": 1000.0, "fp8": 1000.0, "mxfp8": 2400.0, "mxfp4": 4300.0}
-P2P_MIN_FRACTION_OF_MEDIAN = 0.5
+P2P_MIN_FRACTION_OF_MEDIAN = 0.5  # a GPU pair slower than half the node's median pair: suspect link
 HOST_LINK_MIN_GBPS = 28.0     # PCIe Gen5 x16 host link, pinned copies: measured 56.8 / 56.7 GB/s h2d / d2h
-                              # (profiles/diag_mi355x.json); a Gen4 or x8 link lands at about half  # a GPU pair slower than half the node's median pair: suspect link
+                              # (profiles/diag_mi355x.json); a Gen4 or x8 link lands at about half
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -285,6 +285,8 @@ def main(argv=None) -> int:
     ap.add_argument("--level", type=int, default=1, choices=(1, 2))
     ap.add_argument("--device", type=int, action="append", help="GPU index (repeatable; default: all)")
     ap.add_argument("--no-p2p", dest="p2p", action="store_false", help="skip the level-2 xGMI pair matrix")
+    ap.add_argument("--no-rccl", dest="rccl", action="store_false",
+                    help="skip the level-2 RCCL collectives (ops/fabric.py)")
     args = ap.parse_args(argv)
     devices = args.device if args.device else list(range(device_count()))
     out: Dict[str, Any] = {"devices": {d: {"info": device_info(d), "tests": run(args.level, d)} for d in devices}}
@@ -292,6 +294,10 @@ def main(argv=None) -> int:
     if args.level >= 2 and args.p2p:
         out["fabric"] = {"p2p": p2p_matrix(devices)}
         ok = ok and out["fabric"]["p2p"]["pass"]
+    if args.level >= 2 and args.rccl:
+        from . import fabric  # with one GPU: RCCL's data path and the result checks, no bandwidth verdict
+        out.setdefault("fabric", {})["rccl"] = fabric.collective_suite(devices)
+        ok = ok and out["fabric"]["rccl"]["pass"]
     out["pass"] = ok
     print(json.dumps(out, indent=1))
     return 0 if out["pass"] else 1

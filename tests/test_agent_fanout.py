@@ -190,11 +190,55 @@ def test_agent_metrics_cover_diag_kinds_and_fabric():
     rep = fixtures.mi355x_probe_report("n", gpus=1)
     rep["gpus"][0]["diag"] = {"mfma": {"pass": True, "kinds": {"mxfp4": {"tflops": 7600.0, "errors": 0}}},
                               "host_link": {"pass": True, "h2d_gbps": 56.8, "d2h_gbps": 56.7}}
-    rep["fabric"] = {"p2p": {"pass": True, "median_gbps": 48.0, "min_gbps": 45.0}}
+    rep["fabric"] = {"p2p": {"pass": True, "median_gbps": 48.0, "min_gbps": 45.0},
+                     "rccl": {"pass": True, "best_busbw_by_op": {"all_reduce": 310.5, "all_to_all": 280.0}}}
     m = A._metrics(rep)
     assert 'mi355x_gpu_diag_tflops{gpu="0",bdf="0000:05:00.0",test="mfma",dtype="mxfp4"} 7600.0' in m
     assert 'mi355x_gpu_diag_h2d_gbps{gpu="0",bdf="0000:05:00.0",test="host_link"} 56.8' in m
     assert 'mi355x_node_xgmi_p2p_gbps{stat="min"} 45.0' in m
+    assert 'mi355x_node_rccl_busbw_gbps{op="all_reduce"} 310.5' in m
+
+
+def test_fabric_suite_rows_and_verdict_with_a_stub_library(monkeypatch):
+    """ops/fabric.py over a stand-in for libmi355x_fabric.so: row shape, the 8-GPU busbw floor, bad data,
+    and an RCCL init failure reported as a failed check (not a crash)."""
+    import ctypes
+    from k8s_gpu_node_checker_amd.ops import fabric
+
+    class Stub:
+        def __init__(self, busbw, errors=0, fail_open=False):
+            self.busbw, self.errors, self.fail_open, self.closed = busbw, errors, fail_open, 0
+
+        def fabric_open(self, arr, n):
+            return None if self.fail_open else 1
+
+        def fabric_run(self, ctx, op, nbytes, iters, warmup, out):
+            out[0], out[1], out[2], out[3] = 1.0, self.busbw * 0.57, self.busbw, float(self.errors if op == 3 else 0)
+            return 0
+
+        def fabric_close(self, ctx):
+            self.closed += 1
+
+        def fabric_last_error(self):
+            return b"ncclCommInitAll: unhandled system error"
+
+        def fabric_rccl_version(self):
+            return 22703
+    assert ctypes  # the stub stands in for the ctypes.CDLL
+    stub = Stub(busbw=320.0)
+    monkeypatch.setattr(fabric, "_lib", stub)
+    res = fabric.collective_suite(range(8), sizes=[256 << 20])
+    assert res["pass"] and res["world"] == 8 and res["rccl"] == "2.27.3" and stub.closed == 1
+    assert [r["op"] for r in res["rows"]] == list(fabric.OPS) and res["best_busbw_gbps"] == 320.0
+    monkeypatch.setattr(fabric, "_lib", Stub(busbw=60.0))
+    slow = fabric.collective_suite(range(8), sizes=[256 << 20])
+    assert not slow["pass"] and "busbw 60.0 GB/s" in slow["detail"]
+    monkeypatch.setattr(fabric, "_lib", Stub(busbw=320.0, errors=5))
+    bad = fabric.collective_suite(range(8), sizes=[256 << 20])
+    assert not bad["pass"] and bad["detail"] == "result mismatch: all_to_all"
+    monkeypatch.setattr(fabric, "_lib", Stub(busbw=0.0, fail_open=True))
+    dead = fabric.collective_suite(range(8))
+    assert not dead["pass"] and "unhandled system error" in dead["detail"]
 
 
 def test_agent_writes_only_changes_plus_heartbeats(mock_cluster, fixture_report):

@@ -222,6 +222,18 @@ def test_rccl_collective_single_rank(repo):
     assert d["backend"] == "nccl" and d["pass"] and all(r["correct"] for r in d["rows"])
 
 
+def test_rccl_in_process_fabric_suite(dev):
+    """libmi355x_fabric.so: ncclCommInitAll over the box's GPUs, all four collectives, every received
+    element checked on its GPU against the rank-coded expectation."""
+    from k8s_gpu_node_checker_amd.ops import diag, fabric
+    n = min(diag.device_count(), 8)
+    res = fabric.collective_suite(list(range(n)), sizes=[1 << 20, 64 << 20], iters=3, warmup=1)
+    assert res["pass"], res
+    assert [(r["op"], r["bytes"]) for r in res["rows"]] == [(op, b) for op in fabric.OPS for b in (1 << 20, 64 << 20)]
+    assert all(r["errors"] == 0 and r["algbw_gbps"] > 0 for r in res["rows"]), res["rows"]
+    assert res["rccl"] != "unknown"
+
+
 def test_agent_diagnostics_threads_per_device(dev):
     from k8s_gpu_node_checker_amd.agent.agent import Agent
     from k8s_gpu_node_checker_amd.ops import diag
