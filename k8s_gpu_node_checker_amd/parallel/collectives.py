@@ -16,7 +16,8 @@ op and message size it times ``iters`` calls and reports
   must be ``i + 1``; all-to-all chunk ``i`` received by rank ``r`` must be
   ``i * n + r`` (a broken link, a wrong route or a bad GPU corrupts it).
 
-Run on a node (the agent's level-3 check, or by hand)::
+Run on a node by hand (the node agent's level-2 diagnostics run the same four ops from one
+process through ``libmi355x_fabric.so``, ``ops/fabric.py``)::
 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
         -m k8s_gpu_node_checker_amd.parallel.collectives --sizes 64M,256M,1G [--ops all_reduce,all_to_all]
