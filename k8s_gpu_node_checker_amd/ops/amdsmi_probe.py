@@ -45,6 +45,12 @@ def native_available() -> bool:
     return _native() is not None
 
 
+def close() -> None:
+    """Shut amd-smi down (the native probe keeps it initialised between probes); the next probe re-opens."""
+    if _lib is not None:
+        _lib.mi355x_probe_close()
+
+
 def probe_native(node: str) -> Dict[str, Any]:
     L = _native()
     if L is None:

@@ -62,7 +62,11 @@ def load_cdll(filename: str, required: bool = False) -> Optional[ctypes.CDLL]:
     err = None
     if os.path.exists(path):
         try:
-            lib = ctypes.CDLL(path, mode=getattr(os, "RTLD_NOW", 2) | ctypes.RTLD_GLOBAL)
+            # RTLD_LOCAL: libamd_smi.so embeds rocm_smi and exports its rsmi_* symbols.  Loaded into the
+            # global scope it would interpose librocm_smi64 for every library loaded after it, and
+            # librccl (which links librocm_smi64) then crashed in its load-time initialisers
+            # (tools/exit_repro.py, MI355X).  Nothing resolves symbols across these libraries.
+            lib = ctypes.CDLL(path, mode=getattr(os, "RTLD_NOW", 2) | ctypes.RTLD_LOCAL)
         except OSError as e:  # missing ROCm runtime, wrong arch, ...
             err = e
     else:

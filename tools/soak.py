@@ -3,7 +3,11 @@
 verdict and rates, plus min/median/max per metric.  A burn-in tool that faults, hangs or drifts under
 sustained load is worse than none; this is the evidence that it does not.
 
-    python tools/soak.py --minutes 5 --out gpurun_out/soak.json
+    python tools/soak.py --minutes 5 --out gpurun_out/soak.json [--rccl]
+
+``--rccl`` adds the in-process RCCL collectives (``ops/fabric.py``: communicator set up and torn down
+every round, as the agent does hourly) and tracks host RSS and amd-smi VRAM in use across the run, so
+a per-round leak shows as drift.
 """
 
 from __future__ import annotations
@@ -22,11 +26,26 @@ METRICS = (("gemm", "tflops"), ("gemm_fp8", "tflops"), ("hbm", "copy_tbs"), ("hb
            ("hbm", "write_tbs"), ("memtest", "errors"), ("host_link", "h2d_gbps"), ("host_link", "d2h_gbps"))
 
 
+def _rss_mb() -> float:
+    with open("/proc/self/status") as f:
+        for line in f:
+            if line.startswith("VmRSS:"):
+                return round(int(line.split()[1]) / 1024, 1)
+    return 0.0
+
+
+def _vram_used_mb(device: int):
+    from k8s_gpu_node_checker_amd.ops import amdsmi_probe
+    gpus = amdsmi_probe.probe_native("soak").get("gpus") or []
+    return gpus[device].get("vram_used_mb") if device < len(gpus) else None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--minutes", type=float, default=5.0)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/soak.json")
+    ap.add_argument("--rccl", action="store_true", help="also run the RCCL collectives every round")
     args = ap.parse_args()
     deadline = time.monotonic() + args.minutes * 60
     rounds, failures = [], []
@@ -34,7 +53,20 @@ def main() -> int:
     t0 = time.time()
     while time.monotonic() < deadline:
         res = diag.run(2, args.device)
-        rnd = {"t": round(time.time() - t0, 1), "pass": all(r.get("pass") for r in res.values())}
+        rnd_extra: dict = {}
+        if args.rccl:
+            from k8s_gpu_node_checker_amd.ops import fabric
+            fab = fabric.collective_suite([args.device], sizes=[64 << 20], iters=3, warmup=1)
+            res["rccl"] = {"pass": fab["pass"], "detail": fab.get("detail", "")}
+            for row in fab["rows"]:
+                series.setdefault(f"rccl.{row['op']}.algbw_gbps", []).append(row["algbw_gbps"])
+            series.setdefault("host.rss_mb", []).append(_rss_mb())
+            vram = _vram_used_mb(args.device)
+            if isinstance(vram, (int, float)):
+                series.setdefault("gpu.vram_used_mb", []).append(vram)
+                rnd_extra["vram_mb"] = vram
+            rnd_extra["rss_mb"] = series["host.rss_mb"][-1]
+        rnd = {"t": round(time.time() - t0, 1), "pass": all(r.get("pass") for r in res.values()), **rnd_extra}
         for test, key in METRICS:
             v = (res.get(test) or {}).get(key)
             if isinstance(v, (int, float)):
@@ -50,6 +82,11 @@ def main() -> int:
                for k, v in series.items()}
     out = {"device": diag.device_info(args.device), "minutes": args.minutes, "rounds": len(rounds),
            "all_pass": not failures, "failures": failures[:20], "summary": summary}
+    if args.rccl:
+        rss, vram = series.get("host.rss_mb") or [None], series.get("gpu.vram_used_mb") or [None]
+        out["leak_check"] = {"rss_mb_first_round": rss[0], "rss_mb_last_round": rss[-1],
+                             "vram_used_mb_first_round": vram[0], "vram_used_mb_last_round": vram[-1],
+                             "vram_used_mb_every_10th_round": vram[::10], "rss_mb_every_10th_round": rss[::10]}
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with open(args.out, "w") as f:
         json.dump(out, f, indent=1)
