@@ -46,3 +46,30 @@ def test_rbac_matches_what_the_code_calls():
     assert ("nodes/status", "patch") in verbs["mi355x-node-agent"] and ("nodes", "patch") in verbs["mi355x-node-agent"]
     assert {("nodes", "get"), ("events", "create")} <= verbs["mi355x-node-agent"]  # taint read-modify-write, events
     assert ("nodes", "watch") in verbs["gpu-node-watcher"]
+
+
+def test_manifests_are_self_consistent():
+    """Everything a workload references (namespace, ServiceAccount, PVC) is defined in deploy/, and the
+    kustomization lists every manifest."""
+    docs = [d for path in MANIFESTS for d in yaml.safe_load_all(open(path)) if d]
+    defined = {(d["kind"], (d.get("metadata") or {}).get("namespace"), d["metadata"]["name"])
+               for d in docs if d["kind"] != "Kustomization"}
+    namespaces = {name for kind, _, name in defined if kind == "Namespace"}
+    for d in docs:
+        if d["kind"] in ("Kustomization", "Namespace") or d["kind"].startswith("Cluster"):
+            continue
+        ns = d["metadata"]["namespace"]
+        assert ns in namespaces, (d["kind"], d["metadata"]["name"])
+        spec = d.get("spec") or {}
+        if d["kind"] == "CronJob":
+            spec = spec["jobTemplate"]["spec"]
+        pod = (spec.get("template") or {}).get("spec")
+        if not pod:
+            continue
+        assert ("ServiceAccount", ns, pod["serviceAccountName"]) in defined, pod["serviceAccountName"]
+        for v in pod.get("volumes") or []:
+            if "persistentVolumeClaim" in v:
+                assert ("PersistentVolumeClaim", ns, v["persistentVolumeClaim"]["claimName"]) in defined
+    kust = yaml.safe_load(open(os.path.join(REPO, "deploy", "kustomization.yaml")))
+    assert sorted(kust["resources"]) == sorted(os.path.basename(p) for p in MANIFESTS
+                                               if not p.endswith("kustomization.yaml"))
