@@ -92,21 +92,25 @@ inline const char* find_quote_or_backslash(const char* p, const char* e) {
   return p;
 }
 
+// Closing quote of a string whose first backslash is at p (nullptr if unterminated); defined below.
+const char* finish_escaped_string(const char* p, const char* e);
+
 RawStr read_raw_string(Cursor& c) {
   c.expect('"');
   const char* b = c.p;
-  const char* p = b;
-  bool esc = false;
-  for (;;) {
-    p = find_quote_or_backslash(p, c.end);
-    if (p >= c.end) throw Fallback{"unterminated string"};
-    if (*p == '"') {
-      c.p = p + 1;
-      return RawStr{b, p, esc};
-    }
-    esc = true;  // backslash: skip it and the escaped character
-    p += 2;
+  const char* p = find_quote_or_backslash(b, c.end);
+  if (p >= c.end) throw Fallback{"unterminated string"};
+  if (*p == '"') {  // the common case: no escapes
+    c.p = p + 1;
+    return RawStr{b, p, false};
   }
+  // Escaped: JSON stored in a string (the agent's health-report annotation) has a backslash every few
+  // bytes, so the rest is scanned 64 bytes per step with the escaped-quote mask instead of stopping at
+  // every backslash.
+  p = finish_escaped_string(p, c.end);
+  if (!p) throw Fallback{"unterminated string"};
+  c.p = p + 1;
+  return RawStr{b, p, true};
 }
 
 void append_utf8(std::string& out, uint32_t cp) {
@@ -418,6 +422,45 @@ const char* skip_container_avx2(const char* p, const char* e) {
 
 const bool g_have_avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("pclmul") &&
                          __builtin_cpu_supports("popcnt") && __builtin_cpu_supports("bmi");
+
+__attribute__((target("avx2,pclmul,popcnt,bmi")))
+const char* finish_escaped_string_avx2(const char* p, const char* e) {
+  // p is a backslash not preceded by one, so no escape carries in
+  uint64_t prev_escaped = 0;
+  const uint64_t even = 0x5555555555555555ULL;
+  alignas(32) char tail[64];
+  for (const char* base = p; base < e; base += 64) {
+    const char* src = base;
+    if (e - base < 64) {
+      memset(tail, ' ', sizeof tail);
+      memcpy(tail, base, static_cast<size_t>(e - base));
+      src = tail;
+    }
+    const __m256i lo = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src));
+    const __m256i hi = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 32));
+    uint64_t bs = eq_mask64(lo, hi, '\\') & ~prev_escaped;
+    const uint64_t follows = (bs << 1) | prev_escaped;
+    const uint64_t odd_starts = bs & ~even & ~follows;
+    uint64_t even_starts;
+    prev_escaped = __builtin_add_overflow(odd_starts, bs, &even_starts) ? 1 : 0;
+    const uint64_t escaped = (even ^ (even_starts << 1)) & follows;
+    const uint64_t quotes = eq_mask64(lo, hi, '"') & ~escaped;
+    if (quotes) {
+      const char* q = base + __builtin_ctzll(quotes);
+      return q < e ? q : nullptr;
+    }
+  }
+  return nullptr;
+}
+
+const char* finish_escaped_string(const char* p, const char* e) {
+  if (g_have_avx2) return finish_escaped_string_avx2(p, e);
+  for (;;) {  // p is at a backslash: skip it and the escaped character, find the next stop
+    p = find_quote_or_backslash(p + 2, e);
+    if (p >= e) return nullptr;
+    if (*p == '"') return p;
+  }
+}
 
 void skip_container(Cursor& c) {
   const char* end = g_have_avx2 ? skip_container_avx2(c.p, c.end) : skip_container_sse2(c.p, c.end);

@@ -183,6 +183,26 @@ def test_skipped_subtrees_with_escapes(junk, pad, ascii_only):
         assert len(r.gpu_nodes) == 2
 
 
+@settings(max_examples=300, suppress_health_check=[HealthCheck.too_slow])
+@given(json_tree, st.integers(0, 130), st.integers(0, 9), st.booleans())
+def test_escaped_modelled_strings_at_every_alignment(junk, pad, run, ascii_only):
+    """Modelled strings with escapes (the health annotation is JSON stored in a string) are read
+    64 bytes per step after their first backslash: backslash runs of every parity ending right
+    before a quote, at every offset from the block edge, and a quote as the final byte, must all
+    decode like json.loads."""
+    tricky = "a" * pad + "\\" * run + '"' + "b" * (pad % 13) + "\\" * (run + 1) + '"'
+    node = {"metadata": {"name": "n" + "\\" * run + '"' + "x" * pad,
+                         "labels": {"k" * (pad % 5) + '"': tricky, "plain": "p" * pad},
+                         "annotations": {HEALTH_ANNOTATION: json.dumps({"j": junk, "t": tricky})}},
+            "spec": {"taints": [{"key": tricky, "value": "\\" * pad, "effect": '"' * run}]},
+            "status": {"capacity": {"amd.com/gpu": "8"}, "conditions": [{"type": "Ready", "status": "True"}]}}
+    body = json.dumps({"items": [node]}, ensure_ascii=ascii_only).encode()
+    assert assert_same(body) == "native"
+    # the same string ending exactly at the end of the buffer is unterminated, never read past
+    with pytest.raises(ext.FallbackError):
+        native_scan(b'{"items": [{"metadata": {"name": "' + b"a" * pad + b"\\\\" * run + b'\\"')
+
+
 def test_string_cache_overflow_escapes_and_long_values():
     """Pass 2 shares repeated short label/taint strings through a per-page cache: a page with more
     distinct strings than the cache holds, escaped and long (uncached) strings, and repeats of each,
