@@ -25,9 +25,32 @@
 #include <string>
 #include <vector>
 
+#include <unistd.h>
+
 namespace {
 
 thread_local std::string g_err;
+
+// RCCL prints its version banner on stdout during communicator init; callers (mi355x-diag, the
+// fabric CLI) write JSON there, so the banner is sent to stderr instead while the scope lives.
+struct StdoutToStderr {
+  int saved = -1;
+  StdoutToStderr() {
+    fflush(stdout);
+    saved = dup(STDOUT_FILENO);
+    if (saved >= 0 && dup2(STDERR_FILENO, STDOUT_FILENO) < 0) {
+      close(saved);
+      saved = -1;
+    }
+  }
+  ~StdoutToStderr() {
+    fflush(stdout);
+    if (saved >= 0) {
+      dup2(saved, STDOUT_FILENO);
+      close(saved);
+    }
+  }
+};
 
 #define HIP_OK(expr)                                                          \
   do {                                                                        \
@@ -172,7 +195,11 @@ void* fabric_open(const int* devices, int n) {
       return fail();
     }
   }
-  ncclResult_t r = ncclCommInitAll(comms.data(), n, devices);
+  ncclResult_t r;
+  {
+    StdoutToStderr quiet;
+    r = ncclCommInitAll(comms.data(), n, devices);
+  }
   if (r != ncclSuccess) {
     g_err = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
     return fail();

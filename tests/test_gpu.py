@@ -234,6 +234,17 @@ def test_rccl_in_process_fabric_suite(dev):
     assert res["rccl"] != "unknown"
 
 
+def test_fabric_cli_stdout_is_pure_json(repo):
+    """RCCL prints a version banner during communicator init; the CLI's stdout must still parse as one
+    JSON document (the banner goes to stderr)."""
+    p = subprocess.run([sys.executable, "-m", "k8s_gpu_node_checker_amd.ops.fabric", "--device", "0",
+                        "--sizes", "1M", "--iters", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=repo)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout)
+    assert d["pass"] and d["rows"]
+
+
 def test_agent_diagnostics_threads_per_device(dev):
     from k8s_gpu_node_checker_amd.agent.agent import Agent
     from k8s_gpu_node_checker_amd.ops import diag
