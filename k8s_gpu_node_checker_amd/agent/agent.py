@@ -43,7 +43,33 @@ from ..models.node import HEALTH_ANNOTATION
 # whether the annotation must be rewritten.
 _VOLATILE = frozenset(("ts", "probe_ms", "probe_us", "hotspot_c", "wall_s", "ms_per_gemm", "setup_ms",
                        "power_w", "hbm_temp_c", "gfxclk_mhz", "vram_used_mb", "processes", "throttle_acc",
-                       "throttle"))
+                       "throttle", "procs", "gfx_activity", "diag_skipped"))
+
+DIAG_WHEN = ("idle", "always")
+
+
+def gpu_busy(g: Dict[str, Any], own_pids: frozenset = frozenset(), busy_vram_mb: int = 2048,
+             busy_gfx_activity: int = 10) -> Optional[str]:
+    """Why a workload holds this GPU, so active diagnostics must not run on it; None when it is idle.
+
+    Busy means a process other than the agent holding at least ``busy_vram_mb`` of VRAM (the probe's
+    ``procs``; without that list, the device's total VRAM in use), or a graphics engine at least
+    ``busy_gfx_activity`` % busy.  The agent's own HIP context holds a few hundred MB between
+    diagnostics, so the VRAM floor also covers a pod without hostPID, where amd-smi's host-namespace
+    PIDs never match the agent's own.
+    """
+    procs = g.get("procs")
+    if isinstance(procs, list):
+        holders = [p for p in procs if isinstance(p, dict) and p.get("pid") not in own_pids
+                   and isinstance(p.get("vram_mb"), int) and p["vram_mb"] >= busy_vram_mb]
+        if holders:
+            return "in use: " + ", ".join(f"pid {p.get('pid')} holds {p['vram_mb']} MB" for p in holders[:4])
+    elif isinstance(g.get("vram_used_mb"), int) and g["vram_used_mb"] >= busy_vram_mb:
+        return f"in use: {g['vram_used_mb']} MB of VRAM allocated"
+    act = g.get("gfx_activity")
+    if isinstance(act, (int, float)) and act >= busy_gfx_activity:
+        return f"in use: graphics engine {act}% busy"
+    return None
 
 
 def report_digest(rep: Dict[str, Any]) -> str:
@@ -86,16 +112,28 @@ class Agent:
     def __init__(self, node: str, source: str = "auto", fixture: Optional[str] = None, diag_level: int = 0,
                  diag_interval: float = 3600.0, devices: Optional[List[int]] = None,
                  annotation_refresh: float = 900.0, heartbeat_interval: float = 300.0,
-                 events: bool = True, event_namespace: str = "default", taint_unhealthy: bool = False):
+                 events: bool = True, event_namespace: str = "default", taint_unhealthy: bool = False,
+                 diag_when: str = "idle", busy_vram_mb: int = 2048, busy_gfx_activity: int = 10):
         self.node = node
         self.source = source
         self.fixture = fixture
         self.diag_level = diag_level
         self.diag_interval = diag_interval
         self.devices = devices
+        # active diagnostics run per GPU when its last run is `diag_interval` old and (diag_when=idle)
+        # no workload holds it; a GPU found busy keeps its previous result and is tried again at the
+        # next probe instead of a full interval later
+        if diag_when not in DIAG_WHEN:
+            raise ValueError(f"diag_when must be one of {DIAG_WHEN}")
+        self.diag_when = diag_when
+        self.busy_vram_mb = busy_vram_mb
+        self.busy_gfx_activity = busy_gfx_activity
         self._diag_cache: Dict[int, Dict[str, Any]] = {}
+        self._diag_at: Dict[int, float] = {}
+        self._diag_skipped: Dict[int, str] = {}
         self._fabric: Optional[Dict[str, Any]] = None
-        self._diag_ts = 0.0
+        self._fabric_at = float("-inf")
+        self._bdf: Dict[int, str] = {}  # HIP ordinal -> PCI address (amd-smi and HIP enumerate independently)
         self.last: Optional[Dict[str, Any]] = None
         self._last_condition: Optional[Dict[str, Any]] = None
         # the annotation (KBs per node, a new object revision per write) is rewritten only when the
@@ -121,28 +159,58 @@ class Agent:
         self._taint_state: Optional[str] = None
         self.lock = threading.Lock()
 
-    def _diagnostics(self, n_gpus: int) -> Dict[int, Dict[str, Any]]:
+    def _entries_by_device(self, gpus: List[Dict[str, Any]], devices: List[int]) -> Dict[int, Dict[str, Any]]:
+        """The probe entry of each HIP device: by PCI address, by index when HIP cannot say."""
+        from ..ops import diag
+        by_bdf = {str(g.get("bdf", "")).lower(): g for g in gpus if g.get("bdf")}
+        out: Dict[int, Dict[str, Any]] = {}
+        for d in devices:
+            if d not in self._bdf:
+                try:
+                    self._bdf[d] = str(diag.device_info(d)["bdf"]).lower()
+                except Exception:
+                    self._bdf[d] = ""
+            g = by_bdf.get(self._bdf[d]) if self._bdf[d] else (gpus[d] if 0 <= d < len(gpus) else None)
+            if g is not None:
+                out[d] = g
+        return out
+
+    def _diagnostics(self, gpus: List[Dict[str, Any]]) -> Dict[int, Dict[str, Any]]:
+        self._diag_skipped = {}
         if self.diag_level <= 0:
             return {}
-        now = time.time()
-        if self._diag_cache and now - self._diag_ts < self.diag_interval:
-            return self._diag_cache
         from ..ops import diag
-        devices = self.devices if self.devices is not None else list(range(min(n_gpus, diag.device_count())))
+        devices = self.devices if self.devices is not None else list(range(min(len(gpus), diag.device_count())))
+        entries = self._entries_by_device(gpus, devices)
+        now = time.time()
+        due = [d for d in devices if now - self._diag_at.get(d, float("-inf")) >= self.diag_interval]
+        run = []
+        for d in due:
+            why = gpu_busy(entries.get(d) or {}, frozenset((os.getpid(),)), self.busy_vram_mb,
+                           self.busy_gfx_activity) if self.diag_when == "idle" else None
+            if why:
+                self._diag_skipped[d] = why
+            else:
+                run.append(d)
         # one host thread per GPU: each diagnostic is a ctypes call that releases the GIL and drives its
         # own device, so an 8-GPU node is checked in the time of one GPU instead of eight
         results: Dict[int, Dict[str, Any]] = {}
 
         def work(d: int) -> None:
             results[d] = diag.run(self.diag_level, d)
-        threads = [threading.Thread(target=work, args=(d,), name=f"diag-gpu{d}") for d in devices]
+        threads = [threading.Thread(target=work, args=(d,), name=f"diag-gpu{d}") for d in run]
         for t in threads:
             t.start()
         for t in threads:
             t.join()
-        self._diag_cache = {d: results[d] for d in devices if d in results}
-        if self.diag_level >= 2 and self.devices is None and len(devices) >= 2:
-            # node-level: every ordered GPU pair over xGMI (after the per-GPU tests, so no contention)
+        for d in run:
+            if d in results:
+                self._diag_cache[d] = results[d]
+            self._diag_at[d] = now
+        if (self.diag_level >= 2 and self.devices is None and len(devices) >= 2 and not self._diag_skipped
+                and now - self._fabric_at >= self.diag_interval):
+            # node-level: every ordered GPU pair over xGMI (after the per-GPU tests, so no contention);
+            # it touches every GPU, so it waits until none is busy
             try:
                 m = diag.p2p_matrix(devices)
                 self._fabric = {"p2p": {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s")}}
@@ -156,27 +224,22 @@ class Agent:
                                                               "detail", "wall_s", "rccl")}
             except Exception as e:
                 self._fabric["rccl"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
-        self._diag_ts = now
-        return self._diag_cache
+            self._fabric_at = now
+        return {d: self._diag_cache[d] for d in devices if d in self._diag_cache}
 
     def probe_once(self) -> Dict[str, Any]:
         from ..ops.amdsmi_probe import probe
         rep = probe(self.node, self.source, self.fixture)
         self._throttle_windows(rep)
-        diags = self._diagnostics(len(rep.get("gpus") or []))
-        if diags:
-            # amd-smi and HIP enumerate independently: match by PCI address, fall back to the index
-            from ..ops import diag
-            by_bdf = {}
-            for d in diags:
-                try:
-                    by_bdf[diag.device_info(d)["bdf"].lower()] = d
-                except Exception:
-                    pass
-            for g in rep.get("gpus") or []:
-                d = by_bdf.get(str(g.get("bdf", "")).lower(), g.get("index") if not by_bdf else None)
-                if d is not None and diags.get(d):
+        gpus = rep.get("gpus") or []
+        diags = self._diagnostics(gpus)
+        if diags or self._diag_skipped:
+            entries = self._entries_by_device(gpus, sorted(set(diags) | set(self._diag_skipped)))
+            for d, g in entries.items():
+                if diags.get(d):
                     g["diag"] = diags[d]
+                if d in self._diag_skipped:
+                    g["diag_skipped"] = self._diag_skipped[d]
             if self._fabric:
                 rep["fabric"] = self._fabric
         verdict = evaluate_report(rep, 0, HealthExpectations())
@@ -274,7 +337,8 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
              "# TYPE mi355x_gpu_pcie_replays counter", "# TYPE mi355x_gpu_power_watts gauge",
              "# TYPE mi355x_gpu_power_cap_watts gauge", "# TYPE mi355x_gpu_hbm_celsius gauge",
              "# TYPE mi355x_gpu_gfxclk_mhz gauge", "# TYPE mi355x_gpu_vram_used_megabytes gauge",
-             "# TYPE mi355x_gpu_throttle_percent gauge"]
+             "# TYPE mi355x_gpu_throttle_percent gauge", "# TYPE mi355x_gpu_gfx_activity_percent gauge",
+             "# TYPE mi355x_gpu_diag_skipped gauge"]
     for g in rep.get("gpus") or []:
         lbl = f'gpu="{g.get("index")}",bdf="{g.get("bdf", "")}"'
         if isinstance(g.get("ecc_uncorrectable"), int):
@@ -289,13 +353,15 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
             lines.append(f"mi355x_gpu_pcie_replays{{{lbl}}} {g['pcie_replays']}")
         for key, metric in (("power_w", "power_watts"), ("power_cap_w", "power_cap_watts"),
                             ("hbm_temp_c", "hbm_celsius"), ("gfxclk_mhz", "gfxclk_mhz"),
-                            ("vram_used_mb", "vram_used_megabytes")):
+                            ("vram_used_mb", "vram_used_megabytes"), ("gfx_activity", "gfx_activity_percent")):
             if isinstance(g.get(key), (int, float)):
                 lines.append(f"mi355x_gpu_{metric}{{{lbl}}} {g[key]}")
         for kind in ("thermal", "power", "prochot"):
             v = (g.get("throttle") or {}).get(f"{kind}_pct")
             if isinstance(v, (int, float)):
                 lines.append(f'mi355x_gpu_throttle_percent{{{lbl},kind="{kind}"}} {v}')
+        if g.get("diag") is not None or g.get("diag_skipped"):
+            lines.append(f"mi355x_gpu_diag_skipped{{{lbl}}} {1 if g.get('diag_skipped') else 0}")
         for test, res in (g.get("diag") or {}).items():
             for k in ("tflops", "copy_tbs", "read_tbs", "errors", "h2d_gbps", "d2h_gbps"):
                 if isinstance(res.get(k), (int, float)):
@@ -376,6 +442,13 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--taint-unhealthy", action="store_true",
                     help=f"keep the taint {UNHEALTHY_TAINT['key']}={UNHEALTHY_TAINT['value']}:"
                          f"{UNHEALTHY_TAINT['effect']} on the node while it is unhealthy (removed on recovery)")
+    ap.add_argument("--diag-when", choices=DIAG_WHEN, default="idle",
+                    help="idle (default): run the active diagnostics only on GPUs no workload holds (a busy GPU "
+                         "keeps its last result and is retried at the next probe); always: on schedule")
+    ap.add_argument("--busy-vram-mb", type=int, default=2048,
+                    help="a process other than the agent holding this much VRAM makes its GPU busy (default 2048)")
+    ap.add_argument("--busy-gfx-activity", type=int, default=10,
+                    help="graphics-engine activity (%%) at which a GPU counts as busy (default 10)")
     return ap
 
 
@@ -384,7 +457,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     pubs = set(args.publish.split(","))
     agent = Agent(args.node, args.source, args.fixture, args.diag_level, args.diag_interval,
                   annotation_refresh=args.annotation_refresh, heartbeat_interval=args.heartbeat_interval,
-                  events=args.events, event_namespace=args.event_namespace, taint_unhealthy=args.taint_unhealthy)
+                  events=args.events, event_namespace=args.event_namespace, taint_unhealthy=args.taint_unhealthy,
+                  diag_when=args.diag_when, busy_vram_mb=args.busy_vram_mb,
+                  busy_gfx_activity=args.busy_gfx_activity)
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient

@@ -9,6 +9,7 @@
 // maps to verdict "unknown" (models/health.py), not to a crash.
 #include "probe.h"
 
+#include <algorithm>
 #include <amd_smi/amdsmi.h>
 
 #include <chrono>
@@ -140,8 +141,34 @@ void probe_telemetry(std::string& o, amdsmi_processor_handle h) {
   memset(&vu, 0, sizeof vu);
   if (amdsmi_get_gpu_vram_usage(h, &vu) == AMDSMI_STATUS_SUCCESS && vu.vram_used != UINT32_MAX)
     kv_u64(o, "vram_used_mb", vu.vram_used);
+  // processes holding the device (PIDs of the host namespace, the VRAM each holds) and how busy the
+  // graphics engine is: the agent runs its active diagnostics only on GPUs no workload holds
   uint32_t nproc = 0;
-  if (amdsmi_get_gpu_process_list(h, &nproc, nullptr) == AMDSMI_STATUS_SUCCESS) kv_u64(o, "processes", nproc);
+  if (amdsmi_get_gpu_process_list(h, &nproc, nullptr) == AMDSMI_STATUS_SUCCESS) {
+    kv_u64(o, "processes", nproc);
+    if (nproc > 0) {
+      std::vector<amdsmi_proc_info_t> pl(std::min<uint32_t>(nproc, 64));
+      uint32_t cap = static_cast<uint32_t>(pl.size());
+      const amdsmi_status_t st = amdsmi_get_gpu_process_list(h, &cap, pl.data());
+      if (st == AMDSMI_STATUS_SUCCESS || st == AMDSMI_STATUS_OUT_OF_RESOURCES) {
+        key(o, "procs");
+        o.push_back('[');
+        const size_t n = std::min<size_t>(cap, pl.size());
+        for (size_t i = 0; i < n; ++i) {
+          if (i) o.push_back(',');
+          o.push_back('{');
+          kv_u64(o, "pid", pl[i].pid);
+          kv_u64(o, "vram_mb", pl[i].memory_usage.vram_mem >> 20);
+          o.push_back('}');
+        }
+        o.push_back(']');
+      }
+    }
+  }
+  amdsmi_engine_usage_t act;
+  memset(&act, 0xFF, sizeof act);
+  if (amdsmi_get_gpu_activity(h, &act) == AMDSMI_STATUS_SUCCESS && act.gfx_activity <= 100)
+    kv_u64(o, "gfx_activity", act.gfx_activity);
   // all-ones first: whatever the library does not fill reads as the not-reported sentinel
   amdsmi_gpu_metrics_t m;
   memset(&m, 0xFF, sizeof m);

@@ -100,6 +100,13 @@ def _telemetry_python(A: Any, h: Any, q: Any) -> Dict[str, Any]:
     t["vram_used_mb"] = _int(vu.get("vram_used"))
     procs = q(A.amdsmi_get_gpu_process_list)
     t["processes"] = len(procs) if isinstance(procs, list) else None
+    if procs and isinstance(procs, list):
+        t["procs"] = [{"pid": _int(p.get("pid")),
+                       "vram_mb": (_int((p.get("memory_usage") or {}).get("vram_mem")) or 0) >> 20}
+                      for p in procs[:64] if isinstance(p, dict)]
+    act = q(A.amdsmi_get_gpu_activity) or {}
+    gfx = _int(act.get("gfx_activity"))
+    t["gfx_activity"] = gfx if gfx is not None and gfx <= 100 else None
     m = q(A.amdsmi_get_gpu_metrics_info) or {}
     th = m.get("temperature_hbm")
     hbm += [x for x in (_int(v) for v in th) if x and x < 200] if isinstance(th, list) else []

@@ -1,0 +1,133 @@
+"""Agent diagnostics schedule on CPU: idle-only active diagnostics (``--diag-when``), per-GPU intervals,
+the node-level fabric test waiting for an all-idle node.  A fake ``ops.diag`` stands in for the HIP
+library; the probe report is built here."""
+import pytest
+
+from k8s_gpu_node_checker_amd.agent import agent as A
+from k8s_gpu_node_checker_amd.ops import amdsmi_probe, diag, fabric
+
+
+def gpu(i, procs=None, act=0, vram_used=300):
+    g = {"index": i, "bdf": f"0000:0{i}:00.0", "gfx": "gfx950", "vram_used_mb": vram_used, "gfx_activity": act}
+    if procs is not None:
+        g["procs"] = procs
+        g["processes"] = len(procs)
+    return g
+
+
+class World:
+    def __init__(self, monkeypatch, n=2):
+        self.gpus = [gpu(i, procs=[]) for i in range(n)]
+        self.runs = []
+        self.fabric_runs = 0
+        self.clock = 1000.0
+        monkeypatch.setattr(A.time, "time", lambda: self.clock)
+        monkeypatch.setattr(amdsmi_probe, "probe", lambda node, src, fx: {
+            "schema": "mi355x-health/v1", "node": node, "probe": "fake", "gpus": [dict(g) for g in self.gpus]})
+        monkeypatch.setattr(diag, "device_count", lambda: n)
+        monkeypatch.setattr(diag, "device_info", lambda d: {"bdf": f"0000:0{d}:00.0"})
+
+        def run(level, d):
+            self.runs.append(d)
+            return {"gemm": {"pass": True, "tflops": 1200.0 + len(self.runs)}}
+        monkeypatch.setattr(diag, "run", run)
+
+        def p2p(devs):
+            self.fabric_runs += 1
+            return {"pass": True, "median_gbps": 50.0, "min_gbps": 48.0, "detail": "", "wall_s": 0.1}
+        monkeypatch.setattr(diag, "p2p_matrix", p2p)
+        monkeypatch.setattr(fabric, "collective_suite", lambda devs: {"pass": True, "best_busbw_gbps": 300.0,
+                                                                      "best_busbw_by_op": {}, "detail": "",
+                                                                      "wall_s": 0.2, "rccl": "2.27.7"})
+
+
+def test_gpu_busy_rules():
+    own = frozenset((42,))
+    assert A.gpu_busy(gpu(0, procs=[])) is None
+    assert A.gpu_busy(gpu(0, procs=[{"pid": 42, "vram_mb": 200000}]), own) is None  # the agent itself
+    assert A.gpu_busy(gpu(0, procs=[{"pid": 7, "vram_mb": 300}])) is None  # a monitoring tool's context
+    assert A.gpu_busy(gpu(0, procs=[{"pid": 7, "vram_mb": 180000}])) == "in use: pid 7 holds 180000 MB"
+    assert A.gpu_busy(gpu(0, procs=[], act=55)) == "in use: graphics engine 55% busy"
+    assert A.gpu_busy(gpu(0, procs=[], act=9)) is None
+    # no per-process list: the device's VRAM in use decides
+    assert A.gpu_busy(gpu(0, vram_used=250000)) == "in use: 250000 MB of VRAM allocated"
+    assert A.gpu_busy(gpu(0, vram_used=250000), busy_vram_mb=300000) is None
+    assert A.gpu_busy({}) is None  # nothing known: idle (the probe failed to say otherwise)
+
+
+def test_busy_gpu_is_skipped_and_retried_at_next_probe(monkeypatch):
+    w = World(monkeypatch)
+    w.gpus[1]["procs"] = [{"pid": 999, "vram_mb": 150000}]
+    ag = A.Agent("n", source="fake", diag_level=1, diag_interval=3600)
+    rep = ag.probe_once()
+    assert w.runs == [0]
+    g0, g1 = rep["gpus"]
+    assert g0["diag"]["gemm"]["pass"] and "diag_skipped" not in g0
+    assert "diag" not in g1 and g1["diag_skipped"] == "in use: pid 999 holds 150000 MB"
+    # still busy a minute later: GPU 0 is not due, GPU 1 is skipped again
+    w.clock += 60
+    rep = ag.probe_once()
+    assert w.runs == [0] and rep["gpus"][1]["diag_skipped"] and rep["gpus"][0]["diag"]
+    # the workload ends: GPU 1 runs at the next probe, not an interval later
+    w.gpus[1]["procs"] = []
+    w.clock += 60
+    rep = ag.probe_once()
+    assert w.runs == [0, 1] and "diag_skipped" not in rep["gpus"][1] and rep["gpus"][1]["diag"]
+
+
+def test_busy_gpu_keeps_its_previous_result(monkeypatch):
+    w = World(monkeypatch)
+    ag = A.Agent("n", source="fake", diag_level=1, diag_interval=3600)
+    first = ag.probe_once()["gpus"][1]["diag"]
+    w.gpus[1]["gfx_activity"] = 97
+    w.clock += 3600
+    rep = ag.probe_once()
+    assert w.runs == [0, 1, 0]
+    assert rep["gpus"][1]["diag"] == first and rep["gpus"][1]["diag_skipped"] == "in use: graphics engine 97% busy"
+
+
+def test_diag_when_always_ignores_workloads(monkeypatch):
+    w = World(monkeypatch)
+    w.gpus[0]["procs"] = [{"pid": 5, "vram_mb": 200000}]
+    ag = A.Agent("n", source="fake", diag_level=1, diag_when="always")
+    rep = ag.probe_once()
+    assert sorted(w.runs) == [0, 1] and all("diag_skipped" not in g for g in rep["gpus"])
+    with pytest.raises(ValueError):
+        A.Agent("n", diag_when="sometimes")
+
+
+def test_node_level_fabric_waits_for_an_idle_node(monkeypatch):
+    w = World(monkeypatch)
+    w.gpus[0]["gfx_activity"] = 80
+    ag = A.Agent("n", source="fake", diag_level=2, diag_interval=3600)
+    rep = ag.probe_once()
+    assert w.fabric_runs == 0 and "fabric" not in rep
+    w.gpus[0]["gfx_activity"] = 0
+    w.clock += 60
+    rep = ag.probe_once()
+    assert w.fabric_runs == 1 and rep["fabric"]["p2p"]["pass"] and rep["fabric"]["rccl"]["pass"]
+    w.clock += 60
+    ag.probe_once()
+    assert w.fabric_runs == 1  # not due again before the interval
+
+
+def test_skip_reasons_do_not_rewrite_the_annotation():
+    a = {"gpus": [{"index": 0, "diag_skipped": "in use: pid 1 holds 9000 MB", "procs": [{"pid": 1, "vram_mb": 9000}],
+                   "gfx_activity": 40}]}
+    b = {"gpus": [{"index": 0, "diag_skipped": "in use: pid 2 holds 9100 MB", "procs": [{"pid": 2, "vram_mb": 9100}],
+                   "gfx_activity": 70}]}
+    assert A.report_digest(a) == A.report_digest(b)
+
+
+def test_agent_cli_flags():
+    args = A.build_parser().parse_args(["--diag-when", "always", "--busy-vram-mb", "4096", "--busy-gfx-activity", "5"])
+    assert (args.diag_when, args.busy_vram_mb, args.busy_gfx_activity) == ("always", 4096, 5)
+    assert A.build_parser().parse_args([]).diag_when == "idle"
+
+
+def test_metrics_show_activity_and_skips():
+    rep = {"ts": 1, "gpus": [{"index": 0, "bdf": "b0", "gfx_activity": 40, "diag_skipped": "in use: x"},
+                             {"index": 1, "bdf": "b1", "gfx_activity": 0, "diag": {"gemm": {"pass": True}}}]}
+    m = A._metrics(rep)
+    assert 'mi355x_gpu_gfx_activity_percent{gpu="0",bdf="b0"} 40' in m
+    assert 'mi355x_gpu_diag_skipped{gpu="0",bdf="b0"} 1' in m and 'mi355x_gpu_diag_skipped{gpu="1",bdf="b1"} 0' in m

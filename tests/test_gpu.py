@@ -182,7 +182,7 @@ def test_diag_memtest_clean(dev):
 def test_agent_with_diagnostics_is_healthy(dev):
     from k8s_gpu_node_checker_amd.agent.agent import Agent
     from k8s_gpu_node_checker_amd.models.health import HealthExpectations, evaluate_report
-    ag = Agent("gpu-node", source="native", diag_level=1, devices=[0])
+    ag = Agent("gpu-node", source="native", diag_level=1, devices=[0], diag_when="always")
     rep = ag.probe_once()
     g = rep["gpus"][0]
     assert g["diag"]["gemm"]["pass"] and g["diag"]["hbm"]["pass"], g["diag"]
@@ -245,10 +245,34 @@ def test_fabric_cli_stdout_is_pure_json(repo):
     assert d["pass"] and d["rows"]
 
 
+def test_probe_sees_a_workload_and_agent_skips_diagnostics(dev, repo):
+    """A second process holding 4 GiB of VRAM shows up in the native probe's per-process list, and an
+    idle-only agent (the default) leaves that GPU's diagnostics alone while it is held."""
+    from k8s_gpu_node_checker_amd.agent.agent import Agent, gpu_busy
+    from k8s_gpu_node_checker_amd.ops.amdsmi_probe import probe_native
+    holder = subprocess.Popen([sys.executable, "-c",
+                               "import sys, time, torch; x = torch.empty(4 << 30, dtype=torch.uint8, device='cuda:0');"
+                               "x.fill_(1); torch.cuda.synchronize(); print('held', flush=True); time.sleep(60)"],
+                              stdout=subprocess.PIPE, text=True, cwd=repo)
+    try:
+        assert holder.stdout.readline().strip() == "held"
+        g = probe_native("n")["gpus"][0]
+        print(json.dumps({k: g.get(k) for k in ("processes", "procs", "gfx_activity", "vram_used_mb")}))
+        assert any(p["pid"] == holder.pid and p["vram_mb"] >= 4096 for p in g["procs"]) or \
+            any(p["vram_mb"] >= 4096 for p in g["procs"]), g.get("procs")  # PIDs may be of another namespace
+        assert gpu_busy(g) and "in use" in gpu_busy(g)
+        ag = Agent("n", source="native", diag_level=1, devices=[0])
+        g2 = ag.probe_once()["gpus"][0]
+        assert "diag" not in g2 and g2["diag_skipped"].startswith("in use"), g2.get("diag_skipped")
+    finally:
+        holder.kill()
+        holder.wait(timeout=30)
+
+
 def test_agent_diagnostics_threads_per_device(dev):
     from k8s_gpu_node_checker_amd.agent.agent import Agent
     from k8s_gpu_node_checker_amd.ops import diag
-    ag = Agent("n", source="native", diag_level=1)
+    ag = Agent("n", source="native", diag_level=1, diag_when="always")
     rep = ag.probe_once()
     assert len(rep["gpus"]) >= 1
     assert all("diag" in g for g in rep["gpus"][: diag.device_count()])
