@@ -1235,60 +1235,66 @@ int append_all(PyObject* result, PyObject* attr, PyObject* items) {
   return rc;
 }
 
-PyObject* scan_nodelist(PyObject*, PyObject* args) {
-  Py_buffer view;
-  PyObject *result, *keys, *extras_cls;
-  int use_alloc, want_extras;
-  const char* health_key_c;
-  const char* health_cond_c = "";
-  int annot_mode = 2;
-  if (!PyArg_ParseTuple(args, "y*OO!ppsO|si", &view, &result, &PyTuple_Type, &keys, &use_alloc, &want_extras,
-                        &health_key_c, &extras_cls, &health_cond_c, &annot_mode))
-    return nullptr;
+// Page-scan state between pass 1 (no GIL, any thread) and pass 2 (GIL): the page's buffer stays
+// exported (RawStr pointers point into it) until the state is released.
+struct PageScan {
+  Py_buffer view{};
+  bool have_view = false;
   std::vector<std::string> kstr;
-  std::vector<PyObject*> pykeys;
+  std::string health_key, health_cond;
+  Pass1Ctx ctx{0, nullptr, nullptr, nullptr, {}};
+  Pass1Out p1;
+  const char* why = nullptr;
+  ~PageScan() {
+    if (have_view) PyBuffer_Release(&view);
+  }
+};
+
+// Keys as UTF-8 strings (kstr) plus borrowed references (pykeys); false with a Python error set.
+bool read_keys(PyObject* keys, std::vector<std::string>& kstr, std::vector<PyObject*>* pykeys) {
   for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(keys); ++i) {
     PyObject* k = PyTuple_GET_ITEM(keys, i);
     Py_ssize_t n;
     const char* s = PyUnicode_AsUTF8AndSize(k, &n);
-    if (!s) {
-      PyBuffer_Release(&view);
-      return nullptr;
-    }
+    if (!s) return false;
     kstr.emplace_back(s, static_cast<size_t>(n));
-    pykeys.push_back(k);
+    if (pykeys) pykeys->push_back(k);
   }
-  std::string health_key(health_key_c), health_cond(health_cond_c);
-  Pass1Ctx ctx{kstr.size(), &kstr, &health_key, &health_cond, {}};
-  Pass1Out p1;
-  const char* why = nullptr;
-  const char* b = static_cast<const char*>(view.buf);
-  // pass 1 without the GIL: the buffer is held by `view` (a bytearray cannot be resized while exported)
-  Py_BEGIN_ALLOW_THREADS
+  return true;
+}
+
+// Pass 1 over an exported page; the caller holds (or has released) the GIL as it sees fit.
+void run_pass1(PageScan& ps) {
+  ps.ctx = Pass1Ctx{ps.kstr.size(), &ps.kstr, &ps.health_key, &ps.health_cond, {}};
+  const char* b = static_cast<const char*>(ps.view.buf);
   try {
-    pass1(b, b + view.len, ctx, p1);
+    pass1(b, b + ps.view.len, ps.ctx, ps.p1);
   } catch (const Fallback& f) {
-    why = f.why;
+    ps.why = f.why;
   } catch (const std::bad_alloc&) {
-    why = "out of memory";
+    ps.why = "out of memory";
   }
-  Py_END_ALLOW_THREADS
+}
+
+// Pass 2 + commit into `result`; returns (continue, items) or nullptr with an error set.
+PyObject* finish_scan(PageScan& ps, PyObject* result, const std::vector<PyObject*>& pykeys, int use_alloc,
+                      int want_extras, PyObject* extras_cls, int annot_mode) {
+  const char* why = ps.why;
   PageOut out;
   if (!why) {
     try {
       if (!out.gpu_nodes.o || !out.ready_nodes.o || !out.extras.o) throw Fallback{"oom"};
-      std::string& scratch = ctx.scratch;
-      StrCache cache(p1.items.size());
+      std::string& scratch = ps.ctx.scratch;
+      StrCache cache(ps.p1.items.size());
       ExtrasMaker maker(extras_cls);
-      for (const NodeRec& r : p1.items)
+      for (const NodeRec& r : ps.p1.items)
         emit_node(r, pykeys, use_alloc, want_extras, maker, annot_mode, out, cache, scratch);
-      out.items = static_cast<Py_ssize_t>(p1.items.size());
-      if (p1.have_cont) out.cont.reset(make_str(p1.cont, scratch));
+      out.items = static_cast<Py_ssize_t>(ps.p1.items.size());
+      if (ps.p1.have_cont) out.cont.reset(make_str(ps.p1.cont, scratch));
     } catch (const Fallback& f) {
       why = f.why;
     }
   }
-  PyBuffer_Release(&view);
   if (why) {
     if (!PyErr_Occurred()) PyErr_SetString(g_fallback, why);
     return nullptr;
@@ -1310,6 +1316,81 @@ PyObject* scan_nodelist(PyObject*, PyObject* args) {
   if (rc < 0) return nullptr;
   PyObject* cont = out.cont.o ? out.cont.o : Py_None;
   return Py_BuildValue("(On)", cont, out.items);
+}
+
+PyObject* scan_nodelist(PyObject*, PyObject* args) {
+  PageScan ps;
+  PyObject *result, *keys, *extras_cls;
+  int use_alloc, want_extras;
+  const char* health_key_c;
+  const char* health_cond_c = "";
+  int annot_mode = 2;
+  if (!PyArg_ParseTuple(args, "y*OO!ppsO|si", &ps.view, &result, &PyTuple_Type, &keys, &use_alloc, &want_extras,
+                        &health_key_c, &extras_cls, &health_cond_c, &annot_mode))
+    return nullptr;
+  ps.have_view = true;
+  std::vector<PyObject*> pykeys;
+  if (!read_keys(keys, ps.kstr, &pykeys)) return nullptr;
+  ps.health_key = health_key_c;
+  ps.health_cond = health_cond_c;
+  // pass 1 without the GIL: the buffer is held by `view` (a bytearray cannot be resized while exported)
+  Py_BEGIN_ALLOW_THREADS
+  run_pass1(ps);
+  Py_END_ALLOW_THREADS
+  return finish_scan(ps, result, pykeys, use_alloc, want_extras, extras_cls, annot_mode);
+}
+
+const char* const kPageScanCapsule = "k8s_gpu_node_checker_amd._fastpath.PageScan";
+
+void page_scan_capsule_free(PyObject* cap) {
+  delete static_cast<PageScan*>(PyCapsule_GetPointer(cap, kPageScanCapsule));
+}
+
+// Pass 1 only, GIL released: the pipelined page reader runs it on its own thread as soon as a page
+// has arrived, so the main thread's pass 2 of the previous page and this page's pass 1 overlap.
+// A page pass 1 cannot model is not an error here; scan_prescanned raises FallbackError for it.
+PyObject* prescan_nodelist(PyObject*, PyObject* args) {
+  auto* ps = new PageScan();
+  PyObject* keys;
+  const char* health_key_c;
+  const char* health_cond_c;
+  if (!PyArg_ParseTuple(args, "y*O!ss", &ps->view, &PyTuple_Type, &keys, &health_key_c, &health_cond_c)) {
+    delete ps;
+    return nullptr;
+  }
+  ps->have_view = true;
+  if (!read_keys(keys, ps->kstr, nullptr)) {
+    delete ps;
+    return nullptr;
+  }
+  ps->health_key = health_key_c;
+  ps->health_cond = health_cond_c;
+  Py_BEGIN_ALLOW_THREADS
+  run_pass1(*ps);
+  Py_END_ALLOW_THREADS
+  PyObject* cap = PyCapsule_New(ps, kPageScanCapsule, page_scan_capsule_free);
+  if (!cap) delete ps;
+  return cap;
+}
+
+// Pass 2 of a prescanned page into `result`; keys must be the ones prescan_nodelist was given.
+PyObject* scan_prescanned(PyObject*, PyObject* args) {
+  PyObject *cap, *result, *keys, *extras_cls;
+  int use_alloc, want_extras;
+  int annot_mode = 2;
+  if (!PyArg_ParseTuple(args, "OOO!ppO|i", &cap, &result, &PyTuple_Type, &keys, &use_alloc, &want_extras,
+                        &extras_cls, &annot_mode))
+    return nullptr;
+  auto* ps = static_cast<PageScan*>(PyCapsule_GetPointer(cap, kPageScanCapsule));
+  if (!ps) return nullptr;
+  std::vector<std::string> kstr;
+  std::vector<PyObject*> pykeys;
+  if (!read_keys(keys, kstr, &pykeys)) return nullptr;
+  if (kstr != ps->kstr) {
+    PyErr_SetString(PyExc_ValueError, "keys differ from the prescan's");
+    return nullptr;
+  }
+  return finish_scan(*ps, result, pykeys, use_alloc, want_extras, extras_cls, annot_mode);
 }
 
 // ---------------------------------------------------------------- emitting --
@@ -1442,6 +1523,8 @@ PyObject* dumps_indent2(PyObject*, PyObject* obj) {
 
 PyMethodDef methods[] = {
     {"scan_nodelist", scan_nodelist, METH_VARARGS, "Scan one NodeList page into a ScanResult."},
+    {"prescan_nodelist", prescan_nodelist, METH_VARARGS, "Pass 1 of a NodeList page (GIL released) -> capsule."},
+    {"scan_prescanned", scan_prescanned, METH_VARARGS, "Pass 2 of a prescanned page into a ScanResult."},
     {"dumps_indent2", dumps_indent2, METH_O, "json.dumps(obj, ensure_ascii=False, indent=2), natively."},
     {nullptr, nullptr, 0, nullptr}};
 

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import json
 import time
-from typing import Any, Callable, Dict, List, Optional, Sequence
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 from urllib.parse import quote
 
 from ..models.node import ScanResult
@@ -62,14 +62,18 @@ class _PageReader:
     """Receives one pipelined LIST page on its own thread.
 
     Socket reads release the GIL, and so does pass 1 of the native NodeList
-    scan, so page k+1 streams in while page k is being scanned.
+    scan, so page k+1 streams in while page k is being scanned.  Once the page
+    is in, this thread also runs page k+1's pass 1 (``fastpath.prescan``), which
+    leaves only pass 2 for the main thread.
     """
 
-    def __init__(self, conn: Connection, path: str):
+    def __init__(self, conn: Connection, path: str, keys: Optional[Sequence[str]] = None):
         import threading
         self.conn = conn
         self.path = path
+        self.keys = keys
         self.resp: Optional[Response] = None
+        self.pre: Any = None
         self.thread = threading.Thread(target=self._run, name="list-prefetch", daemon=True)
         self.thread.start()
 
@@ -78,6 +82,13 @@ class _PageReader:
             self.resp = self.conn.read_pending("GET", self.path)
         except Exception:  # transport trouble: the caller re-requests the page normally
             self.resp = None
+            return
+        if self.keys is not None and 200 <= self.resp.status < 300:
+            try:
+                from ..ops import fastpath
+                self.pre = fastpath.prescan(self.resp.body, self.keys)
+            except Exception:  # the main thread scans the page itself
+                self.pre = None
 
     def join(self) -> Optional[Response]:
         self.thread.join()
@@ -199,12 +210,13 @@ class KubeClient:
                 conn2.send_only("GET", nxt, self._headers())
             except HTTPError:
                 return
-            prefetched[nxt] = _PageReader(conn2, nxt)
+            prefetched[nxt] = _PageReader(conn2, nxt, keys)
 
         while True:
             path = self._list_path(limit, cont, label_selector, resource_version)
+            pre = None
             try:
-                resp = self._take_prefetched(prefetched, path)
+                resp, pre = self._take_prefetched(prefetched, path)
                 if resp is None:
                     resp = self.request("GET", path, peek=peek if limit > 0 else None)
             except ApiException as e:
@@ -216,7 +228,7 @@ class KubeClient:
                     return result
                 raise
             t0 = time.perf_counter()
-            cont, _ = fastpath.scan_page(resp.body, result, keys, gpu_source, want_extras, annotation_mode)
+            cont, _ = fastpath.scan_page(resp.body, result, keys, gpu_source, want_extras, annotation_mode, pre)
             if self.tracer is not None:
                 self.tracer.add("parse", time.perf_counter() - t0)
             if not cont or limit <= 0:
@@ -230,25 +242,27 @@ class KubeClient:
                                      server_hostname=self.cluster.tls_server_name, proxy_url=self.cluster.proxy_url)
         return self._conn2
 
-    def _take_prefetched(self, prefetched: Dict[str, "_PageReader"], path: str) -> Optional[Response]:
-        """Collect the already-sent request for ``path``; swap its connection in as the primary."""
+    def _take_prefetched(self, prefetched: Dict[str, "_PageReader"],
+                         path: str) -> Tuple[Optional[Response], Any]:
+        """Collect the already-sent request for ``path`` (and its pass-1 prescan); swap its
+        connection in as the primary."""
         reader = prefetched.pop(path, None)
         for other in prefetched.values():
             other.join()
         prefetched.clear()
         if reader is None:
-            return None
+            return None, None
         self.requests_made += 1
         conn2 = reader.conn
         resp = reader.join()
         if resp is None:
-            return None  # fall back to a normal (retried) request
+            return None, None  # fall back to a normal (retried) request
         # alternate: the connection that just answered becomes primary, the old primary the spare
         self._conn, self._conn2 = conn2, self._conn
         if 200 <= resp.status < 300:
-            return resp
+            return resp, reader.pre
         if resp.status in _RETRY_STATUS:
-            return None  # retried through request() with backoff
+            return None, None  # retried through request() with backoff
         raise ApiException(resp.status, resp.reason, resp.header_dict(), resp.text)
 
     def get_node(self, name: str) -> Dict[str, Any]:

@@ -42,22 +42,47 @@ def backend() -> str:
     return "native" if ext() is not None else "python"
 
 
+def prescan(body: bytes, keys: Sequence[str] = GPU_RESOURCE_KEYS) -> Optional[Tuple[tuple, Any]]:
+    """Pass 1 of the native scan (GIL released), for a thread that has just received ``body``.
+
+    Hand the result to :func:`scan_page` (``pre=``) with the same ``keys``; ``None`` when the
+    extension is missing.
+    """
+    mod = ext()
+    if mod is None:
+        return None
+    keys = tuple(keys)
+    return keys, mod.prescan_nodelist(body, keys, HEALTH_ANNOTATION, HEALTH_CONDITION)
+
+
 def scan_page(body: bytes, result: ScanResult, keys: Sequence[str] = GPU_RESOURCE_KEYS,
               gpu_source: str = "capacity", want_extras: bool = False,
-              annotation_mode: int = 2) -> Tuple[Optional[str], int]:
+              annotation_mode: int = 2, pre: Optional[Tuple[tuple, Any]] = None) -> Tuple[Optional[str], int]:
     """Scan one ``NodeList`` page into ``result``.
 
     Returns ``(continue_token, item_count)``.  Raises ``ValueError`` on a body
-    that is not a JSON object (mirrors ``json.loads`` errors).
+    that is not a JSON object (mirrors ``json.loads`` errors).  ``pre`` is
+    :func:`prescan` of the same ``body``: only pass 2 is left to do.
     """
     mod = ext()
     if mod is not None:
+        if pre is not None and pre[0] == tuple(keys):
+            try:
+                return mod.scan_prescanned(pre[1], result, pre[0], gpu_source == "allocatable", want_extras,
+                                           NodeExtras, annotation_mode)
+            except mod.FallbackError:
+                return _scan_python(body, result, keys, gpu_source, want_extras, annotation_mode)
         try:
             return mod.scan_nodelist(body, result, tuple(keys), gpu_source == "allocatable",
                                      want_extras, HEALTH_ANNOTATION, NodeExtras, HEALTH_CONDITION,
                                      annotation_mode)
         except mod.FallbackError:
             pass  # unusual shape: let the reference-semantics Python path decide
+    return _scan_python(body, result, keys, gpu_source, want_extras, annotation_mode)
+
+
+def _scan_python(body: bytes, result: ScanResult, keys: Sequence[str], gpu_source: str, want_extras: bool,
+                 annotation_mode: int) -> Tuple[Optional[str], int]:
     doc = json.loads(body)
     if not isinstance(doc, dict):
         raise ValueError("NodeList response is not a JSON object")

@@ -241,3 +241,24 @@ def test_node_extras_built_without_init_has_every_slot():
     r = ScanResult()
     ext.scan_nodelist(body, r, GPU_RESOURCE_KEYS, False, True, HEALTH_ANNOTATION, Custom, HEALTH_CONDITION, 2)
     assert isinstance(r.extras[0], Custom) and len(r.extras[0].args) == 7
+
+
+def test_prescan_then_finish_equals_one_shot_scan():
+    """The page reader's pass 1 (prescan, any thread) + the main thread's pass 2 give exactly what one
+    scan_nodelist call gives, for modelled pages, for pages that fall back, and with other keys."""
+    body = json.dumps(fixtures.node_list(fixtures.cluster(40, "mixed", not_ready=[3], with_health=True), "tok")).encode()
+    for mode in (0, 1, 2):
+        a, ta = native_scan(body, mode=mode)
+        b = ScanResult()
+        tb = fastpath.scan_page(body, b, want_extras=True, annotation_mode=mode, pre=fastpath.prescan(body))
+        assert canon(a) == canon(b) and ta == tb
+    # a page pass 1 cannot model: the Python path answers, as for scan_nodelist
+    odd = b'{"items": [{"metadata": {"name": 5}, "status": {"capacity": {"amd.com/gpu": "1"}}}]}'
+    r = ScanResult()
+    assert fastpath.scan_page(odd, r, pre=fastpath.prescan(odd)) == (None, 1) and r.gpu_nodes[0]["name"] == 5
+    # a prescan made with other keys is ignored, not misapplied
+    r2 = ScanResult()
+    fastpath.scan_page(body, r2, keys=("amd.com/gpu",), pre=fastpath.prescan(body))
+    assert all(set(n["gpu_breakdown"]) <= {"amd.com/gpu"} for n in r2.gpu_nodes)
+    with pytest.raises(ValueError):
+        ext.scan_prescanned(fastpath.prescan(body)[1], ScanResult(), ("x",), False, False, NodeExtras)
