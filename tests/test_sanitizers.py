@@ -34,7 +34,9 @@ def test_fastpath_under_asan_ubsan(tmp_path):
                         "-fno-sanitize-recover=undefined", "-std=c++17", "-shared", "-fPIC", "-I",
                         sysconfig.get_paths()["include"], src, "-o", str(out)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
-    env = dict(os.environ, K8SGPU_NATIVE_DIR=str(tmp_path), LD_PRELOAD=f"{asan} {ubsan}",
+    # the sanitizer runtimes go first (ASan must be the first DSO); anything already preloaded stays
+    preload = " ".join(x for x in (asan, ubsan, os.environ.get("LD_PRELOAD", "")) if x)
+    env = dict(os.environ, K8SGPU_NATIVE_DIR=str(tmp_path), LD_PRELOAD=preload,
                ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     which = subprocess.run([sys.executable, "-c", "from k8s_gpu_node_checker_amd.ops import fastpath; "
                             "print(fastpath.ext().__file__)"], capture_output=True, text=True, env=env, cwd=REPO)
