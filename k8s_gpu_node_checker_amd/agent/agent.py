@@ -238,6 +238,7 @@ class Agent:
             for d, g in entries.items():
                 if diags.get(d):
                     g["diag"] = diags[d]
+                    g["diag_at"] = round(self._diag_at.get(d, 0.0), 1)  # when it ran (a busy GPU's result ages)
                 if d in self._diag_skipped:
                     g["diag_skipped"] = self._diag_skipped[d]
             if self._fabric:

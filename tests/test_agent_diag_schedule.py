@@ -84,6 +84,7 @@ def test_busy_gpu_keeps_its_previous_result(monkeypatch):
     rep = ag.probe_once()
     assert w.runs == [0, 1, 0]
     assert rep["gpus"][1]["diag"] == first and rep["gpus"][1]["diag_skipped"] == "in use: graphics engine 97% busy"
+    assert rep["gpus"][1]["diag_at"] == 1000.0 and rep["gpus"][0]["diag_at"] == 4600.0  # the kept result's age shows
 
 
 def test_diag_when_always_ignores_workloads(monkeypatch):
