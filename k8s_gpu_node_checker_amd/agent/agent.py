@@ -113,7 +113,8 @@ class Agent:
                  diag_interval: float = 3600.0, devices: Optional[List[int]] = None,
                  annotation_refresh: float = 900.0, heartbeat_interval: float = 300.0,
                  events: bool = True, event_namespace: str = "default", taint_unhealthy: bool = False,
-                 diag_when: str = "idle", busy_vram_mb: int = 2048, busy_gfx_activity: int = 10):
+                 diag_when: str = "idle", busy_vram_mb: int = 2048, busy_gfx_activity: int = 10,
+                 diag_timeout: float = 300.0):
         self.node = node
         self.source = source
         self.fixture = fixture
@@ -130,6 +131,8 @@ class Agent:
         self.busy_gfx_activity = busy_gfx_activity
         self._diag_cache: Dict[int, Dict[str, Any]] = {}
         self._diag_at: Dict[int, float] = {}
+        self._diag_threads: Dict[int, Any] = {}  # device -> (thread, start time, result box) until it returns
+        self.diag_timeout = diag_timeout
         self._diag_skipped: Dict[int, str] = {}
         self._fabric: Optional[Dict[str, Any]] = None
         self._fabric_at = float("-inf")
@@ -193,21 +196,34 @@ class Agent:
             else:
                 run.append(d)
         # one host thread per GPU: each diagnostic is a ctypes call that releases the GIL and drives its
-        # own device, so an 8-GPU node is checked in the time of one GPU instead of eight
-        results: Dict[int, Dict[str, Any]] = {}
-
-        def work(d: int) -> None:
-            results[d] = diag.run(self.diag_level, d)
-        threads = [threading.Thread(target=work, args=(d,), name=f"diag-gpu{d}") for d in run]
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
+        # own device, so an 8-GPU node is checked in the time of one GPU instead of eight.  A GPU whose
+        # diagnostic never returns (a hung queue) is reported as failed after `diag_timeout` s instead of
+        # freezing the agent into a stale report; nothing new is started on it while that thread lives.
+        run = [d for d in run if d not in self._diag_threads]
         for d in run:
-            if d in results:
-                self._diag_cache[d] = results[d]
-            self._diag_at[d] = now
+            box: Dict[str, Any] = {}
+
+            def work(d: int = d, box: Dict[str, Any] = box) -> None:
+                try:
+                    box["res"] = diag.run(self.diag_level, d)
+                except Exception as e:  # a broken library or device: a failed test, not a dead agent
+                    box["res"] = {"run": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
+            t = threading.Thread(target=work, name=f"diag-gpu{d}", daemon=True)
+            self._diag_threads[d] = (t, now, box)
+            t.start()
+        for d, (t, started, box) in list(self._diag_threads.items()):
+            t.join(max(0.0, started + self.diag_timeout - time.time()))
+            if not t.is_alive():
+                del self._diag_threads[d]
+                if "res" in box:
+                    self._diag_cache[d] = box["res"]
+                self._diag_at[d] = started
+            else:
+                self._diag_cache[d] = {"watchdog": {
+                    "pass": False, "detail": f"diagnostics did not finish within {self.diag_timeout:g} s (GPU hang?)"}}
+                self._diag_at[d] = started
         if (self.diag_level >= 2 and self.devices is None and len(devices) >= 2 and not self._diag_skipped
+                and not self._diag_threads
                 and now - self._fabric_at >= self.diag_interval):
             # node-level: every ordered GPU pair over xGMI (after the per-GPU tests, so no contention);
             # it touches every GPU, so it waits until none is busy
@@ -448,6 +464,8 @@ def build_parser() -> argparse.ArgumentParser:
                          "keeps its last result and is retried at the next probe); always: on schedule")
     ap.add_argument("--busy-vram-mb", type=int, default=2048,
                     help="a process other than the agent holding this much VRAM makes its GPU busy (default 2048)")
+    ap.add_argument("--diag-timeout", type=float, default=300.0,
+                    help="a GPU whose diagnostics run longer than this (s) is reported failed (hung); default 300")
     ap.add_argument("--busy-gfx-activity", type=int, default=10,
                     help="graphics-engine activity (%%) at which a GPU counts as busy (default 10)")
     return ap
@@ -460,7 +478,7 @@ def main(argv: Optional[List[str]] = None) -> int:
                   annotation_refresh=args.annotation_refresh, heartbeat_interval=args.heartbeat_interval,
                   events=args.events, event_namespace=args.event_namespace, taint_unhealthy=args.taint_unhealthy,
                   diag_when=args.diag_when, busy_vram_mb=args.busy_vram_mb,
-                  busy_gfx_activity=args.busy_gfx_activity)
+                  busy_gfx_activity=args.busy_gfx_activity, diag_timeout=args.diag_timeout)
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient

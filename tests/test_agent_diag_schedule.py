@@ -1,14 +1,19 @@
 """Agent diagnostics schedule on CPU: idle-only active diagnostics (``--diag-when``), per-GPU intervals,
 the node-level fabric test waiting for an all-idle node.  A fake ``ops.diag`` stands in for the HIP
 library; the probe report is built here."""
+import time
+
 import pytest
 
 from k8s_gpu_node_checker_amd.agent import agent as A
 from k8s_gpu_node_checker_amd.ops import amdsmi_probe, diag, fabric
+from k8s_gpu_node_checker_amd.testing import fixtures
 
 
 def gpu(i, procs=None, act=0, vram_used=300):
-    g = {"index": i, "bdf": f"0000:0{i}:00.0", "gfx": "gfx950", "vram_used_mb": vram_used, "gfx_activity": act}
+    g = dict(fixtures.mi355x_probe_report("n", gpus=i + 1)["gpus"][i])  # a healthy MI355X
+    g.update({"index": i, "bdf": f"0000:0{i}:00.0", "vram_used_mb": vram_used, "gfx_activity": act})
+    g.pop("processes", None)
     if procs is not None:
         g["procs"] = procs
         g["processes"] = len(procs)
@@ -23,7 +28,8 @@ class World:
         self.clock = 1000.0
         monkeypatch.setattr(A.time, "time", lambda: self.clock)
         monkeypatch.setattr(amdsmi_probe, "probe", lambda node, src, fx: {
-            "schema": "mi355x-health/v1", "node": node, "probe": "fake", "gpus": [dict(g) for g in self.gpus]})
+            "schema": "mi355x-health/v1", "node": node, "ts": self.clock, "probe": "fake",
+            "gpus": [dict(g) for g in self.gpus]})
         monkeypatch.setattr(diag, "device_count", lambda: n)
         monkeypatch.setattr(diag, "device_info", lambda d: {"bdf": f"0000:0{d}:00.0"})
 
@@ -132,3 +138,45 @@ def test_metrics_show_activity_and_skips():
     m = A._metrics(rep)
     assert 'mi355x_gpu_gfx_activity_percent{gpu="0",bdf="b0"} 40' in m
     assert 'mi355x_gpu_diag_skipped{gpu="0",bdf="b0"} 1' in m and 'mi355x_gpu_diag_skipped{gpu="1",bdf="b1"} 0' in m
+
+
+def test_hung_diagnostic_is_reported_not_waited_for(monkeypatch):
+    import threading
+    from k8s_gpu_node_checker_amd.models.health import HEALTHY, UNHEALTHY
+    w = World(monkeypatch)
+    release = threading.Event()
+    started = []
+
+    def run(level, d):
+        started.append(d)
+        if d == 1:
+            release.wait(30)  # GPU 1's queue hangs
+        return {"gemm": {"pass": True}}
+    monkeypatch.setattr(diag, "run", run)
+    ag = A.Agent("n", source="fake", diag_level=1, diag_interval=3600, diag_timeout=0.2)
+    rep = ag.probe_once()
+    g0, g1 = rep["gpus"]
+    assert g0["diag"]["gemm"]["pass"]
+    assert g1["diag"]["watchdog"]["pass"] is False and "GPU hang" in g1["diag"]["watchdog"]["detail"]
+    assert rep["state"] == UNHEALTHY
+    # an interval later: GPU 0 runs again, GPU 1 gets no second diagnostic while the first one lives
+    w.clock += 3600
+    t = time.monotonic()
+    rep = ag.probe_once()
+    assert started == [0, 1, 0] and time.monotonic() - t < 5
+    assert rep["gpus"][1]["diag"]["watchdog"]["pass"] is False
+    # the hang clears: its real result replaces the watchdog failure
+    release.set()
+    ag._diag_threads[1][0].join(5)
+    rep = ag.probe_once()
+    assert rep["gpus"][1]["diag"] == {"gemm": {"pass": True}} and rep["state"] == HEALTHY
+
+
+def test_diagnostic_that_raises_is_a_failed_test(monkeypatch):
+    World(monkeypatch)
+
+    def boom(level, d):
+        raise RuntimeError("hipErrorIllegalAddress")
+    monkeypatch.setattr(diag, "run", boom)
+    rep = A.Agent("n", source="fake", diag_level=1).probe_once()
+    assert rep["gpus"][0]["diag"]["run"] == {"pass": False, "detail": "RuntimeError: hipErrorIllegalAddress"}
