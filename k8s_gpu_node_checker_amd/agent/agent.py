@@ -138,6 +138,7 @@ class Agent:
         self._fabric_at = float("-inf")
         self._bdf: Dict[int, str] = {}  # HIP ordinal -> PCI address (amd-smi and HIP enumerate independently)
         self.last: Optional[Dict[str, Any]] = None
+        self.last_probe_done: Optional[float] = None  # monotonic time of the last completed probe (/healthz)
         self._last_condition: Optional[Dict[str, Any]] = None
         # the annotation (KBs per node, a new object revision per write) is rewritten only when the
         # report changed or every `annotation_refresh` s; the condition heartbeat goes out every probe
@@ -263,6 +264,7 @@ class Agent:
         rep["state"] = verdict.state
         with self.lock:
             self.last = rep
+            self.last_probe_done = time.monotonic()
         return rep
 
     def _throttle_windows(self, rep: Dict[str, Any]) -> None:
@@ -398,7 +400,11 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
     return "\n".join(lines) + "\n"
 
 
-def serve(agent: Agent, host: str, port: int) -> ThreadingHTTPServer:
+def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = None) -> ThreadingHTTPServer:
+    """/probe, /metrics and /healthz; /healthz answers 503 once no probe has completed for
+    ``stale_after`` s (a wedged amd-smi call or driver), so a livenessProbe restarts the agent."""
+    started = time.monotonic()
+
     class H(BaseHTTPRequestHandler):
         protocol_version = "HTTP/1.1"
 
@@ -415,6 +421,16 @@ def serve(agent: Agent, host: str, port: int) -> ThreadingHTTPServer:
                 body = _metrics(rep).encode()
                 ctype = "text/plain; version=0.0.4"
             elif self.path.startswith("/healthz"):
+                last = agent.last_probe_done if agent.last_probe_done is not None else started
+                idle = time.monotonic() - last
+                if stale_after is not None and idle > stale_after:
+                    body = f"no probe completed for {idle:.0f} s".encode()
+                    self.send_response(503)
+                    self.send_header("Content-Type", "text/plain")
+                    self.send_header("Content-Length", str(len(body)))
+                    self.end_headers()
+                    self.wfile.write(body)
+                    return
                 body, ctype = b"ok", "text/plain"
             else:
                 self.send_response(404)
@@ -486,7 +502,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         client = KubeClient(load_kube_config(args.kubeconfig), timeout=10.0)
     if "http" in pubs:
         host, _, port = args.listen.rpartition(":")
-        serve(agent, host or "0.0.0.0", int(port))
+        # a probe cycle may legitimately include diagnostics (up to --diag-timeout per GPU)
+        serve(agent, host or "0.0.0.0", int(port), stale_after=max(180.0, 3 * args.interval + args.diag_timeout))
     while True:
         started = time.monotonic()
         rep = agent.probe_once()

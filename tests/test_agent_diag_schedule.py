@@ -180,3 +180,26 @@ def test_diagnostic_that_raises_is_a_failed_test(monkeypatch):
     monkeypatch.setattr(diag, "run", boom)
     rep = A.Agent("n", source="fake", diag_level=1).probe_once()
     assert rep["gpus"][0]["diag"]["run"] == {"pass": False, "detail": "RuntimeError: hipErrorIllegalAddress"}
+
+
+def test_healthz_turns_503_when_probes_stop(monkeypatch):
+    import urllib.error
+    import urllib.request
+    w = World(monkeypatch)
+    ag = A.Agent("n", source="fake")
+    srv = A.serve(ag, "127.0.0.1", 0, stale_after=0.3)
+    url = f"http://127.0.0.1:{srv.server_address[1]}/healthz"
+    try:
+        assert urllib.request.urlopen(url, timeout=5).read() == b"ok"  # starting up: grace period
+        ag.probe_once()
+        assert urllib.request.urlopen(url, timeout=5).status == 200
+        time.sleep(0.5)  # the probe loop is stuck
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(url, timeout=5)
+        assert e.value.code == 503
+        ag.probe_once()
+        assert urllib.request.urlopen(url, timeout=5).status == 200
+    finally:
+        srv.shutdown()
+        srv.server_close()
+    assert w.gpus
