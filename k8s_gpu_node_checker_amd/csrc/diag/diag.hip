@@ -41,6 +41,7 @@ namespace {
 
 thread_local std::string g_err;
 int g_gemm_variant = 0;
+int g_gemm_buffer_loads = 0;  // v3 operand staging: 0 = global_load_lds, 1 = buffer_load ... lds
 int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3 kernels;
                           // measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
 
@@ -327,6 +328,52 @@ __device__ __forceinline__ void stg_region(unsigned char* lds_stage, const __bf1
   __builtin_amdgcn_global_load_lds(gp, (lds_void_t*)l, 16, 0, 0);
 }
 
+// The same region through the buffer path (`buffer_load_dwordx4 ... lds`): the tile's A and B slabs
+// are two scalar buffer resources, the per-lane byte offset is loop-invariant and the K-tile moves
+// only the scalar soffset, so no 64-bit per-lane address math is redone per K-tile.
+struct StgBuf {
+  __amdgpu_buffer_rsrc_t a, b;
+};
+
+__device__ __forceinline__ StgBuf stg_buf(const __bf16* A, const __bf16* Bt, int K) {
+  // CDNA raw-buffer dword3 (32-bit data format, no swizzle); num_records = one 256-row slab
+  const int bytes = V2_BM * K * 2;
+  return StgBuf{__builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(A), static_cast<short>(0), bytes, 0x00020000),
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(Bt), static_cast<short>(0), bytes, 0x00020000)};
+}
+
+template <bool FP8>
+__device__ __forceinline__ void stg_region_buf(unsigned char* lds_stage, const StgBuf& rs, int K, int kt, int region,
+                                               int i, int wid, int lane) {
+  const int rsub = lane >> 3, phys = lane & 7;
+  const int g = wid * 2 + i;
+  const bool is_a = region == 0 || region == 3;
+  const int row0 = is_a ? (g >> 3) * 128 + (region == 0 ? 0 : 64) + (g & 7) * 8
+                        : (g >> 2) * 64 + (region == 1 ? 0 : 32) + (g & 3) * 8;
+  const int row = row0 + rsub;
+  const int c = phys ^ swz_row_xor(row, FP8);
+  const int voff = (row * K + c * 8) * 2;
+  unsigned char* l = lds_stage + (is_a ? 0 : V2_BM * BK * 2) + row0 * (BK * 2);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(is_a ? rs.a : rs.b, (lds_void_t*)l, 16, voff, kt * BK * 2, 0, 0);
+}
+
+template <bool FP8>
+__device__ __forceinline__ void v2_fill_buf(unsigned char* lds_stage, const StgBuf& rs, int K, int kt, int wid,
+                                            int lane) {
+  const int rsub = lane >> 3, phys = lane & 7;
+#pragma unroll
+  for (int op = 0; op < 2; ++op) {
+#pragma unroll
+    for (int j = 0; j < V2_ROWS_PER_WAVE / 8; ++j) {
+      const int row = wid * V2_ROWS_PER_WAVE + j * 8 + rsub;
+      const int c = phys ^ swz_row_xor(row, FP8);
+      unsigned char* l = lds_stage + op * (V2_BM * BK * 2) + (wid * V2_ROWS_PER_WAVE + j * 8) * (BK * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(op == 0 ? rs.a : rs.b, (lds_void_t*)l, 16, (row * K + c * 8) * 2,
+                                               kt * BK * 2, 0, 0);
+    }
+  }
+}
+
 __device__ __forceinline__ void stg_mfma(floatx4 (&acc)[8][4], const bf16x8 (&af)[4][2], const bf16x8 (&bf)[2][2],
                                          int m0, int n0) {
 #pragma unroll
@@ -419,7 +466,7 @@ struct StgFrags<DT_FP4> {
 // unit scales) passed as K = row bytes / 2 "bf16 columns", so the byte-identical LDS-DMA staging is
 // shared (a 64-column bf16 K-tile is a 128-byte fp8 or fp4 K-tile); only the swizzle (fp8), the
 // fragment reads and the MFMA differ.
-template <int DT, bool EPI_LDS = false>
+template <int DT, bool EPI_LDS = false, bool BUF = false>
 __global__ void __launch_bounds__(V2_THREADS, 1)
 gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
                int K) {
@@ -450,9 +497,18 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
   const int frow = lane & 15, fq = lane >> 4;
 
   constexpr bool FP8 = DT == DT_FP8;
-  v2_fill<FP8>(smem, Ab, Bb, K, 0, wid, lane);
+  const StgBuf rs = stg_buf(Ab, Bb, K);
+  auto region = [&](unsigned char* stage, int kt_, int r, int i) {
+    if constexpr (BUF) stg_region_buf<FP8>(stage, rs, K, kt_, r, i, wid, lane);
+    else stg_region<FP8>(stage, Ab, Bb, K, kt_, r, i, wid, lane);
+  };
+  auto fill = [&](unsigned char* stage, int kt_) {
+    if constexpr (BUF) v2_fill_buf<FP8>(stage, rs, K, kt_, wid, lane);
+    else v2_fill<FP8>(stage, Ab, Bb, K, kt_, wid, lane);
+  };
+  fill(smem, 0);
   if (KT > 1) {
-    v2_fill<FP8>(smem + V2_STAGE_BYTES, Ab, Bb, K, 1, wid, lane);
+    fill(smem + V2_STAGE_BYTES, 1);
     __builtin_amdgcn_s_waitcnt(0x3f78);  // vmcnt(8): tile 0 landed, tile 1 may be in flight
   } else {
     __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
@@ -469,8 +525,8 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     const bool pre = kt + 2 < KT;
     // phase 0: A(m0), B(n0); R3 of tile kt+1 (tile 1 came whole with the prologue)
     if (kt >= 1 && kt + 1 < KT) {
-      stg_region<FP8>(nxt, Ab, Bb, K, kt + 1, 3, 0, wid, lane);
-      stg_region<FP8>(nxt, Ab, Bb, K, kt + 1, 3, 1, wid, lane);
+      region(nxt, kt + 1, 3, 0);
+      region(nxt, kt + 1, 3, 1);
     }
 #pragma unroll
     for (int n = 0; n < 2; ++n) stg_load(f.b0[n], b_img, wc * 64 + n * 16 + frow, fq);
@@ -489,10 +545,10 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     STG_BARRIER();
     // phase 2: A(m1); restage R0, R1 with tile kt+2
     if (pre) {
-      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
-      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
-      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
-      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
+      region(cur, kt + 2, 0, 0);
+      region(cur, kt + 2, 0, 1);
+      region(cur, kt + 2, 1, 0);
+      region(cur, kt + 2, 1, 1);
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m) stg_load(f.a[m], a_img, wr * 128 + (m + 4) * 16 + frow, fq);
@@ -502,8 +558,8 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     STG_BARRIER();
     // phase 3: no LDS reads; restage R2, retire tile kt+1
     if (pre) {
-      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
-      stg_region<FP8>(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
+      region(cur, kt + 2, 2, 0);
+      region(cur, kt + 2, 2, 1);
       __builtin_amdgcn_s_waitcnt(0x3f76);  // vmcnt(6)
     } else {
       __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
@@ -774,25 +830,29 @@ hipError_t enable_peer(int from, int to) {
   return e;
 }
 
-template <int DT, bool EPI>
+template <int DT, bool EPI, bool BUF>
 int launch_v3_inst(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI>),
+    DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI, BUF>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     attr_set = true;
   }
   const int nwg = (M / V2_BM) * (N / V2_BN);
-  hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, stream,
+  hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI, BUF>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, stream,
                      static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, M, N, Kcols);
   return 0;
 }
 
-// v3 launch (M, N multiples of 256; Kcols = bf16 columns, K8 / 2 for fp8), epilogue per g_gemm_epilogue
+// v3 launch (M, N multiples of 256; Kcols = bf16 columns, K8 / 2 for fp8), epilogue per g_gemm_epilogue,
+// operand staging per g_gemm_buffer_loads
 template <int DT>
 int launch_v3(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
-  return g_gemm_epilogue ? launch_v3_inst<DT, true>(A, Bt, C, M, N, Kcols, stream)
-                         : launch_v3_inst<DT, false>(A, Bt, C, M, N, Kcols, stream);
+  if (g_gemm_buffer_loads)
+    return g_gemm_epilogue ? launch_v3_inst<DT, true, true>(A, Bt, C, M, N, Kcols, stream)
+                           : launch_v3_inst<DT, false, true>(A, Bt, C, M, N, Kcols, stream);
+  return g_gemm_epilogue ? launch_v3_inst<DT, true, false>(A, Bt, C, M, N, Kcols, stream)
+                         : launch_v3_inst<DT, false, false>(A, Bt, C, M, N, Kcols, stream);
 }
 
 }  // namespace
@@ -805,6 +865,7 @@ const char* diag_last_error(void) { return g_err.c_str(); }
 // chip, else v1), 1 = force v1 (128x128 register-staged), 2 = force v2, 3 = force v3
 void diag_set_gemm_variant(int v) { g_gemm_variant = v; }
 void diag_set_gemm_epilogue(int e) { g_gemm_epilogue = e; }
+void diag_set_gemm_buffer_loads(int b) { g_gemm_buffer_loads = b; }
 
 int diag_device_count(void) {
   int n = 0;

@@ -50,6 +50,7 @@ def lib() -> ctypes.CDLL:
         L.diag_last_error.restype = ctypes.c_char_p
         L.diag_set_gemm_variant.argtypes = [ctypes.c_int]
         L.diag_set_gemm_epilogue.argtypes = [ctypes.c_int]
+        L.diag_set_gemm_buffer_loads.argtypes = [ctypes.c_int]
         L.diag_device_count.restype = ctypes.c_int
         L.diag_device_arch.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.diag_gemm_bf16_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -106,6 +107,13 @@ def set_gemm_epilogue(lds_staged: bool) -> None:
     """v3 kernels: write C with 4-byte stores straight from the MFMA layout (False) or staged
     through LDS as 16-byte row pieces (True)."""
     lib().diag_set_gemm_epilogue(1 if lds_staged else 0)
+
+
+def set_gemm_buffer_loads(buffer_loads: bool) -> None:
+    """v3 kernels: stage operands with ``global_load_lds_dwordx4`` (False) or ``buffer_load_dwordx4 ...
+    lds`` from two per-tile buffer resources (True: loop-invariant per-lane offsets, the K step in a
+    scalar register)."""
+    lib().diag_set_gemm_buffer_loads(1 if buffer_loads else 0)
 
 
 def gemm_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int, stream: int = 0) -> None:

@@ -121,6 +121,44 @@ def test_mfma_gemm_variants_match_fp32_reference(dev, variant, m, n, k):
     assert rel < 1e-4 * max(1, k / 512), rel
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 256, 192), (768, 512, 256), (1024, 768, 4096),
+                                   (2048, 2048, 2048)])
+def test_v3_buffer_load_staging_matches(dev, m, n, k):
+    """The buffer_load ... lds staging path of the v3 pipeline (bf16 and MX-fp8) computes exactly what
+    the global_load_lds path computes, and matches the torch reference."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + 3 * n + 7 * k)
+    st = torch.cuda.current_stream().cuda_stream
+    a = torch.randn(m, k, device=dev, generator=g)
+    bt = torch.randn(n, k, device=dev, generator=g)
+    for (x, y, launch) in ((a.to(torch.bfloat16), bt.to(torch.bfloat16), diag.gemm_launch),
+                           (a.to(torch.float8_e4m3fn), bt.to(torch.float8_e4m3fn), diag.gemm_fp8_launch)):
+        if launch is diag.gemm_fp8_launch and k % 128:
+            continue
+        outs = []
+        diag.set_gemm_variant("v3")
+        try:
+            for buf in (False, True):
+                diag.set_gemm_buffer_loads(buf)
+                c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+                launch(x.data_ptr(), y.data_ptr(), c.data_ptr(), m, n, k, st)
+                torch.cuda.synchronize()
+                outs.append(c)
+        finally:
+            diag.set_gemm_buffer_loads(False)
+            diag.set_gemm_variant("auto")
+        assert torch.equal(outs[0], outs[1])
+        if launch is diag.gemm_fp8_launch:  # the MX MFMA's own accumulation error, normalised by sum|a*b|
+            ref = x.double() @ y.double().t()
+            mag = x.double().abs() @ y.double().abs().t()
+            err = ((outs[1].double() - ref).abs() / mag.clamp_min(1e-30)).max().item()
+            assert err < diag.GEMM_FP8_MAX_ERR, err
+        else:
+            ref = x.float() @ y.float().t()
+            rel = ((outs[1] - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
+            assert rel < 1e-4 * max(1, k / 512), rel
+
+
 def test_mfma_gemm_large_auto_uses_v3_and_matches(dev):
     """4096^3 in auto mode runs the staggered v3 kernel; compare every output with a bf16-input,
     fp32-accumulate torch reference."""
