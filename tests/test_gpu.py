@@ -307,6 +307,23 @@ def test_probe_sees_a_workload_and_agent_skips_diagnostics(dev, repo):
         holder.wait(timeout=30)
 
 
+def test_agent_cli_once_runs_idle_diagnostics(repo):
+    """The DaemonSet's entry point end to end: one probe + level-1 diagnostics with the default
+    idle-only policy on an idle GPU, the report on stdout."""
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip("no GPU")
+    p = subprocess.run([sys.executable, "-m", "k8s_gpu_node_checker_amd.agent.agent", "--once", "--publish", "stdout",
+                        "--source", "native", "--diag-level", "1", "--node", "gpu-node"],
+                       capture_output=True, text=True, timeout=300, cwd=repo)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rep = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    g = rep["gpus"][0]
+    assert "diag_skipped" not in g, g.get("diag_skipped")
+    assert g["diag"]["gemm"]["pass"] and g["diag"]["hbm"]["pass"] and g["diag_at"] > 0, g.get("diag")
+    assert rep["state"] in ("healthy", "degraded"), rep["state"]
+
+
 def test_agent_diagnostics_threads_per_device(dev):
     from k8s_gpu_node_checker_amd.agent.agent import Agent
     from k8s_gpu_node_checker_amd.ops import diag
