@@ -32,7 +32,7 @@ import sys
 import threading
 import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Sequence
 
 from ..models.health import (HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, HealthExpectations, Verdict,
                               condition_for, condition_reason, evaluate_report, format_k8s_time, throttle_window)
@@ -114,7 +114,7 @@ class Agent:
                  annotation_refresh: float = 900.0, heartbeat_interval: float = 300.0,
                  events: bool = True, event_namespace: str = "default", taint_unhealthy: bool = False,
                  diag_when: str = "idle", busy_vram_mb: int = 2048, busy_gfx_activity: int = 10,
-                 diag_timeout: float = 300.0):
+                 diag_timeout: float = 300.0, ignore_pids: Sequence[int] = ()):
         self.node = node
         self.source = source
         self.fixture = fixture
@@ -129,6 +129,9 @@ class Agent:
         self.diag_when = diag_when
         self.busy_vram_mb = busy_vram_mb
         self.busy_gfx_activity = busy_gfx_activity
+        # processes whose VRAM never makes a GPU busy: the agent itself and, for harnesses that start
+        # the agent as a child of a GPU-holding process (a test runner), the PIDs given with --ignore-pid
+        self.ignore_pids = frozenset((os.getpid(),) + tuple(int(p) for p in ignore_pids))
         self._diag_cache: Dict[int, Dict[str, Any]] = {}
         self._diag_at: Dict[int, float] = {}
         self._diag_threads: Dict[int, Any] = {}  # device -> (thread, start time, result box) until it returns
@@ -190,7 +193,7 @@ class Agent:
         due = [d for d in devices if now - self._diag_at.get(d, float("-inf")) >= self.diag_interval]
         run = []
         for d in due:
-            why = gpu_busy(entries.get(d) or {}, frozenset((os.getpid(),)), self.busy_vram_mb,
+            why = gpu_busy(entries.get(d) or {}, self.ignore_pids, self.busy_vram_mb,
                            self.busy_gfx_activity) if self.diag_when == "idle" else None
             if why:
                 self._diag_skipped[d] = why
@@ -482,6 +485,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="a process other than the agent holding this much VRAM makes its GPU busy (default 2048)")
     ap.add_argument("--diag-timeout", type=float, default=300.0,
                     help="a GPU whose diagnostics run longer than this (s) is reported failed (hung); default 300")
+    ap.add_argument("--ignore-pid", type=int, action="append", default=[], metavar="PID",
+                    help="a process whose VRAM never makes a GPU busy (repeatable; e.g. the harness that "
+                         "started the agent). The agent's own PID is always ignored")
     ap.add_argument("--busy-gfx-activity", type=int, default=10,
                     help="graphics-engine activity (%%) at which a GPU counts as busy (default 10)")
     return ap
@@ -494,7 +500,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                   annotation_refresh=args.annotation_refresh, heartbeat_interval=args.heartbeat_interval,
                   events=args.events, event_namespace=args.event_namespace, taint_unhealthy=args.taint_unhealthy,
                   diag_when=args.diag_when, busy_vram_mb=args.busy_vram_mb,
-                  busy_gfx_activity=args.busy_gfx_activity, diag_timeout=args.diag_timeout)
+                  busy_gfx_activity=args.busy_gfx_activity, diag_timeout=args.diag_timeout,
+                  ignore_pids=args.ignore_pid)
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient
