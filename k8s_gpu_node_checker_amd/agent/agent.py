@@ -34,9 +34,11 @@ import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional, Sequence
 
-from ..models.health import (HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, HealthExpectations, Verdict,
+from ..models.health import (HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, XGMI_LINKS_EXPECTED,
+                              HealthExpectations, Verdict,
                               condition_for, condition_reason, evaluate_report, format_k8s_time, throttle_window)
 from ..models.node import HEALTH_ANNOTATION
+from ..models.resources import PRIMARY_GPU_KEY, gpu_breakdown
 
 
 # Report fields that change on every probe without saying anything about health; ignored when deciding
@@ -114,8 +116,15 @@ class Agent:
                  annotation_refresh: float = 900.0, heartbeat_interval: float = 300.0,
                  events: bool = True, event_namespace: str = "default", taint_unhealthy: bool = False,
                  diag_when: str = "idle", busy_vram_mb: int = 2048, busy_gfx_activity: int = 10,
-                 diag_timeout: float = 300.0, ignore_pids: Sequence[int] = ()):
+                 diag_timeout: float = 300.0, ignore_pids: Sequence[int] = (),
+                 expect_gpus: Optional[int] = None, expectations: Optional[HealthExpectations] = None):
         self.node = node
+        # the verdict is taken against the GPU count the node registered (amd.com/gpu capacity /
+        # allocatable, read from the Node object) unless --expect-gpus pins it; a GPU that fell off
+        # the bus after the device plugin counted it then makes the node unhealthy at the source
+        self.expect_gpus = expect_gpus
+        self.node_gpus = 0
+        self.expectations = expectations or HealthExpectations()
         self.source = source
         self.fixture = fixture
         self.diag_level = diag_level
@@ -165,6 +174,23 @@ class Agent:
         self._event_state: Optional[str] = None
         self._taint_state: Optional[str] = None
         self.lock = threading.Lock()
+
+    @property
+    def expected_gpus(self) -> int:
+        """GPUs amd-smi must see: ``--expect-gpus`` when given, else the Node's ``amd.com/gpu`` (0: unknown)."""
+        return self.expect_gpus if self.expect_gpus is not None else self.node_gpus
+
+    def observe_node(self, node: Any) -> None:
+        """Take the ``amd.com/gpu`` count from the agent's own Node object (GET, or a PATCH response)."""
+        if not isinstance(node, dict):
+            return
+        status = node.get("status") or {}
+        counts = [gpu_breakdown(status.get(k), (PRIMARY_GPU_KEY,)).get(PRIMARY_GPU_KEY, 0)
+                  for k in ("capacity", "allocatable")]
+        self.node_gpus = max(counts)
+
+    def evaluate(self, rep: Dict[str, Any]) -> Verdict:
+        return evaluate_report(rep, self.expected_gpus, self.expectations)
 
     def _entries_by_device(self, gpus: List[Dict[str, Any]], devices: List[int]) -> Dict[int, Dict[str, Any]]:
         """The probe entry of each HIP device: by PCI address, by index when HIP cannot say."""
@@ -263,8 +289,10 @@ class Agent:
                     g["diag_skipped"] = self._diag_skipped[d]
             if self._fabric:
                 rep["fabric"] = self._fabric
-        verdict = evaluate_report(rep, 0, HealthExpectations())
+        verdict = self.evaluate(rep)
         rep["state"] = verdict.state
+        if self.expected_gpus:
+            rep["expected_gpus"] = self.expected_gpus
         with self.lock:
             self.last = rep
             self.last_probe_done = time.monotonic()
@@ -290,7 +318,7 @@ class Agent:
         return {HEALTH_ANNOTATION: json.dumps(rep, separators=(",", ":"))}
 
     def condition(self, rep: Dict[str, Any]) -> Dict[str, Any]:
-        v = evaluate_report(rep, 0, HealthExpectations())
+        v = self.evaluate(rep)
         cond = condition_for(v, previous=self._last_condition)
         self._last_condition = cond
         self._verdict = v
@@ -313,7 +341,7 @@ class Agent:
         cond = self.condition(rep)
         key = (cond.get("status"), cond.get("reason"), cond.get("message"))
         if force or key != self._cond_key or now - self._cond_at >= self.heartbeat_interval:
-            client.patch_node_condition(self.node, cond)
+            self.observe_node(client.patch_node_condition(self.node, cond))  # the response is the Node
             self._cond_key, self._cond_at = key, now
             wrote["condition"] = True
         v = self._verdict
@@ -488,6 +516,11 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--ignore-pid", type=int, action="append", default=[], metavar="PID",
                     help="a process whose VRAM never makes a GPU busy (repeatable; e.g. the harness that "
                          "started the agent). The agent's own PID is always ignored")
+    ap.add_argument("--expect-gpus", type=int, default=None, metavar="N",
+                    help="GPUs amd-smi must see on this node (default: the Node's amd.com/gpu capacity)")
+    ap.add_argument("--xgmi-links", type=int, default=XGMI_LINKS_EXPECTED, metavar="N",
+                    help=f"xGMI links that must be Up per GPU (default {XGMI_LINKS_EXPECTED}: 8-GPU hive; "
+                         "0 disables the check)")
     ap.add_argument("--busy-gfx-activity", type=int, default=10,
                     help="graphics-engine activity (%%) at which a GPU counts as busy (default 10)")
     return ap
@@ -501,12 +534,17 @@ def main(argv: Optional[List[str]] = None) -> int:
                   events=args.events, event_namespace=args.event_namespace, taint_unhealthy=args.taint_unhealthy,
                   diag_when=args.diag_when, busy_vram_mb=args.busy_vram_mb,
                   busy_gfx_activity=args.busy_gfx_activity, diag_timeout=args.diag_timeout,
-                  ignore_pids=args.ignore_pid)
+                  ignore_pids=args.ignore_pid, expect_gpus=args.expect_gpus,
+                  expectations=HealthExpectations(xgmi_links=args.xgmi_links))
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient
         from ..kube.config import load_kube_config
         client = KubeClient(load_kube_config(args.kubeconfig), timeout=10.0)
+        try:  # the node's registered GPU count; refreshed from every condition PATCH response after this
+            agent.observe_node(client.get_node(args.node))
+        except Exception as e:
+            print(f"could not read node {args.node}: {e}", file=sys.stderr, flush=True)
     if "http" in pubs:
         host, _, port = args.listen.rpartition(":")
         # a probe cycle may legitimately include diagnostics (up to --diag-timeout per GPU)

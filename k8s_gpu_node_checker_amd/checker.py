@@ -22,7 +22,8 @@ from . import report
 from .kube.client import KubeClient
 from .kube.config import ClusterConnection
 from .models import health as H
-from .models.node import ScanResult, primary_gpu_count
+from .models.node import ScanResult, expected_gpu_count
+from .models.node import HEALTH_ANNOTATION
 from .models.resources import GPU_RESOURCE_KEYS, PRIMARY_GPU_KEY
 from .utils.timing import NullTracer, Tracer
 
@@ -73,6 +74,17 @@ class CheckOptions:
     def needs_extras(self) -> bool:
         return self.health_policy != "off" or self.json_extended or self.require_schedulable
 
+    @property
+    def custom_thresholds(self) -> bool:
+        """Checker-side thresholds that differ from the ones the node agent evaluated with."""
+        return self.xgmi_links != H.XGMI_LINKS_EXPECTED
+
+    @property
+    def reeval(self) -> bool:
+        """Re-judge the full report annotation instead of trusting the agent's condition: asked for
+        (``--health-reeval``), or implied by non-default thresholds, which the condition cannot honour."""
+        return self.health_reeval or self.custom_thresholds
+
 
 class CheckResult:
     def __init__(self, scan: ScanResult, verdicts: List[Optional[H.Verdict]], tracer: Tracer):
@@ -80,6 +92,8 @@ class CheckResult:
         self.verdicts = verdicts
         self.tracer = tracer
         self.slack_sent: Optional[bool] = None
+        #: operator-facing notes (stderr), e.g. thresholds that could not be applied to a node
+        self.warnings: List[str] = []
 
     @property
     def gpu_nodes(self) -> List[Dict[str, Any]]:
@@ -120,13 +134,19 @@ def scan_cluster(cluster: ClusterConnection, opts: CheckOptions, tracer: Tracer)
             return client.scan_nodes(limit=opts.page_size, keys=GPU_RESOURCE_KEYS, gpu_source=opts.gpu_source,
                                      want_extras=opts.needs_extras, label_selector=opts.label_selector,
                                      resource_version=opts.resource_version,
-                                     annotation_mode=2 if (opts.health_reeval or opts.json_extended) else 1)
+                                     annotation_mode=2 if (opts.reeval or opts.json_extended) else 1)
     finally:
         client.close()
 
 
-def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer) -> List[Optional[H.Verdict]]:
-    """Evaluate MI355X probe reports and gate ``ready`` (no-op when no node carries one)."""
+def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
+                 warnings: Optional[List[str]] = None) -> List[Optional[H.Verdict]]:
+    """Evaluate MI355X probe reports and gate ``ready`` (no-op when no node carries one).
+
+    Every verdict is cross-checked against the node's ``amd.com/gpu`` count from this LIST
+    (:func:`models.node.expected_gpu_count`): on the condition path through the ``ok/seen`` counts
+    in its message, on the report path through ``evaluate_report``'s ``expected_gpus``.
+    """
     if opts.health_policy == "off" or not scan.gpu_nodes:
         return []
     with tracer.span("health"):
@@ -138,18 +158,25 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer) -> List[O
         verdicts: List[Optional[H.Verdict]] = []
         changed = False
         unknown_ok = opts.probe_unknown == "allow"
+        reeval = opts.reeval
         now = time.time()
+        unapplied: List[str] = []
         for node, ex, rep in zip(scan.gpu_nodes, scan.extras, reports):
             is_amd = PRIMARY_GPU_KEY in node["gpu_breakdown"] or PRIMARY_GPU_KEY in ex.allocatable
+            expected = expected_gpu_count(ex)
             v: Optional[H.Verdict] = None
-            if rep is None and ex.health_condition is not None and not opts.health_reeval:
+            if rep is None and reeval:
+                rep = H.parse_annotation(ex.health_annotation)
+            if rep is None and ex.health_condition is not None:
                 # cheap path: the agent's verdict is a NodeCondition already parsed by the scan
-                v = H.verdict_from_condition(ex.health_condition, opts.probe_max_age, now)
+                v = H.verdict_from_condition(ex.health_condition, opts.probe_max_age, now, expected)
+                if reeval:
+                    unapplied.append(node["name"])
             else:
                 if rep is None:
                     rep = H.parse_annotation(ex.health_annotation)
                 if rep is not None or opts.health_policy == "require":
-                    v = H.evaluate_report(rep, primary_gpu_count(ex, opts.gpu_source), exp, now)
+                    v = H.evaluate_report(rep, expected, exp, now)
             if v is None:
                 verdicts.append(None)
                 continue
@@ -160,6 +187,10 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer) -> List[O
                 changed = True
         if changed:
             scan.recompute_ready()
+        if unapplied and warnings is not None:
+            shown = ", ".join(unapplied[:5]) + (f" (+{len(unapplied) - 5} more)" if len(unapplied) > 5 else "")
+            warnings.append(f"warning: no {HEALTH_ANNOTATION} report on {shown}: checker thresholds "
+                            f"(--xgmi-links {opts.xgmi_links}) not applied, the agent's AMDGPUHealthy verdict is used")
         if not any(verdicts):
             return []
         return verdicts
@@ -186,9 +217,12 @@ def apply_schedulability(scan: ScanResult, opts: CheckOptions) -> None:
 def run_check(cluster: ClusterConnection, opts: CheckOptions, tracer: Optional[Tracer] = None) -> CheckResult:
     tracer = tracer or (Tracer() if (opts.trace or opts.json_extended) else NullTracer())
     scan = scan_cluster(cluster, opts, tracer)
-    verdicts = apply_health(scan, opts, tracer)
+    warnings: List[str] = []
+    verdicts = apply_health(scan, opts, tracer, warnings)
     apply_schedulability(scan, opts)
-    return CheckResult(scan, verdicts, tracer)
+    result = CheckResult(scan, verdicts, tracer)
+    result.warnings = warnings
+    return result
 
 
 def _health_notes(result: CheckResult) -> Optional[List[Optional[str]]]:
@@ -273,6 +307,8 @@ def emit_report(result: CheckResult, opts: CheckOptions, out: Optional[TextIO] =
                 prefix = report.SLACK_SENT + "\n"
             else:
                 print(report.SLACK_FAILED, file=err)
+    for w in result.warnings:
+        print(w, file=err)
     out.write(prefix + body)
     out.flush()
     if opts.trace:

@@ -186,7 +186,9 @@ def _watch_events(args: argparse.Namespace) -> int:
 
         def evaluate(scan):
             tr = Tracer() if (opts.trace or opts.json_extended) else NullTracer()
-            result = CheckResult(scan, apply_health(scan, opts, tr), tr)
+            warnings: list = []
+            result = CheckResult(scan, apply_health(scan, opts, tr, warnings), tr)
+            result.warnings = warnings
             apply_schedulability(scan, opts)
             return result
 

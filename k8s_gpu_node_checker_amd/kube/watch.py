@@ -95,7 +95,7 @@ class NodeWatcher:
         self.debounce = max(0.0, debounce)
         self.page_size = opts.page_size if page_size is None else page_size
         self.sleep = sleep
-        self.view = NodeView(opts.gpu_source, 2 if (opts.health_reeval or opts.json_extended) else 1)
+        self.view = NodeView(opts.gpu_source, 2 if (opts.reeval or opts.json_extended) else 1)
         self.rv: Optional[str] = None
         self.backoff = Backoff(base=0.5, cap=30.0)
         self.relists = 0

@@ -22,6 +22,7 @@ run: driver not loaded, no permission).
 from __future__ import annotations
 
 import json
+import re
 import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -305,15 +306,36 @@ def format_k8s_time(epoch: float) -> str:
     return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(epoch))
 
 
+#: The condition message starts with the GPU counts the verdict was taken on, so the checker can
+#: cross-check them against the node's ``amd.com/gpu`` without the report annotation:
+#: ``8/8 MI355X GPUs healthy``, ``8/8 MI355X GPUs ok; gpu3: HBM 96 C`` (degraded),
+#: ``6/7 MI355X GPUs ok; 7 of 8 GPUs visible to amd-smi; gpu2: ...`` (unhealthy).
+_COUNTS_RE = re.compile(r"^(\d+)/(\d+) MI355X GPUs (?:healthy|ok)\b")
+
+
+def condition_message(verdict: Verdict) -> str:
+    """``AMDGPUHealthy`` message of a verdict: GPU counts first (parseable), then the reasons."""
+    if verdict.state == HEALTHY:
+        return f"{verdict.gpus_ok}/{verdict.gpus_seen} MI355X GPUs healthy"
+    detail = "; ".join(verdict.reasons or verdict.warnings)
+    if verdict.state == UNKNOWN and not verdict.gpus_seen:
+        return detail  # the probe itself failed: there are no counts to report
+    return f"{verdict.gpus_ok}/{verdict.gpus_seen} MI355X GPUs ok" + (f"; {detail}" if detail else "")
+
+
+def parse_condition_counts(message: Optional[str]) -> Optional[Tuple[int, int]]:
+    """``(gpus_ok, gpus_seen)`` from an ``AMDGPUHealthy`` message, None when it carries none
+    (an older agent, or a probe failure)."""
+    m = _COUNTS_RE.match(message or "")
+    return (int(m.group(1)), int(m.group(2))) if m else None
+
+
 def condition_for(verdict: Verdict, now: Optional[float] = None,
                   previous: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
     """The ``AMDGPUHealthy`` NodeCondition the agent publishes for ``verdict``."""
     now = time.time() if now is None else now
     status = "True" if verdict.ok else ("Unknown" if verdict.state == UNKNOWN else "False")
-    if verdict.state == HEALTHY:
-        msg = f"{verdict.gpus_ok}/{verdict.gpus_seen} MI355X GPUs healthy"
-    else:
-        msg = "; ".join(verdict.reasons or verdict.warnings)
+    msg = condition_message(verdict)
     ts = format_k8s_time(now)
     transition = ts
     if previous and previous.get("status") == status and previous.get("lastTransitionTime"):
@@ -323,11 +345,17 @@ def condition_for(verdict: Verdict, now: Optional[float] = None,
 
 
 def verdict_from_condition(cond: Tuple[Optional[str], Optional[str], Optional[str], Optional[float]],
-                           max_age_s: float, now: Optional[float] = None) -> Verdict:
+                           max_age_s: float, now: Optional[float] = None, expected_gpus: int = 0) -> Verdict:
     """``(status, reason, message, heartbeat_epoch)`` of an ``AMDGPUHealthy`` condition -> Verdict.
 
     The cheap path: no annotation JSON to parse, the apiserver already carries
     the agent's verdict in ``status.conditions`` (parsed by the NodeList scan).
+
+    ``expected_gpus`` is the node's ``amd.com/gpu`` count from the same LIST (the reference's
+    definition of a GPU node, ``check-gpu-node.py:181-201``).  The message's ``ok/seen`` counts are
+    cross-checked against it: an agent that saw fewer GPUs than the device plugin registered --
+    a GPU that fell off the bus after registration, or an agent started without the node's
+    count -- makes the node unhealthy even when the agent itself said ``True``.
     """
     status, reason, message, hb = cond
     now = time.time() if now is None else now
@@ -335,14 +363,26 @@ def verdict_from_condition(cond: Tuple[Optional[str], Optional[str], Optional[st
     if age is None or age > max_age_s:
         return Verdict(UNKNOWN, ["stale AMDGPUHealthy condition" if age is not None
                                  else "AMDGPUHealthy condition has no heartbeat"], age_s=age)
-    msg = [message] if message else []
+    counts = parse_condition_counts(message)
+    ok, seen = counts if counts else (0, 0)
+    detail = message or ""
+    if counts:
+        detail = detail.split("; ", 1)[1] if "; " in detail else ""
+    msg = [detail] if detail else []
     if status == "True":
         state = _STATE_OF_REASON.get(reason or "", HEALTHY)
         state = state if state in _OK_STATES else HEALTHY
-        return Verdict(state, warnings=msg if state == DEGRADED else [], age_s=age)
-    if status == "False":
-        return Verdict(UNHEALTHY, msg or ["AMDGPUHealthy=False"], age_s=age)
-    return Verdict(UNKNOWN, msg or ["AMDGPUHealthy=Unknown"], age_s=age)
+        v = Verdict(state, warnings=msg if state == DEGRADED else [], gpus_ok=ok, gpus_seen=seen, age_s=age)
+    elif status == "False":
+        v = Verdict(UNHEALTHY, msg or ["AMDGPUHealthy=False"], gpus_ok=ok, gpus_seen=seen, age_s=age)
+    else:
+        return Verdict(UNKNOWN, msg or ["AMDGPUHealthy=Unknown"], gpus_ok=ok, gpus_seen=seen, age_s=age)
+    if counts and expected_gpus and seen < expected_gpus:
+        missing = f"{seen} of {expected_gpus} GPUs visible to amd-smi"
+        if not any(missing in r for r in v.reasons):
+            v.reasons.insert(0, missing)
+        v.state = UNHEALTHY
+    return v
 
 
 def parse_annotation(raw: Optional[str]) -> Optional[Dict[str, Any]]:

@@ -201,3 +201,14 @@ def scan_items(items: Iterable[Mapping[str, Any]], result: Optional[ScanResult] 
 def primary_gpu_count(extras: NodeExtras, source: str = "capacity") -> int:
     table = extras.capacity if source == "capacity" else extras.allocatable
     return table.get(PRIMARY_GPU_KEY, 0)
+
+
+def expected_gpu_count(extras: NodeExtras) -> int:
+    """How many ``amd.com/gpu`` the node's agent must see: the larger of capacity and allocatable.
+
+    Capacity is what the ROCm device plugin registered (the reference's GPU-node definition,
+    ``check-gpu-node.py:181-201``); allocatable can only be lower (the plugin marked a GPU
+    unhealthy), and a GPU the plugin still counts but amd-smi no longer sees is missing either way.
+    Independent of ``--gpu-source``, which decides what the report *shows*."""
+    return max(extras.capacity.get(PRIMARY_GPU_KEY, 0), extras.allocatable.get(PRIMARY_GPU_KEY, 0))
+

@@ -174,15 +174,77 @@ def test_condition_roundtrip():
 
 
 def test_cli_condition_path_and_reeval(run_cli, mock_cluster, tmp_path):
-    # condition says healthy, but the report would fail a stricter --xgmi-links 8 re-evaluation
+    # condition says healthy, but the report fails a stricter --xgmi-links 8: non-default checker
+    # thresholds re-evaluate the annotation by themselves (the condition cannot honour them)
     rep8 = fixtures.mi355x_probe_report("a", gpus=8)
     cond = fixtures.health_condition(rep8, 8)
     nodes = [fixtures.realistic_node("a", annotations=fixtures.health_annotation(rep8), extra_conditions=[cond])]
     kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc, "--json"])
+    assert p.returncode == 0 and p.stderr == ""  # condition path: the agent's verdict
     p = run_cli(["--kubeconfig", kc, "--json", "--xgmi-links", "8"])
-    assert p.returncode == 0  # condition path: the agent's verdict
+    assert p.returncode == 3 and p.stderr == ""
     p = run_cli(["--kubeconfig", kc, "--json", "--xgmi-links", "8", "--health-reeval"])
     assert p.returncode == 3  # re-evaluated with the checker's thresholds
+
+
+def test_cli_custom_thresholds_without_annotation_warn(run_cli, mock_cluster, tmp_path):
+    rep8 = fixtures.mi355x_probe_report("a", gpus=8)
+    nodes = [fixtures.realistic_node("a", extra_conditions=[fixtures.health_condition(rep8, 8)])]
+    kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc, "--json", "--xgmi-links", "8"])
+    assert p.returncode == 0 and json.loads(p.stdout)["ready_nodes"] == 1
+    assert "--xgmi-links 8" in p.stderr and "not applied" in p.stderr and "a" in p.stderr
+
+
+def _seven_of_eight_cluster(mock_cluster, tmp_path, with_annotation=True):
+    """VERDICT r1 scenario: amd.com/gpu capacity 8, amd-smi on the node sees 7, and the agent (which
+    did not know the node's count) published AMDGPUHealthy=True for its 7 healthy GPUs."""
+    rep7 = fixtures.mi355x_probe_report("n7", gpus=7)
+    cond = fixtures.health_condition(rep7, 0)
+    assert cond["status"] == "True" and cond["message"] == "7/7 MI355X GPUs healthy"
+    ann = fixtures.health_annotation(rep7) if with_annotation else None
+    nodes = [fixtures.realistic_node("n7", gpu_count=8, annotations=ann, extra_conditions=[cond])]
+    return _cluster(mock_cluster, tmp_path, nodes)
+
+
+@pytest.mark.parametrize("flags", [[], ["--mi355x"], ["--health-reeval"], ["--health-policy", "require"]])
+def test_cli_missing_gpu_is_not_ready_on_every_path(run_cli, mock_cluster, tmp_path, flags):
+    kc = _seven_of_eight_cluster(mock_cluster, tmp_path)
+    p = run_cli(["--kubeconfig", kc, "--json"] + flags)
+    assert p.returncode == 3, (flags, p.stdout, p.stderr)
+    assert json.loads(p.stdout)["nodes"][0]["ready"] is False
+
+
+def test_cli_missing_gpu_condition_only_extended_json(run_cli, mock_cluster, tmp_path):
+    kc = _seven_of_eight_cluster(mock_cluster, tmp_path, with_annotation=False)
+    p = run_cli(["--kubeconfig", kc, "--json-extended"])
+    assert p.returncode == 3
+    h = json.loads(p.stdout)["mi355x"]["nodes"][0]["health"]
+    assert h["state"] == "unhealthy" and h["gpus_seen"] == 7 and h["gpus_ok"] == 7
+    assert h["reasons"][0] == "7 of 8 GPUs visible to amd-smi"
+
+
+def test_condition_message_counts_roundtrip():
+    now = 1_800_000_000.0
+    for r, exp_state in ((rep(ts=now), H.HEALTHY), (rep(ts=now, gpu0={"ecc_deferred": 2}), H.DEGRADED),
+                         (rep(ts=now, gpu5={"ecc_uncorrectable": 3}), H.UNHEALTHY)):
+        v = H.evaluate_report(r, 8, now=now)
+        c = H.condition_for(v, now=now)
+        assert H.parse_condition_counts(c["message"]) == (v.gpus_ok, v.gpus_seen)
+        back = H.verdict_from_condition((c["status"], c["reason"], c["message"], now), 900, now, expected_gpus=8)
+        assert back.state == exp_state and (back.gpus_ok, back.gpus_seen) == (v.gpus_ok, v.gpus_seen)
+        assert back.reasons == v.reasons or back.reasons == ["; ".join(v.reasons)]
+    # an older agent's message carries no counts: nothing to cross-check, the verdict stands
+    assert H.parse_condition_counts("gpu3: 2 uncorrectable ECC errors") is None
+    v = H.verdict_from_condition(("True", "MI355XHealthy", "all good", now), 900, now, expected_gpus=8)
+    assert v.state == H.HEALTHY
+    # more GPUs seen than registered (device plugin lagging) is not a failure
+    c = H.condition_for(H.evaluate_report(rep(ts=now), 0, now=now), now=now)
+    assert H.verdict_from_condition((c["status"], c["reason"], c["message"], now), 900, now, 4).state == H.HEALTHY
+    # probe failure: no counts in the message
+    u = H.condition_for(H.evaluate_report(rep(ts=now, error="AMDSMI_STATUS_DRIVER_NOT_LOADED"), 8, now=now), now=now)
+    assert u["message"] == "probe failed: AMDSMI_STATUS_DRIVER_NOT_LOADED"
 
 
 def test_cli_unhealthy_condition_without_annotation(run_cli, mock_cluster, tmp_path):
