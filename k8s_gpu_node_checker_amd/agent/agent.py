@@ -233,9 +233,12 @@ class Agent:
         for d in run:
             box: Dict[str, Any] = {}
 
-            def work(d: int = d, box: Dict[str, Any] = box) -> None:
+            # the partition's memory share comes from amd-smi (NPS mode); CUs and VRAM from HIP
+            part = (entries.get(d) or {}).get("memory_partition")
+
+            def work(d: int = d, box: Dict[str, Any] = box, part: Any = part) -> None:
                 try:
-                    box["res"] = diag.run(self.diag_level, d)
+                    box["res"] = diag.run(self.diag_level, d, memory_partition=part)
                 except Exception as e:  # a broken library or device: a failed test, not a dead agent
                     box["res"] = {"run": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
             t = threading.Thread(target=work, name=f"diag-gpu{d}", daemon=True)

@@ -232,6 +232,9 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str],
             if isinstance(res, dict) and res.get("pass") is False:
                 detail = res.get("detail") or ""
                 fail.append(f"gpu{idx}: diag {test} failed" + (f" ({detail})" if detail else ""))
+            elif isinstance(res, dict) and res.get("degraded"):  # 85-95 % of its reference rate (ops/diag.py)
+                detail = res.get("detail") or ""
+                warn.append(f"gpu{idx}: diag {test} slow" + (f" ({detail})" if detail else ""))
     return fail, warn
 
 

@@ -4,9 +4,9 @@ Each test returns a dict that the node agent folds into its probe report
 under ``gpus[i].diag.<test>`` and that :func:`models.health.evaluate_gpu`
 turns into a failure when ``pass`` is false.
 
-Thresholds are deliberately conservative fractions of what a healthy MI355X
-delivers (numbers in ``profiles/``): they flag a GPU that is broken or badly
-throttled, not one that is a few percent off.
+Rate tests are judged against the measured rates of a healthy MI355X, scaled to
+the device's partition (see the threshold block below): under 85 % fails, 85-95 %
+passes as *degraded*.
 
 The library is *required* on a GPU box: a missing build raises
 :class:`~k8s_gpu_node_checker_amd.ops.native.NativeUnavailable` instead of
@@ -21,23 +21,108 @@ from typing import Any, Dict, Optional
 
 from .native import NativeUnavailable, load_cdll
 
-# Pass thresholds vs a healthy MI355X (measured: profiles/gemm_explore_mi355x.json,
-# profiles/hbm_explore_mi355x.json): GEMM 4096^3 ~1200 / 8192^3 ~1370 TFLOP/s bf16, HBM copy ~6.6 TB/s,
-# read ~7.0 TB/s.  Device-to-device DVFS spread is ~10 %; these flag broken or badly throttled parts.
-GEMM_MIN_TFLOPS = 600.0       # bf16 MFMA GEMM (4096^3 quick / 8192^3 deep)
+# --- Pass / degraded thresholds --------------------------------------------------------------------
+# Every rate test is judged against the *reference rate* of a healthy, unpartitioned MI355X (256 CUs,
+# SPX/NPS1, 1400 W cap): the lower of (a) the median of a sustained soak and (b) what one cold run
+# measures, since the agent runs the suite once per --diag-interval on an idle (clocked-down) GPU:
+#   8192^3 (level 2): profiles/soak_level2_5min_mi355x.json, 589 rounds of the full level-2 suite in 5 min
+#       gemm 1208 (min 1192), gemm_fp8 2343 (min 2110), hbm copy 6.55 / read 6.98 TB/s, mfma bf16 1901,
+#       fp8 1940, mxfp8 4326, mxfp4 7610 TFLOP/s, host link h2d 57.2 / d2h 56.8 GB/s
+#   4096^3 (level 1): profiles/soak_level1_mi355x.json, 970 rounds in 2 min: gemm 1329 warm but 1207-1226
+#       in single cold runs (profiles/bench/*.json probe.diag), gemm_fp8 2274 warm / 2098-2108 cold,
+#       hbm copy 6.49 / read 6.96 TB/s, mfma bf16 1978, fp8 2009, mxfp8 4493, mxfp4 7834
+# A result below FAIL_FRACTION of its reference fails (a GPU at 55 % clock or power is unhealthy); one
+# between FAIL_FRACTION and DEGRADED_FRACTION passes as *degraded* (a warning on the node, still Ready).
+# The 85 % floor sits under every soak minimum (worst: gemm_fp8 8192^3 at 90 % of its median) and under
+# the ~10 % box-to-box DVFS spread; a rate that lands below 95 % is measured a second time before it is
+# reported (best of two), so one noisy sample does not flap the node's verdict.
+#
+# Partitions: the reference rates are scaled by the share of the physical GPU the HIP device is.
+#   compute (GEMM, MFMA burn-in):   cus / 256       (CPX: 32 CUs -> 1/8)
+#   memory (HBM copy / read):       min(mem_bytes / 288 GiB, 1/NPS, cus / 256)
+#   host link (PCIe):               cus / 256       (every partition of one GPU shares its x16 link, and the
+#                                                    agent runs them concurrently)
+# The partition scaling is proportional, not measured (no partitioned MI355X was available): it is the
+# lenient bound, so a healthy partition never fails; a partitioned GPU's degraded band is advisory.
+FAIL_FRACTION = 0.85
+DEGRADED_FRACTION = 0.95
+FULL_CUS = 256
+FULL_MEM_BYTES = 288 << 30
+REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
+    "gemm": {4096: 1220.0, 8192: 1208.0},          # bf16 MFMA GEMM, TFLOP/s
+    "gemm_fp8": {4096: 2100.0, 8192: 2343.0},      # MX-fp8 GEMM, TFLOP/s
+    "hbm": {"copy_tbs": 6.49, "read_tbs": 6.96},   # 16-byte copy (read + write bytes counted) / read, TB/s
+    "mfma": {"bf16": 1901.0, "fp8": 1940.0, "mxfp8": 4326.0, "mxfp4": 7610.0},  # register-resident burn-in
+    "host_link": {"h2d_gbps": 57.0, "d2h_gbps": 56.8},  # pinned copies over PCIe Gen5 x16
+}
 GEMM_MAX_REL_ERR = 2e-3       # vs fp32 reference; bf16 inputs are exact in fp32, so ~1e-5 is typical
-GEMM_FP8_MIN_TFLOPS = 1200.0  # MX-fp8 GEMM (measured 2100 @4096^3, 2590 @8192^3, profiles/gemm_fp8_mi355x.jsonl)
 GEMM_FP8_MAX_ERR = 4e-5       # |C - ref| / sum|a*b|: the MX MFMA's own accumulation error is <= 1.6e-5
-HBM_MIN_COPY_TBS = 4.0        # 16-byte copy (read + write bytes counted)
-HBM_MIN_READ_TBS = 4.5
 MEMTEST_MAX_ERRORS = 0
-# Matrix-core burn-in (register-resident MFMA loops, random {-1,0,1} operands; measured
-# profiles/mfma_lab_mi355x.jsonl: bf16 1687, fp8 1803, MX-fp8 4027, MX-fp4 7171 TFLOP/s dense)
 MFMA_KINDS = ("bf16", "fp8", "mxfp8", "mxfp4")
-MFMA_MIN_TFLOPS = {"bf16": 1000.0, "fp8": 1000.0, "mxfp8": 2400.0, "mxfp4": 4300.0}
 P2P_MIN_FRACTION_OF_MEDIAN = 0.5  # a GPU pair slower than half the node's median pair: suspect link
-HOST_LINK_MIN_GBPS = 28.0     # PCIe Gen5 x16 host link, pinned copies: measured 56.8 / 56.7 GB/s h2d / d2h
-                              # (profiles/diag_mi355x.json); a Gen4 or x8 link lands at about half
+
+
+class Scale:
+    """Share of a full MI355X that one HIP device is (1.0 / 1.0 unpartitioned)."""
+
+    def __init__(self, compute: float = 1.0, memory: float = 1.0):
+        self.compute = compute
+        self.memory = memory
+
+    @classmethod
+    def of(cls, cus: Optional[int] = None, mem_bytes: Optional[int] = None,
+           memory_partition: Optional[str] = None) -> "Scale":
+        c = min(1.0, cus / FULL_CUS) if isinstance(cus, int) and cus > 0 else 1.0
+        m = c
+        if isinstance(mem_bytes, int) and mem_bytes > 0:
+            m = min(m, mem_bytes / FULL_MEM_BYTES)
+        if isinstance(memory_partition, str) and memory_partition.upper().startswith("NPS"):
+            try:
+                m = min(m, 1.0 / max(1, int(memory_partition[3:])))
+            except ValueError:
+                pass
+        return cls(c, min(1.0, m))
+
+    def to_dict(self) -> Dict[str, float]:
+        return {"compute": round(self.compute, 4), "memory": round(self.memory, 4)}
+
+
+FULL = Scale()
+
+
+def judge_rate(value: float, expected: float) -> str:
+    """``pass``, ``degraded`` or ``fail`` for a measured rate against its (scaled) reference."""
+    if value < FAIL_FRACTION * expected:
+        return "fail"
+    if value < DEGRADED_FRACTION * expected:
+        return "degraded"
+    return "pass"
+
+
+def _rated(res: Dict[str, Any], rates: Dict[str, float], expected: Dict[str, float], unit: str,
+           numerics_ok: bool = True, numerics_detail: str = "") -> Dict[str, Any]:
+    """Fold rate verdicts (and a numerics verdict) into a test result: ``pass``, ``degraded``,
+    ``fraction`` (worst rate / reference), ``expect`` and a human ``detail``."""
+    worst, problems, slow = 1e9, [], []
+    for k, v in rates.items():
+        exp = expected[k]
+        frac = v / exp if exp > 0 else 1.0
+        worst = min(worst, frac)
+        j = judge_rate(v, exp)
+        txt = f"{k} {v:.3g} {unit} = {frac:.0%} of {exp:.3g}"
+        if j == "fail":
+            problems.append(txt)
+        elif j == "degraded":
+            slow.append(txt)
+    if not numerics_ok:
+        problems.insert(0, numerics_detail)
+    res["pass"] = not problems
+    res["degraded"] = bool(slow) and not problems
+    res["fraction"] = round(worst, 3)
+    res["expect"] = {k: round(v, 3) for k, v in expected.items()}
+    res["detail"] = "; ".join(problems or slow)
+    return res
+
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -139,39 +224,47 @@ def gemm_fp4_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int,
     _check(lib().diag_gemm_fp4_launch(a_ptr, bt_ptr, c_ptr, m, n, k, stream))
 
 
-def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, samples: int = 4096) -> Dict[str, Any]:
+def _ref(test: str, key: Any, scale: float) -> float:
+    table = REFERENCE_RATES[test]
+    if key not in table:  # a size without its own measurement: the nearest measured one
+        key = min(table, key=lambda k: abs(k - key))
+    return table[key] * scale
+
+
+def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, samples: int = 4096,
+         scale: Scale = FULL) -> Dict[str, Any]:
     tf, err, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     t0 = time.perf_counter()
     _check(lib().diag_gemm_bf16(device, size, size, size, warmup, iters, samples, ctypes.byref(tf),
                                 ctypes.byref(err), ctypes.byref(ms)))
-    ok = tf.value >= GEMM_MIN_TFLOPS and err.value <= GEMM_MAX_REL_ERR
-    return {"pass": ok, "tflops": round(tf.value, 1), "max_rel_err": err.value, "ms_per_gemm": round(ms.value, 4),
-            "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3),
-            "detail": "" if ok else f"{tf.value:.0f} TFLOP/s, rel err {err.value:.2e}"}
+    res = {"tflops": round(tf.value, 1), "max_rel_err": err.value, "ms_per_gemm": round(ms.value, 4),
+           "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3)}
+    return _rated(res, {"tflops": tf.value}, {"tflops": _ref("gemm", size, scale.compute)}, "TFLOP/s",
+                  err.value <= GEMM_MAX_REL_ERR, f"rel err {err.value:.2e} > {GEMM_MAX_REL_ERR:g}")
 
 
 def gemm_fp8(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20,
-             samples: int = 4096) -> Dict[str, Any]:
+             samples: int = 4096, scale: Scale = FULL) -> Dict[str, Any]:
     """MX-fp8 GEMM burn-in: rate and sampled fp64-reference error (normalised by sum|a*b|)."""
     tf, err, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     t0 = time.perf_counter()
     _check(lib().diag_gemm_fp8(device, size, size, size, warmup, iters, samples, ctypes.byref(tf),
                                ctypes.byref(err), ctypes.byref(ms)))
-    ok = tf.value >= GEMM_FP8_MIN_TFLOPS and err.value <= GEMM_FP8_MAX_ERR
-    return {"pass": ok, "tflops": round(tf.value, 1), "max_err_over_mag": err.value, "ms_per_gemm": round(ms.value, 4),
-            "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3),
-            "detail": "" if ok else f"{tf.value:.0f} TFLOP/s, err {err.value:.2e}"}
+    res = {"tflops": round(tf.value, 1), "max_err_over_mag": err.value, "ms_per_gemm": round(ms.value, 4),
+           "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3)}
+    return _rated(res, {"tflops": tf.value}, {"tflops": _ref("gemm_fp8", size, scale.compute)}, "TFLOP/s",
+                  err.value <= GEMM_FP8_MAX_ERR, f"err {err.value:.2e} > {GEMM_FP8_MAX_ERR:g}")
 
 
-def hbm(device: int = 0, gib: float = 4.0, iters: int = 10) -> Dict[str, Any]:
+def hbm(device: int = 0, gib: float = 4.0, iters: int = 10, scale: Scale = FULL) -> Dict[str, Any]:
     c, r, w = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     t0 = time.perf_counter()
     _check(lib().diag_hbm_bandwidth(device, int(gib * (1 << 30)), iters, ctypes.byref(c), ctypes.byref(r),
                                     ctypes.byref(w)))
-    ok = c.value >= HBM_MIN_COPY_TBS and r.value >= HBM_MIN_READ_TBS
-    return {"pass": ok, "copy_tbs": round(c.value, 3), "read_tbs": round(r.value, 3), "write_tbs": round(w.value, 3),
-            "gib": gib, "wall_s": round(time.perf_counter() - t0, 3),
-            "detail": "" if ok else f"copy {c.value:.2f} TB/s, read {r.value:.2f} TB/s"}
+    res = {"copy_tbs": round(c.value, 3), "read_tbs": round(r.value, 3), "write_tbs": round(w.value, 3),
+           "gib": gib, "wall_s": round(time.perf_counter() - t0, 3)}
+    exp = {k: v * scale.memory for k, v in REFERENCE_RATES["hbm"].items()}
+    return _rated(res, {"copy_tbs": c.value, "read_tbs": r.value}, exp, "TB/s")
 
 
 def memtest(device: int = 0, gib: float = 8.0, passes: int = 1, seed: int = 0x5EED) -> Dict[str, Any]:
@@ -188,32 +281,35 @@ def memtest(device: int = 0, gib: float = 8.0, passes: int = 1, seed: int = 0x5E
     return res
 
 
-def mfma_burn(device: int = 0, kinds=MFMA_KINDS, iters: int = 2000, reps: int = 5) -> Dict[str, Any]:
+def mfma_burn(device: int = 0, kinds=MFMA_KINDS, iters: int = 2000, reps: int = 5,
+              scale: Scale = FULL) -> Dict[str, Any]:
     """Every matrix-core precision of the MI355X: dense TFLOP/s and exact-result errors per kind."""
     t0 = time.perf_counter()
     rows: Dict[str, Any] = {}
-    problems = []
+    rates: Dict[str, float] = {}
+    wrong = []
     for kind in kinds:
         tf, errs = ctypes.c_double(), ctypes.c_ulonglong()
         _check(lib().diag_mfma_burn(device, MFMA_KINDS.index(kind), iters, reps, ctypes.byref(tf), ctypes.byref(errs)))
         rows[kind] = {"tflops": round(tf.value, 1), "errors": errs.value}
+        rates[kind] = tf.value
         if errs.value:
-            problems.append(f"{kind}: {errs.value} wrong results")
-        if tf.value < MFMA_MIN_TFLOPS[kind]:
-            problems.append(f"{kind}: {tf.value:.0f} TFLOP/s")
-    return {"pass": not problems, "kinds": rows, "wall_s": round(time.perf_counter() - t0, 3),
-            "detail": "; ".join(problems)}
+            wrong.append(f"{kind}: {errs.value} wrong results")
+    exp = {k: REFERENCE_RATES["mfma"][k] * scale.compute for k in kinds}
+    return _rated({"kinds": rows, "wall_s": round(time.perf_counter() - t0, 3)}, rates, exp, "TFLOP/s",
+                  not wrong, "; ".join(wrong))
 
 
-def host_link(device: int = 0, mib: int = 256, iters: int = 5) -> Dict[str, Any]:
-    """Pinned host <-> device bandwidth over the GPU's PCIe link (GB/s each way)."""
+def host_link(device: int = 0, mib: int = 256, iters: int = 5, scale: Scale = FULL) -> Dict[str, Any]:
+    """Pinned host <-> device bandwidth over the GPU's PCIe link (GB/s each way).  A Gen4 or x8 link
+    lands at about half the Gen5 x16 reference and fails."""
     h2d, d2h = ctypes.c_double(), ctypes.c_double()
     t0 = time.perf_counter()
     _check(lib().diag_host_link(device, mib << 20, iters, ctypes.byref(h2d), ctypes.byref(d2h)))
-    ok = h2d.value >= HOST_LINK_MIN_GBPS and d2h.value >= HOST_LINK_MIN_GBPS
-    return {"pass": ok, "h2d_gbps": round(h2d.value, 1), "d2h_gbps": round(d2h.value, 1),
-            "wall_s": round(time.perf_counter() - t0, 3),
-            "detail": "" if ok else f"h2d {h2d.value:.1f} GB/s, d2h {d2h.value:.1f} GB/s"}
+    res = {"h2d_gbps": round(h2d.value, 1), "d2h_gbps": round(d2h.value, 1),
+           "wall_s": round(time.perf_counter() - t0, 3)}
+    exp = {k: v * scale.compute for k, v in REFERENCE_RATES["host_link"].items()}
+    return _rated(res, {"h2d_gbps": h2d.value, "d2h_gbps": d2h.value}, exp, "GB/s")
 
 
 def p2p_copy(src: int, dst: int, mib: int = 256, iters: int = 5) -> Dict[str, Any]:
@@ -255,33 +351,75 @@ LEVELS = {
 }
 
 
-def run(level: int = 1, device: int = 0) -> Dict[str, Dict[str, Any]]:
-    """Run the diagnostics of ``level`` on ``device`` (1 = ~1 s quick check, 2 = deep)."""
+def device_scale(device: int = 0, memory_partition: Optional[str] = None) -> Scale:
+    """The :class:`Scale` of HIP ``device`` (CU count and memory from HIP; ``memory_partition`` from
+    amd-smi when the caller has it)."""
+    info = device_info(device)
+    return Scale.of(info.get("cus"), info.get("mem_bytes"), memory_partition)
+
+
+def _one(test: str, device: int, scale: Scale) -> Dict[str, Any]:
+    if test == "gemm_quick":
+        return gemm(device, size=4096, warmup=2, iters=10, samples=1024, scale=scale)
+    if test == "gemm_fp8_quick":
+        return gemm_fp8(device, size=4096, warmup=2, iters=10, samples=1024, scale=scale)
+    if test == "gemm_fp8":
+        return gemm_fp8(device, scale=scale)
+    if test == "hbm_quick":
+        return hbm(device, gib=2.0, iters=5, scale=scale)
+    if test == "gemm":
+        return gemm(device, scale=scale)
+    if test == "hbm":
+        return hbm(device, scale=scale)
+    if test == "memtest":
+        return memtest(device)
+    if test == "mfma":
+        return mfma_burn(device, scale=scale)
+    if test == "host_link":
+        return host_link(device, scale=scale)
+    raise ValueError(f"unknown diagnostic {test!r}")
+
+
+def _slow_only(res: Dict[str, Any]) -> bool:
+    """Below the degraded line on rate alone (numerics fine): worth a second measurement."""
+    return (res.get("degraded") or not res.get("pass")) and res.get("fraction", 1.0) < DEGRADED_FRACTION \
+        and "wrong results" not in res.get("detail", "") and "err " not in res.get("detail", "")
+
+
+def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
+        memory_partition: Optional[str] = None) -> Dict[str, Dict[str, Any]]:
+    """Run the diagnostics of ``level`` on ``device`` (1 = ~1 s quick check, 2 = deep).
+
+    ``scale`` defaults to the device's own share of a full MI355X (:func:`device_scale`).  A rate that
+    lands below the degraded line is measured once more and the better of the two is reported."""
     out: Dict[str, Dict[str, Any]] = {}
-    for test in LEVELS.get(level, ()):
+    tests = LEVELS.get(level, ())
+    if tests and scale is None:
         try:
-            if test == "gemm_quick":
-                out["gemm"] = gemm(device, size=4096, warmup=2, iters=10, samples=1024)
-            elif test == "gemm_fp8_quick":
-                out["gemm_fp8"] = gemm_fp8(device, size=4096, warmup=2, iters=10, samples=1024)
-            elif test == "gemm_fp8":
-                out["gemm_fp8"] = gemm_fp8(device)
-            elif test == "hbm_quick":
-                out["hbm"] = hbm(device, gib=2.0, iters=5)
-            elif test == "gemm":
-                out["gemm"] = gemm(device)
-            elif test == "hbm":
-                out["hbm"] = hbm(device)
-            elif test == "memtest":
-                out["memtest"] = memtest(device)
-            elif test == "mfma":
-                out["mfma"] = mfma_burn(device)
-            elif test == "host_link":
-                out["host_link"] = host_link(device)
+            scale = device_scale(device, memory_partition)
+        except NativeUnavailable:
+            raise
+        except Exception:
+            scale = FULL
+    scale = scale or FULL
+    for test in tests:
+        name = test.replace("_quick", "")
+        try:
+            res = _one(test, device, scale)
+            if _slow_only(res):
+                again = _one(test, device, scale)
+                again["retried"] = True
+                if again.get("fraction", 0.0) > res.get("fraction", 0.0):
+                    res = again
+                else:
+                    res["retried"] = True
+            if scale is not FULL and (scale.compute < 1.0 or scale.memory < 1.0):
+                res["scale"] = scale.to_dict()
+            out[name] = res
         except NativeUnavailable:
             raise
         except Exception as e:  # a failing diagnostic is a verdict, not a crash
-            out[test.replace("_quick", "")] = {"pass": False, "detail": str(e)[:200]}
+            out[name] = {"pass": False, "detail": str(e)[:200]}
     return out
 
 

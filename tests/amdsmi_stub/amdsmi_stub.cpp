@@ -1,0 +1,416 @@
+// Replay stub of libamd_smi for host-side sanitizer builds of csrc/probe/probe.cpp (tests/test_sanitizers.py).
+//
+// Compiled against the real <amd_smi/amdsmi.h>, so every signature the probe links against is checked
+// by the compiler.  The values come from a flat "key=value" scenario file named by AMDSMI_STUB_SCENARIO
+// (the test writes it from a recorded MI355X probe, profiles/probe_cli_mi355x.jsonl):
+//
+//   init_status=0|10|34              amdsmi_init result (NO_PERM, DRIVER_NOT_LOADED, ...)
+//   sockets_status=0                 amdsmi_get_socket_handles result
+//   gpus=N                           GPU processors (one socket each)
+//   gpu.<i>.<field>=<value>          one recorded field of GPU i (names as in the probe's JSON)
+//   gpu.<i>.asic_status=<status>     make amdsmi_get_gpu_asic_info fail for GPU i
+//   gpu.<i>.nprocs=<n>               synthesise n processes (exercises the probe's 64-entry cap)
+//
+// Output buffers are written exactly as the real library documents (length-checked), so a probe that
+// passes a short buffer or reads past what was written shows up under ASan.
+#include <amd_smi/amdsmi.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct Gpu {
+  std::map<std::string, std::string> f;
+  bool has(const char* k) const { return f.count(k) != 0; }
+  std::string s(const char* k, const char* d = "") const {
+    auto it = f.find(k);
+    return it == f.end() ? d : it->second;
+  }
+  uint64_t u(const char* k, uint64_t d = 0) const {
+    auto it = f.find(k);
+    return it == f.end() ? d : strtoull(it->second.c_str(), nullptr, 0);
+  }
+};
+
+struct World {
+  bool loaded = false;
+  int init_status = 0;
+  int sockets_status = 0;
+  bool open = false;
+  std::vector<Gpu> gpus;
+};
+
+World g_world;
+
+void load() {
+  if (g_world.loaded) return;
+  g_world.loaded = true;
+  const char* path = getenv("AMDSMI_STUB_SCENARIO");
+  if (!path) return;
+  FILE* fp = fopen(path, "r");
+  if (!fp) return;
+  char line[4096];
+  while (fgets(line, sizeof line, fp)) {
+    std::string l(line);
+    while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+    const size_t eq = l.find('=');
+    if (eq == std::string::npos) continue;
+    const std::string k = l.substr(0, eq), v = l.substr(eq + 1);
+    if (k == "init_status") {
+      g_world.init_status = atoi(v.c_str());
+    } else if (k == "sockets_status") {
+      g_world.sockets_status = atoi(v.c_str());
+    } else if (k == "gpus") {
+      g_world.gpus.resize(static_cast<size_t>(atoi(v.c_str())));
+    } else if (k.rfind("gpu.", 0) == 0) {
+      const size_t dot = k.find('.', 4);
+      if (dot == std::string::npos) continue;
+      const size_t i = static_cast<size_t>(atoi(k.substr(4, dot - 4).c_str()));
+      if (i < g_world.gpus.size()) g_world.gpus[i].f[k.substr(dot + 1)] = v;
+    }
+  }
+  fclose(fp);
+}
+
+const Gpu* gpu_of(amdsmi_processor_handle h) {
+  for (const Gpu& g : g_world.gpus)
+    if (static_cast<const void*>(&g) == h) return &g;
+  return nullptr;
+}
+
+// copy a string into a caller buffer of `len` bytes, NUL-terminated and truncated like strncpy + term
+void put(char* dst, size_t len, const std::string& v) {
+  if (!len) return;
+  const size_t n = v.size() < len - 1 ? v.size() : len - 1;
+  memcpy(dst, v.data(), n);
+  dst[n] = '\0';
+}
+
+#define GPU_OR_FAIL(h)                                   \
+  const Gpu* g = gpu_of(h);                              \
+  if (!g_world.open) return AMDSMI_STATUS_NOT_INIT;      \
+  if (!g) return AMDSMI_STATUS_INVAL
+
+#define FIELD_OR_NA(k) \
+  if (!g->has(k)) return AMDSMI_STATUS_NOT_SUPPORTED
+
+}  // namespace
+
+extern "C" {
+
+amdsmi_status_t amdsmi_init(uint64_t) {
+  load();
+  if (g_world.init_status) return static_cast<amdsmi_status_t>(g_world.init_status);
+  g_world.open = true;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_shut_down(void) {
+  g_world.open = false;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_status_code_to_string(amdsmi_status_t status, const char** status_string) {
+  switch (status) {
+    case AMDSMI_STATUS_SUCCESS: *status_string = "AMDSMI_STATUS_SUCCESS"; break;
+    case AMDSMI_STATUS_NO_PERM: *status_string = "AMDSMI_STATUS_NO_PERM"; break;
+    case AMDSMI_STATUS_DRIVER_NOT_LOADED: *status_string = "AMDSMI_STATUS_DRIVER_NOT_LOADED"; break;
+    case AMDSMI_STATUS_NOT_SUPPORTED: *status_string = "AMDSMI_STATUS_NOT_SUPPORTED"; break;
+    default: *status_string = "AMDSMI_STATUS_UNKNOWN_ERROR";
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_lib_version(amdsmi_version_t* version) {
+  version->major = 26;
+  version->minor = 2;
+  version->release = 1;
+  version->build = "26.2.1-stub";
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_socket_handles(uint32_t* socket_count, amdsmi_socket_handle* socket_handles) {
+  if (!g_world.open) return AMDSMI_STATUS_NOT_INIT;
+  if (g_world.sockets_status) return static_cast<amdsmi_status_t>(g_world.sockets_status);
+  const uint32_t n = static_cast<uint32_t>(g_world.gpus.size());
+  if (socket_handles) {
+    const uint32_t cap = *socket_count < n ? *socket_count : n;
+    for (uint32_t i = 0; i < cap; ++i) socket_handles[i] = &g_world.gpus[i].f;  // any distinct non-null
+    *socket_count = cap;
+  } else {
+    *socket_count = n;
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle socket_handle, uint32_t* processor_count,
+                                             amdsmi_processor_handle* processor_handles) {
+  for (Gpu& g : g_world.gpus) {
+    if (static_cast<void*>(&g.f) != socket_handle) continue;
+    if (processor_handles && *processor_count >= 1) processor_handles[0] = &g;
+    *processor_count = 1;
+    return AMDSMI_STATUS_SUCCESS;
+  }
+  return AMDSMI_STATUS_INVAL;
+}
+
+amdsmi_status_t amdsmi_get_processor_type(amdsmi_processor_handle processor_handle, processor_type_t* processor_type) {
+  GPU_OR_FAIL(processor_handle);
+  (void)g;
+  *processor_type = AMDSMI_PROCESSOR_TYPE_AMD_GPU;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_device_bdf(amdsmi_processor_handle processor_handle, amdsmi_bdf_t* bdf) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("bdf");
+  unsigned dom = 0, bus = 0, dev = 0, fn = 0;
+  if (sscanf(g->s("bdf").c_str(), "%x:%x:%x.%x", &dom, &bus, &dev, &fn) != 4) return AMDSMI_STATUS_INVAL;
+  bdf->as_uint = 0;
+  bdf->domain_number = dom;
+  bdf->bus_number = bus;
+  bdf->device_number = dev;
+  bdf->function_number = fn;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_device_uuid(amdsmi_processor_handle processor_handle, unsigned int* uuid_length,
+                                           char* uuid) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("uuid");
+  if (*uuid_length < AMDSMI_GPU_UUID_SIZE) return AMDSMI_STATUS_INSUFFICIENT_SIZE;
+  put(uuid, *uuid_length, g->s("uuid"));
+  *uuid_length = static_cast<unsigned>(g->s("uuid").size());
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle processor_handle, amdsmi_asic_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  if (g->has("asic_status")) return static_cast<amdsmi_status_t>(g->u("asic_status"));
+  memset(info, 0, sizeof *info);
+  put(info->market_name, sizeof info->market_name, g->s("market_name"));
+  info->device_id = g->u("device_id", 0);
+  const std::string gfx = g->s("gfx");  // "gfx950" -> 0x950
+  info->target_graphics_version = gfx.rfind("gfx", 0) == 0 ? strtoull(gfx.c_str() + 3, nullptr, 16) : UINT64_MAX;
+  info->num_of_compute_units = g->has("cus") ? static_cast<uint32_t>(g->u("cus")) : UINT32_MAX;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_board_info(amdsmi_processor_handle processor_handle, amdsmi_board_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("product_name");
+  memset(info, 0, sizeof *info);
+  put(info->product_name, sizeof info->product_name, g->s("product_name"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_vbios_info(amdsmi_processor_handle processor_handle, amdsmi_vbios_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("vbios_name");
+  memset(info, 0, sizeof *info);
+  put(info->name, sizeof info->name, g->s("vbios_name"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_vram_info(amdsmi_processor_handle processor_handle, amdsmi_vram_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("vram_mb");
+  memset(info, 0, sizeof *info);
+  info->vram_type = static_cast<amdsmi_vram_type_t>(g->u("vram_type"));
+  info->vram_size = g->u("vram_mb");
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_total_ecc_count(amdsmi_processor_handle processor_handle, amdsmi_error_count_t* ec) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("ecc_uncorrectable");
+  memset(ec, 0, sizeof *ec);
+  ec->correctable_count = g->u("ecc_correctable");
+  ec->uncorrectable_count = g->u("ecc_uncorrectable");
+  ec->deferred_count = g->u("ecc_deferred");
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_bad_page_info(amdsmi_processor_handle processor_handle, uint32_t* num_pages,
+                                             amdsmi_retired_page_record_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("bad_pages");
+  const uint32_t n = static_cast<uint32_t>(g->u("bad_pages"));
+  if (info) {
+    const uint32_t cap = *num_pages < n ? *num_pages : n;
+    for (uint32_t i = 0; i < cap; ++i) {
+      memset(&info[i], 0, sizeof info[i]);
+      info[i].page_address = 0x1000ull * (i + 1);
+      info[i].page_size = 4096;
+    }
+    *num_pages = cap;
+  } else {
+    *num_pages = n;
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_xgmi_link_status(amdsmi_processor_handle processor_handle,
+                                                amdsmi_xgmi_link_status_t* link_status) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("xgmi");
+  memset(link_status, 0, sizeof *link_status);
+  const std::string s = g->s("xgmi");
+  const uint32_t n = s.size() < AMDSMI_MAX_NUM_XGMI_LINKS ? static_cast<uint32_t>(s.size()) : AMDSMI_MAX_NUM_XGMI_LINKS;
+  link_status->total_links = n;
+  for (uint32_t i = 0; i < n; ++i)
+    link_status->status[i] = s[i] == 'U' ? AMDSMI_XGMI_LINK_UP
+                             : s[i] == 'D' ? AMDSMI_XGMI_LINK_DOWN
+                                           : AMDSMI_XGMI_LINK_DISABLE;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle processor_handle, amdsmi_kfd_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("kfd_node");
+  memset(info, 0, sizeof *info);
+  info->kfd_id = 1000 + g->u("kfd_node");
+  info->node_id = static_cast<uint32_t>(g->u("kfd_node"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_compute_partition(amdsmi_processor_handle processor_handle, char* compute_partition,
+                                                 uint32_t len) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("compute_partition");
+  if (len < g->s("compute_partition").size() + 1) return AMDSMI_STATUS_INSUFFICIENT_SIZE;
+  put(compute_partition, len, g->s("compute_partition"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_memory_partition(amdsmi_processor_handle processor_handle, char* memory_partition,
+                                                uint32_t len) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("memory_partition");
+  if (len < g->s("memory_partition").size() + 1) return AMDSMI_STATUS_INSUFFICIENT_SIZE;
+  put(memory_partition, len, g->s("memory_partition"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_temp_metric(amdsmi_processor_handle processor_handle, amdsmi_temperature_type_t sensor_type,
+                                       amdsmi_temperature_metric_t metric, int64_t* temperature) {
+  GPU_OR_FAIL(processor_handle);
+  if (metric != AMDSMI_TEMP_CURRENT) return AMDSMI_STATUS_NOT_SUPPORTED;
+  if (sensor_type == AMDSMI_TEMPERATURE_TYPE_HOTSPOT && g->has("hotspot_c")) {
+    *temperature = static_cast<int64_t>(g->u("hotspot_c"));
+    return AMDSMI_STATUS_SUCCESS;
+  }
+  if (sensor_type == AMDSMI_TEMPERATURE_TYPE_HBM_0 && g->has("hbm_temp_c")) {
+    *temperature = static_cast<int64_t>(g->u("hbm_temp_c"));
+    return AMDSMI_STATUS_SUCCESS;
+  }
+  return AMDSMI_STATUS_NOT_SUPPORTED;
+}
+
+amdsmi_status_t amdsmi_get_pcie_info(amdsmi_processor_handle processor_handle, amdsmi_pcie_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("pcie_width");
+  memset(info, 0, sizeof *info);
+  info->pcie_metric.pcie_width = static_cast<uint16_t>(g->u("pcie_width"));
+  info->pcie_metric.pcie_speed = static_cast<uint32_t>(g->u("pcie_speed_mts"));
+  info->pcie_static.max_pcie_width = static_cast<uint16_t>(g->u("pcie_max_width"));
+  info->pcie_static.max_pcie_speed = static_cast<uint32_t>(g->u("pcie_max_speed_mts"));
+  info->pcie_metric.pcie_replay_count = g->u("pcie_replays", UINT64_MAX);
+  info->pcie_metric.pcie_l0_to_recovery_count = g->u("pcie_recoveries", UINT64_MAX);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_power_info(amdsmi_processor_handle processor_handle, amdsmi_power_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("power_w");
+  memset(info, 0, sizeof *info);
+  info->current_socket_power = static_cast<uint32_t>(g->u("power_w"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_power_cap_info(amdsmi_processor_handle processor_handle, uint32_t,
+                                          amdsmi_power_cap_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("power_cap_w");
+  memset(info, 0, sizeof *info);
+  info->power_cap = g->u("power_cap_w") * 1000000ull;  // uW, as the real library reports on Linux
+  info->default_power_cap = g->u("power_cap_default_w") * 1000000ull;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_vram_usage(amdsmi_processor_handle processor_handle, amdsmi_vram_usage_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("vram_used_mb");
+  memset(info, 0, sizeof *info);
+  info->vram_total = static_cast<uint32_t>(g->u("vram_mb"));
+  info->vram_used = static_cast<uint32_t>(g->u("vram_used_mb"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_process_list(amdsmi_processor_handle processor_handle, uint32_t* max_processes,
+                                            amdsmi_proc_info_t* list) {
+  GPU_OR_FAIL(processor_handle);
+  // "procs" = "pid:vram_mb,pid:vram_mb"; or nprocs=N synthetic entries
+  std::vector<std::pair<uint32_t, uint64_t>> procs;
+  if (g->has("nprocs")) {
+    for (uint64_t i = 0; i < g->u("nprocs"); ++i) procs.push_back({static_cast<uint32_t>(5000 + i), i});
+  } else {
+    const std::string s = g->s("procs");
+    size_t p = 0;
+    while (p < s.size()) {
+      size_t e = s.find(',', p);
+      if (e == std::string::npos) e = s.size();
+      unsigned pid = 0;
+      unsigned long long mb = 0;
+      if (sscanf(s.substr(p, e - p).c_str(), "%u:%llu", &pid, &mb) == 2) procs.push_back({pid, mb});
+      p = e + 1;
+    }
+  }
+  const uint32_t n = static_cast<uint32_t>(procs.size());
+  if (!list) {
+    *max_processes = n;
+    return AMDSMI_STATUS_SUCCESS;
+  }
+  const uint32_t cap = *max_processes < n ? *max_processes : n;
+  for (uint32_t i = 0; i < cap; ++i) {
+    memset(&list[i], 0, sizeof list[i]);
+    list[i].pid = procs[i].first;
+    list[i].memory_usage.vram_mem = procs[i].second << 20;
+  }
+  *max_processes = cap;
+  return cap < n ? AMDSMI_STATUS_OUT_OF_RESOURCES : AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_activity(amdsmi_processor_handle processor_handle, amdsmi_engine_usage_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("gfx_activity");
+  memset(info, 0, sizeof *info);
+  info->gfx_activity = static_cast<uint32_t>(g->u("gfx_activity"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_metrics_info(amdsmi_processor_handle processor_handle,
+                                            amdsmi_gpu_metrics_t* pgpu_metrics) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("gfxclk_mhz");
+  // the real library fills only what the firmware reports; the rest keeps the caller's all-ones
+  pgpu_metrics->current_gfxclks[0] = static_cast<uint16_t>(g->u("gfxclk_mhz"));
+  pgpu_metrics->current_gfxclks[1] = static_cast<uint16_t>(g->u("gfxclk_mhz"));
+  if (g->has("throttle_acc.n")) {
+    pgpu_metrics->accumulation_counter = g->u("throttle_acc.n");
+    pgpu_metrics->prochot_residency_acc = g->u("throttle_acc.prochot");
+    pgpu_metrics->ppt_residency_acc = g->u("throttle_acc.ppt");
+    pgpu_metrics->socket_thm_residency_acc = g->u("throttle_acc.socket_thm");
+    pgpu_metrics->vr_thm_residency_acc = g->u("throttle_acc.vr_thm");
+    pgpu_metrics->hbm_thm_residency_acc = g->u("throttle_acc.hbm_thm");
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+}  // extern "C"

@@ -33,7 +33,7 @@ class World:
         monkeypatch.setattr(diag, "device_count", lambda: n)
         monkeypatch.setattr(diag, "device_info", lambda d: {"bdf": f"0000:0{d}:00.0"})
 
-        def run(level, d):
+        def run(level, d, memory_partition=None):
             self.runs.append(d)
             return {"gemm": {"pass": True, "tflops": 1200.0 + len(self.runs)}}
         monkeypatch.setattr(diag, "run", run)
@@ -147,7 +147,7 @@ def test_hung_diagnostic_is_reported_not_waited_for(monkeypatch):
     release = threading.Event()
     started = []
 
-    def run(level, d):
+    def run(level, d, memory_partition=None):
         started.append(d)
         if d == 1:
             release.wait(30)  # GPU 1's queue hangs
@@ -175,7 +175,7 @@ def test_hung_diagnostic_is_reported_not_waited_for(monkeypatch):
 def test_diagnostic_that_raises_is_a_failed_test(monkeypatch):
     World(monkeypatch)
 
-    def boom(level, d):
+    def boom(level, d, **kw):
         raise RuntimeError("hipErrorIllegalAddress")
     monkeypatch.setattr(diag, "run", boom)
     rep = A.Agent("n", source="fake", diag_level=1).probe_once()

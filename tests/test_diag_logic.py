@@ -10,11 +10,51 @@ from k8s_gpu_node_checker_amd.ops import diag
 class FakeLib:
     """Implements the C ABI calls with scripted results (out-params written through ctypes)."""
 
-    def __init__(self, mfma=None, link=(56.8, 56.7), rc=0, err=b"boom"):
-        self.mfma = mfma or {0: (1900.0, 0), 1: (1950.0, 0), 2: (4300.0, 0), 3: (7600.0, 0)}
+    def __init__(self, mfma=None, link=(56.8, 56.7), rc=0, err=b"boom", rate=1.0, cus=256, mem_gib=288,
+                 gemm_err=2e-5, rates=None):
+        self.mfma = mfma or {k: (rate * diag.REFERENCE_RATES["mfma"][n], 0) for k, n in enumerate(diag.MFMA_KINDS)}
         self.link = link
         self.rc = rc
         self.err = err
+        self.rate = rate            # every GEMM / HBM rate = rate x the full-GPU reference
+        self.rates = list(rates or [])  # successive overrides of `rate` (one per measured call)
+        self.cus = cus
+        self.mem_gib = mem_gib
+        self.gemm_err = gemm_err
+        self.calls = []
+
+    def _rate(self):
+        return self.rates.pop(0) if self.rates else self.rate
+
+    def diag_device_arch(self, device, buf, n):
+        v = f"gfx950:sramecc+:xnack-|AMD Instinct MI355X|{self.cus}|{self.mem_gib << 30}|0000:0{device}:00.0"
+        ctypes.memmove(buf, v.encode() + b"\0", len(v) + 1)
+        return 0
+
+    def _gemm(self, test, size, tflops, err, ms):
+        self.calls.append(test)
+        ctypes.cast(tflops, ctypes.POINTER(ctypes.c_double))[0] = self._rate() * diag.REFERENCE_RATES[test][size]
+        ctypes.cast(err, ctypes.POINTER(ctypes.c_double))[0] = self.gemm_err
+        ctypes.cast(ms, ctypes.POINTER(ctypes.c_double))[0] = 0.1
+        return self.rc
+
+    def diag_gemm_bf16(self, device, m, n, k, warmup, iters, samples, tflops, err, ms):
+        return self._gemm("gemm", m, tflops, err, ms)
+
+    def diag_gemm_fp8(self, device, m, n, k, warmup, iters, samples, tflops, err, ms):
+        return self._gemm("gemm_fp8", m, tflops, err, ms)
+
+    def diag_memtest(self, device, nbytes, seed, passes, errs, first, gbps):
+        ctypes.cast(gbps, ctypes.POINTER(ctypes.c_double))[0] = 5400.0
+        return self.rc
+
+    def diag_hbm_bandwidth(self, device, nbytes, iters, c, r, w):
+        self.calls.append("hbm")
+        f = self._rate()
+        ctypes.cast(c, ctypes.POINTER(ctypes.c_double))[0] = f * diag.REFERENCE_RATES["hbm"]["copy_tbs"]
+        ctypes.cast(r, ctypes.POINTER(ctypes.c_double))[0] = f * diag.REFERENCE_RATES["hbm"]["read_tbs"]
+        ctypes.cast(w, ctypes.POINTER(ctypes.c_double))[0] = f * 6.9
+        return self.rc
 
     def diag_last_error(self):
         return self.err
@@ -50,7 +90,7 @@ def test_mfma_burn_pass_and_each_failure_mode(fake):
     r = diag.mfma_burn(0)
     assert not r["pass"] and r["detail"] == "mxfp8: 3 wrong results"
     fake(mfma={0: (400.0, 0), 1: (1950.0, 0), 2: (4300.0, 0), 3: (7600.0, 0)})
-    assert diag.mfma_burn(0)["detail"] == "bf16: 400 TFLOP/s"
+    assert diag.mfma_burn(0)["detail"] == "bf16 400 TFLOP/s = 21% of 1.9e+03"
 
 
 def test_host_link_threshold(fake):
@@ -58,7 +98,7 @@ def test_host_link_threshold(fake):
     assert diag.host_link(0)["pass"]
     fake(link=(24.0, 56.0))  # a Gen4 / x8 link: half rate one way
     r = diag.host_link(0)
-    assert not r["pass"] and "h2d 24.0" in r["detail"]
+    assert not r["pass"] and "h2d_gbps 24 GB/s" in r["detail"] and "d2h" not in r["detail"]
 
 
 def test_c_abi_failure_raises_with_library_message(fake):
@@ -78,3 +118,83 @@ def test_run_turns_a_failing_test_into_a_verdict(fake, monkeypatch):
     out = diag.run(1, 0)
     assert out["gemm"]["pass"] is False and "illegal address" in out["gemm"]["detail"]
     assert out["mfma"]["pass"] and out["hbm"]["pass"]
+
+
+def _verdict(results, memory_partition="NPS1", cus=256):
+    """The agent's verdict for one GPU whose diag results are ``results``."""
+    from k8s_gpu_node_checker_amd.models import health as H
+    from k8s_gpu_node_checker_amd.testing import fixtures
+    rep = fixtures.mi355x_probe_report("n", gpus=1)
+    rep["gpus"][0].update({"diag": results, "memory_partition": memory_partition, "cus": cus,
+                           "compute_partition": "SPX" if cus == 256 else "CPX"})
+    return H.evaluate_report(rep, 1, now=rep["ts"])
+
+
+@pytest.mark.parametrize("level", [1, 2])
+def test_full_rate_gpu_is_healthy(fake, level):
+    lib = fake(link=(57.2, 56.8))
+    out = diag.run(level, 0)
+    assert all(r["pass"] and not r["degraded"] for r in out.values() if "fraction" in r), out
+    assert "scale" not in out["gemm"] and out["gemm"]["fraction"] == 1.0
+    assert "retried" not in out["gemm"] and lib.calls.count("gemm") == 1
+    assert _verdict(out).state == "healthy"
+
+
+def test_gpu_at_55_percent_is_unhealthy(fake):
+    fake(rate=0.55, mfma={k: (0.55 * diag.REFERENCE_RATES["mfma"][n], 0) for k, n in enumerate(diag.MFMA_KINDS)})
+    out = diag.run(1, 0)
+    for t in ("gemm", "gemm_fp8", "hbm", "mfma"):
+        assert out[t]["pass"] is False and out[t]["retried"] and 0.54 < out[t]["fraction"] < 0.56, out[t]
+    assert "tflops 671 TFLOP/s = 55% of 1.22e+03" in out["gemm"]["detail"]
+    v = _verdict(out)
+    assert v.state == "unhealthy" and any("diag gemm failed" in r for r in v.reasons)
+
+
+def test_gpu_at_90_percent_is_degraded_and_measured_twice(fake):
+    lib = fake(rate=0.90)
+    out = diag.run(1, 0)
+    assert out["gemm"]["pass"] and out["gemm"]["degraded"] and out["gemm"]["retried"]
+    assert lib.calls.count("gemm") == 2 and lib.calls.count("hbm") == 2
+    v = _verdict(out)
+    assert v.state == "degraded" and v.ok and any("diag gemm slow" in w for w in v.warnings), v.warnings
+
+
+def test_one_slow_sample_is_remeasured_not_reported(fake):
+    lib = fake(rates=[0.80, 1.0])  # the first gemm sample is slow, the re-measurement is normal
+    out = diag.run(1, 0)
+    assert out["gemm"]["pass"] and not out["gemm"]["degraded"] and out["gemm"]["retried"]
+    assert out["gemm"]["fraction"] == 1.0 and lib.calls.count("gemm") == 2
+
+
+def test_numerics_failure_is_not_remeasured(fake):
+    lib = fake(gemm_err=5e-2)
+    out = diag.run(1, 0)
+    assert out["gemm"]["pass"] is False and out["gemm"]["detail"].startswith("rel err 5.00e-02")
+    assert lib.calls.count("gemm") == 1
+
+
+def test_cpx_partition_at_one_eighth_is_healthy(fake):
+    # CPX: 32 CUs, NPS1 (all of HBM addressable, an eighth of the bandwidth share); every rate 1/8
+    lib = fake(rate=1 / 8, cus=32, link=(57.2 / 8, 56.8 / 8),
+               mfma={k: (diag.REFERENCE_RATES["mfma"][n] / 8, 0) for k, n in enumerate(diag.MFMA_KINDS)})
+    for level in (1, 2):
+        out = diag.run(level, 0, memory_partition="NPS1")
+        assert all(r["pass"] and not r.get("degraded") for r in out.values()), out
+        assert out["gemm"]["scale"] == {"compute": 0.125, "memory": 0.125}
+        assert _verdict(out, cus=32).state == "healthy"
+    # and the same partition at 1/16 (half speed) fails
+    lib.rate = 1 / 16
+    out = diag.run(1, 0, memory_partition="NPS1")
+    assert not out["gemm"]["pass"] and not out["hbm"]["pass"]
+
+
+def test_scale_from_partition_modes():
+    s = diag.Scale.of(256, 288 << 30, "NPS1")
+    assert (s.compute, s.memory) == (1.0, 1.0)
+    s = diag.Scale.of(128, 144 << 30, "NPS2")  # DPX + NPS2: half of everything
+    assert (s.compute, s.memory) == (0.5, 0.5)
+    s = diag.Scale.of(256, 288 << 30, "NPS2")  # SPX but an NPS2 memory partition: memory share halves
+    assert (s.compute, s.memory) == (1.0, 0.5)
+    assert diag.Scale.of(None, None, None).to_dict() == {"compute": 1.0, "memory": 1.0}
+    assert diag.judge_rate(84.9, 100) == "fail" and diag.judge_rate(85, 100) == "degraded"
+    assert diag.judge_rate(95, 100) == "pass"

@@ -45,6 +45,7 @@ def main() -> int:
     ap.add_argument("--minutes", type=float, default=5.0)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/soak.json")
+    ap.add_argument("--level", type=int, default=2, choices=(1, 2), help="diagnostics level (1: 4096^3 quick)")
     ap.add_argument("--rccl", action="store_true", help="also run the RCCL collectives every round")
     args = ap.parse_args()
     deadline = time.monotonic() + args.minutes * 60
@@ -52,7 +53,7 @@ def main() -> int:
     series: dict = {}
     t0 = time.time()
     while time.monotonic() < deadline:
-        res = diag.run(2, args.device)
+        res = diag.run(args.level, args.device)
         rnd_extra: dict = {}
         if args.rccl:
             from k8s_gpu_node_checker_amd.ops import fabric
@@ -80,7 +81,7 @@ def main() -> int:
         print(json.dumps({"round": len(rounds), **rnd}), flush=True)
     summary = {k: {"min": min(v), "median": statistics.median(v), "max": max(v), "n": len(v)}
                for k, v in series.items()}
-    out = {"device": diag.device_info(args.device), "minutes": args.minutes, "rounds": len(rounds),
+    out = {"device": diag.device_info(args.device), "level": args.level, "minutes": args.minutes, "rounds": len(rounds),
            "all_pass": not failures, "failures": failures[:20], "summary": summary}
     if args.rccl:
         rss, vram = series.get("host.rss_mb") or [None], series.get("gpu.vram_used_mb") or [None]
