@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <amd_smi/amdsmi.h>
 
+#include <atomic>
+
 #include <chrono>
 #include <cinttypes>
 #include <cstdio>
@@ -25,7 +27,7 @@ namespace {
 
 std::mutex g_mu;
 bool g_open = false;
-int g_gpus = -1;
+std::atomic<int> g_gpus{-1};  // read without the lock by mi355x_probe_gpu_count
 std::vector<amdsmi_processor_handle> g_handles;
 
 void jstr(std::string& o, const char* s) {
@@ -103,7 +105,7 @@ int open_locked() {
     }
   }
   g_open = true;
-  g_gpus = static_cast<int>(g_handles.size());
+  g_gpus.store(static_cast<int>(g_handles.size()), std::memory_order_relaxed);
   return 0;
 }
 
@@ -332,7 +334,7 @@ extern "C" int mi355x_probe_open(void) {
   return open_locked();
 }
 
-extern "C" int mi355x_probe_gpu_count(void) { return g_gpus; }
+extern "C" int mi355x_probe_gpu_count(void) { return g_gpus.load(std::memory_order_relaxed); }
 
 extern "C" char* mi355x_probe_json(const char* node_name) {
   std::lock_guard<std::mutex> lk(g_mu);

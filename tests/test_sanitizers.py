@@ -1,6 +1,8 @@
 """Host-side ASan/UBSan builds of the native CPU code (SURVEY §5 "Race detection / sanitizers").
 
-The fast-path extension is rebuilt with ``-fsanitize=address,undefined`` into a
+The C++ amd-smi probe (csrc/probe) is built with ASan/UBSan and TSan against a replay stub of
+libamd_smi (tests/amdsmi_stub) that serves a recorded MI355X probe and the DRIVER_NOT_LOADED / NO_PERM
+error statuses.  The fast-path extension is rebuilt with ``-fsanitize=address,undefined`` into a
 temp dir and the fuzzed native-vs-Python equivalence suite runs against it in
 a child interpreter with the sanitizer runtimes preloaded.  (GPU sanitizers
 are not available for the HIP library on this pool; see BENCH.md.)
@@ -46,3 +48,166 @@ def test_fastpath_under_asan_ubsan(tmp_path):
                        cwd=REPO, timeout=600)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert "passed" in p.stdout
+
+
+# --- the C++ amd-smi probe (csrc/probe) under ASan/UBSan and TSan, against a replay stub of libamd_smi ---
+
+STUB_DIR = os.path.join(REPO, "tests", "amdsmi_stub")
+PROBE_DIR = os.path.join(REPO, "k8s_gpu_node_checker_amd", "csrc", "probe")
+RECORDED = os.path.join(STUB_DIR, "mi355x_probe_recorded.json")  # mi355x-probe on an MI355X box (round 2)
+SAN = ["-O1", "-g", "-fno-omit-frame-pointer", "-std=c++17", "-Wall", "-Wextra", "-I", "/opt/rocm/include"]
+ASAN_ENV = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1", "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"}
+
+
+def _recorded_gpu():
+    import json
+    with open(RECORDED) as f:
+        return json.load(f)["gpus"][0]
+
+
+def scenario(path, gpus=8, init_status=0, per_gpu=None):
+    """The stub's key=value scenario: the recorded MI355X replicated to ``gpus`` OAMs (distinct BDFs /
+    UUIDs / KFD nodes), with ``per_gpu[i]`` overriding fields of GPU i."""
+    g0 = _recorded_gpu()
+    lines = [f"init_status={init_status}", f"gpus={gpus}"]
+    for i in range(gpus):
+        g = dict(g0)
+        g["bdf"] = f"0000:{0x05 + 0x10 * i:02x}:00.0"
+        g["uuid"] = g0["uuid"][:-2] + f"{i:02x}"
+        g["kfd_node"] = 2 + i
+        g.update((per_gpu or {}).get(i, {}))
+        for k, v in g.items():
+            if k in ("index", "probe_us", "processes", "kfd"):
+                continue
+            if k == "procs":
+                v = ",".join(f"{p['pid']}:{p['vram_mb']}" for p in v)
+            if k == "throttle_acc":
+                lines += [f"gpu.{i}.throttle_acc.{a}={b}" for a, b in v.items()]
+                continue
+            lines.append(f"gpu.{i}.{k}={v}")
+    path.write_text("\n".join(lines) + "\n")
+    return str(path)
+
+
+def _need(*names):
+    if not shutil.which("g++") or not os.path.exists("/opt/rocm/include/amd_smi/amdsmi.h"):
+        pytest.skip("needs g++ and the amd-smi headers")
+    rts = [_rt(n) for n in names]
+    if not all(rts):
+        pytest.skip("sanitizer runtimes not installed")
+    return rts
+
+
+def _gxx(args):
+    r = subprocess.run(["g++"] + args, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.fixture(scope="module")
+def asan_probe(tmp_path_factory):
+    """libamd_smi.so (stub), libmi355x_probe.so and mi355x-probe, all built with -fsanitize=address,undefined."""
+    asan, ubsan = _need("libasan.so", "libubsan.so")
+    d = tmp_path_factory.mktemp("probe_asan")
+    flags = SAN + ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+    _gxx(flags + ["-shared", "-fPIC", os.path.join(STUB_DIR, "amdsmi_stub.cpp"), "-o", str(d / "libamd_smi.so")])
+    # DT_RPATH (not RUNPATH): found before LD_LIBRARY_PATH, which may name /opt/rocm/lib's real library
+    link = ["-L", str(d), "-lamd_smi", f"-Wl,-rpath,{d}", "-Wl,--disable-new-dtags"]
+    _gxx(flags + ["-shared", "-fPIC", os.path.join(PROBE_DIR, "probe.cpp"), "-o", str(d / "libmi355x_probe.so")] + link)
+    _gxx(flags + [os.path.join(PROBE_DIR, "probe_main.cpp"), os.path.join(PROBE_DIR, "probe.cpp"),
+                  "-o", str(d / "mi355x-probe")] + link)
+    return d, asan, ubsan
+
+
+def _run_cli(d, scen, *args):
+    env = dict(os.environ, AMDSMI_STUB_SCENARIO=scen, **ASAN_ENV)
+    env.pop("LD_PRELOAD", None)  # an executable linked with -fsanitize loads its runtime itself
+    return subprocess.run([str(d / "mi355x-probe"), "--node", "n1"] + list(args), capture_output=True, text=True,
+                          env=env, timeout=120)
+
+
+@pytest.mark.slow
+def test_probe_cli_under_asan_replays_recorded_mi355x(asan_probe, tmp_path):
+    import json
+
+    from k8s_gpu_node_checker_amd.models import health as H
+    d, _, _ = asan_probe
+    # GPU 3 holds 100 processes (past the probe's 64-entry buffer: the OUT_OF_RESOURCES branch)
+    scen = scenario(tmp_path / "s.txt", per_gpu={3: {"nprocs": 100}})
+    p = _run_cli(d, scen, "--repeat", "3")
+    assert p.returncode == 0 and "ERROR: AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr, \
+        p.stderr[-3000:]
+    docs = [json.loads(x) for x in p.stdout.splitlines()]
+    assert len(docs) == 3
+    rec = _recorded_gpu()
+    rep = docs[-1]
+    assert rep["schema"] == "mi355x-health/v1" and rep["node"] == "n1" and len(rep["gpus"]) == 8
+    for i, g in enumerate(rep["gpus"]):
+        assert g["index"] == i and g["bdf"] == f"0000:{0x05 + 0x10 * i:02x}:00.0" and g["kfd_node"] == 2 + i
+        for k in ("gfx", "market_name", "product_name", "vbios_name", "device_id", "cus", "vram_type", "vram_mb",
+                  "ecc_uncorrectable", "bad_pages", "xgmi", "compute_partition", "memory_partition", "pcie_width",
+                  "pcie_max_speed_mts", "power_w", "power_cap_w", "power_cap_default_w", "vram_used_mb",
+                  "gfx_activity", "hbm_temp_c", "gfxclk_mhz", "throttle_acc"):
+            assert g[k] == rec[k], (i, k, g[k], rec[k])
+    assert rep["gpus"][3]["processes"] == 100 and len(rep["gpus"][3]["procs"]) == 64
+    assert rep["gpus"][0]["procs"] == rec["procs"]
+    v = H.evaluate_report(rep, 8, H.HealthExpectations(xgmi_links=7), now=rep["ts"])
+    assert v.state == H.HEALTHY and (v.gpus_ok, v.gpus_seen) == (8, 8), v.to_dict()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("status,name", [(34, "AMDSMI_STATUS_DRIVER_NOT_LOADED"), (10, "AMDSMI_STATUS_NO_PERM")])
+def test_probe_cli_under_asan_maps_init_errors_to_unknown(asan_probe, tmp_path, status, name):
+    import json
+
+    from k8s_gpu_node_checker_amd.models import health as H
+    d, _, _ = asan_probe
+    p = _run_cli(d, scenario(tmp_path / "s.txt", init_status=status))
+    assert p.returncode == 1, (p.stdout, p.stderr[-2000:])  # the CLI's "amd-smi could not be initialised"
+    assert "ERROR: AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr
+    rep = json.loads(p.stdout)
+    assert rep["error"] == name and rep["gpus"] == []
+    v = H.evaluate_report(rep, 8, now=rep["ts"])
+    assert v.state == H.UNKNOWN and v.reasons == [f"probe failed: {name}"]
+
+
+@pytest.mark.slow
+def test_probe_c_abi_under_asan_from_python(asan_probe, tmp_path):
+    """The ctypes path the agent uses (ops/amdsmi_probe.probe_native), sanitized library preloaded; one
+    GPU whose asic query fails (NO_PERM) is reported per GPU, the others still probed."""
+    d, asan, ubsan = asan_probe
+    scen = scenario(tmp_path / "s.txt", gpus=4, per_gpu={2: {"asic_status": 10}, 1: {"xgmi": "XUUDUUUU"}})
+    code = ("import json; from k8s_gpu_node_checker_amd.ops import amdsmi_probe as P; "
+            "from k8s_gpu_node_checker_amd.models import health as H\n"
+            "for _ in range(5): r = P.probe_native('n2')\n"
+            "v = H.evaluate_report(r, 4, H.HealthExpectations(xgmi_links=7), now=r['ts'])\n"
+            "print(json.dumps({'errors': [g.get('error') for g in r['gpus']], 'state': v.state, 'reasons': v.reasons,"
+            " 'ok': v.gpus_ok, 'seen': v.gpus_seen}))")
+    preload = " ".join(x for x in (asan, ubsan, os.environ.get("LD_PRELOAD", "")) if x)
+    env = dict(os.environ, K8SGPU_NATIVE_DIR=str(d), AMDSMI_STUB_SCENARIO=scen, LD_PRELOAD=preload,
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS=ASAN_ENV["UBSAN_OPTIONS"])
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=REPO, timeout=120)
+    assert p.returncode == 0 and "runtime error" not in p.stderr, p.stderr[-3000:]
+    import json
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["errors"] == [None, None, "AMDSMI_STATUS_NO_PERM", None]
+    assert out["state"] == "unhealthy" and (out["ok"], out["seen"]) == (2, 4)
+    assert "gpu2: probe error AMDSMI_STATUS_NO_PERM" in out["reasons"]
+    assert any(r.startswith("gpu1: 1 xGMI link(s) down") for r in out["reasons"])
+
+
+@pytest.mark.slow
+def test_probe_concurrent_calls_under_tsan(tmp_path):
+    """8 threads interleaving open / json / gpu_count / close (the agent's probe loop, its HTTP handlers
+    and a shutdown) must be race-free: the probe's mutex covers every amd-smi call and handle."""
+    _need("libtsan.so")
+    flags = SAN + ["-fsanitize=thread", "-pthread"]
+    _gxx(flags + ["-shared", "-fPIC", os.path.join(STUB_DIR, "amdsmi_stub.cpp"), "-o", str(tmp_path / "libamd_smi.so")])
+    _gxx(flags + ["-I", PROBE_DIR, os.path.join(STUB_DIR, "probe_stress.cpp"), os.path.join(PROBE_DIR, "probe.cpp"),
+                  "-o", str(tmp_path / "probe_stress"), "-L", str(tmp_path), "-lamd_smi", f"-Wl,-rpath,{tmp_path}",
+                  "-Wl,--disable-new-dtags"])
+    env = dict(os.environ, AMDSMI_STUB_SCENARIO=scenario(tmp_path / "s.txt"), TSAN_OPTIONS="halt_on_error=1")
+    env.pop("LD_PRELOAD", None)
+    p = subprocess.run([str(tmp_path / "probe_stress"), "8", "40"], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert p.returncode == 0 and "WARNING: ThreadSanitizer" not in p.stderr, p.stderr[-4000:]
+    assert '"bad_documents":0' in p.stdout and '"threads":8' in p.stdout
