@@ -74,6 +74,12 @@ def gpu_busy(g: Dict[str, Any], own_pids: frozenset = frozenset(), busy_vram_mb:
     return None
 
 
+def normalize_bdf(bdf: Any) -> str:
+    """PCI address in amd-smi's form (``0000:05:00.0``, lower case); a domain-less ``05:00.0`` gets 0000."""
+    b = str(bdf or "").strip().lower()
+    return "0000:" + b if b.count(":") == 1 else b
+
+
 def report_digest(rep: Dict[str, Any]) -> str:
     """Stable digest of a report minus its volatile fields (timestamps, timings, temperature)."""
     import hashlib
@@ -117,8 +123,14 @@ class Agent:
                  events: bool = True, event_namespace: str = "default", taint_unhealthy: bool = False,
                  diag_when: str = "idle", busy_vram_mb: int = 2048, busy_gfx_activity: int = 10,
                  diag_timeout: float = 300.0, ignore_pids: Sequence[int] = (),
-                 expect_gpus: Optional[int] = None, expectations: Optional[HealthExpectations] = None):
+                 expect_gpus: Optional[int] = None, expectations: Optional[HealthExpectations] = None,
+                 pod_resources_socket: Optional[str] = None, gpu_resources: Sequence[str] = (PRIMARY_GPU_KEY,)):
         self.node = node
+        # the kubelet's PodResources socket: a GPU allocated to a pod is never diagnosed, even before the
+        # pod touches it (None: not consulted; a missing socket falls back to the amd-smi heuristic)
+        self.pod_resources_socket = pod_resources_socket
+        self.gpu_resources = tuple(gpu_resources)
+        self.pod_resources_state: Optional[str] = None
         # the verdict is taken against the GPU count the node registered (amd.com/gpu capacity /
         # allocatable, read from the Node object) unless --expect-gpus pins it; a GPU that fell off
         # the bus after the device plugin counted it then makes the node unhealthy at the source
@@ -217,10 +229,16 @@ class Agent:
         entries = self._entries_by_device(gpus, devices)
         now = time.time()
         due = [d for d in devices if now - self._diag_at.get(d, float("-inf")) >= self.diag_interval]
+        allocated = self._allocated() if due and self.diag_when == "idle" else None
         run = []
         for d in due:
-            why = gpu_busy(entries.get(d) or {}, self.ignore_pids, self.busy_vram_mb,
-                           self.busy_gfx_activity) if self.diag_when == "idle" else None
+            why = None
+            if allocated:
+                owner = allocated.get(normalize_bdf((entries.get(d) or {}).get("bdf")) or self._bdf.get(d, ""))
+                if owner:
+                    why = f"allocated to pod {owner}"
+            if why is None and self.diag_when == "idle":
+                why = gpu_busy(entries.get(d) or {}, self.ignore_pids, self.busy_vram_mb, self.busy_gfx_activity)
             if why:
                 self._diag_skipped[d] = why
             else:
@@ -276,6 +294,23 @@ class Agent:
             self._fabric_at = now
         return {d: self._diag_cache[d] for d in devices if d in self._diag_cache}
 
+    def _allocated(self) -> Optional[Dict[str, str]]:
+        """Devices the kubelet allocated to pods (normalised BDF -> "ns/pod"), or None when unknown."""
+        if not self.pod_resources_socket:
+            return None
+        from ..kube import podresources
+        try:
+            got = podresources.allocated_devices(self.pod_resources_socket, self.gpu_resources)
+        except podresources.PodResourcesError as e:
+            state = f"error: {e}"[:200]
+            if state != self.pod_resources_state:
+                print(f"kubelet PodResources unavailable, using the amd-smi busy heuristic: {e}", file=sys.stderr,
+                      flush=True)
+            self.pod_resources_state = state
+            return None
+        self.pod_resources_state = "absent" if got is None else "ok"
+        return None if got is None else {normalize_bdf(k): v for k, v in got.items()}
+
     def probe_once(self) -> Dict[str, Any]:
         from ..ops.amdsmi_probe import probe
         rep = probe(self.node, self.source, self.fixture)
@@ -292,6 +327,8 @@ class Agent:
                     g["diag_skipped"] = self._diag_skipped[d]
             if self._fabric:
                 rep["fabric"] = self._fabric
+        if self.pod_resources_state is not None:
+            rep["pod_resources"] = self.pod_resources_state
         verdict = self.evaluate(rep)
         rep["state"] = verdict.state
         if self.expected_gpus:
@@ -524,6 +561,13 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--xgmi-links", type=int, default=XGMI_LINKS_EXPECTED, metavar="N",
                     help=f"xGMI links that must be Up per GPU (default {XGMI_LINKS_EXPECTED}: 8-GPU hive; "
                          "0 disables the check)")
+    ap.add_argument("--pod-resources-socket", default=None, metavar="PATH",
+                    help="kubelet PodResources socket (e.g. /var/lib/kubelet/pod-resources/kubelet.sock): GPUs "
+                         "allocated to pods are never diagnosed; without it (or when absent) only the amd-smi "
+                         "busy heuristic applies")
+    ap.add_argument("--gpu-resource", action="append", default=None, metavar="NAME",
+                    help=f"extended resource whose kubelet allocations mark GPUs busy (repeatable; default "
+                         f"{PRIMARY_GPU_KEY})")
     ap.add_argument("--busy-gfx-activity", type=int, default=10,
                     help="graphics-engine activity (%%) at which a GPU counts as busy (default 10)")
     return ap
@@ -538,7 +582,9 @@ def main(argv: Optional[List[str]] = None) -> int:
                   diag_when=args.diag_when, busy_vram_mb=args.busy_vram_mb,
                   busy_gfx_activity=args.busy_gfx_activity, diag_timeout=args.diag_timeout,
                   ignore_pids=args.ignore_pid, expect_gpus=args.expect_gpus,
-                  expectations=HealthExpectations(xgmi_links=args.xgmi_links))
+                  expectations=HealthExpectations(xgmi_links=args.xgmi_links),
+                  pod_resources_socket=args.pod_resources_socket,
+                  gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)))
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient

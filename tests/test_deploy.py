@@ -73,3 +73,51 @@ def test_manifests_are_self_consistent():
     kust = yaml.safe_load(open(os.path.join(REPO, "deploy", "kustomization.yaml")))
     assert sorted(kust["resources"]) == sorted(os.path.basename(p) for p in MANIFESTS
                                                if not p.endswith("kustomization.yaml"))
+
+
+def _pods():
+    for path in MANIFESTS:
+        for d in yaml.safe_load_all(open(path)):
+            if not d or d["kind"] not in ("DaemonSet", "Deployment", "CronJob", "Job"):
+                continue
+            spec = d["spec"]["jobTemplate"]["spec"] if d["kind"] == "CronJob" else d["spec"]
+            yield os.path.basename(path), spec["template"]["spec"]
+
+
+def test_gpu_device_access_is_real():
+    """A container that mounts /dev/kfd must be able to open it: hostPath device mounts add no
+    device-cgroup rule, so it is privileged, or it requests the GPU from the device plugin (which adds the
+    rule) and runs in the render/video groups (the unprivileged DaemonSet could not)."""
+    seen = 0
+    for name, pod in _pods():
+        vols = {v["name"]: v for v in pod.get("volumes") or []}
+        for c in pod["containers"]:
+            mounts = {m["mountPath"]: m["name"] for m in c.get("volumeMounts") or []}
+            if "/dev/kfd" not in mounts:
+                continue
+            seen += 1
+            assert vols[mounts["/dev/kfd"]]["hostPath"]["path"] == "/dev/kfd"
+            sc = c.get("securityContext") or {}
+            if sc.get("privileged"):
+                continue
+            limits = (c.get("resources") or {}).get("limits") or {}
+            groups = set((pod.get("securityContext") or {}).get("supplementalGroups") or [])
+            assert any(k.startswith("amd.com/gpu") for k in limits), (name, c["name"])
+            assert groups, (name, c["name"], "needs the render/video GIDs")
+    assert seen, "no container mounts /dev/kfd"
+
+
+def test_agent_daemonset_sees_host_pids_and_kubelet_allocations():
+    [(name, pod)] = [(n, p) for n, p in _pods() if p["containers"][0]["command"][0] == "k8s-gpu-node-agent"]
+    assert pod.get("hostPID") is True
+    c = pod["containers"][0]
+    args = agent.build_parser().parse_args(c["command"][1:])
+    sock = args.pod_resources_socket
+    assert sock and args.diag_when == "idle"
+    mounted = {m["mountPath"] for m in c["volumeMounts"]}
+    assert os.path.dirname(sock) in mounted
+    vols = {v["name"]: v for v in pod["volumes"]}
+    pr = [m for m in c["volumeMounts"] if m["mountPath"] == os.path.dirname(sock)][0]
+    assert vols[pr["name"]]["hostPath"]["path"] == os.path.dirname(sock)
+    sc = c["securityContext"]
+    assert sc.get("readOnlyRootFilesystem") is True and "/tmp" in mounted  # HIP / amd-smi scratch on tmpfs
