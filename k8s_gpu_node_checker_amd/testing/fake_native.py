@@ -1,0 +1,176 @@
+"""CPU stand-ins for the C ABIs of ``libmi355x_diag.so`` and ``libmi355x_fabric.so``.
+
+They implement the same calls with the same out-parameter protocol (values written through ctypes
+pointers), so ``ops/diag.py`` and ``ops/fabric.py`` run unchanged on CPU with scripted results: a node of
+N healthy MI355X by default, with per-GPU rate factors, wrong-result counts, slow or peer-less GPU pairs
+and RCCL failures injectable.  Used by the CPU tests of the verdict logic and of whole 8-GPU agent
+cycles; the real libraries run under ``tests/test_gpu.py`` on an MI355X.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+import time
+from typing import Dict, List, Optional, Tuple
+
+
+def _put(ptr, ctype, value) -> None:
+    ctypes.cast(ptr, ctypes.POINTER(ctype))[0] = value
+
+
+class FakeDiagLib:
+    """``libmi355x_diag.so`` for a node of ``n`` GPUs.
+
+    rate:        every GEMM / HBM / MFMA / host-link rate = rate x the full-GPU reference (per GPU:
+                 ``gpu_rate[d]``; a list ``rates`` overrides it call by call)
+    cus/mem_gib: what HIP reports per device (a CPX partition: 32 CUs)
+    mfma_errors: ``{(device, kind index): wrong results}``
+    p2p_gbps:    rate of every GPU pair; ``slow_pairs[(src, dst)]`` / ``nopeer`` override pairs
+    delay_s:     wall time of each GEMM call (the agent's per-GPU threads overlap them)
+    """
+
+    def __init__(self, n: int = 1, rate: float = 1.0, gpu_rate: Optional[Dict[int, float]] = None,
+                 rates: Optional[List[float]] = None, cus: int = 256, mem_gib: int = 288, gemm_err: float = 2e-5,
+                 mfma: Optional[Dict[int, Tuple[float, int]]] = None,
+                 mfma_errors: Optional[Dict[Tuple[int, int], int]] = None, link: Optional[Tuple[float, float]] = None,
+                 p2p_gbps: float = 48.0, slow_pairs: Optional[Dict[Tuple[int, int], float]] = None,
+                 nopeer: Tuple[Tuple[int, int], ...] = (), rc: int = 0, err: bytes = b"boom", delay_s: float = 0.0):
+        from ..ops import diag
+        self.ref = diag.REFERENCE_RATES
+        self.kinds = diag.MFMA_KINDS
+        self.n = n
+        self.rate = rate
+        self.gpu_rate = dict(gpu_rate or {})
+        self.rates = list(rates or [])
+        self.cus = cus
+        self.mem_gib = mem_gib
+        self.gemm_err = gemm_err
+        self.mfma = mfma
+        self.mfma_errors = dict(mfma_errors or {})
+        self.link = link
+        self.p2p_gbps = p2p_gbps
+        self.slow_pairs = dict(slow_pairs or {})
+        self.nopeer = set(nopeer)
+        self.rc = rc
+        self.err = err
+        self.delay_s = delay_s
+        self.calls: List[str] = []
+        self.threads: Dict[int, set] = {}
+        self.lock = threading.Lock()
+
+    def _rate(self, device: int) -> float:
+        with self.lock:
+            if self.rates:
+                return self.rates.pop(0)
+        return self.gpu_rate.get(device, self.rate)
+
+    def _log(self, device: int, what: str) -> None:
+        with self.lock:
+            self.calls.append(what)
+            self.threads.setdefault(device, set()).add(threading.current_thread().name)
+
+    # --- C ABI ------------------------------------------------------------------------------------------
+    def diag_last_error(self) -> bytes:
+        return self.err
+
+    def diag_device_count(self) -> int:
+        return self.n
+
+    def diag_device_arch(self, device, buf, size):
+        if not 0 <= device < self.n:
+            self.err = b"hipSetDevice: invalid device ordinal"
+            return -1
+        v = f"gfx950:sramecc+:xnack-|AMD Instinct MI355X|{self.cus}|{self.mem_gib << 30}|0000:{0x05 + 0x10 * device:02x}:00.0"
+        ctypes.memmove(buf, v.encode() + b"\0", min(size, len(v) + 1))
+        return 0
+
+    def _gemm(self, test, device, size, tflops, err, ms):
+        self._log(device, test)
+        if self.delay_s:
+            time.sleep(self.delay_s)
+        table = self.ref[test]
+        key = size if size in table else min(table, key=lambda k: abs(k - size))
+        _put(tflops, ctypes.c_double, self._rate(device) * table[key])
+        _put(err, ctypes.c_double, self.gemm_err)
+        _put(ms, ctypes.c_double, 0.1)
+        return self.rc
+
+    def diag_gemm_bf16(self, device, m, n, k, warmup, iters, samples, tflops, err, ms):
+        return self._gemm("gemm", device, m, tflops, err, ms)
+
+    def diag_gemm_fp8(self, device, m, n, k, warmup, iters, samples, tflops, err, ms):
+        return self._gemm("gemm_fp8", device, m, tflops, err, ms)
+
+    def diag_hbm_bandwidth(self, device, nbytes, iters, c, r, w):
+        self._log(device, "hbm")
+        f = self._rate(device)
+        _put(c, ctypes.c_double, f * self.ref["hbm"]["copy_tbs"])
+        _put(r, ctypes.c_double, f * self.ref["hbm"]["read_tbs"])
+        _put(w, ctypes.c_double, f * 6.9)
+        return self.rc
+
+    def diag_memtest(self, device, nbytes, seed, passes, errs, first, gbps):
+        self._log(device, "memtest")
+        _put(errs, ctypes.c_ulonglong, 0)
+        _put(gbps, ctypes.c_double, 5400.0)
+        return self.rc
+
+    def diag_mfma_burn(self, device, kind, iters, reps, tflops, errors):
+        self._log(device, "mfma")
+        if self.rc:
+            return self.rc
+        if self.mfma is not None:
+            tf, e = self.mfma[kind]
+        else:
+            tf, e = self.gpu_rate.get(device, self.rate) * self.ref["mfma"][self.kinds[kind]], 0
+        _put(tflops, ctypes.c_double, tf)
+        _put(errors, ctypes.c_ulonglong, self.mfma_errors.get((device, kind), e))
+        return 0
+
+    def diag_host_link(self, device, nbytes, iters, h2d, d2h):
+        self._log(device, "host_link")
+        f = self.gpu_rate.get(device, self.rate)
+        h, d = self.link or (f * self.ref["host_link"]["h2d_gbps"], f * self.ref["host_link"]["d2h_gbps"])
+        _put(h2d, ctypes.c_double, h)
+        _put(d2h, ctypes.c_double, d)
+        return self.rc
+
+    def diag_p2p_copy(self, src, dst, nbytes, iters, gbps, errors, peer):
+        with self.lock:  # node-level: runs on the agent's main thread, after the per-GPU threads
+            self.calls.append(f"p2p{src}->{dst}")
+        if not (0 <= src < self.n and 0 <= dst < self.n) or src == dst:
+            self.err = b"p2p: invalid device pair"
+            return -1
+        _put(gbps, ctypes.c_double, self.slow_pairs.get((src, dst), self.p2p_gbps))
+        _put(errors, ctypes.c_ulonglong, 0)
+        _put(peer, ctypes.c_int, 0 if (src, dst) in self.nopeer else 1)
+        return 0
+
+
+class FakeFabricLib:
+    """``libmi355x_fabric.so`` (in-process RCCL communicator over the node's GPUs)."""
+
+    def __init__(self, busbw: float = 320.0, errors: int = 0, fail_open: bool = False, version: int = 22707):
+        self.busbw, self.errors, self.fail_open, self.version = busbw, errors, fail_open, version
+        self.opened: List[List[int]] = []
+        self.closed = 0
+
+    def fabric_open(self, arr, n):
+        if self.fail_open:
+            return None
+        self.opened.append([arr[i] for i in range(n)])
+        return 1
+
+    def fabric_run(self, ctx, op, nbytes, iters, warmup, out):
+        out[0], out[1], out[2], out[3] = 1.0, self.busbw * 0.57, self.busbw, float(self.errors if op == 3 else 0)
+        return 0
+
+    def fabric_close(self, ctx):
+        self.closed += 1
+
+    def fabric_last_error(self):
+        return b"ncclCommInitAll: unhandled system error"
+
+    def fabric_rccl_version(self):
+        return self.version

@@ -5,72 +5,10 @@ import ctypes
 import pytest
 
 from k8s_gpu_node_checker_amd.ops import diag
+from k8s_gpu_node_checker_amd.testing.fake_native import FakeDiagLib
 
 
-class FakeLib:
-    """Implements the C ABI calls with scripted results (out-params written through ctypes)."""
-
-    def __init__(self, mfma=None, link=(56.8, 56.7), rc=0, err=b"boom", rate=1.0, cus=256, mem_gib=288,
-                 gemm_err=2e-5, rates=None):
-        self.mfma = mfma or {k: (rate * diag.REFERENCE_RATES["mfma"][n], 0) for k, n in enumerate(diag.MFMA_KINDS)}
-        self.link = link
-        self.rc = rc
-        self.err = err
-        self.rate = rate            # every GEMM / HBM rate = rate x the full-GPU reference
-        self.rates = list(rates or [])  # successive overrides of `rate` (one per measured call)
-        self.cus = cus
-        self.mem_gib = mem_gib
-        self.gemm_err = gemm_err
-        self.calls = []
-
-    def _rate(self):
-        return self.rates.pop(0) if self.rates else self.rate
-
-    def diag_device_arch(self, device, buf, n):
-        v = f"gfx950:sramecc+:xnack-|AMD Instinct MI355X|{self.cus}|{self.mem_gib << 30}|0000:0{device}:00.0"
-        ctypes.memmove(buf, v.encode() + b"\0", len(v) + 1)
-        return 0
-
-    def _gemm(self, test, size, tflops, err, ms):
-        self.calls.append(test)
-        ctypes.cast(tflops, ctypes.POINTER(ctypes.c_double))[0] = self._rate() * diag.REFERENCE_RATES[test][size]
-        ctypes.cast(err, ctypes.POINTER(ctypes.c_double))[0] = self.gemm_err
-        ctypes.cast(ms, ctypes.POINTER(ctypes.c_double))[0] = 0.1
-        return self.rc
-
-    def diag_gemm_bf16(self, device, m, n, k, warmup, iters, samples, tflops, err, ms):
-        return self._gemm("gemm", m, tflops, err, ms)
-
-    def diag_gemm_fp8(self, device, m, n, k, warmup, iters, samples, tflops, err, ms):
-        return self._gemm("gemm_fp8", m, tflops, err, ms)
-
-    def diag_memtest(self, device, nbytes, seed, passes, errs, first, gbps):
-        ctypes.cast(gbps, ctypes.POINTER(ctypes.c_double))[0] = 5400.0
-        return self.rc
-
-    def diag_hbm_bandwidth(self, device, nbytes, iters, c, r, w):
-        self.calls.append("hbm")
-        f = self._rate()
-        ctypes.cast(c, ctypes.POINTER(ctypes.c_double))[0] = f * diag.REFERENCE_RATES["hbm"]["copy_tbs"]
-        ctypes.cast(r, ctypes.POINTER(ctypes.c_double))[0] = f * diag.REFERENCE_RATES["hbm"]["read_tbs"]
-        ctypes.cast(w, ctypes.POINTER(ctypes.c_double))[0] = f * 6.9
-        return self.rc
-
-    def diag_last_error(self):
-        return self.err
-
-    def diag_mfma_burn(self, device, kind, iters, reps, tflops, errors):
-        if self.rc:
-            return self.rc
-        tf, e = self.mfma[kind]
-        ctypes.cast(tflops, ctypes.POINTER(ctypes.c_double))[0] = tf
-        ctypes.cast(errors, ctypes.POINTER(ctypes.c_ulonglong))[0] = e
-        return 0
-
-    def diag_host_link(self, device, nbytes, iters, h2d, d2h):
-        ctypes.cast(h2d, ctypes.POINTER(ctypes.c_double))[0] = self.link[0]
-        ctypes.cast(d2h, ctypes.POINTER(ctypes.c_double))[0] = self.link[1]
-        return self.rc
+FakeLib = FakeDiagLib  # the C ABI with scripted results (testing/fake_native.py)
 
 
 @pytest.fixture
