@@ -1,7 +1,5 @@
 """ops/diag.py verdict logic on CPU: a fake C ABI stands in for libmi355x_diag.so (the real kernels
 run under tests/test_gpu.py on the MI355X)."""
-import ctypes
-
 import pytest
 
 from k8s_gpu_node_checker_amd.ops import diag
