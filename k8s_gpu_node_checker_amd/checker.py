@@ -14,9 +14,10 @@ the node agent's self-test); :func:`one_shot` adds the printing.
 from __future__ import annotations
 
 import sys
-import threading
 import time
-from typing import Any, Callable, Dict, List, Optional, TextIO
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Any, Callable, Dict, List, Optional, TextIO
 
 from . import report
 from .kube.client import KubeClient
@@ -270,7 +271,7 @@ def emit_report(result: CheckResult, opts: CheckOptions, out: Optional[TextIO] =
     gpu_nodes, ready = result.gpu_nodes, result.ready_gpu_nodes
 
     url = slack.get_slack_webhook_url(opts.slack_webhook)
-    worker: Optional[threading.Thread] = None
+    worker: "Optional[threading.Thread]" = None
     box: Dict[str, bool] = {}
     if slack.should_send(url, opts.slack_only_on_error, len(ready)) and (
             opts.slack_gate is None or opts.slack_gate(result)):
@@ -284,6 +285,7 @@ def emit_report(result: CheckResult, opts: CheckOptions, out: Optional[TextIO] =
             with tr.span("slack"):
                 box["ok"] = slack.send_slack_message(url, text, opts.slack_username, opts.slack_retry_count,
                                                      delay, policy=opts.slack_retry_policy, err=err)
+        import threading  # only when a Slack message goes out
         worker = threading.Thread(target=_send, name="slack", daemon=True)
         worker.start()
 

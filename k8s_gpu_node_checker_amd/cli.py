@@ -12,86 +12,147 @@ errors, as in the reference), 1 = any exception (kubeconfig, API, transport).
 
 from __future__ import annotations
 
-import argparse
 import os
 import sys
-from typing import List, Optional
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Any, Dict, List, Optional, Tuple
 
-HIDE = argparse.SUPPRESS
+# Every flag once: (group, flag, options).  group "" = top level, "slack" = the reference's 슬랙 알림
+# group, "x" = MI355X extensions (hidden unless --help-all).  build_parser() turns this table into the
+# argparse parser (--help byte-identical to the reference); _fast_parse() reads the same table to skip
+# the argparse import (+ gettext + locale, ~2.5 ms of a 1-node cold start) for a plain command line.
+_FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
+    ("", "--kubeconfig", {"help": "kubeconfig 경로 직접 지정"}),
+    ("", "--json", {"action": "store_true", "help": "JSON 형태로만 출력(머신 판독용)"}),
+    ("slack", "--slack-webhook", {"help": "슬랙 웹훅 URL (환경변수 SLACK_WEBHOOK_URL로도 설정 가능)"}),
+    ("slack", "--slack-username", {"default": "k8s-gpu-checker", "help": "슬랙 봇 사용자명 (기본: k8s-gpu-checker)"}),
+    ("slack", "--slack-only-on-error", {"action": "store_true",
+                                        "help": "GPU 노드가 없거나 Ready 상태가 아닐 때만 슬랙 메시지 전송"}),
+    ("slack", "--slack-retry-count", {"type": int, "default": 3,
+                                      "help": "슬랙 메시지 전송 실패시 최대 재시도 횟수 (기본: 3)"}),
+    ("slack", "--slack-retry-delay", {"type": int, "default": 30, "help": "슬랙 메시지 재시도 간격(초) (기본: 30)"}),
+    ("x", "--help-all", {"action": "store_true", "help": "모든 옵션(확장 포함) 도움말"}),
+    ("slack*", "--slack-retry-policy", {"choices": ("backoff", "reference"), "default": "backoff",
+                                        "help": "5xx/429 재시도 정책: backoff(지수 백오프, 기본) | reference(즉시 재시도)"}),
+    ("slack*", "--slack-on-change", {"action": "store_true",
+                                     "help": "--state-file 과 함께: 상태가 바뀌었을 때만 전송 (복구 알림 포함)"}),
+    ("x", "--context", {"help": "kubeconfig context (기본: current-context)"}),
+    ("x", "--in-cluster", {"action": "store_true", "help": "Pod ServiceAccount 로 접속"}),
+    ("x", "--kube-timeout", {"type": float, "default": 30.0, "help": "kube-apiserver 요청 타임아웃(초) (기본: 30)"}),
+    ("x", "--kube-retries", {"type": int, "default": 2, "help": "LIST 재시도 횟수 (429/5xx/연결 오류, 기본: 2)"}),
+    ("x", "--page-size", {"type": int, "default": 500, "help": "LIST 페이지 크기 (0 = 한 번에, 기본: 500)"}),
+    ("x", "--label-selector", {"help": "노드 labelSelector"}),
+    ("x", "--resource-version", {"help": "LIST resourceVersion (예: 0 = watch cache)"}),
+    ("x", "--gpu-source", {"choices": ("capacity", "allocatable"), "default": "capacity",
+                           "help": "GPU 수를 읽을 status 필드 (기본: capacity = reference)"}),
+    ("x", "--health-policy", {"choices": ("off", "auto", "require"), "default": "auto",
+                              "help": "MI355X 헬스 게이트: off | auto(리포트가 있으면 반영, 기본) | require"}),
+    ("x", "--probe-max-age", {"type": float, "default": 900.0, "help": "프로브 리포트 최대 나이(초) (기본: 900)"}),
+    ("x", "--probe-unknown", {"choices": ("allow", "deny"), "default": "allow",
+                              "help": "프로브 상태 unknown(만료/실패) 노드 처리 (기본: allow)"}),
+    ("x", "--xgmi-links", {"type": int, "default": 7, "help": "GPU 당 기대 xGMI 링크 수 (0 = 검사 안 함, 기본: 7)"}),
+    ("x", "--health-reeval", {"action": "store_true",
+                              "help": "AMDGPUHealthy 조건 대신 프로브 리포트(annotation)를 이 임계값으로 재평가"}),
+    ("x", "--probe-endpoint", {"help": "노드별 프로브 URL 템플릿, 예: http://{ip}:9464/probe"}),
+    ("x", "--probe-concurrency", {"type": int, "default": 64, "help": "프로브 fan-out 동시성 (기본: 64)"}),
+    ("x", "--probe-timeout", {"type": float, "default": 2.0, "help": "노드별 프로브 타임아웃(초) (기본: 2)"}),
+    ("x", "--require-schedulable", {"action": "store_true",
+                                    "help": "cordon(spec.unschedulable) 되었거나 amd.com/gpu-unhealthy taint 가 있는 "
+                                            "GPU 노드는 Ready 로 세지 않음"}),
+    ("x", "--mi355x", {"action": "store_true",
+                       "help": "MI355X 프리셋: --gpu-source allocatable --health-policy require --require-schedulable"}),
+    ("x", "--json-extended", {"action": "store_true", "help": "JSON 에 MI355X 헬스/타이밍 필드 추가"}),
+    ("x", "--trace", {"action": "store_true", "help": "단계별 소요 시간을 stderr 로 출력"}),
+    ("x", "--prometheus-textfile", {"help": "node-exporter textfile 메트릭 경로"}),
+    ("x", "--state-file", {"help": "직전 결과 저장 파일 (알림 중복 제거)"}),
+    ("x", "--watch", {"type": float, "default": 0.0, "help": "N초마다 반복 점검 (0 = 한 번, 기본)"}),
+    ("x", "--watch-count", {"type": int, "default": 0,
+                            "help": "--watch 반복 횟수 / --watch-events 보고 횟수 (0 = 무제한, 기본); 종료 코드는 "
+                                    "마지막 점검의 것"}),
+    ("x", "--watch-events", {"action": "store_true",
+                             "help": "이벤트 기반 감시: LIST 한 번 후 watch 스트림을 따라가며 상태가 바뀔 때만 보고"}),
+    ("x", "--watch-debounce", {"type": float, "default": 0.2,
+                               "help": "--watch-events: 이 시간(초) 안에 도착한 이벤트를 한 번에 평가 (기본: 0.2)"}),
+    ("x", "--watch-duration", {"type": float, "default": 0.0, "help": "--watch-events: N초 후 종료 (0 = 무제한, 기본)"}),
+)
 
 
-def build_parser(show_all: bool = False, prog: Optional[str] = None) -> argparse.ArgumentParser:
+def build_parser(show_all: bool = False, prog: Optional[str] = None) -> "argparse.ArgumentParser":
+    import argparse
     if prog is None:
         base = os.path.basename(sys.argv[0]) if sys.argv and sys.argv[0] else "check-gpu-node"
         prog = "check-gpu-node" if base in ("__main__.py", "-c", "") else base
     p = argparse.ArgumentParser(prog=prog, description="Kubernetes GPU 노드 점검 스크립트")
-    p.add_argument("--kubeconfig", help="kubeconfig 경로 직접 지정")
-    p.add_argument("--json", action="store_true", help="JSON 형태로만 출력(머신 판독용)")
-
-    g = p.add_argument_group("슬랙 알림", "슬랙으로 메시지를 전송하는 옵션들")
-    g.add_argument("--slack-webhook", help="슬랙 웹훅 URL (환경변수 SLACK_WEBHOOK_URL로도 설정 가능)")
-    g.add_argument("--slack-username", default="k8s-gpu-checker", help="슬랙 봇 사용자명 (기본: k8s-gpu-checker)")
-    g.add_argument("--slack-only-on-error", action="store_true",
-                   help="GPU 노드가 없거나 Ready 상태가 아닐 때만 슬랙 메시지 전송")
-    g.add_argument("--slack-retry-count", type=int, default=3, help="슬랙 메시지 전송 실패시 최대 재시도 횟수 (기본: 3)")
-    g.add_argument("--slack-retry-delay", type=int, default=30, help="슬랙 메시지 재시도 간격(초) (기본: 30)")
-
-    def h(text: str) -> str:
-        return text if show_all else HIDE
-
-    x = p.add_argument_group("MI355X / 확장 옵션", "reference 에 없는 옵션들 (--help-all 에서만 표시)") if show_all else p
-    x.add_argument("--help-all", action="store_true", help=h("모든 옵션(확장 포함) 도움말"))
-    g.add_argument("--slack-retry-policy", choices=("backoff", "reference"), default="backoff",
-                   help=h("5xx/429 재시도 정책: backoff(지수 백오프, 기본) | reference(즉시 재시도)"))
-    g.add_argument("--slack-on-change", action="store_true",
-                   help=h("--state-file 과 함께: 상태가 바뀌었을 때만 전송 (복구 알림 포함)"))
-    x.add_argument("--context", help=h("kubeconfig context (기본: current-context)"))
-    x.add_argument("--in-cluster", action="store_true", help=h("Pod ServiceAccount 로 접속"))
-    x.add_argument("--kube-timeout", type=float, default=30.0, help=h("kube-apiserver 요청 타임아웃(초) (기본: 30)"))
-    x.add_argument("--kube-retries", type=int, default=2, help=h("LIST 재시도 횟수 (429/5xx/연결 오류, 기본: 2)"))
-    x.add_argument("--page-size", type=int, default=500, help=h("LIST 페이지 크기 (0 = 한 번에, 기본: 500)"))
-    x.add_argument("--label-selector", help=h("노드 labelSelector"))
-    x.add_argument("--resource-version", help=h("LIST resourceVersion (예: 0 = watch cache)"))
-    x.add_argument("--gpu-source", choices=("capacity", "allocatable"), default="capacity",
-                   help=h("GPU 수를 읽을 status 필드 (기본: capacity = reference)"))
-    x.add_argument("--health-policy", choices=("off", "auto", "require"), default="auto",
-                   help=h("MI355X 헬스 게이트: off | auto(리포트가 있으면 반영, 기본) | require"))
-    x.add_argument("--probe-max-age", type=float, default=900.0, help=h("프로브 리포트 최대 나이(초) (기본: 900)"))
-    x.add_argument("--probe-unknown", choices=("allow", "deny"), default="allow",
-                   help=h("프로브 상태 unknown(만료/실패) 노드 처리 (기본: allow)"))
-    x.add_argument("--xgmi-links", type=int, default=7, help=h("GPU 당 기대 xGMI 링크 수 (0 = 검사 안 함, 기본: 7)"))
-    x.add_argument("--health-reeval", action="store_true",
-                   help=h("AMDGPUHealthy 조건 대신 프로브 리포트(annotation)를 이 임계값으로 재평가"))
-    x.add_argument("--probe-endpoint", help=h("노드별 프로브 URL 템플릿, 예: http://{ip}:9464/probe"))
-    x.add_argument("--probe-concurrency", type=int, default=64, help=h("프로브 fan-out 동시성 (기본: 64)"))
-    x.add_argument("--probe-timeout", type=float, default=2.0, help=h("노드별 프로브 타임아웃(초) (기본: 2)"))
-    x.add_argument("--require-schedulable", action="store_true",
-                   help=h("cordon(spec.unschedulable) 되었거나 amd.com/gpu-unhealthy taint 가 있는 GPU 노드는 "
-                          "Ready 로 세지 않음"))
-    x.add_argument("--mi355x", action="store_true",
-                   help=h("MI355X 프리셋: --gpu-source allocatable --health-policy require --require-schedulable"))
-    x.add_argument("--json-extended", action="store_true", help=h("JSON 에 MI355X 헬스/타이밍 필드 추가"))
-    x.add_argument("--trace", action="store_true", help=h("단계별 소요 시간을 stderr 로 출력"))
-    x.add_argument("--prometheus-textfile", help=h("node-exporter textfile 메트릭 경로"))
-    x.add_argument("--state-file", help=h("직전 결과 저장 파일 (알림 중복 제거)"))
-    x.add_argument("--watch", type=float, default=0.0, help=h("N초마다 반복 점검 (0 = 한 번, 기본)"))
-    x.add_argument("--watch-count", type=int, default=0,
-                   help=h("--watch 반복 횟수 / --watch-events 보고 횟수 (0 = 무제한, 기본); 종료 코드는 마지막 점검의 것"))
-    x.add_argument("--watch-events", action="store_true",
-                   help=h("이벤트 기반 감시: LIST 한 번 후 watch 스트림을 따라가며 상태가 바뀔 때만 보고"))
-    x.add_argument("--watch-debounce", type=float, default=0.2,
-                   help=h("--watch-events: 이 시간(초) 안에 도착한 이벤트를 한 번에 평가 (기본: 0.2)"))
-    x.add_argument("--watch-duration", type=float, default=0.0,
-                   help=h("--watch-events: N초 후 종료 (0 = 무제한, 기본)"))
+    g = x = None
+    for group, flag, opts in _FLAGS:
+        if group == "slack" and g is None:
+            g = p.add_argument_group("슬랙 알림", "슬랙으로 메시지를 전송하는 옵션들")
+        if group == "x" and x is None:
+            x = p.add_argument_group("MI355X / 확장 옵션", "reference 에 없는 옵션들 (--help-all 에서만 표시)") \
+                if show_all else p
+        kw = dict(opts)
+        if group in ("x", "slack*") and not show_all:
+            kw["help"] = argparse.SUPPRESS
+        {"": p, "slack": g, "slack*": g, "x": x}[group].add_argument(flag, **kw)
     return p
 
 
-def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
+class _Args:
+    """The parsed flags as attributes (what argparse's Namespace gives, without importing argparse)."""
+
+    def __init__(self, values: Dict[str, Any]) -> None:
+        self.__dict__.update(values)
+
+
+def _fast_parse(argv: List[str]) -> Optional[Any]:
+    """The parse argparse would produce, for command lines made only of exact long flags (``--flag``,
+    ``--flag value``, ``--flag=value``) with valid values; ``None`` for anything else (help, errors,
+    abbreviations, values that look like options), which then goes through argparse itself."""
+    table = {flag: opts for _, flag, opts in _FLAGS}
+    ns = {flag[2:].replace("-", "_"): opts.get("default", False if opts.get("action") == "store_true" else None)
+          for flag, opts in table.items()}
+    i = 0
+    while i < len(argv):
+        tok = argv[i]
+        flag, eq, val = tok.partition("=")
+        opts = table.get(flag)
+        if opts is None or flag == "--help-all":
+            return None
+        dest = flag[2:].replace("-", "_")
+        if opts.get("action") == "store_true":
+            if eq:
+                return None
+            ns[dest] = True
+            i += 1
+            continue
+        if not eq:
+            if i + 1 >= len(argv):
+                return None
+            val = argv[i + 1]
+            if val.startswith("-"):
+                return None
+            i += 2
+        else:
+            i += 1
+        try:
+            v = opts.get("type", str)(val)
+        except ValueError:
+            return None
+        if "choices" in opts and v not in opts["choices"]:
+            return None
+        ns[dest] = v
+    return _Args(ns)
+
+
+def parse_args(argv: Optional[List[str]] = None) -> Any:
     argv = sys.argv[1:] if argv is None else argv
     if "--help-all" in argv:
         build_parser(show_all=True).print_help()
         sys.exit(0)
-    args = build_parser().parse_args(argv)
+    args = _fast_parse(argv)
+    if args is None:
+        args = build_parser().parse_args(argv)
     if args.mi355x:
         args.gpu_source = "allocatable"
         args.health_policy = "require"
@@ -101,7 +162,7 @@ def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
     return args
 
 
-def _load_cluster(args: argparse.Namespace):
+def _load_cluster(args: Any):
     from .kube.config import incluster_connection, load_kube_config
     from .kube.errors import ConfigException
     if args.in_cluster:
@@ -112,7 +173,7 @@ def _load_cluster(args: argparse.Namespace):
     return load_kube_config(args.kubeconfig, args.context)
 
 
-def _run_once(args: argparse.Namespace) -> int:
+def _run_once(args: Any) -> int:
     """Reference ``main`` body (``:316-327``) for one iteration."""
     try:
         from .checker import CheckOptions, check_and_report
@@ -135,7 +196,7 @@ def _run_once(args: argparse.Namespace) -> int:
         return _report_error(args, e)
 
 
-def _report_error(args: argparse.Namespace, e: BaseException) -> int:
+def _report_error(args: Any, e: BaseException) -> int:
     """Reference error reporter (``:319-327``): JSON one-liner on stdout or message + traceback."""
     import json
     if getattr(args, "json", False):
@@ -162,7 +223,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     return _run_once(args)
 
 
-def _watch_events(args: argparse.Namespace) -> int:
+def _watch_events(args: Any) -> int:
     """``--watch-events``: LIST once, follow the watch stream, report each change of outcome.
 
     Every report is a complete one-shot report (same JSON/text, same exit-code rule); Slack goes
@@ -211,7 +272,7 @@ def _watch_events(args: argparse.Namespace) -> int:
         return _report_error(args, e)
 
 
-def _watch(args: argparse.Namespace) -> int:
+def _watch(args: Any) -> int:
     """Repeat the check every ``--watch`` seconds (fixed cadence, not fixed sleep).
 
     Ends after ``--watch-count`` checks (0 = forever) or on Ctrl-C, with the

@@ -21,6 +21,10 @@
 //   is the pure-Python _make_iterencode, the dominant render cost at 1000
 //   nodes (reference check-gpu-node.py:279).
 //
+// loads(data)
+//   json.loads for the per-node health-report annotation (see its comment below); anything it cannot
+//   prove identical raises FallbackError and json.loads runs instead.
+//
 // Known, documented divergence: bytes inside *skipped* string values are not
 // UTF-8-validated (json.loads would reject invalid UTF-8 anywhere).
 
@@ -1521,11 +1525,192 @@ PyObject* dumps_indent2(PyObject*, PyObject* obj) {
   return PyUnicode_DecodeUTF8(out.data(), static_cast<Py_ssize_t>(out.size()), "surrogatepass");
 }
 
+// ------------------------------------------------------------------ loads --
+// loads(data: bytes | bytearray | str) -> object: json.loads for documents this parser can prove it
+// reads the same way (RFC 8259 grammar plus Python's NaN / Infinity / -Infinity, duplicate keys: last
+// value at the first key's position, ints of any size via int(), floats via float()).  Anything else
+// -- a syntax error, a raw control character in a string, invalid UTF-8, a lone surrogate escape, a
+// BOM, nesting deeper than kMaxDepth -- raises FallbackError and the caller re-parses with json.loads,
+// which then raises (or succeeds) exactly as it always would.  Used for the agent's health-report
+// annotation on every node, so a cold `check-gpu-node` never imports the json package.
+constexpr int kMaxDepth = 256;
+
+bool has_control(const char* b, const char* e) {
+  const __m128i lim = _mm_set1_epi8(0x1F);
+  while (e - b >= 16) {
+    __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(b));
+    // unsigned v <= 0x1F  <=>  min(v, 0x1F) == v
+    if (_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_min_epu8(v, lim), v))) return true;
+    b += 16;
+  }
+  for (; b < e; ++b)
+    if (static_cast<unsigned char>(*b) < 0x20) return true;
+  return false;
+}
+
+PyObject* loads_string(Cursor& c, std::string& scratch) {
+  RawStr s = read_raw_string(c);
+  if (has_control(s.b, s.e)) throw Fallback{"control character in string"};
+  return make_str(s, scratch);
+}
+
+PyObject* loads_number(Cursor& c, std::string& scratch) {
+  const char* b = c.p;
+  const char* p = b;
+  const char* e = c.end;
+  if (p < e && *p == '-') {
+    ++p;
+    if (e - p >= 8 && memcmp(p, "Infinity", 8) == 0) {
+      c.p = p + 8;
+      return PyFloat_FromDouble(-HUGE_VAL);
+    }
+  }
+  if (p >= e) throw Fallback{"bad number"};
+  if (*p == '0') {
+    ++p;
+  } else if (*p >= '1' && *p <= '9') {
+    while (p < e && *p >= '0' && *p <= '9') ++p;
+  } else {
+    throw Fallback{"bad number"};
+  }
+  bool is_float = false;
+  if (p < e && *p == '.') {
+    ++p;
+    if (p >= e || *p < '0' || *p > '9') throw Fallback{"bad fraction"};
+    while (p < e && *p >= '0' && *p <= '9') ++p;
+    is_float = true;
+  }
+  if (p < e && (*p == 'e' || *p == 'E')) {
+    ++p;
+    if (p < e && (*p == '+' || *p == '-')) ++p;
+    if (p >= e || *p < '0' || *p > '9') throw Fallback{"bad exponent"};
+    while (p < e && *p >= '0' && *p <= '9') ++p;
+    is_float = true;
+  }
+  c.p = p;
+  const size_t n = static_cast<size_t>(p - b);
+  if (!is_float) {
+    PyObject* v = parse_int_text(b, n, scratch);  // int(text): arbitrary size, CPython's digit limit
+    if (!v) throw Fallback{"int() rejected"};
+    return v;
+  }
+  scratch.assign(b, n);
+  double d = PyOS_string_to_double(scratch.c_str(), nullptr, nullptr);  // float(text): overflow -> inf
+  if (d == -1.0 && PyErr_Occurred()) {
+    PyErr_Clear();
+    throw Fallback{"float() rejected"};
+  }
+  return PyFloat_FromDouble(d);
+}
+
+PyObject* loads_value(Cursor& c, std::string& scratch, int depth) {
+  const char ch = c.peek();
+  if (ch == '"') return loads_string(c, scratch);
+  if (ch == '{') {
+    if (depth >= kMaxDepth) throw Fallback{"too deep"};
+    ++c.p;
+    Ref d{PyDict_New()};
+    if (!d.o) throw Fallback{"out of memory"};
+    if (c.consume('}')) return d.release();
+    for (;;) {
+      if (c.peek() != '"') throw Fallback{"expected key"};
+      Ref k{loads_string(c, scratch)};
+      c.expect(':');
+      Ref v{loads_value(c, scratch, depth + 1)};
+      if (PyDict_SetItem(d.o, k.o, v.o) < 0) {
+        PyErr_Clear();
+        throw Fallback{"dict insert failed"};
+      }
+      if (c.consume(',')) continue;
+      c.expect('}');
+      return d.release();
+    }
+  }
+  if (ch == '[') {
+    if (depth >= kMaxDepth) throw Fallback{"too deep"};
+    ++c.p;
+    Ref l{PyList_New(0)};
+    if (!l.o) throw Fallback{"out of memory"};
+    if (c.consume(']')) return l.release();
+    for (;;) {
+      Ref v{loads_value(c, scratch, depth + 1)};
+      if (PyList_Append(l.o, v.o) < 0) {
+        PyErr_Clear();
+        throw Fallback{"list append failed"};
+      }
+      if (c.consume(',')) continue;
+      c.expect(']');
+      return l.release();
+    }
+  }
+  const size_t left = static_cast<size_t>(c.end - c.p);
+  auto lit = [&](const char* w, size_t n) { return left >= n && memcmp(c.p, w, n) == 0; };
+  if (lit("true", 4)) {
+    c.p += 4;
+    Py_RETURN_TRUE;
+  }
+  if (lit("false", 5)) {
+    c.p += 5;
+    Py_RETURN_FALSE;
+  }
+  if (lit("null", 4)) {
+    c.p += 4;
+    Py_RETURN_NONE;
+  }
+  if (lit("NaN", 3)) {
+    c.p += 3;
+    return PyFloat_FromDouble(std::nan(""));
+  }
+  if (lit("Infinity", 8)) {
+    c.p += 8;
+    return PyFloat_FromDouble(HUGE_VAL);
+  }
+  return loads_number(c, scratch);
+}
+
+PyObject* loads(PyObject*, PyObject* obj) {
+  const char* b = nullptr;
+  Py_ssize_t n = 0;
+  Py_buffer view;
+  bool have_view = false;
+  if (PyUnicode_Check(obj)) {
+    b = PyUnicode_AsUTF8AndSize(obj, &n);  // fails on lone surrogates: json.loads handles those
+    if (!b) {
+      PyErr_Clear();
+      PyErr_SetString(g_fallback, "str not representable as UTF-8");
+      return nullptr;
+    }
+  } else if ((PyBytes_Check(obj) || PyByteArray_Check(obj)) && PyObject_GetBuffer(obj, &view, PyBUF_SIMPLE) == 0) {
+    have_view = true;
+    b = static_cast<const char*>(view.buf);
+    n = view.len;
+  } else {
+    PyErr_Clear();
+    PyErr_SetString(g_fallback, "not str, bytes or bytearray");  // json.loads' own TypeError
+    return nullptr;
+  }
+  PyObject* out = nullptr;
+  try {
+    Cursor c{b, b + n};
+    std::string scratch;
+    Ref v{loads_value(c, scratch, 0)};
+    c.ws();
+    if (c.p != c.end) throw Fallback{"trailing data"};
+    out = v.release();
+  } catch (const Fallback& f) {
+    if (PyErr_Occurred()) PyErr_Clear();
+    PyErr_SetString(g_fallback, f.why);
+  }
+  if (have_view) PyBuffer_Release(&view);
+  return out;
+}
+
 PyMethodDef methods[] = {
     {"scan_nodelist", scan_nodelist, METH_VARARGS, "Scan one NodeList page into a ScanResult."},
     {"prescan_nodelist", prescan_nodelist, METH_VARARGS, "Pass 1 of a NodeList page (GIL released) -> capsule."},
     {"scan_prescanned", scan_prescanned, METH_VARARGS, "Pass 2 of a prescanned page into a ScanResult."},
     {"dumps_indent2", dumps_indent2, METH_O, "json.dumps(obj, ensure_ascii=False, indent=2), natively."},
+    {"loads", loads, METH_O, "json.loads(data) for documents it provably reads alike; else FallbackError."},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_fastpath", "Native CPU hot path (NodeList scan, JSON emit).", -1,

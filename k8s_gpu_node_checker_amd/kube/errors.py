@@ -12,7 +12,9 @@ reproduced here with the same text shape:
 
 from __future__ import annotations
 
-from typing import Mapping, Optional
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Mapping, Optional
 
 
 class ConfigException(Exception):

@@ -21,10 +21,10 @@ run: driver not loaded, no permission).
 
 from __future__ import annotations
 
-import json
-import re
 import time
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 SCHEMA = "mi355x-health/v1"
 
@@ -313,7 +313,8 @@ def format_k8s_time(epoch: float) -> str:
 #: cross-check them against the node's ``amd.com/gpu`` without the report annotation:
 #: ``8/8 MI355X GPUs healthy``, ``8/8 MI355X GPUs ok; gpu3: HBM 96 C`` (degraded),
 #: ``6/7 MI355X GPUs ok; 7 of 8 GPUs visible to amd-smi; gpu2: ...`` (unhealthy).
-_COUNTS_RE = re.compile(r"^(\d+)/(\d+) MI355X GPUs (?:healthy|ok)\b")
+#: (parsed by hand, not with ``re``: the regex module is most of this module's import cost)
+_COUNTS_TAIL = " MI355X GPUs "
 
 
 def condition_message(verdict: Verdict) -> str:
@@ -329,8 +330,17 @@ def condition_message(verdict: Verdict) -> str:
 def parse_condition_counts(message: Optional[str]) -> Optional[Tuple[int, int]]:
     """``(gpus_ok, gpus_seen)`` from an ``AMDGPUHealthy`` message, None when it carries none
     (an older agent, or a probe failure)."""
-    m = _COUNTS_RE.match(message or "")
-    return (int(m.group(1)), int(m.group(2))) if m else None
+    msg = message or ""
+    head, sep, rest = msg.partition(_COUNTS_TAIL)
+    ok, slash, seen = head.partition("/")
+    if not sep or not slash or not ok.isdecimal() or not seen.isdecimal():
+        return None
+    for word in ("healthy", "ok"):
+        if rest.startswith(word):
+            nxt = rest[len(word):len(word) + 1]
+            if not nxt or not (nxt.isalnum() or nxt == "_"):  # the regex's \b
+                return int(ok), int(seen)
+    return None
 
 
 def condition_for(verdict: Verdict, now: Optional[float] = None,
@@ -391,8 +401,9 @@ def verdict_from_condition(cond: Tuple[Optional[str], Optional[str], Optional[st
 def parse_annotation(raw: Optional[str]) -> Optional[Dict[str, Any]]:
     if not raw:
         return None
+    from ..ops.fastpath import loads  # native json.loads (falls back to the json package itself)
     try:
-        doc = json.loads(raw)
+        doc = loads(raw)
     except ValueError:
         return {"schema": SCHEMA, "error": "annotation is not JSON", "ts": time.time()}
     return doc if isinstance(doc, dict) else None

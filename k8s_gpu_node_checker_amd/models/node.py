@@ -15,7 +15,10 @@ Report dict schema (reference ``:202-212``)::
 
 from __future__ import annotations
 
-from typing import Any, Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
+from _collections_abc import Mapping  # collections.abc.Mapping; loaded by os, unlike collections
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
 
 from .resources import GPU_RESOURCE_KEYS, PRIMARY_GPU_KEY, gpu_breakdown
 

@@ -28,11 +28,12 @@ Retry policies (``--slack-retry-policy``):
 
 from __future__ import annotations
 
-import json
 import os
 import sys
 import time
-from typing import Any, Callable, Optional, TextIO
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Any, Callable, Optional, TextIO
 
 from ..utils.backoff import Backoff
 from ..utils.http import HTTPError, request
@@ -55,6 +56,7 @@ def should_send(url: Optional[str], only_on_error: bool, ready_count: int) -> bo
 
 
 def slack_payload(message: str, username: str) -> bytes:
+    import json
     return json.dumps({"text": message, "username": username, "icon_emoji": ICON}).encode("ascii")
 
 

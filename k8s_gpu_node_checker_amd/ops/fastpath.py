@@ -19,8 +19,9 @@ SURVEY §6 takeaway 2: at 1000 nodes (5.9 MB NodeList) parse + projection is
 
 from __future__ import annotations
 
-import json
-from typing import Any, Optional, Sequence, Tuple
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Any, Optional, Sequence, Tuple
 
 from ..models.node import HEALTH_ANNOTATION, HEALTH_CONDITION, NodeExtras, ScanResult, scan_items
 from ..models.resources import GPU_RESOURCE_KEYS
@@ -36,6 +37,19 @@ def ext():
         _ext = load_extension("_fastpath")
         _ext_loaded = True
     return _ext
+
+
+def loads(data: Any) -> Any:
+    """``json.loads(data)``: the native parser when it can prove the result identical, else the json
+    package (which then raises exactly what it always raises)."""
+    mod = ext()
+    if mod is not None:
+        try:
+            return mod.loads(data)
+        except mod.FallbackError:
+            pass
+    import json
+    return json.loads(data)
 
 
 def backend() -> str:
@@ -83,6 +97,7 @@ def scan_page(body: bytes, result: ScanResult, keys: Sequence[str] = GPU_RESOURC
 
 def _scan_python(body: bytes, result: ScanResult, keys: Sequence[str], gpu_source: str, want_extras: bool,
                  annotation_mode: int) -> Tuple[Optional[str], int]:
+    import json
     doc = json.loads(body)
     if not isinstance(doc, dict):
         raise ValueError("NodeList response is not a JSON object")
@@ -102,4 +117,5 @@ def dumps_indent2(payload: Any) -> str:
             return mod.dumps_indent2(payload)
         except mod.FallbackError:
             pass
+    import json
     return json.dumps(payload, ensure_ascii=False, indent=2)

@@ -11,12 +11,11 @@ into a user cache.
 
 from __future__ import annotations
 
-import ctypes
-import importlib.machinery
-import importlib.util
 import os
 import sys
-from typing import Dict, Optional
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Dict, Optional
 
 NATIVE_DIR = os.environ.get("K8SGPU_NATIVE_DIR") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
@@ -39,12 +38,17 @@ def load_extension(name: str):
         return _cache[key]
     mod = None
     if os.environ.get("K8SGPU_DISABLE_NATIVE") != "1":
-        for suffix in importlib.machinery.EXTENSION_SUFFIXES:
+        # the import system's own (frozen, always loaded) machinery: importlib.util / .machinery are
+        # thin re-exports of it whose import is ~1 ms of a cold start
+        import _imp
+        from _frozen_importlib import module_from_spec
+        from _frozen_importlib_external import ExtensionFileLoader, spec_from_file_location
+        for suffix in _imp.extension_suffixes():
             path = os.path.join(NATIVE_DIR, name + suffix)
             if os.path.exists(path):
-                spec = importlib.util.spec_from_file_location(name, path)
+                spec = spec_from_file_location(name, path, loader=ExtensionFileLoader(name, path))
                 if spec is not None and spec.loader is not None:
-                    mod = importlib.util.module_from_spec(spec)
+                    mod = module_from_spec(spec)
                     spec.loader.exec_module(mod)  # type: ignore[union-attr]
                     sys.modules.setdefault(name, mod)
                 break
@@ -52,11 +56,12 @@ def load_extension(name: str):
     return mod
 
 
-def load_cdll(filename: str, required: bool = False) -> Optional[ctypes.CDLL]:
+def load_cdll(filename: str, required: bool = False) -> "Optional[ctypes.CDLL]":
     """Load a C-ABI shared library from ``_native``; raise loudly when ``required``."""
     key = "dll:" + filename
     if key in _cache and _cache[key] is not None:
         return _cache[key]  # type: ignore[return-value]
+    import ctypes  # here, not at module level: the checker's CLI path loads only the CPython extension
     path = native_path(filename)
     lib = None
     err = None

@@ -11,8 +11,9 @@ row (reference ``:240-249``); the bytes are the same.
 
 from __future__ import annotations
 
-import json
-from typing import Any, Dict, List, Optional, Sequence
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Any, Dict, List, Optional, Sequence
 
 SUMMARY_READY = "✅ Ready 상태의 GPU 노드: {ready}개 / 전체 GPU 노드: {total}개"
 SUMMARY_NOT_READY = "⚠️ GPU 노드는 {total}개 있으나, Ready 상태 노드는 없습니다."
@@ -82,6 +83,7 @@ def render_json(payload: Dict[str, Any]) -> str:
 
 def render_error_json(message: str) -> str:
     """Reference ``:322``: single line, no indent."""
+    import json
     return json.dumps({"error": message}, ensure_ascii=False) + "\n"
 
 

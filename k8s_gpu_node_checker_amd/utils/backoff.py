@@ -9,10 +9,10 @@ server sent ``Retry-After`` (seconds or an HTTP date), which wins (capped).
 from __future__ import annotations
 
 import time
-from typing import TYPE_CHECKING, Optional
-
-if TYPE_CHECKING:  # `random` costs a few ms of import time; only a real backoff needs it
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # `random` costs a few ms of import time; only a real backoff needs it (typing too)
     import random
+    from typing import Optional
 
 
 class Backoff:

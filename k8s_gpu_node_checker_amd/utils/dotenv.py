@@ -16,7 +16,9 @@ from __future__ import annotations
 
 import os
 import sys
-from typing import Callable, Dict, Iterator, Optional, Tuple
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Callable, Dict, Iterator, Optional, Tuple
 
 _KEY_CHARS = frozenset("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789_.-")
 _DQ_ESC = {"n": "\n", "t": "\t", "r": "\r", '"': '"', "\\": "\\", "'": "'", "$": "$"}

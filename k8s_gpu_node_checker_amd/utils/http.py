@@ -2,7 +2,7 @@
 
 Why not ``requests``/``urllib3``/``aiohttp``: at 1-16 nodes the reference's
 process wall clock is ~95 % interpreter + import cost (``import
-requests`` 138 ms, ``aiohttp`` 310 ms).  This module imports only ``socket``
+requests`` 138 ms, ``aiohttp`` 310 ms).  This module imports only ``_socket``
 (and ``ssl`` for https, ``zlib`` for gzip) and reads bodies with
 ``recv_into`` a pre-sized buffer, so a 5.9 MB NodeList is one allocation.
 
@@ -19,10 +19,13 @@ same failure, because the reference's Slack retry policy keys on that text
 
 from __future__ import annotations
 
+import _socket  # the C module: socket.py's enum setup costs ~2 ms of a 1-node cold start
 import errno
-import socket
-from typing import Dict, List, Optional, Tuple
-from urllib.parse import urlsplit
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Dict, List, Optional, Tuple
+
+from .urls import split as urlsplit
 
 _DEFAULT_PORTS = {"http": 80, "https": 443}
 
@@ -68,11 +71,19 @@ def _pool_name(scheme: str, host: str, port: int) -> str:
     return f"{pool}(host='{host}', port={port})"
 
 
-def _connect(target: Tuple[Optional[str], int], timeout: float) -> socket.socket:
-    """``socket.create_connection`` without the ``getaddrinfo`` round for IPv4 literals."""
+def _connect(target: Tuple[Optional[str], int], timeout: float, plain: bool = True) -> "socket.socket":
+    """``socket.create_connection`` without the ``getaddrinfo`` round for IPv4 literals.
+
+    A plain-TCP connection to an IPv4 literal (a mock or in-cluster service IP over http) uses a bare
+    ``_socket.socket``; names, IPv6 and anything TLS wraps (``ssl`` wants a ``socket.socket``) go
+    through the ``socket`` module, imported then."""
     host, port = target
     if host and host.count(".") == 3 and host.replace(".", "").isdigit():
-        sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        if plain:
+            sock = _socket.socket(_socket.AF_INET, _socket.SOCK_STREAM)
+        else:
+            import socket
+            sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         try:
             sock.settimeout(timeout)
             sock.connect((host, port))
@@ -80,6 +91,7 @@ def _connect(target: Tuple[Optional[str], int], timeout: float) -> socket.socket
         except BaseException:
             sock.close()
             raise
+    import socket
     return socket.create_connection((host, port), timeout=timeout)
 
 
@@ -97,7 +109,7 @@ class Connection:
         self.ssl_context = ssl_context
         self.server_hostname = server_hostname or self.host
         self.proxy = urlsplit(proxy_url) if proxy_url else None
-        self.sock: Optional[socket.socket] = None
+        self.sock: Optional["socket.socket"] = None
         self._buf = bytearray()
         host_hdr = self.host if ":" not in self.host else f"[{self.host}]"
         if self.port != _DEFAULT_PORTS.get(self.scheme):
@@ -128,17 +140,17 @@ class Connection:
             return
         target = (self.proxy.hostname, self.proxy.port or 80) if self.proxy else (self.host, self.port)
         try:
-            sock = _connect(target, self.timeout)
-        except socket.timeout as e:
+            sock = _connect(target, self.timeout, plain=self.scheme != "https")
+        except _socket.timeout as e:
             raise self._fail("connect_timeout", url, e)
-        except socket.gaierror as e:
+        except _socket.gaierror as e:
             raise self._fail("dns", url, e)
         except ConnectionRefusedError as e:
             raise self._fail("refused", url, e)
         except OSError as e:
             raise self._fail("refused" if e.errno in (errno.ECONNREFUSED, errno.EHOSTUNREACH,
                                                       errno.ENETUNREACH) else "aborted", url, e)
-        sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        sock.setsockopt(_socket.IPPROTO_TCP, _socket.TCP_NODELAY, 1)
         try:
             if self.proxy and self.scheme == "https":
                 self._tunnel(sock)
@@ -157,7 +169,7 @@ class Connection:
         self.sock = sock
         self._buf = bytearray()
 
-    def _tunnel(self, sock: socket.socket) -> None:
+    def _tunnel(self, sock: "socket.socket") -> None:
         req = (f"CONNECT {self.host}:{self.port} HTTP/1.1\r\nHost: {self.host}:{self.port}\r\n\r\n").encode()
         sock.sendall(req)
         data = b""
@@ -252,7 +264,7 @@ class Connection:
         except HTTPError:
             self.close()
             raise
-        except socket.timeout as e:
+        except _socket.timeout as e:
             self.close()
             raise self._fail("timeout", path, e)
         except OSError as e:
@@ -280,7 +292,7 @@ class Connection:
                 self.sock.sendall(raw)
                 return self._read_response(method, peek)
             raise
-        except socket.timeout as e:
+        except _socket.timeout as e:
             self.close()
             raise self._fail("timeout", url, e)
         except ConnectionResetError as e:
@@ -344,7 +356,7 @@ class Connection:
         except HTTPError:
             self.close()
             raise
-        except socket.timeout as e:
+        except _socket.timeout as e:
             self.close()
             raise self._fail("timeout", path, e)
         except OSError as e:
@@ -502,7 +514,7 @@ class LineStream:
                 continue
             try:
                 got = self.conn._recv_more()
-            except socket.timeout:
+            except _socket.timeout:
                 return None
             except OSError as e:
                 self.conn.close()

@@ -12,7 +12,9 @@ silently different.
 
 from __future__ import annotations
 
-from typing import Any, List, Optional, Tuple
+TYPE_CHECKING = False
+if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
+    from typing import Any, List, Optional, Tuple
 
 
 class Unsupported(ValueError):

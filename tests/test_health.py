@@ -320,3 +320,19 @@ def test_throttle_window_from_accumulators():
     assert H.throttle_window(b, a, 1.0) is None            # counter went backwards: driver reload
     assert H.throttle_window(a, dict(b, ppt=10), 1.0).get("power_pct") is None
     assert H.throttle_window({"n": 1}, {"n": 5}, 1.0) is None  # no residency fields at all
+
+
+def test_condition_counts_parser_matches_its_regex():
+    import re
+
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+    rx = re.compile(r"^(\d+)/(\d+) MI355X GPUs (?:healthy|ok)\b")
+
+    @settings(max_examples=500, deadline=None)
+    @given(st.from_regex(r"[0-9٣x/ ]{0,4}/?[0-9 ]{0,3} MI355X GPUs (healthy|ok|okay|heal)[ _;!a-zé]{0,3}",
+                         fullmatch=True) | st.text(max_size=30))
+    def check(msg):
+        m = rx.match(msg)
+        assert H.parse_condition_counts(msg) == ((int(m.group(1)), int(m.group(2))) if m else None), msg
+    check()

@@ -44,7 +44,8 @@ def test_fastpath_under_asan_ubsan(tmp_path):
                             "print(fastpath.ext().__file__)"], capture_output=True, text=True, env=env, cwd=REPO)
     assert which.stdout.strip() == str(out), (which.stdout, which.stderr[-1000:])
     p = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
-                        os.path.join(REPO, "tests", "test_fastpath.py")], capture_output=True, text=True, env=env,
+                        os.path.join(REPO, "tests", "test_fastpath.py"), os.path.join(REPO, "tests", "test_native_loads.py")],
+                       capture_output=True, text=True, env=env,
                        cwd=REPO, timeout=600)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert "passed" in p.stdout
