@@ -81,6 +81,28 @@ def _fabric_check(world, local_rank, cuda):
         return {"backend": "nccl(rccl)" if cuda else "gloo", "pass": False, "detail": f"{type(e).__name__}: {e}"}
 
 
+def _coldstart(api_url: str, runs: int) -> dict:
+    """Whole-process wall clock of ``check-gpu-node --json`` against the same mock (what a cron / CI user
+    pays per check), measured in child processes before this process touches the GPU: median of
+    ``runs`` after one untimed run (byte-code cache), and the interpreter's own start-up for scale."""
+    import statistics
+    import tempfile
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+    kc = write_kubeconfig(os.path.join(tempfile.mkdtemp(prefix="bench-kc"), "config"), api_url)
+    cmd = [sys.executable, os.path.join(REPO, "check-gpu-node.py"), "--kubeconfig", kc, "--json"]
+    env = {k: v for k, v in os.environ.items() if k not in ("SLACK_WEBHOOK_URL",)}
+
+    def wall(c):
+        t = time.perf_counter()
+        rc = subprocess.run(c, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env).returncode
+        return (time.perf_counter() - t) * 1e3, rc
+    _, rc = wall(cmd)
+    runs_ms = [wall(cmd)[0] for _ in range(runs)]
+    floor = [wall([sys.executable, "-c", "pass"])[0] for _ in range(runs)]
+    return {"ms": round(statistics.median(runs_ms), 2), "min_ms": round(min(runs_ms), 2), "runs": runs,
+            "exit_code": rc, "python_startup_ms": round(statistics.median(floor), 2)}
+
+
 def _pctl(xs, q):
     xs = sorted(xs)
     if not xs:
@@ -99,6 +121,8 @@ def main() -> int:
     ap.add_argument("--diag-level", type=int, default=1, choices=(0, 1, 2))
     ap.add_argument("--slack", action="store_true", help="also POST the Slack report to a local sink each step")
     ap.add_argument("--page-size", type=int, default=500)
+    ap.add_argument("--coldstart-runs", type=int, default=11,
+                    help="child-process runs of check-gpu-node --json for coldstart_ms (rank 0, before GPU work; 0: skip)")
     ap.add_argument("--no-fabric-check", dest="fabric_check", action="store_false",
                     help="skip the untimed all-reduce fabric check (world > 1)")
     args = ap.parse_args()
@@ -123,6 +147,8 @@ def main() -> int:
             p, sinfo = _spawn("k8s_gpu_node_checker_amd.testing.webhook_sink")
             procs.append(p)
             ctrl["slack"] = sinfo["url"] + "/200"
+    if rank == 0 and args.coldstart_runs > 0:
+        ctrl["coldstart"] = _coldstart(ctrl["api"], args.coldstart_runs)
     try:
         return _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl)
     finally:
@@ -255,11 +281,15 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
             "data": "synthetic: mock kube-apiserver, realistic Node objects, live MI355X probe annotations"
                     if probe_source != "fixture" else "synthetic: mock kube-apiserver, fixture probe annotations (no GPU)",
             "config": {"model": f"{n_nodes}-node MI355X mock cluster (amd.com/gpu:1 per node = 1 GPU per rank)",
-                       "global_batch": n_nodes, "seq_len": node_bytes,
+                       "global_batch": n_nodes, "seq_len": None, "node_bytes": node_bytes,
                        "parallelism": f"dp{n_gpus}" if n_gpus > 1 else "single",
                        "mode": args.mode, "slack": bool(args.slack), "page_size": args.page_size},
+            # p99 of fewer than 100 samples is the max: reported as null then
             "latency_ms": {"p50": round(_pctl(lat, 0.5) * 1e3, 4), "p90": round(_pctl(lat, 0.9) * 1e3, 4),
-                           "p99": round(_pctl(lat, 0.99) * 1e3, 4), "min": round(min(lat) * 1e3, 4)},
+                           "p99": round(_pctl(lat, 0.99) * 1e3, 4) if len(lat) >= 100 else None,
+                           "min": round(min(lat) * 1e3, 4), "samples": len(lat)},
+            "coldstart_ms": (ctrl.get("coldstart") or {}).get("ms"),
+            "coldstart": ctrl.get("coldstart"),
             "baseline_ms": ref,
             "check_ok": ok,
             "exit_code": last.exit_code if last else None,
