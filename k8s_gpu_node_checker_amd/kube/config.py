@@ -22,7 +22,8 @@ client certificate + key (file or ``*-data``), ``certificate-authority``
 (file or data), ``insecure-skip-tls-verify``, ``tls-server-name``,
 ``proxy-url`` (HTTP CONNECT), ``exec`` credential plugins
 (``client.authentication.k8s.io/v1`` and ``v1beta1``) and the legacy
-``auth-provider`` (``id-token`` / ``access-token``).
+``auth-provider`` (``oidc`` with id-token refresh and write-back, ``kube/oidc.py``; other providers'
+``id-token`` / ``access-token`` as static tokens).
 """
 
 from __future__ import annotations
@@ -96,6 +97,7 @@ def merge_kubeconfigs(paths: str) -> Tuple[Optional[Dict[str, Any]], Optional[st
                 body = item.get(inner)
                 if isinstance(body, dict):
                     body.setdefault("__base__", base)
+                    body.setdefault("__file__", os.path.abspath(path))  # where refreshed tokens go back
         if merged is None:
             merged = cfg
             first = path
@@ -147,6 +149,7 @@ class ClusterConnection:
         self.proxy_url: Optional[str] = None
         self.source = "kubeconfig"
         self._exec_cache: Optional[Tuple[Dict[str, Any], float]] = None
+        self.oidc = None  # kube/oidc.OidcProvider for `auth-provider: oidc`
         self._ssl_ctx = None
 
     # -- auth -----------------------------------------------------------------
@@ -162,7 +165,8 @@ class ClusterConnection:
         """Drop cached exec-plugin credentials (after a 401); True if the next request can present
         different credentials (exec plugin re-run or a re-read tokenFile), as client-go does."""
         self._exec_cache = None
-        return self.exec_spec is not None or bool(self.token_file)
+        refreshable = self.oidc is not None and self.oidc.invalidate()
+        return self.exec_spec is not None or bool(self.token_file) or refreshable
 
     def auth_headers(self) -> Dict[str, str]:
         token = self.token
@@ -172,6 +176,8 @@ class ClusterConnection:
                     token = f.read().strip()
             except OSError as e:
                 raise ConfigException("Invalid kube-config file. tokenFile %s: %s" % (self.token_file, e))
+        if self.oidc is not None:  # upstream tries the auth-provider first
+            token = self.oidc.token() or token
         if self.exec_spec is not None:
             status = self._run_exec()
             if status.get("token"):
@@ -238,7 +244,8 @@ class ClusterConnection:
 
     def describe(self) -> Dict[str, Any]:
         return {"server": self.server, "source": self.source, "insecure": self.insecure,
-                "auth": ("exec" if self.exec_spec else "token" if (self.token or self.token_file)
+                "auth": ("exec" if self.exec_spec else "oidc" if self.oidc is not None
+                         else "token" if (self.token or self.token_file)
                          else "cert" if (self.cert_file or self.cert_data) else
                          "basic" if self.username else "none")}
 
@@ -293,7 +300,10 @@ def connection_from_config(cfg: Dict[str, Any], context: Optional[str] = None) -
     conn.username = user.get("username")
     conn.password = user.get("password")
     provider = user.get("auth-provider")
-    if isinstance(provider, dict) and not conn.token:
+    if isinstance(provider, dict) and provider.get("name") == "oidc" and isinstance(provider.get("config"), dict):
+        from .oidc import OidcProvider
+        conn.oidc = OidcProvider(provider["config"], str(user_name), user.get("__file__"), ubase)
+    elif isinstance(provider, dict) and not conn.token:
         pcfg = provider.get("config") or {}
         conn.token = pcfg.get("id-token") or pcfg.get("access-token")
     if isinstance(user.get("exec"), dict):

@@ -111,9 +111,18 @@ def test_basic_auth(tmp_path):
 
 
 def test_auth_provider_id_token(tmp_path):
+    # upstream _load_oid_token: only a well-formed JWT is presented; "idt" is not one -> no header
     conn = K.load_kube_config(write(tmp_path / "x", cfg(user={"auth-provider": {"name": "oidc",
                                                                                 "config": {"id-token": "idt"}}})))
-    assert conn.auth_headers() == {"Authorization": "Bearer idt"}
+    assert conn.auth_headers() == {} and conn.describe()["auth"] == "oidc"
+    jwt = "eyJhbGciOiJub25lIn0.eyJzdWIiOiJ1In0.sig"  # {"sub": "u"}: no exp, never refreshed
+    conn = K.load_kube_config(write(tmp_path / "y", cfg(user={"auth-provider": {"name": "oidc",
+                                                                                "config": {"id-token": jwt}}})))
+    assert conn.auth_headers() == {"Authorization": "Bearer " + jwt}
+    # other providers (gcp/azure legacy configs): the cached access-token as a static bearer token
+    conn = K.load_kube_config(write(tmp_path / "z", cfg(user={"auth-provider": {"name": "gcp",
+                                                                                "config": {"access-token": "at"}}})))
+    assert conn.auth_headers() == {"Authorization": "Bearer at"}
 
 
 def test_tls_fields(tmp_path):
