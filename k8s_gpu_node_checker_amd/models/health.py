@@ -357,6 +357,24 @@ def condition_for(verdict: Verdict, now: Optional[float] = None,
             "lastHeartbeatTime": ts, "lastTransitionTime": transition}
 
 
+_PARTS: Dict[Optional[str], Tuple[Optional[Tuple[int, int]], str]] = {}
+
+
+def _message_parts(message: Optional[str]) -> Tuple[Optional[Tuple[int, int]], str]:
+    """``(counts, detail)`` of a condition message, memoised: across a cluster the agents publish a
+    handful of distinct messages ("8/8 MI355X GPUs healthy" on every healthy node)."""
+    got = _PARTS.get(message)
+    if got is None:
+        counts = parse_condition_counts(message)
+        detail = message or ""
+        if counts:
+            detail = detail.split("; ", 1)[1] if "; " in detail else ""
+        if len(_PARTS) >= 4096:
+            _PARTS.clear()
+        got = _PARTS[message] = (counts, detail)
+    return got
+
+
 def verdict_from_condition(cond: Tuple[Optional[str], Optional[str], Optional[str], Optional[float]],
                            max_age_s: float, now: Optional[float] = None, expected_gpus: int = 0) -> Verdict:
     """``(status, reason, message, heartbeat_epoch)`` of an ``AMDGPUHealthy`` condition -> Verdict.
@@ -376,11 +394,8 @@ def verdict_from_condition(cond: Tuple[Optional[str], Optional[str], Optional[st
     if age is None or age > max_age_s:
         return Verdict(UNKNOWN, ["stale AMDGPUHealthy condition" if age is not None
                                  else "AMDGPUHealthy condition has no heartbeat"], age_s=age)
-    counts = parse_condition_counts(message)
+    counts, detail = _message_parts(message)
     ok, seen = counts if counts else (0, 0)
-    detail = message or ""
-    if counts:
-        detail = detail.split("; ", 1)[1] if "; " in detail else ""
     msg = [detail] if detail else []
     if status == "True":
         state = _STATE_OF_REASON.get(reason or "", HEALTHY)
