@@ -36,7 +36,8 @@ from typing import Any, Dict, List, Optional, Sequence
 
 from ..models.health import (HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, XGMI_LINKS_EXPECTED,
                               HealthExpectations, Verdict,
-                              condition_for, condition_reason, evaluate_report, format_k8s_time, throttle_window)
+                              condition_for, condition_reason, evaluate_report, format_k8s_time, fw_version_str,
+                              throttle_window)
 from ..models.node import HEALTH_ANNOTATION
 from ..models.resources import PRIMARY_GPU_KEY, gpu_breakdown
 
@@ -418,56 +419,73 @@ class Agent:
         return client.update_node_taints(self.node, edit) is not None
 
 
+def _esc(v: Any) -> str:
+    """A Prometheus label value (text exposition format escapes)."""
+    return str(v).replace("\\", "\\\\").replace("\n", "\\n").replace('"', '\\"')
+
+
 def _metrics(rep: Optional[Dict[str, Any]]) -> str:
+    """Prometheus text exposition of the last probe.  Samples are collected per metric family and each
+    family is written as one group under its ``# TYPE`` line (the format requires it; a per-GPU loop
+    that interleaves families makes parsers see the same family twice)."""
     if not rep:
         return "# no probe yet\n"
-    lines = ["# TYPE mi355x_agent_probe_timestamp_seconds gauge", f"mi355x_agent_probe_timestamp_seconds {rep.get('ts', 0)}",
-             "# TYPE mi355x_gpu_ecc_uncorrectable gauge", "# TYPE mi355x_gpu_xgmi_links_up gauge",
-             "# TYPE mi355x_gpu_hotspot_celsius gauge", "# TYPE mi355x_gpu_pcie_width gauge",
-             "# TYPE mi355x_gpu_pcie_replays counter", "# TYPE mi355x_gpu_power_watts gauge",
-             "# TYPE mi355x_gpu_power_cap_watts gauge", "# TYPE mi355x_gpu_hbm_celsius gauge",
-             "# TYPE mi355x_gpu_gfxclk_mhz gauge", "# TYPE mi355x_gpu_vram_used_megabytes gauge",
-             "# TYPE mi355x_gpu_throttle_percent gauge", "# TYPE mi355x_gpu_gfx_activity_percent gauge",
-             "# TYPE mi355x_gpu_diag_skipped gauge"]
+    fams: Dict[str, List[str]] = {}
+    counters = {"mi355x_gpu_pcie_replays"}
+
+    def put(name: str, labels: str, value: Any) -> None:
+        fams.setdefault(name, []).append(f"{name}{{{labels}}} {value}" if labels else f"{name} {value}")
+
+    put("mi355x_agent_probe_timestamp_seconds", "", rep.get("ts", 0))
+    drv = rep.get("driver")
+    if isinstance(drv, dict) and drv.get("version"):
+        put("mi355x_node_driver_info", f'name="{_esc(drv.get("name"))}",version="{_esc(drv["version"])}"', 1)
     for g in rep.get("gpus") or []:
-        lbl = f'gpu="{g.get("index")}",bdf="{g.get("bdf", "")}"'
-        if isinstance(g.get("ecc_uncorrectable"), int):
-            lines.append(f"mi355x_gpu_ecc_uncorrectable{{{lbl}}} {g['ecc_uncorrectable']}")
+        lbl = f'gpu="{g.get("index")}",bdf="{_esc(g.get("bdf", ""))}"'
+        for key, metric in (("ecc_uncorrectable", "ecc_uncorrectable"), ("pcie_width", "pcie_width"),
+                            ("pcie_replays", "pcie_replays"), ("xgmi_error", "xgmi_error_status")):
+            if isinstance(g.get(key), int) and not isinstance(g.get(key), bool):
+                put(f"mi355x_gpu_{metric}", lbl, g[key])
         if isinstance(g.get("xgmi"), str):
-            lines.append(f"mi355x_gpu_xgmi_links_up{{{lbl}}} {g['xgmi'].count('U')}")
-        if isinstance(g.get("hotspot_c"), (int, float)):
-            lines.append(f"mi355x_gpu_hotspot_celsius{{{lbl}}} {g['hotspot_c']}")
-        if isinstance(g.get("pcie_width"), int):
-            lines.append(f"mi355x_gpu_pcie_width{{{lbl}}} {g['pcie_width']}")
-        if isinstance(g.get("pcie_replays"), int):
-            lines.append(f"mi355x_gpu_pcie_replays{{{lbl}}} {g['pcie_replays']}")
-        for key, metric in (("power_w", "power_watts"), ("power_cap_w", "power_cap_watts"),
-                            ("hbm_temp_c", "hbm_celsius"), ("gfxclk_mhz", "gfxclk_mhz"),
-                            ("vram_used_mb", "vram_used_megabytes"), ("gfx_activity", "gfx_activity_percent")):
-            if isinstance(g.get(key), (int, float)):
-                lines.append(f"mi355x_gpu_{metric}{{{lbl}}} {g[key]}")
+            put("mi355x_gpu_xgmi_links_up", lbl, g["xgmi"].count("U"))
+        for key, metric in (("hotspot_c", "hotspot_celsius"), ("power_w", "power_watts"),
+                            ("power_cap_w", "power_cap_watts"), ("hbm_temp_c", "hbm_celsius"),
+                            ("gfxclk_mhz", "gfxclk_mhz"), ("vram_used_mb", "vram_used_megabytes"),
+                            ("gfx_activity", "gfx_activity_percent")):
+            if isinstance(g.get(key), (int, float)) and not isinstance(g.get(key), bool):
+                put(f"mi355x_gpu_{metric}", lbl, g[key])
         for kind in ("thermal", "power", "prochot"):
             v = (g.get("throttle") or {}).get(f"{kind}_pct")
             if isinstance(v, (int, float)):
-                lines.append(f'mi355x_gpu_throttle_percent{{{lbl},kind="{kind}"}} {v}')
+                put("mi355x_gpu_throttle_percent", f'{lbl},kind="{kind}"', v)
+        for block, c in ((g.get("ecc_blocks") or {}) if isinstance(g.get("ecc_blocks"), dict) else {}).items():
+            for kind in ("ce", "ue", "de"):
+                if isinstance(c, dict) and isinstance(c.get(kind), int):
+                    put("mi355x_gpu_ecc_block_errors", f'{lbl},block="{_esc(block)}",kind="{kind}"', c[kind])
+        for image, ver in ((g.get("fw") or {}) if isinstance(g.get("fw"), dict) else {}).items():
+            put("mi355x_gpu_firmware_info", f'{lbl},image="{_esc(image)}",version="{_esc(fw_version_str(image, ver))}"', 1)
         if g.get("diag") is not None or g.get("diag_skipped"):
-            lines.append(f"mi355x_gpu_diag_skipped{{{lbl}}} {1 if g.get('diag_skipped') else 0}")
+            put("mi355x_gpu_diag_skipped", lbl, 1 if g.get("diag_skipped") else 0)
         for test, res in (g.get("diag") or {}).items():
+            if not isinstance(res, dict):
+                continue
             for k in ("tflops", "copy_tbs", "read_tbs", "errors", "h2d_gbps", "d2h_gbps"):
                 if isinstance(res.get(k), (int, float)):
-                    lines.append(f'mi355x_gpu_diag_{k}{{{lbl},test="{test}"}} {res[k]}')
+                    put(f"mi355x_gpu_diag_{k}", f'{lbl},test="{_esc(test)}"', res[k])
             for kind, row in ((res.get("kinds") or {}) if isinstance(res.get("kinds"), dict) else {}).items():
-                lines.append(f'mi355x_gpu_diag_tflops{{{lbl},test="{test}",dtype="{kind}"}} {row.get("tflops", 0)}')
+                put("mi355x_gpu_diag_tflops", f'{lbl},test="{_esc(test)}",dtype="{_esc(kind)}"', row.get("tflops", 0))
     fabric = (rep.get("fabric") or {}).get("p2p")
     if isinstance(fabric, dict) and isinstance(fabric.get("median_gbps"), (int, float)):
-        lines.append("# TYPE mi355x_node_xgmi_p2p_gbps gauge")
-        lines.append(f'mi355x_node_xgmi_p2p_gbps{{stat="median"}} {fabric["median_gbps"]}')
-        lines.append(f'mi355x_node_xgmi_p2p_gbps{{stat="min"}} {fabric.get("min_gbps", 0)}')
+        put("mi355x_node_xgmi_p2p_gbps", 'stat="median"', fabric["median_gbps"])
+        put("mi355x_node_xgmi_p2p_gbps", 'stat="min"', fabric.get("min_gbps", 0))
     rccl = (rep.get("fabric") or {}).get("rccl")
     if isinstance(rccl, dict) and isinstance(rccl.get("best_busbw_by_op"), dict):
-        lines.append("# TYPE mi355x_node_rccl_busbw_gbps gauge")
         for op, bw in sorted(rccl["best_busbw_by_op"].items()):
-            lines.append(f'mi355x_node_rccl_busbw_gbps{{op="{op}"}} {bw}')
+            put("mi355x_node_rccl_busbw_gbps", f'op="{_esc(op)}"', bw)
+    lines: List[str] = []
+    for name, samples in fams.items():
+        lines.append(f"# TYPE {name} {'counter' if name in counters else 'gauge'}")
+        lines += samples
     return "\n".join(lines) + "\n"
 
 

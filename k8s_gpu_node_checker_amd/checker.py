@@ -121,11 +121,44 @@ class CheckResult:
         return {
             "mi355x": {
                 "health_summary": H.summarize(self.verdicts) if self.verdicts else None,
+                "fleet": fleet_versions(self.scan.extras),
                 "nodes": nodes,
             },
             "timings_ms": self.tracer.as_ms(),
             "items_seen": self.scan.items_seen,
         }
+
+
+def fleet_versions(extras: List[Any]) -> Optional[Dict[str, Any]]:
+    """Software versions across the MI355X nodes that publish a report (``--json-extended``): amdgpu
+    driver, and firmware per image, each as ``{version: node count}``.  More than one key in a row is
+    a fleet that was only partly upgraded -- jobs spanning those nodes run on different driver or
+    firmware behaviour.  None when no node carries a report."""
+    drivers: Dict[str, int] = {}
+    firmware: Dict[str, Dict[str, int]] = {}
+    n = 0
+    for ex in extras:
+        rep = H.parse_annotation(ex.health_annotation) if ex is not None else None
+        if not rep or rep.get("error"):
+            continue
+        n += 1
+        drv = (rep.get("driver") or {}).get("version") if isinstance(rep.get("driver"), dict) else None
+        if drv:
+            drivers[str(drv)] = drivers.get(str(drv), 0) + 1
+        node_fw: Dict[str, set] = {}
+        for g in rep.get("gpus") or []:
+            for name, ver in ((g.get("fw") or {}) if isinstance(g, dict) and isinstance(g.get("fw"), dict)
+                              else {}).items():
+                node_fw.setdefault(name, set()).add(H.fw_version_str(name, ver))
+        for name, vers in node_fw.items():
+            row = firmware.setdefault(name, {})
+            for v in vers:  # a node with two versions of one image counts under both
+                row[v] = row.get(v, 0) + 1
+    if not n:
+        return None
+    mixed = sorted([k for k, row in firmware.items() if len(row) > 1] + (["driver"] if len(drivers) > 1 else []))
+    return {"nodes_reporting": n, "driver": drivers, "firmware": {k: firmware[k] for k in sorted(firmware)},
+            "mixed": mixed}
 
 
 def scan_cluster(cluster: ClusterConnection, opts: CheckOptions, tracer: Tracer) -> ScanResult:

@@ -1,8 +1,9 @@
 // MI355X passive health probe: libamd_smi -> "mi355x-health/v1" JSON (see probe.h).
 //
 // Checks what SURVEY §7.1 lists (ASIC/gfx950, HBM3E VRAM size, ECC, xGMI links,
-// KFD node) plus bad pages, partition modes, hotspot temperature, the PCIe link
-// and operating telemetry (power, HBM temperature, clock, throttle residency).  Every
+// KFD node) plus bad pages, partition modes, hotspot temperature, the PCIe link,
+// the driver and firmware versions, the RAS block behind any ECC count, the xGMI error
+// status and operating telemetry (power, HBM temperature, clock, throttle residency).  Every
 // amd-smi status other than success is recorded, never thrown: a node whose
 // driver is not loaded (AMDSMI_STATUS_DRIVER_NOT_LOADED) or that denies access
 // (AMDSMI_STATUS_NO_PERM) yields a report with "error" set, which the checker
@@ -29,6 +30,9 @@ std::mutex g_mu;
 bool g_open = false;
 std::atomic<int> g_gpus{-1};  // read without the lock by mi355x_probe_gpu_count
 std::vector<amdsmi_processor_handle> g_handles;
+// per-handle firmware JSON object; firmware only changes across a driver reload, which also
+// invalidates the handles, so it is read once per open (amdsmi_get_fw_info reads ~80 sysfs files)
+std::vector<std::string> g_fw;
 
 void jstr(std::string& o, const char* s) {
   o.push_back('"');
@@ -104,9 +108,86 @@ int open_locked() {
         g_handles.push_back(hs[i]);
     }
   }
+  g_fw.assign(g_handles.size(), std::string());
   g_open = true;
   g_gpus.store(static_cast<int>(g_handles.size()), std::memory_order_relaxed);
   return 0;
+}
+
+// The firmware images that decide how a GPU behaves under load and under faults: power management
+// (SMU / PM firmware), the security processor's OS, the compute queues (MEC), RLC, SDMA, and the RAS / xGMI
+// trusted apps.  All GPUs of a node are flashed together, so a difference between them is a node
+// that was half-updated (models/health.py compares them).
+const char* fw_name(amdsmi_fw_block_t id) {
+  switch (id) {
+    case AMDSMI_FW_ID_SMU: return "smu";
+    case AMDSMI_FW_ID_PM: return "pm";
+    case AMDSMI_FW_ID_PSP_SOSDRV: return "psp_sos";
+    case AMDSMI_FW_ID_CP_MEC1: return "mec";
+    case AMDSMI_FW_ID_RLC: return "rlc";
+    case AMDSMI_FW_ID_SDMA0: return "sdma";
+    case AMDSMI_FW_ID_TA_RAS: return "ta_ras";
+    case AMDSMI_FW_ID_TA_XGMI: return "ta_xgmi";
+    case AMDSMI_FW_ID_PLDM_BUNDLE: return "pldm_bundle";
+    default: return nullptr;
+  }
+}
+
+const std::string& firmware_locked(size_t i) {
+  std::string& s = g_fw[i];
+  if (!s.empty()) return s;
+  amdsmi_fw_info_t fw;
+  memset(&fw, 0, sizeof fw);
+  s = "{";
+  if (amdsmi_get_fw_info(g_handles[i], &fw) == AMDSMI_STATUS_SUCCESS) {
+    const size_t n = std::min<size_t>(fw.num_fw_info, AMDSMI_FW_ID__MAX);
+    for (size_t k = 0; k < n; ++k) {
+      const char* name = fw_name(fw.fw_info_list[k].fw_id);
+      if (name && fw.fw_info_list[k].fw_version != 0 && fw.fw_info_list[k].fw_version != UINT64_MAX)
+        kv_u64(s, name, fw.fw_info_list[k].fw_version);
+    }
+  }
+  s.push_back('}');
+  return s;
+}
+
+// RAS blocks, named as the kernel's ras sysfs does; asked only when the totals are non-zero, so a clean
+// GPU costs no extra reads
+const struct {
+  amdsmi_gpu_block_t block;
+  const char* name;
+} kRasBlocks[] = {{AMDSMI_GPU_BLOCK_UMC, "umc"},     {AMDSMI_GPU_BLOCK_SDMA, "sdma"},
+                  {AMDSMI_GPU_BLOCK_GFX, "gfx"},     {AMDSMI_GPU_BLOCK_MMHUB, "mmhub"},
+                  {AMDSMI_GPU_BLOCK_ATHUB, "athub"}, {AMDSMI_GPU_BLOCK_PCIE_BIF, "pcie_bif"},
+                  {AMDSMI_GPU_BLOCK_HDP, "hdp"},     {AMDSMI_GPU_BLOCK_XGMI_WAFL, "xgmi_wafl"},
+                  {AMDSMI_GPU_BLOCK_DF, "df"},       {AMDSMI_GPU_BLOCK_SMN, "smn"},
+                  {AMDSMI_GPU_BLOCK_SEM, "sem"},     {AMDSMI_GPU_BLOCK_MP0, "mp0"},
+                  {AMDSMI_GPU_BLOCK_MP1, "mp1"},     {AMDSMI_GPU_BLOCK_FUSE, "fuse"},
+                  {AMDSMI_GPU_BLOCK_MCA, "mca"},     {AMDSMI_GPU_BLOCK_VCN, "vcn"},
+                  {AMDSMI_GPU_BLOCK_JPEG, "jpeg"},   {AMDSMI_GPU_BLOCK_IH, "ih"},
+                  {AMDSMI_GPU_BLOCK_MPIO, "mpio"}};
+
+// {"umc":{"ce":..,"ue":..,"de":..},...}: which hardware block the ECC errors come from (HBM behind the
+// memory controller, the xGMI PHYs, the GFX engines...)
+void ecc_blocks(std::string& o, amdsmi_processor_handle h) {
+  std::string b = "{";
+  for (const auto& rb : kRasBlocks) {
+    amdsmi_error_count_t ec;
+    memset(&ec, 0, sizeof ec);
+    if (amdsmi_get_gpu_ecc_count(h, rb.block, &ec) != AMDSMI_STATUS_SUCCESS) continue;
+    if (!ec.correctable_count && !ec.uncorrectable_count && !ec.deferred_count) continue;
+    key(b, rb.name);
+    b.push_back('{');
+    kv_u64(b, "ce", ec.correctable_count);
+    kv_u64(b, "ue", ec.uncorrectable_count);
+    kv_u64(b, "de", ec.deferred_count);
+    b.push_back('}');
+  }
+  b.push_back('}');
+  if (b.size() > 2) {
+    key(o, "ecc_blocks");
+    o += b;
+  }
 }
 
 // Operating state, not identity: power against its cap, HBM stack temperature, clock, VRAM in use,
@@ -251,7 +332,15 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
   if (amdsmi_get_gpu_board_info(h, &board) == AMDSMI_STATUS_SUCCESS) kv_str(o, "product_name", board.product_name);
   amdsmi_vbios_info_t vb;
   memset(&vb, 0, sizeof vb);
-  if (amdsmi_get_gpu_vbios_info(h, &vb) == AMDSMI_STATUS_SUCCESS) kv_str(o, "vbios_name", vb.name);
+  if (amdsmi_get_gpu_vbios_info(h, &vb) == AMDSMI_STATUS_SUCCESS) {
+    kv_str(o, "vbios_name", vb.name);
+    if (vb.version[0]) kv_str(o, "vbios_version", vb.version);
+  }
+  const std::string& fw = firmware_locked(static_cast<size_t>(index));
+  if (fw.size() > 2) {
+    key(o, "fw");
+    o += fw;
+  }
 
   amdsmi_vram_info_t vram;
   memset(&vram, 0, sizeof vram);
@@ -265,6 +354,7 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
     kv_u64(o, "ecc_correctable", ec.correctable_count);
     kv_u64(o, "ecc_uncorrectable", ec.uncorrectable_count);
     kv_u64(o, "ecc_deferred", ec.deferred_count);
+    if (ec.correctable_count || ec.uncorrectable_count || ec.deferred_count) ecc_blocks(o, h);
   } else {
     kv_null(o, "ecc_uncorrectable");
   }
@@ -287,6 +377,9 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
   } else {
     kv_null(o, "xgmi");
   }
+  // sticky until reset: the xGMI PHYs saw errors (one, or several) since the driver loaded
+  amdsmi_xgmi_status_t xe = AMDSMI_XGMI_STATUS_NO_ERRORS;
+  if (amdsmi_gpu_xgmi_error_status(h, &xe) == AMDSMI_STATUS_SUCCESS) kv_u64(o, "xgmi_error", static_cast<uint64_t>(xe));
   amdsmi_kfd_info_t kfd;
   memset(&kfd, 0, sizeof kfd);
   bool kfd_ok = amdsmi_get_gpu_kfd_info(h, &kfd) == AMDSMI_STATUS_SUCCESS && kfd.kfd_id != UINT64_MAX &&
@@ -363,6 +456,19 @@ extern "C" char* mi355x_probe_json(const char* node_name) {
     o += "[]}";
     return dup(o);
   }
+  if (!g_handles.empty()) {
+    amdsmi_driver_info_t drv;
+    memset(&drv, 0, sizeof drv);
+    if (amdsmi_get_gpu_driver_info(g_handles[0], &drv) == AMDSMI_STATUS_SUCCESS && drv.driver_version[0]) {
+      drv.driver_name[sizeof drv.driver_name - 1] = '\0';
+      drv.driver_version[sizeof drv.driver_version - 1] = '\0';
+      key(o, "driver");
+      o.push_back('{');
+      kv_str(o, "name", drv.driver_name);
+      kv_str(o, "version", drv.driver_version);
+      o.push_back('}');
+    }
+  }
   key(o, "gpus");
   o.push_back('[');
   for (size_t i = 0; i < g_handles.size(); ++i) {
@@ -387,5 +493,6 @@ extern "C" void mi355x_probe_close(void) {
     amdsmi_shut_down();
     g_open = false;
     g_handles.clear();
+    g_fw.clear();
   }
 }

@@ -156,6 +156,64 @@ def throttle_window(prev: Optional[Dict[str, Any]], cur: Optional[Dict[str, Any]
     return out if len(out) > 1 else None
 
 
+#: amdsmi_xgmi_status_t
+XGMI_ERROR_STATUS = {0: "no errors", 1: "errors", 2: "multiple errors"}
+
+
+def _by_block(blocks: Dict[str, Any], kind: str) -> str:
+    """`` (umc 3, xgmi_wafl 1)``: the RAS blocks an ECC count comes from (probe ``ecc_blocks``)."""
+    parts = [f"{name} {c[kind]}" for name, c in blocks.items()
+             if isinstance(c, dict) and isinstance(c.get(kind), int) and c[kind] > 0]
+    return f" ({', '.join(parts)})" if parts else ""
+
+
+_FW_HEX = frozenset(("psp_sos", "ta_ras", "ta_xgmi"))
+_FW_DEC = frozenset(("pm", "pldm_bundle"))
+
+
+def fw_version_str(name: str, v: Any) -> str:
+    """A firmware version as ``amd-smi firmware`` prints it: the security-processor images as dotted hex
+    bytes (``00.45.00.2F``), PM firmware and the PLDM bundle as dotted decimal bytes (``04.86.15.106``),
+    the rest as the plain number."""
+    if not isinstance(v, int) or isinstance(v, bool) or v < 0:
+        return str(v)
+    if name in _FW_HEX or name in _FW_DEC:
+        h = f"{v:08x}"
+        parts = [h[i:i + 2] for i in range(0, len(h), 2)]
+        if name in _FW_HEX:
+            return ".".join(parts).upper()
+        return ".".join(f"{int(b, 16):02d}" for b in parts)
+    return str(v)
+
+
+def firmware_mismatch(gpus: Sequence[Any]) -> List[str]:
+    """Firmware images whose version differs between the GPUs of one node (probe ``fw``).
+
+    The GPUs of a node are flashed as one bundle; two versions of the same image on one node mean an
+    update that stopped half-way, and GPUs that will behave differently under the same job.  One entry
+    per image: ``psp_sos: gpu0-6 00.45.00.2F, gpu7 00.45.00.00``; versions are stable, so the condition message stays
+    stable probe to probe."""
+    seen: Dict[str, Dict[Any, List[Any]]] = {}
+    for g in gpus:
+        if not isinstance(g, dict) or not isinstance(g.get("fw"), dict):
+            continue
+        for name, ver in g["fw"].items():
+            seen.setdefault(name, {}).setdefault(ver, []).append(g.get("index", "?"))
+    out = []
+    for name in sorted(seen):
+        vers = seen[name]
+        if len(vers) > 1:
+            groups = sorted(vers.items(), key=lambda kv: (-len(kv[1]), str(kv[0])))
+            out.append(f"{name}: " + ", ".join(f"gpu{_span(ix)} {fw_version_str(name, v)}" for v, ix in groups))
+    return out
+
+
+def _span(ix: List[Any]) -> str:
+    if len(ix) > 1 and all(isinstance(i, int) for i in ix) and ix == list(range(ix[0], ix[0] + len(ix))):
+        return f"{ix[0]}-{ix[-1]}"
+    return ",".join(str(i) for i in ix)
+
+
 def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str], List[str]]:
     """Return ``(failures, warnings)`` for one GPU entry of a probe report."""
     fail: List[str] = []
@@ -177,15 +235,16 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str],
         need = VRAM_MB_FULL / _nps(g.get("memory_partition")) * exp.vram_min_fraction
         if vram < need:
             fail.append(f"gpu{idx}: VRAM {vram} MB < {need:.0f} MB expected")
+    blocks = g.get("ecc_blocks") if isinstance(g.get("ecc_blocks"), dict) else {}
     ue = g.get("ecc_uncorrectable")
     if isinstance(ue, int) and ue > 0:
-        fail.append(f"gpu{idx}: {ue} uncorrectable ECC errors")
+        fail.append(f"gpu{idx}: {ue} uncorrectable ECC errors{_by_block(blocks, 'ue')}")
     de = g.get("ecc_deferred")
     if isinstance(de, int) and de > 0:
-        warn.append(f"gpu{idx}: {de} deferred ECC errors")
+        warn.append(f"gpu{idx}: {de} deferred ECC errors{_by_block(blocks, 'de')}")
     ce = g.get("ecc_correctable")
     if isinstance(ce, int) and ce > exp.correctable_warn:
-        warn.append(f"gpu{idx}: {ce} correctable ECC errors")
+        warn.append(f"gpu{idx}: {ce} correctable ECC errors{_by_block(blocks, 'ce')}")
     bp = g.get("bad_pages")
     if isinstance(bp, int):
         if bp > exp.bad_page_limit:
@@ -199,6 +258,10 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str],
             fail.append(f"gpu{idx}: {down} xGMI link(s) down ({links})")
         elif up < exp.xgmi_links:
             fail.append(f"gpu{idx}: {up}/{exp.xgmi_links} xGMI links up ({links})")
+    xe = g.get("xgmi_error")
+    if isinstance(xe, int) and xe > 0 and exp.xgmi_links > 0:
+        # sticky since the driver loaded: the link PHYs retried or dropped traffic at least once
+        warn.append(f"gpu{idx}: xGMI error status {XGMI_ERROR_STATUS.get(xe, xe)}")
     if g.get("kfd") is False:
         fail.append(f"gpu{idx}: no KFD node (not usable by ROCm)")
     cus = g.get("cus")
@@ -266,6 +329,9 @@ def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
         ok += 0 if f else 1
     if expected_gpus and len(gpus) < expected_gpus:
         fails.append(f"{len(gpus)} of {expected_gpus} GPUs visible to amd-smi")
+    mism = firmware_mismatch(gpus)
+    if mism:
+        warns.append("firmware differs across GPUs: " + "; ".join(mism))
     fabric = report.get("fabric")
     if isinstance(fabric, dict):
         for test, res in fabric.items():  # node-level: the xGMI pair matrix (ops/diag.p2p_matrix)

@@ -127,6 +127,46 @@ def _telemetry_python(A: Any, h: Any, q: Any) -> Dict[str, Any]:
     return {k: v for k, v in t.items() if v is not None}
 
 
+# csrc/probe/probe.cpp fw_name() and kRasBlocks: the same images and blocks, under the same names
+_FW_NAMES = {"SMU": "smu", "PM": "pm", "PSP_SOSDRV": "psp_sos", "CP_MEC1": "mec", "RLC": "rlc", "SDMA0": "sdma",
+             "TA_RAS": "ta_ras", "TA_XGMI": "ta_xgmi", "PLDM_BUNDLE": "pldm_bundle"}
+_RAS_BLOCKS = ("UMC", "SDMA", "GFX", "MMHUB", "ATHUB", "PCIE_BIF", "HDP", "XGMI_WAFL", "DF", "SMN", "SEM", "MP0",
+               "MP1", "FUSE", "MCA", "VCN", "JPEG", "IH", "MPIO")
+
+
+def _firmware_python(A: Any, h: Any) -> Optional[Dict[str, int]]:
+    """Raw firmware versions (integers, as the native probe reports them): the binding's
+    ``amdsmi_get_fw_info`` re-formats some of them as dotted strings, so the C struct is read directly."""
+    try:
+        W = A.amdsmi_interface.amdsmi_wrapper
+        info = W.amdsmi_fw_info_t()
+        if W.amdsmi_get_fw_info(h, ctypes.byref(info)) != 0:
+            return None
+        out = {}
+        for i in range(min(int(info.num_fw_info), len(info.fw_info_list))):
+            e = info.fw_info_list[i]
+            name = A.AmdSmiFwBlock(e.fw_id).name.replace("AMDSMI_FW_ID_", "")
+            if name in _FW_NAMES and e.fw_version not in (0, 0xFFFFFFFFFFFFFFFF):
+                out[_FW_NAMES[name]] = int(e.fw_version)
+        return out or None
+    except Exception:
+        return None
+
+
+def _ecc_blocks_python(A: Any, h: Any) -> Optional[Dict[str, Dict[str, int]]]:
+    out = {}
+    for name in _RAS_BLOCKS:
+        try:
+            c = A.amdsmi_get_gpu_ecc_count(h, getattr(A.AmdSmiGpuBlock, name))
+        except Exception:
+            continue
+        row = {"ce": _int(c.get("correctable_count")) or 0, "ue": _int(c.get("uncorrectable_count")) or 0,
+               "de": _int(c.get("deferred_count")) or 0}
+        if any(row.values()):
+            out[name.lower()] = row
+    return out or None
+
+
 def probe_python(node: str) -> Dict[str, Any]:
     rep: Dict[str, Any] = {"schema": SCHEMA, "node": node, "ts": time.time(), "probe": "python", "gpus": []}
     t0 = time.perf_counter()
@@ -137,7 +177,14 @@ def probe_python(node: str) -> Dict[str, Any]:
         rep["error"] = f"amdsmi init: {e}"
         return rep
     try:
-        for i, h in enumerate(A.amdsmi_get_processor_handles()):
+        handles = A.amdsmi_get_processor_handles()
+        try:
+            drv = A.amdsmi_get_gpu_driver_info(handles[0]) if handles else {}
+            if drv.get("driver_version") not in (None, "", "N/A"):
+                rep["driver"] = {"name": drv.get("driver_name"), "version": drv.get("driver_version")}
+        except Exception:
+            pass
+        for i, h in enumerate(handles):
             g: Dict[str, Any] = {"index": i}
 
             def q(fn, *a):
@@ -157,6 +204,8 @@ def probe_python(node: str) -> Dict[str, Any]:
             g["product_name"] = board.get("product_name")
             vb = q(A.amdsmi_get_gpu_vbios_info) or {}
             g["vbios_name"] = vb.get("name")
+            g["vbios_version"] = vb.get("version") or None
+            g["fw"] = _firmware_python(A, h)
             vram = q(A.amdsmi_get_gpu_vram_info) or {}
             g["vram_type"], g["vram_mb"] = vram.get("vram_type"), vram.get("vram_size")
             ecc = q(A.amdsmi_get_gpu_total_ecc_count)
@@ -164,9 +213,13 @@ def probe_python(node: str) -> Dict[str, Any]:
                 g.update({"ecc_correctable": ecc.get("correctable_count"),
                           "ecc_uncorrectable": ecc.get("uncorrectable_count"),
                           "ecc_deferred": ecc.get("deferred_count")})
+                if any(_int(ecc.get(k)) for k in ("correctable_count", "uncorrectable_count", "deferred_count")):
+                    g["ecc_blocks"] = _ecc_blocks_python(A, h)
             bp = q(A.amdsmi_get_gpu_bad_page_info)
             g["bad_pages"] = len(bp) if isinstance(bp, list) else None
             g["xgmi"] = _xgmi_string(q(A.amdsmi_get_gpu_xgmi_link_status))
+            xe = q(A.amdsmi_gpu_xgmi_error_status)
+            g["xgmi_error"] = int(xe) if xe is not None else None
             kfd = q(A.amdsmi_get_gpu_kfd_info) or {}
             g["kfd"] = bool(kfd.get("kfd_id") not in (None, "N/A"))
             g["compute_partition"] = q(A.amdsmi_get_gpu_compute_partition)

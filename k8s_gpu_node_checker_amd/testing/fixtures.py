@@ -101,6 +101,12 @@ def realistic_node(name: str, gpu_key: Optional[str] = "amd.com/gpu", gpu_count:
     return node
 
 
+#: firmware image versions amd-smi reported on an MI355X box (csrc/probe fw_name(); round 2)
+MI355X_FW = {"mec": 44, "rlc": 43, "sdma": 14, "psp_sos": 4522031, "ta_ras": 457506826, "ta_xgmi": 536870932,
+             "pm": 72748906, "pldm_bundle": 18419975}
+MI355X_DRIVER = {"name": "amdgpu", "version": "6.18.54"}
+
+
 def mi355x_probe_report(node: str, gpus: int = 8, ts: Optional[float] = None, **overrides: Any) -> Dict[str, Any]:
     """A probe report as the node agent publishes it (values measured on a real MI355X)."""
     entries = []
@@ -115,11 +121,12 @@ def mi355x_probe_report(node: str, gpus: int = 8, ts: Optional[float] = None, **
              "pcie_replays": 0, "pcie_recoveries": 0, "power_w": 260, "power_cap_w": 1400,
              "power_cap_default_w": 1400, "hbm_temp_c": 34, "gfxclk_mhz": 157, "vram_used_mb": 283,
              "processes": 0, "throttle_acc": {"n": 499923464, "prochot": 0, "ppt": 1486216, "socket_thm": 0,
-                                              "vr_thm": 0, "hbm_thm": 0}}
+                                              "vr_thm": 0, "hbm_thm": 0},
+             "vbios_version": "00175784", "fw": dict(MI355X_FW)}
         g.update(overrides.get(f"gpu{i}", {}))
         entries.append(g)
     rep = {"schema": "mi355x-health/v1", "node": node, "ts": time.time() if ts is None else ts,
-           "probe": "fixture", "gpus": entries}
+           "probe": "fixture", "driver": dict(MI355X_DRIVER), "gpus": entries}
     for k, v in overrides.items():
         if not k.startswith("gpu"):
             rep[k] = v

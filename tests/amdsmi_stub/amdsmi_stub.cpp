@@ -10,6 +10,8 @@
 //   gpu.<i>.<field>=<value>          one recorded field of GPU i (names as in the probe's JSON)
 //   gpu.<i>.asic_status=<status>     make amdsmi_get_gpu_asic_info fail for GPU i
 //   gpu.<i>.nprocs=<n>               synthesise n processes (exercises the probe's 64-entry cap)
+//   gpu.<i>.fw.<name>=<version>      firmware versions; gpu.<i>.ecc_blocks.<block>.ce|ue|de per-block ECC
+//   driver_version=<v>               amdsmi_get_gpu_driver_info (absent: NOT_SUPPORTED)
 //
 // Output buffers are written exactly as the real library documents (length-checked), so a probe that
 // passes a short buffer or reads past what was written shows up under ASan.
@@ -42,6 +44,7 @@ struct World {
   bool loaded = false;
   int init_status = 0;
   int sockets_status = 0;
+  std::string driver_version;
   bool open = false;
   std::vector<Gpu> gpus;
 };
@@ -66,6 +69,8 @@ void load() {
       g_world.init_status = atoi(v.c_str());
     } else if (k == "sockets_status") {
       g_world.sockets_status = atoi(v.c_str());
+    } else if (k == "driver_version") {
+      g_world.driver_version = v;
     } else if (k == "gpus") {
       g_world.gpus.resize(static_cast<size_t>(atoi(v.c_str())));
     } else if (k.rfind("gpu.", 0) == 0) {
@@ -215,6 +220,70 @@ amdsmi_status_t amdsmi_get_gpu_vbios_info(amdsmi_processor_handle processor_hand
   FIELD_OR_NA("vbios_name");
   memset(info, 0, sizeof *info);
   put(info->name, sizeof info->name, g->s("vbios_name"));
+  put(info->version, sizeof info->version, g->s("vbios_version"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+// gpu.<i>.fw.<name>=<version>, names as the probe emits them
+amdsmi_status_t amdsmi_get_fw_info(amdsmi_processor_handle processor_handle, amdsmi_fw_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  static const struct {
+    amdsmi_fw_block_t id;
+    const char* key;
+  } ids[] = {{AMDSMI_FW_ID_SMU, "fw.smu"},       {AMDSMI_FW_ID_CP_ME, "fw.me"}, {AMDSMI_FW_ID_PM, "fw.pm"},
+             {AMDSMI_FW_ID_PSP_SOSDRV, "fw.psp_sos"}, {AMDSMI_FW_ID_CP_MEC1, "fw.mec"},
+             {AMDSMI_FW_ID_RLC, "fw.rlc"},       {AMDSMI_FW_ID_SDMA0, "fw.sdma"},
+             {AMDSMI_FW_ID_TA_RAS, "fw.ta_ras"}, {AMDSMI_FW_ID_TA_XGMI, "fw.ta_xgmi"},
+             {AMDSMI_FW_ID_PLDM_BUNDLE, "fw.pldm_bundle"}};
+  memset(info, 0, sizeof *info);
+  uint8_t n = 0;
+  for (const auto& e : ids) {
+    if (!g->has(e.key) && e.id != AMDSMI_FW_ID_CP_ME) continue;
+    info->fw_info_list[n].fw_id = e.id;
+    info->fw_info_list[n].fw_version = g->u(e.key, 0x1234);  // CP_ME: a block the probe does not report
+    ++n;
+  }
+  info->num_fw_info = n;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_gpu_xgmi_error_status(amdsmi_processor_handle processor_handle, amdsmi_xgmi_status_t* status) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("xgmi_error");
+  *status = static_cast<amdsmi_xgmi_status_t>(g->u("xgmi_error"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+// gpu.<i>.ecc_blocks.<block>.{ce,ue,de}; blocks without a line read as zero counts
+amdsmi_status_t amdsmi_get_gpu_ecc_count(amdsmi_processor_handle processor_handle, amdsmi_gpu_block_t block,
+                                         amdsmi_error_count_t* ec) {
+  GPU_OR_FAIL(processor_handle);
+  static const struct {
+    amdsmi_gpu_block_t b;
+    const char* name;
+  } names[] = {{AMDSMI_GPU_BLOCK_UMC, "umc"}, {AMDSMI_GPU_BLOCK_GFX, "gfx"}, {AMDSMI_GPU_BLOCK_SDMA, "sdma"},
+               {AMDSMI_GPU_BLOCK_MMHUB, "mmhub"}, {AMDSMI_GPU_BLOCK_XGMI_WAFL, "xgmi_wafl"},
+               {AMDSMI_GPU_BLOCK_PCIE_BIF, "pcie_bif"}};
+  if (!ec) return AMDSMI_STATUS_INVAL;
+  memset(ec, 0, sizeof *ec);
+  for (const auto& n : names) {
+    if (n.b != block) continue;
+    const std::string k = std::string("ecc_blocks.") + n.name + ".";
+    ec->correctable_count = g->u((k + "ce").c_str());
+    ec->uncorrectable_count = g->u((k + "ue").c_str());
+    ec->deferred_count = g->u((k + "de").c_str());
+    return AMDSMI_STATUS_SUCCESS;
+  }
+  return AMDSMI_STATUS_NOT_SUPPORTED;
+}
+
+amdsmi_status_t amdsmi_get_gpu_driver_info(amdsmi_processor_handle processor_handle, amdsmi_driver_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  (void)g;
+  if (g_world.driver_version.empty()) return AMDSMI_STATUS_NOT_SUPPORTED;
+  memset(info, 0, sizeof *info);
+  put(info->driver_name, sizeof info->driver_name, "amdgpu");
+  put(info->driver_version, sizeof info->driver_version, g_world.driver_version);
   return AMDSMI_STATUS_SUCCESS;
 }
 

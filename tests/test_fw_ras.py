@@ -1,0 +1,142 @@
+"""Firmware consistency, per-block ECC and the xGMI error status (probe fields beyond SURVEY §7.1).
+
+The reference sees none of this (``check-gpu-node.py:172-196`` reads Ready and capacity only); these
+are the fleet failure modes an MI355X node has besides a dead GPU: a half-applied firmware update,
+HBM errors attributed to the memory controller vs the xGMI PHYs, a link that retried traffic.
+"""
+import json
+
+from k8s_gpu_node_checker_amd.checker import CheckOptions, fleet_versions, run_check
+from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+from k8s_gpu_node_checker_amd.models import health as H
+from k8s_gpu_node_checker_amd.models.node import NodeExtras
+from k8s_gpu_node_checker_amd.testing import fixtures
+from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+
+
+def rep(**kw):
+    return fixtures.mi355x_probe_report("n", gpus=8, **kw)
+
+
+def test_fixture_with_firmware_is_healthy():
+    v = H.evaluate_report(rep(), 8)
+    assert v.state == H.HEALTHY and not v.warnings, v.to_dict()
+
+
+def test_uncorrectable_ecc_names_the_blocks():
+    blocks = {"umc": {"ce": 4, "ue": 3, "de": 0}, "xgmi_wafl": {"ce": 0, "ue": 1, "de": 0}}
+    v = H.evaluate_report(rep(gpu5={"ecc_uncorrectable": 4, "ecc_correctable": 4, "ecc_blocks": blocks}), 8)
+    assert v.state == H.UNHEALTHY
+    assert v.reasons == ["gpu5: 4 uncorrectable ECC errors (umc 3, xgmi_wafl 1)"]
+    # the same totals from an agent without the per-block read keep the plain message
+    v = H.evaluate_report(rep(gpu5={"ecc_uncorrectable": 4}), 8)
+    assert v.reasons == ["gpu5: 4 uncorrectable ECC errors"]
+
+
+def test_correctable_and_deferred_warnings_name_the_blocks():
+    blocks = {"xgmi_wafl": {"ce": 5000, "ue": 0, "de": 0}, "umc": {"ce": 1, "ue": 0, "de": 2}}
+    v = H.evaluate_report(rep(gpu1={"ecc_correctable": 5001, "ecc_deferred": 2, "ecc_blocks": blocks}), 8)
+    assert v.state == H.DEGRADED
+    assert "gpu1: 2 deferred ECC errors (umc 2)" in v.warnings
+    assert "gpu1: 5001 correctable ECC errors (xgmi_wafl 5000, umc 1)" in v.warnings
+
+
+def test_xgmi_error_status_degrades_unless_links_are_not_checked():
+    v = H.evaluate_report(rep(gpu2={"xgmi_error": 2}, gpu6={"xgmi_error": 1}), 8)
+    assert v.state == H.DEGRADED and v.ok
+    assert v.warnings == ["gpu2: xGMI error status multiple errors", "gpu6: xGMI error status errors"]
+    assert H.evaluate_report(rep(gpu2={"xgmi_error": 0}), 8).state == H.HEALTHY
+    # a single-GPU box / --xgmi-links 0: no hive, the status is not judged
+    one = fixtures.mi355x_probe_report("n", gpus=1, gpu0={"xgmi_error": 1, "xgmi": "XXXXXXXX"})
+    assert H.evaluate_report(one, 1, H.HealthExpectations(xgmi_links=0)).state == H.HEALTHY
+
+
+def test_firmware_versions_print_as_amd_smi_does():
+    # amd-smi firmware on the MI355X box (gpurun_out/fw_list.txt): the same images, formatted
+    got = {k: H.fw_version_str(k, v) for k, v in fixtures.MI355X_FW.items()}
+    assert got == {"mec": "44", "rlc": "43", "sdma": "14", "psp_sos": "00.45.00.2F", "ta_ras": "1B.45.00.0A",
+                   "ta_xgmi": "20.00.00.14", "pm": "04.86.15.106", "pldm_bundle": "01.25.17.07"}
+
+
+def test_firmware_mismatch_across_gpus():
+    fw7 = dict(fixtures.MI355X_FW, psp_sos=4521984)
+    v = H.evaluate_report(rep(gpu7={"fw": fw7}), 8)
+    assert v.state == H.DEGRADED and v.gpus_ok == 8
+    assert v.warnings == ["firmware differs across GPUs: psp_sos: gpu0-6 00.45.00.2F, gpu7 00.45.00.00"]
+    # two images differ, groups are ordered by size, non-contiguous GPUs are listed
+    fw = dict(fixtures.MI355X_FW, mec=45, rlc=40)
+    v = H.evaluate_report(rep(gpu1={"fw": fw}, gpu4={"fw": fw}), 8)
+    assert v.warnings == ["firmware differs across GPUs: mec: gpu0,2,3,5,6,7 44, gpu1,4 45; "
+                          "rlc: gpu0,2,3,5,6,7 43, gpu1,4 40"]
+    # the message is what the condition carries: stable between probes (no counters, no timestamps)
+    c1 = H.condition_for(v, now=1.0)["message"]
+    c2 = H.condition_for(H.evaluate_report(rep(gpu1={"fw": fw}, gpu4={"fw": fw}), 8), now=2.0)["message"]
+    assert c1 == c2 and c1.startswith("8/8 MI355X GPUs ok; firmware differs")
+    # a GPU whose firmware could not be read is not a mismatch
+    assert H.firmware_mismatch([{"index": 0, "fw": {"mec": 1}}, {"index": 1}]) == []
+
+
+def _extras(reports):
+    return [NodeExtras(True, {}, {}, False, json.dumps(r) if r is not None else None) for r in reports]
+
+
+def test_fleet_versions_counts_drivers_and_firmware():
+    a = rep()
+    b = rep(driver={"name": "amdgpu", "version": "6.18.60"})
+    c = rep(gpu3={"fw": dict(fixtures.MI355X_FW, mec=46)})
+    f = fleet_versions(_extras([a, b, c, None, {"schema": H.SCHEMA, "error": "AMDSMI_STATUS_NO_PERM"}]))
+    assert f["nodes_reporting"] == 3
+    assert f["driver"] == {"6.18.54": 2, "6.18.60": 1}
+    assert f["firmware"]["mec"] == {"44": 3, "46": 1}  # node c runs both
+    assert f["firmware"]["psp_sos"] == {"00.45.00.2F": 3} and f["firmware"]["pm"] == {"04.86.15.106": 3}
+    assert f["mixed"] == ["driver", "mec"]
+    assert fleet_versions(_extras([None])) is None
+
+
+def test_extended_json_carries_the_fleet_summary(mock_cluster, tmp_path):
+    nodes = [fixtures.realistic_node(f"n{i}", index=i, annotations=fixtures.health_annotation(
+        fixtures.mi355x_probe_report(f"n{i}", driver={"name": "amdgpu", "version": "6.18.54" if i else "6.18.50"})))
+        for i in range(3)]
+    srv = mock_cluster(nodes)
+    res = run_check(ClusterConnection(srv.url), CheckOptions(json_extended=True))
+    fleet = res.extended_fields()["mi355x"]["fleet"]
+    assert fleet["driver"] == {"6.18.50": 1, "6.18.54": 2} and fleet["mixed"] == ["driver"]
+    assert res.exit_code == 0  # a version drift is reported, it does not gate Ready
+
+
+def test_cli_extended_fleet(run_cli, mock_cluster, tmp_path):
+    nodes = [fixtures.realistic_node("a", annotations=fixtures.health_annotation(rep()))]
+    kc = write_kubeconfig(str(tmp_path / "kc"), mock_cluster(nodes).url)
+    p = run_cli(["--kubeconfig", kc, "--json-extended"])
+    assert p.returncode == 0, p.stderr
+    fleet = json.loads(p.stdout)["mi355x"]["fleet"]
+    assert fleet["nodes_reporting"] == 1 and fleet["mixed"] == [] and fleet["firmware"]["ta_xgmi"] == {"20.00.00.14": 1}
+
+
+def test_agent_metrics_expose_firmware_driver_and_ras_blocks():
+    from prometheus_client.parser import text_string_to_metric_families
+
+    from k8s_gpu_node_checker_amd.agent.agent import _metrics
+    r = fixtures.mi355x_probe_report("n", gpus=2, driver={"name": "amdgpu", "version": 'odd "v"\\1'},
+                                     gpu1={"xgmi_error": 2, "ecc_blocks": {"umc": {"ce": 7, "ue": 1, "de": 0}}})
+    fams = {f.name: f for f in text_string_to_metric_families(_metrics(r))}  # parses: the exposition is valid
+    drv = fams["mi355x_node_driver_info"].samples[0]
+    assert drv.labels["version"] == 'odd "v"\\1' and drv.value == 1
+    fw = {(s.labels["gpu"], s.labels["image"]): s.labels["version"] for s in fams["mi355x_gpu_firmware_info"].samples}
+    assert fw[("1", "psp_sos")] == "00.45.00.2F" and fw[("0", "pm")] == "04.86.15.106"
+    ecc = {(s.labels["block"], s.labels["kind"]): s.value for s in fams["mi355x_gpu_ecc_block_errors"].samples}
+    assert ecc == {("umc", "ce"): 7, ("umc", "ue"): 1, ("umc", "de"): 0}
+    assert [s.value for s in fams["mi355x_gpu_xgmi_error_status"].samples] == [2]
+
+
+def test_agent_metrics_group_each_family_once_on_a_multi_gpu_node():
+    from prometheus_client.parser import text_string_to_metric_families
+
+    from k8s_gpu_node_checker_amd.agent.agent import _metrics
+    r = fixtures.mi355x_probe_report("n", gpus=8)
+    r["gpus"][3]["diag"] = {"gemm": {"pass": True, "tflops": 1200.0}}
+    names = [f.name for f in text_string_to_metric_families(_metrics(r))]
+    assert len(names) == len(set(names)), sorted(n for n in names if names.count(n) > 1)
+    fams = {f.name: f for f in text_string_to_metric_families(_metrics(r))}
+    assert len(fams["mi355x_gpu_power_watts"].samples) == 8
+    assert fams["mi355x_gpu_pcie_replays"].type == "counter"

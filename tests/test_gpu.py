@@ -57,11 +57,15 @@ def test_native_probe_reports_healthy_mi355x(dev):
 def test_python_probe_agrees_with_native(dev):
     pytest.importorskip("amdsmi")
     from k8s_gpu_node_checker_amd.ops.amdsmi_probe import probe_native, probe_python
-    a = probe_native("n")["gpus"][0]
-    b = probe_python("n")["gpus"][0]
+    ra, rb = probe_native("n"), probe_python("n")
+    a, b = ra["gpus"][0], rb["gpus"][0]
     for k in ("gfx", "vram_type", "vram_mb", "ecc_uncorrectable", "xgmi", "compute_partition",
-              "memory_partition", "cus", "power_cap_w", "power_cap_default_w"):
+              "memory_partition", "cus", "power_cap_w", "power_cap_default_w", "fw", "vbios_version",
+              "xgmi_error", "ecc_blocks"):
         assert a.get(k) == b.get(k), (k, a.get(k), b.get(k))
+    assert ra.get("driver") == rb.get("driver") and ra["driver"]["name"] == "amdgpu", (ra.get("driver"), rb.get("driver"))
+    # the firmware a node runs: power management / security processor / compute-queue images
+    assert a["fw"] and {"mec", "psp_sos"} <= set(a["fw"]), a["fw"]
     assert set(a.get("throttle_acc") or {}) == set(b.get("throttle_acc") or {})
 
 

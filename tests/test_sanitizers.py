@@ -69,8 +69,20 @@ def _recorded_gpu():
 def scenario(path, gpus=8, init_status=0, per_gpu=None):
     """The stub's key=value scenario: the recorded MI355X replicated to ``gpus`` OAMs (distinct BDFs /
     UUIDs / KFD nodes), with ``per_gpu[i]`` overriding fields of GPU i."""
-    g0 = _recorded_gpu()
+    import json
+    with open(RECORDED) as f:
+        rec = json.load(f)
+    g0 = rec["gpus"][0]
     lines = [f"init_status={init_status}", f"gpus={gpus}"]
+    if (rec.get("driver") or {}).get("version"):
+        lines.append(f"driver_version={rec['driver']['version']}")
+
+    def flat(prefix, v):  # nested objects (fw, ecc_blocks, throttle_acc) become dotted keys
+        if isinstance(v, dict):
+            for a, b in v.items():
+                flat(f"{prefix}.{a}", b)
+        else:
+            lines.append(f"{prefix}={v}")
     for i in range(gpus):
         g = dict(g0)
         g["bdf"] = f"0000:{0x05 + 0x10 * i:02x}:00.0"
@@ -82,10 +94,7 @@ def scenario(path, gpus=8, init_status=0, per_gpu=None):
                 continue
             if k == "procs":
                 v = ",".join(f"{p['pid']}:{p['vram_mb']}" for p in v)
-            if k == "throttle_acc":
-                lines += [f"gpu.{i}.throttle_acc.{a}={b}" for a, b in v.items()]
-                continue
-            lines.append(f"gpu.{i}.{k}={v}")
+            flat(f"gpu.{i}.{k}", v)
     path.write_text("\n".join(lines) + "\n")
     return str(path)
 
@@ -212,3 +221,33 @@ def test_probe_concurrent_calls_under_tsan(tmp_path):
                        timeout=300)
     assert p.returncode == 0 and "WARNING: ThreadSanitizer" not in p.stderr, p.stderr[-4000:]
     assert '"bad_documents":0' in p.stdout and '"threads":8' in p.stdout
+
+
+@pytest.mark.slow
+def test_probe_cli_under_asan_firmware_ras_blocks_xgmi_error(asan_probe, tmp_path):
+    """The probe's per-block ECC read (only when the totals are non-zero), the firmware table (read once
+    per open, reused across probes) and the xGMI error status, under ASan/UBSan; the verdict names the
+    failing block and the half-updated GPU."""
+    import json
+
+    from k8s_gpu_node_checker_amd.models import health as H
+    d, _, _ = asan_probe
+    rec = _recorded_gpu()
+    fw5 = dict(rec["fw"], psp_sos=rec["fw"]["psp_sos"] - 47)
+    scen = scenario(tmp_path / "s.txt", per_gpu={5: {"ecc_uncorrectable": 3, "ecc_correctable": 2, "fw": fw5,
+                                                     "ecc_blocks": {"umc": {"ce": 2, "ue": 3, "de": 0}},
+                                                     "xgmi_error": 1}})
+    p = _run_cli(d, scen, "--repeat", "2")
+    assert p.returncode == 0 and "ERROR: AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr, \
+        p.stderr[-3000:]
+    r = json.loads(p.stdout.splitlines()[-1])
+    assert r["driver"]["name"] == "amdgpu" and r["driver"]["version"]
+    g5, g0 = r["gpus"][5], r["gpus"][0]
+    assert g5["ecc_blocks"] == {"umc": {"ce": 2, "ue": 3, "de": 0}} and "ecc_blocks" not in g0
+    assert g5["xgmi_error"] == 1 and g5["fw"] == fw5 and g0["fw"] == rec["fw"]
+    assert "xgmi_error" not in g0 or g0["xgmi_error"] == 0
+    v = H.evaluate_report(r, 8, H.HealthExpectations(xgmi_links=7), now=r["ts"])
+    assert v.state == H.UNHEALTHY and v.reasons == ["gpu5: 3 uncorrectable ECC errors (umc 3)"]
+    assert "gpu5: xGMI error status errors" in v.warnings
+    assert any(w.startswith("firmware differs across GPUs: psp_sos: gpu0-4,6,7") or
+               w.startswith("firmware differs across GPUs: psp_sos: gpu0,1,2,3,4,6,7") for w in v.warnings), v.warnings
