@@ -776,10 +776,20 @@ __device__ __forceinline__ floatx4 burn_mfma(const i32x8& a, const i32x8& b, flo
   }
 }
 
+// Physical location of the calling wave: XCD (XCC_ID), shader engine, shader array and CU (HW_ID), packed
+// as xcd<<7 | se<<5 | sh<<4 | cu -- one of BURN_SLOTS slots; the CUs of one MI355X occupy 256 of them.
+constexpr int BURN_SLOTS = 1024;
+__device__ __forceinline__ unsigned wave_slot() {
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_ID, all 32 bits
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // XCC_ID[3:0]
+  return ((xcc & 7u) << 7) | (((hw >> 13) & 3u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u);
+}
+
 template <int KIND>
 __global__ void __launch_bounds__(256) mfma_burn_kernel(const i32x8* __restrict__ fa, const i32x8* __restrict__ fb,
                                                         const float* __restrict__ expect, int iters,
-                                                        unsigned long long* errors) {
+                                                        unsigned long long* errors, unsigned long long* cu_map) {
+  const long long t0 = wall_clock64();  // constant-rate clock (hipDeviceAttributeWallClockRate)
   const int lane = threadIdx.x & 63;
   const i32x8 a = fa[lane], b = fb[lane];
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
@@ -793,7 +803,20 @@ __global__ void __launch_bounds__(256) mfma_burn_kernel(const i32x8* __restrict_
     }
   }
   const floatx4 s = acc0 + acc1 + acc2 + acc3;
-  if (s[0] + s[1] + s[2] + s[3] != expect[lane]) atomicAdd(errors, 1ULL);
+  const bool bad = s[0] + s[1] + s[2] + s[3] != expect[lane];
+  if (bad) atomicAdd(errors, 1ULL);
+  if (cu_map != nullptr) {
+    // per physical CU: waves run, wrong lanes, summed wave time -- a miscomputing CU is named, and an
+    // XCD whose waves take longer than the others' (its own clock domain) stands out
+    const unsigned long long nbad = __popcll(__ballot(bad));
+    const unsigned long long dt = static_cast<unsigned long long>(wall_clock64() - t0);
+    if (lane == 0) {
+      unsigned long long* row = cu_map + 3 * wave_slot();
+      atomicAdd(row, 1ULL);
+      if (nbad) atomicAdd(row + 1, nbad);
+      atomicAdd(row + 2, dt);
+    }
+  }
 }
 
 // Device allocation owned by its device (frees with that device current), for the multi-GPU test.
@@ -1245,7 +1268,19 @@ int diag_p2p_copy(int src, int dst, size_t bytes, int iters, double* gbps, unsig
 
 // Matrix-core burn-in of one precision (`kind` as mfma_burn_kernel): `reps` launches of `iters`
 // iterations on every CU; *tflops = dense rate, *errors = wave-lanes whose exact result differed.
+int diag_mfma_burn_map(int device, int kind, int iters, int reps, double* tflops, unsigned long long* errors,
+                       unsigned long long* cu_map);
+
 int diag_mfma_burn(int device, int kind, int iters, int reps, double* tflops, unsigned long long* errors) {
+  return diag_mfma_burn_map(device, kind, iters, reps, tflops, errors, nullptr);
+}
+
+int diag_mfma_burn_slots(void) { return BURN_SLOTS; }
+
+// As diag_mfma_burn, plus (cu_map != NULL) a BURN_SLOTS x 3 table of (waves, wrong lanes, wave time in
+// wall-clock ticks) per physical CU slot (wave_slot()), over every launch including the warm-up.
+int diag_mfma_burn_map(int device, int kind, int iters, int reps, double* tflops, unsigned long long* errors,
+                       unsigned long long* cu_map) {
   if (kind < 0 || kind > 3 || iters < 1 || iters > 65536 || reps < 1) {
     g_err = "mfma_burn: kind 0..3, 1 <= iters <= 65536, reps >= 1";
     return -2;
@@ -1303,7 +1338,12 @@ int diag_mfma_burn(int device, int kind, int iters, int reps, double* tflops, un
     }
     expect[l] = static_cast<float>(tot * 4L * iters);  // exact: bounded below 2^24 by the check above
   }
-  DevBuf dfa, dfb, dex, dcnt;
+  DevBuf dfa, dfb, dex, dcnt, dmap;
+  const size_t map_bytes = static_cast<size_t>(BURN_SLOTS) * 3 * sizeof(unsigned long long);
+  if (cu_map != nullptr) {
+    DIAG_CHECK(dmap.alloc(device, map_bytes));
+    DIAG_CHECK(hipMemset(dmap.ptr, 0, map_bytes));
+  }
   DIAG_CHECK(dfa.alloc(device, fa.size()));
   DIAG_CHECK(dfb.alloc(device, fb.size()));
   DIAG_CHECK(dex.alloc(device, expect.size() * sizeof(float)));
@@ -1318,11 +1358,12 @@ int diag_mfma_burn(int device, int kind, int iters, int reps, double* tflops, un
     const i32x8* b = static_cast<const i32x8*>(dfb.ptr);
     const float* ex = static_cast<const float*>(dex.ptr);
     unsigned long long* c = static_cast<unsigned long long*>(dcnt.ptr);
+    unsigned long long* m = static_cast<unsigned long long*>(dmap.ptr);  // null without a map
     switch (kind) {
-      case 0: hipLaunchKernelGGL(mfma_burn_kernel<0>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c); break;
-      case 1: hipLaunchKernelGGL(mfma_burn_kernel<1>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c); break;
-      case 2: hipLaunchKernelGGL(mfma_burn_kernel<2>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c); break;
-      default: hipLaunchKernelGGL(mfma_burn_kernel<3>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c);
+      case 0: hipLaunchKernelGGL(mfma_burn_kernel<0>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c, m); break;
+      case 1: hipLaunchKernelGGL(mfma_burn_kernel<1>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c, m); break;
+      case 2: hipLaunchKernelGGL(mfma_burn_kernel<2>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c, m); break;
+      default: hipLaunchKernelGGL(mfma_burn_kernel<3>, dim3(blocks), dim3(256), 0, nullptr, a, b, ex, iters, c, m);
     }
   };
   launch();  // warm-up (also checked)
@@ -1340,6 +1381,7 @@ int diag_mfma_burn(int device, int kind, int iters, int reps, double* tflops, un
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   DIAG_CHECK(hipMemcpy(errors, dcnt.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (cu_map != nullptr) DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   const double flop = static_cast<double>(blocks) * 4 /*waves*/ * iters * 16 /*MFMA per iter*/ * 2.0 * 16 * 16 * K;
   *tflops = ms > 0.f ? flop * reps / (ms * 1e-3) / 1e12 : 0.0;
   return 0;

@@ -28,6 +28,8 @@ class FakeDiagLib:
     mfma_errors: ``{(device, kind index): wrong results}``
     p2p_gbps:    rate of every GPU pair; ``slow_pairs[(src, dst)]`` / ``nopeer`` override pairs
     delay_s:     wall time of each GEMM call (the agent's per-GPU threads overlap them)
+    slow_xcd:    ``{xcd: factor}`` on the burn-in's per-XCD wave time; ``bad_cu[(device, kind)]`` = the CU
+                 slot its ``mfma_errors`` come from
     """
 
     def __init__(self, n: int = 1, rate: float = 1.0, gpu_rate: Optional[Dict[int, float]] = None,
@@ -35,7 +37,8 @@ class FakeDiagLib:
                  mfma: Optional[Dict[int, Tuple[float, int]]] = None,
                  mfma_errors: Optional[Dict[Tuple[int, int], int]] = None, link: Optional[Tuple[float, float]] = None,
                  p2p_gbps: float = 48.0, slow_pairs: Optional[Dict[Tuple[int, int], float]] = None,
-                 nopeer: Tuple[Tuple[int, int], ...] = (), rc: int = 0, err: bytes = b"boom", delay_s: float = 0.0):
+                 nopeer: Tuple[Tuple[int, int], ...] = (), rc: int = 0, err: bytes = b"boom", delay_s: float = 0.0,
+                 slow_xcd: Optional[Dict[int, float]] = None, bad_cu: Optional[Dict[Tuple[int, int], int]] = None):
         from ..ops import diag
         self.ref = diag.REFERENCE_RATES
         self.kinds = diag.MFMA_KINDS
@@ -55,6 +58,8 @@ class FakeDiagLib:
         self.rc = rc
         self.err = err
         self.delay_s = delay_s
+        self.slow_xcd = dict(slow_xcd or {})
+        self.bad_cu = dict(bad_cu or {})
         self.calls: List[str] = []
         self.threads: Dict[int, set] = {}
         self.lock = threading.Lock()
@@ -126,6 +131,28 @@ class FakeDiagLib:
             tf, e = self.gpu_rate.get(device, self.rate) * self.ref["mfma"][self.kinds[kind]], 0
         _put(tflops, ctypes.c_double, tf)
         _put(errors, ctypes.c_ulonglong, self.mfma_errors.get((device, kind), e))
+        return 0
+
+    def diag_mfma_burn_slots(self):
+        return 1024
+
+    def diag_mfma_burn_map(self, device, kind, iters, reps, tflops, errors, cu_map):
+        """diag_mfma_burn plus the per-CU table: 8 XCDs x 32 CUs (4 SEs x 8), 8 waves per CU and
+        launch; ``slow_xcd`` {xcd: time factor} and ``bad_cu`` {(device, kind): slot} shape it."""
+        rc = self.diag_mfma_burn(device, kind, iters, reps, tflops, errors)
+        if rc or not cu_map:
+            return rc
+        nerr = self.mfma_errors.get((device, kind), 0)
+        bad_slot = self.bad_cu.get((device, kind))
+        for xcd in range(8 if self.cus >= 256 else max(1, self.cus // 32)):
+            for se in range(4):
+                for cu in range(8):
+                    slot = (xcd << 7) | (se << 5) | cu
+                    waves = 8 * (reps + 1)
+                    cu_map[3 * slot] = waves
+                    cu_map[3 * slot + 2] = int(waves * 40000 * self.slow_xcd.get(xcd, 1.0))
+        if bad_slot is not None and nerr:
+            cu_map[3 * bad_slot + 1] = nerr
         return 0
 
     def diag_host_link(self, device, nbytes, iters, h2d, d2h):

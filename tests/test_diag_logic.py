@@ -134,3 +134,50 @@ def test_scale_from_partition_modes():
     assert diag.Scale.of(None, None, None).to_dict() == {"compute": 1.0, "memory": 1.0}
     assert diag.judge_rate(84.9, 100) == "fail" and diag.judge_rate(85, 100) == "degraded"
     assert diag.judge_rate(95, 100) == "pass"
+
+
+def test_mfma_burn_maps_waves_to_cus_and_xcds(fake):
+    fake()
+    r = diag.mfma_burn(0)
+    m = r["map"]
+    assert m["cus"] == 256 and len(m["xcds"]) == 8 and all(x == {"cus": 32, "rel_time": 1.0} for x in m["xcds"].values())
+    assert "bad_cus" not in m and r["pass"] and not r["degraded"]
+
+
+def test_mfma_wrong_results_are_located_to_their_cu(fake):
+    slot = (3 << 7) | (1 << 5) | 5
+    fake(mfma_errors={(0, 0): 12, (0, 2): 2}, bad_cu={(0, 0): slot, (0, 2): slot})
+    r = diag.mfma_burn(0)
+    assert not r["pass"]
+    assert r["map"]["bad_cus"] == ["xcd3/se1/cu5 (bf16 12, mxfp8 2)"]
+    assert r["detail"] == "bf16: 12 wrong results; mxfp8: 2 wrong results; on xcd3/se1/cu5 (bf16 12, mxfp8 2)"
+    assert diag.slot_name((7 << 7) | (3 << 5) | (1 << 4) | 15) == "xcd7/se3/cu15/sh1"
+
+
+def test_a_lagging_xcd_degrades_the_burn_in(fake):
+    fake(slow_xcd={6: 1.3})
+    r = diag.mfma_burn(0)
+    assert r["pass"] and r["degraded"]
+    assert r["map"]["slowest_xcd"] == 6 and r["map"]["slowest_rel"] == 1.3
+    assert r["detail"] == "xcd6 waves take 1.30x the median XCD's time"
+    assert _verdict({"mfma": r}).state == "degraded"
+    fake(slow_xcd={6: 1.1})  # inside the spread of a healthy chip
+    r = diag.mfma_burn(0)
+    assert r["pass"] and not r["degraded"] and r["map"]["slowest_rel"] == 1.1
+
+
+def test_cpx_partition_has_one_xcd_and_no_xcd_verdict(fake):
+    fake(cus=32, mfma={k: (diag.REFERENCE_RATES["mfma"][n] / 8, 0) for k, n in enumerate(diag.MFMA_KINDS)})
+    r = diag.mfma_burn(0, scale=diag.Scale(0.125, 0.125))
+    assert r["pass"] and not r["degraded"] and r["map"]["cus"] == 32 and "slowest_xcd" not in r["map"]
+
+
+def test_a_lagging_xcd_is_measured_twice(fake):
+    lib = fake(slow_xcd={2: 1.4})
+    out = diag.run(1, 0)
+    assert lib.calls.count("mfma") == 8  # 4 kinds, twice
+    assert out["mfma"]["retried"] and out["mfma"]["degraded"]
+    lib.slow_xcd = {}
+    lib.calls.clear()
+    out = diag.run(1, 0)
+    assert lib.calls.count("mfma") == 4 and not out["mfma"].get("retried")

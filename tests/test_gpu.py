@@ -384,6 +384,13 @@ def test_mfma_burn_every_precision(dev):
     k = r["kinds"]
     assert all(v["errors"] == 0 for v in k.values())
     assert k["mxfp8"]["tflops"] > 1.5 * k["bf16"]["tflops"] and k["mxfp4"]["tflops"] > 1.5 * k["mxfp8"]["tflops"]
+    # where the waves ran: every CU of the SPX device, 32 in each of the 8 XCDs, none lagging
+    m = r["map"]
+    info = diag.device_info(0)
+    assert m["cus"] == info["cus"] and "bad_cus" not in m, m
+    if info["cus"] == 256:
+        assert sorted(m["xcds"]) == [str(x) for x in range(8)] and all(x["cus"] == 32 for x in m["xcds"].values()), m
+    assert m.get("slowest_rel", 1.0) <= diag.XCD_SLOW_RATIO, m
 
 
 def test_mfma_burn_rejects_inexact_iteration_counts():
