@@ -46,7 +46,7 @@ from ..models.resources import PRIMARY_GPU_KEY, gpu_breakdown
 # whether the annotation must be rewritten.
 _VOLATILE = frozenset(("ts", "probe_ms", "probe_us", "hotspot_c", "wall_s", "ms_per_gemm", "setup_ms",
                        "power_w", "hbm_temp_c", "gfxclk_mhz", "vram_used_mb", "processes", "throttle_acc",
-                       "throttle", "procs", "gfx_activity", "diag_skipped"))
+                       "throttle", "procs", "gfx_activity", "diag_skipped", "xgmi_kb"))
 
 DIAG_WHEN = ("idle", "always")
 
@@ -431,7 +431,7 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
     if not rep:
         return "# no probe yet\n"
     fams: Dict[str, List[str]] = {}
-    counters = {"mi355x_gpu_pcie_replays"}
+    counters = {"mi355x_gpu_pcie_replays", "mi355x_gpu_xgmi_kilobytes"}
 
     def put(name: str, labels: str, value: Any) -> None:
         fams.setdefault(name, []).append(f"{name}{{{labels}}} {value}" if labels else f"{name} {value}")
@@ -462,6 +462,12 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
             for kind in ("ce", "ue", "de"):
                 if isinstance(c, dict) and isinstance(c.get(kind), int):
                     put("mi355x_gpu_ecc_block_errors", f'{lbl},block="{_esc(block)}",kind="{kind}"', c[kind])
+        peers, kb = g.get("xgmi_peers"), g.get("xgmi_kb")
+        if isinstance(peers, list) and isinstance(kb, list):
+            for peer, rw in zip(peers, kb):
+                if isinstance(rw, list) and len(rw) == 2:
+                    for d, v in zip(("read", "write"), rw):
+                        put("mi355x_gpu_xgmi_kilobytes", f'{lbl},peer="{_esc(peer)}",dir="{d}"', v)
         for image, ver in ((g.get("fw") or {}) if isinstance(g.get("fw"), dict) else {}).items():
             put("mi355x_gpu_firmware_info", f'{lbl},image="{_esc(image)}",version="{_esc(fw_version_str(image, ver))}"', 1)
         if g.get("diag") is not None or g.get("diag_skipped"):

@@ -271,6 +271,10 @@ void probe_telemetry(std::string& o, amdsmi_processor_handle h) {
     }
   }
   if (clk_n) kv_u64(o, "gfxclk_mhz", clk_sum / clk_n);
+  // the trained xGMI link: lanes and per-lane rate (MI355X: x16 at 38 Gb/s); a link that retrained
+  // lower still reports Up
+  if (m.xgmi_link_width != UINT16_MAX && m.xgmi_link_width > 0) kv_u64(o, "xgmi_width", m.xgmi_link_width);
+  if (m.xgmi_link_speed != UINT16_MAX && m.xgmi_link_speed > 0) kv_u64(o, "xgmi_speed_gbps", m.xgmi_link_speed);
   if (m.accumulation_counter != UINT64_MAX && m.accumulation_counter != 0) {
     key(o, "throttle_acc");
     o.push_back('{');
@@ -376,6 +380,43 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
     kv_str(o, "xgmi", links.c_str());
   } else {
     kv_null(o, "xgmi");
+  }
+  // the fabric this GPU is wired into: its hive (every GPU of an 8-GPU board shares one) and, per xGMI
+  // link, the PCI address of the GPU at the other end and the traffic it has carried (KB since load)
+  amdsmi_xgmi_info_t xi;
+  memset(&xi, 0, sizeof xi);
+  if (amdsmi_get_xgmi_info(h, &xi) == AMDSMI_STATUS_SUCCESS && xi.xgmi_hive_id != 0 && xi.xgmi_hive_id != UINT64_MAX) {
+    char buf[24];
+    snprintf(buf, sizeof buf, "%016" PRIx64, xi.xgmi_hive_id);
+    kv_str(o, "xgmi_hive", buf);
+  }
+  amdsmi_link_metrics_t lm;
+  memset(&lm, 0, sizeof lm);
+  if (amdsmi_get_link_metrics(h, &lm) == AMDSMI_STATUS_SUCCESS) {
+    std::string peers = "[", kb = "[";
+    // num_links counts the connected links, but the table also holds the disabled port (all-ones BDF)
+    // ahead of them (MI355X: num_links 7, entries 0..7), so every entry is scanned; the memset leaves
+    // the unused ones as type INTERNAL
+    for (uint32_t i = 0; i < AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK; ++i) {
+      const auto& l = lm.links[i];
+      if (l.link_type != AMDSMI_LINK_TYPE_XGMI || l.bdf.as_uint == UINT64_MAX) continue;  // a disabled port
+      char buf[32];
+      snprintf(buf, sizeof buf, "%04" PRIx64 ":%02x:%02x.%x", static_cast<uint64_t>(l.bdf.domain_number),
+               static_cast<unsigned>(l.bdf.bus_number), static_cast<unsigned>(l.bdf.device_number),
+               static_cast<unsigned>(l.bdf.function_number));
+      if (peers.size() > 1) {
+        peers.push_back(',');
+        kb.push_back(',');
+      }
+      jstr(peers, buf);
+      kb += "[" + std::to_string(l.read) + "," + std::to_string(l.write) + "]";
+    }
+    peers.push_back(']');
+    kb.push_back(']');
+    key(o, "xgmi_peers");
+    o += peers;
+    key(o, "xgmi_kb");
+    o += kb;
   }
   // sticky until reset: the xGMI PHYs saw errors (one, or several) since the driver loaded
   amdsmi_xgmi_status_t xe = AMDSMI_XGMI_STATUS_NO_ERRORS;

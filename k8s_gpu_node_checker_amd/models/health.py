@@ -36,6 +36,8 @@ HBM3E_VRAM_TYPE = 5                           # amdsmi.h AMDSMI_VRAM_TYPE_HBM3E
 VRAM_MB_FULL = 294896                         # measured vram_size, SPX/NPS1 (288 GB class)
 VRAM_MIN_FRACTION = 0.97
 XGMI_LINKS_EXPECTED = 7                       # 8-GPU hive: 7 peers per GPU
+XGMI_LINK_WIDTH = 16                          # measured: lanes per trained xGMI link
+XGMI_LINK_GBPS = 38                           # measured: Gb/s per lane (x16 -> 608 Gb/s, 76 GB/s each way)
 NUM_CUS = 256
 HOTSPOT_WARN_C = 100
 HBM_TEMP_WARN_C = 95                          # HBM3E stacks throttle in the 95-105 C band
@@ -208,6 +210,51 @@ def firmware_mismatch(gpus: Sequence[Any]) -> List[str]:
     return out
 
 
+def _bdf(b: Any) -> str:
+    b = str(b or "").strip().lower()
+    return "0000:" + b if b.count(":") == 1 else b
+
+
+def xgmi_topology(gpus: Sequence[Any], links_expected: int) -> List[str]:
+    """Node-level xGMI wiring from the probe's ``xgmi_hive`` and ``xgmi_peers`` (amd-smi link metrics).
+
+    * Every GPU of an 8-GPU board belongs to one hive; GPUs reporting two hive ids cannot run a
+      collective over xGMI together (a board that came up split).
+    * With the whole board visible (``links_expected + 1`` unpartitioned GPUs), each GPU's Up links
+      must reach every other GPU of the node once: a link wired or trained to the wrong peer, or two
+      links to the same one, leaves some pair without its direct link -- traffic between them detours
+      through a third GPU at half the bandwidth, while every link still reads "Up".
+    """
+    if links_expected <= 0:
+        return []
+    gs = [g for g in gpus if isinstance(g, dict) and not g.get("error")]
+    out: List[str] = []
+    hives: Dict[str, List[Any]] = {}
+    for g in gs:
+        if isinstance(g.get("xgmi_hive"), str) and g["xgmi_hive"]:
+            hives.setdefault(g["xgmi_hive"], []).append(g.get("index", "?"))
+    if len(hives) > 1:
+        groups = sorted(hives.items(), key=lambda kv: (-len(kv[1]), kv[0]))
+        out.append(f"GPUs span {len(hives)} xGMI hives: " + ", ".join(f"gpu{_span(ix)} {h}" for h, ix in groups))
+    bdfs = {_bdf(g.get("bdf")): g for g in gs if g.get("bdf")}
+    full_board = len(bdfs) == links_expected + 1 and all(
+        str(g.get("compute_partition") or "SPX").upper() == "SPX" for g in gs)
+    if not full_board:
+        return out
+    for me, g in bdfs.items():
+        peers = g.get("xgmi_peers")
+        if not isinstance(peers, list):
+            continue
+        reached = {_bdf(p) for p in peers} & (set(bdfs) - {me})
+        foreign = sorted({_bdf(p) for p in peers} - set(bdfs))
+        if len(reached) < links_expected:
+            missing = sorted(set(bdfs) - reached - {me})
+            out.append(f"gpu{g.get('index', '?')}: xGMI links reach {len(reached)} of the node's {len(bdfs) - 1} "
+                       f"other GPUs (no link to {', '.join(missing[:3])}{' ...' if len(missing) > 3 else ''})"
+                       + (f", {len(foreign)} to devices outside the node" if foreign else ""))
+    return out
+
+
 def _span(ix: List[Any]) -> str:
     if len(ix) > 1 and all(isinstance(i, int) for i in ix) and ix == list(range(ix[0], ix[0] + len(ix))):
         return f"{ix[0]}-{ix[-1]}"
@@ -258,6 +305,12 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str],
             fail.append(f"gpu{idx}: {down} xGMI link(s) down ({links})")
         elif up < exp.xgmi_links:
             fail.append(f"gpu{idx}: {up}/{exp.xgmi_links} xGMI links up ({links})")
+    if isinstance(links, str) and "U" in links and exp.xgmi_links > 0:
+        w, sp = g.get("xgmi_width"), g.get("xgmi_speed_gbps")
+        if (isinstance(w, int) and 0 < w < XGMI_LINK_WIDTH) or (isinstance(sp, int) and 0 < sp < XGMI_LINK_GBPS):
+            # still "Up", but retrained narrower or slower: every collective through it runs at that rate
+            warn.append(f"gpu{idx}: xGMI links trained at x{w} {sp} Gb/s (MI355X: x{XGMI_LINK_WIDTH} "
+                        f"{XGMI_LINK_GBPS} Gb/s)")
     xe = g.get("xgmi_error")
     if isinstance(xe, int) and xe > 0 and exp.xgmi_links > 0:
         # sticky since the driver loaded: the link PHYs retried or dropped traffic at least once
@@ -329,6 +382,7 @@ def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
         ok += 0 if f else 1
     if expected_gpus and len(gpus) < expected_gpus:
         fails.append(f"{len(gpus)} of {expected_gpus} GPUs visible to amd-smi")
+    fails += xgmi_topology(gpus, exp.xgmi_links)
     mism = firmware_mismatch(gpus)
     if mism:
         warns.append("firmware differs across GPUs: " + "; ".join(mism))

@@ -114,6 +114,8 @@ def _telemetry_python(A: Any, h: Any, q: Any) -> Dict[str, Any]:
     clks = m.get("current_gfxclks")
     clks = [x for x in (_int(v) for v in clks) if x] if isinstance(clks, list) else []
     t["gfxclk_mhz"] = sum(clks) // len(clks) if clks else None
+    t["xgmi_width"] = _int(m.get("xgmi_link_width")) or None
+    t["xgmi_speed_gbps"] = _int(m.get("xgmi_link_speed")) or None
     n = _int(m.get("accumulation_counter"))
     if n:
         acc = {"n": n}
@@ -165,6 +167,27 @@ def _ecc_blocks_python(A: Any, h: Any) -> Optional[Dict[str, Dict[str, int]]]:
         if any(row.values()):
             out[name.lower()] = row
     return out or None
+
+
+def _xgmi_fabric_python(A: Any, h: Any, q: Any) -> Dict[str, Any]:
+    """The native probe's xGMI fabric fields: hive id, peer BDF and traffic of every XGMI link."""
+    out: Dict[str, Any] = {}
+    xi = q(A.amdsmi_get_xgmi_info) or {}
+    hive = _int(xi.get("xgmi_hive_id"))
+    if hive:
+        out["xgmi_hive"] = f"{hive:016x}"
+    lm = q(A.amdsmi_get_link_metrics)
+    if isinstance(lm, dict) and isinstance(lm.get("links"), list):
+        peers, kb = [], []
+        xgmi_type = int(getattr(getattr(A, "AmdSmiLinkType", None), "XGMI", 2))
+        for link in lm["links"]:
+            bdf = str(link.get("bdf") or "").lower()
+            if int(link.get("link_type", -1)) != xgmi_type or not bdf or bdf.startswith("ffff"):
+                continue
+            peers.append(bdf)
+            kb.append([_int(link.get("read")) or 0, _int(link.get("write")) or 0])
+        out["xgmi_peers"], out["xgmi_kb"] = peers, kb
+    return out
 
 
 def probe_python(node: str) -> Dict[str, Any]:
@@ -220,6 +243,7 @@ def probe_python(node: str) -> Dict[str, Any]:
             g["xgmi"] = _xgmi_string(q(A.amdsmi_get_gpu_xgmi_link_status))
             xe = q(A.amdsmi_gpu_xgmi_error_status)
             g["xgmi_error"] = int(xe) if xe is not None else None
+            g.update(_xgmi_fabric_python(A, h, q))
             kfd = q(A.amdsmi_get_gpu_kfd_info) or {}
             g["kfd"] = bool(kfd.get("kfd_id") not in (None, "N/A"))
             g["compute_partition"] = q(A.amdsmi_get_gpu_compute_partition)

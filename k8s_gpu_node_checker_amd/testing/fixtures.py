@@ -105,6 +105,7 @@ def realistic_node(name: str, gpu_key: Optional[str] = "amd.com/gpu", gpu_count:
 MI355X_FW = {"mec": 44, "rlc": 43, "sdma": 14, "psp_sos": 4522031, "ta_ras": 457506826, "ta_xgmi": 536870932,
              "pm": 72748906, "pldm_bundle": 18419975}
 MI355X_DRIVER = {"name": "amdgpu", "version": "6.18.54"}
+MI355X_HIVE = "bbf0a3c1d2e4f5fe"
 
 
 def mi355x_probe_report(node: str, gpus: int = 8, ts: Optional[float] = None, **overrides: Any) -> Dict[str, Any]:
@@ -122,7 +123,9 @@ def mi355x_probe_report(node: str, gpus: int = 8, ts: Optional[float] = None, **
              "power_cap_default_w": 1400, "hbm_temp_c": 34, "gfxclk_mhz": 157, "vram_used_mb": 283,
              "processes": 0, "throttle_acc": {"n": 499923464, "prochot": 0, "ppt": 1486216, "socket_thm": 0,
                                               "vr_thm": 0, "hbm_thm": 0},
-             "vbios_version": "00175784", "fw": dict(MI355X_FW)}
+             "vbios_version": "00175784", "fw": dict(MI355X_FW), "xgmi_hive": MI355X_HIVE,
+             "xgmi_width": 16, "xgmi_speed_gbps": 38,
+             "xgmi_peers": [f"0000:{0x05 + 0x10 * j:02x}:00.0" for j in range(gpus) if j != i]}
         g.update(overrides.get(f"gpu{i}", {}))
         entries.append(g)
     rep = {"schema": "mi355x-health/v1", "node": node, "ts": time.time() if ts is None else ts,

@@ -12,6 +12,7 @@
 //   gpu.<i>.nprocs=<n>               synthesise n processes (exercises the probe's 64-entry cap)
 //   gpu.<i>.fw.<name>=<version>      firmware versions; gpu.<i>.ecc_blocks.<block>.ce|ue|de per-block ECC
 //   driver_version=<v>               amdsmi_get_gpu_driver_info (absent: NOT_SUPPORTED)
+//   gpu.<i>.xgmi_hive=<hex>, gpu.<i>.xgmi_peers=<bdf>,...   amdsmi_get_xgmi_info / amdsmi_get_link_metrics
 //
 // Output buffers are written exactly as the real library documents (length-checked), so a probe that
 // passes a short buffer or reads past what was written shows up under ASan.
@@ -247,6 +248,49 @@ amdsmi_status_t amdsmi_get_fw_info(amdsmi_processor_handle processor_handle, amd
   return AMDSMI_STATUS_SUCCESS;
 }
 
+amdsmi_status_t amdsmi_get_xgmi_info(amdsmi_processor_handle processor_handle, amdsmi_xgmi_info_t* info) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("xgmi_hive");
+  memset(info, 0, sizeof *info);
+  info->xgmi_hive_id = strtoull(g->s("xgmi_hive").c_str(), nullptr, 16);
+  info->xgmi_lanes = 0;  // what the MI355X box reports
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+// gpu.<i>.xgmi_peers=<bdf>,<bdf>,...: one XGMI link per peer, plus the disabled port (all-ones BDF) first,
+// as the MI355X box reports them
+amdsmi_status_t amdsmi_get_link_metrics(amdsmi_processor_handle processor_handle, amdsmi_link_metrics_t* lm) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("xgmi_peers");
+  memset(lm, 0, sizeof *lm);
+  uint32_t n = 0;
+  lm->links[n].bdf.as_uint = UINT64_MAX;
+  lm->links[n].link_type = AMDSMI_LINK_TYPE_XGMI;
+  ++n;
+  const std::string s = g->s("xgmi_peers");
+  size_t pos = 0;
+  while (pos < s.size() && n < AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK) {
+    size_t end = s.find(',', pos);
+    if (end == std::string::npos) end = s.size();
+    unsigned dom = 0, bus = 0, dev = 0, fn = 0;
+    if (sscanf(s.substr(pos, end - pos).c_str(), "%x:%x:%x.%x", &dom, &bus, &dev, &fn) == 4) {
+      auto& l = lm->links[n++];
+      l.bdf.domain_number = dom;
+      l.bdf.bus_number = bus;
+      l.bdf.device_number = dev;
+      l.bdf.function_number = fn;
+      l.bit_rate = static_cast<uint32_t>(g->u("xgmi_speed_gbps", 38));
+      l.max_bandwidth = 16 * l.bit_rate;
+      l.link_type = AMDSMI_LINK_TYPE_XGMI;
+      l.read = 1000 * n;
+      l.write = 2000 * n;
+    }
+    pos = end + 1;
+  }
+  lm->num_links = n - 1;  // as the real library: the disabled port is in the table but not counted
+  return AMDSMI_STATUS_SUCCESS;
+}
+
 amdsmi_status_t amdsmi_gpu_xgmi_error_status(amdsmi_processor_handle processor_handle, amdsmi_xgmi_status_t* status) {
   GPU_OR_FAIL(processor_handle);
   FIELD_OR_NA("xgmi_error");
@@ -469,6 +513,8 @@ amdsmi_status_t amdsmi_get_gpu_metrics_info(amdsmi_processor_handle processor_ha
   GPU_OR_FAIL(processor_handle);
   FIELD_OR_NA("gfxclk_mhz");
   // the real library fills only what the firmware reports; the rest keeps the caller's all-ones
+  if (g->has("xgmi_width")) pgpu_metrics->xgmi_link_width = static_cast<uint16_t>(g->u("xgmi_width"));
+  if (g->has("xgmi_speed_gbps")) pgpu_metrics->xgmi_link_speed = static_cast<uint16_t>(g->u("xgmi_speed_gbps"));
   pgpu_metrics->current_gfxclks[0] = static_cast<uint16_t>(g->u("gfxclk_mhz"));
   pgpu_metrics->current_gfxclks[1] = static_cast<uint16_t>(g->u("gfxclk_mhz"));
   if (g->has("throttle_acc.n")) {

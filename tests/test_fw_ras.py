@@ -140,3 +140,67 @@ def test_agent_metrics_group_each_family_once_on_a_multi_gpu_node():
     fams = {f.name: f for f in text_string_to_metric_families(_metrics(r))}
     assert len(fams["mi355x_gpu_power_watts"].samples) == 8
     assert fams["mi355x_gpu_pcie_replays"].type == "counter"
+
+
+def _bdf(i):
+    return f"0000:{0x05 + 0x10 * i:02x}:00.0"
+
+
+def test_full_board_topology_is_healthy():
+    v = H.evaluate_report(rep(), 8)
+    assert v.state == H.HEALTHY, v.to_dict()
+    assert H.xgmi_topology(rep()["gpus"], 7) == []
+
+
+def test_split_hive_is_unhealthy():
+    other = {"xgmi_hive": "00000000000000aa"}
+    v = H.evaluate_report(rep(gpu6=other, gpu7=other), 8)
+    assert v.state == H.UNHEALTHY
+    assert v.reasons == [f"GPUs span 2 xGMI hives: gpu0-5 {fixtures.MI355X_HIVE}, gpu6-7 00000000000000aa"]
+
+
+def test_a_link_to_the_wrong_peer_is_unhealthy():
+    peers3 = [_bdf(j) for j in range(8) if j not in (3, 6)] + [_bdf(5)]  # two links to gpu5, none to gpu6
+    peers6 = [_bdf(j) for j in range(8) if j not in (6, 3)] + ["0000:ff:00.0"]  # its gpu3 link lands elsewhere
+    v = H.evaluate_report(rep(gpu3={"xgmi_peers": peers3}, gpu6={"xgmi_peers": peers6}), 8)
+    assert v.state == H.UNHEALTHY and v.gpus_ok == 8  # a node-level finding: no single GPU is at fault
+    assert v.reasons == [f"gpu3: xGMI links reach 6 of the node's 7 other GPUs (no link to {_bdf(6)})",
+                         f"gpu6: xGMI links reach 6 of the node's 7 other GPUs (no link to {_bdf(3)}), "
+                         "1 to devices outside the node"]
+
+
+def test_topology_needs_the_whole_unpartitioned_board():
+    # one GPU missing: the count rule fires, the wiring is not judged from a partial view
+    seven = fixtures.mi355x_probe_report("n", gpus=7)
+    v = H.evaluate_report(seven, 8)
+    assert v.reasons == ["7 of 8 GPUs visible to amd-smi"]
+    # a single-GPU VM sees peers it cannot resolve (profiles: its 7 links reach other VMs' GPUs)
+    one = fixtures.mi355x_probe_report("n", gpus=1, gpu0={"xgmi_peers": [_bdf(j) for j in range(1, 8)]})
+    assert H.xgmi_topology(one["gpus"], 7) == []
+    # CPX partitions report per-partition devices: not judged
+    cpx = rep(**{f"gpu{i}": {"compute_partition": "CPX", "cus": 32, "xgmi_peers": []} for i in range(8)})
+    assert H.xgmi_topology(cpx["gpus"], 7) == []
+    # --xgmi-links 0 turns every fabric rule off
+    assert H.xgmi_topology(rep(gpu3={"xgmi_peers": []})["gpus"], 0) == []
+
+
+def test_link_trained_down_degrades():
+    v = H.evaluate_report(rep(gpu4={"xgmi_speed_gbps": 25}), 8)
+    assert v.state == H.DEGRADED and v.warnings == ["gpu4: xGMI links trained at x16 25 Gb/s (MI355X: x16 38 Gb/s)"]
+    v = H.evaluate_report(rep(gpu4={"xgmi_width": 8}), 8)
+    assert v.warnings == ["gpu4: xGMI links trained at x8 38 Gb/s (MI355X: x16 38 Gb/s)"]
+
+
+def test_agent_metrics_xgmi_traffic_counters():
+    from prometheus_client.parser import text_string_to_metric_families
+
+    from k8s_gpu_node_checker_amd.agent.agent import _metrics, report_digest
+    r = fixtures.mi355x_probe_report("n", gpus=2)
+    r["gpus"][0]["xgmi_kb"] = [[1000, 2000]]
+    fams = {f.name: f for f in text_string_to_metric_families(_metrics(r))}
+    got = {(s.labels["peer"], s.labels["dir"]): s.value for s in fams["mi355x_gpu_xgmi_kilobytes"].samples}
+    assert got == {(_bdf(1), "read"): 1000, (_bdf(1), "write"): 2000}
+    # traffic moves every probe: it must not make the agent rewrite the annotation
+    r2 = json.loads(json.dumps(r))
+    r2["gpus"][0]["xgmi_kb"] = [[5000, 9000]]
+    assert report_digest(r) == report_digest(r2)

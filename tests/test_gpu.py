@@ -61,11 +61,14 @@ def test_python_probe_agrees_with_native(dev):
     a, b = ra["gpus"][0], rb["gpus"][0]
     for k in ("gfx", "vram_type", "vram_mb", "ecc_uncorrectable", "xgmi", "compute_partition",
               "memory_partition", "cus", "power_cap_w", "power_cap_default_w", "fw", "vbios_version",
-              "xgmi_error", "ecc_blocks"):
+              "xgmi_error", "ecc_blocks", "xgmi_hive", "xgmi_peers", "xgmi_width", "xgmi_speed_gbps"):
         assert a.get(k) == b.get(k), (k, a.get(k), b.get(k))
     assert ra.get("driver") == rb.get("driver") and ra["driver"]["name"] == "amdgpu", (ra.get("driver"), rb.get("driver"))
     # the firmware a node runs: power management / security processor / compute-queue images
     assert a["fw"] and {"mec", "psp_sos"} <= set(a["fw"]), a["fw"]
+    # the fabric: one peer per Up link, trained x16 at 38 Gb/s, a hive id
+    assert len(a["xgmi_peers"]) == a["xgmi"].count("U") == len(a["xgmi_kb"]), a
+    assert a["xgmi_width"] == 16 and a["xgmi_speed_gbps"] == 38 and len(a["xgmi_hive"]) == 16, a
     assert set(a.get("throttle_acc") or {}) == set(b.get("throttle_acc") or {})
 
 

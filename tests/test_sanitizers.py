@@ -77,20 +77,24 @@ def scenario(path, gpus=8, init_status=0, per_gpu=None):
     if (rec.get("driver") or {}).get("version"):
         lines.append(f"driver_version={rec['driver']['version']}")
 
-    def flat(prefix, v):  # nested objects (fw, ecc_blocks, throttle_acc) become dotted keys
+    def flat(prefix, v):  # nested objects (fw, ecc_blocks, throttle_acc) become dotted keys, lists commas
         if isinstance(v, dict):
             for a, b in v.items():
                 flat(f"{prefix}.{a}", b)
+        elif isinstance(v, list):
+            lines.append(f"{prefix}={','.join(str(x) for x in v)}")
         else:
             lines.append(f"{prefix}={v}")
+    bdfs = [f"0000:{0x05 + 0x10 * i:02x}:00.0" for i in range(gpus)]
     for i in range(gpus):
         g = dict(g0)
-        g["bdf"] = f"0000:{0x05 + 0x10 * i:02x}:00.0"
+        g["bdf"] = bdfs[i]
         g["uuid"] = g0["uuid"][:-2] + f"{i:02x}"
         g["kfd_node"] = 2 + i
+        g["xgmi_peers"] = [b for b in bdfs if b != bdfs[i]]  # one board: every link reaches another GPU of it
         g.update((per_gpu or {}).get(i, {}))
         for k, v in g.items():
-            if k in ("index", "probe_us", "processes", "kfd"):
+            if k in ("index", "probe_us", "processes", "kfd", "xgmi_kb"):
                 continue
             if k == "procs":
                 v = ",".join(f"{p['pid']}:{p['vram_mb']}" for p in v)
