@@ -190,6 +190,58 @@ void ecc_blocks(std::string& o, amdsmi_processor_handle h) {
   }
 }
 
+// RAS error records (CPER) the driver keeps for this GPU, by severity, with the newest timestamp of each:
+// {"fatal":n,"uncorrected":n,"corrected":n,"last_fatal":"2026-10-16T10:00:00Z",...}.  Reading them needs
+// root (the DaemonSet is privileged); any other status is reported as "cper_error", not judged.
+void probe_cper(std::string& o, amdsmi_processor_handle h) {
+  static const char* kSev[3] = {"uncorrected", "fatal", "corrected"};  // amdsmi_cper_sev_t order
+  std::vector<char> buf(1 << 20);
+  std::vector<amdsmi_cper_hdr_t*> hdrs(64);
+  uint64_t count[3] = {0, 0, 0}, last[3] = {0, 0, 0};  // last: YYYYMMDDhhmmss, comparable
+  uint64_t cursor = 0;
+  for (int call = 0; call < 256; ++call) {
+    uint64_t size = buf.size(), n = hdrs.size();
+    std::fill(hdrs.begin(), hdrs.end(), nullptr);
+    const amdsmi_status_t st = amdsmi_get_gpu_cper_entries(h, 0x7, buf.data(), &size, hdrs.data(), &n, &cursor);
+    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_MORE_DATA) {
+      if (call == 0) kv_str(o, "cper_error", status_name(st));
+      if (call == 0) return;
+      break;
+    }
+    const char* lo = buf.data();
+    const char* hi = buf.data() + std::min<uint64_t>(size, buf.size());
+    for (uint64_t i = 0; i < std::min<uint64_t>(n, hdrs.size()); ++i) {
+      const char* p = reinterpret_cast<const char*>(hdrs[i]);
+      if (p == nullptr || p < lo || p + sizeof(amdsmi_cper_hdr_t) > hi) continue;  // only headers inside buf
+      amdsmi_cper_hdr_t hd;
+      memcpy(&hd, p, sizeof hd);  // packed struct: copied out, never read through a misaligned pointer
+      const unsigned sev = static_cast<unsigned>(hd.error_severity);
+      if (sev > 2) continue;
+      ++count[sev];
+      const amdsmi_cper_timestamp_t& t = hd.timestamp;
+      const uint64_t year = t.year < 100 ? 2000u + t.year : t.year;
+      const uint64_t stamp = ((((year * 100 + t.month) * 100 + t.day) * 100 + t.hours) * 100 + t.minutes) * 100 + t.seconds;
+      last[sev] = std::max(last[sev], stamp);
+    }
+    if (st != AMDSMI_STATUS_MORE_DATA) break;
+  }
+  key(o, "cper");
+  o.push_back('{');
+  for (int sv = 0; sv < 3; ++sv) kv_u64(o, kSev[sv], count[sv]);
+  for (int sv = 0; sv < 3; ++sv) {
+    if (!count[sv]) continue;
+    const uint64_t v = last[sv];
+    char ts[32];
+    snprintf(ts, sizeof ts, "%04u-%02u-%02uT%02u:%02u:%02uZ", static_cast<unsigned>(v / 10000000000ull),
+             static_cast<unsigned>(v / 100000000ull % 100), static_cast<unsigned>(v / 1000000ull % 100),
+             static_cast<unsigned>(v / 10000ull % 100), static_cast<unsigned>(v / 100ull % 100),
+             static_cast<unsigned>(v % 100));
+    std::string k = std::string("last_") + kSev[sv];
+    kv_str(o, k.c_str(), ts);
+  }
+  o.push_back('}');
+}
+
 // Operating state, not identity: power against its cap, HBM stack temperature, clock, VRAM in use,
 // processes holding the device, and the firmware's throttle-residency accumulators.
 // The accumulators count since driver load; the agent turns two consecutive probes into the share
@@ -364,6 +416,7 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
   }
   uint32_t pages = 0;
   if (amdsmi_get_gpu_bad_page_info(h, &pages, nullptr) == AMDSMI_STATUS_SUCCESS) kv_u64(o, "bad_pages", pages);
+  probe_cper(o, h);
 
   amdsmi_xgmi_link_status_t xs;
   memset(&xs, 0, sizeof xs);

@@ -55,13 +55,15 @@ class HealthExpectations:
 
     def __init__(self, xgmi_links: int = XGMI_LINKS_EXPECTED, max_age_s: float = 900.0,
                  require_product: bool = True, vram_min_fraction: float = VRAM_MIN_FRACTION,
-                 bad_page_limit: int = 64, correctable_warn: int = 1000):
+                 bad_page_limit: int = 64, correctable_warn: int = 1000, cper_window_s: float = 86400.0):
         self.xgmi_links = xgmi_links
         self.max_age_s = max_age_s
         self.require_product = require_product
         self.vram_min_fraction = vram_min_fraction
         self.bad_page_limit = bad_page_limit
         self.correctable_warn = correctable_warn
+        #: a fatal CPER record newer than this (s, against the report's time) makes the GPU unhealthy
+        self.cper_window_s = cper_window_s
 
 
 class Verdict:
@@ -261,8 +263,15 @@ def _span(ix: List[Any]) -> str:
     return ",".join(str(i) for i in ix)
 
 
-def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str], List[str]]:
-    """Return ``(failures, warnings)`` for one GPU entry of a probe report."""
+def _age_s(stamp: Any, now: Optional[float]) -> Optional[float]:
+    """Seconds since an RFC 3339 ``...Z`` timestamp (None when either is missing or unparseable)."""
+    t = parse_k8s_time(stamp) if isinstance(stamp, str) else None
+    return None if t is None or now is None else now - t
+
+
+def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float] = None) -> Tuple[List[str], List[str]]:
+    """Return ``(failures, warnings)`` for one GPU entry of a probe report (``now``: the report's time,
+    against which record timestamps are aged)."""
     fail: List[str] = []
     warn: List[str] = []
     idx = g.get("index", "?")
@@ -292,6 +301,22 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations) -> Tuple[List[str],
     ce = g.get("ecc_correctable")
     if isinstance(ce, int) and ce > exp.correctable_warn:
         warn.append(f"gpu{idx}: {ce} correctable ECC errors{_by_block(blocks, 'ce')}")
+    cper = g.get("cper")
+    if isinstance(cper, dict):
+        # the driver's RAS error records (since it loaded): a recent fatal one means the GPU went through
+        # an error reset -- drain and look; an older one is history worth showing
+        fatal, last = cper.get("fatal"), cper.get("last_fatal")
+        if isinstance(fatal, int) and fatal > 0:
+            age = _age_s(last, now)
+            if age is None or age <= exp.cper_window_s:
+                fail.append(f"gpu{idx}: fatal RAS error record (CPER) at {last or '?'}")
+            else:
+                warn.append(f"gpu{idx}: {fatal} fatal RAS error record(s) since driver load, last {last}")
+        unc, last_u = cper.get("uncorrected"), cper.get("last_uncorrected")
+        if isinstance(unc, int) and unc > 0:
+            age = _age_s(last_u, now)
+            if age is None or age <= exp.cper_window_s:
+                warn.append(f"gpu{idx}: uncorrected non-fatal RAS error record (CPER) at {last_u or '?'}")
     bp = g.get("bad_pages")
     if isinstance(bp, int):
         if bp > exp.bad_page_limit:
@@ -376,7 +401,7 @@ def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
     for g in gpus:
         if not isinstance(g, dict):
             continue
-        f, w = evaluate_gpu(g, exp)
+        f, w = evaluate_gpu(g, exp, float(ts) if isinstance(ts, (int, float)) else now)
         fails += f
         warns += w
         ok += 0 if f else 1

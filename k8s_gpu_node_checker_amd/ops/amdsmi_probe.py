@@ -169,6 +169,67 @@ def _ecc_blocks_python(A: Any, h: Any) -> Optional[Dict[str, Dict[str, int]]]:
     return out or None
 
 
+_CPER_SEV = ("uncorrected", "fatal", "corrected")  # amdsmi_cper_sev_t order
+
+
+def _status_name(W: Any, st: int) -> str:
+    """The library's own text for a status (what the native probe's ``status_name`` reports)."""
+    try:
+        txt = ctypes.POINTER(ctypes.c_char)()
+        if W.amdsmi_status_code_to_string(st, ctypes.byref(txt)) == 0 and txt:
+            return ctypes.string_at(txt).decode(errors="replace")
+    except Exception:
+        pass
+    return getattr(W, "amdsmi_status_t__enumvalues", {}).get(st, f"AMDSMI_STATUS_{st}")
+
+
+def _cper_python(A: Any, h: Any) -> Dict[str, Any]:
+    """The native probe's ``probe_cper``: RAS error records by severity and the newest of each
+    (``cper``), or ``cper_error`` with the status name when they cannot be read (non-root: NO_PERM)."""
+    try:
+        W = A.amdsmi_interface.amdsmi_wrapper
+        hdr_t = W.amdsmi_cper_hdr_t
+    except Exception:
+        return {}
+    count, last = [0, 0, 0], [0, 0, 0]
+    buf = ctypes.create_string_buffer(1 << 20)
+    hdrs = (ctypes.POINTER(hdr_t) * 64)()
+    cursor = ctypes.c_uint64(0)
+    for call in range(256):
+        size, n = ctypes.c_uint64(len(buf)), ctypes.c_uint64(len(hdrs))
+        st = W.amdsmi_get_gpu_cper_entries(h, ctypes.c_uint32(0x7), buf, ctypes.byref(size),
+                                           ctypes.cast(hdrs, ctypes.POINTER(ctypes.POINTER(hdr_t))),
+                                           ctypes.byref(n), ctypes.byref(cursor))
+        if st not in (0, 39):  # SUCCESS, MORE_DATA
+            if call == 0:
+                return {"cper_error": _status_name(W, st)}
+            break
+        base, top = ctypes.addressof(buf), ctypes.addressof(buf) + min(size.value, len(buf))
+        for i in range(min(n.value, len(hdrs))):
+            if not hdrs[i]:
+                continue
+            addr = ctypes.cast(hdrs[i], ctypes.c_void_p).value or 0
+            if addr < base or addr + ctypes.sizeof(hdr_t) > top:
+                continue
+            hd = hdrs[i].contents
+            sev = int(hd.error_severity)
+            if not 0 <= sev <= 2:
+                continue
+            t = hd.timestamp
+            year = t.year + 2000 if t.year < 100 else t.year
+            stamp = (((((year * 100 + t.month) * 100 + t.day) * 100 + t.hours) * 100 + t.minutes) * 100) + t.seconds
+            count[sev] += 1
+            last[sev] = max(last[sev], stamp)
+        if st != 39:
+            break
+    out: Dict[str, Any] = {name: count[i] for i, name in enumerate(_CPER_SEV)}
+    for i, name in enumerate(_CPER_SEV):
+        if count[i]:
+            v = f"{last[i]:014d}"
+            out[f"last_{name}"] = f"{v[0:4]}-{v[4:6]}-{v[6:8]}T{v[8:10]}:{v[10:12]}:{v[12:14]}Z"
+    return {"cper": out}
+
+
 def _xgmi_fabric_python(A: Any, h: Any, q: Any) -> Dict[str, Any]:
     """The native probe's xGMI fabric fields: hive id, peer BDF and traffic of every XGMI link."""
     out: Dict[str, Any] = {}
@@ -240,6 +301,7 @@ def probe_python(node: str) -> Dict[str, Any]:
                     g["ecc_blocks"] = _ecc_blocks_python(A, h)
             bp = q(A.amdsmi_get_gpu_bad_page_info)
             g["bad_pages"] = len(bp) if isinstance(bp, list) else None
+            g.update(_cper_python(A, h))
             g["xgmi"] = _xgmi_string(q(A.amdsmi_get_gpu_xgmi_link_status))
             xe = q(A.amdsmi_gpu_xgmi_error_status)
             g["xgmi_error"] = int(xe) if xe is not None else None

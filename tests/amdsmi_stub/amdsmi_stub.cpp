@@ -291,6 +291,59 @@ amdsmi_status_t amdsmi_get_link_metrics(amdsmi_processor_handle processor_handle
   return AMDSMI_STATUS_SUCCESS;
 }
 
+// gpu.<i>.cper_entries=<sev>@<YYYYMMDDhhmmss>,... : records laid out back to back in cper_data (header +
+// 32 payload bytes each), paged by the caller's header-array length and buffer size with the cursor;
+// gpu.<i>.cper_error=... : NO_PERM (what a non-root caller gets on the MI355X box)
+amdsmi_status_t amdsmi_get_gpu_cper_entries(amdsmi_processor_handle processor_handle, uint32_t severity_mask,
+                                            char* cper_data, uint64_t* buf_size, amdsmi_cper_hdr_t** cper_hdrs,
+                                            uint64_t* entry_count, uint64_t* cursor) {
+  GPU_OR_FAIL(processor_handle);
+  if (g->has("cper_error")) return AMDSMI_STATUS_NO_PERM;
+  FIELD_OR_NA("cper_entries");
+  struct Rec {
+    unsigned sev;
+    uint64_t stamp;
+  };
+  std::vector<Rec> recs;
+  const std::string s = g->s("cper_entries");
+  size_t pos = 0;
+  while (pos < s.size()) {
+    size_t end = s.find(',', pos);
+    if (end == std::string::npos) end = s.size();
+    unsigned sev = 0;
+    unsigned long long stamp = 0;
+    if (sscanf(s.substr(pos, end - pos).c_str(), "%u@%llu", &sev, &stamp) == 2 && ((severity_mask >> sev) & 1u))
+      recs.push_back({sev, stamp});
+    pos = end + 1;
+  }
+  const size_t rec_len = sizeof(amdsmi_cper_hdr_t) + 32;
+  uint64_t n = 0, used = 0, i = *cursor;
+  for (; i < recs.size() && n < *entry_count && used + rec_len <= *buf_size; ++i, ++n) {
+    amdsmi_cper_hdr_t h;
+    memset(&h, 0, sizeof h);
+    memcpy(h.signature, "CPER", 4);
+    h.signature_end = 0xFFFFFFFFu;
+    h.sec_cnt = 1;
+    h.error_severity = static_cast<amdsmi_cper_sev_t>(recs[i].sev);
+    h.record_length = static_cast<uint32_t>(rec_len);
+    const uint64_t t = recs[i].stamp;
+    h.timestamp.year = static_cast<uint8_t>(t / 10000000000ull % 100);  // two digits, as the driver fills it
+    h.timestamp.month = static_cast<uint8_t>(t / 100000000ull % 100);
+    h.timestamp.day = static_cast<uint8_t>(t / 1000000ull % 100);
+    h.timestamp.hours = static_cast<uint8_t>(t / 10000ull % 100);
+    h.timestamp.minutes = static_cast<uint8_t>(t / 100ull % 100);
+    h.timestamp.seconds = static_cast<uint8_t>(t % 100);
+    memcpy(cper_data + used, &h, sizeof h);
+    memset(cper_data + used + sizeof h, 0xAB, 32);
+    cper_hdrs[n] = reinterpret_cast<amdsmi_cper_hdr_t*>(cper_data + used);
+    used += rec_len;
+  }
+  *entry_count = n;
+  *buf_size = used;
+  *cursor = i;
+  return i < recs.size() ? AMDSMI_STATUS_MORE_DATA : AMDSMI_STATUS_SUCCESS;
+}
+
 amdsmi_status_t amdsmi_gpu_xgmi_error_status(amdsmi_processor_handle processor_handle, amdsmi_xgmi_status_t* status) {
   GPU_OR_FAIL(processor_handle);
   FIELD_OR_NA("xgmi_error");

@@ -204,3 +204,30 @@ def test_agent_metrics_xgmi_traffic_counters():
     r2 = json.loads(json.dumps(r))
     r2["gpus"][0]["xgmi_kb"] = [[5000, 9000]]
     assert report_digest(r) == report_digest(r2)
+
+
+def test_cper_fatal_record_recent_is_unhealthy_old_is_history():
+    now = 1_800_000_000.0  # 2027-01-15T08:00:00Z
+    recent = {"fatal": 1, "uncorrected": 0, "corrected": 4, "last_fatal": "2027-01-15T07:10:00Z",
+              "last_corrected": "2027-01-15T07:00:00Z"}
+    v = H.evaluate_report(rep(ts=now, gpu2={"cper": recent}), 8, now=now)
+    assert v.state == H.UNHEALTHY and v.reasons == ["gpu2: fatal RAS error record (CPER) at 2027-01-15T07:10:00Z"]
+    old = dict(recent, last_fatal="2027-01-10T07:10:00Z")
+    v = H.evaluate_report(rep(ts=now, gpu2={"cper": old}), 8, now=now)
+    assert v.state == H.DEGRADED
+    assert v.warnings == ["gpu2: 1 fatal RAS error record(s) since driver load, last 2027-01-10T07:10:00Z"]
+    # the window is a threshold like any other
+    v = H.evaluate_report(rep(ts=now, gpu2={"cper": old}), 8, H.HealthExpectations(cper_window_s=7 * 86400), now=now)
+    assert v.state == H.UNHEALTHY
+
+
+def test_cper_uncorrected_recent_degrades_corrected_only_is_healthy():
+    now = 1_800_000_000.0
+    unc = {"fatal": 0, "uncorrected": 2, "corrected": 0, "last_uncorrected": "2027-01-15T06:00:00Z"}
+    v = H.evaluate_report(rep(ts=now, gpu0={"cper": unc}), 8, now=now)
+    assert v.state == H.DEGRADED and v.warnings == [
+        "gpu0: uncorrected non-fatal RAS error record (CPER) at 2027-01-15T06:00:00Z"]
+    ok = {"fatal": 0, "uncorrected": 0, "corrected": 12, "last_corrected": "2027-01-15T06:00:00Z"}
+    assert H.evaluate_report(rep(ts=now, gpu0={"cper": ok}), 8, now=now).state == H.HEALTHY
+    # a probe that could not read the records (non-root) is not judged on them
+    assert H.evaluate_report(rep(ts=now, gpu0={"cper_error": "AMDSMI_STATUS_NO_PERM"}), 8, now=now).state == H.HEALTHY

@@ -61,7 +61,8 @@ def test_python_probe_agrees_with_native(dev):
     a, b = ra["gpus"][0], rb["gpus"][0]
     for k in ("gfx", "vram_type", "vram_mb", "ecc_uncorrectable", "xgmi", "compute_partition",
               "memory_partition", "cus", "power_cap_w", "power_cap_default_w", "fw", "vbios_version",
-              "xgmi_error", "ecc_blocks", "xgmi_hive", "xgmi_peers", "xgmi_width", "xgmi_speed_gbps"):
+              "xgmi_error", "ecc_blocks", "xgmi_hive", "xgmi_peers", "xgmi_width", "xgmi_speed_gbps",
+              "cper", "cper_error"):
         assert a.get(k) == b.get(k), (k, a.get(k), b.get(k))
     assert ra.get("driver") == rb.get("driver") and ra["driver"]["name"] == "amdgpu", (ra.get("driver"), rb.get("driver"))
     # the firmware a node runs: power management / security processor / compute-queue images

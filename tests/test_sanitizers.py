@@ -93,6 +93,7 @@ def scenario(path, gpus=8, init_status=0, per_gpu=None):
         g["kfd_node"] = 2 + i
         g["xgmi_peers"] = [b for b in bdfs if b != bdfs[i]]  # one board: every link reaches another GPU of it
         g.update((per_gpu or {}).get(i, {}))
+        g = {k: v for k, v in g.items() if v is not None}
         for k, v in g.items():
             if k in ("index", "probe_us", "processes", "kfd", "xgmi_kb"):
                 continue
@@ -255,3 +256,26 @@ def test_probe_cli_under_asan_firmware_ras_blocks_xgmi_error(asan_probe, tmp_pat
     assert "gpu5: xGMI error status errors" in v.warnings
     assert any(w.startswith("firmware differs across GPUs: psp_sos: gpu0-4,6,7") or
                w.startswith("firmware differs across GPUs: psp_sos: gpu0,1,2,3,4,6,7") for w in v.warnings), v.warnings
+
+
+@pytest.mark.slow
+def test_probe_cli_under_asan_pages_cper_records(asan_probe, tmp_path):
+    """CPER records walked page by page (71 records > the probe's 64 header slots: MORE_DATA + cursor), every
+    header pointer bounds-checked against the buffer, severities counted, newest timestamp kept; a
+    NO_PERM GPU reports cper_error."""
+    import json
+
+    from k8s_gpu_node_checker_amd.models import health as H
+    d, _, _ = asan_probe
+    recs = ",".join([f"2@2610160900{i % 60:02d}" for i in range(70)] + ["1@20261016101500"])
+    scen = scenario(tmp_path / "s.txt", gpus=2, per_gpu={0: {"cper_entries": recs, "cper_error": None},
+                                                         1: {"cper_error": "AMDSMI_STATUS_NO_PERM"}})
+    p = _run_cli(d, scen)
+    assert p.returncode == 0 and "ERROR: AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr, \
+        p.stderr[-3000:]
+    r = json.loads(p.stdout)
+    assert r["gpus"][0]["cper"] == {"uncorrected": 0, "fatal": 1, "corrected": 70,
+                                    "last_fatal": "2026-10-16T10:15:00Z", "last_corrected": "2026-10-16T09:00:59Z"}
+    assert r["gpus"][1]["cper_error"] == "AMDSMI_STATUS_NO_PERM" and "cper" not in r["gpus"][1]
+    v = H.evaluate_report(r, 2, H.HealthExpectations(xgmi_links=0), now=H.parse_k8s_time("2026-10-16T12:00:00Z"))
+    assert v.reasons == ["gpu0: fatal RAS error record (CPER) at 2026-10-16T10:15:00Z"], v.to_dict()
