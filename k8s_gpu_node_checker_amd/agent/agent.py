@@ -462,6 +462,11 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
             for kind in ("ce", "ue", "de"):
                 if isinstance(c, dict) and isinstance(c.get(kind), int):
                     put("mi355x_gpu_ecc_block_errors", f'{lbl},block="{_esc(block)}",kind="{kind}"', c[kind])
+        cper = g.get("cper")
+        if isinstance(cper, dict):
+            for sev in ("fatal", "uncorrected", "corrected"):
+                if isinstance(cper.get(sev), int):
+                    put("mi355x_gpu_cper_records", f'{lbl},severity="{sev}"', cper[sev])
         peers, kb = g.get("xgmi_peers"), g.get("xgmi_kb")
         if isinstance(peers, list) and isinstance(kb, list):
             for peer, rw in zip(peers, kb):

@@ -127,6 +127,10 @@ def test_agent_metrics_expose_firmware_driver_and_ras_blocks():
     ecc = {(s.labels["block"], s.labels["kind"]): s.value for s in fams["mi355x_gpu_ecc_block_errors"].samples}
     assert ecc == {("umc", "ce"): 7, ("umc", "ue"): 1, ("umc", "de"): 0}
     assert [s.value for s in fams["mi355x_gpu_xgmi_error_status"].samples] == [2]
+    r["gpus"][0]["cper"] = {"fatal": 0, "uncorrected": 1, "corrected": 9}
+    fams = {f.name: f for f in text_string_to_metric_families(_metrics(r))}
+    assert {s.labels["severity"]: s.value for s in fams["mi355x_gpu_cper_records"].samples} == {
+        "fatal": 0, "uncorrected": 1, "corrected": 9}
 
 
 def test_agent_metrics_group_each_family_once_on_a_multi_gpu_node():
