@@ -49,6 +49,8 @@ _VOLATILE = frozenset(("ts", "probe_ms", "probe_us", "hotspot_c", "wall_s", "ms_
                        "throttle", "procs", "gfx_activity", "diag_skipped", "xgmi_kb"))
 
 DIAG_WHEN = ("idle", "always")
+# per-GPU fields kept out of the node annotation (Agent.annotation)
+_ANNOTATION_DROP = frozenset(("xgmi_kb", "throttle_acc", "procs", "probe_us"))
 
 
 def gpu_busy(g: Dict[str, Any], own_pids: frozenset = frozenset(), busy_vram_mb: int = 2048,
@@ -356,7 +358,13 @@ class Agent:
             self._acc_prev[key] = (now, acc)
 
     def annotation(self, rep: Dict[str, Any]) -> Dict[str, str]:
-        return {HEALTH_ANNOTATION: json.dumps(rep, separators=(",", ":"))}
+        """The report as the node annotation, minus the raw counters (xGMI traffic, throttle accumulators,
+        per-process VRAM, per-GPU probe time): every client that LISTs or watches nodes receives the
+        annotation, it is rewritten only when the health content changes, so those would only be stale
+        bytes there; they stay on ``/probe`` and ``/metrics``."""
+        gpus = [{k: v for k, v in g.items() if k not in _ANNOTATION_DROP} if isinstance(g, dict) else g
+                for g in rep.get("gpus") or []]
+        return {HEALTH_ANNOTATION: json.dumps(dict(rep, gpus=gpus), separators=(",", ":"))}
 
     def condition(self, rep: Dict[str, Any]) -> Dict[str, Any]:
         v = self.evaluate(rep)

@@ -235,3 +235,15 @@ def test_cper_uncorrected_recent_degrades_corrected_only_is_healthy():
     assert H.evaluate_report(rep(ts=now, gpu0={"cper": ok}), 8, now=now).state == H.HEALTHY
     # a probe that could not read the records (non-root) is not judged on them
     assert H.evaluate_report(rep(ts=now, gpu0={"cper_error": "AMDSMI_STATUS_NO_PERM"}), 8, now=now).state == H.HEALTHY
+
+
+def test_annotation_leaves_raw_counters_to_metrics():
+    from k8s_gpu_node_checker_amd.agent.agent import Agent
+    from k8s_gpu_node_checker_amd.models.node import HEALTH_ANNOTATION
+    r = fixtures.mi355x_probe_report("n", gpus=2)
+    r["gpus"][0].update(xgmi_kb=[[1, 2]], procs=[{"pid": 7, "vram_mb": 9}], probe_us=800)
+    ann = json.loads(Agent("n").annotation(r)[HEALTH_ANNOTATION])
+    assert not {"xgmi_kb", "throttle_acc", "procs", "probe_us"} & set(ann["gpus"][0])
+    assert ann["gpus"][0]["fw"] == fixtures.MI355X_FW and ann["gpus"][0]["xgmi_peers"] == r["gpus"][0]["xgmi_peers"]
+    assert "xgmi_kb" in r["gpus"][0]  # the live report (/probe) keeps them
+    assert H.evaluate_report(ann, 2, H.HealthExpectations(xgmi_links=0)).state == H.HEALTHY
