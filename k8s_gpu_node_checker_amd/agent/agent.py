@@ -34,7 +34,7 @@ import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional, Sequence
 
-from ..models.health import (HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, XGMI_LINKS_EXPECTED,
+from ..models.health import (DEGRADED, HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, XGMI_LINKS_EXPECTED,
                               HealthExpectations, Verdict,
                               condition_for, condition_reason, evaluate_report, format_k8s_time, fw_version_str,
                               throttle_window)
@@ -445,6 +445,10 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
         fams.setdefault(name, []).append(f"{name}{{{labels}}} {value}" if labels else f"{name} {value}")
 
     put("mi355x_agent_probe_timestamp_seconds", "", rep.get("ts", 0))
+    if isinstance(rep.get("state"), str):
+        # the verdict the agent publishes as AMDGPUHealthy, one series per state (1 for the current one)
+        for st in (HEALTHY, DEGRADED, UNHEALTHY, UNKNOWN):
+            put("mi355x_node_health", f'state="{st}"', 1 if rep["state"] == st else 0)
     drv = rep.get("driver")
     if isinstance(drv, dict) and drv.get("version"):
         put("mi355x_node_driver_info", f'name="{_esc(drv.get("name"))}",version="{_esc(drv["version"])}"', 1)

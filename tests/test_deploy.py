@@ -121,3 +121,61 @@ def test_agent_daemonset_sees_host_pids_and_kubelet_allocations():
     assert vols[pr["name"]]["hostPath"]["path"] == os.path.dirname(sock)
     sc = c["securityContext"]
     assert sc.get("readOnlyRootFilesystem") is True and "/tmp" in mounted  # HIP / amd-smi scratch on tmpfs
+
+
+def _rich_report():
+    """A report carrying every field the agent turns into a metric."""
+    from k8s_gpu_node_checker_amd.testing import fixtures
+    r = fixtures.mi355x_probe_report("n", gpus=2)
+    r["state"] = "healthy"
+    g = r["gpus"][0]
+    g.update(xgmi_error=0, xgmi_kb=[[1, 2]] * 1, cper={"fatal": 0, "uncorrected": 0, "corrected": 1},
+             ecc_blocks={"umc": {"ce": 1, "ue": 0, "de": 0}}, gfx_activity=0,
+             throttle={"s": 60, "thermal_pct": 0.0, "power_pct": 1.0, "prochot_pct": 0.0},
+             diag={"gemm": {"pass": True, "tflops": 1200.0}})
+    return r
+
+
+def test_monitoring_rules_use_metrics_the_agent_emits():
+    import re
+
+    from prometheus_client.parser import text_string_to_metric_families
+    docs = [d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "monitoring", "monitoring.yaml"))) if d]
+    kinds = {d["kind"] for d in docs}
+    assert kinds == {"Service", "ServiceMonitor", "PrometheusRule"}
+    fams = {f.name: f for f in text_string_to_metric_families(agent._metrics(_rich_report()))}
+    labels = {name: set().union(*(set(s.labels) for s in f.samples)) | {"node"} for name, f in fams.items()}
+    rules = [r for d in docs if d["kind"] == "PrometheusRule" for grp in d["spec"]["groups"] for r in grp["rules"]]
+    assert len(rules) >= 10
+    for r in rules:
+        names = set(re.findall(r"\bmi355x_[a-z0-9_]+", r["expr"]))
+        assert names, r["alert"]
+        for n in names:
+            assert n in fams, (r["alert"], n)
+        # every label a summary prints exists on the alert's series: a label of its metric(s), the
+        # relabelled `node`, or a label the expression aggregates by
+        have = set().union(*(labels[n] for n in names))
+        outer = re.match(r"\s*count by \(([^)]*)\)", r["expr"])
+        if outer:
+            have = {x.strip() for x in outer.group(1).split(",")}
+        for lbl in re.findall(r"\$labels\.([a-z_]+)", r["annotations"]["summary"]):
+            assert lbl in have, (r["alert"], lbl, have)
+    # the Service and ServiceMonitor find the DaemonSet's pods and its metrics port
+    ds = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
+    pod_labels = ds["spec"]["template"]["metadata"]["labels"]
+    port_names = {p["name"] for c in ds["spec"]["template"]["spec"]["containers"] for p in c.get("ports", [])}
+    svc = next(d for d in docs if d["kind"] == "Service")
+    assert svc["spec"]["selector"].items() <= pod_labels.items()
+    assert {p["targetPort"] for p in svc["spec"]["ports"]} <= port_names
+    sm = next(d for d in docs if d["kind"] == "ServiceMonitor")
+    assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
+    assert {e["port"] for e in sm["spec"]["endpoints"]} <= {p["name"] for p in svc["spec"]["ports"]}
+
+
+def test_agent_metrics_carry_the_verdict_state():
+    from prometheus_client.parser import text_string_to_metric_families
+    r = _rich_report()
+    r["state"] = "degraded"
+    fams = {f.name: f for f in text_string_to_metric_families(agent._metrics(r))}
+    assert {s.labels["state"]: s.value for s in fams["mi355x_node_health"].samples} == {
+        "healthy": 0, "degraded": 1, "unhealthy": 0, "unknown": 0}
