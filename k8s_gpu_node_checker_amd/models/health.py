@@ -243,6 +243,11 @@ def xgmi_topology(gpus: Sequence[Any], links_expected: int) -> List[str]:
         str(g.get("compute_partition") or "SPX").upper() == "SPX" for g in gs)
     if not full_board:
         return out
+    # a VM that remaps the GPUs' PCI addresses sees its links name host addresses none of its GPUs
+    # carry: nothing to match the wiring against, so it is not judged
+    named = {_bdf(p) for g in bdfs.values() if isinstance(g.get("xgmi_peers"), list) for p in g["xgmi_peers"]}
+    if not named & set(bdfs):
+        return out
     for me, g in bdfs.items():
         peers = g.get("xgmi_peers")
         if not isinstance(peers, list):

@@ -184,6 +184,9 @@ def test_topology_needs_the_whole_unpartitioned_board():
     # CPX partitions report per-partition devices: not judged
     cpx = rep(**{f"gpu{i}": {"compute_partition": "CPX", "cus": 32, "xgmi_peers": []} for i in range(8)})
     assert H.xgmi_topology(cpx["gpus"], 7) == []
+    # a VM whose guest PCI addresses differ from the host's: no link names a GPU it sees -> not judged
+    host = {f"gpu{i}": {"xgmi_peers": [f"0001:{0x80 + j:02x}:00.0" for j in range(8) if j != i]} for i in range(8)}
+    assert H.xgmi_topology(rep(**host)["gpus"], 7) == []
     # --xgmi-links 0 turns every fabric rule off
     assert H.xgmi_topology(rep(gpu3={"xgmi_peers": []})["gpus"], 0) == []
 
