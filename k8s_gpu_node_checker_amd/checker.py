@@ -214,6 +214,13 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
             if v is None:
                 verdicts.append(None)
                 continue
+            cap, alloc = ex.capacity.get(PRIMARY_GPU_KEY), ex.allocatable.get(PRIMARY_GPU_KEY)
+            if is_amd and cap and alloc is not None and alloc < cap:
+                # SURVEY §5 failure detection: the device plugin withholds GPUs it judged unhealthy
+                # (allocatable < capacity); the scheduler already avoids them, so a hint, not a failure
+                v.warnings.append(f"device plugin allocates {alloc} of {cap} {PRIMARY_GPU_KEY}")
+                if v.state == H.HEALTHY:
+                    v.state = H.DEGRADED
             verdicts.append(v)
             gated = H.gate_ready(ex.ready_condition, v, opts.health_policy, is_amd, unknown_ok)
             if gated != node["ready"]:

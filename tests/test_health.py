@@ -336,3 +336,22 @@ def test_condition_counts_parser_matches_its_regex():
         m = rx.match(msg)
         assert H.parse_condition_counts(msg) == ((int(m.group(1)), int(m.group(2))) if m else None), msg
     check()
+
+
+def test_allocatable_below_capacity_is_a_degraded_hint(run_cli, mock_cluster, tmp_path):
+    """the device plugin withholding GPUs (allocatable < capacity) is a health hint: a node
+    whose agent says healthy becomes degraded (still Ready), and the hint names the counts."""
+    r8 = fixtures.mi355x_probe_report("a", gpus=8)
+    nodes = [fixtures.realistic_node("a", index=0, allocatable_gpus=7, extra_conditions=[fixtures.health_condition(r8, 8)]),
+             fixtures.realistic_node("b", index=1, extra_conditions=[fixtures.health_condition(r8, 8)])]
+    kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc, "--json-extended"])
+    assert p.returncode == 0, p.stderr
+    doc = json.loads(p.stdout)
+    assert [n["ready"] for n in doc["nodes"]] == [True, True]
+    h = [n["health"] for n in doc["mi355x"]["nodes"]]
+    assert h[0]["state"] == "degraded" and h[0]["warnings"] == ["device plugin allocates 7 of 8 amd.com/gpu"]
+    assert h[1]["state"] == "healthy"
+    # --mi355x counts allocatable GPUs: the node is still a GPU node with 7
+    p = run_cli(["--kubeconfig", kc, "--json", "--mi355x"])
+    assert json.loads(p.stdout)["nodes"][0]["gpus"] == 7
