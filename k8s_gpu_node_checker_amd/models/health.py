@@ -262,6 +262,22 @@ def xgmi_topology(gpus: Sequence[Any], links_expected: int) -> List[str]:
     return out
 
 
+def partition_mismatch(gpus: Sequence[Any]) -> List[str]:
+    """Compute / memory partition modes that differ between the GPUs of one node.  An 8-GPU board is
+    partitioned as a whole (the device plugin advertises one resource shape per node); one GPU left in
+    another mode after a repartition hands the scheduler devices of two sizes under one name."""
+    out = []
+    for key, name in (("compute_partition", "compute"), ("memory_partition", "memory")):
+        seen: Dict[str, List[Any]] = {}
+        for g in gpus:
+            if isinstance(g, dict) and isinstance(g.get(key), str) and g[key]:
+                seen.setdefault(g[key], []).append(g.get("index", "?"))
+        if len(seen) > 1:
+            groups = sorted(seen.items(), key=lambda kv: (-len(kv[1]), kv[0]))
+            out.append(f"{name}: " + ", ".join(f"gpu{_span(ix)} {mode}" for mode, ix in groups))
+    return out
+
+
 def _span(ix: List[Any]) -> str:
     if len(ix) > 1 and all(isinstance(i, int) for i in ix) and ix == list(range(ix[0], ix[0] + len(ix))):
         return f"{ix[0]}-{ix[-1]}"
@@ -416,6 +432,9 @@ def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
     mism = firmware_mismatch(gpus)
     if mism:
         warns.append("firmware differs across GPUs: " + "; ".join(mism))
+    modes = partition_mismatch(gpus)
+    if modes:
+        warns.append("partition modes differ across GPUs: " + "; ".join(modes))
     fabric = report.get("fabric")
     if isinstance(fabric, dict):
         for test, res in fabric.items():  # node-level: the xGMI pair matrix (ops/diag.p2p_matrix)

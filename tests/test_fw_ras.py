@@ -250,3 +250,14 @@ def test_annotation_leaves_raw_counters_to_metrics():
     assert ann["gpus"][0]["fw"] == fixtures.MI355X_FW and ann["gpus"][0]["xgmi_peers"] == r["gpus"][0]["xgmi_peers"]
     assert "xgmi_kb" in r["gpus"][0]  # the live report (/probe) keeps them
     assert H.evaluate_report(ann, 2, H.HealthExpectations(xgmi_links=0)).state == H.HEALTHY
+
+
+def test_partition_modes_differing_across_gpus_degrade():
+    v = H.evaluate_report(rep(gpu7={"compute_partition": "CPX", "cus": 32}), 8)
+    assert v.state == H.DEGRADED
+    assert v.warnings == ["partition modes differ across GPUs: compute: gpu0-6 SPX, gpu7 CPX"]
+    v = H.evaluate_report(rep(gpu2={"memory_partition": "NPS2", "vram_mb": 147448}), 8)
+    assert v.warnings == ["partition modes differ across GPUs: memory: gpu0,1,3,4,5,6,7 NPS1, gpu2 NPS2"]
+    # a board partitioned as a whole is one mode everywhere: nothing to report
+    cpx = rep(**{f"gpu{i}": {"compute_partition": "CPX", "cus": 32} for i in range(8)})
+    assert H.partition_mismatch(cpx["gpus"]) == []
