@@ -59,7 +59,8 @@ def test_warnings_degrade_but_stay_ok(override, needle):
 
 
 def test_partition_modes_scale_vram_expectation():
-    v = H.evaluate_report(rep(gpu0={"vram_mb": 147448, "memory_partition": "NPS2"}), 8)
+    nps2 = {f"gpu{i}": {"vram_mb": 147448, "memory_partition": "NPS2"} for i in range(8)}  # the whole board
+    v = H.evaluate_report(rep(**nps2), 8)
     assert v.state == H.HEALTHY
     assert H.evaluate_report(rep(gpu0={"vram_mb": 147448}), 8).state == H.UNHEALTHY
 
