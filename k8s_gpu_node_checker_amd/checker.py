@@ -23,7 +23,7 @@ from . import report
 from .kube.client import KubeClient
 from .kube.config import ClusterConnection
 from .models import health as H
-from .models.node import ScanResult, expected_gpu_count
+from .models.node import ScanResult
 from .models.node import HEALTH_ANNOTATION
 from .models.resources import GPU_RESOURCE_KEYS, PRIMARY_GPU_KEY
 from .utils.timing import NullTracer, Tracer
@@ -195,34 +195,39 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
         reeval = opts.reeval
         now = time.time()
         unapplied: List[str] = []
+        key = PRIMARY_GPU_KEY
+        policy = opts.health_policy
+        max_age = opts.probe_max_age
+        from_condition = H.verdict_from_condition
+        gate = H.gate_ready
         for node, ex, rep in zip(scan.gpu_nodes, scan.extras, reports):
-            is_amd = PRIMARY_GPU_KEY in node["gpu_breakdown"] or PRIMARY_GPU_KEY in ex.allocatable
-            expected = expected_gpu_count(ex)
+            cap, alloc = ex.capacity.get(key), ex.allocatable.get(key)
+            is_amd = alloc is not None or key in node["gpu_breakdown"]
+            expected = max(cap or 0, alloc or 0)  # models.node.expected_gpu_count
             v: Optional[H.Verdict] = None
             if rep is None and reeval:
                 rep = H.parse_annotation(ex.health_annotation)
             if rep is None and ex.health_condition is not None:
                 # cheap path: the agent's verdict is a NodeCondition already parsed by the scan
-                v = H.verdict_from_condition(ex.health_condition, opts.probe_max_age, now, expected)
+                v = from_condition(ex.health_condition, max_age, now, expected)
                 if reeval:
                     unapplied.append(node["name"])
             else:
                 if rep is None:
                     rep = H.parse_annotation(ex.health_annotation)
-                if rep is not None or opts.health_policy == "require":
+                if rep is not None or policy == "require":
                     v = H.evaluate_report(rep, expected, exp, now)
             if v is None:
                 verdicts.append(None)
                 continue
-            cap, alloc = ex.capacity.get(PRIMARY_GPU_KEY), ex.allocatable.get(PRIMARY_GPU_KEY)
-            if is_amd and cap and alloc is not None and alloc < cap:
+            if cap and alloc is not None and alloc < cap:
                 # SURVEY §5 failure detection: the device plugin withholds GPUs it judged unhealthy
                 # (allocatable < capacity); the scheduler already avoids them, so a hint, not a failure
-                v.warnings.append(f"device plugin allocates {alloc} of {cap} {PRIMARY_GPU_KEY}")
+                v.warnings.append(f"device plugin allocates {alloc} of {cap} {key}")
                 if v.state == H.HEALTHY:
                     v.state = H.DEGRADED
             verdicts.append(v)
-            gated = H.gate_ready(ex.ready_condition, v, opts.health_policy, is_amd, unknown_ok)
+            gated = gate(ex.ready_condition, v, policy, is_amd, unknown_ok)
             if gated != node["ready"]:
                 node["ready"] = gated
                 changed = True
