@@ -179,3 +179,30 @@ def test_agent_metrics_carry_the_verdict_state():
     fams = {f.name: f for f in text_string_to_metric_families(agent._metrics(r))}
     assert {s.labels["state"]: s.value for s in fams["mi355x_node_health"].samples} == {
         "healthy": 0, "degraded": 1, "unhealthy": 0, "unknown": 0}
+
+
+def test_image_carries_every_third_party_runtime_import():
+    """Every non-stdlib module the package imports is either installed in the image's runtime stage or is
+    optional by design (torch: bench / torchrun collectives; amdsmi: the Python probe fallback, shipped by
+    ROCm itself; prometheus_client / requests: tests and tools only)."""
+    import ast
+    import sys
+    pkg = os.path.join(REPO, "k8s_gpu_node_checker_amd")
+    mods = set()
+    for root, _, files in os.walk(pkg):
+        if "testing" in root.split(os.sep):
+            continue
+        for f in files:
+            if f.endswith(".py"):
+                tree = ast.parse(open(os.path.join(root, f)).read())
+                for n in ast.walk(tree):
+                    if isinstance(n, ast.Import):
+                        mods |= {a.name.split(".")[0] for a in n.names}
+                    elif isinstance(n, ast.ImportFrom) and n.level == 0 and n.module:
+                        mods.add(n.module.split(".")[0])
+    third = {m for m in mods if m not in sys.stdlib_module_names and m != "k8s_gpu_node_checker_amd"}
+    runtime = open(os.path.join(REPO, "deploy", "Dockerfile")).read().rsplit("\nFROM ", 1)[1]
+    installed = {"yaml": "python3-yaml" in runtime, "grpc": "grpcio" in runtime}
+    optional = {"torch", "amdsmi"}
+    assert third <= set(installed) | optional, third - set(installed) - optional
+    assert all(installed[m] for m in third & set(installed)), installed
