@@ -819,6 +819,51 @@ __global__ void __launch_bounds__(256) mfma_burn_kernel(const i32x8* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS test: every workgroup takes the CU's whole LDS (160 KiB on gfx950), writes four patterns over it
+// (address hash, its inverse, 0x55.., 0xAA..: every bit at 0 and at 1), and reads each back through a
+// different thread than the one that wrote it (half-buffer rotation), so a stuck or coupled bit in any
+// bank of any CU is counted -- the register-resident burn-in never touches LDS, and the GEMMs only
+// sample their outputs.  Errors are attributed to the physical CU (wave_slot()); `inject_block` >= 0
+// corrupts one word of that block's first pattern after the write (the test's own self-check).
+__device__ __forceinline__ uint32_t lds_pattern(uint32_t i, uint32_t seed, int p) {
+  switch (p & 3) {
+    case 0: return mix32(static_cast<uint64_t>(i) * 0x9E3779B97F4A7C15ULL + seed);
+    case 1: return ~mix32(static_cast<uint64_t>(i) * 0x9E3779B97F4A7C15ULL + seed);
+    case 2: return 0x55555555u;
+    default: return 0xAAAAAAAAu;
+  }
+}
+
+__global__ void __launch_bounds__(1024) lds_test_kernel(uint32_t words, uint32_t seed, int inject_block,
+                                                        unsigned long long* errors, unsigned long long* cu_map) {
+  extern __shared__ uint32_t lds_words[];
+  __shared__ unsigned int block_bad;
+  if (threadIdx.x == 0) block_bad = 0;
+  unsigned int bad = 0;
+  for (int p = 0; p < 4; ++p) {
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds_words[i] = lds_pattern(i, seed, p);
+    __syncthreads();
+    if (p == 0 && static_cast<int>(blockIdx.x) == inject_block && threadIdx.x == 0) lds_words[words / 3] ^= 0x10u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
+      const uint32_t j = i + words / 2 < words ? i + words / 2 : i + words / 2 - words;
+      bad += lds_words[j] != lds_pattern(j, seed, p);
+    }
+    __syncthreads();  // every read of pattern p done before pattern p+1 overwrites it
+  }
+  if (bad) atomicAdd(&block_bad, bad);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long* row = cu_map + 2 * wave_slot();
+    atomicAdd(row, 1ULL);
+    if (block_bad) {
+      atomicAdd(row + 1, static_cast<unsigned long long>(block_bad));
+      atomicAdd(errors, static_cast<unsigned long long>(block_bad));
+    }
+  }
+}
+
 // Device allocation owned by its device (frees with that device current), for the multi-GPU test.
 struct DevBuf {
   int device = -1;
@@ -1384,6 +1429,50 @@ int diag_mfma_burn_map(int device, int kind, int iters, int reps, double* tflops
   if (cu_map != nullptr) DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   const double flop = static_cast<double>(blocks) * 4 /*waves*/ * iters * 16 /*MFMA per iter*/ * 2.0 * 16 * 16 * K;
   *tflops = ms > 0.f ? flop * reps / (ms * 1e-3) / 1e12 : 0.0;
+  return 0;
+}
+
+// LDS test over `rounds` x CUs workgroups of the largest LDS allocation a workgroup may take.
+// cu_map: BURN_SLOTS x 2 (workgroups run, bad words) per physical CU slot; *lds_bytes = bytes per CU tested.
+int diag_lds_test(int device, int rounds, uint32_t seed, int inject_block, unsigned long long* errors,
+                  unsigned long long* cu_map, int* lds_bytes, double* ms) {
+  if (rounds < 1 || rounds > 64) {
+    g_err = "lds_test: 1 <= rounds <= 64";
+    return -2;
+  }
+  DIAG_CHECK(hipSetDevice(device));
+  int max_lds = 0;
+  DIAG_CHECK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device));
+  if (max_lds < 65536 || max_lds > (1 << 20)) {
+    g_err = "lds_test: unexpected LDS size " + std::to_string(max_lds);
+    return -2;
+  }
+  // the kernel's own 4-byte counter shares the allocation
+  const uint32_t dyn = static_cast<uint32_t>(max_lds) - 16u;
+  DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_test_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(dyn)));
+  const size_t map_bytes = static_cast<size_t>(BURN_SLOTS) * 2 * sizeof(unsigned long long);
+  DevBuf derr, dmap;
+  DIAG_CHECK(derr.alloc(device, sizeof(unsigned long long)));
+  DIAG_CHECK(dmap.alloc(device, map_bytes));
+  DIAG_CHECK(hipMemset(derr.ptr, 0, sizeof(unsigned long long)));
+  DIAG_CHECK(hipMemset(dmap.ptr, 0, map_bytes));
+  const int blocks = grid_for(device, rounds);
+  hipEvent_t e0, e1;
+  DIAG_CHECK(hipEventCreate(&e0));
+  DIAG_CHECK(hipEventCreate(&e1));
+  DIAG_CHECK(hipEventRecord(e0, nullptr));
+  hipLaunchKernelGGL(lds_test_kernel, dim3(blocks), dim3(1024), dyn, nullptr, dyn / 4u, seed, inject_block,
+                     static_cast<unsigned long long*>(derr.ptr), static_cast<unsigned long long*>(dmap.ptr));
+  DIAG_CHECK(hipGetLastError());
+  DIAG_CHECK(hipEventRecord(e1, nullptr));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  *ms = elapsed_ms(e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  DIAG_CHECK(hipMemcpy(errors, derr.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
+  *lds_bytes = static_cast<int>(dyn);
   return 0;
 }
 

@@ -161,6 +161,9 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                          ctypes.POINTER(ctypes.c_ulonglong)]
         L.diag_mfma_burn_slots.restype = ctypes.c_int
+        L.diag_lds_test.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong),
+                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]
         L.diag_host_link.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double)]
         L.diag_p2p_copy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
@@ -378,6 +381,29 @@ def mfma_burn(device: int = 0, kinds=MFMA_KINDS, iters: int = 2000, reps: int = 
     return res
 
 
+def lds_test(device: int = 0, rounds: int = 4, seed: int = 0x1D5, inject_block: int = -1) -> Dict[str, Any]:
+    """Every CU's whole LDS (160 KiB on gfx950) under four patterns, each word read back by another
+    thread than its writer; errors are located to their CU.  ``inject_block`` corrupts one word of that
+    workgroup (self-check of the detection path)."""
+    L = lib()
+    nslots = L.diag_mfma_burn_slots()
+    errs, nbytes, ms = ctypes.c_ulonglong(), ctypes.c_int(), ctypes.c_double()
+    m = (ctypes.c_ulonglong * (2 * nslots))()
+    t0 = time.perf_counter()
+    _check(L.diag_lds_test(device, rounds, seed, inject_block, ctypes.byref(errs), m, ctypes.byref(nbytes),
+                           ctypes.byref(ms)))
+    cus = [s for s in range(nslots) if m[2 * s]]
+    bad = [f"{slot_name(s)} ({m[2 * s + 1]} words)" for s in cus if m[2 * s + 1]]
+    res: Dict[str, Any] = {"pass": errs.value == 0, "errors": errs.value, "cus": len(cus),
+                           "bytes_per_cu": nbytes.value, "workgroups": sum(m[2 * s] for s in cus),
+                           "ms": round(ms.value, 3), "wall_s": round(time.perf_counter() - t0, 3), "detail": ""}
+    if bad:
+        res["bad_cus"] = bad
+    if errs.value:
+        res["detail"] = f"{errs.value} LDS words wrong on " + ", ".join(bad[:4]) + (" ..." if len(bad) > 4 else "")
+    return res
+
+
 def host_link(device: int = 0, mib: int = 256, iters: int = 5, scale: Scale = FULL) -> Dict[str, Any]:
     """Pinned host <-> device bandwidth over the GPU's PCIe link (GB/s each way).  A Gen4 or x8 link
     lands at about half the Gen5 x16 reference and fails."""
@@ -424,8 +450,8 @@ def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5) -
 
 LEVELS = {
     0: (),
-    1: ("gemm_quick", "gemm_fp8_quick", "hbm_quick", "mfma"),
-    2: ("gemm", "gemm_fp8", "hbm", "memtest", "mfma", "host_link"),
+    1: ("gemm_quick", "gemm_fp8_quick", "hbm_quick", "mfma", "lds"),
+    2: ("gemm", "gemm_fp8", "hbm", "memtest", "mfma", "lds", "host_link"),
 }
 
 
@@ -455,6 +481,8 @@ def _one(test: str, device: int, scale: Scale) -> Dict[str, Any]:
         return mfma_burn(device, scale=scale)
     if test == "host_link":
         return host_link(device, scale=scale)
+    if test == "lds":
+        return lds_test(device)
     raise ValueError(f"unknown diagnostic {test!r}")
 
 

@@ -38,7 +38,8 @@ class FakeDiagLib:
                  mfma_errors: Optional[Dict[Tuple[int, int], int]] = None, link: Optional[Tuple[float, float]] = None,
                  p2p_gbps: float = 48.0, slow_pairs: Optional[Dict[Tuple[int, int], float]] = None,
                  nopeer: Tuple[Tuple[int, int], ...] = (), rc: int = 0, err: bytes = b"boom", delay_s: float = 0.0,
-                 slow_xcd: Optional[Dict[int, float]] = None, bad_cu: Optional[Dict[Tuple[int, int], int]] = None):
+                 slow_xcd: Optional[Dict[int, float]] = None, bad_cu: Optional[Dict[Tuple[int, int], int]] = None,
+                 lds_bad: Optional[Dict[Tuple[int, int], int]] = None):
         from ..ops import diag
         self.ref = diag.REFERENCE_RATES
         self.kinds = diag.MFMA_KINDS
@@ -60,6 +61,7 @@ class FakeDiagLib:
         self.delay_s = delay_s
         self.slow_xcd = dict(slow_xcd or {})
         self.bad_cu = dict(bad_cu or {})
+        self.lds_bad = dict(lds_bad or {})
         self.calls: List[str] = []
         self.threads: Dict[int, set] = {}
         self.lock = threading.Lock()
@@ -153,6 +155,25 @@ class FakeDiagLib:
                     cu_map[3 * slot + 2] = int(waves * 40000 * self.slow_xcd.get(xcd, 1.0))
         if bad_slot is not None and nerr:
             cu_map[3 * bad_slot + 1] = nerr
+        return 0
+
+    def diag_lds_test(self, device, rounds, seed, inject_block, errors, cu_map, lds_bytes, ms):
+        """Every CU of the device runs `rounds` workgroups; ``lds_bad[(device, slot)]`` = bad words there."""
+        self._log(device, "lds")
+        if self.rc:
+            return self.rc
+        total = 0
+        for xcd in range(8 if self.cus >= 256 else max(1, self.cus // 32)):
+            for se in range(4):
+                for cu in range(8):
+                    slot = (xcd << 7) | (se << 5) | cu
+                    cu_map[2 * slot] = rounds
+                    bad = self.lds_bad.get((device, slot), 0) + (1 if inject_block >= 0 and slot == 0 else 0)
+                    cu_map[2 * slot + 1] = bad
+                    total += bad
+        _put(errors, ctypes.c_ulonglong, total)
+        _put(lds_bytes, ctypes.c_int, 163840 - 16)
+        _put(ms, ctypes.c_double, 0.2)
         return 0
 
     def diag_host_link(self, device, nbytes, iters, h2d, d2h):

@@ -181,3 +181,24 @@ def test_a_lagging_xcd_is_measured_twice(fake):
     lib.calls.clear()
     out = diag.run(1, 0)
     assert lib.calls.count("mfma") == 4 and not out["mfma"].get("retried")
+
+
+def test_lds_test_passes_on_every_cu_and_locates_bad_words(fake):
+    fake()
+    r = diag.lds_test(0)
+    assert r["pass"] and r["errors"] == 0 and r["cus"] == 256 and r["bytes_per_cu"] == 163824
+    assert r["workgroups"] == 256 * 4 and "bad_cus" not in r
+    slot = (5 << 7) | (2 << 5) | 7
+    fake(lds_bad={(0, slot): 3})
+    r = diag.lds_test(0)
+    assert not r["pass"] and r["bad_cus"] == ["xcd5/se2/cu7 (3 words)"]
+    assert r["detail"] == "3 LDS words wrong on xcd5/se2/cu7 (3 words)"
+    assert _verdict({"lds": r}).state == "unhealthy"
+
+
+def test_lds_runs_at_both_levels(fake):
+    lib = fake()
+    for level in (1, 2):
+        lib.calls.clear()
+        out = diag.run(level, 0)
+        assert out["lds"]["pass"] and lib.calls.count("lds") == 1

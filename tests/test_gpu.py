@@ -483,3 +483,16 @@ def test_host_link_bandwidth_and_pcie_fields(dev):
     assert r["h2d_gbps"] > 1.0 and r["d2h_gbps"] > 1.0
     g = amdsmi_probe.probe_native("n")["gpus"][0]
     assert g.get("pcie_max_width", 0) >= 1 and g.get("pcie_width", 0) >= 1, g
+
+
+def test_lds_test_every_cu_and_injected_fault(dev):
+    """Every CU's 160 KiB LDS holds all four patterns; one word flipped in one workgroup is counted
+    once and located to that workgroup's CU."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    info = diag.device_info(0)
+    r = diag.lds_test(0)
+    assert r["pass"] and r["errors"] == 0 and r["cus"] == info["cus"], r
+    assert r["bytes_per_cu"] >= 160 * 1024 - 64, r  # gfx950: the whole 160 KiB per workgroup
+    bad = diag.lds_test(0, rounds=1, inject_block=5)
+    assert not bad["pass"] and bad["errors"] == 1 and len(bad["bad_cus"]) == 1, bad
+    assert bad["bad_cus"][0].endswith("(1 words)") and bad["bad_cus"][0].startswith("xcd"), bad
