@@ -195,8 +195,8 @@ def firmware_mismatch(gpus: Sequence[Any]) -> List[str]:
 
     The GPUs of a node are flashed as one bundle; two versions of the same image on one node mean an
     update that stopped half-way, and GPUs that will behave differently under the same job.  One entry
-    per image: ``psp_sos: gpu0-6 00.45.00.2F, gpu7 00.45.00.00``; versions are stable, so the condition message stays
-    stable probe to probe."""
+    per image: ``psp_sos: gpu0-6 00.45.00.2F, gpu7 00.45.00.00``; versions are stable, so the condition
+    message stays stable probe to probe."""
     seen: Dict[str, Dict[Any, List[Any]]] = {}
     for g in gpus:
         if not isinstance(g, dict) or not isinstance(g.get("fw"), dict):
@@ -355,8 +355,9 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float
         w, sp = g.get("xgmi_width"), g.get("xgmi_speed_gbps")
         if (isinstance(w, int) and 0 < w < XGMI_LINK_WIDTH) or (isinstance(sp, int) and 0 < sp < XGMI_LINK_GBPS):
             # still "Up", but retrained narrower or slower: every collective through it runs at that rate
-            warn.append(f"gpu{idx}: xGMI links trained at x{w} {sp} Gb/s (MI355X: x{XGMI_LINK_WIDTH} "
-                        f"{XGMI_LINK_GBPS} Gb/s)")
+            trained = " ".join(x for x in (f"x{w}" if isinstance(w, int) else "",
+                                           f"{sp} Gb/s" if isinstance(sp, int) else "") if x)
+            warn.append(f"gpu{idx}: xGMI links trained at {trained} (MI355X: x{XGMI_LINK_WIDTH} {XGMI_LINK_GBPS} Gb/s)")
     xe = g.get("xgmi_error")
     if isinstance(xe, int) and xe > 0 and exp.xgmi_links > 0:
         # sticky since the driver loaded: the link PHYs retried or dropped traffic at least once

@@ -261,3 +261,11 @@ def test_partition_modes_differing_across_gpus_degrade():
     # a board partitioned as a whole is one mode everywhere: nothing to report
     cpx = rep(**{f"gpu{i}": {"compute_partition": "CPX", "cus": 32} for i in range(8)})
     assert H.partition_mismatch(cpx["gpus"]) == []
+
+
+def test_link_trained_down_with_only_one_field_reported():
+    g = dict(rep()["gpus"][0])
+    g.pop("xgmi_width")
+    g["xgmi_speed_gbps"] = 19
+    _, warns = H.evaluate_gpu(g, H.HealthExpectations())
+    assert warns == ["gpu0: xGMI links trained at 19 Gb/s (MI355X: x16 38 Gb/s)"]
