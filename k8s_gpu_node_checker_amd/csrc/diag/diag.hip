@@ -864,6 +864,58 @@ __global__ void __launch_bounds__(1024) lds_test_kernel(uint32_t words, uint32_t
   }
 }
 
+// ---------------------------------------------------------------------------
+// L2 test: each XCD has its own 4 MiB L2.  Every workgroup finds its XCD (XCC_ID) and streams that XCD's
+// private slice of the buffer (smaller than the L2) `passes` times, checking every word; after the
+// untimed first launch the slice is L2-resident, so the timed launch measures each XCD's L2 read
+// bandwidth.  Per-CU map as the burn-in's (waves, wrong words, wave time): an XCD whose L2 has lost
+// ways or runs slow falls behind the others; a corrupting path is located to the CU that read it.
+__global__ void __launch_bounds__(256) l2_read_kernel(const uint4* __restrict__ buf, uint32_t slice_vec, int passes,
+                                                      uint32_t seed, unsigned long long* errors,
+                                                      unsigned long long* cu_map) {
+  const long long t0 = wall_clock64();
+  const unsigned slot = wave_slot();
+  const uint32_t base = (slot >> 7) * slice_vec;  // this XCD's slice
+  unsigned int bad = 0;
+  auto check = [&](const uint4& v, uint32_t i) {
+    const uint32_t w = 4u * (base + i);
+    return (v.x != (w ^ seed)) + (v.y != ((w + 1u) ^ seed)) + (v.z != ((w + 2u) ^ seed)) + (v.w != ((w + 3u) ^ seed));
+  };
+  // L2 hits still take hundreds of ns: 8 independent 16-byte loads per lane are issued before any is
+  // consumed, so enough bytes are in flight per CU to reach the L2's bandwidth rather than its latency
+  constexpr uint32_t U = 8;
+  const uint32_t stride = blockDim.x, full = slice_vec - slice_vec % (U * stride);
+  for (int p = 0; p < passes; ++p) {
+    for (uint32_t i = threadIdx.x; i < full; i += U * stride) {
+      uint4 v[U];
+#pragma unroll
+      for (uint32_t k = 0; k < U; ++k) v[k] = buf[base + i + k * stride];
+#pragma unroll
+      for (uint32_t k = 0; k < U; ++k) bad += check(v[k], i + k * stride);
+    }
+    for (uint32_t i = full + threadIdx.x; i < slice_vec; i += stride) bad += check(buf[base + i], i);
+  }
+  unsigned long long wave_bad = bad;
+  for (int off = 32; off > 0; off >>= 1) wave_bad += __shfl_down(wave_bad, off, 64);
+  const unsigned long long dt = static_cast<unsigned long long>(wall_clock64() - t0);
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long* row = cu_map + 3 * slot;
+    atomicAdd(row, 1ULL);
+    if (wave_bad) {
+      atomicAdd(row + 1, wave_bad);
+      atomicAdd(errors, wave_bad);
+    }
+    atomicAdd(row + 2, dt);
+  }
+}
+
+__global__ void __launch_bounds__(256) l2_fill_kernel(uint4* buf, uint32_t n_vec, uint32_t seed) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += gridDim.x * blockDim.x) {
+    const uint32_t w = 4u * i;
+    buf[i] = uint4{w ^ seed, (w + 1u) ^ seed, (w + 2u) ^ seed, (w + 3u) ^ seed};
+  }
+}
+
 // Device allocation owned by its device (frees with that device current), for the multi-GPU test.
 struct DevBuf {
   int device = -1;
@@ -1473,6 +1525,55 @@ int diag_lds_test(int device, int rounds, uint32_t seed, int inject_block, unsig
   DIAG_CHECK(hipMemcpy(errors, derr.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   *lds_bytes = static_cast<int>(dyn);
+  return 0;
+}
+
+// L2 read bandwidth per XCD: 8 slices of `slice_bytes` (one per XCD id), `passes` reads of its slice by
+// every workgroup, `blocks_per_cu` workgroups of 4 waves per CU.  *tbs = aggregate bytes read / timed launch; cu_map as
+// diag_mfma_burn_map's (BURN_SLOTS x 3).
+int diag_l2_bandwidth(int device, size_t slice_bytes, int passes, int blocks_per_cu, uint32_t seed, double* tbs,
+                      unsigned long long* errors, unsigned long long* cu_map) {
+  if (slice_bytes < 4096 || slice_bytes > (64u << 20) || slice_bytes % 16 || passes < 1 || passes > 1024 ||
+      blocks_per_cu < 1 || blocks_per_cu > 8) {
+    g_err = "l2_bandwidth: 4 KiB <= slice_bytes <= 64 MiB (multiple of 16), 1 <= passes <= 1024, 1..8 blocks/CU";
+    return -2;
+  }
+  DIAG_CHECK(hipSetDevice(device));
+  const uint32_t slice_vec = static_cast<uint32_t>(slice_bytes / 16);
+  const uint32_t n_vec = 8u * slice_vec;  // XCC_ID is 0..7
+  const size_t map_bytes = static_cast<size_t>(BURN_SLOTS) * 3 * sizeof(unsigned long long);
+  DevBuf dbuf, derr, dmap;
+  DIAG_CHECK(dbuf.alloc(device, static_cast<size_t>(n_vec) * 16));
+  DIAG_CHECK(derr.alloc(device, sizeof(unsigned long long)));
+  DIAG_CHECK(dmap.alloc(device, map_bytes));
+  hipLaunchKernelGGL(l2_fill_kernel, dim3(1024), dim3(256), 0, nullptr, static_cast<uint4*>(dbuf.ptr), n_vec, seed);
+  DIAG_CHECK(hipGetLastError());
+  const int blocks = grid_for(device, blocks_per_cu);
+  auto launch = [&]() {
+    hipLaunchKernelGGL(l2_read_kernel, dim3(blocks), dim3(256), 0, nullptr, static_cast<const uint4*>(dbuf.ptr),
+                       slice_vec, passes, seed, static_cast<unsigned long long*>(derr.ptr),
+                       static_cast<unsigned long long*>(dmap.ptr));
+  };
+  launch();  // untimed: brings every slice into its XCD's L2
+  DIAG_CHECK(hipGetLastError());
+  DIAG_CHECK(hipDeviceSynchronize());
+  DIAG_CHECK(hipMemset(derr.ptr, 0, sizeof(unsigned long long)));
+  DIAG_CHECK(hipMemset(dmap.ptr, 0, map_bytes));
+  hipEvent_t e0, e1;
+  DIAG_CHECK(hipEventCreate(&e0));
+  DIAG_CHECK(hipEventCreate(&e1));
+  DIAG_CHECK(hipEventRecord(e0, nullptr));
+  launch();
+  DIAG_CHECK(hipEventRecord(e1, nullptr));
+  DIAG_CHECK(hipEventSynchronize(e1));
+  DIAG_CHECK(hipGetLastError());
+  const float ms = elapsed_ms(e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  DIAG_CHECK(hipMemcpy(errors, derr.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
+  const double bytes = static_cast<double>(blocks) * passes * static_cast<double>(slice_bytes);
+  *tbs = ms > 0.f ? bytes / (ms * 1e-3) / 1e12 : 0.0;
   return 0;
 }
 

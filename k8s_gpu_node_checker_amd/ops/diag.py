@@ -54,6 +54,8 @@ REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
     "hbm": {"copy_tbs": 6.49, "read_tbs": 6.96},   # 16-byte copy (read + write bytes counted) / read, TB/s
     "mfma": {"bf16": 1901.0, "fp8": 1940.0, "mxfp8": 4326.0, "mxfp4": 7610.0},  # register-resident burn-in
     "host_link": {"h2d_gbps": 57.0, "d2h_gbps": 56.8},  # pinned copies over PCIe Gen5 x16
+    "l2": {"read_tbs": 30.5},                      # per-XCD L2 reads, 2 MiB slices, 8 WG/CU: 31.6-31.9 measured
+                                                   # (profiles/l2_explore_mi355x.json; 34.5 TB/s is the L2's own figure)
 }
 GEMM_MAX_REL_ERR = 2e-3       # vs fp32 reference; bf16 inputs are exact in fp32, so ~1e-5 is typical
 GEMM_FP8_MAX_ERR = 4e-5       # |C - ref| / sum|a*b|: the MX MFMA's own accumulation error is <= 1.6e-5
@@ -161,6 +163,9 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                          ctypes.POINTER(ctypes.c_ulonglong)]
         L.diag_mfma_burn_slots.restype = ctypes.c_int
+        L.diag_l2_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
+                                        ctypes.POINTER(ctypes.c_ulonglong)]
         L.diag_lds_test.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong),
                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]
@@ -404,6 +409,32 @@ def lds_test(device: int = 0, rounds: int = 4, seed: int = 0x1D5, inject_block: 
     return res
 
 
+def l2_bandwidth(device: int = 0, slice_kib: int = 2048, passes: int = 32, blocks_per_cu: int = 8,
+                 seed: int = 0x12C3, scale: Scale = FULL) -> Dict[str, Any]:
+    """Each XCD's 4 MiB L2, read by that XCD's own CUs (a ``slice_kib`` slice per XCD, every word checked):
+    aggregate TB/s against the reference, per-XCD wave time against the median XCD (degraded beyond
+    ``XCD_SLOW_RATIO``: an L2 that lost ways or a slow XCD), wrong words located to the CU."""
+    L = lib()
+    nslots = L.diag_mfma_burn_slots()
+    tbs, errs = ctypes.c_double(), ctypes.c_ulonglong()
+    m = (ctypes.c_ulonglong * (3 * nslots))()
+    t0 = time.perf_counter()
+    _check(L.diag_l2_bandwidth(device, slice_kib << 10, passes, blocks_per_cu, seed, ctypes.byref(tbs),
+                               ctypes.byref(errs), m))
+    where = cu_map_summary({"l2": list(m)})
+    wrong = f"{errs.value} wrong words on " + ", ".join(where.get("bad_cus", [])[:4]) if errs.value else ""
+    exp = {"read_tbs": REFERENCE_RATES["l2"]["read_tbs"] * scale.compute}
+    res = _rated({"read_tbs": round(tbs.value, 2), "errors": errs.value, "map": where,
+                  "wall_s": round(time.perf_counter() - t0, 3)}, {"read_tbs": tbs.value}, exp, "TB/s",
+                 not errs.value, wrong)
+    rel = where.get("slowest_rel")
+    if res["pass"] and isinstance(rel, float) and rel > XCD_SLOW_RATIO:
+        res["degraded"] = True
+        note = f"xcd{where['slowest_xcd']} L2 reads take {rel:.2f}x the median XCD's time"
+        res["detail"] = "; ".join(x for x in (res["detail"], note) if x)
+    return res
+
+
 def host_link(device: int = 0, mib: int = 256, iters: int = 5, scale: Scale = FULL) -> Dict[str, Any]:
     """Pinned host <-> device bandwidth over the GPU's PCIe link (GB/s each way).  A Gen4 or x8 link
     lands at about half the Gen5 x16 reference and fails."""
@@ -450,8 +481,8 @@ def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5) -
 
 LEVELS = {
     0: (),
-    1: ("gemm_quick", "gemm_fp8_quick", "hbm_quick", "mfma", "lds"),
-    2: ("gemm", "gemm_fp8", "hbm", "memtest", "mfma", "lds", "host_link"),
+    1: ("gemm_quick", "gemm_fp8_quick", "hbm_quick", "mfma", "lds", "l2"),
+    2: ("gemm", "gemm_fp8", "hbm", "memtest", "mfma", "lds", "l2", "host_link"),
 }
 
 
@@ -483,6 +514,8 @@ def _one(test: str, device: int, scale: Scale) -> Dict[str, Any]:
         return host_link(device, scale=scale)
     if test == "lds":
         return lds_test(device)
+    if test == "l2":
+        return l2_bandwidth(device, scale=scale)
     raise ValueError(f"unknown diagnostic {test!r}")
 
 

@@ -39,7 +39,8 @@ class FakeDiagLib:
                  p2p_gbps: float = 48.0, slow_pairs: Optional[Dict[Tuple[int, int], float]] = None,
                  nopeer: Tuple[Tuple[int, int], ...] = (), rc: int = 0, err: bytes = b"boom", delay_s: float = 0.0,
                  slow_xcd: Optional[Dict[int, float]] = None, bad_cu: Optional[Dict[Tuple[int, int], int]] = None,
-                 lds_bad: Optional[Dict[Tuple[int, int], int]] = None):
+                 lds_bad: Optional[Dict[Tuple[int, int], int]] = None,
+                 l2_bad: Optional[Dict[Tuple[int, int], int]] = None):
         from ..ops import diag
         self.ref = diag.REFERENCE_RATES
         self.kinds = diag.MFMA_KINDS
@@ -62,6 +63,7 @@ class FakeDiagLib:
         self.slow_xcd = dict(slow_xcd or {})
         self.bad_cu = dict(bad_cu or {})
         self.lds_bad = dict(lds_bad or {})
+        self.l2_bad = dict(l2_bad or {})
         self.calls: List[str] = []
         self.threads: Dict[int, set] = {}
         self.lock = threading.Lock()
@@ -155,6 +157,27 @@ class FakeDiagLib:
                     cu_map[3 * slot + 2] = int(waves * 40000 * self.slow_xcd.get(xcd, 1.0))
         if bad_slot is not None and nerr:
             cu_map[3 * bad_slot + 1] = nerr
+        return 0
+
+    def diag_l2_bandwidth(self, device, slice_bytes, passes, blocks_per_cu, seed, tbs, errors, cu_map):
+        """Aggregate rate = rate x reference; per-CU table shaped like the burn-in's (``slow_xcd`` applies,
+        ``l2_bad[(device, slot)]`` = wrong words read there)."""
+        self._log(device, "l2")
+        if self.rc:
+            return self.rc
+        _put(tbs, ctypes.c_double, self._rate(device) * self.ref["l2"]["read_tbs"])
+        total = 0
+        for xcd in range(8 if self.cus >= 256 else max(1, self.cus // 32)):
+            for se in range(4):
+                for cu in range(8):
+                    slot = (xcd << 7) | (se << 5) | cu
+                    waves = 4 * blocks_per_cu
+                    cu_map[3 * slot] = waves
+                    cu_map[3 * slot + 2] = int(waves * 90000 * self.slow_xcd.get(xcd, 1.0))
+                    bad = self.l2_bad.get((device, slot), 0)
+                    cu_map[3 * slot + 1] = bad
+                    total += bad
+        _put(errors, ctypes.c_ulonglong, total)
         return 0
 
     def diag_lds_test(self, device, rounds, seed, inject_block, errors, cu_map, lds_bytes, ms):

@@ -202,3 +202,22 @@ def test_lds_runs_at_both_levels(fake):
         lib.calls.clear()
         out = diag.run(level, 0)
         assert out["lds"]["pass"] and lib.calls.count("lds") == 1
+
+
+def test_l2_bandwidth_rate_xcd_lag_and_located_errors(fake):
+    fake()
+    r = diag.l2_bandwidth(0)
+    assert r["pass"] and not r["degraded"] and r["map"]["cus"] == 256 and len(r["map"]["xcds"]) == 8
+    fake(slow_xcd={3: 1.25})
+    r = diag.l2_bandwidth(0)
+    assert r["pass"] and r["degraded"] and r["detail"] == "xcd3 L2 reads take 1.25x the median XCD's time"
+    fake(l2_bad={(0, (1 << 7) | 4): 2})
+    r = diag.l2_bandwidth(0)
+    assert not r["pass"] and r["detail"] == "2 wrong words on xcd1/se0/cu4 (l2 2)"
+    fake(rate=0.5)
+    r = diag.l2_bandwidth(0)
+    assert not r["pass"] and r["detail"].startswith("read_tbs 15.2 TB/s = 50% of 30.5")
+    # a CPX partition (one XCD): its share of the rate, no XCD comparison
+    fake(cus=32, rate=1 / 8)
+    r = diag.l2_bandwidth(0, scale=diag.Scale(0.125, 0.125))
+    assert r["pass"] and not r["degraded"] and "slowest_xcd" not in r["map"]

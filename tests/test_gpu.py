@@ -496,3 +496,14 @@ def test_lds_test_every_cu_and_injected_fault(dev):
     bad = diag.lds_test(0, rounds=1, inject_block=5)
     assert not bad["pass"] and bad["errors"] == 1 and len(bad["bad_cus"]) == 1, bad
     assert bad["bad_cus"][0].endswith("(1 words)") and bad["bad_cus"][0].startswith("xcd"), bad
+
+
+def test_l2_bandwidth_per_xcd(dev):
+    """Each XCD reads its own L2-resident slice: aggregate rate above the floor, every CU and XCD seen,
+    no XCD lagging, every word intact."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.l2_bandwidth(0)
+    info = diag.device_info(0)
+    assert r["pass"] and r["errors"] == 0 and r["map"]["cus"] == info["cus"], r
+    if info["cus"] == 256:
+        assert len(r["map"]["xcds"]) == 8 and r["read_tbs"] > 25.0, r
