@@ -64,8 +64,13 @@ MFMA_KINDS = ("bf16", "fp8", "mxfp8", "mxfp4")
 P2P_MIN_FRACTION_OF_MEDIAN = 0.5  # a GPU pair slower than half the node's median pair: suspect link
 # burn-in waves of one XCD taking this much longer than the median XCD's: that XCD's clock domain (or a
 # CU in it) lags -- degraded, not failed (the rate floors above judge the chip as a whole).  A healthy
-# MI355X spreads 1.004-1.016 (20 burn-ins, profiles/mfma_xcd_map_mi355x.json), so 1.15 is ~10x its noise.
+# MI355X spreads 1.003-1.024 (20 burn-ins, profiles/mfma_xcd_map_mi355x.json), so 1.15 is ~6x its noise.
 XCD_SLOW_RATIO = 1.15
+# the same for one CU against the median CU of its own XCD (so an XCD-wide lag names the XCD, not its
+# CUs).  Healthy MI355X (profiles/mfma_xcd_map_mi355x.json, every CU dealt the same workgroup count): the
+# burn-in's register-resident waves take the same time to the 10 ns tick on every CU of an XCD (1.000 in
+# 20 runs: one clock per XCD, no memory traffic); the L2 test's 1.016-1.022
+CU_SLOW_RATIO = 1.15
 
 
 class Scale:
@@ -316,11 +321,14 @@ def cu_map_summary(maps: Dict[str, Any]) -> Dict[str, Any]:
     * ``slowest_xcd`` / ``slowest_rel``: the XCD furthest behind (each XCD is its own clock domain).
     """
     per_kind_rel: Dict[int, List[float]] = {}
+    per_cu_rel: Dict[int, List[float]] = {}
+    cu_waves: Dict[int, List[int]] = {}
     cus: Dict[int, set] = {}
     bad: Dict[int, Dict[str, int]] = {}
     for kind, flat in maps.items():
         waves: Dict[int, int] = {}
         ticks: Dict[int, int] = {}
+        cu_mean: Dict[int, float] = {}
         for slot in range(len(flat) // 3):
             w, e, t = flat[3 * slot], flat[3 * slot + 1], flat[3 * slot + 2]
             if not w:
@@ -329,6 +337,8 @@ def cu_map_summary(maps: Dict[str, Any]) -> Dict[str, Any]:
             cus.setdefault(x, set()).add(slot)
             waves[x] = waves.get(x, 0) + w
             ticks[x] = ticks.get(x, 0) + t
+            cu_mean[slot] = t / w
+            cu_waves.setdefault(slot, []).append(int(w))
             if e:
                 bad.setdefault(slot, {})[kind] = int(e)
         mean = {x: ticks[x] / waves[x] for x in waves if waves[x]}
@@ -336,6 +346,15 @@ def cu_map_summary(maps: Dict[str, Any]) -> Dict[str, Any]:
             med = sorted(mean.values())[len(mean) // 2]
             for x, m in mean.items():
                 per_kind_rel.setdefault(x, []).append(m / med if med > 0 else 1.0)
+        # each CU against the median CU of its own XCD, so a whole XCD running behind (reported above)
+        # does not also name its CUs
+        by_xcd: Dict[int, List[float]] = {}
+        for slot, m in cu_mean.items():
+            by_xcd.setdefault(slot >> 7, []).append(m)
+        xmed = {x: sorted(v)[len(v) // 2] for x, v in by_xcd.items()}
+        for slot, m in cu_mean.items():
+            med = xmed[slot >> 7]
+            per_cu_rel.setdefault(slot, []).append(m / med if med > 0 else 1.0)
     xcds = {}
     for x in sorted(cus):
         rels = sorted(per_kind_rel.get(x, [1.0]))
@@ -344,6 +363,14 @@ def cu_map_summary(maps: Dict[str, Any]) -> Dict[str, Any]:
     if len(xcds) >= 2:
         slow = max(xcds, key=lambda k: xcds[k]["rel_time"])
         out["slowest_xcd"], out["slowest_rel"] = int(slow), xcds[slow]["rel_time"]
+    if per_cu_rel:
+        # the CU furthest behind its XCD's median CU (median over the kinds), and how evenly the hardware
+        # dealt the workgroups out (waves per CU per kind, min..max)
+        rel_cu = {slot: sorted(r)[len(r) // 2] for slot, r in per_cu_rel.items()}
+        worst = max(rel_cu, key=rel_cu.get)
+        out["slowest_cu"], out["slowest_cu_rel"] = slot_name(worst), round(rel_cu[worst], 3)
+        ws = [w for lst in cu_waves.values() for w in lst]
+        out["waves_per_cu"] = [min(ws), max(ws)]
     if bad:
         out["bad_cus"] = [f"{slot_name(s)} (" + ", ".join(f"{k} {n}" for k, n in kinds.items()) + ")"
                           for s, kinds in sorted(bad.items())]
@@ -378,11 +405,28 @@ def mfma_burn(device: int = 0, kinds=MFMA_KINDS, iters: int = 2000, reps: int = 
     exp = {k: REFERENCE_RATES["mfma"][k] * scale.compute for k in kinds}
     res = _rated({"kinds": rows, "map": where, "wall_s": round(time.perf_counter() - t0, 3)}, rates, exp,
                  "TFLOP/s", not wrong, "; ".join(wrong))
+    return _lag_verdict(res, where, "waves")
+
+
+def _lag_notes(where: Dict[str, Any], what: str) -> List[str]:
+    """An XCD, or a single CU, falling behind the rest of the chip on identical work (cu_map_summary).
+    The per-CU comparison needs an even deal of workgroups (measured: every CU gets the same count);
+    with an uneven one the co-resident waves differ and the times are not comparable."""
+    notes = []
     rel = where.get("slowest_rel")
-    if res["pass"] and isinstance(rel, float) and rel > XCD_SLOW_RATIO:
+    if isinstance(rel, float) and rel > XCD_SLOW_RATIO:
+        notes.append(f"xcd{where['slowest_xcd']} {what} take {rel:.2f}x the median XCD's time")
+    crel, wpc = where.get("slowest_cu_rel"), where.get("waves_per_cu")
+    if isinstance(crel, float) and crel > CU_SLOW_RATIO and isinstance(wpc, list) and wpc[0] == wpc[-1]:
+        notes.append(f"{where['slowest_cu']} {what} take {crel:.2f}x its XCD's median CU's time")
+    return notes
+
+
+def _lag_verdict(res: Dict[str, Any], where: Dict[str, Any], what: str) -> Dict[str, Any]:
+    notes = _lag_notes(where, what)
+    if res["pass"] and notes:
         res["degraded"] = True
-        note = f"xcd{where['slowest_xcd']} waves take {rel:.2f}x the median XCD's time"
-        res["detail"] = "; ".join(x for x in (res["detail"], note) if x)
+        res["detail"] = "; ".join(x for x in [res["detail"]] + notes if x)
     return res
 
 
@@ -427,12 +471,7 @@ def l2_bandwidth(device: int = 0, slice_kib: int = 2048, passes: int = 32, block
     res = _rated({"read_tbs": round(tbs.value, 2), "errors": errs.value, "map": where,
                   "wall_s": round(time.perf_counter() - t0, 3)}, {"read_tbs": tbs.value}, exp, "TB/s",
                  not errs.value, wrong)
-    rel = where.get("slowest_rel")
-    if res["pass"] and isinstance(rel, float) and rel > XCD_SLOW_RATIO:
-        res["degraded"] = True
-        note = f"xcd{where['slowest_xcd']} L2 reads take {rel:.2f}x the median XCD's time"
-        res["detail"] = "; ".join(x for x in (res["detail"], note) if x)
-    return res
+    return _lag_verdict(res, where, "L2 reads")
 
 
 def host_link(device: int = 0, mib: int = 256, iters: int = 5, scale: Scale = FULL) -> Dict[str, Any]:
@@ -522,7 +561,7 @@ def _one(test: str, device: int, scale: Scale) -> Dict[str, Any]:
 def _slow_only(res: Dict[str, Any]) -> bool:
     """Below the degraded line on rate alone, or one XCD lagging the others (numerics fine): worth a
     second measurement."""
-    lagging = ((res.get("map") or {}).get("slowest_rel") or 0.0) > XCD_SLOW_RATIO
+    lagging = bool(_lag_notes(res.get("map") or {}, ""))
     return (res.get("degraded") or not res.get("pass")) \
         and (res.get("fraction", 1.0) < DEGRADED_FRACTION or lagging) \
         and "wrong results" not in res.get("detail", "") and "err " not in res.get("detail", "")
@@ -530,8 +569,9 @@ def _slow_only(res: Dict[str, Any]) -> bool:
 
 def _goodness(res: Dict[str, Any]) -> tuple:
     """Order two measurements of one test: passing, then not degraded, then the better rate."""
+    where = res.get("map") or {}
     return (bool(res.get("pass")), not res.get("degraded"), res.get("fraction", 0.0),
-            -((res.get("map") or {}).get("slowest_rel") or 0.0))
+            -max(where.get("slowest_rel") or 0.0, where.get("slowest_cu_rel") or 0.0))
 
 
 def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,

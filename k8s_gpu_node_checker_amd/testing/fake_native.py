@@ -40,7 +40,7 @@ class FakeDiagLib:
                  nopeer: Tuple[Tuple[int, int], ...] = (), rc: int = 0, err: bytes = b"boom", delay_s: float = 0.0,
                  slow_xcd: Optional[Dict[int, float]] = None, bad_cu: Optional[Dict[Tuple[int, int], int]] = None,
                  lds_bad: Optional[Dict[Tuple[int, int], int]] = None,
-                 l2_bad: Optional[Dict[Tuple[int, int], int]] = None):
+                 l2_bad: Optional[Dict[Tuple[int, int], int]] = None, slow_cu: Optional[Dict[int, float]] = None):
         from ..ops import diag
         self.ref = diag.REFERENCE_RATES
         self.kinds = diag.MFMA_KINDS
@@ -64,6 +64,7 @@ class FakeDiagLib:
         self.bad_cu = dict(bad_cu or {})
         self.lds_bad = dict(lds_bad or {})
         self.l2_bad = dict(l2_bad or {})
+        self.slow_cu = dict(slow_cu or {})
         self.calls: List[str] = []
         self.threads: Dict[int, set] = {}
         self.lock = threading.Lock()
@@ -154,7 +155,7 @@ class FakeDiagLib:
                     slot = (xcd << 7) | (se << 5) | cu
                     waves = 8 * (reps + 1)
                     cu_map[3 * slot] = waves
-                    cu_map[3 * slot + 2] = int(waves * 40000 * self.slow_xcd.get(xcd, 1.0))
+                    cu_map[3 * slot + 2] = int(waves * 40000 * self.slow_xcd.get(xcd, 1.0) * self.slow_cu.get(slot, 1.0))
         if bad_slot is not None and nerr:
             cu_map[3 * bad_slot + 1] = nerr
         return 0

@@ -221,3 +221,27 @@ def test_l2_bandwidth_rate_xcd_lag_and_located_errors(fake):
     fake(cus=32, rate=1 / 8)
     r = diag.l2_bandwidth(0, scale=diag.Scale(0.125, 0.125))
     assert r["pass"] and not r["degraded"] and "slowest_xcd" not in r["map"]
+
+
+def test_a_single_lagging_cu_degrades_the_burn_in(fake):
+    slot = (6 << 7) | (1 << 5) | 3
+    fake(slow_cu={slot: 1.4})
+    r = diag.mfma_burn(0)
+    m = r["map"]
+    assert m["slowest_cu"] == "xcd6/se1/cu3" and m["slowest_cu_rel"] == 1.4 and m["waves_per_cu"] == [48, 48]
+    # one CU of 32 barely moves its XCD's mean: only the per-CU comparison sees it
+    assert m["slowest_rel"] < diag.XCD_SLOW_RATIO
+    assert r["pass"] and r["degraded"] and r["detail"] == "xcd6/se1/cu3 waves take 1.40x its XCD's median CU's time"
+    fake(slow_cu={slot: 1.05})
+    assert not diag.mfma_burn(0)["degraded"]
+
+
+def test_cu_lag_is_not_judged_on_an_uneven_deal():
+    m = diag.cu_map_summary({"k": [0] * 3 * 1024})
+    assert m["cus"] == 0
+    flat = [0] * 3 * 1024
+    for slot, (w, t) in {0: (8, 8000), 1: (8, 8100), 2: (16, 24000)}.items():  # slot 2 got twice the waves
+        flat[3 * slot], flat[3 * slot + 2] = w, t
+    where = diag.cu_map_summary({"k": flat})
+    assert where["waves_per_cu"] == [8, 16] and where["slowest_cu_rel"] > 1.4
+    assert diag._lag_notes(where, "waves") == []
