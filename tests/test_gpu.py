@@ -395,6 +395,8 @@ def test_mfma_burn_every_precision(dev):
     if info["cus"] == 256:
         assert sorted(m["xcds"]) == [str(x) for x in range(8)] and all(x["cus"] == 32 for x in m["xcds"].values()), m
     assert m.get("slowest_rel", 1.0) <= diag.XCD_SLOW_RATIO, m
+    # the hardware deals every CU the same number of workgroups, and no CU lags its XCD
+    assert m["waves_per_cu"][0] == m["waves_per_cu"][1] and m["slowest_cu_rel"] <= diag.CU_SLOW_RATIO, m
 
 
 def test_mfma_burn_rejects_inexact_iteration_counts():
