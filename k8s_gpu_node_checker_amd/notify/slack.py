@@ -36,7 +36,7 @@ if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a
     from typing import Any, Callable, Optional, TextIO
 
 from ..utils.backoff import Backoff
-from ..utils.http import HTTPError, request
+from ..utils.http import HTTPError, env_proxy, request
 
 ICON = ":robot_face:"
 DEFAULT_USERNAME = "k8s-gpu-checker"
@@ -60,6 +60,18 @@ def slack_payload(message: str, username: str) -> bytes:
     return json.dumps({"text": message, "username": username, "icon_emoji": ICON}).encode("ascii")
 
 
+def _env_ssl_context():
+    """``REQUESTS_CA_BUNDLE`` / ``CURL_CA_BUNDLE`` (a file or an OpenSSL hashed directory), as requests
+    verifies with; None keeps the default trust store."""
+    bundle = os.environ.get("REQUESTS_CA_BUNDLE") or os.environ.get("CURL_CA_BUNDLE")
+    if not bundle:
+        return None
+    import ssl
+    if os.path.isdir(bundle):
+        return ssl.create_default_context(capath=bundle)
+    return ssl.create_default_context(cafile=bundle)
+
+
 def send_slack_message(webhook_url: Optional[str], message: str, username: str = DEFAULT_USERNAME,
                        max_retries: int = 3, retry_delay: float = 30, *, policy: str = "backoff",
                        timeout: float = 10.0, err: Optional[TextIO] = None,
@@ -74,9 +86,14 @@ def send_slack_message(webhook_url: Optional[str], message: str, username: str =
                "User-Agent": "k8s-gpu-node-checker-amd/0.1"}
     bo = backoff or Backoff(base=1.0, cap=max(0.0, float(retry_delay)), jitter=0.5)
     attempts = max_retries + 1
+    # what requests.post does by default (trust_env): the environment's proxy and CA bundle
+    proxy = env_proxy(webhook_url)
+    if ssl_context is None and webhook_url.startswith("https"):
+        ssl_context = _env_ssl_context()
     for attempt in range(attempts):
         try:
-            resp = request(webhook_url, "POST", headers, body, timeout=timeout, ssl_context=ssl_context)
+            resp = request(webhook_url, "POST", headers, body, timeout=timeout, ssl_context=ssl_context,
+                           proxy_url=proxy)
         except HTTPError as e:
             if e.retryable_reset:
                 if attempt < max_retries:

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import _socket  # the C module: socket.py's enum setup costs ~2 ms of a 1-node cold start
 import errno
+import os
 TYPE_CHECKING = False
 if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
     from typing import Dict, List, Optional, Tuple
@@ -169,8 +170,17 @@ class Connection:
         self.sock = sock
         self._buf = bytearray()
 
+    def _proxy_auth(self) -> str:
+        """``Proxy-Authorization: Basic ...`` line for a proxy URL with credentials (requests does the same)."""
+        if self.proxy is None or self.proxy.username is None:
+            return ""
+        import base64
+        cred = f"{self.proxy.username}:{self.proxy.password or ''}".encode("latin-1")
+        return f"Proxy-Authorization: Basic {base64.b64encode(cred).decode('ascii')}\r\n"
+
     def _tunnel(self, sock: "socket.socket") -> None:
-        req = (f"CONNECT {self.host}:{self.port} HTTP/1.1\r\nHost: {self.host}:{self.port}\r\n\r\n").encode()
+        req = (f"CONNECT {self.host}:{self.port} HTTP/1.1\r\nHost: {self.host}:{self.port}\r\n"
+               f"{self._proxy_auth()}\r\n").encode("latin-1")
         sock.sendall(req)
         data = b""
         while b"\r\n\r\n" not in data:
@@ -237,6 +247,8 @@ class Connection:
         if self.proxy and self.scheme == "http":
             req_target = f"http://{self.host_header}{req_target}"
         lines = [f"{method} {req_target} HTTP/1.1", f"Host: {self.host_header}"]
+        if self.proxy and self.scheme == "http" and self.proxy.username is not None:
+            lines.append(self._proxy_auth().rstrip("\r\n"))
         for k, v in (headers or {}).items():
             lines.append(f"{k}: {v}")
         if body is not None:
@@ -530,9 +542,81 @@ class LineStream:
         self.conn.close()
 
 
+def env_proxy(url: str, environ: Optional[Dict[str, str]] = None) -> Optional[str]:
+    """The proxy ``requests`` would use for ``url`` from the environment (``trust_env``; the reference's
+    Slack POST goes through it, ``check-gpu-node.py:73``):
+
+    * ``<scheme>_proxy`` then ``all_proxy``, the lower-case spelling winning over the upper-case one
+      (``urllib.request.getproxies``); ``HTTP_PROXY`` is ignored under CGI (``REQUEST_METHOD`` set),
+      ``http_proxy`` is not;
+    * ``no_proxy`` bypasses: ``*``; for an IPv4 host an exact address or a CIDR block; otherwise a
+      suffix of the host or of ``host:port`` (so ``example.com`` and ``.example.com`` both match
+      ``hooks.example.com``);
+    * a proxy given without a scheme is ``http://``.
+    """
+    env = os.environ if environ is None else environ
+    parts = urlsplit(url)
+    host = parts.hostname
+    if not host:
+        return None
+    # urllib.request.getproxies_environment: every *_proxy (any case), then the "_proxy"-suffixed
+    # spellings again, which win (an empty one removes the entry)
+    proxies: Dict[str, str] = {}
+    for k, v in env.items():
+        if v and k.lower().endswith("_proxy"):
+            proxies[k[:-6].lower()] = v
+    if "REQUEST_METHOD" in env:  # CGI: HTTP_PROXY may come from a client header (CVE-2016-1000110)
+        proxies.pop("http", None)
+    for k, v in env.items():
+        if k.endswith("_proxy"):
+            if v:
+                proxies[k[:-6].lower()] = v
+            else:
+                proxies.pop(k[:-6].lower(), None)
+    no_proxy = env.get("no_proxy") or env.get("NO_PROXY")  # requests' own lookup
+    if no_proxy:
+        entries = [h for h in no_proxy.replace(" ", "").split(",") if h]
+        if "*" in entries:
+            return None
+        if _is_ipv4(host):
+            for e in entries:
+                if ("/" in e and _in_cidr(host, e)) or host == e:
+                    return None
+        else:
+            host_port = f"{host}:{parts.port}" if parts.port else host
+            for e in entries:
+                if host.endswith(e) or host_port.endswith(e):
+                    return None
+                if e.lstrip(".") and (host == e.lstrip(".") or host.endswith("." + e.lstrip("."))):
+                    return None
+    proxy = proxies.get(parts.scheme) or proxies.get("all")
+    if not proxy:
+        return None
+    return proxy if "://" in proxy else "http://" + proxy
+
+
+def _is_ipv4(host: str) -> bool:
+    ps = host.split(".")
+    return len(ps) == 4 and all(p.isdigit() and int(p) < 256 for p in ps)
+
+
+def _in_cidr(ip: str, cidr: str) -> bool:
+    net, _, bits = cidr.partition("/")
+    if not _is_ipv4(net) or not bits.isdigit() or not 0 <= int(bits) <= 32:
+        return False
+
+    def num(a: str) -> int:
+        x = 0
+        for p in a.split("."):
+            x = (x << 8) | int(p)
+        return x
+    mask = (0xFFFFFFFF << (32 - int(bits))) & 0xFFFFFFFF
+    return (num(ip) & mask) == (num(net) & mask)
+
+
 def request(url: str, method: str = "GET", headers: Optional[Dict[str, str]] = None, body: Optional[bytes] = None,
-            timeout: float = 30.0, ssl_context=None) -> Response:
-    """One-shot request on a fresh connection."""
+            timeout: float = 30.0, ssl_context=None, proxy_url: Optional[str] = None) -> Response:
+    """One-shot request on a fresh connection (through ``proxy_url`` when given)."""
     parts = urlsplit(url)
     if parts.scheme not in ("http", "https"):
         if not parts.scheme:
@@ -544,7 +628,11 @@ def request(url: str, method: str = "GET", headers: Optional[Dict[str, str]] = N
     path = parts.path or "/"
     if parts.query:
         path += "?" + parts.query
-    conn = Connection(base, timeout=timeout, ssl_context=ssl_context)
+    if proxy_url and proxy_url.split("://", 1)[0].lower() not in ("http", "https"):
+        # requests' InvalidSchema for socks*:// without PySocks (and any other scheme it has no adapter for)
+        raise HTTPError("invalid_url", "Missing dependencies for SOCKS support."
+                        if proxy_url.lower().startswith("socks") else f"No connection adapters were found for '{url}'")
+    conn = Connection(base, timeout=timeout, ssl_context=ssl_context, proxy_url=proxy_url)
     try:
         return conn.request(method, path, headers, body)
     finally:

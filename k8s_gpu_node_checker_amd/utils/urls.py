@@ -19,25 +19,30 @@ _UNRESERVED = frozenset("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz012
 class SplitURL:
     """The parts of ``urllib.parse.urlsplit`` the transport reads."""
 
-    __slots__ = ("scheme", "netloc", "hostname", "port", "path", "query")
+    __slots__ = ("scheme", "netloc", "hostname", "port", "path", "query", "username", "password")
 
     def __init__(self, scheme: str, netloc: str, hostname: "Optional[str]", port: "Optional[int]", path: str,
-                 query: str):
+                 query: str, username: "Optional[str]" = None, password: "Optional[str]" = None):
         self.scheme = scheme
         self.netloc = netloc
         self.hostname = hostname
         self.port = port
         self.path = path
         self.query = query
+        #: user info, percent-decoded (a proxy's credentials); only URLs with '@' have any
+        self.username = username
+        self.password = password
 
     def astuple(self) -> "Tuple":
         return (self.scheme, self.netloc, self.hostname, self.port, self.path, self.query)
 
 
 def _slow(url: str) -> SplitURL:
-    from urllib.parse import urlsplit
+    from urllib.parse import unquote, urlsplit
     p = urlsplit(url)
-    return SplitURL(p.scheme, p.netloc, p.hostname, p.port, p.path, p.query)
+    return SplitURL(p.scheme, p.netloc, p.hostname, p.port, p.path, p.query,
+                    unquote(p.username) if p.username is not None else None,
+                    unquote(p.password) if p.password is not None else None)
 
 
 def split(url: str) -> SplitURL:

@@ -64,3 +64,16 @@ def run_cli(tmp_path):
         return subprocess.run([sys.executable, os.path.join(REPO, "check-gpu-node.py")] + list(args),
                               capture_output=True, text=True, env=e, timeout=timeout, cwd=str(tmp_path))
     return run
+
+
+@pytest.fixture(scope="session")
+def certs(tmp_path_factory):
+    """A self-signed server certificate for 127.0.0.1 / localhost: (crt path, key path)."""
+    d = tmp_path_factory.mktemp("pki")
+    key, crt = d / "srv.key", d / "srv.crt"
+    r = subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
+                        "-days", "1", "-subj", "/CN=mock-apiserver", "-addext", "subjectAltName=IP:127.0.0.1,DNS:localhost"],
+                       capture_output=True)
+    if r.returncode != 0:
+        pytest.skip("openssl unavailable")
+    return str(crt), str(key)

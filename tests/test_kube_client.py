@@ -130,18 +130,6 @@ def test_patch_annotations_and_get(mock_cluster):
     assert srv.log[0]["method"] == "PATCH"
 
 
-@pytest.fixture(scope="module")
-def certs(tmp_path_factory):
-    d = tmp_path_factory.mktemp("pki")
-    key, crt = d / "srv.key", d / "srv.crt"
-    r = subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
-                        "-days", "1", "-subj", "/CN=mock-apiserver", "-addext", "subjectAltName=IP:127.0.0.1,DNS:localhost"],
-                       capture_output=True)
-    if r.returncode != 0:
-        pytest.skip("openssl unavailable")
-    return str(crt), str(key)
-
-
 def test_tls_with_ca_file_and_sni(certs):
     crt, key = certs
     with MockApiServer(fixtures.cluster(3, "amd"), certfile=crt, keyfile=key) as srv:
@@ -224,50 +212,15 @@ def test_mutual_tls_client_certificate_data(mtls, tmp_path):
 
 def test_https_through_connect_proxy(certs, tmp_path):
     """cluster.proxy-url: HTTPS to the apiserver tunnelled through an HTTP CONNECT proxy."""
-    import select
-    import socket
-    import socketserver
-    import threading
-    seen = []
-
-    class Proxy(socketserver.BaseRequestHandler):
-        def handle(self):
-            data = b""
-            while b"\r\n\r\n" not in data:
-                data += self.request.recv(4096)
-            line = data.split(b"\r\n", 1)[0].decode()
-            seen.append(line)
-            host, port = line.split()[1].rsplit(":", 1)
-            up = socket.create_connection((host, int(port)))
-            self.request.sendall(b"HTTP/1.1 200 Connection established\r\n\r\n")
-            socks = [self.request, up]
-            while True:
-                r, _, _ = select.select(socks, [], [], 5)
-                if not r:
-                    break
-                for s in r:
-                    chunk = s.recv(65536)
-                    if not chunk:
-                        up.close()
-                        return
-                    (up if s is self.request else self.request).sendall(chunk)
-
-    class PS(socketserver.ThreadingTCPServer):
-        daemon_threads = True
-        allow_reuse_address = True
-    proxy = PS(("127.0.0.1", 0), Proxy)
-    threading.Thread(target=proxy.serve_forever, daemon=True).start()
+    from k8s_gpu_node_checker_amd.testing.proxy import ForwardProxy
     crt, key = certs
-    try:
-        with MockApiServer(fixtures.cluster(3, "amd"), certfile=crt, keyfile=key) as srv:
-            conn = ClusterConnection(srv.url)
-            conn.ca_file = crt
-            conn.proxy_url = f"http://127.0.0.1:{proxy.server_address[1]}"
-            with KubeClient(conn) as c:
-                assert len(c.scan_nodes().gpu_nodes) == 3
-        assert seen and seen[0].startswith("CONNECT 127.0.0.1:")
-    finally:
-        proxy.shutdown()
+    with ForwardProxy() as px, MockApiServer(fixtures.cluster(3, "amd"), certfile=crt, keyfile=key) as srv:
+        conn = ClusterConnection(srv.url)
+        conn.ca_file = crt
+        conn.proxy_url = px.url
+        with KubeClient(conn) as c:
+            assert len(c.scan_nodes().gpu_nodes) == 3
+        assert px.seen and px.seen[0][0].startswith("CONNECT 127.0.0.1:") and px.seen[0][1] is None
 
 
 def test_pipelined_pagination_uses_two_connections(mock_cluster):
