@@ -36,7 +36,8 @@ from typing import Any, Dict, List, Optional, Sequence
 
 from ..models.health import (DEGRADED, HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, XGMI_LINKS_EXPECTED,
                               HealthExpectations, Verdict,
-                              condition_for, condition_reason, evaluate_report, format_k8s_time, fw_version_str,
+                              condition_for, condition_reason, driver_release, evaluate_report, format_k8s_time,
+                              fw_version_str,
                               throttle_window)
 from ..models.node import HEALTH_ANNOTATION
 from ..models.resources import PRIMARY_GPU_KEY, gpu_breakdown
@@ -98,6 +99,41 @@ def report_digest(rep: Dict[str, Any]) -> str:
     return hashlib.sha256(json.dumps(strip(rep), sort_keys=True).encode()).hexdigest()
 
 
+#: labels the agent maintains with ``--label-node`` (for nodeSelector / nodeAffinity and inventory)
+NODE_LABELS = ("amd.com/mi355x-health", "amd.com/gpu.count", "amd.com/gpu.compute-partition",
+               "amd.com/gpu.memory-partition", "amd.com/gpu.vbios", "amd.com/gpu.driver")
+
+
+def label_value(v: Any) -> str:
+    """A Kubernetes label value: at most 63 characters of ``[A-Za-z0-9._-]``, starting and ending
+    alphanumeric (other characters dropped; the driver version amd-smi reports for an in-tree
+    kernel driver is the whole uname string)."""
+    s = "".join(c for c in str(v) if c.isascii() and (c.isalnum() or c in "._-"))[:63]
+    while s and not s[0].isalnum():
+        s = s[1:]
+    while s and not s[-1].isalnum():
+        s = s[:-1]
+    return s
+
+
+def node_labels(rep: Dict[str, Any], state: str) -> Dict[str, Optional[str]]:
+    """The ``--label-node`` labels for a report: the verdict, the GPU count amd-smi sees, the partition
+    modes (``mixed`` when the GPUs disagree), the VBIOS and the amdgpu driver; a value the probe cannot
+    give removes the label (``None``)."""
+    gpus = [g for g in rep.get("gpus") or [] if isinstance(g, dict) and not g.get("error")]
+
+    def common(key: str) -> Optional[str]:
+        vals = {str(g.get(key)) for g in gpus if g.get(key)}
+        return None if not vals else ("mixed" if len(vals) > 1 else vals.pop())
+    drv = rep.get("driver") if isinstance(rep.get("driver"), dict) else {}
+    raw = {"amd.com/mi355x-health": state, "amd.com/gpu.count": str(len(rep.get("gpus") or [])),
+           "amd.com/gpu.compute-partition": common("compute_partition"),
+           "amd.com/gpu.memory-partition": common("memory_partition"),
+           "amd.com/gpu.vbios": common("vbios_version"),
+           "amd.com/gpu.driver": driver_release(drv.get("version")) if drv.get("version") else None}
+    return {k: (label_value(v) or None) if v is not None else None for k, v in raw.items()}
+
+
 def node_event(node: str, verdict: Verdict, previous: Optional[str], namespace: str = "default",
                now: Optional[float] = None) -> Dict[str, Any]:
     """A core/v1 Event on the Node for one verdict change -- what ``kubectl describe node`` and event
@@ -127,8 +163,12 @@ class Agent:
                  diag_when: str = "idle", busy_vram_mb: int = 2048, busy_gfx_activity: int = 10,
                  diag_timeout: float = 300.0, ignore_pids: Sequence[int] = (),
                  expect_gpus: Optional[int] = None, expectations: Optional[HealthExpectations] = None,
-                 pod_resources_socket: Optional[str] = None, gpu_resources: Sequence[str] = (PRIMARY_GPU_KEY,)):
+                 pod_resources_socket: Optional[str] = None, gpu_resources: Sequence[str] = (PRIMARY_GPU_KEY,),
+                 label_node: bool = False):
         self.node = node
+        # --label-node: node_labels() kept on the Node, written when they change
+        self.label_node = label_node
+        self._labels: Optional[Dict[str, Optional[str]]] = None
         # the kubelet's PodResources socket: a GPU allocated to a pod is never diagnosed, even before the
         # pod touches it (None: not consulted; a missing socket falls back to the amd-smi heuristic)
         self.pod_resources_socket = pod_resources_socket
@@ -382,7 +422,7 @@ class Agent:
         verdict change an Event and (``taint_unhealthy``) the taint.  Returns what was written."""
         digest = report_digest(rep)
         now = time.monotonic()
-        wrote = {"annotation": False, "condition": False, "event": False, "taint": False}
+        wrote = {"annotation": False, "condition": False, "event": False, "taint": False, "labels": False}
         if force or digest != self._annotated or now - self._annotated_at >= self.annotation_refresh:
             client.patch_node_annotations(self.node, self.annotation(rep))
             self._annotated, self._annotated_at = digest, now
@@ -396,6 +436,12 @@ class Agent:
         v = self._verdict
         if v is None:
             return wrote
+        if self.label_node:
+            labels = node_labels(rep, v.state)
+            if labels != self._labels:
+                client.patch_node_labels(self.node, labels)  # raises -> retried next publish
+                self._labels = labels
+                wrote["labels"] = True
         if self.events and v.state != self._event_state:
             prev, self._event_state = self._event_state, v.state
             if prev is not None or v.state != HEALTHY:  # an agent (re)starting on a healthy node is no news
@@ -451,7 +497,7 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
             put("mi355x_node_health", f'state="{st}"', 1 if rep["state"] == st else 0)
     drv = rep.get("driver")
     if isinstance(drv, dict) and drv.get("version"):
-        put("mi355x_node_driver_info", f'name="{_esc(drv.get("name"))}",version="{_esc(drv["version"])}"', 1)
+        put("mi355x_node_driver_info", f'name="{_esc(drv.get("name"))}",version="{_esc(driver_release(drv["version"]))}"', 1)
     for g in rep.get("gpus") or []:
         lbl = f'gpu="{g.get("index")}",bdf="{_esc(g.get("bdf", ""))}"'
         for key, metric in (("ecc_uncorrectable", "ecc_uncorrectable"), ("pcie_width", "pcie_width"),
@@ -609,6 +655,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--gpu-resource", action="append", default=None, metavar="NAME",
                     help=f"extended resource whose kubelet allocations mark GPUs busy (repeatable; default "
                          f"{PRIMARY_GPU_KEY})")
+    ap.add_argument("--label-node", action="store_true",
+                    help="keep node labels " + ", ".join(NODE_LABELS) + " current (verdict, GPU count, partition "
+                         "modes, VBIOS, driver) for nodeSelector / nodeAffinity")
     ap.add_argument("--busy-gfx-activity", type=int, default=10,
                     help="graphics-engine activity (%%) at which a GPU counts as busy (default 10)")
     return ap
@@ -625,7 +674,7 @@ def main(argv: Optional[List[str]] = None) -> int:
                   ignore_pids=args.ignore_pid, expect_gpus=args.expect_gpus,
                   expectations=HealthExpectations(xgmi_links=args.xgmi_links),
                   pod_resources_socket=args.pod_resources_socket,
-                  gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)))
+                  gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)), label_node=args.label_node)
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient

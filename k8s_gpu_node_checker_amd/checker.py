@@ -144,7 +144,8 @@ def fleet_versions(extras: List[Any]) -> Optional[Dict[str, Any]]:
         n += 1
         drv = (rep.get("driver") or {}).get("version") if isinstance(rep.get("driver"), dict) else None
         if drv:
-            drivers[str(drv)] = drivers.get(str(drv), 0) + 1
+            rel = H.driver_release(drv)
+            drivers[rel] = drivers.get(rel, 0) + 1
         node_fw: Dict[str, set] = {}
         for g in rep.get("gpus") or []:
             for name, ver in ((g.get("fw") or {}) if isinstance(g, dict) and isinstance(g.get("fw"), dict)

@@ -290,6 +290,14 @@ class KubeClient:
                             content_type="application/merge-patch+json", idempotent=True)
         return json.loads(resp.body) if resp.body else {}
 
+    def patch_node_labels(self, name: str, labels: Dict[str, Optional[str]]) -> Dict[str, Any]:
+        """JSON merge-patch ``metadata.labels`` (``None`` removes a label; RBAC ``nodes: patch``)."""
+        import json
+        body = json.dumps({"metadata": {"labels": labels}}).encode()
+        resp = self.request("PATCH", "/api/v1/nodes/" + quote(name), body,
+                            content_type="application/merge-patch+json", idempotent=True)
+        return json.loads(resp.body) if resp.body else {}
+
     def update_node_taints(self, name: str,
                            edit: Callable[[List[Dict[str, Any]]], Optional[List[Dict[str, Any]]]],
                            attempts: int = 5) -> Optional[List[Dict[str, Any]]]:

@@ -190,6 +190,22 @@ def fw_version_str(name: str, v: Any) -> str:
     return str(v)
 
 
+def driver_release(version: Any) -> str:
+    """The amdgpu driver version as a release string: a DKMS driver reports its own (``6.10.5``); an
+    in-tree one reports the kernel's uname with the spaces removed (``Linuxversion6.18.54-ant.1(nixbld@
+    ...)#1...``, measured on the MI355X box), of which the kernel release is kept (``6.18.54-ant.1``)."""
+    v = str(version or "")
+    if not v or v[0].isdigit():
+        return v
+    i = next((k for k, c in enumerate(v) if c.isdigit()), -1)
+    if i < 0:
+        return v
+    j = i
+    while j < len(v) and (v[j].isalnum() or v[j] in ".-"):
+        j += 1
+    return v[i:j].rstrip(".-") or v
+
+
 def firmware_mismatch(gpus: Sequence[Any]) -> List[str]:
     """Firmware images whose version differs between the GPUs of one node (probe ``fw``).
 

@@ -117,11 +117,11 @@ def test_agent_metrics_expose_firmware_driver_and_ras_blocks():
     from prometheus_client.parser import text_string_to_metric_families
 
     from k8s_gpu_node_checker_amd.agent.agent import _metrics
-    r = fixtures.mi355x_probe_report("n", gpus=2, driver={"name": "amdgpu", "version": 'odd "v"\\1'},
+    r = fixtures.mi355x_probe_report("n", gpus=2, driver={"name": "amdgpu", "version": '6.1 "v"\\1'},
                                      gpu1={"xgmi_error": 2, "ecc_blocks": {"umc": {"ce": 7, "ue": 1, "de": 0}}})
     fams = {f.name: f for f in text_string_to_metric_families(_metrics(r))}  # parses: the exposition is valid
     drv = fams["mi355x_node_driver_info"].samples[0]
-    assert drv.labels["version"] == 'odd "v"\\1' and drv.value == 1
+    assert drv.labels["version"] == '6.1 "v"\\1' and drv.value == 1
     fw = {(s.labels["gpu"], s.labels["image"]): s.labels["version"] for s in fams["mi355x_gpu_firmware_info"].samples}
     assert fw[("1", "psp_sos")] == "00.45.00.2F" and fw[("0", "pm")] == "04.86.15.106"
     ecc = {(s.labels["block"], s.labels["kind"]): s.value for s in fams["mi355x_gpu_ecc_block_errors"].samples}
@@ -269,3 +269,9 @@ def test_link_trained_down_with_only_one_field_reported():
     g["xgmi_speed_gbps"] = 19
     _, warns = H.evaluate_gpu(g, H.HealthExpectations())
     assert warns == ["gpu0: xGMI links trained at 19 Gb/s (MI355X: x16 38 Gb/s)"]
+
+
+def test_driver_release_from_what_amd_smi_reports():
+    assert H.driver_release("6.10.5") == "6.10.5"
+    assert H.driver_release("Linuxversion6.18.54-ant.1(nixbld@localhost)(gcc(GCC)15.3.0)#1") == "6.18.54-ant.1"
+    assert H.driver_release("") == "" and H.driver_release(None) == "" and H.driver_release("dev") == "dev"

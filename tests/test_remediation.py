@@ -149,3 +149,41 @@ def test_require_schedulable_in_event_watch(mock_cluster, tmp_path, capsys):
     kc = srv.kubeconfig(str(tmp_path / "kc"))
     rc = cli.main(["--kubeconfig", kc, "--json", "--require-schedulable", "--watch-events", "--watch-count", "1"])
     assert rc == 3 and json.loads(capsys.readouterr().out)["ready_nodes"] == 0
+
+
+def test_label_node_keeps_inventory_and_verdict_labels(mock_cluster, fixture_report):
+    srv = mock_cluster([fixtures.realistic_node("n")])
+    ag = A.Agent("n", source="fixture", fixture=fixture_report, label_node=True, events=False)
+    with KubeClient(ClusterConnection(srv.url)) as kc:
+        w = ag.publish(kc, ag.probe_once())
+        assert w["labels"]
+        lab = kc.get_node("n")["metadata"]["labels"]
+        assert lab["amd.com/mi355x-health"] == "healthy" and lab["amd.com/gpu.count"] == "8"
+        assert lab["amd.com/gpu.compute-partition"] == "SPX" and lab["amd.com/gpu.memory-partition"] == "NPS1"
+        assert lab["amd.com/gpu.vbios"] == "00175784" and lab["amd.com/gpu.driver"] == "6.18.54"
+        assert lab["kubernetes.io/hostname"]  # the node's own labels are untouched
+        assert not ag.publish(kc, ag.probe_once())["labels"]  # unchanged: no write
+        w = ag.publish(kc, _bad(ag))
+        assert w["labels"] and kc.get_node("n")["metadata"]["labels"]["amd.com/mi355x-health"] == "unhealthy"
+
+
+def test_label_values_are_valid_kubernetes_labels():
+    import re
+    from hypothesis import given, strategies as st
+    ok = re.compile(r"^(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])?$")
+
+    @given(st.text(max_size=200))
+    def check(v):
+        out = A.label_value(v)
+        assert len(out) <= 63 and ok.match(out), (v, out)
+    check()
+    drv = "Linuxversion6.18.54-ant.1(nixbld@localhost)(gcc(GCC)15.3.0,GNUld(GNUBinutils)2.46)#1-ant-oci"
+    out = A.label_value(drv)
+    assert len(out) == 63 and out.startswith("Linuxversion6.18.54-ant.1nixbldlocalhost")
+    # what the MI355X box's in-tree driver reports becomes its kernel release
+    rep = fixtures.mi355x_probe_report("n", gpus=1, driver={"name": "amdgpu", "version": drv})
+    assert A.node_labels(rep, "healthy")["amd.com/gpu.driver"] == "6.18.54-ant.1"
+    rep = fixtures.mi355x_probe_report("n", gpus=2, gpu1={"compute_partition": "CPX"})
+    rep.pop("driver")
+    lab = A.node_labels(rep, "degraded")
+    assert lab["amd.com/gpu.compute-partition"] == "mixed" and lab["amd.com/gpu.driver"] is None
