@@ -611,8 +611,63 @@ def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
     return out
 
 
+def _summary(test: str, r: Dict[str, Any]) -> str:
+    """One line of numbers for a test result (render_text)."""
+    if test in ("gemm", "gemm_fp8"):
+        return f"{r.get('tflops', 0):.0f} TFLOP/s" + (f" ({r['fraction']:.0%} of reference)" if "fraction" in r else "")
+    if test == "hbm":
+        return f"copy {r.get('copy_tbs', 0):.2f} / read {r.get('read_tbs', 0):.2f} / write {r.get('write_tbs', 0):.2f} TB/s"
+    if test == "mfma":
+        m = r.get("map") or {}
+        kinds = " · ".join(f"{k} {v.get('tflops', 0):.0f}" for k, v in (r.get("kinds") or {}).items())
+        return f"{kinds} TFLOP/s; {m.get('cus', '?')} CUs, XCD spread {m.get('slowest_rel', 1.0):.3f}"
+    if test == "lds":
+        return f"{r.get('cus', '?')} CUs x {r.get('bytes_per_cu', 0) // 1024} KiB, {r.get('errors', 0)} bad words"
+    if test == "l2":
+        m = r.get("map") or {}
+        return f"{r.get('read_tbs', 0):.1f} TB/s, XCD spread {m.get('slowest_rel', 1.0):.3f}, {r.get('errors', 0)} bad words"
+    if test == "memtest":
+        return f"{r.get('gib', 0):g} GiB, {r.get('errors', 0)} errors"
+    if test == "host_link":
+        return f"h2d {r.get('h2d_gbps', 0):.1f} / d2h {r.get('d2h_gbps', 0):.1f} GB/s"
+    if test == "p2p":
+        if r.get("skipped"):
+            return f"skipped ({r['skipped']})"
+        return f"median {r.get('median_gbps', 0)} / min {r.get('min_gbps', 0)} GB/s over {len(r.get('pairs') or [])} pairs"
+    if test == "rccl":
+        rows = r.get("rows") or []
+        ops = len({x.get("op") for x in rows})
+        if r.get("best_busbw_gbps") is None:
+            return f"{r.get('world', '?')} GPU: {ops} collectives' data verified, no bandwidth to judge"
+        return f"best busbw {r.get('best_busbw_gbps')} GB/s over {r.get('world', '?')} GPUs, {ops} collectives verified"
+    return ""
+
+
+def render_text(out: Dict[str, Any]) -> str:
+    """``mi355x-diag --format text``: one block per GPU, one line per test (PASS / DEGRADED / FAIL, the
+    numbers, and the detail of anything not passing), then the node-level fabric and the result."""
+    lines = []
+    for d, dev in out.get("devices", {}).items():
+        info = dev.get("info") or {}
+        mem = info.get("mem_bytes")
+        head = [f"GPU {d}", info.get("bdf", ""), info.get("name", ""), info.get("arch", "").split(":")[0],
+                f"{info.get('cus', '?')} CUs", f"{mem / (1 << 30):.0f} GiB" if isinstance(mem, int) else ""]
+        lines.append("  ".join(x for x in head if x))
+        for test, r in (dev.get("tests") or {}).items():
+            state = "FAIL" if not r.get("pass") else ("DEGRADED" if r.get("degraded") else "pass")
+            lines.append(f"  {test:<10} {state:<9} {_summary(test, r)}")
+            if state != "pass" and r.get("detail"):
+                lines.append(f"  {'':<10} {'':<9} {r['detail']}")
+    for test, r in (out.get("fabric") or {}).items():
+        state = "FAIL" if not r.get("pass") else "pass"
+        lines.append(f"fabric {test:<5} {state:<9} {_summary(test, r)}" + (f"  {r['detail']}" if r.get("detail") else ""))
+    lines.append(f"result: {'PASS' if out.get('pass') else 'FAIL'}")
+    return "\n".join(lines) + "\n"
+
+
 def main(argv=None) -> int:
-    """``mi355x-diag [--level N] [--device D]``: run the active diagnostics, print one JSON document."""
+    """``mi355x-diag [--level N] [--device D] [--format json|text]``: run the active diagnostics, print one
+    JSON document (or a text summary)."""
     import argparse
     import json
     ap = argparse.ArgumentParser(prog="mi355x-diag", description="MI355X active diagnostics (HIP, gfx950)")
@@ -621,6 +676,7 @@ def main(argv=None) -> int:
     ap.add_argument("--no-p2p", dest="p2p", action="store_false", help="skip the level-2 xGMI pair matrix")
     ap.add_argument("--no-rccl", dest="rccl", action="store_false",
                     help="skip the level-2 RCCL collectives (ops/fabric.py)")
+    ap.add_argument("--format", choices=("json", "text"), default="json")
     args = ap.parse_args(argv)
     devices = args.device if args.device else list(range(device_count()))
     out: Dict[str, Any] = {"devices": {d: {"info": device_info(d), "tests": run(args.level, d)} for d in devices}}
@@ -633,7 +689,7 @@ def main(argv=None) -> int:
         out.setdefault("fabric", {})["rccl"] = fabric.collective_suite(devices)
         ok = ok and out["fabric"]["rccl"]["pass"]
     out["pass"] = ok
-    print(json.dumps(out, indent=1))
+    print(render_text(out) if args.format == "text" else json.dumps(out, indent=1), end="" if args.format == "text" else "\n")
     return 0 if out["pass"] else 1
 
 

@@ -245,3 +245,16 @@ def test_cu_lag_is_not_judged_on_an_uneven_deal():
     where = diag.cu_map_summary({"k": flat})
     assert where["waves_per_cu"] == [8, 16] and where["slowest_cu_rel"] > 1.4
     assert diag._lag_notes(where, "waves") == []
+
+
+def test_text_summary(fake, capsys):
+    fake(slow_xcd={2: 1.3})
+    rc = diag.main(["--level", "1", "--format", "text"])
+    out = capsys.readouterr().out.splitlines()
+    assert out[0].startswith("GPU 0  0000:05:00.0  AMD Instinct MI355X  gfx950  256 CUs  288 GiB")
+    rows = {ln.split()[0]: ln for ln in out[1:] if ln.startswith("  ") and ln.split()}
+    assert rows["gemm"].split()[1] == "pass" and "TFLOP/s" in rows["gemm"]
+    assert rows["mfma"].split()[1] == "DEGRADED" and "XCD spread 1.300" in rows["mfma"]
+    assert any("xcd2 waves take 1.30x" in ln for ln in out)
+    assert rows["lds"].endswith("256 CUs x 159 KiB, 0 bad words")
+    assert out[-1] == "result: PASS" and rc == 0  # degraded still passes
