@@ -34,8 +34,8 @@ from .native import NativeUnavailable, load_cdll
 # A result below FAIL_FRACTION of its reference fails (a GPU at 55 % clock or power is unhealthy); one
 # between FAIL_FRACTION and DEGRADED_FRACTION passes as *degraded* (a warning on the node, still Ready).
 # The 85 % floor sits under every soak minimum (worst: gemm_fp8 8192^3 at 90 % of its median) and under
-# the ~10 % box-to-box DVFS spread; a rate that lands below 95 % is measured a second time before it is
-# reported (best of two), so one noisy sample does not flap the node's verdict.
+# the ~10 % box-to-box DVFS spread; a rate that lands below 95 % is measured again (REMEASURE) before it is
+# reported (best of three), so a noisy sample does not flap the node's verdict.
 #
 # Partitions: the reference rates are scaled by the share of the physical GPU the HIP device is.
 #   compute (GEMM, MFMA burn-in):   cus / 256       (CPX: 32 CUs -> 1/8)
@@ -45,6 +45,11 @@ from .native import NativeUnavailable, load_cdll
 # The partition scaling is proportional, not measured (no partitioned MI355X was available): it is the
 # lenient bound, so a healthy partition never fails; a partitioned GPU's degraded band is advisory.
 FAIL_FRACTION = 0.85
+# A rate below the degraded line (numerics fine) is measured again, up to REMEASURE more times, and the best
+# is kept: under sustained load the burn-in dips below 95 % in ~10 % of single runs (power management),
+# two dips in a row were 19 of 1,913 soak rounds (profiles/soak_level1_r2_mi355x.json); three in a row
+# would be ~0.1 %.
+REMEASURE = 2
 DEGRADED_FRACTION = 0.95
 FULL_CUS = 256
 FULL_MEM_BYTES = 288 << 30
@@ -594,7 +599,9 @@ def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
         name = test.replace("_quick", "")
         try:
             res = _one(test, device, scale)
-            if _slow_only(res):
+            for _ in range(REMEASURE):
+                if not _slow_only(res):
+                    break
                 again = _one(test, device, scale)
                 again["retried"] = True
                 if _goodness(again) > _goodness(res):

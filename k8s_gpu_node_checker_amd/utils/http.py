@@ -573,22 +573,29 @@ def env_proxy(url: str, environ: Optional[Dict[str, str]] = None) -> Optional[st
                 proxies[k[:-6].lower()] = v
             else:
                 proxies.pop(k[:-6].lower(), None)
-    no_proxy = env.get("no_proxy") or env.get("NO_PROXY")  # requests' own lookup
+    # requests.utils.should_bypass_proxies, part 1: its own no_proxy lookup and suffix / IP / CIDR test
+    no_proxy = env.get("no_proxy") or env.get("NO_PROXY")
     if no_proxy:
         entries = [h for h in no_proxy.replace(" ", "").split(",") if h]
-        if "*" in entries:
-            return None
         if _is_ipv4(host):
             for e in entries:
                 if ("/" in e and _in_cidr(host, e)) or host == e:
                     return None
         else:
             host_port = f"{host}:{parts.port}" if parts.port else host
-            for e in entries:
-                if host.endswith(e) or host_port.endswith(e):
-                    return None
-                if e.lstrip(".") and (host == e.lstrip(".") or host.endswith("." + e.lstrip("."))):
-                    return None
+            if any(host.endswith(e) or host_port.endswith(e) for e in entries):
+                return None
+    # part 2: urllib.request.proxy_bypass_environment(hostname) over the merged "no" entry ('*', or a
+    # name that is the host or a parent domain of it)
+    merged_no = proxies.pop("no", None)
+    if merged_no:
+        if merged_no == "*":
+            return None
+        h = host.lower()
+        for name in (n.strip() for n in merged_no.split(",")):
+            name = name.lstrip(".").lower()
+            if name and (h == name or h.endswith("." + name)):
+                return None
     proxy = proxies.get(parts.scheme) or proxies.get("all")
     if not proxy:
         return None

@@ -23,7 +23,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from k8s_gpu_node_checker_amd.ops import diag  # noqa: E402
 
 METRICS = (("gemm", "tflops"), ("gemm_fp8", "tflops"), ("hbm", "copy_tbs"), ("hbm", "read_tbs"),
-           ("hbm", "write_tbs"), ("memtest", "errors"), ("host_link", "h2d_gbps"), ("host_link", "d2h_gbps"))
+           ("hbm", "write_tbs"), ("memtest", "errors"), ("host_link", "h2d_gbps"), ("host_link", "d2h_gbps"),
+           ("l2", "read_tbs"), ("l2", "errors"), ("lds", "errors"))
 
 
 def _rss_mb() -> float:
@@ -72,6 +73,16 @@ def main() -> int:
             v = (res.get(test) or {}).get(key)
             if isinstance(v, (int, float)):
                 series.setdefault(f"{test}.{key}", []).append(v)
+        for test in ("mfma", "l2"):  # where on the chip: the XCD / CU lag of the per-CU maps
+            m = (res.get(test) or {}).get("map") or {}
+            for key in ("slowest_rel", "slowest_cu_rel"):
+                if isinstance(m.get(key), (int, float)):
+                    series.setdefault(f"{test}.map.{key}", []).append(m[key])
+        degraded = sorted(k for k, v in res.items() if v.get("degraded"))
+        if degraded:
+            rnd_extra["degraded"] = degraded
+            for k in degraded:
+                series.setdefault(f"degraded.{k}", []).append(1)
         for kind, row in ((res.get("mfma") or {}).get("kinds") or {}).items():
             series.setdefault(f"mfma.{kind}.tflops", []).append(row["tflops"])
             series.setdefault(f"mfma.{kind}.errors", []).append(row["errors"])
