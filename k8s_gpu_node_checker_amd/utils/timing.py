@@ -12,7 +12,7 @@ import time
 
 TYPE_CHECKING = False
 if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
-    from typing import Dict, Iterator
+    from typing import Dict
 
 
 class Tracer:
