@@ -199,8 +199,9 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
 
     # --- node agent on this rank's GPU: probe (+ diagnostics), publish annotation
     # diag_when="always": this process is the GPU's only user and runs the diagnostics on purpose
+    # the DaemonSet's publishing configuration (deploy/daemonset.yaml: gzip-encoded report annotation)
     agent = Agent(node, source="auto", diag_level=args.diag_level if cuda else 0,
-                  devices=[local_rank] if cuda else [], diag_when="always")
+                  devices=[local_rank] if cuda else [], diag_when="always", annotation_encoding="gzip")
     t0 = time.perf_counter()
     rep = agent.probe_once()
     probe_source = rep.get("probe")

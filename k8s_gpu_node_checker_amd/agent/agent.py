@@ -36,7 +36,8 @@ from typing import Any, Dict, List, Optional, Sequence
 
 from ..models.health import (DEGRADED, HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, XGMI_LINKS_EXPECTED,
                               HealthExpectations, Verdict,
-                              condition_for, condition_reason, driver_release, evaluate_report, format_k8s_time,
+                              condition_for, condition_reason, driver_release, encode_annotation, evaluate_report,
+                              format_k8s_time,
                               fw_version_str,
                               throttle_window)
 from ..models.node import HEALTH_ANNOTATION
@@ -164,8 +165,12 @@ class Agent:
                  diag_timeout: float = 300.0, ignore_pids: Sequence[int] = (),
                  expect_gpus: Optional[int] = None, expectations: Optional[HealthExpectations] = None,
                  pod_resources_socket: Optional[str] = None, gpu_resources: Sequence[str] = (PRIMARY_GPU_KEY,),
-                 label_node: bool = False):
+                 label_node: bool = False, annotation_encoding: str = "json"):
         self.node = node
+        # "json" (readable with kubectl) or "gzip" (gz: + base64, ~12x smaller in every node LIST / watch)
+        if annotation_encoding not in ("json", "gzip"):
+            raise ValueError("annotation_encoding must be json or gzip")
+        self.annotation_encoding = annotation_encoding
         # --label-node: node_labels() kept on the Node, written when they change
         self.label_node = label_node
         self._labels: Optional[Dict[str, Optional[str]]] = None
@@ -404,7 +409,7 @@ class Agent:
         bytes there; they stay on ``/probe`` and ``/metrics``."""
         gpus = [{k: v for k, v in g.items() if k not in _ANNOTATION_DROP} if isinstance(g, dict) else g
                 for g in rep.get("gpus") or []]
-        return {HEALTH_ANNOTATION: json.dumps(dict(rep, gpus=gpus), separators=(",", ":"))}
+        return {HEALTH_ANNOTATION: encode_annotation(dict(rep, gpus=gpus), self.annotation_encoding)}
 
     def condition(self, rep: Dict[str, Any]) -> Dict[str, Any]:
         v = self.evaluate(rep)
@@ -655,6 +660,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--gpu-resource", action="append", default=None, metavar="NAME",
                     help=f"extended resource whose kubelet allocations mark GPUs busy (repeatable; default "
                          f"{PRIMARY_GPU_KEY})")
+    ap.add_argument("--annotation-encoding", choices=("json", "gzip"), default="json",
+                    help="report annotation as JSON (readable with kubectl) or gz: + base64(gzip(JSON)), "
+                         "~12x smaller in every node LIST and watch event (the checker reads both)")
     ap.add_argument("--label-node", action="store_true",
                     help="keep node labels " + ", ".join(NODE_LABELS) + " current (verdict, GPU count, partition "
                          "modes, VBIOS, driver) for nodeSelector / nodeAffinity")
@@ -674,7 +682,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                   ignore_pids=args.ignore_pid, expect_gpus=args.expect_gpus,
                   expectations=HealthExpectations(xgmi_links=args.xgmi_links),
                   pod_resources_socket=args.pod_resources_socket,
-                  gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)), label_node=args.label_node)
+                  gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)), label_node=args.label_node,
+                  annotation_encoding=args.annotation_encoding)
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient

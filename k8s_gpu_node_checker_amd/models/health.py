@@ -599,9 +599,39 @@ def verdict_from_condition(cond: Tuple[Optional[str], Optional[str], Optional[st
     return v
 
 
+#: prefix of a compressed report annotation: ``gz:`` + base64(gzip(JSON)) (agent ``--annotation-encoding
+#: gzip``; an 8-GPU report with level-2 results shrinks 22 KB -> 1.8 KB in every node LIST and watch event)
+GZIP_PREFIX = "gz:"
+
+
+def encode_annotation(report: Dict[str, Any], encoding: str = "json") -> str:
+    """The ``amd.com/mi355x-health`` value of a report: compact JSON, or ``gz:`` + base64 of it gzipped."""
+    import json
+    text = json.dumps(report, separators=(",", ":"))
+    if encoding == "json":
+        return text
+    if encoding != "gzip":
+        raise ValueError(f"unknown annotation encoding {encoding!r}")
+    import base64
+    import gzip
+    # mtime=0: the same report always encodes to the same bytes (the agent compares before rewriting)
+    return GZIP_PREFIX + base64.b64encode(gzip.compress(text.encode(), 9, mtime=0)).decode("ascii")
+
+
 def parse_annotation(raw: Optional[str]) -> Optional[Dict[str, Any]]:
+    """A report annotation in either encoding -> the report dict; an undecodable one becomes a probe
+    error (verdict unknown), never an exception."""
     if not raw:
         return None
+    if raw.startswith(GZIP_PREFIX):
+        import base64
+        import binascii
+        import gzip
+        import zlib
+        try:
+            raw = gzip.decompress(base64.b64decode(raw[len(GZIP_PREFIX):], validate=True)).decode("utf-8")
+        except (binascii.Error, OSError, EOFError, zlib.error, UnicodeDecodeError, ValueError):
+            return {"schema": SCHEMA, "error": "annotation is not gzip+base64 JSON", "ts": time.time()}
     from ..ops.fastpath import loads  # native json.loads (falls back to the json package itself)
     try:
         doc = loads(raw)

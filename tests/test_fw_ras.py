@@ -275,3 +275,34 @@ def test_driver_release_from_what_amd_smi_reports():
     assert H.driver_release("6.10.5") == "6.10.5"
     assert H.driver_release("Linuxversion6.18.54-ant.1(nixbld@localhost)(gcc(GCC)15.3.0)#1") == "6.18.54-ant.1"
     assert H.driver_release("") == "" and H.driver_release(None) == "" and H.driver_release("dev") == "dev"
+
+
+def test_gzip_annotation_roundtrip_and_corruption():
+    r = rep()
+    for enc in ("json", "gzip"):
+        raw = H.encode_annotation(r, enc)
+        assert H.parse_annotation(raw) == json.loads(json.dumps(r))
+    gz = H.encode_annotation(r, "gzip")
+    assert gz.startswith("gz:") and len(gz) * 4 < len(H.encode_annotation(r, "json"))
+    assert H.encode_annotation(r, "gzip") == gz  # deterministic: no gzip timestamp
+    bad = H.parse_annotation("gz:!!notbase64")
+    assert bad["error"] == "annotation is not gzip+base64 JSON"
+    assert H.evaluate_report(bad, 8).state == H.UNKNOWN
+
+
+def test_agent_gzip_annotation_read_by_the_checker(mock_cluster, tmp_path):
+    from k8s_gpu_node_checker_amd.agent.agent import Agent
+    from k8s_gpu_node_checker_amd.kube.client import KubeClient
+    from k8s_gpu_node_checker_amd.models.node import HEALTH_ANNOTATION
+    fx = tmp_path / "probe.json"
+    fx.write_text(json.dumps(fixtures.mi355x_probe_report("n", gpus=7)))  # 7 of the node's 8 GPUs
+    srv = mock_cluster([fixtures.realistic_node("n", gpu_count=8)])
+    ag = Agent("n", source="fixture", fixture=str(fx), annotation_encoding="gzip", events=False)
+    with KubeClient(ClusterConnection(srv.url)) as kc:
+        ag.publish(kc, ag.probe_once())
+        assert kc.get_node("n")["metadata"]["annotations"][HEALTH_ANNOTATION].startswith("gz:")
+    for opts in (CheckOptions(json_extended=True), CheckOptions(json=True, health_reeval=True)):
+        res = run_check(ClusterConnection(srv.url), opts)
+        assert res.exit_code == 3 and res.verdicts[0].reasons[0] == "7 of 8 GPUs visible to amd-smi"
+    fleet = run_check(ClusterConnection(srv.url), CheckOptions(json_extended=True)).extended_fields()["mi355x"]["fleet"]
+    assert fleet["nodes_reporting"] == 1 and fleet["driver"] == {"6.18.54": 1}
