@@ -137,10 +137,11 @@ def main() -> int:
     procs = []
     ctrl = {}
     if rank == 0:
-        # nodes beyond the GPU count start with a recorded MI355X probe (condition + annotation); the
-        # ranks' own nodes get their live probe PATCHed below
+        # nodes beyond the GPU count start with a recorded MI355X probe (condition + annotation, gzip-encoded
+        # as the DaemonSet writes it); the ranks' own nodes get their live probe PATCHed below
         p, info = _spawn("k8s_gpu_node_checker_amd.testing.mock_apiserver", "--nodes", str(n_nodes), "--kind", "amd",
-                         "--gpus-per-node", "1", *(["--with-health"] if n_nodes > n_gpus else []))
+                         "--gpus-per-node", "1", "--annotation-encoding", "gzip",
+                         *(["--with-health"] if n_nodes > n_gpus else []))
         procs.append(p)
         ctrl["api"] = info["url"]
         if args.slack:

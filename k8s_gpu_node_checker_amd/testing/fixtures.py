@@ -136,8 +136,10 @@ def mi355x_probe_report(node: str, gpus: int = 8, ts: Optional[float] = None, **
     return rep
 
 
-def health_annotation(report: Dict[str, Any]) -> Dict[str, str]:
-    return {HEALTH_ANNOTATION: json.dumps(report, separators=(",", ":"))}
+def health_annotation(report: Dict[str, Any], encoding: str = "json") -> Dict[str, str]:
+    """The report annotation as an agent with ``--annotation-encoding <encoding>`` writes it."""
+    from ..models.health import encode_annotation
+    return {HEALTH_ANNOTATION: encode_annotation(report, encoding)}
 
 
 def health_condition(report: Dict[str, Any], expected_gpus: int = 0) -> Dict[str, Any]:
@@ -147,7 +149,8 @@ def health_condition(report: Dict[str, Any], expected_gpus: int = 0) -> Dict[str
 
 
 def cluster(n: int, kind: str = "amd", not_ready: Sequence[int] = (), gpus_per_node: int = 8,
-            with_health: bool = False, prefix: str = "mi355x-node") -> List[Dict[str, Any]]:
+            with_health: bool = False, prefix: str = "mi355x-node",
+            annotation_encoding: str = "json") -> List[Dict[str, Any]]:
     """``kind``: ``amd`` | ``nvidia`` | ``mixed`` (alternating, as the survey's 1000-node run) | ``cpu``."""
     nodes = []
     for i in range(n):
@@ -163,7 +166,7 @@ def cluster(n: int, kind: str = "amd", not_ready: Sequence[int] = (), gpus_per_n
         ann, conds = None, None
         if with_health and key == "amd.com/gpu":
             rep = mi355x_probe_report(name, gpus_per_node)
-            ann, conds = health_annotation(rep), [health_condition(rep, gpus_per_node)]
+            ann, conds = health_annotation(rep, annotation_encoding), [health_condition(rep, gpus_per_node)]
         nodes.append(realistic_node(name, key, gpus_per_node, ready=i not in not_ready, index=i, annotations=ann,
                                     extra_conditions=conds))
     return nodes

@@ -494,8 +494,9 @@ def write_kubeconfig(path: str, server: str, token: Optional[str] = None,
 
 
 def build_nodes(n: int, kind: str, not_ready: int = 0, with_health: bool = False,
-                gpus_per_node: int = 8) -> List[Dict[str, Any]]:
-    return fixtures.cluster(n, kind, not_ready=range(not_ready), with_health=with_health, gpus_per_node=gpus_per_node)
+                gpus_per_node: int = 8, annotation_encoding: str = "json") -> List[Dict[str, Any]]:
+    return fixtures.cluster(n, kind, not_ready=range(not_ready), with_health=with_health, gpus_per_node=gpus_per_node,
+                            annotation_encoding=annotation_encoding)
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -505,13 +506,15 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--not-ready", type=int, default=0)
     ap.add_argument("--gpus-per-node", type=int, default=8)
     ap.add_argument("--with-health", action="store_true")
+    ap.add_argument("--annotation-encoding", choices=("json", "gzip"), default="json",
+                    help="how the --with-health report annotations are written (the agent's flag of that name)")
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--token")
     ap.add_argument("--golden", help="serve a golden fixture instead of a generated cluster")
     args = ap.parse_args(argv)
     nodes = fixtures.golden(args.golden) if args.golden else build_nodes(
-        args.nodes, args.kind, args.not_ready, args.with_health, args.gpus_per_node)
+        args.nodes, args.kind, args.not_ready, args.with_health, args.gpus_per_node, args.annotation_encoding)
     srv = MockApiServer(nodes, args.host, args.port, MockConfig(token=args.token))
     print(json.dumps({"url": srv.url, "port": srv.server_address[1], "nodes": len(nodes)}), flush=True)
     try:
