@@ -64,6 +64,7 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
                        "help": "MI355X 프리셋: --gpu-source allocatable --health-policy require --require-schedulable"}),
     ("x", "--json-extended", {"action": "store_true", "help": "JSON 에 MI355X 헬스/타이밍 필드 추가"}),
     ("x", "--trace", {"action": "store_true", "help": "단계별 소요 시간을 stderr 로 출력"}),
+    ("x", "--explain", {"metavar": "NODE", "help": "한 노드가 Ready 로 집계되는(또는 안 되는) 이유를 출력"}),
     ("x", "--prometheus-textfile", {"help": "node-exporter textfile 메트릭 경로"}),
     ("x", "--state-file", {"help": "직전 결과 저장 파일 (알림 중복 제거)"}),
     ("x", "--watch", {"type": float, "default": 0.0, "help": "N초마다 반복 점검 (0 = 한 번, 기본)"}),
@@ -216,6 +217,13 @@ def _report_error(args: Any, e: BaseException) -> int:
 
 def main(argv: Optional[List[str]] = None) -> int:
     args = parse_args(argv)
+    if args.explain:
+        try:
+            from .checker import CheckOptions
+            from .explain import explain
+            return explain(_load_cluster(args), args.explain, CheckOptions.from_args(args), sys.stdout)
+        except Exception as e:
+            return _report_error(args, e)
     if args.watch_events:
         return _watch_events(args)
     if args.watch and args.watch > 0:

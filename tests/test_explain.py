@@ -1,0 +1,52 @@
+"""``check-gpu-node --explain NODE``: one node's Ready verdict, its AMDGPUHealthy condition and the GPU
+rows of its report, with the reference's exit codes applied to that node."""
+import json
+
+from k8s_gpu_node_checker_amd.models import health as H
+from k8s_gpu_node_checker_amd.testing import fixtures
+from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+
+
+def _cluster(mock_cluster, tmp_path):
+    bad = fixtures.mi355x_probe_report("bad", gpus=8, gpu3={"ecc_uncorrectable": 2,
+                                                            "ecc_blocks": {"umc": {"ce": 0, "ue": 2, "de": 0}}})
+    good = fixtures.mi355x_probe_report("good", gpus=8)
+    nodes = [fixtures.realistic_node("good", index=0, annotations=fixtures.health_annotation(good, "gzip"),
+                                     extra_conditions=[fixtures.health_condition(good, 8)]),
+             fixtures.realistic_node("bad", index=1, annotations=fixtures.health_annotation(bad),
+                                     extra_conditions=[fixtures.health_condition(bad, 8)]),
+             fixtures.realistic_node("plain", index=2),
+             fixtures.realistic_node("cpu", gpu_key=None, index=3)]
+    return write_kubeconfig(str(tmp_path / "kc"), mock_cluster(nodes).url)
+
+
+def test_explain_unhealthy_node(run_cli, mock_cluster, tmp_path):
+    kc = _cluster(mock_cluster, tmp_path)
+    p = run_cli(["--kubeconfig", kc, "--explain", "bad"])
+    assert p.returncode == 3, p.stdout + p.stderr
+    out = p.stdout
+    assert out.startswith("node bad: Ready=True  GPUs 8 (amd.com/gpu:8)")
+    assert "AMDGPUHealthy=False (MI355XUnhealthy" in out
+    assert "MI355X verdict: unhealthy, 7/8 GPUs ok" in out
+    assert "  reason: gpu3: 2 uncorrectable ECC errors (umc 2)" in out
+    row3 = next(ln for ln in out.splitlines() if ln.startswith("  3 "))
+    assert "0000:35:00.0" in row3 and "2/0" in row3 and row3.endswith("2 uncorrectable ECC errors (umc 2)")
+    assert out.rstrip().endswith("=> counts as Ready: no")
+
+
+def test_explain_healthy_plain_and_missing(run_cli, mock_cluster, tmp_path):
+    kc = _cluster(mock_cluster, tmp_path)
+    p = run_cli(["--kubeconfig", kc, "--explain", "good"])
+    assert p.returncode == 0 and "MI355X verdict: healthy, 8/8 GPUs ok" in p.stdout
+    assert "report: probe fixture" in p.stdout and "driver 6.18.54" in p.stdout  # gzip annotation read
+    rows = [ln for ln in p.stdout.splitlines() if ln.startswith("  ") and ln.split()[0].isdigit()]
+    assert len(rows) == 8 and all(r.endswith("ok") for r in rows)
+    p = run_cli(["--kubeconfig", kc, "--explain", "plain"])  # no agent: the reference's Ready rule
+    assert p.returncode == 0 and "AMDGPUHealthy: not published" in p.stdout and "verdict: none" in p.stdout
+    p = run_cli(["--kubeconfig", kc, "--explain", "plain", "--mi355x"])  # the probe is required there
+    assert p.returncode == 3 and "verdict: unknown" in p.stdout
+    p = run_cli(["--kubeconfig", kc, "--explain", "cpu"])
+    assert p.returncode == 2 and "not a GPU node" in p.stdout
+    p = run_cli(["--kubeconfig", str(tmp_path / "missing"), "--explain", "x", "--json"])
+    assert p.returncode == 1 and "error" in json.loads(p.stdout)
+    assert H.HEALTH_CONDITION == "AMDGPUHealthy"
