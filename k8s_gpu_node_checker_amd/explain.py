@@ -89,7 +89,8 @@ def explain(cluster: ClusterConnection, node_name: str, opts: CheckOptions, out:
         widths = [max(len(r[c]) for r in rows) for c in range(len(head) - 1)]
         for r in rows:
             out.write("  " + "  ".join(r[c].ljust(widths[c]) for c in range(len(head) - 1)) + "  " + r[-1] + "\n")
-        node_level = [ln for ln in lines if not ln.startswith("gpu")]
+        shown = {f"gpu{g.get('index')}:" for g in rep.get("gpus") or [] if isinstance(g, dict)}
+        node_level = [ln for ln in lines if ln.split(" ", 1)[0] not in shown]  # incl. spans ("gpu6-7: ...")
         for ln in node_level:
             out.write(f"  node: {ln}\n")
     elif rep and rep.get("error"):

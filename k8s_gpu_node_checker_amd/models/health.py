@@ -295,9 +295,16 @@ def partition_mismatch(gpus: Sequence[Any]) -> List[str]:
 
 
 def _span(ix: List[Any]) -> str:
-    if len(ix) > 1 and all(isinstance(i, int) for i in ix) and ix == list(range(ix[0], ix[0] + len(ix))):
-        return f"{ix[0]}-{ix[-1]}"
-    return ",".join(str(i) for i in ix)
+    """GPU indices as runs: [0, 1, 2, 4, 6, 7] -> "0-2,4,6-7" (non-integers listed as they are)."""
+    if not all(isinstance(i, int) for i in ix):
+        return ",".join(str(i) for i in ix)
+    runs: List[List[int]] = []
+    for i in ix:
+        if runs and i == runs[-1][1] + 1:
+            runs[-1][1] = i
+        else:
+            runs.append([i, i])
+    return ",".join(f"{a}-{b}" if b > a else f"{a}" for a, b in runs)
 
 
 def _age_s(stamp: Any, now: Optional[float]) -> Optional[float]:

@@ -9,7 +9,8 @@ from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
 
 def _cluster(mock_cluster, tmp_path):
     bad = fixtures.mi355x_probe_report("bad", gpus=8, gpu3={"ecc_uncorrectable": 2,
-                                                            "ecc_blocks": {"umc": {"ce": 0, "ue": 2, "de": 0}}})
+                                                            "ecc_blocks": {"umc": {"ce": 0, "ue": 2, "de": 0}},
+                                                            "fw": dict(fixtures.MI355X_FW, pm=0x04560000)})
     good = fixtures.mi355x_probe_report("good", gpus=8)
     nodes = [fixtures.realistic_node("good", index=0, annotations=fixtures.health_annotation(good, "gzip"),
                                      extra_conditions=[fixtures.health_condition(good, 8)]),
@@ -31,6 +32,7 @@ def test_explain_unhealthy_node(run_cli, mock_cluster, tmp_path):
     assert "  reason: gpu3: 2 uncorrectable ECC errors (umc 2)" in out
     row3 = next(ln for ln in out.splitlines() if ln.startswith("  3 "))
     assert "0000:35:00.0" in row3 and "2/0" in row3 and row3.endswith("2 uncorrectable ECC errors (umc 2)")
+    assert "  node: firmware differs across GPUs: pm: gpu0-2,4-7 " in out  # a node-level finding naming a GPU span is kept
     assert out.rstrip().endswith("=> counts as Ready: no")
 
 

@@ -66,8 +66,8 @@ def test_firmware_mismatch_across_gpus():
     # two images differ, groups are ordered by size, non-contiguous GPUs are listed
     fw = dict(fixtures.MI355X_FW, mec=45, rlc=40)
     v = H.evaluate_report(rep(gpu1={"fw": fw}, gpu4={"fw": fw}), 8)
-    assert v.warnings == ["firmware differs across GPUs: mec: gpu0,2,3,5,6,7 44, gpu1,4 45; "
-                          "rlc: gpu0,2,3,5,6,7 43, gpu1,4 40"]
+    assert v.warnings == ["firmware differs across GPUs: mec: gpu0,2-3,5-7 44, gpu1,4 45; "
+                          "rlc: gpu0,2-3,5-7 43, gpu1,4 40"]
     # the message is what the condition carries: stable between probes (no counters, no timestamps)
     c1 = H.condition_for(v, now=1.0)["message"]
     c2 = H.condition_for(H.evaluate_report(rep(gpu1={"fw": fw}, gpu4={"fw": fw}), 8), now=2.0)["message"]
@@ -257,7 +257,7 @@ def test_partition_modes_differing_across_gpus_degrade():
     assert v.state == H.DEGRADED
     assert v.warnings == ["partition modes differ across GPUs: compute: gpu0-6 SPX, gpu7 CPX"]
     v = H.evaluate_report(rep(gpu2={"memory_partition": "NPS2", "vram_mb": 147448}), 8)
-    assert v.warnings == ["partition modes differ across GPUs: memory: gpu0,1,3,4,5,6,7 NPS1, gpu2 NPS2"]
+    assert v.warnings == ["partition modes differ across GPUs: memory: gpu0-1,3-7 NPS1, gpu2 NPS2"]
     # a board partitioned as a whole is one mode everywhere: nothing to report
     cpx = rep(**{f"gpu{i}": {"compute_partition": "CPX", "cus": 32} for i in range(8)})
     assert H.partition_mismatch(cpx["gpus"]) == []
