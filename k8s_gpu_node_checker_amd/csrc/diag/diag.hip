@@ -49,6 +49,7 @@ int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte ro
   do {                                                                                    \
     hipError_t e_ = (expr);                                                               \
     if (e_ != hipSuccess) {                                                               \
+      (void)hipGetLastError(); /* a failed allocation must not fail the next call's check */ \
       g_err = std::string(#expr) + ": " + hipGetErrorString(e_);                          \
       return -1;                                                                          \
     }                                                                                     \
@@ -939,6 +940,27 @@ struct DevBuf {
   }
 };
 
+// A pair of timing events and an optional stream, released on every return path: the agent calls the
+// entry points below for the life of its pod, so an early DIAG_CHECK return must not leak them.
+struct Timer {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipStream_t stream = nullptr;
+  Timer() = default;
+  Timer(const Timer&) = delete;
+  Timer& operator=(const Timer&) = delete;
+  hipError_t create(bool own_stream = false) {
+    hipError_t e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess && own_stream) e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+    return e;
+  }
+  ~Timer() {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
 hipError_t enable_peer(int from, int to) {
   hipError_t e = hipSetDevice(from);
   if (e != hipSuccess) return e;
@@ -1075,16 +1097,20 @@ int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int n
     return -2;
   }
   DIAG_CHECK(hipSetDevice(device));
-  __bf16 *A = nullptr, *Bt = nullptr;
-  float *C = nullptr, *ref = nullptr;
-  int *rows = nullptr, *cols = nullptr;
-  hipEvent_t e0, e1;
-  DIAG_CHECK(hipMalloc(&A, sizeof(__bf16) * static_cast<size_t>(M) * K));
-  DIAG_CHECK(hipMalloc(&Bt, sizeof(__bf16) * static_cast<size_t>(N) * K));
-  DIAG_CHECK(hipMalloc(&C, sizeof(float) * static_cast<size_t>(M) * N));
-  DIAG_CHECK(hipMalloc(&ref, sizeof(float) * nsamp));
-  DIAG_CHECK(hipMalloc(&rows, sizeof(int) * nsamp));
-  DIAG_CHECK(hipMalloc(&cols, sizeof(int) * nsamp));
+  DevBuf bA, bBt, bC, bref, brows, bcols, bgot;
+  DIAG_CHECK(bA.alloc(device, sizeof(__bf16) * static_cast<size_t>(M) * K));
+  DIAG_CHECK(bBt.alloc(device, sizeof(__bf16) * static_cast<size_t>(N) * K));
+  DIAG_CHECK(bC.alloc(device, sizeof(float) * static_cast<size_t>(M) * N));
+  DIAG_CHECK(bref.alloc(device, sizeof(float) * nsamp));
+  DIAG_CHECK(brows.alloc(device, sizeof(int) * nsamp));
+  DIAG_CHECK(bcols.alloc(device, sizeof(int) * nsamp));
+  DIAG_CHECK(bgot.alloc(device, sizeof(float) * nsamp));
+  __bf16* A = static_cast<__bf16*>(bA.ptr);
+  __bf16* Bt = static_cast<__bf16*>(bBt.ptr);
+  float* C = static_cast<float*>(bC.ptr);
+  float* ref = static_cast<float*>(bref.ptr);
+  int* rows = static_cast<int*>(brows.ptr);
+  int* cols = static_cast<int*>(bcols.ptr);
   hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, A, static_cast<size_t>(M) * K, 0x1234ULL);
   hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, Bt, static_cast<size_t>(N) * K, 0xBEEFULL);
   DIAG_CHECK(hipGetLastError());
@@ -1098,8 +1124,9 @@ int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int n
   }
   DIAG_CHECK(hipMemcpy(rows, hr.data(), sizeof(int) * nsamp, hipMemcpyHostToDevice));
   DIAG_CHECK(hipMemcpy(cols, hc.data(), sizeof(int) * nsamp, hipMemcpyHostToDevice));
-  DIAG_CHECK(hipEventCreate(&e0));
-  DIAG_CHECK(hipEventCreate(&e1));
+  Timer tm;
+  DIAG_CHECK(tm.create());
+  hipEvent_t e0 = tm.e0, e1 = tm.e1;
   for (int i = 0; i < warmup; ++i)
     if (diag_gemm_bf16_launch(A, Bt, C, M, N, K, nullptr)) return -1;
   DIAG_CHECK(hipEventRecord(e0, nullptr));
@@ -1112,14 +1139,12 @@ int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int n
                      nsamp, K);
   DIAG_CHECK(hipGetLastError());
   // gather the sampled outputs on the device: one copy instead of nsamp tiny ones
-  float* got = nullptr;
-  DIAG_CHECK(hipMalloc(&got, sizeof(float) * nsamp));
+  float* got = static_cast<float*>(bgot.ptr);
   hipLaunchKernelGGL(gather_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, C, rows, cols, got, nsamp, N);
   DIAG_CHECK(hipGetLastError());
   std::vector<float> href(nsamp), hC(nsamp);
   DIAG_CHECK(hipMemcpy(href.data(), ref, sizeof(float) * nsamp, hipMemcpyDeviceToHost));
   DIAG_CHECK(hipMemcpy(hC.data(), got, sizeof(float) * nsamp, hipMemcpyDeviceToHost));
-  hipFree(got);
   double worst = 0.0;
   for (int i = 0; i < nsamp; ++i) {
     const double denom = std::max(1.0, std::fabs(static_cast<double>(href[i])));
@@ -1128,14 +1153,6 @@ int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int n
   *max_rel_err = worst;
   *ms_per_iter = ms;
   *tflops = 2.0 * M * N * static_cast<double>(K) / (ms * 1e-3) / 1e12;
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipFree(A);
-  hipFree(Bt);
-  hipFree(C);
-  hipFree(ref);
-  hipFree(rows);
-  hipFree(cols);
   return 0;
 }
 
@@ -1174,17 +1191,15 @@ int diag_gemm_fp8(int device, int M, int N, int K, int warmup, int iters, int ns
   float* c = static_cast<float*>(C.ptr);
   for (int i = 0; i < warmup; ++i)
     if (diag_gemm_fp8_launch(A.ptr, Bt.ptr, c, M, N, K, nullptr)) return -1;
-  hipEvent_t e0, e1;
-  DIAG_CHECK(hipEventCreate(&e0));
-  DIAG_CHECK(hipEventCreate(&e1));
+  Timer tm;
+  DIAG_CHECK(tm.create());
+  hipEvent_t e0 = tm.e0, e1 = tm.e1;
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   for (int i = 0; i < iters; ++i)
     if (diag_gemm_fp8_launch(A.ptr, Bt.ptr, c, M, N, K, nullptr)) return -1;
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   const double ms = elapsed_ms(e0, e1) / std::max(iters, 1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   const int* r = static_cast<const int*>(rows.ptr);
   const int* cl = static_cast<const int*>(cols.ptr);
   hipLaunchKernelGGL(gemm_ref_fp8_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr,
@@ -1211,18 +1226,20 @@ int diag_gemm_fp8(int device, int M, int N, int K, int warmup, int iters, int ns
 int diag_hbm_bandwidth(int device, size_t bytes, int iters, double* copy_tbs, double* read_tbs, double* write_tbs) {
   DIAG_CHECK(hipSetDevice(device));
   const size_t n = bytes / sizeof(f32x4);
-  f32x4 *a = nullptr, *b = nullptr;
-  float* sink = nullptr;
-  DIAG_CHECK(hipMalloc(&a, n * sizeof(f32x4)));
-  DIAG_CHECK(hipMalloc(&b, n * sizeof(f32x4)));
-  DIAG_CHECK(hipMalloc(&sink, sizeof(float)));
+  DevBuf ba, bb, bsink;
+  DIAG_CHECK(ba.alloc(device, n * sizeof(f32x4)));
+  DIAG_CHECK(bb.alloc(device, n * sizeof(f32x4)));
+  DIAG_CHECK(bsink.alloc(device, sizeof(float)));
+  f32x4* a = static_cast<f32x4*>(ba.ptr);
+  f32x4* b = static_cast<f32x4*>(bb.ptr);
+  float* sink = static_cast<float*>(bsink.ptr);
   const unsigned grid = flat_grid(n);
   hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, a, n, 1.0f);
   hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, b, n, 2.0f);
   DIAG_CHECK(hipGetLastError());
-  hipEvent_t e0, e1;
-  DIAG_CHECK(hipEventCreate(&e0));
-  DIAG_CHECK(hipEventCreate(&e1));
+  Timer tm;
+  DIAG_CHECK(tm.create());
+  hipEvent_t e0 = tm.e0, e1 = tm.e1;
   const size_t nb = n * sizeof(f32x4);
   // copy
   hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, nullptr, a, b, n);
@@ -1246,11 +1263,6 @@ int diag_hbm_bandwidth(int device, size_t bytes, int iters, double* copy_tbs, do
   DIAG_CHECK(hipEventSynchronize(e1));
   *write_tbs = 1.0 * nb * iters / (elapsed_ms(e0, e1) * 1e-3) / 1e12;
   DIAG_CHECK(hipGetLastError());
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipFree(a);
-  hipFree(b);
-  hipFree(sink);
   return 0;
 }
 
@@ -1259,16 +1271,17 @@ int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned l
                  unsigned long long* first_bad_byte, double* gbps) {
   DIAG_CHECK(hipSetDevice(device));
   const size_t n = bytes / sizeof(uint4);
-  uint4* p = nullptr;
-  unsigned long long* dev = nullptr;
-  DIAG_CHECK(hipMalloc(&p, n * sizeof(uint4)));
-  DIAG_CHECK(hipMalloc(&dev, 2 * sizeof(unsigned long long)));
+  DevBuf bp, bdev;
+  DIAG_CHECK(bp.alloc(device, n * sizeof(uint4)));
+  DIAG_CHECK(bdev.alloc(device, 2 * sizeof(unsigned long long)));
+  uint4* p = static_cast<uint4*>(bp.ptr);
+  unsigned long long* dev = static_cast<unsigned long long*>(bdev.ptr);
   const unsigned long long init[2] = {0ULL, ~0ULL};
   DIAG_CHECK(hipMemcpy(dev, init, sizeof init, hipMemcpyHostToDevice));
   const unsigned grid = flat_grid(n);
-  hipEvent_t e0, e1;
-  DIAG_CHECK(hipEventCreate(&e0));
-  DIAG_CHECK(hipEventCreate(&e1));
+  Timer tm;
+  DIAG_CHECK(tm.create());
+  hipEvent_t e0 = tm.e0, e1 = tm.e1;
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   for (int pass = 0; pass < passes; ++pass) {
     for (int inv = 0; inv < 2; ++inv) {
@@ -1285,10 +1298,6 @@ int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned l
   *errors = h[0];
   *first_bad_byte = h[0] ? h[1] * sizeof(uint4) : ~0ULL;
   *gbps = 4.0 * passes * static_cast<double>(n * sizeof(uint4)) / (elapsed_ms(e0, e1) * 1e-3) / 1e9;
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipFree(p);
-  hipFree(dev);
   return 0;
 }
 
@@ -1335,20 +1344,16 @@ int diag_p2p_copy(int src, int dst, size_t bytes, int iters, double* gbps, unsig
   DIAG_CHECK(hipDeviceSynchronize());
   // timed copies on a stream of the source device
   DIAG_CHECK(hipSetDevice(src));
-  hipStream_t st;
-  DIAG_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  hipEvent_t e0, e1;
-  DIAG_CHECK(hipEventCreate(&e0));
-  DIAG_CHECK(hipEventCreate(&e1));
+  Timer tm;
+  DIAG_CHECK(tm.create(true));
+  hipEvent_t e0 = tm.e0, e1 = tm.e1;
+  hipStream_t st = tm.stream;
   DIAG_CHECK(hipMemcpyPeerAsync(b.ptr, dst, a.ptr, src, nbytes, st));  // warm-up (maps, engine)
   DIAG_CHECK(hipEventRecord(e0, st));
   for (int i = 0; i < iters; ++i) DIAG_CHECK(hipMemcpyPeerAsync(b.ptr, dst, a.ptr, src, nbytes, st));
   DIAG_CHECK(hipEventRecord(e1, st));
   DIAG_CHECK(hipEventSynchronize(e1));
   const float ms = elapsed_ms(e0, e1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  (void)hipStreamDestroy(st);
   *gbps = ms > 0.f ? static_cast<double>(iters) * static_cast<double>(nbytes) / (ms * 1e-3) / 1e9 : 0.0;
   // verify what arrived
   DIAG_CHECK(hipSetDevice(dst));
@@ -1466,17 +1471,15 @@ int diag_mfma_burn_map(int device, int kind, int iters, int reps, double* tflops
   launch();  // warm-up (also checked)
   DIAG_CHECK(hipGetLastError());
   DIAG_CHECK(hipDeviceSynchronize());
-  hipEvent_t e0, e1;
-  DIAG_CHECK(hipEventCreate(&e0));
-  DIAG_CHECK(hipEventCreate(&e1));
+  Timer tm;
+  DIAG_CHECK(tm.create());
+  hipEvent_t e0 = tm.e0, e1 = tm.e1;
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   for (int r = 0; r < reps; ++r) launch();
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   DIAG_CHECK(hipGetLastError());
   const float ms = elapsed_ms(e0, e1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   DIAG_CHECK(hipMemcpy(errors, dcnt.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   if (cu_map != nullptr) DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   const double flop = static_cast<double>(blocks) * 4 /*waves*/ * iters * 16 /*MFMA per iter*/ * 2.0 * 16 * 16 * K;
@@ -1510,9 +1513,9 @@ int diag_lds_test(int device, int rounds, uint32_t seed, int inject_block, unsig
   DIAG_CHECK(hipMemset(derr.ptr, 0, sizeof(unsigned long long)));
   DIAG_CHECK(hipMemset(dmap.ptr, 0, map_bytes));
   const int blocks = grid_for(device, rounds);
-  hipEvent_t e0, e1;
-  DIAG_CHECK(hipEventCreate(&e0));
-  DIAG_CHECK(hipEventCreate(&e1));
+  Timer tm;
+  DIAG_CHECK(tm.create());
+  hipEvent_t e0 = tm.e0, e1 = tm.e1;
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   hipLaunchKernelGGL(lds_test_kernel, dim3(blocks), dim3(1024), dyn, nullptr, dyn / 4u, seed, inject_block,
                      static_cast<unsigned long long*>(derr.ptr), static_cast<unsigned long long*>(dmap.ptr));
@@ -1520,8 +1523,6 @@ int diag_lds_test(int device, int rounds, uint32_t seed, int inject_block, unsig
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   *ms = elapsed_ms(e0, e1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   DIAG_CHECK(hipMemcpy(errors, derr.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   *lds_bytes = static_cast<int>(dyn);
@@ -1559,17 +1560,15 @@ int diag_l2_bandwidth(int device, size_t slice_bytes, int passes, int blocks_per
   DIAG_CHECK(hipDeviceSynchronize());
   DIAG_CHECK(hipMemset(derr.ptr, 0, sizeof(unsigned long long)));
   DIAG_CHECK(hipMemset(dmap.ptr, 0, map_bytes));
-  hipEvent_t e0, e1;
-  DIAG_CHECK(hipEventCreate(&e0));
-  DIAG_CHECK(hipEventCreate(&e1));
+  Timer tm;
+  DIAG_CHECK(tm.create());
+  hipEvent_t e0 = tm.e0, e1 = tm.e1;
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   launch();
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   DIAG_CHECK(hipGetLastError());
   const float ms = elapsed_ms(e0, e1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   DIAG_CHECK(hipMemcpy(errors, derr.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   const double bytes = static_cast<double>(blocks) * passes * static_cast<double>(slice_bytes);
@@ -1594,11 +1593,10 @@ int diag_host_link(int device, size_t bytes, int iters, double* h2d_gbps, double
   memset(host, 0x5A, bytes);
   DevBuf dev;
   DIAG_CHECK(dev.alloc(device, bytes));
-  hipStream_t st;
-  DIAG_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  hipEvent_t e0, e1;
-  DIAG_CHECK(hipEventCreate(&e0));
-  DIAG_CHECK(hipEventCreate(&e1));
+  Timer tm;
+  DIAG_CHECK(tm.create(true));
+  hipEvent_t e0 = tm.e0, e1 = tm.e1;
+  hipStream_t st = tm.stream;
   for (int dir = 0; dir < 2; ++dir) {
     auto copy = [&]() {
       return dir == 0 ? hipMemcpyAsync(dev.ptr, host, bytes, hipMemcpyHostToDevice, st)
@@ -1613,9 +1611,6 @@ int diag_host_link(int device, size_t bytes, int iters, double* h2d_gbps, double
     const double gbps = ms > 0.f ? static_cast<double>(iters) * static_cast<double>(bytes) / (ms * 1e-3) / 1e9 : 0.0;
     *(dir == 0 ? h2d_gbps : d2h_gbps) = gbps;
   }
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  (void)hipStreamDestroy(st);
   return 0;
 }
 

@@ -56,6 +56,7 @@ struct StdoutToStderr {
   do {                                                                        \
     hipError_t e_ = (expr);                                                   \
     if (e_ != hipSuccess) {                                                   \
+      (void)hipGetLastError(); /* not left for the next call's check */      \
       g_err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
       return -1;                                                              \
     }                                                                         \

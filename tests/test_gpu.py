@@ -225,6 +225,29 @@ def test_diag_memtest_clean(dev):
     assert r["errors"] == 0 and r["pass"], r
 
 
+def test_diag_failed_allocation_leaks_nothing(dev):
+    """A diagnostic that runs out of device memory half-way (the agent's GPU got busy) frees what it
+    already took and leaves no error behind for the next call: the agent calls these for the life
+    of its pod."""
+    import ctypes
+    import torch
+    from k8s_gpu_node_checker_amd.ops import diag
+    L = diag.lib()
+    torch.cuda.synchronize()
+    free0, total = torch.cuda.mem_get_info(0)
+    d = [ctypes.c_double() for _ in range(3)]
+    big = int(free0 * 0.7) // (1 << 20) << 20  # the first buffer fits, the second cannot
+    for _ in range(3):
+        assert L.diag_hbm_bandwidth(0, big, 1, *(ctypes.byref(x) for x in d)) == -1
+        assert b"out of memory" in L.diag_last_error().lower()
+        m = 393216  # C alone is 618 GB; A and Bt (805 MB each) are allocated first
+        assert L.diag_gemm_bf16(0, m, m, 1024, 0, 1, 16, *(ctypes.byref(x) for x in d)) == -1
+    free1, _ = torch.cuda.mem_get_info(0)
+    assert free0 - free1 < (256 << 20), (free0, free1)
+    r = diag.hbm(0, gib=0.5, iters=2)  # and the next call runs clean
+    assert r["pass"], r
+
+
 def test_agent_with_diagnostics_is_healthy(dev):
     from k8s_gpu_node_checker_amd.agent.agent import Agent
     from k8s_gpu_node_checker_amd.models.health import HealthExpectations, evaluate_report
