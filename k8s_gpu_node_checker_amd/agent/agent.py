@@ -156,6 +156,14 @@ def node_event(node: str, verdict: Verdict, previous: Optional[str], namespace: 
             "firstTimestamp": ts, "lastTimestamp": ts, "count": 1}
 
 
+class PublishError(RuntimeError):
+    """Some of a publish's writes failed (message: which, and why); ``wrote`` is what did go out."""
+
+    def __init__(self, message: str, wrote: Dict[str, bool]):
+        super().__init__(message)
+        self.wrote = wrote
+
+
 class Agent:
     def __init__(self, node: str, source: str = "auto", fixture: Optional[str] = None, diag_level: int = 0,
                  diag_interval: float = 3600.0, devices: Optional[List[int]] = None,
@@ -360,8 +368,12 @@ class Agent:
         return None if got is None else {normalize_bdf(k): v for k, v in got.items()}
 
     def probe_once(self) -> Dict[str, Any]:
-        from ..ops.amdsmi_probe import probe
-        rep = probe(self.node, self.source, self.fixture)
+        from ..ops.amdsmi_probe import SCHEMA, probe
+        try:
+            rep = probe(self.node, self.source, self.fixture)
+        except Exception as e:  # a probe that cannot run is an unknown verdict, published, not a crash loop
+            rep = {"schema": SCHEMA, "node": self.node, "ts": time.time(), "gpus": [],
+                   "error": f"probe: {type(e).__name__}: {e}"[:300]}
         self._throttle_windows(rep)
         gpus = rep.get("gpus") or []
         diags = self._diagnostics(gpus)
@@ -428,33 +440,52 @@ class Agent:
         digest = report_digest(rep)
         now = time.monotonic()
         wrote = {"annotation": False, "condition": False, "event": False, "taint": False, "labels": False}
+        # each write stands alone: a rejected annotation (e.g. the node's 256 KiB annotation budget) or
+        # label/taint PATCH must not stop the condition heartbeat the checker gates on.  A failed write
+        # keeps its old state, so it is retried at the next publish; the errors are raised together at
+        # the end for the caller to log.
+        errors: List[str] = []
+
+        def attempt(what: str, fn: Any) -> None:
+            try:
+                fn()
+            except Exception as e:
+                errors.append(f"{what}: {e}")
         if force or digest != self._annotated or now - self._annotated_at >= self.annotation_refresh:
-            client.patch_node_annotations(self.node, self.annotation(rep))
-            self._annotated, self._annotated_at = digest, now
-            wrote["annotation"] = True
+            def annotate() -> None:
+                client.patch_node_annotations(self.node, self.annotation(rep))
+                self._annotated, self._annotated_at = digest, now
+                wrote["annotation"] = True
+            attempt("annotation", annotate)
         cond = self.condition(rep)
         key = (cond.get("status"), cond.get("reason"), cond.get("message"))
         if force or key != self._cond_key or now - self._cond_at >= self.heartbeat_interval:
-            self.observe_node(client.patch_node_condition(self.node, cond))  # the response is the Node
-            self._cond_key, self._cond_at = key, now
-            wrote["condition"] = True
+            def heartbeat() -> None:
+                self.observe_node(client.patch_node_condition(self.node, cond))  # the response is the Node
+                self._cond_key, self._cond_at = key, now
+                wrote["condition"] = True
+            attempt("condition", heartbeat)
         v = self._verdict
-        if v is None:
-            return wrote
-        if self.label_node:
+        if v is not None and self.label_node:
             labels = node_labels(rep, v.state)
             if labels != self._labels:
-                client.patch_node_labels(self.node, labels)  # raises -> retried next publish
-                self._labels = labels
-                wrote["labels"] = True
-        if self.events and v.state != self._event_state:
+                def relabel() -> None:
+                    client.patch_node_labels(self.node, labels)
+                    self._labels = labels
+                    wrote["labels"] = True
+                attempt("labels", relabel)
+        if v is not None and self.events and v.state != self._event_state:
             prev, self._event_state = self._event_state, v.state
             if prev is not None or v.state != HEALTHY:  # an agent (re)starting on a healthy node is no news
                 wrote["event"] = self._post_event(client, v, prev)
         # UNKNOWN (probe failed) leaves the taint as it is: a flaky probe must not flap scheduling
-        if self.taint_unhealthy and v.state != UNKNOWN and v.state != self._taint_state:
-            wrote["taint"] = self._sync_taint(client, v.state == UNHEALTHY)  # raises -> retried next publish
-            self._taint_state = v.state
+        if v is not None and self.taint_unhealthy and v.state != UNKNOWN and v.state != self._taint_state:
+            def taint() -> None:
+                wrote["taint"] = self._sync_taint(client, v.state == UNHEALTHY)
+                self._taint_state = v.state
+            attempt("taint", taint)
+        if errors:
+            raise PublishError("; ".join(errors), wrote)
         return wrote
 
     def _post_event(self, client: Any, verdict: Verdict, previous: Optional[str]) -> bool:

@@ -187,3 +187,41 @@ def test_label_values_are_valid_kubernetes_labels():
     rep.pop("driver")
     lab = A.node_labels(rep, "degraded")
     assert lab["amd.com/gpu.compute-partition"] == "mixed" and lab["amd.com/gpu.driver"] is None
+
+
+def test_rejected_annotation_never_blocks_the_condition(mock_cluster, fixture_report):
+    """A failed annotation / label / taint write is reported, the condition heartbeat still goes out,
+    and the failed write is retried at the next publish."""
+    srv = mock_cluster([fixtures.realistic_node("n")])
+    ag = A.Agent("n", source="fixture", fixture=fixture_report, label_node=True, taint_unhealthy=True)
+    with KubeClient(ClusterConnection(srv.url)) as kc:
+        real = kc.patch_node_annotations, kc.patch_node_labels
+
+        def too_big(node, ann):
+            raise ApiException(422, "Unprocessable Entity", body="metadata.annotations: Too long: must have at most "
+                                                                 "262144 bytes")
+
+        def no_labels(node, labels):
+            raise ApiException(403, "Forbidden", body="nodes is forbidden")
+        kc.patch_node_annotations, kc.patch_node_labels = too_big, no_labels
+        with pytest.raises(A.PublishError) as ei:
+            ag.publish(kc, _bad(ag))
+        assert "annotation: " in str(ei.value) and "Too long" in str(ei.value) and "labels: " in str(ei.value)
+        assert ei.value.wrote["condition"] and ei.value.wrote["taint"] and not ei.value.wrote["annotation"]
+        hc = [c for c in kc.get_node("n")["status"]["conditions"] if c["type"] == "AMDGPUHealthy"][0]
+        assert hc["status"] == "False"
+        kc.patch_node_annotations, kc.patch_node_labels = real
+        w = ag.publish(kc, _bad(ag))  # same verdict: only the writes that failed go out again
+        assert w["annotation"] and w["labels"] and not w["condition"] and not w["taint"]
+        assert kc.get_node("n")["metadata"]["labels"]["amd.com/mi355x-health"] == "unhealthy"
+
+
+def test_probe_that_cannot_run_publishes_unknown(mock_cluster, tmp_path):
+    srv = mock_cluster([fixtures.realistic_node("n")])
+    ag = A.Agent("n", source="fixture", fixture=str(tmp_path / "gone.json"))
+    rep = ag.probe_once()
+    assert rep["state"] == "unknown" and rep["error"].startswith("probe: ") and "gone.json" in rep["error"]
+    with KubeClient(ClusterConnection(srv.url)) as kc:
+        assert ag.publish(kc, rep)["condition"]
+        hc = [c for c in kc.get_node("n")["status"]["conditions"] if c["type"] == "AMDGPUHealthy"][0]
+        assert hc["status"] == "Unknown"
