@@ -733,13 +733,15 @@ def main(argv: Optional[List[str]] = None) -> int:
         rep = agent.probe_once()
         if "stdout" in pubs:
             print(json.dumps(rep, separators=(",", ":")), flush=True)
+        published = True
         if client is not None:
             try:
                 agent.publish(client, rep)
             except Exception as e:
+                published = False
                 print(f"node status publish failed: {e}", file=sys.stderr, flush=True)
-        if args.once:
-            return 0
+        if args.once:  # a one-shot run (CI, a harness) says whether the node saw its verdict
+            return 0 if published else 1
         time.sleep(max(0.0, args.interval - (time.monotonic() - started)))
 
 

@@ -225,3 +225,11 @@ def test_probe_that_cannot_run_publishes_unknown(mock_cluster, tmp_path):
         assert ag.publish(kc, rep)["condition"]
         hc = [c for c in kc.get_node("n")["status"]["conditions"] if c["type"] == "AMDGPUHealthy"][0]
         assert hc["status"] == "Unknown"
+
+
+def test_agent_once_exit_code_reflects_publish(mock_cluster, fixture_report, tmp_path):
+    srv = mock_cluster([fixtures.realistic_node("n")])
+    kc = srv.kubeconfig(str(tmp_path / "kc"))
+    base = ["--source", "fixture", "--fixture", fixture_report, "--once", "--kubeconfig", kc]
+    assert A.main(["--node", "n"] + base) == 0
+    assert A.main(["--node", "no-such-node"] + base) == 1  # every write 404s
