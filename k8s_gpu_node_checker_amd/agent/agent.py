@@ -537,7 +537,10 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
     for g in rep.get("gpus") or []:
         lbl = f'gpu="{g.get("index")}",bdf="{_esc(g.get("bdf", ""))}"'
         for key, metric in (("ecc_uncorrectable", "ecc_uncorrectable"), ("pcie_width", "pcie_width"),
-                            ("pcie_replays", "pcie_replays"), ("xgmi_error", "xgmi_error_status")):
+                            ("pcie_replays", "pcie_replays"), ("xgmi_error", "xgmi_error_status"),
+                            ("bad_pages", "retired_pages"), ("bad_pages_pending", "retired_pages_pending"),
+                            ("bad_pages_unreservable", "retired_pages_unreservable"),
+                            ("bad_page_threshold", "retired_page_threshold")):
             if isinstance(g.get(key), int) and not isinstance(g.get(key), bool):
                 put(f"mi355x_gpu_{metric}", lbl, g[key])
         if isinstance(g.get("xgmi"), str):

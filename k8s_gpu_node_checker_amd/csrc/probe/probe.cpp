@@ -33,6 +33,16 @@ std::vector<amdsmi_processor_handle> g_handles;
 // per-handle firmware JSON object; firmware only changes across a driver reload, which also
 // invalidates the handles, so it is read once per open (amdsmi_get_fw_info reads ~80 sysfs files)
 std::vector<std::string> g_fw;
+// per-handle RAS retirement state that is costly or static: the driver's bad-page threshold (a module
+// parameter, fixed per load) and the RAS EEPROM checksum, validated again only when the retired-page
+// count moved (the driver writes the EEPROM when it retires a page).  Both need root; -1 = not known.
+struct RasCache {
+  bool threshold_read = false;
+  int64_t threshold = -1;
+  int64_t eeprom = -1;  // 1 valid, 0 corrupted
+  int64_t eeprom_pages = -1;
+};
+std::vector<RasCache> g_ras;
 
 void jstr(std::string& o, const char* s) {
   o.push_back('"');
@@ -109,6 +119,7 @@ int open_locked() {
     }
   }
   g_fw.assign(g_handles.size(), std::string());
+  g_ras.assign(g_handles.size(), RasCache());
   g_open = true;
   g_gpus.store(static_cast<int>(g_handles.size()), std::memory_order_relaxed);
   return 0;
@@ -149,6 +160,42 @@ const std::string& firmware_locked(size_t i) {
   }
   s.push_back('}');
   return s;
+}
+
+// Retired HBM pages: the total, and by status -- "pending" pages are marked bad and leave service at the
+// next reset window, "unreservable" ones the driver could not take out of service (a bad page still in
+// use).  Then the driver's retirement threshold (the GPU is declared bad once the count reaches it) and
+// whether the RAS EEPROM that persists the list across reboots still checksums.
+void probe_bad_pages(std::string& o, amdsmi_processor_handle h, RasCache& rc) {
+  uint32_t n = 0;
+  if (amdsmi_get_gpu_bad_page_info(h, &n, nullptr) == AMDSMI_STATUS_SUCCESS) {
+    kv_u64(o, "bad_pages", n);
+    if (n > 0) {
+      std::vector<amdsmi_retired_page_record_t> rec(std::min<uint32_t>(n, 1u << 16));
+      uint32_t got = static_cast<uint32_t>(rec.size());
+      if (amdsmi_get_gpu_bad_page_info(h, &got, rec.data()) == AMDSMI_STATUS_SUCCESS) {
+        uint64_t pending = 0, unreservable = 0;
+        for (uint32_t i = 0; i < got && i < rec.size(); ++i) {
+          pending += rec[i].status == AMDSMI_MEM_PAGE_STATUS_PENDING;
+          unreservable += rec[i].status == AMDSMI_MEM_PAGE_STATUS_UNRESERVABLE;
+        }
+        kv_u64(o, "bad_pages_pending", pending);
+        kv_u64(o, "bad_pages_unreservable", unreservable);
+      }
+    }
+  }
+  if (!rc.threshold_read) {
+    rc.threshold_read = true;
+    uint32_t t = 0;
+    if (amdsmi_get_gpu_bad_page_threshold(h, &t) == AMDSMI_STATUS_SUCCESS) rc.threshold = t;
+  }
+  if (rc.threshold >= 0) kv_u64(o, "bad_page_threshold", static_cast<uint64_t>(rc.threshold));
+  if (rc.eeprom_pages != static_cast<int64_t>(n)) {
+    rc.eeprom_pages = n;
+    const amdsmi_status_t st = amdsmi_gpu_validate_ras_eeprom(h);
+    rc.eeprom = st == AMDSMI_STATUS_SUCCESS ? 1 : st == AMDSMI_STATUS_CORRUPTED_EEPROM ? 0 : -1;
+  }
+  if (rc.eeprom >= 0) kv_str(o, "ras_eeprom", rc.eeprom ? "ok" : "corrupted");
 }
 
 // RAS blocks, named as the kernel's ras sysfs does; asked only when the totals are non-zero, so a clean
@@ -414,8 +461,7 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
   } else {
     kv_null(o, "ecc_uncorrectable");
   }
-  uint32_t pages = 0;
-  if (amdsmi_get_gpu_bad_page_info(h, &pages, nullptr) == AMDSMI_STATUS_SUCCESS) kv_u64(o, "bad_pages", pages);
+  probe_bad_pages(o, h, g_ras[static_cast<size_t>(index)]);
   probe_cper(o, h);
 
   amdsmi_xgmi_link_status_t xs;
@@ -588,5 +634,6 @@ extern "C" void mi355x_probe_close(void) {
     g_open = false;
     g_handles.clear();
     g_fw.clear();
+    g_ras.clear();
   }
 }

@@ -363,10 +363,25 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float
                 warn.append(f"gpu{idx}: uncorrected non-fatal RAS error record (CPER) at {last_u or '?'}")
     bp = g.get("bad_pages")
     if isinstance(bp, int):
-        if bp > exp.bad_page_limit:
+        # the driver's own retirement threshold when the probe could read it (root), else the fixed limit;
+        # past 90 % of the threshold the GPU is a reset or two from being declared bad by the driver
+        thr = g.get("bad_page_threshold")
+        limit = thr if isinstance(thr, int) and thr > 0 else None
+        if limit is not None and bp >= limit:
+            fail.append(f"gpu{idx}: {bp} retired pages reached the driver's threshold {limit}")
+        elif limit is None and bp > exp.bad_page_limit:
             fail.append(f"gpu{idx}: {bp} retired pages > {exp.bad_page_limit}")
+        elif limit is not None and bp >= 0.9 * limit:
+            warn.append(f"gpu{idx}: {bp} retired pages, {limit} is the driver's threshold")
         elif bp > 0:
             warn.append(f"gpu{idx}: {bp} retired pages")
+    unres, pend = g.get("bad_pages_unreservable"), g.get("bad_pages_pending")
+    if isinstance(unres, int) and unres > 0:
+        fail.append(f"gpu{idx}: {unres} bad HBM page(s) could not be retired (still in use)")
+    if isinstance(pend, int) and pend > 0:
+        warn.append(f"gpu{idx}: {pend} bad HBM page(s) pending retirement (retired at the next GPU reset)")
+    if g.get("ras_eeprom") == "corrupted":
+        fail.append(f"gpu{idx}: RAS EEPROM checksum invalid (the retired-page list may not survive a reboot)")
     links = g.get("xgmi")
     if isinstance(links, str) and exp.xgmi_links > 0:
         up, down = links.count("U"), links.count("D")

@@ -251,6 +251,29 @@ def _xgmi_fabric_python(A: Any, h: Any, q: Any) -> Dict[str, Any]:
     return out
 
 
+def _bad_pages_python(A: Any, h: Any, q: Any) -> Dict[str, Any]:
+    """The native probe's ``probe_bad_pages`` fields (csrc/probe/probe.cpp): retired pages by status
+    (1 = pending, 2 = unreservable), the driver's threshold and the RAS EEPROM checksum (both root-only)."""
+    out: Dict[str, Any] = {}
+    bp = q(A.amdsmi_get_gpu_bad_page_info)
+    out["bad_pages"] = len(bp) if isinstance(bp, list) else None
+    if isinstance(bp, list) and bp:
+        st = [r.get("status") if isinstance(r, dict) else None for r in bp]
+        out["bad_pages_pending"] = sum(1 for s in st if int(s or 0) == 1)
+        out["bad_pages_unreservable"] = sum(1 for s in st if int(s or 0) == 2)
+    thr = q(A.amdsmi_get_gpu_bad_page_threshold)
+    if isinstance(thr, int) and not isinstance(thr, bool):
+        out["bad_page_threshold"] = thr
+    try:
+        A.amdsmi_gpu_validate_ras_eeprom(h)
+        out["ras_eeprom"] = "ok"
+    except Exception as e:  # AMDSMI_STATUS_CORRUPTED_EEPROM (56); anything else (NO_PERM, ...) = unknown
+        code = e.get_error_code() if hasattr(e, "get_error_code") else None
+        if code == 56:
+            out["ras_eeprom"] = "corrupted"
+    return out
+
+
 def probe_python(node: str) -> Dict[str, Any]:
     rep: Dict[str, Any] = {"schema": SCHEMA, "node": node, "ts": time.time(), "probe": "python", "gpus": []}
     t0 = time.perf_counter()
@@ -299,8 +322,7 @@ def probe_python(node: str) -> Dict[str, Any]:
                           "ecc_deferred": ecc.get("deferred_count")})
                 if any(_int(ecc.get(k)) for k in ("correctable_count", "uncorrectable_count", "deferred_count")):
                     g["ecc_blocks"] = _ecc_blocks_python(A, h)
-            bp = q(A.amdsmi_get_gpu_bad_page_info)
-            g["bad_pages"] = len(bp) if isinstance(bp, list) else None
+            g.update(_bad_pages_python(A, h, q))
             g.update(_cper_python(A, h))
             g["xgmi"] = _xgmi_string(q(A.amdsmi_get_gpu_xgmi_link_status))
             xe = q(A.amdsmi_gpu_xgmi_error_status)

@@ -414,12 +414,40 @@ amdsmi_status_t amdsmi_get_gpu_bad_page_info(amdsmi_processor_handle processor_h
       memset(&info[i], 0, sizeof info[i]);
       info[i].page_address = 0x1000ull * (i + 1);
       info[i].page_size = 4096;
+      // bad_page_status: one letter per record, r(eserved) p(ending) u(nreservable); reserved by default
+      const std::string st = g->s("bad_page_status");
+      const char c = i < st.size() ? st[i] : 'r';
+      info[i].status = c == 'p' ? AMDSMI_MEM_PAGE_STATUS_PENDING
+                     : c == 'u' ? AMDSMI_MEM_PAGE_STATUS_UNRESERVABLE : AMDSMI_MEM_PAGE_STATUS_RESERVED;
     }
     *num_pages = cap;
   } else {
     *num_pages = n;
   }
   return AMDSMI_STATUS_SUCCESS;
+}
+
+// bad_page_threshold=N, or bad_page_threshold=noperm (non-root, as on a real box)
+amdsmi_status_t amdsmi_get_gpu_bad_page_threshold(amdsmi_processor_handle processor_handle, uint32_t* threshold) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("bad_page_threshold");
+  if (g->s("bad_page_threshold") == "noperm") return AMDSMI_STATUS_NO_PERM;
+  *threshold = static_cast<uint32_t>(g->u("bad_page_threshold"));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+// ras_eeprom=ok|corrupted|noperm; validations counted in the scenario-visible call log
+amdsmi_status_t amdsmi_gpu_validate_ras_eeprom(amdsmi_processor_handle processor_handle) {
+  GPU_OR_FAIL(processor_handle);
+  FIELD_OR_NA("ras_eeprom");
+  const std::string v = g->s("ras_eeprom");
+  if (const char* log = getenv("AMDSMI_STUB_EEPROM_LOG")) {
+    if (FILE* fp = fopen(log, "a")) {
+      fputs("validate\n", fp);
+      fclose(fp);
+    }
+  }
+  return v == "ok" ? AMDSMI_STATUS_SUCCESS : v == "corrupted" ? AMDSMI_STATUS_CORRUPTED_EEPROM : AMDSMI_STATUS_NO_PERM;
 }
 
 amdsmi_status_t amdsmi_get_gpu_xgmi_link_status(amdsmi_processor_handle processor_handle,

@@ -306,3 +306,22 @@ def test_agent_gzip_annotation_read_by_the_checker(mock_cluster, tmp_path):
         assert res.exit_code == 3 and res.verdicts[0].reasons[0] == "7 of 8 GPUs visible to amd-smi"
     fleet = run_check(ClusterConnection(srv.url), CheckOptions(json_extended=True)).extended_fields()["mi355x"]["fleet"]
     assert fleet["nodes_reporting"] == 1 and fleet["driver"] == {"6.18.54": 1}
+
+
+def test_retired_pages_use_the_drivers_threshold_when_known():
+    def v(**g0):
+        rep = fixtures.mi355x_probe_report("n", gpus=1, gpu0=g0)
+        return H.evaluate_report(rep, 1, H.HealthExpectations(xgmi_links=0), now=rep["ts"])
+    # threshold known (root): the driver's line decides, the fixed 64-page limit does not apply
+    assert v(bad_pages=100, bad_page_threshold=2048).state == H.DEGRADED
+    assert v(bad_pages=100, bad_page_threshold=2048).warnings == ["gpu0: 100 retired pages"]
+    assert v(bad_pages=1900, bad_page_threshold=2048).warnings == ["gpu0: 1900 retired pages, 2048 is the "
+                                                                   "driver's threshold"]
+    r = v(bad_pages=2048, bad_page_threshold=2048)
+    assert r.state == H.UNHEALTHY and r.reasons == ["gpu0: 2048 retired pages reached the driver's threshold 2048"]
+    # unknown threshold (non-root probe): the fixed limit
+    assert v(bad_pages=65).reasons == ["gpu0: 65 retired pages > 64"]
+    assert v(bad_pages=3, bad_pages_unreservable=1).state == H.UNHEALTHY
+    assert v(bad_pages=3, bad_pages_pending=3).state == H.DEGRADED
+    assert v(ras_eeprom="ok").state == H.HEALTHY
+    assert v(ras_eeprom="corrupted").state == H.UNHEALTHY

@@ -279,3 +279,39 @@ def test_probe_cli_under_asan_pages_cper_records(asan_probe, tmp_path):
     assert r["gpus"][1]["cper_error"] == "AMDSMI_STATUS_NO_PERM" and "cper" not in r["gpus"][1]
     v = H.evaluate_report(r, 2, H.HealthExpectations(xgmi_links=0), now=H.parse_k8s_time("2026-10-16T12:00:00Z"))
     assert v.reasons == ["gpu0: fatal RAS error record (CPER) at 2026-10-16T10:15:00Z"], v.to_dict()
+
+
+@pytest.mark.slow
+def test_probe_cli_under_asan_retired_pages_threshold_eeprom(asan_probe, tmp_path):
+    """Retired HBM pages by status, the driver's threshold and the RAS EEPROM checksum (root-only: NO_PERM
+    leaves them out); the EEPROM is validated once per GPU while the page count stands still."""
+    import json
+
+    from k8s_gpu_node_checker_amd.models import health as H
+    d, _, _ = asan_probe
+    scen = scenario(tmp_path / "s.txt", gpus=3, per_gpu={
+        0: {"bad_pages": 5, "bad_page_status": "rrppu", "bad_page_threshold": 10, "ras_eeprom": "ok"},
+        1: {"bad_pages": 9, "bad_page_threshold": 10, "ras_eeprom": "corrupted"},
+        2: {"bad_page_threshold": "noperm", "ras_eeprom": "noperm"}})
+    log = tmp_path / "eeprom.log"
+    env = dict(os.environ, AMDSMI_STUB_SCENARIO=scen, AMDSMI_STUB_EEPROM_LOG=str(log), **ASAN_ENV)
+    env.pop("LD_PRELOAD", None)
+    p = subprocess.run([str(d / "mi355x-probe"), "--node", "n1", "--repeat", "3"], capture_output=True, text=True,
+                       env=env, timeout=120)
+    assert p.returncode == 0 and "ERROR: AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr, \
+        p.stderr[-3000:]
+    r = json.loads(p.stdout.splitlines()[-1])
+    pick = ("bad_pages", "bad_pages_pending", "bad_pages_unreservable", "bad_page_threshold", "ras_eeprom")
+    got = [{k: g[k] for k in pick if k in g} for g in r["gpus"]]
+    assert got == [{"bad_pages": 5, "bad_pages_pending": 2, "bad_pages_unreservable": 1, "bad_page_threshold": 10,
+                    "ras_eeprom": "ok"},
+                   {"bad_pages": 9, "bad_pages_pending": 0, "bad_pages_unreservable": 0, "bad_page_threshold": 10,
+                    "ras_eeprom": "corrupted"},
+                   {"bad_pages": 0}]
+    assert log.read_text().count("validate") == 3  # once per GPU over 3 probes: the count did not move
+    v = H.evaluate_report(r, 3, H.HealthExpectations(xgmi_links=0), now=r["ts"])
+    assert v.state == H.UNHEALTHY
+    assert v.reasons == ["gpu0: 1 bad HBM page(s) could not be retired (still in use)",
+                         "gpu1: RAS EEPROM checksum invalid (the retired-page list may not survive a reboot)"]
+    assert "gpu0: 2 bad HBM page(s) pending retirement (retired at the next GPU reset)" in v.warnings
+    assert "gpu1: 9 retired pages, 10 is the driver's threshold" in v.warnings
