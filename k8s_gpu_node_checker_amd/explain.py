@@ -9,6 +9,7 @@ the verdict rests on.  Exit code: 0 the node counts as Ready, 3 it does not, 2 n
 
 from __future__ import annotations
 
+import json
 import time
 from typing import Any, Dict, List, Optional, TextIO
 
@@ -29,75 +30,121 @@ def _age(seconds: Optional[float]) -> str:
     return f"{seconds / 3600:.1f} h"
 
 
-def _gpu_row(g: Dict[str, Any], verdict_lines: List[str]) -> List[str]:
+_COLUMNS = ("GPU", "BDF", "gfx", "CUs", "VRAM MB", "ECC ue/ce", "xGMI", "PM fw", "diag", "findings")
+
+
+def _gpu_entry(g: Dict[str, Any], verdict_lines: List[str]) -> Dict[str, Any]:
+    """One GPU of the report, reduced to the fields its verdict rests on, with its findings."""
     idx = g.get("index", "?")
     diag = g.get("diag") if isinstance(g.get("diag"), dict) else {}
-    bad_diag = sorted(t for t, r in diag.items() if isinstance(r, dict) and r.get("pass") is False)
-    slow_diag = sorted(t for t, r in diag.items() if isinstance(r, dict) and r.get("degraded"))
-    dstate = ("fail: " + ",".join(bad_diag)) if bad_diag else ("slow: " + ",".join(slow_diag)) if slow_diag else \
-        ("pass" if diag else "-")
     fw = g.get("fw") if isinstance(g.get("fw"), dict) else {}
-    mine = [ln for ln in verdict_lines if ln.startswith(f"gpu{idx}:")]
-    return [str(idx), str(g.get("bdf", "")), str(g.get("gfx", "")), str(g.get("cus", "")),
-            f"{g.get('vram_mb', '')}", f"{g.get('ecc_uncorrectable', '-')}/{g.get('ecc_correctable', '-')}",
-            str(g.get("xgmi", "")), H.fw_version_str("pm", fw["pm"]) if "pm" in fw else "-", dstate,
-            "ok" if not mine else "; ".join(m.split(": ", 1)[1] for m in mine)]
+    return {"index": idx, "bdf": g.get("bdf"), "gfx": g.get("gfx"), "cus": g.get("cus"), "vram_mb": g.get("vram_mb"),
+            "ecc_uncorrectable": g.get("ecc_uncorrectable"), "ecc_correctable": g.get("ecc_correctable"),
+            "xgmi": g.get("xgmi"), "pm_fw": H.fw_version_str("pm", fw["pm"]) if "pm" in fw else None,
+            "diag_failed": sorted(t for t, r in diag.items() if isinstance(r, dict) and r.get("pass") is False),
+            "diag_slow": sorted(t for t, r in diag.items() if isinstance(r, dict) and r.get("degraded")),
+            "diag_ran": bool(diag),
+            "findings": [ln.split(": ", 1)[1] for ln in verdict_lines if ln.startswith(f"gpu{idx}:")]}
 
 
-def explain(cluster: ClusterConnection, node_name: str, opts: CheckOptions, out: TextIO) -> int:
+def _gpu_row(e: Dict[str, Any]) -> List[str]:
+    def txt(v: Any, none: str = "") -> str:
+        return none if v is None else str(v)
+    dstate = ("fail: " + ",".join(e["diag_failed"])) if e["diag_failed"] else \
+        ("slow: " + ",".join(e["diag_slow"])) if e["diag_slow"] else ("pass" if e["diag_ran"] else "-")
+    return [txt(e["index"]), txt(e["bdf"]), txt(e["gfx"]), txt(e["cus"]), txt(e["vram_mb"]),
+            f"{txt(e['ecc_uncorrectable'], '-')}/{txt(e['ecc_correctable'], '-')}", txt(e["xgmi"]),
+            txt(e["pm_fw"], "-"), dstate, "; ".join(e["findings"]) or "ok"]
+
+
+def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> Dict[str, Any]:
+    """Everything ``--explain`` says about one node, as data (``--explain NODE --json`` prints it)."""
     opts.json_extended = True  # the full report annotation is read (annotation mode 2)
     scan = scan_cluster(cluster, opts, NullTracer())
     names = [n["name"] for n in scan.gpu_nodes]
     if node_name not in names:
-        out.write(f"{node_name}: not a GPU node in this cluster (no {', '.join(opts_keys())} capacity)\n"
-                  if scan.items_seen else f"{node_name}: no nodes listed\n")
-        return 2
+        return {"node": node_name, "gpu_node": False, "nodes_listed": scan.items_seen}
     i = names.index(node_name)
     node, ex = scan.gpu_nodes[i], scan.extras[i]
-    ready_cond = ex.ready_condition
     verdicts = apply_health(scan, opts, NullTracer(), [])
     apply_schedulability(scan, opts)
     v = verdicts[i] if i < len(verdicts) else None
-    breakdown = ", ".join(f"{k}:{c}" for k, c in node["gpu_breakdown"].items())
-    out.write(f"node {node_name}: Ready={ready_cond}  GPUs {node['gpus']} ({breakdown})"
-              f"  allocatable {ex.allocatable or '-'}{'  cordoned' if ex.unschedulable else ''}\n")
     now = time.time()
+    doc: Dict[str, Any] = {"node": node_name, "gpu_node": True, "ready_condition": ex.ready_condition,
+                           "gpus": node["gpus"], "gpu_breakdown": node["gpu_breakdown"],
+                           "allocatable": ex.allocatable, "unschedulable": ex.unschedulable,
+                           "health_policy": opts.health_policy, "health_condition": None,
+                           "verdict": v.to_dict() if v is not None else None, "report": None}
     if ex.health_condition is not None:
         status, reason, message, hb = ex.health_condition
-        out.write(f"{HEALTH_CONDITION}={status} ({reason}, heartbeat {_age(now - hb if hb else None)} ago): "
-                  f"{message}\n")
-    else:
-        out.write(f"{HEALTH_CONDITION}: not published (no node agent)\n")
-    if v is None:
-        out.write(f"MI355X verdict: none (policy {opts.health_policy}: the reference's Ready rule applies)\n")
-    else:
-        out.write(f"MI355X verdict: {v.state}, {v.gpus_ok}/{v.gpus_seen} GPUs ok"
-                  + (f", report {_age(v.age_s)} old" if v.age_s is not None else "") + "\n")
-        for title, items in (("reasons", v.reasons), ("warnings", v.warnings)):
-            for r in items:
-                out.write(f"  {title[:-1]}: {r}\n")
+        doc["health_condition"] = {"status": status, "reason": reason, "message": message,
+                                   "heartbeat_age_s": round(now - hb, 1) if hb else None}
     rep = H.parse_annotation(ex.health_annotation)
-    if rep and not rep.get("error"):
+    if rep and rep.get("error"):
+        doc["report"] = {"error": rep["error"]}
+    elif rep:
         drv = rep.get("driver") if isinstance(rep.get("driver"), dict) else {}
-        out.write(f"report: probe {rep.get('probe', '?')}, amd-smi {rep.get('amdsmi', '?')}, driver "
-                  f"{H.driver_release(drv.get('version')) or '?'}, {len(rep.get('gpus') or [])} GPUs\n")
         re_v = H.evaluate_report(rep, max(ex.capacity.get("amd.com/gpu", 0), ex.allocatable.get("amd.com/gpu", 0)),
                                  H.HealthExpectations(xgmi_links=opts.xgmi_links, max_age_s=opts.probe_max_age), now)
         lines = re_v.reasons + re_v.warnings
-        head = ["GPU", "BDF", "gfx", "CUs", "VRAM MB", "ECC ue/ce", "xGMI", "PM fw", "diag", "findings"]
-        rows = [head] + [_gpu_row(g, lines) for g in rep.get("gpus") or [] if isinstance(g, dict)]
-        widths = [max(len(r[c]) for r in rows) for c in range(len(head) - 1)]
-        for r in rows:
-            out.write("  " + "  ".join(r[c].ljust(widths[c]) for c in range(len(head) - 1)) + "  " + r[-1] + "\n")
-        shown = {f"gpu{g.get('index')}:" for g in rep.get("gpus") or [] if isinstance(g, dict)}
-        node_level = [ln for ln in lines if ln.split(" ", 1)[0] not in shown]  # incl. spans ("gpu6-7: ...")
-        for ln in node_level:
-            out.write(f"  node: {ln}\n")
-    elif rep and rep.get("error"):
+        gpus = [_gpu_entry(g, lines) for g in rep.get("gpus") or [] if isinstance(g, dict)]
+        shown = {f"gpu{e['index']}:" for e in gpus}
+        doc["report"] = {"probe": rep.get("probe"), "amdsmi": rep.get("amdsmi"),
+                         "driver": H.driver_release(drv.get("version")) if drv.get("version") else None,
+                         "gpus": gpus,
+                         # findings not about one GPU of the table, incl. spans ("... gpu0-2,4-7 ...")
+                         "node_findings": [ln for ln in lines if ln.split(" ", 1)[0] not in shown]}
+    doc["counts_as_ready"] = bool(node["ready"])
+    return doc
+
+
+def render(doc: Dict[str, Any], out: TextIO) -> None:
+    name = doc["node"]
+    if not doc["gpu_node"]:
+        out.write(f"{name}: not a GPU node in this cluster (no {', '.join(opts_keys())} capacity)\n"
+                  if doc["nodes_listed"] else f"{name}: no nodes listed\n")
+        return
+    breakdown = ", ".join(f"{k}:{c}" for k, c in doc["gpu_breakdown"].items())
+    out.write(f"node {name}: Ready={doc['ready_condition']}  GPUs {doc['gpus']} ({breakdown})"
+              f"  allocatable {doc['allocatable'] or '-'}{'  cordoned' if doc['unschedulable'] else ''}\n")
+    hc = doc["health_condition"]
+    if hc is not None:
+        out.write(f"{HEALTH_CONDITION}={hc['status']} ({hc['reason']}, heartbeat {_age(hc['heartbeat_age_s'])} ago): "
+                  f"{hc['message']}\n")
+    else:
+        out.write(f"{HEALTH_CONDITION}: not published (no node agent)\n")
+    v = doc["verdict"]
+    if v is None:
+        out.write(f"MI355X verdict: none (policy {doc['health_policy']}: the reference's Ready rule applies)\n")
+    else:
+        out.write(f"MI355X verdict: {v['state']}, {v['gpus_ok']}/{v['gpus_seen']} GPUs ok"
+                  + (f", report {_age(v['age_s'])} old" if v.get("age_s") is not None else "") + "\n")
+        for title in ("reasons", "warnings"):
+            for r in v.get(title) or []:
+                out.write(f"  {title[:-1]}: {r}\n")
+    rep = doc["report"]
+    if rep and rep.get("error"):
         out.write(f"report: unreadable ({rep['error']})\n")
-    counts = node["ready"]
-    out.write(f"=> counts as Ready: {'yes' if counts else 'no'}\n")
-    return 0 if counts else 3
+    elif rep:
+        out.write(f"report: probe {rep['probe'] or '?'}, amd-smi {rep['amdsmi'] or '?'}, driver "
+                  f"{rep['driver'] or '?'}, {len(rep['gpus'])} GPUs\n")
+        rows = [list(_COLUMNS)] + [_gpu_row(e) for e in rep["gpus"]]
+        widths = [max(len(r[c]) for r in rows) for c in range(len(_COLUMNS) - 1)]
+        for r in rows:
+            out.write("  " + "  ".join(r[c].ljust(widths[c]) for c in range(len(_COLUMNS) - 1)) + "  " + r[-1] + "\n")
+        for ln in rep["node_findings"]:
+            out.write(f"  node: {ln}\n")
+    out.write(f"=> counts as Ready: {'yes' if doc['counts_as_ready'] else 'no'}\n")
+
+
+def explain(cluster: ClusterConnection, node_name: str, opts: CheckOptions, out: TextIO) -> int:
+    as_json = opts.json
+    doc = diagnose(cluster, node_name, opts)
+    if as_json:
+        out.write(json.dumps(doc, indent=2, ensure_ascii=False) + "\n")
+    else:
+        render(doc, out)
+    return 2 if not doc["gpu_node"] else 0 if doc["counts_as_ready"] else 3
 
 
 def opts_keys() -> List[str]:

@@ -52,3 +52,18 @@ def test_explain_healthy_plain_and_missing(run_cli, mock_cluster, tmp_path):
     p = run_cli(["--kubeconfig", str(tmp_path / "missing"), "--explain", "x", "--json"])
     assert p.returncode == 1 and "error" in json.loads(p.stdout)
     assert H.HEALTH_CONDITION == "AMDGPUHealthy"
+
+
+def test_explain_json(run_cli, mock_cluster, tmp_path):
+    kc = _cluster(mock_cluster, tmp_path)
+    p = run_cli(["--kubeconfig", kc, "--explain", "bad", "--json"])
+    assert p.returncode == 3
+    d = json.loads(p.stdout)
+    assert d["node"] == "bad" and d["gpu_node"] and not d["counts_as_ready"] and d["gpus"] == 8
+    assert d["verdict"]["state"] == "unhealthy" and d["health_condition"]["status"] == "False"
+    g3 = d["report"]["gpus"][3]
+    assert g3["bdf"] == "0000:35:00.0" and g3["ecc_uncorrectable"] == 2
+    assert g3["findings"][0] == "2 uncorrectable ECC errors (umc 2)"
+    assert d["report"]["node_findings"][0].startswith("firmware differs across GPUs: pm: gpu0-2,4-7 ")
+    p = run_cli(["--kubeconfig", kc, "--explain", "cpu", "--json"])
+    assert p.returncode == 2 and json.loads(p.stdout)["gpu_node"] is False
