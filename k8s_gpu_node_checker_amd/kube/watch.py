@@ -13,7 +13,9 @@ keeps the GPU-node view current from ``GET /api/v1/nodes?watch=1``:
   triggers a re-LIST, a dropped stream is re-opened from the last
   resourceVersion with backoff;
 * events arriving within ``debounce`` seconds are folded into one
-  evaluation; the MI355X health gate runs on the new state and a report
+  evaluation; the MI355X health gate runs on the new state (and again every
+  ``recheck`` seconds without events: an agent that stopped publishing sends
+  no event, its condition only goes stale with time) and a report
   (identical in format to a one-shot check) is emitted only when the
   outcome changed: exit code, or any node's name / Ready / GPU count /
   health verdict.
@@ -88,11 +90,14 @@ def outcome_signature(result: Any) -> Tuple[Any, ...]:
 
 class NodeWatcher:
     def __init__(self, cluster: ClusterConnection, opts: Any, watch_timeout: int = 300, debounce: float = 0.2,
-                 page_size: Optional[int] = None, sleep: Callable[[float], None] = time.sleep):
+                 page_size: Optional[int] = None, sleep: Callable[[float], None] = time.sleep,
+                 recheck: float = 30.0):
         self.cluster = cluster
         self.opts = opts
         self.watch_timeout = max(1, int(watch_timeout))
         self.debounce = max(0.0, debounce)
+        # re-evaluate a quiet cluster this often (0: only on events): the health gate ages heartbeats
+        self.recheck = max(0.0, recheck)
         self.page_size = opts.page_size if page_size is None else page_size
         self.sleep = sleep
         self.view = NodeView(opts.gpu_source, 2 if (opts.reeval or opts.json_extended) else 1)
@@ -183,9 +188,11 @@ class NodeWatcher:
         reports = 0
         last_sig: Optional[Tuple[Any, ...]] = None
         failures = 0
+        last_eval = time.monotonic()
 
         def consider() -> None:
-            nonlocal reports, last_sig
+            nonlocal reports, last_sig, last_eval
+            last_eval = time.monotonic()
             result = evaluate(self.view.scan_result())
             sig = outcome_signature(result)
             if sig != last_sig:
@@ -209,20 +216,21 @@ class NodeWatcher:
                 failures = 0
                 pending = False
                 while not done():
+                    wait = self.debounce if pending else self.watch_timeout + 30
+                    if self.recheck > 0:
+                        wait = min(wait, max(0.01, last_eval + self.recheck - time.monotonic()))
                     if deadline is not None:
                         remaining = deadline - time.monotonic()
                         if remaining <= 0:
                             break
-                        client._connection().sock.settimeout(min(remaining, self.debounce or remaining)
-                                                             if pending else min(remaining, self.watch_timeout + 30))
-                    else:
-                        client._connection().sock.settimeout(self.debounce if pending else self.watch_timeout + 30)
+                        wait = min(wait, remaining)
+                    client._connection().sock.settimeout(wait)
                     try:
                         line = stream.next_line()
                     except EOFError:
                         break  # server ended the watch (timeoutSeconds): re-open from self.rv
-                    if line is None:  # quiet for `debounce` s (or the deadline): evaluate the batch
-                        if pending:
+                    if line is None:  # quiet for `debounce` s: evaluate the batch; or time for a recheck
+                        if pending or (self.recheck > 0 and time.monotonic() - last_eval >= self.recheck):
                             consider()
                             pending = False
                         continue

@@ -205,3 +205,24 @@ def test_cli_watch_events_json(mock_cluster, tmp_path):
     assert p.returncode == 3, err
     second = json.loads(out)
     assert second["ready_nodes"] == 0 and second["total_nodes"] >= 1
+
+
+def test_node_watcher_notices_a_heartbeat_going_stale_without_events(mock_cluster):
+    """An agent that stops publishing sends no watch event; its AMDGPUHealthy heartbeat only ages.
+    The watcher re-evaluates a quiet cluster every ``recheck`` s, so the stale verdict is reported."""
+    from k8s_gpu_node_checker_amd.models import health as H
+    rep = fixtures.mi355x_probe_report("n", gpus=8)
+    cond = fixtures.health_condition(rep, 8)
+    cond["lastHeartbeatTime"] = H.format_k8s_time(time.time() - 1.0)  # fresh for 1 more second (max age 2 s)
+    srv = mock_cluster([fixtures.realistic_node("n", extra_conditions=[cond])])
+    opts = CheckOptions(json=True)
+    opts.health_policy, opts.probe_max_age, opts.probe_unknown = "require", 2.0, "deny"
+    reports = []
+
+    def evaluate(scan):
+        return CheckResult(scan, apply_health(scan, opts, NullTracer()), NullTracer())
+    w = NodeWatcher(ClusterConnection(srv.url), opts, watch_timeout=30, debounce=0.05, recheck=0.2)
+    w.run(evaluate, reports.append, max_reports=2, duration=6.0)
+    assert [r.exit_code for r in reports] == [0, 3]
+    assert [r.verdicts[0].state for r in reports] == ["healthy", "unknown"]
+    assert w.events == 0  # nothing arrived on the stream: the second report came from the recheck
