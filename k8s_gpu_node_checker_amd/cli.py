@@ -263,7 +263,8 @@ def _watch_events(args: Any) -> int:
 
         def report(result) -> None:
             emit_report(result, opts)
-            memo["prev"] = {"fingerprint": statefile.fingerprint(result), "exit_code": result.exit_code}
+            memo["prev"] = {"fingerprint": statefile.fingerprint(result), "exit_code": result.exit_code,
+                            "slack_pending": result.slack_sent is False}
             if args.state_file:
                 statefile.save(args.state_file, result, prev)
             if args.prometheus_textfile:

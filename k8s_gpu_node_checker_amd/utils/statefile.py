@@ -6,7 +6,10 @@ checker remembers the previous outcome and only notifies when it changes:
 
 * a different exit code or a different set of (node, ready) pairs -> send;
 * with ``--slack-only-on-error``: send on a change *into* an error state, and
-  once more on the recovery back to exit 0.
+  once more on the recovery back to exit 0;
+* a notification that was due but not delivered (the webhook failed on every
+  attempt) stays due: the next run sends it, so an alert is not lost to a
+  Slack outage.
 
 Without ``--slack-on-change`` the file is still written (last outcome, for
 dashboards) and Slack behaves exactly like the reference.
@@ -49,6 +52,8 @@ def save(path: str, result: Any, prev: Optional[Dict[str, Any]] = None) -> None:
         "ready_nodes": len(result.ready_gpu_nodes),
         "not_ready": [n["name"] for n in result.gpu_nodes if not n["ready"]],
         "slack_sent": result.slack_sent,
+        # sent and failed (None: nothing was due): the next run's gate sends again
+        "slack_pending": result.slack_sent is False,
         "runs": (prev or {}).get("runs", 0) + 1,
     }
     d = os.path.dirname(os.path.abspath(path))
@@ -61,6 +66,8 @@ def save(path: str, result: Any, prev: Optional[Dict[str, Any]] = None) -> None:
 
 def should_notify(prev: Optional[Dict[str, Any]], result: Any, only_on_error: bool) -> bool:
     fp = fingerprint(result)
+    if prev is not None and prev.get("slack_pending"):
+        return True  # the last notification never arrived
     if prev is not None and prev.get("fingerprint") == fp:
         return False
     if not only_on_error:

@@ -127,3 +127,21 @@ def test_cli_watch_bounded(run_cli, mock_cluster, sink, tmp_path):
     srv.state.set_nodes(fixtures.golden("notready"))
     assert run_cli(args).returncode == 3
     assert len(sink.requests) == 1  # four failing checks, one alert
+
+
+def test_cli_slack_on_change_keeps_an_undelivered_alert_due(run_cli, mock_cluster, sink, tmp_path):
+    """A failing webhook does not consume the alert: the next run (same outcome) sends it, then it is
+    de-duplicated as usual."""
+    from k8s_gpu_node_checker_amd.testing import fixtures
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+    srv = mock_cluster(fixtures.golden("notready"))
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    base = ["--kubeconfig", kc, "--slack-only-on-error", "--slack-retry-count", "0",
+            "--state-file", str(tmp_path / "st.json"), "--slack-on-change"]
+    assert run_cli(base + ["--slack-webhook", sink.url("500")]).returncode == 3
+    assert statefile.load(str(tmp_path / "st.json"))["slack_pending"] is True
+    assert len(sink.requests) == 1
+    for _ in range(2):
+        assert run_cli(base + ["--slack-webhook", sink.url("200")]).returncode == 3
+    assert len(sink.requests) == 2  # delivered on the second run, not repeated on the third
+    assert statefile.load(str(tmp_path / "st.json"))["slack_pending"] is False
