@@ -48,7 +48,11 @@ from ..models.resources import PRIMARY_GPU_KEY, gpu_breakdown
 # whether the annotation must be rewritten.
 _VOLATILE = frozenset(("ts", "probe_ms", "probe_us", "hotspot_c", "wall_s", "ms_per_gemm", "setup_ms",
                        "power_w", "hbm_temp_c", "gfxclk_mhz", "vram_used_mb", "processes", "throttle_acc",
-                       "throttle", "procs", "gfx_activity", "diag_skipped", "xgmi_kb"))
+                       "throttle", "procs", "gfx_activity", "diag_skipped", "xgmi_kb", "ecc_ce_per_h"))
+
+# correctable-ECC trend: the rate is taken over the probes of the last hour, once they span 10 minutes
+CE_WINDOW_S = 3600.0
+CE_MIN_SPAN_S = 600.0
 
 DIAG_WHEN = ("idle", "always")
 # per-GPU fields kept out of the node annotation (Agent.annotation)
@@ -233,6 +237,8 @@ class Agent:
         self._cond_at = 0.0
         # previous throttle-residency sample per GPU (bdf or index) -> (monotonic time, accumulators)
         self._acc_prev: Dict[str, Any] = {}
+        # correctable ECC count history per GPU (bdf or index) -> [(monotonic time, count)], last CE_WINDOW_S
+        self._ce_hist: Dict[str, List[Any]] = {}
         # remediation signals, both driven by verdict *changes*: an Event per change (advisory, never
         # repeated) and, opt-in, the UNHEALTHY_TAINT while unhealthy (retried until written)
         self.events = events
@@ -375,6 +381,7 @@ class Agent:
             rep = {"schema": SCHEMA, "node": self.node, "ts": time.time(), "gpus": [],
                    "error": f"probe: {type(e).__name__}: {e}"[:300]}
         self._throttle_windows(rep)
+        self._ce_rates(rep)
         gpus = rep.get("gpus") or []
         diags = self._diagnostics(gpus)
         if diags or self._diag_skipped:
@@ -397,6 +404,25 @@ class Agent:
             self.last = rep
             self.last_probe_done = time.monotonic()
         return rep
+
+    def _ce_rates(self, rep: Dict[str, Any], now: Optional[float] = None) -> None:
+        """``gpus[i].ecc_ce_per_h``: correctable ECC errors per hour over the agent's probes of the last
+        hour (once they span ``CE_MIN_SPAN_S``); a counter that went down (driver reload) restarts it."""
+        now = time.monotonic() if now is None else now
+        for g in rep.get("gpus") or []:
+            ce = g.get("ecc_correctable")
+            if not isinstance(ce, int) or isinstance(ce, bool):
+                continue
+            key = str(g.get("bdf") or g.get("index"))
+            hist = self._ce_hist.setdefault(key, [])
+            if hist and ce < hist[-1][1]:
+                hist.clear()
+            hist.append((now, ce))
+            while len(hist) > 2 and now - hist[1][0] >= CE_WINDOW_S:
+                hist.pop(0)  # keep the newest sample that is at least a window old as the baseline
+            span = now - hist[0][0]
+            if span >= CE_MIN_SPAN_S:
+                g["ecc_ce_per_h"] = round((ce - hist[0][1]) * 3600.0 / span, 1)
 
     def _throttle_windows(self, rep: Dict[str, Any]) -> None:
         """Turn the firmware's since-boot throttle accumulators into the share of the time since the
@@ -521,7 +547,7 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
     if not rep:
         return "# no probe yet\n"
     fams: Dict[str, List[str]] = {}
-    counters = {"mi355x_gpu_pcie_replays", "mi355x_gpu_xgmi_kilobytes"}
+    counters = {"mi355x_gpu_pcie_replays", "mi355x_gpu_xgmi_kilobytes", "mi355x_gpu_ecc_correctable"}
 
     def put(name: str, labels: str, value: Any) -> None:
         fams.setdefault(name, []).append(f"{name}{{{labels}}} {value}" if labels else f"{name} {value}")
@@ -536,7 +562,8 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
         put("mi355x_node_driver_info", f'name="{_esc(drv.get("name"))}",version="{_esc(driver_release(drv["version"]))}"', 1)
     for g in rep.get("gpus") or []:
         lbl = f'gpu="{g.get("index")}",bdf="{_esc(g.get("bdf", ""))}"'
-        for key, metric in (("ecc_uncorrectable", "ecc_uncorrectable"), ("pcie_width", "pcie_width"),
+        for key, metric in (("ecc_uncorrectable", "ecc_uncorrectable"), ("ecc_correctable", "ecc_correctable"),
+                            ("pcie_width", "pcie_width"),
                             ("pcie_replays", "pcie_replays"), ("xgmi_error", "xgmi_error_status"),
                             ("bad_pages", "retired_pages"), ("bad_pages_pending", "retired_pages_pending"),
                             ("bad_pages_unreservable", "retired_pages_unreservable"),
@@ -545,7 +572,8 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
                 put(f"mi355x_gpu_{metric}", lbl, g[key])
         if isinstance(g.get("xgmi"), str):
             put("mi355x_gpu_xgmi_links_up", lbl, g["xgmi"].count("U"))
-        for key, metric in (("hotspot_c", "hotspot_celsius"), ("power_w", "power_watts"),
+        for key, metric in (("ecc_ce_per_h", "ecc_correctable_per_hour"), ("hotspot_c", "hotspot_celsius"),
+                            ("power_w", "power_watts"),
                             ("power_cap_w", "power_cap_watts"), ("hbm_temp_c", "hbm_celsius"),
                             ("gfxclk_mhz", "gfxclk_mhz"), ("vram_used_mb", "vram_used_megabytes"),
                             ("gfx_activity", "gfx_activity_percent")):

@@ -55,7 +55,8 @@ class HealthExpectations:
 
     def __init__(self, xgmi_links: int = XGMI_LINKS_EXPECTED, max_age_s: float = 900.0,
                  require_product: bool = True, vram_min_fraction: float = VRAM_MIN_FRACTION,
-                 bad_page_limit: int = 64, correctable_warn: int = 1000, cper_window_s: float = 86400.0):
+                 bad_page_limit: int = 64, correctable_warn: int = 1000, cper_window_s: float = 86400.0,
+                 ce_rate_warn_per_h: float = 60.0):
         self.xgmi_links = xgmi_links
         self.max_age_s = max_age_s
         self.require_product = require_product
@@ -64,6 +65,10 @@ class HealthExpectations:
         self.correctable_warn = correctable_warn
         #: a fatal CPER record newer than this (s, against the report's time) makes the GPU unhealthy
         self.cper_window_s = cper_window_s
+        #: correctable ECC errors per hour (the agent's ``ecc_ce_per_h`` over its last hour of probes) at which a
+        #: GPU is "degraded": a steady trickle of corrected HBM errors is normal, a burst is a part going bad
+        #: before it ever reports an uncorrectable one
+        self.ce_rate_warn_per_h = ce_rate_warn_per_h
 
 
 class Verdict:
@@ -345,6 +350,9 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float
     ce = g.get("ecc_correctable")
     if isinstance(ce, int) and ce > exp.correctable_warn:
         warn.append(f"gpu{idx}: {ce} correctable ECC errors{_by_block(blocks, 'ce')}")
+    rate = g.get("ecc_ce_per_h")
+    if isinstance(rate, (int, float)) and not isinstance(rate, bool) and rate >= exp.ce_rate_warn_per_h > 0:
+        warn.append(f"gpu{idx}: correctable ECC errors rising at {rate:.0f}/h{_by_block(blocks, 'ce')}")
     cper = g.get("cper")
     if isinstance(cper, dict):
         # the driver's RAS error records (since it loaded): a recent fatal one means the GPU went through

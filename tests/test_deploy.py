@@ -133,7 +133,7 @@ def _rich_report():
              ecc_blocks={"umc": {"ce": 1, "ue": 0, "de": 0}}, gfx_activity=0,
              throttle={"s": 60, "thermal_pct": 0.0, "power_pct": 1.0, "prochot_pct": 0.0},
              diag={"gemm": {"pass": True, "tflops": 1200.0}}, bad_pages=3, bad_pages_pending=1,
-             bad_pages_unreservable=0, bad_page_threshold=2048)
+             bad_pages_unreservable=0, bad_page_threshold=2048, ecc_ce_per_h=1.5)
     return r
 
 

@@ -325,3 +325,24 @@ def test_retired_pages_use_the_drivers_threshold_when_known():
     assert v(bad_pages=3, bad_pages_pending=3).state == H.DEGRADED
     assert v(ras_eeprom="ok").state == H.HEALTHY
     assert v(ras_eeprom="corrupted").state == H.UNHEALTHY
+
+
+def test_correctable_ecc_rate_over_the_agents_last_hour():
+    from k8s_gpu_node_checker_amd.agent.agent import Agent
+    ag = Agent("n", source="fixture")
+
+    def probe(t, ce, bdf="0000:05:00.0"):
+        rep = {"gpus": [{"index": 0, "bdf": bdf, "ecc_correctable": ce}]}
+        ag._ce_rates(rep, now=t)
+        return rep["gpus"][0].get("ecc_ce_per_h")
+    assert probe(0, 0) is None
+    assert probe(300, 10) is None  # the samples span less than 10 minutes
+    assert probe(600, 20) == 120.0
+    assert probe(4000, 20) == round(10 * 3600 / 3700, 1)  # baseline: the newest sample >= 1 h old (t=300)
+    assert probe(4100, 5) is None  # the counter went down (driver reload): history restarts
+    rep = fixtures.mi355x_probe_report("n", gpus=1, gpu0={"ecc_correctable": 140, "ecc_ce_per_h": 120.0,
+                                                          "ecc_blocks": {"umc": {"ce": 140, "ue": 0, "de": 0}}})
+    v = H.evaluate_report(rep, 1, H.HealthExpectations(xgmi_links=0), now=rep["ts"])
+    assert v.state == H.DEGRADED and v.warnings == ["gpu0: correctable ECC errors rising at 120/h (umc 140)"]
+    rep["gpus"][0]["ecc_ce_per_h"] = 12.0
+    assert H.evaluate_report(rep, 1, H.HealthExpectations(xgmi_links=0), now=rep["ts"]).state == H.HEALTHY
