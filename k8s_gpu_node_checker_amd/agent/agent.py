@@ -608,6 +608,9 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
             for k in ("tflops", "copy_tbs", "read_tbs", "errors", "h2d_gbps", "d2h_gbps"):
                 if isinstance(res.get(k), (int, float)):
                     put(f"mi355x_gpu_diag_{k}", f'{lbl},test="{_esc(test)}"', res[k])
+            for xcd, v in ((res.get("alone_tbs") or {}) if isinstance(res.get("alone_tbs"), dict) else {}).items():
+                if isinstance(v, (int, float)):
+                    put("mi355x_gpu_diag_xcd_hbm_read_tbs", f'{lbl},xcd="{_esc(xcd)}"', v)
             for kind, row in ((res.get("kinds") or {}) if isinstance(res.get("kinds"), dict) else {}).items():
                 put("mi355x_gpu_diag_tflops", f'{lbl},test="{_esc(test)}",dtype="{_esc(kind)}"', row.get("tflops", 0))
     fabric = (rep.get("fabric") or {}).get("p2p")

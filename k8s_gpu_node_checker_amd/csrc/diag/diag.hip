@@ -910,6 +910,64 @@ __global__ void __launch_bounds__(256) l2_read_kernel(const uint4* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------
+// HBM per XCD: each XCD streams its own slice of a buffer far larger than the L2s and the 256 MiB MALL,
+// so every byte comes from HBM through that XCD's path to memory.  The XCD's workgroups share its slice
+// through a per-XCD chunk counter (found by XCC_ID, so the mapping of workgroups to XCDs does not matter);
+// every word is checked.  All XCDs get the same bytes: on a healthy chip they finish together, and an XCD
+// whose fabric path to the memory stacks runs slow falls behind the others (per-CU map as the burn-in's).
+// Work queue exit: the counter only grows, so every workgroup leaves once it passes nchunks * passes.
+constexpr uint32_t HBM_XCD_CHUNK_VEC = 8192;  // 128 KiB per grab
+// only_xcd >= 0: the other XCDs' workgroups leave at once, so that XCD streams alone (its own path's rate,
+// without the others contending for the memory stacks).
+__global__ void __launch_bounds__(256) hbm_xcd_kernel(const uint4* __restrict__ buf, uint32_t slice_vec, int passes,
+                                                      uint32_t seed, int only_xcd, unsigned int* next,
+                                                      unsigned long long* errors, unsigned long long* cu_map) {
+  __shared__ uint32_t s_chunk;
+  const long long t0 = wall_clock64();
+  const unsigned slot = wave_slot();
+  const unsigned xcd = slot >> 7;
+  if (only_xcd >= 0 && static_cast<int>(xcd) != only_xcd) return;
+  const uint32_t nchunks = slice_vec / HBM_XCD_CHUNK_VEC;
+  const uint32_t total = nchunks * static_cast<uint32_t>(passes);
+  unsigned int bad = 0;
+  constexpr uint32_t U = 8;
+  constexpr uint32_t STEP = U * 256;
+  static_assert(HBM_XCD_CHUNK_VEC % STEP == 0, "chunk is a whole number of 8-deep block steps");
+  for (;;) {
+    if (threadIdx.x == 0) s_chunk = atomicAdd(next + xcd, 1u);
+    __syncthreads();
+    const uint32_t c = s_chunk;
+    __syncthreads();  // everyone has read it before thread 0 overwrites it
+    if (c >= total) break;
+    const uint32_t base = xcd * slice_vec + (c % nchunks) * HBM_XCD_CHUNK_VEC;
+    for (uint32_t i = threadIdx.x; i < HBM_XCD_CHUNK_VEC; i += STEP) {
+      u32x4 v[U];
+      const u32x4* src = reinterpret_cast<const u32x4*>(buf) + base + i;
+#pragma unroll
+      for (uint32_t k = 0; k < U; ++k) v[k] = __builtin_nontemporal_load(src + k * 256);
+#pragma unroll
+      for (uint32_t k = 0; k < U; ++k) {
+        const uint32_t w = 4u * (base + i + k * 256);
+        bad += (v[k].x != (w ^ seed)) + (v[k].y != ((w + 1u) ^ seed)) + (v[k].z != ((w + 2u) ^ seed)) +
+               (v[k].w != ((w + 3u) ^ seed));
+      }
+    }
+  }
+  unsigned long long wave_bad = bad;
+  for (int off = 32; off > 0; off >>= 1) wave_bad += __shfl_down(wave_bad, off, 64);
+  const unsigned long long dt = static_cast<unsigned long long>(wall_clock64() - t0);
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long* row = cu_map + 3 * slot;
+    atomicAdd(row, 1ULL);
+    if (wave_bad) {
+      atomicAdd(row + 1, wave_bad);
+      atomicAdd(errors, wave_bad);
+    }
+    atomicAdd(row + 2, dt);
+  }
+}
+
 __global__ void __launch_bounds__(256) l2_fill_kernel(uint4* buf, uint32_t n_vec, uint32_t seed) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += gridDim.x * blockDim.x) {
     const uint32_t w = 4u * i;
@@ -1573,6 +1631,87 @@ int diag_l2_bandwidth(int device, size_t slice_bytes, int passes, int blocks_per
   DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   const double bytes = static_cast<double>(blocks) * passes * static_cast<double>(slice_bytes);
   *tbs = ms > 0.f ? bytes / (ms * 1e-3) / 1e12 : 0.0;
+  return 0;
+}
+
+// HBM per XCD (hbm_xcd_kernel): `slice_bytes` per XCD (8 slices, a multiple of 128 KiB, at most 512 MiB),
+// read `passes` times by the XCD's own workgroups, all XCDs at once: aggregate read TB/s, wrong words,
+// per-CU map.  With `xcd_tbs` (8 doubles) each XCD then streams its slice alone: its own read TB/s (0 for an
+// XCD without CUs on this device).
+int diag_hbm_xcd(int device, size_t slice_bytes, int passes, int blocks_per_cu, uint32_t seed, double* tbs,
+                 unsigned long long* errors, unsigned long long* cu_map, double* xcd_tbs) {
+  const size_t chunk = static_cast<size_t>(HBM_XCD_CHUNK_VEC) * 16;
+  if (slice_bytes < chunk || slice_bytes > (512u << 20) || slice_bytes % chunk || passes < 1 || passes > 64 ||
+      blocks_per_cu < 1 || blocks_per_cu > 8) {
+    g_err = "hbm_xcd: 128 KiB <= slice_bytes <= 512 MiB (multiple of 128 KiB), 1 <= passes <= 64, 1..8 blocks/CU";
+    return -2;
+  }
+  DIAG_CHECK(hipSetDevice(device));
+  const uint32_t slice_vec = static_cast<uint32_t>(slice_bytes / 16);
+  const uint32_t n_vec = 8u * slice_vec;  // XCC_ID is 0..7; 8 x 512 MiB keeps word indices in 32 bits
+  const size_t map_bytes = static_cast<size_t>(BURN_SLOTS) * 3 * sizeof(unsigned long long);
+  DevBuf dbuf, dnext, derr, dmap;
+  DIAG_CHECK(dbuf.alloc(device, static_cast<size_t>(n_vec) * 16));
+  DIAG_CHECK(dnext.alloc(device, 8 * sizeof(unsigned int)));
+  DIAG_CHECK(derr.alloc(device, sizeof(unsigned long long)));
+  DIAG_CHECK(dmap.alloc(device, map_bytes));
+  hipLaunchKernelGGL(l2_fill_kernel, dim3(4096), dim3(256), 0, nullptr, static_cast<uint4*>(dbuf.ptr), n_vec, seed);
+  DIAG_CHECK(hipGetLastError());
+  const int blocks = grid_for(device, blocks_per_cu);
+  Timer tm;
+  DIAG_CHECK(tm.create());
+  // one timed run (the queue counters reset first); returns its milliseconds, < 0 on a HIP error
+  auto timed = [&](int only_xcd) -> float {
+    if (hipMemset(dnext.ptr, 0, 8 * sizeof(unsigned int)) != hipSuccess) return -1.f;
+    if (hipEventRecord(tm.e0, nullptr) != hipSuccess) return -1.f;
+    hipLaunchKernelGGL(hbm_xcd_kernel, dim3(blocks), dim3(256), 0, nullptr, static_cast<const uint4*>(dbuf.ptr),
+                       slice_vec, passes, seed, only_xcd, static_cast<unsigned int*>(dnext.ptr),
+                       static_cast<unsigned long long*>(derr.ptr), static_cast<unsigned long long*>(dmap.ptr));
+    if (hipGetLastError() != hipSuccess || hipEventRecord(tm.e1, nullptr) != hipSuccess ||
+        hipEventSynchronize(tm.e1) != hipSuccess)
+      return -1.f;
+    return elapsed_ms(tm.e0, tm.e1);
+  };
+  if (timed(-1) < 0.f) DIAG_CHECK(hipGetLastError());  // untimed warm-up: page tables, clocks up
+  DIAG_CHECK(hipMemset(derr.ptr, 0, sizeof(unsigned long long)));
+  DIAG_CHECK(hipMemset(dmap.ptr, 0, map_bytes));
+  const float ms = timed(-1);
+  if (ms < 0.f) {
+    DIAG_CHECK(hipGetLastError());
+    g_err = "hbm_xcd: timed run failed";
+    return -1;
+  }
+  DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
+  // bytes actually read: every XCD that has CUs reads its slice `passes` times
+  bool present[8] = {false, false, false, false, false, false, false, false};
+  int xcds_seen = 0;
+  for (int x = 0; x < 8; ++x) {
+    for (int sl = 0; sl < 128 && !present[x]; ++sl) present[x] = cu_map[3 * (x * 128 + sl)] != 0;
+    xcds_seen += present[x];
+  }
+  const double bytes = static_cast<double>(xcds_seen) * passes * static_cast<double>(slice_bytes);
+  *tbs = ms > 0.f ? bytes / (ms * 1e-3) / 1e12 : 0.0;
+  if (xcd_tbs != nullptr) {
+    // untimed: the first lone-XCD run of a process measured ~8 % low (one XCD's clocks and queues ramping
+    // after the full-chip run), so the first present XCD streams once before the timed ones
+    for (int x = 0; x < 8; ++x)
+      if (present[x]) {
+        if (timed(x) < 0.f) DIAG_CHECK(hipGetLastError());
+        break;
+      }
+    for (int x = 0; x < 8; ++x) {
+      xcd_tbs[x] = 0.0;
+      if (!present[x]) continue;
+      const float xms = timed(x);
+      if (xms < 0.f) {
+        DIAG_CHECK(hipGetLastError());
+        g_err = "hbm_xcd: isolated run failed";
+        return -1;
+      }
+      xcd_tbs[x] = xms > 0.f ? passes * static_cast<double>(slice_bytes) / (xms * 1e-3) / 1e12 : 0.0;
+    }
+  }
+  DIAG_CHECK(hipMemcpy(errors, derr.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return 0;
 }
 

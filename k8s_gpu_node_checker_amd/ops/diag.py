@@ -59,6 +59,9 @@ REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
     "hbm": {"copy_tbs": 6.49, "read_tbs": 6.96},   # 16-byte copy (read + write bytes counted) / read, TB/s
     "mfma": {"bf16": 1901.0, "fp8": 1940.0, "mxfp8": 4326.0, "mxfp4": 7610.0},  # register-resident burn-in
     "host_link": {"h2d_gbps": 57.0, "d2h_gbps": 56.8},  # pinned copies over PCIe Gen5 x16
+    # per-XCD HBM reads, 8 x 256 MiB slices read twice: all XCDs together 6.02-6.25 TB/s, each XCD alone
+    # 1.28-1.33 TB/s (profiles/hbm_xcd_explore_mi355x.json)
+    "hbm_xcd": {"read_tbs": 6.0, "alone_tbs": 1.28},
     "l2": {"read_tbs": 30.5},                      # per-XCD L2 reads, 2 MiB slices, 8 WG/CU: 31.6-31.9 measured
                                                    # (profiles/l2_explore_mi355x.json; 34.5 TB/s is the L2's own figure)
 }
@@ -76,6 +79,9 @@ XCD_SLOW_RATIO = 1.15
 # burn-in's register-resident waves take the same time to the 10 ns tick on every CU of an XCD (1.000 in
 # 20 runs: one clock per XCD, no memory traffic); the L2 test's 1.016-1.022
 CU_SLOW_RATIO = 1.15
+# an XCD reading HBM alone at less than this share of the median XCD alone: its path to the memory stacks is
+# slow (healthy spread < 3 %, profiles/hbm_xcd_explore_mi355x.json)
+XCD_ALONE_MIN_RATIO = 0.9
 
 
 class Scale:
@@ -176,6 +182,7 @@ def lib() -> ctypes.CDLL:
         L.diag_l2_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                         ctypes.POINTER(ctypes.c_ulonglong)]
+        L.diag_hbm_xcd.argtypes = list(L.diag_l2_bandwidth.argtypes) + [ctypes.POINTER(ctypes.c_double)]
         L.diag_lds_test.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong),
                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]
@@ -479,6 +486,49 @@ def l2_bandwidth(device: int = 0, slice_kib: int = 2048, passes: int = 32, block
     return _lag_verdict(res, where, "L2 reads")
 
 
+def hbm_xcd(device: int = 0, slice_mib: int = 256, passes: int = 2, blocks_per_cu: int = 4,
+            seed: int = 0x4B3D, scale: Scale = FULL) -> Dict[str, Any]:
+    """HBM reads per XCD.  Each XCD streams its own ``slice_mib`` slice (8 of them, far past the L2s and the
+    MALL) with its own workgroups, every word checked: first all XCDs together (aggregate read TB/s), then
+    each XCD alone (``alone_tbs``: that XCD's own path to the memory stacks).  All XCDs together saturate
+    HBM, so the aggregate hides one slow XCD; alone, every XCD of a healthy MI355X reads at 1.28-1.33 TB/s
+    (spread < 3 %, profiles/hbm_xcd_explore_mi355x.json).  Judged: the aggregate against the HBM-read
+    reference, the slowest XCD alone against the per-XCD reference, and an XCD below
+    ``XCD_ALONE_MIN_RATIO`` of the median XCD is degraded even when above the floor."""
+    L = lib()
+    nslots = L.diag_mfma_burn_slots()
+    tbs, errs = ctypes.c_double(), ctypes.c_ulonglong()
+    m = (ctypes.c_ulonglong * (3 * nslots))()
+    alone = (ctypes.c_double * 8)()
+    t0 = time.perf_counter()
+    _check(L.diag_hbm_xcd(device, slice_mib << 20, passes, blocks_per_cu, seed, ctypes.byref(tbs),
+                          ctypes.byref(errs), m, alone))
+    where = cu_map_summary({"hbm_xcd": list(m)})
+    # under contention the XCDs' shares of HBM are not even (measured 1.02-1.29x between runs): reported only
+    where = {k: v for k, v in where.items() if k in ("cus", "xcds", "bad_cus")}
+    per = {x: alone[x] for x in range(8) if alone[x] > 0}
+    res: Dict[str, Any] = {"read_tbs": round(tbs.value, 3), "errors": errs.value,
+                           "alone_tbs": {str(x): round(v, 3) for x, v in per.items()}, "map": where}
+    rates = {"read_tbs": tbs.value}
+    exp = {"read_tbs": REFERENCE_RATES["hbm_xcd"]["read_tbs"] * scale.memory}
+    notes = []
+    if per:
+        slow = min(per, key=per.get)
+        med = sorted(per.values())[len(per) // 2]
+        res["slowest_xcd"], res["slowest_xcd_rel"] = slow, round(per[slow] / med, 3) if med > 0 else None
+        rates["slowest_xcd_tbs"] = per[slow]
+        exp["slowest_xcd_tbs"] = min(REFERENCE_RATES["hbm_xcd"]["alone_tbs"], exp["read_tbs"])
+        if med > 0 and per[slow] < XCD_ALONE_MIN_RATIO * med:
+            notes.append(f"xcd{slow} reads HBM at {per[slow]:.2f} TB/s alone, {per[slow] / med:.2f}x the median XCD")
+    wrong = f"{errs.value} wrong words on " + ", ".join(where.get("bad_cus", [])[:4]) if errs.value else ""
+    res["wall_s"] = round(time.perf_counter() - t0, 3)
+    res = _rated(res, rates, exp, "TB/s", not errs.value, wrong)
+    if res["pass"] and notes:
+        res["degraded"] = True
+        res["detail"] = "; ".join(x for x in [res["detail"]] + notes if x)
+    return res
+
+
 def host_link(device: int = 0, mib: int = 256, iters: int = 5, scale: Scale = FULL) -> Dict[str, Any]:
     """Pinned host <-> device bandwidth over the GPU's PCIe link (GB/s each way).  A Gen4 or x8 link
     lands at about half the Gen5 x16 reference and fails."""
@@ -525,8 +575,8 @@ def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5) -
 
 LEVELS = {
     0: (),
-    1: ("gemm_quick", "gemm_fp8_quick", "hbm_quick", "mfma", "lds", "l2"),
-    2: ("gemm", "gemm_fp8", "hbm", "memtest", "mfma", "lds", "l2", "host_link"),
+    1: ("gemm_quick", "gemm_fp8_quick", "hbm_quick", "hbm_xcd", "mfma", "lds", "l2"),
+    2: ("gemm", "gemm_fp8", "hbm", "hbm_xcd", "memtest", "mfma", "lds", "l2", "host_link"),
 }
 
 
@@ -560,13 +610,15 @@ def _one(test: str, device: int, scale: Scale) -> Dict[str, Any]:
         return lds_test(device)
     if test == "l2":
         return l2_bandwidth(device, scale=scale)
+    if test == "hbm_xcd":
+        return hbm_xcd(device, scale=scale)
     raise ValueError(f"unknown diagnostic {test!r}")
 
 
 def _slow_only(res: Dict[str, Any]) -> bool:
     """Below the degraded line on rate alone, or one XCD lagging the others (numerics fine): worth a
     second measurement."""
-    lagging = bool(_lag_notes(res.get("map") or {}, ""))
+    lagging = bool(_lag_notes(res.get("map") or {}, "")) or (res.get("slowest_xcd_rel") or 1.0) < XCD_ALONE_MIN_RATIO
     return (res.get("degraded") or not res.get("pass")) \
         and (res.get("fraction", 1.0) < DEGRADED_FRACTION or lagging) \
         and "wrong results" not in res.get("detail", "") and "err " not in res.get("detail", "")
@@ -576,7 +628,8 @@ def _goodness(res: Dict[str, Any]) -> tuple:
     """Order two measurements of one test: passing, then not degraded, then the better rate."""
     where = res.get("map") or {}
     return (bool(res.get("pass")), not res.get("degraded"), res.get("fraction", 0.0),
-            -max(where.get("slowest_rel") or 0.0, where.get("slowest_cu_rel") or 0.0))
+            -max(where.get("slowest_rel") or 0.0, where.get("slowest_cu_rel") or 0.0),
+            res.get("slowest_xcd_rel") or 0.0)
 
 
 def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
@@ -635,6 +688,10 @@ def _summary(test: str, r: Dict[str, Any]) -> str:
         return f"{r.get('read_tbs', 0):.1f} TB/s, XCD spread {m.get('slowest_rel', 1.0):.3f}, {r.get('errors', 0)} bad words"
     if test == "memtest":
         return f"{r.get('gib', 0):g} GiB, {r.get('errors', 0)} errors"
+    if test == "hbm_xcd":
+        alone = r.get("alone_tbs") or {}
+        span = f"{min(alone.values()):.2f}-{max(alone.values()):.2f} TB/s per XCD alone" if alone else "no XCD map"
+        return f"{r.get('read_tbs', 0):.2f} TB/s all XCDs, {span}, {r.get('errors', 0)} bad words"
     if test == "host_link":
         return f"h2d {r.get('h2d_gbps', 0):.1f} / d2h {r.get('d2h_gbps', 0):.1f} GB/s"
     if test == "p2p":

@@ -40,7 +40,8 @@ class FakeDiagLib:
                  nopeer: Tuple[Tuple[int, int], ...] = (), rc: int = 0, err: bytes = b"boom", delay_s: float = 0.0,
                  slow_xcd: Optional[Dict[int, float]] = None, bad_cu: Optional[Dict[Tuple[int, int], int]] = None,
                  lds_bad: Optional[Dict[Tuple[int, int], int]] = None,
-                 l2_bad: Optional[Dict[Tuple[int, int], int]] = None, slow_cu: Optional[Dict[int, float]] = None):
+                 l2_bad: Optional[Dict[Tuple[int, int], int]] = None, slow_cu: Optional[Dict[int, float]] = None,
+                 hbm_xcd_slow: Optional[Dict[int, float]] = None, hbm_bad: Optional[Dict[Tuple[int, int], int]] = None):
         from ..ops import diag
         self.ref = diag.REFERENCE_RATES
         self.kinds = diag.MFMA_KINDS
@@ -63,6 +64,10 @@ class FakeDiagLib:
         self.slow_xcd = dict(slow_xcd or {})
         self.bad_cu = dict(bad_cu or {})
         self.lds_bad = dict(lds_bad or {})
+        # per-XCD HBM: hbm_xcd_slow[xcd] = that XCD's alone rate as a share of the reference; hbm_bad[(device,
+        # slot)] = wrong words read there
+        self.hbm_xcd_slow = dict(hbm_xcd_slow or {})
+        self.hbm_bad = dict(hbm_bad or {})
         self.l2_bad = dict(l2_bad or {})
         self.slow_cu = dict(slow_cu or {})
         self.calls: List[str] = []
@@ -176,6 +181,33 @@ class FakeDiagLib:
                     cu_map[3 * slot] = waves
                     cu_map[3 * slot + 2] = int(waves * 90000 * self.slow_xcd.get(xcd, 1.0))
                     bad = self.l2_bad.get((device, slot), 0)
+                    cu_map[3 * slot + 1] = bad
+                    total += bad
+        _put(errors, ctypes.c_ulonglong, total)
+        return 0
+
+    def diag_hbm_xcd(self, device, slice_bytes, passes, blocks_per_cu, seed, tbs, errors, cu_map, xcd_tbs):
+        """All XCDs together at rate x reference; each XCD alone at rate x reference x ``hbm_xcd_slow``."""
+        self._log(device, "hbm_xcd")
+        if self.rc:
+            return self.rc
+        r = self._rate(device)
+        _put(tbs, ctypes.c_double, r * self.ref["hbm_xcd"]["read_tbs"])
+        total = 0
+        nx = 8 if self.cus >= 256 else max(1, self.cus // 32)
+        for xcd in range(8):
+            # an XCD alone reads at its own path's rate whatever the partition: the device's rate share
+            # (rate) is normalised by its CU share
+            share = min(1.0, self.cus / 256)
+            xcd_tbs[xcd] = r / share * 1.31 * self.hbm_xcd_slow.get(xcd, 1.0) if xcd < nx else 0.0
+        for xcd in range(nx):
+            for se in range(4):
+                for cu in range(8):
+                    slot = (xcd << 7) | (se << 5) | cu
+                    waves = 4 * blocks_per_cu
+                    cu_map[3 * slot] = waves
+                    cu_map[3 * slot + 2] = waves * 50000
+                    bad = self.hbm_bad.get((device, slot), 0)
                     cu_map[3 * slot + 1] = bad
                     total += bad
         _put(errors, ctypes.c_ulonglong, total)

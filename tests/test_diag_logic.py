@@ -264,3 +264,31 @@ def test_text_summary(fake, capsys):
     assert any("xcd2 waves take 1.30x" in ln for ln in out)
     assert rows["lds"].endswith("256 CUs x 159 KiB, 0 bad words")
     assert out[-1] == "result: PASS" and rc == 0  # degraded still passes
+
+
+def test_hbm_per_xcd_alone_rates_find_one_slow_xcd(fake):
+    lib = fake()
+    r = diag.hbm_xcd(0)
+    assert r["pass"] and not r["degraded"] and len(r["alone_tbs"]) == 8 and r["slowest_xcd_rel"] == 1.0
+    assert r["expect"] == {"read_tbs": 6.0, "slowest_xcd_tbs": 1.28}
+    # one XCD's path at 85 % of the others: the aggregate (HBM-bound) would not show it; alone it is 0.85x
+    # the median XCD -> degraded, and measured again before it is reported
+    lib = fake(hbm_xcd_slow={5: 0.97 * 0.85 / 0.97})
+    out = diag.run(1, 0)
+    r = out["hbm_xcd"]
+    assert r["pass"] and r["degraded"] and r["slowest_xcd"] == 5 and r["retried"]
+    assert "xcd5 reads HBM at 1.11 TB/s alone, 0.85x the median XCD" in r["detail"]
+    assert lib.calls.count("hbm_xcd") == 1 + diag.REMEASURE
+    # an XCD at half rate fails outright (below 85 % of the per-XCD reference)
+    fake(hbm_xcd_slow={2: 0.5})
+    r = diag.hbm_xcd(0)
+    assert not r["pass"] and r["detail"].startswith("slowest_xcd_tbs 0.655 TB/s = 51% of 1.28")
+    assert _verdict({"hbm_xcd": r}).state == "unhealthy"
+    # wrong words are located to the CU that read them
+    fake(hbm_bad={(0, (3 << 7) | (1 << 5) | 2): 4})
+    r = diag.hbm_xcd(0)
+    assert not r["pass"] and r["detail"] == "4 wrong words on xcd3/se1/cu2 (hbm_xcd 4)"
+    # a CPX partition: one XCD, the partition's memory share of the aggregate
+    fake(cus=32, rate=1 / 8)
+    r = diag.hbm_xcd(0, scale=diag.Scale(0.125, 0.125))
+    assert list(r["alone_tbs"]) == ["0"] and r["expect"]["read_tbs"] == 0.75

@@ -523,6 +523,17 @@ def test_lds_test_every_cu_and_injected_fault(dev):
     assert bad["bad_cus"][0].endswith("(1 words)") and bad["bad_cus"][0].startswith("xcd"), bad
 
 
+def test_hbm_per_xcd_together_and_alone(dev):
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.hbm_xcd(0)
+    print(json.dumps(r))
+    assert r["pass"] and r["errors"] == 0, r
+    info = diag.device_info(0)
+    if info["cus"] >= 256:
+        assert len(r["alone_tbs"]) == 8 and r["slowest_xcd_rel"] >= diag.XCD_ALONE_MIN_RATIO
+        assert r["read_tbs"] < 8.5  # cannot beat the HBM3E spec
+
+
 def test_l2_bandwidth_per_xcd(dev):
     """Each XCD reads its own L2-resident slice: aggregate rate above the floor, every CU and XCD seen,
     no XCD lagging, every word intact."""

@@ -46,7 +46,7 @@ def test_eight_gpu_level2_cycle_is_healthy_and_parallel(node8):
     assert {d: lib.threads[d] for d in range(8)} == {d: {f"diag-gpu{d}"} for d in range(8)}
     assert wall < 8 * 2 * 0.15 * 0.6, wall
     for g in rep["gpus"]:
-        assert set(g["diag"]) == {"gemm", "gemm_fp8", "hbm", "memtest", "mfma", "lds", "l2", "host_link"}
+        assert set(g["diag"]) == {"gemm", "gemm_fp8", "hbm", "hbm_xcd", "memtest", "mfma", "lds", "l2", "host_link"}
         assert all(r["pass"] and not r.get("degraded") for r in g["diag"].values()), g["diag"]
     p2p, rccl = rep["fabric"]["p2p"], rep["fabric"]["rccl"]
     assert p2p["pass"] and p2p["median_gbps"] == 48.0
