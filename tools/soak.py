@@ -24,7 +24,8 @@ from k8s_gpu_node_checker_amd.ops import diag  # noqa: E402
 
 METRICS = (("gemm", "tflops"), ("gemm_fp8", "tflops"), ("hbm", "copy_tbs"), ("hbm", "read_tbs"),
            ("hbm", "write_tbs"), ("memtest", "errors"), ("host_link", "h2d_gbps"), ("host_link", "d2h_gbps"),
-           ("l2", "read_tbs"), ("l2", "errors"), ("lds", "errors"))
+           ("l2", "read_tbs"), ("l2", "errors"), ("lds", "errors"), ("hbm_xcd", "read_tbs"), ("hbm_xcd", "errors"),
+           ("hbm_xcd", "slowest_xcd_rel"))
 
 
 def _rss_mb() -> float:
