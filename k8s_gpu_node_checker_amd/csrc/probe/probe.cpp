@@ -43,6 +43,13 @@ struct RasCache {
   int64_t eeprom_pages = -1;
 };
 std::vector<RasCache> g_ras;
+// The processor list is enumerated at amdsmi_init.  A driver reload, a GPU reset or a repartition (SPX ->
+// CPX turns one GPU into eight processors) changes it under a long-lived session, so the session is
+// re-opened every g_reopen_s seconds (MI355X_PROBE_REOPEN_S, default 600; 0 = never) and right after a
+// probe in which a GPU stopped answering (its handle may be stale).
+double g_reopen_s = -1.0;  // < 0: not read from the environment yet
+bool g_reenumerate = false;
+std::chrono::steady_clock::time_point g_opened_at;
 
 void jstr(std::string& o, const char* s) {
   o.push_back('"');
@@ -94,6 +101,15 @@ const char* status_name(amdsmi_status_t st) {
   return "AMDSMI_STATUS_UNKNOWN";
 }
 
+void close_locked() {
+  if (!g_open) return;
+  amdsmi_shut_down();
+  g_open = false;
+  g_handles.clear();
+  g_fw.clear();
+  g_ras.clear();
+}
+
 int open_locked() {
   if (g_open) return 0;
   amdsmi_status_t st = amdsmi_init(AMDSMI_INIT_AMD_GPUS);
@@ -121,6 +137,8 @@ int open_locked() {
   g_fw.assign(g_handles.size(), std::string());
   g_ras.assign(g_handles.size(), RasCache());
   g_open = true;
+  g_reenumerate = false;
+  g_opened_at = std::chrono::steady_clock::now();
   g_gpus.store(static_cast<int>(g_handles.size()), std::memory_order_relaxed);
   return 0;
 }
@@ -390,7 +408,7 @@ void probe_telemetry(std::string& o, amdsmi_processor_handle h) {
   }
 }
 
-void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
+bool probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
   auto t0 = std::chrono::steady_clock::now();
   o.push_back('{');
   kv_i64(o, "index", index);
@@ -412,7 +430,7 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
   if (st != AMDSMI_STATUS_SUCCESS) {
     kv_str(o, "error", status_name(st));
     o.push_back('}');
-    return;
+    return false;
   }
   if (asic.target_graphics_version != UINT64_MAX) {
     char buf[32];
@@ -552,6 +570,7 @@ void probe_gpu(std::string& o, int index, amdsmi_processor_handle h) {
   key(o, "probe_us");
   o += std::to_string(static_cast<int64_t>(us));
   o.push_back('}');
+  return true;
 }
 
 char* dup(const std::string& s) {
@@ -589,6 +608,15 @@ extern "C" char* mi355x_probe_json(const char* node_name) {
     snprintf(buf, sizeof buf, "%u.%u.%u", ver.major, ver.minor, ver.release);
     kv_str(o, "amdsmi", buf);
   }
+  if (g_reopen_s < 0) {
+    const char* e = getenv("MI355X_PROBE_REOPEN_S");
+    g_reopen_s = e && *e ? std::max(0.0, atof(e)) : 600.0;
+  }
+  if (g_open && (g_reenumerate ||
+                 (g_reopen_s > 0 &&
+                  std::chrono::duration<double>(std::chrono::steady_clock::now() - g_opened_at).count() >= g_reopen_s)))
+    close_locked();  // enumerate again: the processor list may have changed under the session
+  const bool fresh = !g_open;
   int st = open_locked();
   if (st != 0) {
     kv_str(o, "error", status_name(static_cast<amdsmi_status_t>(st)));
@@ -613,7 +641,9 @@ extern "C" char* mi355x_probe_json(const char* node_name) {
   o.push_back('[');
   for (size_t i = 0; i < g_handles.size(); ++i) {
     if (i) o.push_back(',');
-    probe_gpu(o, static_cast<int>(i), g_handles[i]);
+    // a GPU that stops answering in an older session: enumerate again at the next probe (once: if it
+    // still fails in the fresh session, only the periodic re-open retries it)
+    if (!probe_gpu(o, static_cast<int>(i), g_handles[i]) && !fresh) g_reenumerate = true;
   }
   o.push_back(']');
   double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -629,11 +659,10 @@ extern "C" void mi355x_probe_free(char* doc) { free(doc); }
 
 extern "C" void mi355x_probe_close(void) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_open) {
-    amdsmi_shut_down();
-    g_open = false;
-    g_handles.clear();
-    g_fw.clear();
-    g_ras.clear();
-  }
+  close_locked();
+}
+
+extern "C" void mi355x_probe_set_reopen_interval(double seconds) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_reopen_s = seconds < 0 ? 0.0 : seconds;
 }

@@ -24,6 +24,10 @@ void mi355x_probe_free(char* doc);
 void mi355x_probe_close(void);
 // Number of GPU processors seen by the last successful open (or -1).
 int mi355x_probe_gpu_count(void);
+// Re-enumerate (shut amd-smi down and initialise it again) when the session is this old at a probe, so a
+// driver reload, GPU reset or repartition is seen; 0 = never.  Default 600 s or MI355X_PROBE_REOPEN_S.
+// A probe in which a GPU stopped answering also re-enumerates at the next call.
+void mi355x_probe_set_reopen_interval(double seconds);
 
 #ifdef __cplusplus
 }

@@ -111,6 +111,12 @@ void put(char* dst, size_t len, const std::string& v) {
 extern "C" {
 
 amdsmi_status_t amdsmi_init(uint64_t) {
+  if (const char* log = getenv("AMDSMI_STUB_INIT_LOG")) {
+    if (FILE* fp = fopen(log, "a")) {
+      fputs("init\n", fp);
+      fclose(fp);
+    }
+  }
   load();
   if (g_world.init_status) return static_cast<amdsmi_status_t>(g_world.init_status);
   g_world.open = true;
@@ -118,7 +124,9 @@ amdsmi_status_t amdsmi_init(uint64_t) {
 }
 
 amdsmi_status_t amdsmi_shut_down(void) {
-  g_world.open = false;
+  // the next init reads the scenario again (a changed file = a driver reload / repartition); handles of
+  // this session become invalid, as with the real library
+  g_world = World();
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -54,6 +54,26 @@ def test_native_probe_reports_healthy_mi355x(dev):
     assert rep2["probe_ms"] < 200, rep2["probe_ms"]
 
 
+def test_native_probe_reopens_its_session_cleanly(dev):
+    """Re-enumeration (driver reload / repartition) on the real library: the session is shut down and
+    initialised again between probes, and the GPUs come back the same."""
+    import ctypes
+    import time
+    from k8s_gpu_node_checker_amd.ops import amdsmi_probe as P
+    L = P._native()
+    L.mi355x_probe_set_reopen_interval.argtypes = [ctypes.c_double]
+    first = P.probe_native("n")
+    try:
+        L.mi355x_probe_set_reopen_interval(0.01)
+        for _ in range(3):
+            time.sleep(0.05)
+            r = P.probe_native("n")
+            assert not r.get("error") and [g["bdf"] for g in r["gpus"]] == [g["bdf"] for g in first["gpus"]]
+            assert all(not g.get("error") for g in r["gpus"])
+    finally:
+        L.mi355x_probe_set_reopen_interval(600.0)
+
+
 def test_python_probe_agrees_with_native(dev):
     pytest.importorskip("amdsmi")
     from k8s_gpu_node_checker_amd.ops.amdsmi_probe import probe_native, probe_python

@@ -315,3 +315,46 @@ def test_probe_cli_under_asan_retired_pages_threshold_eeprom(asan_probe, tmp_pat
                          "gpu1: RAS EEPROM checksum invalid (the retired-page list may not survive a reboot)"]
     assert "gpu0: 2 bad HBM page(s) pending retirement (retired at the next GPU reset)" in v.warnings
     assert "gpu1: 9 retired pages, 10 is the driver's threshold" in v.warnings
+
+
+@pytest.mark.slow
+def test_probe_reenumerates_after_a_repartition_or_a_lost_gpu(asan_probe, tmp_path):
+    """The amd-smi session is re-opened when it is older than the re-open interval (a repartition turned
+    2 GPUs into 3 processors here) and right after a probe in which a GPU stopped answering -- once: a GPU
+    that still fails in the fresh session does not re-open it every probe."""
+    d, asan, ubsan = asan_probe
+    scen = tmp_path / "s.txt"
+    scenario(scen, gpus=2)
+    log = tmp_path / "init.log"
+    code = f"""
+import json, time, shutil
+from k8s_gpu_node_checker_amd.ops import amdsmi_probe as P
+L = P._native()
+L.mi355x_probe_set_reopen_interval.argtypes = [__import__('ctypes').c_double]
+out = []
+L.mi355x_probe_set_reopen_interval(0.5)
+out.append(len(P.probe_native('n')['gpus']))
+shutil.copy({str(tmp_path / 's3.txt')!r}, {str(scen)!r})
+out.append(len(P.probe_native('n')['gpus']))   # session younger than 0.5 s: still 2
+time.sleep(0.6)
+out.append(len(P.probe_native('n')['gpus']))   # re-opened: 3
+shutil.copy({str(tmp_path / 'sbad.txt')!r}, {str(scen)!r})
+time.sleep(0.6)
+r = P.probe_native('n'); out.append([g.get('error') for g in r['gpus']])  # re-opened by age, GPU 1 fails
+L.mi355x_probe_set_reopen_interval(0)
+for _ in range(3):
+    P.probe_native('n')
+print(json.dumps(out))
+"""
+    scenario(tmp_path / "s3.txt", gpus=3)
+    scenario(tmp_path / "sbad.txt", gpus=2, per_gpu={1: {"asic_status": 10}})
+    preload = " ".join(x for x in (asan, ubsan, os.environ.get("LD_PRELOAD", "")) if x)
+    env = dict(os.environ, K8SGPU_NATIVE_DIR=str(d), AMDSMI_STUB_SCENARIO=str(scen), AMDSMI_STUB_INIT_LOG=str(log),
+               LD_PRELOAD=preload, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
+               UBSAN_OPTIONS=ASAN_ENV["UBSAN_OPTIONS"])
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=REPO, timeout=120)
+    assert p.returncode == 0 and "runtime error" not in p.stderr, p.stderr[-3000:]
+    import json
+    assert json.loads(p.stdout.splitlines()[-1]) == [2, 2, 3, [None, "AMDSMI_STATUS_NO_PERM"]]
+    # opens: first, age (3 GPUs), age (bad GPU), once more after the failing probe, then no more
+    assert log.read_text().count("init") == 4
