@@ -83,6 +83,23 @@ def gpu_busy(g: Dict[str, Any], own_pids: frozenset = frozenset(), busy_vram_mb:
     return None
 
 
+# HIP errors that say this process's runtime lost its devices (a driver reload or GPU reset under a running
+# agent): not the GPU's fault, and not curable in-process -- the agent needs a fresh process
+_HIP_RUNTIME_LOST = ("no ROCm-capable device", "invalid device ordinal", "initialization error",
+                     "context is destroyed", "hipErrorNoDevice", "hipErrorInvalidDevice", "hipErrorNotInitialized",
+                     "hipErrorContextIsDestroyed")
+
+
+def runtime_lost(res: Dict[str, Any]) -> Optional[str]:
+    """The first detail when every test of one GPU's diagnostic result failed because the HIP runtime lost
+    its devices, else None."""
+    tests = [r for r in res.values() if isinstance(r, dict)]
+    details = [str(r.get("detail", "")) for r in tests if r.get("pass") is False]
+    if details and len(details) == len(tests) and all(any(m in d for m in _HIP_RUNTIME_LOST) for d in details):
+        return details[0]
+    return None
+
+
 def normalize_bdf(bdf: Any) -> str:
     """PCI address in amd-smi's form (``0000:05:00.0``, lower case); a domain-less ``05:00.0`` gets 0000."""
     b = str(bdf or "").strip().lower()
@@ -218,6 +235,9 @@ class Agent:
         self._diag_threads: Dict[int, Any] = {}  # device -> (thread, start time, result box) until it returns
         self.diag_timeout = diag_timeout
         self._diag_skipped: Dict[int, str] = {}
+        # set when the HIP runtime lost its devices (runtime_lost): no further diagnostics in this process,
+        # /healthz answers 503 so the liveness probe restarts the agent
+        self.hip_lost: Optional[str] = None
         self._fabric: Optional[Dict[str, Any]] = None
         self._fabric_at = float("-inf")
         self._bdf: Dict[int, str] = {}  # HIP ordinal -> PCI address (amd-smi and HIP enumerate independently)
@@ -309,7 +329,7 @@ class Agent:
         # own device, so an 8-GPU node is checked in the time of one GPU instead of eight.  A GPU whose
         # diagnostic never returns (a hung queue) is reported as failed after `diag_timeout` s instead of
         # freezing the agent into a stale report; nothing new is started on it while that thread lives.
-        run = [d for d in run if d not in self._diag_threads]
+        run = [d for d in run if d not in self._diag_threads] if self.hip_lost is None else []
         for d in run:
             box: Dict[str, Any] = {}
 
@@ -328,13 +348,22 @@ class Agent:
             t.join(max(0.0, started + self.diag_timeout - time.time()))
             if not t.is_alive():
                 del self._diag_threads[d]
-                if "res" in box:
+                lost = runtime_lost(box["res"]) if "res" in box else None
+                if lost is not None:
+                    if self.hip_lost is None:
+                        print(f"HIP runtime lost its devices ({lost}); diagnostics stop, /healthz fails so the "
+                              "agent is restarted", file=sys.stderr, flush=True)
+                    self.hip_lost = lost
+                elif "res" in box:
                     self._diag_cache[d] = box["res"]
                 self._diag_at[d] = started
             else:
                 self._diag_cache[d] = {"watchdog": {
                     "pass": False, "detail": f"diagnostics did not finish within {self.diag_timeout:g} s (GPU hang?)"}}
                 self._diag_at[d] = started
+        if self.hip_lost is not None:
+            for d in devices:
+                self._diag_skipped[d] = f"HIP runtime lost its devices ({self.hip_lost[:120]}): agent restart pending"
         if (self.diag_level >= 2 and self.devices is None and len(devices) >= 2 and not self._diag_skipped
                 and not self._diag_threads
                 and now - self._fabric_at >= self.diag_interval):
@@ -651,8 +680,10 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
             elif self.path.startswith("/healthz"):
                 last = agent.last_probe_done if agent.last_probe_done is not None else started
                 idle = time.monotonic() - last
-                if stale_after is not None and idle > stale_after:
-                    body = f"no probe completed for {idle:.0f} s".encode()
+                lost = agent.hip_lost
+                if lost is not None or (stale_after is not None and idle > stale_after):
+                    body = (f"HIP runtime lost its devices: {lost}" if lost is not None
+                            else f"no probe completed for {idle:.0f} s").encode()
                     self.send_response(503)
                     self.send_header("Content-Type", "text/plain")
                     self.send_header("Content-Length", str(len(body)))

@@ -241,3 +241,33 @@ def test_healthz_turns_503_when_probes_stop(monkeypatch):
         srv.shutdown()
         srv.server_close()
     assert w.gpus
+
+
+def test_hip_runtime_losing_its_devices_restarts_the_agent_not_the_verdict(monkeypatch):
+    """After a driver reload under a running agent every HIP call fails: that is the process's runtime, not
+    the GPU.  The agent records no failed diagnostic (the verdict stays healthy), starts no more of them,
+    and /healthz answers 503 so the liveness probe restarts it."""
+    import urllib.error
+    import urllib.request
+    w = World(monkeypatch)
+    lost = "mi355x diag failed (-1): hipSetDevice(device): no ROCm-capable device is detected"
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: (
+        w.runs.append(d), {"gemm": {"pass": False, "detail": lost}, "hbm": {"pass": False, "detail": lost}})[1])
+    ag = A.Agent("n", source="fake", diag_level=1, diag_interval=0.0)
+    srv = A.serve(ag, "127.0.0.1", 0, stale_after=60)
+    try:
+        rep = ag.probe_once()
+        assert rep["state"] == "healthy" and "diag" not in rep["gpus"][0]
+        assert rep["gpus"][0]["diag_skipped"].startswith("HIP runtime lost its devices (mi355x diag failed")
+        assert ag.hip_lost == lost and len(w.runs) == 2
+        ag.probe_once()
+        assert len(w.runs) == 2  # nothing new starts in this process
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(f"http://127.0.0.1:{srv.server_address[1]}/healthz", timeout=5)
+        assert e.value.code == 503 and b"HIP runtime lost its devices" in e.value.read()
+    finally:
+        srv.shutdown()
+        srv.server_close()
+    # a GPU fault (illegal address) is still the GPU's failure
+    assert A.runtime_lost({"gemm": {"pass": False, "detail": "hipMemcpy: an illegal memory access"}}) is None
+    assert A.runtime_lost({"gemm": {"pass": False, "detail": lost}, "hbm": {"pass": True}}) is None
