@@ -240,6 +240,7 @@ class Agent:
         self.hip_lost: Optional[str] = None
         self._fabric: Optional[Dict[str, Any]] = None
         self._fabric_at = float("-inf")
+        self._fabric_thread: Optional[Any] = None  # (thread, start time, result box) until it returns
         self._bdf: Dict[int, str] = {}  # HIP ordinal -> PCI address (amd-smi and HIP enumerate independently)
         self.last: Optional[Dict[str, Any]] = None
         self.last_probe_done: Optional[float] = None  # monotonic time of the last completed probe (/healthz)
@@ -365,25 +366,48 @@ class Agent:
             for d in devices:
                 self._diag_skipped[d] = f"HIP runtime lost its devices ({self.hip_lost[:120]}): agent restart pending"
         if (self.diag_level >= 2 and self.devices is None and len(devices) >= 2 and not self._diag_skipped
-                and not self._diag_threads
+                and not self._diag_threads and self._fabric_thread is None
                 and now - self._fabric_at >= self.diag_interval):
-            # node-level: every ordered GPU pair over xGMI (after the per-GPU tests, so no contention);
-            # it touches every GPU, so it waits until none is busy
-            try:
-                m = diag.p2p_matrix(devices)
-                self._fabric = {"p2p": {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s")}}
-            except Exception as e:
-                self._fabric = {"p2p": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
-            # the collectives the node's jobs run, over the same links: RCCL in this process (ops/fabric.py)
-            try:
-                from ..ops import fabric
-                r = fabric.collective_suite(devices)
-                self._fabric["rccl"] = {k: r.get(k) for k in ("pass", "best_busbw_gbps", "best_busbw_by_op",
-                                                              "detail", "wall_s", "rccl")}
-            except Exception as e:
-                self._fabric["rccl"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
-            self._fabric_at = now
+            # node-level: every ordered GPU pair over xGMI (after the per-GPU tests, so no contention) and the
+            # RCCL collectives; it touches every GPU, so it waits until none is busy.  On its own thread under
+            # the same watchdog as the per-GPU tests: a collective that never completes (a link that stopped
+            # passing traffic) is a failed fabric, not a frozen agent.
+            box: Dict[str, Any] = {}
+            t = threading.Thread(target=lambda: box.update(res=self._fabric_suite(devices)), name="diag-fabric",
+                                 daemon=True)
+            self._fabric_thread = (t, now, box)
+            t.start()
+        if self._fabric_thread is not None:
+            t, started, box = self._fabric_thread
+            t.join(max(0.0, started + self.diag_timeout - time.time()))
+            self._fabric_at = started
+            if not t.is_alive():
+                self._fabric_thread = None
+                self._fabric = box.get("res")
+            else:
+                self._fabric = {"watchdog": {
+                    "pass": False,
+                    "detail": f"node-level xGMI/RCCL tests did not finish within {self.diag_timeout:g} s (fabric hang?)"}}
         return {d: self._diag_cache[d] for d in devices if d in self._diag_cache}
+
+    @staticmethod
+    def _fabric_suite(devices: List[int]) -> Dict[str, Any]:
+        """The node-level tests: xGMI pair matrix and the RCCL collectives in this process (ops/fabric.py)."""
+        from ..ops import diag
+        out: Dict[str, Any] = {}
+        try:
+            m = diag.p2p_matrix(devices)
+            out["p2p"] = {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s")}
+        except Exception as e:
+            out["p2p"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
+        try:
+            from ..ops import fabric
+            r = fabric.collective_suite(devices)
+            out["rccl"] = {k: r.get(k) for k in ("pass", "best_busbw_gbps", "best_busbw_by_op", "detail", "wall_s",
+                                                 "rccl")}
+        except Exception as e:
+            out["rccl"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
+        return out
 
     def _allocated(self) -> Optional[Dict[str, str]]:
         """Devices the kubelet allocated to pods (normalised BDF -> "ns/pod"), or None when unknown."""

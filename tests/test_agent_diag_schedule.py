@@ -271,3 +271,28 @@ def test_hip_runtime_losing_its_devices_restarts_the_agent_not_the_verdict(monke
     # a GPU fault (illegal address) is still the GPU's failure
     assert A.runtime_lost({"gemm": {"pass": False, "detail": "hipMemcpy: an illegal memory access"}}) is None
     assert A.runtime_lost({"gemm": {"pass": False, "detail": lost}, "hbm": {"pass": True}}) is None
+
+
+def test_a_hung_fabric_test_is_a_failure_not_a_frozen_agent(monkeypatch):
+    import threading
+    w = World(monkeypatch, n=2)
+    release = threading.Event()
+
+    def hang(devs):
+        w.fabric_runs += 1
+        release.wait(10)
+        return {"pass": True, "best_busbw_gbps": 300.0, "best_busbw_by_op": {}, "detail": "", "wall_s": 9.0}
+    monkeypatch.setattr(fabric, "collective_suite", hang)
+    ag = A.Agent("n", source="fake", diag_level=2, diag_interval=0.0, diag_timeout=0.3)
+    t0 = time.monotonic()
+    rep = ag.probe_once()
+    assert time.monotonic() - t0 < 3  # the probe came back
+    assert rep["fabric"]["watchdog"]["pass"] is False and "fabric hang" in rep["fabric"]["watchdog"]["detail"]
+    assert rep["state"] == "unhealthy"
+    runs = w.fabric_runs  # the pair matrix and the hung collectives
+    rep = ag.probe_once()  # still stuck: no second suite starts
+    assert w.fabric_runs == runs and "watchdog" in rep["fabric"]
+    release.set()
+    time.sleep(0.2)
+    rep = ag.probe_once()  # it finished: its real result replaces the watchdog failure
+    assert rep["fabric"]["rccl"]["pass"] and rep["fabric"]["p2p"]["pass"]
