@@ -817,7 +817,13 @@ def main(argv: Optional[List[str]] = None) -> int:
         host, _, port = args.listen.rpartition(":")
         # a probe cycle may legitimately include diagnostics (up to --diag-timeout per GPU)
         serve(agent, host or "0.0.0.0", int(port), stale_after=max(180.0, 3 * args.interval + args.diag_timeout))
-    while True:
+    # SIGTERM (pod deletion, rolling update): finish the cycle in flight and leave with 0 instead of dying
+    # mid-write; the condition keeps its last heartbeat and ages out at the checker's --probe-max-age
+    stop = threading.Event()
+    if threading.current_thread() is threading.main_thread():
+        import signal
+        signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    while not stop.is_set():
         started = time.monotonic()
         rep = agent.probe_once()
         if "stdout" in pubs:
@@ -831,7 +837,9 @@ def main(argv: Optional[List[str]] = None) -> int:
                 print(f"node status publish failed: {e}", file=sys.stderr, flush=True)
         if args.once:  # a one-shot run (CI, a harness) says whether the node saw its verdict
             return 0 if published else 1
-        time.sleep(max(0.0, args.interval - (time.monotonic() - started)))
+        stop.wait(max(0.0, args.interval - (time.monotonic() - started)))
+    print("SIGTERM: agent stopped", file=sys.stderr, flush=True)
+    return 0
 
 
 if __name__ == "__main__":

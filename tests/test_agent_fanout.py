@@ -341,3 +341,24 @@ def test_agent_xgmi_links_flag(mock_cluster, tmp_path):
         cond = [c for c in srv.state.find("mi355x-node-0000")["status"]["conditions"]
                 if c["type"] == "AMDGPUHealthy"][0]
         assert cond["status"] == status, (links, cond)
+
+
+def test_agent_exits_cleanly_on_sigterm(tmp_path):
+    import signal
+    import subprocess
+    import sys
+    import time as _t
+    fx = tmp_path / "p.json"
+    fx.write_text(json.dumps(fixtures.mi355x_probe_report("x", gpus=1)))
+    p = subprocess.Popen([sys.executable, "-m", "k8s_gpu_node_checker_amd.agent.agent", "--node", "n", "--source",
+                          "fixture", "--fixture", str(fx), "--publish", "stdout", "--interval", "30"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        assert json.loads(p.stdout.readline())["state"] == "healthy"  # the first cycle ran; now it sleeps
+        t0 = _t.monotonic()
+        p.send_signal(signal.SIGTERM)
+        out, err = p.communicate(timeout=20)
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert p.returncode == 0 and "SIGTERM: agent stopped" in err and _t.monotonic() - t0 < 10
