@@ -138,7 +138,7 @@ def fleet_versions(extras: List[Any]) -> Optional[Dict[str, Any]]:
     firmware: Dict[str, Dict[str, int]] = {}
     n = 0
     for ex in extras:
-        rep = H.parse_annotation(ex.health_annotation) if ex is not None else None
+        rep = ex.report() if ex is not None else None
         if not rep or rep.get("error"):
             continue
         n += 1
@@ -146,11 +146,15 @@ def fleet_versions(extras: List[Any]) -> Optional[Dict[str, Any]]:
         if drv:
             rel = H.driver_release(drv)
             drivers[rel] = drivers.get(rel, 0) + 1
-        node_fw: Dict[str, set] = {}
+        raw_fw: Dict[str, set] = {}
         for g in rep.get("gpus") or []:
             for name, ver in ((g.get("fw") or {}) if isinstance(g, dict) and isinstance(g.get("fw"), dict)
                               else {}).items():
-                node_fw.setdefault(name, set()).add(H.fw_version_str(name, ver))
+                try:
+                    raw_fw.setdefault(name, set()).add(ver)
+                except TypeError:  # an unhashable value: kept as its text
+                    raw_fw.setdefault(name, set()).add(str(ver))
+        node_fw = {name: {H.fw_version_str(name, v) for v in vers} for name, vers in raw_fw.items()}
         for name, vers in node_fw.items():
             row = firmware.setdefault(name, {})
             for v in vers:  # a node with two versions of one image counts under both
@@ -207,7 +211,7 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
             expected = max(cap or 0, alloc or 0)  # models.node.expected_gpu_count
             v: Optional[H.Verdict] = None
             if rep is None and reeval:
-                rep = H.parse_annotation(ex.health_annotation)
+                rep = ex.report()
             if rep is None and ex.health_condition is not None:
                 # cheap path: the agent's verdict is a NodeCondition already parsed by the scan
                 v = from_condition(ex.health_condition, max_age, now, expected)
@@ -215,7 +219,7 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
                     unapplied.append(node["name"])
             else:
                 if rep is None:
-                    rep = H.parse_annotation(ex.health_annotation)
+                    rep = ex.report()
                 if rep is not None or policy == "require":
                     v = H.evaluate_report(rep, expected, exp, now)
             if v is None:

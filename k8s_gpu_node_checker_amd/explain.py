@@ -79,7 +79,7 @@ def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> 
         status, reason, message, hb = ex.health_condition
         doc["health_condition"] = {"status": status, "reason": reason, "message": message,
                                    "heartbeat_age_s": round(now - hb, 1) if hb else None}
-    rep = H.parse_annotation(ex.health_annotation)
+    rep = ex.report()
     if rep and rep.get("error"):
         doc["report"] = {"error": rep["error"]}
     elif rep:

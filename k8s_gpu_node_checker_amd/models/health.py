@@ -218,6 +218,9 @@ def firmware_mismatch(gpus: Sequence[Any]) -> List[str]:
     update that stopped half-way, and GPUs that will behave differently under the same job.  One entry
     per image: ``psp_sos: gpu0-6 00.45.00.2F, gpu7 00.45.00.00``; versions are stable, so the condition
     message stays stable probe to probe."""
+    fws = [g["fw"] for g in gpus if isinstance(g, dict) and isinstance(g.get("fw"), dict)]
+    if not fws or all(f == fws[0] for f in fws):
+        return []  # the common case, settled by dict equality
     seen: Dict[str, Dict[Any, List[Any]]] = {}
     for g in gpus:
         if not isinstance(g, dict) or not isinstance(g.get("fw"), dict):
@@ -233,9 +236,21 @@ def firmware_mismatch(gpus: Sequence[Any]) -> List[str]:
     return out
 
 
+_BDF_CACHE: Dict[Any, str] = {}
+
+
 def _bdf(b: Any) -> str:
-    b = str(b or "").strip().lower()
-    return "0000:" + b if b.count(":") == 1 else b
+    """PCI address, normalised (lower case, domain added); memoised: the same few addresses recur on every
+    GPU of every node of a fleet (1000 8-GPU reports carry ~0.5 M of them)."""
+    try:
+        return _BDF_CACHE[b]
+    except (KeyError, TypeError):
+        pass
+    n = str(b or "").strip().lower()
+    n = "0000:" + n if n.count(":") == 1 else n
+    if isinstance(b, str) and len(_BDF_CACHE) < 65536:
+        _BDF_CACHE[b] = n
+    return n
 
 
 def xgmi_topology(gpus: Sequence[Any], links_expected: int) -> List[str]:
@@ -264,19 +279,19 @@ def xgmi_topology(gpus: Sequence[Any], links_expected: int) -> List[str]:
         str(g.get("compute_partition") or "SPX").upper() == "SPX" for g in gs)
     if not full_board:
         return out
+    peer_sets = {me: {_bdf(p) for p in g["xgmi_peers"]} for me, g in bdfs.items()
+                 if isinstance(g.get("xgmi_peers"), list)}
+    board = set(bdfs)
     # a VM that remaps the GPUs' PCI addresses sees its links name host addresses none of its GPUs
     # carry: nothing to match the wiring against, so it is not judged
-    named = {_bdf(p) for g in bdfs.values() if isinstance(g.get("xgmi_peers"), list) for p in g["xgmi_peers"]}
-    if not named & set(bdfs):
+    if not any(ps & board for ps in peer_sets.values()):
         return out
-    for me, g in bdfs.items():
-        peers = g.get("xgmi_peers")
-        if not isinstance(peers, list):
-            continue
-        reached = {_bdf(p) for p in peers} & (set(bdfs) - {me})
-        foreign = sorted({_bdf(p) for p in peers} - set(bdfs))
+    for me, ps in peer_sets.items():
+        g = bdfs[me]
+        reached = ps & (board - {me})
+        foreign = sorted(ps - board)
         if len(reached) < links_expected:
-            missing = sorted(set(bdfs) - reached - {me})
+            missing = sorted(board - reached - {me})
             out.append(f"gpu{g.get('index', '?')}: xGMI links reach {len(reached)} of the node's {len(bdfs) - 1} "
                        f"other GPUs (no link to {', '.join(missing[:3])}{' ...' if len(missing) > 3 else ''})"
                        + (f", {len(foreign)} to devices outside the node" if foreign else ""))
@@ -659,7 +674,15 @@ def parse_annotation(raw: Optional[str]) -> Optional[Dict[str, Any]]:
         import gzip
         import zlib
         try:
-            raw = gzip.decompress(base64.b64decode(raw[len(GZIP_PREFIX):], validate=True)).decode("utf-8")
+            data = base64.b64decode(raw[len(GZIP_PREFIX):], validate=True)
+            try:  # one gzip member, as the agent writes it: zlib directly (GzipFile costs ~3x as much)
+                d = zlib.decompressobj(16 + zlib.MAX_WBITS)
+                body = d.decompress(data)
+                if not d.eof or d.unused_data:
+                    raise zlib.error("not a single complete member")
+            except zlib.error:
+                body = gzip.decompress(data)  # several members / trailing data: the general reader decides
+            raw = body.decode("utf-8")
         except (binascii.Error, OSError, EOFError, zlib.error, UnicodeDecodeError, ValueError):
             return {"schema": SCHEMA, "error": "annotation is not gzip+base64 JSON", "ts": time.time()}
     from ..ops.fastpath import loads  # native json.loads (falls back to the json package itself)

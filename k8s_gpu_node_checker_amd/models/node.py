@@ -95,11 +95,14 @@ def project_node(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEY
     }
 
 
+_UNPARSED = object()
+
+
 class NodeExtras:
     """Side information the default report does not show but the health gate uses."""
 
     __slots__ = ("ready_condition", "capacity", "allocatable", "unschedulable", "health_annotation", "internal_ip",
-                 "health_condition")
+                 "health_condition", "_report")
 
     def __init__(self, ready_condition: bool, capacity: Dict[str, int], allocatable: Dict[str, int],
                  unschedulable: bool, health_annotation: Optional[str], internal_ip: Optional[str] = None,
@@ -112,6 +115,20 @@ class NodeExtras:
         self.internal_ip = internal_ip
         #: ``(status, reason, message, lastHeartbeatTime epoch)`` of the AMDGPUHealthy condition
         self.health_condition = health_condition
+        self._report: Any = _UNPARSED
+
+    def report(self) -> Optional[Dict[str, Any]]:
+        """The report annotation parsed (``models.health.parse_annotation``), once per node object: the
+        health gate, ``--json-extended``'s fleet view and ``--explain`` share it, and the watcher keeps the
+        object until the node changes."""
+        try:
+            r = self._report
+        except AttributeError:  # built by the native scanner, which sets only __init__'s slots
+            r = _UNPARSED
+        if r is _UNPARSED:
+            from .health import parse_annotation
+            r = self._report = parse_annotation(self.health_annotation)
+        return r
 
     def to_dict(self) -> Dict[str, Any]:
         return {
