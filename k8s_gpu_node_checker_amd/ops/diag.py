@@ -59,9 +59,10 @@ REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
     "hbm": {"copy_tbs": 6.49, "read_tbs": 6.96},   # 16-byte copy (read + write bytes counted) / read, TB/s
     "mfma": {"bf16": 1901.0, "fp8": 1940.0, "mxfp8": 4326.0, "mxfp4": 7610.0},  # register-resident burn-in
     "host_link": {"h2d_gbps": 57.0, "d2h_gbps": 56.8},  # pinned copies over PCIe Gen5 x16
-    # per-XCD HBM reads, 8 x 256 MiB slices read twice: all XCDs together 6.02-6.25 TB/s, each XCD alone
-    # 1.28-1.33 TB/s (profiles/hbm_xcd_explore_mi355x.json)
-    "hbm_xcd": {"read_tbs": 6.0, "alone_tbs": 1.28},
+    # per-XCD HBM reads, 8 x 256 MiB slices read twice: all XCDs together 5.83-6.27 TB/s (a cold level-2
+    # run and 1,299 level-1 soak rounds), each XCD alone 1.23-1.33 TB/s (profiles/hbm_xcd_explore_mi355x.json,
+    # profiles/soak_level1_hbm_xcd_mi355x.json)
+    "hbm_xcd": {"read_tbs": 5.8, "alone_tbs": 1.28},
     "l2": {"read_tbs": 30.5},                      # per-XCD L2 reads, 2 MiB slices, 8 WG/CU: 31.6-31.9 measured
                                                    # (profiles/l2_explore_mi355x.json; 34.5 TB/s is the L2's own figure)
 }
