@@ -207,3 +207,17 @@ def test_image_carries_every_third_party_runtime_import():
     optional = {"torch", "amdsmi"}
     assert third <= set(installed) | optional, third - set(installed) - optional
     assert all(installed[m] for m in third & set(installed)), installed
+
+
+def test_agent_port_network_policy_selects_the_agent_and_its_port():
+    pol = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "monitoring", "networkpolicy.yaml")))
+               if d)
+    ds = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
+    pod = ds["spec"]["template"]
+    assert pol["metadata"]["namespace"] == ds["metadata"]["namespace"]
+    assert pol["spec"]["podSelector"]["matchLabels"].items() <= pod["metadata"]["labels"].items()
+    assert not pod["spec"].get("hostNetwork")  # a host-network pod would ignore the policy
+    ports = {p["name"] for c in pod["spec"]["containers"] for p in c.get("ports", [])}
+    assert {p["port"] for r in pol["spec"]["ingress"] for p in r["ports"]} <= ports
+    kust = yaml.safe_load(open(os.path.join(REPO, "deploy", "monitoring", "kustomization.yaml")))
+    assert "networkpolicy.yaml" in kust["resources"]
