@@ -10,7 +10,8 @@ HBM bandwidth, memtest) at ``--diag-level``.  The merged report is published
   verdict from the LIST it already does, zero extra API calls, no JSON to
   parse per node) plus the full report as the annotation
   ``amd.com/mi355x-health`` (``--json-extended`` details, ``--health-reeval``), and/or
-* over HTTP at ``/probe`` (JSON) and ``/metrics`` (Prometheus) for the
+* over HTTP at ``/probe`` (JSON), ``/metrics`` (Prometheus) and ``/status`` (text, for a person with
+  ``kubectl port-forward``) for the
   checker's ``--probe-endpoint`` fan-out, and/or
 * on stdout (``--publish stdout``, one JSON line per probe).
 
@@ -682,7 +683,7 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
 
 
 def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = None) -> ThreadingHTTPServer:
-    """/probe, /metrics and /healthz; /healthz answers 503 once no probe has completed for
+    """/probe, /metrics, /status (text) and /healthz; /healthz answers 503 once no probe has completed for
     ``stale_after`` s (a wedged amd-smi call or driver), so a livenessProbe restarts the agent."""
     started = time.monotonic()
 
@@ -701,6 +702,14 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
             elif self.path.startswith("/metrics"):
                 body = _metrics(rep).encode()
                 ctype = "text/plain; version=0.0.4"
+            elif self.path.startswith("/status"):
+                # the last report for a human (kubectl port-forward): verdict, reasons, per-GPU table
+                if rep:
+                    from ..explain import report_text
+                    body = report_text(rep, agent.evaluate(rep)).encode()
+                else:
+                    body = b"no probe yet\n"
+                ctype = "text/plain; charset=utf-8"
             elif self.path.startswith("/healthz"):
                 last = agent.last_probe_done if agent.last_probe_done is not None else started
                 idle = time.monotonic() - last

@@ -57,6 +57,36 @@ def _gpu_row(e: Dict[str, Any]) -> List[str]:
             txt(e["pm_fw"], "-"), dstate, "; ".join(e["findings"]) or "ok"]
 
 
+def gpu_table(entries: List[Dict[str, Any]]) -> List[str]:
+    """The per-GPU table (one line per :func:`_gpu_entry`, header first), as ``--explain`` and the agent's
+    ``/status`` print it."""
+    rows = [list(_COLUMNS)] + [_gpu_row(e) for e in entries]
+    widths = [max(len(r[c]) for r in rows) for c in range(len(_COLUMNS) - 1)]
+    return ["  ".join(r[c].ljust(widths[c]) for c in range(len(_COLUMNS) - 1)) + "  " + r[-1] for r in rows]
+
+
+def report_text(rep: Dict[str, Any], verdict: Any) -> str:
+    """One report and its verdict as text (the agent's ``/status``): verdict, reasons and warnings, the
+    per-GPU table, node-level findings, GPUs whose diagnostics were skipped and why."""
+    drv = rep.get("driver") if isinstance(rep.get("driver"), dict) else {}
+    lines = [f"node {rep.get('node', '?')}: MI355X verdict {verdict.state}, {verdict.gpus_ok}/{verdict.gpus_seen} GPUs "
+             f"ok (probe {rep.get('probe', '?')}, amd-smi {rep.get('amdsmi', '?')}, driver "
+             f"{H.driver_release(drv.get('version')) if drv.get('version') else '?'})"]
+    if rep.get("error"):
+        lines.append(f"  probe error: {rep['error']}")
+    for title in ("reasons", "warnings"):
+        for r in getattr(verdict, title):
+            lines.append(f"  {title[:-1]}: {r}")
+    found = verdict.reasons + verdict.warnings
+    entries = [_gpu_entry(g, found) for g in rep.get("gpus") or [] if isinstance(g, dict)]
+    if entries:
+        lines += ["  " + ln for ln in gpu_table(entries)]
+    for g in rep.get("gpus") or []:
+        if isinstance(g, dict) and g.get("diag_skipped"):
+            lines.append(f"  gpu{g.get('index', '?')} diagnostics skipped: {g['diag_skipped']}")
+    return "\n".join(lines) + "\n"
+
+
 def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> Dict[str, Any]:
     """Everything ``--explain`` says about one node, as data (``--explain NODE --json`` prints it)."""
     opts.json_extended = True  # the full report annotation is read (annotation mode 2)
@@ -128,10 +158,8 @@ def render(doc: Dict[str, Any], out: TextIO) -> None:
     elif rep:
         out.write(f"report: probe {rep['probe'] or '?'}, amd-smi {rep['amdsmi'] or '?'}, driver "
                   f"{rep['driver'] or '?'}, {len(rep['gpus'])} GPUs\n")
-        rows = [list(_COLUMNS)] + [_gpu_row(e) for e in rep["gpus"]]
-        widths = [max(len(r[c]) for r in rows) for c in range(len(_COLUMNS) - 1)]
-        for r in rows:
-            out.write("  " + "  ".join(r[c].ljust(widths[c]) for c in range(len(_COLUMNS) - 1)) + "  " + r[-1] + "\n")
+        for ln in gpu_table(rep["gpus"]):
+            out.write("  " + ln + "\n")
         for ln in rep["node_findings"]:
             out.write(f"  node: {ln}\n")
     out.write(f"=> counts as Ready: {'yes' if doc['counts_as_ready'] else 'no'}\n")

@@ -296,3 +296,24 @@ def test_a_hung_fabric_test_is_a_failure_not_a_frozen_agent(monkeypatch):
     time.sleep(0.2)
     rep = ag.probe_once()  # it finished: its real result replaces the watchdog failure
     assert rep["fabric"]["rccl"]["pass"] and rep["fabric"]["p2p"]["pass"]
+
+
+def test_status_endpoint_is_the_verdict_in_text(monkeypatch):
+    import urllib.request
+    w = World(monkeypatch)
+    w.gpus[1]["ecc_uncorrectable"] = 3
+    ag = A.Agent("n", source="fake")
+    srv = A.serve(ag, "127.0.0.1", 0)
+    url = f"http://127.0.0.1:{srv.server_address[1]}/status"
+    try:
+        assert urllib.request.urlopen(url, timeout=5).read() == b"no probe yet\n"
+        ag.probe_once()
+        txt = urllib.request.urlopen(url, timeout=5).read().decode()
+    finally:
+        srv.shutdown()
+        srv.server_close()
+    lines = txt.splitlines()
+    assert lines[0].startswith("node n: MI355X verdict unhealthy, 1/2 GPUs ok (probe fake")
+    assert "  reason: gpu1: 3 uncorrectable ECC errors" in lines
+    row1 = next(ln for ln in lines if ln.startswith("  1 "))
+    assert "0000:01:00.0" in row1 and row1.endswith("3 uncorrectable ECC errors")
