@@ -58,6 +58,8 @@ CE_MIN_SPAN_S = 600.0
 DIAG_WHEN = ("idle", "always")
 # per-GPU fields kept out of the node annotation (Agent.annotation)
 _ANNOTATION_DROP = frozenset(("xgmi_kb", "throttle_acc", "procs", "probe_us"))
+# a JSON report annotation above this goes out gzip-encoded (the apiserver caps a node's annotations at 256 KiB)
+ANNOTATION_JSON_MAX = 128 << 10
 
 
 def gpu_busy(g: Dict[str, Any], own_pids: frozenset = frozenset(), busy_vram_mb: int = 2048,
@@ -201,6 +203,7 @@ class Agent:
         if annotation_encoding not in ("json", "gzip"):
             raise ValueError("annotation_encoding must be json or gzip")
         self.annotation_encoding = annotation_encoding
+        self._gz_fallback_noted = False
         # --label-node: node_labels() kept on the Node, written when they change
         self.label_node = label_node
         self._labels: Optional[Dict[str, Optional[str]]] = None
@@ -501,7 +504,18 @@ class Agent:
         bytes there; they stay on ``/probe`` and ``/metrics``."""
         gpus = [{k: v for k, v in g.items() if k not in _ANNOTATION_DROP} if isinstance(g, dict) else g
                 for g in rep.get("gpus") or []]
-        return {HEALTH_ANNOTATION: encode_annotation(dict(rep, gpus=gpus), self.annotation_encoding)}
+        doc = dict(rep, gpus=gpus)
+        value = encode_annotation(doc, self.annotation_encoding)
+        if len(value) > ANNOTATION_JSON_MAX and self.annotation_encoding == "json":
+            # a node's annotations share 256 KiB; a CPX node's 64 processors at level 2 come near that as
+            # JSON, so an oversized report goes out gzip-encoded (the checker reads both) instead of being
+            # rejected
+            if not self._gz_fallback_noted:
+                print(f"report annotation is {len(value)} bytes as JSON: writing it gzip-encoded", file=sys.stderr,
+                      flush=True)
+                self._gz_fallback_noted = True
+            value = encode_annotation(doc, "gzip")
+        return {HEALTH_ANNOTATION: value}
 
     def condition(self, rep: Dict[str, Any]) -> Dict[str, Any]:
         v = self.evaluate(rep)

@@ -362,3 +362,21 @@ def test_agent_exits_cleanly_on_sigterm(tmp_path):
         if p.poll() is None:
             p.kill()
     assert p.returncode == 0 and "SIGTERM: agent stopped" in err and _t.monotonic() - t0 < 10
+
+
+def test_oversized_json_annotation_goes_out_gzip_encoded(capsys):
+    from k8s_gpu_node_checker_amd.models import health as H
+    from k8s_gpu_node_checker_amd.models.node import HEALTH_ANNOTATION
+    ag = A.Agent("n", source="fixture")
+    small = fixtures.mi355x_probe_report("n", gpus=8)
+    assert ag.annotation(small)[HEALTH_ANNOTATION].startswith("{")  # JSON as configured
+    # a CPX node: 64 processors with fat level-2 diagnostic results
+    big = fixtures.mi355x_probe_report("n", gpus=64)
+    for g in big["gpus"]:
+        g["diag"] = {f"t{i}": {"pass": True, "detail": "x" * 200, "map": {"xcds": {str(x): {"rel_time": 1.0}
+                                                                                  for x in range(8)}}}
+                     for i in range(8)}
+    v = ag.annotation(big)[HEALTH_ANNOTATION]
+    assert v.startswith(H.GZIP_PREFIX) and len(v) < A.ANNOTATION_JSON_MAX
+    assert H.parse_annotation(v)["gpus"][63]["diag"]["t7"]["pass"] is True
+    assert "writing it gzip-encoded" in capsys.readouterr().err
