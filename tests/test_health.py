@@ -356,3 +356,13 @@ def test_allocatable_below_capacity_is_a_degraded_hint(run_cli, mock_cluster, tm
     # --mi355x counts allocatable GPUs: the node is still a GPU node with 7
     p = run_cli(["--kubeconfig", kc, "--json", "--mi355x"])
     assert json.loads(p.stdout)["nodes"][0]["gpus"] == 7
+
+
+def test_partitions_are_judged_on_down_links_only():
+    exp = H.HealthExpectations()  # 7 links per GPU
+    for part in ("CPX", "DPX"):
+        assert H.evaluate_report(rep(gpu0={"xgmi": "XXXXXXXX", "compute_partition": part}), 8, exp).state \
+            != H.UNHEALTHY
+        assert "xGMI link(s) down" in " ".join(
+            H.evaluate_report(rep(gpu0={"xgmi": "XUUUDUUU", "compute_partition": part}), 8, exp).reasons)
+    assert H.evaluate_report(rep(gpu0={"xgmi": "XXXXXXXX"}), 8, exp).state == H.UNHEALTHY  # SPX: all 7 must be Up
