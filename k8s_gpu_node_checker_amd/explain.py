@@ -148,7 +148,7 @@ def render(doc: Dict[str, Any], out: TextIO) -> None:
         out.write(f"MI355X verdict: none (policy {doc['health_policy']}: the reference's Ready rule applies)\n")
     else:
         out.write(f"MI355X verdict: {v['state']}, {v['gpus_ok']}/{v['gpus_seen']} GPUs ok"
-                  + (f", report {_age(v['age_s'])} old" if v.get("age_s") is not None else "") + "\n")
+                  + (f", published {_age(v['age_s'])} ago" if v.get("age_s") is not None else "") + "\n")
         for title in ("reasons", "warnings"):
             for r in v.get(title) or []:
                 out.write(f"  {title[:-1]}: {r}\n")

@@ -121,6 +121,8 @@ def main() -> int:
         verdict = json.loads(checker.stdout)
     except ValueError:
         verdict = {"raw": checker.stdout[-2000:]}
+    explain = subprocess.run([sys.executable, os.path.join(REPO, "check-gpu-node.py"), "--kubeconfig", kc,
+                              "--explain", name], capture_output=True, text=True, env=env, timeout=60)
     writes = [e for e in srv.log if e["method"] in ("PATCH", "POST")]
     rss = [s["agent_rss_mb"] for s in samples if s["agent_rss_mb"]]
     out = {
@@ -135,6 +137,7 @@ def main() -> int:
         "apiserver_writes": {p: sum(1 for e in writes if e["path"] == p) for p in sorted({e["path"] for e in writes})},
         "labels_last": samples[-1]["labels"] if samples else None,
         "checker": {"exit_code": checker.returncode, "output": verdict},
+        "explain": {"exit_code": explain.returncode, "text": explain.stdout.splitlines()},
         "series": samples,
     }
     out["ok"] = (alive and out["conditions_seen"] == ["True"] and out["healthz_seen"] == ["200"]
