@@ -744,6 +744,11 @@ def main(argv=None) -> int:
     ap.add_argument("--format", choices=("json", "text"), default="json")
     args = ap.parse_args(argv)
     devices = args.device if args.device else list(range(device_count()))
+    if not devices:  # no GPU is not a passing GPU (driver not loaded, devices not mounted into the pod)
+        msg = "no HIP devices visible (amdgpu driver loaded? /dev/kfd and /dev/dri mounted?)"
+        print(f"result: FAIL ({msg})" if args.format == "text" else json.dumps({"devices": {}, "pass": False,
+                                                                                "error": msg}, indent=1))
+        return 1
     out: Dict[str, Any] = {"devices": {d: {"info": device_info(d), "tests": run(args.level, d)} for d in devices}}
     ok = all(t.get("pass") for d in out["devices"].values() for t in d["tests"].values())
     if args.level >= 2 and args.p2p:

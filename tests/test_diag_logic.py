@@ -292,3 +292,10 @@ def test_hbm_per_xcd_alone_rates_find_one_slow_xcd(fake):
     fake(cus=32, rate=1 / 8)
     r = diag.hbm_xcd(0, scale=diag.Scale(0.125, 0.125))
     assert list(r["alone_tbs"]) == ["0"] and r["expect"]["read_tbs"] == 0.725
+
+
+def test_no_device_is_a_failure_not_a_pass(fake, capsys):
+    fake(n=0)
+    assert diag.main(["--level", "1"]) == 1
+    doc = __import__("json").loads(capsys.readouterr().out)
+    assert doc["pass"] is False and "no HIP devices" in doc["error"]
