@@ -312,7 +312,14 @@ class Agent:
         if self.diag_level <= 0:
             return {}
         from ..ops import diag
-        devices = self.devices if self.devices is not None else list(range(min(len(gpus), diag.device_count())))
+        visible = diag.device_count() if self.devices is None else len(self.devices)
+        if self.devices is None and gpus and visible == 0:
+            # amd-smi sees GPUs but HIP sees none: a deployment fault (device files not mounted, wrong
+            # container), said per GPU rather than silently running no diagnostics
+            for i in range(len(gpus)):
+                self._diag_skipped[i] = "no HIP device visible to the agent (/dev/kfd and /dev/dri mounted?)"
+            return {}
+        devices = self.devices if self.devices is not None else list(range(min(len(gpus), visible)))
         entries = self._entries_by_device(gpus, devices)
         now = time.time()
         due = [d for d in devices if now - self._diag_at.get(d, float("-inf")) >= self.diag_interval]

@@ -317,3 +317,11 @@ def test_status_endpoint_is_the_verdict_in_text(monkeypatch):
     assert "  reason: gpu1: 3 uncorrectable ECC errors" in lines
     row1 = next(ln for ln in lines if ln.startswith("  1 "))
     assert "0000:01:00.0" in row1 and row1.endswith("3 uncorrectable ECC errors")
+
+
+def test_no_hip_device_is_said_per_gpu(monkeypatch):
+    World(monkeypatch)
+    monkeypatch.setattr(diag, "device_count", lambda: 0)
+    rep = A.Agent("n", source="fake", diag_level=1).probe_once()
+    assert [g.get("diag_skipped") for g in rep["gpus"]] == \
+        ["no HIP device visible to the agent (/dev/kfd and /dev/dri mounted?)"] * 2
