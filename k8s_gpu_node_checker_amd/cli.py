@@ -65,6 +65,7 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
     ("x", "--json-extended", {"action": "store_true", "help": "JSON 에 MI355X 헬스/타이밍 필드 추가"}),
     ("x", "--trace", {"action": "store_true", "help": "단계별 소요 시간을 stderr 로 출력"}),
     ("x", "--explain", {"metavar": "NODE", "help": "한 노드가 Ready 로 집계되는(또는 안 되는) 이유를 출력"}),
+    ("x", "--fleet", {"action": "store_true", "help": "MI355X 플릿 요약 (판정별 노드 수, 문제 노드, 드라이버/펌웨어 버전)"}),
     ("x", "--prometheus-textfile", {"help": "node-exporter textfile 메트릭 경로"}),
     ("x", "--state-file", {"help": "직전 결과 저장 파일 (알림 중복 제거)"}),
     ("x", "--watch", {"type": float, "default": 0.0, "help": "N초마다 반복 점검 (0 = 한 번, 기본)"}),
@@ -222,6 +223,13 @@ def main(argv: Optional[List[str]] = None) -> int:
             from .checker import CheckOptions
             from .explain import explain
             return explain(_load_cluster(args), args.explain, CheckOptions.from_args(args), sys.stdout)
+        except Exception as e:
+            return _report_error(args, e)
+    if args.fleet:
+        try:
+            from .checker import CheckOptions
+            from .explain import fleet
+            return fleet(_load_cluster(args), CheckOptions.from_args(args), sys.stdout)
         except Exception as e:
             return _report_error(args, e)
     if args.watch_events:

@@ -13,7 +13,7 @@ import json
 import time
 from typing import Any, Dict, List, Optional, TextIO
 
-from .checker import CheckOptions, apply_health, apply_schedulability, scan_cluster
+from .checker import CheckOptions, apply_health, apply_schedulability, fleet_versions, run_check, scan_cluster
 from .kube.config import ClusterConnection
 from .models import health as H
 from .models.node import HEALTH_CONDITION
@@ -178,3 +178,43 @@ def explain(cluster: ClusterConnection, node_name: str, opts: CheckOptions, out:
 def opts_keys() -> List[str]:
     from .models.resources import GPU_RESOURCE_KEYS
     return list(GPU_RESOURCE_KEYS)
+
+
+def fleet(cluster: ClusterConnection, opts: CheckOptions, out: TextIO) -> int:
+    """``check-gpu-node --fleet``: the cluster's MI355X nodes at a glance -- how many count as Ready, the
+    verdicts by state, every node that is not healthy with its first reason, and the driver / firmware
+    versions across the nodes that publish a report (two versions of one image = a partial upgrade).
+    Exit code as the plain check (0 / 2 / 3)."""
+    opts.json_extended = True  # every report annotation is read (fleet versions)
+    res = run_check(cluster, opts)
+    nodes = res.gpu_nodes
+    out.write(f"GPU nodes: {len(nodes)}, counting as Ready: {len(res.ready_gpu_nodes)}\n")
+    verdicts = res.verdicts or []
+    by_state: Dict[str, int] = {}
+    for v in verdicts:
+        if v is not None:
+            by_state[v.state] = by_state.get(v.state, 0) + 1
+    unjudged = len(nodes) - sum(by_state.values())
+    parts = [f"{n} {s}" for s, n in sorted(by_state.items(), key=lambda kv: ("healthy", "degraded", "unhealthy",
+                                                                              "unknown").index(kv[0])
+                                                  if kv[0] in ("healthy", "degraded", "unhealthy", "unknown") else 9)]
+    out.write("MI355X verdicts: " + (", ".join(parts) if parts else "none") +
+              (f"; {unjudged} without a verdict" if unjudged and parts else "") + "\n")
+    for i, n in enumerate(nodes):
+        v = verdicts[i] if i < len(verdicts) else None
+        if v is not None and v.state != "healthy":
+            why = (v.reasons or v.warnings or [""])[0]
+            more = len(v.reasons) + len(v.warnings) - 1
+            out.write(f"  {n['name']}: {v.state}{' (not Ready)' if not n['ready'] else ''}  {why}"
+                      + (f"  (+{more} more)" if more > 0 else "") + "\n")
+        elif not n["ready"]:
+            out.write(f"  {n['name']}: not Ready\n")
+    fv = fleet_versions(res.scan.extras)
+    if fv:
+        out.write(f"versions across {fv['nodes_reporting']} reporting nodes"
+                  + (f" (mixed: {', '.join(fv['mixed'])})" if fv["mixed"] else "") + ":\n")
+        if fv["driver"]:
+            out.write("  driver: " + ", ".join(f"{k} x{c}" for k, c in sorted(fv["driver"].items())) + "\n")
+        for image, row in fv["firmware"].items():
+            out.write(f"  {image}: " + ", ".join(f"{k} x{c}" for k, c in sorted(row.items())) + "\n")
+    return res.exit_code

@@ -67,3 +67,15 @@ def test_explain_json(run_cli, mock_cluster, tmp_path):
     assert d["report"]["node_findings"][0].startswith("firmware differs across GPUs: pm: gpu0-2,4-7 ")
     p = run_cli(["--kubeconfig", kc, "--explain", "cpu", "--json"])
     assert p.returncode == 2 and json.loads(p.stdout)["gpu_node"] is False
+
+
+def test_fleet_summary(run_cli, mock_cluster, tmp_path):
+    kc = _cluster(mock_cluster, tmp_path)
+    p = run_cli(["--kubeconfig", kc, "--fleet"])
+    assert p.returncode == 0, p.stderr  # good and plain count as Ready
+    lines = p.stdout.splitlines()
+    assert lines[0] == "GPU nodes: 3, counting as Ready: 2"
+    assert lines[1] == "MI355X verdicts: 1 healthy, 1 unhealthy; 1 without a verdict"
+    assert lines[2] == "  bad: unhealthy (not Ready)  gpu3: 2 uncorrectable ECC errors (umc 2)"
+    assert "versions across 2 reporting nodes (mixed: pm):" in p.stdout
+    assert "  driver: 6.18.54 x2" in p.stdout and "  pm: 04.86.00.00 x1, 04.86.15.106 x2" in lines
