@@ -325,3 +325,22 @@ def test_no_hip_device_is_said_per_gpu(monkeypatch):
     rep = A.Agent("n", source="fake", diag_level=1).probe_once()
     assert [g.get("diag_skipped") for g in rep["gpus"]] == \
         ["no HIP device visible to the agent (/dev/kfd and /dev/dri mounted?)"] * 2
+
+
+def test_a_slow_result_is_measured_again_soon(monkeypatch):
+    w = World(monkeypatch, n=1)
+    results = [{"gemm": {"pass": True, "degraded": True, "detail": "tflops 1100 = 90% of 1220"}},
+               {"gemm": {"pass": True, "degraded": False}}]
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: (w.runs.append(d), results[len(w.runs) - 1])[1])
+    ag = A.Agent("n", source="fake", diag_level=1, diag_interval=3600.0)
+    rep = ag.probe_once()
+    assert rep["gpus"][0]["diag"]["gemm"]["degraded"] and rep["state"] == "degraded"
+    w.clock += 120
+    ag.probe_once()
+    assert len(w.runs) == 1  # not yet
+    w.clock += A.DIAG_RECHECK_S
+    rep = ag.probe_once()
+    assert len(w.runs) == 2 and rep["state"] == "healthy"  # the one-off cleared in minutes, not an hour
+    w.clock += A.DIAG_RECHECK_S * 2
+    ag.probe_once()
+    assert len(w.runs) == 2  # clean: back to the full interval
