@@ -59,7 +59,8 @@ REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
     "hbm": {"copy_tbs": 6.49, "read_tbs": 6.96},   # 16-byte copy (read + write bytes counted) / read, TB/s
     "mfma": {"bf16": 1901.0, "fp8": 1940.0, "mxfp8": 4326.0, "mxfp4": 7610.0},  # register-resident burn-in
     "host_link": {"h2d_gbps": 57.0, "d2h_gbps": 56.8},  # pinned copies over PCIe Gen5 x16
-    # per-XCD HBM reads, 8 x 256 MiB slices read twice: all XCDs together 5.83-6.27 TB/s (a cold level-2
+    # per-XCD HBM reads, 8 x 256 MiB slices (read 4x since profiles/hbm_xcd_passes_mi355x.json: lone-XCD
+    # spread 0.994 at 4 passes vs 0.987 at 2, +5 ms); at 2 passes all XCDs together 5.83-6.27 TB/s (a cold level-2
     # run and 1,299 level-1 soak rounds), each XCD alone 1.23-1.33 TB/s (profiles/hbm_xcd_explore_mi355x.json,
     # profiles/soak_level1_hbm_xcd_mi355x.json)
     "hbm_xcd": {"read_tbs": 5.8, "alone_tbs": 1.28},
@@ -487,7 +488,7 @@ def l2_bandwidth(device: int = 0, slice_kib: int = 2048, passes: int = 32, block
     return _lag_verdict(res, where, "L2 reads")
 
 
-def hbm_xcd(device: int = 0, slice_mib: int = 256, passes: int = 2, blocks_per_cu: int = 4,
+def hbm_xcd(device: int = 0, slice_mib: int = 256, passes: int = 4, blocks_per_cu: int = 4,
             seed: int = 0x4B3D, scale: Scale = FULL) -> Dict[str, Any]:
     """HBM reads per XCD.  Each XCD streams its own ``slice_mib`` slice (8 of them, far past the L2s and the
     MALL) with its own workgroups, every word checked: first all XCDs together (aggregate read TB/s), then
