@@ -8,7 +8,7 @@
 //             "hotspot_c"}...],
 //    "error": null | "<amdsmi status name>"}
 // amd-smi stays initialised between calls (the node agent probes on a cadence;
-// the first query after init costs ~0.7 s on MI355X, later full probes ~2 ms/GPU).
+// the first query after init costs ~0.7 s on MI355X, later full probes 2-5 ms/GPU).
 #pragma once
 
 #ifdef __cplusplus
