@@ -185,16 +185,28 @@ def fleet(cluster: ClusterConnection, opts: CheckOptions, out: TextIO) -> int:
     verdicts by state, every node that is not healthy with its first reason, and the driver / firmware
     versions across the nodes that publish a report (two versions of one image = a partial upgrade).
     Exit code as the plain check (0 / 2 / 3)."""
+    as_json = opts.json
     opts.json_extended = True  # every report annotation is read (fleet versions)
     res = run_check(cluster, opts)
     nodes = res.gpu_nodes
-    out.write(f"GPU nodes: {len(nodes)}, counting as Ready: {len(res.ready_gpu_nodes)}\n")
     verdicts = res.verdicts or []
     by_state: Dict[str, int] = {}
     for v in verdicts:
         if v is not None:
             by_state[v.state] = by_state.get(v.state, 0) + 1
     unjudged = len(nodes) - sum(by_state.values())
+    if as_json:
+        attention = []
+        for i, n in enumerate(nodes):
+            v = verdicts[i] if i < len(verdicts) else None
+            if (v is not None and v.state != "healthy") or not n["ready"]:
+                attention.append({"name": n["name"], "ready": n["ready"], "state": v.state if v else None,
+                                  "reasons": v.reasons if v else [], "warnings": v.warnings if v else []})
+        out.write(json.dumps({"total_nodes": len(nodes), "ready_nodes": len(res.ready_gpu_nodes),
+                              "verdicts": by_state, "without_verdict": unjudged, "attention": attention,
+                              "fleet": fleet_versions(res.scan.extras)}, indent=2, ensure_ascii=False) + "\n")
+        return res.exit_code
+    out.write(f"GPU nodes: {len(nodes)}, counting as Ready: {len(res.ready_gpu_nodes)}\n")
     parts = [f"{n} {s}" for s, n in sorted(by_state.items(), key=lambda kv: ("healthy", "degraded", "unhealthy",
                                                                               "unknown").index(kv[0])
                                                   if kv[0] in ("healthy", "degraded", "unhealthy", "unknown") else 9)]

@@ -79,3 +79,13 @@ def test_fleet_summary(run_cli, mock_cluster, tmp_path):
     assert lines[2] == "  bad: unhealthy (not Ready)  gpu3: 2 uncorrectable ECC errors (umc 2)"
     assert "versions across 2 reporting nodes (mixed: pm):" in p.stdout
     assert "  driver: 6.18.54 x2" in p.stdout and "  pm: 04.86.00.00 x1, 04.86.15.106 x2" in lines
+
+
+def test_fleet_summary_json(run_cli, mock_cluster, tmp_path):
+    kc = _cluster(mock_cluster, tmp_path)
+    p = run_cli(["--kubeconfig", kc, "--fleet", "--json"])
+    d = json.loads(p.stdout)
+    assert p.returncode == 0 and d["total_nodes"] == 3 and d["ready_nodes"] == 2
+    assert d["verdicts"] == {"healthy": 1, "unhealthy": 1} and d["without_verdict"] == 1
+    assert [a["name"] for a in d["attention"]] == ["bad"] and d["attention"][0]["reasons"][0].startswith("gpu3:")
+    assert d["fleet"]["mixed"] == ["pm"]
