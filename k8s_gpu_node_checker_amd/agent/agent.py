@@ -244,7 +244,8 @@ class Agent:
         # the agent as a child of a GPU-holding process (a test runner), the PIDs given with --ignore-pid
         self.ignore_pids = frozenset((os.getpid(),) + tuple(int(p) for p in ignore_pids))
         self._diag_cache: Dict[int, Dict[str, Any]] = {}
-        self._diag_at: Dict[int, float] = {}
+        self._diag_at: Dict[int, float] = {}  # schedule: when the next run counts from (a recheck moves it back)
+        self._diag_ran: Dict[int, float] = {}  # when the cached result was measured (reported as diag_at)
         self._diag_threads: Dict[int, Any] = {}  # device -> (thread, start time, result box) until it returns
         self.diag_timeout = diag_timeout
         self._diag_skipped: Dict[int, str] = {}
@@ -377,6 +378,7 @@ class Agent:
                     self.hip_lost = lost
                 elif "res" in box:
                     self._diag_cache[d] = box["res"]
+                    self._diag_ran[d] = started
                 self._diag_at[d] = started
                 if lost is None and "res" in box and not_clean(box["res"]) and self.diag_interval > DIAG_RECHECK_S:
                     # a slow or failed result is measured again after DIAG_RECHECK_S instead of a whole
@@ -386,6 +388,7 @@ class Agent:
             else:
                 self._diag_cache[d] = {"watchdog": {
                     "pass": False, "detail": f"diagnostics did not finish within {self.diag_timeout:g} s (GPU hang?)"}}
+                self._diag_ran[d] = started
                 self._diag_at[d] = started
         if self.hip_lost is not None:
             for d in devices:
@@ -467,7 +470,7 @@ class Agent:
             for d, g in entries.items():
                 if diags.get(d):
                     g["diag"] = diags[d]
-                    g["diag_at"] = round(self._diag_at.get(d, 0.0), 1)  # when it ran (a busy GPU's result ages)
+                    g["diag_at"] = round(self._diag_ran.get(d, 0.0), 1)  # when it ran (a busy GPU's result ages)
                 if d in self._diag_skipped:
                     g["diag_skipped"] = self._diag_skipped[d]
             if self._fabric:

@@ -335,6 +335,7 @@ def test_a_slow_result_is_measured_again_soon(monkeypatch):
     ag = A.Agent("n", source="fake", diag_level=1, diag_interval=3600.0)
     rep = ag.probe_once()
     assert rep["gpus"][0]["diag"]["gemm"]["degraded"] and rep["state"] == "degraded"
+    assert rep["gpus"][0]["diag_at"] == w.clock  # reported as when it ran, whatever the schedule says
     w.clock += 120
     ag.probe_once()
     assert len(w.runs) == 1  # not yet
