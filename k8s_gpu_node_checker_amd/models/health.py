@@ -304,6 +304,9 @@ def partition_mismatch(gpus: Sequence[Any]) -> List[str]:
     another mode after a repartition hands the scheduler devices of two sizes under one name."""
     out = []
     for key, name in (("compute_partition", "compute"), ("memory_partition", "memory")):
+        modes = {g[key] for g in gpus if isinstance(g, dict) and isinstance(g.get(key), str) and g[key]}
+        if len(modes) < 2:
+            continue  # the common case: one mode across the node
         seen: Dict[str, List[Any]] = {}
         for g in gpus:
             if isinstance(g, dict) and isinstance(g.get(key), str) and g[key]:
