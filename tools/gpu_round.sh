@@ -25,6 +25,10 @@ cat gpurun_out/diag_level2.json
 step rocprof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_diag -o diag -- python -m k8s_gpu_node_checker_amd.ops.diag --level 2 > gpurun_out/prof_diag.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof_diag.log; exit 1; }
 find gpurun_out/prof_diag -name "*.csv" | head -20
+step agent-soak
+timeout -k 10 200 python tools/agent_soak.py --minutes 1 --diag-level 1 --interval 5 --sample 10 --out gpurun_out/agent_soak_round.json > gpurun_out/agent_soak_round.log 2>&1 || { echo "agent soak failed"; tail -20 gpurun_out/agent_soak_round.log; exit 1; }
+step contention
+timeout -k 10 200 python tools/contention_demo.py --out gpurun_out/contention_round.json > gpurun_out/contention_round.log 2>&1 || { echo "contention demo failed"; tail -20 gpurun_out/contention_round.log; exit 1; }
 step probe-cli
 timeout -k 10 60 ./k8s_gpu_node_checker_amd/_native/mi355x-probe --repeat 5 --interval-ms 100 > gpurun_out/probe_cli.jsonl 2>&1 || { echo "probe cli failed"; cat gpurun_out/probe_cli.jsonl; exit 1; }
 tail -1 gpurun_out/probe_cli.jsonl
