@@ -104,6 +104,8 @@ def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> 
                            "gpus": node["gpus"], "gpu_breakdown": node["gpu_breakdown"],
                            "allocatable": ex.allocatable, "unschedulable": ex.unschedulable,
                            "health_policy": opts.health_policy, "health_condition": None,
+                           "amd_labels": {k: v for k, v in sorted((node.get("labels") or {}).items())
+                                          if k.startswith("amd.com/")},
                            "verdict": v.to_dict() if v is not None else None, "report": None}
     if ex.health_condition is not None:
         status, reason, message, hb = ex.health_condition
@@ -137,6 +139,8 @@ def render(doc: Dict[str, Any], out: TextIO) -> None:
     breakdown = ", ".join(f"{k}:{c}" for k, c in doc["gpu_breakdown"].items())
     out.write(f"node {name}: Ready={doc['ready_condition']}  GPUs {doc['gpus']} ({breakdown})"
               f"  allocatable {doc['allocatable'] or '-'}{'  cordoned' if doc['unschedulable'] else ''}\n")
+    if doc.get("amd_labels"):
+        out.write("labels: " + ", ".join(f"{k}={v}" for k, v in doc["amd_labels"].items()) + "\n")
     hc = doc["health_condition"]
     if hc is not None:
         out.write(f"{HEALTH_CONDITION}={hc['status']} ({hc['reason']}, heartbeat {_age(hc['heartbeat_age_s'])} ago): "

@@ -40,6 +40,7 @@ def test_explain_healthy_plain_and_missing(run_cli, mock_cluster, tmp_path):
     kc = _cluster(mock_cluster, tmp_path)
     p = run_cli(["--kubeconfig", kc, "--explain", "good"])
     assert p.returncode == 0 and "MI355X verdict: healthy, 8/8 GPUs ok" in p.stdout
+    assert "labels: amd.com/gpu.family=MI355X" in p.stdout  # the agent's --label-node labels, when present
     assert "report: probe fixture" in p.stdout and "driver 6.18.54" in p.stdout  # gzip annotation read
     rows = [ln for ln in p.stdout.splitlines() if ln.startswith("  ") and ln.split()[0].isdigit()]
     assert len(rows) == 8 and all(r.endswith("ok") for r in rows)
