@@ -278,7 +278,12 @@ def connection_from_config(cfg: Dict[str, Any], context: Optional[str] = None) -
     if cluster.get("certificate-authority-data"):
         conn.ca_data = _b64(cluster["certificate-authority-data"])
     conn.ca_file = _path(cbase, cluster.get("certificate-authority"))
-    conn.insecure = bool(cluster.get("insecure-skip-tls-verify"))
+    insecure = cluster.get("insecure-skip-tls-verify")
+    if insecure is not None and not isinstance(insecure, bool):
+        # kubectl refuses a non-boolean here (Go's bool unmarshal); bool("no") would silently turn TLS off
+        raise ConfigException("Invalid kube-config file. kube-config/clusters/%s/cluster/insecure-skip-tls-verify "
+                              "must be a boolean, got %r" % (cluster_name, insecure))
+    conn.insecure = bool(insecure)
     conn.tls_server_name = cluster.get("tls-server-name")
     conn.proxy_url = cluster.get("proxy-url")
     user_name = ctx_body.get("user")

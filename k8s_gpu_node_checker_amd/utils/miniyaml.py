@@ -8,6 +8,15 @@ parser handles exactly that and raises :class:`Unsupported` on anything else
 (anchors, tags, block scalars, flow collections with content, multi-document
 streams), in which case the caller falls back to PyYAML -- results are never
 silently different.
+
+Plain scalars (values *and* keys) resolve with PyYAML's YAML 1.1 implicit
+resolver (``yaml/resolver.py``, the loader ``kubernetes.config`` uses for the
+reference, ``check-gpu-node.py:160-169``): the 18 bool spellings
+``yes/no/on/off/true/false`` in three cases, the four null forms, decimal
+ints.  Every other form PyYAML's resolver would turn into a non-string (octal,
+hex, binary and sexagesimal ints, floats, ``.inf``/``.nan``, timestamps,
+``<<``, ``=``) is refused, so PyYAML decides it.  A kubeconfig line
+``insecure-skip-tls-verify: no`` is therefore ``False`` here exactly as there.
 """
 
 from __future__ import annotations
@@ -21,8 +30,13 @@ class Unsupported(ValueError):
     pass
 
 
-_BOOLS = {"true": True, "True": True, "TRUE": True, "false": False, "False": False, "FALSE": False}
+# PyYAML's tag:yaml.org,2002:bool resolver (YAML 1.1) and SafeConstructor.bool_values
+_BOOLS = {w: v for v, words in ((True, ("yes", "true", "on")), (False, ("no", "false", "off")))
+          for b in words for w in (b, b.capitalize(), b.upper())}
 _NULLS = {"", "~", "null", "Null", "NULL"}
+_DIGITS = "0123456789"
+# printable ASCII, LF and CR; tabs are refused (PyYAML's tab rules differ by context and kubeconfigs have none)
+_ASCII_OK = bytes([10, 13]) + bytes(range(0x20, 0x7F))
 
 
 def _strip_comment(s: str) -> str:
@@ -66,6 +80,8 @@ def _scalar(tok: str) -> Any:
         i = 0
         while i < len(body):
             ch = body[i]
+            if ch == '"':
+                raise Unsupported("content after a double-quoted scalar")
             if ch == "\\":
                 nx = body[i + 1:i + 2]
                 if nx in _ESC:
@@ -87,25 +103,37 @@ def _scalar(tok: str) -> Any:
     if c == "'":
         if len(t) < 2 or t[-1] != "'":
             raise Unsupported("multi-line or unterminated single-quoted scalar")
-        return t[1:-1].replace("''", "'")
+        body = t[1:-1]
+        if "'" in body.replace("''", ""):
+            raise Unsupported("content after a single-quoted scalar")
+        return body.replace("''", "'")
     if t == "{}":
         return {}
     if t == "[]":
         return []
-    if c in "{[&*!|>%@`":
+    return _plain(t)
+
+
+def _plain(t: str) -> Any:
+    """Resolve a stripped, non-empty plain scalar the way PyYAML's SafeLoader does, or refuse."""
+    c = t[0]
+    if c in "{[]},#&*!|>'\"%@`" or (c in "-?:" and (len(t) == 1 or t[1] in " \t")):
         raise Unsupported(f"construct {c!r}")
+    if t.endswith(":") or ": " in t or "\t" in t or " #" in t:
+        raise Unsupported("indicator inside a plain scalar")
     if t in _NULLS:
         return None
-    if t in _BOOLS:
-        return _BOOLS[t]
-    if t.lstrip("-+").isdigit() and not (len(t.lstrip("-+")) > 1 and t.lstrip("-+")[0] == "0"):
-        return int(t)
-    if t[0].isdigit() or t[0] in "-+.":
-        try:
-            float(t)
-        except ValueError:
-            return t
-        raise Unsupported("float scalar")  # YAML float forms differ from Python's; let PyYAML decide
+    b = _BOOLS.get(t)
+    if b is not None:
+        return b
+    # int / float / timestamp resolvers all start with [-+]?[0-9.]; merge is "<<", value is "="
+    num = t[1:] if c in "-+" else t
+    if num[:1] in _DIGITS or num[:1] == ".":
+        if num.isdigit() and num.isascii() and (num == "0" or num[0] != "0"):
+            return int(t)
+        raise Unsupported("non-decimal number, float or timestamp scalar")
+    if t in ("<<", "="):
+        raise Unsupported("merge/value key")
     return t
 
 
@@ -131,24 +159,37 @@ def _split_key(s: str) -> Optional[Tuple[str, str]]:
         return _scalar(s[:end + 1]), rest[1:]
     i = s.find(": ")
     if i < 0:
-        if s.endswith(":"):
-            return s[:-1], ""
-        return None
-    return s[:i], s[i + 2:]
+        if not s.endswith(":"):
+            return None
+        i = len(s) - 1
+    k = s[:i].rstrip(" ")
+    if not k:
+        raise Unsupported("empty key")
+    return _plain(k), s[i + 2:]
 
 
 class _Parser:
     def __init__(self, text: str):
         self.lines: List[Tuple[int, str]] = []
-        for raw in text.splitlines():
+        try:
+            bad = text.encode("ascii").translate(None, _ASCII_OK)
+        except UnicodeEncodeError:
+            bad = b"non-ASCII"  # rare in kubeconfigs: PyYAML's reader rules for it are not replicated here
+        if bad:
+            raise Unsupported("tab, control or non-ASCII character")
+        for raw in text.split("\n"):
+            if raw.endswith("\r"):
+                raw = raw[:-1]
+            if "\r" in raw:
+                raise Unsupported("bare carriage return")
             if "\t" in raw[: len(raw) - len(raw.lstrip())]:
                 raise Unsupported("tab indentation")
             body = _strip_comment(raw)
             if not body.strip():
                 continue
-            if body.strip() in ("---", "..."):
-                if self.lines:
-                    raise Unsupported("multi-document stream")
+            if body[:3] in ("---", "..."):
+                if body != "---" or self.lines:
+                    raise Unsupported("document marker with content, document end or multi-document stream")
                 continue
             ind = len(body) - len(body.lstrip(" "))
             self.lines.append((ind, body.strip()))
