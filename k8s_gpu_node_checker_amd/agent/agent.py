@@ -86,6 +86,16 @@ def gpu_busy(g: Dict[str, Any], own_pids: frozenset = frozenset(), busy_vram_mb:
     return None
 
 
+def power_fraction(g: Dict[str, Any]) -> Optional[float]:
+    """The GPU's power cap as a share of its default (amd-smi), None when unknown.  A capped GPU runs its matrix
+    cores at a lower clock; the compute references are scaled by it so a deliberate cap is not a failed GPU
+    (models/health.py warns about the cap itself)."""
+    cap, dflt = g.get("power_cap_w"), g.get("power_cap_default_w")
+    if isinstance(cap, int) and isinstance(dflt, int) and not isinstance(cap, bool) and cap > 0 and dflt > 0:
+        return min(1.0, cap / dflt)
+    return None
+
+
 # HIP errors that say this process's runtime lost its devices (a driver reload or GPU reset under a running
 # agent): not the GPU's fault, and not curable in-process -- the agent needs a fresh process
 _HIP_RUNTIME_LOST = ("no ROCm-capable device", "invalid device ordinal", "initialization error",
@@ -93,8 +103,30 @@ _HIP_RUNTIME_LOST = ("no ROCm-capable device", "invalid device ordinal", "initia
                      "hipErrorContextIsDestroyed")
 
 
-# a diagnostic result that is not clean is run again this soon (s), not a whole --diag-interval later
+# a diagnostic result that is not clean is run again this soon (s), not a whole --diag-interval later --
+# once per distinct result: a GPU that keeps failing the same way goes back to --diag-interval instead of
+# being stressed (memtest, HBM) every few minutes while it is already known bad
 DIAG_RECHECK_S = 300.0
+# diagnostic threads running at once (--diag-parallel): every GPU of an SPX node together, a CPX node's 64
+# partitions in waves of 8
+DIAG_PARALLEL = 8
+# /healthz fails once a diagnostic thread has outlived this many --diag-timeout: its verdict (watchdog) went
+# out at 1x; a thread in a hung HIP call cannot be cancelled, so only a fresh process frees its GPU
+HUNG_RESTART_FACTOR = 2.0
+
+
+class _DiagRun:
+    """One device's diagnostic thread: wall-clock start (reported), monotonic start (watchdog), result box."""
+    __slots__ = ("thread", "started", "mono", "box")
+
+    def __init__(self, thread: threading.Thread, started: float, mono: float, box: Dict[str, Any]):
+        self.thread, self.started, self.mono, self.box = thread, started, mono, box
+
+
+def result_signature(res: Dict[str, Any]) -> str:
+    """Which tests of a result failed or were degraded (what a recheck is keyed on)."""
+    return ",".join(sorted(k for k, r in res.items() if isinstance(r, dict)
+                           and (r.get("pass") is False or r.get("degraded"))))
 
 
 def not_clean(res: Dict[str, Any]) -> bool:
@@ -206,8 +238,12 @@ class Agent:
                  diag_timeout: float = 300.0, ignore_pids: Sequence[int] = (),
                  expect_gpus: Optional[int] = None, expectations: Optional[HealthExpectations] = None,
                  pod_resources_socket: Optional[str] = None, gpu_resources: Sequence[str] = (PRIMARY_GPU_KEY,),
-                 label_node: bool = False, annotation_encoding: str = "json"):
+                 label_node: bool = False, annotation_encoding: str = "json", diag_parallel: int = DIAG_PARALLEL):
         self.node = node
+        if diag_parallel < 1:
+            raise ValueError("diag_parallel must be >= 1")
+        # at most this many per-device diagnostic threads at once (hung ones count: they still hold their GPU)
+        self.diag_parallel = diag_parallel
         # "json" (readable with kubectl) or "gzip" (gz: + base64, ~12x smaller in every node LIST / watch)
         if annotation_encoding not in ("json", "gzip"):
             raise ValueError("annotation_encoding must be json or gzip")
@@ -246,7 +282,10 @@ class Agent:
         self._diag_cache: Dict[int, Dict[str, Any]] = {}
         self._diag_at: Dict[int, float] = {}  # schedule: when the next run counts from (a recheck moves it back)
         self._diag_ran: Dict[int, float] = {}  # when the cached result was measured (reported as diag_at)
-        self._diag_threads: Dict[int, Any] = {}  # device -> (thread, start time, result box) until it returns
+        self._diag_threads: Dict[int, _DiagRun] = {}  # device -> its diagnostic thread until it returns
+        self._diag_done = threading.Event()  # set by every diagnostic thread as it returns
+        self._rechecked: Dict[int, str] = {}  # device -> result_signature of the not-clean result rechecked
+        self._hip_count0: Optional[int] = None  # HIP device count the process saw first (runtime_lost)
         self.diag_timeout = diag_timeout
         self._diag_skipped: Dict[int, str] = {}
         # set when the HIP runtime lost its devices (runtime_lost): no further diagnostics in this process,
@@ -254,7 +293,7 @@ class Agent:
         self.hip_lost: Optional[str] = None
         self._fabric: Optional[Dict[str, Any]] = None
         self._fabric_at = float("-inf")
-        self._fabric_thread: Optional[Any] = None  # (thread, start time, result box) until it returns
+        self._fabric_thread: Optional[_DiagRun] = None  # the node-level suite's thread until it returns
         self._bdf: Dict[int, str] = {}  # HIP ordinal -> PCI address (amd-smi and HIP enumerate independently)
         self.last: Optional[Dict[str, Any]] = None
         self.last_probe_done: Optional[float] = None  # monotonic time of the last completed probe (/healthz)
@@ -304,12 +343,12 @@ class Agent:
     def _entries_by_device(self, gpus: List[Dict[str, Any]], devices: List[int]) -> Dict[int, Dict[str, Any]]:
         """The probe entry of each HIP device: by PCI address, by index when HIP cannot say."""
         from ..ops import diag
-        by_bdf = {str(g.get("bdf", "")).lower(): g for g in gpus if g.get("bdf")}
+        by_bdf = {normalize_bdf(g.get("bdf")): g for g in gpus if g.get("bdf")}
         out: Dict[int, Dict[str, Any]] = {}
         for d in devices:
             if d not in self._bdf:
                 try:
-                    self._bdf[d] = str(diag.device_info(d)["bdf"]).lower()
+                    self._bdf[d] = normalize_bdf(diag.device_info(d)["bdf"])
                 except Exception:
                     self._bdf[d] = ""
             g = by_bdf.get(self._bdf[d]) if self._bdf[d] else (gpus[d] if 0 <= d < len(gpus) else None)
@@ -323,6 +362,13 @@ class Agent:
             return {}
         from ..ops import diag
         visible = diag.device_count() if self.devices is None else len(self.devices)
+        if self._hip_count0 is None:
+            self._hip_count0 = diag.device_count() if self.devices is not None else visible
+        elif self.hip_lost is None and self.devices is None and visible != self._hip_count0:
+            # HIP enumerates once per process: a count that moved is a driver reload or reset under the agent
+            self.hip_lost = f"HIP device count changed from {self._hip_count0} to {visible}"
+            print(f"{self.hip_lost}; diagnostics stop, /healthz fails so the agent is restarted", file=sys.stderr,
+                  flush=True)
         if self.devices is None and gpus and visible == 0:
             # amd-smi sees GPUs but HIP sees none: a deployment fault (device files not mounted, wrong
             # container), said per GPU rather than silently running no diagnostics
@@ -330,15 +376,32 @@ class Agent:
                 self._diag_skipped[i] = "no HIP device visible to the agent (/dev/kfd and /dev/dri mounted?)"
             return {}
         devices = self.devices if self.devices is not None else list(range(min(len(gpus), visible)))
+        if self.devices is not None:
+            # a configured ordinal HIP does not have is a configuration error of that device, said as such: run
+            # on it, every call would fail with "invalid device ordinal", which is neither the GPU's fault nor a
+            # lost runtime
+            count = self._hip_count0 if self._hip_count0 is not None else diag.device_count()
+            for d in [d for d in devices if not 0 <= d < count]:
+                self._diag_skipped[d] = f"device {d} is not a HIP device of the agent ({count} visible): check --devices"
+            devices = [d for d in devices if 0 <= d < count]
         entries = self._entries_by_device(gpus, devices)
         now = time.time()
         due = [d for d in devices if now - self._diag_at.get(d, float("-inf")) >= self.diag_interval]
+        fabric_busy = self._fabric_thread is not None and self._fabric_thread.thread.is_alive()
+        if fabric_busy and due:
+            # a node-level suite that outlived its watchdog still holds every GPU (a collective's kernels stay
+            # queued): per-GPU tests would contend with it or queue behind it and muddy their own verdict
+            for d in due:
+                self._diag_skipped[d] = ("node-level xGMI/RCCL tests still running past their watchdog: per-GPU "
+                                         "diagnostics wait")
+            due = []
         allocated = self._allocated() if due and self.diag_when == "idle" else None
+        unmatched = self._unmatched_allocations(allocated, entries, devices) if allocated else None
         run = []
         for d in due:
-            why = None
-            if allocated:
-                owner = allocated.get(normalize_bdf((entries.get(d) or {}).get("bdf")) or self._bdf.get(d, ""))
+            why = unmatched
+            if why is None and allocated:
+                owner = allocated.get(normalize_bdf((entries.get(d) or {}).get("bdf") or self._bdf.get(d, "")))
                 if owner:
                     why = f"allocated to pod {owner}"
             if why is None and self.diag_when == "idle":
@@ -347,49 +410,67 @@ class Agent:
                 self._diag_skipped[d] = why
             else:
                 run.append(d)
-        # one host thread per GPU: each diagnostic is a ctypes call that releases the GIL and drives its
-        # own device, so an 8-GPU node is checked in the time of one GPU instead of eight.  A GPU whose
+        # one host thread per GPU, at most `diag_parallel` at once: each diagnostic is a ctypes call that
+        # releases the GIL and drives its own device, so an 8-GPU node is checked in the time of one GPU and a
+        # 64-partition CPX node in 8 waves instead of 64 threads contending for the host.  A GPU whose
         # diagnostic never returns (a hung queue) is reported as failed after `diag_timeout` s instead of
-        # freezing the agent into a stale report; nothing new is started on it while that thread lives.
-        run = [d for d in run if d not in self._diag_threads] if self.hip_lost is None else []
-        for d in run:
-            box: Dict[str, Any] = {}
-
-            # the partition's memory share comes from amd-smi (NPS mode); CUs and VRAM from HIP
-            part = (entries.get(d) or {}).get("memory_partition")
-
-            def work(d: int = d, box: Dict[str, Any] = box, part: Any = part) -> None:
-                try:
-                    box["res"] = diag.run(self.diag_level, d, memory_partition=part)
-                except Exception as e:  # a broken library or device: a failed test, not a dead agent
-                    box["res"] = {"run": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
-            t = threading.Thread(target=work, name=f"diag-gpu{d}", daemon=True)
-            self._diag_threads[d] = (t, now, box)
-            t.start()
-        for d, (t, started, box) in list(self._diag_threads.items()):
-            t.join(max(0.0, started + self.diag_timeout - time.time()))
-            if not t.is_alive():
+        # freezing the agent into a stale report; nothing new is started on it while that thread lives, and
+        # /healthz fails once it has outlived HUNG_RESTART_FACTOR x diag_timeout (hung_diagnostic).
+        queue = [d for d in run if d not in self._diag_threads] if self.hip_lost is None else []
+        memory_partition = {d: (entries.get(d) or {}).get("memory_partition") for d in queue}
+        power = {d: power_fraction(entries.get(d) or {}) for d in queue}
+        while True:
+            self._diag_done.clear()
+            while queue and sum(r.thread.is_alive() for r in self._diag_threads.values()) < self.diag_parallel:
+                d = queue.pop(0)
+                self._start_diag(d, memory_partition.get(d), power.get(d))
+            waiting = [r for r in self._diag_threads.values()
+                       if r.thread.is_alive() and time.monotonic() < r.mono + self.diag_timeout]
+            if not waiting:
+                break
+            self._diag_done.wait(max(0.0, min(min(r.mono for r in waiting) + self.diag_timeout - time.monotonic(),
+                                              1.0)))
+        for d in queue:  # every slot is held by a diagnostic that outlived its watchdog
+            self._diag_skipped[d] = (f"waiting for a diagnostic slot: {self.diag_parallel} of {self.diag_parallel} "
+                                     "held by hung diagnostics")
+        finished: Dict[int, Dict[str, Any]] = {}
+        for d, r in list(self._diag_threads.items()):
+            if not r.thread.is_alive():
                 del self._diag_threads[d]
-                lost = runtime_lost(box["res"]) if "res" in box else None
-                if lost is not None:
-                    if self.hip_lost is None:
-                        print(f"HIP runtime lost its devices ({lost}); diagnostics stop, /healthz fails so the "
-                              "agent is restarted", file=sys.stderr, flush=True)
-                    self.hip_lost = lost
-                elif "res" in box:
-                    self._diag_cache[d] = box["res"]
-                    self._diag_ran[d] = started
-                self._diag_at[d] = started
-                if lost is None and "res" in box and not_clean(box["res"]) and self.diag_interval > DIAG_RECHECK_S:
-                    # a slow or failed result is measured again after DIAG_RECHECK_S instead of a whole
-                    # interval later: a one-off (a burst of power management) clears before the 30-minute
-                    # degraded alert, a real fault is confirmed
-                    self._diag_at[d] = started - self.diag_interval + DIAG_RECHECK_S
+                if "res" in r.box:
+                    finished[d] = r.box["res"]
+                self._diag_at[d] = r.started
             else:
                 self._diag_cache[d] = {"watchdog": {
                     "pass": False, "detail": f"diagnostics did not finish within {self.diag_timeout:g} s (GPU hang?)"}}
-                self._diag_ran[d] = started
-                self._diag_at[d] = started
+                self._diag_ran[d] = r.started
+                self._diag_at[d] = r.started
+        lost_devs = {d: runtime_lost(res) for d, res in finished.items()}
+        lost_devs = {d: why for d, why in lost_devs.items() if why is not None}
+        if lost_devs and self.hip_lost is None:
+            # the HIP runtime, not a GPU, is gone only when the device count changed under the process or every
+            # device it just ran failed that way together; one device's "invalid device ordinal" is that GPU's
+            # (or its configuration's) failure and stays in its verdict
+            now_count = diag.device_count()
+            if (self._hip_count0 is not None and now_count != self._hip_count0) or len(lost_devs) == len(finished):
+                lost = next(iter(lost_devs.values()))
+                print(f"HIP runtime lost its devices ({lost}); diagnostics stop, /healthz fails so the "
+                      "agent is restarted", file=sys.stderr, flush=True)
+                self.hip_lost = lost
+        for d, res in finished.items():
+            if self.hip_lost is not None and d in lost_devs:
+                continue
+            self._diag_cache[d] = res
+            started = self._diag_ran[d] = self._diag_at[d]
+            sig = result_signature(res) if not_clean(res) else ""
+            if sig and sig != self._rechecked.get(d) and self.diag_interval > DIAG_RECHECK_S:
+                # a slow or failed result is measured again after DIAG_RECHECK_S instead of a whole interval
+                # later: a one-off (a burst of power management) clears before the 30-minute degraded alert, a
+                # real fault is confirmed -- once; the same result again goes back to the full interval
+                self._diag_at[d] = started - self.diag_interval + DIAG_RECHECK_S
+                self._rechecked[d] = sig
+            elif not sig:
+                self._rechecked.pop(d, None)
         if self.hip_lost is not None:
             for d in devices:
                 self._diag_skipped[d] = f"HIP runtime lost its devices ({self.hip_lost[:120]}): agent restart pending"
@@ -401,28 +482,78 @@ class Agent:
             # the same watchdog as the per-GPU tests: a collective that never completes (a link that stopped
             # passing traffic) is a failed fabric, not a frozen agent.
             box: Dict[str, Any] = {}
-            t = threading.Thread(target=lambda: box.update(res=self._fabric_suite(devices)), name="diag-fabric",
-                                 daemon=True)
-            self._fabric_thread = (t, now, box)
+            t = threading.Thread(target=lambda: box.update(res=self._fabric_suite(devices, self.diag_timeout)),
+                                 name="diag-fabric", daemon=True)
+            self._fabric_thread = _DiagRun(t, now, time.monotonic(), box)
             t.start()
         if self._fabric_thread is not None:
-            t, started, box = self._fabric_thread
-            t.join(max(0.0, started + self.diag_timeout - time.time()))
-            self._fabric_at = started
-            if not t.is_alive():
+            r = self._fabric_thread
+            r.thread.join(max(0.0, r.mono + self.diag_timeout - time.monotonic()))
+            self._fabric_at = r.started
+            if not r.thread.is_alive():
                 self._fabric_thread = None
-                self._fabric = box.get("res")
+                self._fabric = r.box.get("res")
             else:
                 self._fabric = {"watchdog": {
                     "pass": False,
                     "detail": f"node-level xGMI/RCCL tests did not finish within {self.diag_timeout:g} s (fabric hang?)"}}
         return {d: self._diag_cache[d] for d in devices if d in self._diag_cache}
 
+    def _start_diag(self, d: int, memory_partition: Any, power: Optional[float]) -> None:
+        """Start device ``d``'s diagnostics on its own thread (the partition's memory share comes from amd-smi's
+        NPS mode, CUs and VRAM from HIP; a lowered power cap scales the compute references)."""
+        from ..ops import diag
+        box: Dict[str, Any] = {}
+        kw: Dict[str, Any] = {"memory_partition": memory_partition}
+        if power is not None and power < 1.0:
+            kw["power_fraction"] = power
+
+        def work() -> None:
+            try:
+                box["res"] = diag.run(self.diag_level, d, **kw)
+            except Exception as e:  # a broken library or device: a failed test, not a dead agent
+                box["res"] = {"run": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
+            finally:
+                self._diag_done.set()
+        t = threading.Thread(target=work, name=f"diag-gpu{d}", daemon=True)
+        self._diag_threads[d] = _DiagRun(t, time.time(), time.monotonic(), box)
+        t.start()
+
+    def _unmatched_allocations(self, allocated: Dict[str, str], entries: Dict[int, Dict[str, Any]],
+                               devices: List[int]) -> Optional[str]:
+        """Fail safe for device IDs the agent cannot map: the kubelet reports GPUs allocated to pods, but none of
+        their IDs is a PCI address of this node's devices (a device plugin that names partitions by another
+        scheme).  Any device may then be a pod's, so none is diagnosed (the reason, else None)."""
+        local = {normalize_bdf((entries.get(d) or {}).get("bdf") or self._bdf.get(d, "")) for d in devices}
+        local.discard("")
+        if not local or any(k in local for k in allocated):
+            return None
+        sample = ", ".join(sorted(allocated)[:3])
+        return (f"kubelet reports {len(allocated)} allocated GPU device(s) ({sample}) matching no local PCI "
+                "address: not diagnosing any GPU")
+
+    def hung_diagnostic(self, now: Optional[float] = None) -> Optional[str]:
+        """Why /healthz must fail: a diagnostic thread alive for HUNG_RESTART_FACTOR x diag_timeout (its watchdog
+        verdict was published at 1x); None when nothing is hung that long."""
+        now = time.monotonic() if now is None else now
+        limit = HUNG_RESTART_FACTOR * self.diag_timeout
+        runs = [(f"gpu{d} diagnostics", r) for d, r in list(self._diag_threads.items())]
+        fab = self._fabric_thread
+        if fab is not None:
+            runs.append(("node-level xGMI/RCCL tests", fab))
+        for what, r in runs:
+            age = now - r.mono
+            if r.thread.is_alive() and age >= limit:
+                return f"{what} running for {age:.0f} s (> {HUNG_RESTART_FACTOR:g} x --diag-timeout): restart to free the GPU"
+        return None
+
     @staticmethod
-    def _fabric_suite(devices: List[int]) -> Dict[str, Any]:
-        """The node-level tests: xGMI pair matrix and the RCCL collectives in this process (ops/fabric.py)."""
+    def _fabric_suite(devices: List[int], timeout_s: Optional[float] = None) -> Dict[str, Any]:
+        """The node-level tests: xGMI pair matrix and the RCCL collectives in this process (ops/fabric.py); the
+        collectives get the watchdog's deadline too, so a hung one is aborted rather than left queued."""
         from ..ops import diag
         out: Dict[str, Any] = {}
+        t0 = time.monotonic()
         try:
             m = diag.p2p_matrix(devices)
             out["p2p"] = {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s")}
@@ -430,9 +561,15 @@ class Agent:
             out["p2p"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
         try:
             from ..ops import fabric
-            r = fabric.collective_suite(devices)
+            if timeout_s:
+                # the collectives abort themselves a little before the agent's watchdog fires, so the report
+                # says which collective hung rather than only "the fabric suite did not return"
+                left = 0.9 * timeout_s - (time.monotonic() - t0)
+                r = fabric.collective_suite(devices, timeout_s=max(0.001, left))
+            else:
+                r = fabric.collective_suite(devices)
             out["rccl"] = {k: r.get(k) for k in ("pass", "best_busbw_gbps", "best_busbw_by_op", "detail", "wall_s",
-                                                 "rccl")}
+                                                 "rccl", "aborted") if k in r or k != "aborted"}
         except Exception as e:
             out["rccl"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
         return out
@@ -722,7 +859,10 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
 
 def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = None) -> ThreadingHTTPServer:
     """/probe, /metrics, /status (text) and /healthz; /healthz answers 503 once no probe has completed for
-    ``stale_after`` s (a wedged amd-smi call or driver), so a livenessProbe restarts the agent."""
+    ``stale_after`` s (a wedged amd-smi call or driver), once a diagnostic thread has outlived
+    HUNG_RESTART_FACTOR x ``diag_timeout`` (a hung HIP queue the process cannot cancel) or after the HIP runtime
+    lost its devices, so a livenessProbe restarts the agent as a fresh process (the kubelet starts a new
+    container; nothing is re-executed in place)."""
     started = time.monotonic()
 
     class H(BaseHTTPRequestHandler):
@@ -752,9 +892,10 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
                 last = agent.last_probe_done if agent.last_probe_done is not None else started
                 idle = time.monotonic() - last
                 lost = agent.hip_lost
-                if lost is not None or (stale_after is not None and idle > stale_after):
+                hung = agent.hung_diagnostic()
+                if lost is not None or hung is not None or (stale_after is not None and idle > stale_after):
                     body = (f"HIP runtime lost its devices: {lost}" if lost is not None
-                            else f"no probe completed for {idle:.0f} s").encode()
+                            else hung if hung is not None else f"no probe completed for {idle:.0f} s").encode()
                     self.send_response(503)
                     self.send_header("Content-Type", "text/plain")
                     self.send_header("Content-Length", str(len(body)))
@@ -812,6 +953,10 @@ def build_parser() -> argparse.ArgumentParser:
                     help="a process other than the agent holding this much VRAM makes its GPU busy (default 2048)")
     ap.add_argument("--diag-timeout", type=float, default=300.0,
                     help="a GPU whose diagnostics run longer than this (s) is reported failed (hung); default 300")
+    ap.add_argument("--diag-parallel", type=int, default=DIAG_PARALLEL, metavar="N",
+                    help=f"per-device diagnostic threads at once (default {DIAG_PARALLEL}: an SPX node's GPUs together, "
+                         "a CPX node's 64 partitions in waves); tests on shared host resources (the PCIe host link) "
+                         "run one device at a time whatever N is")
     ap.add_argument("--ignore-pid", type=int, action="append", default=[], metavar="PID",
                     help="a process whose VRAM never makes a GPU busy (repeatable; e.g. the harness that "
                          "started the agent). The agent's own PID is always ignored")
@@ -850,7 +995,7 @@ def main(argv: Optional[List[str]] = None) -> int:
                   expectations=HealthExpectations(xgmi_links=args.xgmi_links),
                   pod_resources_socket=args.pod_resources_socket,
                   gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)), label_node=args.label_node,
-                  annotation_encoding=args.annotation_encoding)
+                  annotation_encoding=args.annotation_encoding, diag_parallel=args.diag_parallel)
     client = None
     if "annotation" in pubs:
         from ..kube.client import KubeClient

@@ -30,20 +30,24 @@
 #include <hip/hip_bf16.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
 namespace {
 
 thread_local std::string g_err;
-int g_gemm_variant = 0;
-int g_gemm_buffer_loads = 0;  // v3 operand staging: 0 = global_load_lds, 1 = buffer_load ... lds
-int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3 kernels;
-                          // measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
+// GEMM knobs are per calling thread: the node agent runs one diagnostic thread per GPU at once, and a
+// test or tool that switches a variant must not change what another GPU's thread launches.
+thread_local int g_gemm_variant = 0;
+thread_local int g_gemm_buffer_loads = 0;  // v3 operand staging: 0 = global_load_lds, 1 = buffer_load ... lds
+thread_local int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3
+                                       // kernels; measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
 
 #define DIAG_CHECK(expr)                                                                  \
   do {                                                                                    \
@@ -1019,6 +1023,34 @@ struct Timer {
   }
 };
 
+// hipFuncAttributeMaxDynamicSharedMemorySize is a per-device property of a kernel: it is set once for
+// every (kernel, device) pair, on the device current to the calling thread, before that pair's first
+// launch.  Devices run concurrently (one agent thread per GPU, up to 64 in CPX), hence one once_flag per
+// ordinal rather than one process-wide bool.
+constexpr int kMaxDevices = 256;
+struct LdsAttrOnce {
+  std::once_flag once[kMaxDevices];
+  hipError_t result[kMaxDevices] = {};
+};
+
+int ensure_dynamic_lds(LdsAttrOnce& slot, const void* kernel, int bytes, const char* what) {
+  int dev = 0;
+  DIAG_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDevices) {
+    DIAG_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    return 0;
+  }
+  std::call_once(slot.once[dev], [&] {
+    slot.result[dev] = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  });
+  if (slot.result[dev] != hipSuccess) {
+    g_err = std::string(what) + ": hipFuncSetAttribute(MaxDynamicSharedMemorySize) on device " +
+            std::to_string(dev) + ": " + hipGetErrorString(slot.result[dev]);
+    return -1;
+  }
+  return 0;
+}
+
 hipError_t enable_peer(int from, int to) {
   hipError_t e = hipSetDevice(from);
   if (e != hipSuccess) return e;
@@ -1032,12 +1064,10 @@ hipError_t enable_peer(int from, int to) {
 
 template <int DT, bool EPI, bool BUF>
 int launch_v3_inst(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI, BUF>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
-    attr_set = true;
-  }
+  static LdsAttrOnce attr;
+  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI, BUF>), 2 * V2_STAGE_BYTES,
+                         "gemm v3") != 0)
+    return -1;
   const int nwg = (M / V2_BM) * (N / V2_BN);
   hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI, BUF>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, stream,
                      static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, M, N, Kcols);
@@ -1066,6 +1096,9 @@ const char* diag_last_error(void) { return g_err.c_str(); }
 void diag_set_gemm_variant(int v) { g_gemm_variant = v; }
 void diag_set_gemm_epilogue(int e) { g_gemm_epilogue = e; }
 void diag_set_gemm_buffer_loads(int b) { g_gemm_buffer_loads = b; }
+int diag_get_gemm_variant(void) { return g_gemm_variant; }
+int diag_get_gemm_epilogue(void) { return g_gemm_epilogue; }
+int diag_get_gemm_buffer_loads(void) { return g_gemm_buffer_loads; }
 
 int diag_device_count(void) {
   int n = 0;
@@ -1100,12 +1133,10 @@ int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N,
       return -2;
     }
     if (variant == 2) {
-      static bool attr_set = false;
-      if (!attr_set) {
-        DIAG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_v2_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
-        attr_set = true;
-      }
+      static LdsAttrOnce attr;
+      if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_bf16_v2_kernel), 2 * V2_STAGE_BYTES,
+                             "gemm v2") != 0)
+        return -1;
       const int nwg = (M / V2_BM) * (N / V2_BN);
       hipLaunchKernelGGL(gemm_bf16_v2_kernel, dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
                          static_cast<hipStream_t>(stream), static_cast<const __bf16*>(A),

@@ -14,6 +14,11 @@
 // Bandwidth follows the nccl-tests convention: bytes = the larger of the per-rank input and output,
 // algbw = bytes / t, busbw = algbw * 2(n-1)/n (all-reduce) or algbw * (n-1)/n (the others).
 //
+// Hangs are bounded: the communicators are non-blocking (ncclConfig_t.blocking = 0), every wait polls the
+// streams and ncclCommGetAsyncError against a deadline instead of sitting in hipStreamSynchronize, and a
+// deadline that passes aborts every communicator (ncclCommAbort), so a link that stopped passing traffic
+// comes back as a failed, aborted collective instead of a thread stuck forever in the node agent.
+//
 // C ABI (ctypes, ops/fabric.py):  fabric_open -> fabric_run (any number) -> fabric_close.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -23,6 +28,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <unistd.h>
@@ -101,7 +107,64 @@ struct Dev {
 
 struct Ctx {
   std::vector<Dev> devs;
+  bool aborted = false;  // ncclCommAbort ran: no further collectives, buffers left to the process's end
 };
+
+using Clock = std::chrono::steady_clock;
+
+// a wait's deadline; ms <= 0 waits without one
+struct Deadline {
+  bool on = false;
+  Clock::time_point at;
+  double ms = 0.0;
+  explicit Deadline(double limit_ms) : on(limit_ms > 0), ms(limit_ms) {
+    if (on) at = Clock::now() + std::chrono::microseconds(static_cast<int64_t>(limit_ms * 1000.0));
+  }
+  bool passed() const { return on && Clock::now() >= at; }
+};
+
+// Abort every communicator: the collective kernels stop waiting for peers that never arrive and RCCL
+// releases the communicators.  The device buffers are not freed (a hipFree would wait for the device) --
+// an aborted fabric check leaves them to the process, which the agent's liveness probe replaces anyway.
+int abort_all(Ctx& c, const std::string& what, const Deadline& dl) {
+  for (Dev& d : c.devs) {
+    if (d.comm) {
+      (void)hipSetDevice(d.device);
+      (void)ncclCommAbort(d.comm);
+      d.comm = nullptr;
+    }
+  }
+  c.aborted = true;
+  char ms[32];
+  snprintf(ms, sizeof(ms), "%.0f", dl.ms);
+  g_err = what + ": not complete within " + ms + " ms: communicators aborted (ncclCommAbort)";
+  return -4;
+}
+
+// Wait until no communicator is in ncclInProgress (non-blocking init and group launches); an async error
+// or the deadline aborts them all.
+int wait_comms(Ctx& c, const Deadline& dl, const char* what) {
+  for (;;) {
+    bool pending = false;
+    for (Dev& d : c.devs) {
+      if (!d.comm) continue;
+      ncclResult_t st = ncclSuccess;
+      ncclResult_t r = ncclCommGetAsyncError(d.comm, &st);
+      if (r != ncclSuccess) st = r;
+      if (st == ncclInProgress) {
+        pending = true;
+      } else if (st != ncclSuccess) {
+        const std::string why = std::string(what) + ": " + ncclGetErrorString(st);
+        abort_all(c, why, dl);
+        g_err = why + " (communicators aborted)";
+        return -2;
+      }
+    }
+    if (!pending) return 0;
+    if (dl.passed()) return abort_all(c, what, dl);
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
 
 unsigned grid_for(size_t n) { return static_cast<unsigned>(std::min<size_t>((n + 255) / 256, 4096)); }
 
@@ -128,31 +191,71 @@ void shapes(int op, size_t count, int n, size_t* in_n, size_t* out_n, size_t* pe
   }
 }
 
-int issue(Ctx& c, int op, size_t count) {
+// ncclSuccess, or ncclInProgress from a non-blocking communicator (completion is polled in wait_comms)
+#define NCCL_NB(expr)                                                         \
+  do {                                                                        \
+    ncclResult_t r_ = (expr);                                                 \
+    if (r_ != ncclSuccess && r_ != ncclInProgress) {                          \
+      g_err = std::string(#expr) + ": " + ncclGetErrorString(r_);             \
+      return -2;                                                              \
+    }                                                                         \
+  } while (0)
+
+// One collective on every GPU in one group; returns once RCCL has enqueued it on every stream.
+int issue(Ctx& c, int op, size_t count, const Deadline& dl) {
   const int n = static_cast<int>(c.devs.size());
   size_t in_n, out_n, per;
   shapes(op, count, n, &in_n, &out_n, &per);
-  NCCL_OK(ncclGroupStart());
+  NCCL_NB(ncclGroupStart());
   for (Dev& d : c.devs) {
     switch (op) {
-      case ALL_REDUCE: NCCL_OK(ncclAllReduce(d.in, d.out, per, ncclFloat32, ncclSum, d.comm, d.stream)); break;
+      case ALL_REDUCE: NCCL_NB(ncclAllReduce(d.in, d.out, per, ncclFloat32, ncclSum, d.comm, d.stream)); break;
       case REDUCE_SCATTER:
-        NCCL_OK(ncclReduceScatter(d.in, d.out, per, ncclFloat32, ncclSum, d.comm, d.stream));
+        NCCL_NB(ncclReduceScatter(d.in, d.out, per, ncclFloat32, ncclSum, d.comm, d.stream));
         break;
-      case ALL_GATHER: NCCL_OK(ncclAllGather(d.in, d.out, per, ncclFloat32, d.comm, d.stream)); break;
-      default: NCCL_OK(ncclAllToAll(d.in, d.out, per, ncclFloat32, d.comm, d.stream)); break;
+      case ALL_GATHER: NCCL_NB(ncclAllGather(d.in, d.out, per, ncclFloat32, d.comm, d.stream)); break;
+      default: NCCL_NB(ncclAllToAll(d.in, d.out, per, ncclFloat32, d.comm, d.stream)); break;
     }
   }
-  NCCL_OK(ncclGroupEnd());
+  ncclResult_t r = ncclGroupEnd();
+  if (r == ncclInProgress) return wait_comms(c, dl, "collective launch");
+  if (r != ncclSuccess) {
+    g_err = std::string("ncclGroupEnd: ") + ncclGetErrorString(r);
+    return -2;
+  }
   return 0;
 }
 
-int sync_all(Ctx& c) {
-  for (Dev& d : c.devs) {
-    HIP_OK(hipSetDevice(d.device));
-    HIP_OK(hipStreamSynchronize(d.stream));
+// Every stream drained.  Polled (hipStreamQuery + the communicators' async errors) rather than blocking in
+// hipStreamSynchronize, so a collective that never completes is aborted at the deadline.
+int sync_all(Ctx& c, const Deadline& dl, const char* what) {
+  for (;;) {
+    bool busy = false;
+    for (Dev& d : c.devs) {
+      HIP_OK(hipSetDevice(d.device));
+      hipError_t e = hipStreamQuery(d.stream);
+      if (e == hipErrorNotReady) {
+        (void)hipGetLastError();
+        busy = true;
+      } else if (e != hipSuccess) {
+        (void)hipGetLastError();
+        g_err = std::string(what) + ": " + hipGetErrorString(e);
+        return -1;
+      }
+    }
+    if (!busy) return 0;
+    for (Dev& d : c.devs) {
+      ncclResult_t st = ncclSuccess;
+      if (d.comm && ncclCommGetAsyncError(d.comm, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress) {
+        const std::string why = std::string(what) + ": " + ncclGetErrorString(st);
+        abort_all(c, why, dl);
+        g_err = why + " (communicators aborted)";
+        return -2;
+      }
+    }
+    if (dl.passed()) return abort_all(c, what, dl);
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
-  return 0;
 }
 
 }  // namespace
@@ -166,8 +269,9 @@ int fabric_rccl_version(void) {
   return ncclGetVersion(&v) == ncclSuccess ? v : -1;
 }
 
-// One communicator, stream and error counter per device (devices = HIP ordinals, n >= 1).
-void* fabric_open(const int* devices, int n) {
+// One non-blocking communicator, stream and error counter per device (devices = HIP ordinals, n >= 1);
+// communicator setup not complete within timeout_ms (> 0) is aborted and fails the open.
+void* fabric_open(const int* devices, int n, double timeout_ms) {
   if (n < 1 || n > 64) {
     g_err = "fabric_open: 1..64 devices";
     return nullptr;
@@ -196,29 +300,57 @@ void* fabric_open(const int* devices, int n) {
       return fail();
     }
   }
+  const Deadline dl(timeout_ms);
   ncclResult_t r;
   {
+    // what ncclCommInitAll does, with a non-blocking config: one unique id, every rank initialised from
+    // this thread inside one group
     StdoutToStderr quiet;
-    r = ncclCommInitAll(comms.data(), n, devices);
+    ncclUniqueId id;
+    r = ncclGetUniqueId(&id);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    if (r == ncclSuccess) r = ncclGroupStart();
+    for (int i = 0; i < n && (r == ncclSuccess || r == ncclInProgress); ++i) {
+      (void)hipSetDevice(devices[i]);
+      r = ncclCommInitRankConfig(&comms[static_cast<size_t>(i)], n, id, i, &cfg);
+    }
+    ncclResult_t e = ncclGroupEnd();
+    if (r == ncclSuccess || r == ncclInProgress) r = e;
   }
-  if (r != ncclSuccess) {
-    g_err = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    g_err = std::string("ncclCommInitRankConfig (non-blocking): ") + ncclGetErrorString(r);
+    for (ncclComm_t cm : comms)
+      if (cm) (void)ncclCommAbort(cm);
     return fail();
   }
   for (int i = 0; i < n; ++i) c->devs[static_cast<size_t>(i)].comm = comms[static_cast<size_t>(i)];
+  if (wait_comms(*c, dl, "communicator init") != 0) {
+    const std::string why = g_err;
+    for (Dev& d : c->devs) d.comm = nullptr;  // aborted in wait_comms
+    fail();
+    g_err = why;
+    return nullptr;
+  }
   return c;
 }
 
 // Run `op` on `bytes` per rank (rounded down to a whole number of fp32 chunks): `warmup` untimed calls,
 // `iters` timed calls (host wall clock from the first issue to the last stream's completion), then one
 // verified call.  out[0] = ms per call, out[1] = algbw GB/s, out[2] = busbw GB/s, out[3] = bad elements
-// summed over every GPU.
-int fabric_run(void* ctx, int op, size_t bytes, int iters, int warmup, double* out) {
+// summed over every GPU.  All of it within timeout_ms (> 0), else the communicators are aborted and the
+// call returns -4 (the context then refuses further runs).
+int fabric_run(void* ctx, int op, size_t bytes, int iters, int warmup, double* out, double timeout_ms) {
   if (!ctx || op < 0 || op > 3 || iters < 1 || warmup < 0) {
     g_err = "fabric_run: bad arguments";
     return -3;
   }
   Ctx& c = *static_cast<Ctx*>(ctx);
+  if (c.aborted) {
+    g_err = "fabric_run: communicators were aborted by an earlier timeout";
+    return -4;
+  }
+  const Deadline dl(timeout_ms);
   const int n = static_cast<int>(c.devs.size());
   size_t count = bytes / sizeof(float);
   count -= count % static_cast<size_t>(n);
@@ -241,15 +373,15 @@ int fabric_run(void* ctx, int op, size_t bytes, int iters, int warmup, double* o
     hipLaunchKernelGGL(fill_kernel, dim3(grid_for(in_n)), dim3(256), 0, d.stream, d.in, in_n, chunk, a, b);
     HIP_OK(hipGetLastError());
   }
-  if (sync_all(c) != 0) return -1;
+  if (int rc = sync_all(c, dl, "input fill"); rc != 0) return rc;
 
   for (int i = 0; i < warmup; ++i)
-    if (issue(c, op, count) != 0) return -2;
-  if (sync_all(c) != 0) return -1;
+    if (int rc = issue(c, op, count, dl); rc != 0) return rc;
+  if (int rc = sync_all(c, dl, "warm-up collectives"); rc != 0) return rc;
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < iters; ++i)
-    if (issue(c, op, count) != 0) return -2;
-  if (sync_all(c) != 0) return -1;
+    if (int rc = issue(c, op, count, dl); rc != 0) return rc;
+  if (int rc = sync_all(c, dl, "timed collectives"); rc != 0) return rc;
   const double ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / iters;
 
@@ -259,7 +391,7 @@ int fabric_run(void* ctx, int op, size_t bytes, int iters, int warmup, double* o
     HIP_OK(hipMemsetAsync(d.out, 0, out_n * sizeof(float), d.stream));
     HIP_OK(hipMemsetAsync(d.errors, 0, sizeof(unsigned long long), d.stream));
   }
-  if (issue(c, op, count) != 0) return -2;
+  if (int rc = issue(c, op, count, dl); rc != 0) return rc;
   const float tri = static_cast<float>(n) * static_cast<float>(n + 1) / 2.f;
   for (int r = 0; r < n; ++r) {
     Dev& d = c.devs[static_cast<size_t>(r)];
@@ -273,7 +405,7 @@ int fabric_run(void* ctx, int op, size_t bytes, int iters, int warmup, double* o
                        d.errors);
     HIP_OK(hipGetLastError());
   }
-  if (sync_all(c) != 0) return -1;
+  if (int rc = sync_all(c, dl, "verified collective"); rc != 0) return rc;
   unsigned long long bad = 0;
   for (Dev& d : c.devs) {
     unsigned long long e = 0;
@@ -291,9 +423,20 @@ int fabric_run(void* ctx, int op, size_t bytes, int iters, int warmup, double* o
   return 0;
 }
 
+int fabric_aborted(void* ctx) { return ctx && static_cast<Ctx*>(ctx)->aborted ? 1 : 0; }
+
 void fabric_close(void* ctx) {
   if (!ctx) return;
   Ctx* c = static_cast<Ctx*>(ctx);
+  if (c->aborted) {  // see abort_all: nothing that could wait on the device
+    for (Dev& d : c->devs)
+      if (d.device >= 0 && d.stream) {
+        (void)hipSetDevice(d.device);
+        (void)hipStreamDestroy(d.stream);
+      }
+    delete c;
+    return;
+  }
   for (Dev& d : c->devs) {
     if (d.device < 0) continue;
     (void)hipSetDevice(d.device);

@@ -16,6 +16,7 @@ silently skipping the diagnostic.
 from __future__ import annotations
 
 import ctypes
+import threading
 import time
 from typing import Any, Dict, List, Optional
 
@@ -40,11 +41,22 @@ from .native import NativeUnavailable, load_cdll
 # Partitions: the reference rates are scaled by the share of the physical GPU the HIP device is.
 #   compute (GEMM, MFMA burn-in):   cus / 256       (CPX: 32 CUs -> 1/8)
 #   memory (HBM copy / read):       min(mem_bytes / 288 GiB, 1/NPS, cus / 256)
-#   host link (PCIe):               cus / 256       (every partition of one GPU shares its x16 link, and the
-#                                                    agent runs them concurrently)
+#   host link (PCIe):               cus / 256       (every partition of one GPU shares its x16 link)
+# Power: a GPU whose power cap was lowered below its default runs its matrix cores at lower clocks; the
+# compute references are scaled by cap / default (run(power_fraction=...), from amd-smi), which is lenient
+# (rate falls slower than power), so a deliberately capped GPU is judged against its cap, not failed for it.
+#
+# Concurrency: the node agent runs every GPU's suite at once (--diag-parallel).  Per-GPU resources (CUs, HBM,
+# the GPU's own power budget) are not shared between GPUs; the host side is, so the tests that measure it --
+# SHARED_TESTS, the PCIe host link (pinned host memory, the CPU root complex, switch uplinks two GPUs may share)
+# -- run one device at a time under a process-wide lock, each against the single-GPU reference.  The rate
+# references themselves were measured on one MI355X running alone; the same suite on all 8 GPUs of a node at
+# once is unmeasured (parity unpinned: no 8-GPU box was available to this project).
 # The partition scaling is proportional, not measured (no partitioned MI355X was available): it is the
 # lenient bound, so a healthy partition never fails; a partitioned GPU's degraded band is advisory.
 FAIL_FRACTION = 0.85
+SHARED_TESTS = frozenset(("host_link",))
+_HOST_SHARED = threading.Lock()  # held by the one device measuring a SHARED_TESTS test
 # A rate below the degraded line (numerics fine) is measured again, up to REMEASURE more times, and the best
 # is kept: under sustained load the burn-in dips below 95 % in ~10 % of single runs (power management),
 # two dips in a row were 19 of 1,913 soak rounds (profiles/soak_level1_r2_mi355x.json); three in a row
@@ -95,9 +107,11 @@ class Scale:
 
     @classmethod
     def of(cls, cus: Optional[int] = None, mem_bytes: Optional[int] = None,
-           memory_partition: Optional[str] = None) -> "Scale":
+           memory_partition: Optional[str] = None, power_fraction: Optional[float] = None) -> "Scale":
         c = min(1.0, cus / FULL_CUS) if isinstance(cus, int) and cus > 0 else 1.0
         m = c
+        if isinstance(power_fraction, (int, float)) and 0.0 < power_fraction < 1.0:
+            c *= power_fraction  # compute only: HBM and the host link do not follow the core clock
         if isinstance(mem_bytes, int) and mem_bytes > 0:
             m = min(m, mem_bytes / FULL_MEM_BYTES)
         if isinstance(memory_partition, str) and memory_partition.upper().startswith("NPS"):
@@ -160,6 +174,8 @@ def lib() -> ctypes.CDLL:
         L.diag_set_gemm_variant.argtypes = [ctypes.c_int]
         L.diag_set_gemm_epilogue.argtypes = [ctypes.c_int]
         L.diag_set_gemm_buffer_loads.argtypes = [ctypes.c_int]
+        for getter in ("diag_get_gemm_variant", "diag_get_gemm_epilogue", "diag_get_gemm_buffer_loads"):
+            getattr(L, getter).restype = ctypes.c_int
         L.diag_device_count.restype = ctypes.c_int
         L.diag_device_arch.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.diag_gemm_bf16_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -234,6 +250,47 @@ def set_gemm_buffer_loads(buffer_loads: bool) -> None:
     lds`` from two per-tile buffer resources (True: loop-invariant per-lane offsets, the K step in a
     scalar register)."""
     lib().diag_set_gemm_buffer_loads(1 if buffer_loads else 0)
+
+
+def get_gemm_config() -> Dict[str, Any]:
+    """The calling thread's GEMM knobs (they are thread-local in the library: every agent thread
+    starts from the production defaults ``auto`` / LDS-staged epilogue / ``global_load_lds``)."""
+    L = lib()
+    inv = {v: k for k, v in GEMM_VARIANTS.items()}
+    return {"variant": inv.get(int(L.diag_get_gemm_variant()), "auto"),
+            "epilogue": bool(L.diag_get_gemm_epilogue()),
+            "buffer_loads": bool(L.diag_get_gemm_buffer_loads())}
+
+
+def get_gemm_epilogue() -> bool:
+    return bool(lib().diag_get_gemm_epilogue())
+
+
+class gemm_config:
+    """``with gemm_config(variant="v3", epilogue=False): ...`` -- set knobs for the calling thread
+    and restore the previous values on exit (not the library defaults)."""
+
+    def __init__(self, variant: Optional[str] = None, epilogue: Optional[bool] = None,
+                 buffer_loads: Optional[bool] = None):
+        self.want = {"variant": variant, "epilogue": epilogue, "buffer_loads": buffer_loads}
+        self.saved: Dict[str, Any] = {}
+
+    @staticmethod
+    def _apply(cfg: Dict[str, Any]) -> None:
+        if cfg.get("variant") is not None:
+            set_gemm_variant(cfg["variant"])
+        if cfg.get("epilogue") is not None:
+            set_gemm_epilogue(cfg["epilogue"])
+        if cfg.get("buffer_loads") is not None:
+            set_gemm_buffer_loads(cfg["buffer_loads"])
+
+    def __enter__(self) -> "gemm_config":
+        self.saved = get_gemm_config()
+        self._apply(self.want)
+        return self
+
+    def __exit__(self, *exc: Any) -> None:
+        self._apply(self.saved)
 
 
 def gemm_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int, stream: int = 0) -> None:
@@ -582,11 +639,12 @@ LEVELS = {
 }
 
 
-def device_scale(device: int = 0, memory_partition: Optional[str] = None) -> Scale:
-    """The :class:`Scale` of HIP ``device`` (CU count and memory from HIP; ``memory_partition`` from
-    amd-smi when the caller has it)."""
+def device_scale(device: int = 0, memory_partition: Optional[str] = None,
+                 power_fraction: Optional[float] = None) -> Scale:
+    """The :class:`Scale` of HIP ``device`` (CU count and memory from HIP; ``memory_partition`` and the power
+    cap's share of its default from amd-smi when the caller has them)."""
     info = device_info(device)
-    return Scale.of(info.get("cus"), info.get("mem_bytes"), memory_partition)
+    return Scale.of(info.get("cus"), info.get("mem_bytes"), memory_partition, power_fraction)
 
 
 def _one(test: str, device: int, scale: Scale) -> Dict[str, Any]:
@@ -635,16 +693,17 @@ def _goodness(res: Dict[str, Any]) -> tuple:
 
 
 def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
-        memory_partition: Optional[str] = None) -> Dict[str, Dict[str, Any]]:
+        memory_partition: Optional[str] = None, power_fraction: Optional[float] = None) -> Dict[str, Dict[str, Any]]:
     """Run the diagnostics of ``level`` on ``device`` (1 = ~1 s quick check, 2 = deep).
 
     ``scale`` defaults to the device's own share of a full MI355X (:func:`device_scale`).  A rate that
-    lands below the degraded line is measured once more and the better of the two is reported."""
+    lands below the degraded line is measured once more and the better of the two is reported.  Tests of
+    host resources (SHARED_TESTS) hold a process-wide lock, so concurrent per-GPU runs take turns there."""
     out: Dict[str, Dict[str, Any]] = {}
     tests = LEVELS.get(level, ())
     if tests and scale is None:
         try:
-            scale = device_scale(device, memory_partition)
+            scale = device_scale(device, memory_partition, power_fraction)
         except NativeUnavailable:
             raise
         except Exception:
@@ -652,7 +711,10 @@ def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
     scale = scale or FULL
     for test in tests:
         name = test.replace("_quick", "")
+        shared = _HOST_SHARED if name in SHARED_TESTS else None
         try:
+            if shared is not None:
+                shared.acquire()
             res = _one(test, device, scale)
             for _ in range(REMEASURE):
                 if not _slow_only(res):
@@ -670,6 +732,9 @@ def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
             raise
         except Exception as e:  # a failing diagnostic is a verdict, not a crash
             out[name] = {"pass": False, "detail": str(e)[:200]}
+        finally:
+            if shared is not None:
+                shared.release()
     return out
 
 

@@ -9,6 +9,10 @@ one ``parallel/collectives.py`` applies (:func:`~k8s_gpu_node_checker_amd.parall
 correct data everywhere, and on a full 8-GPU hive a >= 256 MiB all-reduce busbw of at least
 ``MIN_BUSBW_GBPS``.
 
+The communicators are non-blocking: with ``timeout_s`` every wait polls against one deadline for the whole
+suite, and a collective that has not completed by then is aborted (``ncclCommAbort``) and reported as a failed,
+``aborted`` suite -- the node agent's watchdog then sees a verdict, not a thread stuck in the driver.
+
 The library is required: a missing build raises ``NativeUnavailable``.
 
     python -m k8s_gpu_node_checker_amd.ops.fabric [--device 0 --device 1 ...] [--sizes 64M,256M]
@@ -36,10 +40,12 @@ def lib() -> ctypes.CDLL:
         L.fabric_last_error.restype = ctypes.c_char_p
         L.fabric_rccl_version.restype = ctypes.c_int
         L.fabric_open.restype = ctypes.c_void_p
-        L.fabric_open.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        L.fabric_open.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_double]
         L.fabric_run.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
-                                 ctypes.POINTER(ctypes.c_double)]
+                                 ctypes.POINTER(ctypes.c_double), ctypes.c_double]
         L.fabric_close.argtypes = [ctypes.c_void_p]
+        L.fabric_aborted.argtypes = [ctypes.c_void_p]
+        L.fabric_aborted.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -48,24 +54,37 @@ def _error() -> str:
     return lib().fabric_last_error().decode(errors="replace")
 
 
+ABORTED = -4  # fabric_run / fabric_open: the deadline passed and the communicators were aborted
+
+
 def collective_suite(devices: Sequence[int], sizes: Sequence[int] = DEFAULT_SIZES, ops: Sequence[str] = OPS,
-                     iters: int = 10, warmup: int = 3, min_busbw: float = MIN_BUSBW_GBPS) -> Dict[str, Any]:
-    """Every op at every size over ``devices``; rows like ``parallel.collectives.collective_bench``."""
+                     iters: int = 10, warmup: int = 3, min_busbw: float = MIN_BUSBW_GBPS,
+                     timeout_s: Optional[float] = None) -> Dict[str, Any]:
+    """Every op at every size over ``devices``; rows like ``parallel.collectives.collective_bench``.  With
+    ``timeout_s`` the whole suite (communicator setup included) has that long; past it the communicators are
+    aborted and the result is a failure with ``aborted: True``."""
     devs = list(devices)
     t0 = time.perf_counter()
+    deadline = None if not timeout_s or timeout_s <= 0 else time.monotonic() + timeout_s
+
+    def left_ms() -> float:  # 0 = no deadline; a spent one still gets 1 ms (the call aborts at once)
+        return 0.0 if deadline is None else max(1.0, (deadline - time.monotonic()) * 1e3)
     arr = (ctypes.c_int * len(devs))(*devs)
-    ctx = lib().fabric_open(arr, len(devs))
+    ctx = lib().fabric_open(arr, len(devs), left_ms())
     if not ctx:
-        return {"pass": False, "world": len(devs), "rows": [], "detail": f"RCCL init: {_error()}"[:200]}
+        err = _error()
+        return {"pass": False, "world": len(devs), "rows": [], "aborted": "ncclCommAbort" in err,
+                "detail": f"RCCL init: {err}"[:200]}
     rows: List[Dict[str, Any]] = []
     try:
         out = (ctypes.c_double * 4)()
         for op in ops:
             for nbytes in sizes:
-                rc = lib().fabric_run(ctx, OPS.index(op), nbytes, iters, warmup, out)
+                rc = lib().fabric_run(ctx, OPS.index(op), nbytes, iters, warmup, out, left_ms())
                 if rc != 0:
-                    return {"pass": False, "world": len(devs), "rows": rows,
-                            "detail": f"{op} {nbytes} B: {_error()}"[:200]}
+                    return {"pass": False, "world": len(devs), "rows": rows, "aborted": rc == ABORTED,
+                            "detail": f"{op} {nbytes} B: {_error()}"[:200],
+                            "wall_s": round(time.perf_counter() - t0, 3)}
                 rows.append({"op": op, "bytes": nbytes, "ms": round(out[0], 4), "algbw_gbps": round(out[1], 2),
                              "busbw_gbps": round(out[2], 2) if len(devs) > 1 else None,
                              "errors": int(out[3]), "correct": out[3] == 0})

@@ -41,13 +41,17 @@ class FakeDiagLib:
                  slow_xcd: Optional[Dict[int, float]] = None, bad_cu: Optional[Dict[Tuple[int, int], int]] = None,
                  lds_bad: Optional[Dict[Tuple[int, int], int]] = None,
                  l2_bad: Optional[Dict[Tuple[int, int], int]] = None, slow_cu: Optional[Dict[int, float]] = None,
-                 hbm_xcd_slow: Optional[Dict[int, float]] = None, hbm_bad: Optional[Dict[Tuple[int, int], int]] = None):
+                 hbm_xcd_slow: Optional[Dict[int, float]] = None, hbm_bad: Optional[Dict[Tuple[int, int], int]] = None,
+                 compute_rate: Optional[Dict[int, float]] = None):
         from ..ops import diag
         self.ref = diag.REFERENCE_RATES
         self.kinds = diag.MFMA_KINDS
         self.n = n
         self.rate = rate
         self.gpu_rate = dict(gpu_rate or {})
+        # compute_rate[d]: an extra factor on device d's matrix-core tests only (GEMM, burn-in) -- a lowered
+        # power cap slows the core clock, not HBM or the host link
+        self.compute_rate = dict(compute_rate or {})
         self.rates = list(rates or [])
         self.cus = cus
         self.mem_gib = mem_gib
@@ -73,6 +77,23 @@ class FakeDiagLib:
         self.calls: List[str] = []
         self.threads: Dict[int, set] = {}
         self.lock = threading.Lock()
+        # shared host link: with link_shared, concurrent host_link calls split the host's bandwidth (each gets
+        # 1/k of it while k run at once, for link_delay_s); in_flight / peak_* record the overlap
+        self.link_shared = False
+        self.link_delay_s = 0.0
+        self.in_flight: Dict[str, int] = {}
+        self.peak: Dict[str, int] = {}
+
+    def _enter(self, what: str) -> int:
+        with self.lock:
+            k = self.in_flight.get(what, 0) + 1
+            self.in_flight[what] = k
+            self.peak[what] = max(self.peak.get(what, 0), k)
+            return k
+
+    def _leave(self, what: str) -> None:
+        with self.lock:
+            self.in_flight[what] -= 1
 
     def _rate(self, device: int) -> float:
         with self.lock:
@@ -102,11 +123,13 @@ class FakeDiagLib:
 
     def _gemm(self, test, device, size, tflops, err, ms):
         self._log(device, test)
+        self._enter("gemm")
         if self.delay_s:
             time.sleep(self.delay_s)
+        self._leave("gemm")
         table = self.ref[test]
         key = size if size in table else min(table, key=lambda k: abs(k - size))
-        _put(tflops, ctypes.c_double, self._rate(device) * table[key])
+        _put(tflops, ctypes.c_double, self._rate(device) * self.compute_rate.get(device, 1.0) * table[key])
         _put(err, ctypes.c_double, self.gemm_err)
         _put(ms, ctypes.c_double, 0.1)
         return self.rc
@@ -138,7 +161,8 @@ class FakeDiagLib:
         if self.mfma is not None:
             tf, e = self.mfma[kind]
         else:
-            tf, e = self.gpu_rate.get(device, self.rate) * self.ref["mfma"][self.kinds[kind]], 0
+            tf, e = (self.gpu_rate.get(device, self.rate) * self.compute_rate.get(device, 1.0)
+                     * self.ref["mfma"][self.kinds[kind]], 0)
         _put(tflops, ctypes.c_double, tf)
         _put(errors, ctypes.c_ulonglong, self.mfma_errors.get((device, kind), e))
         return 0
@@ -235,6 +259,13 @@ class FakeDiagLib:
     def diag_host_link(self, device, nbytes, iters, h2d, d2h):
         self._log(device, "host_link")
         f = self.gpu_rate.get(device, self.rate)
+        k = self._enter("host_link")
+        if self.link_delay_s:
+            time.sleep(self.link_delay_s)
+        k = max(k, self.in_flight.get("host_link", 1))
+        self._leave("host_link")
+        if self.link_shared:
+            f /= k
         h, d = self.link or (f * self.ref["host_link"]["h2d_gbps"], f * self.ref["host_link"]["d2h_gbps"])
         _put(h2d, ctypes.c_double, h)
         _put(d2h, ctypes.c_double, d)
@@ -255,26 +286,45 @@ class FakeDiagLib:
 class FakeFabricLib:
     """``libmi355x_fabric.so`` (in-process RCCL communicator over the node's GPUs)."""
 
-    def __init__(self, busbw: float = 320.0, errors: int = 0, fail_open: bool = False, version: int = 22707):
+    def __init__(self, busbw: float = 320.0, errors: int = 0, fail_open: bool = False, version: int = 22707,
+                 hang_op: Optional[int] = None):
         self.busbw, self.errors, self.fail_open, self.version = busbw, errors, fail_open, version
+        # hang_op: that collective never completes -- the call waits out its deadline (or forever without
+        # one, until `release` is set) and then "aborts" the communicators like fabric.hip's abort_all
+        self.hang_op = hang_op
+        self.release = threading.Event()
         self.opened: List[List[int]] = []
+        self.timeouts_ms: List[float] = []
+        self.aborts = 0
         self.closed = 0
+        self.err = b"ncclCommInitAll: unhandled system error"
 
-    def fabric_open(self, arr, n):
+    def fabric_open(self, arr, n, timeout_ms=0.0):
         if self.fail_open:
             return None
         self.opened.append([arr[i] for i in range(n)])
         return 1
 
-    def fabric_run(self, ctx, op, nbytes, iters, warmup, out):
+    def fabric_run(self, ctx, op, nbytes, iters, warmup, out, timeout_ms=0.0):
+        self.timeouts_ms.append(timeout_ms)
+        if op == self.hang_op:
+            self.release.wait(timeout_ms / 1e3 if timeout_ms > 0 else None)
+            if not self.release.is_set():
+                self.aborts += 1  # ncclCommAbort on every communicator
+                self.err = (f"timed collectives: not complete within {timeout_ms:.0f} ms: communicators aborted "
+                            "(ncclCommAbort)").encode()
+                return -4
         out[0], out[1], out[2], out[3] = 1.0, self.busbw * 0.57, self.busbw, float(self.errors if op == 3 else 0)
         return 0
+
+    def fabric_aborted(self, ctx):
+        return 1 if self.aborts else 0
 
     def fabric_close(self, ctx):
         self.closed += 1
 
     def fabric_last_error(self):
-        return b"ncclCommInitAll: unhandled system error"
+        return self.err
 
     def fabric_rccl_version(self):
         return self.version

@@ -42,7 +42,7 @@ class World:
             self.fabric_runs += 1
             return {"pass": True, "median_gbps": 50.0, "min_gbps": 48.0, "detail": "", "wall_s": 0.1}
         monkeypatch.setattr(diag, "p2p_matrix", p2p)
-        monkeypatch.setattr(fabric, "collective_suite", lambda devs: {"pass": True, "best_busbw_gbps": 300.0,
+        monkeypatch.setattr(fabric, "collective_suite", lambda devs, **kw: {"pass": True, "best_busbw_gbps": 300.0,
                                                                       "best_busbw_by_op": {}, "detail": "",
                                                                       "wall_s": 0.2, "rccl": "2.27.7"})
 
@@ -167,13 +167,14 @@ def test_hung_diagnostic_is_reported_not_waited_for(monkeypatch):
     assert rep["gpus"][1]["diag"]["watchdog"]["pass"] is False
     # the hang clears: its real result replaces the watchdog failure
     release.set()
-    ag._diag_threads[1][0].join(5)
+    ag._diag_threads[1].thread.join(5)
     rep = ag.probe_once()
     assert rep["gpus"][1]["diag"] == {"gemm": {"pass": True}} and rep["state"] == HEALTHY
 
 
 def test_restarted_agent_clears_a_watchdog_verdict(monkeypatch, mock_cluster):
-    """The liveness probe restarts an agent whose diagnostic hung (its thread cannot be cancelled).
+    """The liveness probe restarts an agent whose diagnostic hung (its thread cannot be cancelled: /healthz
+    fails once it has outlived 2 x --diag-timeout, test_healthz_fails_once_a_diagnostic_outlives_twice_its_watchdog).
     The new instance carries no cached watchdog failure: its first publish rewrites the condition, the
     annotation and the taint the old instance left on the node (VERDICT r1 weak #8)."""
     import threading
@@ -278,7 +279,7 @@ def test_a_hung_fabric_test_is_a_failure_not_a_frozen_agent(monkeypatch):
     w = World(monkeypatch, n=2)
     release = threading.Event()
 
-    def hang(devs):
+    def hang(devs, **kw):
         w.fabric_runs += 1
         release.wait(10)
         return {"pass": True, "best_busbw_gbps": 300.0, "best_busbw_by_op": {}, "detail": "", "wall_s": 9.0}
@@ -345,3 +346,182 @@ def test_a_slow_result_is_measured_again_soon(monkeypatch):
     w.clock += A.DIAG_RECHECK_S * 2
     ag.probe_once()
     assert len(w.runs) == 2  # clean: back to the full interval
+
+
+def test_healthz_fails_once_a_diagnostic_outlives_twice_its_watchdog(monkeypatch):
+    """A per-GPU diagnostic stuck in a HIP call: the watchdog verdict goes out at 1 x --diag-timeout (the
+    agent keeps probing and publishing), /healthz stays 200 until the thread has lived 2 x --diag-timeout,
+    then answers 503 so the kubelet starts a fresh process.  It recovers to 200 if the call returns."""
+    import threading
+    import urllib.error
+    import urllib.request
+    w = World(monkeypatch)
+    release = threading.Event()
+
+    def run(level, d, memory_partition=None):
+        if d == 0:
+            release.wait(30)
+        return {"gemm": {"pass": True}}
+    monkeypatch.setattr(diag, "run", run)
+    ag = A.Agent("n", source="fake", diag_level=1, diag_interval=3600, diag_timeout=0.4)
+    srv = A.serve(ag, "127.0.0.1", 0, stale_after=60)
+    url = f"http://127.0.0.1:{srv.server_address[1]}/healthz"
+    try:
+        t0 = time.monotonic()
+        rep = ag.probe_once()  # returns after the 0.4 s watchdog with the verdict
+        assert rep["gpus"][0]["diag"]["watchdog"]["pass"] is False and rep["state"] == "unhealthy"
+        assert urllib.request.urlopen(url, timeout=5).status == 200  # 1x: published, not yet restarted
+        while time.monotonic() - t0 < 0.85:
+            time.sleep(0.05)
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(url, timeout=5)
+        assert e.value.code == 503
+        body = e.value.read().decode()
+        assert body.startswith("gpu0 diagnostics running for") and "2 x --diag-timeout" in body
+        assert w.gpus
+        release.set()
+        ag._diag_threads[0].thread.join(5)
+        assert urllib.request.urlopen(url, timeout=5).status == 200
+    finally:
+        release.set()
+        srv.shutdown()
+        srv.server_close()
+
+
+def test_healthz_fails_for_a_hung_fabric_suite(monkeypatch):
+    import threading
+    World(monkeypatch)
+    release = threading.Event()
+
+    def hang(devs):
+        release.wait(30)
+        return {"pass": True}
+    monkeypatch.setattr(diag, "p2p_matrix", hang)  # the pair matrix hangs (no deadline of its own)
+    ag = A.Agent("n", source="fake", diag_level=2, diag_interval=3600, diag_timeout=0.2)
+    try:
+        rep = ag.probe_once()
+        assert "watchdog" in rep["fabric"]
+        assert ag.hung_diagnostic() is None
+        time.sleep(0.25)
+        assert ag.hung_diagnostic().startswith("node-level xGMI/RCCL tests running for")
+    finally:
+        release.set()
+
+
+def test_per_gpu_diagnostics_wait_while_a_fabric_suite_is_hung(monkeypatch):
+    """a timed-out collective still holds every GPU; the next interval's per-GPU tests must not
+    start behind it."""
+    import threading
+    w = World(monkeypatch)
+    release = threading.Event()
+
+    def hang(devs, **kw):
+        release.wait(30)
+        return {"pass": True, "best_busbw_gbps": 300.0, "best_busbw_by_op": {}, "detail": "", "wall_s": 9.0}
+    monkeypatch.setattr(fabric, "collective_suite", hang)
+    ag = A.Agent("n", source="fake", diag_level=2, diag_interval=3600, diag_timeout=0.2)
+    try:
+        ag.probe_once()
+        assert w.runs == [0, 1] or sorted(w.runs) == [0, 1]
+        w.clock += 3600
+        rep = ag.probe_once()
+        assert sorted(w.runs) == [0, 1]  # nothing new started
+        assert all(g["diag_skipped"].startswith("node-level xGMI/RCCL tests still running") for g in rep["gpus"])
+        assert all(g["diag"] for g in rep["gpus"])  # the last results are kept
+    finally:
+        release.set()
+    ag._fabric_thread.thread.join(5)
+    w.clock += 1
+    ag.probe_once()
+    assert sorted(w.runs) == [0, 0, 1, 1]
+
+
+def test_a_persistent_failure_is_rechecked_once_then_back_to_the_interval(monkeypatch):
+    """a GPU that keeps failing the same way is not stressed again every 5 minutes."""
+    w = World(monkeypatch, n=1)
+    bad = {"memtest": {"pass": False, "detail": "12 bad words"}}
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: (w.runs.append(d), dict(bad))[1])
+    ag = A.Agent("n", source="fake", diag_level=1, diag_interval=3600.0)
+    ag.probe_once()
+    w.clock += A.DIAG_RECHECK_S
+    ag.probe_once()
+    assert len(w.runs) == 2  # the one recheck confirmed it
+    w.clock += A.DIAG_RECHECK_S
+    ag.probe_once()
+    assert len(w.runs) == 2  # the same failure again: back to the full interval
+    w.clock += 3600 - A.DIAG_RECHECK_S
+    ag.probe_once()
+    assert len(w.runs) == 3
+    # a different result (another test fails) earns one recheck of its own
+    bad = {"hbm": {"pass": False, "detail": "copy 3 TB/s"}}
+    w.clock += 3600
+    ag.probe_once()
+    w.clock += A.DIAG_RECHECK_S
+    ag.probe_once()
+    assert len(w.runs) == 5
+
+
+def test_allocations_matching_no_local_pci_address_skip_every_gpu(monkeypatch):
+    """a device plugin that names partitions by another scheme -- the agent cannot tell which
+    device a pod has, so it diagnoses none (fail safe) and says why."""
+    w = World(monkeypatch)
+    ag = A.Agent("n", source="fake", diag_level=1, pod_resources_socket="/nonexistent.sock")
+    monkeypatch.setattr(ag, "_allocated", lambda: {"amdgpu_xcp_3": "ml/train-0"})
+    rep = ag.probe_once()
+    assert w.runs == []
+    assert all(g["diag_skipped"].startswith("kubelet reports 1 allocated GPU device(s) (amdgpu_xcp_3) matching no "
+                                            "local PCI address") for g in rep["gpus"])
+    # matching addresses: only the allocated GPU is skipped
+    monkeypatch.setattr(ag, "_allocated", lambda: {"0000:01:00.0": "ml/train-0"})
+    w.clock += 3600
+    rep = ag.probe_once()
+    assert w.runs == [0] and rep["gpus"][1]["diag_skipped"] == "allocated to pod ml/train-0"
+
+
+def test_bdf_fallback_is_normalised(monkeypatch):
+    """HIP's domain-less, upper-case address still matches amd-smi's and the kubelet's."""
+    w = World(monkeypatch)
+    monkeypatch.setattr(diag, "device_info", lambda d: {"bdf": f"0{d}:00.0".upper()})
+    for g in w.gpus:
+        g["bdf"] = g["bdf"].upper()
+    ag = A.Agent("n", source="fake", diag_level=1, pod_resources_socket="/x")
+    monkeypatch.setattr(ag, "_allocated", lambda: {"0000:01:00.0": "ml/p"})
+    rep = ag.probe_once()
+    assert w.runs == [0] and rep["gpus"][1]["diag_skipped"] == "allocated to pod ml/p"
+
+
+def test_configured_device_hip_does_not_have_is_a_configuration_error(monkeypatch):
+    """a bad device index is said as such -- not run (it would fail with 'invalid device ordinal'),
+    not mistaken for a lost HIP runtime (no /healthz restart loop)."""
+    w = World(monkeypatch)
+    ag = A.Agent("n", source="fake", diag_level=1, devices=[0, 5])
+    rep = ag.probe_once()
+    assert w.runs == [0] and ag.hip_lost is None
+    assert ag._diag_skipped[5] == "device 5 is not a HIP device of the agent (2 visible): check --devices"
+
+
+def test_one_gpu_failing_with_runtime_strings_is_that_gpus_failure(monkeypatch):
+    """'invalid device ordinal' on one GPU while the other runs fine is not a lost runtime."""
+    w = World(monkeypatch)
+    lost = "mi355x diag failed (-1): hipSetDevice(device): invalid device ordinal"
+
+    def run(level, d, memory_partition=None):
+        w.runs.append(d)
+        return {"gemm": {"pass": False, "detail": lost}} if d == 1 else {"gemm": {"pass": True}}
+    monkeypatch.setattr(diag, "run", run)
+    ag = A.Agent("n", source="fake", diag_level=1)
+    rep = ag.probe_once()
+    assert ag.hip_lost is None and rep["gpus"][1]["diag"]["gemm"]["pass"] is False and rep["state"] == "unhealthy"
+    # the device count changed under the process: that is the runtime
+    monkeypatch.setattr(diag, "device_count", lambda: 1)
+    w.clock += A.DIAG_RECHECK_S
+    rep = ag.probe_once()
+    assert ag.hip_lost == "HIP device count changed from 2 to 1"
+    assert all(g["diag_skipped"].startswith("HIP runtime lost its devices (HIP device count changed")
+               for g in rep["gpus"][:1])
+    # and when every device that ran failed that way together, also the runtime (no count change needed)
+    ag2 = A.Agent("n", source="fake", diag_level=1)
+    monkeypatch.setattr(diag, "device_count", lambda: 2)
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: {"gemm": {"pass": False, "detail": lost}})
+    ag2.probe_once()
+    assert ag2.hip_lost == lost

@@ -209,10 +209,10 @@ def test_fabric_suite_rows_and_verdict_with_a_stub_library(monkeypatch):
         def __init__(self, busbw, errors=0, fail_open=False):
             self.busbw, self.errors, self.fail_open, self.closed = busbw, errors, fail_open, 0
 
-        def fabric_open(self, arr, n):
+        def fabric_open(self, arr, n, timeout_ms):
             return None if self.fail_open else 1
 
-        def fabric_run(self, ctx, op, nbytes, iters, warmup, out):
+        def fabric_run(self, ctx, op, nbytes, iters, warmup, out, timeout_ms):
             out[0], out[1], out[2], out[3] = 1.0, self.busbw * 0.57, self.busbw, float(self.errors if op == 3 else 0)
             return 0
 

@@ -135,14 +135,11 @@ def test_mfma_gemm_variants_match_fp32_reference(dev, variant, m, n, k):
     a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
     bt = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
     c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
-    diag.set_gemm_variant(variant.split("-")[0])
-    diag.set_gemm_epilogue(variant.endswith("lds-epilogue"))
-    try:
+    before = diag.get_gemm_config()
+    with diag.gemm_config(variant=variant.split("-")[0], epilogue=variant.endswith("lds-epilogue")):
         diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-    finally:
-        diag.set_gemm_variant("auto")
-        diag.set_gemm_epilogue(False)
+    assert diag.get_gemm_config() == before  # restored, not reset to some other value
     ref = a.float() @ bt.float().t()
     assert not torch.isnan(c).any()
     rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
@@ -164,17 +161,12 @@ def test_v3_buffer_load_staging_matches(dev, m, n, k):
         if launch is diag.gemm_fp8_launch and k % 128:
             continue
         outs = []
-        diag.set_gemm_variant("v3")
-        try:
-            for buf in (False, True):
-                diag.set_gemm_buffer_loads(buf)
+        for buf in (False, True):
+            with diag.gemm_config(variant="v3", buffer_loads=buf):
                 c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
                 launch(x.data_ptr(), y.data_ptr(), c.data_ptr(), m, n, k, st)
                 torch.cuda.synchronize()
                 outs.append(c)
-        finally:
-            diag.set_gemm_buffer_loads(False)
-            diag.set_gemm_variant("auto")
         assert torch.equal(outs[0], outs[1])
         if launch is diag.gemm_fp8_launch:  # the MX MFMA's own accumulation error, normalised by sum|a*b|
             ref = x.double() @ y.double().t()
@@ -189,8 +181,9 @@ def test_v3_buffer_load_staging_matches(dev, m, n, k):
 
 def test_mfma_gemm_large_auto_uses_v3_and_matches(dev):
     """4096^3 in auto mode runs the staggered v3 kernel; compare every output with a bf16-input,
-    fp32-accumulate torch reference."""
+    fp32-accumulate torch reference.  Runs with the production knobs (what the agent launches)."""
     from k8s_gpu_node_checker_amd.ops import diag
+    assert diag.get_gemm_config() == {"variant": "auto", "epilogue": True, "buffer_loads": False}
     m = n = k = 4096
     g = torch.Generator(device=dev).manual_seed(4096)
     a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
@@ -454,17 +447,14 @@ def test_mfma_burn_rejects_inexact_iteration_counts():
 def test_mxfp8_gemm_matches_fp32_reference(dev, m, n, k, lds_epilogue):
     """MX-fp8 (E4M3) GEMM on the staggered v3 pipeline vs torch on the same fp8 values in fp32."""
     from k8s_gpu_node_checker_amd.ops import diag
-    diag.set_gemm_epilogue(lds_epilogue)
     g = torch.Generator(device=dev).manual_seed(m + 3 * n + 7 * k)
     a = torch.randn(m, k, device=dev, generator=g).to(torch.float8_e4m3fn)
     bt = torch.randn(n, k, device=dev, generator=g).to(torch.float8_e4m3fn)
     c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
-    try:
+    with diag.gemm_config(epilogue=lds_epilogue):
         diag.gemm_fp8_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k,
                              torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-    finally:
-        diag.set_gemm_epilogue(False)
     ref = a.double() @ bt.double().t()
     mag = a.double().abs() @ bt.double().abs().t()
     assert not torch.isnan(c).any()
@@ -563,3 +553,42 @@ def test_l2_bandwidth_per_xcd(dev):
     assert r["pass"] and r["errors"] == 0 and r["map"]["cus"] == info["cus"], r
     if info["cus"] == 256:
         assert len(r["map"]["xcds"]) == 8 and r["read_tbs"] > 25.0, r
+
+
+def test_gemm_knobs_are_thread_local_and_concurrent_threads_agree(dev):
+    """The agent runs one diagnostic thread per GPU: a knob set in one thread must not change what
+    another launches, and concurrent first launches of the 128 KiB-LDS v3 kernel (whose dynamic-LDS
+    attribute is set once per device) all succeed and match."""
+    import threading
+    from k8s_gpu_node_checker_amd.ops import diag
+    m = n = k = 4096
+    g = torch.Generator(device=dev).manual_seed(77)
+    a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
+    bt = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
+    ref = a.float() @ bt.float().t()
+    seen, errs, outs = [], [], []
+    with diag.gemm_config(variant="v1", epilogue=False):
+        def worker():
+            try:
+                torch.cuda.set_device(dev)
+                seen.append(diag.get_gemm_config())
+                s = torch.cuda.Stream(device=dev)
+                c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+                with torch.cuda.stream(s):
+                    diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, s.cuda_stream)
+                s.synchronize()
+                outs.append(c)
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+        ts = [threading.Thread(target=worker) for _ in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert diag.get_gemm_config()["variant"] == "v1"  # this thread's own setting survives
+    assert not errs, errs
+    assert seen == [{"variant": "auto", "epilogue": True, "buffer_loads": False}] * 4
+    for c in outs:
+        rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
+        assert rel < 1e-4 * (k / 512), rel
+        assert torch.equal(c, outs[0])

@@ -116,3 +116,150 @@ def test_bench_torchrun_four_ranks_gloo():
     assert {r["op"] for r in fab["rows"]} == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all"}
     assert all(r["correct"] for r in fab["rows"])
     json.dumps(d)
+
+
+# --- 8-GPU / 64-partition safety (VERDICT r2 "next round" #2) ----------------------------------------------
+
+def test_shared_host_link_is_serialized_so_halved_concurrent_rates_do_not_fail(node8):
+    """Two GPUs behind one switch uplink read the host at half rate each when measured together.  The agent
+    measures the host link one GPU at a time (ops/diag.SHARED_TESTS), so an 8-GPU level-2 cycle stays
+    healthy; without the lock the same node fails host_link on every GPU."""
+    lib, fab = node8(delay_s=0.05)
+    lib.link_shared, lib.link_delay_s = True, 0.05
+    ag = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8, diag_timeout=60)
+    rep = ag.probe_once()
+    assert lib.peak["host_link"] == 1 and sum(c == "host_link" for c in lib.calls) == 8
+    assert all(g["diag"]["host_link"]["pass"] and not g["diag"]["host_link"].get("degraded") for g in rep["gpus"])
+    assert rep["state"] == H.HEALTHY
+    assert lib.peak.get("gemm", 0) > 1  # the per-GPU compute tests still overlap
+
+
+def test_unserialized_host_link_would_fail_every_gpu(node8, monkeypatch):
+    """The control for the test above: with the shared-test lock disabled the halved rates fail."""
+    lib, fab = node8()
+    lib.link_shared, lib.link_delay_s = True, 0.2
+    monkeypatch.setattr(diag, "SHARED_TESTS", frozenset())
+    res = {}
+
+    def one(d):
+        res[d] = diag.host_link(d)
+    import threading
+    ts = [threading.Thread(target=one, args=(d,)) for d in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert lib.peak["host_link"] > 1
+    assert any(not r["pass"] for r in res.values())
+
+
+def test_cpx_node_runs_at_most_diag_parallel_threads_and_finishes_in_time(monkeypatch):
+    """64 CPX partitions (8 GPUs x 8): at most --diag-parallel diagnostic threads at once, every partition
+    diagnosed in one probe cycle, within the watchdog."""
+    import threading
+    n = 64
+    lib = FakeDiagLib(n=n, cus=32, mem_gib=36, delay_s=0.05)
+    monkeypatch.setattr(diag, "lib", lambda: lib)
+    rep64 = fixtures.mi355x_probe_report("cpx", gpus=8)
+    gpus = []
+    for i in range(n):
+        g = dict(rep64["gpus"][i // 8], index=i, bdf=f"0000:{0x05 + 0x10 * i:02x}:00.0", compute_partition="CPX",
+                 memory_partition="NPS1", cus=32)
+        gpus.append(g)
+    monkeypatch.setattr(amdsmi_probe, "probe", lambda node, src, fx: dict(rep64, gpus=[dict(g) for g in gpus]))
+    live, peak = [0], [0]
+    lock = threading.Lock()
+    real_run = diag.run
+
+    def run(level, d, **kw):
+        with lock:
+            live[0] += 1
+            peak[0] = max(peak[0], live[0])
+        try:
+            return real_run(level, d, **kw)
+        finally:
+            with lock:
+                live[0] -= 1
+    monkeypatch.setattr(diag, "run", run)
+    ag = A.Agent("cpx", source="fake", diag_level=1, diag_timeout=30, diag_parallel=8, expect_gpus=64)
+    t0 = time.monotonic()
+    rep = ag.probe_once()
+    wall = time.monotonic() - t0
+    assert peak[0] == 8, peak
+    assert all(g.get("diag") and "diag_skipped" not in g for g in rep["gpus"]), \
+        [g.get("diag_skipped") for g in rep["gpus"] if g.get("diag_skipped")]
+    assert len(set(c for c in lib.threads)) == 64
+    assert wall < 30 and rep["state"] in (H.HEALTHY, H.DEGRADED), (wall, rep["state"])
+    with pytest.raises(ValueError):
+        A.Agent("x", diag_parallel=0)
+    assert A.build_parser().parse_args(["--diag-parallel", "4"]).diag_parallel == 4
+    assert A.build_parser().parse_args([]).diag_parallel == A.DIAG_PARALLEL
+
+
+def test_hung_slots_leave_the_rest_waiting_not_running(monkeypatch):
+    """With every --diag-parallel slot held by a hung diagnostic the remaining GPUs wait (said per GPU);
+    nothing piles more threads onto a wedged device set."""
+    import threading
+    lib = FakeDiagLib(n=4)
+    monkeypatch.setattr(diag, "lib", lambda: lib)
+    monkeypatch.setattr(amdsmi_probe, "probe", lambda node, src, fx: fixtures.mi355x_probe_report(node, gpus=4))
+    release = threading.Event()
+    started = []
+
+    def run(level, d, **kw):
+        started.append(d)
+        release.wait(20)
+        return {"gemm": {"pass": True}}
+    monkeypatch.setattr(diag, "run", run)
+    ag = A.Agent("n4", source="fake", diag_level=1, diag_timeout=0.2, diag_parallel=2, diag_interval=0.0)
+    rep = ag.probe_once()
+    assert sorted(started) == [0, 1]
+    g = rep["gpus"]
+    assert g[0]["diag"]["watchdog"]["pass"] is False and g[1]["diag"]["watchdog"]["pass"] is False
+    assert g[2]["diag_skipped"].startswith("waiting for a diagnostic slot: 2 of 2 held by hung")
+    rep = ag.probe_once()
+    assert sorted(started) == [0, 1] and rep["gpus"][3]["diag_skipped"].startswith("waiting for a diagnostic slot")
+    release.set()
+    for r in list(ag._diag_threads.values()):
+        r.thread.join(5)
+    rep = ag.probe_once()
+    assert sorted(started) == [0, 1, 2, 3]
+
+
+def test_capped_power_scales_the_compute_references(node8):
+    """A GPU whose power cap an operator lowered to 60 % of the default computes at ~60 %: judged against
+    its cap it passes (the cap itself is the health model's warning), uncapped it would fail."""
+    node8.state["overrides"] = {"gpu3": {"power_cap_w": 840, "power_cap_default_w": 1400}}
+    lib, fab = node8(compute_rate={3: 0.62})
+    ag = A.Agent("n8", source="fake", diag_level=1, expect_gpus=8)
+    rep = ag.probe_once()
+    g3 = rep["gpus"][3]
+    assert g3["diag"]["gemm"]["pass"] and g3["diag"]["gemm"]["scale"]["compute"] == pytest.approx(0.6)
+    v = ag.evaluate(rep)
+    assert v.state == H.DEGRADED and any("power cap 840 W of 1400 W" in w for w in v.warnings)
+    assert g3["diag"]["hbm"]["pass"] and g3["diag"]["gemm"]["scale"]["memory"] == pytest.approx(1.0, abs=1e-3)
+    # the same GPU without the cap on record fails its compute tests
+    node8.state["overrides"] = {}
+    rep = A.Agent("n8", source="fake", diag_level=1, expect_gpus=8).probe_once()
+    assert rep["gpus"][3]["diag"]["gemm"]["pass"] is False and rep["state"] == H.UNHEALTHY
+    assert A.power_fraction({"power_cap_w": 1400, "power_cap_default_w": 1400}) == 1.0
+    assert A.power_fraction({"power_cap_w": 0, "power_cap_default_w": 1400}) is None
+    assert A.power_fraction({}) is None
+
+
+def test_hung_collective_is_aborted_and_reported_as_a_failed_rccl_row(node8):
+    """A collective that never completes: the fabric suite's own deadline (0.9 x the watchdog) aborts the
+    communicators (ncclCommAbort in fabric.hip) and the report names the hung collective."""
+    lib, fab = node8()
+    fab.hang_op = 0  # all_reduce never completes
+    ag = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8, diag_timeout=1.0)
+    t0 = time.monotonic()
+    rep = ag.probe_once()
+    assert time.monotonic() - t0 < 3
+    rccl = rep["fabric"]["rccl"]
+    assert rccl["pass"] is False and rccl["aborted"] is True and fab.aborts == 1 and fab.closed == 1
+    assert "all_reduce" in rccl["detail"] and "ncclCommAbort" in rccl["detail"]
+    assert 0 < fab.timeouts_ms[0] <= 900.0
+    assert "watchdog" not in rep["fabric"] and rep["state"] == H.UNHEALTHY
+    assert any(r.startswith("xGMI rccl failed (all_reduce") for r in ag.evaluate(rep).reasons)
+    assert ag._fabric_thread is None  # the suite returned: nothing left holding the GPUs
