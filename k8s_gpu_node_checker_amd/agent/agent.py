@@ -221,6 +221,57 @@ def node_event(node: str, verdict: Verdict, previous: Optional[str], namespace: 
             "firstTimestamp": ts, "lastTimestamp": ts, "count": 1}
 
 
+def token_node_name(token: Optional[str]) -> Optional[str]:
+    """The node a pod-bound ServiceAccount token was issued for (its ``kubernetes.io.node.name`` claim, the one
+    the API server exposes to admission as ``authentication.kubernetes.io/node-name``), None when the token has
+    none or is not a JWT.  Read without verifying the signature: it only tells the agent which node the API
+    server will let it write (deploy/agent-policy.yaml), so a mismatch with ``--node`` is caught at start-up."""
+    import base64
+    parts = (token or "").strip().split(".")
+    if len(parts) != 3:
+        return None
+    try:
+        claims = json.loads(base64.urlsafe_b64decode(parts[1] + "=" * (-len(parts[1]) % 4)))
+        name = ((claims.get("kubernetes.io") or {}).get("node") or {}).get("name")
+    except (ValueError, AttributeError, TypeError):
+        return None
+    return name if isinstance(name, str) and name else None
+
+
+class ForeignNodeError(RuntimeError):
+    """A write for a node other than the agent's own (``--node``): refused before it reaches the API server."""
+
+
+class _OwnNodeClient:
+    """The kube client as the agent may use it: every node-addressed call must name the agent's own node, and
+    Events must be about it.  Defense in depth under deploy/agent-policy.yaml, which enforces the same on the
+    API server side."""
+
+    _NODE_CALLS = ("get_node", "patch_node_condition", "patch_node_annotations", "patch_node_labels",
+                   "update_node_taints")
+
+    def __init__(self, client: Any, node: str):
+        self._client, self._node = client, node
+
+    def __getattr__(self, name: str) -> Any:
+        fn = getattr(self._client, name)
+        if name in self._NODE_CALLS:
+            def own(node: str, *a: Any, **kw: Any) -> Any:
+                if node != self._node:
+                    raise ForeignNodeError(f"refusing {name} on node {node!r}: this agent writes only {self._node!r}")
+                return fn(node, *a, **kw)
+            return own
+        if name == "create_event":
+            def event(namespace: str, ev: Dict[str, Any], *a: Any, **kw: Any) -> Any:
+                obj = ev.get("involvedObject") or {}
+                if obj.get("kind") != "Node" or obj.get("name") != self._node:
+                    raise ForeignNodeError(f"refusing an Event about {obj.get('kind')} {obj.get('name')!r}: this "
+                                           f"agent reports only on node {self._node!r}")
+                return fn(namespace, ev, *a, **kw)
+            return event
+        return fn
+
+
 class PublishError(RuntimeError):
     """Some of a publish's writes failed (message: which, and why); ``wrote`` is what did go out."""
 
@@ -686,12 +737,18 @@ class Agent:
         return cond
 
     def publish_annotation(self, client: Any, rep: Dict[str, Any]) -> None:
-        client.patch_node_annotations(self.node, self.annotation(rep))
+        _OwnNodeClient(client, self.node).patch_node_annotations(self.node, self.annotation(rep))
 
     def publish(self, client: Any, rep: Dict[str, Any], force: bool = False) -> Dict[str, bool]:
         """Full report as annotation when it changed (or every ``annotation_refresh`` s), verdict as the
         ``AMDGPUHealthy`` NodeCondition when it changed (or every ``heartbeat_interval`` s), and on a
         verdict change an Event and (``taint_unhealthy``) the taint.  Returns what was written."""
+        if rep.get("node") is not None and rep.get("node") != self.node:
+            # a report of another node (a misrouted or replayed one) must never become this node's verdict
+            raise ForeignNodeError(f"report is for node {rep.get('node')!r}; this agent publishes only for "
+                                   f"{self.node!r}")
+        if not isinstance(client, _OwnNodeClient):
+            client = _OwnNodeClient(client, self.node)
         digest = report_digest(rep)
         now = time.monotonic()
         wrote = {"annotation": False, "condition": False, "event": False, "taint": False, "labels": False}
@@ -1000,7 +1057,21 @@ def main(argv: Optional[List[str]] = None) -> int:
     if "annotation" in pubs:
         from ..kube.client import KubeClient
         from ..kube.config import load_kube_config
-        client = KubeClient(load_kube_config(args.kubeconfig), timeout=10.0)
+        conn = load_kube_config(args.kubeconfig)
+        tok = conn.token
+        if conn.token_file:
+            try:
+                with open(conn.token_file, encoding="utf-8") as f:
+                    tok = f.read()
+            except OSError:
+                pass
+        bound = token_node_name(tok)
+        if bound is not None and bound != args.node:
+            # deploy/agent-policy.yaml would refuse every write anyway; say why at start-up instead
+            print(f"--node {args.node!r} is not the node this pod's ServiceAccount token is bound to ({bound!r}): "
+                  "refusing to publish another node's status", file=sys.stderr, flush=True)
+            return 2
+        client = KubeClient(conn, timeout=10.0)
         try:  # the node's registered GPU count; refreshed from every condition PATCH response after this
             agent.observe_node(client.get_node(args.node))
         except Exception as e:

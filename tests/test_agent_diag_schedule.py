@@ -525,3 +525,54 @@ def test_one_gpu_failing_with_runtime_strings_is_that_gpus_failure(monkeypatch):
     monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: {"gemm": {"pass": False, "detail": lost}})
     ag2.probe_once()
     assert ag2.hip_lost == lost
+
+
+def test_publish_refuses_a_foreign_node(monkeypatch, mock_cluster):
+    """VERDICT r2 #4: the agent writes only the node it was started for, whatever report or call reaches it."""
+    from k8s_gpu_node_checker_amd.kube.client import KubeClient
+    from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+    World(monkeypatch)
+    srv = mock_cluster([fixtures.realistic_node("n", gpu_count=2), fixtures.realistic_node("other", gpu_count=2)])
+    with KubeClient(ClusterConnection(srv.url)) as kc:
+        ag = A.Agent("n", source="fake")
+        rep = ag.probe_once()
+        assert ag.publish(kc, rep)["condition"]
+        foreign = dict(rep, node="other")
+        with pytest.raises(A.ForeignNodeError, match="report is for node 'other'"):
+            ag.publish(kc, foreign)
+        guard = A._OwnNodeClient(kc, "n")
+        with pytest.raises(A.ForeignNodeError, match="refusing patch_node_condition on node 'other'"):
+            guard.patch_node_condition("other", {"type": "AMDGPUHealthy", "status": "True"})
+        with pytest.raises(A.ForeignNodeError, match="refusing an Event about Node 'other'"):
+            guard.create_event("default", {"involvedObject": {"kind": "Node", "name": "other"}})
+        other = kc.get_node("other")
+    assert not any(c["type"] == "AMDGPUHealthy" for c in other["status"]["conditions"])
+
+
+def test_token_node_claim_is_read_and_a_mismatch_stops_the_agent(monkeypatch, tmp_path):
+    import base64
+    import json as _json
+
+    def jwt(claims):
+        b = lambda d: base64.urlsafe_b64encode(_json.dumps(d).encode()).rstrip(b"=").decode()  # noqa: E731
+        return f"{b({'alg': 'RS256'})}.{b(claims)}.sig"
+    tok = jwt({"sub": "system:serviceaccount:gpu-health:mi355x-node-agent",
+               "kubernetes.io": {"namespace": "gpu-health", "node": {"name": "gpu-7", "uid": "u"}}})
+    assert A.token_node_name(tok) == "gpu-7"
+    assert A.token_node_name(jwt({"sub": "x"})) is None and A.token_node_name("opaque") is None
+    assert A.token_node_name(None) is None
+    kc = tmp_path / "kc"
+    (tmp_path / "token").write_text(tok)
+    kc.write_text(f"""clusters:
+- cluster: {{server: "http://127.0.0.1:1"}}
+  name: c
+contexts:
+- context: {{cluster: c, user: u}}
+  name: x
+current-context: x
+users:
+- name: u
+  user: {{tokenFile: {tmp_path / 'token'}}}
+""")
+    assert A.main(["--node", "gpu-3", "--kubeconfig", str(kc), "--once", "--source", "fixture",
+                   "--fixture", "/nonexistent"]) == 2

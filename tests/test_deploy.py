@@ -56,8 +56,9 @@ def test_manifests_are_self_consistent():
                for d in docs if d["kind"] != "Kustomization"}
     namespaces = {name for kind, _, name in defined if kind == "Namespace"}
     for d in docs:
-        if d["kind"] in ("Kustomization", "Namespace") or d["kind"].startswith("Cluster"):
-            continue
+        if d["kind"] in ("Kustomization", "Namespace", "ValidatingAdmissionPolicy",
+                         "ValidatingAdmissionPolicyBinding") or d["kind"].startswith("Cluster"):
+            continue  # cluster-scoped
         ns = d["metadata"]["namespace"]
         assert ns in namespaces, (d["kind"], d["metadata"]["name"])
         spec = d.get("spec") or {}
@@ -221,3 +222,125 @@ def test_agent_port_network_policy_selects_the_agent_and_its_port():
     assert {p["port"] for r in pol["spec"]["ingress"] for p in r["ports"]} <= ports
     kust = yaml.safe_load(open(os.path.join(REPO, "deploy", "monitoring", "kustomization.yaml")))
     assert "networkpolicy.yaml" in kust["resources"]
+
+
+# --- the agent's write authority is scoped to its own Node (deploy/agent-policy.yaml) ------------------------
+
+import copy  # noqa: E402
+
+from k8s_gpu_node_checker_amd.models import health as H  # noqa: E402
+from k8s_gpu_node_checker_amd.models.node import HEALTH_ANNOTATION  # noqa: E402
+from k8s_gpu_node_checker_amd.testing import cel, fixtures  # noqa: E402
+
+AGENT_USER = "system:serviceaccount:gpu-health:mi355x-node-agent"
+
+
+def _policy():
+    docs = [d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "agent-policy.yaml"))) if d]
+    pol = next(d for d in docs if d["kind"] == "ValidatingAdmissionPolicy")
+    binding = next(d for d in docs if d["kind"] == "ValidatingAdmissionPolicyBinding")
+    return pol, binding
+
+
+def _req(resource="nodes", sub="", user=AGENT_USER, node_claim="gpu-a", op="UPDATE"):
+    extra = {} if node_claim is None else {"authentication.kubernetes.io/node-name": [node_claim]}
+    return {"operation": op, "resource": {"group": "", "version": "v1", "resource": resource}, "subResource": sub,
+            "userInfo": {"username": user, "extra": extra}}
+
+
+def _node(name="gpu-a"):
+    return fixtures.realistic_node(name, gpu_count=8)
+
+
+def _admit(req, new, old):
+    pol, _ = _policy()
+    return cel.admit(pol, req, new, old)
+
+
+def test_policy_is_bound_to_the_agent_service_account_and_names_the_node_claim():
+    pol, binding = _policy()
+    assert binding["spec"]["policyName"] == pol["metadata"]["name"] and binding["spec"]["validationActions"] == ["Deny"]
+    assert pol["spec"]["failurePolicy"] == "Fail"
+    mc = " ".join(m["expression"] for m in pol["spec"]["matchConditions"])
+    assert AGENT_USER in mc
+    sa = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "rbac.yaml")))
+              if d and d["kind"] == "ServiceAccount" and d["metadata"]["name"] == "mi355x-node-agent")
+    assert AGENT_USER == f"system:serviceaccount:{sa['metadata']['namespace']}:{sa['metadata']['name']}"
+    assert "authentication.kubernetes.io/node-name" in yaml.safe_dump(pol)
+    rules = {(r, o) for rr in pol["spec"]["matchConstraints"]["resourceRules"] for r in rr["resources"]
+             for o in rr["operations"]}
+    assert {("nodes", "UPDATE"), ("nodes/status", "UPDATE"), ("events", "CREATE")} <= rules
+    kust = yaml.safe_load(open(os.path.join(REPO, "deploy", "kustomization.yaml")))
+    assert "agent-policy.yaml" in kust["resources"]
+
+
+def test_policy_admits_every_write_the_agent_makes_to_its_own_node():
+    old = _node()
+    ann = copy.deepcopy(old)
+    ann["metadata"]["annotations"][HEALTH_ANNOTATION] = '{"schema":"mi355x-health/v1"}'
+    assert _admit(_req(), ann, old) == (True, "")
+    lab = copy.deepcopy(old)
+    lab["metadata"]["labels"].update({"amd.com/mi355x-health": "healthy", "amd.com/gpu.count": "8"})
+    del lab["metadata"]["labels"]["amd.com/gpu.family"]  # an amd.com/ label the agent removes
+    assert _admit(_req(), lab, old) == (True, "")
+    tainted = copy.deepcopy(old)
+    tainted["spec"]["taints"] = list(old["spec"].get("taints") or []) + [dict(H.UNHEALTHY_TAINT)]
+    assert _admit(_req(), tainted, old) == (True, "")
+    assert _admit(_req(), old, tainted) == (True, "")  # and removes it again
+    st = copy.deepcopy(old)
+    st["status"]["conditions"] = old["status"]["conditions"] + [
+        {"type": H.HEALTH_CONDITION, "status": "True", "reason": "MI355XHealthy", "message": "8/8"}]
+    assert _admit(_req(sub="status"), st, old) == (True, "")
+    ev = {"involvedObject": {"kind": "Node", "name": "gpu-a"}, "reason": "MI355XUnhealthy"}
+    assert _admit(_req(resource="events", op="CREATE"), ev, None) == (True, "")
+
+
+def test_policy_refuses_writes_to_other_nodes_and_other_fields():
+    old = _node()
+    ann = copy.deepcopy(old)
+    ann["metadata"]["annotations"][HEALTH_ANNOTATION] = "{}"
+    # a compromised agent on gpu-b writing gpu-a's verdict
+    ok, msg = _admit(_req(node_claim="gpu-b"), ann, old)
+    assert ok is False and msg == "the MI355X node agent on gpu-b may only write its own Node, not gpu-a"
+    ok, msg = _admit(_req(node_claim=None), ann, old)  # a token without the claim: fail closed
+    assert ok is False and "node-name claim" in msg
+    bad = copy.deepcopy(old)
+    bad["metadata"]["labels"]["pool"] = "inference"
+    assert _admit(_req(), bad, old) == (False, "the MI355X node agent may only change amd.com/ labels")
+    bad = copy.deepcopy(old)
+    del bad["metadata"]["labels"]["pool"]
+    assert _admit(_req(), bad, old)[0] is False
+    bad = copy.deepcopy(old)
+    bad["metadata"]["annotations"]["node.alpha.kubernetes.io/ttl"] = "30"
+    assert _admit(_req(), bad, old) == (False, "the MI355X node agent may only change the amd.com/mi355x-health "
+                                               "annotation")
+    bad = copy.deepcopy(old)
+    bad["spec"]["taints"] = [{"key": "dedicated", "value": "x", "effect": "NoExecute"}]
+    assert _admit(_req(), bad, old)[1] == "the MI355X node agent may only add or remove the amd.com/gpu-unhealthy taint"
+    bad = copy.deepcopy(old)
+    bad["spec"]["unschedulable"] = True
+    assert _admit(_req(), bad, old)[1] == "the MI355X node agent may not cordon, uncordon or re-address a Node"
+    bad = copy.deepcopy(old)
+    bad["status"]["conditions"][0] = dict(bad["status"]["conditions"][0], status="Unknown")  # the kubelet's Ready
+    assert _admit(_req(sub="status"), bad, old)[0] is False
+    bad = copy.deepcopy(old)
+    bad["status"]["capacity"]["amd.com/gpu"] = "0"
+    assert _admit(_req(sub="status"), bad, old)[0] is False
+    ev = {"involvedObject": {"kind": "Node", "name": "gpu-z"}, "reason": "MI355XHealthy"}
+    assert _admit(_req(resource="events", op="CREATE"), ev, None) == (
+        False, "the MI355X node agent may only post Events about its own Node")
+    # other users are not this policy's business (the kubelet, an operator)
+    assert _admit(_req(user="system:node:gpu-a"), bad, old) == (None, "")
+
+
+def test_cel_subset_semantics():
+    e = cel.eval_expr
+    assert e("[1, 2, 3].filter(x, x > 1) == [2, 3]", {}) is True
+    assert e("{'a': 1, 'b': 2}.all(k, k.startsWith('a') || k == 'b')", {}) is True
+    assert e("has(o.a) && o.a.b == 1 ? 'y' : 'n'", {"o": {"a": {"b": 1}}}) == "y"
+    assert e("has(o.x) ? 1 : 2", {"o": {}}) == 2
+    assert e("o.x == 1 || true", {"o": {}}) is True  # commutative with errors
+    with pytest.raises(cel.CelError):
+        e("o.x == 1 && true", {"o": {}})
+    assert e("'k' in m && size(m['k']) == 2", {"m": {"k": ["a", "b"]}}) is True
+    assert e("true == 1", {}) is False

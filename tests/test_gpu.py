@@ -8,6 +8,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -314,6 +315,23 @@ def test_rccl_in_process_fabric_suite(dev):
     assert [(r["op"], r["bytes"]) for r in res["rows"]] == [(op, b) for op in fabric.OPS for b in (1 << 20, 64 << 20)]
     assert all(r["errors"] == 0 and r["algbw_gbps"] > 0 for r in res["rows"]), res["rows"]
     assert res["rccl"] != "unknown"
+
+
+def test_rccl_suite_with_a_deadline_and_an_abort(dev):
+    """Non-blocking communicators: the suite under a generous deadline passes exactly as without one; a
+    deadline too short for communicator setup aborts (ncclCommAbort) and comes back as a failed, aborted
+    result instead of blocking; the process can build a fresh communicator afterwards."""
+    from k8s_gpu_node_checker_amd.ops import diag, fabric
+    n = diag.device_count()
+    ok = fabric.collective_suite(list(range(n)), sizes=[1 << 20], iters=2, warmup=1, timeout_s=60)
+    assert ok["pass"] and not ok.get("aborted"), ok
+    t0 = time.monotonic()
+    bad = fabric.collective_suite(list(range(n)), sizes=[64 << 20], iters=50, warmup=1, timeout_s=1e-6)
+    assert time.monotonic() - t0 < 30
+    print(json.dumps({k: bad.get(k) for k in ("pass", "aborted", "detail")}))
+    assert bad["pass"] is False and bad["aborted"] is True and "ncclCommAbort" in bad["detail"], bad
+    again = fabric.collective_suite(list(range(n)), sizes=[1 << 20], iters=2, warmup=1, timeout_s=60)
+    assert again["pass"], again
 
 
 def test_fabric_cli_stdout_is_pure_json(repo):
