@@ -54,6 +54,7 @@ class CheckOptions:
         self.probe_endpoint: Optional[str] = None
         self.probe_concurrency = 64
         self.probe_timeout = 2.0
+        self.probe_ca: Optional[str] = None
         self.health_reeval = False
         self.require_schedulable = False
         self.trace = False
@@ -193,7 +194,8 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
         reports: List[Optional[Dict[str, Any]]] = [None] * len(scan.gpu_nodes)
         if opts.probe_endpoint:
             from .parallel.fanout import fetch_probe_reports
-            reports = fetch_probe_reports(scan, opts.probe_endpoint, opts.probe_concurrency, opts.probe_timeout)
+            reports = fetch_probe_reports(scan, opts.probe_endpoint, opts.probe_concurrency, opts.probe_timeout,
+                                          ca_file=opts.probe_ca)
         verdicts: List[Optional[H.Verdict]] = []
         changed = False
         unknown_ok = opts.probe_unknown == "allow"
@@ -220,7 +222,12 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
             else:
                 if rep is None:
                     rep = ex.report()
-                if rep is not None or policy == "require":
+                other = rep.get("node") if isinstance(rep, dict) else None
+                if other is not None and other != node["name"]:
+                    # a report names the node it was taken on: one fetched from a reassigned or stale IP (or an
+                    # annotation copied between nodes) says nothing about this node
+                    v = H.Verdict(H.UNKNOWN, [f"report is for node {other}"])
+                elif rep is not None or policy == "require":
                     v = H.evaluate_report(rep, expected, exp, now)
             if v is None:
                 verdicts.append(None)

@@ -57,6 +57,7 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
     ("x", "--probe-endpoint", {"help": "노드별 프로브 URL 템플릿, 예: http://{ip}:9464/probe"}),
     ("x", "--probe-concurrency", {"type": int, "default": 64, "help": "프로브 fan-out 동시성 (기본: 64)"}),
     ("x", "--probe-timeout", {"type": float, "default": 2.0, "help": "노드별 프로브 타임아웃(초) (기본: 2)"}),
+    ("x", "--probe-ca", {"help": "https 프로브 엔드포인트를 검증할 CA 파일 (기본: 시스템 CA)"}),
     ("x", "--require-schedulable", {"action": "store_true",
                                     "help": "cordon(spec.unschedulable) 되었거나 amd.com/gpu-unhealthy taint 가 있는 "
                                             "GPU 노드는 Ready 로 세지 않음"}),

@@ -380,3 +380,200 @@ def test_oversized_json_annotation_goes_out_gzip_encoded(capsys):
     assert v.startswith(H.GZIP_PREFIX) and len(v) < A.ANNOTATION_JSON_MAX
     assert H.parse_annotation(v)["gpus"][63]["diag"]["t7"]["pass"] is True
     assert "writing it gzip-encoded" in capsys.readouterr().err
+
+
+# --- reports bound to their node; a hardened fan-out (VERDICT r2 "next round" #5) -----------------------------
+
+def test_swapped_ips_yield_unknown_not_the_other_nodes_verdict(run_cli, mock_cluster, tmp_path, fixture_report):
+    """Node a's InternalIP now points at node b's agent and vice versa (a reassigned IP): each report names
+    its node, so neither verdict is taken for the other node -- both are unknown, and --mi355x exits 3."""
+    a = A.Agent("a", source="fixture", fixture=fixture_report)
+    a.probe_once()
+    b = A.Agent("b", source="fixture", fixture=fixture_report)
+    b.probe_once()
+    srv_a = A.serve(a, "127.0.0.1", 0)
+    port = srv_a.server_address[1]
+    srv_b = A.serve(b, "127.0.0.2", port)
+    try:
+        nodes = []
+        for i, name in enumerate(["a", "b"]):
+            n = fixtures.realistic_node(name, index=i, gpu_count=1)
+            n["status"]["addresses"][0]["address"] = f"127.0.0.{2 - i}"  # swapped
+            nodes.append(n)
+        srv = mock_cluster(nodes)
+        kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+        p = run_cli(["--kubeconfig", kc, "--json-extended", "--mi355x", "--xgmi-links", "0",
+                     "--probe-endpoint", f"http://{{ip}}:{port}/probe", "--probe-timeout", "2"])
+        doc = json.loads(p.stdout)
+        hs = [n["health"] for n in doc["mi355x"]["nodes"]]
+        assert [h["state"] for h in hs] == ["unknown", "unknown"], hs
+        assert hs[0]["reasons"] == ["report is for node b"] and hs[1]["reasons"] == ["report is for node a"]
+        assert p.returncode == 3
+        # the right IPs: both healthy
+        for i, n in enumerate(nodes):
+            n["status"]["addresses"][0]["address"] = f"127.0.0.{i + 1}"
+        srv2 = mock_cluster(nodes)
+        kc2 = write_kubeconfig(str(tmp_path / "kc2"), srv2.url)
+        p = run_cli(["--kubeconfig", kc2, "--json-extended", "--mi355x", "--xgmi-links", "0",
+                     "--probe-endpoint", f"http://{{ip}}:{port}/probe", "--probe-timeout", "2"])
+        assert [n["health"]["state"] for n in json.loads(p.stdout)["mi355x"]["nodes"]] == ["healthy", "healthy"]
+        assert p.returncode == 0
+    finally:
+        srv_a.shutdown()
+        srv_b.shutdown()
+
+
+def test_annotation_copied_from_another_node_is_unknown(mock_cluster, tmp_path, fixture_report):
+    from k8s_gpu_node_checker_amd.checker import CheckOptions, run_check
+    from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+    ag = A.Agent("src-node", source="fixture", fixture=fixture_report)
+    rep = ag.probe_once()
+    n = fixtures.realistic_node("dst-node", gpu_count=1, annotations=ag.annotation(rep))
+    srv = mock_cluster([n])
+    o = CheckOptions()
+    o.health_reeval, o.xgmi_links = True, 0
+    res = run_check(ClusterConnection(srv.url), o)
+    assert res.verdicts[0].state == "unknown" and res.verdicts[0].reasons == ["report is for node src-node"]
+
+
+def _raw_server(handler):
+    """A TCP server whose connections are handled by ``handler(conn)`` on a thread (raw HTTP control)."""
+    import socket
+    import threading
+    ls = socket.socket()
+    ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    ls.bind(("127.0.0.1", 0))
+    ls.listen(16)
+    stop = threading.Event()
+
+    def loop():
+        ls.settimeout(0.2)
+        while not stop.is_set():
+            try:
+                c, _ = ls.accept()
+            except OSError:
+                continue
+            threading.Thread(target=handler, args=(c, stop), daemon=True).start()
+    threading.Thread(target=loop, daemon=True).start()
+    return ls, stop
+
+
+def test_endless_body_fails_within_the_timeout_with_bounded_memory():
+    """An endpoint that streams forever without Content-Length: the reader stops at MAX_BODY (not at the
+    timeout, with everything buffered), and the node gets an error report."""
+    import asyncio
+    import time
+    from k8s_gpu_node_checker_amd.parallel import fanout
+
+    sent = {"bytes": 0}
+
+    def endless(c, stop):
+        c.recv(65536)
+        c.sendall(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\n\r\n")
+        chunk = b"[" * 65536
+        try:
+            while not stop.is_set():
+                c.sendall(chunk)
+                sent["bytes"] += len(chunk)
+        except OSError:
+            pass
+        c.close()
+    ls, stop = _raw_server(endless)
+    try:
+        url = f"http://127.0.0.1:{ls.getsockname()[1]}/probe"
+        t = time.time()
+        out = asyncio.run(fanout.fetch_all([{"name": "x", "url": url}], timeout=5.0))
+        assert time.time() - t < 5.0
+        assert out[0]["error"].startswith("probe response too large: body exceeds 1048576 bytes"), out[0]
+        # a Content-Length over the cap is refused before any body is read
+        def big(c, stop):
+            c.recv(65536)
+            c.sendall(b"HTTP/1.1 200 OK\r\nContent-Length: 999999999\r\n\r\n{")
+            stop.wait(5)
+            c.close()
+        ls2, stop2 = _raw_server(big)
+        try:
+            out = asyncio.run(fanout.fetch_all([{"name": "y", "url": f"http://127.0.0.1:{ls2.getsockname()[1]}/"}],
+                                               timeout=5.0))
+            assert out[0]["error"] == "probe response too large: body of 999999999 bytes exceeds 1048576"
+        finally:
+            stop2.set()
+            ls2.close()
+    finally:
+        stop.set()
+        ls.close()
+
+
+def test_chunked_body_is_decoded():
+    import asyncio
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    doc = json.dumps({"schema": "mi355x-health/v1", "node": "x", "gpus": []}).encode()
+
+    def chunked(c, stop):
+        c.recv(65536)
+        parts = [doc[:7], doc[7:20], doc[20:]]
+        body = b"".join(b"%x;ext=1\r\n%s\r\n" % (len(p), p) for p in parts) + b"0\r\nX-Trailer: 1\r\n\r\n"
+        c.sendall(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n" + body)
+        c.close()
+    ls, stop = _raw_server(chunked)
+    try:
+        out = asyncio.run(fanout.fetch_all([{"name": "x", "url": f"http://127.0.0.1:{ls.getsockname()[1]}/p"}]))
+        assert out[0] == json.loads(doc)
+    finally:
+        stop.set()
+        ls.close()
+
+
+def test_fetch_probe_reports_inside_a_running_event_loop(fixture_report):
+    """An async caller (a notebook, an embedding service) can use the blocking entry point."""
+    import asyncio
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    ag = A.Agent("a", source="fixture", fixture=fixture_report)
+    ag.probe_once()
+    srv = A.serve(ag, "127.0.0.1", 0)
+
+    class Scan:
+        gpu_nodes = [{"name": "a"}]
+        extras = [type("E", (), {"internal_ip": "127.0.0.1"})()]
+    try:
+        async def main():
+            return fanout.fetch_probe_reports(Scan(), f"http://{{ip}}:{srv.server_address[1]}/probe")
+        out = asyncio.run(main())
+        assert out[0]["node"] == "a" and out[0]["gpus"]
+    finally:
+        srv.shutdown()
+
+
+def test_https_probe_endpoint_verified_with_probe_ca(certs, fixture_report):
+    import asyncio
+    import ssl
+    import threading
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    crt, key = certs
+    body = json.dumps({"schema": "mi355x-health/v1", "node": "t", "gpus": []}).encode()
+
+    class Hnd(BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+    s = ThreadingHTTPServer(("127.0.0.1", 0), Hnd)
+    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+    ctx.load_cert_chain(crt, key)
+    s.socket = ctx.wrap_socket(s.socket, server_side=True)
+    threading.Thread(target=s.serve_forever, daemon=True).start()
+    try:
+        url = f"https://127.0.0.1:{s.server_address[1]}/probe"
+        out = asyncio.run(fanout.fetch_all([{"name": "t", "url": url}], timeout=5, retries=0))
+        assert "CERTIFICATE_VERIFY_FAILED" in out[0]["error"] or "certificate verify failed" in out[0]["error"]
+        out = asyncio.run(fanout.fetch_all([{"name": "t", "url": url}], timeout=5, ca_file=crt))
+        assert out[0] == json.loads(body)
+    finally:
+        s.shutdown()
+    from k8s_gpu_node_checker_amd import cli
+    assert cli.parse_args(["--probe-ca", "/etc/ca.pem"]).probe_ca == "/etc/ca.pem"
