@@ -37,6 +37,9 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
                                         "help": "5xx/429 재시도 정책: backoff(지수 백오프, 기본) | reference(즉시 재시도)"}),
     ("slack*", "--slack-on-change", {"action": "store_true",
                                      "help": "--state-file 과 함께: 상태가 바뀌었을 때만 전송 (복구 알림 포함)"}),
+    ("slack*", "--slack-on-node-change", {"action": "store_true",
+                                          "help": "--slack-on-change 포함: --slack-only-on-error 여도 Ready 가 아닌 "
+                                                  "GPU 노드 집합이 바뀌면 전송 (노드 하나의 장애/복구)"}),
     ("x", "--context", {"help": "kubeconfig context (기본: current-context)"}),
     ("x", "--in-cluster", {"action": "store_true", "help": "Pod ServiceAccount 로 접속"}),
     ("x", "--kube-timeout", {"type": float, "default": 30.0, "help": "kube-apiserver 요청 타임아웃(초) (기본: 30)"}),
@@ -162,6 +165,8 @@ def parse_args(argv: Optional[List[str]] = None) -> Any:
         args.require_schedulable = True
     if args.json_extended:
         args.json = True
+    if args.slack_on_node_change:
+        args.slack_on_change = True
     return args
 
 
@@ -187,7 +192,7 @@ def _run_once(args: Any) -> int:
             from .utils import statefile
             prev = statefile.load(args.state_file)
             if args.slack_on_change:
-                opts.slack_webhook = statefile.gate_webhook(prev, opts, cluster)
+                opts.slack_webhook = statefile.gate_webhook(prev, opts, cluster, args.slack_on_node_change)
         result = check_and_report(cluster, opts)
         if args.state_file:
             statefile.save(args.state_file, result, prev)
@@ -259,7 +264,8 @@ def _watch_events(args: Any) -> int:
         prev = statefile.load(args.state_file) if args.state_file else None
         memo = {"prev": prev}
         only = opts.slack_only_on_error
-        opts.slack_gate = lambda result: statefile.should_notify(memo["prev"], result, only)
+        opts.slack_gate = lambda result: statefile.should_notify(memo["prev"], result, only,
+                                                                 args.slack_on_node_change)
         opts.slack_only_on_error = False  # the gate decides (a recovery must be able to send)
 
         def evaluate(scan):
@@ -273,7 +279,7 @@ def _watch_events(args: Any) -> int:
         def report(result) -> None:
             emit_report(result, opts)
             memo["prev"] = {"fingerprint": statefile.fingerprint(result), "exit_code": result.exit_code,
-                            "slack_pending": result.slack_sent is False}
+                            "slack_pending": result.slack_sent is False, "not_ready": statefile.not_ready(result)}
             if args.state_file:
                 statefile.save(args.state_file, result, prev)
             if args.prometheus_textfile:

@@ -7,6 +7,10 @@ checker remembers the previous outcome and only notifies when it changes:
 * a different exit code or a different set of (node, ready) pairs -> send;
 * with ``--slack-only-on-error``: send on a change *into* an error state, and
   once more on the recovery back to exit 0;
+* with ``--slack-only-on-error --slack-on-node-change``: also send when the set of
+  not-Ready GPU nodes changes while the exit code stays 0 (1 of 8 MI355X nodes turning
+  unhealthy, and its recovery) -- the reference's "zero Ready nodes" rule
+  (``check-gpu-node.py:154-155``) alone never reports a single node;
 * a notification that was due but not delivered (the webhook failed on every
   attempt) stays due: the next run sends it, so an alert is not lost to a
   Slack outage.
@@ -50,7 +54,7 @@ def save(path: str, result: Any, prev: Optional[Dict[str, Any]] = None) -> None:
         "fingerprint": fingerprint(result),
         "total_nodes": len(result.gpu_nodes),
         "ready_nodes": len(result.ready_gpu_nodes),
-        "not_ready": [n["name"] for n in result.gpu_nodes if not n["ready"]],
+        "not_ready": not_ready(result),
         "slack_sent": result.slack_sent,
         # sent and failed (None: nothing was due): the next run's gate sends again
         "slack_pending": result.slack_sent is False,
@@ -64,7 +68,12 @@ def save(path: str, result: Any, prev: Optional[Dict[str, Any]] = None) -> None:
     os.replace(tmp, path)
 
 
-def should_notify(prev: Optional[Dict[str, Any]], result: Any, only_on_error: bool) -> bool:
+def not_ready(result: Any) -> list:
+    return sorted(n["name"] for n in result.gpu_nodes if not n["ready"])
+
+
+def should_notify(prev: Optional[Dict[str, Any]], result: Any, only_on_error: bool,
+                  on_node_change: bool = False) -> bool:
     fp = fingerprint(result)
     if prev is not None and prev.get("slack_pending"):
         return True  # the last notification never arrived
@@ -74,15 +83,20 @@ def should_notify(prev: Optional[Dict[str, Any]], result: Any, only_on_error: bo
         return True
     if result.exit_code != 0:
         return True
-    return prev is not None and prev.get("exit_code", 0) != 0  # recovery
+    if prev is not None and prev.get("exit_code", 0) != 0:
+        return True  # recovery
+    if on_node_change:
+        before = sorted(prev.get("not_ready") or []) if prev is not None else []
+        return not_ready(result) != before  # a node went down (or came back) while others stay Ready
+    return False
 
 
-def gate_webhook(prev: Optional[Dict[str, Any]], opts: Any, cluster: Any) -> Optional[str]:
+def gate_webhook(prev: Optional[Dict[str, Any]], opts: Any, cluster: Any, on_node_change: bool = False) -> Optional[str]:
     """Install a de-dup gate on ``opts``; returns the (unchanged) webhook flag value."""
     only = opts.slack_only_on_error
 
     def gate(result: Any) -> bool:
-        return should_notify(prev, result, only)
+        return should_notify(prev, result, only, on_node_change)
 
     opts.slack_gate = gate
     if only:

@@ -18,7 +18,8 @@ def test_dotenv_parsing(tmp_path, monkeypatch):
     assert vals["C"] == "two\nlines-dflt"
     assert vals["NOVAL"] is None
     for k in ("SLACK_WEBHOOK_URL", "A", "B", "C"):
-        monkeypatch.delenv(k, raising=False)
+        monkeypatch.setenv(k, "")  # recorded, so what load_dotenv sets is undone after the test
+        monkeypatch.delenv(k)
     assert dotenv.load_dotenv(str(p))
     assert os.environ["EXISTING"] == "env"  # real env wins (override=False)
     assert os.environ["SLACK_WEBHOOK_URL"] == "https://hooks/x"
@@ -145,3 +146,63 @@ def test_cli_slack_on_change_keeps_an_undelivered_alert_due(run_cli, mock_cluste
         assert run_cli(base + ["--slack-webhook", sink.url("200")]).returncode == 3
     assert len(sink.requests) == 2  # delivered on the second run, not repeated on the third
     assert statefile.load(str(tmp_path / "st.json"))["slack_pending"] is False
+
+
+def _cronjob_command():
+    import os
+    import yaml
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cj = yaml.safe_load(open(os.path.join(repo, "deploy", "cronjob.yaml")))
+    return cj["spec"]["jobTemplate"]["spec"]["template"]["spec"]["containers"][0]["command"]
+
+
+def test_shipped_cronjob_alerts_once_per_single_node_failure_and_recovery(run_cli, mock_cluster, sink, tmp_path):
+    """with the shipped CronJob's flags, 1 of 8 MI355X nodes turning unhealthy (exit code stays
+    0: seven are Ready) is one Slack POST, and its recovery one more; unchanged runs send nothing."""
+    from k8s_gpu_node_checker_amd.testing import fixtures
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+    cmd = _cronjob_command()
+    assert cmd[0] == "check-gpu-node" and "--slack-on-node-change" in cmd and "--slack-only-on-error" in cmd
+    healthy = fixtures.cluster(8, "amd", with_health=True)
+    sick = fixtures.cluster(8, "amd", with_health=True)
+    rep = fixtures.mi355x_probe_report(sick[3]["metadata"]["name"], 8, gpu2={"ecc_uncorrectable": 4})
+    sick[3]["metadata"]["annotations"].update(fixtures.health_annotation(rep))
+    sick[3]["status"]["conditions"] = [c for c in sick[3]["status"]["conditions"] if c["type"] != "AMDGPUHealthy"] + \
+        [fixtures.health_condition(rep, 8)]
+    srv = mock_cluster(healthy)
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    args = [a for a in cmd[1:] if a != "--in-cluster"]
+    args[args.index("/state/last.json")] = str(tmp_path / "last.json")
+    args += ["--kubeconfig", kc]
+    env = {"SLACK_WEBHOOK_URL": sink.url("200")}
+    for _ in range(2):
+        assert run_cli(args, env=env).returncode == 0
+    assert len(sink.requests) == 0  # all healthy: nothing to say
+    srv.state.set_nodes(sick)
+    for _ in range(3):
+        p = run_cli(args, env=env)
+        assert p.returncode == 0, p.stderr  # 7 of 8 Ready
+    assert len(sink.requests) == 1
+    text = sink.payloads()[0]["text"]
+    assert f"`{sick[3]['metadata']['name']}`: ❌ Not Ready" in text
+    srv.state.set_nodes(healthy)
+    for _ in range(2):
+        assert run_cli(args, env=env).returncode == 0
+    assert len(sink.requests) == 2  # the recovery, once
+    # without --slack-on-node-change (the round-2 CronJob) the same failure never reaches Slack
+    base = [a for a in args if a != "--slack-on-node-change"]
+    base[base.index(str(tmp_path / "last.json"))] = str(tmp_path / "other.json")
+    srv.state.set_nodes(sick)
+    assert run_cli(base, env=env).returncode == 0
+    assert len(sink.requests) == 2
+
+
+def test_should_notify_on_node_change_rules():
+    bad = R(0, [node("a", True), node("b", False)])
+    good = R(0, [node("a", True), node("b", True)])
+    assert statefile.should_notify(None, bad, True, on_node_change=True)
+    assert not statefile.should_notify(None, good, True, on_node_change=True)
+    assert not statefile.should_notify(None, bad, True)  # the reference rule: ready > 0 -> quiet
+    prev = {"fingerprint": statefile.fingerprint(bad), "exit_code": 0, "not_ready": ["b"]}
+    assert not statefile.should_notify(prev, bad, True, on_node_change=True)
+    assert statefile.should_notify(prev, good, True, on_node_change=True)
