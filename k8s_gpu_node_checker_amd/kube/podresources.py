@@ -15,8 +15,21 @@ format here (fields from ``k8s.io/kubelet/pkg/apis/podresources/v1/api.proto``):
 
     ListPodResourcesResponse { repeated PodResources pod_resources = 1; }
     PodResources             { string name = 1; string namespace = 2; repeated ContainerResources containers = 3; }
-    ContainerResources       { string name = 1; repeated ContainerDevices devices = 2; ... }
+    ContainerResources       { string name = 1; repeated ContainerDevices devices = 2; ...;
+                               repeated DynamicResource dynamic_resources = 5; }
     ContainerDevices         { string resource_name = 1; repeated string device_ids = 2; ... }
+    DynamicResource          { string claim_name = 2; string claim_namespace = 3;
+                               repeated ClaimResource claim_resources = 4; }
+    ClaimResource            { repeated CDIDevice cdi_devices = 1; string driver_name = 2; string pool_name = 3;
+                               string device_name = 4; }
+    CDIDevice                { string name = 1; }
+
+Dynamic Resource Allocation: a GPU can reach a pod through a ResourceClaim of a DRA driver instead of the
+``amd.com/gpu`` extended resource; the kubelet reports those under ``dynamic_resources``
+(KubeletPodResourcesDynamicResources).  A claim device of an AMD GPU DRA driver (``gpu.amd.com`` /
+``amd.com``, or a CDI name in those vendors' namespaces) counts as allocated: keyed by the PCI address when
+its device or CDI name carries one, else by ``driver/pool/device`` -- an ID the agent cannot map to a local
+GPU, which makes it skip every GPU rather than guess (``Agent._unmatched_allocations``).
 
 ``grpc`` is optional: without it (or without the socket) :func:`allocated_devices` returns ``None`` and the
 agent falls back to its amd-smi VRAM / activity heuristic.
@@ -30,6 +43,7 @@ from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 DEFAULT_SOCKET = "/var/lib/kubelet/pod-resources/kubelet.sock"
 LIST_METHOD = "/v1.PodResourcesLister/List"
 GPU_RESOURCES = ("amd.com/gpu",)
+DRA_DRIVERS = ("gpu.amd.com", "amd.com")
 
 
 class PodResourcesError(RuntimeError):
@@ -106,9 +120,37 @@ def decode_list_response(buf: bytes) -> List[Dict[str, object]]:
                             elif dn == 2 and dw == 2:
                                 dev["device_ids"].append(_str(dv))  # type: ignore[union-attr]
                         ctr["devices"].append(dev)  # type: ignore[union-attr]
+                    elif cn == 5 and cw == 2:
+                        ctr.setdefault("dynamic", []).append(_decode_dynamic(bytes(cv)))  # type: ignore[union-attr]
                 pod["containers"].append(ctr)  # type: ignore[union-attr]
         pods.append(pod)
     return pods
+
+
+def _decode_dynamic(buf: bytes) -> Dict[str, object]:
+    """``DynamicResource`` -> ``{"claim_name", "claim_namespace", "devices": [{"driver", "pool", "device",
+    "cdi": [...]}]}``."""
+    out: Dict[str, object] = {"claim_name": "", "claim_namespace": "", "devices": []}
+    for n, w, v in _fields(buf):
+        if n == 2 and w == 2:
+            out["claim_name"] = _str(v)
+        elif n == 3 and w == 2:
+            out["claim_namespace"] = _str(v)
+        elif n == 4 and w == 2:
+            dev: Dict[str, object] = {"driver": "", "pool": "", "device": "", "cdi": []}
+            for rn, rw, rv in _fields(bytes(v)):  # type: ignore[arg-type]
+                if rn == 1 and rw == 2:
+                    for cn, cw, cv in _fields(bytes(rv)):  # type: ignore[arg-type]
+                        if cn == 1 and cw == 2:
+                            dev["cdi"].append(_str(cv))  # type: ignore[union-attr]
+                elif rn == 2 and rw == 2:
+                    dev["driver"] = _str(rv)
+                elif rn == 3 and rw == 2:
+                    dev["pool"] = _str(rv)
+                elif rn == 4 and rw == 2:
+                    dev["device"] = _str(rv)
+            out["devices"].append(dev)  # type: ignore[union-attr]
+    return out
 
 
 def _enc_varint(v: int) -> bytes:
@@ -137,6 +179,16 @@ def encode_list_response(pods: Sequence[Dict[str, object]]) -> bytes:
                 for did in dev.get("device_ids") or []:
                     d += _enc_bytes(2, str(did).encode())
                 c += _enc_bytes(2, d)
+            for dyn in ctr.get("dynamic") or []:
+                r = _enc_bytes(2, str(dyn.get("claim_name", "")).encode()) + \
+                    _enc_bytes(3, str(dyn.get("claim_namespace", "")).encode())
+                for dev in dyn.get("devices") or []:
+                    cr = b"".join(_enc_bytes(1, _enc_bytes(1, str(name).encode())) for name in dev.get("cdi") or [])
+                    cr += _enc_bytes(2, str(dev.get("driver", "")).encode()) + \
+                        _enc_bytes(3, str(dev.get("pool", "")).encode()) + \
+                        _enc_bytes(4, str(dev.get("device", "")).encode())
+                    r += _enc_bytes(4, cr)
+                c += _enc_bytes(5, r)
             p += _enc_bytes(3, c)
         out += _enc_bytes(1, p)
     return bytes(out)
@@ -163,10 +215,38 @@ def list_pod_resources(socket_path: str = DEFAULT_SOCKET, timeout: float = 5.0) 
         raise PodResourcesError(f"PodResources List: bad response ({e})") from e
 
 
+def _pci_address(text: str) -> Optional[str]:
+    """The first PCI address (``0000:05:00.0`` or ``05:00.0``) inside a device or CDI name, lower case."""
+    t = text.lower()
+    for i in range(len(t)):
+        for width in (12, 7):  # dddd:bb:dd.f / bb:dd.f
+            cand = t[i:i + width]
+            if len(cand) != width or (i and t[i - 1] in "0123456789abcdef:"):
+                continue
+            if width == 12 and not (cand[4] == ":" and cand[7] == ":" and cand[10] == "."):
+                continue
+            if width == 7 and not (cand[2] == ":" and cand[5] == "."):
+                continue
+            hexpart = cand.replace(":", "").replace(".", "")
+            if all(c in "0123456789abcdef" for c in hexpart) and cand[-1] in "01234567":
+                if i + width < len(t) and t[i + width] in "0123456789abcdef":
+                    continue
+                return cand
+    return None
+
+
+def _is_amd_claim_device(dev: Dict[str, object], drivers: Sequence[str]) -> bool:
+    if str(dev.get("driver") or "") in drivers:
+        return True
+    return any(str(c).split("/", 1)[0] in drivers for c in dev.get("cdi") or [])  # type: ignore[union-attr]
+
+
 def allocated_devices(socket_path: str = DEFAULT_SOCKET, resources: Sequence[str] = GPU_RESOURCES,
-                      timeout: float = 5.0) -> Optional[Dict[str, str]]:
+                      timeout: float = 5.0, dra_drivers: Sequence[str] = DRA_DRIVERS) -> Optional[Dict[str, str]]:
     """``{device id (lower case): "namespace/pod"}`` for every device of ``resources`` the kubelet has
-    allocated; ``None`` when the node has no PodResources socket (not a kubelet host / not mounted)."""
+    allocated, and every AMD GPU a DRA claim gave a pod (by PCI address when its name carries one, else
+    ``driver/pool/device``); ``None`` when the node has no PodResources socket (not a kubelet host / not
+    mounted)."""
     if not os.path.exists(socket_path):
         return None
     out: Dict[str, str] = {}
@@ -177,4 +257,13 @@ def allocated_devices(socket_path: str = DEFAULT_SOCKET, resources: Sequence[str
                 if dev.get("resource_name") in resources:
                     for did in dev.get("device_ids") or []:
                         out[str(did).lower()] = owner
+            for dyn in ctr.get("dynamic") or []:
+                claim = f"{owner} (claim {dyn.get('claim_namespace') or pod.get('namespace')}/{dyn.get('claim_name')})"
+                for dev in dyn.get("devices") or []:  # type: ignore[union-attr]
+                    if not _is_amd_claim_device(dev, dra_drivers):
+                        continue
+                    names = [str(dev.get("device") or "")] + [str(c) for c in dev.get("cdi") or []]  # type: ignore[union-attr]
+                    bdf = next((a for a in map(_pci_address, names) if a), None)
+                    key = bdf or "/".join(str(dev.get(k) or "") for k in ("driver", "pool", "device")).lower()
+                    out[key] = claim
     return out

@@ -133,3 +133,57 @@ def test_agent_cli_flags():
     a = A.build_parser().parse_args(["--pod-resources-socket", "/var/lib/kubelet/pod-resources/kubelet.sock",
                                      "--gpu-resource", "amd.com/gpu", "--gpu-resource", "amd.com/gpu-cpx"])
     assert a.pod_resources_socket.endswith("kubelet.sock") and a.gpu_resource == ["amd.com/gpu", "amd.com/gpu-cpx"]
+
+
+DRA_PODS = [
+    {"name": "dra-trainer", "namespace": "ml", "containers": [
+        {"name": "main", "devices": [], "dynamic": [
+            {"claim_name": "gpu-claim", "claim_namespace": "ml", "devices": [
+                {"driver": "gpu.amd.com", "pool": "node-a", "device": "gpu-0000-15-00-0",
+                 "cdi": ["gpu.amd.com/gpu=0000:15:00.0"]},
+                {"driver": "example.com", "pool": "p", "device": "nic-0", "cdi": ["example.com/nic=0000:05:00.0"]}]}]}]},
+]
+
+
+def test_dra_wire_roundtrip_and_allocation():
+    buf = PR.encode_list_response(DRA_PODS)
+    got = PR.decode_list_response(buf)
+    assert got[0]["containers"][0]["dynamic"] == DRA_PODS[0]["containers"][0]["dynamic"]
+    assert PR._pci_address("gpu.amd.com/gpu=0000:15:00.0") == "0000:15:00.0"
+    assert PR._pci_address("card-15:00.0") == "15:00.0"
+    assert PR._pci_address("gpu-0") is None and PR._pci_address("00000:15:00.0x") is None
+
+
+def test_agent_skips_a_gpu_allocated_only_through_dra(monkeypatch):
+    """a GPU handed to a pod by a DRA driver (no amd.com/gpu extended resource) is not
+    diagnosed; the other GPU is."""
+    ran = []
+    two = fixtures.mi355x_probe_report("n", gpus=2)
+    two["gpus"][0]["bdf"], two["gpus"][1]["bdf"] = "0000:05:00.0", "0000:15:00.0"
+    monkeypatch.setattr(amdsmi_probe, "probe", lambda node, src, fx: two)
+    monkeypatch.setattr(diag, "device_count", lambda: 2)
+    monkeypatch.setattr(diag, "device_info", lambda d: {"bdf": ["0000:05:00.0", "0000:15:00.0"][d]})
+    monkeypatch.setattr(diag, "run", lambda level, d, **kw: (ran.append(d), {"gemm": {"pass": True}})[1])
+    with FakeKubelet(DRA_PODS) as kub:
+        got = PR.allocated_devices(kub.sock)
+        assert got == {"0000:15:00.0": "ml/dra-trainer (claim ml/gpu-claim)"}
+        ag = A.Agent("n", source="fake", diag_level=1, pod_resources_socket=kub.sock)
+        rep = ag.probe_once()
+    assert ran == [0]
+    assert rep["gpus"][1]["diag_skipped"] == "allocated to pod ml/dra-trainer (claim ml/gpu-claim)"
+
+
+def test_dra_device_without_a_pci_address_makes_the_agent_fail_safe(monkeypatch):
+    pods = [{"name": "p", "namespace": "ml", "containers": [{"name": "c", "devices": [], "dynamic": [
+        {"claim_name": "c1", "claim_namespace": "ml", "devices": [
+            {"driver": "gpu.amd.com", "pool": "node-a", "device": "gpu-3", "cdi": ["gpu.amd.com/gpu=gpu-3"]}]}]}]}]
+    ran = []
+    monkeypatch.setattr(amdsmi_probe, "probe", lambda node, src, fx: fixtures.mi355x_probe_report("n", gpus=2))
+    monkeypatch.setattr(diag, "device_count", lambda: 2)
+    monkeypatch.setattr(diag, "device_info", lambda d: {"bdf": ["0000:05:00.0", "0000:15:00.0"][d]})
+    monkeypatch.setattr(diag, "run", lambda level, d, **kw: (ran.append(d), {"gemm": {"pass": True}})[1])
+    with FakeKubelet(pods) as kub:
+        assert PR.allocated_devices(kub.sock) == {"gpu.amd.com/node-a/gpu-3": "ml/p (claim ml/c1)"}
+        rep = A.Agent("n", source="fake", diag_level=1, pod_resources_socket=kub.sock).probe_once()
+    assert ran == []
+    assert all("matching no local PCI address" in g["diag_skipped"] for g in rep["gpus"])
