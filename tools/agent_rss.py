@@ -19,12 +19,30 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def mem() -> dict:
+    """RSS and peak, split into anonymous memory (allocations: what grows per device and per test) and
+    file-backed pages (shared libraries: loaded once per process whatever the device count)."""
     out = {}
     with open("/proc/self/status") as f:
         for line in f:
-            if line.startswith(("VmRSS:", "VmHWM:")):
+            if line.startswith(("VmRSS:", "VmHWM:", "RssAnon:", "RssFile:", "RssShmem:")):
                 out[line.split(":")[0]] = int(line.split()[1]) // 1024
-    return {"rss_mib": out.get("VmRSS"), "peak_mib": out.get("VmHWM")}
+    return {"rss_mib": out.get("VmRSS"), "peak_mib": out.get("VmHWM"), "anon_mib": out.get("RssAnon"),
+            "file_mib": out.get("RssFile"), "shmem_mib": out.get("RssShmem")}
+
+
+def top_mappings(n: int = 12) -> list:
+    """The largest resident mappings (/proc/self/smaps), by backing file or [anon]/[heap]."""
+    sizes: dict = {}
+    name = "?"
+    with open("/proc/self/smaps") as f:
+        for line in f:
+            head = line.split()
+            if head and "-" in head[0] and len(head) >= 5 and not line.startswith(("Rss", "Size")):
+                name = head[5] if len(head) >= 6 else "[anon]"
+                name = os.path.basename(name) if name.startswith("/") else name
+            elif line.startswith("Rss:"):
+                sizes[name] = sizes.get(name, 0) + int(line.split()[1])
+    return [{"mapping": k, "rss_mib": round(v / 1024, 1)} for k, v in sorted(sizes.items(), key=lambda kv: -kv[1])[:n]]
 
 
 def main() -> int:
@@ -42,18 +60,21 @@ def main() -> int:
     n = diag.device_count()
     info = diag.device_info(0)
     stages.append(("HIP device 0 initialised", dict(mem(), hip_devices=n, cus=info["cus"])))
+    tops = {}
     for level in range(1, args.level + 1):
         t = time.perf_counter()
         res = diag.run(level, 0)
+        tops[level] = top_mappings()
         stages.append((f"diag level {level}", dict(mem(), all_pass=all(r.get("pass") for r in res.values()),
                                                     s=round(time.perf_counter() - t, 2))))
     r = fabric.collective_suite(list(range(n)), sizes=[64 << 20, 256 << 20], timeout_s=120)
     stages.append(("RCCL suite", dict(mem(), rccl_pass=r["pass"])))
     by = {k: v for k, v in stages}
-    out = {"stages": [dict(stage=k, **v) for k, v in stages],
+    by_stage_top = top_mappings()
+    out = {"stages": [dict(stage=k, **v) for k, v in stages], "top_mappings_after_level1": tops.get(1),
            # HIP runtime + the device's context and code objects (loaded at the first kernel) + test buffers
            "per_device_hip_mib": by["diag level 1"]["rss_mib"] - by["amd-smi probe"]["rss_mib"],
-           "peak_mib": stages[-1][1]["peak_mib"]}
+           "peak_mib": stages[-1][1]["peak_mib"], "top_mappings_end": by_stage_top}
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     with open(args.out, "w") as f:
         json.dump(out, f, indent=1)
