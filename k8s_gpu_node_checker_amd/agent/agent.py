@@ -115,6 +115,39 @@ DIAG_PARALLEL = 8
 HUNG_RESTART_FACTOR = 2.0
 
 
+# Host memory of the agent process (MiB), measured on one MI355X (profiles/agent_rss_*_mi355x.json,
+# tools/agent_rss.py, tools/rccl_rss.py): Python + amd-smi probe + HIP runtime up, before any kernel
+MEM_BASE_MIB = 60
+# the first launch of the level-1 kernels (HIP queues, kernel-argument pools, comgr's code-object loading;
+# RSS 54 -> 695 MiB, flat afterwards at any problem size).  How much of it recurs per additional device could
+# not be measured on one GPU: the budget counts all of it per device, an upper bound
+MEM_PER_DEVICE_MIB = 640
+# level 2 on top (memtest, 8192^3 GEMMs; 695 -> 1,059 MiB) plus the host-link test's pinned 256 MiB buffer --
+# one at a time, ops/diag.SHARED_TESTS -- (peak 1,326 MiB)
+MEM_LEVEL2_MIB = 640
+# the in-process RCCL suite (level 2, >= 2 GPUs) with a warm comgr cache: peak 2,712 MiB on one GPU
+MEM_RCCL_WARM_MIB = 1400
+# ... and with a cold one: comgr decompresses RCCL's compressed code objects on the first load, peak 11,786 MiB
+# (profiles/rccl_rss_comgr_cache_mi355x.json); the level-2 overlay keeps the cache on the node
+# (AMD_COMGR_CACHE_DIR on a hostPath) and fills it from an init container with its own limit
+MEM_RCCL_COLD_PEAK_MIB = 11786
+
+
+def memory_budget_mib(devices: int, level: int, rccl: bool = False) -> int:
+    """Upper bound of the agent's host memory for ``devices`` HIP devices at diagnostics ``level`` (the
+    DaemonSet's memory limit; tests/test_deploy.py holds the manifests to it).  Measured on one MI355X; beyond one
+    device the per-device part is an extrapolation (MEM_PER_DEVICE_MIB), unmeasured: no multi-GPU box was
+    available to this project."""
+    mib = MEM_BASE_MIB
+    if level >= 1:
+        mib += max(1, devices) * MEM_PER_DEVICE_MIB
+    if level >= 2:
+        mib += MEM_LEVEL2_MIB
+        if rccl and devices >= 2:
+            mib += MEM_RCCL_WARM_MIB
+    return mib
+
+
 class _DiagRun:
     """One device's diagnostic thread: wall-clock start (reported), monotonic start (watchdog), result box."""
     __slots__ = ("thread", "started", "mono", "box")

@@ -344,3 +344,50 @@ def test_cel_subset_semantics():
         e("o.x == 1 && true", {"o": {}})
     assert e("'k' in m && size(m['k']) == 2", {"m": {"k": ["a", "b"]}}) is True
     assert e("true == 1", {}) is False
+
+
+# --- memory limits from the measured budget ---------------------------------------------------
+
+def _mib(q):
+    units = {"Ki": 1 / 1024, "Mi": 1, "Gi": 1024}
+    for u, f in units.items():
+        if q.endswith(u):
+            return float(q[:-2]) * f
+    return float(q) / (1 << 20)
+
+
+def _agent_container(doc):
+    return next(c for c in doc["spec"]["template"]["spec"]["containers"] if c["name"] == "agent")
+
+
+def test_daemonset_memory_limit_covers_the_budget_of_an_eight_gpu_node():
+    ds = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
+    c = _agent_container(ds)
+    level = int(c["command"][c["command"].index("--diag-level") + 1])
+    assert level == 1
+    assert _mib(c["resources"]["limits"]["memory"]) >= agent.memory_budget_mib(8, level)
+    assert agent.memory_budget_mib(1, 1) >= 695  # the measured one-GPU level-1 RSS (profiles/agent_rss_mi355x.json)
+    assert agent.memory_budget_mib(1, 2, rccl=True) >= agent.memory_budget_mib(1, 2)
+
+
+def test_level2_overlay_keeps_the_comgr_cache_and_sizes_both_containers():
+    base = os.path.join(REPO, "deploy", "level2")
+    kust = yaml.safe_load(open(os.path.join(base, "kustomization.yaml")))
+    assert kust["resources"] == ["../"] and kust["patches"][0]["path"] == "daemonset-level2.yaml"
+    patch = yaml.safe_load(open(os.path.join(base, "daemonset-level2.yaml")))
+    c = _agent_container(patch)
+    agent.build_parser().parse_args(c["command"][1:])
+    assert c["command"][c["command"].index("--diag-level") + 1] == "2"
+    assert _mib(c["resources"]["limits"]["memory"]) >= agent.memory_budget_mib(8, 2, rccl=True)
+    init = patch["spec"]["template"]["spec"]["initContainers"][0]
+    assert init["command"][0] == "mi355x-fabric"
+    from k8s_gpu_node_checker_amd.ops import fabric
+    fabric.main.__code__  # the console script's target exists
+    assert 'mi355x-fabric = "k8s_gpu_node_checker_amd.ops.fabric:main"' in open(os.path.join(REPO, "pyproject.toml")).read()
+    assert _mib(init["resources"]["limits"]["memory"]) >= agent.MEM_RCCL_COLD_PEAK_MIB
+    for ctr in (c, init):
+        env = {e["name"]: e["value"] for e in ctr["env"]}
+        mount = next(m["mountPath"] for m in ctr["volumeMounts"] if m["name"] == "comgr-cache")
+        assert env["AMD_COMGR_CACHE_DIR"].startswith(mount)
+    vol = next(v for v in patch["spec"]["template"]["spec"]["volumes"] if v["name"] == "comgr-cache")
+    assert vol["hostPath"]["type"] == "DirectoryOrCreate"

@@ -45,11 +45,85 @@ def top_mappings(n: int = 12) -> list:
     return [{"mapping": k, "rss_mib": round(v / 1024, 1)} for k, v in sorted(sizes.items(), key=lambda kv: -kv[1])[:n]]
 
 
+def breakdown(out_path: str) -> int:
+    """Anonymous/peak RSS after every level-1/2 test, then after each RCCL step (open, every op x size),
+    blocking ncclCommInitAll path vs the agent's non-blocking one is not distinguishable from Python; the
+    steps show where host memory goes."""
+    import ctypes
+    from k8s_gpu_node_checker_amd.ops import diag, fabric
+    rows = [dict(step="start", **mem())]
+    diag.device_info(0)
+    rows.append(dict(step="hip init", **mem()))
+    for test in diag.LEVELS[2]:
+        try:
+            diag._one(test, 0, diag.FULL)
+            ok = True
+        except Exception as e:  # noqa: BLE001
+            ok = repr(e)[:100]
+        rows.append(dict(step=f"diag {test}", ok=ok, **mem()))
+    n = diag.device_count()
+    L = fabric.lib()
+    arr = (ctypes.c_int * n)(*range(n))
+    ctx = L.fabric_open(arr, n, 60000.0)
+    rows.append(dict(step="fabric_open (non-blocking)", ok=bool(ctx), **mem()))
+    out = (ctypes.c_double * 4)()
+    for op in fabric.OPS:
+        for size in (64 << 20, 256 << 20):
+            rc = L.fabric_run(ctx, fabric.OPS.index(op), size, 10, 3, out, 60000.0)
+            rows.append(dict(step=f"{op} {size >> 20}M", rc=rc, **mem()))
+    L.fabric_close(ctx)
+    rows.append(dict(step="fabric_close", **mem()))
+    os.makedirs(os.path.dirname(out_path) or ".", exist_ok=True)
+    with open(out_path, "w") as f:
+        json.dump({"rows": rows, "top_mappings_end": top_mappings()}, f, indent=1)
+    for r in rows:
+        print(json.dumps(r))
+    return 0
+
+
+def first_launch(out_path: str) -> int:
+    """Is the host memory a GEMM adds a one-time cost of the first launch (runtime, code objects) or does it
+    grow with the problem size?  Small calls of every kernel family first, then the large ones."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    rows = [dict(step="start", **mem())]
+    diag.device_info(0)
+    rows.append(dict(step="hip init", **mem()))
+    steps = [("hbm 0.25 GiB", lambda: diag.hbm(0, gib=0.25, iters=2)),
+             ("gemm 256", lambda: diag.gemm(0, size=256, warmup=1, iters=2, samples=64)),
+             ("gemm 1024", lambda: diag.gemm(0, size=1024, warmup=1, iters=2, samples=64)),
+             ("gemm 4096", lambda: diag.gemm(0, size=4096, warmup=1, iters=2, samples=256)),
+             ("gemm 8192", lambda: diag.gemm(0, size=8192, warmup=1, iters=2, samples=256)),
+             ("gemm 8192 again", lambda: diag.gemm(0, size=8192, warmup=1, iters=2, samples=256)),
+             ("gemm_fp8 256", lambda: diag.gemm_fp8(0, size=256, warmup=1, iters=2, samples=64)),
+             ("gemm_fp8 8192", lambda: diag.gemm_fp8(0, size=8192, warmup=1, iters=2, samples=256)),
+             ("mfma", lambda: diag.mfma_burn(0, iters=200, reps=1))]
+    for name, fn in steps:
+        try:
+            fn()
+            ok = True
+        except Exception as e:  # noqa: BLE001
+            ok = repr(e)[:120]
+        rows.append(dict(step=name, ok=ok, **mem()))
+    with open(out_path, "w") as f:
+        json.dump({"rows": rows, "top_mappings_end": top_mappings()}, f, indent=1)
+    for r in rows:
+        print(json.dumps(r))
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/agent_rss.json")
     ap.add_argument("--level", type=int, default=2)
+    ap.add_argument("--first-launch", action="store_true",
+                    help="RSS across small-then-large calls of each kernel family (one-time vs size-dependent)")
+    ap.add_argument("--breakdown", action="store_true",
+                    help="RSS after each diagnostic test and each RCCL step instead of the stage summary")
     args = ap.parse_args()
+    if args.breakdown:
+        return breakdown(args.out)
+    if args.first_launch:
+        return first_launch(args.out)
     stages = [("python", mem())]
     from k8s_gpu_node_checker_amd.agent import agent as A  # noqa: F401
     from k8s_gpu_node_checker_amd.ops import amdsmi_probe, diag, fabric
