@@ -81,6 +81,30 @@ def _fabric_check(world, local_rank, cuda):
         return {"backend": "nccl(rccl)" if cuda else "gloo", "pass": False, "detail": f"{type(e).__name__}: {e}"}
 
 
+def _node_cycle(world: int, timeout_s: float = 150.0) -> dict:
+    """Untimed, rank 0, world > 1 on GPUs: the node agent's multi-device cycle over every GPU of the job
+    (``agent/node_cycle.py``: per-device diagnostic threads at once, xGMI pair matrix, in-process RCCL suite
+    under its deadline) in a child process with a time limit, so a failure there is reported in the bench
+    line and never costs the benchmark.  The other ranks wait on a CPU (gloo) barrier meanwhile: no spinning
+    collective kernel on their GPUs."""
+    cmd = [sys.executable, "-m", "k8s_gpu_node_checker_amd.agent.node_cycle", "--devices",
+           ",".join(str(d) for d in range(world)), "--level", "1", "--timeout", str(timeout_s)]
+    env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    t = time.perf_counter()
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=2 * timeout_s + 60)
+    except subprocess.TimeoutExpired:
+        return {"pass": False, "detail": f"node cycle did not finish within {2 * timeout_s + 60:g} s"}
+    line = next((x for x in reversed(p.stdout.splitlines()) if x.startswith("{")), None)
+    if p.returncode != 0 or line is None:
+        return {"pass": False, "rc": p.returncode, "detail": (p.stderr or p.stdout)[-400:]}
+    res = json.loads(line)
+    res["pass"] = all(d.get("pass") for d in res.get("per_device", {}).values()) and all(
+        (r or {}).get("pass") is not False for r in (res.get("fabric") or {}).values())
+    res["child_wall_s"] = round(time.perf_counter() - t, 2)
+    return res
+
+
 def _coldstart(api_url: str, runs: int) -> dict:
     """Whole-process wall clock of ``check-gpu-node --json`` against the same mock (what a cron / CI user
     pays per check), measured in child processes before this process touches the GPU: median of
@@ -125,6 +149,8 @@ def main() -> int:
                     help="child-process runs of check-gpu-node --json for coldstart_ms (rank 0, before GPU work; 0: skip)")
     ap.add_argument("--no-fabric-check", dest="fabric_check", action="store_false",
                     help="skip the untimed all-reduce fabric check (world > 1)")
+    ap.add_argument("--no-node-cycle", dest="node_cycle", action="store_false",
+                    help="skip the untimed multi-GPU node-agent cycle (world > 1 on GPUs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -219,6 +245,12 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
     for g in rep.get("gpus") or []:
         diag = g.get("diag") or {}
     fabric = _fabric_check(world, local_rank, cuda) if world > 1 and args.fabric_check else None
+    node_cycle = None
+    if world > 1 and cuda and args.node_cycle:
+        dist.barrier(group=group)  # CPU barrier: every rank's own setup is done, its GPU idle
+        if rank == 0:
+            node_cycle = _node_cycle(world)
+        dist.barrier(group=group)
     barrier()
 
     opts = CheckOptions(json=True, page_size=args.page_size, health_policy="auto",
@@ -299,6 +331,7 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
             "backend": fastpath.backend(),
             "probe": {"source": probe_source, "setup_ms": round(probe_ms, 1), "diag": diag},
             "fabric": fabric,
+            "node_cycle": node_cycle,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

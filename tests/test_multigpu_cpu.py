@@ -263,3 +263,17 @@ def test_hung_collective_is_aborted_and_reported_as_a_failed_rccl_row(node8):
     assert "watchdog" not in rep["fabric"] and rep["state"] == H.UNHEALTHY
     assert any(r.startswith("xGMI rccl failed (all_reduce") for r in ag.evaluate(rep).reasons)
     assert ag._fabric_thread is None  # the suite returned: nothing left holding the GPUs
+
+
+def test_node_cycle_module_over_eight_fake_gpus(node8):
+    """agent/node_cycle.py (what bench.py runs on a multi-GPU job): every device diagnosed at once, the
+    pair matrix and the RCCL suite, one summary."""
+    from k8s_gpu_node_checker_amd.agent import node_cycle
+    lib, fab = node8(delay_s=0.05)
+    res = node_cycle.run(list(range(8)), level=1, timeout_s=30, parallel=8)
+    assert res["peak_threads"] == 8 and res["verdict"] == H.HEALTHY
+    assert all(d["pass"] for d in res["per_device"].values()) and len(res["per_device"]) == 8
+    assert res["fabric"]["p2p"]["pass"] and res["fabric"]["rccl"]["pass"]
+    assert diag.run.__name__ == "run"  # the counting wrapper is removed again
+    res4 = node_cycle.run(list(range(8)), level=1, timeout_s=30, parallel=4, fabric=False)
+    assert res4["peak_threads"] == 4 and "fabric" not in res4

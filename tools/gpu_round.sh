@@ -29,6 +29,9 @@ step agent-soak
 timeout -k 10 200 python tools/agent_soak.py --minutes 1 --diag-level 1 --interval 5 --sample 10 --out gpurun_out/agent_soak_round.json > gpurun_out/agent_soak_round.log 2>&1 || { echo "agent soak failed"; tail -20 gpurun_out/agent_soak_round.log; exit 1; }
 step contention
 timeout -k 10 200 python tools/contention_demo.py --out gpurun_out/contention_round.json > gpurun_out/contention_round.log 2>&1 || { echo "contention demo failed"; tail -20 gpurun_out/contention_round.log; exit 1; }
+step node-cycle
+timeout -k 10 200 python -m k8s_gpu_node_checker_amd.agent.node_cycle --devices 0 --level 2 --timeout 60 > gpurun_out/node_cycle.json 2> gpurun_out/node_cycle.err || { echo "node cycle failed"; tail -20 gpurun_out/node_cycle.err; exit 1; }
+cat gpurun_out/node_cycle.json
 step probe-cli
 timeout -k 10 60 ./k8s_gpu_node_checker_amd/_native/mi355x-probe --repeat 5 --interval-ms 100 > gpurun_out/probe_cli.jsonl 2>&1 || { echo "probe cli failed"; cat gpurun_out/probe_cli.jsonl; exit 1; }
 tail -1 gpurun_out/probe_cli.jsonl
