@@ -226,3 +226,36 @@ def test_node_watcher_notices_a_heartbeat_going_stale_without_events(mock_cluste
     assert [r.exit_code for r in reports] == [0, 3]
     assert [r.verdicts[0].state for r in reports] == ["healthy", "unknown"]
     assert w.events == 0  # nothing arrived on the stream: the second report came from the recheck
+
+
+def test_cli_watch_events_slack_on_node_change(mock_cluster, sink, tmp_path):
+    """The shipped watcher's flags: one node of three going NotReady (exit stays 0) is one Slack POST, its
+    recovery one more; the first report of a healthy cluster sends nothing."""
+    srv = mock_cluster(fixtures.cluster(3, "amd", gpus_per_node=8, with_health=True), bookmark_interval=0.2)
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    env = {k: v for k, v in os.environ.items() if k not in ("SLACK_WEBHOOK_URL", "KUBECONFIG")}
+    env["SLACK_WEBHOOK_URL"] = sink.url("200")
+    p = subprocess.Popen([sys.executable, os.path.join(REPO, "check-gpu-node.py"), "--kubeconfig", kc, "--json",
+                          "--watch-events", "--slack-only-on-error", "--slack-on-node-change", "--watch-count", "3",
+                          "--watch-duration", "30", "--watch-debounce", "0.1"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=str(tmp_path))
+
+    def next_report():
+        lines = []
+        while True:
+            line = p.stdout.readline()
+            assert line, p.stderr.read()
+            lines.append(line)
+            if line == "}\n":
+                return json.loads("".join(lines))
+    assert next_report()["ready_nodes"] == 3
+    time.sleep(0.3)
+    assert len(sink.requests) == 0
+    _set_ready(srv, "mi355x-node-0001", False)
+    assert next_report()["ready_nodes"] == 2
+    time.sleep(0.3)
+    assert len(sink.requests) == 1
+    _set_ready(srv, "mi355x-node-0001", True)
+    p.communicate(timeout=30)
+    assert p.returncode == 0
+    assert len(sink.requests) == 2
