@@ -947,7 +947,23 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
     return "\n".join(lines) + "\n"
 
 
-def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = None) -> ThreadingHTTPServer:
+def tls_context(cert_file: str, key_file: str, client_ca: Optional[str] = None) -> Any:
+    """Server-side TLS for the agent's port.  With ``client_ca`` a client certificate is requested and, when
+    presented, verified against it (``CERT_OPTIONAL``): the kubelet's liveness probe presents none and still
+    reaches ``/healthz``; ``serve`` then refuses ``/probe``, ``/metrics`` and ``/status`` (host PIDs, the full
+    report) to a client without a verified certificate."""
+    import ssl
+    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+    ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+    ctx.load_cert_chain(cert_file, key_file)
+    if client_ca:
+        ctx.load_verify_locations(cafile=client_ca)
+        ctx.verify_mode = ssl.CERT_OPTIONAL
+    return ctx
+
+
+def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = None, tls: Any = None,
+          require_client_cert: bool = False) -> ThreadingHTTPServer:
     """/probe, /metrics, /status (text) and /healthz; /healthz answers 503 once no probe has completed for
     ``stale_after`` s (a wedged amd-smi call or driver), once a diagnostic thread has outlived
     HUNG_RESTART_FACTOR x ``diag_timeout`` (a hung HIP queue the process cannot cancel) or after the HIP runtime
@@ -962,6 +978,16 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
             pass
 
         def do_GET(self) -> None:  # noqa: N802
+            if require_client_cert and not self.path.startswith("/healthz"):
+                peer = self.connection.getpeercert() if hasattr(self.connection, "getpeercert") else None
+                if not peer:
+                    body = b"client certificate required\n"
+                    self.send_response(403)
+                    self.send_header("Content-Type", "text/plain")
+                    self.send_header("Content-Length", str(len(body)))
+                    self.end_headers()
+                    self.wfile.write(body)
+                    return
             with agent.lock:
                 rep = agent.last
             if self.path.startswith("/probe"):
@@ -1007,6 +1033,18 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
     class Srv(ThreadingHTTPServer):
         daemon_threads = True
         request_queue_size = 128  # the checker's fan-out connects in bursts
+
+        def finish_request(self, request: Any, client_address: Any) -> None:
+            if tls is not None:
+                # the handshake runs on the connection's own thread (never on the accept loop), bounded
+                request.settimeout(10.0)
+                try:
+                    request = tls.wrap_socket(request, server_side=True)
+                except OSError:
+                    request.close()
+                    return
+                request.settimeout(None)
+            super().finish_request(request, client_address)
 
     srv = Srv((host, port), H)
     threading.Thread(target=srv.serve_forever, daemon=True).start()
@@ -1065,6 +1103,13 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--annotation-encoding", choices=("json", "gzip"), default="json",
                     help="report annotation as JSON (readable with kubectl) or gz: + base64(gzip(JSON)), "
                          "~12x smaller in every node LIST and watch event (the checker reads both)")
+    ap.add_argument("--tls-cert-file", default=None, metavar="PEM",
+                    help="serve the HTTP port over TLS with this certificate (with --tls-key-file)")
+    ap.add_argument("--tls-key-file", default=None, metavar="PEM")
+    ap.add_argument("--tls-client-ca", default=None, metavar="PEM",
+                    help="with TLS: /probe, /metrics and /status need a client certificate signed by this CA "
+                         "(the checker's --probe-client-cert, Prometheus' tlsConfig); /healthz stays open for "
+                         "the kubelet's probe")
     ap.add_argument("--label-node", action="store_true",
                     help="keep node labels " + ", ".join(NODE_LABELS) + " current (verdict, GPU count, partition "
                          "modes, VBIOS, driver) for nodeSelector / nodeAffinity")
@@ -1112,7 +1157,13 @@ def main(argv: Optional[List[str]] = None) -> int:
     if "http" in pubs:
         host, _, port = args.listen.rpartition(":")
         # a probe cycle may legitimately include diagnostics (up to --diag-timeout per GPU)
-        serve(agent, host or "0.0.0.0", int(port), stale_after=max(180.0, 3 * args.interval + args.diag_timeout))
+        if bool(args.tls_cert_file) != bool(args.tls_key_file) or (args.tls_client_ca and not args.tls_cert_file):
+            print("--tls-cert-file and --tls-key-file go together (and --tls-client-ca needs them)", file=sys.stderr,
+                  flush=True)
+            return 2
+        tls = tls_context(args.tls_cert_file, args.tls_key_file, args.tls_client_ca) if args.tls_cert_file else None
+        serve(agent, host or "0.0.0.0", int(port), stale_after=max(180.0, 3 * args.interval + args.diag_timeout),
+              tls=tls, require_client_cert=bool(args.tls_client_ca))
     # SIGTERM (pod deletion, rolling update): finish the cycle in flight and leave with 0 instead of dying
     # mid-write; the condition keeps its last heartbeat and ages out at the checker's --probe-max-age
     stop = threading.Event()

@@ -55,6 +55,8 @@ class CheckOptions:
         self.probe_concurrency = 64
         self.probe_timeout = 2.0
         self.probe_ca: Optional[str] = None
+        self.probe_client_cert: Optional[str] = None
+        self.probe_client_key: Optional[str] = None
         self.health_reeval = False
         self.require_schedulable = False
         self.trace = False
@@ -195,7 +197,8 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
         if opts.probe_endpoint:
             from .parallel.fanout import fetch_probe_reports
             reports = fetch_probe_reports(scan, opts.probe_endpoint, opts.probe_concurrency, opts.probe_timeout,
-                                          ca_file=opts.probe_ca)
+                                          ca_file=opts.probe_ca, client_cert=opts.probe_client_cert,
+                                          client_key=opts.probe_client_key)
         verdicts: List[Optional[H.Verdict]] = []
         changed = False
         unknown_ok = opts.probe_unknown == "allow"

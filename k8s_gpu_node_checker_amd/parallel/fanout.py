@@ -74,16 +74,30 @@ async def _read_chunked(reader: asyncio.StreamReader, cap: int) -> bytes:
             raise ValueError("malformed chunk")
 
 
-def _ssl_context(ca_file: Optional[str]) -> Any:
-    import ssl
-    return ssl.create_default_context(cafile=ca_file) if ca_file else ssl.create_default_context()
+_SSL_CACHE: Dict[Any, Any] = {}
 
 
-async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None, max_body: int = MAX_BODY) -> Any:
+def _ssl_context(ca_file: Optional[str], client_cert: Optional[str] = None, client_key: Optional[str] = None) -> Any:
+    """Client TLS for agent endpoints (one context per configuration for the whole fan-out): verified against
+    ``ca_file`` or the system roots, presenting ``client_cert`` when the agents require one (their
+    ``--tls-client-ca``)."""
+    key = (ca_file, client_cert, client_key)
+    ctx = _SSL_CACHE.get(key)
+    if ctx is None:
+        import ssl
+        ctx = ssl.create_default_context(cafile=ca_file) if ca_file else ssl.create_default_context()
+        if client_cert:
+            ctx.load_cert_chain(client_cert, client_key or None)
+        _SSL_CACHE[key] = ctx
+    return ctx
+
+
+async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None, max_body: int = MAX_BODY,
+                         client_cert: Optional[str] = None, client_key: Optional[str] = None) -> Any:
     parts = urlsplit(url)
     host = parts.hostname or "localhost"
     port = parts.port or (443 if parts.scheme == "https" else 80)
-    ssl_ctx = _ssl_context(ca_file) if parts.scheme == "https" else None
+    ssl_ctx = _ssl_context(ca_file, client_cert, client_key) if parts.scheme == "https" else None
     path = (parts.path or "/") + (("?" + parts.query) if parts.query else "")
 
     async def run() -> Any:
@@ -115,7 +129,8 @@ async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None
 
 
 async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, timeout: float = 2.0,
-                    retries: int = 1, ca_file: Optional[str] = None) -> List[Dict[str, Any]]:
+                    retries: int = 1, ca_file: Optional[str] = None, client_cert: Optional[str] = None,
+                    client_key: Optional[str] = None) -> List[Dict[str, Any]]:
     sem = asyncio.Semaphore(max(1, concurrency))
 
     async def one(t: Dict[str, str]) -> Dict[str, Any]:
@@ -123,7 +138,8 @@ async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, ti
             last = "unreachable"
             for attempt in range(retries + 1):
                 try:
-                    doc = await _http_get_json(t["url"], timeout, ca_file)
+                    doc = await _http_get_json(t["url"], timeout, ca_file, client_cert=client_cert,
+                                               client_key=client_key)
                     if not isinstance(doc, dict):
                         return _error_report(t["name"], "probe endpoint returned non-object JSON")
                     return doc
@@ -174,9 +190,11 @@ def run_coroutine(coro: Any) -> Any:
 
 
 def fetch_probe_reports(scan: Any, template: str, concurrency: int = 64, timeout: float = 2.0,
-                        ca_file: Optional[str] = None) -> List[Optional[Dict[str, Any]]]:
+                        ca_file: Optional[str] = None, client_cert: Optional[str] = None,
+                        client_key: Optional[str] = None) -> List[Optional[Dict[str, Any]]]:
     """Fetch one probe report per GPU node (parallel to ``scan.gpu_nodes``)."""
     targets = build_targets(scan, template)
     if not targets:
         return []
-    return list(run_coroutine(fetch_all(targets, concurrency, timeout, ca_file=ca_file)))
+    return list(run_coroutine(fetch_all(targets, concurrency, timeout, ca_file=ca_file, client_cert=client_cert,
+                                        client_key=client_key)))

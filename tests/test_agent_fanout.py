@@ -577,3 +577,66 @@ def test_https_probe_endpoint_verified_with_probe_ca(certs, fixture_report):
         s.shutdown()
     from k8s_gpu_node_checker_amd import cli
     assert cli.parse_args(["--probe-ca", "/etc/ca.pem"]).probe_ca == "/etc/ca.pem"
+
+
+@pytest.fixture(scope="module")
+def pki(tmp_path_factory):
+    """A CA, a server certificate for 127.0.0.1 and a client certificate, both signed by the CA."""
+    import subprocess
+    d = tmp_path_factory.mktemp("mtls")
+
+    def run(*args):
+        r = subprocess.run(["openssl", *args], capture_output=True, cwd=d)
+        if r.returncode != 0:
+            pytest.skip(f"openssl: {r.stderr[-200:]}")
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "ca.key", "-out", "ca.crt", "-days", "1",
+        "-subj", "/CN=agents-ca")
+    for name, ext in (("srv", "subjectAltName=IP:127.0.0.1"), ("cli", "extendedKeyUsage=clientAuth")):
+        run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", f"{name}.key", "-out", f"{name}.csr", "-subj",
+            f"/CN={name}")
+        (d / f"{name}.ext").write_text(ext + "\n")
+        run("x509", "-req", "-in", f"{name}.csr", "-CA", "ca.crt", "-CAkey", "ca.key", "-CAcreateserial", "-out",
+            f"{name}.crt", "-days", "1", "-extfile", f"{name}.ext")
+    return {k: str(d / k) for k in ("ca.crt", "srv.crt", "srv.key", "cli.crt", "cli.key")}
+
+
+def test_agent_serves_tls_and_requires_client_certs_except_for_healthz(pki, fixture_report):
+    """--tls-cert-file/--tls-key-file/--tls-client-ca on the agent, --probe-ca/--probe-client-cert on the
+    checker: the report travels over verified mTLS; without a client certificate /probe is refused while the
+    kubelet's /healthz still answers."""
+    import asyncio
+    import ssl
+    import urllib.error
+    import urllib.request
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    ag = A.Agent("a", source="fixture", fixture=fixture_report)
+    ag.probe_once()
+    tls = A.tls_context(pki["srv.crt"], pki["srv.key"], pki["ca.crt"])
+    srv = A.serve(ag, "127.0.0.1", 0, tls=tls, require_client_cert=True)
+    base = f"https://127.0.0.1:{srv.server_address[1]}"
+    try:
+        out = asyncio.run(fanout.fetch_all([{"name": "a", "url": base + "/probe"}], timeout=5, retries=0,
+                                           ca_file=pki["ca.crt"], client_cert=pki["cli.crt"],
+                                           client_key=pki["cli.key"]))
+        assert out[0]["node"] == "a" and out[0]["gpus"], out[0]
+        out = asyncio.run(fanout.fetch_all([{"name": "a", "url": base + "/probe"}], timeout=5, retries=0,
+                                           ca_file=pki["ca.crt"]))
+        assert out[0]["error"] == "RuntimeError: HTTP 403"
+        ctx = ssl.create_default_context(cafile=pki["ca.crt"])
+        assert urllib.request.urlopen(base + "/healthz", context=ctx, timeout=5).read() == b"ok"
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(base + "/metrics", context=ctx, timeout=5)
+        assert e.value.code == 403
+        # plain HTTP to a TLS port is not served (the handshake fails on the connection's own thread)
+        with pytest.raises(Exception):
+            urllib.request.urlopen(base.replace("https", "http") + "/healthz", timeout=5).read()
+        assert urllib.request.urlopen(base + "/healthz", context=ctx, timeout=5).status == 200  # still serving
+    finally:
+        srv.shutdown()
+    args = A.build_parser().parse_args(["--tls-cert-file", "c", "--tls-key-file", "k", "--tls-client-ca", "ca"])
+    assert (args.tls_cert_file, args.tls_key_file, args.tls_client_ca) == ("c", "k", "ca")
+    assert A.main(["--publish", "http", "--tls-cert-file", "c", "--once", "--source", "fixture",
+                   "--fixture", fixture_report]) == 2
+    from k8s_gpu_node_checker_amd import cli
+    a = cli.parse_args(["--probe-client-cert", "/c.pem", "--probe-client-key", "/k.pem"])
+    assert (a.probe_client_cert, a.probe_client_key) == ("/c.pem", "/k.pem")
