@@ -227,3 +227,8 @@ def test_handwritten_structures_differential(lines):
     """Hand-written block structure (indent, sequences, keys, comments) around hand-written scalars."""
     text = "".join(" " * i + d + a + sep + b + "\n" for i, d, a, sep, b in lines)
     assert _agrees(text), text
+
+
+@pytest.mark.parametrize("text", [KUBECTL_STYLE.replace("\n", "\r\n"), "a: b\r\nc: d\r", "a: 'x\ry'\n", "a: b\rc: d\n"])
+def test_line_endings_match_pyyaml_or_refuse(text):
+    assert _agrees(text)
