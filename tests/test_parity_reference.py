@@ -139,3 +139,76 @@ def test_env_webhook_and_empty_flag_fallback(cluster, sink):
     a = run_ref(["--kubeconfig", kc, "--slack-webhook", ""], env=env)
     b = run_new(["--kubeconfig", kc, "--slack-webhook", ""], env=env)
     assert a.stdout == b.stdout and a.stdout.startswith("✅ 슬랙 메시지를 성공적으로 전송했습니다.")
+
+
+# --- differential fuzz: random NodeLists through the unmodified reference and this CLI -------------------------
+
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+_GPU_KEYS = ["nvidia.com/gpu", "amd.com/gpu", "gpu.intel.com/i915", "intel.com/gpu"]
+_QTY = st.sampled_from(["0", "1", "2", "8", "16", "1k", "500m", "x", "-2", "007", " 3", "+4", "٣", "1_0", "",
+                        "2Gi", "１"])
+_TXT = st.text(alphabet=st.sampled_from(list("abz-09._/한글 \"\\") + ["é", " ", "\t"]), max_size=8)
+
+
+@st.composite
+def _fuzz_node(draw, i):
+    node = {"metadata": None if draw(st.integers(0, 12)) == 0 else {
+                "name": f"n{i}-" + draw(st.text(alphabet=st.sampled_from(list("abc-09한")), max_size=6)),
+                "labels": draw(st.one_of(st.none(), st.dictionaries(_TXT, _TXT, max_size=3)))},
+            "spec": {"taints": draw(st.one_of(st.none(), st.lists(st.fixed_dictionaries({
+                "key": _TXT, "value": st.one_of(st.none(), _TXT),
+                "effect": st.sampled_from(["NoSchedule", "NoExecute", "PreferNoSchedule"])}), max_size=2)))},
+            "status": None if draw(st.integers(0, 15)) == 0 else {
+                "capacity": draw(st.one_of(st.none(), st.dictionaries(st.sampled_from(_GPU_KEYS + ["cpu", "memory"]),
+                                                                     _QTY, max_size=4))),
+                "conditions": draw(st.one_of(st.none(), st.lists(st.fixed_dictionaries({
+                    "type": st.sampled_from(["Ready", "MemoryPressure", "ready"]),
+                    "status": st.sampled_from(["True", "False", "Unknown", "true"])}), max_size=3)))}}
+    return node
+
+
+@st.composite
+def _fuzz_cluster(draw):
+    n = draw(st.integers(0, 5))
+    return [draw(_fuzz_node(i)) for i in range(n)]
+
+
+@settings(max_examples=int(os.environ.get("K8SGPU_FUZZ_EXAMPLES", "25")), deadline=None,
+          suppress_health_check=list(HealthCheck))
+@given(_fuzz_cluster(), st.booleans())
+def test_random_clusters_byte_identical(tmp_path_factory, nodes, as_json):
+    """Random NodeLists (odd quantities such as '\\u0663', ' 3', '1k', missing metadata/status/conditions,
+    unicode and control characters in labels and taints, lower-case condition strings): stdout and exit code
+    of the unmodified reference and of this CLI are identical."""
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import MockApiServer
+    d = tmp_path_factory.mktemp("fz")
+    with MockApiServer(nodes) as srv:
+        kc = write_kubeconfig(str(d / "kc"), srv.url)
+        flags = ["--kubeconfig", kc] + (["--json"] if as_json else [])
+        a, b = run_ref(flags), run_new(flags)
+    assert (a.returncode, a.stdout) == (b.returncode, b.stdout), (nodes, a.stdout, b.stdout, a.stderr[-500:],
+                                                                  b.stderr[-500:])
+
+
+@settings(max_examples=int(os.environ.get("K8SGPU_FUZZ_EXAMPLES", "15")), deadline=None,
+          suppress_health_check=list(HealthCheck))
+@given(_fuzz_cluster(), st.booleans())
+def test_random_clusters_same_slack_message(tmp_path_factory, sink, nodes, only_on_error):
+    """The Slack payload (text, username, icon, in requests' ASCII-escaped JSON) and the gating decision for
+    random clusters, reference vs this CLI."""
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import MockApiServer
+    d = tmp_path_factory.mktemp("fzs")
+    with MockApiServer(nodes) as srv:
+        kc = write_kubeconfig(str(d / "kc"), srv.url)
+        flags = ["--kubeconfig", kc, "--slack-webhook", sink.url("200"), "--slack-username", "fuzz-bot"] + \
+            (["--slack-only-on-error"] if only_on_error else [])
+        n0 = len(sink.requests)
+        a = run_ref(flags)
+        n1 = len(sink.requests)
+        b = run_new(flags)
+        n2 = len(sink.requests)
+    ra, rb = sink.requests[n0:n1], sink.requests[n1:n2]
+    assert (a.returncode, a.stdout) == (b.returncode, b.stdout)
+    assert len(ra) == len(rb) <= 1
+    assert [r["body"] for r in ra] == [r["body"] for r in rb]
