@@ -533,10 +533,12 @@ class Agent:
         lost_devs = {d: why for d, why in lost_devs.items() if why is not None}
         if lost_devs and self.hip_lost is None:
             # the HIP runtime, not a GPU, is gone only when the device count changed under the process or every
-            # device it just ran failed that way together; one device's "invalid device ordinal" is that GPU's
-            # (or its configuration's) failure and stays in its verdict
+            # device of the node (two or more) failed that way together; one device's "invalid device ordinal"
+            # is that GPU's (or its configuration's) failure and stays in its verdict -- restarting the agent
+            # for it would only loop, diagnosing the same broken GPU on every start
             now_count = diag.device_count()
-            if (self._hip_count0 is not None and now_count != self._hip_count0) or len(lost_devs) == len(finished):
+            everyone = len(lost_devs) == len(finished) == len(devices) >= 2
+            if (self._hip_count0 is not None and now_count != self._hip_count0) or everyone:
                 lost = next(iter(lost_devs.values()))
                 print(f"HIP runtime lost its devices ({lost}); diagnostics stop, /healthz fails so the "
                       "agent is restarted", file=sys.stderr, flush=True)

@@ -576,3 +576,20 @@ users:
 """)
     assert A.main(["--node", "gpu-3", "--kubeconfig", str(kc), "--once", "--source", "fixture",
                    "--fixture", "/nonexistent"]) == 2
+
+
+def test_single_gpu_failing_with_runtime_strings_is_not_a_restart_loop(monkeypatch):
+    """A one-GPU node whose GPU fails every test with a runtime-looking error (device count unchanged) is an
+    unhealthy GPU, not a lost runtime: restarting would only re-run the same diagnostics forever."""
+    w = World(monkeypatch, n=1)
+    bad = "mi355x diag failed (-1): hipSetDevice(device): initialization error"
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: (
+        w.runs.append(d), {"gemm": {"pass": False, "detail": bad}, "hbm": {"pass": False, "detail": bad}})[1])
+    ag = A.Agent("n", source="fake", diag_level=1)
+    rep = ag.probe_once()
+    assert ag.hip_lost is None and ag.hung_diagnostic() is None
+    assert rep["state"] == "unhealthy" and rep["gpus"][0]["diag"]["gemm"]["pass"] is False
+    monkeypatch.setattr(diag, "device_count", lambda: 0)  # ... but a count that drops is the runtime
+    w.clock += A.DIAG_RECHECK_S
+    ag.probe_once()
+    assert ag.hip_lost == "HIP device count changed from 1 to 0"
