@@ -13,6 +13,8 @@ The URL path selects the behaviour, so one sink serves every test:
 ``/resetflaky`` RST once, then ``200``
 ``/slow``       sleep ``slow_s`` (default 11 s) before answering ``200``
 ``/close``      close without a response ("Remote end closed connection")
+``/seq/ID/A,B``  scripted: the n-th POST to this exact path gets step n (the last step repeats); a step is
+                 ``200``, ``204``, ``404``, ``429``, ``500``, ``reset`` or ``close``; ``ID`` keeps runs apart
 ==============  =============================================================
 
 Every request is logged (path, headers, body) for assertions.
@@ -70,6 +72,9 @@ class _SinkHandler(socketserver.BaseRequestHandler):
             count = srv.counts.get(req["path"], 0) + 1
             srv.counts[req["path"]] = count
         path = req["path"].split("?", 1)[0]
+        if path.startswith("/seq/"):
+            steps = path.rsplit("/", 1)[-1].split(",")
+            path = "/" + steps[min(count, len(steps)) - 1]
         if path == "/reset" or (path == "/resetflaky" and count == 1):
             self.request.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
             self.request.close()

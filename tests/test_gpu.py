@@ -334,6 +334,30 @@ def test_rccl_suite_with_a_deadline_and_an_abort(dev):
     assert again["pass"], again
 
 
+def test_rccl_abort_while_collectives_are_in_flight(dev):
+    """A deadline that passes in the middle of the timed collectives (not during setup): the communicators are
+    aborted with kernels in flight, the suite reports which collective, and the process recovers."""
+    from k8s_gpu_node_checker_amd.ops import diag, fabric
+    n = diag.device_count()
+    t0 = time.monotonic()
+    warm = fabric.collective_suite(list(range(n)), sizes=[1 << 20], ops=["all_reduce"], iters=1, warmup=0,
+                                   timeout_s=60)
+    setup = time.monotonic() - t0
+    assert warm["pass"], warm
+    # ~2000 x 256 MiB all-reduces take seconds; the deadline leaves the setup plus a fraction of that
+    t0 = time.monotonic()
+    cut = fabric.collective_suite(list(range(n)), sizes=[256 << 20], ops=["all_reduce"], iters=2000, warmup=1,
+                                  timeout_s=setup + 0.3)
+    took = time.monotonic() - t0
+    print(json.dumps({"setup_s": round(setup, 3), "took_s": round(took, 3),
+                      **{k: cut.get(k) for k in ("pass", "aborted", "detail")}}))
+    assert cut["pass"] is False and cut["aborted"] is True, cut
+    assert "all_reduce" in cut["detail"] and "ncclCommAbort" in cut["detail"]
+    assert took < setup + 10
+    again = fabric.collective_suite(list(range(n)), sizes=[1 << 20], iters=2, warmup=1, timeout_s=60)
+    assert again["pass"], again
+
+
 def test_fabric_cli_stdout_is_pure_json(repo):
     """RCCL prints a version banner during communicator init; the CLI's stdout must still parse as one
     JSON document (the banner goes to stderr)."""

@@ -212,3 +212,40 @@ def test_random_clusters_same_slack_message(tmp_path_factory, sink, nodes, only_
     assert (a.returncode, a.stdout) == (b.returncode, b.stdout)
     assert len(ra) == len(rb) <= 1
     assert [r["body"] for r in ra] == [r["body"] for r in rb]
+
+
+_STEP = st.sampled_from(["200", "500", "204", "404", "429", "reset", "close"])
+
+
+@settings(max_examples=int(os.environ.get("K8SGPU_FUZZ_EXAMPLES", "15")), deadline=None,
+          suppress_health_check=list(HealthCheck))
+@given(st.lists(_STEP, min_size=1, max_size=5), st.integers(-1, 3), st.booleans())
+def test_random_webhook_behaviour_same_retry_state_machine(tmp_path_factory, sink, steps, retries, as_json):
+    """Scripted webhook answers (any mix of 200 / 204 / 404 / 429 / 500 / TCP reset / close without a
+    response) and retry counts: with ``--slack-retry-policy reference`` both programs make the same number of
+    POSTs with the same bodies, print the same stdout and the same stderr lines (modulo the transport's
+    exception text inside a connection-error line) and exit the same way."""
+    import uuid
+    d = tmp_path_factory.mktemp("fzw")
+    kc = None
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import MockApiServer
+    with MockApiServer(fixtures.golden("readme")) as srv:
+        kc = write_kubeconfig(str(d / "kc"), srv.url)
+        script = ",".join(steps)
+        common = ["--kubeconfig", kc, "--slack-retry-count", str(retries), "--slack-retry-delay", "0"] + \
+            (["--json"] if as_json else [])
+        tag = uuid.uuid4().hex[:8]
+        a = run_ref(common + ["--slack-webhook", sink.url(f"seq/{tag}-a/{script}")])
+        b = run_new(common + ["--slack-webhook", sink.url(f"seq/{tag}-b/{script}"), "--slack-retry-policy", "reference"])
+    ra = [r for r in sink.requests if f"/{tag}-a/" in r["path"]]
+    rb = [r for r in sink.requests if f"/{tag}-b/" in r["path"]]
+    assert (a.returncode, a.stdout) == (b.returncode, b.stdout), (steps, retries, a.stderr, b.stderr)
+    assert len(ra) == len(rb), (steps, retries, a.stderr, b.stderr)
+    assert [r["body"] for r in ra] == [r["body"] for r in rb]
+    la, lb = a.stderr.splitlines(), b.stderr.splitlines()
+    assert len(la) == len(lb), (steps, retries, a.stderr, b.stderr)
+    for x, y in zip(la, lb):
+        if "Connection aborted" in x or "Connection reset" in x or "RemoteDisconnected" in x:
+            assert x.split(":")[0] == y.split(":")[0], (x, y)
+        else:
+            assert x == y, (steps, retries, x, y)
