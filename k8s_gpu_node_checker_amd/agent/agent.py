@@ -20,7 +20,14 @@ Each verdict change is also posted as a Kubernetes Event on the node (``Warning 
 ``amd.com/gpu-unhealthy=true:NoSchedule`` while it is unhealthy (read-modify-write under the node's
 ``resourceVersion``, so a concurrent ``kubectl taint`` is never lost).
 
-RBAC: ``nodes: get, patch``, ``nodes/status: patch`` and ``events: create`` (``deploy/rbac.yaml``).
+RBAC: ``nodes: get, patch``, ``nodes/status: patch`` and ``events: create`` (``deploy/rbac.yaml``), narrowed to
+the agent's own node and to the fields it owns by ``deploy/agent-policy.yaml`` (a ValidatingAdmissionPolicy on the
+node-name claim of its pod-bound token) and by :class:`_OwnNodeClient` here.
+
+Multi-device nodes (8 GPUs, or 64 CPX partitions): per-device diagnostic threads, at most ``--diag-parallel`` at
+once, tests of shared host resources serialized (``ops/diag.SHARED_TESTS``); a diagnostic that outlives
+``--diag-timeout`` is a failed GPU and one that outlives twice that fails ``/healthz`` (fresh process); the RCCL
+suite aborts its own communicators at its deadline (``csrc/fabric/fabric.hip``).
 """
 
 from __future__ import annotations
