@@ -375,12 +375,17 @@ int fabric_run(void* ctx, int op, size_t bytes, int iters, int warmup, double* o
   }
   if (int rc = sync_all(c, dl, "input fill"); rc != 0) return rc;
 
-  for (int i = 0; i < warmup; ++i)
+  // the deadline is checked between launches too: a long run must not enqueue past it before any wait
+  for (int i = 0; i < warmup; ++i) {
+    if (dl.passed()) return abort_all(c, "warm-up collectives", dl);
     if (int rc = issue(c, op, count, dl); rc != 0) return rc;
+  }
   if (int rc = sync_all(c, dl, "warm-up collectives"); rc != 0) return rc;
   const auto t0 = std::chrono::steady_clock::now();
-  for (int i = 0; i < iters; ++i)
+  for (int i = 0; i < iters; ++i) {
+    if (dl.passed()) return abort_all(c, "timed collectives", dl);
     if (int rc = issue(c, op, count, dl); rc != 0) return rc;
+  }
   if (int rc = sync_all(c, dl, "timed collectives"); rc != 0) return rc;
   const double ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / iters;

@@ -354,7 +354,7 @@ def test_rccl_abort_while_collectives_are_in_flight(dev):
                       **{k: cut.get(k) for k in ("pass", "aborted", "detail")}}))
     assert cut["pass"] is False and cut["aborted"] is True, cut
     assert "all_reduce" in cut["detail"] and "ncclCommAbort" in cut["detail"]
-    assert took < setup + 10
+    assert took < 1.5 * setup + 0.3 + 3.0, took  # the deadline holds while launches are still being issued
     again = fabric.collective_suite(list(range(n)), sizes=[1 << 20], iters=2, warmup=1, timeout_s=60)
     assert again["pass"], again
 
