@@ -120,6 +120,9 @@ DIAG_PARALLEL = 8
 # /healthz fails once a diagnostic thread has outlived this many --diag-timeout: its verdict (watchdog) went
 # out at 1x; a thread in a hung HIP call cannot be cancelled, so only a fresh process frees its GPU
 HUNG_RESTART_FACTOR = 2.0
+# share of --diag-timeout the node-level xGMI pair matrix may use before the RCCL suite (an 8-GPU matrix is
+# 56 pairs of 6 x 256 MiB copies plus a verify pass each: seconds at xGMI rates, far inside 0.45 x the timeout)
+P2P_SHARE = 0.45
 
 
 # Host memory of the agent process (MiB), measured on one MI355X (profiles/agent_rss_*_mi355x.json,
@@ -642,14 +645,18 @@ class Agent:
 
     @staticmethod
     def _fabric_suite(devices: List[int], timeout_s: Optional[float] = None) -> Dict[str, Any]:
-        """The node-level tests: xGMI pair matrix and the RCCL collectives in this process (ops/fabric.py); the
-        collectives get the watchdog's deadline too, so a hung one is aborted rather than left queued."""
+        """The node-level tests: xGMI pair matrix and the RCCL collectives in this process (ops/fabric.py).  Both
+        run under the watchdog's deadline -- the pair matrix within the first ``P2P_SHARE`` of it, the collectives
+        within what is left up to 90 % -- so a hung copy or collective is given up (and named in the report)
+        rather than left holding the fabric thread."""
         from ..ops import diag
         out: Dict[str, Any] = {}
         t0 = time.monotonic()
         try:
-            m = diag.p2p_matrix(devices)
+            m = diag.p2p_matrix(devices, timeout_s=P2P_SHARE * timeout_s) if timeout_s else diag.p2p_matrix(devices)
             out["p2p"] = {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s")}
+            if m.get("stopped"):
+                out["p2p"]["stopped"] = m["stopped"]
         except Exception as e:
             out["p2p"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
         try:

@@ -31,12 +31,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -1087,6 +1089,30 @@ int launch_v3(const void* A, const void* Bt, float* C, int M, int N, int Kcols, 
 
 }  // namespace
 
+// Polled completion with a deadline (diag_p2p_copy_t): a hung copy engine or link must not block the caller.
+namespace {
+using SteadyClock = std::chrono::steady_clock;
+struct PollDeadline {
+  double limit_ms;
+  SteadyClock::time_point t0 = SteadyClock::now();
+  explicit PollDeadline(double ms) : limit_ms(ms) {}
+  bool bounded() const { return limit_ms > 0.0; }
+  bool passed() const {
+    return bounded() && std::chrono::duration<double, std::milli>(SteadyClock::now() - t0).count() >= limit_ms;
+  }
+};
+// hipSuccess once `ev` completed, hipErrorNotReady when the deadline passed first, else the query's error.
+hipError_t wait_event_polled(hipEvent_t ev, const PollDeadline& dl) {
+  if (!dl.bounded()) return hipEventSynchronize(ev);
+  for (;;) {
+    hipError_t q = hipEventQuery(ev);
+    if (q != hipErrorNotReady) return q;
+    if (dl.passed()) return hipErrorNotReady;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+}  // namespace
+
 extern "C" {
 
 const char* diag_last_error(void) { return g_err.c_str(); }
@@ -1396,7 +1422,14 @@ int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned l
 // buffer is then verified against the address-hash pattern on `dst`.  *peer = 1 if direct peer
 // access was available.  A slow pair (a link trained down or retrying) shows up as an outlier
 // against the node's other pairs; a corrupting one as errors.
-int diag_p2p_copy(int src, int dst, size_t bytes, int iters, double* gbps, unsigned long long* errors, int* peer) {
+//
+// `timeout_ms` > 0 bounds the copies and the verification: the completion events are polled rather than
+// waited on, and a pair that has not finished by then returns -4 ("hung") instead of blocking the agent's
+// node-level thread forever on a link that stopped making progress.  On that path the buffers, events and
+// stream are deliberately leaked: freeing memory an in-flight copy still targets would block (hipFree
+// synchronises the device) or let the engine write into a reused allocation.
+int diag_p2p_copy_t(int src, int dst, size_t bytes, int iters, double timeout_ms, double* gbps,
+                    unsigned long long* errors, int* peer) {
   int n = 0;
   DIAG_CHECK(hipGetDeviceCount(&n));
   if (src < 0 || dst < 0 || src >= n || dst >= n || src == dst || iters < 1 || bytes < 16) {
@@ -1441,20 +1474,44 @@ int diag_p2p_copy(int src, int dst, size_t bytes, int iters, double* gbps, unsig
   DIAG_CHECK(hipEventRecord(e0, st));
   for (int i = 0; i < iters; ++i) DIAG_CHECK(hipMemcpyPeerAsync(b.ptr, dst, a.ptr, src, nbytes, st));
   DIAG_CHECK(hipEventRecord(e1, st));
-  DIAG_CHECK(hipEventSynchronize(e1));
+  const PollDeadline dl(timeout_ms);
+  Timer tv;  // the verification's completion event lives on `dst`
+  auto hung = [&](const char* stage) {
+    a.ptr = b.ptr = cnt.ptr = nullptr;
+    tm.e0 = tm.e1 = tv.e0 = tv.e1 = nullptr;
+    tm.stream = nullptr;
+    (void)hipSetDevice(cur);
+    char msg[192];
+    std::snprintf(msg, sizeof msg, "p2p %d->%d: %s did not complete within %.0f ms (xGMI link or engine hung)", src,
+                  dst, stage, timeout_ms);
+    g_err = msg;
+    return -4;
+  };
+  hipError_t w = wait_event_polled(e1, dl);
+  if (w == hipErrorNotReady) return hung("copies");
+  DIAG_CHECK(w);
   const float ms = elapsed_ms(e0, e1);
   *gbps = ms > 0.f ? static_cast<double>(iters) * static_cast<double>(nbytes) / (ms * 1e-3) / 1e9 : 0.0;
   // verify what arrived
   DIAG_CHECK(hipSetDevice(dst));
+  DIAG_CHECK(tv.create(false));
   unsigned long long* c = static_cast<unsigned long long*>(cnt.ptr);
   hipLaunchKernelGGL(mt_verify_kernel, dim3(grid_for(dst, 4)), dim3(256), 0, nullptr,
                      static_cast<const uint4*>(b.ptr), nvec, seed, 0, c, c + 1);
   DIAG_CHECK(hipGetLastError());
+  DIAG_CHECK(hipEventRecord(tv.e0, nullptr));
+  w = wait_event_polled(tv.e0, dl);
+  if (w == hipErrorNotReady) return hung("verification");
+  DIAG_CHECK(w);
   unsigned long long h[2];
   DIAG_CHECK(hipMemcpy(h, cnt.ptr, sizeof h, hipMemcpyDeviceToHost));
   *errors = h[0];
   DIAG_CHECK(hipSetDevice(cur));
   return 0;
+}
+
+int diag_p2p_copy(int src, int dst, size_t bytes, int iters, double* gbps, unsigned long long* errors, int* peer) {
+  return diag_p2p_copy_t(src, dst, bytes, iters, 0.0, gbps, errors, peer);
 }
 
 // Matrix-core burn-in of one precision (`kind` as mfma_burn_kernel): `reps` launches of `iters`

@@ -209,6 +209,9 @@ def lib() -> ctypes.CDLL:
         L.diag_p2p_copy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                     ctypes.POINTER(ctypes.c_int)]
+        L.diag_p2p_copy_t.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
+                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
+                                      ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -600,36 +603,69 @@ def host_link(device: int = 0, mib: int = 256, iters: int = 5, scale: Scale = FU
     return _rated(res, {"h2d_gbps": h2d.value, "d2h_gbps": d2h.value}, exp, "GB/s")
 
 
-def p2p_copy(src: int, dst: int, mib: int = 256, iters: int = 5) -> Dict[str, Any]:
-    """One ordered GPU pair: copy bandwidth over xGMI (GB/s) and pattern errors on arrival."""
+P2P_HUNG = -4  # diag_p2p_copy_t: the copies (or their verification) missed the deadline
+
+
+def p2p_copy(src: int, dst: int, mib: int = 256, iters: int = 5, timeout_s: Optional[float] = None) -> Dict[str, Any]:
+    """One ordered GPU pair: copy bandwidth over xGMI (GB/s) and pattern errors on arrival.
+
+    With ``timeout_s`` the native side polls for completion and gives up at the deadline: the pair comes back
+    ``{"hung": True, ...}`` (its buffers stay allocated, as an in-flight copy may still write them) rather than
+    blocking the caller on a link that stopped making progress."""
     gbps, errs, peer = ctypes.c_double(), ctypes.c_ulonglong(), ctypes.c_int()
-    _check(lib().diag_p2p_copy(src, dst, mib << 20, iters, ctypes.byref(gbps), ctypes.byref(errs),
-                               ctypes.byref(peer)))
+    ms = 0.0 if not timeout_s else max(1.0, 1000.0 * timeout_s)
+    rc = lib().diag_p2p_copy_t(src, dst, mib << 20, iters, ms, ctypes.byref(gbps), ctypes.byref(errs),
+                               ctypes.byref(peer))
+    if rc == P2P_HUNG:
+        return {"src": src, "dst": dst, "gbps": 0.0, "errors": 0, "peer": bool(peer.value), "hung": True,
+                "detail": lib().diag_last_error().decode(errors="replace")}
+    _check(rc)
     return {"src": src, "dst": dst, "gbps": round(gbps.value, 1), "errors": errs.value, "peer": bool(peer.value)}
 
 
-def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5) -> Dict[str, Any]:
+def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5,
+               timeout_s: Optional[float] = None) -> Dict[str, Any]:
     """Every ordered pair of ``devices`` (default: all): the node's xGMI fabric, link by link.
 
     Pass: every pair has direct peer access, delivers its bytes intact, and runs at no less than
     ``P2P_MIN_FRACTION_OF_MEDIAN`` of the median pair (relative, so it holds for any hive size,
     partition mode or firmware; an absolute floor would need per-platform numbers).
+
+    ``timeout_s`` bounds the whole matrix: each pair gets what is left of it, and the first pair that hangs
+    ends the matrix (its devices are in an unknown state, with copies possibly still queued behind it), as
+    does a deadline that passes between pairs; both fail the test and name the pair.
     """
     devs = list(range(device_count())) if devices is None else list(devices)
     t0 = time.perf_counter()
     if len(devs) < 2:
         return {"pass": True, "skipped": f"{len(devs)} GPU(s): no pairs", "pairs": [], "detail": ""}
-    pairs = [p2p_copy(a, b, mib, iters) for a in devs for b in devs if a != b]
-    rates = sorted(p["gbps"] for p in pairs)
+    order = [(a, b) for a in devs for b in devs if a != b]
+    pairs: List[Dict[str, Any]] = []
+    stopped = ""
+    for a, b in order:
+        left = None if not timeout_s else timeout_s - (time.perf_counter() - t0)
+        if left is not None and left <= 0:
+            stopped = f"deadline of {timeout_s:g} s passed after {len(pairs)}/{len(order)} pairs"
+            break
+        p = p2p_copy(a, b, mib, iters) if left is None else p2p_copy(a, b, mib, iters, timeout_s=left)
+        if p.get("hung"):
+            stopped = f"{a}->{b} hung: {p['detail']}"
+            break
+        pairs.append(p)
+    rates = sorted(p["gbps"] for p in pairs) or [0.0]
     median = rates[len(rates) // 2]
     slow = [p for p in pairs if p["gbps"] < P2P_MIN_FRACTION_OF_MEDIAN * median]
     bad = [p for p in pairs if p["errors"]]
     nopeer = [p for p in pairs if not p["peer"]]
-    problems = ([f"{p['src']}->{p['dst']} {p['gbps']} GB/s" for p in slow]
+    problems = (([stopped] if stopped else [])
+                + [f"{p['src']}->{p['dst']} {p['gbps']} GB/s" for p in slow]
                 + [f"{p['src']}->{p['dst']} {p['errors']} bad words" for p in bad]
                 + [f"{p['src']}->{p['dst']} no peer access" for p in nopeer])
-    return {"pass": not problems, "pairs": pairs, "median_gbps": median, "min_gbps": rates[0],
-            "wall_s": round(time.perf_counter() - t0, 3), "detail": "; ".join(problems[:8])}
+    out = {"pass": not problems, "pairs": pairs, "median_gbps": median, "min_gbps": rates[0],
+           "wall_s": round(time.perf_counter() - t0, 3), "detail": "; ".join(problems[:8])}
+    if stopped:
+        out["stopped"] = stopped
+    return out
 
 
 LEVELS = {

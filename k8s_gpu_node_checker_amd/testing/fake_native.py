@@ -26,7 +26,9 @@ class FakeDiagLib:
                  ``gpu_rate[d]``; a list ``rates`` overrides it call by call)
     cus/mem_gib: what HIP reports per device (a CPX partition: 32 CUs)
     mfma_errors: ``{(device, kind index): wrong results}``
-    p2p_gbps:    rate of every GPU pair; ``slow_pairs[(src, dst)]`` / ``nopeer`` override pairs
+    p2p_gbps:    rate of every GPU pair; ``slow_pairs[(src, dst)]`` / ``nopeer`` override pairs; a pair in
+                 ``hung_pairs`` never completes (with a deadline: returns -4 at it; without: blocks until
+                 ``release`` is set); ``p2p_wall_s`` = wall time of each completed pair
     delay_s:     wall time of each GEMM call (the agent's per-GPU threads overlap them)
     slow_xcd:    ``{xcd: factor}`` on the burn-in's per-XCD wave time; ``bad_cu[(device, kind)]`` = the CU
                  slot its ``mfma_errors`` come from
@@ -42,7 +44,8 @@ class FakeDiagLib:
                  lds_bad: Optional[Dict[Tuple[int, int], int]] = None,
                  l2_bad: Optional[Dict[Tuple[int, int], int]] = None, slow_cu: Optional[Dict[int, float]] = None,
                  hbm_xcd_slow: Optional[Dict[int, float]] = None, hbm_bad: Optional[Dict[Tuple[int, int], int]] = None,
-                 compute_rate: Optional[Dict[int, float]] = None):
+                 compute_rate: Optional[Dict[int, float]] = None,
+                 hung_pairs: Tuple[Tuple[int, int], ...] = (), p2p_wall_s: float = 0.0):
         from ..ops import diag
         self.ref = diag.REFERENCE_RATES
         self.kinds = diag.MFMA_KINDS
@@ -62,6 +65,10 @@ class FakeDiagLib:
         self.p2p_gbps = p2p_gbps
         self.slow_pairs = dict(slow_pairs or {})
         self.nopeer = set(nopeer)
+        self.hung_pairs = set(hung_pairs)
+        self.p2p_wall_s = p2p_wall_s
+        self.p2p_timeouts_ms: List[float] = []
+        self.release = threading.Event()
         self.rc = rc
         self.err = err
         self.delay_s = delay_s
@@ -272,11 +279,23 @@ class FakeDiagLib:
         return self.rc
 
     def diag_p2p_copy(self, src, dst, nbytes, iters, gbps, errors, peer):
+        return self.diag_p2p_copy_t(src, dst, nbytes, iters, 0.0, gbps, errors, peer)
+
+    def diag_p2p_copy_t(self, src, dst, nbytes, iters, timeout_ms, gbps, errors, peer):
         with self.lock:  # node-level: runs on the agent's main thread, after the per-GPU threads
             self.calls.append(f"p2p{src}->{dst}")
+            self.p2p_timeouts_ms.append(float(timeout_ms))
         if not (0 <= src < self.n and 0 <= dst < self.n) or src == dst:
             self.err = b"p2p: invalid device pair"
             return -1
+        if (src, dst) in self.hung_pairs:
+            if timeout_ms > 0 and not self.release.wait(timeout_ms / 1000.0):
+                self.err = b"p2p %d->%d: copies did not complete within %d ms (xGMI link or engine hung)" % (
+                    src, dst, int(timeout_ms))
+                return -4
+            self.release.wait()
+        elif self.p2p_wall_s:
+            time.sleep(self.p2p_wall_s)
         _put(gbps, ctypes.c_double, self.slow_pairs.get((src, dst), self.p2p_gbps))
         _put(errors, ctypes.c_ulonglong, 0)
         _put(peer, ctypes.c_int, 0 if (src, dst) in self.nopeer else 1)

@@ -38,7 +38,7 @@ class World:
             return {"gemm": {"pass": True, "tflops": 1200.0 + len(self.runs)}}
         monkeypatch.setattr(diag, "run", run)
 
-        def p2p(devs):
+        def p2p(devs, **kw):
             self.fabric_runs += 1
             return {"pass": True, "median_gbps": 50.0, "min_gbps": 48.0, "detail": "", "wall_s": 0.1}
         monkeypatch.setattr(diag, "p2p_matrix", p2p)
@@ -393,10 +393,10 @@ def test_healthz_fails_for_a_hung_fabric_suite(monkeypatch):
     World(monkeypatch)
     release = threading.Event()
 
-    def hang(devs):
+    def hang(devs, **kw):
         release.wait(30)
         return {"pass": True}
-    monkeypatch.setattr(diag, "p2p_matrix", hang)  # the pair matrix hangs (no deadline of its own)
+    monkeypatch.setattr(diag, "p2p_matrix", hang)  # the pair matrix hangs (and ignores its deadline)
     ag = A.Agent("n", source="fake", diag_level=2, diag_interval=3600, diag_timeout=0.2)
     try:
         rep = ag.probe_once()

@@ -299,3 +299,30 @@ def test_no_device_is_a_failure_not_a_pass(fake, capsys):
     assert diag.main(["--level", "1"]) == 1
     doc = __import__("json").loads(capsys.readouterr().out)
     assert doc["pass"] is False and "no HIP devices" in doc["error"]
+
+
+def test_p2p_matrix_deadline_names_a_hung_pair_and_stops(fake):
+    """A pair whose copies never complete comes back at the deadline as a failed, named pair (the native side
+    polls its completion event) and ends the matrix; every pair gets only what is left of the budget."""
+    lib = fake(n=3, hung_pairs=((1, 0),))
+    m = diag.p2p_matrix([0, 1, 2], timeout_s=0.3)
+    assert not m["pass"] and m["stopped"].startswith("1->0 hung: p2p 1->0: copies did not complete within")
+    assert [f"{p['src']}->{p['dst']}" for p in m["pairs"]] == ["0->1", "0->2"]  # order: 0->1 0->2 1->0 ...
+    assert "1->0 hung" in m["detail"]
+    assert len(lib.p2p_timeouts_ms) == 3 and all(0 < t <= 300.0 for t in lib.p2p_timeouts_ms)
+    assert lib.p2p_timeouts_ms[2] <= lib.p2p_timeouts_ms[0]
+    assert 0.25 <= m["wall_s"] < 2.0
+
+
+def test_p2p_matrix_deadline_between_pairs(fake):
+    fake(n=3, p2p_wall_s=0.06)
+    m = diag.p2p_matrix([0, 1, 2], timeout_s=0.1)
+    assert not m["pass"] and m["stopped"].startswith("deadline of 0.1 s passed after 2/6 pairs")
+    assert len(m["pairs"]) == 2 and m["min_gbps"] == 48.0
+
+
+def test_p2p_matrix_without_a_deadline_blocks_and_with_one_passes(fake):
+    lib = fake(n=2)
+    m = diag.p2p_matrix([0, 1], timeout_s=5.0)
+    assert m["pass"] and "stopped" not in m and len(m["pairs"]) == 2
+    assert diag.p2p_matrix([0, 1])["pass"] and lib.p2p_timeouts_ms[-1] == 0.0  # no deadline: 0 to the ABI

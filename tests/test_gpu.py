@@ -454,9 +454,13 @@ def test_p2p_diag_on_this_box(dev):
         assert diag.p2p_matrix()["skipped"]
         with pytest.raises(RuntimeError, match="two distinct devices"):
             diag.p2p_copy(0, 0)
+        with pytest.raises(RuntimeError, match="two distinct devices"):  # the polled (deadline) entry point
+            diag.p2p_copy(0, 0, timeout_s=5.0)
     else:
         m = diag.p2p_matrix([0, 1], mib=64, iters=3)
         assert all(p["errors"] == 0 for p in m["pairs"]) and m["min_gbps"] > 1.0, m
+        t = diag.p2p_matrix([0, 1], mib=64, iters=3, timeout_s=60.0)  # polled completion: same result
+        assert t["pass"] and "stopped" not in t and abs(t["median_gbps"] - m["median_gbps"]) < 0.5 * m["median_gbps"]
 
 
 def test_mfma_burn_every_precision(dev):

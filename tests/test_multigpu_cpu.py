@@ -265,6 +265,22 @@ def test_hung_collective_is_aborted_and_reported_as_a_failed_rccl_row(node8):
     assert ag._fabric_thread is None  # the suite returned: nothing left holding the GPUs
 
 
+def test_hung_xgmi_pair_is_given_up_at_its_share_of_the_deadline(node8):
+    """A pair whose copies never complete (diag_p2p_copy_t polls its completion event): the matrix gives up at
+    P2P_SHARE of the watchdog, names the pair, and the RCCL suite still runs in what is left."""
+    lib, fab = node8(hung_pairs=((3, 5),))
+    ag = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8, diag_timeout=1.0)
+    t0 = time.monotonic()
+    rep = ag.probe_once()
+    assert time.monotonic() - t0 < 3
+    p2p = rep["fabric"]["p2p"]
+    assert p2p["pass"] is False and p2p["stopped"].startswith("3->5 hung: p2p 3->5: copies did not complete")
+    assert max(lib.p2p_timeouts_ms) <= A.P2P_SHARE * 1000.0
+    assert rep["fabric"]["rccl"]["pass"] and fab.closed == 1 and "watchdog" not in rep["fabric"]
+    assert any(r.startswith("xGMI p2p failed (3->5 hung") for r in ag.evaluate(rep).reasons)
+    assert ag._fabric_thread is None
+
+
 def test_node_cycle_module_over_eight_fake_gpus(node8):
     """agent/node_cycle.py (what bench.py runs on a multi-GPU job): every device diagnosed at once, the
     pair matrix and the RCCL suite, one summary."""
