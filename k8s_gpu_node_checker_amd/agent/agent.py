@@ -27,7 +27,9 @@ node-name claim of its pod-bound token) and by :class:`_OwnNodeClient` here.
 Multi-device nodes (8 GPUs, or 64 CPX partitions): per-device diagnostic threads, at most ``--diag-parallel`` at
 once, tests of shared host resources serialized (``ops/diag.SHARED_TESTS``); a diagnostic that outlives
 ``--diag-timeout`` is a failed GPU and one that outlives twice that fails ``/healthz`` (fresh process); the RCCL
-suite aborts its own communicators at its deadline (``csrc/fabric/fabric.hip``).
+suite aborts its own communicators at its deadline (``csrc/fabric/fabric.hip``) and the xGMI pair copies are
+polled against theirs (``diag_p2p_copy_t``); a node-level test given up that way is not run again in the same
+process (:func:`fabric_abandoned`).
 """
 
 from __future__ import annotations
@@ -184,6 +186,21 @@ def runtime_lost(res: Dict[str, Any]) -> Optional[str]:
     details = [str(r.get("detail", "")) for r in tests if r.get("pass") is False]
     if details and len(details) == len(tests) and all(any(m in d for m in _HIP_RUNTIME_LOST) for d in details):
         return details[0]
+    return None
+
+
+def fabric_abandoned(fab: Optional[Dict[str, Any]]) -> Optional[str]:
+    """Why a node-level suite that returned had to give a test up at its deadline (an xGMI pair whose copies
+    never completed, collectives aborted with ``ncclCommAbort``), else None.  What such a test leaves behind --
+    copies still queued on a copy engine, the buffers they target, aborted communicators' memory -- stays
+    with the process."""
+    if not isinstance(fab, dict):
+        return None
+    p2p, rccl = fab.get("p2p"), fab.get("rccl")
+    if isinstance(p2p, dict) and " hung" in str(p2p.get("stopped") or ""):
+        return f"xGMI pair test abandoned: {p2p['stopped']}"[:200]
+    if isinstance(rccl, dict) and rccl.get("aborted"):
+        return f"RCCL collectives aborted at their deadline: {rccl.get('detail') or ''}"[:200]
     return None
 
 
@@ -388,6 +405,10 @@ class Agent:
         self._fabric: Optional[Dict[str, Any]] = None
         self._fabric_at = float("-inf")
         self._fabric_thread: Optional[_DiagRun] = None  # the node-level suite's thread until it returns
+        # set when the node-level suite gave a test up at its deadline (fabric_abandoned): that suite is not run
+        # again in this process, so what the abandoned test left queued and allocated is left once, not once per
+        # --diag-interval; its failed result stays in the report until the agent is restarted
+        self.fabric_abandoned: Optional[str] = None
         self._bdf: Dict[int, str] = {}  # HIP ordinal -> PCI address (amd-smi and HIP enumerate independently)
         self.last: Optional[Dict[str, Any]] = None
         self.last_probe_done: Optional[float] = None  # monotonic time of the last completed probe (/healthz)
@@ -571,7 +592,7 @@ class Agent:
             for d in devices:
                 self._diag_skipped[d] = f"HIP runtime lost its devices ({self.hip_lost[:120]}): agent restart pending"
         if (self.diag_level >= 2 and self.devices is None and len(devices) >= 2 and not self._diag_skipped
-                and not self._diag_threads and self._fabric_thread is None
+                and not self._diag_threads and self._fabric_thread is None and self.fabric_abandoned is None
                 and now - self._fabric_at >= self.diag_interval):
             # node-level: every ordered GPU pair over xGMI (after the per-GPU tests, so no contention) and the
             # RCCL collectives; it touches every GPU, so it waits until none is busy.  On its own thread under
@@ -589,6 +610,14 @@ class Agent:
             if not r.thread.is_alive():
                 self._fabric_thread = None
                 self._fabric = r.box.get("res")
+                why = fabric_abandoned(self._fabric)
+                if why:
+                    self.fabric_abandoned = why
+                    for res in self._fabric.values():
+                        if isinstance(res, dict) and res.get("pass") is False:
+                            res["retest"] = "not re-run in this process: restart the agent to re-test"
+                    print(f"{why}; the node-level tests are not re-run until the agent restarts", file=sys.stderr,
+                          flush=True)
             else:
                 self._fabric = {"watchdog": {
                     "pass": False,

@@ -263,6 +263,7 @@ def test_hung_collective_is_aborted_and_reported_as_a_failed_rccl_row(node8):
     assert "watchdog" not in rep["fabric"] and rep["state"] == H.UNHEALTHY
     assert any(r.startswith("xGMI rccl failed (all_reduce") for r in ag.evaluate(rep).reasons)
     assert ag._fabric_thread is None  # the suite returned: nothing left holding the GPUs
+    assert ag.fabric_abandoned.startswith("RCCL collectives aborted at their deadline")
 
 
 def test_hung_xgmi_pair_is_given_up_at_its_share_of_the_deadline(node8):
@@ -279,6 +280,17 @@ def test_hung_xgmi_pair_is_given_up_at_its_share_of_the_deadline(node8):
     assert rep["fabric"]["rccl"]["pass"] and fab.closed == 1 and "watchdog" not in rep["fabric"]
     assert any(r.startswith("xGMI p2p failed (3->5 hung") for r in ag.evaluate(rep).reasons)
     assert ag._fabric_thread is None
+    # what the hung pair left (queued copies, their buffers) stays with the process: the node-level suite is
+    # not run again here -- the failed result stays, marked, until a restart re-tests
+    assert ag.fabric_abandoned.startswith("xGMI pair test abandoned: 3->5 hung")
+    assert p2p["retest"].startswith("not re-run in this process")
+    pairs = sum(1 for c in lib.calls if c.startswith("p2p"))
+    ag._fabric_at -= 2 * ag.diag_interval
+    for d in list(ag._diag_at):
+        ag._diag_at[d] -= 2 * ag.diag_interval
+    rep2 = ag.probe_once()
+    assert sum(1 for c in lib.calls if c.startswith("p2p")) == pairs and fab.opened == [list(range(8))]
+    assert rep2["fabric"]["p2p"]["pass"] is False and rep2["state"] == H.UNHEALTHY
 
 
 def test_node_cycle_module_over_eight_fake_gpus(node8):
