@@ -334,17 +334,26 @@ class Connection:
 
     def _read_head(self) -> Tuple[int, str, List[Tuple[str, str]], Dict[str, str]]:
         while True:
-            status_line = self._read_line()
+            # the whole header block at once (one find for its end, one split) rather than line by line
+            buf = self._buf
+            end = buf.find(b"\r\n\r\n")
+            while end < 0:
+                seen = len(buf)
+                if not self._recv_more():
+                    raise HTTPError("aborted", "('Connection aborted.', RemoteDisconnected("
+                                               "'Remote end closed connection without response'))")
+                buf = self._buf
+                end = buf.find(b"\r\n\r\n", max(0, seen - 3))
+            lines = bytes(buf[:end]).split(b"\r\n")
+            del buf[:end + 4]
+            status_line = lines[0]
             parts = status_line.split(None, 2)
             if len(parts) < 2 or not parts[0].startswith(b"HTTP/"):
                 raise HTTPError("protocol", f"bad status line {status_line[:80]!r}")
             status = int(parts[1])
             reason = parts[2].decode("latin-1") if len(parts) > 2 else ""
             headers: List[Tuple[str, str]] = []
-            while True:
-                line = self._read_line()
-                if not line:
-                    break
+            for line in lines[1:]:
                 k, _, v = line.partition(b":")
                 headers.append((k.decode("latin-1").strip(), v.decode("latin-1").strip()))
             if 100 <= status < 200 and status != 101:

@@ -47,8 +47,9 @@ def _slow(url: str) -> SplitURL:
 
 def split(url: str) -> SplitURL:
     """``urlsplit(url)`` -> scheme, hostname (lower case, IPv6 without brackets), port, path, query."""
-    if not url.isascii() or "@" in url or "%" in url or "#" in url or "\\" in url or \
-            any(ord(c) <= 32 or ord(c) == 127 for c in url):
+    # ASCII and printable without space = no byte <= 32 and no DEL (127)
+    if not url.isascii() or not url.isprintable() or " " in url or "@" in url or "%" in url or "#" in url or \
+            "\\" in url:
         return _slow(url)
     scheme, sep, rest = url.partition("://")
     if not sep or not scheme.isalpha():
