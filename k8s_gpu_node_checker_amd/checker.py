@@ -223,7 +223,7 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
                 if reeval:
                     unapplied.append(node["name"])
             else:
-                if rep is None:
+                if rep is None and ex.health_annotation:
                     rep = ex.report()
                 other = rep.get("node") if isinstance(rep, dict) else None
                 if other is not None and other != node["name"]:
