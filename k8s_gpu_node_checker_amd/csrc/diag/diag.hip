@@ -47,6 +47,7 @@ thread_local std::string g_err;
 // GEMM knobs are per calling thread: the node agent runs one diagnostic thread per GPU at once, and a
 // test or tool that switches a variant must not change what another GPU's thread launches.
 thread_local int g_gemm_variant = 0;
+thread_local int g_gemm_schedule = 1;  // v3 restaging order (V3_PHASE): 1 = LDS-DMA pieces per phase 0/2/2/4, 0 = 2/0/4/2
 thread_local int g_gemm_buffer_loads = 0;  // v3 operand staging: 0 = global_load_lds, 1 = buffer_load ... lds
 thread_local int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3
                                        // kernels; measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
@@ -307,10 +308,11 @@ gemm_bf16_v2_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
 // A(m1), phase 3 reuses B(n0) from registers.  A stage is restaged region by region (16 KiB each):
 // R0 = A rows of m0, R1 = B rows of n0, R2 = B rows of n1, R3 = A rows of m1.  Reads retire after
 // the barrier that closes their load slot, so a region read in phase p is free two phases later:
-// R0/R1 of tile t+2 go out in phase 2 of tile t, R2 in phase 3, and R3 of tile t+1 (other buffer,
-// last read in phase 2 of tile t-1) in phase 0.  Tile t+1 is retired at phase 3 of tile t with a
-// counted vmcnt(6) (tile t+2's R0-R2 may stay in flight); raw s_barrier only -- __syncthreads()
-// would drain the in-flight LDS-DMA with vmcnt(0).
+// R0 of tile t+2 goes out in phase 2 of tile t, R1 and R2 in phase 3, and R3 of tile t+1 (other
+// buffer, last read in phase 2 of tile t-1) in phase 1 (V3_PHASE: which phase carries which piece
+// is worth 4-9 %).  Tile t+1 is retired at phase 3 of tile t with a counted vmcnt(6) (tile t+2's
+// R0-R2 may stay in flight); raw s_barrier only -- __syncthreads() would drain the in-flight
+// LDS-DMA with vmcnt(0).
 #define STG_BARRIER()                  \
   do {                                 \
     __builtin_amdgcn_sched_barrier(0); \
@@ -469,11 +471,23 @@ struct StgFrags<DT_FP4> {
   u32x4 a[4][2], b0[2][2], b1[2][2];
 };
 
+// v3 restaging orders (region r = 0: A rows of m0, 1: B rows of n0, 2: B rows of n1, 3: A rows of m1).
+// V3_PHASE[s][r]: the phase of a K-tile whose load slot issues region r, for tile kt+2 into this buffer (R0/R1
+// are free from phase 2 on, R2 from phase 3) or, R3, tile kt+1 into the other one (free since tile kt-1).
+// Phase 3 retires tile kt+1 with vmcnt(6): tile kt+2's R0-R2 (2 pieces each) may stay in flight.
+//   0: R3@0, R0 R1@2, R2@3 -> LDS-DMA pieces per phase 2/0/4/2 (round-2/3 kernel)
+//   1: R3@1, R0@2, R1 R2@3 -> 0/2/2/4: no DMA issue beside phase 0's 12 fragment reads, 2 beside phase 2's 8
+// An LDS-DMA piece costs 60-185 issue cycles depending on what else its slot does, and a load slot that outruns
+// the other group's 256-cycle MFMA slot stalls both: schedule 1 is 4-9 % faster on MI355X (bf16 and MX-fp8,
+// 4096^3 / 8192^3, tools/gemm_schedule_ab.py -> profiles/gemm_schedule_ab_mi355x.jsonl; orders 2/2/2/2,
+// 0/4/2/2, 0/2/0/6 and DMA between the MFMAs of phase 3 measured in between or below it).
+__device__ constexpr int V3_PHASE[2][4] = {{2, 2, 3, 0}, {2, 3, 3, 1}};
+
 // DT_BF16: bf16 A[M][K] . Bt[N][K]^T.  DT_FP8 / DT_FP4: MX operands (E4M3 bytes / packed E2M1 pairs,
 // unit scales) passed as K = row bytes / 2 "bf16 columns", so the byte-identical LDS-DMA staging is
 // shared (a 64-column bf16 K-tile is a 128-byte fp8 or fp4 K-tile); only the swizzle (fp8), the
 // fragment reads and the MFMA differ.
-template <int DT, bool EPI_LDS = false, bool BUF = false>
+template <int DT, bool EPI_LDS = false, bool BUF = false, int SCHED = 1>
 __global__ void __launch_bounds__(V2_THREADS, 1)
 gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
                int K) {
@@ -530,11 +544,20 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     const u32x4* a_img = reinterpret_cast<const u32x4*>(cur);
     const u32x4* b_img = reinterpret_cast<const u32x4*>(cur + V2_BM * BK * 2);
     const bool pre = kt + 2 < KT;
-    // phase 0: A(m0), B(n0); R3 of tile kt+1 (tile 1 came whole with the prologue)
-    if (kt >= 1 && kt + 1 < KT) {
-      region(nxt, kt + 1, 3, 0);
-      region(nxt, kt + 1, 3, 1);
-    }
+    // the phase's restaging (V3_PHASE): R0-R2 of tile kt+2 into this buffer, R3 of tile kt+1 into the other
+    // (tile 1 came whole with the prologue)
+    auto restage = [&](int phase) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (V3_PHASE[SCHED][r] != phase) continue;
+        if (r == 3 ? (kt >= 1 && kt + 1 < KT) : pre) {
+          region(r == 3 ? nxt : cur, kt + (r == 3 ? 1 : 2), r, 0);
+          region(r == 3 ? nxt : cur, kt + (r == 3 ? 1 : 2), r, 1);
+        }
+      }
+    };
+    // phase 0: A(m0), B(n0)
+    restage(0);
 #pragma unroll
     for (int n = 0; n < 2; ++n) stg_load(f.b0[n], b_img, wc * 64 + n * 16 + frow, fq);
 #pragma unroll
@@ -544,29 +567,24 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     stg_mfma(acc, f.a, f.b0, 0, 0);
     STG_BARRIER();
     // phase 1: B(n1)
+    restage(1);
 #pragma unroll
     for (int n = 0; n < 2; ++n) stg_load(f.b1[n], b_img, wc * 64 + (n + 2) * 16 + frow, fq);
     STG_BARRIER();
     __builtin_amdgcn_s_waitcnt(0xc07f);
     stg_mfma(acc, f.a, f.b1, 0, 2);
     STG_BARRIER();
-    // phase 2: A(m1); restage R0, R1 with tile kt+2
-    if (pre) {
-      region(cur, kt + 2, 0, 0);
-      region(cur, kt + 2, 0, 1);
-      region(cur, kt + 2, 1, 0);
-      region(cur, kt + 2, 1, 1);
-    }
+    // phase 2: A(m1)
+    restage(2);
 #pragma unroll
     for (int m = 0; m < 4; ++m) stg_load(f.a[m], a_img, wr * 128 + (m + 4) * 16 + frow, fq);
     STG_BARRIER();
     __builtin_amdgcn_s_waitcnt(0xc07f);
     stg_mfma(acc, f.a, f.b1, 4, 2);
     STG_BARRIER();
-    // phase 3: no LDS reads; restage R2, retire tile kt+1
+    // phase 3: no LDS reads; retire tile kt+1 (tile kt+2's pieces may stay in flight)
+    restage(3);
     if (pre) {
-      region(cur, kt + 2, 2, 0);
-      region(cur, kt + 2, 2, 1);
       __builtin_amdgcn_s_waitcnt(0x3f76);  // vmcnt(6)
     } else {
       __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
@@ -1064,27 +1082,30 @@ hipError_t enable_peer(int from, int to) {
   return e;
 }
 
-template <int DT, bool EPI, bool BUF>
+template <int DT, bool EPI, bool BUF, int SCHED = 1>
 int launch_v3_inst(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
   static LdsAttrOnce attr;
-  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI, BUF>), 2 * V2_STAGE_BYTES,
-                         "gemm v3") != 0)
+  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI, BUF, SCHED>),
+                         2 * V2_STAGE_BYTES, "gemm v3") != 0)
     return -1;
   const int nwg = (M / V2_BM) * (N / V2_BN);
-  hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI, BUF>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, stream,
+  hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI, BUF, SCHED>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, stream,
                      static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, M, N, Kcols);
   return 0;
 }
 
 // v3 launch (M, N multiples of 256; Kcols = bf16 columns, K8 / 2 for fp8), epilogue per g_gemm_epilogue,
-// operand staging per g_gemm_buffer_loads
+// operand staging per g_gemm_buffer_loads, restaging order per g_gemm_schedule (the buffer path: order 1)
 template <int DT>
 int launch_v3(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
   if (g_gemm_buffer_loads)
     return g_gemm_epilogue ? launch_v3_inst<DT, true, true>(A, Bt, C, M, N, Kcols, stream)
                            : launch_v3_inst<DT, false, true>(A, Bt, C, M, N, Kcols, stream);
-  return g_gemm_epilogue ? launch_v3_inst<DT, true, false>(A, Bt, C, M, N, Kcols, stream)
-                         : launch_v3_inst<DT, false, false>(A, Bt, C, M, N, Kcols, stream);
+  if (g_gemm_schedule == 0)
+    return g_gemm_epilogue ? launch_v3_inst<DT, true, false, 0>(A, Bt, C, M, N, Kcols, stream)
+                           : launch_v3_inst<DT, false, false, 0>(A, Bt, C, M, N, Kcols, stream);
+  return g_gemm_epilogue ? launch_v3_inst<DT, true, false, 1>(A, Bt, C, M, N, Kcols, stream)
+                         : launch_v3_inst<DT, false, false, 1>(A, Bt, C, M, N, Kcols, stream);
 }
 
 }  // namespace
@@ -1122,6 +1143,8 @@ const char* diag_last_error(void) { return g_err.c_str(); }
 void diag_set_gemm_variant(int v) { g_gemm_variant = v; }
 void diag_set_gemm_epilogue(int e) { g_gemm_epilogue = e; }
 void diag_set_gemm_buffer_loads(int b) { g_gemm_buffer_loads = b; }
+void diag_set_gemm_schedule(int s) { g_gemm_schedule = s; }
+int diag_get_gemm_schedule(void) { return g_gemm_schedule; }
 int diag_get_gemm_variant(void) { return g_gemm_variant; }
 int diag_get_gemm_epilogue(void) { return g_gemm_epilogue; }
 int diag_get_gemm_buffer_loads(void) { return g_gemm_buffer_loads; }

@@ -27,11 +27,14 @@ from .native import NativeUnavailable, load_cdll
 # SPX/NPS1, 1400 W cap): the lower of (a) the median of a sustained soak and (b) what one cold run
 # measures, since the agent runs the suite once per --diag-interval on an idle (clocked-down) GPU:
 #   8192^3 (level 2): profiles/soak_level2_5min_mi355x.json, 589 rounds of the full level-2 suite in 5 min
-#       gemm 1208 (min 1192), gemm_fp8 2343 (min 2110), hbm copy 6.55 / read 6.98 TB/s, mfma bf16 1901,
-#       fp8 1940, mxfp8 4326, mxfp4 7610 TFLOP/s, host link h2d 57.2 / d2h 56.8 GB/s
-#   4096^3 (level 1): profiles/soak_level1_mi355x.json, 970 rounds in 2 min: gemm 1329 warm but 1207-1226
-#       in single cold runs (profiles/bench/*.json probe.diag), gemm_fp8 2274 warm / 2098-2108 cold,
-#       hbm copy 6.49 / read 6.96 TB/s, mfma bf16 1978, fp8 2009, mxfp8 4493, mxfp4 7834
+#       hbm copy 6.55 / read 6.98 TB/s, mfma bf16 1901, fp8 1940, mxfp8 4326, mxfp4 7610 TFLOP/s, host link
+#       h2d 57.2 / d2h 56.8 GB/s; the GEMMs since the v3 restaging order 1 (round 3):
+#       profiles/soak_level2_sched1_mi355x.json (314 rounds, 3 min) gemm 1232 (min 1214), gemm_fp8 2440
+#       (min 2337); cold single runs (profiles/diag_cold_sched1_mi355x.jsonl) 1228-1240 / 2376-2457
+#   4096^3 (level 1): profiles/soak_level1_mi355x.json, 970 rounds in 2 min: hbm copy 6.49 / read 6.96 TB/s,
+#       mfma bf16 1978, fp8 2009, mxfp8 4493, mxfp4 7834; GEMMs with order 1:
+#       profiles/soak_level1_sched1_mi355x.json (963 rounds, 3 min) gemm 1343 warm but 1275-1294 in single
+#       cold runs, gemm_fp8 2300 warm / 2208-2242 cold (order 0 measured 1207-1226 / 2098-2108 cold)
 # A result below FAIL_FRACTION of its reference fails (a GPU at 55 % clock or power is unhealthy); one
 # between FAIL_FRACTION and DEGRADED_FRACTION passes as *degraded* (a warning on the node, still Ready).
 # The 85 % floor sits under every soak minimum (worst: gemm_fp8 8192^3 at 90 % of its median) and under
@@ -66,8 +69,8 @@ DEGRADED_FRACTION = 0.95
 FULL_CUS = 256
 FULL_MEM_BYTES = 288 << 30
 REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
-    "gemm": {4096: 1220.0, 8192: 1208.0},          # bf16 MFMA GEMM, TFLOP/s
-    "gemm_fp8": {4096: 2100.0, 8192: 2343.0},      # MX-fp8 GEMM, TFLOP/s
+    "gemm": {4096: 1280.0, 8192: 1228.0},          # bf16 MFMA GEMM, TFLOP/s
+    "gemm_fp8": {4096: 2210.0, 8192: 2380.0},      # MX-fp8 GEMM, TFLOP/s
     "hbm": {"copy_tbs": 6.49, "read_tbs": 6.96},   # 16-byte copy (read + write bytes counted) / read, TB/s
     "mfma": {"bf16": 1901.0, "fp8": 1940.0, "mxfp8": 4326.0, "mxfp4": 7610.0},  # register-resident burn-in
     "host_link": {"h2d_gbps": 57.0, "d2h_gbps": 56.8},  # pinned copies over PCIe Gen5 x16
@@ -174,7 +177,9 @@ def lib() -> ctypes.CDLL:
         L.diag_set_gemm_variant.argtypes = [ctypes.c_int]
         L.diag_set_gemm_epilogue.argtypes = [ctypes.c_int]
         L.diag_set_gemm_buffer_loads.argtypes = [ctypes.c_int]
-        for getter in ("diag_get_gemm_variant", "diag_get_gemm_epilogue", "diag_get_gemm_buffer_loads"):
+        L.diag_set_gemm_schedule.argtypes = [ctypes.c_int]
+        for getter in ("diag_get_gemm_variant", "diag_get_gemm_epilogue", "diag_get_gemm_buffer_loads",
+                       "diag_get_gemm_schedule"):
             getattr(L, getter).restype = ctypes.c_int
         L.diag_device_count.restype = ctypes.c_int
         L.diag_device_arch.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
@@ -255,14 +260,23 @@ def set_gemm_buffer_loads(buffer_loads: bool) -> None:
     lib().diag_set_gemm_buffer_loads(1 if buffer_loads else 0)
 
 
+def set_gemm_schedule(schedule: int) -> None:
+    """v3 kernels: the K-tile phase that issues each LDS-DMA restaging piece (``V3_PHASE`` in diag.hip):
+    1 (default) = 0/2/2/4 pieces over the four phases, 0 = the earlier 2/0/4/2 order, kept for A/B."""
+    if schedule not in (0, 1):
+        raise ValueError(f"gemm schedule must be 0 or 1, not {schedule!r}")
+    lib().diag_set_gemm_schedule(schedule)
+
+
 def get_gemm_config() -> Dict[str, Any]:
     """The calling thread's GEMM knobs (they are thread-local in the library: every agent thread
-    starts from the production defaults ``auto`` / LDS-staged epilogue / ``global_load_lds``)."""
+    starts from the production defaults ``auto`` / LDS-staged epilogue / ``global_load_lds`` / schedule 1)."""
     L = lib()
     inv = {v: k for k, v in GEMM_VARIANTS.items()}
     return {"variant": inv.get(int(L.diag_get_gemm_variant()), "auto"),
             "epilogue": bool(L.diag_get_gemm_epilogue()),
-            "buffer_loads": bool(L.diag_get_gemm_buffer_loads())}
+            "buffer_loads": bool(L.diag_get_gemm_buffer_loads()),
+            "schedule": int(L.diag_get_gemm_schedule())}
 
 
 def get_gemm_epilogue() -> bool:
@@ -274,8 +288,8 @@ class gemm_config:
     and restore the previous values on exit (not the library defaults)."""
 
     def __init__(self, variant: Optional[str] = None, epilogue: Optional[bool] = None,
-                 buffer_loads: Optional[bool] = None):
-        self.want = {"variant": variant, "epilogue": epilogue, "buffer_loads": buffer_loads}
+                 buffer_loads: Optional[bool] = None, schedule: Optional[int] = None):
+        self.want = {"variant": variant, "epilogue": epilogue, "buffer_loads": buffer_loads, "schedule": schedule}
         self.saved: Dict[str, Any] = {}
 
     @staticmethod
@@ -286,6 +300,8 @@ class gemm_config:
             set_gemm_epilogue(cfg["epilogue"])
         if cfg.get("buffer_loads") is not None:
             set_gemm_buffer_loads(cfg["buffer_loads"])
+        if cfg.get("schedule") is not None:
+            set_gemm_schedule(cfg["schedule"])
 
     def __enter__(self) -> "gemm_config":
         self.saved = get_gemm_config()

@@ -180,11 +180,45 @@ def test_v3_buffer_load_staging_matches(dev, m, n, k):
             assert rel < 1e-4 * max(1, k / 512), rel
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (768, 512, 320),
+                                   (1024, 768, 4096), (2048, 2048, 2048)])
+def test_v3_restaging_schedules_compute_the_same(dev, m, n, k):
+    """Both LDS-DMA restaging orders of the v3 pipeline (schedule 1, the default, and the earlier 0) give
+    bit-identical outputs for bf16 and MX-fp8, including 1-5 K-tiles (prologue / tail paths), and match torch."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + 5 * n + 11 * k)
+    st = torch.cuda.current_stream().cuda_stream
+    a = torch.randn(m, k, device=dev, generator=g)
+    bt = torch.randn(n, k, device=dev, generator=g)
+    for (x, y, launch) in ((a.to(torch.bfloat16), bt.to(torch.bfloat16), diag.gemm_launch),
+                           (a.to(torch.float8_e4m3fn), bt.to(torch.float8_e4m3fn), diag.gemm_fp8_launch)):
+        if launch is diag.gemm_fp8_launch and k % 128:
+            continue
+        outs = []
+        for sched in (0, 1):
+            with diag.gemm_config(variant="v3", schedule=sched):
+                c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+                launch(x.data_ptr(), y.data_ptr(), c.data_ptr(), m, n, k, st)
+                torch.cuda.synchronize()
+                outs.append(c)
+        assert torch.equal(outs[0], outs[1])
+        if launch is diag.gemm_launch:
+            ref = x.float() @ y.float().t()
+            rel = ((outs[1] - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
+            assert rel < 1e-4 * max(1, k / 512), rel
+        else:
+            ref = x.double() @ y.double().t()
+            mag = x.double().abs() @ y.double().abs().t()
+            assert ((outs[1].double() - ref).abs() / mag.clamp_min(1e-30)).max().item() < diag.GEMM_FP8_MAX_ERR
+    with pytest.raises(ValueError):
+        diag.set_gemm_schedule(2)
+
+
 def test_mfma_gemm_large_auto_uses_v3_and_matches(dev):
     """4096^3 in auto mode runs the staggered v3 kernel; compare every output with a bf16-input,
     fp32-accumulate torch reference.  Runs with the production knobs (what the agent launches)."""
     from k8s_gpu_node_checker_amd.ops import diag
-    assert diag.get_gemm_config() == {"variant": "auto", "epilogue": True, "buffer_loads": False}
+    assert diag.get_gemm_config() == {"variant": "auto", "epilogue": True, "buffer_loads": False, "schedule": 1}
     m = n = k = 4096
     g = torch.Generator(device=dev).manual_seed(4096)
     a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
@@ -634,7 +668,7 @@ def test_gemm_knobs_are_thread_local_and_concurrent_threads_agree(dev):
             t.join(60)
         assert diag.get_gemm_config()["variant"] == "v1"  # this thread's own setting survives
     assert not errs, errs
-    assert seen == [{"variant": "auto", "epilogue": True, "buffer_loads": False}] * 4
+    assert seen == [{"variant": "auto", "epilogue": True, "buffer_loads": False, "schedule": 1}] * 4
     for c in outs:
         rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
         assert rel < 1e-4 * (k / 512), rel

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""v3 GEMM restaging-order A/B (``diag_set_gemm_schedule``), with torch/hipBLASLt in the same rounds.
+
+Schedule 0 issues the LDS-DMA pieces of a K-tile 2/0/4/2 over its four phases, schedule 1 issues them 0/2/2/4,
+so no phase carries both the largest fragment-read load (phase 0: 12 ``ds_read_b128``) and DMA issue, and the
+phase with 8 reads carries 2 pieces instead of 4.  Interleaved rounds in one process on the same random
+operands, every variant's full output checked against torch; one JSON line per (dtype, size).
+
+    python tools/gemm_schedule_ab.py --rounds 7
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from k8s_gpu_node_checker_amd.ops import diag  # noqa: E402
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--sizes", default="4096,8192")
+    ap.add_argument("--schedules", default="0,1")
+    args = ap.parse_args()
+    L = diag.lib()
+    scheds = [int(x) for x in args.schedules.split(",")]
+    st = torch.cuda.current_stream().cuda_stream
+    diag.set_gemm_epilogue(True)
+    diag.set_gemm_buffer_loads(False)
+    for n in (int(x) for x in args.sizes.split(",")):
+        iters = 40 if n <= 4096 else 15
+        g = torch.Generator(device="cuda").manual_seed(n)
+        a = torch.rand(n, n, device="cuda", generator=g) * 2 - 1
+        b = torch.rand(n, n, device="cuda", generator=g) * 2 - 1
+        c = torch.empty(n, n, device="cuda")
+        ops = {
+            "bf16": (a.to(torch.bfloat16), b.to(torch.bfloat16), diag.gemm_launch, n),
+            "mxfp8": (a.to(torch.float8_e4m3fn), b.to(torch.float8_e4m3fn), diag.gemm_fp8_launch, n),
+        }
+        for name, (x, y, launch, k) in ops.items():
+            ref = x.float() @ y.float().t()
+            res = {}
+            for sc in scheds:
+                L.diag_set_gemm_schedule(sc)
+                c.fill_(float("nan"))
+                launch(x.data_ptr(), y.data_ptr(), c.data_ptr(), n, n, k, st)
+                torch.cuda.synchronize()
+                res[sc] = {"err": ((c - ref).abs().max() / ref.abs().max()).item(), "tf": []}
+            lib_tf = []
+            yt = y.t()
+            for _ in range(args.rounds):
+                for sc in scheds:
+                    L.diag_set_gemm_schedule(sc)
+                    ms = timed(lambda: launch(x.data_ptr(), y.data_ptr(), c.data_ptr(), n, n, k, st), iters)
+                    res[sc]["tf"].append(2.0 * n * n * k / ms / 1e9)
+                if name == "bf16":
+                    ms = timed(lambda: torch.matmul(x, yt), iters)
+                    lib_tf.append(2.0 * n * n * k / ms / 1e9)
+            L.diag_set_gemm_schedule(0)
+            out = {"dtype": name, "size": n}
+            for sc in scheds:
+                tf = res[sc]["tf"]
+                out[f"schedule{sc}"] = {"median_tflops": round(statistics.median(tf), 1),
+                                        "best_tflops": round(max(tf), 1), "max_err_vs_torch": res[sc]["err"]}
+            if lib_tf:
+                out["torch_hipblaslt_bf16_out"] = {"median_tflops": round(statistics.median(lib_tf), 1)}
+            print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
