@@ -483,6 +483,23 @@ struct StgFrags<DT_FP4> {
 // 0/4/2/2, 0/2/0/6 and DMA between the MFMAs of phase 3 measured in between or below it).
 __device__ constexpr int V3_PHASE[2][4] = {{2, 2, 3, 0}, {2, 3, 3, 1}};
 
+// In-kernel stamps of the v3 schedule (a diagnostic build only: -DDIAG_GEMM_STAMPS, tools/gemm_stamps.py).
+// Lane 0 of wave 0 (group 0) and wave 4 (group 1) of the first 8 workgroups record s_memtime at four points
+// of each phase of the middle K-tile -- load slot start, MFMA slot start, MFMA issue done, slot end -- into a
+// buffer of their own that nothing else reads.  The production build compiles the macro to nothing.
+#ifdef DIAG_GEMM_STAMPS
+__device__ unsigned long long g_gemm_stamps[8][2][4][4];
+#define V3_STAMP(p, q)                                                                                   \
+  do {                                                                                                 \
+    if (kt == KT / 2 && blockIdx.x < 8 && lane == 0 && (wid == 0 || wid == 4))                          \
+      g_gemm_stamps[blockIdx.x][wid >> 2][p][q] = __builtin_amdgcn_s_memtime();                         \
+  } while (0)
+#else
+#define V3_STAMP(p, q) \
+  do {                 \
+  } while (0)
+#endif
+
 // DT_BF16: bf16 A[M][K] . Bt[N][K]^T.  DT_FP8 / DT_FP4: MX operands (E4M3 bytes / packed E2M1 pairs,
 // unit scales) passed as K = row bytes / 2 "bf16 columns", so the byte-identical LDS-DMA staging is
 // shared (a 64-column bf16 K-tile is a 128-byte fp8 or fp4 K-tile); only the swizzle (fp8), the
@@ -557,32 +574,45 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
       }
     };
     // phase 0: A(m0), B(n0)
+    V3_STAMP(0, 0);
     restage(0);
 #pragma unroll
     for (int n = 0; n < 2; ++n) stg_load(f.b0[n], b_img, wc * 64 + n * 16 + frow, fq);
 #pragma unroll
     for (int m = 0; m < 4; ++m) stg_load(f.a[m], a_img, wr * 128 + m * 16 + frow, fq);
     STG_BARRIER();
+    V3_STAMP(0, 1);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     stg_mfma(acc, f.a, f.b0, 0, 0);
+    V3_STAMP(0, 2);
     STG_BARRIER();
+    V3_STAMP(0, 3);
     // phase 1: B(n1)
+    V3_STAMP(1, 0);
     restage(1);
 #pragma unroll
     for (int n = 0; n < 2; ++n) stg_load(f.b1[n], b_img, wc * 64 + (n + 2) * 16 + frow, fq);
     STG_BARRIER();
+    V3_STAMP(1, 1);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     stg_mfma(acc, f.a, f.b1, 0, 2);
+    V3_STAMP(1, 2);
     STG_BARRIER();
+    V3_STAMP(1, 3);
     // phase 2: A(m1)
+    V3_STAMP(2, 0);
     restage(2);
 #pragma unroll
     for (int m = 0; m < 4; ++m) stg_load(f.a[m], a_img, wr * 128 + (m + 4) * 16 + frow, fq);
     STG_BARRIER();
+    V3_STAMP(2, 1);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     stg_mfma(acc, f.a, f.b1, 4, 2);
+    V3_STAMP(2, 2);
     STG_BARRIER();
+    V3_STAMP(2, 3);
     // phase 3: no LDS reads; retire tile kt+1 (tile kt+2's pieces may stay in flight)
+    V3_STAMP(3, 0);
     restage(3);
     if (pre) {
       __builtin_amdgcn_s_waitcnt(0x3f76);  // vmcnt(6)
@@ -590,8 +620,11 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
       __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
     }
     STG_BARRIER();
+    V3_STAMP(3, 1);
     stg_mfma(acc, f.a, f.b0, 4, 0);
+    V3_STAMP(3, 2);
     STG_BARRIER();
+    V3_STAMP(3, 3);
   }
   if (wr == 0) STG_BARRIER();  // balance the stagger
   const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 64;
@@ -1148,6 +1181,15 @@ int diag_get_gemm_schedule(void) { return g_gemm_schedule; }
 int diag_get_gemm_variant(void) { return g_gemm_variant; }
 int diag_get_gemm_epilogue(void) { return g_gemm_epilogue; }
 int diag_get_gemm_buffer_loads(void) { return g_gemm_buffer_loads; }
+
+#ifdef DIAG_GEMM_STAMPS
+// the stamps of the last v3 launch (8 x 2 x 4 x 4 64-bit clock values, diagnostic build only)
+int diag_gemm_stamps(unsigned long long* out) {
+  DIAG_CHECK(hipDeviceSynchronize());
+  DIAG_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gemm_stamps), sizeof(g_gemm_stamps)));
+  return 0;
+}
+#endif
 
 int diag_device_count(void) {
   int n = 0;
