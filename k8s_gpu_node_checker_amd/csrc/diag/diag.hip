@@ -504,7 +504,7 @@ __device__ unsigned long long g_gemm_stamps[8][2][4][4];
 // unit scales) passed as K = row bytes / 2 "bf16 columns", so the byte-identical LDS-DMA staging is
 // shared (a 64-column bf16 K-tile is a 128-byte fp8 or fp4 K-tile); only the swizzle (fp8), the
 // fragment reads and the MFMA differ.
-template <int DT, bool EPI_LDS = false, bool BUF = false, int SCHED = 1>
+template <int DT, bool EPI_LDS = false, bool BUF = false, int SCHED = 1, bool PRIO_G1 = DT == DT_BF16>
 __global__ void __launch_bounds__(V2_THREADS, 1)
 gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
                int K) {
@@ -553,6 +553,13 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
   }
   STG_BARRIER();
   if (wr == 1) STG_BARRIER();  // the stagger
+  // bf16: the second wave group (waves 4-7, one barrier behind) issues at raised priority for the whole loop,
+  // so on each SIMD its load slot is not starved behind the other group's MFMA stream (+2-3 % at 4096^3 and
+  // 8192^3; neutral-to-negative for MX-fp8, profiles/gemm_schedule_ab_mi355x.jsonl); per-slot priority flips
+  // measured below it
+  if constexpr (PRIO_G1) {
+    if (wr == 1) __builtin_amdgcn_s_setprio(1);
+  }
 
   StgFrags<DT> f;
   for (int kt = 0; kt < KT; ++kt) {
