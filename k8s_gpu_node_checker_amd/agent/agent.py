@@ -979,61 +979,71 @@ def main(argv: Optional[List[str]] = None) -> int:
                   gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)), label_node=args.label_node,
                   annotation_encoding=args.annotation_encoding, diag_parallel=args.diag_parallel)
     client = None
-    if "annotation" in pubs:
-        from ..kube.client import KubeClient
-        from ..kube.config import load_kube_config
-        conn = load_kube_config(args.kubeconfig)
-        tok = conn.token
-        if conn.token_file:
-            try:
-                with open(conn.token_file, encoding="utf-8") as f:
-                    tok = f.read()
-            except OSError:
-                pass
-        bound = token_node_name(tok)
-        if bound is not None and bound != args.node:
-            # deploy/agent-policy.yaml would refuse every write anyway; say why at start-up instead
-            print(f"--node {args.node!r} is not the node this pod's ServiceAccount token is bound to ({bound!r}): "
-                  "refusing to publish another node's status", file=sys.stderr, flush=True)
-            return 2
-        client = KubeClient(conn, timeout=10.0)
-        try:  # the node's registered GPU count; refreshed from every condition PATCH response after this
-            agent.observe_node(client.get_node(args.node))
-        except Exception as e:
-            print(f"could not read node {args.node}: {e}", file=sys.stderr, flush=True)
-    if "http" in pubs:
-        host, _, port = args.listen.rpartition(":")
-        # a probe cycle may legitimately include diagnostics (up to --diag-timeout per GPU)
-        if bool(args.tls_cert_file) != bool(args.tls_key_file) or (args.tls_client_ca and not args.tls_cert_file):
-            print("--tls-cert-file and --tls-key-file go together (and --tls-client-ca needs them)", file=sys.stderr,
-                  flush=True)
-            return 2
-        tls = tls_context(args.tls_cert_file, args.tls_key_file, args.tls_client_ca) if args.tls_cert_file else None
-        serve(agent, host or "0.0.0.0", int(port), stale_after=max(180.0, 3 * args.interval + args.diag_timeout),
-              tls=tls, require_client_cert=bool(args.tls_client_ca))
-    # SIGTERM (pod deletion, rolling update): finish the cycle in flight and leave with 0 instead of dying
-    # mid-write; the condition keeps its last heartbeat and ages out at the checker's --probe-max-age
-    stop = threading.Event()
-    if threading.current_thread() is threading.main_thread():
-        import signal
-        signal.signal(signal.SIGTERM, lambda *_: stop.set())
-    while not stop.is_set():
-        started = time.monotonic()
-        rep = agent.probe_once()
-        if "stdout" in pubs:
-            print(json.dumps(rep, separators=(",", ":")), flush=True)
-        published = True
-        if client is not None:
-            try:
-                agent.publish(client, rep)
+    srv = None
+    try:
+        if "annotation" in pubs:
+            from ..kube.client import KubeClient
+            from ..kube.config import load_kube_config
+            conn = load_kube_config(args.kubeconfig)
+            tok = conn.token
+            if conn.token_file:
+                try:
+                    with open(conn.token_file, encoding="utf-8") as f:
+                        tok = f.read()
+                except OSError:
+                    pass
+            bound = token_node_name(tok)
+            if bound is not None and bound != args.node:
+                # deploy/agent-policy.yaml would refuse every write anyway; say why at start-up instead
+                print(f"--node {args.node!r} is not the node this pod's ServiceAccount token is bound to ({bound!r}): "
+                      "refusing to publish another node's status", file=sys.stderr, flush=True)
+                return 2
+            client = KubeClient(conn, timeout=10.0)
+            try:  # the node's registered GPU count; refreshed from every condition PATCH response after this
+                agent.observe_node(client.get_node(args.node))
             except Exception as e:
-                published = False
-                print(f"node status publish failed: {e}", file=sys.stderr, flush=True)
-        if args.once:  # a one-shot run (CI, a harness) says whether the node saw its verdict
-            return 0 if published else 1
-        stop.wait(max(0.0, args.interval - (time.monotonic() - started)))
-    print("SIGTERM: agent stopped", file=sys.stderr, flush=True)
-    return 0
+                print(f"could not read node {args.node}: {e}", file=sys.stderr, flush=True)
+        if "http" in pubs:
+            host, _, port = args.listen.rpartition(":")
+            # a probe cycle may legitimately include diagnostics (up to --diag-timeout per GPU)
+            if bool(args.tls_cert_file) != bool(args.tls_key_file) or (args.tls_client_ca and not args.tls_cert_file):
+                print("--tls-cert-file and --tls-key-file go together (and --tls-client-ca needs them)", file=sys.stderr,
+                      flush=True)
+                return 2
+            tls = tls_context(args.tls_cert_file, args.tls_key_file, args.tls_client_ca) if args.tls_cert_file else None
+            srv = serve(agent, host or "0.0.0.0", int(port),
+                        stale_after=max(180.0, 3 * args.interval + args.diag_timeout), tls=tls,
+                        require_client_cert=bool(args.tls_client_ca))
+        # SIGTERM (pod deletion, rolling update): finish the cycle in flight and leave with 0 instead of dying
+        # mid-write; the condition keeps its last heartbeat and ages out at the checker's --probe-max-age
+        stop = threading.Event()
+        if threading.current_thread() is threading.main_thread():
+            import signal
+            signal.signal(signal.SIGTERM, lambda *_: stop.set())
+        while not stop.is_set():
+            started = time.monotonic()
+            rep = agent.probe_once()
+            if "stdout" in pubs:
+                print(json.dumps(rep, separators=(",", ":")), flush=True)
+            published = True
+            if client is not None:
+                try:
+                    agent.publish(client, rep)
+                except Exception as e:
+                    published = False
+                    print(f"node status publish failed: {e}", file=sys.stderr, flush=True)
+            if args.once:  # a one-shot run (CI, a harness) says whether the node saw its verdict
+                return 0 if published else 1
+            stop.wait(max(0.0, args.interval - (time.monotonic() - started)))
+        print("SIGTERM: agent stopped", file=sys.stderr, flush=True)
+        return 0
+    finally:
+        # --once, SIGTERM or a start-up refusal: the kube connection and the HTTP server do not outlive main
+        if client is not None:
+            client.close()
+        if srv is not None:
+            srv.shutdown()
+            srv.server_close()
 
 
 if __name__ == "__main__":

@@ -200,16 +200,25 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
         request_queue_size = 128  # the checker's fan-out connects in bursts
 
         def finish_request(self, request: Any, client_address: Any) -> None:
-            if tls is not None:
-                # the handshake runs on the connection's own thread (never on the accept loop), bounded
-                request.settimeout(10.0)
+            if tls is None:
+                super().finish_request(request, client_address)
+                return
+            # the handshake runs on the connection's own thread (never on the accept loop), bounded
+            request.settimeout(10.0)
+            try:
+                conn = tls.wrap_socket(request, server_side=True)
+            except OSError:
+                request.close()
+                return
+            conn.settimeout(None)
+            try:
+                super().finish_request(conn, client_address)
+            finally:
+                # wrap_socket detached the accepted socket (socketserver closes that empty shell): the TLS one is ours
                 try:
-                    request = tls.wrap_socket(request, server_side=True)
+                    conn.close()
                 except OSError:
-                    request.close()
-                    return
-                request.settimeout(None)
-            super().finish_request(request, client_address)
+                    pass
 
     srv = Srv((host, port), H)
     threading.Thread(target=srv.serve_forever, daemon=True).start()

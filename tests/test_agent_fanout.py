@@ -61,6 +61,7 @@ def test_agent_http_endpoint(fixture_report):
         assert request(base + "/nope").status == 404
     finally:
         srv.shutdown()
+        srv.server_close()
 
 
 def test_checker_probe_endpoint_fanout(run_cli, mock_cluster, tmp_path, fixture_report):
@@ -90,7 +91,9 @@ def test_checker_probe_endpoint_fanout(run_cli, mock_cluster, tmp_path, fixture_
         assert p.returncode == 0
     finally:
         srv_a.shutdown()
+        srv_a.server_close()
         srv_b.shutdown()
+        srv_b.server_close()
 
 
 def test_fanout_is_concurrent(fixture_report):
@@ -129,6 +132,7 @@ def test_fanout_is_concurrent(fixture_report):
         assert out[0]["error"].startswith("timeout") and time.time() - t < 1
     finally:
         s.shutdown()
+        s.server_close()
 
 
 def test_fanout_asyncio_debug_mode_clean(fixture_report):
@@ -184,6 +188,7 @@ def test_fanout_asyncio_debug_mode_clean(fixture_report):
         assert not leaks, leaks
     finally:
         s.shutdown()
+        s.server_close()
 
 
 def test_agent_metrics_cover_diag_kinds_and_fabric():
@@ -420,7 +425,9 @@ def test_swapped_ips_yield_unknown_not_the_other_nodes_verdict(run_cli, mock_clu
         assert p.returncode == 0
     finally:
         srv_a.shutdown()
+        srv_a.server_close()
         srv_b.shutdown()
+        srv_b.server_close()
 
 
 def test_annotation_copied_from_another_node_is_unknown(mock_cluster, tmp_path, fixture_report):
@@ -542,6 +549,7 @@ def test_fetch_probe_reports_inside_a_running_event_loop(fixture_report):
         assert out[0]["node"] == "a" and out[0]["gpus"]
     finally:
         srv.shutdown()
+        srv.server_close()
 
 
 def test_https_probe_endpoint_verified_with_probe_ca(certs, fixture_report):
@@ -575,6 +583,7 @@ def test_https_probe_endpoint_verified_with_probe_ca(certs, fixture_report):
         assert out[0] == json.loads(body)
     finally:
         s.shutdown()
+        s.server_close()
     from k8s_gpu_node_checker_amd import cli
     assert cli.parse_args(["--probe-ca", "/etc/ca.pem"]).probe_ca == "/etc/ca.pem"
 
@@ -633,6 +642,7 @@ def test_agent_serves_tls_and_requires_client_certs_except_for_healthz(pki, fixt
         assert urllib.request.urlopen(base + "/healthz", context=ctx, timeout=5).status == 200  # still serving
     finally:
         srv.shutdown()
+        srv.server_close()
     args = A.build_parser().parse_args(["--tls-cert-file", "c", "--tls-key-file", "k", "--tls-client-ca", "ca"])
     assert (args.tls_cert_file, args.tls_key_file, args.tls_client_ca) == ("c", "k", "ca")
     assert A.main(["--publish", "http", "--tls-cert-file", "c", "--once", "--source", "fixture",

@@ -12,6 +12,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MANIFESTS = sorted(glob.glob(os.path.join(REPO, "deploy", "*.yaml")))
 
 
+def _read(path):
+    with open(path, encoding="utf-8") as f:
+        return f.read()
+
+
 def _containers(doc):
     spec = doc.get("spec") or {}
     if doc["kind"] == "CronJob":
@@ -22,7 +27,7 @@ def _containers(doc):
 
 @pytest.mark.parametrize("path", MANIFESTS, ids=os.path.basename)
 def test_manifest_commands_parse(path):
-    docs = [d for d in yaml.safe_load_all(open(path)) if d]
+    docs = [d for d in yaml.safe_load_all(_read(path)) if d]
     assert docs and all("kind" in d and "apiVersion" in d for d in docs)
     for d in docs:
         for c in _containers(d):
@@ -38,7 +43,7 @@ def test_manifest_commands_parse(path):
 def test_rbac_matches_what_the_code_calls():
     verbs = {}
     for path in MANIFESTS:
-        for d in yaml.safe_load_all(open(path)):
+        for d in yaml.safe_load_all(_read(path)):
             if d and d["kind"] == "ClusterRole":
                 verbs[d["metadata"]["name"]] = {(r, v) for rule in d["rules"] for r in rule["resources"]
                                                 for v in rule["verbs"]}
@@ -51,7 +56,7 @@ def test_rbac_matches_what_the_code_calls():
 def test_manifests_are_self_consistent():
     """Everything a workload references (namespace, ServiceAccount, PVC) is defined in deploy/, and the
     kustomization lists every manifest."""
-    docs = [d for path in MANIFESTS for d in yaml.safe_load_all(open(path)) if d]
+    docs = [d for path in MANIFESTS for d in yaml.safe_load_all(_read(path)) if d]
     defined = {(d["kind"], (d.get("metadata") or {}).get("namespace"), d["metadata"]["name"])
                for d in docs if d["kind"] != "Kustomization"}
     namespaces = {name for kind, _, name in defined if kind == "Namespace"}
@@ -71,14 +76,14 @@ def test_manifests_are_self_consistent():
         for v in pod.get("volumes") or []:
             if "persistentVolumeClaim" in v:
                 assert ("PersistentVolumeClaim", ns, v["persistentVolumeClaim"]["claimName"]) in defined
-    kust = yaml.safe_load(open(os.path.join(REPO, "deploy", "kustomization.yaml")))
+    kust = yaml.safe_load(_read(os.path.join(REPO, "deploy", "kustomization.yaml")))
     assert sorted(kust["resources"]) == sorted(os.path.basename(p) for p in MANIFESTS
                                                if not p.endswith("kustomization.yaml"))
 
 
 def _pods():
     for path in MANIFESTS:
-        for d in yaml.safe_load_all(open(path)):
+        for d in yaml.safe_load_all(_read(path)):
             if not d or d["kind"] not in ("DaemonSet", "Deployment", "CronJob", "Job"):
                 continue
             spec = d["spec"]["jobTemplate"]["spec"] if d["kind"] == "CronJob" else d["spec"]
@@ -142,7 +147,7 @@ def test_monitoring_rules_use_metrics_the_agent_emits():
     import re
 
     from prometheus_client.parser import text_string_to_metric_families
-    docs = [d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "monitoring", "monitoring.yaml"))) if d]
+    docs = [d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "monitoring", "monitoring.yaml"))) if d]
     kinds = {d["kind"] for d in docs}
     assert kinds == {"Service", "ServiceMonitor", "PrometheusRule"}
     fams = {f.name: f for f in text_string_to_metric_families(agent._metrics(_rich_report()))}
@@ -163,7 +168,7 @@ def test_monitoring_rules_use_metrics_the_agent_emits():
         for lbl in re.findall(r"\$labels\.([a-z_]+)", r["annotations"]["summary"]):
             assert lbl in have, (r["alert"], lbl, have)
     # the Service and ServiceMonitor find the DaemonSet's pods and its metrics port
-    ds = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
+    ds = next(d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
     pod_labels = ds["spec"]["template"]["metadata"]["labels"]
     port_names = {p["name"] for c in ds["spec"]["template"]["spec"]["containers"] for p in c.get("ports", [])}
     svc = next(d for d in docs if d["kind"] == "Service")
@@ -196,14 +201,14 @@ def test_image_carries_every_third_party_runtime_import():
             continue
         for f in files:
             if f.endswith(".py"):
-                tree = ast.parse(open(os.path.join(root, f)).read())
+                tree = ast.parse(_read(os.path.join(root, f)))
                 for n in ast.walk(tree):
                     if isinstance(n, ast.Import):
                         mods |= {a.name.split(".")[0] for a in n.names}
                     elif isinstance(n, ast.ImportFrom) and n.level == 0 and n.module:
                         mods.add(n.module.split(".")[0])
     third = {m for m in mods if m not in sys.stdlib_module_names and m != "k8s_gpu_node_checker_amd"}
-    runtime = open(os.path.join(REPO, "deploy", "Dockerfile")).read().rsplit("\nFROM ", 1)[1]
+    runtime = _read(os.path.join(REPO, "deploy", "Dockerfile")).rsplit("\nFROM ", 1)[1]
     installed = {"yaml": "python3-yaml" in runtime, "grpc": "grpcio" in runtime}
     optional = {"torch", "amdsmi"}
     assert third <= set(installed) | optional, third - set(installed) - optional
@@ -211,16 +216,16 @@ def test_image_carries_every_third_party_runtime_import():
 
 
 def test_agent_port_network_policy_selects_the_agent_and_its_port():
-    pol = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "monitoring", "networkpolicy.yaml")))
+    pol = next(d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "monitoring", "networkpolicy.yaml")))
                if d)
-    ds = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
+    ds = next(d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
     pod = ds["spec"]["template"]
     assert pol["metadata"]["namespace"] == ds["metadata"]["namespace"]
     assert pol["spec"]["podSelector"]["matchLabels"].items() <= pod["metadata"]["labels"].items()
     assert not pod["spec"].get("hostNetwork")  # a host-network pod would ignore the policy
     ports = {p["name"] for c in pod["spec"]["containers"] for p in c.get("ports", [])}
     assert {p["port"] for r in pol["spec"]["ingress"] for p in r["ports"]} <= ports
-    kust = yaml.safe_load(open(os.path.join(REPO, "deploy", "monitoring", "kustomization.yaml")))
+    kust = yaml.safe_load(_read(os.path.join(REPO, "deploy", "monitoring", "kustomization.yaml")))
     assert "networkpolicy.yaml" in kust["resources"]
 
 
@@ -236,7 +241,7 @@ AGENT_USER = "system:serviceaccount:gpu-health:mi355x-node-agent"
 
 
 def _policy():
-    docs = [d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "agent-policy.yaml"))) if d]
+    docs = [d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "agent-policy.yaml"))) if d]
     pol = next(d for d in docs if d["kind"] == "ValidatingAdmissionPolicy")
     binding = next(d for d in docs if d["kind"] == "ValidatingAdmissionPolicyBinding")
     return pol, binding
@@ -263,14 +268,14 @@ def test_policy_is_bound_to_the_agent_service_account_and_names_the_node_claim()
     assert pol["spec"]["failurePolicy"] == "Fail"
     mc = " ".join(m["expression"] for m in pol["spec"]["matchConditions"])
     assert AGENT_USER in mc
-    sa = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "rbac.yaml")))
+    sa = next(d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "rbac.yaml")))
               if d and d["kind"] == "ServiceAccount" and d["metadata"]["name"] == "mi355x-node-agent")
     assert AGENT_USER == f"system:serviceaccount:{sa['metadata']['namespace']}:{sa['metadata']['name']}"
     assert "authentication.kubernetes.io/node-name" in yaml.safe_dump(pol)
     rules = {(r, o) for rr in pol["spec"]["matchConstraints"]["resourceRules"] for r in rr["resources"]
              for o in rr["operations"]}
     assert {("nodes", "UPDATE"), ("nodes/status", "UPDATE"), ("events", "CREATE")} <= rules
-    kust = yaml.safe_load(open(os.path.join(REPO, "deploy", "kustomization.yaml")))
+    kust = yaml.safe_load(_read(os.path.join(REPO, "deploy", "kustomization.yaml")))
     assert "agent-policy.yaml" in kust["resources"]
 
 
@@ -361,7 +366,7 @@ def _agent_container(doc):
 
 
 def test_daemonset_memory_limit_covers_the_budget_of_an_eight_gpu_node():
-    ds = next(d for d in yaml.safe_load_all(open(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
+    ds = next(d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
     c = _agent_container(ds)
     level = int(c["command"][c["command"].index("--diag-level") + 1])
     assert level == 1
@@ -372,9 +377,9 @@ def test_daemonset_memory_limit_covers_the_budget_of_an_eight_gpu_node():
 
 def test_level2_overlay_keeps_the_comgr_cache_and_sizes_both_containers():
     base = os.path.join(REPO, "deploy", "level2")
-    kust = yaml.safe_load(open(os.path.join(base, "kustomization.yaml")))
+    kust = yaml.safe_load(_read(os.path.join(base, "kustomization.yaml")))
     assert kust["resources"] == ["../"] and kust["patches"][0]["path"] == "daemonset-level2.yaml"
-    patch = yaml.safe_load(open(os.path.join(base, "daemonset-level2.yaml")))
+    patch = yaml.safe_load(_read(os.path.join(base, "daemonset-level2.yaml")))
     c = _agent_container(patch)
     agent.build_parser().parse_args(c["command"][1:])
     assert c["command"][c["command"].index("--diag-level") + 1] == "2"
@@ -383,7 +388,7 @@ def test_level2_overlay_keeps_the_comgr_cache_and_sizes_both_containers():
     assert init["command"][0] == "mi355x-fabric"
     from k8s_gpu_node_checker_amd.ops import fabric
     fabric.main.__code__  # the console script's target exists
-    assert 'mi355x-fabric = "k8s_gpu_node_checker_amd.ops.fabric:main"' in open(os.path.join(REPO, "pyproject.toml")).read()
+    assert 'mi355x-fabric = "k8s_gpu_node_checker_amd.ops.fabric:main"' in _read(os.path.join(REPO, "pyproject.toml"))
     assert _mib(init["resources"]["limits"]["memory"]) >= agent.MEM_RCCL_COLD_PEAK_MIB
     for ctr in (c, init):
         env = {e["name"]: e["value"] for e in ctr["env"]}

@@ -152,7 +152,8 @@ def _cronjob_command():
     import os
     import yaml
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cj = yaml.safe_load(open(os.path.join(repo, "deploy", "cronjob.yaml")))
+    with open(os.path.join(repo, "deploy", "cronjob.yaml"), encoding="utf-8") as f:
+        cj = yaml.safe_load(f)
     return cj["spec"]["jobTemplate"]["spec"]["template"]["spec"]["containers"][0]["command"]
 
 

@@ -138,7 +138,8 @@ def test_tls_with_ca_file_and_sni(certs):
         with KubeClient(conn) as c:
             assert len(c.scan_nodes().gpu_nodes) == 3
         conn2 = ClusterConnection(srv.url.replace("127.0.0.1", "localhost"))
-        conn2.ca_data = open(crt, "rb").read()
+        with open(crt, "rb") as f:
+            conn2.ca_data = f.read()
         conn2.tls_server_name = "localhost"
         with KubeClient(conn2) as c:
             assert len(c.scan_nodes().gpu_nodes) == 3

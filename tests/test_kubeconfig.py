@@ -171,7 +171,8 @@ def test_client_cert_data_staged_privately(tmp_path, monkeypatch):
     class Ctx:
         def load_cert_chain(self, cert, key):
             seen["mode"] = stat.S_IMODE(os.stat(key).st_mode)
-            seen["cert"] = open(cert, "rb").read()
+            with open(cert, "rb") as f:
+                seen["cert"] = f.read()
             seen["path"] = cert
     conn = K.ClusterConnection("https://x")
     conn.cert_data, conn.key_data = b"CERT", b"KEY"

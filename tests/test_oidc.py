@@ -104,7 +104,8 @@ def kubeconfig(path, api_url, idp_url, id_token, refresh="rt-0"):
 
 
 def persisted(path):
-    d = yaml.safe_load(open(path))
+    with open(path) as f:
+        d = yaml.safe_load(f)
     return d["users"][0]["user"]["auth-provider"]["config"]
 
 
@@ -196,7 +197,8 @@ def test_concurrent_checkers_refresh_once(tmp_path):
         assert len(idp.grants) == 1, idp.grants
         assert persisted(kc)["refresh-token"] == "rt-1" and persisted(kc)["id-token"] == api.cfg.token
         assert not (tmp_path / "config.lock").exists()
-        assert open(kc).read().startswith("apiVersion")  # rewritten as YAML (the comment is not kept)
+        with open(kc) as f:
+            assert f.read().startswith("apiVersion")  # rewritten as YAML (the comment is not kept)
 
 
 def test_stale_lock_is_broken(tmp_path, monkeypatch):

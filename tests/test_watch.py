@@ -67,8 +67,10 @@ def test_line_stream_chunked_split_records_idle_and_eof():
 def test_line_stream_non_2xx_returns_full_response():
     body = b'{"kind":"Status","code":403}'
     url = _raw_server([b"HTTP/1.1 403 Forbidden\r\nContent-Length: %d\r\n\r\n" % len(body) + body])
-    r = Connection(url, timeout=5).open_stream("GET", "/w", {})
+    c = Connection(url, timeout=5)
+    r = c.open_stream("GET", "/w", {})
     assert not isinstance(r, LineStream) and r.status == 403 and r.body == body
+    c.close()
 
 
 def _watch_lines(url, rv, n, extra="", timeout=5.0):
