@@ -83,6 +83,11 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
     ("x", "--watch-debounce", {"type": float, "default": 0.2,
                                "help": "--watch-events: 이 시간(초) 안에 도착한 이벤트를 한 번에 평가 (기본: 0.2)"}),
     ("x", "--watch-duration", {"type": float, "default": 0.0, "help": "--watch-events: N초 후 종료 (0 = 무제한, 기본)"}),
+    ("x", "--leader-elect", {"action": "store_true",
+                             "help": "--watch-events 를 여러 복제본으로: coordination.k8s.io Lease 를 가진 하나만 감시/보고"}),
+    ("x", "--leader-elect-lease", {"help": "--leader-elect: Lease 네임스페이스/이름 (기본: <파드 네임스페이스>/gpu-node-watcher)"}),
+    ("x", "--leader-elect-timing", {"default": "15,10,2",
+                                    "help": "--leader-elect: lease 기간, 갱신 기한, 재시도 간격(초) (기본: 15,10,2)"}),
 )
 
 
@@ -289,13 +294,55 @@ def _watch_events(args: Any) -> int:
                 write_textfile(args.prometheus_textfile, result)
             last["code"] = result.exit_code
 
-        NodeWatcher(cluster, opts, debounce=args.watch_debounce).run(
-            evaluate, report, max_reports=args.watch_count, duration=args.watch_duration)
-        return last["code"]
+        if not args.leader_elect:
+            NodeWatcher(cluster, opts, debounce=args.watch_debounce).run(
+                evaluate, report, max_reports=args.watch_count, duration=args.watch_duration)
+            return last["code"]
+        elector = _start_elector(args, cluster)
+        try:
+            while not elector.leading.wait(0.2):
+                pass
+            print(f"leader election: {elector.identity} leads {elector.namespace}/{elector.name}", file=sys.stderr,
+                  flush=True)
+            NodeWatcher(cluster, opts, debounce=args.watch_debounce).run(
+                evaluate, report, max_reports=args.watch_count, duration=args.watch_duration,
+                should_stop=lambda: not elector.is_leader())
+            if elector.lost.is_set() or not elector.is_leader():
+                # client-go's rule: a replica that could not renew in time stops acting and exits; the
+                # Deployment restarts it as a candidate
+                print(f"leader election: {elector.identity} lost {elector.namespace}/{elector.name} "
+                      f"({elector.last_error or 'not renewed in time'}): stopping", file=sys.stderr, flush=True)
+            return last["code"]
+        finally:
+            elector.stop()  # a holder releases the Lease: the next replica takes over without waiting it out
     except KeyboardInterrupt:
         return last["code"]
     except Exception as e:
         return _report_error(args, e)
+
+
+def _start_elector(args: Any, cluster: Any) -> Any:
+    """``--leader-elect``: campaign for the Lease (kube/lease.py) from a thread; SIGTERM (pod deletion, rolling
+    update) ends the watch like Ctrl-C, so the holder releases the Lease on its way out."""
+    import signal
+    import threading
+    from .kube.client import KubeClient
+    from .kube.lease import LeaderElector, default_identity, default_namespace
+    spec = args.leader_elect_lease or f"{default_namespace()}/gpu-node-watcher"
+    ns, _, name = spec.rpartition("/")
+    try:
+        duration, renew, retry = (float(x) for x in args.leader_elect_timing.split(","))
+    except ValueError:
+        raise ValueError(f"--leader-elect-timing: three numbers 'lease,renew,retry', not {args.leader_elect_timing!r}")
+    if threading.current_thread() is threading.main_thread():
+        def _term(*_: Any) -> None:
+            raise KeyboardInterrupt
+        signal.signal(signal.SIGTERM, _term)
+    elector = LeaderElector(lambda: KubeClient(cluster, timeout=max(0.5, min(5.0, renew / 2)), retries=0),
+                            ns or default_namespace(), name, default_identity(), duration, renew, retry)
+    print(f"leader election: {elector.identity} campaigning for {elector.namespace}/{elector.name}", file=sys.stderr,
+          flush=True)
+    return elector.start()
 
 
 def _watch(args: Any) -> int:

@@ -88,6 +88,9 @@ def outcome_signature(result: Any) -> Tuple[Any, ...]:
     return tuple(sig)
 
 
+STOP_POLL_S = 0.25  # how often a quiet watch stream checks run()'s should_stop
+
+
 class NodeWatcher:
     def __init__(self, cluster: ClusterConnection, opts: Any, watch_timeout: int = 300, debounce: float = 0.2,
                  page_size: Optional[int] = None, sleep: Callable[[float], None] = time.sleep,
@@ -177,8 +180,10 @@ class NodeWatcher:
         return resp
 
     def run(self, evaluate: Callable[[ScanResult], Any], report: Callable[[Any], None], max_reports: int = 0,
-            duration: float = 0.0) -> int:
-        """Follow the cluster until ``max_reports`` reports were emitted or ``duration`` seconds passed.
+            duration: float = 0.0, should_stop: Optional[Callable[[], bool]] = None) -> int:
+        """Follow the cluster until ``max_reports`` reports were emitted, ``duration`` seconds passed or
+        ``should_stop()`` turns true (checked at least every ``STOP_POLL_S``, and before every report: a
+        replica that lost its leader Lease never reports after it).
 
         ``evaluate(scan)`` turns a state into a result (health gate applied); ``report(result)`` is
         called for the first result and for every result whose :func:`outcome_signature` differs
@@ -195,14 +200,14 @@ class NodeWatcher:
             last_eval = time.monotonic()
             result = evaluate(self.view.scan_result())
             sig = outcome_signature(result)
-            if sig != last_sig:
+            if sig != last_sig and not (should_stop is not None and should_stop()):
                 last_sig = sig
                 report(result)
                 reports += 1
 
         def done() -> bool:
             return (max_reports > 0 and reports >= max_reports) or (
-                deadline is not None and time.monotonic() >= deadline)
+                deadline is not None and time.monotonic() >= deadline) or (should_stop is not None and should_stop())
 
         while not done():
             client = KubeClient(self.cluster, timeout=self.opts.kube_timeout, retries=self.opts.kube_retries)
@@ -219,6 +224,8 @@ class NodeWatcher:
                     wait = self.debounce if pending else self.watch_timeout + 30
                     if self.recheck > 0:
                         wait = min(wait, max(0.01, last_eval + self.recheck - time.monotonic()))
+                    if should_stop is not None:
+                        wait = min(wait, STOP_POLL_S)
                     if deadline is not None:
                         remaining = deadline - time.monotonic()
                         if remaining <= 0:

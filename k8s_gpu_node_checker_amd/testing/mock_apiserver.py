@@ -163,6 +163,9 @@ def _merge_patch(target: Dict[str, Any], patch: Dict[str, Any]) -> None:
             target[k] = copy.deepcopy(v)
 
 
+LEASES = "/apis/coordination.k8s.io/v1/namespaces/"
+
+
 class MockConfig:
     def __init__(self, token: Optional[str] = None, status: Optional[int] = None, fail_first: int = 0,
                  fail_status: int = 503, retry_after: Optional[str] = None, delay: float = 0.0,
@@ -285,7 +288,70 @@ class _Handler(BaseHTTPRequestHandler):
         if path in ("/healthz", "/readyz", "/livez"):
             self._send(200, b"ok")
             return
+        if path.startswith(LEASES):
+            self._lease("GET", path, b"")
+            return
         self._send(404, self._status_body(404, "NotFound", "not found"), reason="Not Found")
+
+    def _lease(self, method: str, path: str, body: bytes) -> None:
+        """``coordination.k8s.io/v1`` Leases: GET / POST (create, 409 if it exists) / PUT (update, 409 unless the
+        body carries the current ``resourceVersion``).  ``server.lease_status`` fails every lease call with that
+        status (a replica that lost the apiserver)."""
+        srv = self.server
+        parts = path[len(LEASES):].strip("/").split("/")
+        if srv.lease_status is not None:
+            self._send(srv.lease_status, self._status_body(srv.lease_status, "InternalError", "lease store unavailable"))
+            return
+        if len(parts) < 2 or parts[1] != "leases" or len(parts) > 3 or (method == "POST") != (len(parts) == 2):
+            self._send(404, self._status_body(404, "NotFound", "not found"), reason="Not Found")
+            return
+        ns = unquote(parts[0])
+        try:
+            obj = json.loads(body) if body else None
+        except ValueError:
+            obj = None
+        with srv.lock:
+            if method == "GET":
+                cur = srv.leases.get((ns, unquote(parts[2])))
+                if cur is None:
+                    self._send(404, self._status_body(404, "NotFound", "leases not found"), reason="Not Found")
+                else:
+                    self._send(200, json.dumps(cur).encode())
+                return
+            if not isinstance(obj, dict) or not isinstance(obj.get("metadata"), dict):
+                self._send(400, self._status_body(400, "BadRequest", "invalid lease"))
+                return
+            name = obj["metadata"].get("name") if method == "POST" else unquote(parts[2])
+            cur = srv.leases.get((ns, name))
+            if method == "POST" and cur is not None:
+                self._send(409, self._status_body(409, "AlreadyExists", f'leases "{name}" already exists'),
+                           reason="Conflict")
+                return
+            if method == "PUT":
+                if cur is None:
+                    self._send(404, self._status_body(404, "NotFound", "leases not found"), reason="Not Found")
+                    return
+                if obj["metadata"].get("resourceVersion") != cur["metadata"]["resourceVersion"]:
+                    self._send(409, self._status_body(409, "Conflict", "the object has been modified"),
+                               reason="Conflict")
+                    return
+            srv.lease_rv += 1
+            obj["metadata"].update(name=name, namespace=ns, resourceVersion=str(srv.lease_rv))
+            srv.leases[(ns, name)] = obj
+            srv.lease_writes.append((method, name, (obj.get("spec") or {}).get("holderIdentity")))
+        self._send(201 if method == "POST" else 200, json.dumps(obj).encode(),
+                   reason="Created" if method == "POST" else None)
+
+    def do_PUT(self) -> None:  # noqa: N802
+        length = int(self.headers.get("Content-Length") or 0)
+        body = self.rfile.read(length) if length else b""
+        if not self._pre():
+            return
+        path = urlsplit(self.path).path
+        if path.startswith(LEASES):
+            self._lease("PUT", path, body)
+            return
+        self._send(405, self._status_body(405, "MethodNotAllowed", "PUT is served for leases only"))
 
     def _watch(self, q: Dict[str, List[str]]) -> None:
         """Stream node events (chunked, one JSON object per line) like the apiserver's watch."""
@@ -401,6 +467,9 @@ class _Handler(BaseHTTPRequestHandler):
         body = self.rfile.read(length) if length else b""
         if not self._pre():
             return
+        if urlsplit(self.path).path.startswith(LEASES):
+            self._lease("POST", urlsplit(self.path).path, body)
+            return
         parts = urlsplit(self.path).path.strip("/").split("/")
         if len(parts) != 5 or parts[:3] != ["api", "v1", "namespaces"] or parts[4] != "events":
             self._send(404, self._status_body(404, "NotFound", "not found"), reason="Not Found")
@@ -440,6 +509,10 @@ class MockApiServer(ThreadingHTTPServer):
         self.log: List[Dict[str, Any]] = []
         self.k8s_events: List[Dict[str, Any]] = []  # core/v1 Events POSTed by clients
         self.event_seq = 0
+        self.leases: Dict[Any, Dict[str, Any]] = {}  # (namespace, name) -> coordination.k8s.io/v1 Lease
+        self.lease_rv = 0
+        self.lease_writes: List[Any] = []  # (method, name, holderIdentity) of every accepted write
+        self.lease_status: Optional[int] = None
         self.scheme = "http"
         if certfile:
             import ssl

@@ -53,6 +53,28 @@ def test_rbac_matches_what_the_code_calls():
     assert ("nodes", "watch") in verbs["gpu-node-watcher"]
 
 
+def test_replicated_watcher_has_the_lease_rbac_its_elector_uses():
+    """deploy/watcher.yaml runs 2 replicas with --leader-elect: the Role grants exactly what kube/lease.py calls
+    (GET and PUT of the named Lease, POST to create it) in the namespace of the Lease the command names."""
+    docs = [d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "watcher.yaml"))) if d]
+    dep = next(d for d in docs if d["kind"] == "Deployment")
+    cmd = dep["spec"]["template"]["spec"]["containers"][0]["command"]
+    args = cli.parse_args(cmd[1:])
+    assert dep["spec"]["replicas"] >= 2 and args.leader_elect and args.watch_events
+    ns, name = args.leader_elect_lease.split("/")
+    env = {e["name"]: e for e in dep["spec"]["template"]["spec"]["containers"][0]["env"]}
+    assert env["POD_NAME"]["valueFrom"]["fieldRef"]["fieldPath"] == "metadata.name"
+    role = next(d for d in docs if d["kind"] == "Role")
+    binding = next(d for d in docs if d["kind"] == "RoleBinding")
+    assert role["metadata"]["namespace"] == ns == binding["metadata"]["namespace"]
+    assert binding["roleRef"]["name"] == role["metadata"]["name"]
+    assert {(s["name"], s["namespace"]) for s in binding["subjects"]} == {
+        (dep["spec"]["template"]["spec"]["serviceAccountName"], dep["metadata"]["namespace"])}
+    grants = {(v, n) for r in role["rules"] for v in r["verbs"] for n in (r.get("resourceNames") or ["*"])
+              if r["resources"] == ["leases"] and r["apiGroups"] == ["coordination.k8s.io"]}
+    assert grants == {("get", name), ("update", name), ("create", "*")}
+
+
 def test_manifests_are_self_consistent():
     """Everything a workload references (namespace, ServiceAccount, PVC) is defined in deploy/, and the
     kustomization lists every manifest."""
