@@ -57,7 +57,11 @@ def run(devices: List[int], level: int = 1, timeout_s: float = 150.0, parallel: 
                        "failed": sorted(k for k, r in res.items() if isinstance(r, dict) and r.get("pass") is False),
                        "degraded": sorted(k for k, r in res.items() if isinstance(r, dict) and r.get("degraded")),
                        "gemm_tflops": (res.get("gemm") or {}).get("tflops"),
-                       "hbm_read_tbs": (res.get("hbm") or {}).get("read_tbs")}
+                       "hbm_read_tbs": (res.get("hbm") or {}).get("read_tbs"),
+                       # every rate test as a share of its single-GPU reference: with all GPUs of the node running
+                       # the suite at once, this is the measurement the lone-GPU calibration lacks
+                       "fractions": {k: r["fraction"] for k, r in res.items()
+                                     if isinstance(r, dict) and isinstance(r.get("fraction"), (int, float))}}
     out["per_device"] = per
     out["peak_threads"] = peak[0]
     out["diag_wall_s"] = round(time.monotonic() - t0, 2)
