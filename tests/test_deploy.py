@@ -160,8 +160,14 @@ def _rich_report():
     g.update(xgmi_error=0, xgmi_kb=[[1, 2]] * 1, cper={"fatal": 0, "uncorrected": 0, "corrected": 1},
              ecc_blocks={"umc": {"ce": 1, "ue": 0, "de": 0}}, gfx_activity=0,
              throttle={"s": 60, "thermal_pct": 0.0, "power_pct": 1.0, "prochot_pct": 0.0},
-             diag={"gemm": {"pass": True, "tflops": 1200.0}}, bad_pages=3, bad_pages_pending=1,
+             diag={"gemm": {"pass": True, "tflops": 1200.0}, "gemm_fp8": {"pass": True, "tflops": 2300.0},
+                   "mfma": {"pass": True, "kinds": {"bf16": {"tflops": 1900.0, "errors": 0}}},
+                   "hbm": {"pass": True, "copy_tbs": 6.4, "read_tbs": 7.0},
+                   "hbm_xcd": {"pass": True, "read_tbs": 6.1, "errors": 0, "alone_tbs": {"0": 1.3}},
+                   "memtest": {"pass": True, "errors": 0}}, bad_pages=3, bad_pages_pending=1,
              bad_pages_unreservable=0, bad_page_threshold=2048, ecc_ce_per_h=1.5)
+    r["fabric"] = {"p2p": {"pass": True, "median_gbps": 50.0, "min_gbps": 48.0},
+                   "rccl": {"pass": True, "best_busbw_by_op": {"all_reduce": 300.0}}}
     return r
 
 
@@ -199,6 +205,45 @@ def test_monitoring_rules_use_metrics_the_agent_emits():
     sm = next(d for d in docs if d["kind"] == "ServiceMonitor")
     assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
     assert {e["port"] for e in sm["spec"]["endpoints"]} <= {p["name"] for p in svc["spec"]["ports"]}
+
+
+def test_grafana_dashboard_queries_series_that_exist():
+    """deploy/monitoring/dashboard.yaml (generated by tools/make_dashboard.py): valid dashboard JSON with unique
+    panel ids, listed in the monitoring kustomization, and every metric it queries is one the agent's /metrics or
+    the checker's textfile emits (so no panel is silently empty), with every label its legends use."""
+    import json
+    import re
+    import subprocess
+    import sys
+    import types
+
+    from prometheus_client.parser import text_string_to_metric_families
+    from k8s_gpu_node_checker_amd.utils import prom
+    path = os.path.join(REPO, "deploy", "monitoring", "dashboard.yaml")
+    before = _read(path)
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "make_dashboard.py")], check=True, capture_output=True)
+    assert _read(path) == before, "deploy/monitoring/dashboard.yaml is stale: run tools/make_dashboard.py"
+    cm = yaml.safe_load(before)
+    assert cm["kind"] == "ConfigMap" and cm["metadata"]["labels"]["grafana_dashboard"] == "1"
+    assert "dashboard.yaml" in yaml.safe_load(_read(os.path.join(REPO, "deploy", "monitoring",
+                                                                 "kustomization.yaml")))["resources"]
+    dash = json.loads(cm["data"]["mi355x-node-health.json"])
+    ids = [p["id"] for p in dash["panels"]]
+    assert len(ids) == len(set(ids)) and dash["uid"] == "mi355x-node-health"
+    fams = {f.name: f for f in text_string_to_metric_families(agent._metrics(_rich_report()))}
+    node = {"name": "n0", "ready": True, "gpus": 8, "gpu_breakdown": {"amd.com/gpu": 8}}
+    res = types.SimpleNamespace(gpu_nodes=[node], ready_gpu_nodes=[node], exit_code=0, verdicts=[], tracer=None)
+    fams.update({f.name: f for f in text_string_to_metric_families("\n".join(prom.render(res)) + "\n")})
+    queried = 0
+    for p in dash["panels"]:
+        for t in p.get("targets", []):
+            for name in re.findall(r"\b((?:mi355x|k8s_gpu_checker)_[a-z0-9_]+)", t["expr"]):
+                assert name in fams, (p["title"], name)
+                queried += 1
+                have = set().union(*(set(s.labels) for s in fams[name].samples)) | {"node"}
+                for lbl in re.findall(r"\{\{(\w+)\}\}", t["legendFormat"]):
+                    assert lbl in have, (p["title"], lbl)
+    assert queried >= 25
 
 
 def test_agent_metrics_carry_the_verdict_state():
