@@ -848,17 +848,103 @@ def render_text(out: Dict[str, Any]) -> str:
     return "\n".join(lines) + "\n"
 
 
+def run_devices(level: int, devices: List[int], parallel: int = 8) -> Dict[int, Dict[str, Dict[str, Any]]]:
+    """:func:`run` on every device, at most ``parallel`` at once (one host thread per GPU, as the node agent
+    runs them; host-resource tests still take turns under their lock).  A device whose run raised reports it
+    as a failed ``run`` test instead of losing the other devices' results."""
+    out: Dict[int, Dict[str, Dict[str, Any]]] = {}
+
+    def one(d: int) -> None:
+        try:
+            out[d] = run(level, d)
+        except NativeUnavailable:
+            raise
+        except Exception as e:  # a broken device: a failed test, not a lost report
+            out[d] = {"run": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
+    if parallel <= 1 or len(devices) <= 1:
+        for d in devices:
+            one(d)
+        return {d: out[d] for d in devices}
+    queue = list(devices)
+    while queue:
+        batch, queue = queue[:parallel], queue[parallel:]
+        threads = [threading.Thread(target=one, args=(d,), name=f"diag-gpu{d}", daemon=True) for d in batch]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    return {d: out[d] for d in devices}
+
+
+def fabric_tests(devices: List[int], p2p: bool = True, rccl: bool = True,
+                 timeout_s: Optional[float] = None) -> Dict[str, Any]:
+    """The node-level tests of level 2: the xGMI pair matrix (within 45 % of ``timeout_s``) and the RCCL
+    collectives (within what is left up to 90 %); without a timeout both wait as long as they take."""
+    import time as _time
+    out: Dict[str, Any] = {}
+    t0 = _time.monotonic()
+    if p2p:
+        out["p2p"] = p2p_matrix(devices, timeout_s=0.45 * timeout_s if timeout_s else None)
+    if rccl:
+        from . import fabric  # with one GPU: RCCL's data path and the result checks, no bandwidth verdict
+        left = None if not timeout_s else max(0.001, 0.9 * timeout_s - (_time.monotonic() - t0))
+        out["rccl"] = fabric.collective_suite(devices, timeout_s=left) if left else fabric.collective_suite(devices)
+    return out
+
+
+def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
+            clock: Any = None) -> Dict[str, Any]:
+    """Acceptance burn-in: the per-device suite of ``level`` on every device, round after round, for
+    ``minutes``.  Passes only if every round of every device passed; reports each rate per device as
+    min / median / max over the rounds (a GPU that drifts or throttles under sustained load shows as a wide
+    spread or a late failure) and the first failing rounds."""
+    import statistics
+    import time as _time
+    clock = clock or _time.monotonic
+    t0 = clock()
+    rounds = 0
+    series: Dict[int, Dict[str, List[float]]] = {d: {} for d in devices}
+    failures: List[Dict[str, Any]] = []
+    while True:
+        res = run_devices(level, devices, parallel)
+        rounds += 1
+        for d, tests in res.items():
+            for test, r in tests.items():
+                if not isinstance(r, dict):
+                    continue
+                for key in ("tflops", "copy_tbs", "read_tbs", "write_tbs", "h2d_gbps", "d2h_gbps", "fraction"):
+                    if isinstance(r.get(key), (int, float)) and not isinstance(r.get(key), bool):
+                        series[d].setdefault(f"{test}.{key}", []).append(float(r[key]))
+                for kind, row in ((r.get("kinds") or {}) if isinstance(r.get("kinds"), dict) else {}).items():
+                    series[d].setdefault(f"{test}.{kind}.tflops", []).append(float(row.get("tflops", 0)))
+                if r.get("pass") is False and len(failures) < 20:
+                    failures.append({"round": rounds, "t_s": round(clock() - t0, 1), "device": d, "test": test,
+                                     "detail": r.get("detail", "")})
+        if clock() - t0 >= 60.0 * minutes:
+            break
+    summary = {d: {k: {"min": round(min(v), 3), "median": round(statistics.median(v), 3), "max": round(max(v), 3)}
+                   for k, v in m.items()} for d, m in series.items()}
+    return {"minutes": minutes, "rounds": rounds, "wall_s": round(clock() - t0, 1), "pass": not failures,
+            "failures": failures, "devices": summary}
+
+
 def main(argv=None) -> int:
-    """``mi355x-diag [--level N] [--device D] [--format json|text]``: run the active diagnostics, print one
-    JSON document (or a text summary)."""
+    """``mi355x-diag [--level N] [--device D] [--parallel P] [--timeout S] [--duration MIN] [--format json|text]``:
+    run the active diagnostics (every device at once, as the node agent does), print one JSON document (or a
+    text summary); ``--duration`` turns it into an acceptance burn-in of that many minutes."""
     import argparse
     import json
     ap = argparse.ArgumentParser(prog="mi355x-diag", description="MI355X active diagnostics (HIP, gfx950)")
     ap.add_argument("--level", type=int, default=1, choices=(1, 2))
     ap.add_argument("--device", type=int, action="append", help="GPU index (repeatable; default: all)")
+    ap.add_argument("--parallel", type=int, default=8, help="devices tested at once (default 8; 1 = one by one)")
     ap.add_argument("--no-p2p", dest="p2p", action="store_false", help="skip the level-2 xGMI pair matrix")
     ap.add_argument("--no-rccl", dest="rccl", action="store_false",
                     help="skip the level-2 RCCL collectives (ops/fabric.py)")
+    ap.add_argument("--timeout", type=float, default=0.0,
+                    help="level 2: bound the node-level tests (s); a hung xGMI pair or collective is reported failed")
+    ap.add_argument("--duration", type=float, default=0.0,
+                    help="burn-in: repeat the per-device suite for this many minutes (0 = one run)")
     ap.add_argument("--format", choices=("json", "text"), default="json")
     args = ap.parse_args(argv)
     devices = args.device if args.device else list(range(device_count()))
@@ -867,15 +953,28 @@ def main(argv=None) -> int:
         print(f"result: FAIL ({msg})" if args.format == "text" else json.dumps({"devices": {}, "pass": False,
                                                                                 "error": msg}, indent=1))
         return 1
-    out: Dict[str, Any] = {"devices": {d: {"info": device_info(d), "tests": run(args.level, d)} for d in devices}}
+    if args.duration > 0:
+        b = burn_in(args.level, devices, args.duration, max(1, args.parallel))
+        if args.format == "text":
+            lines = [f"burn-in: {b['rounds']} rounds in {b['wall_s']} s on {len(devices)} GPU(s)"]
+            for d, m in b["devices"].items():
+                for k in sorted(m):
+                    if k.endswith(".fraction"):
+                        continue
+                    v = m[k]
+                    lines.append(f"  GPU {d} {k:<28} min {v['min']:<10g} median {v['median']:<10g} max {v['max']:g}")
+            lines += [f"  FAIL round {f['round']} GPU {f['device']} {f['test']}: {f['detail']}" for f in b["failures"]]
+            lines.append(f"result: {'PASS' if b['pass'] else 'FAIL'}")
+            print("\n".join(lines))
+        else:
+            print(json.dumps(b, indent=1))
+        return 0 if b["pass"] else 1
+    results = run_devices(args.level, devices, max(1, args.parallel))
+    out: Dict[str, Any] = {"devices": {d: {"info": device_info(d), "tests": results[d]} for d in devices}}
     ok = all(t.get("pass") for d in out["devices"].values() for t in d["tests"].values())
-    if args.level >= 2 and args.p2p:
-        out["fabric"] = {"p2p": p2p_matrix(devices)}
-        ok = ok and out["fabric"]["p2p"]["pass"]
-    if args.level >= 2 and args.rccl:
-        from . import fabric  # with one GPU: RCCL's data path and the result checks, no bandwidth verdict
-        out.setdefault("fabric", {})["rccl"] = fabric.collective_suite(devices)
-        ok = ok and out["fabric"]["rccl"]["pass"]
+    if args.level >= 2 and (args.p2p or args.rccl):
+        out["fabric"] = fabric_tests(devices, args.p2p, args.rccl, args.timeout or None)
+        ok = ok and all(r.get("pass") for r in out["fabric"].values())
     out["pass"] = ok
     print(render_text(out) if args.format == "text" else json.dumps(out, indent=1), end="" if args.format == "text" else "\n")
     return 0 if out["pass"] else 1

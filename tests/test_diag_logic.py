@@ -326,3 +326,48 @@ def test_p2p_matrix_without_a_deadline_blocks_and_with_one_passes(fake):
     m = diag.p2p_matrix([0, 1], timeout_s=5.0)
     assert m["pass"] and "stopped" not in m and len(m["pairs"]) == 2
     assert diag.p2p_matrix([0, 1])["pass"] and lib.p2p_timeouts_ms[-1] == 0.0  # no deadline: 0 to the ABI
+
+
+def test_diag_cli_runs_devices_concurrently_like_the_agent(fake, capsys):
+    import json
+    import time
+    lib = fake(n=4, delay_s=0.15)
+    t0 = time.monotonic()
+    assert diag.main(["--level", "1", "--parallel", "4"]) == 0
+    wall = time.monotonic() - t0
+    out = json.loads(capsys.readouterr().out)
+    assert sorted(out["devices"], key=int) == ["0", "1", "2", "3"] and out["pass"]
+    assert {d: lib.threads[d] for d in range(4)} == {d: {f"diag-gpu{d}"} for d in range(4)}
+    assert wall < 4 * 2 * 0.15 * 0.7, wall  # 2 GEMMs of 0.15 s per device, overlapped
+    lib2 = fake(n=2)
+    assert diag.main(["--level", "1", "--parallel", "1"]) == 0
+    assert all(len(t) == 1 for t in lib2.threads.values())
+
+
+def test_burn_in_reports_spread_and_every_failing_round(fake, capsys):
+    import json
+    fake(n=2, rates=[1.0, 1.0, 0.98, 0.97] * 50)
+    b = diag.burn_in(1, [0, 1], minutes=0.0005)
+    assert b["pass"] and b["rounds"] >= 1 and not b["failures"]
+    g = b["devices"][0]["gemm.tflops"]
+    assert g["min"] <= g["median"] <= g["max"]
+    assert "mfma.bf16.tflops" in b["devices"][1]
+    # a GPU at half speed fails every round it runs, and the report names the rounds
+    fake(n=2, gpu_rate={1: 0.5})
+    b = diag.burn_in(1, [0, 1], minutes=0.0005)
+    assert not b["pass"] and {f["device"] for f in b["failures"]} == {1} and b["failures"][0]["round"] == 1
+    assert diag.main(["--level", "1", "--duration", "0.0005"]) == 1
+    assert json.loads(capsys.readouterr().out)["failures"]
+    fake(n=1)
+    assert diag.main(["--level", "1", "--duration", "0.0005", "--format", "text"]) == 0
+    text = capsys.readouterr().out
+    assert text.startswith("burn-in: ") and "GPU 0 gemm.tflops" in text and text.rstrip().endswith("result: PASS")
+
+
+def test_diag_cli_fabric_timeout_reports_a_hung_pair(fake, capsys):
+    import json
+    fake(n=3, hung_pairs=((2, 1),))
+    assert diag.main(["--level", "2", "--no-rccl", "--timeout", "0.4"]) == 1
+    out = json.loads(capsys.readouterr().out)
+    assert out["fabric"]["p2p"]["stopped"].startswith("2->1 hung") and "rccl" not in out["fabric"]
+    assert all(t["pass"] for d in out["devices"].values() for t in d["tests"].values())

@@ -479,6 +479,18 @@ def test_agent_diagnostics_threads_per_device(dev):
     assert all("diag" in g for g in rep["gpus"][: diag.device_count()])
 
 
+def test_burn_in_on_this_box(dev):
+    """``mi355x-diag --duration``: the level-1 suite round after round on the real GPU, every round passing,
+    each rate reported as a min / median / max spread."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    b = diag.burn_in(1, [0], minutes=0.05)
+    assert b["pass"], b["failures"]
+    assert b["rounds"] >= 2 and b["wall_s"] >= 3.0
+    g = b["devices"][0]["gemm.tflops"]
+    assert 0 < g["min"] <= g["median"] <= g["max"]
+    assert b["devices"][0]["gemm.fraction"]["min"] > diag.FAIL_FRACTION
+
+
 def test_p2p_diag_on_this_box(dev):
     """The pair matrix is a node-level xGMI test: with one visible GPU it is skipped, and the C ABI
     rejects a pair that is not two distinct devices instead of faulting."""
