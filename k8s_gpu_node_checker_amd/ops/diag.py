@@ -955,6 +955,9 @@ def main(argv=None) -> int:
         return 1
     if args.duration > 0:
         b = burn_in(args.level, devices, args.duration, max(1, args.parallel))
+        if args.level >= 2 and (args.p2p or args.rccl):  # the node-level tests once, after the rounds
+            b["fabric"] = fabric_tests(devices, args.p2p, args.rccl, args.timeout or None)
+            b["pass"] = b["pass"] and all(r.get("pass") for r in b["fabric"].values())
         if args.format == "text":
             lines = [f"burn-in: {b['rounds']} rounds in {b['wall_s']} s on {len(devices)} GPU(s)"]
             for d, m in b["devices"].items():
@@ -964,6 +967,9 @@ def main(argv=None) -> int:
                     v = m[k]
                     lines.append(f"  GPU {d} {k:<28} min {v['min']:<10g} median {v['median']:<10g} max {v['max']:g}")
             lines += [f"  FAIL round {f['round']} GPU {f['device']} {f['test']}: {f['detail']}" for f in b["failures"]]
+            for test, r in (b.get("fabric") or {}).items():
+                lines.append(f"fabric {test:<5} {'pass' if r.get('pass') else 'FAIL':<9} {_summary(test, r)}"
+                             + (f"  {r['detail']}" if r.get("detail") else ""))
             lines.append(f"result: {'PASS' if b['pass'] else 'FAIL'}")
             print("\n".join(lines))
         else:

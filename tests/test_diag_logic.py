@@ -371,3 +371,7 @@ def test_diag_cli_fabric_timeout_reports_a_hung_pair(fake, capsys):
     out = json.loads(capsys.readouterr().out)
     assert out["fabric"]["p2p"]["stopped"].startswith("2->1 hung") and "rccl" not in out["fabric"]
     assert all(t["pass"] for d in out["devices"].values() for t in d["tests"].values())
+    # the burn-in runs the node-level tests once after its rounds, under the same deadline
+    assert diag.main(["--level", "2", "--no-rccl", "--timeout", "0.4", "--duration", "0.0005"]) == 1
+    b = json.loads(capsys.readouterr().out)
+    assert not b["failures"] and b["fabric"]["p2p"]["stopped"].startswith("2->1 hung") and not b["pass"]
