@@ -149,3 +149,26 @@ def test_replicated_watchers_report_once_and_fail_over(mock_cluster, sink, tmp_p
         if a.poll() is None:
             a.kill()
         a.communicate(timeout=20)
+
+
+def test_a_watcher_that_cannot_renew_stops_acting_and_exits(mock_cluster, sink, tmp_path):
+    """The leader loses the Lease API (every lease call fails) while the node API keeps working: at its renew
+    deadline it stops following the cluster and exits (the Deployment restarts it as a candidate), before any
+    other replica could take the Lease over."""
+    srv = mock_cluster(fixtures.cluster(2, "amd"))
+    kc = srv.kubeconfig(str(tmp_path / "kc"))
+    a = _watcher(kc, sink.url("ok"), "replica-a")
+    try:
+        assert _wait(lambda: len(sink.requests) >= 1, 30.0)
+        srv.lease_status = 500
+        t0 = time.monotonic()
+        a.wait(15)
+        took = time.monotonic() - t0
+        out, err = a.communicate(timeout=10)
+        assert "lost gpu-health/gpu-node-watcher" in err, err[-800:]
+        assert took < 5.0, took
+        assert len(sink.requests) == 1  # nothing reported after leadership was given up
+    finally:
+        if a.poll() is None:
+            a.kill()
+            a.communicate(timeout=10)
