@@ -236,6 +236,7 @@ def test_healthz_turns_503_when_probes_stop(monkeypatch):
         with pytest.raises(urllib.error.HTTPError) as e:
             urllib.request.urlopen(url, timeout=5)
         assert e.value.code == 503
+        e.value.close()
         ag.probe_once()
         assert urllib.request.urlopen(url, timeout=5).status == 200
     finally:
