@@ -167,9 +167,12 @@ class LeaderElector:
         client = self.make_client()
         try:
             # acquire: one round every retry_period until the Lease is ours (or we are stopped)
+            # a renewal counts from the moment its round *started*: the apiserver applied the write no earlier,
+            # so others' lease expiry (observed after the write) is later than ours by at least the write's latency
             while not self._stop.is_set():
+                started = self.clock()
                 if self._round(client):
-                    self._last_renew = self.clock()
+                    self._last_renew = started
                     self.leading.set()
                     break
                 self._stop.wait(self.retry_period)
@@ -178,8 +181,9 @@ class LeaderElector:
                 self._stop.wait(self.retry_period)
                 if self._stop.is_set():
                     break
+                started = self.clock()
                 if self._round(client):
-                    self._last_renew = self.clock()
+                    self._last_renew = started
                 elif self.clock() - self._last_renew >= self.renew_deadline:
                     self.leading.clear()
                     self.lost.set()
