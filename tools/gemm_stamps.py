@@ -9,6 +9,7 @@ MFMA slot -- the barrier wait is time the other group's load slot took beyond th
 
     python tools/gemm_stamps.py --build            # CPU: hipcc the stamp build
     python tools/gemm_stamps.py --schedules 0,1    # GPU: one JSON line per schedule
+    python tools/gemm_stamps.py --no-store-ab      # GPU: shipped kernels vs the build that skips the C write
 """
 import argparse
 import ctypes
@@ -21,15 +22,58 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT_DIR = os.path.join(REPO, "tools", "_stamps")
 SO = os.path.join(OUT_DIR, "libmi355x_diag_stamps.so")
+SO_NOSTORE = os.path.join(OUT_DIR, "libmi355x_diag_nostore.so")
 
 
 def build() -> None:
     os.makedirs(OUT_DIR, exist_ok=True)
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-DDIAG_GEMM_STAMPS", "-Wno-unused-result", os.path.join(REPO, "k8s_gpu_node_checker_amd", "csrc", "diag",
-                                                                   "diag.hip"), "-o", SO]
-    subprocess.run(cmd, check=True)
-    print(SO)
+    src = os.path.join(REPO, "k8s_gpu_node_checker_amd", "csrc", "diag", "diag.hip")
+    base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
+            "-Wno-unused-result"]
+    subprocess.run(base + ["-DDIAG_GEMM_STAMPS", src, "-o", SO], check=True)
+    # ablation: the same kernels with the C write skipped at run time (the epilogue's LDS staging still runs)
+    subprocess.run(base + ["-DDIAG_GEMM_NO_STORE", src, "-o", SO_NOSTORE], check=True)
+    print(SO, SO_NOSTORE)
+
+
+def no_store_ab(rounds: int = 7) -> None:
+    """Time the shipped kernels against the no-store ablation (same process, interleaved): how much of the
+    run the C write costs."""
+    import torch
+    libs = {"shipped": ctypes.CDLL(os.path.join(REPO, "k8s_gpu_node_checker_amd", "_native", "libmi355x_diag.so")),
+            "no_store": ctypes.CDLL(os.environ.get("GEMM_AB_LIB", SO_NOSTORE))}
+    for L in libs.values():
+        for f in ("diag_gemm_bf16_launch", "diag_gemm_fp8_launch"):
+            getattr(L, f).argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
+        L.diag_set_gemm_variant.argtypes = [ctypes.c_int]
+        L.diag_set_gemm_variant(3)
+    st = torch.cuda.current_stream().cuda_stream
+    for n in (4096, 8192):
+        g = torch.Generator(device="cuda").manual_seed(n)
+        a = torch.rand(n, n, device="cuda", generator=g) * 2 - 1
+        b = torch.rand(n, n, device="cuda", generator=g) * 2 - 1
+        c = torch.empty(n, n, device="cuda")
+        for name, dt, fn in (("bf16", torch.bfloat16, "diag_gemm_bf16_launch"),
+                             ("mxfp8", torch.float8_e4m3fn, "diag_gemm_fp8_launch")):
+            x, y = a.to(dt), b.to(dt)
+            tf = {k: [] for k in libs}
+            for _ in range(rounds):
+                for k, L in libs.items():
+                    launch = getattr(L, fn)
+                    for _ in range(3):
+                        launch(x.data_ptr(), y.data_ptr(), c.data_ptr(), n, n, n, st)
+                    torch.cuda.synchronize()
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    it = 30 if n <= 4096 else 10
+                    s.record()
+                    for _ in range(it):
+                        launch(x.data_ptr(), y.data_ptr(), c.data_ptr(), n, n, n, st)
+                    e.record()
+                    torch.cuda.synchronize()
+                    tf[k].append(2.0 * n ** 3 / (s.elapsed_time(e) / it) / 1e9)
+            med = {k: round(statistics.median(v), 1) for k, v in tf.items()}
+            print(json.dumps({"dtype": name, "size": n, "median_tflops": med,
+                              "c_write_share": round(1 - med["shipped"] / med["no_store"], 3)}), flush=True)
 
 
 def main() -> int:
@@ -38,9 +82,13 @@ def main() -> int:
     ap.add_argument("--schedules", default="0,1")
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "mxfp8"))
+    ap.add_argument("--no-store-ab", action="store_true", help="time the shipped kernels against the no-store build")
     args = ap.parse_args()
     if args.build:
         build()
+        return 0
+    if args.no_store_ab:
+        no_store_ab()
         return 0
     import torch
     L = ctypes.CDLL(SO)
