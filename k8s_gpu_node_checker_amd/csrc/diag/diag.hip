@@ -655,11 +655,7 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
 #ifdef DIAG_GEMM_NO_STORE  // lab build (tools/gemm_stamps.py --no-store): everything but the C write itself
         if (N > (1 << 30))
 #endif
-#ifdef DIAG_GEMM_NT_STORE  // lab build: the C write as nontemporal stores
-        __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(C + static_cast<size_t>(row0 + m * 16 + r) * N + col0 + c4));
-#else
         *reinterpret_cast<floatx4*>(C + static_cast<size_t>(row0 + m * 16 + r) * N + col0 + c4) = v;
-#endif
       }
     }
   } else {

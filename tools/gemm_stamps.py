@@ -41,7 +41,7 @@ def no_store_ab(rounds: int = 7) -> None:
     run the C write costs."""
     import torch
     libs = {"shipped": ctypes.CDLL(os.path.join(REPO, "k8s_gpu_node_checker_amd", "_native", "libmi355x_diag.so")),
-            "no_store": ctypes.CDLL(os.environ.get("GEMM_AB_LIB", SO_NOSTORE))}
+            "no_store": ctypes.CDLL(SO_NOSTORE)}
     for L in libs.values():
         for f in ("diag_gemm_bf16_launch", "diag_gemm_fp8_launch"):
             getattr(L, f).argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
