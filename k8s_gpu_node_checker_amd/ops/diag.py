@@ -853,26 +853,29 @@ def run_devices(level: int, devices: List[int], parallel: int = 8) -> Dict[int, 
     runs them; host-resource tests still take turns under their lock).  A device whose run raised reports it
     as a failed ``run`` test instead of losing the other devices' results."""
     out: Dict[int, Dict[str, Dict[str, Any]]] = {}
+    missing: List[NativeUnavailable] = []  # no library at all: raised in the caller's thread, not per device
 
     def one(d: int) -> None:
         try:
             out[d] = run(level, d)
-        except NativeUnavailable:
-            raise
+        except NativeUnavailable as e:
+            missing.append(e)
         except Exception as e:  # a broken device: a failed test, not a lost report
             out[d] = {"run": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
     if parallel <= 1 or len(devices) <= 1:
         for d in devices:
             one(d)
-        return {d: out[d] for d in devices}
-    queue = list(devices)
-    while queue:
-        batch, queue = queue[:parallel], queue[parallel:]
-        threads = [threading.Thread(target=one, args=(d,), name=f"diag-gpu{d}", daemon=True) for d in batch]
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
+    else:
+        queue = list(devices)
+        while queue:
+            batch, queue = queue[:parallel], queue[parallel:]
+            threads = [threading.Thread(target=one, args=(d,), name=f"diag-gpu{d}", daemon=True) for d in batch]
+            for t in threads:
+                t.start()
+            for t in threads:
+                t.join()
+    if missing:
+        raise missing[0]
     return {d: out[d] for d in devices}
 
 

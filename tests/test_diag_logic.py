@@ -375,3 +375,23 @@ def test_diag_cli_fabric_timeout_reports_a_hung_pair(fake, capsys):
     assert diag.main(["--level", "2", "--no-rccl", "--timeout", "0.4", "--duration", "0.0005"]) == 1
     b = json.loads(capsys.readouterr().out)
     assert not b["failures"] and b["fabric"]["p2p"]["stopped"].startswith("2->1 hung") and not b["pass"]
+
+
+def test_run_devices_raises_a_missing_library_in_the_caller(monkeypatch):
+    from k8s_gpu_node_checker_amd.ops.native import NativeUnavailable
+
+    def gone(level, d, **kw):
+        raise NativeUnavailable("libmi355x_diag.so not built")
+    monkeypatch.setattr(diag, "run", gone)
+    with pytest.raises(NativeUnavailable):
+        diag.run_devices(1, [0, 1, 2], parallel=3)
+    calls = []
+
+    def flaky(level, d, **kw):
+        calls.append(d)
+        if d == 1:
+            raise RuntimeError("mi355x diag failed (-1): hipMalloc: out of memory")
+        return {"gemm": {"pass": True}}
+    monkeypatch.setattr(diag, "run", flaky)
+    out = diag.run_devices(1, [0, 1, 2], parallel=3)
+    assert out[1]["run"]["pass"] is False and "out of memory" in out[1]["run"]["detail"] and out[0]["gemm"]["pass"]
