@@ -34,6 +34,8 @@ ROWS = [
           ('mi355x_gpu_diag_copy_tbs{test="hbm"}', "{{node}} gpu{{gpu}} copy")], 12, 7),
         ("HBM read TB/s per XCD, each alone", "timeseries", "none",
          [("mi355x_gpu_diag_xcd_hbm_read_tbs", "{{node}} gpu{{gpu}} xcd{{xcd}}")], 12, 7),
+        ("Diagnostic rates as a share of their reference (fails below 0.85, degraded below 0.95)", "timeseries",
+         "percentunit", [("mi355x_gpu_diag_fraction", "{{node}} gpu{{gpu}} {{test}}")], 24, 7),
         ("Diagnostics skipped (GPU busy or allocated)", "timeseries", "none",
          [("mi355x_gpu_diag_skipped", "{{node}} gpu{{gpu}}")], 12, 6),
         ("Wrong results found by the diagnostics", "timeseries", "none",
