@@ -896,7 +896,7 @@ def fabric_tests(devices: List[int], p2p: bool = True, rccl: bool = True,
 
 
 def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
-            clock: Any = None) -> Dict[str, Any]:
+            clock: Any = None, progress: Any = None) -> Dict[str, Any]:
     """Acceptance burn-in: the per-device suite of ``level`` on every device, round after round, for
     ``minutes``.  Passes only if every round of every device passed; reports each rate per device as
     min / median / max over the rounds (a GPU that drifts or throttles under sustained load shows as a wide
@@ -923,6 +923,9 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
                 if r.get("pass") is False and len(failures) < 20:
                     failures.append({"round": rounds, "t_s": round(clock() - t0, 1), "device": d, "test": test,
                                      "detail": r.get("detail", "")})
+        if progress is not None:  # one line per round (operators watching a long burn-in, CI log liveness)
+            bad = sorted({f"gpu{f['device']}:{f['test']}" for f in failures if f["round"] == rounds})
+            progress(f"burn-in round {rounds} at {clock() - t0:.0f} s: " + ("FAIL " + " ".join(bad) if bad else "pass"))
         if clock() - t0 >= 60.0 * minutes:
             break
     summary = {d: {k: {"min": round(min(v), 3), "median": round(statistics.median(v), 3), "max": round(max(v), 3)}
@@ -957,7 +960,9 @@ def main(argv=None) -> int:
                                                                                 "error": msg}, indent=1))
         return 1
     if args.duration > 0:
-        b = burn_in(args.level, devices, args.duration, max(1, args.parallel))
+        import sys as _sys
+        b = burn_in(args.level, devices, args.duration, max(1, args.parallel),
+                    progress=lambda line: print(line, file=_sys.stderr, flush=True))
         if args.level >= 2 and (args.p2p or args.rccl):  # the node-level tests once, after the rounds
             b["fabric"] = fabric_tests(devices, args.p2p, args.rccl, args.timeout or None)
             b["pass"] = b["pass"] and all(r.get("pass") for r in b["fabric"].values())
