@@ -908,9 +908,11 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
     rounds = 0
     series: Dict[int, Dict[str, List[float]]] = {d: {} for d in devices}
     failures: List[Dict[str, Any]] = []
+    failed_rounds = 0
     while True:
         res = run_devices(level, devices, parallel)
         rounds += 1
+        bad: List[str] = []
         for d, tests in res.items():
             for test, r in tests.items():
                 if not isinstance(r, dict):
@@ -920,18 +922,20 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
                         series[d].setdefault(f"{test}.{key}", []).append(float(r[key]))
                 for kind, row in ((r.get("kinds") or {}) if isinstance(r.get("kinds"), dict) else {}).items():
                     series[d].setdefault(f"{test}.{kind}.tflops", []).append(float(row.get("tflops", 0)))
-                if r.get("pass") is False and len(failures) < 20:
-                    failures.append({"round": rounds, "t_s": round(clock() - t0, 1), "device": d, "test": test,
-                                     "detail": r.get("detail", "")})
+                if r.get("pass") is False:
+                    bad.append(f"gpu{d}:{test}")
+                    if len(failures) < 20:
+                        failures.append({"round": rounds, "t_s": round(clock() - t0, 1), "device": d, "test": test,
+                                         "detail": r.get("detail", "")})
+        failed_rounds += 1 if bad else 0
         if progress is not None:  # one line per round (operators watching a long burn-in, CI log liveness)
-            bad = sorted({f"gpu{f['device']}:{f['test']}" for f in failures if f["round"] == rounds})
             progress(f"burn-in round {rounds} at {clock() - t0:.0f} s: " + ("FAIL " + " ".join(bad) if bad else "pass"))
         if clock() - t0 >= 60.0 * minutes:
             break
     summary = {d: {k: {"min": round(min(v), 3), "median": round(statistics.median(v), 3), "max": round(max(v), 3)}
                    for k, v in m.items()} for d, m in series.items()}
-    return {"minutes": minutes, "rounds": rounds, "wall_s": round(clock() - t0, 1), "pass": not failures,
-            "failures": failures, "devices": summary}
+    return {"minutes": minutes, "rounds": rounds, "failed_rounds": failed_rounds, "wall_s": round(clock() - t0, 1),
+            "pass": failed_rounds == 0, "failures": failures, "devices": summary}
 
 
 def main(argv=None) -> int:

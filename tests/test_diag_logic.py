@@ -356,6 +356,11 @@ def test_burn_in_reports_spread_and_every_failing_round(fake, capsys):
     fake(n=2, gpu_rate={1: 0.5})
     b = diag.burn_in(1, [0, 1], minutes=0.0005)
     assert not b["pass"] and {f["device"] for f in b["failures"]} == {1} and b["failures"][0]["round"] == 1
+    assert b["failed_rounds"] == b["rounds"]
+    lines = []
+    fake(n=2, gpu_rate={1: 0.5})
+    diag.burn_in(1, [0, 1], minutes=0.0005, progress=lines.append)
+    assert lines and all(ln.startswith("burn-in round ") and "FAIL gpu1:" in ln for ln in lines)
     assert diag.main(["--level", "1", "--duration", "0.0005"]) == 1
     assert json.loads(capsys.readouterr().out)["failures"]
     fake(n=1)
