@@ -1585,6 +1585,43 @@ int diag_p2p_copy_t(int src, int dst, size_t bytes, int iters, double timeout_ms
   return 0;
 }
 
+// Self-test of the polled deadline the pair copies wait with (wait_event_polled), on one GPU: queue `launches`
+// full-buffer writes of 1 GiB (finite work, ~0.15 ms each on MI355X) on a stream of their own, wait for them
+// with a `deadline_ms` deadline -- *timed_out = 1 when the deadline passed first, *waited_ms how long that
+// took -- then drain the stream (*drained_ms) before freeing, so nothing is left running.  The hung-pair path
+// of diag_p2p_copy_t cannot be provoked on a healthy node; this shows the same wait returning at its deadline.
+int diag_poll_selftest(int device, int launches, double deadline_ms, int* timed_out, double* waited_ms,
+                       double* drained_ms) {
+  if (launches < 1 || launches > 100000 || deadline_ms <= 0.0) {
+    g_err = "poll selftest: launches in [1, 100000] and a positive deadline";
+    return -2;
+  }
+  int cur = 0;
+  DIAG_CHECK(hipGetDevice(&cur));
+  constexpr size_t bytes = size_t(1) << 30;
+  DevBuf buf;
+  DIAG_CHECK(buf.alloc(device, bytes));
+  Timer tm;
+  DIAG_CHECK(tm.create(true));
+  const size_t n = bytes / sizeof(f32x4);
+  for (int i = 0; i < launches; ++i)
+    hipLaunchKernelGGL(write_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, tm.stream,
+                       static_cast<f32x4*>(buf.ptr), n, 1.0f);
+  DIAG_CHECK(hipGetLastError());
+  DIAG_CHECK(hipEventRecord(tm.e1, tm.stream));
+  const auto t0 = SteadyClock::now();
+  const hipError_t w = wait_event_polled(tm.e1, PollDeadline(deadline_ms));
+  const auto t1 = SteadyClock::now();
+  *timed_out = w == hipErrorNotReady;
+  *waited_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  const hipError_t d = hipEventSynchronize(tm.e1);  // finite work: drain before the buffer is freed
+  *drained_ms = std::chrono::duration<double, std::milli>(SteadyClock::now() - t1).count();
+  if (w != hipSuccess && w != hipErrorNotReady) DIAG_CHECK(w);
+  DIAG_CHECK(d);
+  DIAG_CHECK(hipSetDevice(cur));
+  return 0;
+}
+
 int diag_p2p_copy(int src, int dst, size_t bytes, int iters, double* gbps, unsigned long long* errors, int* peer) {
   return diag_p2p_copy_t(src, dst, bytes, iters, 0.0, gbps, errors, peer);
 }

@@ -214,6 +214,8 @@ def lib() -> ctypes.CDLL:
         L.diag_p2p_copy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                     ctypes.POINTER(ctypes.c_int)]
+        L.diag_poll_selftest.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.diag_p2p_copy_t.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                       ctypes.POINTER(ctypes.c_int)]
@@ -617,6 +619,14 @@ def host_link(device: int = 0, mib: int = 256, iters: int = 5, scale: Scale = FU
            "wall_s": round(time.perf_counter() - t0, 3)}
     exp = {k: v * scale.compute for k, v in REFERENCE_RATES["host_link"].items()}
     return _rated(res, {"h2d_gbps": h2d.value, "d2h_gbps": d2h.value}, exp, "GB/s")
+
+
+def poll_selftest(device: int = 0, launches: int = 1000, deadline_ms: float = 20.0) -> Dict[str, Any]:
+    """The polled deadline the xGMI pair copies wait with, shown on one GPU: ``launches`` queued 1 GiB writes
+    waited for with a ``deadline_ms`` deadline (``timed_out``: the deadline came first), then drained."""
+    t, w, d = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+    _check(lib().diag_poll_selftest(device, launches, deadline_ms, ctypes.byref(t), ctypes.byref(w), ctypes.byref(d)))
+    return {"timed_out": bool(t.value), "waited_ms": round(w.value, 3), "drained_ms": round(d.value, 3)}
 
 
 P2P_HUNG = -4  # diag_p2p_copy_t: the copies (or their verification) missed the deadline

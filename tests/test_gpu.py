@@ -479,6 +479,18 @@ def test_agent_diagnostics_threads_per_device(dev):
     assert all("diag" in g for g in rep["gpus"][: diag.device_count()])
 
 
+def test_polled_deadline_returns_at_its_deadline(dev):
+    """The wait the xGMI pair copies use (diag_p2p_copy_t) on real HIP: ~150 ms of queued work waited for with a
+    20 ms deadline comes back at the deadline, and the work then drains; with a generous deadline it completes."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.poll_selftest(0, launches=1000, deadline_ms=20.0)
+    assert r["timed_out"] and 19.0 <= r["waited_ms"] < 60.0 and r["drained_ms"] > 10.0, r
+    r = diag.poll_selftest(0, launches=10, deadline_ms=5000.0)
+    assert not r["timed_out"] and r["waited_ms"] < 1000.0, r
+    with pytest.raises(RuntimeError, match="positive deadline"):
+        diag.poll_selftest(0, launches=10, deadline_ms=0.0)
+
+
 def test_burn_in_on_this_box(dev):
     """``mi355x-diag --duration``: the level-1 suite round after round on the real GPU, every round passing,
     each rate reported as a min / median / max spread."""
