@@ -1457,9 +1457,15 @@ int diag_hbm_bandwidth(int device, size_t bytes, int iters, double* copy_tbs, do
 }
 
 // Pattern test over `bytes` of HBM; `passes` x (pattern, inverted pattern).
-int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned long long* errors,
-                 unsigned long long* first_bad_byte, double* gbps) {
+// `inject_word` >= 0: that 16-byte word is overwritten (0xA5 bytes) between the first write and its verify --
+// the fault-injection check that a corrupted word is counted and located (diag.memtest(inject_word=...))
+int diag_memtest_x(int device, size_t bytes, uint64_t seed, int passes, long long inject_word,
+                   unsigned long long* errors, unsigned long long* first_bad_byte, double* gbps) {
   DIAG_CHECK(hipSetDevice(device));
+  if (inject_word >= 0 && static_cast<size_t>(inject_word) >= bytes / sizeof(uint4)) {
+    g_err = "memtest: inject_word outside the buffer";
+    return -2;
+  }
   const size_t n = bytes / sizeof(uint4);
   DevBuf bp, bdev;
   DIAG_CHECK(bp.alloc(device, n * sizeof(uint4)));
@@ -1477,6 +1483,8 @@ int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned l
     for (int inv = 0; inv < 2; ++inv) {
       const uint64_t s = seed + static_cast<uint64_t>(pass) * 0x9E3779B97F4A7C15ULL;
       hipLaunchKernelGGL(mt_write_kernel, dim3(grid), dim3(256), 0, nullptr, p, n, s, inv);
+      if (inject_word >= 0 && pass == 0 && inv == 0)
+        DIAG_CHECK(hipMemsetAsync(p + inject_word, 0xA5, sizeof(uint4), nullptr));
       hipLaunchKernelGGL(mt_verify_kernel, dim3(grid), dim3(256), 0, nullptr, p, n, s, inv, dev, dev + 1);
     }
   }
@@ -1489,6 +1497,11 @@ int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned l
   *first_bad_byte = h[0] ? h[1] * sizeof(uint4) : ~0ULL;
   *gbps = 4.0 * passes * static_cast<double>(n * sizeof(uint4)) / (elapsed_ms(e0, e1) * 1e-3) / 1e9;
   return 0;
+}
+
+int diag_memtest(int device, size_t bytes, uint64_t seed, int passes, unsigned long long* errors,
+                 unsigned long long* first_bad_byte, double* gbps) {
+  return diag_memtest_x(device, bytes, seed, passes, -1, errors, first_bad_byte, gbps);
 }
 
 // xGMI point-to-point check between two GPUs of the node: `iters` copies of `bytes` from `src` to

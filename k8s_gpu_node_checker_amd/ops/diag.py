@@ -214,6 +214,9 @@ def lib() -> ctypes.CDLL:
         L.diag_p2p_copy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                     ctypes.POINTER(ctypes.c_int)]
+        L.diag_memtest_x.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, ctypes.c_longlong,
+                                     ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong),
+                                     ctypes.POINTER(ctypes.c_double)]
         L.diag_poll_selftest.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_int),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.diag_p2p_copy_t.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
@@ -380,11 +383,18 @@ def hbm(device: int = 0, gib: float = 4.0, iters: int = 10, scale: Scale = FULL)
     return _rated(res, {"copy_tbs": c.value, "read_tbs": r.value}, exp, "TB/s")
 
 
-def memtest(device: int = 0, gib: float = 8.0, passes: int = 1, seed: int = 0x5EED) -> Dict[str, Any]:
+def memtest(device: int = 0, gib: float = 8.0, passes: int = 1, seed: int = 0x5EED,
+            inject_word: Optional[int] = None) -> Dict[str, Any]:
+    """Pattern + inverse over ``gib`` of HBM, every word checked.  ``inject_word`` (a test hook) overwrites that
+    16-byte word between the first write and its check, to show a corrupted word is counted and located."""
     errs, first, gbps = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_double()
     t0 = time.perf_counter()
-    _check(lib().diag_memtest(device, int(gib * (1 << 30)), seed, passes, ctypes.byref(errs), ctypes.byref(first),
-                              ctypes.byref(gbps)))
+    if inject_word is None:
+        _check(lib().diag_memtest(device, int(gib * (1 << 30)), seed, passes, ctypes.byref(errs),
+                                  ctypes.byref(first), ctypes.byref(gbps)))
+    else:
+        _check(lib().diag_memtest_x(device, int(gib * (1 << 30)), seed, passes, inject_word, ctypes.byref(errs),
+                                    ctypes.byref(first), ctypes.byref(gbps)))
     ok = errs.value <= MEMTEST_MAX_ERRORS
     res: Dict[str, Any] = {"pass": ok, "errors": errs.value, "gib": gib, "passes": passes,
                            "gbps": round(gbps.value, 1), "wall_s": round(time.perf_counter() - t0, 3),

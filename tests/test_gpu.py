@@ -273,6 +273,17 @@ def test_diag_memtest_clean(dev):
     assert r["errors"] == 0 and r["pass"], r
 
 
+def test_memtest_counts_and_locates_an_injected_word(dev):
+    """A 16-byte word overwritten between the pattern write and its check is counted once and located to its
+    byte offset; the same run without the injection is clean."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.memtest(0, gib=1.0, inject_word=123457)
+    assert not r["pass"] and r["errors"] == 1 and r["first_bad_byte"] == 123457 * 16, r
+    assert diag.memtest(0, gib=1.0)["errors"] == 0
+    with pytest.raises(RuntimeError, match="outside the buffer"):
+        diag.memtest(0, gib=1.0, inject_word=1 << 40)
+
+
 def test_diag_failed_allocation_leaks_nothing(dev):
     """A diagnostic that runs out of device memory half-way (the agent's GPU got busy) frees what it
     already took and leaves no error behind for the next call: the agent calls these for the life
