@@ -121,9 +121,7 @@ DIAG_PARALLEL = 8
 # /healthz fails once a diagnostic thread has outlived this many --diag-timeout: its verdict (watchdog) went
 # out at 1x; a thread in a hung HIP call cannot be cancelled, so only a fresh process frees its GPU
 HUNG_RESTART_FACTOR = 2.0
-# share of --diag-timeout the node-level xGMI pair matrix may use before the RCCL suite (an 8-GPU matrix is
-# 56 pairs of 6 x 256 MiB copies plus a verify pass each: seconds at xGMI rates, far inside 0.45 x the timeout)
-P2P_SHARE = 0.45
+from ..ops.diag import P2P_SHARE  # noqa: E402  (share of --diag-timeout the xGMI pair matrix may use)
 
 
 # Host memory of the agent process (MiB), measured on one MI355X (profiles/agent_rss_*_mi355x.json,
@@ -673,33 +671,20 @@ class Agent:
 
     @staticmethod
     def _fabric_suite(devices: List[int], timeout_s: Optional[float] = None) -> Dict[str, Any]:
-        """The node-level tests: xGMI pair matrix and the RCCL collectives in this process (ops/fabric.py).  Both
-        run under the watchdog's deadline -- the pair matrix within the first ``P2P_SHARE`` of it, the collectives
-        within what is left up to 90 % -- so a hung copy or collective is given up (and named in the report)
+        """The node-level tests (``ops/diag.fabric_tests``): the xGMI pair matrix and the RCCL collectives in this
+        process, both under the watchdog's deadline -- the matrix within ``P2P_SHARE`` of it, the collectives
+        within what is left up to 90 % -- so a hung copy or collective is given up, and named in the report,
         rather than left holding the fabric thread."""
         from ..ops import diag
-        out: Dict[str, Any] = {}
-        t0 = time.monotonic()
         try:
-            m = diag.p2p_matrix(devices, timeout_s=P2P_SHARE * timeout_s) if timeout_s else diag.p2p_matrix(devices)
-            out["p2p"] = {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s")}
-            if m.get("stopped"):
-                out["p2p"]["stopped"] = m["stopped"]
-        except Exception as e:
-            out["p2p"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
-        try:
-            from ..ops import fabric
-            if timeout_s:
-                # the collectives abort themselves a little before the agent's watchdog fires, so the report
-                # says which collective hung rather than only "the fabric suite did not return"
-                left = 0.9 * timeout_s - (time.monotonic() - t0)
-                r = fabric.collective_suite(devices, timeout_s=max(0.001, left))
-            else:
-                r = fabric.collective_suite(devices)
-            out["rccl"] = {k: r.get(k) for k in ("pass", "best_busbw_gbps", "best_busbw_by_op", "detail", "wall_s",
-                                                 "rccl", "aborted") if k in r or k != "aborted"}
-        except Exception as e:
-            out["rccl"] = {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}
+            res = diag.fabric_tests(devices, timeout_s=timeout_s or None)
+        except Exception as e:  # the diag library itself is missing
+            return {"p2p": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
+        m, r = res.get("p2p") or {}, res.get("rccl") or {}
+        out: Dict[str, Any] = {"p2p": {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s",
+                                                         "stopped") if k in m}}
+        out["rccl"] = {k: r.get(k) for k in ("pass", "best_busbw_gbps", "best_busbw_by_op", "detail", "wall_s",
+                                             "rccl", "aborted") if k in r or k not in ("aborted",)}
         return out
 
     def _allocated(self) -> Optional[Dict[str, str]]:
