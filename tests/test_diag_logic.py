@@ -400,3 +400,20 @@ def test_run_devices_raises_a_missing_library_in_the_caller(monkeypatch):
     monkeypatch.setattr(diag, "run", flaky)
     out = diag.run_devices(1, [0, 1, 2], parallel=3)
     assert out[1]["run"]["pass"] is False and "out of memory" in out[1]["run"]["detail"] and out[0]["gemm"]["pass"]
+
+
+def test_fabric_tests_report_a_raising_test_as_failed(fake, monkeypatch):
+    from k8s_gpu_node_checker_amd.ops import fabric
+    fake(n=2)
+
+    def boom(*a, **kw):
+        raise OSError("librccl.so.1: cannot open shared object file")
+    monkeypatch.setattr(fabric, "collective_suite", boom)
+    out = diag.fabric_tests([0, 1], timeout_s=10.0)
+    assert out["p2p"]["pass"] and out["rccl"]["pass"] is False and "librccl" in out["rccl"]["detail"]
+
+    def bad_pair(*a, **kw):
+        raise RuntimeError("mi355x diag failed (-1): hipMalloc: out of memory")
+    monkeypatch.setattr(diag, "p2p_matrix", bad_pair)
+    out = diag.fabric_tests([0, 1], rccl=False)
+    assert out["p2p"]["pass"] is False and "out of memory" in out["p2p"]["detail"] and "rccl" not in out
