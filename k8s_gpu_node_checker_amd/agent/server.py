@@ -89,7 +89,8 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
         for test, res in (g.get("diag") or {}).items():
             if not isinstance(res, dict):
                 continue
-            for k in ("tflops", "copy_tbs", "read_tbs", "errors", "h2d_gbps", "d2h_gbps", "fraction"):
+            for k in ("tflops", "copy_tbs", "read_tbs", "errors", "h2d_gbps", "d2h_gbps", "fraction",
+                      "checksum_bad_tiles"):
                 if isinstance(res.get(k), (int, float)) and not isinstance(res.get(k), bool):
                     put(f"mi355x_gpu_diag_{k}", f'{lbl},test="{_esc(test)}"', res[k])
             for xcd, v in ((res.get("alone_tbs") or {}) if isinstance(res.get("alone_tbs"), dict) else {}).items():

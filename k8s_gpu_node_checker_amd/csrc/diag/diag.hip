@@ -740,6 +740,88 @@ __global__ void gemm_ref_fp8_kernel(const uint8_t* A, const uint8_t* Bt, const i
   mag[i] = m;
 }
 
+// ---------------------------------------------------------------- whole-output GEMM check
+// The sampled check above reads 4,096 of the 67 M outputs of an 8192^2 GEMM: a matrix core that corrupts the
+// tiles of one workgroup slot is found only if a sample lands there.  Checksums cover every output at the cost
+// of one pass over C (Huang & Abraham's algorithm-based fault tolerance): for each tile-high block of rows tb,
+// sum_i C[i][j] (i in tb) must equal sum_k (sum_i A[i][k]) Bt[j][k].  Both sides are formed in fp64 from the
+// exact operand values, so the only difference is the GEMM's own fp32 rounding, bounded by
+// mag[tb][j] = sum_k (sum_i |A[i][k]|) |Bt[j][k]|; a column whose difference exceeds tol * mag marks the tile
+// (tb, j / tile width) bad, and the launch's blockIdx -> tile order names the XCD that computed it.
+template <int DT>
+__device__ __forceinline__ double ck_value(const void* p, size_t i) {
+  if constexpr (DT == DT_BF16) return static_cast<double>(static_cast<const __bf16*>(p)[i]);
+  else return e4m3_value(static_cast<const uint8_t*>(p)[i]);
+}
+
+// asum[tb][k] = sum of the RB rows of block tb in column k, aabs the same over |A|; thread per column (coalesced)
+template <int DT>
+__global__ void __launch_bounds__(256) ck_asum_kernel(const void* A, double* asum, double* aabs, int K, int RB) {
+  const int k = blockIdx.x * 256 + threadIdx.x, tb = blockIdx.y;
+  if (k >= K) return;
+  double s = 0.0, m = 0.0;
+  for (int i = 0; i < RB; ++i) {
+    const double v = ck_value<DT>(A, static_cast<size_t>(tb * RB + i) * K + k);
+    s += v;
+    m += fabs(v);
+  }
+  asum[static_cast<size_t>(tb) * K + k] = s;
+  aabs[static_cast<size_t>(tb) * K + k] = m;
+}
+
+// ref[tb][j] = asum[tb] . Bt[j], mag[tb][j] = aabs[tb] . |Bt[j]|: thread per column j, CK_TB row blocks per
+// workgroup, Bt staged through LDS 32 k at a time (coalesced along k; the +1 pad keeps the column reads apart)
+constexpr int CK_TB = 8, CK_KC = 32;
+template <int DT>
+__global__ void __launch_bounds__(256) ck_ref_kernel(const void* Bt, const double* asum, const double* aabs,
+                                                     double* ref, double* mag, int N, int K, int nblk) {
+  __shared__ float bs[256][CK_KC + 1];
+  __shared__ double as[CK_TB][CK_KC], am[CK_TB][CK_KC];
+  const int tid = threadIdx.x, j0 = blockIdx.x * 256, tb0 = blockIdx.y * CK_TB;
+  double r[CK_TB], g[CK_TB];
+#pragma unroll
+  for (int t = 0; t < CK_TB; ++t) r[t] = g[t] = 0.0;
+  for (int k0 = 0; k0 < K; k0 += CK_KC) {
+    for (int idx = tid; idx < 256 * CK_KC; idx += 256) {
+      const int row = idx / CK_KC, kk = idx % CK_KC;
+      bs[row][kk] = j0 + row < N ? static_cast<float>(ck_value<DT>(Bt, static_cast<size_t>(j0 + row) * K + k0 + kk))
+                                 : 0.f;
+    }
+    for (int idx = tid; idx < CK_TB * CK_KC; idx += 256) {
+      const int t = idx / CK_KC, kk = idx % CK_KC;
+      const bool ok = tb0 + t < nblk;
+      as[t][kk] = ok ? asum[static_cast<size_t>(tb0 + t) * K + k0 + kk] : 0.0;
+      am[t][kk] = ok ? aabs[static_cast<size_t>(tb0 + t) * K + k0 + kk] : 0.0;
+    }
+    __syncthreads();
+    for (int kk = 0; kk < CK_KC; ++kk) {
+      const double b = bs[tid][kk], bb = fabs(b);
+#pragma unroll
+      for (int t = 0; t < CK_TB; ++t) {
+        r[t] += as[t][kk] * b;
+        g[t] += am[t][kk] * bb;
+      }
+    }
+    __syncthreads();
+  }
+  if (j0 + tid >= N) return;
+#pragma unroll
+  for (int t = 0; t < CK_TB; ++t)
+    if (tb0 + t < nblk) {
+      ref[static_cast<size_t>(tb0 + t) * N + j0 + tid] = r[t];
+      mag[static_cast<size_t>(tb0 + t) * N + j0 + tid] = g[t];
+    }
+}
+
+// csum[tb][j] = sum of the RB rows of block tb of C in column j, in fp64; thread per column (coalesced)
+__global__ void __launch_bounds__(256) ck_csum_kernel(const float* C, double* csum, int N, int RB) {
+  const int j = blockIdx.x * 256 + threadIdx.x, tb = blockIdx.y;
+  if (j >= N) return;
+  double s = 0.0;
+  for (int i = 0; i < RB; ++i) s += C[static_cast<size_t>(tb * RB + i) * N + j];
+  csum[static_cast<size_t>(tb) * N + j] = s;
+}
+
 // ---------------------------------------------------------------- HBM streams
 // Forms picked by the sweeps in tools/hbm_explore.hip on MI355X (profiles/hbm_explore_mi355x.json):
 // one 16-byte element per thread and a grid over the whole buffer (no grid-stride loop), nontemporal
@@ -1151,6 +1233,100 @@ int launch_v3(const void* A, const void* Bt, float* C, int M, int N, int Kcols, 
                          : launch_v3_inst<DT, false, false, 1>(A, Bt, C, M, N, Kcols, stream);
 }
 
+// The bf16 kernel diag_gemm_bf16_launch runs for M x N: 1 = v1 (128^2 tiles), 2 = v2, 3 = v3 (256^2).  v2/v3
+// need 256-multiples and enough 256^2 tiles to occupy the 256 CUs (one block per CU); below that the 128^2
+// kernel's 4x larger grid wins (measured: 2048^3 v1 543 vs v2 321 TFLOP/s).
+int bf16_variant(int M, int N) {
+  const bool big_ok = M % V2_BM == 0 && N % V2_BN == 0 && (M / V2_BM) * (N / V2_BN) >= 256;
+  return g_gemm_variant == 0 ? (big_ok ? 3 : 1) : g_gemm_variant;
+}
+
+// Output tiles of a launch and their blockIdx regrouping (the mapping at the top of every GEMM kernel).
+struct TileGeom {
+  int rows, cols, group_m;
+};
+constexpr TileGeom kGeomV1{BM, BN, 8}, kGeomV3{V2_BM, V2_BN, 4};
+
+// The XCD that computed each tile: workgroup b is dispatched to XCD b % 8 and computes the tile the regrouping
+// gives it.
+std::vector<int> tile_xcds(int tiles_m, int tiles_n, int group_m) {
+  const int nwg = tiles_m * tiles_n, q = nwg / 8, r = nwg % 8;
+  std::vector<int> out(static_cast<size_t>(nwg), -1);
+  for (int b = 0; b < nwg; ++b) {
+    const int xcd = b % 8;
+    const int bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+    const int first_m = bid / (group_m * tiles_n) * group_m;
+    const int gsize = std::min(tiles_m - first_m, group_m);
+    const int tm = first_m + (bid % (group_m * tiles_n)) % gsize, tn = (bid % (group_m * tiles_n)) / gsize;
+    out[static_cast<size_t>(tm) * tiles_n + tn] = xcd;
+  }
+  return out;
+}
+
+// Whole-output check of C = A . Bt^T (the ck_* kernels).  ck_out[0] bad tiles, [1] bad columns, [2..9] bad tiles
+// per XCD, [10] / [11] the first bad tile's (row, column) in tiles or -1; *max_err the worst |csum - ref| / mag.
+// A NaN or infinite sum counts as bad.
+constexpr int kCkOut = 12;
+template <int DT>
+int gemm_checksum(int device, const void* A, const void* Bt, const float* C, int M, int N, int K, TileGeom g,
+                  double tol, double* max_err, long long* ck_out) {
+  const int nblk = M / g.rows, tiles_n = N / g.cols;
+  const size_t kb = sizeof(double) * static_cast<size_t>(nblk) * K, nb = sizeof(double) * static_cast<size_t>(nblk) * N;
+  DevBuf asum, aabs, ref, mag, csum;
+  DIAG_CHECK(asum.alloc(device, kb));
+  DIAG_CHECK(aabs.alloc(device, kb));
+  DIAG_CHECK(ref.alloc(device, nb));
+  DIAG_CHECK(mag.alloc(device, nb));
+  DIAG_CHECK(csum.alloc(device, nb));
+  double* as = static_cast<double*>(asum.ptr);
+  double* am = static_cast<double*>(aabs.ptr);
+  hipLaunchKernelGGL(ck_asum_kernel<DT>, dim3((K + 255) / 256, nblk), dim3(256), 0, nullptr, A, as, am, K, g.rows);
+  hipLaunchKernelGGL(ck_ref_kernel<DT>, dim3((N + 255) / 256, (nblk + CK_TB - 1) / CK_TB), dim3(256), 0, nullptr, Bt,
+                     as, am, static_cast<double*>(ref.ptr), static_cast<double*>(mag.ptr), N, K, nblk);
+  hipLaunchKernelGGL(ck_csum_kernel, dim3((N + 255) / 256, nblk), dim3(256), 0, nullptr, C,
+                     static_cast<double*>(csum.ptr), N, g.rows);
+  DIAG_CHECK(hipGetLastError());
+  const size_t cnt = static_cast<size_t>(nblk) * N;
+  std::vector<double> hr(cnt), hm(cnt), hc(cnt);
+  DIAG_CHECK(hipMemcpy(hr.data(), ref.ptr, nb, hipMemcpyDeviceToHost));
+  DIAG_CHECK(hipMemcpy(hm.data(), mag.ptr, nb, hipMemcpyDeviceToHost));
+  DIAG_CHECK(hipMemcpy(hc.data(), csum.ptr, nb, hipMemcpyDeviceToHost));
+  const std::vector<int> xcd = tile_xcds(nblk, tiles_n, g.group_m);
+  std::vector<char> bad(static_cast<size_t>(nblk) * tiles_n, 0);
+  double worst = 0.0;
+  long long cols = 0;
+  for (size_t i = 0; i < cnt; ++i) {
+    const double e = std::fabs(hc[i] - hr[i]) / std::max(hm[i], 1e-30);
+    if (!(e <= tol)) {  // also NaN
+      ++cols;
+      const size_t tb = i / N, j = i % N;
+      bad[tb * tiles_n + j / g.cols] = 1;
+    }
+    worst = std::isfinite(e) ? std::max(worst, e) : HUGE_VAL;
+  }
+  for (int i = 0; i < kCkOut; ++i) ck_out[i] = 0;
+  ck_out[1] = cols;
+  ck_out[10] = ck_out[11] = -1;
+  for (size_t t = 0; t < bad.size(); ++t) {
+    if (!bad[t]) continue;
+    ++ck_out[0];
+    if (xcd[t] >= 0) ++ck_out[2 + xcd[t]];
+    if (ck_out[10] < 0) {
+      ck_out[10] = static_cast<long long>(t / tiles_n);
+      ck_out[11] = static_cast<long long>(t % tiles_n);
+    }
+  }
+  *max_err = worst;
+  return 0;
+}
+
+// A test hook: overwrite output element `elem` of C with 1e6 (an error every check must see).
+hipError_t inject_output(float* C, long long elem, long long count) {
+  if (elem < 0 || elem >= count) return hipSuccess;
+  const float v = 1e6f;
+  return hipMemcpy(C + elem, &v, sizeof(v), hipMemcpyHostToDevice);
+}
+
 }  // namespace
 
 // Polled completion with a deadline (diag_p2p_copy_t): a hung copy engine or link must not block the caller.
@@ -1224,10 +1400,7 @@ int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N,
     g_err = "gemm_bf16: M, N must be multiples of 128 and K a multiple of 64";
     return -2;
   }
-  // v2 needs 256-multiples and enough 256x256 tiles to occupy the 256 CUs (one block per CU);
-  // below that the 128x128 kernel's 4x larger grid wins (measured: 2048^3 v1 543 vs v2 321 TFLOP/s)
-  const bool big_ok = M % V2_BM == 0 && N % V2_BN == 0 && (M / V2_BM) * (N / V2_BN) >= 256;
-  const int variant = g_gemm_variant == 0 ? (big_ok ? 3 : 1) : g_gemm_variant;
+  const int variant = bf16_variant(M, N);
   if (variant == 2 || variant == 3) {
     if (M % V2_BM || N % V2_BN) {
       g_err = "gemm_bf16 v2/v3: M, N must be multiples of 256";
@@ -1278,10 +1451,16 @@ int diag_gemm_fp4_launch(const void* A, const void* Bt, float* C, int M, int N, 
   return 0;
 }
 
-// Self-contained MFMA burn-in: allocate, fill, run `iters` GEMMs, time them,
-// verify `nsamp` sampled outputs against the fp32 reference kernel.
-int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int nsamp, double* tflops,
-                   double* max_rel_err, double* ms_per_iter) {
+// Self-contained MFMA burn-in: allocate, fill, run `iters` GEMMs, time them, verify `nsamp` sampled outputs
+// against the fp32 reference kernel and, with ck_tol >= 0, every output by tile checksums (gemm_checksum:
+// *ck_err, ck_out[kCkOut]).  `inject_elem` >= 0 overwrites that output between the timing and the checks.
+int diag_gemm_bf16_x(int device, int M, int N, int K, int warmup, int iters, int nsamp, long long inject_elem,
+                     double ck_tol, double* tflops, double* max_rel_err, double* ms_per_iter, double* ck_err,
+                     long long* ck_out) {
+  if (inject_elem >= static_cast<long long>(M) * N) {
+    g_err = "gemm: inject_elem outside the output";
+    return -2;
+  }
   if (M % BM || N % BN || K % BK) {
     g_err = "gemm_bf16: M, N must be multiples of 128 and K a multiple of 64";
     return -2;
@@ -1325,6 +1504,7 @@ int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int n
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   const double ms = elapsed_ms(e0, e1) / std::max(iters, 1);
+  DIAG_CHECK(inject_output(C, inject_elem, static_cast<long long>(M) * N));
   hipLaunchKernelGGL(gemm_ref_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, A, Bt, rows, cols, ref,
                      nsamp, K);
   DIAG_CHECK(hipGetLastError());
@@ -1343,12 +1523,27 @@ int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int n
   *max_rel_err = worst;
   *ms_per_iter = ms;
   *tflops = 2.0 * M * N * static_cast<double>(K) / (ms * 1e-3) / 1e12;
+  if (ck_tol >= 0.0) {
+    const int v = bf16_variant(M, N);
+    return gemm_checksum<DT_BF16>(device, A, Bt, C, M, N, K, v == 1 ? kGeomV1 : kGeomV3, ck_tol, ck_err, ck_out);
+  }
   return 0;
 }
 
-// MX-fp8 counterpart of diag_gemm_bf16: *max_err = max |C - ref| / sum|a*b| over the samples.
-int diag_gemm_fp8(int device, int M, int N, int K, int warmup, int iters, int nsamp, double* tflops,
-                  double* max_err, double* ms_per_iter) {
+int diag_gemm_bf16(int device, int M, int N, int K, int warmup, int iters, int nsamp, double* tflops,
+                   double* max_rel_err, double* ms_per_iter) {
+  return diag_gemm_bf16_x(device, M, N, K, warmup, iters, nsamp, -1, -1.0, tflops, max_rel_err, ms_per_iter,
+                          nullptr, nullptr);
+}
+
+// MX-fp8 counterpart of diag_gemm_bf16_x: *max_err = max |C - ref| / sum|a*b| over the samples.
+int diag_gemm_fp8_x(int device, int M, int N, int K, int warmup, int iters, int nsamp, long long inject_elem,
+                    double ck_tol, double* tflops, double* max_err, double* ms_per_iter, double* ck_err,
+                    long long* ck_out) {
+  if (inject_elem >= static_cast<long long>(M) * N) {
+    g_err = "gemm: inject_elem outside the output";
+    return -2;
+  }
   if (M % V2_BM || N % V2_BN || K % 128 || nsamp < 1) {
     g_err = "gemm_fp8: M, N must be multiples of 256, K a multiple of 128";
     return -2;
@@ -1390,6 +1585,7 @@ int diag_gemm_fp8(int device, int M, int N, int K, int warmup, int iters, int ns
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   const double ms = elapsed_ms(e0, e1) / std::max(iters, 1);
+  DIAG_CHECK(inject_output(c, inject_elem, static_cast<long long>(M) * N));
   const int* r = static_cast<const int*>(rows.ptr);
   const int* cl = static_cast<const int*>(cols.ptr);
   hipLaunchKernelGGL(gemm_ref_fp8_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr,
@@ -1409,7 +1605,15 @@ int diag_gemm_fp8(int device, int M, int N, int K, int warmup, int iters, int ns
   *max_err = worst;
   *ms_per_iter = ms;
   *tflops = 2.0 * M * N * static_cast<double>(K) / (ms * 1e-3) / 1e12;
+  if (ck_tol >= 0.0)
+    return gemm_checksum<DT_FP8>(device, A.ptr, Bt.ptr, c, M, N, K, kGeomV3, ck_tol, ck_err, ck_out);
   return 0;
+}
+
+int diag_gemm_fp8(int device, int M, int N, int K, int warmup, int iters, int nsamp, double* tflops,
+                  double* max_err, double* ms_per_iter) {
+  return diag_gemm_fp8_x(device, M, N, K, warmup, iters, nsamp, -1, -1.0, tflops, max_err, ms_per_iter, nullptr,
+                         nullptr);
 }
 
 // HBM streams over `bytes` per buffer: copy (read+write), read-only, write-only, in TB/s.

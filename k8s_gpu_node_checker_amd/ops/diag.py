@@ -18,7 +18,7 @@ from __future__ import annotations
 import ctypes
 import threading
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 from .native import NativeUnavailable, load_cdll
 
@@ -84,6 +84,12 @@ REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
 }
 GEMM_MAX_REL_ERR = 2e-3       # vs fp32 reference; bf16 inputs are exact in fp32, so ~1e-5 is typical
 GEMM_FP8_MAX_ERR = 4e-5       # |C - ref| / sum|a*b|: the MX MFMA's own accumulation error is <= 1.6e-5
+# whole-output tile checksums (diag.hip gemm_checksum): |column sum of a tile - fp64 reference| / sum|a*b| over
+# the same outputs.  Healthy MI355X maxima (profiles/gemm_checksum_mi355x.jsonl, deterministic run to run): bf16
+# 2.3e-9, MX-fp8 5.4e-7, so 43x / 18x margins.  At 8192^3 bf16 a tile column's sum|a*b| is ~5.2e5, so one output
+# off by more than ~0.05 (a typical output is ~30) fails its tile.
+GEMM_CK_TOL = 1e-7
+GEMM_FP8_CK_TOL = 1e-5
 MEMTEST_MAX_ERRORS = 0
 MFMA_KINDS = ("bf16", "fp8", "mxfp8", "mxfp4")
 P2P_MIN_FRACTION_OF_MEDIAN = 0.5  # a GPU pair slower than half the node's median pair: suspect link
@@ -187,6 +193,9 @@ def lib() -> ctypes.CDLL:
                                             ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_gemm_bf16.argtypes = [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_double)] * 3
         L.diag_gemm_fp8.argtypes = [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_double)] * 3
+        for f in ("diag_gemm_bf16_x", "diag_gemm_fp8_x"):
+            getattr(L, f).argtypes = [ctypes.c_int] * 7 + [ctypes.c_longlong, ctypes.c_double] + \
+                [ctypes.POINTER(ctypes.c_double)] * 4 + [ctypes.POINTER(ctypes.c_longlong)]
         L.diag_gemm_fp4_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_gemm_fp8_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -347,29 +356,62 @@ def _ref(test: str, key: Any, scale: float) -> float:
     return table[key] * scale
 
 
+def _checked_gemm(fn: str, device: int, size: int, warmup: int, iters: int, samples: int,
+                  inject_elem: Optional[int], ck_tol: float) -> Tuple[float, float, float, float, List[int]]:
+    tf, err, ms, ck = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    out = (ctypes.c_longlong * 12)()
+    _check(getattr(lib(), fn)(device, size, size, size, warmup, iters, samples,
+                              -1 if inject_elem is None else int(inject_elem), ck_tol, ctypes.byref(tf),
+                              ctypes.byref(err), ctypes.byref(ms), ctypes.byref(ck), out))
+    return tf.value, err.value, ms.value, ck.value, list(out)
+
+
+def _checksum_verdict(res: Dict[str, Any], ck_err: float, out: List[int], tol: float) -> str:
+    """Record the tile checksums in ``res``; a non-empty string describes the tiles that failed them."""
+    res["checksum_err"] = ck_err
+    res["checksum_bad_tiles"] = out[0]
+    if not out[0]:
+        return ""
+    xcds = {x: n for x, n in enumerate(out[2:10]) if n}
+    res["checksum_bad_columns"] = out[1]
+    res["checksum_bad_xcds"] = {str(x): n for x, n in xcds.items()}
+    res["checksum_first_bad_tile"] = [out[10], out[11]]
+    where = ", ".join(f"XCD {x}: {n}" for x, n in xcds.items())
+    return (f"{out[0]} output tile(s) fail their checksums ({where}; first at tile row {out[10]}, column "
+            f"{out[11]}; err {ck_err:.2e} > {tol:g})")
+
+
 def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, samples: int = 4096,
-         scale: Scale = FULL) -> Dict[str, Any]:
-    tf, err, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+         scale: Scale = FULL, inject_elem: Optional[int] = None) -> Dict[str, Any]:
+    """bf16 GEMM burn-in: rate, sampled fp32-reference error, and every output tile checked by its column
+    checksums (a bad tile is named with the XCD that computed it).  ``inject_elem`` (a test hook) overwrites
+    that output between the timing and the checks."""
     t0 = time.perf_counter()
-    _check(lib().diag_gemm_bf16(device, size, size, size, warmup, iters, samples, ctypes.byref(tf),
-                                ctypes.byref(err), ctypes.byref(ms)))
-    res = {"tflops": round(tf.value, 1), "max_rel_err": err.value, "ms_per_gemm": round(ms.value, 4),
+    tf, err, ms, ck, out = _checked_gemm("diag_gemm_bf16_x", device, size, warmup, iters, samples, inject_elem,
+                                         GEMM_CK_TOL)
+    res = {"tflops": round(tf, 1), "max_rel_err": err, "ms_per_gemm": round(ms, 4),
            "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3)}
-    return _rated(res, {"tflops": tf.value}, {"tflops": _ref("gemm", size, scale.compute)}, "TFLOP/s",
-                  err.value <= GEMM_MAX_REL_ERR, f"rel err {err.value:.2e} > {GEMM_MAX_REL_ERR:g}")
+    problems = [f"rel err {err:.2e} > {GEMM_MAX_REL_ERR:g}"] if not err <= GEMM_MAX_REL_ERR else []
+    bad = _checksum_verdict(res, ck, out, GEMM_CK_TOL)
+    problems += [bad] if bad else []
+    return _rated(res, {"tflops": tf}, {"tflops": _ref("gemm", size, scale.compute)}, "TFLOP/s",
+                  not problems, "; ".join(problems))
 
 
 def gemm_fp8(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20,
-             samples: int = 4096, scale: Scale = FULL) -> Dict[str, Any]:
-    """MX-fp8 GEMM burn-in: rate and sampled fp64-reference error (normalised by sum|a*b|)."""
-    tf, err, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+             samples: int = 4096, scale: Scale = FULL, inject_elem: Optional[int] = None) -> Dict[str, Any]:
+    """MX-fp8 GEMM burn-in: rate, sampled fp64-reference error (normalised by sum|a*b|) and the tile
+    checksums of every output, as ``gemm``."""
     t0 = time.perf_counter()
-    _check(lib().diag_gemm_fp8(device, size, size, size, warmup, iters, samples, ctypes.byref(tf),
-                               ctypes.byref(err), ctypes.byref(ms)))
-    res = {"tflops": round(tf.value, 1), "max_err_over_mag": err.value, "ms_per_gemm": round(ms.value, 4),
+    tf, err, ms, ck, out = _checked_gemm("diag_gemm_fp8_x", device, size, warmup, iters, samples, inject_elem,
+                                         GEMM_FP8_CK_TOL)
+    res = {"tflops": round(tf, 1), "max_err_over_mag": err, "ms_per_gemm": round(ms, 4),
            "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3)}
-    return _rated(res, {"tflops": tf.value}, {"tflops": _ref("gemm_fp8", size, scale.compute)}, "TFLOP/s",
-                  err.value <= GEMM_FP8_MAX_ERR, f"err {err.value:.2e} > {GEMM_FP8_MAX_ERR:g}")
+    problems = [f"err {err:.2e} > {GEMM_FP8_MAX_ERR:g}"] if not err <= GEMM_FP8_MAX_ERR else []
+    bad = _checksum_verdict(res, ck, out, GEMM_FP8_CK_TOL)
+    problems += [bad] if bad else []
+    return _rated(res, {"tflops": tf}, {"tflops": _ref("gemm_fp8", size, scale.compute)}, "TFLOP/s",
+                  not problems, "; ".join(problems))
 
 
 def hbm(device: int = 0, gib: float = 4.0, iters: int = 10, scale: Scale = FULL) -> Dict[str, Any]:
@@ -753,7 +795,7 @@ def _slow_only(res: Dict[str, Any]) -> bool:
     lagging = bool(_lag_notes(res.get("map") or {}, "")) or (res.get("slowest_xcd_rel") or 1.0) < XCD_ALONE_MIN_RATIO
     return (res.get("degraded") or not res.get("pass")) \
         and (res.get("fraction", 1.0) < DEGRADED_FRACTION or lagging) \
-        and "wrong results" not in res.get("detail", "") and "err " not in res.get("detail", "")
+        and not any(w in res.get("detail", "") for w in ("wrong results", "err ", "checksums"))
 
 
 def _goodness(res: Dict[str, Any]) -> tuple:

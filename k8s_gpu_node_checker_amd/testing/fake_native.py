@@ -30,6 +30,7 @@ class FakeDiagLib:
                  ``hung_pairs`` never completes (with a deadline: returns -4 at it; without: blocks until
                  ``release`` is set); ``p2p_wall_s`` = wall time of each completed pair
     delay_s:     wall time of each GEMM call (the agent's per-GPU threads overlap them)
+    gemm_bad_tiles: ``{(device, "gemm" | "gemm_fp8"): {xcd: tiles}}`` failing the GEMM's output checksums
     slow_xcd:    ``{xcd: factor}`` on the burn-in's per-XCD wave time; ``bad_cu[(device, kind)]`` = the CU
                  slot its ``mfma_errors`` come from
     """
@@ -45,7 +46,8 @@ class FakeDiagLib:
                  l2_bad: Optional[Dict[Tuple[int, int], int]] = None, slow_cu: Optional[Dict[int, float]] = None,
                  hbm_xcd_slow: Optional[Dict[int, float]] = None, hbm_bad: Optional[Dict[Tuple[int, int], int]] = None,
                  compute_rate: Optional[Dict[int, float]] = None,
-                 hung_pairs: Tuple[Tuple[int, int], ...] = (), p2p_wall_s: float = 0.0):
+                 hung_pairs: Tuple[Tuple[int, int], ...] = (), p2p_wall_s: float = 0.0,
+                 gemm_bad_tiles: Optional[Dict[Tuple[int, str], Dict[int, int]]] = None):
         from ..ops import diag
         self.ref = diag.REFERENCE_RATES
         self.kinds = diag.MFMA_KINDS
@@ -59,6 +61,7 @@ class FakeDiagLib:
         self.cus = cus
         self.mem_gib = mem_gib
         self.gemm_err = gemm_err
+        self.gemm_bad_tiles = dict(gemm_bad_tiles or {})
         self.mfma = mfma
         self.mfma_errors = dict(mfma_errors or {})
         self.link = link
@@ -143,6 +146,34 @@ class FakeDiagLib:
 
     def diag_gemm_bf16(self, device, m, n, k, warmup, iters, samples, tflops, err, ms):
         return self._gemm("gemm", device, m, tflops, err, ms)
+
+    def _checksums(self, test, device, inject, ck_err, out):
+        """Tile checksums: ``gemm_bad_tiles[(device, test)] = {xcd: tiles}``; an injected element = one bad
+        tile on XCD 0, as on the GPU (workgroup 0 computes tile (0, 0) on XCD 0)."""
+        bad = dict(self.gemm_bad_tiles.get((device, test), {}))
+        if inject >= 0:
+            bad[0] = bad.get(0, 0) + 1
+        vals = [0] * 12
+        vals[0] = sum(bad.values())
+        vals[1] = 256 * vals[0]
+        for x, t in bad.items():
+            vals[2 + x] = t
+        vals[10], vals[11] = (0, 0) if vals[0] else (-1, -1)
+        for i, v in enumerate(vals):
+            out[i] = v
+        _put(ck_err, ctypes.c_double, 0.4 if vals[0] else 3e-8)
+
+    def diag_gemm_bf16_x(self, device, m, n, k, warmup, iters, samples, inject, tol, tflops, err, ms, ck_err, out):
+        rc = self._gemm("gemm", device, m, tflops, err, ms)
+        if rc == 0 and tol >= 0:
+            self._checksums("gemm", device, inject, ck_err, out)
+        return rc
+
+    def diag_gemm_fp8_x(self, device, m, n, k, warmup, iters, samples, inject, tol, tflops, err, ms, ck_err, out):
+        rc = self._gemm("gemm_fp8", device, m, tflops, err, ms)
+        if rc == 0 and tol >= 0:
+            self._checksums("gemm_fp8", device, inject, ck_err, out)
+        return rc
 
     def diag_gemm_fp8(self, device, m, n, k, warmup, iters, samples, tflops, err, ms):
         return self._gemm("gemm_fp8", device, m, tflops, err, ms)

@@ -160,7 +160,8 @@ def _rich_report():
     g.update(xgmi_error=0, xgmi_kb=[[1, 2]] * 1, cper={"fatal": 0, "uncorrected": 0, "corrected": 1},
              ecc_blocks={"umc": {"ce": 1, "ue": 0, "de": 0}}, gfx_activity=0,
              throttle={"s": 60, "thermal_pct": 0.0, "power_pct": 1.0, "prochot_pct": 0.0},
-             diag={"gemm": {"pass": True, "tflops": 1200.0, "fraction": 0.98}, "gemm_fp8": {"pass": True, "tflops": 2300.0},
+             diag={"gemm": {"pass": True, "tflops": 1200.0, "fraction": 0.98, "checksum_bad_tiles": 0},
+                   "gemm_fp8": {"pass": True, "tflops": 2300.0, "checksum_bad_tiles": 0},
                    "mfma": {"pass": True, "kinds": {"bf16": {"tflops": 1900.0, "errors": 0}}},
                    "hbm": {"pass": True, "copy_tbs": 6.4, "read_tbs": 7.0},
                    "hbm_xcd": {"pass": True, "read_tbs": 6.1, "errors": 0, "alone_tbs": {"0": 1.3}},

@@ -115,6 +115,24 @@ def test_numerics_failure_is_not_remeasured(fake):
     assert lib.calls.count("gemm") == 1
 
 
+def test_gemm_tiles_failing_their_checksums_fail_the_gpu_and_name_the_xcd(fake):
+    """Every GEMM output is covered by tile checksums: tiles that fail them fail the test (not measured again:
+    a wrong result does not get better), the detail names the XCDs, and the agent's verdict is unhealthy."""
+    lib = fake(gemm_bad_tiles={(0, "gemm_fp8"): {5: 2}})
+    out = diag.run(1, 0)
+    assert out["gemm"]["pass"] and out["gemm"]["checksum_bad_tiles"] == 0 and out["gemm"]["checksum_err"] < 1e-7
+    r = out["gemm_fp8"]
+    assert not r["pass"] and r["checksum_bad_tiles"] == 2 and r["checksum_bad_xcds"] == {"5": 2}, r
+    assert r["detail"].startswith("2 output tile(s) fail their checksums (XCD 5: 2; first at tile row 0"), r
+    assert lib.calls.count("gemm_fp8") == 1
+    v = _verdict(out)
+    assert v.state == "unhealthy" and any("diag gemm_fp8 failed" in x for x in v.reasons), v.reasons
+    # the test hook: one injected output is one bad tile
+    fake()
+    r = diag.gemm(0, inject_elem=12345)
+    assert not r["pass"] and r["checksum_bad_tiles"] == 1 and r["checksum_first_bad_tile"] == [0, 0]
+
+
 def test_cpx_partition_at_one_eighth_is_healthy(fake):
     # CPX: 32 CUs, NPS1 (all of HBM addressable, an eighth of the bandwidth share); every rate 1/8
     lib = fake(rate=1 / 8, cus=32, link=(57.2 / 8, 56.8 / 8),

@@ -284,6 +284,43 @@ def test_memtest_counts_and_locates_an_injected_word(dev):
         diag.memtest(0, gib=1.0, inject_word=1 << 40)
 
 
+def _tile_xcd(tm, tn, tiles_m, tiles_n, group_m=4):
+    """The XCD whose workgroup computes tile (tm, tn): blockIdx b runs on XCD b % 8 (the kernels' regrouping,
+    written out independently of diag.hip's tile_xcds)."""
+    nwg = tiles_m * tiles_n
+    q, r = divmod(nwg, 8)
+    for b in range(nwg):
+        x = b % 8
+        bid = (x * (q + 1) if x < r else r * (q + 1) + (x - r) * q) + b // 8
+        first = bid // (group_m * tiles_n) * group_m
+        gsize = min(tiles_m - first, group_m)
+        if (first + (bid % (group_m * tiles_n)) % gsize, (bid % (group_m * tiles_n)) // gsize) == (tm, tn):
+            return x
+    raise AssertionError("tile not computed by any workgroup")
+
+
+@pytest.mark.parametrize("kind,n,tile,group_m", [("gemm", 4096, 256, 4), ("gemm", 2048, 128, 8),
+                                                  ("gemm_fp8", 4096, 256, 4), ("gemm_fp8", 2048, 256, 4)])
+def test_gemm_checksums_catch_and_locate_one_corrupted_output(dev, kind, n, tile, group_m):
+    """The GEMM tests check every output through tile column checksums, not only the 4,096 sampled ones: a
+    healthy run is clean, and one output overwritten after the timing is found in exactly one tile -- its own
+    -- and attributed to the XCD that computed it (bf16 2048^2 runs the 128^2-tile kernel, the others 256^2)."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    fn = getattr(diag, kind)
+    tol = diag.GEMM_CK_TOL if kind == "gemm" else diag.GEMM_FP8_CK_TOL
+    ok = fn(0, size=n, warmup=1, iters=2)  # (small sizes fall short of the 8192^3 rate: only numerics matter)
+    assert ok["checksum_bad_tiles"] == 0 and ok["checksum_err"] < tol / 10 and "checksum" not in ok["detail"], ok
+    row, col = n // 2 + 297, n // 3 + 501
+    r = fn(0, size=n, warmup=1, iters=2, inject_elem=row * n + col)
+    assert not r["pass"] and r["checksum_bad_tiles"] == 1, r
+    assert r["checksum_first_bad_tile"] == [row // tile, col // tile], r
+    xcd = _tile_xcd(row // tile, col // tile, n // tile, n // tile, group_m)
+    assert r["checksum_bad_xcds"] == {str(xcd): 1}, r
+    assert "fail their checksums" in r["detail"], r
+    with pytest.raises(RuntimeError, match="outside the output"):
+        fn(0, size=n, warmup=0, iters=1, inject_elem=n * n)
+
+
 def test_diag_failed_allocation_leaks_nothing(dev):
     """A diagnostic that runs out of device memory half-way (the agent's GPU got busy) frees what it
     already took and leaves no error behind for the next call: the agent calls these for the life

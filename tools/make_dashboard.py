@@ -38,8 +38,10 @@ ROWS = [
          "percentunit", [("mi355x_gpu_diag_fraction", "{{node}} gpu{{gpu}} {{test}}")], 24, 7),
         ("Diagnostics skipped (GPU busy or allocated)", "timeseries", "none",
          [("mi355x_gpu_diag_skipped", "{{node}} gpu{{gpu}}")], 12, 6),
-        ("Wrong results found by the diagnostics", "timeseries", "none",
-         [("mi355x_gpu_diag_errors", "{{node}} gpu{{gpu}} {{test}}")], 12, 6),
+        ("Wrong results found by the diagnostics (words, lanes; GEMM output tiles failing their checksums)",
+         "timeseries", "none",
+         [("mi355x_gpu_diag_errors", "{{node}} gpu{{gpu}} {{test}}"),
+          ("mi355x_gpu_diag_checksum_bad_tiles", "{{node}} gpu{{gpu}} {{test}} tiles")], 12, 6),
     ]),
     ("Memory RAS", [
         ("Uncorrectable ECC", "timeseries", "none", [("mi355x_gpu_ecc_uncorrectable", "{{node}} gpu{{gpu}}")], 8, 6),
