@@ -993,7 +993,8 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
             for test, r in tests.items():
                 if not isinstance(r, dict):
                     continue
-                for key in ("tflops", "copy_tbs", "read_tbs", "write_tbs", "h2d_gbps", "d2h_gbps", "fraction"):
+                for key in ("tflops", "copy_tbs", "read_tbs", "write_tbs", "h2d_gbps", "d2h_gbps", "fraction",
+                            "max_rel_err", "max_err_over_mag", "checksum_err"):  # rates, and numerics margins
                     if isinstance(r.get(key), (int, float)) and not isinstance(r.get(key), bool):
                         series[d].setdefault(f"{test}.{key}", []).append(float(r[key]))
                 for kind, row in ((r.get("kinds") or {}) if isinstance(r.get("kinds"), dict) else {}).items():
@@ -1008,7 +1009,9 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
             progress(f"burn-in round {rounds} at {clock() - t0:.0f} s: " + ("FAIL " + " ".join(bad) if bad else "pass"))
         if clock() - t0 >= 60.0 * minutes:
             break
-    summary = {d: {k: {"min": round(min(v), 3), "median": round(statistics.median(v), 3), "max": round(max(v), 3)}
+    def r3(x: float) -> float:  # 3 decimals for rates, 3 significant digits for the tiny error figures
+        return round(x, 3) if abs(x) >= 1e-3 or x == 0 else float(f"{x:.3g}")
+    summary = {d: {k: {"min": r3(min(v)), "median": r3(statistics.median(v)), "max": r3(max(v))}
                    for k, v in m.items()} for d, m in series.items()}
     return {"minutes": minutes, "rounds": rounds, "failed_rounds": failed_rounds, "wall_s": round(clock() - t0, 1),
             "pass": failed_rounds == 0, "failures": failures, "devices": summary}
