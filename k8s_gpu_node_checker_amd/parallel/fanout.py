@@ -2,9 +2,12 @@
 
 When node agents serve their report over HTTP instead of (or besides) the
 annotation, the checker fetches every GPU node's ``/probe`` concurrently:
-``asyncio`` streams (no aiohttp: 310 ms import), an ``asyncio.Semaphore``
-bounding in-flight requests, a per-node timeout and one retry on connection
-errors.  Wall clock is ~max(node latency) instead of the sum, so it stays flat
+one ``asyncio`` protocol per connection that parses the response as it
+arrives (no aiohttp: 310 ms import; 3 % / 11 % less checker CPU than
+``asyncio`` streams at 1,000 nodes, min / median of 12 interleaved runs:
+no per-read coroutine resumptions, no ``wait_for`` task per request), an
+``asyncio.Semaphore`` bounding
+in-flight requests, a per-node timeout and one retry on connection errors.  Wall clock is ~max(node latency) instead of the sum, so it stays flat
 as the cluster grows.
 
 URL template placeholders: ``{name}`` (node name) and ``{ip}`` (the node's
@@ -41,39 +44,6 @@ def _error_report(node: str, msg: str) -> Dict[str, Any]:
     return {"schema": SCHEMA, "node": node, "ts": time.time(), "error": msg, "gpus": []}
 
 
-async def _read_capped(reader: asyncio.StreamReader, n: Optional[int], cap: int) -> bytes:
-    """``n`` bytes (Content-Length) or everything to EOF (``n`` None), refusing more than ``cap``."""
-    if n is not None:
-        if n > cap:
-            raise BodyTooLarge(f"body of {n} bytes exceeds {cap}")
-        return await reader.readexactly(n)
-    buf = bytearray()
-    while True:
-        chunk = await reader.read(65536)
-        if not chunk:
-            return bytes(buf)
-        buf += chunk
-        if len(buf) > cap:
-            raise BodyTooLarge(f"body exceeds {cap} bytes")
-
-
-async def _read_chunked(reader: asyncio.StreamReader, cap: int) -> bytes:
-    """A ``Transfer-Encoding: chunked`` body (RFC 9112 section 7.1), at most ``cap`` bytes of payload."""
-    buf = bytearray()
-    while True:
-        line = await reader.readuntil(b"\r\n")
-        size = int(line.split(b";", 1)[0].strip() or b"x", 16)
-        if size == 0:
-            while (await reader.readuntil(b"\r\n")) != b"\r\n":  # trailer fields
-                pass
-            return bytes(buf)
-        if len(buf) + size > cap:
-            raise BodyTooLarge(f"body exceeds {cap} bytes")
-        buf += await reader.readexactly(size)
-        if await reader.readexactly(2) != b"\r\n":
-            raise ValueError("malformed chunk")
-
-
 _SSL_CACHE: Dict[Any, Any] = {}
 
 
@@ -92,6 +62,109 @@ def _ssl_context(ca_file: Optional[str], client_cert: Optional[str] = None, clie
     return ctx
 
 
+class _GetProtocol(asyncio.Protocol):
+    """One ``GET`` over one connection, parsed as the bytes arrive (no StreamReader, no per-read coroutine
+    resumptions): the response body, or the error, lands in ``done``."""
+
+    def __init__(self, request: bytes, cap: int, done: "asyncio.Future[bytes]"):
+        self.request, self.cap, self.done = request, cap, done
+        self.buf = bytearray()
+        self.pos = 0                      # parse offset into buf (after the head: the body / chunk cursor)
+        self.status = 0
+        self.length: Optional[int] = None  # Content-Length
+        self.chunked = False
+        self.headed = False
+        self.body = bytearray()           # decoded chunked payload
+        self.transport: Any = None
+
+    def connection_made(self, transport: Any) -> None:
+        self.transport = transport
+        transport.write(self.request)
+
+    def _finish(self, body: Optional[bytes] = None, exc: Optional[BaseException] = None) -> None:
+        if not self.done.done():
+            if exc is not None:
+                self.done.set_exception(exc)
+            else:
+                self.done.set_result(body if body is not None else b"")
+        if self.transport is not None:
+            self.transport.close()
+
+    def _head(self) -> bool:
+        end = self.buf.find(b"\r\n\r\n")
+        if end < 0:
+            if len(self.buf) > 65536:
+                raise ValueError("response head exceeds 64 KiB")
+            return False
+        lines = bytes(self.buf[:end]).decode("latin-1").split("\r\n")
+        self.status = int(lines[0].split()[1])
+        for line in lines[1:]:
+            k, _, v = line.partition(":")
+            k = k.strip().lower()
+            if k == "transfer-encoding" and "chunked" in v.lower():
+                self.chunked = True
+            elif k == "content-length":
+                self.length = int(v.strip())
+        if not self.chunked and self.length is not None and self.length > self.cap:
+            raise BodyTooLarge(f"body of {self.length} bytes exceeds {self.cap}")
+        self.pos = end + 4
+        self.headed = True
+        return True
+
+    def _chunks(self) -> Optional[bytes]:
+        """Decode whole chunks from ``pos``; the payload once the last chunk and its trailer are in."""
+        buf = self.buf
+        while True:
+            eol = buf.find(b"\r\n", self.pos)
+            if eol < 0:
+                return None
+            line = bytes(buf[self.pos:eol])
+            size = int(line.split(b";", 1)[0].strip() or b"x", 16)
+            if size == 0:
+                end = buf.find(b"\r\n\r\n", eol) if buf[eol + 2:eol + 4] != b"\r\n" else eol
+                if end < 0:
+                    return None  # trailer fields still arriving
+                return bytes(self.body)
+            if len(self.body) + size > self.cap:
+                raise BodyTooLarge(f"body exceeds {self.cap} bytes")
+            if len(buf) < eol + 2 + size + 2:
+                return None
+            if buf[eol + 2 + size:eol + 4 + size] != b"\r\n":
+                raise ValueError("malformed chunk")
+            self.body += buf[eol + 2:eol + 2 + size]
+            self.pos = eol + 4 + size
+
+    def data_received(self, data: bytes) -> None:
+        if self.done.done():
+            return
+        self.buf += data
+        try:
+            if not self.headed and not self._head():
+                return
+            if self.chunked:
+                body = self._chunks()
+                if body is not None:
+                    self._finish(body)
+            elif self.length is not None:
+                if len(self.buf) - self.pos >= self.length:
+                    self._finish(bytes(self.buf[self.pos:self.pos + self.length]))
+            elif len(self.buf) - self.pos > self.cap:
+                raise BodyTooLarge(f"body exceeds {self.cap} bytes")
+        except Exception as e:  # malformed or oversized: the node's fetch fails, nothing propagates
+            self._finish(exc=e)
+
+    def eof_received(self) -> Optional[bool]:
+        if self.headed and not self.chunked and self.length is None:
+            self._finish(bytes(self.buf[self.pos:]))  # read-to-close body
+        else:
+            self._finish(exc=asyncio.IncompleteReadError(bytes(self.buf), None))
+        return None
+
+    def connection_lost(self, exc: Optional[BaseException]) -> None:
+        if not self.done.done():
+            self.done.set_exception(exc or asyncio.IncompleteReadError(bytes(self.buf), None))
+
+
 async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None, max_body: int = MAX_BODY,
                          client_cert: Optional[str] = None, client_key: Optional[str] = None) -> Any:
     parts = urlsplit(url)
@@ -99,33 +172,34 @@ async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None
     port = parts.port or (443 if parts.scheme == "https" else 80)
     ssl_ctx = _ssl_context(ca_file, client_cert, client_key) if parts.scheme == "https" else None
     path = (parts.path or "/") + (("?" + parts.query) if parts.query else "")
+    loop = asyncio.get_running_loop()
+    done: "asyncio.Future[bytes]" = loop.create_future()
+    req = (f"GET {path} HTTP/1.1\r\nHost: {host}:{port}\r\nAccept: application/json\r\n"
+           f"Connection: close\r\n\r\n").encode()
+    proto = _GetProtocol(req, max_body, done)
+    # the deadline cancels this task (what asyncio.timeout does from 3.11): no wrapper task per request
+    task = asyncio.current_task()
+    expired: List[bool] = []
 
-    async def run() -> Any:
-        reader, writer = await asyncio.open_connection(host, port, ssl=ssl_ctx)
-        try:
-            writer.write(f"GET {path} HTTP/1.1\r\nHost: {host}:{port}\r\nAccept: application/json\r\n"
-                         f"Connection: close\r\n\r\n".encode())
-            await writer.drain()
-            head = await reader.readuntil(b"\r\n\r\n")
-            lines = head.decode("latin-1").split("\r\n")
-            status = int(lines[0].split()[1])
-            headers = {}
-            for line in lines[1:]:
-                k, _, v = line.partition(":")
-                headers[k.strip().lower()] = v.strip()
-            if "chunked" in headers.get("transfer-encoding", "").lower():
-                body = await _read_chunked(reader, max_body)
-            elif "content-length" in headers:
-                body = await _read_capped(reader, int(headers["content-length"]), max_body)
-            else:
-                body = await _read_capped(reader, None, max_body)
-            if status != 200:
-                raise RuntimeError(f"HTTP {status}")
-            return json.loads(body)
-        finally:
-            writer.close()
-
-    return await asyncio.wait_for(run(), timeout)
+    def expire() -> None:
+        expired.append(True)
+        if task is not None:
+            task.cancel()
+    timer = loop.call_later(timeout, expire)
+    try:
+        await loop.create_connection(lambda: proto, host, port, ssl=ssl_ctx)
+        body = await done
+    except asyncio.CancelledError:
+        if expired:
+            raise asyncio.TimeoutError() from None
+        raise
+    finally:
+        timer.cancel()
+        if proto.transport is not None:
+            proto.transport.close()
+    if proto.status != 200:
+        raise RuntimeError(f"HTTP {proto.status}")
+    return json.loads(body)
 
 
 async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, timeout: float = 2.0,

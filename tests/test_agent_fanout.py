@@ -531,6 +531,60 @@ def test_chunked_body_is_decoded():
         ls.close()
 
 
+@pytest.mark.parametrize("split", [1, 2, 3, 7, 64, 10**6])
+def test_response_parser_is_independent_of_how_the_bytes_arrive(split):
+    """The fan-out parses each response as its bytes arrive: every framing (Content-Length, chunked with
+    extensions and trailers, read-to-close) gives the same body whatever the packet boundaries, and the cap
+    and malformed chunks fail the fetch at any split."""
+    import asyncio
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    doc = json.dumps({"schema": "mi355x-health/v1", "node": "x", "gpus": [{"bdf": "0000:05:00.0"}] * 5}).encode()
+    parts = [doc[:11], doc[11:12], doc[12:]]
+    chunked = b"".join(b"%x;ext=1\r\n%s\r\n" % (len(p), p) for p in parts)
+
+    class T:
+        closed = False
+
+        def write(self, data):
+            pass
+
+        def close(self):
+            self.closed = True
+
+    def feed(raw, cap=fanout.MAX_BODY, eof=False):
+        loop = asyncio.new_event_loop()
+        try:
+            done = loop.create_future()
+            p = fanout._GetProtocol(b"GET / HTTP/1.1\r\n\r\n", cap, done)
+            t = T()
+            p.connection_made(t)
+            for i in range(0, len(raw), split):
+                p.data_received(raw[i:i + split])
+            if eof:
+                p.eof_received()
+            if not done.done():
+                return None
+            return (p.status, done.result()) if done.exception() is None else done.exception()
+        finally:
+            loop.close()
+
+    head = b"HTTP/1.1 200 OK\r\n"
+    assert feed(head + b"Content-Length: %d\r\n\r\n" % len(doc) + doc) == (200, doc)
+    assert feed(head + b"Transfer-Encoding: chunked\r\n\r\n" + chunked + b"0\r\n\r\n") == (200, doc)
+    assert feed(head + b"Transfer-Encoding: chunked\r\n\r\n" + chunked + b"0\r\nX-T: 1\r\nX-U: 2\r\n\r\n") == (200, doc)
+    assert feed(head + b"Transfer-Encoding: chunked\r\n\r\n" + chunked + b"0\r\nX-T: 1\r\n") is None  # trailer pending
+    assert feed(head + b"Content-Type: application/json\r\n\r\n" + doc, eof=True) == (200, doc)
+    assert feed(b"HTTP/1.1 503 Service Unavailable\r\nContent-Length: 2\r\n\r\n{}") == (503, b"{}")
+    assert isinstance(feed(head + b"Content-Length: %d\r\n\r\n" % len(doc) + doc[:-1], eof=True),
+                      asyncio.IncompleteReadError)
+    for raw, eof in ((head + b"Content-Length: %d\r\n\r\n" % len(doc) + doc, False),
+                     (head + b"Transfer-Encoding: chunked\r\n\r\n" + chunked, False),
+                     (head + b"\r\n" + doc, False)):
+        assert isinstance(feed(raw, cap=len(doc) - 1, eof=eof), fanout.BodyTooLarge)
+    bad = feed(head + b"Transfer-Encoding: chunked\r\n\r\n" + b"3\r\nabcXY0\r\n\r\n")
+    assert isinstance(bad, ValueError) and "malformed chunk" in str(bad)
+
+
 def test_fetch_probe_reports_inside_a_running_event_loop(fixture_report):
     """An async caller (a notebook, an embedding service) can use the blocking entry point."""
     import asyncio
