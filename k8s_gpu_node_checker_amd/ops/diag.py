@@ -976,7 +976,8 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
     """Acceptance burn-in: the per-device suite of ``level`` on every device, round after round, for
     ``minutes``.  Passes only if every round of every device passed; reports each rate per device as
     min / median / max over the rounds (a GPU that drifts or throttles under sustained load shows as a wide
-    spread or a late failure) and the first failing rounds."""
+    spread or a late failure), how many rounds each test passed only as degraded, and the first failing
+    rounds."""
     import statistics
     import time as _time
     clock = clock or _time.monotonic
@@ -985,6 +986,7 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
     series: Dict[int, Dict[str, List[float]]] = {d: {} for d in devices}
     failures: List[Dict[str, Any]] = []
     failed_rounds = 0
+    degraded: Dict[int, Dict[str, int]] = {d: {} for d in devices}  # rounds a test passed only as degraded
     while True:
         res = run_devices(level, devices, parallel)
         rounds += 1
@@ -999,6 +1001,8 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
                         series[d].setdefault(f"{test}.{key}", []).append(float(r[key]))
                 for kind, row in ((r.get("kinds") or {}) if isinstance(r.get("kinds"), dict) else {}).items():
                     series[d].setdefault(f"{test}.{kind}.tflops", []).append(float(row.get("tflops", 0)))
+                if r.get("pass") and r.get("degraded"):
+                    degraded[d][test] = degraded[d].get(test, 0) + 1
                 if r.get("pass") is False:
                     bad.append(f"gpu{d}:{test}")
                     if len(failures) < 20:
@@ -1014,7 +1018,8 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
     summary = {d: {k: {"min": r3(min(v)), "median": r3(statistics.median(v)), "max": r3(max(v))}
                    for k, v in m.items()} for d, m in series.items()}
     return {"minutes": minutes, "rounds": rounds, "failed_rounds": failed_rounds, "wall_s": round(clock() - t0, 1),
-            "pass": failed_rounds == 0, "failures": failures, "devices": summary}
+            "pass": failed_rounds == 0, "failures": failures, "devices": summary,
+            "degraded_rounds": {d: v for d, v in degraded.items() if v}}
 
 
 def main(argv=None) -> int:
@@ -1057,6 +1062,9 @@ def main(argv=None) -> int:
                         continue
                     v = m[k]
                     lines.append(f"  GPU {d} {k:<28} min {v['min']:<10g} median {v['median']:<10g} max {v['max']:g}")
+            for d, tests in b["degraded_rounds"].items():
+                lines.append(f"  GPU {d} degraded (below {DEGRADED_FRACTION:.0%} of the reference after re-measuring) in "
+                             + ", ".join(f"{t} {n}/{b['rounds']} rounds" for t, n in sorted(tests.items())))
             lines += [f"  FAIL round {f['round']} GPU {f['device']} {f['test']}: {f['detail']}" for f in b["failures"]]
             for test, r in (b.get("fabric") or {}).items():
                 lines.append(f"fabric {test:<5} {'pass' if r.get('pass') else 'FAIL':<9} {_summary(test, r)}"

@@ -381,6 +381,13 @@ def test_burn_in_reports_spread_and_every_failing_round(fake, capsys):
     assert lines and all(ln.startswith("burn-in round ") and "FAIL gpu1:" in ln for ln in lines)
     assert diag.main(["--level", "1", "--duration", "0.0005"]) == 1
     assert json.loads(capsys.readouterr().out)["failures"]
+    # a GPU at 90 %: every round passes, as degraded, and the count says so
+    fake(n=2, gpu_rate={1: 0.9})
+    b = diag.burn_in(1, [0, 1], minutes=0.0005)
+    assert b["pass"] and list(b["degraded_rounds"]) == [1], b
+    assert b["degraded_rounds"][1]["gemm"] == b["degraded_rounds"][1]["gemm_fp8"] == b["rounds"], b
+    assert diag.main(["--level", "1", "--duration", "0.0005", "--format", "text", "--device", "1"]) == 0
+    assert f"GPU 1 degraded (below 95% of the reference after re-measuring) in " in capsys.readouterr().out
     fake(n=1)
     assert diag.main(["--level", "1", "--duration", "0.0005", "--format", "text"]) == 0
     text = capsys.readouterr().out
