@@ -64,6 +64,7 @@ thread_local int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-stag
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native 16-byte vector (SROA-friendly, unlike uint4)
 typedef int i32x8 __attribute__((ext_vector_type(8)));            // 32 fp8 / 64 fp4 operand bytes
 
@@ -504,10 +505,17 @@ __device__ unsigned long long g_gemm_stamps[8][2][4][4];
 // unit scales) passed as K = row bytes / 2 "bf16 columns", so the byte-identical LDS-DMA staging is
 // shared (a 64-column bf16 K-tile is a 128-byte fp8 or fp4 K-tile); only the swizzle (fp8), the
 // fragment reads and the MFMA differ.
-template <int DT, bool EPI_LDS = false, bool BUF = false, int SCHED = 1, bool PRIO_G1 = DT == DT_BF16>
+// OUT_F32: C is fp32 [M][N].  OUT_BF16_CK (with EPI_LDS): C is bf16 [M][N] -- the output hipBLASLt writes, half
+// the bytes -- and csum[M / 128][N] receives every column's sum over each wave row's 128 rows, formed in fp64
+// from the fp32 accumulators before the rounding, so the whole-output check (gemm_checksum) needs no second
+// pass over C and keeps the accumulators' precision.
+enum GemmOut { OUT_F32 = 0, OUT_BF16_CK = 1 };
+template <int DT, bool EPI_LDS = false, bool BUF = false, int SCHED = 1, int OUT = OUT_F32,
+          bool PRIO_G1 = DT == DT_BF16>
 __global__ void __launch_bounds__(V2_THREADS, 1)
-gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
-               int K) {
+gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv,
+               double* __restrict__ csum, int M, int N, int K) {
+  static_assert(OUT == OUT_F32 || EPI_LDS, "the bf16 output goes through the LDS-staged epilogue");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
@@ -635,7 +643,48 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
   }
   if (wr == 0) STG_BARRIER();  // balance the stagger
   const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 64;
-  if constexpr (EPI_LDS) {
+  float* __restrict__ C = static_cast<float*>(Cv);
+  if constexpr (OUT == OUT_BF16_CK) {
+    // column sums over this wave's 128 rows: 32 per lane (rows m * 16 + fq * 4 + j), then over the 4 lanes
+    // (fq) that hold the same column
+    double s[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      s[n] = 0.0;
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[n] += static_cast<double>(acc[m][n][j]);
+      s[n] += __shfl_xor(s[n], 16);
+      s[n] += __shfl_xor(s[n], 32);
+    }
+    if (fq == 0) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) csum[static_cast<size_t>(row0 / 128) * N + col0 + n * 16 + frow] = s[n];
+    }
+    // C through the wave's LDS patch as in the fp32 epilogue, leaving as 8 bf16 (16 bytes) per lane: one
+    // store instruction covers 8 rows x 128 contiguous bytes
+    constexpr int LD = 64 + 4;
+    __builtin_amdgcn_s_barrier();
+    float* patch = reinterpret_cast<float*>(smem) + wid * (16 * LD);
+    __bf16* __restrict__ Cb = static_cast<__bf16*>(Cv);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) patch[(fq * 4 + j) * LD + n * 16 + frow] = acc[m][n][j];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int r = q * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+        const floatx4 lo = *reinterpret_cast<const floatx4*>(patch + r * LD + c8);
+        const floatx4 hi = *reinterpret_cast<const floatx4*>(patch + r * LD + c8 + 4);
+        const floatx8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        *reinterpret_cast<bf16x8*>(Cb + static_cast<size_t>(row0 + m * 16 + r) * N + col0 + c8) =
+            __builtin_convertvector(v, bf16x8);
+      }
+    }
+  } else if constexpr (EPI_LDS) {
     // Each 16x64 fp32 slice goes through the wave's own LDS patch (no DMA is in flight and every
     // fragment read retired before the last barrier), then leaves as 16-byte row pieces: one store
     // instruction covers 4 rows x 256 contiguous bytes instead of 4 rows x 64.
@@ -681,9 +730,10 @@ __global__ void gemm_ref_kernel(const __bf16* A, const __bf16* Bt, const int* ro
   out[i] = s;
 }
 
-__global__ void gather_kernel(const float* C, const int* rows, const int* cols, float* out, int nsamp, int N) {
+template <typename T>
+__global__ void gather_kernel(const T* C, const int* rows, const int* cols, float* out, int nsamp, int N) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nsamp) out[i] = C[static_cast<size_t>(rows[i]) * N + cols[i]];
+  if (i < nsamp) out[i] = static_cast<float>(C[static_cast<size_t>(rows[i]) * N + cols[i]]);
 }
 
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {
@@ -1207,17 +1257,35 @@ hipError_t enable_peer(int from, int to) {
   return e;
 }
 
-template <int DT, bool EPI, bool BUF, int SCHED = 1>
-int launch_v3_inst(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
+template <int DT, bool EPI, bool BUF, int SCHED = 1, int OUT = OUT_F32>
+int launch_v3_inst(const void* A, const void* Bt, void* C, double* csum, int M, int N, int Kcols,
+                   hipStream_t stream) {
   static LdsAttrOnce attr;
-  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI, BUF, SCHED>),
+  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI, BUF, SCHED, OUT>),
                          2 * V2_STAGE_BYTES, "gemm v3") != 0)
     return -1;
   const int nwg = (M / V2_BM) * (N / V2_BN);
-  hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI, BUF, SCHED>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, stream,
-                     static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, M, N, Kcols);
+  hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI, BUF, SCHED, OUT>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
+                     stream, static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, csum, M, N, Kcols);
   return 0;
 }
+template <int DT, bool EPI, bool BUF, int SCHED = 1>
+int launch_v3_inst(const void* A, const void* Bt, float* C, int M, int N, int Kcols, hipStream_t stream) {
+  return launch_v3_inst<DT, EPI, BUF, SCHED, OUT_F32>(A, Bt, C, nullptr, M, N, Kcols, stream);
+}
+
+// bf16 C + fused 128-row column sums (OUT_BF16_CK), restaging order per g_gemm_schedule
+template <int DT>
+int launch_v3_ck(const void* A, const void* Bt, __bf16* C, double* csum, int M, int N, int Kcols,
+                 hipStream_t stream) {
+  return g_gemm_schedule == 0
+             ? launch_v3_inst<DT, true, false, 0, OUT_BF16_CK>(A, Bt, C, csum, M, N, Kcols, stream)
+             : launch_v3_inst<DT, true, false, 1, OUT_BF16_CK>(A, Bt, C, csum, M, N, Kcols, stream);
+}
+
+// The diagnostic runs (diag_gemm_*_x) take the bf16-output kernel wherever the production v3 configuration
+// would run (LDS-staged epilogue, global_load_lds staging); other knob settings keep fp32 C.
+bool v3_ck_path() { return g_gemm_epilogue == 1 && !g_gemm_buffer_loads; }
 
 // v3 launch (M, N multiples of 256; Kcols = bf16 columns, K8 / 2 for fp8), epilogue per g_gemm_epilogue,
 // operand staging per g_gemm_buffer_loads, restaging order per g_gemm_schedule (the buffer path: order 1)
@@ -1267,30 +1335,46 @@ std::vector<int> tile_xcds(int tiles_m, int tiles_n, int group_m) {
 // per XCD, [10] / [11] the first bad tile's (row, column) in tiles or -1; *max_err the worst |csum - ref| / mag.
 // A NaN or infinite sum counts as bad.
 constexpr int kCkOut = 12;
+// With `fused` (the OUT_BF16_CK kernel's csum[M / 128][N], device memory) the column sums come from the
+// kernel itself, its 128-row halves added per tile row in fp64, and C is not read.
 template <int DT>
 int gemm_checksum(int device, const void* A, const void* Bt, const float* C, int M, int N, int K, TileGeom g,
-                  double tol, double* max_err, long long* ck_out) {
-  const int nblk = M / g.rows, tiles_n = N / g.cols;
+                  double tol, double* max_err, long long* ck_out, const double* fused = nullptr) {
+  const int rb = g.rows;
+  const int nblk = M / rb, tiles_n = N / g.cols;
   const size_t kb = sizeof(double) * static_cast<size_t>(nblk) * K, nb = sizeof(double) * static_cast<size_t>(nblk) * N;
   DevBuf asum, aabs, ref, mag, csum;
   DIAG_CHECK(asum.alloc(device, kb));
   DIAG_CHECK(aabs.alloc(device, kb));
   DIAG_CHECK(ref.alloc(device, nb));
   DIAG_CHECK(mag.alloc(device, nb));
-  DIAG_CHECK(csum.alloc(device, nb));
+  if (!fused) DIAG_CHECK(csum.alloc(device, nb));
   double* as = static_cast<double*>(asum.ptr);
   double* am = static_cast<double*>(aabs.ptr);
-  hipLaunchKernelGGL(ck_asum_kernel<DT>, dim3((K + 255) / 256, nblk), dim3(256), 0, nullptr, A, as, am, K, g.rows);
+  hipLaunchKernelGGL(ck_asum_kernel<DT>, dim3((K + 255) / 256, nblk), dim3(256), 0, nullptr, A, as, am, K, rb);
   hipLaunchKernelGGL(ck_ref_kernel<DT>, dim3((N + 255) / 256, (nblk + CK_TB - 1) / CK_TB), dim3(256), 0, nullptr, Bt,
                      as, am, static_cast<double*>(ref.ptr), static_cast<double*>(mag.ptr), N, K, nblk);
-  hipLaunchKernelGGL(ck_csum_kernel, dim3((N + 255) / 256, nblk), dim3(256), 0, nullptr, C,
-                     static_cast<double*>(csum.ptr), N, g.rows);
+  if (!fused)
+    hipLaunchKernelGGL(ck_csum_kernel, dim3((N + 255) / 256, nblk), dim3(256), 0, nullptr, C,
+                       static_cast<double*>(csum.ptr), N, rb);
   DIAG_CHECK(hipGetLastError());
   const size_t cnt = static_cast<size_t>(nblk) * N;
   std::vector<double> hr(cnt), hm(cnt), hc(cnt);
   DIAG_CHECK(hipMemcpy(hr.data(), ref.ptr, nb, hipMemcpyDeviceToHost));
   DIAG_CHECK(hipMemcpy(hm.data(), mag.ptr, nb, hipMemcpyDeviceToHost));
-  DIAG_CHECK(hipMemcpy(hc.data(), csum.ptr, nb, hipMemcpyDeviceToHost));
+  if (fused) {
+    const int halves = rb / 128;
+    std::vector<double> h128(cnt * halves);
+    DIAG_CHECK(hipMemcpy(h128.data(), fused, nb * halves, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < cnt; ++i) {
+      const size_t tb = i / N, j = i % N;
+      double v = 0.0;
+      for (int h = 0; h < halves; ++h) v += h128[(tb * halves + h) * N + j];
+      hc[i] = v;
+    }
+  } else {
+    DIAG_CHECK(hipMemcpy(hc.data(), csum.ptr, nb, hipMemcpyDeviceToHost));
+  }
   const std::vector<int> xcd = tile_xcds(nblk, tiles_n, g.group_m);
   std::vector<char> bad(static_cast<size_t>(nblk) * tiles_n, 0);
   double worst = 0.0;
@@ -1325,6 +1409,28 @@ hipError_t inject_output(float* C, long long elem, long long count) {
   if (elem < 0 || elem >= count) return hipSuccess;
   const float v = 1e6f;
   return hipMemcpy(C + elem, &v, sizeof(v), hipMemcpyHostToDevice);
+}
+
+// The same for the bf16-output kernel: the element becomes 1e6 in C and in its 128-row block's fused column
+// sum, as if the matrix core had produced that value.
+hipError_t inject_output_ck(__bf16* C, double* csum, long long elem, int M, int N) {
+  if (elem < 0 || elem >= static_cast<long long>(M) * N) return hipSuccess;
+  __bf16 old;
+  hipError_t e = hipMemcpy(&old, C + elem, sizeof(old), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  const __bf16 v = static_cast<__bf16>(1e6f);
+  if ((e = hipMemcpy(C + elem, &v, sizeof(v), hipMemcpyHostToDevice)) != hipSuccess) return e;
+  double* cs = csum + (elem / N) / 128 * N + elem % N;
+  double sum;
+  if ((e = hipMemcpy(&sum, cs, sizeof(sum), hipMemcpyDeviceToHost)) != hipSuccess) return e;
+  sum += static_cast<double>(static_cast<float>(v)) - static_cast<double>(static_cast<float>(old));
+  return hipMemcpy(cs, &sum, sizeof(sum), hipMemcpyHostToDevice);
+}
+
+// |got - ref| beyond the rounding of a bf16 output (at most half an ulp: 2^-8 of |value|, with margin), so the
+// sampled checks of the bf16-output kernel keep the tolerances of the fp32 one
+inline double beyond_bf16_rounding(double got, double ref) {
+  return std::max(0.0, std::fabs(got - ref) - std::ldexp(std::max(std::fabs(got), std::fabs(ref)), -8) * 1.01);
 }
 
 }  // namespace
@@ -1451,6 +1557,24 @@ int diag_gemm_fp4_launch(const void* A, const void* Bt, float* C, int M, int N, 
   return 0;
 }
 
+// The v3 kernel with bf16 output and fused column sums (what the diagnostic runs time and check):
+// C[M,N] (bf16) = A . Bt^T, csum[M / 128][N] (fp64) = each column's sum over every 128-row block, formed from
+// the fp32 accumulators.  bf16 (dt 0) or MX-fp8 (dt 1) operands; M, N multiples of 256, K of 64 (bf16) or 128.
+int diag_gemm_launch_ck(int dt, const void* A, const void* Bt, void* C, double* csum, int M, int N, int K,
+                        void* stream) {
+  if (M % V2_BM || N % V2_BN || K % (dt == DT_FP8 ? 128 : BK) || M <= 0 || N <= 0 || K <= 0 ||
+      (dt != DT_BF16 && dt != DT_FP8)) {
+    g_err = "gemm_ck: bf16 or fp8, M, N multiples of 256, K a multiple of 64 (bf16) or 128 (fp8)";
+    return -2;
+  }
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  const int rc = dt == DT_FP8 ? launch_v3_ck<DT_FP8>(A, Bt, static_cast<__bf16*>(C), csum, M, N, K / 2, st)
+                              : launch_v3_ck<DT_BF16>(A, Bt, static_cast<__bf16*>(C), csum, M, N, K, st);
+  if (rc != 0) return -1;
+  DIAG_CHECK(hipGetLastError());
+  return 0;
+}
+
 // Self-contained MFMA burn-in: allocate, fill, run `iters` GEMMs, time them, verify `nsamp` sampled outputs
 // against the fp32 reference kernel and, with ck_tol >= 0, every output by tile checksums (gemm_checksum:
 // *ck_err, ck_out[kCkOut]).  `inject_elem` >= 0 overwrites that output between the timing and the checks.
@@ -1466,10 +1590,18 @@ int diag_gemm_bf16_x(int device, int M, int N, int K, int warmup, int iters, int
     return -2;
   }
   DIAG_CHECK(hipSetDevice(device));
-  DevBuf bA, bBt, bC, bref, brows, bcols, bgot;
+  // the v3 kernel writes bf16 C and its own column sums (OUT_BF16_CK); the 128^2 v1 kernel fp32 C
+  const bool fused = bf16_variant(M, N) == 3 && v3_ck_path();
+  DevBuf bA, bBt, bC, bref, brows, bcols, bgot, bcs;
   DIAG_CHECK(bA.alloc(device, sizeof(__bf16) * static_cast<size_t>(M) * K));
   DIAG_CHECK(bBt.alloc(device, sizeof(__bf16) * static_cast<size_t>(N) * K));
-  DIAG_CHECK(bC.alloc(device, sizeof(float) * static_cast<size_t>(M) * N));
+  DIAG_CHECK(bC.alloc(device, (fused ? sizeof(__bf16) : sizeof(float)) * static_cast<size_t>(M) * N));
+  if (fused) DIAG_CHECK(bcs.alloc(device, sizeof(double) * static_cast<size_t>(M / 128) * N));
+  double* cs = static_cast<double*>(bcs.ptr);
+  auto run = [&]() -> int {
+    return fused ? launch_v3_ck<DT_BF16>(bA.ptr, bBt.ptr, static_cast<__bf16*>(bC.ptr), cs, M, N, K, nullptr)
+                 : diag_gemm_bf16_launch(bA.ptr, bBt.ptr, static_cast<float*>(bC.ptr), M, N, K, nullptr);
+  };
   DIAG_CHECK(bref.alloc(device, sizeof(float) * nsamp));
   DIAG_CHECK(brows.alloc(device, sizeof(int) * nsamp));
   DIAG_CHECK(bcols.alloc(device, sizeof(int) * nsamp));
@@ -1497,20 +1629,27 @@ int diag_gemm_bf16_x(int device, int M, int N, int K, int warmup, int iters, int
   DIAG_CHECK(tm.create());
   hipEvent_t e0 = tm.e0, e1 = tm.e1;
   for (int i = 0; i < warmup; ++i)
-    if (diag_gemm_bf16_launch(A, Bt, C, M, N, K, nullptr)) return -1;
+    if (run()) return -1;
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   for (int i = 0; i < iters; ++i)
-    if (diag_gemm_bf16_launch(A, Bt, C, M, N, K, nullptr)) return -1;
+    if (run()) return -1;
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
+  DIAG_CHECK(hipGetLastError());
   const double ms = elapsed_ms(e0, e1) / std::max(iters, 1);
-  DIAG_CHECK(inject_output(C, inject_elem, static_cast<long long>(M) * N));
+  if (fused) DIAG_CHECK(inject_output_ck(static_cast<__bf16*>(bC.ptr), cs, inject_elem, M, N));
+  else DIAG_CHECK(inject_output(C, inject_elem, static_cast<long long>(M) * N));
   hipLaunchKernelGGL(gemm_ref_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, A, Bt, rows, cols, ref,
                      nsamp, K);
   DIAG_CHECK(hipGetLastError());
   // gather the sampled outputs on the device: one copy instead of nsamp tiny ones
   float* got = static_cast<float*>(bgot.ptr);
-  hipLaunchKernelGGL(gather_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, C, rows, cols, got, nsamp, N);
+  if (fused)
+    hipLaunchKernelGGL(gather_kernel<__bf16>, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr,
+                       static_cast<const __bf16*>(bC.ptr), rows, cols, got, nsamp, N);
+  else
+    hipLaunchKernelGGL(gather_kernel<float>, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, C, rows, cols, got,
+                       nsamp, N);
   DIAG_CHECK(hipGetLastError());
   std::vector<float> href(nsamp), hC(nsamp);
   DIAG_CHECK(hipMemcpy(href.data(), ref, sizeof(float) * nsamp, hipMemcpyDeviceToHost));
@@ -1518,14 +1657,16 @@ int diag_gemm_bf16_x(int device, int M, int N, int K, int warmup, int iters, int
   double worst = 0.0;
   for (int i = 0; i < nsamp; ++i) {
     const double denom = std::max(1.0, std::fabs(static_cast<double>(href[i])));
-    worst = std::max(worst, std::fabs(static_cast<double>(hC[i]) - href[i]) / denom);
+    const double d = fused ? beyond_bf16_rounding(hC[i], href[i]) : std::fabs(static_cast<double>(hC[i]) - href[i]);
+    worst = std::max(worst, std::isnan(d) ? HUGE_VAL : d / denom);
   }
   *max_rel_err = worst;
   *ms_per_iter = ms;
   *tflops = 2.0 * M * N * static_cast<double>(K) / (ms * 1e-3) / 1e12;
   if (ck_tol >= 0.0) {
     const int v = bf16_variant(M, N);
-    return gemm_checksum<DT_BF16>(device, A, Bt, C, M, N, K, v == 1 ? kGeomV1 : kGeomV3, ck_tol, ck_err, ck_out);
+    return gemm_checksum<DT_BF16>(device, A, Bt, C, M, N, K, v == 1 ? kGeomV1 : kGeomV3, ck_tol, ck_err, ck_out,
+                                  fused ? cs : nullptr);
   }
   return 0;
 }
@@ -1549,10 +1690,17 @@ int diag_gemm_fp8_x(int device, int M, int N, int K, int warmup, int iters, int 
     return -2;
   }
   DIAG_CHECK(hipSetDevice(device));
-  DevBuf A, Bt, C, ref, mag, rows, cols, got;
+  const bool fused = v3_ck_path();  // bf16 C + the kernel's own column sums (OUT_BF16_CK)
+  DevBuf A, Bt, C, ref, mag, rows, cols, got, bcs;
   DIAG_CHECK(A.alloc(device, static_cast<size_t>(M) * K));
   DIAG_CHECK(Bt.alloc(device, static_cast<size_t>(N) * K));
-  DIAG_CHECK(C.alloc(device, sizeof(float) * static_cast<size_t>(M) * N));
+  DIAG_CHECK(C.alloc(device, (fused ? sizeof(__bf16) : sizeof(float)) * static_cast<size_t>(M) * N));
+  if (fused) DIAG_CHECK(bcs.alloc(device, sizeof(double) * static_cast<size_t>(M / 128) * N));
+  double* cs = static_cast<double*>(bcs.ptr);
+  auto run = [&]() -> int {
+    return fused ? launch_v3_ck<DT_FP8>(A.ptr, Bt.ptr, static_cast<__bf16*>(C.ptr), cs, M, N, K / 2, nullptr)
+                 : diag_gemm_fp8_launch(A.ptr, Bt.ptr, static_cast<float*>(C.ptr), M, N, K, nullptr);
+  };
   DIAG_CHECK(ref.alloc(device, sizeof(double) * nsamp));
   DIAG_CHECK(mag.alloc(device, sizeof(double) * nsamp));
   DIAG_CHECK(rows.alloc(device, sizeof(int) * nsamp));
@@ -1575,24 +1723,30 @@ int diag_gemm_fp8_x(int device, int M, int N, int K, int warmup, int iters, int 
   DIAG_CHECK(hipMemcpy(cols.ptr, hc.data(), sizeof(int) * nsamp, hipMemcpyHostToDevice));
   float* c = static_cast<float*>(C.ptr);
   for (int i = 0; i < warmup; ++i)
-    if (diag_gemm_fp8_launch(A.ptr, Bt.ptr, c, M, N, K, nullptr)) return -1;
+    if (run()) return -1;
   Timer tm;
   DIAG_CHECK(tm.create());
   hipEvent_t e0 = tm.e0, e1 = tm.e1;
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   for (int i = 0; i < iters; ++i)
-    if (diag_gemm_fp8_launch(A.ptr, Bt.ptr, c, M, N, K, nullptr)) return -1;
+    if (run()) return -1;
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
+  DIAG_CHECK(hipGetLastError());
   const double ms = elapsed_ms(e0, e1) / std::max(iters, 1);
-  DIAG_CHECK(inject_output(c, inject_elem, static_cast<long long>(M) * N));
+  if (fused) DIAG_CHECK(inject_output_ck(static_cast<__bf16*>(C.ptr), cs, inject_elem, M, N));
+  else DIAG_CHECK(inject_output(c, inject_elem, static_cast<long long>(M) * N));
   const int* r = static_cast<const int*>(rows.ptr);
   const int* cl = static_cast<const int*>(cols.ptr);
   hipLaunchKernelGGL(gemm_ref_fp8_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr,
                      static_cast<const uint8_t*>(A.ptr), static_cast<const uint8_t*>(Bt.ptr), r, cl,
                      static_cast<double*>(ref.ptr), static_cast<double*>(mag.ptr), nsamp, K);
-  hipLaunchKernelGGL(gather_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, c, r, cl,
-                     static_cast<float*>(got.ptr), nsamp, N);
+  if (fused)
+    hipLaunchKernelGGL(gather_kernel<__bf16>, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr,
+                       static_cast<const __bf16*>(C.ptr), r, cl, static_cast<float*>(got.ptr), nsamp, N);
+  else
+    hipLaunchKernelGGL(gather_kernel<float>, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, c, r, cl,
+                       static_cast<float*>(got.ptr), nsamp, N);
   DIAG_CHECK(hipGetLastError());
   std::vector<double> href(nsamp), hmag(nsamp);
   std::vector<float> hC(nsamp);
@@ -1600,13 +1754,16 @@ int diag_gemm_fp8_x(int device, int M, int N, int K, int warmup, int iters, int 
   DIAG_CHECK(hipMemcpy(hmag.data(), mag.ptr, sizeof(double) * nsamp, hipMemcpyDeviceToHost));
   DIAG_CHECK(hipMemcpy(hC.data(), got.ptr, sizeof(float) * nsamp, hipMemcpyDeviceToHost));
   double worst = 0.0;
-  for (int i = 0; i < nsamp; ++i)
-    worst = std::max(worst, std::fabs(static_cast<double>(hC[i]) - href[i]) / std::max(hmag[i], 1e-30));
+  for (int i = 0; i < nsamp; ++i) {
+    const double d = fused ? beyond_bf16_rounding(hC[i], href[i]) : std::fabs(static_cast<double>(hC[i]) - href[i]);
+    worst = std::max(worst, std::isnan(d) ? HUGE_VAL : d / std::max(hmag[i], 1e-30));
+  }
   *max_err = worst;
   *ms_per_iter = ms;
   *tflops = 2.0 * M * N * static_cast<double>(K) / (ms * 1e-3) / 1e12;
   if (ck_tol >= 0.0)
-    return gemm_checksum<DT_FP8>(device, A.ptr, Bt.ptr, c, M, N, K, kGeomV3, ck_tol, ck_err, ck_out);
+    return gemm_checksum<DT_FP8>(device, A.ptr, Bt.ptr, c, M, N, K, kGeomV3, ck_tol, ck_err, ck_out,
+                                 fused ? cs : nullptr);
   return 0;
 }
 

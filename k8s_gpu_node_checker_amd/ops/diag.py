@@ -200,6 +200,8 @@ def lib() -> ctypes.CDLL:
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_gemm_fp8_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.diag_gemm_launch_ck.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_hbm_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int] + \
             [ctypes.POINTER(ctypes.c_double)] * 3
         L.diag_memtest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
@@ -349,6 +351,17 @@ def gemm_fp4_launch(a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int,
     _check(lib().diag_gemm_fp4_launch(a_ptr, bt_ptr, c_ptr, m, n, k, stream))
 
 
+def gemm_launch_ck(dtype: str, a_ptr: int, bt_ptr: int, c_ptr: int, csum_ptr: int, m: int, n: int, k: int,
+                   stream: int = 0) -> None:
+    """The kernel the ``gemm`` / ``gemm_fp8`` diagnostics time: ``C = A @ Bt.T`` written as bf16 (the output
+    hipBLASLt writes) plus ``csum[m // 128][n]`` (fp64), each column's sum over every 128-row block formed from
+    the fp32 accumulators.  ``dtype`` ``"bf16"`` or ``"fp8"`` (OCP E4M3, unit block scales); 256-multiples."""
+    dt = {"bf16": 0, "fp8": 1}[dtype]
+    if m % 256 or n % 256 or k % (128 if dt else 64):
+        raise ValueError("gemm_ck: M, N must be multiples of 256 and K of 64 (bf16) or 128 (fp8)")
+    _check(lib().diag_gemm_launch_ck(dt, a_ptr, bt_ptr, c_ptr, csum_ptr, m, n, k, stream))
+
+
 def _ref(test: str, key: Any, scale: float) -> float:
     table = REFERENCE_RATES[test]
     if key not in table:  # a size without its own measurement: the nearest measured one
@@ -385,7 +398,11 @@ def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, sa
          scale: Scale = FULL, inject_elem: Optional[int] = None) -> Dict[str, Any]:
     """bf16 GEMM burn-in: rate, sampled fp32-reference error, and every output tile checked by its column
     checksums (a bad tile is named with the XCD that computed it).  ``inject_elem`` (a test hook) overwrites
-    that output between the timing and the checks."""
+    that output between the timing and the checks.
+
+    At 256-multiple sizes that fill the chip the timed kernel writes bf16 C -- the output hipBLASLt writes, so
+    the rate compares like for like -- and forms the column sums itself, in fp64 from its fp32 accumulators
+    (``gemm_launch_ck``); the sampled error is then what lies beyond the bf16 rounding of the output."""
     t0 = time.perf_counter()
     tf, err, ms, ck, out = _checked_gemm("diag_gemm_bf16_x", device, size, warmup, iters, samples, inject_elem,
                                          GEMM_CK_TOL)
@@ -401,7 +418,7 @@ def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, sa
 def gemm_fp8(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20,
              samples: int = 4096, scale: Scale = FULL, inject_elem: Optional[int] = None) -> Dict[str, Any]:
     """MX-fp8 GEMM burn-in: rate, sampled fp64-reference error (normalised by sum|a*b|) and the tile
-    checksums of every output, as ``gemm``."""
+    checksums of every output, as ``gemm`` (bf16 C with fused column sums)."""
     t0 = time.perf_counter()
     tf, err, ms, ck, out = _checked_gemm("diag_gemm_fp8_x", device, size, warmup, iters, samples, inject_elem,
                                          GEMM_FP8_CK_TOL)

@@ -214,6 +214,36 @@ def test_v3_restaging_schedules_compute_the_same(dev, m, n, k):
         diag.set_gemm_schedule(2)
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (512, 256, 256), (768, 512, 384), (1024, 768, 4096),
+                                   (2048, 2048, 2048)])
+def test_v3_bf16_output_and_fused_checksums_match(dev, m, n, k):
+    """The kernel the GEMM diagnostics time (``gemm_launch_ck``): bf16 C is the fp32 kernel's output rounded to
+    bf16 (bit-exact, both restaging orders), and the fused column sums equal the fp64 sums of the fp32 kernel's
+    output over every 128-row block, for bf16 and MX-fp8 operands, 1-64 K-tiles."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + 7 * n + 13 * k)
+    st = torch.cuda.current_stream().cuda_stream
+    a = torch.randn(m, k, device=dev, generator=g)
+    bt = torch.randn(n, k, device=dev, generator=g)
+    for dt, x, y, launch in (("bf16", a.to(torch.bfloat16), bt.to(torch.bfloat16), diag.gemm_launch),
+                             ("fp8", a.to(torch.float8_e4m3fn), bt.to(torch.float8_e4m3fn), diag.gemm_fp8_launch)):
+        with diag.gemm_config(variant="v3"):
+            c32 = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+            launch(x.data_ptr(), y.data_ptr(), c32.data_ptr(), m, n, k, st)
+            for sched in (0, 1):
+                with diag.gemm_config(schedule=sched):
+                    c16 = torch.full((m, n), float("nan"), device=dev, dtype=torch.bfloat16)
+                    cs = torch.full((m // 128, n), float("nan"), device=dev, dtype=torch.float64)
+                    diag.gemm_launch_ck(dt, x.data_ptr(), y.data_ptr(), c16.data_ptr(), cs.data_ptr(), m, n, k, st)
+                    torch.cuda.synchronize()
+                assert torch.equal(c16, c32.to(torch.bfloat16)), (dt, sched)
+                want = c32.double().view(m // 128, 128, n).sum(dim=1)
+                mag = c32.double().abs().view(m // 128, 128, n).sum(dim=1)
+                assert ((cs - want).abs() / mag).max().item() < 1e-12, (dt, sched)
+    with pytest.raises(ValueError):
+        diag.gemm_launch_ck("fp8", 0, 0, 0, 0, 256, 256, 64)
+
+
 def test_mfma_gemm_large_auto_uses_v3_and_matches(dev):
     """4096^3 in auto mode runs the staggered v3 kernel; compare every output with a bf16-input,
     fp32-accumulate torch reference.  Runs with the production knobs (what the agent launches)."""
