@@ -277,6 +277,7 @@ def test_probe_cli_under_asan_pages_cper_records(asan_probe, tmp_path):
     assert r["gpus"][0]["cper"] == {"uncorrected": 0, "fatal": 1, "corrected": 70,
                                     "last_fatal": "2026-10-16T10:15:00Z", "last_corrected": "2026-10-16T09:00:59Z"}
     assert r["gpus"][1]["cper_error"] == "AMDSMI_STATUS_NO_PERM" and "cper" not in r["gpus"][1]
+    r["ts"] = H.parse_k8s_time("2026-10-16T12:00:00Z")  # records are aged against the report's own time: pin it
     v = H.evaluate_report(r, 2, H.HealthExpectations(xgmi_links=0), now=H.parse_k8s_time("2026-10-16T12:00:00Z"))
     assert v.reasons == ["gpu0: fatal RAS error record (CPER) at 2026-10-16T10:15:00Z"], v.to_dict()
 
