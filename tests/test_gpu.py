@@ -334,7 +334,8 @@ def _tile_xcd(tm, tn, tiles_m, tiles_n, group_m=4):
 def test_gemm_checksums_catch_and_locate_one_corrupted_output(dev, kind, n, tile, group_m):
     """The GEMM tests check every output through tile column checksums, not only the 4,096 sampled ones: a
     healthy run is clean, and one output overwritten after the timing is found in exactly one tile -- its own
-    -- and attributed to the XCD that computed it (bf16 2048^2 runs the 128^2-tile kernel, the others 256^2)."""
+    -- and attributed to the XCD that computed it (bf16 2048^2 runs the 128^2-tile kernel with fp32 C, the others
+    the 256^2 one with bf16 C, where the hook overwrites the output and its share of the fused column sum)."""
     from k8s_gpu_node_checker_amd.ops import diag
     fn = getattr(diag, kind)
     tol = diag.GEMM_CK_TOL if kind == "gemm" else diag.GEMM_FP8_CK_TOL
