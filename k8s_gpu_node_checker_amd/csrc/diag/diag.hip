@@ -1429,8 +1429,10 @@ hipError_t inject_output_ck(__bf16* C, double* csum, long long elem, int M, int 
 
 // |got - ref| beyond the rounding of a bf16 output (at most half an ulp: 2^-8 of |value|, with margin), so the
 // sampled checks of the bf16-output kernel keep the tolerances of the fp32 one
+// (a NaN stays NaN: std::max would turn it into 0)
 inline double beyond_bf16_rounding(double got, double ref) {
-  return std::max(0.0, std::fabs(got - ref) - std::ldexp(std::max(std::fabs(got), std::fabs(ref)), -8) * 1.01);
+  const double e = std::fabs(got - ref) - std::ldexp(std::max(std::fabs(got), std::fabs(ref)), -8) * 1.01;
+  return e > 0.0 || std::isnan(e) ? e : 0.0;
 }
 
 }  // namespace
