@@ -97,13 +97,18 @@ class _GetProtocol(asyncio.Protocol):
                 raise ValueError("response head exceeds 64 KiB")
             return False
         lines = bytes(self.buf[:end]).decode("latin-1").split("\r\n")
-        self.status = int(lines[0].split()[1])
+        status = lines[0].split(None, 2)
+        if len(status) < 2 or not status[0].startswith("HTTP/") or not status[1].isdigit():
+            raise ValueError(f"malformed status line {lines[0][:80]!r}")
+        self.status = int(status[1])
         for line in lines[1:]:
             k, _, v = line.partition(":")
             k = k.strip().lower()
             if k == "transfer-encoding" and "chunked" in v.lower():
                 self.chunked = True
             elif k == "content-length":
+                if not v.strip().isdigit():
+                    raise ValueError(f"malformed Content-Length {v.strip()[:40]!r}")
                 self.length = int(v.strip())
         if not self.chunked and self.length is not None and self.length > self.cap:
             raise BodyTooLarge(f"body of {self.length} bytes exceeds {self.cap}")
@@ -151,7 +156,7 @@ class _GetProtocol(asyncio.Protocol):
             elif len(self.buf) - self.pos > self.cap:
                 raise BodyTooLarge(f"body exceeds {self.cap} bytes")
         except Exception as e:  # malformed or oversized: the node's fetch fails, nothing propagates
-            self._finish(exc=e)
+            self._finish(exc=e if isinstance(e, ValueError) else ValueError(f"malformed response: {e!r}"))
 
     def eof_received(self) -> Optional[bool]:
         if self.headed and not self.chunked and self.length is None:
@@ -174,7 +179,8 @@ async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None
     path = (parts.path or "/") + (("?" + parts.query) if parts.query else "")
     loop = asyncio.get_running_loop()
     done: "asyncio.Future[bytes]" = loop.create_future()
-    req = (f"GET {path} HTTP/1.1\r\nHost: {host}:{port}\r\nAccept: application/json\r\n"
+    req = (f"GET {path} HTTP/1.1\r\nHost: {f'[{host}]' if ':' in host else host}:{port}\r\n"
+           f"Accept: application/json\r\n"
            f"Connection: close\r\n\r\n").encode()
     proto = _GetProtocol(req, max_body, done)
     # the deadline cancels this task (what asyncio.timeout does from 3.11): no wrapper task per request
@@ -227,6 +233,9 @@ async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, ti
                     last = f"{type(e).__name__}: {e}"
                     if attempt < retries:
                         await asyncio.sleep(0.05 * (attempt + 1))
+                except Exception as e:  # anything else one endpoint provokes fails that node, not the check
+                    last = f"{type(e).__name__}: {e}"
+                    break
             return _error_report(t["name"], last)
 
     return list(await asyncio.gather(*(one(t) for t in targets)))

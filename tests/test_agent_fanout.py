@@ -511,6 +511,46 @@ def test_endless_body_fails_within_the_timeout_with_bounded_memory():
         ls.close()
 
 
+@pytest.mark.parametrize("resp,err", [
+    (b"HTTP/1.1\r\n\r\n", "malformed status line 'HTTP/1.1'"),
+    (b"\r\n\r\n", "malformed status line ''"),
+    (b"ICY 200 OK\r\n\r\n{}", "malformed status line 'ICY 200 OK'"),
+    (b"HTTP/1.1 2x0 OK\r\n\r\n{}", "malformed status line"),
+    (b"HTTP/1.1 200 OK\r\nContent-Length: -5\r\n\r\n{}", "malformed Content-Length '-5'"),
+    (b"HTTP/1.1 200 OK\r\nContent-Length: 1e3\r\n\r\n{}", "malformed Content-Length '1e3'"),
+    (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n", "ValueError"),
+])
+def test_a_malformed_response_fails_its_node_not_the_check(resp, err):
+    """Whatever one endpoint answers, the fan-out returns: that node gets an error report naming the problem,
+    and the other nodes' reports are unaffected."""
+    import asyncio
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    doc = {"schema": "mi355x-health/v1", "node": "good", "gpus": []}
+
+    def bad(c, stop):
+        c.recv(65536)
+        c.sendall(resp)
+        c.close()
+
+    def good(c, stop):
+        c.recv(65536)
+        body = json.dumps(doc).encode()
+        c.sendall(b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body))
+        c.close()
+    (ls, stop), (ls2, stop2) = _raw_server(bad), _raw_server(good)
+    try:
+        out = asyncio.run(fanout.fetch_all([{"name": "bad", "url": f"http://127.0.0.1:{ls.getsockname()[1]}/"},
+                                            {"name": "good", "url": f"http://127.0.0.1:{ls2.getsockname()[1]}/"}],
+                                           timeout=3.0))
+        assert out[0]["node"] == "bad" and err in out[0]["error"], out[0]
+        assert out[1] == doc
+    finally:
+        stop.set()
+        stop2.set()
+        ls.close()
+        ls2.close()
+
+
 def test_chunked_body_is_decoded():
     import asyncio
     from k8s_gpu_node_checker_amd.parallel import fanout
