@@ -348,7 +348,7 @@ class Connection:
             del buf[:end + 4]
             status_line = lines[0]
             parts = status_line.split(None, 2)
-            if len(parts) < 2 or not parts[0].startswith(b"HTTP/"):
+            if len(parts) < 2 or not parts[0].startswith(b"HTTP/") or not parts[1].isdigit():
                 raise HTTPError("protocol", f"bad status line {status_line[:80]!r}")
             status = int(parts[1])
             reason = parts[2].decode("latin-1") if len(parts) > 2 else ""
