@@ -128,6 +128,11 @@ def tls_context(cert_file: str, key_file: str, client_ca: Optional[str] = None) 
     return ctx
 
 
+# a connection that sends no complete request for this long is closed (an idle keep-alive or a stalled client
+# would otherwise hold its handler thread for the life of the agent)
+IDLE_TIMEOUT_S = 30.0
+
+
 def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = None, tls: Any = None,
           require_client_cert: bool = False) -> ThreadingHTTPServer:
     """/probe, /metrics, /status (text) and /healthz; /healthz answers 503 once no probe has completed for
@@ -139,6 +144,7 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
 
     class H(BaseHTTPRequestHandler):
         protocol_version = "HTTP/1.1"
+        timeout = IDLE_TIMEOUT_S
 
         def log_message(self, *a: Any) -> None:
             pass

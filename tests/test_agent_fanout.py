@@ -64,6 +64,28 @@ def test_agent_http_endpoint(fixture_report):
         srv.server_close()
 
 
+def test_agent_http_closes_a_silent_connection(fixture_report, monkeypatch):
+    """A client that connects and never sends a request (or leaves a keep-alive idle) is dropped after
+    IDLE_TIMEOUT_S instead of holding a handler thread for the life of the agent; the server keeps serving."""
+    import socket
+    import time
+    from k8s_gpu_node_checker_amd.agent import server
+    from k8s_gpu_node_checker_amd.utils.http import request
+    monkeypatch.setattr(server, "IDLE_TIMEOUT_S", 0.3)
+    ag = A.Agent("n", source="fixture", fixture=fixture_report)
+    srv = server.serve(ag, "127.0.0.1", 0)
+    try:
+        s = socket.create_connection(srv.server_address, timeout=5)
+        t = time.monotonic()
+        assert s.recv(1) == b""  # closed by the server, not by our timeout
+        assert 0.2 < time.monotonic() - t < 4
+        s.close()
+        assert request(f"http://127.0.0.1:{srv.server_address[1]}/healthz").text == "ok"
+    finally:
+        srv.shutdown()
+        srv.server_close()
+
+
 def test_checker_probe_endpoint_fanout(run_cli, mock_cluster, tmp_path, fixture_report):
     # three nodes whose InternalIPs are 127.0.0.x; agents for two of them, one of them unhealthy
     good = A.Agent("a", source="fixture", fixture=fixture_report)
