@@ -1,4 +1,5 @@
-"""Same operands, two GEMMs at 8192^3 bf16: diag v3 (fp32 C) and torch.matmul (hipBLASLt, bf16 C).
+"""Same operands, three GEMMs (bf16 or MX-fp8, default 8192^3): diag v3 with fp32 C, diag v3 with bf16 C and fused
+column sums (the kernel the diagnostics time), and torch (hipBLASLt, bf16 C).
 
 Run under ``rocprofv3 --kernel-trace --pmc ...`` to compare L2 behaviour (TCC hit/miss, FETCH_SIZE) and the
 clock (GRBM_GUI_ACTIVE / kernel time) of the two kernels on identical random data
@@ -18,11 +19,16 @@ g = torch.Generator(device=dev).manual_seed(7)
 a = (torch.rand(n, n, device=dev, generator=g) * 2 - 1)
 b = (torch.rand(n, n, device=dev, generator=g) * 2 - 1)
 st = torch.cuda.current_stream().cuda_stream
+c16 = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
+cs = torch.empty(n // 128, n, device=dev, dtype=torch.float64)
 if dt == "bf16":
     a, b = a.to(torch.bfloat16), b.to(torch.bfloat16)
     c = torch.empty(n, n, device=dev, dtype=torch.float32)
     for _ in range(3):
         diag.gemm_launch(a.data_ptr(), b.data_ptr(), c.data_ptr(), n, n, n, st)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        diag.gemm_launch_ck("bf16", a.data_ptr(), b.data_ptr(), c16.data_ptr(), cs.data_ptr(), n, n, n, st)
     torch.cuda.synchronize()
     for _ in range(3):
         torch.matmul(a, b.t())
@@ -33,6 +39,9 @@ else:
     one = torch.ones((), device=dev)
     for _ in range(3):
         diag.gemm_fp8_launch(a8.data_ptr(), b8.data_ptr(), c.data_ptr(), n, n, n, st)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        diag.gemm_launch_ck("fp8", a8.data_ptr(), b8.data_ptr(), c16.data_ptr(), cs.data_ptr(), n, n, n, st)
     torch.cuda.synchronize()
     for _ in range(3):
         torch._scaled_mm(a8, b8.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
