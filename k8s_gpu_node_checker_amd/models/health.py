@@ -21,6 +21,7 @@ run: driver not loaded, no permission).
 
 from __future__ import annotations
 
+import math
 import time
 TYPE_CHECKING = False
 if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
@@ -470,20 +471,38 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float
 
 def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
                     exp: Optional[HealthExpectations] = None, now: Optional[float] = None) -> Verdict:
+    """The verdict on one probe report.  A report is untrusted input (an agent endpoint, an annotation): one
+    whose fields have the wrong types is ``unknown`` with the reason, never an exception out of the check."""
+    try:
+        return _evaluate_report(report, expected_gpus, exp, now)
+    except (TypeError, ValueError, AttributeError, KeyError, IndexError, OverflowError) as e:
+        return Verdict(UNKNOWN, [f"malformed probe report ({type(e).__name__}: {str(e)[:80]})"])
+
+
+def _evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
+                     exp: Optional[HealthExpectations] = None, now: Optional[float] = None) -> Verdict:
     exp = exp or HealthExpectations()
     if not report:
         return Verdict(UNKNOWN, ["no probe report"])
+    if not isinstance(report, dict):
+        return Verdict(UNKNOWN, [f"malformed probe report (a JSON {type(report).__name__}, not an object)"])
     if report.get("schema") != SCHEMA:
         return Verdict(UNKNOWN, [f"unsupported probe schema {report.get('schema')!r}"])
     now = time.time() if now is None else now
     ts = report.get("ts")
-    age = (now - float(ts)) if isinstance(ts, (int, float)) else None
+    age = (now - float(ts)) if isinstance(ts, (int, float)) and math.isfinite(ts) else None
     if age is None or age > exp.max_age_s:
         return Verdict(UNKNOWN, ["stale probe report" if age is not None else "probe report has no timestamp"],
                        age_s=age)
+    if age < -exp.max_age_s:
+        # from further in the future than a report may be old: the agent's clock (or the report) is wrong, and
+        # such a report would otherwise count as fresh for as long as the clocks disagree
+        return Verdict(UNKNOWN, [f"probe report is {-age:.0f} s in the future (clock skew?)"], age_s=age)
     if report.get("error"):
         return Verdict(UNKNOWN, [f"probe failed: {report['error']}"], age_s=age)
     gpus = report.get("gpus") or []
+    if not isinstance(gpus, list):
+        return Verdict(UNKNOWN, [f"malformed probe report (gpus is a JSON {type(gpus).__name__})"], age_s=age)
     fails: List[str] = []
     warns: List[str] = []
     ok = 0
