@@ -142,7 +142,7 @@ def fleet_versions(extras: List[Any]) -> Optional[Dict[str, Any]]:
     n = 0
     for ex in extras:
         rep = ex.report() if ex is not None else None
-        if not rep or rep.get("error"):
+        if not rep or not isinstance(rep, dict) or rep.get("error"):
             continue
         n += 1
         drv = (rep.get("driver") or {}).get("version") if isinstance(rep.get("driver"), dict) else None
@@ -150,7 +150,7 @@ def fleet_versions(extras: List[Any]) -> Optional[Dict[str, Any]]:
             rel = H.driver_release(drv)
             drivers[rel] = drivers.get(rel, 0) + 1
         raw_fw: Dict[str, set] = {}
-        for g in rep.get("gpus") or []:
+        for g in H.report_gpus(rep):
             for name, ver in ((g.get("fw") or {}) if isinstance(g, dict) and isinstance(g.get("fw"), dict)
                               else {}).items():
                 try:

@@ -78,10 +78,10 @@ def report_text(rep: Dict[str, Any], verdict: Any) -> str:
         for r in getattr(verdict, title):
             lines.append(f"  {title[:-1]}: {r}")
     found = verdict.reasons + verdict.warnings
-    entries = [_gpu_entry(g, found) for g in rep.get("gpus") or [] if isinstance(g, dict)]
+    entries = [_gpu_entry(g, found) for g in H.report_gpus(rep) if isinstance(g, dict)]
     if entries:
         lines += ["  " + ln for ln in gpu_table(entries)]
-    for g in rep.get("gpus") or []:
+    for g in H.report_gpus(rep):
         if isinstance(g, dict) and g.get("diag_skipped"):
             lines.append(f"  gpu{g.get('index', '?')} diagnostics skipped: {g['diag_skipped']}")
     return "\n".join(lines) + "\n"
@@ -112,6 +112,8 @@ def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> 
         doc["health_condition"] = {"status": status, "reason": reason, "message": message,
                                    "heartbeat_age_s": round(now - hb, 1) if hb else None}
     rep = ex.report()
+    if rep and not isinstance(rep, dict):
+        rep = {"error": f"malformed report (a JSON {type(rep).__name__}, not an object)"}
     if rep and rep.get("error"):
         doc["report"] = {"error": rep["error"]}
     elif rep:
@@ -119,7 +121,7 @@ def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> 
         re_v = H.evaluate_report(rep, max(ex.capacity.get("amd.com/gpu", 0), ex.allocatable.get("amd.com/gpu", 0)),
                                  H.HealthExpectations(xgmi_links=opts.xgmi_links, max_age_s=opts.probe_max_age), now)
         lines = re_v.reasons + re_v.warnings
-        gpus = [_gpu_entry(g, lines) for g in rep.get("gpus") or [] if isinstance(g, dict)]
+        gpus = [_gpu_entry(g, lines) for g in H.report_gpus(rep) if isinstance(g, dict)]
         shown = {f"gpu{e['index']}:" for e in gpus}
         doc["report"] = {"probe": rep.get("probe"), "amdsmi": rep.get("amdsmi"),
                          "driver": H.driver_release(drv.get("version")) if drv.get("version") else None,

@@ -21,6 +21,7 @@ run: driver not loaded, no permission).
 
 from __future__ import annotations
 
+import io
 import math
 import time
 TYPE_CHECKING = False
@@ -469,6 +470,12 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float
     return fail, warn
 
 
+def report_gpus(report: Any) -> List[Any]:
+    """The ``gpus`` list of a report, or [] when the report (untrusted JSON) has none or something else there."""
+    g = report.get("gpus") if isinstance(report, dict) else None
+    return g if isinstance(g, list) else []
+
+
 def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
                     exp: Optional[HealthExpectations] = None, now: Optional[float] = None) -> Verdict:
     """The verdict on one probe report.  A report is untrusted input (an agent endpoint, an annotation): one
@@ -688,6 +695,11 @@ def encode_annotation(report: Dict[str, Any], encoding: str = "json") -> str:
     return GZIP_PREFIX + base64.b64encode(gzip.compress(text.encode(), 9, mtime=0)).decode("ascii")
 
 
+# a decompressed report annotation larger than this is refused (a 256 KiB gzip annotation can inflate ~1000x);
+# a level-2 report of a 64-partition CPX node is under 256 KiB as JSON
+MAX_REPORT_BYTES = 4 << 20
+
+
 def parse_annotation(raw: Optional[str]) -> Optional[Dict[str, Any]]:
     """A report annotation in either encoding -> the report dict; an undecodable one becomes a probe
     error (verdict unknown), never an exception."""
@@ -702,18 +714,26 @@ def parse_annotation(raw: Optional[str]) -> Optional[Dict[str, Any]]:
             data = base64.b64decode(raw[len(GZIP_PREFIX):], validate=True)
             try:  # one gzip member, as the agent writes it: zlib directly (GzipFile costs ~3x as much)
                 d = zlib.decompressobj(16 + zlib.MAX_WBITS)
-                body = d.decompress(data)
+                body = d.decompress(data, MAX_REPORT_BYTES + 1)
+                if len(body) > MAX_REPORT_BYTES:
+                    return {"schema": SCHEMA, "ts": time.time(),
+                            "error": f"annotation decompresses to more than {MAX_REPORT_BYTES} bytes"}
                 if not d.eof or d.unused_data:
                     raise zlib.error("not a single complete member")
             except zlib.error:
-                body = gzip.decompress(data)  # several members / trailing data: the general reader decides
+                # several members / trailing data: the general reader decides, on a bounded output
+                with gzip.GzipFile(fileobj=io.BytesIO(data)) as f:
+                    body = f.read(MAX_REPORT_BYTES + 1)
+                if len(body) > MAX_REPORT_BYTES:
+                    return {"schema": SCHEMA, "ts": time.time(),
+                            "error": f"annotation decompresses to more than {MAX_REPORT_BYTES} bytes"}
             raw = body.decode("utf-8")
         except (binascii.Error, OSError, EOFError, zlib.error, UnicodeDecodeError, ValueError):
             return {"schema": SCHEMA, "error": "annotation is not gzip+base64 JSON", "ts": time.time()}
     from ..ops.fastpath import loads  # native json.loads (falls back to the json package itself)
     try:
         doc = loads(raw)
-    except ValueError:
+    except (ValueError, RecursionError):  # RecursionError: nesting deeper than the parser's stack
         return {"schema": SCHEMA, "error": "annotation is not JSON", "ts": time.time()}
     return doc if isinstance(doc, dict) else None
 

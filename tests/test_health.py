@@ -366,3 +366,60 @@ def test_partitions_are_judged_on_down_links_only():
         assert "xGMI link(s) down" in " ".join(
             H.evaluate_report(rep(gpu0={"xgmi": "XUUUDUUU", "compute_partition": part}), 8, exp).reasons)
     assert H.evaluate_report(rep(gpu0={"xgmi": "XXXXXXXX"}), 8, exp).state == H.UNHEALTHY  # SPX: all 7 must be Up
+
+
+@pytest.mark.parametrize("mutate,needle", [
+    (lambda r: r.update(gpus=5), "gpus is a JSON int"),
+    (lambda r: r.update(gpus="abc"), "gpus is a JSON str"),
+    (lambda r: r["gpus"][2].update(fw=[1, "a"], power_cap_w="x", throttle_acc={"n": "x"}), None),
+    (lambda r: r.update(ts=float("nan")), "probe report has no timestamp"),
+    (lambda r: r.update(ts=float("inf")), "probe report has no timestamp"),
+    (lambda r: r.update(ts=time.time() + 3600), "in the future (clock skew?)"),
+])
+def test_a_malformed_report_is_unknown_not_an_exception(mutate, needle):
+    """A report is untrusted JSON (an agent endpoint, an annotation): fields of the wrong type never raise out of
+    the verdict, and a report dated further in the future than a report may be old does not count as fresh."""
+    r = rep()
+    mutate(r)
+    v = H.evaluate_report(r, 8)
+    if needle is None:
+        assert v.state in (H.UNKNOWN, H.UNHEALTHY, H.DEGRADED, H.HEALTHY)
+    else:
+        assert v.state == H.UNKNOWN and any(needle in x for x in v.reasons), v.to_dict()
+    assert H.evaluate_report([1, 2], 8).state == H.UNKNOWN
+    assert H.report_gpus({"gpus": 5}) == [] and H.report_gpus(None) == []
+
+
+def test_hostile_annotations_are_probe_errors_not_crashes_or_memory():
+    """A report annotation nested deeper than the JSON parser's stack, or a gzip member that inflates past
+    MAX_REPORT_BYTES (~1000x from a 256 KiB annotation), is a probe error (verdict unknown), bounded in time and
+    memory; a report of two gzip members still parses."""
+    import base64
+    import gzip
+    for raw in ("[" * 200000, '{"a":' * 100000):
+        doc = H.parse_annotation(raw)
+        assert doc["error"] == "annotation is not JSON"
+        assert H.evaluate_report(doc, 8).state == H.UNKNOWN
+    bomb = H.GZIP_PREFIX + base64.b64encode(gzip.compress(b" " * (64 << 20) + b"{}")).decode()
+    assert len(bomb) < 256 << 10
+    t = time.perf_counter()
+    doc = H.parse_annotation(bomb)
+    assert doc["error"] == f"annotation decompresses to more than {H.MAX_REPORT_BYTES} bytes"
+    assert time.perf_counter() - t < 1.0
+    multi = H.GZIP_PREFIX + base64.b64encode(gzip.compress(b" " * (8 << 20)) + gzip.compress(b"{}")).decode()
+    assert "more than" in H.parse_annotation(multi)["error"]
+    two = H.GZIP_PREFIX + base64.b64encode(gzip.compress(b'{"a":') + gzip.compress(b"1}")).decode()
+    assert H.parse_annotation(two) == {"a": 1}
+
+
+def test_cli_survives_a_deeply_nested_annotation(run_cli, mock_cluster, tmp_path):
+    """One node's hostile annotation makes that node unknown -- not Ready under --mi355x -- and the check
+    completes (exit 0: one GPU node is Ready) with the other node judged as usual."""
+    good = fixtures.mi355x_probe_report("a", gpus=8)
+    nodes = [fixtures.realistic_node("a", annotations=fixtures.health_annotation(good), index=0),
+             fixtures.realistic_node("b", index=1, annotations={fixtures.HEALTH_ANNOTATION: "[" * 100000})]
+    kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc, "--json", "--mi355x"])
+    assert p.returncode == 0, p.stderr
+    doc = json.loads(p.stdout)
+    assert [n["ready"] for n in doc["nodes"]] == [True, False] and doc["ready_nodes"] == 1
