@@ -657,6 +657,8 @@ def verdict_from_condition(cond: Tuple[Optional[str], Optional[str], Optional[st
     if age is None or age > max_age_s:
         return Verdict(UNKNOWN, ["stale AMDGPUHealthy condition" if age is not None
                                  else "AMDGPUHealthy condition has no heartbeat"], age_s=age)
+    if age < -max_age_s:  # as for reports: a heartbeat from the future would count as fresh indefinitely
+        return Verdict(UNKNOWN, [f"AMDGPUHealthy heartbeat is {-age:.0f} s in the future (clock skew?)"], age_s=age)
     counts, detail = _message_parts(message)
     ok, seen = counts if counts else (0, 0)
     msg = [detail] if detail else []

@@ -171,6 +171,10 @@ def test_condition_roundtrip():
                                  900, now)
     assert v.state == H.DEGRADED and v.ok
     assert H.verdict_from_condition(("True", "MI355XHealthy", "", now - 5000), 900, now).state == H.UNKNOWN
+    # a heartbeat from further in the future than the max age (an agent clock ahead by hours) is not fresh
+    fut = H.verdict_from_condition(("True", "MI355XHealthy", "", now + 5000), 900, now)
+    assert fut.state == H.UNKNOWN and "in the future" in fut.reasons[0]
+    assert H.verdict_from_condition(("True", "MI355XHealthy", "", now + 60), 900, now).state == H.HEALTHY
     assert H.verdict_from_condition(("Unknown", "MI355XProbeFailed", "no driver", now), 900, now).state == H.UNKNOWN
 
 
