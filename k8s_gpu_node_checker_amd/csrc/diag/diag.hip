@@ -1569,6 +1569,10 @@ int diag_gemm_launch_ck(int dt, const void* A, const void* Bt, void* C, double* 
     g_err = "gemm_ck: bf16 or fp8, M, N multiples of 256, K a multiple of 64 (bf16) or 128 (fp8)";
     return -2;
   }
+  if (!A || !Bt || !C || !csum) {
+    g_err = "gemm_ck: null operand, output or column-sum pointer";
+    return -2;
+  }
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const int rc = dt == DT_FP8 ? launch_v3_ck<DT_FP8>(A, Bt, static_cast<__bf16*>(C), csum, M, N, K / 2, st)
                               : launch_v3_ck<DT_BF16>(A, Bt, static_cast<__bf16*>(C), csum, M, N, K, st);

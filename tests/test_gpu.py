@@ -242,6 +242,8 @@ def test_v3_bf16_output_and_fused_checksums_match(dev, m, n, k):
                 assert ((cs - want).abs() / mag).max().item() < 1e-12, (dt, sched)
     with pytest.raises(ValueError):
         diag.gemm_launch_ck("fp8", 0, 0, 0, 0, 256, 256, 64)
+    with pytest.raises(RuntimeError, match="null"):  # refused on the host, nothing launched
+        diag.gemm_launch_ck("bf16", x.data_ptr(), y.data_ptr(), 0, 0, 256, 256, 128)
 
 
 def test_mfma_gemm_large_auto_uses_v3_and_matches(dev):
