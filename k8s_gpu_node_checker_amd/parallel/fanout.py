@@ -214,6 +214,8 @@ async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, ti
     sem = asyncio.Semaphore(max(1, concurrency))
 
     async def one(t: Dict[str, str]) -> Dict[str, Any]:
+        if t.get("error"):
+            return _error_report(t["name"], t["error"])
         async with sem:
             last = "unreachable"
             for attempt in range(retries + 1):
@@ -242,10 +244,17 @@ async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, ti
 
 
 def build_targets(scan: Any, template: str) -> List[Dict[str, str]]:
+    """One ``{"name", "url"}`` per GPU node; a node the template cannot address (``{ip}`` with no InternalIP:
+    the URL would name no host, and the client would fall back to localhost) carries an ``error`` instead."""
     out = []
+    needs_ip = "{ip}" in template
     for node, ex in zip(scan.gpu_nodes, scan.extras):
+        name = node["name"] or ""
         ip = getattr(ex, "internal_ip", None) or ""
-        out.append({"name": node["name"] or "", "url": template.format(name=node["name"] or "", ip=ip)})
+        if needs_ip and not ip:
+            out.append({"name": name, "url": "", "error": "node has no InternalIP for the probe endpoint"})
+            continue
+        out.append({"name": name, "url": template.format(name=name, ip=ip)})
     return out
 
 

@@ -573,6 +573,24 @@ def test_a_malformed_response_fails_its_node_not_the_check(resp, err):
         ls2.close()
 
 
+def test_a_node_without_internal_ip_is_not_fetched_from_localhost():
+    """``{ip}`` on a node with no InternalIP would give ``http://:9464/probe`` -- a URL the client resolves to
+    localhost (the checker's own node, when it runs beside an agent): that node gets an error report instead,
+    and no request is made for it."""
+    import asyncio
+    import types
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    scan = types.SimpleNamespace(gpu_nodes=[{"name": "a"}, {"name": "b"}],
+                                 extras=[types.SimpleNamespace(internal_ip="10.0.0.1"),
+                                         types.SimpleNamespace(internal_ip=None)])
+    t = fanout.build_targets(scan, "http://{ip}:9464/probe")
+    assert t[0] == {"name": "a", "url": "http://10.0.0.1:9464/probe"}
+    assert t[1]["url"] == "" and "no InternalIP" in t[1]["error"]
+    assert fanout.build_targets(scan, "http://{name}.agents:9464/probe")[1]["url"] == "http://b.agents:9464/probe"
+    out = asyncio.run(fanout.fetch_all(t[1:], timeout=1.0))
+    assert out[0]["node"] == "b" and out[0]["error"] == "node has no InternalIP for the probe endpoint"
+
+
 def test_chunked_body_is_decoded():
     import asyncio
     from k8s_gpu_node_checker_amd.parallel import fanout
