@@ -246,8 +246,16 @@ async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, ti
 def build_targets(scan: Any, template: str) -> List[Dict[str, str]]:
     """One ``{"name", "url"}`` per GPU node; a node the template cannot address (``{ip}`` with no InternalIP:
     the URL would name no host, and the client would fall back to localhost) carries an ``error`` instead."""
+    import string
+    try:
+        fields = {f for _, f, _, _ in string.Formatter().parse(template) if f is not None}
+    except ValueError as e:
+        raise ValueError(f"--probe-endpoint {template!r}: {e}") from None
+    if not fields <= {"name", "ip"}:
+        raise ValueError(f"--probe-endpoint {template!r}: only {{name}} and {{ip}} can be filled in, "
+                         f"not {', '.join(sorted('{' + f + '}' for f in fields - {'name', 'ip'}))}")
     out = []
-    needs_ip = "{ip}" in template
+    needs_ip = "ip" in fields
     for node, ex in zip(scan.gpu_nodes, scan.extras):
         name = node["name"] or ""
         ip = getattr(ex, "internal_ip", None) or ""

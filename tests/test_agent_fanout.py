@@ -589,6 +589,9 @@ def test_a_node_without_internal_ip_is_not_fetched_from_localhost():
     assert fanout.build_targets(scan, "http://{name}.agents:9464/probe")[1]["url"] == "http://b.agents:9464/probe"
     out = asyncio.run(fanout.fetch_all(t[1:], timeout=1.0))
     assert out[0]["node"] == "b" and out[0]["error"] == "node has no InternalIP for the probe endpoint"
+    for bad, msg in (("http://{ip}:{port}/probe", "not {port}"), ("http://{ip/probe", "--probe-endpoint")):
+        with pytest.raises(ValueError, match=msg):
+            fanout.build_targets(scan, bad)
 
 
 def test_chunked_body_is_decoded():
