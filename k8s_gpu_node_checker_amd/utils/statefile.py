@@ -38,12 +38,21 @@ def fingerprint(result: Any) -> str:
 
 
 def load(path: str) -> Optional[Dict[str, Any]]:
+    """The previous run's state, or None when there is none or it is unreadable; a field of the wrong type (a
+    hand-edited or truncated-and-rewritten file) is dropped rather than failing the run."""
     try:
         with open(path, encoding="utf-8") as f:
             doc = json.load(f)
-        return doc if isinstance(doc, dict) else None
-    except (OSError, ValueError):
+    except (OSError, ValueError, RecursionError):
         return None
+    if not isinstance(doc, dict):
+        return None
+    if not isinstance(doc.get("not_ready", []), list) or not all(isinstance(n, str) for n in doc.get("not_ready", [])):
+        doc.pop("not_ready", None)
+    for k in ("exit_code", "runs"):
+        if not isinstance(doc.get(k, 0), int) or isinstance(doc.get(k), bool):
+            doc.pop(k, None)
+    return doc
 
 
 def save(path: str, result: Any, prev: Optional[Dict[str, Any]] = None) -> None:

@@ -207,3 +207,20 @@ def test_should_notify_on_node_change_rules():
     prev = {"fingerprint": statefile.fingerprint(bad), "exit_code": 0, "not_ready": ["b"]}
     assert not statefile.should_notify(prev, bad, True, on_node_change=True)
     assert statefile.should_notify(prev, good, True, on_node_change=True)
+
+
+def test_state_file_with_wrong_types_is_tolerated(tmp_path):
+    """A hand-edited state file with fields of the wrong type does not fail the run: those fields are dropped
+    (the gate then treats the run as it would a first one for them)."""
+    import json as _json
+    import types
+    from k8s_gpu_node_checker_amd.utils import statefile
+    p = tmp_path / "state.json"
+    p.write_text(_json.dumps({"version": 1, "not_ready": 5, "exit_code": "x", "runs": True, "fingerprint": "f"}))
+    doc = statefile.load(str(p))
+    assert doc == {"version": 1, "fingerprint": "f"}
+    res = types.SimpleNamespace(exit_code=0, gpu_nodes=[{"name": "a", "ready": False, "gpus": 8},
+                                                         {"name": "b", "ready": True, "gpus": 8}])
+    assert statefile.should_notify(doc, res, only_on_error=True, on_node_change=True) is True
+    p.write_text("[" * 100000)
+    assert statefile.load(str(p)) is None
