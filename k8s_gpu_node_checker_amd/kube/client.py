@@ -213,7 +213,17 @@ class KubeClient:
                 return
             prefetched[nxt] = _PageReader(conn2, nxt, keys)
 
+        seen_tokens = set()
         while True:
+            if cont is not None:
+                if cont in seen_tokens:
+                    # a continue token handed out twice (a misbehaving proxy or aggregator) would page forever,
+                    # collecting the same nodes again: take one consistent full LIST instead, as on a 410
+                    result = ScanResult()
+                    resp = self.request("GET", self._list_path(0, None, label_selector, None))
+                    fastpath.scan_page(resp.body, result, keys, gpu_source, want_extras, annotation_mode)
+                    return result
+                seen_tokens.add(cont)
             path = self._list_path(limit, cont, label_selector, resource_version)
             pre = None
             try:

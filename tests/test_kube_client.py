@@ -272,3 +272,43 @@ def test_401_refetches_rotated_credentials_once(tmp_path, mock_cluster):
         with pytest.raises(ApiException) as ei:
             c.scan_nodes()
     assert ei.value.status == 401
+
+
+def test_a_repeated_continue_token_ends_in_one_full_list():
+    """An apiserver (or a proxy in front of it) that hands out the same continue token again would make the
+    pager loop forever, collecting the same nodes each time: the second sighting of a token switches to one
+    consistent full LIST, as an expired token does."""
+    import json
+    import threading
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+    nodes = fixtures.cluster(6, "amd")
+    paths = []
+
+    class H(BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):  # noqa: N802
+            paths.append(self.path)
+            full = "limit=" not in self.path
+            doc = {"kind": "NodeList", "apiVersion": "v1",
+                   "metadata": {"resourceVersion": "7"} if full else {"resourceVersion": "7", "continue": "same"},
+                   "items": nodes if full else nodes[:2]}
+            body = json.dumps(doc).encode()
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+    srv = ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        with KubeClient(ClusterConnection(f"http://127.0.0.1:{srv.server_address[1]}"), sleep=lambda s: None) as c:
+            res = c.scan_nodes(limit=2)
+        assert names(res) == names(scan_items(nodes))  # each node once
+        assert paths[-1] == "/api/v1/nodes" and len(paths) <= 4, paths
+    finally:
+        srv.shutdown()
+        srv.server_close()
