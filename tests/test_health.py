@@ -427,3 +427,20 @@ def test_cli_survives_a_deeply_nested_annotation(run_cli, mock_cluster, tmp_path
     assert p.returncode == 0, p.stderr
     doc = json.loads(p.stdout)
     assert [n["ready"] for n in doc["nodes"]] == [True, False] and doc["ready_nodes"] == 1
+
+
+@pytest.mark.parametrize("args", [["--json-extended", "--mi355x"], ["--health-reeval", "--json-extended"],
+                                  ["--fleet", "--json"], ["--explain", "b", "--json"], ["--explain", "c"]])
+def test_every_report_path_survives_hostile_annotations(run_cli, mock_cluster, tmp_path, args):
+    """Deep nesting, a wrong-typed ``gpus`` and a JSON array as the annotation: every report-reading path of the
+    CLI (health gate, re-evaluation, --fleet, --explain) completes without a traceback."""
+    bad_types = fixtures.mi355x_probe_report("c", gpus=8)
+    bad_types["gpus"] = 5
+    nodes = [fixtures.realistic_node("a", index=0,
+                                     annotations=fixtures.health_annotation(fixtures.mi355x_probe_report("a", gpus=8))),
+             fixtures.realistic_node("b", index=1, annotations={fixtures.HEALTH_ANNOTATION: "[" * 100000}),
+             fixtures.realistic_node("c", index=2, annotations={fixtures.HEALTH_ANNOTATION: json.dumps(bad_types)}),
+             fixtures.realistic_node("d", index=3, annotations={fixtures.HEALTH_ANNOTATION: "[1, 2]"})]
+    kc = _cluster(mock_cluster, tmp_path, nodes)
+    p = run_cli(["--kubeconfig", kc] + args)
+    assert "Traceback" not in p.stderr and p.returncode in (0, 3), p.stderr[-2000:]
