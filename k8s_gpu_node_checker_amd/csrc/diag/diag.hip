@@ -1581,6 +1581,12 @@ int diag_gemm_launch_ck(int dt, const void* A, const void* Bt, void* C, double* 
   return 0;
 }
 
+// 1 when diag_gemm_bf16_x (dt 0) / diag_gemm_fp8_x (dt 1) at M x N would time the bf16-output kernel with fused
+// column sums under the calling thread's knobs, 0 when it would write fp32 C
+int diag_gemm_ck_path(int dt, int M, int N) {
+  return v3_ck_path() && (dt == DT_FP8 || bf16_variant(M, N) == 3) ? 1 : 0;
+}
+
 // Self-contained MFMA burn-in: allocate, fill, run `iters` GEMMs, time them, verify `nsamp` sampled outputs
 // against the fp32 reference kernel and, with ck_tol >= 0, every output by tile checksums (gemm_checksum:
 // *ck_err, ck_out[kCkOut]).  `inject_elem` >= 0 overwrites that output between the timing and the checks.

@@ -206,6 +206,8 @@ def lib() -> ctypes.CDLL:
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_gemm_fp8_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.diag_gemm_ck_path.argtypes = [ctypes.c_int] * 3
+        L.diag_gemm_ck_path.restype = ctypes.c_int
         L.diag_gemm_launch_ck.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.diag_hbm_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int] + \
@@ -385,6 +387,15 @@ def _checked_gemm(fn: str, device: int, size: int, warmup: int, iters: int, samp
     return tf.value, err.value, ms.value, ck.value, list(out)
 
 
+def _gemm_output(dt: int, size: int) -> str:
+    """What the timed GEMM wrote (the library decides, under this thread's knobs): ``bf16+colsums`` -- bf16 C,
+    what hipBLASLt writes, with the column sums formed in the kernel -- or ``fp32``."""
+    probe = getattr(lib(), "diag_gemm_ck_path", None)  # (absent from the test doubles of the library)
+    if probe is None:
+        return "unknown"
+    return "bf16+colsums" if probe(dt, size, size) else "fp32"
+
+
 def _checksum_verdict(res: Dict[str, Any], ck_err: float, out: List[int], tol: float) -> str:
     """Record the tile checksums in ``res``; a non-empty string describes the tiles that failed them."""
     res["checksum_err"] = ck_err
@@ -413,7 +424,8 @@ def gemm(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20, sa
     tf, err, ms, ck, out = _checked_gemm("diag_gemm_bf16_x", device, size, warmup, iters, samples, inject_elem,
                                          GEMM_CK_TOL)
     res = {"tflops": round(tf, 1), "max_rel_err": err, "ms_per_gemm": round(ms, 4),
-           "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3)}
+           "shape": [size, size, size], "output": _gemm_output(0, size),
+           "wall_s": round(time.perf_counter() - t0, 3)}
     problems = [f"rel err {err:.2e} > {GEMM_MAX_REL_ERR:g}"] if not err <= GEMM_MAX_REL_ERR else []
     bad = _checksum_verdict(res, ck, out, GEMM_CK_TOL)
     problems += [bad] if bad else []
@@ -429,7 +441,8 @@ def gemm_fp8(device: int = 0, size: int = 8192, warmup: int = 3, iters: int = 20
     tf, err, ms, ck, out = _checked_gemm("diag_gemm_fp8_x", device, size, warmup, iters, samples, inject_elem,
                                          GEMM_FP8_CK_TOL)
     res = {"tflops": round(tf, 1), "max_err_over_mag": err, "ms_per_gemm": round(ms, 4),
-           "shape": [size, size, size], "wall_s": round(time.perf_counter() - t0, 3)}
+           "shape": [size, size, size], "output": _gemm_output(1, size),
+           "wall_s": round(time.perf_counter() - t0, 3)}
     problems = [f"err {err:.2e} > {GEMM_FP8_MAX_ERR:g}"] if not err <= GEMM_FP8_MAX_ERR else []
     bad = _checksum_verdict(res, ck, out, GEMM_FP8_CK_TOL)
     problems += [bad] if bad else []

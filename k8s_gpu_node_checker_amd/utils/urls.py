@@ -70,6 +70,8 @@ def split(url: str) -> SplitURL:
             return _slow(url)
         port_s = after[1:] if after else ""
     else:
+        if "]" in netloc or "[" in netloc:
+            return _slow(url)  # a stray bracket: urlsplit's "Invalid IPv6 URL"
         host, _, port_s = netloc.partition(":")
         if ":" in port_s:
             return _slow(url)

@@ -342,6 +342,7 @@ def test_gemm_checksums_catch_and_locate_one_corrupted_output(dev, kind, n, tile
     fn = getattr(diag, kind)
     tol = diag.GEMM_CK_TOL if kind == "gemm" else diag.GEMM_FP8_CK_TOL
     ok = fn(0, size=n, warmup=1, iters=2)  # (small sizes fall short of the 8192^3 rate: only numerics matter)
+    assert ok["output"] == ("fp32" if tile == 128 else "bf16+colsums"), ok
     assert ok["checksum_bad_tiles"] == 0 and ok["checksum_err"] < tol / 10 and "checksum" not in ok["detail"], ok
     row, col = n // 2 + 297, n // 3 + 501
     r = fn(0, size=n, warmup=1, iters=2, inject_elem=row * n + col)

@@ -11,7 +11,7 @@ CASES = ["https://10.0.0.1:6443", "http://127.0.0.1:8080/base/path?x=1", "https:
          "https://[::1]:6443/", "https://[FE80::1]", "http://host:/p", "http://:80/", "https://h.example.com:443",
          "HTTP://Host", "https://u:p@h:1/", "https://h/%20", "http://h#frag", "https://hooks.slack.com/services/T/B/X",
          "https://h:99999", "https://h:x", "http://h\t/", "http://é.example/", "noscheme", "/path/only", "",
-         "ftp://h/x", "http://[::1", "https://h:1:2", "http://h?q", "http://h:65535"]
+         "ftp://h/x", "http://[::1", "a://]", "http://h]:1/", "https://h:1:2", "http://h?q", "http://h:65535"]
 
 
 def _ref(u):
