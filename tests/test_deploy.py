@@ -276,8 +276,11 @@ def test_image_carries_every_third_party_runtime_import():
                     elif isinstance(n, ast.ImportFrom) and n.level == 0 and n.module:
                         mods.add(n.module.split(".")[0])
     third = {m for m in mods if m not in sys.stdlib_module_names and m != "k8s_gpu_node_checker_amd"}
-    runtime = _read(os.path.join(REPO, "deploy", "Dockerfile")).rsplit("\nFROM ", 1)[1]
-    installed = {"yaml": "python3-yaml" in runtime, "grpc": "grpcio" in runtime}
+    # the runtime stage copies the build stage's venv: third-party modules are whatever its pip install names
+    lines = [ln for ln in _read(os.path.join(REPO, "deploy", "Dockerfile")).splitlines() if not ln.lstrip().startswith("#")]
+    pip = " ".join(ln for ln in lines if "/opt/venv/bin/pip install" in ln)
+    assert "COPY --from=build /opt/venv /opt/venv" in lines
+    installed = {"yaml": "PyYAML" in pip, "grpc": "grpcio" in pip}
     optional = {"torch", "amdsmi"}
     assert third <= set(installed) | optional, third - set(installed) - optional
     assert all(installed[m] for m in third & set(installed)), installed
@@ -456,7 +459,7 @@ def test_level2_overlay_keeps_the_comgr_cache_and_sizes_both_containers():
     assert init["command"][0] == "mi355x-fabric"
     from k8s_gpu_node_checker_amd.ops import fabric
     fabric.main.__code__  # the console script's target exists
-    assert 'mi355x-fabric = "k8s_gpu_node_checker_amd.ops.fabric:main"' in _read(os.path.join(REPO, "pyproject.toml"))
+    assert '"mi355x-fabric = k8s_gpu_node_checker_amd.ops.fabric:main"' in _read(os.path.join(REPO, "setup.py"))
     assert _mib(init["resources"]["limits"]["memory"]) >= agent.MEM_RCCL_COLD_PEAK_MIB
     for ctr in (c, init):
         env = {e["name"]: e["value"] for e in ctr["env"]}
