@@ -17,7 +17,7 @@ import sys
 import time
 TYPE_CHECKING = False
 if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
-    from typing import Any, Callable, Dict, List, Optional, TextIO
+    from typing import Any, Callable, Dict, List, Optional, TextIO, Tuple
 
 from . import report
 from .kube.client import KubeClient
@@ -27,6 +27,9 @@ from .models.node import ScanResult
 from .models.node import HEALTH_ANNOTATION
 from .models.resources import GPU_RESOURCE_KEYS, PRIMARY_GPU_KEY
 from .utils.timing import NullTracer, Tracer
+
+#: the node agents' headless Service (deploy/daemonset.yaml): its EndpointSlices fill ``{pod_ip}``
+AGENT_SERVICE = "gpu-health/mi355x-node-agent"
 
 
 class CheckOptions:
@@ -52,6 +55,7 @@ class CheckOptions:
         self.probe_unknown = "allow"
         self.xgmi_links = H.XGMI_LINKS_EXPECTED
         self.probe_endpoint: Optional[str] = None
+        self.probe_service = AGENT_SERVICE
         self.probe_concurrency = 64
         self.probe_timeout = 2.0
         self.probe_ca: Optional[str] = None
@@ -181,8 +185,33 @@ def scan_cluster(cluster: ClusterConnection, opts: CheckOptions, tracer: Tracer)
         client.close()
 
 
+def resolve_agent_endpoints(cluster: Optional[ClusterConnection], opts: CheckOptions,
+                            tracer: Tracer) -> Tuple[Optional[Dict[str, str]], Optional[str]]:
+    """``{pod_ip}`` in ``--probe-endpoint``: the agent pod's address per node, from the EndpointSlices of
+    ``--probe-service`` (one paged GET; RBAC ``endpointslices: list`` in that namespace,
+    ``deploy/rbac.yaml``).  Returns ``(addresses, None)`` or ``(None, error)``; an error makes every node
+    ``unknown`` with that reason instead of failing the check."""
+    from .parallel.fanout import agent_addresses, template_fields
+    if not opts.probe_endpoint or "pod_ip" not in template_fields(opts.probe_endpoint):
+        return None, None
+    if cluster is None:
+        return None, "no cluster connection to read the agent's EndpointSlices"
+    ns, _, svc = (opts.probe_service or AGENT_SERVICE).partition("/")
+    if not ns or not svc:
+        return None, f"--probe-service {opts.probe_service!r} is not NAMESPACE/NAME"
+    client = KubeClient(cluster, timeout=opts.kube_timeout, retries=opts.kube_retries, tracer=tracer)
+    try:
+        with tracer.span("endpoints"):
+            return agent_addresses(client.list_endpoint_slices(ns, svc, limit=opts.page_size)), None
+    except Exception as e:  # 403 without the Role, 404 without discovery.k8s.io/v1, transport errors
+        return None, str(e).strip().splitlines()[0] if str(e).strip() else type(e).__name__
+    finally:
+        client.close()
+
+
 def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
-                 warnings: Optional[List[str]] = None) -> List[Optional[H.Verdict]]:
+                 warnings: Optional[List[str]] = None,
+                 cluster: Optional[ClusterConnection] = None) -> List[Optional[H.Verdict]]:
     """Evaluate MI355X probe reports and gate ``ready`` (no-op when no node carries one).
 
     Every verdict is cross-checked against the node's ``amd.com/gpu`` count from this LIST
@@ -196,9 +225,11 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
         reports: List[Optional[Dict[str, Any]]] = [None] * len(scan.gpu_nodes)
         if opts.probe_endpoint:
             from .parallel.fanout import fetch_probe_reports
+            pod_ips, pod_err = resolve_agent_endpoints(cluster, opts, tracer)
             reports = fetch_probe_reports(scan, opts.probe_endpoint, opts.probe_concurrency, opts.probe_timeout,
                                           ca_file=opts.probe_ca, client_cert=opts.probe_client_cert,
-                                          client_key=opts.probe_client_key)
+                                          client_key=opts.probe_client_key, pod_ips=pod_ips,
+                                          pod_ip_error=pod_err)
         verdicts: List[Optional[H.Verdict]] = []
         changed = False
         unknown_ok = opts.probe_unknown == "allow"
@@ -279,7 +310,7 @@ def run_check(cluster: ClusterConnection, opts: CheckOptions, tracer: Optional[T
     tracer = tracer or (Tracer() if (opts.trace or opts.json_extended) else NullTracer())
     scan = scan_cluster(cluster, opts, tracer)
     warnings: List[str] = []
-    verdicts = apply_health(scan, opts, tracer, warnings)
+    verdicts = apply_health(scan, opts, tracer, warnings, cluster)
     apply_schedulability(scan, opts)
     result = CheckResult(scan, verdicts, tracer)
     result.warnings = warnings

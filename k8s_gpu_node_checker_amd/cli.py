@@ -57,7 +57,10 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
     ("x", "--xgmi-links", {"type": int, "default": 7, "help": "GPU 당 기대 xGMI 링크 수 (0 = 검사 안 함, 기본: 7)"}),
     ("x", "--health-reeval", {"action": "store_true",
                               "help": "AMDGPUHealthy 조건 대신 프로브 리포트(annotation)를 이 임계값으로 재평가"}),
-    ("x", "--probe-endpoint", {"help": "노드별 프로브 URL 템플릿, 예: http://{ip}:9464/probe"}),
+    ("x", "--probe-endpoint", {"help": "노드별 프로브 URL 템플릿, 예: http://{pod_ip}:9464/probe "
+                                       "({pod_ip}: --probe-service 의 EndpointSlice, {ip}: 노드 InternalIP, {name})"}),
+    ("x", "--probe-service", {"default": "gpu-health/mi355x-node-agent", "metavar": "NS/NAME",
+                              "help": "{pod_ip} 를 채울 에이전트 Service (기본: gpu-health/mi355x-node-agent)"}),
     ("x", "--probe-concurrency", {"type": int, "default": 64, "help": "프로브 fan-out 동시성 (기본: 64)"}),
     ("x", "--probe-timeout", {"type": float, "default": 2.0, "help": "노드별 프로브 타임아웃(초) (기본: 2)"}),
     ("x", "--probe-ca", {"help": "https 프로브 엔드포인트를 검증할 CA 파일 (기본: 시스템 CA)"}),
@@ -278,7 +281,7 @@ def _watch_events(args: Any) -> int:
         def evaluate(scan):
             tr = Tracer() if (opts.trace or opts.json_extended) else NullTracer()
             warnings: list = []
-            result = CheckResult(scan, apply_health(scan, opts, tr, warnings), tr)
+            result = CheckResult(scan, apply_health(scan, opts, tr, warnings, cluster), tr)
             result.warnings = warnings
             apply_schedulability(scan, opts)
             return result

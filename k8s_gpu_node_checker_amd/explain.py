@@ -96,7 +96,7 @@ def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> 
         return {"node": node_name, "gpu_node": False, "nodes_listed": scan.items_seen}
     i = names.index(node_name)
     node, ex = scan.gpu_nodes[i], scan.extras[i]
-    verdicts = apply_health(scan, opts, NullTracer(), [])
+    verdicts = apply_health(scan, opts, NullTracer(), [], cluster)
     apply_schedulability(scan, opts)
     v = verdicts[i] if i < len(verdicts) else None
     now = time.time()

@@ -280,6 +280,24 @@ class KubeClient:
         import json
         return json.loads(self.request("GET", "/api/v1/nodes/" + quote(name)).body)
 
+    # -- discovery ------------------------------------------------------------
+    def list_endpoint_slices(self, namespace: str, service: str, limit: int = 500) -> List[Dict[str, Any]]:
+        """Every ``discovery.k8s.io/v1`` EndpointSlice of one Service (label ``kubernetes.io/service-name``),
+        paged like the node LIST.  Needs RBAC ``endpointslices: list`` in ``namespace`` only."""
+        import json
+        base = (f"/apis/discovery.k8s.io/v1/namespaces/{quote(namespace)}/endpointslices"
+                f"?labelSelector={quote('kubernetes.io/service-name=' + service)}&limit={int(limit)}")
+        items: List[Dict[str, Any]] = []
+        cont: Optional[str] = None
+        seen = set()
+        while True:
+            doc = json.loads(self.request("GET", base + (f"&continue={quote(cont)}" if cont else "")).body)
+            items.extend(x for x in doc.get("items") or [] if isinstance(x, dict))
+            cont = (doc.get("metadata") or {}).get("continue") or None
+            if not cont or cont in seen:
+                return items
+            seen.add(cont)
+
     def patch_node_condition(self, name: str, condition: Dict[str, Any]) -> Dict[str, Any]:
         """Upsert one ``status.conditions`` entry (strategic merge by ``type``; RBAC ``nodes/status: patch``).
 

@@ -10,8 +10,19 @@ no per-read coroutine resumptions, no ``wait_for`` task per request), an
 in-flight requests, a per-node timeout and one retry on connection errors.  Wall clock is ~max(node latency) instead of the sum, so it stays flat
 as the cluster grows.
 
-URL template placeholders: ``{name}`` (node name) and ``{ip}`` (the node's
-``InternalIP`` from ``status.addresses``).
+URL template placeholders: ``{name}`` (node name), ``{ip}`` (the node's
+``InternalIP`` from ``status.addresses``) and ``{pod_ip}`` (the address of the
+node agent pod on that node, from the EndpointSlices of the agent's Service,
+``--probe-service``, default ``gpu-health/mi355x-node-agent``).  The shipped
+agent listens on the pod network (``deploy/daemonset.yaml``: no
+``hostNetwork``, no ``hostPort``), so ``{pod_ip}`` is the placeholder that
+reaches it; ``{ip}`` suits agents run with ``hostNetwork``.  IPv6 addresses
+are filled in bracketed (``[fd00::7]``), ready for the host part of a URL.
+Each report stays keyed to the node it was fetched for (the reference keys its
+verdict to the node it read, ``/root/reference/check-gpu-node.py:199-212``):
+the endpoint's ``nodeName`` picks the address, and a node with no agent
+endpoint is ``unknown`` ("no agent endpoint") rather than a fetch from
+another host.
 
 Every endpoint is untrusted input: a body is read up to ``MAX_BODY`` bytes (``Content-Length``, chunked or
 read-to-close; one over the cap fails the node instead of filling the checker's memory), the whole request
@@ -243,26 +254,75 @@ async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, ti
     return list(await asyncio.gather(*(one(t) for t in targets)))
 
 
-def build_targets(scan: Any, template: str) -> List[Dict[str, str]]:
-    """One ``{"name", "url"}`` per GPU node; a node the template cannot address (``{ip}`` with no InternalIP:
-    the URL would name no host, and the client would fall back to localhost) carries an ``error`` instead."""
+def _url_host(addr: str) -> str:
+    return f"[{addr}]" if ":" in addr and not addr.startswith("[") else addr
+
+
+def agent_addresses(slices: Sequence[Dict[str, Any]]) -> Dict[str, str]:
+    """``nodeName -> address`` of the agent pod on each node, from a Service's EndpointSlices.
+
+    Per node the best endpoint wins: ready (``conditions.ready`` true, or absent, which Kubernetes reads as
+    ready) before not ready, not terminating before terminating (a rolling update briefly has two agent
+    pods on a node), then the lowest address for a stable choice.  Endpoints without ``nodeName`` or
+    address are skipped."""
+    best: Dict[str, Any] = {}
+    for sl in slices:
+        if not isinstance(sl, dict):
+            continue
+        for ep in sl.get("endpoints") or []:
+            if not isinstance(ep, dict):
+                continue
+            node = ep.get("nodeName")
+            addrs = [a for a in ep.get("addresses") or [] if isinstance(a, str) and a]
+            if not isinstance(node, str) or not node or not addrs:
+                continue
+            cond = ep.get("conditions") if isinstance(ep.get("conditions"), dict) else {}
+            rank = (cond.get("ready") is False, cond.get("terminating") is True, addrs[0])
+            if node not in best or rank < best[node][0]:
+                best[node] = (rank, addrs[0])
+    return {node: addr for node, (_, addr) in best.items()}
+
+
+def template_fields(template: str) -> set:
     import string
     try:
         fields = {f for _, f, _, _ in string.Formatter().parse(template) if f is not None}
     except ValueError as e:
         raise ValueError(f"--probe-endpoint {template!r}: {e}") from None
-    if not fields <= {"name", "ip"}:
-        raise ValueError(f"--probe-endpoint {template!r}: only {{name}} and {{ip}} can be filled in, "
-                         f"not {', '.join(sorted('{' + f + '}' for f in fields - {'name', 'ip'}))}")
+    allowed = {"name", "ip", "pod_ip"}
+    if not fields <= allowed:
+        raise ValueError(f"--probe-endpoint {template!r}: only {{name}}, {{ip}} and {{pod_ip}} can be filled in, "
+                         f"not {', '.join(sorted('{' + f + '}' for f in fields - allowed))}")
+    return fields
+
+
+def build_targets(scan: Any, template: str, pod_ips: Optional[Dict[str, str]] = None,
+                  pod_ip_error: Optional[str] = None) -> List[Dict[str, str]]:
+    """One ``{"name", "url"}`` per GPU node; a node the template cannot address carries an ``error``
+    instead: ``{ip}`` with no InternalIP (the URL would name no host, and the client would fall back to
+    localhost), ``{pod_ip}`` with no agent endpoint on the node, or with the EndpointSlices unreadable
+    (``pod_ip_error``)."""
+    fields = template_fields(template)
     out = []
     needs_ip = "ip" in fields
+    needs_pod = "pod_ip" in fields
+    pod_ips = pod_ips or {}
     for node, ex in zip(scan.gpu_nodes, scan.extras):
         name = node["name"] or ""
         ip = getattr(ex, "internal_ip", None) or ""
         if needs_ip and not ip:
             out.append({"name": name, "url": "", "error": "node has no InternalIP for the probe endpoint"})
             continue
-        out.append({"name": name, "url": template.format(name=name, ip=ip)})
+        pod_ip = ""
+        if needs_pod:
+            if pod_ip_error:
+                out.append({"name": name, "url": "", "error": f"agent endpoints unavailable: {pod_ip_error}"})
+                continue
+            pod_ip = pod_ips.get(name, "")
+            if not pod_ip:
+                out.append({"name": name, "url": "", "error": "no agent endpoint on this node"})
+                continue
+        out.append({"name": name, "url": template.format(name=name, ip=_url_host(ip), pod_ip=_url_host(pod_ip))})
     return out
 
 
@@ -291,9 +351,10 @@ def run_coroutine(coro: Any) -> Any:
 
 def fetch_probe_reports(scan: Any, template: str, concurrency: int = 64, timeout: float = 2.0,
                         ca_file: Optional[str] = None, client_cert: Optional[str] = None,
-                        client_key: Optional[str] = None) -> List[Optional[Dict[str, Any]]]:
+                        client_key: Optional[str] = None, pod_ips: Optional[Dict[str, str]] = None,
+                        pod_ip_error: Optional[str] = None) -> List[Optional[Dict[str, Any]]]:
     """Fetch one probe report per GPU node (parallel to ``scan.gpu_nodes``)."""
-    targets = build_targets(scan, template)
+    targets = build_targets(scan, template, pod_ips, pod_ip_error)
     if not targets:
         return []
     return list(run_coroutine(fetch_all(targets, concurrency, timeout, ca_file=ca_file, client_cert=client_cert,

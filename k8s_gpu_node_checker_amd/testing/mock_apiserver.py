@@ -164,6 +164,38 @@ def _merge_patch(target: Dict[str, Any], patch: Dict[str, Any]) -> None:
 
 
 LEASES = "/apis/coordination.k8s.io/v1/namespaces/"
+SLICES = "/apis/discovery.k8s.io/v1/namespaces/"
+
+
+def _selector_matches(selector: str, labels: Dict[str, Any]) -> bool:
+    """Equality-based label selectors (``k=v,k2==v2,k3!=v3``): what the clients here send."""
+    for term in filter(None, (t.strip() for t in selector.split(","))):
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            if labels.get(k.strip()) == v.strip():
+                return False
+        else:
+            k, v = term.replace("==", "=").split("=", 1)
+            if labels.get(k.strip()) != v.strip():
+                return False
+    return True
+
+
+def endpoint_slice(namespace: str, service: str, endpoints: List[Dict[str, Any]], port: int = 9464,
+                   name: Optional[str] = None) -> Dict[str, Any]:
+    """A ``discovery.k8s.io/v1`` EndpointSlice of ``service``; each endpoint dict has ``node`` and ``ip`` and
+    optionally ``ready`` / ``terminating`` (omitted conditions are left out, as the apiserver does)."""
+    eps = []
+    for e in endpoints:
+        cond = {k: e[k] for k in ("ready", "serving", "terminating") if k in e}
+        ep: Dict[str, Any] = {"addresses": [e["ip"]], "nodeName": e["node"], "conditions": cond,
+                              "targetRef": {"kind": "Pod", "namespace": namespace, "name": f"{service}-{e['node']}"}}
+        eps.append(ep)
+    return {"kind": "EndpointSlice", "apiVersion": "discovery.k8s.io/v1", "addressType": "IPv4",
+            "metadata": {"name": name or f"{service}-{len(eps)}", "namespace": namespace,
+                         "labels": {"kubernetes.io/service-name": service,
+                                    "endpointslice.kubernetes.io/managed-by": "endpointslice-controller.k8s.io"}},
+            "endpoints": eps, "ports": [{"name": "probe", "port": port, "protocol": "TCP"}]}
 
 
 class MockConfig:
@@ -291,7 +323,34 @@ class _Handler(BaseHTTPRequestHandler):
         if path.startswith(LEASES):
             self._lease("GET", path, b"")
             return
+        if path.startswith(SLICES) and path.endswith("/endpointslices"):
+            self._endpoint_slices(unquote(path[len(SLICES):-len("/endpointslices")]), parse_qs(parts.query))
+            return
         self._send(404, self._status_body(404, "NotFound", "not found"), reason="Not Found")
+
+    def _endpoint_slices(self, namespace: str, q: Dict[str, List[str]]) -> None:
+        """``GET .../namespaces/{ns}/endpointslices?labelSelector=&limit=&continue=`` over
+        ``server.endpoint_slices``; ``server.endpoint_slices_status`` fails it (e.g. 403 without the Role)."""
+        srv = self.server
+        if srv.endpoint_slices_status is not None:
+            code = srv.endpoint_slices_status
+            reason = {403: "Forbidden", 404: "NotFound"}.get(code, "InternalError")
+            msg = (f'endpointslices.discovery.k8s.io is forbidden: User "system:anonymous" cannot list resource '
+                   f'"endpointslices" in API group "discovery.k8s.io" in the namespace "{namespace}"'
+                   if code == 403 else "not available")
+            self._send(code, self._status_body(code, reason, msg), reason=reason)
+            return
+        sel = q.get("labelSelector", [""])[0]
+        items = [sl for sl in srv.endpoint_slices if (sl.get("metadata") or {}).get("namespace") == namespace
+                 and _selector_matches(sel, (sl.get("metadata") or {}).get("labels") or {})]
+        limit = int(q.get("limit", ["0"])[0] or 0)
+        start = int(q.get("continue", ["0"])[0] or 0)
+        page = items[start:start + limit] if limit else items[start:]
+        meta: Dict[str, Any] = {"resourceVersion": "1"}
+        if limit and start + limit < len(items):
+            meta["continue"] = str(start + limit)
+        self._send(200, json.dumps({"kind": "EndpointSliceList", "apiVersion": "discovery.k8s.io/v1",
+                                    "metadata": meta, "items": page}).encode())
 
     def _lease(self, method: str, path: str, body: bytes) -> None:
         """``coordination.k8s.io/v1`` Leases: GET / POST (create, 409 if it exists) / PUT (update, 409 unless the
@@ -513,6 +572,8 @@ class MockApiServer(ThreadingHTTPServer):
         self.lease_rv = 0
         self.lease_writes: List[Any] = []  # (method, name, holderIdentity) of every accepted write
         self.lease_status: Optional[int] = None
+        self.endpoint_slices: List[Dict[str, Any]] = []  # discovery.k8s.io/v1 EndpointSlices (any namespace)
+        self.endpoint_slices_status: Optional[int] = None
         self.scheme = "http"
         if certfile:
             import ssl

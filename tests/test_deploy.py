@@ -178,7 +178,7 @@ def test_monitoring_rules_use_metrics_the_agent_emits():
     from prometheus_client.parser import text_string_to_metric_families
     docs = [d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "monitoring", "monitoring.yaml"))) if d]
     kinds = {d["kind"] for d in docs}
-    assert kinds == {"Service", "ServiceMonitor", "PrometheusRule"}
+    assert kinds == {"ServiceMonitor", "PrometheusRule"}
     fams = {f.name: f for f in text_string_to_metric_families(agent._metrics(_rich_report()))}
     labels = {name: set().union(*(set(s.labels) for s in f.samples)) | {"node"} for name, f in fams.items()}
     rules = [r for d in docs if d["kind"] == "PrometheusRule" for grp in d["spec"]["groups"] for r in grp["rules"]]
@@ -197,10 +197,11 @@ def test_monitoring_rules_use_metrics_the_agent_emits():
         for lbl in re.findall(r"\$labels\.([a-z_]+)", r["annotations"]["summary"]):
             assert lbl in have, (r["alert"], lbl, have)
     # the Service and ServiceMonitor find the DaemonSet's pods and its metrics port
-    ds = next(d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
+    base = [d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d]
+    ds = next(d for d in base if d["kind"] == "DaemonSet")
     pod_labels = ds["spec"]["template"]["metadata"]["labels"]
     port_names = {p["name"] for c in ds["spec"]["template"]["spec"]["containers"] for p in c.get("ports", [])}
-    svc = next(d for d in docs if d["kind"] == "Service")
+    svc = next(d for d in base if d["kind"] == "Service")
     assert svc["spec"]["selector"].items() <= pod_labels.items()
     assert {p["targetPort"] for p in svc["spec"]["ports"]} <= port_names
     sm = next(d for d in docs if d["kind"] == "ServiceMonitor")

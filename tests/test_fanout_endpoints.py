@@ -1,0 +1,184 @@
+"""``--probe-endpoint 'http://{pod_ip}:9464/probe'`` reaches the agents the shipped manifests deploy.
+
+The agent DaemonSet listens on the pod network only, so the fan-out addresses it through the EndpointSlices
+of the agents' headless Service (``deploy/daemonset.yaml``), read with the namespaced Role in
+``deploy/rbac.yaml``.  These tests take the Service, port, RBAC and documented template from the real
+manifests, serve matching EndpointSlices from the mock apiserver and run the checker against mock agents
+bound to those pod addresses (127.0.0.x).  Reference: each verdict belongs to the node it was read for
+(``/root/reference/check-gpu-node.py:199-212``).
+"""
+import json
+import os
+import re
+import types
+
+import pytest
+import yaml
+
+from k8s_gpu_node_checker_amd import cli
+from k8s_gpu_node_checker_amd.agent import agent as A
+from k8s_gpu_node_checker_amd.parallel import fanout
+from k8s_gpu_node_checker_amd.testing import fixtures
+from k8s_gpu_node_checker_amd.testing.mock_apiserver import endpoint_slice, write_kubeconfig
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _docs(*rel):
+    with open(os.path.join(REPO, "deploy", *rel), encoding="utf-8") as f:
+        return [d for d in yaml.safe_load_all(f) if d]
+
+
+def _agent_service():
+    """(namespace, name, port) of the agents' Service, checked against the DaemonSet it fronts."""
+    docs = _docs("daemonset.yaml")
+    ds = next(d for d in docs if d["kind"] == "DaemonSet")
+    svc = next(d for d in docs if d["kind"] == "Service")
+    pod = ds["spec"]["template"]
+    assert svc["metadata"]["namespace"] == ds["metadata"]["namespace"]
+    assert svc["spec"]["selector"].items() <= pod["metadata"]["labels"].items()
+    c = pod["spec"]["containers"][0]
+    ports = {p["name"]: p["containerPort"] for p in c["ports"]}
+    [sp] = svc["spec"]["ports"]
+    port = ports[sp["targetPort"]]
+    # the agent really listens on that port on every pod address
+    args = A.build_parser().parse_args(c["command"][1:])
+    assert args.listen == f"0.0.0.0:{port}"
+    assert not pod["spec"].get("hostNetwork") and "hostPort" not in c["ports"][0]
+    return svc["metadata"]["namespace"], svc["metadata"]["name"], port
+
+
+def test_manifests_wire_the_pod_ip_source_end_to_end():
+    ns, name, port = _agent_service()
+    # the checker's default --probe-service is that Service
+    assert cli.parse_args([]).probe_service == f"{ns}/{name}"
+    # the checker's ServiceAccount may list EndpointSlices in that namespace (and nothing more is added)
+    rbac = _docs("rbac.yaml")
+    roles = {d["metadata"]["name"]: d for d in rbac if d["kind"] == "Role"}
+    grants = set()
+    for b in (d for d in rbac if d["kind"] == "RoleBinding"):
+        if {"kind": "ServiceAccount", "name": "gpu-node-checker", "namespace": ns} not in b["subjects"]:
+            continue
+        role = roles[b["roleRef"]["name"]]
+        assert role["metadata"]["namespace"] == b["metadata"]["namespace"] == ns
+        grants |= {(g, r, v) for rule in role["rules"] for g in rule["apiGroups"] for r in rule["resources"]
+                   for v in rule["verbs"]}
+    assert grants == {("discovery.k8s.io", "endpointslices", "list")}
+    # the documented template is the one that reaches the agents
+    with open(os.path.join(REPO, "README.md"), encoding="utf-8") as f:
+        readme = f.read()
+    assert f"--probe-endpoint 'http://{{pod_ip}}:{port}/probe'" in readme
+    assert "'http://{ip}:9464/probe'" not in readme
+
+
+def test_agent_addresses_prefers_ready_then_live_endpoints():
+    slices = [
+        endpoint_slice("gpu-health", "svc", [{"node": "a", "ip": "10.0.0.9", "ready": False, "terminating": True},
+                                             {"node": "b", "ip": "10.0.1.2", "ready": False}]),
+        endpoint_slice("gpu-health", "svc", [{"node": "a", "ip": "10.0.0.3", "ready": True},
+                                             {"node": "b", "ip": "10.0.1.1", "ready": False},
+                                             {"node": "c", "ip": "fd00::7"}], name="svc-2"),
+        {"endpoints": [{"addresses": [], "nodeName": "d"}, {"addresses": ["10.9.9.9"]}, "junk"]},
+    ]
+    assert fanout.agent_addresses(slices) == {"a": "10.0.0.3", "b": "10.0.1.1", "c": "fd00::7"}
+    scan = types.SimpleNamespace(gpu_nodes=[{"name": n} for n in "abcd"],
+                                 extras=[types.SimpleNamespace(internal_ip=None)] * 4)
+    t = fanout.build_targets(scan, "http://{pod_ip}:9464/probe", fanout.agent_addresses(slices))
+    assert [x["url"] for x in t] == ["http://10.0.0.3:9464/probe", "http://10.0.1.1:9464/probe",
+                                     "http://[fd00::7]:9464/probe", ""]
+    assert t[3]["error"] == "no agent endpoint on this node"
+    t = fanout.build_targets(scan, "http://{pod_ip}:9464/probe", None, "(403) Forbidden")
+    assert all(x["error"] == "agent endpoints unavailable: (403) Forbidden" for x in t)
+
+
+@pytest.fixture
+def pod_network(fixture_report_factory):
+    """Mock agents on 127.0.0.2-4 (one port), as the DaemonSet's pods a, b, c; b reports an ECC fault."""
+    servers = []
+    port = 0
+    for i, name in enumerate("abc"):
+        ag = A.Agent(name, source="fixture", fixture=fixture_report_factory(name))
+        rep = ag.probe_once()
+        if name == "b":
+            rep["gpus"][0]["ecc_uncorrectable"] = 3
+        srv = A.serve(ag, f"127.0.0.{i + 2}", port)
+        port = srv.server_address[1]
+        servers.append(srv)
+    yield port
+    for s in servers:
+        s.shutdown()
+        s.server_close()
+
+
+@pytest.fixture
+def fixture_report_factory(tmp_path):
+    def make(name):
+        p = tmp_path / f"probe-{name}.json"
+        p.write_text(json.dumps(fixtures.mi355x_probe_report(name, gpus=8)))
+        return str(p)
+    return make
+
+
+def _cluster(mock_cluster, ns, name, port, status=None):
+    nodes = []
+    for i, n in enumerate("abcd"):
+        node = fixtures.realistic_node(n, "amd.com/gpu", 8, index=i)
+        # the InternalIP reaches nothing: only {pod_ip} can find the agents
+        node["status"]["addresses"][0]["address"] = "127.0.0.1"
+        nodes.append(node)
+    srv = mock_cluster(nodes)
+    # two slices, as the EndpointSlice controller splits large Services; a stale terminating pod on node a
+    srv.endpoint_slices = [
+        endpoint_slice(ns, name, [{"node": "a", "ip": "127.0.0.9", "ready": False, "terminating": True},
+                                  {"node": "a", "ip": "127.0.0.2", "ready": True},
+                                  {"node": "b", "ip": "127.0.0.3", "ready": True}], port=port, name=f"{name}-x1"),
+        endpoint_slice(ns, name, [{"node": "c", "ip": "127.0.0.4"}], port=port, name=f"{name}-x2"),
+        # another Service's slice in the namespace, and one of the same name elsewhere: neither is read
+        endpoint_slice(ns, "other", [{"node": "d", "ip": "127.0.0.5", "ready": True}], port=port),
+        endpoint_slice("default", name, [{"node": "d", "ip": "127.0.0.6", "ready": True}], port=port),
+    ]
+    srv.endpoint_slices_status = status
+    return srv
+
+
+def test_pod_ip_fanout_reaches_each_nodes_own_agent(pod_network, mock_cluster, run_cli, tmp_path):
+    ns, name, _ = _agent_service()
+    port = pod_network
+    srv = _cluster(mock_cluster, ns, name, port)
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    # --page-size 1: the EndpointSlice LIST is paged like the node LIST
+    p = run_cli(["--kubeconfig", kc, "--mi355x", "--json-extended", "--probe-unknown", "deny", "--page-size", "1",
+                 "--probe-endpoint", f"http://{{pod_ip}}:{port}/probe", "--probe-timeout", "2"])
+    doc = json.loads(p.stdout)
+    health = {n["name"]: n["health"] for n in doc["mi355x"]["nodes"]}
+    assert {k: v["state"] for k, v in health.items()} == {"a": "healthy", "b": "unhealthy", "c": "healthy",
+                                                          "d": "unknown"}
+    assert any("no agent endpoint" in r for r in health["d"].get("reasons", [])), health["d"]
+    assert not any("report is for node" in r for v in health.values() for r in v.get("reasons", []))
+    assert [n["ready"] for n in doc["nodes"]] == [True, False, True, False]
+    assert p.returncode == 0
+    paths = [e["path"] for e in srv.log if "endpointslices" in e["path"]]
+    assert paths and all(pth.startswith(f"/apis/discovery.k8s.io/v1/namespaces/{ns}/endpointslices?") for pth in paths)
+    assert len(paths) == 2  # two slices of this Service at one per page
+
+
+def test_pod_ip_fanout_without_rbac_makes_nodes_unknown_not_wrong(pod_network, mock_cluster, run_cli, tmp_path):
+    ns, name, _ = _agent_service()
+    srv = _cluster(mock_cluster, ns, name, pod_network, status=403)
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    p = run_cli(["--kubeconfig", kc, "--mi355x", "--json-extended", "--probe-unknown", "deny",
+                 "--probe-endpoint", f"http://{{pod_ip}}:{pod_network}/probe"])
+    doc = json.loads(p.stdout)
+    for n in doc["mi355x"]["nodes"]:
+        assert n["health"]["state"] == "unknown"
+        assert any(re.search(r"agent endpoints unavailable: \(403\)", r) for r in n["health"]["reasons"]), n
+    assert p.returncode == 3
+
+
+def test_probe_service_flag_selects_another_service(pod_network, mock_cluster, run_cli, tmp_path):
+    srv = _cluster(mock_cluster, "monitoring", "gpu-agents", pod_network)
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    p = run_cli(["--kubeconfig", kc, "--mi355x", "--json-extended", "--probe-service", "monitoring/gpu-agents",
+                 "--probe-endpoint", f"http://{{pod_ip}}:{pod_network}/probe"])
+    states = [n["health"]["state"] for n in json.loads(p.stdout)["mi355x"]["nodes"]]
+    assert states == ["healthy", "unhealthy", "healthy", "unknown"]
