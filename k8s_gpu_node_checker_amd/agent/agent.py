@@ -48,6 +48,7 @@ from ..models.health import (HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, XGMI_
                               condition_for, condition_reason, driver_release, encode_annotation, evaluate_report,
                               format_k8s_time,
                               throttle_window)
+from ..models.baseline import Baselines, gpu_key
 from ..models.node import HEALTH_ANNOTATION
 from ..models.resources import PRIMARY_GPU_KEY, gpu_breakdown
 from .server import _metrics, serve, tls_context  # noqa: F401  (the agent's HTTP side; re-exported)
@@ -64,6 +65,13 @@ CE_WINDOW_S = 3600.0
 CE_MIN_SPAN_S = 600.0
 
 DIAG_WHEN = ("idle", "always")
+# a GPU's latest diagnostic result counts as a peer of the others' for this long (a busy GPU keeps an older one)
+PEER_MAX_AGE_S = 86400.0
+
+
+def baseline_key(entry: Dict[str, Any], bdf: str, device: int) -> str:
+    """Whose self-baseline a device's result feeds: amd-smi UUID, else PCI address, else the HIP ordinal."""
+    return gpu_key(entry) or (f"bdf:{bdf}" if bdf else f"hip:{device}")
 # per-GPU fields kept out of the node annotation (Agent.annotation)
 _ANNOTATION_DROP = frozenset(("xgmi_kb", "throttle_acc", "procs", "probe_us"))
 # a JSON report annotation above this goes out gzip-encoded (the apiserver caps a node's annotations at 256 KiB)
@@ -346,7 +354,8 @@ class Agent:
                  diag_timeout: float = 300.0, ignore_pids: Sequence[int] = (),
                  expect_gpus: Optional[int] = None, expectations: Optional[HealthExpectations] = None,
                  pod_resources_socket: Optional[str] = None, gpu_resources: Sequence[str] = (PRIMARY_GPU_KEY,),
-                 label_node: bool = False, annotation_encoding: str = "json", diag_parallel: int = DIAG_PARALLEL):
+                 label_node: bool = False, annotation_encoding: str = "json", diag_parallel: int = DIAG_PARALLEL,
+                 diag_baseline: bool = True, baseline_file: Optional[str] = None):
         self.node = node
         if diag_parallel < 1:
             raise ValueError("diag_parallel must be >= 1")
@@ -396,6 +405,10 @@ class Agent:
         self._hip_count0: Optional[int] = None  # HIP device count the process saw first (runtime_lost)
         self.diag_timeout = diag_timeout
         self._diag_skipped: Dict[int, str] = {}
+        # node-level findings of the last judgement (models/peers.judge_node): every GPU slow alike
+        self.diag_findings: List[Dict[str, Any]] = []
+        # per-GPU self-baselines of the diagnostics' rates (models/baseline.py); None: not kept
+        self.baselines = Baselines(baseline_file) if diag_baseline else None
         # set when the HIP runtime lost its devices (runtime_lost): no further diagnostics in this process,
         # /healthz answers 503 so the liveness probe restarts the agent
         self.hip_lost: Optional[str] = None
@@ -571,11 +584,17 @@ class Agent:
                 print(f"HIP runtime lost its devices ({lost}); diagnostics stop, /healthz fails so the "
                       "agent is restarted", file=sys.stderr, flush=True)
                 self.hip_lost = lost
+        fresh = []
         for d, res in finished.items():
             if self.hip_lost is not None and d in lost_devs:
                 continue
             self._diag_cache[d] = res
-            started = self._diag_ran[d] = self._diag_at[d]
+            self._diag_ran[d] = self._diag_at[d]
+            fresh.append(d)
+        self._judge_diagnostics(devices, entries, fresh)
+        for d in fresh:
+            res = self._diag_cache[d]
+            started = self._diag_ran[d]
             sig = result_signature(res) if not_clean(res) else ""
             if sig and sig != self._rechecked.get(d) and self.diag_interval > DIAG_RECHECK_S:
                 # a slow or failed result is measured again after DIAG_RECHECK_S instead of a whole interval
@@ -620,6 +639,23 @@ class Agent:
                     "pass": False,
                     "detail": f"node-level xGMI/RCCL tests did not finish within {self.diag_timeout:g} s (fabric hang?)"}}
         return {d: self._diag_cache[d] for d in devices if d in self._diag_cache}
+
+    def _judge_diagnostics(self, devices: List[int], entries: Dict[int, Dict[str, Any]], fresh: List[int]) -> None:
+        """Judge the GPUs' latest diagnostic results together (``models/peers.judge_node``): each rate against the
+        node's other GPUs measured within ``PEER_MAX_AGE_S`` (a lone GPU against the references), a shortfall
+        every GPU shares as one node-level finding (``self.diag_findings``).  Fresh results also update their
+        GPU's self-baseline (``models/baseline.py``), whose drift notes the judgement then includes."""
+        from ..models import peers
+        now = time.time()
+        pool = {d: self._diag_cache[d] for d in devices
+                if d in self._diag_cache and now - self._diag_ran.get(d, float("-inf")) <= PEER_MAX_AGE_S}
+        label = {d: f"gpu{(entries.get(d) or {}).get('index', d)}" for d in pool}
+        self.diag_findings = peers.judge_node(pool, label)
+        if self.baselines is not None and fresh:
+            for d in fresh:
+                key = baseline_key(entries.get(d) or {}, self._bdf.get(d, ""), d)
+                self.baselines.observe(key, self._diag_cache[d], now)
+            self.diag_findings = peers.judge_node(pool, label)
 
     def _start_diag(self, d: int, memory_partition: Any, power: Optional[float]) -> None:
         """Start device ``d``'s diagnostics on its own thread (the partition's memory share comes from amd-smi's
@@ -725,6 +761,8 @@ class Agent:
                     g["diag_skipped"] = self._diag_skipped[d]
             if self._fabric:
                 rep["fabric"] = self._fabric
+            if self.diag_findings:
+                rep["diag_node"] = {"findings": self.diag_findings}
         if self.pod_resources_state is not None:
             rep["pod_resources"] = self.pod_resources_state
         verdict = self.evaluate(rep)
@@ -947,6 +985,11 @@ def build_parser() -> argparse.ArgumentParser:
                          "modes, VBIOS, driver) for nodeSelector / nodeAffinity")
     ap.add_argument("--busy-gfx-activity", type=int, default=10,
                     help="graphics-engine activity (%%) at which a GPU counts as busy (default 10)")
+    ap.add_argument("--diag-baseline-file", default=None, metavar="PATH",
+                    help="keep each GPU's self-baseline of the diagnostics' rates (its first clean runs) in this "
+                         "JSON file across restarts (default: in memory only)")
+    ap.add_argument("--no-diag-baseline", dest="diag_baseline", action="store_false",
+                    help="do not keep per-GPU self-baselines (no drift warnings)")
     return ap
 
 
@@ -962,7 +1005,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                   expectations=HealthExpectations(xgmi_links=args.xgmi_links),
                   pod_resources_socket=args.pod_resources_socket,
                   gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)), label_node=args.label_node,
-                  annotation_encoding=args.annotation_encoding, diag_parallel=args.diag_parallel)
+                  annotation_encoding=args.annotation_encoding, diag_parallel=args.diag_parallel,
+                  diag_baseline=args.diag_baseline, baseline_file=args.diag_baseline_file)
     client = None
     srv = None
     try:

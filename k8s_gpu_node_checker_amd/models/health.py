@@ -529,6 +529,12 @@ def _evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
     modes = partition_mismatch(gpus)
     if modes:
         warns.append("partition modes differ across GPUs: " + "; ".join(modes))
+    node_diag = report.get("diag_node")
+    if isinstance(node_diag, dict) and isinstance(node_diag.get("findings"), list):
+        # every GPU of the node slow alike (models/peers.judge_node): the node's condition, a warning, never a
+        # GPU failure
+        from .peers import finding_text
+        warns += [finding_text(f) for f in node_diag["findings"] if isinstance(f, dict)]
     fabric = report.get("fabric")
     if isinstance(fabric, dict):
         for test, res in fabric.items():  # node-level: the xGMI pair matrix (ops/diag.p2p_matrix)

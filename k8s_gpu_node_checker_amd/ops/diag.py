@@ -57,6 +57,13 @@ from .native import NativeUnavailable, load_cdll
 # once is unmeasured (parity unpinned: no 8-GPU box was available to this project).
 # The partition scaling is proportional, not measured (no partitioned MI355X was available): it is the
 # lenient bound, so a healthy partition never fails; a partitioned GPU's degraded band is advisory.
+#
+# These absolute lines judge a GPU *alone*.  GPUs measured together on one node are judged against each other
+# (models/peers.judge_node, applied by the node agent, `mi355x-diag` and the burn-in): a GPU under 85 % of its
+# node's other GPUs fails by name, a shortfall every GPU shares alike is one node-level *degraded* finding (the
+# platform's cooling / power / firmware, never `unhealthy`), and each GPU also keeps a self-baseline of its first
+# clean runs (models/baseline.py) whose drift is a warning.  So the references below are not re-tuned to
+# whichever box ran last: a slower healthy platform shows as a node-level note, not as failed GPUs.
 FAIL_FRACTION = 0.85
 SHARED_TESTS = frozenset(("host_link",))
 _HOST_SHARED = threading.Lock()  # held by the one device measuring a SHARED_TESTS test
@@ -154,11 +161,32 @@ def judge_rate(value: float, expected: float) -> str:
 
 def _rated(res: Dict[str, Any], rates: Dict[str, float], expected: Dict[str, float], unit: str,
            numerics_ok: bool = True, numerics_detail: str = "") -> Dict[str, Any]:
-    """Fold rate verdicts (and a numerics verdict) into a test result: ``pass``, ``degraded``,
-    ``fraction`` (worst rate / reference), ``expect`` and a human ``detail``."""
+    """Record a rate test's raw findings in ``res`` -- ``rates``, ``expect`` (the scaled references), ``unit``
+    and ``numerics`` (what was wrong with the results, "" when nothing) -- and judge them against the
+    references (:func:`judge_absolute`).  The raw fields stay so a node-level judgement
+    (``models/peers.judge_node``: the GPU against the node's other GPUs) can re-judge the same result."""
+    res["rates"] = {k: round(float(v), 4) for k, v in rates.items()}
+    res["expect"] = {k: round(v, 3) for k, v in expected.items()}
+    res["unit"] = unit
+    res["numerics"] = "" if numerics_ok else (numerics_detail or "wrong results")
+    return judge_absolute(res)
+
+
+def _notes(res: Dict[str, Any]) -> List[str]:
+    """The degraded-only notes of a result: lagging XCDs / CUs (``lag``), drift from the GPU's own
+    baseline (``drift``, models/baseline.py)."""
+    return [str(x) for key in ("lag", "drift") for x in (res.get(key) or []) if x]
+
+
+def judge_absolute(res: Dict[str, Any]) -> Dict[str, Any]:
+    """``pass`` / ``degraded`` / ``fraction`` / ``detail`` of a rate test from its raw fields: numerics wrong ->
+    failed; a rate under FAIL_FRACTION of its reference -> failed, under DEGRADED_FRACTION -> degraded; a lag or
+    drift note -> degraded.  How a lone GPU (or one with no peers this cycle) is judged."""
     worst, problems, slow = 1e9, [], []
-    for k, v in rates.items():
-        exp = expected[k]
+    unit = res.get("unit", "")
+    expected = res.get("expect") or {}
+    for k, v in (res.get("rates") or {}).items():
+        exp = expected.get(k, 0.0)
         frac = v / exp if exp > 0 else 1.0
         worst = min(worst, frac)
         j = judge_rate(v, exp)
@@ -167,13 +195,14 @@ def _rated(res: Dict[str, Any], rates: Dict[str, float], expected: Dict[str, flo
             problems.append(txt)
         elif j == "degraded":
             slow.append(txt)
-    if not numerics_ok:
-        problems.insert(0, numerics_detail)
+    if res.get("numerics"):
+        problems.insert(0, res["numerics"])
+    notes = _notes(res)
     res["pass"] = not problems
-    res["degraded"] = bool(slow) and not problems
-    res["fraction"] = round(worst, 3)
-    res["expect"] = {k: round(v, 3) for k, v in expected.items()}
-    res["detail"] = "; ".join(problems or slow)
+    res["degraded"] = bool(slow or notes) and not problems
+    res["fraction"] = round(worst, 3) if worst < 1e9 else 1.0
+    res["detail"] = "; ".join(problems or (slow + notes))
+    res.pop("peers", None)
     return res
 
 
@@ -604,9 +633,9 @@ def _lag_notes(where: Dict[str, Any], what: str) -> List[str]:
 
 def _lag_verdict(res: Dict[str, Any], where: Dict[str, Any], what: str) -> Dict[str, Any]:
     notes = _lag_notes(where, what)
-    if res["pass"] and notes:
-        res["degraded"] = True
-        res["detail"] = "; ".join(x for x in [res["detail"]] + notes if x)
+    if notes:
+        res["lag"] = notes
+        judge_absolute(res)
     return res
 
 
@@ -690,11 +719,9 @@ def hbm_xcd(device: int = 0, slice_mib: int = 256, passes: int = 4, blocks_per_c
             notes.append(f"xcd{slow} reads HBM at {per[slow]:.2f} TB/s alone, {per[slow] / med:.2f}x the median XCD")
     wrong = f"{errs.value} wrong words on " + ", ".join(where.get("bad_cus", [])[:4]) if errs.value else ""
     res["wall_s"] = round(time.perf_counter() - t0, 3)
-    res = _rated(res, rates, exp, "TB/s", not errs.value, wrong)
-    if res["pass"] and notes:
-        res["degraded"] = True
-        res["detail"] = "; ".join(x for x in [res["detail"]] + notes if x)
-    return res
+    if notes:
+        res["lag"] = notes
+    return _rated(res, rates, exp, "TB/s", not errs.value, wrong)
 
 
 def host_link(device: int = 0, mib: int = 256, iters: int = 5, scale: Scale = FULL) -> Dict[str, Any]:
@@ -830,7 +857,7 @@ def _slow_only(res: Dict[str, Any]) -> bool:
     second measurement."""
     lagging = bool(_lag_notes(res.get("map") or {}, "")) or (res.get("slowest_xcd_rel") or 1.0) < XCD_ALONE_MIN_RATIO
     return (res.get("degraded") or not res.get("pass")) \
-        and (res.get("fraction", 1.0) < DEGRADED_FRACTION or lagging) \
+        and (res.get("fraction", 1.0) < DEGRADED_FRACTION or lagging) and not res.get("numerics") \
         and not any(w in res.get("detail", "") for w in ("wrong results", "err ", "checksums"))
 
 
@@ -942,6 +969,8 @@ def render_text(out: Dict[str, Any]) -> str:
     for test, r in (out.get("fabric") or {}).items():
         state = "FAIL" if not r.get("pass") else "pass"
         lines.append(f"fabric {test:<5} {state:<9} {_summary(test, r)}" + (f"  {r['detail']}" if r.get("detail") else ""))
+    for w in (out.get("node") or {}).get("warnings") or []:
+        lines.append(f"node   DEGRADED  {w}")
     lines.append(f"result: {'PASS' if out.get('pass') else 'FAIL'}")
     return "\n".join(lines) + "\n"
 
@@ -1023,8 +1052,13 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
     failures: List[Dict[str, Any]] = []
     failed_rounds = 0
     degraded: Dict[int, Dict[str, int]] = {d: {} for d in devices}  # rounds a test passed only as degraded
+    from ..models.peers import judge_node
+    node_rounds: Dict[str, int] = {}  # rounds with a node-wide shortfall, per test.metric
     while True:
         res = run_devices(level, devices, parallel)
+        for f in judge_node(res):  # each round's GPUs against each other, as the agent judges them
+            key = f"{f['test']}.{f['metric']}"
+            node_rounds[key] = node_rounds.get(key, 0) + 1
         rounds += 1
         bad: List[str] = []
         for d, tests in res.items():
@@ -1055,7 +1089,7 @@ def burn_in(level: int, devices: List[int], minutes: float, parallel: int = 8,
                    for k, v in m.items()} for d, m in series.items()}
     return {"minutes": minutes, "rounds": rounds, "failed_rounds": failed_rounds, "wall_s": round(clock() - t0, 1),
             "pass": failed_rounds == 0, "failures": failures, "devices": summary,
-            "degraded_rounds": {d: v for d, v in degraded.items() if v}}
+            "degraded_rounds": {d: v for d, v in degraded.items() if v}, "node_degraded_rounds": node_rounds}
 
 
 def main(argv=None) -> int:
@@ -1111,7 +1145,11 @@ def main(argv=None) -> int:
             print(json.dumps(b, indent=1))
         return 0 if b["pass"] else 1
     results = run_devices(args.level, devices, max(1, args.parallel))
+    from ..models.peers import finding_text, judge_node
+    findings = judge_node(results)  # GPUs measured together: each against the others (lone: the references)
     out: Dict[str, Any] = {"devices": {d: {"info": device_info(d), "tests": results[d]} for d in devices}}
+    if findings:
+        out["node"] = {"findings": findings, "warnings": [finding_text(f) for f in findings]}
     ok = all(t.get("pass") for d in out["devices"].values() for t in d["tests"].values())
     if args.level >= 2 and (args.p2p or args.rccl):
         out["fabric"] = fabric_tests(devices, args.p2p, args.rccl, args.timeout or None)

@@ -468,3 +468,19 @@ def test_level2_overlay_keeps_the_comgr_cache_and_sizes_both_containers():
         assert env["AMD_COMGR_CACHE_DIR"].startswith(mount)
     vol = next(v for v in patch["spec"]["template"]["spec"]["volumes"] if v["name"] == "comgr-cache")
     assert vol["hostPath"]["type"] == "DirectoryOrCreate"
+
+
+def test_agent_baseline_file_is_on_a_writable_host_volume():
+    """--diag-baseline-file must sit on a mounted hostPath (the root filesystem is read-only) so each GPU's
+    self-baseline survives agent restarts; the level-2 overlay keeps the same file."""
+    ds = next(d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
+    pod = ds["spec"]["template"]["spec"]
+    c = pod["containers"][0]
+    overlay = yaml.safe_load(_read(os.path.join(REPO, "deploy", "level2", "daemonset-level2.yaml")))
+    for cmd in (c["command"], _agent_container(overlay)["command"]):
+        path = agent.build_parser().parse_args(cmd[1:]).diag_baseline_file
+        assert path == "/var/lib/mi355x-node-agent/baseline.json"
+        mount = next(m for m in c["volumeMounts"] if m["mountPath"] == os.path.dirname(path))
+        assert not mount.get("readOnly")
+        vol = next(v for v in pod["volumes"] if v["name"] == mount["name"])
+        assert vol["hostPath"] == {"path": os.path.dirname(path), "type": "DirectoryOrCreate"}

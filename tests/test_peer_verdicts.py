@@ -1,0 +1,218 @@
+"""Peer-relative and self-baselined diagnostic verdicts (models/peers.py, models/baseline.py) through whole agent
+cycles on the fake C ABI of libmi355x_diag.so (testing/fake_native.py).
+
+The reference's verdict is a stable binary read off the node (/root/reference/check-gpu-node.py:172-178); here
+a node's GPUs are judged against each other, so a platform slower than the box the absolute references were
+measured on is one node-level warning, while one GPU slower than its peers still fails, by name.
+"""
+import json
+
+import pytest
+
+from k8s_gpu_node_checker_amd.agent import agent as A
+from k8s_gpu_node_checker_amd.models import baseline as B
+from k8s_gpu_node_checker_amd.models import health as H
+from k8s_gpu_node_checker_amd.models import peers as P
+from k8s_gpu_node_checker_amd.ops import amdsmi_probe, diag, fabric
+from k8s_gpu_node_checker_amd.testing import fixtures
+from k8s_gpu_node_checker_amd.testing.fake_native import FakeDiagLib, FakeFabricLib
+
+RATE_TESTS = ("gemm", "gemm_fp8", "hbm", "hbm_xcd", "mfma", "l2")
+
+
+@pytest.fixture
+def node(monkeypatch):
+    """``node(n, **FakeDiagLib kwargs)`` -> the fake library of an n x MI355X node (all idle)."""
+    def install(n=8, **kw):
+        lib = FakeDiagLib(n=n, **kw)
+        monkeypatch.setattr(diag, "lib", lambda: lib)
+        monkeypatch.setattr(fabric, "_lib", FakeFabricLib())
+        monkeypatch.setattr(amdsmi_probe, "probe", lambda nd, src, fx: fixtures.mi355x_probe_report(nd, gpus=n))
+        return lib
+    return install
+
+
+def _agent(n, level=1, **kw):
+    return A.Agent("n", source="fake", diag_level=level, expect_gpus=n, diag_timeout=60, **kw)
+
+
+def test_eight_gpus_alike_at_088_are_one_node_level_warning(node):
+    node(8, rate=0.88)
+    rep = _agent(8).probe_once()
+    v = H.evaluate_report(rep, 8)
+    assert rep["state"] == v.state == H.DEGRADED and v.reasons == []
+    assert (v.gpus_ok, v.gpus_seen) == (8, 8)
+    # no GPU is singled out: every per-GPU rate test passed, not degraded, judged against its peers
+    for g in rep["gpus"]:
+        for t in RATE_TESTS:
+            r = g["diag"][t]
+            assert r["pass"] and not r.get("degraded") and r["peers"]["gpus"] == 8, (g["index"], t, r)
+    node_warn = [w for w in v.warnings if w.startswith("node-wide: ")]
+    assert node_warn and not [w for w in v.warnings if not w.startswith("node-wide: ")], v.warnings
+    assert any("diag gemm tflops at 88% of the MI355X reference on all 8 GPUs alike" in w for w in node_warn)
+    assert {f["test"] for f in rep["diag_node"]["findings"]} >= {"gemm", "gemm_fp8", "hbm", "mfma", "l2"}
+
+
+def test_a_node_wide_shortfall_under_the_floor_is_never_unhealthy(node):
+    node(8, rate=0.70)
+    rep = _agent(8).probe_once()
+    v = H.evaluate_report(rep, 8)
+    assert v.state == H.DEGRADED and not v.reasons
+    assert all(f["below_floor"] for f in rep["diag_node"]["findings"])
+    assert H.condition_for(v)["status"] == "True"  # degraded still counts as Ready
+
+
+def test_one_gpu_at_080_of_its_peers_is_unhealthy_by_name(node):
+    node(8, gpu_rate={3: 0.80})
+    rep = _agent(8).probe_once()
+    v = H.evaluate_report(rep, 8)
+    assert v.state == H.UNHEALTHY and (v.gpus_ok, v.gpus_seen) == (7, 8)
+    assert v.reasons and all(r.startswith("gpu3: diag ") for r in v.reasons), v.reasons
+    gemm = next(r for r in v.reasons if r.startswith("gpu3: diag gemm failed"))
+    assert "80% of the node's other GPUs' median" in gemm
+    assert "diag_node" not in rep  # the other seven are at the reference
+    assert all(g["diag"]["gemm"]["pass"] for g in rep["gpus"] if g["index"] != 3)
+
+
+def test_one_gpu_behind_peers_on_a_slow_platform_still_fails(node):
+    """Peers at 0.90 of the references, gpu5 at 0.72: gpu5 fails (80 % of its peers) while the other seven
+    share one node-level warning -- the slow platform excuses the node, not the outlier."""
+    node(8, rate=0.90, gpu_rate={5: 0.72})
+    rep = _agent(8).probe_once()
+    v = H.evaluate_report(rep, 8)
+    assert v.state == H.UNHEALTHY and all(r.startswith("gpu5: ") for r in v.reasons)
+    assert any(w.startswith("node-wide: diag gemm tflops at 90%") for w in v.warnings)
+
+
+def test_a_majority_of_slow_gpus_falls_back_to_the_references(node):
+    """Five of eight at half rate: no clear outlier (the slow GPUs are each other's peers) and the GPUs
+    disagree, so each is judged absolutely -- the five fail, the three at the reference pass."""
+    node(8, gpu_rate={d: 0.5 for d in range(5)})
+    rep = _agent(8).probe_once()
+    v = H.evaluate_report(rep, 8)
+    assert v.state == H.UNHEALTHY and (v.gpus_ok, v.gpus_seen) == (3, 8)
+    assert {r.split(":")[0] for r in v.reasons} == {f"gpu{d}" for d in range(5)}
+    assert "diag_node" not in rep
+
+
+def test_a_lone_gpu_is_judged_as_before(node):
+    node(1, rate=0.88)
+    rep = _agent(1).probe_once()
+    v = H.evaluate_report(rep, 1)
+    assert v.state == H.DEGRADED and "diag_node" not in rep
+    assert any(w.startswith("gpu0: diag gemm slow (tflops") for w in v.warnings)
+    assert "peers" not in rep["gpus"][0]["diag"]["gemm"]
+    node(1, rate=0.80)
+    v = H.evaluate_report(_agent(1).probe_once(), 1)
+    assert v.state == H.UNHEALTHY and any(r.startswith("gpu0: diag gemm failed (tflops") for r in v.reasons)
+
+
+def test_two_gpus_the_slower_is_the_outlier(node):
+    node(2, gpu_rate={1: 0.80})
+    rep = _agent(2).probe_once()
+    v = H.evaluate_report(rep, 2)
+    assert v.state == H.UNHEALTHY and all(r.startswith("gpu1: ") for r in v.reasons)
+
+
+def test_numerics_failures_are_not_excused_by_peers(node):
+    node(8, rate=0.88, gemm_bad_tiles={(2, "gemm"): {4: 1}})
+    rep = _agent(8).probe_once()
+    v = H.evaluate_report(rep, 8)
+    assert v.state == H.UNHEALTHY
+    assert [r.split(" (")[0] for r in v.reasons] == ["gpu2: diag gemm failed"]
+    assert "checksums" in v.reasons[0]
+
+
+def test_judgement_is_idempotent_and_recovers_when_peers_leave():
+    """judge_node re-derives every verdict from the raw fields: judging twice changes nothing, and a result
+    left without peers goes back to the absolute references."""
+    def res(frac):
+        return diag._rated({}, {"tflops": 1228.0 * frac}, {"tflops": 1228.0}, "TFLOP/s")
+    pool = {d: {"gemm": res(0.88)} for d in range(4)}
+    f1 = P.judge_node(pool)
+    snap = json.dumps(pool, sort_keys=True)
+    f2 = P.judge_node(pool)
+    assert f1 == f2 and json.dumps(pool, sort_keys=True) == snap
+    assert all(r["gemm"]["pass"] and not r["gemm"]["degraded"] for r in pool.values())
+    lone = {0: pool[0]}
+    assert P.judge_node(lone) == []
+    assert lone[0]["gemm"]["degraded"] and "peers" not in lone[0]["gemm"]
+
+
+def test_peer_ratios_compare_partitions_by_their_own_references():
+    """A CPX partition (1/8 of the CUs, 1/8 the reference) next to a full GPU of the same node: compared as
+    fractions of their own scaled references, both at 100 %."""
+    full = diag._rated({}, {"tflops": 1228.0}, {"tflops": 1228.0}, "TFLOP/s")
+    part = diag._rated({}, {"tflops": 153.5}, {"tflops": 153.5}, "TFLOP/s")
+    P.judge_node({0: {"gemm": full}, 1: {"gemm": part}})
+    assert full["pass"] and part["pass"] and part["peers"]["ratio"]["tflops"] == 1.0
+
+
+def test_mi355x_diag_cli_judges_devices_together(node, capsys):
+    node(4, rate=0.88)
+    assert diag.main(["--level", "1"]) == 0
+    out = json.loads(capsys.readouterr().out)
+    assert out["pass"] and out["node"]["findings"]
+    assert all(t["pass"] and not t.get("degraded") for d in out["devices"].values() for t in d["tests"].values())
+    node(4, gpu_rate={2: 0.8})
+    assert diag.main(["--level", "1", "--format", "text"]) == 1
+    text = capsys.readouterr().out
+    assert "of the node's other GPUs' median" in text and "result: FAIL" in text
+
+
+# --- self-baselines ----------------------------------------------------------------------------------------
+
+def test_baseline_forms_from_clean_runs_then_flags_drift(node, tmp_path):
+    """A fast node (1.10 of the references) forms each GPU's baseline over its first 5 clean cycles; when
+    every GPU then drops to 0.96 -- above the references, alike across the node, so neither the absolute nor
+    the peer judgement objects -- each GPU is degraded for drifting to 87 % of its own baseline."""
+    lib = node(4, rate=1.10)
+    path = tmp_path / "baseline.json"
+    ag = _agent(4, diag_interval=0.0, baseline_file=str(path))
+    for _ in range(B.BASELINE_RUNS):
+        rep = ag.probe_once()
+        assert rep["state"] == H.HEALTHY
+    doc = json.loads(path.read_text())
+    assert doc["schema"] == B.SCHEMA and len(doc["gpus"]) == 4
+    entry = next(iter(doc["gpus"].values()))
+    assert entry["gemm@[4096,4096,4096]"]["baseline"]["tflops"] == pytest.approx(1.10, rel=1e-3)
+    lib.rate = 0.96
+    rep = ag.probe_once()
+    v = H.evaluate_report(rep, 4)
+    assert v.state == H.DEGRADED and not v.reasons and "diag_node" not in rep
+    drift = [w for w in v.warnings if "of this GPU's own baseline" in w]
+    assert {w.split(":")[0] for w in drift} == {f"gpu{d}" for d in range(4)}
+    assert any("gpu0: diag gemm slow (tflops at 87% of this GPU's own baseline (5 clean runs))" in w for w in drift)
+    # a restarted agent keeps the baselines (the file), so the drift is still seen
+    ag2 = _agent(4, diag_interval=0.0, baseline_file=str(path))
+    assert H.evaluate_report(ag2.probe_once(), 4).state == H.DEGRADED
+    # back to its own normal: clean again
+    lib.rate = 1.10
+    assert ag2.probe_once()["state"] == H.HEALTHY
+
+
+def test_unclean_runs_do_not_enter_the_baseline(node):
+    lib = node(2, rate=1.0, gpu_rate={1: 0.5})
+    ag = _agent(2, diag_interval=0.0)
+    for _ in range(B.BASELINE_RUNS):
+        ag.probe_once()
+    keys = {d: A.baseline_key(g, "", d) for d, g in enumerate(fixtures.mi355x_probe_report("n", gpus=2)["gpus"])}
+    assert ag.baselines.baseline(keys[0], "gemm", {"shape": [4096, 4096, 4096]}) is not None
+    assert ag.baselines.baseline(keys[1], "gemm", {"shape": [4096, 4096, 4096]}) is None  # failed every run
+
+
+def test_baselines_can_be_turned_off(node):
+    node(2)
+    ag = _agent(2, diag_baseline=False)
+    assert ag.probe_once()["state"] == H.HEALTHY and ag.baselines is None
+    args = A.build_parser().parse_args(["--node", "n", "--no-diag-baseline", "--diag-baseline-file", "/x"])
+    assert args.diag_baseline is False and args.diag_baseline_file == "/x"
+
+
+def test_unreadable_baseline_file_starts_empty(tmp_path):
+    p = tmp_path / "b.json"
+    p.write_text("{not json")
+    b = B.Baselines(str(p))
+    assert b.data == {}
+    p.write_text(json.dumps({"schema": "other", "gpus": {"x": {}}}))
+    assert B.Baselines(str(p)).data == {}
