@@ -21,6 +21,11 @@ annotation -> JSON report rendered -> exit code.  Nothing is cached between
 steps.  ``--mode sweep`` additionally re-probes every GPU and re-PATCHes its
 annotation inside each step.
 
+Untimed extras (coldstart runs, the agent's diagnostics, the RCCL fabric check and the multi-GPU node
+cycle) share one wall-clock budget (``--extras-budget``, 180 s from start): an extra that would not fit in
+what is left is recorded as ``{"skipped": "budget"}``, the node-cycle child is killed at the budget, and the
+timed loop never waits on any of them.  Every phase's wall time is in the line (``phases_s``).
+
 Prints ONE JSON line (rank 0): value = nodes/s over the whole job.
 """
 
@@ -81,20 +86,58 @@ def _fabric_check(world, local_rank, cuda):
         return {"backend": "nccl(rccl)" if cuda else "gloo", "pass": False, "detail": f"{type(e).__name__}: {e}"}
 
 
-def _node_cycle(world: int, timeout_s: float = 150.0) -> dict:
+class Budget:
+    """Wall clock left for the untimed extras (from process start) and the phases' wall times."""
+
+    def __init__(self, total_s: float):
+        self.total = total_s
+        self.t0 = time.monotonic()
+        self.phases: dict = {}
+
+    def left(self) -> float:
+        return self.total - (time.monotonic() - self.t0)
+
+    def fits(self, need_s: float) -> bool:
+        """Whether an extra that needs ``need_s`` may start (a small budget scales the need down with it)."""
+        return self.left() >= min(need_s, 0.25 * self.total) and self.left() > 0
+
+    class _Phase:
+        def __init__(self, b: "Budget", name: str):
+            self.b, self.name = b, name
+
+        def __enter__(self):
+            self.t = time.monotonic()
+
+        def __exit__(self, *exc):
+            self.b.phases[self.name] = round(self.b.phases.get(self.name, 0.0) + time.monotonic() - self.t, 3)
+
+    def phase(self, name: str) -> "Budget._Phase":
+        return Budget._Phase(self, name)
+
+
+# the least budget an extra must have left to start (s): RCCL's first communicator loads comgr cold
+FABRIC_MIN_S = 60.0
+NODE_CYCLE_MIN_S = 30.0
+AGENT_DIAG_MIN_S = 10.0
+COLDSTART_MIN_S = 5.0
+
+
+def _node_cycle(world: int, timeout_s: float = 150.0, cmd: "list | None" = None, kill_after_s: "float | None" = None) -> dict:
     """Untimed, rank 0, world > 1 on GPUs: the node agent's multi-device cycle over every GPU of the job
     (``agent/node_cycle.py``: per-device diagnostic threads at once, xGMI pair matrix, in-process RCCL suite
     under its deadline) in a child process with a time limit, so a failure there is reported in the bench
     line and never costs the benchmark.  The other ranks wait on a CPU (gloo) barrier meanwhile: no spinning
     collective kernel on their GPUs."""
-    cmd = [sys.executable, "-m", "k8s_gpu_node_checker_amd.agent.node_cycle", "--devices",
-           ",".join(str(d) for d in range(world)), "--level", "1", "--timeout", str(timeout_s)]
+    cmd = cmd or [sys.executable, "-m", "k8s_gpu_node_checker_amd.agent.node_cycle", "--devices",
+                  ",".join(str(d) for d in range(world)), "--level", "1", "--timeout", str(round(timeout_s, 1))]
     env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    limit = kill_after_s if kill_after_s is not None else 2 * timeout_s + 60
     t = time.perf_counter()
     try:
-        p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=2 * timeout_s + 60)
+        p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=limit)
     except subprocess.TimeoutExpired:
-        return {"pass": False, "detail": f"node cycle did not finish within {2 * timeout_s + 60:g} s"}
+        return {"pass": False, "killed": "budget", "child_wall_s": round(time.perf_counter() - t, 2),
+                "detail": f"node cycle did not finish within the {limit:.0f} s left of the extras budget"}
     line = next((x for x in reversed(p.stdout.splitlines()) if x.startswith("{")), None)
     if p.returncode != 0 or line is None:
         return {"pass": False, "rc": p.returncode, "detail": (p.stderr or p.stdout)[-400:]}
@@ -151,7 +194,14 @@ def main() -> int:
                     help="skip the untimed all-reduce fabric check (world > 1)")
     ap.add_argument("--no-node-cycle", dest="node_cycle", action="store_false",
                     help="skip the untimed multi-GPU node-agent cycle (world > 1 on GPUs)")
+    ap.add_argument("--extras-budget", type=float, default=180.0, metavar="S",
+                    help="wall clock for all untimed extras together (coldstart, agent diagnostics, fabric check, "
+                         "node cycle); what does not fit is skipped and recorded (default 180)")
+    # tests: run the node cycle without GPUs / replace its command (e.g. a child that sleeps past the budget)
+    ap.add_argument("--node-cycle-always", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--node-cycle-cmd", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    budget = Budget(args.extras_budget)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -162,6 +212,8 @@ def main() -> int:
     # --- control-plane processes first: nothing below has touched the GPU yet
     procs = []
     ctrl = {}
+    control = budget.phase("control_plane")
+    control.__enter__()
     if rank == 0:
         # nodes beyond the GPU count start with a recorded MI355X probe (condition + annotation, gzip-encoded
         # as the DaemonSet writes it); the ranks' own nodes get their live probe PATCHed below
@@ -174,10 +226,15 @@ def main() -> int:
             p, sinfo = _spawn("k8s_gpu_node_checker_amd.testing.webhook_sink")
             procs.append(p)
             ctrl["slack"] = sinfo["url"] + "/200"
+    control.__exit__(None, None, None)
     if rank == 0 and args.coldstart_runs > 0:
-        ctrl["coldstart"] = _coldstart(ctrl["api"], args.coldstart_runs)
+        if budget.fits(COLDSTART_MIN_S):
+            with budget.phase("coldstart"):
+                ctrl["coldstart"] = _coldstart(ctrl["api"], args.coldstart_runs)
+        else:
+            ctrl["coldstart"] = {"skipped": "budget"}
     try:
-        return _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl)
+        return _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget)
     finally:
         for p in procs:
             p.terminate()
@@ -187,7 +244,9 @@ def main() -> int:
                 p.kill()
 
 
-def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
+def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
+    init = budget.phase("init")  # torch import, process group, control-plane broadcast
+    init.__enter__()
     import torch
     import torch.distributed as dist
 
@@ -221,16 +280,34 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
         if cuda:
             torch.cuda.synchronize()
 
+    def agree(flag: bool) -> bool:
+        """Rank 0's decision for every rank (an extra that involves all of them runs everywhere or nowhere)."""
+        if world <= 1:
+            return flag
+        box = [flag]
+        dist.broadcast_object_list(box, src=0, group=group)
+        return bool(box[0])
+
     cluster = ClusterConnection(ctrl["api"])
     node = f"mi355x-node-{rank:04d}"
+    init.__exit__(None, None, None)
+    skipped = {}
 
     # --- node agent on this rank's GPU: probe (+ diagnostics), publish annotation
     # diag_when="always": this process is the GPU's only user and runs the diagnostics on purpose
     # the DaemonSet's publishing configuration (deploy/daemonset.yaml: gzip-encoded report annotation)
-    agent = Agent(node, source="auto", diag_level=args.diag_level if cuda else 0,
-                  devices=[local_rank] if cuda else [], diag_when="always", annotation_encoding="gzip")
+    # The diagnostics get what is left of the extras budget as their watchdog (a GPU still running then is
+    # reported failed and the bench goes on); with less than AGENT_DIAG_MIN_S left only the probe runs.
+    diag_level = args.diag_level if cuda else 0
+    if diag_level and not agree(budget.fits(AGENT_DIAG_MIN_S)):
+        diag_level = 0
+        skipped["agent_diag"] = "budget"
+    agent = Agent(node, source="auto", diag_level=diag_level,
+                  devices=[local_rank] if cuda else [], diag_when="always", annotation_encoding="gzip",
+                  diag_timeout=max(AGENT_DIAG_MIN_S, min(300.0, budget.left())))
     t0 = time.perf_counter()
-    rep = agent.probe_once()
+    with budget.phase("agent_cycle"):
+        rep = agent.probe_once()
     probe_source = rep.get("probe")
     if rep.get("error") or not rep.get("gpus"):
         # no amdgpu driver (CPU CI): publish a recorded MI355X report instead, and say so
@@ -239,18 +316,33 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
     else:
         rep["gpus"] = _own_gpu(rep["gpus"], local_rank, cuda)
     probe_ms = (time.perf_counter() - t0) * 1e3
-    with KubeClient(cluster) as kc:
+    with budget.phase("publish"), KubeClient(cluster) as kc:
         agent.publish(kc, rep, force=True)  # AMDGPUHealthy NodeCondition + full report annotation
     diag = {}
     for g in rep.get("gpus") or []:
         diag = g.get("diag") or {}
-    fabric = _fabric_check(world, local_rank, cuda) if world > 1 and args.fabric_check else None
+    if skipped.get("agent_diag"):
+        diag = {"skipped": "budget"}
+    fabric = None
+    if world > 1 and args.fabric_check:
+        if agree(budget.fits(FABRIC_MIN_S)):
+            with budget.phase("fabric"):
+                fabric = _fabric_check(world, local_rank, cuda)
+        else:
+            fabric = {"skipped": "budget"}
     node_cycle = None
-    if world > 1 and cuda and args.node_cycle:
-        dist.barrier(group=group)  # CPU barrier: every rank's own setup is done, its GPU idle
-        if rank == 0:
-            node_cycle = _node_cycle(world)
-        dist.barrier(group=group)
+    if world > 1 and args.node_cycle and (cuda or args.node_cycle_always):
+        if agree(budget.fits(NODE_CYCLE_MIN_S)):
+            dist.barrier(group=group)  # CPU barrier: every rank's own setup is done, its GPU idle
+            with budget.phase("node_cycle"):
+                if rank == 0:
+                    left = budget.left()
+                    node_cycle = _node_cycle(world, timeout_s=min(150.0, max(5.0, (left - 10.0) / 2)),
+                                             cmd=args.node_cycle_cmd.split() if args.node_cycle_cmd else None,
+                                             kill_after_s=max(1.0, left))
+            dist.barrier(group=group)
+        else:
+            node_cycle = {"skipped": "budget"}
     barrier()
 
     opts = CheckOptions(json=True, page_size=args.page_size, health_policy="auto",
@@ -273,9 +365,10 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
         return None
 
     last = None
-    for _ in range(args.warmup):
-        last = step()
-    barrier()
+    with budget.phase("warmup"):
+        for _ in range(args.warmup):
+            last = step()
+        barrier()
     lat = []
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -284,6 +377,7 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
         lat.append(time.perf_counter() - s)
     barrier()
     elapsed = time.perf_counter() - t_start
+    budget.phases["timed"] = round(elapsed, 3)
 
     if world > 1:
         import torch as _t
@@ -332,6 +426,14 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl) -> int:
             "probe": {"source": probe_source, "setup_ms": round(probe_ms, 1), "diag": diag},
             "fabric": fabric,
             "node_cycle": node_cycle,
+            "phases_s": budget.phases,
+            "extras_budget_s": {"budget": budget.total,
+                                "used": round(sum(v for k, v in budget.phases.items()
+                                                  if k in ("coldstart", "agent_cycle", "fabric", "node_cycle")), 3),
+                                "skipped": sorted(k for k, v in (("coldstart", ctrl.get("coldstart")),
+                                                                 ("agent_diag", diag), ("fabric", fabric),
+                                                                 ("node_cycle", node_cycle))
+                                                  if isinstance(v, dict) and v.get("skipped") == "budget")},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

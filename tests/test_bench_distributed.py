@@ -5,6 +5,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -90,3 +91,40 @@ def test_collective_verdict_logic():
     assert not verdict([dict(rows[0], correct=False)], 8, 1)["pass"]
     bad = verdict(rows + [{"op": "all_to_all", "bytes": 1 << 20, "busbw_gbps": 9.0, "correct": False}], 8, 40)
     assert not bad["pass"] and bad["detail"] == "result mismatch: all_to_all"
+
+
+def _torchrun(n, *extra, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"), "--gpus", str(n),
+           "--steps", "20", "--warmup", "2", "--coldstart-runs", "2", *extra]
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env(), cwd=REPO)
+
+
+def test_bench_kills_a_node_cycle_that_outlives_the_extras_budget(tmp_path):
+    """A node cycle that would run for minutes is killed when the extras budget runs out; the timed loop
+    still runs and the line prints with check_ok, every phase's wall time and the kill recorded."""
+    sleeper = tmp_path / "sleepy_node_cycle.py"
+    sleeper.write_text("import time\ntime.sleep(600)\n")
+    t = time.monotonic()
+    p = _torchrun(2, "--extras-budget", "12", "--node-cycle-always", "--node-cycle-cmd", f"{sys.executable} {sleeper}")
+    wall = time.monotonic() - t
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = last_json(p.stdout)
+    assert d["check_ok"] and d["n_gpus"] == 2 and d["steps"] == 20
+    nc = d["node_cycle"]
+    assert nc["pass"] is False and nc["killed"] == "budget" and nc["child_wall_s"] < 12
+    assert set(d["phases_s"]) >= {"control_plane", "coldstart", "init", "agent_cycle", "publish", "fabric",
+                                  "node_cycle", "warmup", "timed"}
+    assert d["phases_s"]["node_cycle"] < 12 and d["extras_budget_s"]["budget"] == 12.0
+    assert wall < 120, wall
+
+
+def test_bench_with_no_budget_skips_every_extra_and_still_measures():
+    p = _torchrun(2, "--extras-budget", "0", "--node-cycle-always")
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = last_json(p.stdout)
+    assert d["check_ok"] and d["ms_per_step"] > 0
+    assert d["coldstart"] == {"skipped": "budget"}
+    assert d["fabric"] == {"skipped": "budget"} and d["node_cycle"] == {"skipped": "budget"}
+    assert set(d["extras_budget_s"]["skipped"]) == {"coldstart", "fabric", "node_cycle"}
+    assert "timed" in d["phases_s"] and "node_cycle" not in d["phases_s"]
