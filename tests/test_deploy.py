@@ -396,7 +396,8 @@ def test_policy_refuses_writes_to_other_nodes_and_other_fields():
     assert _admit(_req(), bad, old)[1] == "the MI355X node agent may only add or remove the amd.com/gpu-unhealthy taint"
     bad = copy.deepcopy(old)
     bad["spec"]["unschedulable"] = True
-    assert _admit(_req(), bad, old)[1] == "the MI355X node agent may not cordon, uncordon or re-address a Node"
+    assert _admit(_req(), bad, old)[1] == ("the MI355X node agent may only change the amd.com/gpu-unhealthy taint in a "
+                                           "Node's spec (no cordon, no re-addressing)")
     bad = copy.deepcopy(old)
     bad["status"]["conditions"][0] = dict(bad["status"]["conditions"][0], status="Unknown")  # the kubelet's Ready
     assert _admit(_req(sub="status"), bad, old)[0] is False
@@ -408,6 +409,155 @@ def test_policy_refuses_writes_to_other_nodes_and_other_fields():
         False, "the MI355X node agent may only post Events about its own Node")
     # other users are not this policy's business (the kubelet, an operator)
     assert _admit(_req(user="system:node:gpu-a"), bad, old) == (None, "")
+
+
+def _full_node():
+    """A Node carrying every optional spec / status / metadata field the policy guards."""
+    n = _node()
+    n["metadata"]["finalizers"] = ["example.com/decommission"]
+    n["metadata"]["ownerReferences"] = [{"apiVersion": "example.com/v1", "kind": "Machine", "name": "m-1",
+                                         "uid": "0000-1111"}]
+    n["spec"]["configSource"] = {"configMap": {"name": "kubelet", "namespace": "kube-system",
+                                               "kubeletConfigKey": "kubelet"}}
+    n["spec"]["externalID"] = "i-0123456789"
+    n["status"]["phase"] = "Running"
+    n["status"]["volumesInUse"] = ["kubernetes.io/csi/ebs.csi.aws.com^vol-1"]
+    n["status"]["volumesAttached"] = [{"name": "kubernetes.io/csi/ebs.csi.aws.com^vol-1", "devicePath": ""}]
+    n["status"]["config"] = {"active": {"configMap": {"name": "kubelet", "namespace": "kube-system"}}}
+    n["status"]["runtimeHandlers"] = [{"name": "runc", "features": {"recursiveReadOnlyMounts": True}}]
+    n["status"]["features"] = {"supplementalGroupsPolicy": True}
+    return n
+
+
+def _drop(path):
+    def f(n):
+        obj = n
+        for k in path[:-1]:
+            obj = obj[k]
+        del obj[path[-1]]
+    return f
+
+
+SPEC_MSG = "the MI355X node agent may only change the amd.com/gpu-unhealthy taint in a Node's spec (no cordon, no re-addressing)"
+STATUS_MSG = "the MI355X node agent may only change its AMDGPUHealthy condition in a Node's status"
+META_MSG = "the MI355X node agent may not change a Node's finalizers or ownerReferences"
+GUARDED = [  # (subresource, field, mutation, refusal): one refused agent write per guarded field
+    ("status", "addresses", lambda n: n["status"]["addresses"][0].update(address="10.66.0.1"), STATUS_MSG),
+    ("status", "nodeInfo", lambda n: n["status"]["nodeInfo"].update(kubeletVersion="v1.99.0"), STATUS_MSG),
+    ("status", "daemonEndpoints", lambda n: n["status"]["daemonEndpoints"]["kubeletEndpoint"].update(Port=1),
+     STATUS_MSG),
+    ("status", "images", lambda n: n["status"]["images"].pop(), STATUS_MSG),
+    ("status", "volumesInUse", _drop(["status", "volumesInUse"]), STATUS_MSG),
+    ("status", "volumesAttached", lambda n: n["status"]["volumesAttached"].append({"name": "x", "devicePath": ""}),
+     STATUS_MSG),
+    ("status", "phase", lambda n: n["status"].update(phase="Terminated"), STATUS_MSG),
+    ("status", "config", _drop(["status", "config"]), STATUS_MSG),
+    ("status", "runtimeHandlers", lambda n: n["status"]["runtimeHandlers"][0].update(name="kata"), STATUS_MSG),
+    ("status", "features", lambda n: n["status"]["features"].update(supplementalGroupsPolicy=False), STATUS_MSG),
+    ("status", "capacity", lambda n: n["status"]["capacity"].update(cpu="1"), STATUS_MSG),
+    ("status", "allocatable", _drop(["status", "allocatable"]), STATUS_MSG),
+    ("", "podCIDR", lambda n: n["spec"].update(podCIDR="10.0.0.0/8"), SPEC_MSG),
+    ("", "podCIDRs", lambda n: n["spec"]["podCIDRs"].append("fd00::/64"), SPEC_MSG),
+    ("", "providerID", _drop(["spec", "providerID"]), SPEC_MSG),
+    ("", "configSource", lambda n: n["spec"]["configSource"]["configMap"].update(name="evil"), SPEC_MSG),
+    ("", "externalID", lambda n: n["spec"].update(externalID="i-other"), SPEC_MSG),
+    ("", "unschedulable", lambda n: n["spec"].update(unschedulable=True), SPEC_MSG),
+    ("", "finalizers", lambda n: n["metadata"].update(finalizers=[]), META_MSG),
+    ("status", "finalizers", _drop(["metadata", "finalizers"]), META_MSG),
+    ("", "ownerReferences", lambda n: n["metadata"]["ownerReferences"].append(
+        {"apiVersion": "v1", "kind": "Pod", "name": "p", "uid": "u"}), META_MSG),
+]
+
+
+@pytest.mark.parametrize("sub,field,mutate,msg", GUARDED, ids=[f"{s or 'main'}-{f}" for s, f, _, _ in GUARDED])
+def test_policy_refuses_a_write_to_every_guarded_field(sub, field, mutate, msg):
+    old = _full_node()
+    assert _admit(_req(sub=sub), copy.deepcopy(old), old) == (True, "")  # the unchanged node is admitted
+    new = copy.deepcopy(old)
+    mutate(new)
+    assert new != old
+    assert _admit(_req(sub=sub), new, old) == (False, msg)
+    # a field that was absent and appears is refused as well
+    if field in ("phase", "externalID", "features"):
+        where = "status" if sub == "status" else "spec"
+        bare = copy.deepcopy(old)
+        del bare[where][field]
+        assert _admit(_req(sub=sub), old, bare) == (False, msg)
+
+
+def test_policy_header_names_every_guarded_field():
+    text = _read(os.path.join(REPO, "deploy", "agent-policy.yaml"))
+    header = text.split("apiVersion:")[0]
+    for _, field, _, _ in GUARDED:
+        assert field in header, field
+
+
+class _RecordingClient:
+    """The agent's KubeClient against the mock apiserver; each node write is recorded as (subresource, merged
+    Node after, Node before) -- what admission sees -- and each Event as posted."""
+
+    def __init__(self, kc, srv, node):
+        self.kc, self.srv, self.node = kc, srv, node
+        self.writes = []
+        self.events = []
+        self.calls = []
+
+    def _snap(self):
+        return copy.deepcopy(self.srv.state.find(self.node))
+
+    def __getattr__(self, name):
+        fn = getattr(self.kc, name)
+        sub = {"patch_node_condition": "status", "patch_node_annotations": "", "patch_node_labels": "",
+               "update_node_taints": ""}.get(name)
+        if name == "create_event":
+            def post(namespace, ev, *a, **kw):
+                self.events.append(copy.deepcopy(ev))
+                return fn(namespace, ev, *a, **kw)
+            return post
+        if sub is None:
+            return fn
+
+        def write(*a, **kw):
+            before = self._snap()
+            out = fn(*a, **kw)
+            self.calls.append(name)
+            self.writes.append((sub, self._snap(), before))
+            return out
+        return write
+
+
+def test_policy_admits_the_agents_real_patches_replayed_through_the_apiserver(mock_cluster):
+    """The agent's own condition, annotation (JSON and gzip), label, taint and Event writes -- healthy, then
+    an uncorrectable ECC error (unhealthy: taint added, labels and condition flip), then recovered -- on a Node
+    carrying every guarded field: each merged result is admitted."""
+    from k8s_gpu_node_checker_amd.kube.client import KubeClient
+    from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+    srv = mock_cluster([_full_node()])
+    healthy = fixtures.mi355x_probe_report("gpu-a", gpus=8)
+    sick = copy.deepcopy(healthy)
+    sick["gpus"][2]["ecc_uncorrectable"] = 4
+    kinds = set()
+    for encoding in ("json", "gzip"):
+        ag = agent.Agent("gpu-a", source="fixture", label_node=True, taint_unhealthy=True,
+                         annotation_encoding=encoding, expect_gpus=8)
+        with KubeClient(ClusterConnection(srv.url)) as kc:
+            rec = _RecordingClient(kc, srv, "gpu-a")
+            for rep in (healthy, sick, healthy):
+                rep = dict(rep, ts=__import__("time").time())
+                ag.publish(rec, rep, force=True)
+        assert set(rec.calls) == {"patch_node_condition", "patch_node_annotations", "patch_node_labels",
+                                  "update_node_taints"}, rec.calls
+        for sub, new, old in rec.writes:
+            assert new != old or sub == ""
+            assert _admit(_req(sub=sub), new, old) == (True, ""), (sub, encoding)
+            kinds.add(sub)
+        for ev in rec.events:
+            assert _admit(_req(resource="events", op="CREATE"), ev, None) == (True, "")
+        assert len(rec.events) >= 2
+    assert kinds == {"", "status"}
+    final = srv.state.find("gpu-a")
+    assert final["metadata"]["finalizers"] == ["example.com/decommission"]
+    assert not any(t["key"] == H.UNHEALTHY_TAINT["key"] for t in final["spec"].get("taints") or [])
 
 
 def test_cel_subset_semantics():
