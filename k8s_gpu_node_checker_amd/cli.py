@@ -76,6 +76,8 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
     ("x", "--explain", {"metavar": "NODE", "help": "한 노드가 Ready 로 집계되는(또는 안 되는) 이유를 출력"}),
     ("x", "--fleet", {"action": "store_true", "help": "MI355X 플릿 요약 (판정별 노드 수, 문제 노드, 드라이버/펌웨어 버전)"}),
     ("x", "--prometheus-textfile", {"help": "node-exporter textfile 메트릭 경로"}),
+    ("x", "--metrics-listen", {"metavar": "HOST:PORT",
+                               "help": "--watch-events: Prometheus /metrics 를 이 주소에서 제공 (예: 0.0.0.0:9465)"}),
     ("x", "--state-file", {"help": "직전 결과 저장 파일 (알림 중복 제거)"}),
     ("x", "--watch", {"type": float, "default": 0.0, "help": "N초마다 반복 점검 (0 = 한 번, 기본)"}),
     ("x", "--watch-count", {"type": int, "default": 0,
@@ -277,6 +279,13 @@ def _watch_events(args: Any) -> int:
         opts.slack_gate = lambda result: statefile.should_notify(memo["prev"], result, only,
                                                                  args.slack_on_node_change)
         opts.slack_only_on_error = False  # the gate decides (a recovery must be able to send)
+        metrics = None
+        if args.metrics_listen:
+            from .utils.prom import MetricsServer, parse_listen
+            metrics = MetricsServer(*parse_listen(args.metrics_listen)).start()
+            print(f"metrics: serving http://{args.metrics_listen.rpartition(':')[0] or '0.0.0.0'}:{metrics.port}"
+                  "/metrics", file=sys.stderr, flush=True)
+        elector = None
 
         def evaluate(scan):
             tr = Tracer() if (opts.trace or opts.json_extended) else NullTracer()
@@ -295,18 +304,35 @@ def _watch_events(args: Any) -> int:
             if args.prometheus_textfile:
                 from .utils.prom import write_textfile
                 write_textfile(args.prometheus_textfile, result)
+            if metrics is not None:
+                metrics.update(result)
+            if elector is not None:
+                # the last-notified outcome rides on the Lease: a replica taking over starts from it (no repeated
+                # alert, no lost recovery notice across a failover)
+                elector.publish_state(memo["prev"])
             last["code"] = result.exit_code
 
         if not args.leader_elect:
-            NodeWatcher(cluster, opts, debounce=args.watch_debounce).run(
-                evaluate, report, max_reports=args.watch_count, duration=args.watch_duration)
+            try:
+                NodeWatcher(cluster, opts, debounce=args.watch_debounce).run(
+                    evaluate, report, max_reports=args.watch_count, duration=args.watch_duration)
+            finally:
+                if metrics is not None:
+                    metrics.stop()
             return last["code"]
         elector = _start_elector(args, cluster)
+        if metrics is not None:
+            metrics.set_leader(False)
         try:
             while not elector.leading.wait(0.2):
                 pass
-            print(f"leader election: {elector.identity} leads {elector.namespace}/{elector.name}", file=sys.stderr,
-                  flush=True)
+            if elector.inherited_state is not None:
+                memo["prev"] = elector.inherited_state
+            if metrics is not None:
+                metrics.set_leader(True)
+            print(f"leader election: {elector.identity} leads {elector.namespace}/{elector.name}"
+                  + (" (resuming the previous leader's notification state)" if elector.inherited_state else ""),
+                  file=sys.stderr, flush=True)
             NodeWatcher(cluster, opts, debounce=args.watch_debounce).run(
                 evaluate, report, max_reports=args.watch_count, duration=args.watch_duration,
                 should_stop=lambda: not elector.is_leader())
@@ -318,6 +344,8 @@ def _watch_events(args: Any) -> int:
             return last["code"]
         finally:
             elector.stop()  # a holder releases the Lease: the next replica takes over without waiting it out
+            if metrics is not None:
+                metrics.stop()
     except KeyboardInterrupt:
         return last["code"]
     except Exception as e:

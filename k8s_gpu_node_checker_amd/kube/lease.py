@@ -16,6 +16,11 @@ Kubernetes component can share a Lease correctly:
 * a holder that stops cleanly releases the Lease (empty holder, duration 1 s) so the next replica need not
   wait for the lease to expire.
 
+The holder also keeps a small JSON state on the Lease (annotation ``STATE_ANNOTATION``, written with its
+renewals: :meth:`LeaderElector.publish_state`), and a replica that takes the Lease over reads it
+(:attr:`LeaderElector.inherited_state`).  The watcher keeps its last-notified outcome there, so a failover
+neither re-sends the alert the old leader already sent nor loses a recovery that happened during the handover.
+
 The reference has no counterpart: it is a one-shot script (``/root/reference/check-gpu-node.py:296-327``); this
 is what running its check as a long-lived, replicated Deployment needs (``deploy/watcher.yaml``).
 """
@@ -34,6 +39,7 @@ if TYPE_CHECKING:
 LEASE_DURATION_S = 15.0  # client-go defaults (kube-controller-manager, kube-scheduler)
 RENEW_DEADLINE_S = 10.0
 RETRY_PERIOD_S = 2.0
+STATE_ANNOTATION = "gpu-health.amd.com/leader-state"
 
 
 def _micro_time(epoch: float) -> str:
@@ -78,6 +84,11 @@ class LeaderElector:
         self._last_renew = 0.0
         self.transitions = 0
         self.last_error: Optional[str] = None
+        # the leader's shared state: what the holder writes with its renewals, what a new holder found there
+        self._state: Optional[str] = None
+        self._state_lock = threading.Lock()
+        self._wake = threading.Event()
+        self.inherited_state: Optional[Dict[str, Any]] = None
 
     # -- one round -------------------------------------------------------------------------------------
     def try_acquire_or_renew(self, client: "KubeClient") -> bool:
@@ -118,6 +129,12 @@ class LeaderElector:
         else:
             record["leaseTransitions"] = int(spec.get("leaseTransitions") or 0) + 1
         lease["spec"] = record
+        meta = lease.setdefault("metadata", {})
+        found = (meta.get("annotations") or {}).get(STATE_ANNOTATION)
+        with self._state_lock:
+            mine = self._state
+        if mine is not None:
+            meta["annotations"] = dict(meta.get("annotations") or {}, **{STATE_ANNOTATION: mine})
         try:
             client.request("PUT", _lease_path(self.namespace, self.name), json.dumps(lease).encode(),
                            content_type="application/json", idempotent=False)
@@ -127,6 +144,11 @@ class LeaderElector:
             raise
         if holder != self.identity:
             self.transitions += 1
+            try:  # what the previous holder left: this replica's starting point
+                state = json.loads(found) if isinstance(found, str) else None
+                self.inherited_state = state if isinstance(state, dict) else None
+            except ValueError:
+                self.inherited_state = None
         self._observe(tuple(record[k] for k in ("holderIdentity", "renewTime", "acquireTime", "leaseTransitions")))
         return True
 
@@ -178,7 +200,8 @@ class LeaderElector:
                 self._stop.wait(self.retry_period)
             # renew: give up when no round succeeded for renew_deadline
             while not self._stop.is_set() and self.leading.is_set():
-                self._stop.wait(self.retry_period)
+                self._wake.wait(self.retry_period)  # a new state to publish renews at once
+                self._wake.clear()
                 if self._stop.is_set():
                     break
                 started = self.clock()
@@ -198,9 +221,16 @@ class LeaderElector:
         self._thread.start()
         return self
 
+    def publish_state(self, state: Dict[str, Any]) -> None:
+        """Keep ``state`` (JSON) on the Lease: written by the next renewal, which is started right away."""
+        with self._state_lock:
+            self._state = json.dumps(state, sort_keys=True, separators=(",", ":"))
+        self._wake.set()
+
     def stop(self, timeout: float = 5.0) -> None:
         """Stop campaigning; a holder releases the Lease on the way out."""
         self._stop.set()
+        self._wake.set()
         if self._thread is not None:
             self._thread.join(timeout)
 

@@ -1,8 +1,15 @@
-"""Prometheus node-exporter textfile output (SURVEY §5 "Metrics": the reference has bare prints only).
+"""Prometheus metrics of the checker (SURVEY §5 "Metrics": the reference has bare prints only).
 
-Written atomically (temp file + ``rename``) so the textfile collector never
-reads a half-written file.  No ``prometheus_client`` import: the exposition
-format is a few lines of text.
+Two outputs of the same exposition text (:func:`render`):
+
+* a node-exporter textfile (``--prometheus-textfile``), written atomically (temp file + ``rename``) so the
+  textfile collector never reads a half-written file -- for the CronJob, whose pod is gone between runs;
+* an HTTP ``/metrics`` endpoint (``--metrics-listen``, :class:`MetricsServer`) for the long-running event
+  watcher (``--watch-events``, ``deploy/watcher.yaml``), scraped through its Service by a ServiceMonitor
+  (``deploy/monitoring/monitoring.yaml``).  With ``--leader-elect`` every replica serves
+  ``k8s_gpu_checker_leader`` (1 on the holder) and only the holder the cluster's gauges.
+
+No ``prometheus_client`` import: the exposition format is a few lines of text.
 """
 
 from __future__ import annotations
@@ -81,3 +88,85 @@ def write_error_textfile(path: str, message: str) -> None:
         f'k8s_gpu_checker_error{{message="{_esc(message[:200])}"}} 1',
         f"k8s_gpu_checker_last_run_timestamp_seconds {time.time():.3f}",
     ])
+
+
+LEADER_HELP = ["# HELP k8s_gpu_checker_leader 1 on the watcher replica that holds the leader Lease (it reports).",
+               "# TYPE k8s_gpu_checker_leader gauge"]
+
+
+class MetricsServer:
+    """``GET /metrics`` (the last rendered report, plus the leader gauge) and ``GET /healthz`` on a thread.
+
+    ``update(result)`` swaps in a new report's lines; ``set_leader(bool)`` the replica's role.  Before the first
+    report (or on a follower) only the leader gauge is served, so a scrape never shows a stale cluster."""
+
+    def __init__(self, host: str, port: int):
+        import threading
+        from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+        self._lock = threading.Lock()
+        self._lines: List[str] = []
+        self._leader: Any = None
+        outer = self
+
+        class Handler(BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+            timeout = 30
+
+            def log_message(self, *a: Any) -> None:
+                pass
+
+            def do_GET(self) -> None:  # noqa: N802
+                if self.path.split("?")[0] == "/metrics":
+                    body, ctype, code = outer.text().encode(), "text/plain; version=0.0.4; charset=utf-8", 200
+                elif self.path.split("?")[0] == "/healthz":
+                    body, ctype, code = b"ok\n", "text/plain", 200
+                else:
+                    body, ctype, code = b"not found\n", "text/plain", 404
+                self.send_response(code)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        self.httpd = ThreadingHTTPServer((host, port), Handler)
+        self.httpd.daemon_threads = True
+        self._thread = threading.Thread(target=self.httpd.serve_forever, kwargs={"poll_interval": 0.2},
+                                        name="metrics", daemon=True)
+
+    @property
+    def port(self) -> int:
+        return self.httpd.server_address[1]
+
+    def start(self) -> "MetricsServer":
+        self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self.httpd.shutdown()
+        self.httpd.server_close()
+
+    def update(self, result: Any) -> None:
+        lines = render(result)
+        with self._lock:
+            self._lines = lines
+
+    def set_leader(self, leading: bool) -> None:
+        with self._lock:
+            self._leader = bool(leading)
+            if not leading:
+                self._lines = []  # a follower serves no cluster gauges (the leader does)
+
+    def text(self) -> str:
+        with self._lock:
+            lines = list(self._lines)
+            if self._leader is not None:
+                lines += LEADER_HELP + [f"k8s_gpu_checker_leader {1 if self._leader else 0}"]
+        return "\n".join(lines) + "\n" if lines else "\n"
+
+
+def parse_listen(spec: str) -> "tuple[str, int]":
+    """``HOST:PORT`` / ``:PORT`` / ``[v6]:PORT`` -> (host, port); host defaults to all interfaces."""
+    host, sep, port = spec.rpartition(":")
+    if not sep or not port.isdigit():
+        raise ValueError(f"--metrics-listen {spec!r}: expected HOST:PORT")
+    return (host.strip("[]") or "0.0.0.0"), int(port)

@@ -179,12 +179,15 @@ def test_monitoring_rules_use_metrics_the_agent_emits():
     docs = [d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "monitoring", "monitoring.yaml"))) if d]
     kinds = {d["kind"] for d in docs}
     assert kinds == {"ServiceMonitor", "PrometheusRule"}
+    assert {d["metadata"]["name"] for d in docs if d["kind"] == "ServiceMonitor"} == {"mi355x-node-agent",
+                                                                                      "gpu-node-watcher"}
     fams = {f.name: f for f in text_string_to_metric_families(agent._metrics(_rich_report()))}
+    fams.update(_watcher_families())
     labels = {name: set().union(*(set(s.labels) for s in f.samples)) | {"node"} for name, f in fams.items()}
     rules = [r for d in docs if d["kind"] == "PrometheusRule" for grp in d["spec"]["groups"] for r in grp["rules"]]
     assert len(rules) >= 10
     for r in rules:
-        names = set(re.findall(r"\bmi355x_[a-z0-9_]+", r["expr"]))
+        names = set(re.findall(r"\b(?:mi355x|k8s_gpu_checker)_[a-z0-9_]+", r["expr"]))
         assert names, r["alert"]
         for n in names:
             assert n in fams, (r["alert"], n)
@@ -204,9 +207,98 @@ def test_monitoring_rules_use_metrics_the_agent_emits():
     svc = next(d for d in base if d["kind"] == "Service")
     assert svc["spec"]["selector"].items() <= pod_labels.items()
     assert {p["targetPort"] for p in svc["spec"]["ports"]} <= port_names
-    sm = next(d for d in docs if d["kind"] == "ServiceMonitor")
+    sm = next(d for d in docs if d["kind"] == "ServiceMonitor" and d["metadata"]["name"] == "mi355x-node-agent")
     assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
     assert {e["port"] for e in sm["spec"]["endpoints"]} <= {p["name"] for p in svc["spec"]["ports"]}
+
+
+def _watcher_families():
+    """The metric families the event watcher's /metrics serves (leader: report gauges + leader gauge)."""
+    import types
+
+    from prometheus_client.parser import text_string_to_metric_families
+    from k8s_gpu_node_checker_amd.models import health as H
+    from k8s_gpu_node_checker_amd.utils import prom
+    node = {"name": "n0", "ready": True, "gpus": 8, "gpu_breakdown": {"amd.com/gpu": 8}}
+    res = types.SimpleNamespace(gpu_nodes=[node], ready_gpu_nodes=[node], exit_code=0,
+                                verdicts=[H.Verdict(H.HEALTHY)], tracer=None)
+    srv = prom.MetricsServer("127.0.0.1", 0)
+    try:
+        srv.update(res)
+        srv.set_leader(True)
+        srv.update(res)
+        return {f.name: f for f in text_string_to_metric_families(srv.text())}
+    finally:
+        srv.httpd.server_close()
+
+
+def _all_deploy_docs():
+    for path in sorted(glob.glob(os.path.join(REPO, "deploy", "**", "*.yaml"), recursive=True)):
+        for d in yaml.safe_load_all(_read(path)):
+            if isinstance(d, dict) and "kind" in d:
+                yield os.path.relpath(path, REPO), d
+
+
+def _pod_of(doc):
+    spec = doc.get("spec") or {}
+    if doc["kind"] == "CronJob":
+        spec = spec["jobTemplate"]["spec"]
+    return spec.get("template")
+
+
+def test_every_metrics_output_in_deploy_has_a_consumer():
+    """Each metrics output a workload in deploy/ produces is read by something: an HTTP /metrics port is behind
+    a Service that a ServiceMonitor scrapes on that port; a --prometheus-textfile is on a volume another
+    container of the pod (a node-exporter) mounts.  No metrics written into the void."""
+    # kustomize patches (deploy/level2/) amend a base workload checked here in full: not workloads of their own
+    patches = {os.path.normpath(os.path.join(os.path.dirname(p), x["path"]))
+               for p, d in _all_deploy_docs() if d["kind"] == "Kustomization" for x in d.get("patches") or []}
+    docs = [(p, d) for p, d in _all_deploy_docs() if p not in patches]
+    services = [d for _, d in docs if d["kind"] == "Service"]
+    monitors = [d for _, d in docs if d["kind"] == "ServiceMonitor"]
+    outputs = 0
+    for path, d in docs:
+        tpl = _pod_of(d) if d["kind"] in ("DaemonSet", "Deployment", "CronJob", "Job") else None
+        if not tpl or "containers" not in (tpl.get("spec") or {}):
+            continue
+        pod, labels, ns = tpl["spec"], (tpl.get("metadata") or {}).get("labels") or {}, d["metadata"].get("namespace")
+        for c in pod["containers"]:
+            cmd = c.get("command") or []
+            ports, textfiles = [], []
+            if cmd and cmd[0] == "k8s-gpu-node-agent":
+                a = agent.build_parser().parse_args(cmd[1:])
+                if "http" in a.publish.split(","):
+                    ports.append(int(a.listen.rpartition(":")[2]))
+            elif cmd and cmd[0] == "check-gpu-node":
+                a = cli.parse_args(cmd[1:])
+                if a.metrics_listen:
+                    ports.append(int(a.metrics_listen.rpartition(":")[2]))
+                if a.prometheus_textfile:
+                    textfiles.append(a.prometheus_textfile)
+            for port in ports:
+                outputs += 1
+                named = {p["containerPort"]: p.get("name") for p in c.get("ports") or []}
+                assert port in named, (path, c["name"], port)
+                scraped = False
+                for svc in services:
+                    if svc["metadata"].get("namespace") != ns or not svc["spec"].get("selector"):
+                        continue
+                    if not svc["spec"]["selector"].items() <= labels.items():
+                        continue
+                    sports = [p["name"] for p in svc["spec"]["ports"] if p.get("targetPort") in (port, named[port])]
+                    for sm in monitors:
+                        if (sm["spec"]["selector"]["matchLabels"].items() <= (svc["metadata"].get("labels") or {}).items()
+                                and any(e["port"] in sports for e in sm["spec"]["endpoints"])):
+                            scraped = True
+                assert scraped, f"{path}: {c['name']} serves /metrics on {port} but no ServiceMonitor scrapes it"
+            for tf in textfiles:
+                outputs += 1
+                mine = [m for m in c.get("volumeMounts") or [] if tf.startswith(m["mountPath"].rstrip("/") + "/")]
+                assert mine, (path, tf, "textfile not on a volume")
+                readers = [o for o in pod["containers"] if o is not c
+                           and any(m["name"] == mine[0]["name"] for m in o.get("volumeMounts") or [])]
+                assert readers, f"{path}: {c['name']} writes {tf} but no container of the pod reads it"
+    assert outputs >= 2  # the agent's /metrics and the watcher's
 
 
 def test_grafana_dashboard_queries_series_that_exist():

@@ -119,16 +119,24 @@ def _watcher(kc, sink_url, ident, extra=()):
                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
 
 
+def _holder(srv):
+    return srv.leases.get(("gpu-health", "gpu-node-watcher"), {}).get("spec", {}).get("holderIdentity")
+
+
+def _stdout_reports(out):
+    return [json.loads(x + "\n}") for x in out.split("\n}\n") if x.strip()]
+
+
 def test_replicated_watchers_report_once_and_fail_over(mock_cluster, sink, tmp_path):
     """Two watcher replicas on one Lease: only the leader reports (one Slack message); when it stops, the
-    other takes over and reports the cluster once from its own LIST."""
+    other takes over, reports the cluster from its own LIST on stdout -- and does not repeat the Slack message
+    the old leader delivered (the last-notified outcome is on the Lease)."""
     srv = mock_cluster(fixtures.cluster(2, "amd"))
     kc = srv.kubeconfig(str(tmp_path / "kc"))
-    a = _watcher(kc, sink.url("ok"), "replica-a")
+    a = _watcher(kc, sink.url("200"), "replica-a")
     try:
-        assert _wait(lambda: srv.leases.get(("gpu-health", "gpu-node-watcher"), {}).get("spec", {})
-                     .get("holderIdentity") == "replica-a", 30.0)
-        b = _watcher(kc, sink.url("ok"), "replica-b")
+        assert _wait(lambda: _holder(srv) == "replica-a", 30.0)
+        b = _watcher(kc, sink.url("200"), "replica-b")
         try:
             assert _wait(lambda: len(sink.requests) >= 1, 30.0)
             time.sleep(1.5)
@@ -136,19 +144,71 @@ def test_replicated_watchers_report_once_and_fail_over(mock_cluster, sink, tmp_p
             a.terminate()  # SIGTERM: a releases the Lease on the way out
             a.wait(20)
             assert ("PUT", "gpu-node-watcher", "") in srv.lease_writes
-            assert _wait(lambda: srv.leases[("gpu-health", "gpu-node-watcher")]["spec"]["holderIdentity"]
-                         == "replica-b", 10.0)
+            assert _wait(lambda: _holder(srv) == "replica-b", 10.0)
+            time.sleep(1.5)
+            assert len(sink.requests) == 1  # nothing new to say: not sent again
+            srv.state.set_nodes(fixtures.cluster(3, "amd"))  # a change after the takeover is b's to send
             assert _wait(lambda: len(sink.requests) >= 2, 20.0)
-            time.sleep(1.0)  # the report's stdout follows its Slack POST (the reference's order)
+            time.sleep(0.5)
         finally:
             b.terminate()
             out_b, err_b = b.communicate(timeout=20)
-        assert "leader" in err_b
-        assert json.loads(out_b.split("\n}\n")[0] + "\n}")["total_nodes"] == 2
+        assert "resuming the previous leader's notification state" in err_b
+        reports = _stdout_reports(out_b)
+        assert [r["total_nodes"] for r in reports] == [2, 3]
     finally:
         if a.poll() is None:
             a.kill()
         a.communicate(timeout=20)
+
+
+def _handover(srv, kc, sink, mode, between):
+    """a leads and reports; a stops; ``between()`` changes the cluster while nobody leads; b takes over.
+    Returns (Slack POSTs while a led, Slack POSTs after b's first report)."""
+    extra = ("--slack-only-on-error", "--slack-on-node-change")
+    a = _watcher(kc, sink.url(mode), "replica-a", extra)
+    b = None
+    try:
+        assert _wait(lambda: _holder(srv) == "replica-a", 30.0)
+        assert _wait(lambda: srv.leases[("gpu-health", "gpu-node-watcher")]["metadata"].get("annotations"), 10.0)
+        time.sleep(0.5)
+        first = len(sink.requests)
+        a.terminate()
+        a.wait(20)
+        between()
+        b = _watcher(kc, sink.url(mode), "replica-b", extra)
+        assert _wait(lambda: _holder(srv) == "replica-b", 20.0)
+        time.sleep(2.0)
+        return first, len(sink.requests)
+    finally:
+        for p in (a, b):
+            if p is not None:
+                if p.poll() is None:
+                    p.terminate()
+                p.communicate(timeout=20)
+
+
+def test_failover_does_not_repeat_a_delivered_alert(mock_cluster, sink, tmp_path):
+    """a new leader used to start with no memory and re-send the current error alert."""
+    srv = mock_cluster(fixtures.golden("notready"))
+    kc = srv.kubeconfig(str(tmp_path / "kc"))
+    first, after = _handover(srv, kc, sink, "200", lambda: None)
+    assert first == 1 and after == 1
+
+
+def test_a_recovery_during_the_handover_is_announced(mock_cluster, sink, tmp_path):
+    srv = mock_cluster(fixtures.golden("notready"))
+    kc = srv.kubeconfig(str(tmp_path / "kc"))
+    first, after = _handover(srv, kc, sink, "200", lambda: srv.state.set_nodes(fixtures.golden("readme")))
+    assert first == 1 and after == 2
+    assert "Ready 상태의 GPU 노드: 2개" in json.loads(sink.requests[-1]["body"])["text"]
+
+
+def test_an_undelivered_alert_is_retried_by_the_next_leader(mock_cluster, sink, tmp_path):
+    srv = mock_cluster(fixtures.golden("notready"))
+    kc = srv.kubeconfig(str(tmp_path / "kc"))
+    first, after = _handover(srv, kc, sink, "500", lambda: None)
+    assert first >= 1 and after > first  # a's alert never arrived (HTTP 500): b sends it again
 
 
 def test_a_watcher_that_cannot_renew_stops_acting_and_exits(mock_cluster, sink, tmp_path):

@@ -7,6 +7,8 @@ import sys
 import threading
 import time
 
+import pytest
+
 from k8s_gpu_node_checker_amd.checker import CheckOptions, CheckResult, apply_health
 from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
 from k8s_gpu_node_checker_amd.kube.watch import NodeWatcher, outcome_signature
@@ -261,3 +263,77 @@ def test_cli_watch_events_slack_on_node_change(mock_cluster, sink, tmp_path):
     p.communicate(timeout=30)
     assert p.returncode == 0
     assert len(sink.requests) == 2
+
+
+def _scrape(port):
+    from k8s_gpu_node_checker_amd.utils.http import request
+    from prometheus_client.parser import text_string_to_metric_families
+    r = request(f"http://127.0.0.1:{port}/metrics")
+    assert r.status == 200
+    return {s.name: s for f in text_string_to_metric_families(r.text) for s in f.samples
+            if not s.labels}, r.text
+
+
+def test_watcher_serves_metrics_that_follow_watch_events(mock_cluster, tmp_path):
+    """deploy/watcher.yaml's metrics endpoint (--metrics-listen): the ready-node gauge changes after a watch
+    event, without a textfile in between."""
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    srv = mock_cluster(fixtures.golden("readme"), bookmark_interval=0.2)
+    kc = write_kubeconfig(str(tmp_path / "kc"), srv.url)
+    env = {k: v for k, v in os.environ.items() if k not in ("SLACK_WEBHOOK_URL", "KUBECONFIG")}
+    p = subprocess.Popen([sys.executable, os.path.join(REPO, "check-gpu-node.py"), "--kubeconfig", kc, "--json",
+                          "--watch-events", "--watch-duration", "30", "--watch-debounce", "0.1",
+                          "--metrics-listen", f"127.0.0.1:{port}"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, env=env, cwd=str(tmp_path))
+    try:
+        def ready():
+            try:
+                return _scrape(port)[0].get("k8s_gpu_checker_ready_gpu_nodes")
+            except Exception:  # not listening yet
+                return None
+        t0 = time.monotonic()
+        while time.monotonic() - t0 < 20 and (ready() is None or ready().value != 2):
+            time.sleep(0.1)
+        samples, text = _scrape(port)
+        assert samples["k8s_gpu_checker_ready_gpu_nodes"].value == 2 and samples["k8s_gpu_checker_exit_code"].value == 0
+        assert 'k8s_gpu_checker_node_ready{node="gpu-node-1"} 1' in text
+        assert "k8s_gpu_checker_leader" not in text  # no --leader-elect: no leader gauge
+        srv.state.set_nodes(fixtures.golden("notready"))
+        t0 = time.monotonic()
+        while time.monotonic() - t0 < 20 and ready().value != 0:
+            time.sleep(0.1)
+        samples, text = _scrape(port)
+        assert samples["k8s_gpu_checker_ready_gpu_nodes"].value == 0 and samples["k8s_gpu_checker_exit_code"].value == 3
+        from k8s_gpu_node_checker_amd.utils.http import request
+        assert request(f"http://127.0.0.1:{port}/healthz").status == 200
+    finally:
+        p.terminate()
+        p.communicate(timeout=20)
+
+
+def test_metrics_server_leader_gauge_and_follower_view():
+    import types
+    from k8s_gpu_node_checker_amd.utils import prom
+    node = {"name": "n0", "ready": True, "gpus": 8, "gpu_breakdown": {"amd.com/gpu": 8}}
+    res = types.SimpleNamespace(gpu_nodes=[node], ready_gpu_nodes=[node], exit_code=0, verdicts=[], tracer=None)
+    srv = prom.MetricsServer("127.0.0.1", 0)
+    try:
+        assert srv.text() == "\n"  # nothing before the first report
+        srv.set_leader(False)
+        assert srv.text().splitlines()[-1] == "k8s_gpu_checker_leader 0"
+        srv.set_leader(True)
+        srv.update(res)
+        t = srv.text()
+        assert "k8s_gpu_checker_ready_gpu_nodes 1" in t and t.splitlines()[-1] == "k8s_gpu_checker_leader 1"
+        srv.set_leader(False)  # lost the Lease: the cluster gauges go, a follower must not serve stale ones
+        assert "k8s_gpu_checker_ready_gpu_nodes" not in srv.text()
+    finally:
+        srv.httpd.server_close()
+    assert prom.parse_listen("0.0.0.0:9465") == ("0.0.0.0", 9465)
+    assert prom.parse_listen(":9465") == ("0.0.0.0", 9465)
+    assert prom.parse_listen("[::1]:9465") == ("::1", 9465)
+    with pytest.raises(ValueError):
+        prom.parse_listen("9465x")
