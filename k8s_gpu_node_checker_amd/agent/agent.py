@@ -205,7 +205,8 @@ def fabric_abandoned(fab: Optional[Dict[str, Any]]) -> Optional[str]:
     if isinstance(p2p, dict) and " hung" in str(p2p.get("stopped") or ""):
         return f"xGMI pair test abandoned: {p2p['stopped']}"[:200]
     if isinstance(rccl, dict) and rccl.get("aborted"):
-        return f"RCCL collectives aborted at their deadline: {rccl.get('detail') or ''}"[:200]
+        # at their deadline, or on a communicator's async error: either way ncclCommAbort ran and the buffers stay
+        return f"RCCL collectives aborted: {rccl.get('detail') or ''}"[:200]
     return None
 
 
@@ -574,11 +575,12 @@ class Agent:
         lost_devs = {d: why for d, why in lost_devs.items() if why is not None}
         if lost_devs and self.hip_lost is None:
             # the HIP runtime, not a GPU, is gone only when the device count changed under the process or every
-            # device of the node (two or more) failed that way together; one device's "invalid device ordinal"
-            # is that GPU's (or its configuration's) failure and stays in its verdict -- restarting the agent
-            # for it would only loop, diagnosing the same broken GPU on every start
+            # device that ran this cycle (two or more) failed that way together -- GPUs skipped because a pod
+            # holds them, or scheduled at another time by a recheck, did not run and say nothing either way; one
+            # device's "invalid device ordinal" is that GPU's (or its configuration's) failure and stays in its
+            # verdict -- restarting the agent for it would only loop, diagnosing the same broken GPU every start
             now_count = diag.device_count()
-            everyone = len(lost_devs) == len(finished) == len(devices) >= 2
+            everyone = len(lost_devs) == len(finished) >= 2
             if (self._hip_count0 is not None and now_count != self._hip_count0) or everyone:
                 lost = next(iter(lost_devs.values()))
                 print(f"HIP runtime lost its devices ({lost}); diagnostics stop, /healthz fails so the "
@@ -666,6 +668,10 @@ class Agent:
         if power is not None and power < 1.0:
             kw["power_fraction"] = power
 
+        # the host-link turn is waited for only within this device's watchdog (a GPU stuck in its turn is that
+        # GPU's hang, not every GPU's)
+        kw["deadline"] = time.monotonic() + 0.9 * self.diag_timeout
+
         def work() -> None:
             try:
                 box["res"] = diag.run(self.diag_level, d, **kw)
@@ -679,15 +685,17 @@ class Agent:
 
     def _unmatched_allocations(self, allocated: Dict[str, str], entries: Dict[int, Dict[str, Any]],
                                devices: List[int]) -> Optional[str]:
-        """Fail safe for device IDs the agent cannot map: the kubelet reports GPUs allocated to pods, but none of
-        their IDs is a PCI address of this node's devices (a device plugin that names partitions by another
-        scheme).  Any device may then be a pod's, so none is diagnosed (the reason, else None)."""
+        """Fail safe for device IDs the agent cannot map: the kubelet reports a GPU allocated to a pod whose ID is
+        not a PCI address of this node's devices (a device plugin that names partitions by another scheme, a DRA
+        claim keyed by driver/pool/device).  That allocation may be any of the GPUs, so none is diagnosed -- even
+        when other allocations do map (the reason, else None)."""
         local = {normalize_bdf((entries.get(d) or {}).get("bdf") or self._bdf.get(d, "")) for d in devices}
         local.discard("")
-        if not local or any(k in local for k in allocated):
+        unmapped = sorted(k for k in allocated if k not in local)
+        if not local or not unmapped:
             return None
-        sample = ", ".join(sorted(allocated)[:3])
-        return (f"kubelet reports {len(allocated)} allocated GPU device(s) ({sample}) matching no local PCI "
+        sample = ", ".join(unmapped[:3])
+        return (f"kubelet reports {len(unmapped)} allocated GPU device(s) ({sample}) matching no local PCI "
                 "address: not diagnosing any GPU")
 
     def hung_diagnostic(self, now: Optional[float] = None) -> Optional[str]:

@@ -157,7 +157,7 @@ int wait_comms(Ctx& c, const Deadline& dl, const char* what) {
         const std::string why = std::string(what) + ": " + ncclGetErrorString(st);
         abort_all(c, why, dl);
         g_err = why + " (communicators aborted)";
-        return -2;
+        return -4;  // aborted like a missed deadline: the caller stops re-running the suite in this process
       }
     }
     if (!pending) return 0;
@@ -250,7 +250,7 @@ int sync_all(Ctx& c, const Deadline& dl, const char* what) {
         const std::string why = std::string(what) + ": " + ncclGetErrorString(st);
         abort_all(c, why, dl);
         g_err = why + " (communicators aborted)";
-        return -2;
+        return -4;  // aborted like a missed deadline: the caller stops re-running the suite in this process
       }
     }
     if (dl.passed()) return abort_all(c, what, dl);

@@ -67,6 +67,10 @@ from .native import NativeUnavailable, load_cdll
 FAIL_FRACTION = 0.85
 SHARED_TESTS = frozenset(("host_link",))
 _HOST_SHARED = threading.Lock()  # held by the one device measuring a SHARED_TESTS test
+_HOST_HOLDER: Dict[str, Any] = {}  # who holds it: {"device": d, "since": monotonic time}
+# how long a device waits for the host-resource lock when run() is given no deadline (s): a healthy 8-GPU turn
+# at the host link is ~8 x 0.1 s, so this only ever expires behind a device stuck inside its host-link test
+SHARED_WAIT_S = 120.0
 # A rate below the degraded line (numerics fine) is measured again, up to REMEASURE more times, and the best
 # is kept: under sustained load the burn-in dips below 95 % in ~10 % of single runs (power management),
 # two dips in a row were 19 of 1,913 soak rounds (profiles/soak_level1_r2_mi355x.json); three in a row
@@ -869,13 +873,33 @@ def _goodness(res: Dict[str, Any]) -> tuple:
             res.get("slowest_xcd_rel") or 0.0)
 
 
+def _acquire_shared(device: int, deadline: Optional[float]) -> Optional[str]:
+    """Take the host-resource lock for ``device``; None when taken, else why not (the holder and for how long).
+    Waits until ``deadline`` (monotonic; default SHARED_WAIT_S from now): one GPU hung inside its host-link
+    test must not hold every other GPU's diagnostics past their watchdog and get them all reported hung."""
+    wait = SHARED_WAIT_S if deadline is None else max(0.0, deadline - time.monotonic())
+    if _HOST_SHARED.acquire(timeout=wait):
+        _HOST_HOLDER.update(device=device, since=time.monotonic())
+        return None
+    holder = dict(_HOST_HOLDER)
+    age = time.monotonic() - holder.get("since", time.monotonic())
+    return f"host link held by gpu{holder.get('device', '?')} for {age:.0f} s"
+
+
+def _release_shared() -> None:
+    _HOST_HOLDER.clear()
+    _HOST_SHARED.release()
+
+
 def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
-        memory_partition: Optional[str] = None, power_fraction: Optional[float] = None) -> Dict[str, Dict[str, Any]]:
+        memory_partition: Optional[str] = None, power_fraction: Optional[float] = None,
+        deadline: Optional[float] = None) -> Dict[str, Dict[str, Any]]:
     """Run the diagnostics of ``level`` on ``device`` (1 = ~1 s quick check, 2 = deep).
 
     ``scale`` defaults to the device's own share of a full MI355X (:func:`device_scale`).  A rate that
     lands below the degraded line is measured once more and the better of the two is reported.  Tests of
-    host resources (SHARED_TESTS) hold a process-wide lock, so concurrent per-GPU runs take turns there."""
+    host resources (SHARED_TESTS) hold a process-wide lock, so concurrent per-GPU runs take turns there; a device
+    that cannot get its turn before ``deadline`` (monotonic) reports that test ``skipped``, naming the holder."""
     out: Dict[str, Dict[str, Any]] = {}
     tests = LEVELS.get(level, ())
     if tests and scale is None:
@@ -888,10 +912,13 @@ def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
     scale = scale or FULL
     for test in tests:
         name = test.replace("_quick", "")
-        shared = _HOST_SHARED if name in SHARED_TESTS else None
+        shared = name in SHARED_TESTS
+        if shared:
+            why = _acquire_shared(device, deadline)
+            if why is not None:  # not this GPU's finding: the report says whose turn it still is
+                out[name] = {"pass": True, "skipped": why, "detail": ""}
+                continue
         try:
-            if shared is not None:
-                shared.acquire()
             res = _one(test, device, scale)
             for _ in range(REMEASURE):
                 if not _slow_only(res):
@@ -910,8 +937,8 @@ def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,
         except Exception as e:  # a failing diagnostic is a verdict, not a crash
             out[name] = {"pass": False, "detail": str(e)[:200]}
         finally:
-            if shared is not None:
-                shared.release()
+            if shared:
+                _release_shared()
     return out
 
 
@@ -962,6 +989,9 @@ def render_text(out: Dict[str, Any]) -> str:
                 f"{info.get('cus', '?')} CUs", f"{mem / (1 << 30):.0f} GiB" if isinstance(mem, int) else ""]
         lines.append("  ".join(x for x in head if x))
         for test, r in (dev.get("tests") or {}).items():
+            if r.get("skipped"):
+                lines.append(f"  {test:<10} {'SKIPPED':<9} {r['skipped']}")
+                continue
             state = "FAIL" if not r.get("pass") else ("DEGRADED" if r.get("degraded") else "pass")
             lines.append(f"  {test:<10} {state:<9} {_summary(test, r)}")
             if state != "pass" and r.get("detail"):

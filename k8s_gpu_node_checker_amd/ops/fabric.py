@@ -82,7 +82,10 @@ def collective_suite(devices: Sequence[int], sizes: Sequence[int] = DEFAULT_SIZE
             for nbytes in sizes:
                 rc = lib().fabric_run(ctx, OPS.index(op), nbytes, iters, warmup, out, left_ms())
                 if rc != 0:
-                    return {"pass": False, "world": len(devs), "rows": rows, "aborted": rc == ABORTED,
+                    # aborted: the deadline passed, or a communicator's async error aborted them all -- either way
+                    # the context leaked its buffers, so the agent must not re-run the suite (fabric_abandoned)
+                    aborted = rc == ABORTED or bool(lib().fabric_aborted(ctx))
+                    return {"pass": False, "world": len(devs), "rows": rows, "aborted": aborted,
                             "detail": f"{op} {nbytes} B: {_error()}"[:200],
                             "wall_s": round(time.perf_counter() - t0, 3)}
                 rows.append({"op": op, "bytes": nbytes, "ms": round(out[0], 4), "algbw_gbps": round(out[1], 2),

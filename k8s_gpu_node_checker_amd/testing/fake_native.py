@@ -337,11 +337,14 @@ class FakeFabricLib:
     """``libmi355x_fabric.so`` (in-process RCCL communicator over the node's GPUs)."""
 
     def __init__(self, busbw: float = 320.0, errors: int = 0, fail_open: bool = False, version: int = 22707,
-                 hang_op: Optional[int] = None):
+                 hang_op: Optional[int] = None, async_error_op: Optional[int] = None):
         self.busbw, self.errors, self.fail_open, self.version = busbw, errors, fail_open, version
         # hang_op: that collective never completes -- the call waits out its deadline (or forever without
         # one, until `release` is set) and then "aborts" the communicators like fabric.hip's abort_all
         self.hang_op = hang_op
+        # async_error_op: a communicator reports an async error during that collective (a link dropping
+        # traffic): fabric.hip's wait_comms / sync_all abort every communicator and return ABORTED
+        self.async_error_op = async_error_op
         self.release = threading.Event()
         self.opened: List[List[int]] = []
         self.timeouts_ms: List[float] = []
@@ -364,6 +367,10 @@ class FakeFabricLib:
                 self.err = (f"timed collectives: not complete within {timeout_ms:.0f} ms: communicators aborted "
                             "(ncclCommAbort)").encode()
                 return -4
+        if op == self.async_error_op:
+            self.aborts += 1
+            self.err = b"collective wait: remote process exited or there was a network error (communicators aborted)"
+            return -4
         out[0], out[1], out[2], out[3] = 1.0, self.busbw * 0.57, self.busbw, float(self.errors if op == 3 else 0)
         return 0
 

@@ -33,7 +33,7 @@ class World:
         monkeypatch.setattr(diag, "device_count", lambda: n)
         monkeypatch.setattr(diag, "device_info", lambda d: {"bdf": f"0000:0{d}:00.0"})
 
-        def run(level, d, memory_partition=None):
+        def run(level, d, memory_partition=None, **kw):
             self.runs.append(d)
             return {"gemm": {"pass": True, "tflops": 1200.0 + len(self.runs)}}
         monkeypatch.setattr(diag, "run", run)
@@ -147,7 +147,7 @@ def test_hung_diagnostic_is_reported_not_waited_for(monkeypatch):
     release = threading.Event()
     started = []
 
-    def run(level, d, memory_partition=None):
+    def run(level, d, memory_partition=None, **kw):
         started.append(d)
         if d == 1:
             release.wait(30)  # GPU 1's queue hangs
@@ -186,7 +186,7 @@ def test_restarted_agent_clears_a_watchdog_verdict(monkeypatch, mock_cluster):
     srv = mock_cluster([fixtures.realistic_node("n", gpu_count=2)])
     release = threading.Event()
 
-    def hang(level, d, memory_partition=None):
+    def hang(level, d, memory_partition=None, **kw):
         if d == 1:
             release.wait(30)
         return {"gemm": {"pass": True}}
@@ -200,7 +200,7 @@ def test_restarted_agent_clears_a_watchdog_verdict(monkeypatch, mock_cluster):
         assert any(t["key"] == H.UNHEALTHY_TAINT["key"] for t in node["spec"].get("taints") or [])
         release.set()  # the old process is gone; its hung thread with it
 
-        monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: {"gemm": {"pass": True}})
+        monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None, **kw: {"gemm": {"pass": True}})
         new = A.Agent("n", source="fake", diag_level=1, taint_unhealthy=True)
         wrote = new.publish(kc, new.probe_once())
         assert wrote["annotation"] and wrote["condition"] and wrote["taint"]
@@ -253,7 +253,7 @@ def test_hip_runtime_losing_its_devices_restarts_the_agent_not_the_verdict(monke
     import urllib.request
     w = World(monkeypatch)
     lost = "mi355x diag failed (-1): hipSetDevice(device): no ROCm-capable device is detected"
-    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: (
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None, **kw: (
         w.runs.append(d), {"gemm": {"pass": False, "detail": lost}, "hbm": {"pass": False, "detail": lost}})[1])
     ag = A.Agent("n", source="fake", diag_level=1, diag_interval=0.0)
     srv = A.serve(ag, "127.0.0.1", 0, stale_after=60)
@@ -333,7 +333,7 @@ def test_a_slow_result_is_measured_again_soon(monkeypatch):
     w = World(monkeypatch, n=1)
     results = [{"gemm": {"pass": True, "degraded": True, "detail": "tflops 1100 = 90% of 1220"}},
                {"gemm": {"pass": True, "degraded": False}}]
-    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: (w.runs.append(d), results[len(w.runs) - 1])[1])
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None, **kw: (w.runs.append(d), results[len(w.runs) - 1])[1])
     ag = A.Agent("n", source="fake", diag_level=1, diag_interval=3600.0)
     rep = ag.probe_once()
     assert rep["gpus"][0]["diag"]["gemm"]["degraded"] and rep["state"] == "degraded"
@@ -359,7 +359,7 @@ def test_healthz_fails_once_a_diagnostic_outlives_twice_its_watchdog(monkeypatch
     w = World(monkeypatch)
     release = threading.Event()
 
-    def run(level, d, memory_partition=None):
+    def run(level, d, memory_partition=None, **kw):
         if d == 0:
             release.wait(30)
         return {"gemm": {"pass": True}}
@@ -441,7 +441,7 @@ def test_a_persistent_failure_is_rechecked_once_then_back_to_the_interval(monkey
     """a GPU that keeps failing the same way is not stressed again every 5 minutes."""
     w = World(monkeypatch, n=1)
     bad = {"memtest": {"pass": False, "detail": "12 bad words"}}
-    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: (w.runs.append(d), dict(bad))[1])
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None, **kw: (w.runs.append(d), dict(bad))[1])
     ag = A.Agent("n", source="fake", diag_level=1, diag_interval=3600.0)
     ag.probe_once()
     w.clock += A.DIAG_RECHECK_S
@@ -506,7 +506,7 @@ def test_one_gpu_failing_with_runtime_strings_is_that_gpus_failure(monkeypatch):
     w = World(monkeypatch)
     lost = "mi355x diag failed (-1): hipSetDevice(device): invalid device ordinal"
 
-    def run(level, d, memory_partition=None):
+    def run(level, d, memory_partition=None, **kw):
         w.runs.append(d)
         return {"gemm": {"pass": False, "detail": lost}} if d == 1 else {"gemm": {"pass": True}}
     monkeypatch.setattr(diag, "run", run)
@@ -523,7 +523,7 @@ def test_one_gpu_failing_with_runtime_strings_is_that_gpus_failure(monkeypatch):
     # and when every device that ran failed that way together, also the runtime (no count change needed)
     ag2 = A.Agent("n", source="fake", diag_level=1)
     monkeypatch.setattr(diag, "device_count", lambda: 2)
-    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: {"gemm": {"pass": False, "detail": lost}})
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None, **kw: {"gemm": {"pass": False, "detail": lost}})
     ag2.probe_once()
     assert ag2.hip_lost == lost
 
@@ -584,7 +584,7 @@ def test_single_gpu_failing_with_runtime_strings_is_not_a_restart_loop(monkeypat
     unhealthy GPU, not a lost runtime: restarting would only re-run the same diagnostics forever."""
     w = World(monkeypatch, n=1)
     bad = "mi355x diag failed (-1): hipSetDevice(device): initialization error"
-    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None: (
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None, **kw: (
         w.runs.append(d), {"gemm": {"pass": False, "detail": bad}, "hbm": {"pass": False, "detail": bad}})[1])
     ag = A.Agent("n", source="fake", diag_level=1)
     rep = ag.probe_once()
@@ -594,3 +594,31 @@ def test_single_gpu_failing_with_runtime_strings_is_not_a_restart_loop(monkeypat
     w.clock += A.DIAG_RECHECK_S
     ag.probe_once()
     assert ag.hip_lost == "HIP device count changed from 1 to 0"
+
+
+def test_runtime_loss_is_judged_on_the_devices_that_ran(monkeypatch):
+    """after a driver reload on a busy node the idle GPUs fail with 'invalid device ordinal' while the
+    GPU a pod holds is skipped.  Every device that *ran* failed that way (two or more): the runtime is lost, so
+    /healthz restarts the agent -- the idle GPUs are not published as broken hardware for ever."""
+    w = World(monkeypatch, n=4)
+    lost = "mi355x diag failed (-1): hipSetDevice(device): invalid device ordinal"
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None, **kw: (
+        w.runs.append(d), {"gemm": {"pass": False, "detail": lost}})[1])
+    w.gpus[2] = gpu(2, procs=[{"pid": 7, "vram_mb": 200000}])  # a training job holds gpu2
+    ag = A.Agent("n", source="fake", diag_level=1)
+    rep = ag.probe_once()
+    assert sorted(w.runs) == [0, 1, 3]
+    assert ag.hip_lost == lost
+    assert all(g["diag_skipped"].startswith("HIP runtime lost its devices") for g in rep["gpus"])
+
+
+def test_one_busy_one_failing_gpu_is_not_a_lost_runtime(monkeypatch):
+    """Only one device ran (the other is busy) and it failed with a runtime string: one GPU's failure."""
+    w = World(monkeypatch, n=2)
+    lost = "mi355x diag failed (-1): hipSetDevice(device): invalid device ordinal"
+    monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None, **kw: (
+        w.runs.append(d), {"gemm": {"pass": False, "detail": lost}})[1])
+    w.gpus[1] = gpu(1, procs=[{"pid": 7, "vram_mb": 200000}])
+    ag = A.Agent("n", source="fake", diag_level=1)
+    rep = ag.probe_once()
+    assert w.runs == [0] and ag.hip_lost is None and rep["state"] == "unhealthy"

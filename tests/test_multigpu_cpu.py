@@ -263,7 +263,7 @@ def test_hung_collective_is_aborted_and_reported_as_a_failed_rccl_row(node8):
     assert "watchdog" not in rep["fabric"] and rep["state"] == H.UNHEALTHY
     assert any(r.startswith("xGMI rccl failed (all_reduce") for r in ag.evaluate(rep).reasons)
     assert ag._fabric_thread is None  # the suite returned: nothing left holding the GPUs
-    assert ag.fabric_abandoned.startswith("RCCL collectives aborted at their deadline")
+    assert ag.fabric_abandoned.startswith("RCCL collectives aborted: all_reduce")
 
 
 def test_hung_xgmi_pair_is_given_up_at_its_share_of_the_deadline(node8):
@@ -305,3 +305,44 @@ def test_node_cycle_module_over_eight_fake_gpus(node8):
     assert diag.run.__name__ == "run"  # the counting wrapper is removed again
     res4 = node_cycle.run(list(range(8)), level=1, timeout_s=30, parallel=4, fabric=False)
     assert res4["peak_threads"] == 4 and "fabric" not in res4
+
+
+def test_async_rccl_error_aborts_and_latches_like_a_deadline(node8):
+    """a communicator's async error aborts every communicator (fabric.hip wait_comms / sync_all) and
+    leaks their buffers like a missed deadline; the suite reports ``aborted`` and the agent does not re-run it
+    every --diag-interval (it used to come back as a plain failure and be re-run, leaking each time)."""
+    lib, fab = node8()
+    fab.async_error_op = 1  # reduce_scatter
+    ag = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8, diag_timeout=5.0)
+    rep = ag.probe_once()
+    rccl = rep["fabric"]["rccl"]
+    assert rccl["pass"] is False and rccl["aborted"] is True and "communicators aborted" in rccl["detail"]
+    assert ag.fabric_abandoned.startswith("RCCL collectives aborted: reduce_scatter")
+    ag._fabric_at -= 2 * ag.diag_interval
+    for d in list(ag._diag_at):
+        ag._diag_at[d] -= 2 * ag.diag_interval
+    rep2 = ag.probe_once()
+    assert fab.opened == [list(range(8))]  # not opened again
+    assert rep2["fabric"]["rccl"]["retest"].startswith("not re-run in this process")
+
+
+def test_a_gpu_stuck_in_its_host_link_turn_does_not_hang_the_others(node8):
+    """the host-link lock was taken with a blocking acquire, so one GPU hung inside its host-link test
+    held every other GPU's diagnostics past their watchdog (all reported hung).  Now a device waits only until its
+    own deadline and reports the test skipped, naming the holder; its other tests still run."""
+    lib, fab = node8()
+    assert diag._acquire_shared(5, None) is None  # gpu5 is stuck inside its turn
+    try:
+        t0 = time.monotonic()
+        res = diag.run(2, 1, deadline=time.monotonic() + 0.3)
+        assert time.monotonic() - t0 < 2.0
+        assert res["host_link"]["skipped"].startswith("host link held by gpu5 for ")
+        assert res["host_link"]["pass"] is True and res["gemm"]["pass"]
+        v = H.evaluate_report(dict(fixtures.mi355x_probe_report("n", gpus=1), gpus=[
+            dict(fixtures.mi355x_probe_report("n", gpus=1)["gpus"][0], diag=res)]), 1)
+        assert v.state == H.HEALTHY  # gpu1 is not blamed for gpu5's hang
+        text = diag.render_text({"devices": {1: {"info": {}, "tests": res}}, "pass": True})
+        assert "host_link  SKIPPED   host link held by gpu5" in text
+    finally:
+        diag._release_shared()
+    assert diag.run(2, 1)["host_link"].get("skipped") is None  # the lock is free again

@@ -89,7 +89,7 @@ def _world(monkeypatch, n=2):
     monkeypatch.setattr(diag, "device_count", lambda: n)
     monkeypatch.setattr(diag, "device_info", lambda d: {"bdf": f"0000:{0x05 + 0x10 * d:02x}:00.0"})
 
-    def run(level, d, memory_partition=None):
+    def run(level, d, memory_partition=None, **kw):
         runs.append(d)
         return {"gemm": {"pass": True, "tflops": 1220.0}}
     monkeypatch.setattr(diag, "run", run)
@@ -187,3 +187,26 @@ def test_dra_device_without_a_pci_address_makes_the_agent_fail_safe(monkeypatch)
         rep = A.Agent("n", source="fake", diag_level=1, pod_resources_socket=kub.sock).probe_once()
     assert ran == []
     assert all("matching no local PCI address" in g["diag_skipped"] for g in rep["gpus"])
+
+
+def test_one_mappable_and_one_unmappable_allocation_still_fail_safe(monkeypatch):
+    """a device-plugin allocation that maps to a local PCI address next to a DRA claim keyed by
+    driver/pool/device: the claim may be any GPU, so no GPU is diagnosed (it used to diagnose all but the mapped
+    one, possibly under a running pod)."""
+    pods = [{"name": "a", "namespace": "ml", "containers": [{"name": "c", "devices": [
+                {"resource_name": "amd.com/gpu", "device_ids": ["0000:05:00.0"]}], "dynamic": []}]},
+            {"name": "p", "namespace": "ml", "containers": [{"name": "c", "devices": [], "dynamic": [
+                {"claim_name": "c1", "claim_namespace": "ml", "devices": [
+                    {"driver": "gpu.amd.com", "pool": "node-a", "device": "gpu-3", "cdi": ["gpu.amd.com/gpu=gpu-3"]}]}]}]}]
+    ran = []
+    monkeypatch.setattr(amdsmi_probe, "probe", lambda node, src, fx: fixtures.mi355x_probe_report("n", gpus=2))
+    monkeypatch.setattr(diag, "device_count", lambda: 2)
+    monkeypatch.setattr(diag, "device_info", lambda d: {"bdf": ["0000:05:00.0", "0000:15:00.0"][d]})
+    monkeypatch.setattr(diag, "run", lambda level, d, **kw: (ran.append(d), {"gemm": {"pass": True}})[1])
+    with FakeKubelet(pods) as kub:
+        got = PR.allocated_devices(kub.sock)
+        assert got == {"0000:05:00.0": "ml/a", "gpu.amd.com/node-a/gpu-3": "ml/p (claim ml/c1)"}
+        rep = A.Agent("n", source="fake", diag_level=1, pod_resources_socket=kub.sock).probe_once()
+    assert ran == []
+    assert all("gpu.amd.com/node-a/gpu-3" in g["diag_skipped"] and "matching no local PCI address" in g["diag_skipped"]
+               for g in rep["gpus"])
