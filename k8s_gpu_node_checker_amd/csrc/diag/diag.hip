@@ -49,6 +49,8 @@ thread_local std::string g_err;
 thread_local int g_gemm_variant = 0;
 thread_local int g_gemm_schedule = 1;  // v3 restaging order (V3_PHASE): 1 = LDS-DMA pieces per phase 0/2/2/4, 0 = 2/0/4/2
 thread_local int g_gemm_buffer_loads = 0;  // v3 operand staging: 0 = global_load_lds, 1 = buffer_load ... lds
+thread_local int g_gemm_fp8_unscaled = 0;  // fp8 v3 MFMA: 0 = v_mfma_scale_..._f8f6f4 with unit E8M0 scales,
+                                           // 1 = the unscaled v_mfma_f32_16x16x128_f8f6f4 (hipBLASLt's fp8 form)
 thread_local int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3
                                        // kernels; measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
 
@@ -416,6 +418,22 @@ __device__ __forceinline__ void stg_mfma(floatx4 (&acc)[8][4], const i32x8 (&af)
     for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[m0 + m][n0 + n]));
 }
 
+// The same K-tile on the unscaled instruction (zero scale operands select v_mfma_f32_16x16x128_f8f6f4): with unit
+// scales the two compute the same products, so the knob only changes which matrix-core path runs.
+__device__ __forceinline__ void stg_mfma_unscaled(floatx4 (&acc)[8][4], const i32x8 (&af)[4], const i32x8 (&bf)[2],
+                                                  int m0, int n0) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+      acc[m0 + m][n0 + n] =
+          __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bf[n], acc[m0 + m][n0 + n], 0, 0, 0, 0, 0, 0);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[m0 + m][n0 + n]));
+}
+
 // Fragment of one 16-row block: bf16 = two K=32 steps (chunks fq, fq+4); fp8 = the lane's 32
 // contiguous bytes of K (chunks 2fq, 2fq+1; lane layout measured by tools/mfma_lab.hip).
 __device__ __forceinline__ void stg_load(bf16x8 (&f)[2], const u32x4* img, int row, int fq) {
@@ -457,7 +475,7 @@ __device__ __forceinline__ void stg_mfma(floatx4 (&acc)[8][4], const u32x4 (&af)
     for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[m0 + m][n0 + n]));
 }
 
-enum GemmDtype { DT_BF16 = 0, DT_FP8 = 1, DT_FP4 = 2 };
+enum GemmDtype { DT_BF16 = 0, DT_FP8 = 1, DT_FP4 = 2, DT_FP8U = 3 /* fp8 operands, unscaled MFMA */ };
 
 template <int DT>
 struct StgFrags {
@@ -467,6 +485,17 @@ template <>
 struct StgFrags<DT_FP8> {
   i32x8 a[4], b0[2], b1[2];
 };
+template <>
+struct StgFrags<DT_FP8U> {
+  i32x8 a[4], b0[2], b1[2];
+};
+
+// One phase's MFMAs for the kernel's data type.
+template <int DT, typename FA, typename FB>
+__device__ __forceinline__ void phase_mfma(floatx4 (&acc)[8][4], const FA& af, const FB& bf, int m0, int n0) {
+  if constexpr (DT == DT_FP8U) stg_mfma_unscaled(acc, af, bf, m0, n0);
+  else stg_mfma(acc, af, bf, m0, n0);
+}
 template <>
 struct StgFrags<DT_FP4> {
   u32x4 a[4][2], b0[2][2], b1[2][2];
@@ -542,7 +571,7 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
   const int KT = K / BK;
   const int frow = lane & 15, fq = lane >> 4;
 
-  constexpr bool FP8 = DT == DT_FP8;
+  constexpr bool FP8 = DT == DT_FP8 || DT == DT_FP8U;
   const StgBuf rs = stg_buf(Ab, Bb, K);
   auto region = [&](unsigned char* stage, int kt_, int r, int i) {
     if constexpr (BUF) stg_region_buf<FP8>(stage, rs, K, kt_, r, i, wid, lane);
@@ -598,7 +627,7 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
     STG_BARRIER();
     V3_STAMP(0, 1);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    stg_mfma(acc, f.a, f.b0, 0, 0);
+    phase_mfma<DT>(acc, f.a, f.b0, 0, 0);
     V3_STAMP(0, 2);
     STG_BARRIER();
     V3_STAMP(0, 3);
@@ -610,7 +639,7 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
     STG_BARRIER();
     V3_STAMP(1, 1);
     __builtin_amdgcn_s_waitcnt(0xc07f);
-    stg_mfma(acc, f.a, f.b1, 0, 2);
+    phase_mfma<DT>(acc, f.a, f.b1, 0, 2);
     V3_STAMP(1, 2);
     STG_BARRIER();
     V3_STAMP(1, 3);
@@ -622,7 +651,7 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
     STG_BARRIER();
     V3_STAMP(2, 1);
     __builtin_amdgcn_s_waitcnt(0xc07f);
-    stg_mfma(acc, f.a, f.b1, 4, 2);
+    phase_mfma<DT>(acc, f.a, f.b1, 4, 2);
     V3_STAMP(2, 2);
     STG_BARRIER();
     V3_STAMP(2, 3);
@@ -636,7 +665,7 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
     }
     STG_BARRIER();
     V3_STAMP(3, 1);
-    stg_mfma(acc, f.a, f.b0, 4, 0);
+    phase_mfma<DT>(acc, f.a, f.b0, 4, 0);
     V3_STAMP(3, 2);
     STG_BARRIER();
     V3_STAMP(3, 3);
@@ -952,7 +981,11 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b) {
 // measured by tools/mfma_lab.hip: lane l holds A[l&15][k = (K/4)(l>>4) + e] and B[k][l&15] in element
 // e, fp4 low nibble first):
 //   0 bf16  v_mfma_f32_16x16x32_bf16          2 MX-fp8 (E4M3)  v_mfma_scale_f32_16x16x128_f8f6f4
-//   1 fp8   v_mfma_f32_16x16x32_fp8_fp8       3 MX-fp4 (E2M1)  v_mfma_scale_f32_16x16x128_f8f6f4
+//   1 fp8   v_mfma_f32_16x16x128_f8f6f4       3 MX-fp4 (E2M1)  v_mfma_scale_f32_16x16x128_f8f6f4
+// Kind 1 is the unscaled f8f6f4 instruction (E4M3, no block scales): what hipBLASLt's fp8 GEMMs issue on gfx950
+// (its TensileLibrary_F8F8_*_gfx950.co holds 13,773 of them and 12 of the gfx94x-era v_mfma_f32_16x16x32_fp8_fp8,
+// which this kind used to burn; that older datapath ran at the bf16 rate and no production fp8 GEMM depends on
+// it).  The builtin with zero scale operands is selected as the unscaled instruction (checked in the ISA).
 // Register-resident (no memory traffic), 4 independent accumulators per wave, 2 waves per SIMD on every
 // CU.  Operands are {-1, 0, +1}: every product and partial sum is an integer below 2^24, so the fp32
 // result is exact and each lane's final sum must equal the host-computed value bit for bit -- a SIMD
@@ -965,10 +998,7 @@ __device__ __forceinline__ floatx4 burn_mfma(const i32x8& a, const i32x8& b, flo
     __builtin_memcpy(&bv, &b, 16);
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c, 0, 0, 0);
   } else if constexpr (KIND == 1) {
-    long av, bv;
-    __builtin_memcpy(&av, &a, 8);
-    __builtin_memcpy(&bv, &b, 8);
-    return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av, bv, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 0, 0, 0);  // E4M3, unscaled form
   } else if constexpr (KIND == 2) {
     return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);  // E4M3, scales 2^0
   } else {
@@ -1283,6 +1313,13 @@ int launch_v3_ck(const void* A, const void* Bt, __bf16* C, double* csum, int M, 
              : launch_v3_inst<DT, true, false, 1, OUT_BF16_CK>(A, Bt, C, csum, M, N, Kcols, stream);
 }
 
+// fp8 operands on the MFMA form the thread's knob picks (g_gemm_fp8_unscaled)
+int launch_v3_ck_fp8(const void* A, const void* Bt, __bf16* C, double* csum, int M, int N, int Kcols,
+                     hipStream_t stream) {
+  return g_gemm_fp8_unscaled ? launch_v3_ck<DT_FP8U>(A, Bt, C, csum, M, N, Kcols, stream)
+                             : launch_v3_ck<DT_FP8>(A, Bt, C, csum, M, N, Kcols, stream);
+}
+
 // The diagnostic runs (diag_gemm_*_x) take the bf16-output kernel wherever the production v3 configuration
 // would run (LDS-staged epilogue, global_load_lds staging); other knob settings keep fp32 C.
 bool v3_ck_path() { return g_gemm_epilogue == 1 && !g_gemm_buffer_loads; }
@@ -1472,6 +1509,8 @@ void diag_set_gemm_epilogue(int e) { g_gemm_epilogue = e; }
 void diag_set_gemm_buffer_loads(int b) { g_gemm_buffer_loads = b; }
 void diag_set_gemm_schedule(int s) { g_gemm_schedule = s; }
 int diag_get_gemm_schedule(void) { return g_gemm_schedule; }
+void diag_set_gemm_fp8_unscaled(int u) { g_gemm_fp8_unscaled = u ? 1 : 0; }
+int diag_get_gemm_fp8_unscaled(void) { return g_gemm_fp8_unscaled; }
 int diag_get_gemm_variant(void) { return g_gemm_variant; }
 int diag_get_gemm_epilogue(void) { return g_gemm_epilogue; }
 int diag_get_gemm_buffer_loads(void) { return g_gemm_buffer_loads; }
@@ -1542,7 +1581,9 @@ int diag_gemm_fp8_launch(const void* A, const void* Bt, float* C, int M, int N, 
     g_err = "gemm_fp8: M, N must be multiples of 256 and K a multiple of 128";
     return -2;
   }
-  if (launch_v3<DT_FP8>(A, Bt, C, M, N, K / 2, static_cast<hipStream_t>(stream)) != 0) return -1;
+  if ((g_gemm_fp8_unscaled ? launch_v3<DT_FP8U>(A, Bt, C, M, N, K / 2, static_cast<hipStream_t>(stream))
+                           : launch_v3<DT_FP8>(A, Bt, C, M, N, K / 2, static_cast<hipStream_t>(stream))) != 0)
+    return -1;
   DIAG_CHECK(hipGetLastError());
   return 0;
 }
@@ -1574,7 +1615,7 @@ int diag_gemm_launch_ck(int dt, const void* A, const void* Bt, void* C, double* 
     return -2;
   }
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  const int rc = dt == DT_FP8 ? launch_v3_ck<DT_FP8>(A, Bt, static_cast<__bf16*>(C), csum, M, N, K / 2, st)
+  const int rc = dt == DT_FP8 ? launch_v3_ck_fp8(A, Bt, static_cast<__bf16*>(C), csum, M, N, K / 2, st)
                               : launch_v3_ck<DT_BF16>(A, Bt, static_cast<__bf16*>(C), csum, M, N, K, st);
   if (rc != 0) return -1;
   DIAG_CHECK(hipGetLastError());
@@ -1710,7 +1751,7 @@ int diag_gemm_fp8_x(int device, int M, int N, int K, int warmup, int iters, int 
   if (fused) DIAG_CHECK(bcs.alloc(device, sizeof(double) * static_cast<size_t>(M / 128) * N));
   double* cs = static_cast<double*>(bcs.ptr);
   auto run = [&]() -> int {
-    return fused ? launch_v3_ck<DT_FP8>(A.ptr, Bt.ptr, static_cast<__bf16*>(C.ptr), cs, M, N, K / 2, nullptr)
+    return fused ? launch_v3_ck_fp8(A.ptr, Bt.ptr, static_cast<__bf16*>(C.ptr), cs, M, N, K / 2, nullptr)
                  : diag_gemm_fp8_launch(A.ptr, Bt.ptr, static_cast<float*>(C.ptr), M, N, K, nullptr);
   };
   DIAG_CHECK(ref.alloc(device, sizeof(double) * nsamp));
@@ -2032,7 +2073,7 @@ int diag_mfma_burn_map(int device, int kind, int iters, int reps, double* tflops
     return -2;
   }
   DIAG_CHECK(hipSetDevice(device));
-  static const int kK[4] = {32, 32, 128, 128};
+  static const int kK[4] = {32, 128, 128, 128};
   const int K = kK[kind], per = K / 4;
   // a lane's final sum is bounded by 16 outputs * K * 4 MFMA per accumulator-iteration * iters
   if (16.0 * K * 4 * iters >= 16777216.0) {

@@ -223,8 +223,9 @@ def lib() -> ctypes.CDLL:
         L.diag_set_gemm_epilogue.argtypes = [ctypes.c_int]
         L.diag_set_gemm_buffer_loads.argtypes = [ctypes.c_int]
         L.diag_set_gemm_schedule.argtypes = [ctypes.c_int]
+        L.diag_set_gemm_fp8_unscaled.argtypes = [ctypes.c_int]
         for getter in ("diag_get_gemm_variant", "diag_get_gemm_epilogue", "diag_get_gemm_buffer_loads",
-                       "diag_get_gemm_schedule"):
+                       "diag_get_gemm_schedule", "diag_get_gemm_fp8_unscaled"):
             getattr(L, getter).restype = ctypes.c_int
         L.diag_device_count.restype = ctypes.c_int
         L.diag_device_arch.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
@@ -323,6 +324,18 @@ def set_gemm_schedule(schedule: int) -> None:
     if schedule not in (0, 1):
         raise ValueError(f"gemm schedule must be 0 or 1, not {schedule!r}")
     lib().diag_set_gemm_schedule(schedule)
+
+
+def set_gemm_fp8_unscaled(unscaled: bool) -> None:
+    """fp8 v3 GEMMs: the MFMA form -- ``v_mfma_scale_f32_16x16x128_f8f6f4`` with unit E8M0 scales (False, the
+    MX path) or the unscaled ``v_mfma_f32_16x16x128_f8f6f4`` hipBLASLt's fp8 GEMMs issue (True).  Unit scales make
+    the two compute the same products; the knob picks the matrix-core path timed.  Per calling thread."""
+    lib().diag_set_gemm_fp8_unscaled(1 if unscaled else 0)
+
+
+def get_gemm_fp8_unscaled() -> bool:
+    f = getattr(lib(), "diag_get_gemm_fp8_unscaled", None)  # (absent from the test doubles of the library)
+    return bool(f()) if f is not None else False
 
 
 def get_gemm_config() -> Dict[str, Any]:
