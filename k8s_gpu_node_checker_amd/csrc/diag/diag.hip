@@ -49,8 +49,10 @@ thread_local std::string g_err;
 thread_local int g_gemm_variant = 0;
 thread_local int g_gemm_schedule = 1;  // v3 restaging order (V3_PHASE): 1 = LDS-DMA pieces per phase 0/2/2/4, 0 = 2/0/4/2
 thread_local int g_gemm_buffer_loads = 0;  // v3 operand staging: 0 = global_load_lds, 1 = buffer_load ... lds
-thread_local int g_gemm_fp8_unscaled = 0;  // fp8 v3 MFMA: 0 = v_mfma_scale_..._f8f6f4 with unit E8M0 scales,
-                                           // 1 = the unscaled v_mfma_f32_16x16x128_f8f6f4 (hipBLASLt's fp8 form)
+// fp8 v3 MFMA: 1 = the unscaled v_mfma_f32_16x16x128_f8f6f4 (hipBLASLt's fp8 form, the default: +5.6 % over the
+// scaled form at 4096^3 and 8192^3 with bit-identical C, profiles/gemm_fp8_mfma_ab_mi355x.jsonl), 0 = the
+// v_mfma_scale_..._f8f6f4 MX path with unit E8M0 scales (kept for A/B)
+thread_local int g_gemm_fp8_unscaled = 1;
 thread_local int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3
                                        // kernels; measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
 

@@ -87,7 +87,10 @@ REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
     # 0.956, above the degraded line (the fp32-output 2,380 left a slow healthy box degraded in most rounds)
     "gemm_fp8": {4096: 2210.0, 8192: 2300.0},
     "hbm": {"copy_tbs": 6.49, "read_tbs": 6.96},   # 16-byte copy (read + write bytes counted) / read, TB/s
-    "mfma": {"bf16": 1901.0, "fp8": 1940.0, "mxfp8": 4326.0, "mxfp4": 7610.0},  # register-resident burn-in
+    # register-resident burn-in.  fp8 is the unscaled f8f6f4 instruction since round 4 (it was the gfx94x
+    # v_mfma_f32_16x16x32_fp8_fp8, 1,940): 40 runs median 4,872 vs MX-fp8's 4,844 in the same runs, first (cold)
+    # run 4,058 (profiles/mfma_kinds_mi355x.json) -> MX-fp8's reference x 4,872 / 4,844
+    "mfma": {"bf16": 1901.0, "fp8": 4350.0, "mxfp8": 4326.0, "mxfp4": 7610.0},
     "host_link": {"h2d_gbps": 57.0, "d2h_gbps": 56.8},  # pinned copies over PCIe Gen5 x16
     # per-XCD HBM reads, 8 x 256 MiB slices (read 4x since profiles/hbm_xcd_passes_mi355x.json: lone-XCD
     # spread 0.994 at 4 passes vs 0.987 at 2, +5 ms); at 2 passes all XCDs together 5.83-6.27 TB/s (a cold level-2
@@ -327,15 +330,16 @@ def set_gemm_schedule(schedule: int) -> None:
 
 
 def set_gemm_fp8_unscaled(unscaled: bool) -> None:
-    """fp8 v3 GEMMs: the MFMA form -- ``v_mfma_scale_f32_16x16x128_f8f6f4`` with unit E8M0 scales (False, the
-    MX path) or the unscaled ``v_mfma_f32_16x16x128_f8f6f4`` hipBLASLt's fp8 GEMMs issue (True).  Unit scales make
-    the two compute the same products; the knob picks the matrix-core path timed.  Per calling thread."""
+    """fp8 v3 GEMMs: the MFMA form -- the unscaled ``v_mfma_f32_16x16x128_f8f6f4`` hipBLASLt's fp8 GEMMs issue
+    (True, the default: 5.6 % faster, 92 % of hipBLASLt at 8192^3) or ``v_mfma_scale_f32_16x16x128_f8f6f4`` with
+    unit E8M0 scales (False, the MX path).  Unit scales make the two compute the same products (bit-identical C);
+    the knob picks the matrix-core path timed.  Per calling thread."""
     lib().diag_set_gemm_fp8_unscaled(1 if unscaled else 0)
 
 
 def get_gemm_fp8_unscaled() -> bool:
     f = getattr(lib(), "diag_get_gemm_fp8_unscaled", None)  # (absent from the test doubles of the library)
-    return bool(f()) if f is not None else False
+    return bool(f()) if f is not None else True
 
 
 def get_gemm_config() -> Dict[str, Any]:
@@ -346,7 +350,8 @@ def get_gemm_config() -> Dict[str, Any]:
     return {"variant": inv.get(int(L.diag_get_gemm_variant()), "auto"),
             "epilogue": bool(L.diag_get_gemm_epilogue()),
             "buffer_loads": bool(L.diag_get_gemm_buffer_loads()),
-            "schedule": int(L.diag_get_gemm_schedule())}
+            "schedule": int(L.diag_get_gemm_schedule()),
+            "fp8_unscaled": get_gemm_fp8_unscaled()}
 
 
 def get_gemm_epilogue() -> bool:
@@ -358,8 +363,10 @@ class gemm_config:
     and restore the previous values on exit (not the library defaults)."""
 
     def __init__(self, variant: Optional[str] = None, epilogue: Optional[bool] = None,
-                 buffer_loads: Optional[bool] = None, schedule: Optional[int] = None):
-        self.want = {"variant": variant, "epilogue": epilogue, "buffer_loads": buffer_loads, "schedule": schedule}
+                 buffer_loads: Optional[bool] = None, schedule: Optional[int] = None,
+                 fp8_unscaled: Optional[bool] = None):
+        self.want = {"variant": variant, "epilogue": epilogue, "buffer_loads": buffer_loads, "schedule": schedule,
+                     "fp8_unscaled": fp8_unscaled}
         self.saved: Dict[str, Any] = {}
 
     @staticmethod
@@ -372,6 +379,8 @@ class gemm_config:
             set_gemm_buffer_loads(cfg["buffer_loads"])
         if cfg.get("schedule") is not None:
             set_gemm_schedule(cfg["schedule"])
+        if cfg.get("fp8_unscaled") is not None:
+            set_gemm_fp8_unscaled(cfg["fp8_unscaled"])
 
     def __enter__(self) -> "gemm_config":
         self.saved = get_gemm_config()

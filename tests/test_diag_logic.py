@@ -22,10 +22,10 @@ def test_mfma_burn_pass_and_each_failure_mode(fake):
     fake()
     r = diag.mfma_burn(0)
     assert r["pass"] and set(r["kinds"]) == {"bf16", "fp8", "mxfp8", "mxfp4"} and r["detail"] == ""
-    fake(mfma={0: (1900.0, 0), 1: (1950.0, 0), 2: (4300.0, 3), 3: (7600.0, 0)})
+    fake(mfma={0: (1900.0, 0), 1: (4350.0, 0), 2: (4300.0, 3), 3: (7600.0, 0)})
     r = diag.mfma_burn(0)
     assert not r["pass"] and r["detail"] == "mxfp8: 3 wrong results"
-    fake(mfma={0: (400.0, 0), 1: (1950.0, 0), 2: (4300.0, 0), 3: (7600.0, 0)})
+    fake(mfma={0: (400.0, 0), 1: (4350.0, 0), 2: (4300.0, 0), 3: (7600.0, 0)})
     assert diag.mfma_burn(0)["detail"] == "bf16 400 TFLOP/s = 21% of 1.9e+03"
 
 

@@ -246,11 +246,51 @@ def test_v3_bf16_output_and_fused_checksums_match(dev, m, n, k):
         diag.gemm_launch_ck("bf16", x.data_ptr(), y.data_ptr(), 0, 0, 256, 256, 128)
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (1024, 768, 4096), (2048, 2048, 2048)])
+def test_fp8_gemm_mfma_forms_are_bit_identical(dev, m, n, k):
+    """The fp8 v3 GEMM on the unscaled v_mfma_f32_16x16x128_f8f6f4 (the default, hipBLASLt's form) and on the
+    scaled MX form with unit scales: the same fp32 C, bf16 C and fused column sums, bit for bit, and within the
+    fp8 error bound of an fp64 reference."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + 3 * n + 5 * k)
+    st = torch.cuda.current_stream().cuda_stream
+    x = torch.randn(m, k, device=dev, generator=g).to(torch.float8_e4m3fn)
+    y = torch.randn(n, k, device=dev, generator=g).to(torch.float8_e4m3fn)
+    outs = {}
+    for unscaled in (True, False):
+        with diag.gemm_config(variant="v3", fp8_unscaled=unscaled):
+            assert diag.get_gemm_fp8_unscaled() is unscaled
+            c32 = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+            diag.gemm_fp8_launch(x.data_ptr(), y.data_ptr(), c32.data_ptr(), m, n, k, st)
+            c16 = torch.full((m, n), float("nan"), device=dev, dtype=torch.bfloat16)
+            cs = torch.full((m // 128, n), float("nan"), device=dev, dtype=torch.float64)
+            diag.gemm_launch_ck("fp8", x.data_ptr(), y.data_ptr(), c16.data_ptr(), cs.data_ptr(), m, n, k, st)
+            torch.cuda.synchronize()
+            outs[unscaled] = (c32, c16, cs)
+    assert diag.get_gemm_fp8_unscaled() is True  # restored
+    for a, b in zip(outs[True], outs[False]):
+        assert torch.equal(a, b)
+    ref = x.double() @ y.double().t()
+    mag = x.double().abs() @ y.double().abs().t()
+    assert ((outs[True][0].double() - ref).abs() / mag.clamp_min(1e-30)).max().item() < diag.GEMM_FP8_MAX_ERR
+
+
+def test_fp8_burn_in_kind_runs_the_unscaled_f8f6f4_path_exactly(dev):
+    """The burn-in's fp8 kind (the unscaled f8f6f4 instruction) computes its exact integer sums on every CU at
+    the fp8 rate -- well above the bf16 rate the gfx94x-era instruction it replaced ran at."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = diag.mfma_burn(0)
+    fp8, bf16 = r["kinds"]["fp8"], r["kinds"]["bf16"]
+    assert fp8["errors"] == 0 and r["map"]["cus"] == 256
+    assert fp8["tflops"] > 1.5 * bf16["tflops"], r["kinds"]
+
+
 def test_mfma_gemm_large_auto_uses_v3_and_matches(dev):
     """4096^3 in auto mode runs the staggered v3 kernel; compare every output with a bf16-input,
     fp32-accumulate torch reference.  Runs with the production knobs (what the agent launches)."""
     from k8s_gpu_node_checker_amd.ops import diag
-    assert diag.get_gemm_config() == {"variant": "auto", "epilogue": True, "buffer_loads": False, "schedule": 1}
+    assert diag.get_gemm_config() == {"variant": "auto", "epilogue": True, "buffer_loads": False, "schedule": 1,
+                                     "fp8_unscaled": True}
     m = n = k = 4096
     g = torch.Generator(device=dev).manual_seed(4096)
     a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
