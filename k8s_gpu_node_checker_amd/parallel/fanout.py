@@ -269,11 +269,13 @@ def agent_addresses(slices: Sequence[Dict[str, Any]]) -> Dict[str, str]:
     for sl in slices:
         if not isinstance(sl, dict):
             continue
-        for ep in sl.get("endpoints") or []:
+        eps = sl.get("endpoints")
+        for ep in eps if isinstance(eps, list) else []:
             if not isinstance(ep, dict):
                 continue
             node = ep.get("nodeName")
-            addrs = [a for a in ep.get("addresses") or [] if isinstance(a, str) and a]
+            raw = ep.get("addresses")
+            addrs = [a for a in raw if isinstance(a, str) and a] if isinstance(raw, list) else []
             if not isinstance(node, str) or not node or not addrs:
                 continue
             cond = ep.get("conditions") if isinstance(ep.get("conditions"), dict) else {}

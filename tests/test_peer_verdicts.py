@@ -216,3 +216,56 @@ def test_unreadable_baseline_file_starts_empty(tmp_path):
     assert b.data == {}
     p.write_text(json.dumps({"schema": "other", "gpus": {"x": {}}}))
     assert B.Baselines(str(p)).data == {}
+
+
+# --- property tests --------------------------------------------------------------------------------------------
+
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+_fracs = st.floats(min_value=0.05, max_value=1.6, allow_nan=False)
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(_fracs, min_size=1, max_size=12), st.booleans())
+def test_peer_judgement_properties(fracs, numerics_bad):
+    """For any node: judging twice changes nothing; a GPU failing numerics always fails; a lone GPU gets the
+    absolute verdict; a node-wide finding is reported only when no GPU of that metric was failed by the floor;
+    a GPU at or above its peers' median is never failed on rate."""
+    def res(f, bad=False):
+        return diag._rated({}, {"tflops": 1228.0 * f}, {"tflops": 1228.0}, "TFLOP/s", not bad, "wrong" if bad else "")
+    pool = {d: {"gemm": res(f, numerics_bad and d == 0)} for d, f in enumerate(fracs)}
+    f1 = P.judge_node(pool)
+    snap = json.dumps(pool, sort_keys=True)
+    assert P.judge_node(pool) == f1 and json.dumps(pool, sort_keys=True) == snap
+    if numerics_bad:
+        assert pool[0]["gemm"]["pass"] is False
+    if len(fracs) == 1:
+        expect = diag.judge_rate(1228.0 * fracs[0], 1228.0)
+        r = pool[0]["gemm"]
+        assert (r["pass"], r["degraded"]) == ((False, False) if numerics_bad or expect == "fail" else
+                                              (True, expect == "degraded"))
+        return
+    import statistics as S
+    for d, f in enumerate(fracs):
+        others = S.median([x for j, x in enumerate(fracs) if j != d])
+        r = pool[d]["gemm"]
+        if f >= others and not (numerics_bad and d == 0):
+            assert r["pass"] or f < P.FAIL_FRACTION, (fracs, d, r)
+    for f in f1:
+        assert f["test"] == "gemm" and f["median_fraction"] < P.DEGRADED_FRACTION
+        assert f["max_fraction"] <= P.NODE_UNIFORM_SPREAD * f["min_fraction"] + 1e-9
+
+
+_json = st.recursive(st.none() | st.booleans() | st.integers() | st.text(max_size=8),
+                     lambda k: st.lists(k, max_size=4) | st.dictionaries(st.text(max_size=8), k, max_size=4),
+                     max_leaves=12)
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(st.dictionaries(st.sampled_from(["endpoints", "metadata", "x"]), _json | st.lists(
+    st.dictionaries(st.sampled_from(["addresses", "nodeName", "conditions"]), _json), max_size=4)), max_size=4))
+def test_agent_addresses_never_raises_on_untrusted_slices(slices):
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    out = fanout.agent_addresses(slices)
+    assert all(isinstance(k, str) and isinstance(v, str) and k and v for k, v in out.items())
