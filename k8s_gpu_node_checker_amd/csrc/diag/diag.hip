@@ -53,6 +53,7 @@ thread_local int g_gemm_buffer_loads = 0;  // v3 operand staging: 0 = global_loa
 // scaled form at 4096^3 and 8192^3 with bit-identical C, profiles/gemm_fp8_mfma_ab_mi355x.jsonl), 0 = the
 // v_mfma_scale_..._f8f6f4 MX path with unit E8M0 scales (kept for A/B)
 thread_local int g_gemm_fp8_unscaled = 1;
+thread_local int g_gemm_fp8_prio = 0;  // lab A/B: raised priority for the second wave group on the fp8 ck path
 thread_local int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3
                                        // kernels; measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
 
@@ -1289,16 +1290,17 @@ hipError_t enable_peer(int from, int to) {
   return e;
 }
 
-template <int DT, bool EPI, bool BUF, int SCHED = 1, int OUT = OUT_F32>
+template <int DT, bool EPI, bool BUF, int SCHED = 1, int OUT = OUT_F32, bool PRIO = DT == DT_BF16>
 int launch_v3_inst(const void* A, const void* Bt, void* C, double* csum, int M, int N, int Kcols,
                    hipStream_t stream) {
   static LdsAttrOnce attr;
-  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI, BUF, SCHED, OUT>),
+  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_v3_kernel<DT, EPI, BUF, SCHED, OUT, PRIO>),
                          2 * V2_STAGE_BYTES, "gemm v3") != 0)
     return -1;
   const int nwg = (M / V2_BM) * (N / V2_BN);
-  hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI, BUF, SCHED, OUT>), dim3(nwg), dim3(V2_THREADS), 2 * V2_STAGE_BYTES,
-                     stream, static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, csum, M, N, Kcols);
+  hipLaunchKernelGGL((gemm_v3_kernel<DT, EPI, BUF, SCHED, OUT, PRIO>), dim3(nwg), dim3(V2_THREADS),
+                     2 * V2_STAGE_BYTES, stream, static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C,
+                     csum, M, N, Kcols);
   return 0;
 }
 template <int DT, bool EPI, bool BUF, int SCHED = 1>
@@ -1315,9 +1317,12 @@ int launch_v3_ck(const void* A, const void* Bt, __bf16* C, double* csum, int M, 
              : launch_v3_inst<DT, true, false, 1, OUT_BF16_CK>(A, Bt, C, csum, M, N, Kcols, stream);
 }
 
-// fp8 operands on the MFMA form the thread's knob picks (g_gemm_fp8_unscaled)
+// fp8 operands on the MFMA form the thread's knob picks (g_gemm_fp8_unscaled); g_gemm_fp8_prio (lab knob, A/B
+// only) raises the second wave group's priority as the bf16 kernel does
 int launch_v3_ck_fp8(const void* A, const void* Bt, __bf16* C, double* csum, int M, int N, int Kcols,
                      hipStream_t stream) {
+  if (g_gemm_fp8_prio && g_gemm_fp8_unscaled && g_gemm_schedule == 1)
+    return launch_v3_inst<DT_FP8U, true, false, 1, OUT_BF16_CK, true>(A, Bt, C, csum, M, N, Kcols, stream);
   return g_gemm_fp8_unscaled ? launch_v3_ck<DT_FP8U>(A, Bt, C, csum, M, N, Kcols, stream)
                              : launch_v3_ck<DT_FP8>(A, Bt, C, csum, M, N, Kcols, stream);
 }
@@ -1512,6 +1517,7 @@ void diag_set_gemm_buffer_loads(int b) { g_gemm_buffer_loads = b; }
 void diag_set_gemm_schedule(int s) { g_gemm_schedule = s; }
 int diag_get_gemm_schedule(void) { return g_gemm_schedule; }
 void diag_set_gemm_fp8_unscaled(int u) { g_gemm_fp8_unscaled = u ? 1 : 0; }
+void diag_set_gemm_fp8_prio(int p) { g_gemm_fp8_prio = p ? 1 : 0; }
 int diag_get_gemm_fp8_unscaled(void) { return g_gemm_fp8_unscaled; }
 int diag_get_gemm_variant(void) { return g_gemm_variant; }
 int diag_get_gemm_epilogue(void) { return g_gemm_epilogue; }

@@ -34,6 +34,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--sizes", default="4096,8192")
+    ap.add_argument("--prio", action="store_true", help="also the unscaled form with the second group's raised priority")
     args = ap.parse_args()
     st = torch.cuda.current_stream().cuda_stream
     one = torch.ones((), device="cuda")
@@ -47,14 +48,17 @@ def main() -> int:
                     torch.empty(n // 128, n, device="cuda", dtype=torch.float64)) for k in ("scaled", "unscaled")}
 
         def ours(form):
-            c, cs = outs[form]
+            c, cs = outs[form.replace("_prio", "")]
 
             def run():
-                diag.set_gemm_fp8_unscaled(form == "unscaled")
+                diag.set_gemm_fp8_unscaled(form.startswith("unscaled"))
+                diag.lib().diag_set_gemm_fp8_prio(1 if form.endswith("_prio") else 0)
                 diag.gemm_launch_ck("fp8", x.data_ptr(), y.data_ptr(), c.data_ptr(), cs.data_ptr(), n, n, n, st)
             return run
         runs = {"scaled": ours("scaled"), "unscaled": ours("unscaled"),
                 "hipblaslt": lambda: torch._scaled_mm(x, yt, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)}
+        if args.prio:
+            runs["unscaled_prio"] = ours("unscaled_prio")
         runs["scaled"]()
         runs["unscaled"]()
         torch.cuda.synchronize()
@@ -65,11 +69,12 @@ def main() -> int:
         for _ in range(args.rounds):
             for k, fn in runs.items():
                 tf[k].append(2.0 * n ** 3 / timed(fn, iters) / 1e9)
-        diag.set_gemm_fp8_unscaled(False)
+        diag.set_gemm_fp8_unscaled(True)
+        diag.lib().diag_set_gemm_fp8_prio(0)
         med = {k: round(statistics.median(v), 1) for k, v in tf.items()}
         print(json.dumps({"size": n, "rounds": args.rounds, "median_tflops": med,
                           "best_tflops": {k: round(max(v), 1) for k, v in tf.items()},
-                          "fraction_of_hipblaslt": {k: round(med[k] / med["hipblaslt"], 3) for k in ("scaled", "unscaled")},
+                          "fraction_of_hipblaslt": {k: round(med[k] / med["hipblaslt"], 3) for k in med if k != "hipblaslt"},
                           "outputs_identical": same, "rel_err_vs_hipblaslt_fp32": err}), flush=True)
     return 0
 
