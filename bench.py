@@ -262,21 +262,27 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
         torch.cuda.set_device(local_rank)
     group = None
     if world > 1:
-        if cuda:  # device_id binds the group to this rank's GPU (eager RCCL init, no device guessing)
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        from datetime import timedelta
+        if cuda:
+            # RCCL carries only the fabric check (an untimed extra): the group is created lazily, so its
+            # communicator -- and comgr's cold code-object load -- is paid inside the extras budget or not at all,
+            # and a collective that hangs raises at the timeout instead of killing the rank (CleanUpOnly)
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+            dist.init_process_group("nccl", timeout=timedelta(seconds=max(30.0, min(300.0, budget.left()))))
         else:
             dist.init_process_group("gloo")
-        group = dist.new_group(backend="gloo")  # control-plane objects (URLs, reports)
+        # control plane (URLs, decisions, the timing barriers and the MAX over ranks): gloo on the CPU, with room
+        # for rank 0's node cycle (up to the whole extras budget) at the barrier the others wait at
+        group = dist.new_group(backend="gloo", timeout=timedelta(seconds=budget.total + 600.0))
         box = [ctrl]
         dist.broadcast_object_list(box, src=0, group=group)
         ctrl = box[0]
 
     def barrier():
+        if cuda:
+            torch.cuda.synchronize()
         if world > 1:
-            if cuda:
-                dist.barrier(device_ids=[local_rank])
-            else:
-                dist.barrier()
+            dist.barrier(group=group)  # gloo: the timed region never waits on an RCCL communicator
         if cuda:
             torch.cuda.synchronize()
 
@@ -381,8 +387,8 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
 
     if world > 1:
         import torch as _t
-        t = _t.tensor([elapsed], dtype=_t.float64, device=f"cuda:{local_rank}" if cuda else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = _t.tensor([elapsed], dtype=_t.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)  # the slowest rank's clock (gloo, CPU tensor)
         elapsed = float(t.item())
 
     if rank == 0:
