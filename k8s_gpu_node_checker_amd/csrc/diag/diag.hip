@@ -53,7 +53,6 @@ thread_local int g_gemm_buffer_loads = 0;  // v3 operand staging: 0 = global_loa
 // scaled form at 4096^3 and 8192^3 with bit-identical C, profiles/gemm_fp8_mfma_ab_mi355x.jsonl), 0 = the
 // v_mfma_scale_..._f8f6f4 MX path with unit E8M0 scales (kept for A/B)
 thread_local int g_gemm_fp8_unscaled = 1;
-thread_local int g_gemm_fp8_prio = 0;  // lab A/B: raised priority for the second wave group on the fp8 ck path
 thread_local int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3
                                        // kernels; measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
 
@@ -543,7 +542,7 @@ __device__ unsigned long long g_gemm_stamps[8][2][4][4];
 // pass over C and keeps the accumulators' precision.
 enum GemmOut { OUT_F32 = 0, OUT_BF16_CK = 1 };
 template <int DT, bool EPI_LDS = false, bool BUF = false, int SCHED = 1, int OUT = OUT_F32,
-          bool PRIO_G1 = DT == DT_BF16>
+          bool PRIO_G1 = DT == DT_BF16 || DT == DT_FP8U>
 __global__ void __launch_bounds__(V2_THREADS, 1)
 gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv,
                double* __restrict__ csum, int M, int N, int K) {
@@ -593,9 +592,10 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
   }
   STG_BARRIER();
   if (wr == 1) STG_BARRIER();  // the stagger
-  // bf16: the second wave group (waves 4-7, one barrier behind) issues at raised priority for the whole loop,
-  // so on each SIMD its load slot is not starved behind the other group's MFMA stream (+2-3 % at 4096^3 and
-  // 8192^3; neutral-to-negative for MX-fp8, profiles/gemm_schedule_ab_mi355x.jsonl); per-slot priority flips
+  // bf16 and fp8 (unscaled MFMA): the second wave group (waves 4-7, one barrier behind) issues at raised priority
+  // for the whole loop, so on each SIMD its load slot is not starved behind the other group's MFMA stream (bf16
+  // +2-3 % at 4096^3 and 8192^3, profiles/gemm_schedule_ab_mi355x.jsonl; fp8 unscaled +0.7-1.1 %,
+  // profiles/gemm_fp8_prio_ab_mi355x.jsonl; neutral-to-negative for the scaled MX form); per-slot priority flips
   // measured below it
   if constexpr (PRIO_G1) {
     if (wr == 1) __builtin_amdgcn_s_setprio(1);
@@ -1290,7 +1290,7 @@ hipError_t enable_peer(int from, int to) {
   return e;
 }
 
-template <int DT, bool EPI, bool BUF, int SCHED = 1, int OUT = OUT_F32, bool PRIO = DT == DT_BF16>
+template <int DT, bool EPI, bool BUF, int SCHED = 1, int OUT = OUT_F32, bool PRIO = DT == DT_BF16 || DT == DT_FP8U>
 int launch_v3_inst(const void* A, const void* Bt, void* C, double* csum, int M, int N, int Kcols,
                    hipStream_t stream) {
   static LdsAttrOnce attr;
@@ -1317,12 +1317,10 @@ int launch_v3_ck(const void* A, const void* Bt, __bf16* C, double* csum, int M, 
              : launch_v3_inst<DT, true, false, 1, OUT_BF16_CK>(A, Bt, C, csum, M, N, Kcols, stream);
 }
 
-// fp8 operands on the MFMA form the thread's knob picks (g_gemm_fp8_unscaled); g_gemm_fp8_prio (lab knob, A/B
-// only) raises the second wave group's priority as the bf16 kernel does
+// fp8 operands on the MFMA form the thread's knob picks (g_gemm_fp8_unscaled); the unscaled form raises the second
+// wave group's priority as the bf16 kernel does
 int launch_v3_ck_fp8(const void* A, const void* Bt, __bf16* C, double* csum, int M, int N, int Kcols,
                      hipStream_t stream) {
-  if (g_gemm_fp8_prio && g_gemm_fp8_unscaled && g_gemm_schedule == 1)
-    return launch_v3_inst<DT_FP8U, true, false, 1, OUT_BF16_CK, true>(A, Bt, C, csum, M, N, Kcols, stream);
   return g_gemm_fp8_unscaled ? launch_v3_ck<DT_FP8U>(A, Bt, C, csum, M, N, Kcols, stream)
                              : launch_v3_ck<DT_FP8>(A, Bt, C, csum, M, N, Kcols, stream);
 }
@@ -1517,7 +1515,6 @@ void diag_set_gemm_buffer_loads(int b) { g_gemm_buffer_loads = b; }
 void diag_set_gemm_schedule(int s) { g_gemm_schedule = s; }
 int diag_get_gemm_schedule(void) { return g_gemm_schedule; }
 void diag_set_gemm_fp8_unscaled(int u) { g_gemm_fp8_unscaled = u ? 1 : 0; }
-void diag_set_gemm_fp8_prio(int p) { g_gemm_fp8_prio = p ? 1 : 0; }
 int diag_get_gemm_fp8_unscaled(void) { return g_gemm_fp8_unscaled; }
 int diag_get_gemm_variant(void) { return g_gemm_variant; }
 int diag_get_gemm_epilogue(void) { return g_gemm_epilogue; }

@@ -34,7 +34,6 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--sizes", default="4096,8192")
-    ap.add_argument("--prio", action="store_true", help="also the unscaled form with the second group's raised priority")
     args = ap.parse_args()
     st = torch.cuda.current_stream().cuda_stream
     one = torch.ones((), device="cuda")
@@ -48,17 +47,14 @@ def main() -> int:
                     torch.empty(n // 128, n, device="cuda", dtype=torch.float64)) for k in ("scaled", "unscaled")}
 
         def ours(form):
-            c, cs = outs[form.replace("_prio", "")]
+            c, cs = outs[form]
 
             def run():
-                diag.set_gemm_fp8_unscaled(form.startswith("unscaled"))
-                diag.lib().diag_set_gemm_fp8_prio(1 if form.endswith("_prio") else 0)
+                diag.set_gemm_fp8_unscaled(form == "unscaled")
                 diag.gemm_launch_ck("fp8", x.data_ptr(), y.data_ptr(), c.data_ptr(), cs.data_ptr(), n, n, n, st)
             return run
         runs = {"scaled": ours("scaled"), "unscaled": ours("unscaled"),
                 "hipblaslt": lambda: torch._scaled_mm(x, yt, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)}
-        if args.prio:
-            runs["unscaled_prio"] = ours("unscaled_prio")
         runs["scaled"]()
         runs["unscaled"]()
         torch.cuda.synchronize()
@@ -70,7 +66,6 @@ def main() -> int:
             for k, fn in runs.items():
                 tf[k].append(2.0 * n ** 3 / timed(fn, iters) / 1e9)
         diag.set_gemm_fp8_unscaled(True)
-        diag.lib().diag_set_gemm_fp8_prio(0)
         med = {k: round(statistics.median(v), 1) for k, v in tf.items()}
         print(json.dumps({"size": n, "rounds": args.rounds, "median_tflops": med,
                           "best_tflops": {k: round(max(v), 1) for k, v in tf.items()},
