@@ -98,6 +98,18 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
                     put("mi355x_gpu_diag_xcd_hbm_read_tbs", f'{lbl},xcd="{_esc(xcd)}"', v)
             for kind, row in ((res.get("kinds") or {}) if isinstance(res.get("kinds"), dict) else {}).items():
                 put("mi355x_gpu_diag_tflops", f'{lbl},test="{_esc(test)}",dtype="{_esc(kind)}"', row.get("tflops", 0))
+            # the GPU against its node's other GPUs (models/peers.py) and against its own baseline (models/baseline.py)
+            for src, metric in (("peers", "mi355x_gpu_diag_peer_ratio"), ("baseline", "mi355x_gpu_diag_baseline_ratio")):
+                ratios = (res.get(src) or {}).get("ratio") if isinstance(res.get(src), dict) else None
+                for m, v in (ratios.items() if isinstance(ratios, dict) else ()):
+                    if isinstance(v, (int, float)) and not isinstance(v, bool):
+                        put(metric, f'{lbl},test="{_esc(test)}",metric="{_esc(m)}"', v)
+    node_diag = rep.get("diag_node")
+    for f in (node_diag.get("findings") or []) if isinstance(node_diag, dict) else []:
+        # a shortfall every GPU shares: the median rate as a fraction of the MI355X reference
+        if isinstance(f, dict) and isinstance(f.get("median_fraction"), (int, float)):
+            put("mi355x_node_diag_shortfall_fraction", f'test="{_esc(f.get("test"))}",metric="{_esc(f.get("metric"))}"',
+                f["median_fraction"])
     fabric = (rep.get("fabric") or {}).get("p2p")
     if isinstance(fabric, dict) and isinstance(fabric.get("median_gbps"), (int, float)):
         put("mi355x_node_xgmi_p2p_gbps", 'stat="median"', fabric["median_gbps"])

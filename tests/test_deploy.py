@@ -160,7 +160,9 @@ def _rich_report():
     g.update(xgmi_error=0, xgmi_kb=[[1, 2]] * 1, cper={"fatal": 0, "uncorrected": 0, "corrected": 1},
              ecc_blocks={"umc": {"ce": 1, "ue": 0, "de": 0}}, gfx_activity=0,
              throttle={"s": 60, "thermal_pct": 0.0, "power_pct": 1.0, "prochot_pct": 0.0},
-             diag={"gemm": {"pass": True, "tflops": 1200.0, "fraction": 0.98, "checksum_bad_tiles": 0},
+             diag={"gemm": {"pass": True, "tflops": 1200.0, "fraction": 0.98, "checksum_bad_tiles": 0,
+                            "peers": {"gpus": 2, "ratio": {"tflops": 1.01}},
+                            "baseline": {"ratio": {"tflops": 0.99}, "runs": 5}},
                    "gemm_fp8": {"pass": True, "tflops": 2300.0, "checksum_bad_tiles": 0},
                    "mfma": {"pass": True, "kinds": {"bf16": {"tflops": 1900.0, "errors": 0}}},
                    "hbm": {"pass": True, "copy_tbs": 6.4, "read_tbs": 7.0},
@@ -169,6 +171,8 @@ def _rich_report():
              bad_pages_unreservable=0, bad_page_threshold=2048, ecc_ce_per_h=1.5)
     r["fabric"] = {"p2p": {"pass": True, "median_gbps": 50.0, "min_gbps": 48.0},
                    "rccl": {"pass": True, "best_busbw_by_op": {"all_reduce": 300.0}}}
+    r["diag_node"] = {"findings": [{"test": "hbm", "metric": "copy_tbs", "median_fraction": 0.9,
+                                    "min_fraction": 0.89, "max_fraction": 0.91, "gpus": 2, "below_floor": False}]}
     return r
 
 

@@ -269,3 +269,16 @@ def test_agent_addresses_never_raises_on_untrusted_slices(slices):
     from k8s_gpu_node_checker_amd.parallel import fanout
     out = fanout.agent_addresses(slices)
     assert all(isinstance(k, str) and isinstance(v, str) and k and v for k, v in out.items())
+
+
+def test_agent_metrics_carry_peer_ratios_and_node_wide_findings(node):
+    from prometheus_client.parser import text_string_to_metric_families
+    node(8, rate=0.88, gpu_rate={3: 0.70})
+    rep = _agent(8).probe_once()
+    fams = {f.name: f for f in text_string_to_metric_families(A._metrics(rep))}
+    ratios = {(s.labels["gpu"], s.labels["test"], s.labels["metric"]): s.value
+              for s in fams["mi355x_gpu_diag_peer_ratio"].samples}
+    assert ratios[("3", "gemm", "tflops")] == pytest.approx(0.70 / 0.88, abs=0.01)
+    assert ratios[("0", "gemm", "tflops")] == pytest.approx(1.0, abs=0.01)
+    short = {(s.labels["test"], s.labels["metric"]): s.value for s in fams["mi355x_node_diag_shortfall_fraction"].samples}
+    assert short[("gemm", "tflops")] == pytest.approx(0.88, abs=0.01)

@@ -25,7 +25,7 @@ ROWS = [
          [('mi355x_node_health{state!="healthy"} == 1', "{{node}} {{state}}")], 24, 6),
     ]),
     ("Diagnostics (idle GPUs, every --diag-interval)", [
-        ("bf16 / MX-fp8 GEMM TFLOP/s", "timeseries", "none",
+        ("bf16 / fp8 GEMM TFLOP/s", "timeseries", "none",
          [('mi355x_gpu_diag_tflops{test=~"gemm.*"}', "{{node}} gpu{{gpu}} {{test}}")], 12, 7),
         ("Matrix-core burn-in TFLOP/s by precision", "timeseries", "none",
          [('mi355x_gpu_diag_tflops{test="mfma"}', "{{node}} gpu{{gpu}} {{dtype}}")], 12, 7),
@@ -34,8 +34,14 @@ ROWS = [
           ('mi355x_gpu_diag_copy_tbs{test="hbm"}', "{{node}} gpu{{gpu}} copy")], 12, 7),
         ("HBM read TB/s per XCD, each alone", "timeseries", "none",
          [("mi355x_gpu_diag_xcd_hbm_read_tbs", "{{node}} gpu{{gpu}} xcd{{xcd}}")], 12, 7),
-        ("Diagnostic rates as a share of their reference (fails below 0.85, degraded below 0.95)", "timeseries",
-         "percentunit", [("mi355x_gpu_diag_fraction", "{{node}} gpu{{gpu}} {{test}}")], 24, 7),
+        ("Diagnostic rates as a share of their reference (a lone GPU fails below 0.85, degraded below 0.95)",
+         "timeseries", "percentunit", [("mi355x_gpu_diag_fraction", "{{node}} gpu{{gpu}} {{test}}")], 24, 7),
+        ("Each GPU against its node's other GPUs (fails below 0.85)", "timeseries", "percentunit",
+         [("mi355x_gpu_diag_peer_ratio", "{{node}} gpu{{gpu}} {{test}} {{metric}}")], 12, 7),
+        ("Each GPU against its own baseline (drift below 0.90)", "timeseries", "percentunit",
+         [("mi355x_gpu_diag_baseline_ratio", "{{node}} gpu{{gpu}} {{test}} {{metric}}")], 12, 7),
+        ("Node-wide shortfalls: every GPU slow alike (share of the reference)", "timeseries", "percentunit",
+         [("mi355x_node_diag_shortfall_fraction", "{{node}} {{test}} {{metric}}")], 24, 6),
         ("Diagnostics skipped (GPU busy or allocated)", "timeseries", "none",
          [("mi355x_gpu_diag_skipped", "{{node}} gpu{{gpu}}")], 12, 6),
         ("Wrong results found by the diagnostics (words, lanes; GEMM output tiles failing their checksums)",
