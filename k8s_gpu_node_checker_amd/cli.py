@@ -326,7 +326,7 @@ def _watch_events(args: Any) -> int:
         try:
             while not elector.leading.wait(0.2):
                 pass
-            if elector.inherited_state is not None:
+            if elector.inherited_state:  # {}: the previous holder's state was too large to keep on the Lease
                 memo["prev"] = elector.inherited_state
             if metrics is not None:
                 metrics.set_leader(True)

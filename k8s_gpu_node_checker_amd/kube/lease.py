@@ -40,6 +40,8 @@ LEASE_DURATION_S = 15.0  # client-go defaults (kube-controller-manager, kube-sch
 RENEW_DEADLINE_S = 10.0
 RETRY_PERIOD_S = 2.0
 STATE_ANNOTATION = "gpu-health.amd.com/leader-state"
+# the apiserver caps an object's annotations at 256 KiB: a state larger than this is not kept on the Lease
+STATE_MAX_BYTES = 64 << 10
 
 
 def _micro_time(epoch: float) -> str:
@@ -221,11 +223,16 @@ class LeaderElector:
         self._thread.start()
         return self
 
-    def publish_state(self, state: Dict[str, Any]) -> None:
-        """Keep ``state`` (JSON) on the Lease: written by the next renewal, which is started right away."""
+    def publish_state(self, state: Dict[str, Any]) -> bool:
+        """Keep ``state`` (JSON) on the Lease: written by the next renewal, which is started right away.  A state
+        over ``STATE_MAX_BYTES`` (a cluster with thousands of not-Ready node names) is not kept -- the Lease's
+        annotations must stay small -- and the previous one is dropped; False then."""
+        text = json.dumps(state, sort_keys=True, separators=(",", ":"))
+        fits = len(text) <= STATE_MAX_BYTES
         with self._state_lock:
-            self._state = json.dumps(state, sort_keys=True, separators=(",", ":"))
+            self._state = text if fits else "{}"
         self._wake.set()
+        return fits
 
     def stop(self, timeout: float = 5.0) -> None:
         """Stop campaigning; a holder releases the Lease on the way out."""

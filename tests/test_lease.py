@@ -232,3 +232,20 @@ def test_a_watcher_that_cannot_renew_stops_acting_and_exits(mock_cluster, sink, 
         if a.poll() is None:
             a.kill()
             a.communicate(timeout=10)
+
+
+def test_an_oversized_leader_state_is_not_kept_on_the_lease(mock_cluster):
+    from k8s_gpu_node_checker_amd.kube import lease as L
+    srv = mock_cluster(fixtures.cluster(1, "amd"))
+    a = _elector(srv, "a").start()
+    try:
+        assert _wait(a.leading.is_set)
+        assert a.publish_state({"exit_code": 3, "not_ready": ["n"]}) is True
+        assert _wait(lambda: '"not_ready":["n"]' in (srv.leases[("gpu-health", "gpu-node-watcher")]["metadata"]
+                                                       .get("annotations") or {}).get(L.STATE_ANNOTATION, ""))
+        big = {"exit_code": 3, "not_ready": [f"node-{i:06d}" for i in range(10000)]}
+        assert a.publish_state(big) is False
+        assert _wait(lambda: srv.leases[("gpu-health", "gpu-node-watcher")]["metadata"]["annotations"]
+                     [L.STATE_ANNOTATION] == "{}")
+    finally:
+        a.stop()
