@@ -128,7 +128,14 @@ class MetricsServer:
                 self.end_headers()
                 self.wfile.write(body)
 
-        self.httpd = ThreadingHTTPServer((host, port), Handler)
+        server_cls = ThreadingHTTPServer
+        if ":" in host:  # an IPv6 address ("::" for every interface)
+            import socket
+
+            class V6(ThreadingHTTPServer):
+                address_family = socket.AF_INET6
+            server_cls = V6
+        self.httpd = server_cls((host, port), Handler)
         self.httpd.daemon_threads = True
         self._thread = threading.Thread(target=self.httpd.serve_forever, kwargs={"poll_interval": 0.2},
                                         name="metrics", daemon=True)
