@@ -30,7 +30,16 @@ def _age(seconds: Optional[float]) -> str:
     return f"{seconds / 3600:.1f} h"
 
 
-_COLUMNS = ("GPU", "BDF", "gfx", "CUs", "VRAM MB", "ECC ue/ce", "xGMI", "PM fw", "diag", "findings")
+_COLUMNS = ("GPU", "BDF", "gfx", "CUs", "VRAM MB", "ECC ue/ce", "xGMI", "PM fw", "diag", "vs peers", "findings")
+
+
+def _min_ratio(diag: Dict[str, Any], key: str) -> Any:
+    """The lowest rate ratio of a GPU's diagnostics against its node's other GPUs (``peers``) or its own
+    baseline (``baseline``), None when no test was judged that way."""
+    vals = [v for r in diag.values() if isinstance(r, dict) and isinstance(r.get(key), dict)
+            for v in ((r[key].get("ratio") or {}) if isinstance(r[key].get("ratio"), dict) else {}).values()
+            if isinstance(v, (int, float)) and not isinstance(v, bool)]
+    return round(min(vals), 3) if vals else None
 
 
 def _gpu_entry(g: Dict[str, Any], verdict_lines: List[str]) -> Dict[str, Any]:
@@ -44,6 +53,7 @@ def _gpu_entry(g: Dict[str, Any], verdict_lines: List[str]) -> Dict[str, Any]:
             "diag_failed": sorted(t for t, r in diag.items() if isinstance(r, dict) and r.get("pass") is False),
             "diag_slow": sorted(t for t, r in diag.items() if isinstance(r, dict) and r.get("degraded")),
             "diag_ran": bool(diag),
+            "peer_ratio_min": _min_ratio(diag, "peers"), "baseline_ratio_min": _min_ratio(diag, "baseline"),
             "findings": [ln.split(": ", 1)[1] for ln in verdict_lines if ln.startswith(f"gpu{idx}:")]}
 
 
@@ -54,7 +64,9 @@ def _gpu_row(e: Dict[str, Any]) -> List[str]:
         ("slow: " + ",".join(e["diag_slow"])) if e["diag_slow"] else ("pass" if e["diag_ran"] else "-")
     return [txt(e["index"]), txt(e["bdf"]), txt(e["gfx"]), txt(e["cus"]), txt(e["vram_mb"]),
             f"{txt(e['ecc_uncorrectable'], '-')}/{txt(e['ecc_correctable'], '-')}", txt(e["xgmi"]),
-            txt(e["pm_fw"], "-"), dstate, "; ".join(e["findings"]) or "ok"]
+            txt(e["pm_fw"], "-"), dstate,
+            f"x{e['peer_ratio_min']:.2f}" if isinstance(e.get("peer_ratio_min"), (int, float)) else "-",
+            "; ".join(e["findings"]) or "ok"]
 
 
 def gpu_table(entries: List[Dict[str, Any]]) -> List[str]:

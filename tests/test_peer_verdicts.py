@@ -282,3 +282,16 @@ def test_agent_metrics_carry_peer_ratios_and_node_wide_findings(node):
     assert ratios[("0", "gemm", "tflops")] == pytest.approx(1.0, abs=0.01)
     short = {(s.labels["test"], s.labels["metric"]): s.value for s in fams["mi355x_node_diag_shortfall_fraction"].samples}
     assert short[("gemm", "tflops")] == pytest.approx(0.88, abs=0.01)
+
+
+def test_status_table_shows_each_gpus_lowest_ratio_to_its_peers(node):
+    from k8s_gpu_node_checker_amd.explain import report_text
+    node(4, gpu_rate={2: 0.80})
+    ag = _agent(4)
+    rep = ag.probe_once()
+    text = report_text(rep, ag.evaluate(rep))
+    head = next(ln for ln in text.splitlines() if "vs peers" in ln)
+    row2 = next(ln for ln in text.splitlines() if ln.strip().startswith("2 "))
+    row0 = next(ln for ln in text.splitlines() if ln.strip().startswith("0 "))
+    assert "x0.80" in row2 and "fail:" in row2 and "x1.00" in row0
+    assert head.index("vs peers") < head.index("findings")
