@@ -107,10 +107,13 @@ class Baselines:
                 if not fr:
                     continue
                 key = _shape(test, res)
-                entry = per.setdefault(key, {"samples": []})
+                entry = per.get(key)
+                if not isinstance(entry, dict):
+                    entry = per[key] = {"samples": []}
                 base = entry.get("baseline")
                 if isinstance(base, dict):
-                    ratios = {m: round(v / base[m], 3) for m, v in fr.items() if base.get(m)}
+                    ratios = {m: round(v / base[m], 3) for m, v in fr.items()
+                              if isinstance(base.get(m), (int, float)) and base[m] > 0}
                     res["baseline"] = {"ratio": ratios, "runs": entry.get("runs", self.runs)}
                     drift = [f"{m} at {r:.0%} of this GPU's own baseline ({entry.get('runs', self.runs)} clean runs)"
                              for m, r in sorted(ratios.items()) if r < self.drift_ratio]
@@ -122,6 +125,8 @@ class Baselines:
                     continue
                 clean = res.get("pass") is True and not res.get("degraded") and not res.get("numerics")
                 if clean:
+                    samples = entry.get("samples")  # a hand-edited or truncated file: keep what is well-formed
+                    entry["samples"] = [s for s in samples if isinstance(s, dict)] if isinstance(samples, list) else []
                     entry["samples"].append({m: round(v, 4) for m, v in fr.items()})
                     changed = True
                     if len(entry["samples"]) >= self.runs:

@@ -218,6 +218,22 @@ def test_unreadable_baseline_file_starts_empty(tmp_path):
     assert B.Baselines(str(p)).data == {}
 
 
+def test_malformed_baseline_entries_are_rebuilt_not_fatal(tmp_path):
+    p = tmp_path / "b.json"
+    res = lambda: {"pass": True, "rates": {"tflops": 1000.0}, "expect": {"tflops": 1000.0},  # noqa: E731
+                   "shape": [1, 1, 1]}
+    p.write_text(json.dumps({"schema": B.SCHEMA, "gpus": {
+        "a": {"gemm@[1,1,1]": ["not", "a", "dict"]},
+        "b": {"gemm@[1,1,1]": {"samples": "junk"}},
+        "c": {"gemm@[1,1,1]": {"samples": [1, {"tflops": 1.0}]}},
+        "d": {"gemm@[1,1,1]": {"baseline": {"tflops": 0}, "runs": 5}}}}))
+    b = B.Baselines(str(p), runs=2)
+    for gpu in "abcd":
+        assert b.observe(gpu, {"gemm": res()}) == []
+    assert b.baseline("c", "gemm", res()) == {"tflops": 1.0}  # the one well-formed sample + this run
+    assert b.baseline("a", "gemm", res()) is None and b.baseline("b", "gemm", res()) is None
+
+
 # --- property tests --------------------------------------------------------------------------------------------
 
 from hypothesis import given, settings  # noqa: E402
