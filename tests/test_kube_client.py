@@ -1,5 +1,4 @@
 """kube-apiserver client: pagination, retries/backoff, errors, gzip, chunked, TLS (SURVEY §7.2 layer 2)."""
-import os
 import subprocess
 
 import pytest

@@ -1,5 +1,5 @@
 """One-off exploration: dump what amd-smi reports on the GPU box (non-root)."""
-import json, time, os, sys
+import json, time, os
 t0 = time.perf_counter()
 import amdsmi as A
 t1 = time.perf_counter()
