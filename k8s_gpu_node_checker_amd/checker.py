@@ -100,6 +100,8 @@ class CheckResult:
         self.verdicts = verdicts
         self.tracer = tracer
         self.slack_sent: Optional[bool] = None
+        #: the fleet-relative diagnostics summary (``models/fleet.judge_fleet``), when reports were judged
+        self.fleet_diag: Optional[Dict[str, Any]] = None
         #: operator-facing notes (stderr), e.g. thresholds that could not be applied to a node
         self.warnings: List[str] = []
 
@@ -129,6 +131,7 @@ class CheckResult:
             "mi355x": {
                 "health_summary": H.summarize(self.verdicts) if self.verdicts else None,
                 "fleet": fleet_versions(self.scan.extras),
+                "diag_fleet": self.fleet_diag,
                 "nodes": nodes,
             },
             "timings_ms": self.tracer.as_ms(),
@@ -211,8 +214,12 @@ def resolve_agent_endpoints(cluster: Optional[ClusterConnection], opts: CheckOpt
 
 def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
                  warnings: Optional[List[str]] = None,
-                 cluster: Optional[ClusterConnection] = None) -> List[Optional[H.Verdict]]:
+                 cluster: Optional[ClusterConnection] = None,
+                 fleet_out: Optional[Dict[str, Any]] = None) -> List[Optional[H.Verdict]]:
     """Evaluate MI355X probe reports and gate ``ready`` (no-op when no node carries one).
+
+    With three or more current reports the diagnostics' rates are also judged across the fleet
+    (``models/fleet.py``); ``fleet_out``, when given, receives its ``summary`` and the per-node ``views``.
 
     Every verdict is cross-checked against the node's ``amd.com/gpu`` count from this LIST
     (:func:`models.node.expected_gpu_count`): on the condition path through the ``ok/seen`` counts
@@ -241,28 +248,57 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
         max_age = opts.probe_max_age
         from_condition = H.verdict_from_condition
         gate = H.gate_ready
-        for node, ex, rep in zip(scan.gpu_nodes, scan.extras, reports):
-            cap, alloc = ex.capacity.get(key), ex.allocatable.get(key)
-            is_amd = alloc is not None or key in node["gpu_breakdown"]
-            expected = max(cap or 0, alloc or 0)  # models.node.expected_gpu_count
-            v: Optional[H.Verdict] = None
+        # pass 1: which report (if any) judges each node; the condition path needs none
+        judged: List[Optional[Dict[str, Any]]] = [None] * len(scan.gpu_nodes)
+        pre: List[Optional[H.Verdict]] = [None] * len(scan.gpu_nodes)
+        # reports the fleet judgement may compare: the judged ones, plus (when the scan parsed the annotations
+        # anyway, --json-extended / --explain / --fleet) those of nodes judged by their condition
+        compare: List[Optional[Dict[str, Any]]] = [None] * len(scan.gpu_nodes)
+        parsed = opts.json_extended
+        for i, (node, ex, rep) in enumerate(zip(scan.gpu_nodes, scan.extras, reports)):
             if rep is None and reeval:
                 rep = ex.report()
             if rep is None and ex.health_condition is not None:
+                if parsed and ex.health_annotation:
+                    r = ex.report()
+                    compare[i] = r if isinstance(r, dict) and r.get("node") in (None, node["name"]) else None
+                continue
+            if rep is None and ex.health_annotation:
+                rep = ex.report()
+            other = rep.get("node") if isinstance(rep, dict) else None
+            if other is not None and other != node["name"]:
+                # a report names the node it was taken on: one fetched from a reassigned or stale IP (or an
+                # annotation copied between nodes) says nothing about this node
+                pre[i] = H.Verdict(H.UNKNOWN, [f"report is for node {other}"])
+            else:
+                judged[i] = compare[i] = rep
+        # the fleet-relative judgement of the diagnostics' rates (models/fleet.py): only with 3+ reports to compare
+        fleet_views: List[Optional[Dict[str, Any]]] = [None] * len(scan.gpu_nodes)
+        if sum(1 for r in compare if isinstance(r, dict) and r.get("gpus")) >= 3:
+            from .models import fleet as F
+            current = [r if H.report_gate(r, exp, now) is None else None for r in compare]
+            summary, fleet_views = F.judge_fleet([n["name"] for n in scan.gpu_nodes], current)
+            if summary and fleet_out is not None:
+                fleet_out.update(summary=summary, views=fleet_views)
+        for i, (node, ex, rep) in enumerate(zip(scan.gpu_nodes, scan.extras, reports)):
+            cap, alloc = ex.capacity.get(key), ex.allocatable.get(key)
+            is_amd = alloc is not None or key in node["gpu_breakdown"]
+            expected = max(cap or 0, alloc or 0)  # models.node.expected_gpu_count
+            v: Optional[H.Verdict] = pre[i]
+            rep = judged[i]
+            if rep is None and fleet_views[i] is not None:
+                # the fleet has something to say about a node judged by its condition: its report carries the
+                # rates, the condition's message does not
+                rep = compare[i]
+            if v is not None:
+                pass
+            elif rep is None and ex.health_condition is not None:
                 # cheap path: the agent's verdict is a NodeCondition already parsed by the scan
                 v = from_condition(ex.health_condition, max_age, now, expected)
                 if reeval:
                     unapplied.append(node["name"])
-            else:
-                if rep is None and ex.health_annotation:
-                    rep = ex.report()
-                other = rep.get("node") if isinstance(rep, dict) else None
-                if other is not None and other != node["name"]:
-                    # a report names the node it was taken on: one fetched from a reassigned or stale IP (or an
-                    # annotation copied between nodes) says nothing about this node
-                    v = H.Verdict(H.UNKNOWN, [f"report is for node {other}"])
-                elif rep is not None or policy == "require":
-                    v = H.evaluate_report(rep, expected, exp, now)
+            elif rep is not None or policy == "require":
+                v = H.evaluate_report(rep, expected, exp, now, fleet_views[i])
             if v is None:
                 verdicts.append(None)
                 continue
@@ -310,10 +346,12 @@ def run_check(cluster: ClusterConnection, opts: CheckOptions, tracer: Optional[T
     tracer = tracer or (Tracer() if (opts.trace or opts.json_extended) else NullTracer())
     scan = scan_cluster(cluster, opts, tracer)
     warnings: List[str] = []
-    verdicts = apply_health(scan, opts, tracer, warnings, cluster)
+    fleet: Dict[str, Any] = {}
+    verdicts = apply_health(scan, opts, tracer, warnings, cluster, fleet)
     apply_schedulability(scan, opts)
     result = CheckResult(scan, verdicts, tracer)
     result.warnings = warnings
+    result.fleet_diag = fleet.get("summary")
     return result
 
 

@@ -290,8 +290,10 @@ def _watch_events(args: Any) -> int:
         def evaluate(scan):
             tr = Tracer() if (opts.trace or opts.json_extended) else NullTracer()
             warnings: list = []
-            result = CheckResult(scan, apply_health(scan, opts, tr, warnings, cluster), tr)
+            fleet: dict = {}
+            result = CheckResult(scan, apply_health(scan, opts, tr, warnings, cluster, fleet), tr)
             result.warnings = warnings
+            result.fleet_diag = fleet.get("summary")
             apply_schedulability(scan, opts)
             return result
 

@@ -108,7 +108,9 @@ def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> 
         return {"node": node_name, "gpu_node": False, "nodes_listed": scan.items_seen}
     i = names.index(node_name)
     node, ex = scan.gpu_nodes[i], scan.extras[i]
-    verdicts = apply_health(scan, opts, NullTracer(), [], cluster)
+    fleet: Dict[str, Any] = {}
+    verdicts = apply_health(scan, opts, NullTracer(), [], cluster, fleet)
+    view = (fleet.get("views") or [None] * len(names))[i]
     apply_schedulability(scan, opts)
     v = verdicts[i] if i < len(verdicts) else None
     now = time.time()
@@ -131,7 +133,8 @@ def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> 
     elif rep:
         drv = rep.get("driver") if isinstance(rep.get("driver"), dict) else {}
         re_v = H.evaluate_report(rep, max(ex.capacity.get("amd.com/gpu", 0), ex.allocatable.get("amd.com/gpu", 0)),
-                                 H.HealthExpectations(xgmi_links=opts.xgmi_links, max_age_s=opts.probe_max_age), now)
+                                 H.HealthExpectations(xgmi_links=opts.xgmi_links, max_age_s=opts.probe_max_age), now,
+                                 view)
         lines = re_v.reasons + re_v.warnings
         gpus = [_gpu_entry(g, lines) for g in H.report_gpus(rep) if isinstance(g, dict)]
         shown = {f"gpu{e['index']}:" for e in gpus}
@@ -140,6 +143,10 @@ def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> 
                          "gpus": gpus,
                          # findings not about one GPU of the table, incl. spans ("... gpu0-2,4-7 ...")
                          "node_findings": [ln for ln in lines if ln.split(" ", 1)[0] not in shown]}
+    if fleet.get("summary"):
+        # this node's place in the fleet (models/fleet.py): per test, the fleet's median and this node's ratio to it
+        from .models.fleet import explained_text
+        doc["fleet_diag"] = {"summary": fleet["summary"], "explained": explained_text(view) if view else []}
     doc["counts_as_ready"] = bool(node["ready"])
     return doc
 
@@ -180,6 +187,10 @@ def render(doc: Dict[str, Any], out: TextIO) -> None:
             out.write("  " + ln + "\n")
         for ln in rep["node_findings"]:
             out.write(f"  node: {ln}\n")
+    fd = doc.get("fleet_diag")
+    if fd:
+        for ln in fd["explained"]:
+            out.write(f"  fleet: {ln}\n")
     out.write(f"=> counts as Ready: {'yes' if doc['counts_as_ready'] else 'no'}\n")
 
 
@@ -222,7 +233,8 @@ def fleet(cluster: ClusterConnection, opts: CheckOptions, out: TextIO) -> int:
                                   "reasons": v.reasons if v else [], "warnings": v.warnings if v else []})
         out.write(json.dumps({"total_nodes": len(nodes), "ready_nodes": len(res.ready_gpu_nodes),
                               "verdicts": by_state, "without_verdict": unjudged, "attention": attention,
-                              "fleet": fleet_versions(res.scan.extras)}, indent=2, ensure_ascii=False) + "\n")
+                              "fleet": fleet_versions(res.scan.extras), "diag_fleet": res.fleet_diag},
+                             indent=2, ensure_ascii=False) + "\n")
         return res.exit_code
     out.write(f"GPU nodes: {len(nodes)}, counting as Ready: {len(res.ready_gpu_nodes)}\n")
     parts = [f"{n} {s}" for s, n in sorted(by_state.items(), key=lambda kv: ("healthy", "degraded", "unhealthy",
@@ -247,4 +259,13 @@ def fleet(cluster: ClusterConnection, opts: CheckOptions, out: TextIO) -> int:
             out.write("  driver: " + ", ".join(f"{k} x{c}" for k, c in sorted(fv["driver"].items())) + "\n")
         for image, row in fv["firmware"].items():
             out.write(f"  {image}: " + ", ".join(f"{k} x{c}" for k, c in sorted(row.items())) + "\n")
+    if res.fleet_diag:
+        out.write("diagnostics across the fleet (node medians, fraction of the MI355X reference):\n")
+        for test, row in res.fleet_diag.items():
+            out.write(f"  {test}: {row['nodes']} nodes, median {row['median_fraction']:.0%} "
+                      f"({row['min_fraction']:.0%}-{row['max_fraction']:.0%})"
+                      + ("  platform shortfall: nodes in line with it are not degraded for it"
+                         if row["platform_shortfall"] else "")
+                      + ("  outliers: " + ", ".join(f"{o['node']} x{o['ratio']:.2f}" for o in row["outliers"])
+                         if row["outliers"] else "") + "\n")
     return res.exit_code

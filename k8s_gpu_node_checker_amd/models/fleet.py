@@ -1,0 +1,164 @@
+"""Fleet-relative judgement of the active diagnostics' rates: each MI355X node against the other nodes of the
+same check.
+
+The node agent judges a GPU against the other GPUs of its node (``models/peers.py``) and against its own history
+(``models/baseline.py``); what it cannot see is the rest of the fleet.  Two verdicts need that view, and the
+checker has it -- one LIST carries every node's report:
+
+* **platform-wide shortfall** -- when the fleet's median node sits below the degraded line for a test and metric
+  (the whole fleet is a slower platform than the single boxes the references were measured on: its cooling,
+  power limits, firmware), a node in line with that median (within ``FLEET_UNIFORM_SPREAD``) is not degraded
+  for it: its node-wide finding and its GPUs' slow-only results (lone GPUs judged against the references) are
+  the platform's normal, not warnings.  The absolute failure floor stays: a GPU under ``FAIL_FRACTION`` of its
+  reference still fails, as the agent judged it;
+* **node outlier** -- a node whose median GPU is below ``FLEET_FAIL_RATIO`` of the median of the *other* nodes
+  gets a ``degraded`` finding naming the fleet median: all of its GPUs are slow alike (else the agent would
+  have singled one out), which is the node's condition -- cooling, power delivery, a BIOS setting -- and a
+  warning, never a failure.
+
+It needs at least ``FLEET_MIN_NODES`` nodes with results for the same test, shape and metric, and it needs the
+reports themselves (``--health-reeval``, ``--probe-endpoint``, or nodes that publish no condition): on the
+condition-only path the checker trusts the agents' verdicts as they are.  Reference analogue: the reference's
+verdict is a stable binary read off each node (``/root/reference/check-gpu-node.py:172-178``); this keeps the
+MI355X gate equally stable on a fleet whose platform differs from the reference boxes.
+"""
+
+from __future__ import annotations
+
+import statistics
+from typing import Any, Dict, List, Optional, Tuple
+
+from .peers import DEGRADED_FRACTION, FAIL_FRACTION, _rate_fractions
+
+FLEET_MIN_NODES = 3
+# a node below this share of the other nodes' median is an outlier (the per-GPU peer ratio, one level up)
+FLEET_FAIL_RATIO = 0.85
+# a node within this ratio of the fleet's median shares the fleet's condition
+FLEET_UNIFORM_SPREAD = 1.10
+
+Key = Tuple[str, str, str]  # (test, shape, metric)
+
+
+def _shape(res: Dict[str, Any]) -> str:
+    for k in ("shape", "gib", "slice_mib"):
+        if k in res:
+            return repr(res[k])
+    return ""
+
+
+def _gpu_results(report: Any):
+    gpus = report.get("gpus") if isinstance(report, dict) else None
+    for g in gpus if isinstance(gpus, list) else []:
+        diag = g.get("diag") if isinstance(g, dict) else None
+        if not isinstance(diag, dict):
+            continue
+        for test, res in diag.items():
+            if isinstance(res, dict):
+                fr = _rate_fractions(res)
+                if fr:
+                    yield g, test, res, fr
+
+
+def node_fractions(report: Any) -> Dict[Key, float]:
+    """``(test, shape, metric) -> the node's median GPU`` (rate as a fraction of its scaled reference)."""
+    per: Dict[Key, List[float]] = {}
+    for _g, test, res, fr in _gpu_results(report):
+        shape = _shape(res)
+        for m, v in fr.items():
+            per.setdefault((test, shape, m), []).append(v)
+    return {k: statistics.median(v) for k, v in per.items()}
+
+
+def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]]
+                ) -> Tuple[Dict[str, Any], List[Optional[Dict[str, Any]]]]:
+    """Judge every report's rate tests against the fleet.  The reports are not changed (the watcher keeps them
+    across checks); the judgement comes back as one view per node, which ``models/health.evaluate_report``
+    takes as ``fleet=``:
+
+    * ``findings`` -- this node is an outlier for a test and metric (a warning each);
+    * ``explained`` -- ``(test, shape, metric) -> {"fleet_fraction", "nodes"}``: the fleet is short alike there
+      and this node is in line with it, so its node-wide finding and its GPUs' slow-only results for it are
+      not warnings.
+
+    ``reports`` is parallel to ``names`` (None where a node has no report to judge); a node with nothing to say
+    gets None.  The summary, per test: node count, median, min and max fraction, the outliers and whether the
+    fleet is short alike."""
+    values: Dict[Key, Dict[int, float]] = {}
+    for i, rep in enumerate(reports):
+        if not isinstance(rep, dict):
+            continue
+        for key, v in node_fractions(rep).items():
+            values.setdefault(key, {})[i] = v
+    views: List[Optional[Dict[str, Any]]] = [None] * len(reports)
+
+    def view(i: int) -> Dict[str, Any]:
+        if views[i] is None:
+            views[i] = {"findings": [], "explained": {}}
+        return views[i]  # type: ignore[return-value]
+    summary: Dict[str, Any] = {}
+    for key in sorted(values):
+        vals = values[key]
+        if len(vals) < FLEET_MIN_NODES:
+            continue
+        med = statistics.median(vals.values())
+        platform_short = med < DEGRADED_FRACTION
+        row: Dict[str, Any] = {"nodes": len(vals), "median_fraction": round(med, 3),
+                               "min_fraction": round(min(vals.values()), 3),
+                               "max_fraction": round(max(vals.values()), 3), "platform_shortfall": platform_short,
+                               "outliers": []}
+        for i, v in vals.items():
+            others = statistics.median([x for j, x in vals.items() if j != i])
+            ratio = v / others if others > 0 else 1.0
+            if ratio < FLEET_FAIL_RATIO:
+                view(i)["findings"].append({"test": key[0], "metric": key[2], "node_fraction": round(v, 3),
+                                            "fleet_fraction": round(others, 3), "ratio": round(ratio, 3),
+                                            "nodes": len(vals) - 1})
+                row["outliers"].append({"node": names[i], "ratio": round(ratio, 3)})
+            elif platform_short and max(v, med) <= FLEET_UNIFORM_SPREAD * min(v, med):
+                view(i)["explained"][key] = {"fleet_fraction": round(med, 3), "nodes": len(vals)}
+        summary[f"{key[0]}{('@' + key[1]) if key[1] else ''}/{key[2]}"] = row
+    return summary, views
+
+
+def explains_node_finding(fleet: Optional[Dict[str, Any]], f: Dict[str, Any]) -> bool:
+    """A node-wide finding (``models/peers``) the fleet's own shortfall accounts for (not one below the floor)."""
+    if not fleet or not fleet.get("explained") or f.get("below_floor"):
+        return False
+    return any(k[0] == f.get("test") and k[2] == f.get("metric") for k in fleet["explained"])
+
+
+def explains_gpu_result(fleet: Optional[Dict[str, Any]], test: str, res: Dict[str, Any]) -> bool:
+    """A GPU's degraded result that is only slow -- no failure, lag or drift -- on metrics the fleet is short
+    alike on, with the GPU itself in line with the fleet's median."""
+    if not fleet or not fleet.get("explained"):
+        return False
+    if res.get("pass") is not True or not res.get("degraded") or res.get("lag") or res.get("drift"):
+        return False  # failures, and lag / drift notes, are the GPU's own whatever the fleet does
+    fr = _rate_fractions(res)
+    if not fr or min(fr.values()) < FAIL_FRACTION:
+        return False
+    shape = _shape(res)
+    for m, v in fr.items():
+        if v >= DEGRADED_FRACTION:
+            continue
+        ex = fleet["explained"].get((test, shape, m))
+        if not ex:
+            return False
+        med = ex["fleet_fraction"]
+        if max(v, med) > FLEET_UNIFORM_SPREAD * min(v, med):
+            return False
+    return True
+
+
+def explained_text(fleet: Dict[str, Any]) -> List[str]:
+    """What the fleet explained on this node, for ``--explain`` / ``--json-extended`` notes."""
+    return [f"diag {t} {m}: the fleet's median node is at {ex['fleet_fraction']:.0%} of the MI355X reference "
+            f"({ex['nodes']} nodes alike): the platform's normal, not this node's"
+            for (t, _s, m), ex in sorted(fleet.get("explained", {}).items())]
+
+
+def finding_text(f: Dict[str, Any]) -> str:
+    """One fleet outlier finding as a verdict warning."""
+    return (f"fleet: diag {f.get('test')} {f.get('metric')} at {f.get('ratio', 0):.0%} of the other "
+            f"{f.get('nodes')} nodes' median ({f.get('node_fraction', 0):.0%} vs {f.get('fleet_fraction', 0):.0%} of "
+            f"the MI355X reference): this node's cooling, power or firmware")

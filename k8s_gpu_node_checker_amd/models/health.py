@@ -338,9 +338,10 @@ def _age_s(stamp: Any, now: Optional[float]) -> Optional[float]:
     return None if t is None or now is None else now - t
 
 
-def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float] = None) -> Tuple[List[str], List[str]]:
+def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float] = None,
+                 fleet: Optional[Dict[str, Any]] = None) -> Tuple[List[str], List[str]]:
     """Return ``(failures, warnings)`` for one GPU entry of a probe report (``now``: the report's time,
-    against which record timestamps are aged)."""
+    against which record timestamps are aged; ``fleet``: the node's fleet view, ``models/fleet.py``)."""
     fail: List[str] = []
     warn: List[str] = []
     idx = g.get("index", "?")
@@ -465,6 +466,10 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float
                 detail = res.get("detail") or ""
                 fail.append(f"gpu{idx}: diag {test} failed" + (f" ({detail})" if detail else ""))
             elif isinstance(res, dict) and res.get("degraded"):  # 85-95 % of its reference rate (ops/diag.py)
+                if fleet:
+                    from .fleet import explains_gpu_result
+                    if explains_gpu_result(fleet, test, res):
+                        continue  # slow alike with the whole fleet: the platform's normal (models/fleet.py)
                 detail = res.get("detail") or ""
                 warn.append(f"gpu{idx}: diag {test} slow" + (f" ({detail})" if detail else ""))
     return fail, warn
@@ -476,19 +481,17 @@ def report_gpus(report: Any) -> List[Any]:
     return g if isinstance(g, list) else []
 
 
-def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
-                    exp: Optional[HealthExpectations] = None, now: Optional[float] = None) -> Verdict:
-    """The verdict on one probe report.  A report is untrusted input (an agent endpoint, an annotation): one
-    whose fields have the wrong types is ``unknown`` with the reason, never an exception out of the check."""
+def report_gate(report: Any, exp: Optional[HealthExpectations] = None,
+                now: Optional[float] = None) -> Optional[Verdict]:
+    """The ``unknown`` verdict for a report that cannot be judged at all -- none, not a JSON object, another
+    schema, stale or from the future, a failed probe, a malformed ``gpus`` -- else None (judge it)."""
     try:
-        return _evaluate_report(report, expected_gpus, exp, now)
+        return _report_gate(report, exp or HealthExpectations(), now)
     except (TypeError, ValueError, AttributeError, KeyError, IndexError, OverflowError) as e:
         return Verdict(UNKNOWN, [f"malformed probe report ({type(e).__name__}: {str(e)[:80]})"])
 
 
-def _evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
-                     exp: Optional[HealthExpectations] = None, now: Optional[float] = None) -> Verdict:
-    exp = exp or HealthExpectations()
+def _report_gate(report: Any, exp: HealthExpectations, now: Optional[float]) -> Optional[Verdict]:
     if not report:
         return Verdict(UNKNOWN, ["no probe report"])
     if not isinstance(report, dict):
@@ -510,13 +513,39 @@ def _evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
     gpus = report.get("gpus") or []
     if not isinstance(gpus, list):
         return Verdict(UNKNOWN, [f"malformed probe report (gpus is a JSON {type(gpus).__name__})"], age_s=age)
+    return None
+
+
+def evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
+                    exp: Optional[HealthExpectations] = None, now: Optional[float] = None,
+                    fleet: Optional[Dict[str, Any]] = None) -> Verdict:
+    """The verdict on one probe report.  A report is untrusted input (an agent endpoint, an annotation): one
+    whose fields have the wrong types is ``unknown`` with the reason, never an exception out of the check.
+    ``fleet`` is this node's view from ``models/fleet.judge_fleet`` (the checker's fleet-relative judgement)."""
+    try:
+        return _evaluate_report(report, expected_gpus, exp, now, fleet)
+    except (TypeError, ValueError, AttributeError, KeyError, IndexError, OverflowError) as e:
+        return Verdict(UNKNOWN, [f"malformed probe report ({type(e).__name__}: {str(e)[:80]})"])
+
+
+def _evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
+                     exp: Optional[HealthExpectations] = None, now: Optional[float] = None,
+                     fleet: Optional[Dict[str, Any]] = None) -> Verdict:
+    exp = exp or HealthExpectations()
+    gate = report_gate(report, exp, now)
+    if gate is not None:
+        return gate
+    now = time.time() if now is None else now
+    ts = report["ts"]  # type: ignore[index]
+    age = now - float(ts)
+    gpus = report.get("gpus") or []  # type: ignore[union-attr]
     fails: List[str] = []
     warns: List[str] = []
     ok = 0
     for g in gpus:
         if not isinstance(g, dict):
             continue
-        f, w = evaluate_gpu(g, exp, float(ts) if isinstance(ts, (int, float)) else now)
+        f, w = evaluate_gpu(g, exp, float(ts) if isinstance(ts, (int, float)) else now, fleet)
         fails += f
         warns += w
         ok += 0 if f else 1
@@ -534,7 +563,13 @@ def _evaluate_report(report: Optional[Dict[str, Any]], expected_gpus: int,
         # every GPU of the node slow alike (models/peers.judge_node): the node's condition, a warning, never a
         # GPU failure
         from .peers import finding_text
-        warns += [finding_text(f) for f in node_diag["findings"] if isinstance(f, dict)]
+        from .fleet import explains_node_finding
+        warns += [finding_text(f) for f in node_diag["findings"]
+                  if isinstance(f, dict) and not explains_node_finding(fleet, f)]
+    if fleet and fleet.get("findings"):
+        # the node against the fleet's other nodes (models/fleet.judge_fleet, in the checker): a warning too
+        from .fleet import finding_text as fleet_text
+        warns += [fleet_text(f) for f in fleet["findings"]]
     fabric = report.get("fabric")
     if isinstance(fabric, dict):
         for test, res in fabric.items():  # node-level: the xGMI pair matrix (ops/diag.p2p_matrix)

@@ -1,0 +1,163 @@
+"""Fleet-relative diagnostic verdicts (models/fleet.py): the checker judges each MI355X node's diagnostic rates
+against the other nodes of the same LIST.
+
+Agent reports come from whole agent cycles on the fake C ABI of libmi355x_diag.so (testing/fake_native.py), one
+agent per node; the checker reads them from node annotations served by the mock apiserver.  Reference: the
+verdict is a stable binary read off each node (/root/reference/check-gpu-node.py:172-178) -- a fleet whose
+platform is slower than the boxes the references were measured on must not page as degraded.
+"""
+import json
+
+import pytest
+
+from k8s_gpu_node_checker_amd.agent import agent as A
+from k8s_gpu_node_checker_amd.checker import CheckOptions, apply_health, scan_cluster
+from k8s_gpu_node_checker_amd.models import fleet as F
+from k8s_gpu_node_checker_amd.models import health as H
+from k8s_gpu_node_checker_amd.ops import amdsmi_probe, diag, fabric
+from k8s_gpu_node_checker_amd.testing import fixtures
+from k8s_gpu_node_checker_amd.testing.fake_native import FakeDiagLib, FakeFabricLib
+from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+from k8s_gpu_node_checker_amd.utils.timing import NullTracer
+
+
+@pytest.fixture
+def reports(monkeypatch):
+    """``reports({name: rate or {gpu: rate}}, gpus=8, **agent kw)`` -> {name: the agent's report}."""
+    def make(rates, gpus=8, **kw):
+        out = {}
+        monkeypatch.setattr(fabric, "_lib", FakeFabricLib())
+        monkeypatch.setattr(amdsmi_probe, "probe", lambda nd, src, fx: fixtures.mi355x_probe_report(nd, gpus=gpus))
+        for name, rate in rates.items():
+            lib = (FakeDiagLib(n=gpus, gpu_rate=rate) if isinstance(rate, dict) else FakeDiagLib(n=gpus, rate=rate))
+            monkeypatch.setattr(diag, "lib", lambda lib=lib: lib)
+            out[name] = A.Agent(name, source="fake", diag_level=1, expect_gpus=gpus, diag_timeout=60,
+                                diag_baseline=False, **kw).probe_once()
+        return out
+    return make
+
+
+def _judge(reps, gpus=8):
+    names = list(reps)
+    summary, views = F.judge_fleet(names, [reps[n] for n in names])
+    return summary, {n: H.evaluate_report(reps[n], gpus, fleet=v) for n, v in zip(names, views)}
+
+
+def test_a_fleet_slow_alike_is_the_platforms_normal(reports):
+    """Four 8-GPU nodes, every GPU at 0.88 of the references: each agent alone calls its node degraded (one
+    node-wide finding); across the fleet that is the platform, and every node is healthy."""
+    reps = reports({f"n{i}": 0.88 for i in range(4)})
+    assert all(H.evaluate_report(r, 8).state == H.DEGRADED for r in reps.values())
+    summary, verdicts = _judge(reps)
+    assert all(v.state == H.HEALTHY and not v.warnings for v in verdicts.values()), \
+        {n: v.warnings for n, v in verdicts.items()}
+    row = summary["gemm@[4096, 4096, 4096]/tflops"]
+    assert row["nodes"] == 4 and row["platform_shortfall"] and row["median_fraction"] == pytest.approx(0.88, abs=1e-3)
+    assert row["outliers"] == []
+
+
+def test_one_node_behind_the_fleet_is_degraded_by_name(reports):
+    reps = reports({"n0": 1.0, "n1": 1.0, "n2": 1.0, "slow": 0.80})
+    summary, verdicts = _judge(reps)
+    assert all(verdicts[n].state == H.HEALTHY for n in ("n0", "n1", "n2"))
+    v = verdicts["slow"]
+    assert v.state == H.DEGRADED and not v.reasons  # all of its GPUs alike: the node's condition, never unhealthy
+    fleet_w = [w for w in v.warnings if w.startswith("fleet: ")]
+    assert any(w.startswith("fleet: diag gemm tflops at 80% of the other 3 nodes' median (80% vs 100%") for w in fleet_w)
+    assert {"node": "slow", "ratio": 0.8} in summary["gemm@[4096, 4096, 4096]/tflops"]["outliers"]
+
+
+def test_lone_gpu_nodes_slow_alike_pass_but_the_floor_stays(reports):
+    """1-GPU nodes judge their GPU against the references (no peers on the node): a fleet of them at 0.88 is
+    the platform; at 0.80 they are under the absolute floor and still fail -- the fleet excuses slowness only."""
+    reps = reports({f"n{i}": 0.88 for i in range(3)}, gpus=1)
+    assert all(any(w.startswith("gpu0: diag gemm slow") for w in H.evaluate_report(r, 1).warnings)
+               for r in reps.values())
+    _, verdicts = _judge(reps, 1)
+    assert all(v.state == H.HEALTHY for v in verdicts.values()), {n: v.warnings for n, v in verdicts.items()}
+    reps = reports({f"n{i}": 0.80 for i in range(3)}, gpus=1)
+    _, verdicts = _judge(reps, 1)
+    assert all(v.state == H.UNHEALTHY and v.reasons[0].startswith("gpu0: diag gemm failed") for v in verdicts.values())
+
+
+def test_a_gpu_failing_its_peers_is_not_excused_by_the_fleet(reports):
+    reps = reports({"n0": 0.88, "n1": 0.88, "n2": 0.88, "bad": {d: (0.70 if d == 3 else 0.88) for d in range(8)}})
+    _, verdicts = _judge(reps)
+    assert verdicts["bad"].state == H.UNHEALTHY and all(r.startswith("gpu3: ") for r in verdicts["bad"].reasons)
+    assert all(verdicts[n].state == H.HEALTHY for n in ("n0", "n1", "n2"))
+
+
+def test_fewer_than_three_nodes_change_nothing(reports):
+    reps = reports({"n0": 0.88, "n1": 0.88})
+    summary, verdicts = _judge(reps)
+    assert summary == {} and all(v.state == H.DEGRADED for v in verdicts.values())
+
+
+def test_the_fleet_judgement_leaves_the_reports_as_they_were(reports):
+    """The watcher keeps parsed reports across checks: judging must not change them."""
+    reps = reports({f"n{i}": 0.88 for i in range(3)} | {"slow": 0.7})
+    snap = json.dumps(reps, sort_keys=True)
+    a = _judge(reps)
+    assert json.dumps(reps, sort_keys=True) == snap
+    b = _judge(reps)
+    assert a[0] == b[0] and {n: v.to_dict() for n, v in a[1].items()} == {n: v.to_dict() for n, v in b[1].items()}
+
+
+def test_stale_reports_are_left_out_of_the_fleet(reports):
+    reps = reports({f"n{i}": 0.88 for i in range(4)})
+    for n in ("n0", "n1"):
+        reps[n]["ts"] -= 10 * 86400
+    names = list(reps)
+    exp = H.HealthExpectations()
+    current = [r if H.report_gate(r, exp) is None else None for r in reps.values()]
+    summary, views = F.judge_fleet(names, current)
+    assert summary == {} and views == [None] * 4
+
+
+# --- through the checker --------------------------------------------------------------------------------------
+
+def _cluster(mock_cluster, tmp_path, reps, gpus=8):
+    nodes = [fixtures.realistic_node(name, gpu_count=gpus, index=i, annotations=fixtures.health_annotation(rep),
+                                     extra_conditions=[fixtures.health_condition(rep, gpus)])
+             for i, (name, rep) in enumerate(reps.items())]
+    srv = mock_cluster(nodes)
+    return srv, write_kubeconfig(str(tmp_path / "kc"), srv.url)
+
+
+def test_checker_paths(reports, mock_cluster, tmp_path):
+    """The default check trusts each agent's condition (degraded); with the reports read (--health-reeval or
+    --json-extended) the fleet judgement applies; the summary rides in --json-extended."""
+    from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+    reps = reports({f"n{i}": 0.88 for i in range(3)} | {"slow": 0.70})
+    srv, _kc = _cluster(mock_cluster, tmp_path, reps)
+    cluster = ClusterConnection(srv.url)
+
+    def states(**kw):
+        opts = CheckOptions(**kw)
+        scan = scan_cluster(cluster, opts, NullTracer())
+        out: dict = {}
+        vs = apply_health(scan, opts, NullTracer(), [], cluster, out)
+        return {n["name"]: v.state for n, v in zip(scan.gpu_nodes, vs)}, out
+    plain, out = states()
+    assert set(plain.values()) == {H.DEGRADED} and out == {}
+    for kw in ({"health_reeval": True}, {"json_extended": True}):
+        st, out = states(**kw)
+        assert st == {"n0": H.HEALTHY, "n1": H.HEALTHY, "n2": H.HEALTHY, "slow": H.DEGRADED}, (kw, st)
+        assert out["summary"]["gemm@[4096, 4096, 4096]/tflops"]["outliers"][0]["node"] == "slow"
+
+
+def test_cli_fleet_and_explain_show_the_fleet(run_cli, reports, mock_cluster, tmp_path):
+    reps = reports({f"n{i}": 0.88 for i in range(3)} | {"slow": 0.70})
+    _srv, kc = _cluster(mock_cluster, tmp_path, reps)
+    p = run_cli(["--kubeconfig", kc, "--fleet"])
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "MI355X verdicts: 3 healthy, 1 degraded" in p.stdout
+    assert "  slow: degraded  " in p.stdout
+    line = next(ln for ln in p.stdout.splitlines() if ln.startswith("  gemm@[4096, 4096, 4096]/tflops: "))
+    assert "4 nodes, median 88% (70%-88%)" in line and "platform shortfall" in line and "slow x0.80" in line
+    p = run_cli(["--kubeconfig", kc, "--explain", "n1"])
+    assert p.returncode == 0 and "MI355X verdict: healthy" in p.stdout
+    assert "  fleet: diag gemm tflops: the fleet's median node is at 88% of the MI355X reference (4 nodes alike)" \
+        in p.stdout
+    d = json.loads(run_cli(["--kubeconfig", kc, "--json", "--json-extended"]).stdout)
+    assert d["mi355x"]["diag_fleet"]["gemm@[4096, 4096, 4096]/tflops"]["nodes"] == 4
