@@ -65,6 +65,20 @@ def render(result: Any) -> List[str]:
         for n, v in zip(result.gpu_nodes, result.verdicts):
             if v is not None:
                 lines.append(f'k8s_gpu_checker_mi355x_health{{node="{_esc(n["name"])}",state="{v.state}"}} 1')
+    fleet = getattr(result, "fleet_diag", None)
+    if fleet:
+        # models/fleet.py: per test, the fleet's median node as a fraction of the MI355X reference, and how many
+        # nodes fall under 85 % of the others
+        lines += ["# HELP k8s_gpu_checker_diag_fleet_median_fraction The median node's diagnostic rate as a "
+                  "fraction of the MI355X reference, per test.",
+                  "# TYPE k8s_gpu_checker_diag_fleet_median_fraction gauge"]
+        lines += [f'k8s_gpu_checker_diag_fleet_median_fraction{{test="{_esc(t)}"}} {row["median_fraction"]}'
+                  for t, row in fleet.items()]
+        lines += ["# HELP k8s_gpu_checker_diag_fleet_outlier_nodes Nodes under 85 % of the other nodes' median, per "
+                  "test.",
+                  "# TYPE k8s_gpu_checker_diag_fleet_outlier_nodes gauge"]
+        lines += [f'k8s_gpu_checker_diag_fleet_outlier_nodes{{test="{_esc(t)}"}} {len(row["outliers"])}'
+                  for t, row in fleet.items()]
     spans = result.tracer.as_ms() if result.tracer is not None else {}
     if spans:
         lines += ["# HELP k8s_gpu_checker_phase_seconds Wall time per check phase.",

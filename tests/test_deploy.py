@@ -224,8 +224,10 @@ def _watcher_families():
     from k8s_gpu_node_checker_amd.models import health as H
     from k8s_gpu_node_checker_amd.utils import prom
     node = {"name": "n0", "ready": True, "gpus": 8, "gpu_breakdown": {"amd.com/gpu": 8}}
+    fleet = {"gemm@[4096, 4096, 4096]/tflops": {"nodes": 3, "median_fraction": 0.97, "min_fraction": 0.95,
+                                                "max_fraction": 0.99, "platform_shortfall": False, "outliers": []}}
     res = types.SimpleNamespace(gpu_nodes=[node], ready_gpu_nodes=[node], exit_code=0,
-                                verdicts=[H.Verdict(H.HEALTHY)], tracer=None)
+                                verdicts=[H.Verdict(H.HEALTHY)], tracer=None, fleet_diag=fleet)
     srv = prom.MetricsServer("127.0.0.1", 0)
     try:
         srv.update(res)

@@ -100,7 +100,9 @@ def test_the_fleet_judgement_leaves_the_reports_as_they_were(reports):
     a = _judge(reps)
     assert json.dumps(reps, sort_keys=True) == snap
     b = _judge(reps)
-    assert a[0] == b[0] and {n: v.to_dict() for n, v in a[1].items()} == {n: v.to_dict() for n, v in b[1].items()}
+    def verdicts(x):
+        return {n: (v.state, v.reasons, v.warnings) for n, v in x[1].items()}
+    assert a[0] == b[0] and verdicts(a) == verdicts(b)
 
 
 def test_stale_reports_are_left_out_of_the_fleet(reports):
@@ -161,3 +163,16 @@ def test_cli_fleet_and_explain_show_the_fleet(run_cli, reports, mock_cluster, tm
         in p.stdout
     d = json.loads(run_cli(["--kubeconfig", kc, "--json", "--json-extended"]).stdout)
     assert d["mi355x"]["diag_fleet"]["gemm@[4096, 4096, 4096]/tflops"]["nodes"] == 4
+
+
+def test_fleet_gauges_in_the_metrics(reports, mock_cluster, tmp_path):
+    from k8s_gpu_node_checker_amd.checker import run_check
+    from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+    from k8s_gpu_node_checker_amd.utils import prom
+    reps = reports({f"n{i}": 0.88 for i in range(3)} | {"slow": 0.70})
+    srv, _kc = _cluster(mock_cluster, tmp_path, reps)
+    res = run_check(ClusterConnection(srv.url), CheckOptions(health_reeval=True))
+    text = "\n".join(prom.render(res))
+    assert 'k8s_gpu_checker_diag_fleet_median_fraction{test="gemm@[4096, 4096, 4096]/tflops"} 0.88' in text
+    assert 'k8s_gpu_checker_diag_fleet_outlier_nodes{test="gemm@[4096, 4096, 4096]/tflops"} 1' in text
+    assert 'k8s_gpu_checker_mi355x_health{node="n0",state="healthy"} 1' in text
