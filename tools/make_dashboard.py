@@ -41,7 +41,10 @@ ROWS = [
         ("Each GPU against its own baseline (drift below 0.90)", "timeseries", "percentunit",
          [("mi355x_gpu_diag_baseline_ratio", "{{node}} gpu{{gpu}} {{test}} {{metric}}")], 12, 7),
         ("Node-wide shortfalls: every GPU slow alike (share of the reference)", "timeseries", "percentunit",
-         [("mi355x_node_diag_shortfall_fraction", "{{node}} {{test}} {{metric}}")], 24, 6),
+         [("mi355x_node_diag_shortfall_fraction", "{{node}} {{test}} {{metric}}")], 12, 6),
+        ("The fleet's median node and its outliers (checker --health-reeval)", "timeseries", "none",
+         [("k8s_gpu_checker_diag_fleet_median_fraction", "{{test}} median"),
+          ("k8s_gpu_checker_diag_fleet_outlier_nodes", "{{test}} nodes behind")], 12, 6),
         ("Diagnostics skipped (GPU busy or allocated)", "timeseries", "none",
          [("mi355x_gpu_diag_skipped", "{{node}} gpu{{gpu}}")], 12, 6),
         ("Wrong results found by the diagnostics (words, lanes; GEMM output tiles failing their checksums)",
