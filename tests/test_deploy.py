@@ -332,7 +332,10 @@ def test_grafana_dashboard_queries_series_that_exist():
     assert len(ids) == len(set(ids)) and dash["uid"] == "mi355x-node-health"
     fams = {f.name: f for f in text_string_to_metric_families(agent._metrics(_rich_report()))}
     node = {"name": "n0", "ready": True, "gpus": 8, "gpu_breakdown": {"amd.com/gpu": 8}}
-    res = types.SimpleNamespace(gpu_nodes=[node], ready_gpu_nodes=[node], exit_code=0, verdicts=[], tracer=None)
+    fleet = {"gemm@[4096, 4096, 4096]/tflops": {"nodes": 3, "median_fraction": 0.97, "min_fraction": 0.95,
+                                                "max_fraction": 0.99, "platform_shortfall": False, "outliers": []}}
+    res = types.SimpleNamespace(gpu_nodes=[node], ready_gpu_nodes=[node], exit_code=0, verdicts=[], tracer=None,
+                                fleet_diag=fleet)
     fams.update({f.name: f for f in text_string_to_metric_families("\n".join(prom.render(res)) + "\n")})
     queried = 0
     for p in dash["panels"]:
