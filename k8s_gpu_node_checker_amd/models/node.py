@@ -127,7 +127,7 @@ class NodeExtras:
             r = _UNPARSED
         if r is _UNPARSED:
             from .health import parse_annotation
-            r = self._report = parse_annotation(self.health_annotation)
+            r = self._report = _slim(parse_annotation(self.health_annotation))
         return r
 
     def to_dict(self) -> Dict[str, Any]:
@@ -139,6 +139,23 @@ class NodeExtras:
             "internal_ip": self.internal_ip,
             "health_condition": list(self.health_condition) if self.health_condition else None,
         }
+
+
+# per-test fields of a diagnostic result that only the agent's own views read (per-XCD/CU maps, per-kind burn-in
+# rows, wall time): the checker keeps every node's parsed report (the watcher, across checks), and these are
+# ~36 % of it
+_DIAG_AGENT_ONLY = ("map", "kinds", "wall_s")
+
+
+def _slim(report: Any) -> Any:
+    gpus = report.get("gpus") if isinstance(report, dict) else None
+    for g in gpus if isinstance(gpus, list) else ():
+        diag = g.get("diag") if isinstance(g, dict) else None
+        for res in diag.values() if isinstance(diag, dict) else ():
+            if isinstance(res, dict):
+                for k in _DIAG_AGENT_ONLY:
+                    res.pop(k, None)
+    return report
 
 
 def node_extras(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS,
