@@ -176,3 +176,56 @@ def test_fleet_gauges_in_the_metrics(reports, mock_cluster, tmp_path):
     assert 'k8s_gpu_checker_diag_fleet_median_fraction{test="gemm@[4096, 4096, 4096]/tflops"} 0.88' in text
     assert 'k8s_gpu_checker_diag_fleet_outlier_nodes{test="gemm@[4096, 4096, 4096]/tflops"} 1' in text
     assert 'k8s_gpu_checker_mi355x_health{node="n0",state="healthy"} 1' in text
+
+
+# --- property tests --------------------------------------------------------------------------------------------
+
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+from k8s_gpu_node_checker_amd.models import peers as P  # noqa: E402
+
+
+def _node_report(name, fracs):
+    """A report whose GPUs ran only the level-1 GEMM at the given fractions of a 1,228 TFLOP/s reference, judged
+    by the agent's peer rules."""
+    pool = {d: {"gemm": dict(diag._rated({"shape": [4096, 4096, 4096]}, {"tflops": 1228.0 * f}, {"tflops": 1228.0},
+                                         "TFLOP/s"))} for d, f in enumerate(fracs)}
+    findings = P.judge_node(pool)
+    rep = fixtures.mi355x_probe_report(name, gpus=len(fracs))
+    for d, g in enumerate(rep["gpus"]):
+        g["diag"] = pool[d]
+    if findings:
+        rep["diag_node"] = {"findings": findings}
+    return rep
+
+
+_frac = st.floats(min_value=0.3, max_value=1.3, allow_nan=False)
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.lists(st.lists(_frac, min_size=1, max_size=4), min_size=1, max_size=7))
+def test_fleet_properties(nodes):
+    reps = {f"n{i}": _node_report(f"n{i}", fr) for i, fr in enumerate(nodes)}
+    names = list(reps)
+    summary, views = F.judge_fleet(names, [reps[n] for n in names])
+    assert len(views) == len(names)
+    if len(names) < F.FLEET_MIN_NODES:
+        assert summary == {} and views == [None] * len(names)
+    for n, view in zip(names, views):
+        alone = H.evaluate_report(reps[n], 0)
+        v = H.evaluate_report(reps[n], 0, fleet=view)
+        # the fleet never adds a failure and never removes one
+        assert v.reasons == alone.reasons
+        if view is None:
+            assert (v.state, v.warnings) == (alone.state, alone.warnings)
+            continue
+        # it only excuses when the fleet's median is itself short
+        if view["explained"]:
+            row = summary["gemm@[4096, 4096, 4096]/tflops"]
+            assert row["platform_shortfall"] and row["median_fraction"] < P.DEGRADED_FRACTION
+        for f in view["findings"]:
+            assert f["ratio"] < F.FLEET_FAIL_RATIO
+        # every warning the fleet added is a fleet finding
+        added = [w for w in v.warnings if w not in alone.warnings]
+        assert all(w.startswith("fleet: ") for w in added)
