@@ -229,3 +229,53 @@ def test_fleet_properties(nodes):
         # every warning the fleet added is a fleet finding
         added = [w for w in v.warnings if w not in alone.warnings]
         assert all(w.startswith("fleet: ") for w in added)
+
+
+def test_watcher_with_reeval_serves_fleet_gauges_that_follow_events(reports, mock_cluster, tmp_path):
+    """deploy/watcher.yaml plus --health-reeval: the fleet gauges on /metrics, and a node that falls behind the
+    fleet after a watch event shows up as an outlier."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    from k8s_gpu_node_checker_amd.utils.http import request
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    reps = reports({f"n{i}": 1.0 for i in range(4)})
+    srv, kc = _cluster(mock_cluster, tmp_path, reps)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("SLACK_WEBHOOK_URL", "KUBECONFIG")}
+    p = subprocess.Popen([sys.executable, os.path.join(repo, "check-gpu-node.py"), "--kubeconfig", kc, "--json",
+                          "--mi355x", "--health-reeval", "--watch-events", "--watch-duration", "30",
+                          "--watch-debounce", "0.1", "--metrics-listen", f"127.0.0.1:{port}"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=str(tmp_path))
+    gauge = 'k8s_gpu_checker_diag_fleet_outlier_nodes{test="gemm@[4096, 4096, 4096]/tflops"}'
+
+    def outliers():
+        try:
+            text = request(f"http://127.0.0.1:{port}/metrics").text
+        except Exception:  # not listening yet
+            return None
+        line = next((ln for ln in text.splitlines() if ln.startswith(gauge)), None)
+        return float(line.split()[-1]) if line else None
+    try:
+        t0 = time.monotonic()
+        while time.monotonic() - t0 < 20 and outliers() is None:
+            time.sleep(0.1)
+        assert outliers() == 0
+        slow = reports({"n3": 0.70})["n3"]
+        nodes = [fixtures.realistic_node(name, gpu_count=8, index=i,
+                                         annotations=fixtures.health_annotation(slow if name == "n3" else rep),
+                                         extra_conditions=[fixtures.health_condition(slow if name == "n3" else rep, 8)])
+                 for i, (name, rep) in enumerate(reps.items())]
+        srv.state.set_nodes(nodes)
+        t0 = time.monotonic()
+        while time.monotonic() - t0 < 20 and outliers() != 1:
+            time.sleep(0.1)
+        assert outliers() == 1
+    finally:
+        p.terminate()
+        p.communicate(timeout=20)
