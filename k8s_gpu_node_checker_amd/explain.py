@@ -267,5 +267,7 @@ def fleet(cluster: ClusterConnection, opts: CheckOptions, out: TextIO) -> int:
                       + ("  platform shortfall: nodes in line with it are not degraded for it"
                          if row["platform_shortfall"] else "")
                       + ("  outliers: " + ", ".join(f"{o['node']} x{o['ratio']:.2f}" for o in row["outliers"])
-                         if row["outliers"] else "") + "\n")
+                         if row["outliers"] else "")
+                      + ("  slowest: " + ", ".join(f"{x['node']} {x['fraction']:.0%}" for x in row.get("slowest", []))
+                         if not row["outliers"] else "") + "\n")
     return res.exit_code

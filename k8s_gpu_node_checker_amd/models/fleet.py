@@ -81,8 +81,8 @@ def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]]
       not warnings.
 
     ``reports`` is parallel to ``names`` (None where a node has no report to judge); a node with nothing to say
-    gets None.  The summary, per test: node count, median, min and max fraction, the outliers and whether the
-    fleet is short alike."""
+    gets None.  The summary, per test: node count, median, min and max fraction, the outliers, the three slowest
+    nodes and whether the fleet is short alike."""
     values: Dict[Key, Dict[int, float]] = {}
     for i, rep in enumerate(reports):
         if not isinstance(rep, dict):
@@ -105,7 +105,9 @@ def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]]
         row: Dict[str, Any] = {"nodes": len(vals), "median_fraction": round(med, 3),
                                "min_fraction": round(min(vals.values()), 3),
                                "max_fraction": round(max(vals.values()), 3), "platform_shortfall": platform_short,
-                               "outliers": []}
+                               "outliers": [],
+                               "slowest": [{"node": names[i], "fraction": round(v, 3)}
+                                           for i, v in sorted(vals.items(), key=lambda kv: (kv[1], kv[0]))[:3]]}
         for i, v in vals.items():
             others = statistics.median([x for j, x in vals.items() if j != i])
             ratio = v / others if others > 0 else 1.0

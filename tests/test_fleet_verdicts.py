@@ -225,7 +225,7 @@ def test_fleet_properties(nodes):
             row = summary["gemm@[4096, 4096, 4096]/tflops"]
             assert row["platform_shortfall"] and row["median_fraction"] < P.DEGRADED_FRACTION
         for f in view["findings"]:
-            assert f["ratio"] < F.FLEET_FAIL_RATIO
+            assert f["ratio"] <= F.FLEET_FAIL_RATIO  # rounded to 3 places
         # every warning the fleet added is a fleet finding
         added = [w for w in v.warnings if w not in alone.warnings]
         assert all(w.startswith("fleet: ") for w in added)
