@@ -279,3 +279,31 @@ def test_watcher_with_reeval_serves_fleet_gauges_that_follow_events(reports, moc
     finally:
         p.terminate()
         p.communicate(timeout=20)
+
+
+_json = st.recursive(st.none() | st.booleans() | st.integers(-5, 5) | st.floats(allow_nan=True) | st.text(max_size=3),
+                     lambda kids: st.lists(kids, max_size=3) | st.dictionaries(st.text(max_size=4), kids, max_size=3),
+                     max_leaves=12)
+_result = st.fixed_dictionaries({}, optional={
+    "rates": st.dictionaries(st.sampled_from(["tflops", "read_tbs", "x"]), _json | st.floats(0.1, 2.0), max_size=2),
+    "expect": st.dictionaries(st.sampled_from(["tflops", "read_tbs", "x"]), _json | st.just(1.0), max_size=2),
+    "shape": _json, "pass": _json, "degraded": _json, "lag": _json, "drift": _json, "detail": _json})
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.lists(st.dictionaries(st.sampled_from(["gemm", "hbm", "mfma"]), _result | _json, max_size=3)
+                         | _json, max_size=3), min_size=3, max_size=5),
+       st.lists(_json, max_size=2))
+def test_hostile_reports_do_not_break_the_fleet(gpu_diags, node_findings):
+    """Reports are untrusted JSON: whatever their diagnostics hold, the fleet judgement neither raises nor turns a
+    verdict into anything but a verdict."""
+    reps = []
+    for i, diags in enumerate(gpu_diags):
+        r = fixtures.mi355x_probe_report(f"n{i}", gpus=max(1, len(diags)) if isinstance(diags, list) else 1)
+        for g, d in zip(r["gpus"], diags if isinstance(diags, list) else [diags]):
+            g["diag"] = d
+        r["diag_node"] = {"findings": node_findings}
+        reps.append(r)
+    summary, views = F.judge_fleet([f"n{i}" for i in range(len(reps))], reps)
+    for r, v in zip(reps, views):
+        assert H.evaluate_report(r, 0, fleet=v).state in (H.HEALTHY, H.DEGRADED, H.UNHEALTHY, H.UNKNOWN)
