@@ -32,6 +32,7 @@ def main() -> int:
     ap.add_argument("--level", type=int, default=1, choices=(1, 2))
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--runs", type=int, default=B.BASELINE_RUNS, help="clean runs that form the baseline")
+    ap.add_argument("--gap", type=float, default=0.0, help="idle seconds between cycles (a cold GPU each time)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(prefix="baseline-soak-"), "baseline.json")
@@ -41,6 +42,8 @@ def main() -> int:
     rows = []
     t0 = time.time()
     for c in range(args.cycles):
+        if c and args.gap > 0:
+            time.sleep(args.gap)
         t = time.time()
         rep = agent.probe_once()
         v = H.evaluate_report(rep, 1)
@@ -67,7 +70,7 @@ def main() -> int:
             for m, r in (d or {}).items():
                 ratios.setdefault(f"{test}/{m}", []).append(r)
     summary = {
-        "level": args.level, "cycles": args.cycles, "baseline_runs": args.runs, "wall_s": round(time.time() - t0, 1),
+        "level": args.level, "cycles": args.cycles, "gap_s": args.gap, "baseline_runs": args.runs, "wall_s": round(time.time() - t0, 1),
         "states": {s: sum(1 for r in rows if r["state"] == s) for s in {r["state"] for r in rows}},
         "drift_flags": sum(1 for r in rows if r["drift"]),
         "ratio_to_baseline": {k: {"min": min(v), "median": statistics.median(v), "max": max(v), "n": len(v)}
