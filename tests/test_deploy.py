@@ -735,3 +735,14 @@ def test_agent_baseline_file_is_on_a_writable_host_volume():
         assert not mount.get("readOnly")
         vol = next(v for v in pod["volumes"] if v["name"] == mount["name"])
         assert vol["hostPath"] == {"path": os.path.dirname(path), "type": "DirectoryOrCreate"}
+
+
+def test_every_alert_has_a_runbook_section():
+    """RUNBOOK.md has a section per alert of deploy/monitoring/monitoring.yaml, and no section for an alert that
+    is gone."""
+    import re
+    docs = list(yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "monitoring", "monitoring.yaml"))))
+    alerts = {r["alert"] for d in docs if d and d["kind"] == "PrometheusRule" for g in d["spec"]["groups"]
+              for r in g["rules"]}
+    sections = set(re.findall(r"^## (\S+)\s*$", _read(os.path.join(REPO, "RUNBOOK.md")), re.M))
+    assert alerts and alerts == sections, (alerts - sections, sections - alerts)
