@@ -260,14 +260,16 @@ def fleet(cluster: ClusterConnection, opts: CheckOptions, out: TextIO) -> int:
         for image, row in fv["firmware"].items():
             out.write(f"  {image}: " + ", ".join(f"{k} x{c}" for k, c in sorted(row.items())) + "\n")
     if res.fleet_diag:
-        out.write("diagnostics across the fleet (node medians, fraction of the MI355X reference):\n")
+        out.write("diagnostics across the fleet (node medians, fraction of the MI355X reference; fabric in GB/s):\n")
         for test, row in res.fleet_diag.items():
-            out.write(f"  {test}: {row['nodes']} nodes, median {row['median_fraction']:.0%} "
-                      f"({row['min_fraction']:.0%}-{row['max_fraction']:.0%})"
+            def fmt(x, unit=row.get("unit")):
+                return f"{x:.0f} GB/s" if unit == "GB/s" else f"{x:.0%}"
+            out.write(f"  {test}: {row['nodes']} nodes, median {fmt(row['median_fraction'])} "
+                      f"({fmt(row['min_fraction'])}-{fmt(row['max_fraction'])})"
                       + ("  platform shortfall: nodes in line with it are not degraded for it"
                          if row["platform_shortfall"] else "")
                       + ("  outliers: " + ", ".join(f"{o['node']} x{o['ratio']:.2f}" for o in row["outliers"])
                          if row["outliers"] else "")
-                      + ("  slowest: " + ", ".join(f"{x['node']} {x['fraction']:.0%}" for x in row.get("slowest", []))
+                      + ("  slowest: " + ", ".join(f"{x['node']} {fmt(x['fraction'])}" for x in row.get("slowest", []))
                          if not row["outliers"] else "") + "\n")
     return res.exit_code

@@ -59,14 +59,32 @@ def _gpu_results(report: Any):
                     yield g, test, res, fr
 
 
+# node-level fabric results (level 2, ``report["fabric"]``) compared across nodes as raw rates: no reference
+# to be short of, so outliers only (a node whose xGMI pairs or RCCL collectives run well under the others')
+RAW_TESTS = ("xgmi_p2p", "rccl")
+
+
+def _num(v: Any) -> bool:
+    return isinstance(v, (int, float)) and not isinstance(v, bool) and v > 0
+
+
 def node_fractions(report: Any) -> Dict[Key, float]:
-    """``(test, shape, metric) -> the node's median GPU`` (rate as a fraction of its scaled reference)."""
+    """``(test, shape, metric) -> the node's median GPU`` (rate as a fraction of its scaled reference), plus the
+    node-level fabric rates (``RAW_TESTS``, GB/s, keyed by how many GPUs took part)."""
     per: Dict[Key, List[float]] = {}
     for _g, test, res, fr in _gpu_results(report):
         shape = _shape(res)
         for m, v in fr.items():
             per.setdefault((test, shape, m), []).append(v)
-    return {k: statistics.median(v) for k, v in per.items()}
+    out = {k: statistics.median(v) for k, v in per.items()}
+    fab = report.get("fabric") if isinstance(report, dict) else None
+    if isinstance(fab, dict):
+        p2p, rccl = fab.get("p2p"), fab.get("rccl")
+        if isinstance(p2p, dict) and _num(p2p.get("median_gbps")) and isinstance(p2p.get("pairs"), list):
+            out[("xgmi_p2p", f"pairs={len(p2p['pairs'])}", "median_gbps")] = float(p2p["median_gbps"])
+        if isinstance(rccl, dict) and _num(rccl.get("best_busbw_gbps")) and isinstance(rccl.get("world"), int):
+            out[("rccl", f"world={rccl['world']}", "busbw_gbps")] = float(rccl["best_busbw_gbps"])
+    return out
 
 
 def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]]
@@ -101,8 +119,10 @@ def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]]
         if len(vals) < FLEET_MIN_NODES:
             continue
         med = statistics.median(vals.values())
-        platform_short = med < DEGRADED_FRACTION
-        row: Dict[str, Any] = {"nodes": len(vals), "median_fraction": round(med, 3),
+        raw = key[0] in RAW_TESTS
+        platform_short = not raw and med < DEGRADED_FRACTION
+        row: Dict[str, Any] = {"nodes": len(vals), "unit": "GB/s" if raw else "fraction",
+                               "median_fraction": round(med, 3),
                                "min_fraction": round(min(vals.values()), 3),
                                "max_fraction": round(max(vals.values()), 3), "platform_shortfall": platform_short,
                                "outliers": [],
@@ -112,9 +132,12 @@ def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]]
             others = statistics.median([x for j, x in vals.items() if j != i])
             ratio = v / others if others > 0 else 1.0
             if ratio < FLEET_FAIL_RATIO:
-                view(i)["findings"].append({"test": key[0], "metric": key[2], "node_fraction": round(v, 3),
-                                            "fleet_fraction": round(others, 3), "ratio": round(ratio, 3),
-                                            "nodes": len(vals) - 1})
+                f = {"test": key[0], "metric": key[2], "ratio": round(ratio, 3), "nodes": len(vals) - 1}
+                if raw:
+                    f.update(node_value=round(v, 1), fleet_value=round(others, 1))
+                else:
+                    f.update(node_fraction=round(v, 3), fleet_fraction=round(others, 3))
+                view(i)["findings"].append(f)
                 row["outliers"].append({"node": names[i], "ratio": round(ratio, 3)})
             elif platform_short and max(v, med) <= FLEET_UNIFORM_SPREAD * min(v, med):
                 view(i)["explained"][key] = {"fleet_fraction": round(med, 3), "nodes": len(vals)}
@@ -161,6 +184,9 @@ def explained_text(fleet: Dict[str, Any]) -> List[str]:
 
 def finding_text(f: Dict[str, Any]) -> str:
     """One fleet outlier finding as a verdict warning."""
+    if "node_value" in f:
+        return (f"fleet: {f.get('test')} {f.get('metric')} at {f.get('ratio', 0):.0%} of the other {f.get('nodes')} "
+                f"nodes' median ({f.get('node_value')} vs {f.get('fleet_value')}): this node's xGMI fabric")
     return (f"fleet: diag {f.get('test')} {f.get('metric')} at {f.get('ratio', 0):.0%} of the other "
             f"{f.get('nodes')} nodes' median ({f.get('node_fraction', 0):.0%} vs {f.get('fleet_fraction', 0):.0%} of "
             f"the MI355X reference): this node's cooling, power or firmware")

@@ -73,7 +73,7 @@ def render(result: Any) -> List[str]:
                   "fraction of the MI355X reference, per test.",
                   "# TYPE k8s_gpu_checker_diag_fleet_median_fraction gauge"]
         lines += [f'k8s_gpu_checker_diag_fleet_median_fraction{{test="{_esc(t)}"}} {row["median_fraction"]}'
-                  for t, row in fleet.items()]
+                  for t, row in fleet.items() if row.get("unit", "fraction") == "fraction"]
         lines += ["# HELP k8s_gpu_checker_diag_fleet_outlier_nodes Nodes under 85 % of the other nodes' median, per "
                   "test.",
                   "# TYPE k8s_gpu_checker_diag_fleet_outlier_nodes gauge"]

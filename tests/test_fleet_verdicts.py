@@ -307,3 +307,24 @@ def test_hostile_reports_do_not_break_the_fleet(gpu_diags, node_findings):
     summary, views = F.judge_fleet([f"n{i}" for i in range(len(reps))], reps)
     for r, v in zip(reps, views):
         assert H.evaluate_report(r, 0, fleet=v).state in (H.HEALTHY, H.DEGRADED, H.UNHEALTHY, H.UNKNOWN)
+
+
+def test_a_node_whose_fabric_runs_behind_the_fleet(reports):
+    """Level-2 fabric results are node-level raw rates (GB/s): compared across nodes for outliers only -- a node
+    whose RCCL all-reduce busbw is 60 % of the others' is degraded; a fabric the whole fleet shares is no
+    shortfall (there is no reference to be short of)."""
+    def rep(name, busbw, p2p):
+        r = fixtures.mi355x_probe_report(name, gpus=8)
+        r["fabric"] = {"rccl": {"pass": True, "world": 8, "best_busbw_gbps": busbw, "detail": ""},
+                       "p2p": {"pass": True, "pairs": [[0, 1]] * 56, "median_gbps": p2p, "detail": ""}}
+        return r
+    reps = {"n0": rep("n0", 310.0, 48.0), "n1": rep("n1", 300.0, 47.0), "n2": rep("n2", 305.0, 49.0),
+            "weak": rep("weak", 183.0, 47.5)}
+    summary, verdicts = _judge(reps)
+    assert all(verdicts[n].state == H.HEALTHY for n in ("n0", "n1", "n2"))
+    w = verdicts["weak"]
+    assert w.state == H.DEGRADED and w.warnings == [
+        "fleet: rccl busbw_gbps at 60% of the other 3 nodes' median (183.0 vs 305.0): this node's xGMI fabric"]
+    row = summary["rccl@world=8/busbw_gbps"]
+    assert row["unit"] == "GB/s" and not row["platform_shortfall"] and row["outliers"] == [{"node": "weak", "ratio": 0.6}]
+    assert summary["xgmi_p2p@pairs=56/median_gbps"]["outliers"] == []
