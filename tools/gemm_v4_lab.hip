@@ -1,0 +1,249 @@
+// GEMM lab, round 4 (not shipped): the v3 bf16 kernel's 256x256x64 tile and 8 staggered waves, with the K-tile
+// split by k-step instead of by output quadrant, to halve the barriers.
+//
+// v3 runs 4 phases per K-tile, each a 64x32 quadrant of the wave's 128x64 output (16 MFMAs) over both k-steps,
+// with a barrier after every load slot and every MFMA slot: 8 per K-tile.  Its slot stamps
+// (profiles/gemm_v3_stamps_mi355x.jsonl) show ~100 ticks of barrier wait at the end of every slot -- a fifth of
+// the K-tile.  Here a phase is one k-step (32 of the tile's 64 columns) of the whole 128x64 wave tile: 12
+// fragment reads (8 A, 4 B) feed 32 MFMAs, two phases per K-tile, 4 barriers.  Longer slots need the LDS-DMA to
+// restage by k-step, so a stage is laid out by k-half: [half][A | B][256 rows][64 B], each 16 KiB region one
+// operand's half; a row's 4 16-byte chunks are XOR-swizzled by row bit 3 (conflict-free ds_read_b128 for the
+// 16x16x32 fragment pattern, checked by brute force over the lane groups of the LDS table).
+//
+// Schedule (group 1 = waves 4-7 one barrier behind group 0, as in v3):
+//   load slot (kt, h): LDS-DMA of tile kt+1's half h into the other stage (4 pieces / wave) | 12 ds_read_b128
+//                      of half h | vmcnt(4): the previous slot's pieces landed | barrier
+//   MFMA slot (kt, h): lgkmcnt(0) | 32 MFMAs | barrier
+// Half h of the other stage was last read at (kt-1, h), retired by group 1 two slots before group 0 overwrites it.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gemm_v4_lab.hip -o tools/gemm_v4_lab.bin
+//   ./tools/gemm_v4_lab.bin [size] [rounds]
+#include <functional>
+
+#include "../k8s_gpu_node_checker_amd/csrc/diag/diag.hip"
+
+namespace {
+
+constexpr int V4_REGION = V2_BM * 64;       // one operand's k-half of a stage: 256 rows x 64 B = 16 KiB
+constexpr int V4_STAGE = 4 * V4_REGION;     // [half][A | B] = 64 KiB
+static_assert(2 * V4_STAGE <= 160 * 1024, "two stages fit the CU's LDS");
+
+__device__ __forceinline__ int v4_swz(int row) { return (row >> 2) & 2; }
+
+// One 16 KiB region (rows 0..255 of one operand, columns kt*64 + h*32 .. +32) as 16 wave-instructions of 16 rows x
+// 64 B; wave wid issues instructions 2*wid and 2*wid+1.  Lane: row (lane >> 2), physical chunk (lane & 3), which
+// holds logical chunk (lane & 3) ^ v4_swz(row).
+__device__ __forceinline__ void v4_dma(unsigned char* region, const __bf16* __restrict__ src, int K, int kt, int h,
+                                       int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j = wid * 2 + i;
+    const int row = j * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ v4_swz(row);
+    const __bf16* g = src + static_cast<size_t>(row) * K + kt * 64 + h * 32 + c * 8;
+    __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(region + j * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 v4_frag(const unsigned char* region, int row, int fq) {
+  return *reinterpret_cast<const bf16x8*>(region + row * 64 + ((fq ^ v4_swz(row)) << 4));
+}
+
+template <bool PRIO>
+__global__ void __launch_bounds__(V2_THREADS, 1)
+gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
+               int K) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int tiles_m = M / V2_BM, tiles_n = N / V2_BN, nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  constexpr int GROUP_M = 4;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % (GROUP_M * tiles_n)) % gsize;
+  const int tn = (bid % (GROUP_M * tiles_n)) / gsize;
+  const __bf16* Ab = A + static_cast<size_t>(tm) * V2_BM * K;
+  const __bf16* Bb = Bt + static_cast<size_t>(tn) * V2_BN * K;
+  auto region = [&](int stage, int h, int op) { return smem + stage * V4_STAGE + (h * 2 + op) * V4_REGION; };
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int KT = K / 64;
+  const int frow = lane & 15, fq = lane >> 4;
+
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    v4_dma(region(0, h, 0), Ab, K, 0, h, wid, lane);
+    v4_dma(region(0, h, 1), Bb, K, 0, h, wid, lane);
+  }
+  __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
+  STG_BARRIER();
+  if (wr == 1) STG_BARRIER();  // the stagger
+  if constexpr (PRIO) {
+    if (wr == 1) __builtin_amdgcn_s_setprio(1);
+  }
+
+  bf16x8 fa[8], fb[4];
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1, nxt = cur ^ 1;
+    const bool more = kt + 1 < KT;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // load slot
+      if (more) {
+        v4_dma(region(nxt, h, 0), Ab, K, kt + 1, h, wid, lane);
+        v4_dma(region(nxt, h, 1), Bb, K, kt + 1, h, wid, lane);
+      }
+      const unsigned char* ra = region(cur, h, 0);
+      const unsigned char* rb = region(cur, h, 1);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) fb[n] = v4_frag(rb, wc * 64 + n * 16 + frow, fq);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) fa[m] = v4_frag(ra, wr * 128 + m * 16 + frow, fq);
+      if (more) {
+        __builtin_amdgcn_s_waitcnt(0x3f74);  // vmcnt(4): the previous load slot's pieces landed
+      } else {
+        __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
+      }
+      STG_BARRIER();
+      // MFMA slot
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) asm volatile("" : "+v"(acc[m][n]));
+      STG_BARRIER();
+    }
+  }
+  if (wr == 0) STG_BARRIER();  // balance the stagger
+  const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 64;
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        C[static_cast<size_t>(row0 + m * 16 + fq * 4 + j) * N + col0 + n * 16 + frow] = acc[m][n][j];
+}
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      printf("%s: %s\n", #x, hipGetErrorString(e_));                           \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+template <class L>
+double time_ms(L launch, int iters) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  launch();
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(a));
+  for (int i = 0; i < iters; ++i) launch();
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return ms / iters;
+}
+
+template <bool PRIO>
+void launch_v4(const __bf16* A, const __bf16* Bt, float* C, int M, int N, int K) {
+  hipLaunchKernelGGL((gemm_v4_kernel<PRIO>), dim3((M / V2_BM) * (N / V2_BN)), dim3(V2_THREADS), 2 * V4_STAGE,
+                     nullptr, A, Bt, C, M, N, K);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::vector<int> sizes = {4096, 8192};
+  if (argc > 1 && atoi(argv[1]) > 0) sizes = {atoi(argv[1])};
+  const int reps = argc > 2 ? atoi(argv[2]) : 5;  // timed rounds per kernel, interleaved (DVFS drift)
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<false>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<true>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
+  for (int size : sizes) {
+    if (size % 256 || size < 512) {
+      printf("size must be a multiple of 256, >= 512\n");
+      return 1;
+    }
+    const int M = size, N = size, K = size;
+    __bf16 *A, *Bt;
+    float *C0, *C1;
+    CK(hipMalloc(&A, sizeof(__bf16) * M * K));
+    CK(hipMalloc(&Bt, sizeof(__bf16) * N * K));
+    CK(hipMalloc(&C0, sizeof(float) * M * N));
+    CK(hipMalloc(&C1, sizeof(float) * M * N));
+    hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, A, (size_t)M * K, 7ULL);
+    hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, Bt, (size_t)N * K, 11ULL);
+    // reference: the shipped v3 kernel (fp32 C), exact same accumulation order per k-step pair is not
+    // guaranteed, so outputs are compared to a relative tolerance
+    if (launch_v3_inst<DT_BF16, false, false, 1>(A, Bt, C0, M, N, K, nullptr) != 0) return 1;
+    CK(hipDeviceSynchronize());
+    std::vector<float> h0((size_t)M * N), h1((size_t)M * N);
+    CK(hipMemcpy(h0.data(), C0, sizeof(float) * M * N, hipMemcpyDeviceToHost));
+    const int it = size >= 8192 ? 20 : 50;
+    struct Row {
+      const char* name;
+      std::function<void()> go;
+      double best = 1e30, worst_diff = 0;
+      std::vector<double> all;
+    };
+    std::vector<Row> rows;
+    rows.push_back({"v3(direct-epi)", [&] { launch_v3_inst<DT_BF16, false, false, 1>(A, Bt, C1, M, N, K, nullptr); }});
+    rows.push_back({"v3(lds-epi)", [&] { launch_v3_inst<DT_BF16, true, false, 1>(A, Bt, C1, M, N, K, nullptr); }});
+    rows.push_back({"v4", [&] { launch_v4<false>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"v4(prio)", [&] { launch_v4<true>(A, Bt, C1, M, N, K); }});
+    for (int r = 0; r < reps; ++r) {
+      for (Row& row : rows) {
+        CK(hipMemset(C1, 0xff, sizeof(float) * M * N));
+        const double ms = time_ms(row.go, it);
+        row.all.push_back(ms);
+        row.best = std::min(row.best, ms);
+        if (r == 0) {
+          CK(hipMemcpy(h1.data(), C1, sizeof(float) * M * N, hipMemcpyDeviceToHost));
+          for (size_t i = 0; i < h0.size(); ++i) {
+            const double d = std::isnan(h1[i]) ? 1e30
+                                               : (double)std::fabs(h0[i] - h1[i]) / std::max(1.0, (double)std::fabs(h0[i]));
+            row.worst_diff = std::max(row.worst_diff, d);
+          }
+        }
+      }
+    }
+    for (Row& row : rows) {
+      std::sort(row.all.begin(), row.all.end());
+      const double med = row.all[row.all.size() / 2];
+      printf("{\"kernel\": \"%s\", \"size\": %d, \"tflops_best\": %.1f, \"tflops_median\": %.1f, \"ms\": %.4f, "
+             "\"max_rel_diff_vs_v3\": %.3g}\n",
+             row.name, size, 2.0 * M * N * (double)K / (row.best * 1e-3) / 1e12,
+             2.0 * M * N * (double)K / (med * 1e-3) / 1e12, row.best, row.worst_diff);
+      fflush(stdout);
+    }
+    CK(hipFree(A));
+    CK(hipFree(Bt));
+    CK(hipFree(C0));
+    CK(hipFree(C1));
+  }
+  return 0;
+}
