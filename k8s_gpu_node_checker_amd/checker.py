@@ -255,13 +255,16 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
         # anyway, --json-extended / --explain / --fleet) those of nodes judged by their condition
         compare: List[Optional[Dict[str, Any]]] = [None] * len(scan.gpu_nodes)
         parsed = opts.json_extended
+        comparable = 0
         for i, (node, ex, rep) in enumerate(zip(scan.gpu_nodes, scan.extras, reports)):
             if rep is None and reeval:
                 rep = ex.report()
             if rep is None and ex.health_condition is not None:
                 if parsed and ex.health_annotation:
                     r = ex.report()
-                    compare[i] = r if isinstance(r, dict) and r.get("node") in (None, node["name"]) else None
+                    if isinstance(r, dict) and r.get("node") in (None, node["name"]):
+                        compare[i] = r
+                        comparable += 1
                 continue
             if rep is None and ex.health_annotation:
                 rep = ex.report()
@@ -272,9 +275,10 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
                 pre[i] = H.Verdict(H.UNKNOWN, [f"report is for node {other}"])
             else:
                 judged[i] = compare[i] = rep
+                comparable += rep is not None
         # the fleet-relative judgement of the diagnostics' rates (models/fleet.py): only with 3+ reports to compare
         fleet_views: List[Optional[Dict[str, Any]]] = [None] * len(scan.gpu_nodes)
-        if sum(1 for r in compare if isinstance(r, dict) and r.get("gpus")) >= 3:
+        if comparable >= 3:
             from .models import fleet as F
             current = [r if H.report_gate(r, exp, now) is None else None for r in compare]
             summary, fleet_views = F.judge_fleet([n["name"] for n in scan.gpu_nodes], current)
