@@ -59,6 +59,7 @@ class CheckOptions:
         self.probe_concurrency = 64
         self.probe_timeout = 2.0
         self.probe_ca: Optional[str] = None
+        self.probe_tls_server_name: Optional[str] = None
         self.probe_client_cert: Optional[str] = None
         self.probe_client_key: Optional[str] = None
         self.health_reeval = False
@@ -236,7 +237,7 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
             reports = fetch_probe_reports(scan, opts.probe_endpoint, opts.probe_concurrency, opts.probe_timeout,
                                           ca_file=opts.probe_ca, client_cert=opts.probe_client_cert,
                                           client_key=opts.probe_client_key, pod_ips=pod_ips,
-                                          pod_ip_error=pod_err)
+                                          pod_ip_error=pod_err, server_name=opts.probe_tls_server_name)
         verdicts: List[Optional[H.Verdict]] = []
         changed = False
         unknown_ok = opts.probe_unknown == "allow"

@@ -64,6 +64,10 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
     ("x", "--probe-concurrency", {"type": int, "default": 64, "help": "프로브 fan-out 동시성 (기본: 64)"}),
     ("x", "--probe-timeout", {"type": float, "default": 2.0, "help": "노드별 프로브 타임아웃(초) (기본: 2)"}),
     ("x", "--probe-ca", {"help": "https 프로브 엔드포인트를 검증할 CA 파일 (기본: 시스템 CA)"}),
+    ("x", "--probe-tls-server-name", {"metavar": "NAME",
+                                      "help": "https 프로브의 서버 인증서를 URL 의 호스트 대신 이 이름으로 검증 "
+                                              "({pod_ip} 처럼 인증서에 없는 주소로 접속할 때, 예: "
+                                              "mi355x-node-agent.gpu-health.svc)"}),
     ("x", "--probe-client-cert", {"help": "에이전트가 클라이언트 인증서를 요구할 때 제시할 인증서 (PEM)"}),
     ("x", "--probe-client-key", {"help": "--probe-client-cert 의 개인 키 (PEM)"}),
     ("x", "--require-schedulable", {"action": "store_true",

@@ -182,7 +182,10 @@ class _GetProtocol(asyncio.Protocol):
 
 
 async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None, max_body: int = MAX_BODY,
-                         client_cert: Optional[str] = None, client_key: Optional[str] = None) -> Any:
+                         client_cert: Optional[str] = None, client_key: Optional[str] = None,
+                         server_name: Optional[str] = None) -> Any:
+    """GET ``url`` and parse its JSON body.  ``server_name``: verify an https peer's certificate against this
+    name instead of the URL's host (agents reached by pod IP present the Service's name)."""
     parts = urlsplit(url)
     host = parts.hostname or "localhost"
     port = parts.port or (443 if parts.scheme == "https" else 80)
@@ -204,7 +207,10 @@ async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None
             task.cancel()
     timer = loop.call_later(timeout, expire)
     try:
-        await loop.create_connection(lambda: proto, host, port, ssl=ssl_ctx)
+        if ssl_ctx is not None and server_name:
+            await loop.create_connection(lambda: proto, host, port, ssl=ssl_ctx, server_hostname=server_name)
+        else:
+            await loop.create_connection(lambda: proto, host, port, ssl=ssl_ctx)
         body = await done
     except asyncio.CancelledError:
         if expired:
@@ -221,7 +227,7 @@ async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None
 
 async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, timeout: float = 2.0,
                     retries: int = 1, ca_file: Optional[str] = None, client_cert: Optional[str] = None,
-                    client_key: Optional[str] = None) -> List[Dict[str, Any]]:
+                    client_key: Optional[str] = None, server_name: Optional[str] = None) -> List[Dict[str, Any]]:
     sem = asyncio.Semaphore(max(1, concurrency))
 
     async def one(t: Dict[str, str]) -> Dict[str, Any]:
@@ -232,7 +238,7 @@ async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, ti
             for attempt in range(retries + 1):
                 try:
                     doc = await _http_get_json(t["url"], timeout, ca_file, client_cert=client_cert,
-                                               client_key=client_key)
+                                               client_key=client_key, server_name=server_name)
                     if not isinstance(doc, dict):
                         return _error_report(t["name"], "probe endpoint returned non-object JSON")
                     return doc
@@ -354,10 +360,11 @@ def run_coroutine(coro: Any) -> Any:
 def fetch_probe_reports(scan: Any, template: str, concurrency: int = 64, timeout: float = 2.0,
                         ca_file: Optional[str] = None, client_cert: Optional[str] = None,
                         client_key: Optional[str] = None, pod_ips: Optional[Dict[str, str]] = None,
-                        pod_ip_error: Optional[str] = None) -> List[Optional[Dict[str, Any]]]:
+                        pod_ip_error: Optional[str] = None,
+                        server_name: Optional[str] = None) -> List[Optional[Dict[str, Any]]]:
     """Fetch one probe report per GPU node (parallel to ``scan.gpu_nodes``)."""
     targets = build_targets(scan, template, pod_ips, pod_ip_error)
     if not targets:
         return []
     return list(run_coroutine(fetch_all(targets, concurrency, timeout, ca_file=ca_file, client_cert=client_cert,
-                                        client_key=client_key)))
+                                        client_key=client_key, server_name=server_name)))

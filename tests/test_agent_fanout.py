@@ -787,3 +787,43 @@ def test_agent_serves_tls_and_requires_client_certs_except_for_healthz(pki, fixt
     from k8s_gpu_node_checker_amd import cli
     a = cli.parse_args(["--probe-client-cert", "/c.pem", "--probe-client-key", "/k.pem"])
     assert (a.probe_client_cert, a.probe_client_key) == ("/c.pem", "/k.pem")
+
+
+def test_probe_tls_server_name_verifies_agents_reached_by_pod_ip(tmp_path, fixture_report):
+    """Agents reached by ``{pod_ip}`` present one certificate for the Service's name, not for every pod IP:
+    ``--probe-tls-server-name`` verifies against that name; without it the IP does not match the certificate
+    and the node is unknown with the TLS error."""
+    import asyncio
+    import subprocess
+    from k8s_gpu_node_checker_amd.parallel import fanout
+
+    def run(*args):
+        r = subprocess.run(["openssl", *args], capture_output=True, cwd=tmp_path)
+        if r.returncode != 0:
+            pytest.skip(f"openssl: {r.stderr[-200:]}")
+    name = "mi355x-node-agent.gpu-health.svc"
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "ca.key", "-out", "ca.crt", "-days", "1",
+        "-subj", "/CN=agents-ca")
+    run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", "srv.key", "-out", "srv.csr", "-subj", "/CN=agent")
+    (tmp_path / "srv.ext").write_text(f"subjectAltName=DNS:{name}\n")
+    run("x509", "-req", "-in", "srv.csr", "-CA", "ca.crt", "-CAkey", "ca.key", "-CAcreateserial", "-out", "srv.crt",
+        "-days", "1", "-extfile", "srv.ext")
+    ag = A.Agent("a", source="fixture", fixture=fixture_report)
+    ag.probe_once()
+    srv = A.serve(ag, "127.0.0.1", 0, tls=A.tls_context(str(tmp_path / "srv.crt"), str(tmp_path / "srv.key")))
+    url = f"https://127.0.0.1:{srv.server_address[1]}/probe"
+    try:
+        out = asyncio.run(fanout.fetch_all([{"name": "a", "url": url}], timeout=5, retries=0,
+                                           ca_file=str(tmp_path / "ca.crt")))
+        assert "CERTIFICATE_VERIFY_FAILED" in out[0]["error"] or "match" in out[0]["error"], out[0]
+        out = asyncio.run(fanout.fetch_all([{"name": "a", "url": url}], timeout=5, retries=0,
+                                           ca_file=str(tmp_path / "ca.crt"), server_name=name))
+        assert out[0]["node"] == "a" and out[0]["gpus"], out[0]
+        out = asyncio.run(fanout.fetch_all([{"name": "a", "url": url}], timeout=5, retries=0,
+                                           ca_file=str(tmp_path / "ca.crt"), server_name="other.svc"))
+        assert "error" in out[0]
+    finally:
+        srv.shutdown()
+        srv.server_close()
+    from k8s_gpu_node_checker_amd import cli
+    assert cli.parse_args(["--probe-tls-server-name", name]).probe_tls_server_name == name
