@@ -746,3 +746,39 @@ def test_every_alert_has_a_runbook_section():
               for r in g["rules"]}
     sections = set(re.findall(r"^## (\S+)\s*$", _read(os.path.join(REPO, "RUNBOOK.md")), re.M))
     assert alerts and alerts == sections, (alerts - sections, sections - alerts)
+
+
+def test_mtls_overlay_serves_the_agent_over_tls_and_documents_a_checker_that_reads_it():
+    """deploy/mtls/: the agent's command is the base command plus the three TLS flags, whose files are on the
+    mounted Secret; the kubelet probes switch to HTTPS; the checker command the overlay documents parses, uses
+    {pod_ip} over https and verifies against the Service's DNS name."""
+    import re
+    import shlex
+    base = os.path.join(REPO, "deploy", "mtls")
+    kust_text = _read(os.path.join(base, "kustomization.yaml"))
+    kust = yaml.safe_load(kust_text)
+    assert kust["resources"] == ["../"] and kust["patches"][0]["path"] == "daemonset-mtls.yaml"
+    patch = yaml.safe_load(_read(os.path.join(base, "daemonset-mtls.yaml")))
+    c = _agent_container(patch)
+    ds = next(d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "daemonset.yaml"))) if d)
+    base_cmd = ds["spec"]["template"]["spec"]["containers"][0]["command"]
+    assert c["command"][:len(base_cmd)] == base_cmd  # nothing else of the agent changes
+    a = agent.build_parser().parse_args(c["command"][1:])
+    mount = next(m for m in c["volumeMounts"] if m["name"] == "tls")
+    for path in (a.tls_cert_file, a.tls_key_file, a.tls_client_ca):
+        assert path and os.path.dirname(path) == mount["mountPath"]
+    vol = next(v for v in patch["spec"]["template"]["spec"]["volumes"] if v["name"] == "tls")
+    assert vol["secret"]["secretName"] == "mi355x-node-agent-tls" and mount["readOnly"]
+    for probe in ("readinessProbe", "livenessProbe"):
+        assert c[probe]["httpGet"]["scheme"] == "HTTPS" and c[probe]["httpGet"]["path"] == "/healthz"
+    # the documented checker command
+    doc = " ".join(ln.lstrip("# ").rstrip("\\ ") for ln in kust_text.splitlines() if ln.startswith("#"))
+    m = re.search(r"(check-gpu-node --mi355x .*?--probe-client-key \S+)", doc)
+    assert m, doc
+    from k8s_gpu_node_checker_amd import cli
+    args = cli.parse_args(shlex.split(m.group(1))[1:])
+    assert args.probe_endpoint == "https://{pod_ip}:9464/probe"
+    svc = next(d for d in yaml.safe_load_all(_read(os.path.join(REPO, "deploy", "daemonset.yaml")))
+               if d and d["kind"] == "Service")
+    assert args.probe_tls_server_name == f"{svc['metadata']['name']}.{svc['metadata']['namespace']}.svc"
+    assert args.probe_ca and args.probe_client_cert and args.probe_client_key
