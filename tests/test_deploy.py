@@ -782,3 +782,23 @@ def test_mtls_overlay_serves_the_agent_over_tls_and_documents_a_checker_that_rea
                if d and d["kind"] == "Service")
     assert args.probe_tls_server_name == f"{svc['metadata']['name']}.{svc['metadata']['namespace']}.svc"
     assert args.probe_ca and args.probe_client_cert and args.probe_client_key
+
+
+def test_monitoring_mtls_overlay_scrapes_the_tls_agents():
+    """deploy/monitoring/mtls/: the agents' ServiceMonitor endpoint is the base one (port, path, interval,
+    relabelings -- the list is replaced whole, CRD lists do not merge) plus https and a tlsConfig naming the same
+    Service DNS name as deploy/mtls/."""
+    base_dir = os.path.join(REPO, "deploy", "monitoring")
+    kust = yaml.safe_load(_read(os.path.join(base_dir, "mtls", "kustomization.yaml")))
+    assert kust["resources"] == ["../"] and kust["patches"][0]["path"] == "servicemonitor-mtls.yaml"
+    patch = yaml.safe_load(_read(os.path.join(base_dir, "mtls", "servicemonitor-mtls.yaml")))
+    base = next(d for d in yaml.safe_load_all(_read(os.path.join(base_dir, "monitoring.yaml")))
+                if d and d["kind"] == "ServiceMonitor" and d["metadata"]["name"] == patch["metadata"]["name"])
+    (ep,), (base_ep,) = patch["spec"]["endpoints"], base["spec"]["endpoints"]
+    assert {k: v for k, v in ep.items() if k not in ("scheme", "tlsConfig")} == base_ep
+    assert ep["scheme"] == "https"
+    tls = ep["tlsConfig"]
+    assert tls["serverName"] == "mi355x-node-agent.gpu-health.svc"
+    assert tls["ca"]["secret"]["key"] == "ca.crt" and tls["cert"]["secret"]["key"] == "tls.crt"
+    assert tls["keySecret"]["key"] == "tls.key"
+    assert "mi355x-node-agent.gpu-health.svc" in _read(os.path.join(REPO, "deploy", "mtls", "kustomization.yaml"))
