@@ -223,7 +223,7 @@ def test_fleet_properties(nodes):
         # it only excuses when the fleet's median is itself short
         if view["explained"]:
             row = summary["gemm@[4096, 4096, 4096]/tflops"]
-            assert row["platform_shortfall"] and row["median_fraction"] < P.DEGRADED_FRACTION
+            assert row["platform_shortfall"] and row["median_fraction"] <= P.DEGRADED_FRACTION  # rounded
         for f in view["findings"]:
             assert f["ratio"] <= F.FLEET_FAIL_RATIO  # rounded to 3 places
         # every warning the fleet added is a fleet finding
