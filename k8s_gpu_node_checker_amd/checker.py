@@ -255,6 +255,7 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
         # reports the fleet judgement may compare: the judged ones, plus (when the scan parsed the annotations
         # anyway, --json-extended / --explain / --fleet) those of nodes judged by their condition
         compare: List[Optional[Dict[str, Any]]] = [None] * len(scan.gpu_nodes)
+        cached: List[bool] = [False] * len(scan.gpu_nodes)  # compare[i] is ex.report(): its fractions are cached
         parsed = opts.json_extended
         comparable = 0
         for i, (node, ex, rep) in enumerate(zip(scan.gpu_nodes, scan.extras, reports)):
@@ -265,10 +266,12 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
                     r = ex.report()
                     if isinstance(r, dict) and r.get("node") in (None, node["name"]):
                         compare[i] = r
+                        cached[i] = True
                         comparable += 1
                 continue
             if rep is None and ex.health_annotation:
                 rep = ex.report()
+            cached[i] = rep is not None and reports[i] is None
             other = rep.get("node") if isinstance(rep, dict) else None
             if other is not None and other != node["name"]:
                 # a report names the node it was taken on: one fetched from a reassigned or stale IP (or an
@@ -282,7 +285,9 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
         if comparable >= 3:
             from .models import fleet as F
             current = [r if H.report_gate(r, exp, now) is None else None for r in compare]
-            summary, fleet_views = F.judge_fleet([n["name"] for n in scan.gpu_nodes], current)
+            fracs = [ex.fleet_fractions() if cached[i] and current[i] is not None else None
+                     for i, ex in enumerate(scan.extras)]
+            summary, fleet_views = F.judge_fleet([n["name"] for n in scan.gpu_nodes], current, fracs)
             if summary and fleet_out is not None:
                 fleet_out.update(summary=summary, views=fleet_views)
         for i, (node, ex, rep) in enumerate(zip(scan.gpu_nodes, scan.extras, reports)):

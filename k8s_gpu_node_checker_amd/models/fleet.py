@@ -71,12 +71,28 @@ def _num(v: Any) -> bool:
 def node_fractions(report: Any) -> Dict[Key, float]:
     """``(test, shape, metric) -> the node's median GPU`` (rate as a fraction of its scaled reference), plus the
     node-level fabric rates (``RAW_TESTS``, GB/s, keyed by how many GPUs took part)."""
+    # the checker runs this over every node of a --health-reeval LIST: one flat pass, no per-result helpers
     per: Dict[Key, List[float]] = {}
-    for _g, test, res, fr in _gpu_results(report):
-        shape = _shape(res)
-        for m, v in fr.items():
-            per.setdefault((test, shape, m), []).append(v)
-    out = {k: statistics.median(v) for k, v in per.items()}
+    num = (int, float)
+    gpus = report.get("gpus") if isinstance(report, dict) else None
+    for g in gpus if isinstance(gpus, list) else ():
+        diag = g.get("diag") if isinstance(g, dict) else None
+        if not isinstance(diag, dict):
+            continue
+        for test, res in diag.items():
+            if not isinstance(res, dict):
+                continue
+            rates, expect = res.get("rates"), res.get("expect")
+            if not isinstance(rates, dict) or not isinstance(expect, dict):
+                continue
+            shape = None
+            for m, v in rates.items():
+                e = expect.get(m)
+                if isinstance(v, num) and isinstance(e, num) and e > 0:
+                    if shape is None:
+                        shape = _shape(res)
+                    per.setdefault((test, shape, m), []).append(float(v) / float(e))
+    out = {k: (v[0] if len(v) == 1 else statistics.median(v)) for k, v in per.items()}
     fab = report.get("fabric") if isinstance(report, dict) else None
     if isinstance(fab, dict):
         p2p, rccl = fab.get("p2p"), fab.get("rccl")
@@ -87,7 +103,24 @@ def node_fractions(report: Any) -> Dict[Key, float]:
     return out
 
 
-def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]]
+def _loo_medians(vals: Dict[int, float]) -> Dict[int, float]:
+    """Each member's leave-one-out median (the median of the *other* members' values), O(n log n) for the
+    whole set: one sort, then the median of the sorted list with one position skipped."""
+    order = sorted(vals, key=lambda i: vals[i])
+    s = [vals[i] for i in order]
+    n = len(s)
+    L = n - 1
+
+    def at(j: int, k: int) -> float:  # element j of s with position k removed
+        return s[j] if j < k else s[j + 1]
+    out = {}
+    for k, i in enumerate(order):
+        out[i] = at(L // 2, k) if L % 2 else (at(L // 2 - 1, k) + at(L // 2, k)) / 2.0
+    return out
+
+
+def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]],
+                fractions: Optional[List[Optional[Dict[Key, float]]]] = None
                 ) -> Tuple[Dict[str, Any], List[Optional[Dict[str, Any]]]]:
     """Judge every report's rate tests against the fleet.  The reports are not changed (the watcher keeps them
     across checks); the judgement comes back as one view per node, which ``models/health.evaluate_report``
@@ -100,12 +133,14 @@ def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]]
 
     ``reports`` is parallel to ``names`` (None where a node has no report to judge); a node with nothing to say
     gets None.  The summary, per test: node count, median, min and max fraction, the outliers, the three slowest
-    nodes and whether the fleet is short alike."""
+    nodes and whether the fleet is short alike.  ``fractions`` (parallel, optional): reports' ``node_fractions``
+    already computed (``NodeExtras.fleet_fractions`` caches them per node object)."""
     values: Dict[Key, Dict[int, float]] = {}
     for i, rep in enumerate(reports):
         if not isinstance(rep, dict):
             continue
-        for key, v in node_fractions(rep).items():
+        fr = fractions[i] if fractions is not None and fractions[i] is not None else node_fractions(rep)
+        for key, v in fr.items():
             values.setdefault(key, {})[i] = v
     views: List[Optional[Dict[str, Any]]] = [None] * len(reports)
 
@@ -128,8 +163,9 @@ def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]]
                                "outliers": [],
                                "slowest": [{"node": names[i], "fraction": round(v, 3)}
                                            for i, v in sorted(vals.items(), key=lambda kv: (kv[1], kv[0]))[:3]]}
+        loo = _loo_medians(vals)
         for i, v in vals.items():
-            others = statistics.median([x for j, x in vals.items() if j != i])
+            others = loo[i]
             ratio = v / others if others > 0 else 1.0
             if ratio < FLEET_FAIL_RATIO:
                 f = {"test": key[0], "metric": key[2], "ratio": round(ratio, 3), "nodes": len(vals) - 1}

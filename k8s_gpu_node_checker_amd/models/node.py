@@ -102,7 +102,7 @@ class NodeExtras:
     """Side information the default report does not show but the health gate uses."""
 
     __slots__ = ("ready_condition", "capacity", "allocatable", "unschedulable", "health_annotation", "internal_ip",
-                 "health_condition", "_report")
+                 "health_condition", "_report", "_fleet")
 
     def __init__(self, ready_condition: bool, capacity: Dict[str, int], allocatable: Dict[str, int],
                  unschedulable: bool, health_annotation: Optional[str], internal_ip: Optional[str] = None,
@@ -116,6 +116,7 @@ class NodeExtras:
         #: ``(status, reason, message, lastHeartbeatTime epoch)`` of the AMDGPUHealthy condition
         self.health_condition = health_condition
         self._report: Any = _UNPARSED
+        self._fleet: Any = None
 
     def report(self) -> Optional[Dict[str, Any]]:
         """The report annotation parsed (``models.health.parse_annotation``), once per node object: the
@@ -129,6 +130,18 @@ class NodeExtras:
             from .health import parse_annotation
             r = self._report = _slim(parse_annotation(self.health_annotation))
         return r
+
+    def fleet_fractions(self) -> Dict[Any, float]:
+        """``models/fleet.node_fractions`` of :meth:`report`, once per node object: the watcher re-judges the
+        fleet on every event, and only the nodes that changed are new objects."""
+        try:
+            f = self._fleet
+        except AttributeError:  # built by the native scanner
+            f = None
+        if f is None:
+            from .fleet import node_fractions
+            f = self._fleet = node_fractions(self.report())
+        return f
 
     def to_dict(self) -> Dict[str, Any]:
         return {

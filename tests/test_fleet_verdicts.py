@@ -328,3 +328,27 @@ def test_a_node_whose_fabric_runs_behind_the_fleet(reports):
     row = summary["rccl@world=8/busbw_gbps"]
     assert row["unit"] == "GB/s" and not row["platform_shortfall"] and row["outliers"] == [{"node": "weak", "ratio": 0.6}]
     assert summary["xgmi_p2p@pairs=56/median_gbps"]["outliers"] == []
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.dictionaries(st.integers(0, 50), st.floats(0.01, 2.0) | st.sampled_from([0.5, 1.0]), min_size=2,
+                       max_size=40))
+def test_leave_one_out_medians_match_the_definition(vals):
+    import statistics
+    loo = F._loo_medians(vals)
+    for i in vals:
+        assert loo[i] == pytest.approx(statistics.median([x for j, x in vals.items() if j != i]), abs=1e-12)
+
+
+def test_node_fractions_are_cached_per_node_object(reports, monkeypatch):
+    """The watcher re-judges the fleet on every event: a node object computes its fractions once."""
+    from k8s_gpu_node_checker_amd.models.node import NodeExtras
+    rep = reports({"n0": 0.9})["n0"]
+    ex = NodeExtras(True, {"amd.com/gpu": 8}, {"amd.com/gpu": 8}, False,
+                    next(iter(fixtures.health_annotation(rep).values())))
+    calls = []
+    real = F.node_fractions
+    monkeypatch.setattr(F, "node_fractions", lambda r: calls.append(1) or real(r))
+    first = ex.fleet_fractions()
+    assert ex.fleet_fractions() is first and len(calls) == 1
+    assert first == real(ex.report()) and first[("gemm", "[4096, 4096, 4096]", "tflops")] == pytest.approx(0.9)
