@@ -346,6 +346,17 @@ class PublishError(RuntimeError):
         self.wrote = wrote
 
 
+def _annotation_gpu(g: Dict[str, Any]) -> Dict[str, Any]:
+    """One GPU entry as the node annotation carries it (``Agent.annotation``)."""
+    from ..models.node import DIAG_AGENT_ONLY
+    out = {k: v for k, v in g.items() if k not in _ANNOTATION_DROP}
+    diag = out.get("diag")
+    if isinstance(diag, dict):
+        out["diag"] = {t: ({k: v for k, v in r.items() if k not in DIAG_AGENT_ONLY} if isinstance(r, dict) else r)
+                       for t, r in diag.items()}
+    return out
+
+
 class Agent:
     def __init__(self, node: str, source: str = "auto", fixture: Optional[str] = None, diag_level: int = 0,
                  diag_interval: float = 3600.0, devices: Optional[List[int]] = None,
@@ -821,9 +832,10 @@ class Agent:
         """The report as the node annotation, minus the raw counters (xGMI traffic, throttle accumulators,
         per-process VRAM, per-GPU probe time): every client that LISTs or watches nodes receives the
         annotation, it is rewritten only when the health content changes, so those would only be stale
-        bytes there; they stay on ``/probe`` and ``/metrics``."""
-        gpus = [{k: v for k, v in g.items() if k not in _ANNOTATION_DROP} if isinstance(g, dict) else g
-                for g in rep.get("gpus") or []]
+        bytes there; they stay on ``/probe`` and ``/metrics``.  The diagnostics' per-XCD/CU maps, burn-in rows
+        and wall times stay there too (``models/node.DIAG_AGENT_ONLY``): the checker judges from the rest, and
+        at fleet scale parsing them was a third of a report-reading check."""
+        gpus = [_annotation_gpu(g) if isinstance(g, dict) else g for g in rep.get("gpus") or []]
         doc = dict(rep, gpus=gpus)
         value = encode_annotation(doc, self.annotation_encoding)
         if len(value) > ANNOTATION_JSON_MAX and self.annotation_encoding == "json":

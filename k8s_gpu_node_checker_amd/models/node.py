@@ -155,9 +155,9 @@ class NodeExtras:
 
 
 # per-test fields of a diagnostic result that only the agent's own views read (per-XCD/CU maps, per-kind burn-in
-# rows, wall time): the checker keeps every node's parsed report (the watcher, across checks), and these are
-# ~36 % of it
-_DIAG_AGENT_ONLY = ("map", "kinds", "wall_s")
+# rows, wall time): the agent leaves them out of the node annotation, and the checker drops them from reports
+# fetched from /probe too -- it keeps every node's parsed report (the watcher, across checks)
+DIAG_AGENT_ONLY = ("map", "kinds", "wall_s")
 
 
 def _slim(report: Any) -> Any:
@@ -166,7 +166,7 @@ def _slim(report: Any) -> Any:
         diag = g.get("diag") if isinstance(g, dict) else None
         for res in diag.values() if isinstance(diag, dict) else ():
             if isinstance(res, dict):
-                for k in _DIAG_AGENT_ONLY:
+                for k in DIAG_AGENT_ONLY:
                     res.pop(k, None)
     return report
 
