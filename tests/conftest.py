@@ -9,6 +9,17 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
+# Property tests (hypothesis): the same examples every run, so the suite's result is a function of the tree (the
+# round driver and CI run it once); HYPOTHESIS_PROFILE=explore draws fresh examples to hunt for new failures.
+try:
+    from hypothesis import settings as _hsettings
+
+    _hsettings.register_profile("ci", derandomize=True, print_blob=True)
+    _hsettings.register_profile("explore", derandomize=False, print_blob=True)
+    _hsettings.load_profile(os.environ.get("HYPOTHESIS_PROFILE", "ci"))
+except ImportError:  # hypothesis is optional: its tests import it themselves
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
