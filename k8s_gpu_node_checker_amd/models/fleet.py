@@ -31,6 +31,8 @@ from typing import Any, Dict, List, Optional, Tuple
 from .peers import DEGRADED_FRACTION, FAIL_FRACTION, _rate_fractions
 
 FLEET_MIN_NODES = 3
+# the MI355X's identifiers (models/health.MI35X_DEVICE_IDS, amd-smi product name): results keyed without a model
+MI355X_IDS = ("0x75a3", "amd instinct mi355 oam")
 # a node below this share of the other nodes' median is an outlier (the per-GPU peer ratio, one level up)
 FLEET_FAIL_RATIO = 0.85
 # a node within this ratio of the fleet's median shares the fleet's condition
@@ -39,11 +41,16 @@ FLEET_UNIFORM_SPREAD = 1.10
 Key = Tuple[str, str, str]  # (test, shape, metric)
 
 
-def _shape(res: Dict[str, Any]) -> str:
+def _shape(res: Dict[str, Any], gpu: Any = None) -> str:
+    """What makes two results comparable besides the test: its size, and the GPU model (an MI350X is compared
+    with MI350Xs -- its rates sit under an MI355X's at the same fraction of the MI355X references)."""
+    size = ""
     for k in ("shape", "gib", "slice_mib"):
         if k in res:
-            return repr(res[k])
-    return ""
+            size = repr(res[k])
+            break
+    model = (gpu.get("device_id") or gpu.get("product_name")) if isinstance(gpu, dict) else None
+    return f"{size} on {model}" if isinstance(model, str) and model and model.lower() not in MI355X_IDS else size
 
 
 def _gpu_results(report: Any):
@@ -90,7 +97,7 @@ def node_fractions(report: Any) -> Dict[Key, float]:
                 e = expect.get(m)
                 if isinstance(v, num) and isinstance(e, num) and e > 0:
                     if shape is None:
-                        shape = _shape(res)
+                        shape = _shape(res, g)
                     per.setdefault((test, shape, m), []).append(float(v) / float(e))
     out = {k: (v[0] if len(v) == 1 else statistics.median(v)) for k, v in per.items()}
     fab = report.get("fabric") if isinstance(report, dict) else None
@@ -188,7 +195,7 @@ def explains_node_finding(fleet: Optional[Dict[str, Any]], f: Dict[str, Any]) ->
     return any(k[0] == f.get("test") and k[2] == f.get("metric") for k in fleet["explained"])
 
 
-def explains_gpu_result(fleet: Optional[Dict[str, Any]], test: str, res: Dict[str, Any]) -> bool:
+def explains_gpu_result(fleet: Optional[Dict[str, Any]], test: str, res: Dict[str, Any], gpu: Any = None) -> bool:
     """A GPU's degraded result that is only slow -- no failure, lag or drift -- on metrics the fleet is short
     alike on, with the GPU itself in line with the fleet's median."""
     if not fleet or not fleet.get("explained"):
@@ -198,7 +205,7 @@ def explains_gpu_result(fleet: Optional[Dict[str, Any]], test: str, res: Dict[st
     fr = _rate_fractions(res)
     if not fr or min(fr.values()) < FAIL_FRACTION:
         return False
-    shape = _shape(res)
+    shape = _shape(res, gpu)
     for m, v in fr.items():
         if v >= DEGRADED_FRACTION:
             continue

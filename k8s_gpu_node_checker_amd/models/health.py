@@ -468,7 +468,7 @@ def evaluate_gpu(g: Dict[str, Any], exp: HealthExpectations, now: Optional[float
             elif isinstance(res, dict) and res.get("degraded"):  # 85-95 % of its reference rate (ops/diag.py)
                 if fleet:
                     from .fleet import explains_gpu_result
-                    if explains_gpu_result(fleet, test, res):
+                    if explains_gpu_result(fleet, test, res, g):
                         continue  # slow alike with the whole fleet: the platform's normal (models/fleet.py)
                 detail = res.get("detail") or ""
                 warn.append(f"gpu{idx}: diag {test} slow" + (f" ({detail})" if detail else ""))

@@ -352,3 +352,16 @@ def test_node_fractions_are_cached_per_node_object(reports, monkeypatch):
     first = ex.fleet_fractions()
     assert ex.fleet_fractions() is first and len(calls) == 1
     assert first == real(ex.report()) and first[("gemm", "[4096, 4096, 4096]", "tflops")] == pytest.approx(0.9)
+
+
+def test_other_gpu_models_are_compared_with_their_own_kind(reports):
+    """An MI350X node (another device id) is not an outlier of an MI355X fleet: each model is its own fleet."""
+    reps = reports({"n0": 1.0, "n1": 1.0, "n2": 1.0, "m0": 0.80, "m1": 0.80, "m2": 0.80})
+    for n in ("m0", "m1", "m2"):
+        for g in reps[n]["gpus"]:
+            g["device_id"] = "0x75a0"
+    summary, verdicts = _judge(reps)
+    assert summary["gemm@[4096, 4096, 4096]/tflops"]["outliers"] == []
+    assert summary["gemm@[4096, 4096, 4096] on 0x75a0/tflops"]["nodes"] == 3
+    assert not any(w.startswith("fleet: ") for v in verdicts.values() for w in v.warnings)
+    assert F._shape({"shape": [1, 2, 3]}) == "[1, 2, 3]" and F._shape({}, None) == ""
