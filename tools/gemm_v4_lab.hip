@@ -49,7 +49,10 @@ __device__ __forceinline__ bf16x8 v4_frag(const unsigned char* region, int row, 
   return *reinterpret_cast<const bf16x8*>(region + row * 64 + ((fq ^ v4_swz(row)) << 4));
 }
 
-template <bool PRIO>
+// LATE: group 0 waits for the LDS-DMA at the end of its MFMA slot instead of its load slot -- one slot more for
+// the pieces to land (its deadline is the next barrier's load slot; group 1's, one slot behind, is its own load
+// slot's end).
+template <bool PRIO, bool LATE = false>
 __global__ void __launch_bounds__(V2_THREADS, 1)
 gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
                int K) {
@@ -109,10 +112,12 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
       for (int n = 0; n < 4; ++n) fb[n] = v4_frag(rb, wc * 64 + n * 16 + frow, fq);
 #pragma unroll
       for (int m = 0; m < 8; ++m) fa[m] = v4_frag(ra, wr * 128 + m * 16 + frow, fq);
-      if (more) {
-        __builtin_amdgcn_s_waitcnt(0x3f74);  // vmcnt(4): the previous load slot's pieces landed
-      } else {
-        __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
+      if (!LATE || wr == 1) {
+        if (more) {
+          __builtin_amdgcn_s_waitcnt(0x3f74);  // vmcnt(4): the previous load slot's pieces landed
+        } else {
+          __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
+        }
       }
       STG_BARRIER();
       // MFMA slot
@@ -126,6 +131,13 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
       for (int m = 0; m < 8; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n) asm volatile("" : "+v"(acc[m][n]));
+      if (LATE && wr == 0) {
+        if (more) {
+          __builtin_amdgcn_s_waitcnt(0x3f74);  // vmcnt(4): the half the next load slot reads landed
+        } else {
+          __builtin_amdgcn_s_waitcnt(0x3f70);
+        }
+      }
       STG_BARRIER();
     }
   }
@@ -167,9 +179,9 @@ double time_ms(L launch, int iters) {
   return ms / iters;
 }
 
-template <bool PRIO>
+template <bool PRIO, bool LATE = false>
 void launch_v4(const __bf16* A, const __bf16* Bt, float* C, int M, int N, int K) {
-  hipLaunchKernelGGL((gemm_v4_kernel<PRIO>), dim3((M / V2_BM) * (N / V2_BN)), dim3(V2_THREADS), 2 * V4_STAGE,
+  hipLaunchKernelGGL((gemm_v4_kernel<PRIO, LATE>), dim3((M / V2_BM) * (N / V2_BN)), dim3(V2_THREADS), 2 * V4_STAGE,
                      nullptr, A, Bt, C, M, N, K);
 }
 
@@ -182,6 +194,10 @@ int main(int argc, char** argv) {
   CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<false>),
                          hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
   CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<true>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<false, true>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<true, true>),
                          hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
   for (int size : sizes) {
     if (size % 256 || size < 512) {
@@ -215,6 +231,8 @@ int main(int argc, char** argv) {
     rows.push_back({"v3(lds-epi)", [&] { launch_v3_inst<DT_BF16, true, false, 1>(A, Bt, C1, M, N, K, nullptr); }});
     rows.push_back({"v4", [&] { launch_v4<false>(A, Bt, C1, M, N, K); }});
     rows.push_back({"v4(prio)", [&] { launch_v4<true>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"v4(late)", [&] { launch_v4<false, true>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"v4(late,prio)", [&] { launch_v4<true, true>(A, Bt, C1, M, N, K); }});
     for (int r = 0; r < reps; ++r) {
       for (Row& row : rows) {
         CK(hipMemset(C1, 0xff, sizeof(float) * M * N));
