@@ -30,7 +30,8 @@ def _age(seconds: Optional[float]) -> str:
     return f"{seconds / 3600:.1f} h"
 
 
-_COLUMNS = ("GPU", "BDF", "gfx", "CUs", "VRAM MB", "ECC ue/ce", "xGMI", "PM fw", "diag", "vs peers", "findings")
+_COLUMNS = ("GPU", "BDF", "gfx", "CUs", "VRAM MB", "ECC ue/ce", "xGMI", "PM fw", "diag", "vs peers", "vs own",
+            "findings")
 
 
 def _min_ratio(diag: Dict[str, Any], key: str) -> Any:
@@ -66,6 +67,7 @@ def _gpu_row(e: Dict[str, Any]) -> List[str]:
             f"{txt(e['ecc_uncorrectable'], '-')}/{txt(e['ecc_correctable'], '-')}", txt(e["xgmi"]),
             txt(e["pm_fw"], "-"), dstate,
             f"x{e['peer_ratio_min']:.2f}" if isinstance(e.get("peer_ratio_min"), (int, float)) else "-",
+            f"x{e['baseline_ratio_min']:.2f}" if isinstance(e.get("baseline_ratio_min"), (int, float)) else "-",
             "; ".join(e["findings"]) or "ok"]
 
 

@@ -311,3 +311,18 @@ def test_status_table_shows_each_gpus_lowest_ratio_to_its_peers(node):
     row0 = next(ln for ln in text.splitlines() if ln.strip().startswith("0 "))
     assert "x0.80" in row2 and "fail:" in row2 and "x1.00" in row0
     assert head.index("vs peers") < head.index("findings")
+
+
+def test_status_table_shows_each_gpus_lowest_ratio_to_its_own_baseline(node):
+    from k8s_gpu_node_checker_amd.explain import report_text
+    lib = node(2, rate=1.10)
+    ag = _agent(2, diag_interval=0.0)
+    for _ in range(B.BASELINE_RUNS):
+        ag.probe_once()
+    lib.rate = 0.96
+    rep = ag.probe_once()
+    text = report_text(rep, ag.evaluate(rep))
+    head = next(ln for ln in text.splitlines() if "vs own" in ln)
+    row0 = next(ln for ln in text.splitlines() if ln.strip().startswith("0 "))
+    assert head.index("vs peers") < head.index("vs own") < head.index("findings")
+    assert "x0.87" in row0 and "own baseline" in row0
