@@ -53,19 +53,6 @@ def _shape(res: Dict[str, Any], gpu: Any = None) -> str:
     return f"{size} on {model}" if isinstance(model, str) and model and model.lower() not in MI355X_IDS else size
 
 
-def _gpu_results(report: Any):
-    gpus = report.get("gpus") if isinstance(report, dict) else None
-    for g in gpus if isinstance(gpus, list) else []:
-        diag = g.get("diag") if isinstance(g, dict) else None
-        if not isinstance(diag, dict):
-            continue
-        for test, res in diag.items():
-            if isinstance(res, dict):
-                fr = _rate_fractions(res)
-                if fr:
-                    yield g, test, res, fr
-
-
 # node-level fabric results (level 2, ``report["fabric"]``) compared across nodes as raw rates: no reference
 # to be short of, so outliers only (a node whose xGMI pairs or RCCL collectives run well under the others')
 RAW_TESTS = ("xgmi_p2p", "rccl")
@@ -75,12 +62,15 @@ def _num(v: Any) -> bool:
     return isinstance(v, (int, float)) and not isinstance(v, bool) and v > 0
 
 
+def _rate(v: Any) -> bool:  # a measured rate may be 0 (a GPU that did nothing), never negative or a bool
+    return isinstance(v, (int, float)) and not isinstance(v, bool) and v >= 0
+
+
 def node_fractions(report: Any) -> Dict[Key, float]:
     """``(test, shape, metric) -> the node's median GPU`` (rate as a fraction of its scaled reference), plus the
     node-level fabric rates (``RAW_TESTS``, GB/s, keyed by how many GPUs took part)."""
     # the checker runs this over every node of a --health-reeval LIST: one flat pass, no per-result helpers
     per: Dict[Key, List[float]] = {}
-    num = (int, float)
     gpus = report.get("gpus") if isinstance(report, dict) else None
     for g in gpus if isinstance(gpus, list) else ():
         diag = g.get("diag") if isinstance(g, dict) else None
@@ -95,7 +85,7 @@ def node_fractions(report: Any) -> Dict[Key, float]:
             shape = None
             for m, v in rates.items():
                 e = expect.get(m)
-                if isinstance(v, num) and isinstance(e, num) and e > 0:
+                if _rate(v) and _num(e):
                     if shape is None:
                         shape = _shape(res, g)
                     per.setdefault((test, shape, m), []).append(float(v) / float(e))
