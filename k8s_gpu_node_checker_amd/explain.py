@@ -147,8 +147,12 @@ def diagnose(cluster: ClusterConnection, node_name: str, opts: CheckOptions) -> 
                          "node_findings": [ln for ln in lines if ln.split(" ", 1)[0] not in shown]}
     if fleet.get("summary"):
         # this node's place in the fleet (models/fleet.py): per test, the fleet's median and this node's ratio to it
-        from .models.fleet import explained_text
-        doc["fleet_diag"] = {"summary": fleet["summary"], "explained": explained_text(view) if view else []}
+        from .models.fleet import explained_text, summary_key
+        mine = {summary_key(k): v for k, v in ex.fleet_fractions().items()}
+        ratios = {k: round(mine[k] / row["median_fraction"], 3) for k, row in fleet["summary"].items()
+                  if k in mine and row.get("median_fraction")}
+        doc["fleet_diag"] = {"summary": fleet["summary"], "explained": explained_text(view) if view else [],
+                             "node_ratio": ratios}
     doc["counts_as_ready"] = bool(node["ready"])
     return doc
 
@@ -191,6 +195,10 @@ def render(doc: Dict[str, Any], out: TextIO) -> None:
             out.write(f"  node: {ln}\n")
     fd = doc.get("fleet_diag")
     if fd:
+        low = sorted(fd.get("node_ratio", {}).items(), key=lambda kv: kv[1])[:3]
+        if low:
+            out.write("  fleet: lowest against the fleet's median node: "
+                      + ", ".join(f"{k} x{r:.2f}" for k, r in low) + "\n")
         for ln in fd["explained"]:
             out.write(f"  fleet: {ln}\n")
     out.write(f"=> counts as Ready: {'yes' if doc['counts_as_ready'] else 'no'}\n")

@@ -100,6 +100,11 @@ def node_fractions(report: Any) -> Dict[Key, float]:
     return out
 
 
+def summary_key(key: Key) -> str:
+    """``test@shape/metric``: a key of ``judge_fleet``'s summary."""
+    return f"{key[0]}{('@' + key[1]) if key[1] else ''}/{key[2]}"
+
+
 def _loo_medians(vals: Dict[int, float]) -> Dict[int, float]:
     """Each member's leave-one-out median (the median of the *other* members' values), O(n log n) for the
     whole set: one sort, then the median of the sorted list with one position skipped."""
@@ -174,7 +179,7 @@ def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]],
                 row["outliers"].append({"node": names[i], "ratio": round(ratio, 3)})
             elif platform_short and max(v, med) <= FLEET_UNIFORM_SPREAD * min(v, med):
                 view(i)["explained"][key] = {"fleet_fraction": round(med, 3), "nodes": len(vals)}
-        summary[f"{key[0]}{('@' + key[1]) if key[1] else ''}/{key[2]}"] = row
+        summary[summary_key(key)] = row
     return summary, views
 
 

@@ -161,6 +161,12 @@ def test_cli_fleet_and_explain_show_the_fleet(run_cli, reports, mock_cluster, tm
     assert p.returncode == 0 and "MI355X verdict: healthy" in p.stdout
     assert "  fleet: diag gemm tflops: the fleet's median node is at 88% of the MI355X reference (4 nodes alike)" \
         in p.stdout
+    assert "  fleet: lowest against the fleet's median node: " in p.stdout
+    p = run_cli(["--kubeconfig", kc, "--explain", "slow"])
+    low = next(ln for ln in p.stdout.splitlines() if "lowest against the fleet's median node" in ln)
+    assert "x0.80" in low, low
+    d = json.loads(run_cli(["--kubeconfig", kc, "--explain", "slow", "--json"]).stdout)
+    assert d["fleet_diag"]["node_ratio"]["gemm@[4096, 4096, 4096]/tflops"] == pytest.approx(0.795, abs=0.01)
     d = json.loads(run_cli(["--kubeconfig", kc, "--json", "--json-extended"]).stdout)
     assert d["mi355x"]["diag_fleet"]["gemm@[4096, 4096, 4096]/tflops"]["nodes"] == 4
 
