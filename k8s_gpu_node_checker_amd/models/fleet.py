@@ -111,6 +111,8 @@ def _loo_medians(vals: Dict[int, float]) -> Dict[int, float]:
     order = sorted(vals, key=lambda i: vals[i])
     s = [vals[i] for i in order]
     n = len(s)
+    if n < 2:
+        return {}  # nobody else to compare with
     L = n - 1
 
     def at(j: int, k: int) -> float:  # element j of s with position k removed
