@@ -41,16 +41,19 @@ FLEET_UNIFORM_SPREAD = 1.10
 Key = Tuple[str, str, str]  # (test, shape, metric)
 
 
+def _size(res: Dict[str, Any]) -> str:
+    for k in ("shape", "gib", "slice_mib"):
+        if k in res:
+            return repr(res[k])
+    return ""
+
+
 def _shape(res: Dict[str, Any], gpu: Any = None) -> str:
     """What makes two results comparable besides the test: its size, and the GPU model (an MI350X is compared
     with MI350Xs -- its rates sit under an MI355X's at the same fraction of the MI355X references)."""
-    size = ""
-    for k in ("shape", "gib", "slice_mib"):
-        if k in res:
-            size = repr(res[k])
-            break
     model = (gpu.get("device_id") or gpu.get("product_name")) if isinstance(gpu, dict) else None
-    return f"{size} on {model}" if isinstance(model, str) and model and model.lower() not in MI355X_IDS else size
+    suffix = f" on {model}" if isinstance(model, str) and model and model.lower() not in MI355X_IDS else ""
+    return _size(res) + suffix
 
 
 # node-level fabric results (level 2, ``report["fabric"]``) compared across nodes as raw rates: no reference
@@ -62,33 +65,37 @@ def _num(v: Any) -> bool:
     return isinstance(v, (int, float)) and not isinstance(v, bool) and v > 0
 
 
-def _rate(v: Any) -> bool:  # a measured rate may be 0 (a GPU that did nothing), never negative or a bool
-    return isinstance(v, (int, float)) and not isinstance(v, bool) and v >= 0
-
-
 def node_fractions(report: Any) -> Dict[Key, float]:
     """``(test, shape, metric) -> the node's median GPU`` (rate as a fraction of its scaled reference), plus the
     node-level fabric rates (``RAW_TESTS``, GB/s, keyed by how many GPUs took part)."""
-    # the checker runs this over every node of a --health-reeval LIST: one flat pass, no per-result helpers
+    # the checker runs this over every node of a report-reading LIST (1000 nodes x 8 GPUs x 7 tests): one flat
+    # pass, the GPU model resolved once per GPU, numbers tested by exact type (a bool is not a rate)
     per: Dict[Key, List[float]] = {}
     gpus = report.get("gpus") if isinstance(report, dict) else None
     for g in gpus if isinstance(gpus, list) else ():
         diag = g.get("diag") if isinstance(g, dict) else None
         if not isinstance(diag, dict):
             continue
+        suffix = _shape({}, g)  # " on <model>" for other GPU models, "" for the MI355X
         for test, res in diag.items():
-            if not isinstance(res, dict):
+            if type(res) is not dict:
                 continue
             rates, expect = res.get("rates"), res.get("expect")
-            if not isinstance(rates, dict) or not isinstance(expect, dict):
+            if type(rates) is not dict or type(expect) is not dict:
                 continue
             shape = None
             for m, v in rates.items():
                 e = expect.get(m)
-                if _rate(v) and _num(e):
+                tv, te = type(v), type(e)
+                if (tv is float or tv is int) and (te is float or te is int) and v >= 0 and e > 0:
                     if shape is None:
-                        shape = _shape(res, g)
-                    per.setdefault((test, shape, m), []).append(float(v) / float(e))
+                        shape = _size(res) + suffix
+                    key = (test, shape, m)
+                    lst = per.get(key)
+                    if lst is None:
+                        per[key] = [v / e]
+                    else:
+                        lst.append(v / e)
     out = {k: (v[0] if len(v) == 1 else statistics.median(v)) for k, v in per.items()}
     fab = report.get("fabric") if isinstance(report, dict) else None
     if isinstance(fab, dict):
