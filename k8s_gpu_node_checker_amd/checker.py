@@ -60,6 +60,9 @@ class CheckOptions:
         self.probe_timeout = 2.0
         self.probe_ca: Optional[str] = None
         self.probe_tls_server_name: Optional[str] = None
+        #: ``--watch-events``: a ``parallel.fanout.ProbeCache`` reused across evaluations (``--probe-cache-ttl``)
+        self.probe_cache: Optional[Any] = None
+        self.probe_cache_ttl = 30.0
         self.probe_client_cert: Optional[str] = None
         self.probe_client_key: Optional[str] = None
         self.health_reeval = False
@@ -195,7 +198,7 @@ def resolve_agent_endpoints(cluster: Optional[ClusterConnection], opts: CheckOpt
     ``--probe-service`` (one paged GET; RBAC ``endpointslices: list`` in that namespace,
     ``deploy/rbac.yaml``).  Returns ``(addresses, None)`` or ``(None, error)``; an error makes every node
     ``unknown`` with that reason instead of failing the check."""
-    from .parallel.fanout import agent_addresses, template_fields
+    from .parallel.fanout import template_fields
     if not opts.probe_endpoint or "pod_ip" not in template_fields(opts.probe_endpoint):
         return None, None
     if cluster is None:
@@ -203,6 +206,20 @@ def resolve_agent_endpoints(cluster: Optional[ClusterConnection], opts: CheckOpt
     ns, _, svc = (opts.probe_service or AGENT_SERVICE).partition("/")
     if not ns or not svc:
         return None, f"--probe-service {opts.probe_service!r} is not NAMESPACE/NAME"
+    cache = opts.probe_cache
+    if cache is not None:
+        hit = cache.fresh_endpoints(time.monotonic())
+        if hit is not None:
+            return hit
+        res = _list_agent_endpoints(cluster, opts, tracer, ns, svc)
+        cache.endpoints = (time.monotonic(), res)
+        return res
+    return _list_agent_endpoints(cluster, opts, tracer, ns, svc)
+
+
+def _list_agent_endpoints(cluster: ClusterConnection, opts: CheckOptions, tracer: Tracer, ns: str,
+                          svc: str) -> Tuple[Optional[Dict[str, str]], Optional[str]]:
+    from .parallel.fanout import agent_addresses
     client = KubeClient(cluster, timeout=opts.kube_timeout, retries=opts.kube_retries, tracer=tracer)
     try:
         with tracer.span("endpoints"):
@@ -237,7 +254,8 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
             reports = fetch_probe_reports(scan, opts.probe_endpoint, opts.probe_concurrency, opts.probe_timeout,
                                           ca_file=opts.probe_ca, client_cert=opts.probe_client_cert,
                                           client_key=opts.probe_client_key, pod_ips=pod_ips,
-                                          pod_ip_error=pod_err, server_name=opts.probe_tls_server_name)
+                                          pod_ip_error=pod_err, server_name=opts.probe_tls_server_name,
+                                          cache=opts.probe_cache)
         verdicts: List[Optional[H.Verdict]] = []
         changed = False
         unknown_ok = opts.probe_unknown == "allow"

@@ -68,6 +68,9 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
                                       "help": "https 프로브의 서버 인증서를 URL 의 호스트 대신 이 이름으로 검증 "
                                               "({pod_ip} 처럼 인증서에 없는 주소로 접속할 때, 예: "
                                               "mi355x-node-agent.gpu-health.svc)"}),
+    ("x", "--probe-cache-ttl", {"type": float, "default": 30.0, "metavar": "SEC",
+                                "help": "--watch-events + --probe-endpoint: 노드별로 가져온 리포트를 이 시간(초) 동안 "
+                                        "재사용 (에이전트는 1분마다 프로브; 기본: 30)"}),
     ("x", "--probe-client-cert", {"help": "에이전트가 클라이언트 인증서를 요구할 때 제시할 인증서 (PEM)"}),
     ("x", "--probe-client-key", {"help": "--probe-client-cert 의 개인 키 (PEM)"}),
     ("x", "--require-schedulable", {"action": "store_true",
@@ -283,6 +286,10 @@ def _watch_events(args: Any) -> int:
         opts.slack_gate = lambda result: statefile.should_notify(memo["prev"], result, only,
                                                                  args.slack_on_node_change)
         opts.slack_only_on_error = False  # the gate decides (a recovery must be able to send)
+        if opts.probe_endpoint:
+            # every batch of events re-evaluates the fleet: reuse the agents' reports and EndpointSlices a while
+            from .parallel.fanout import ProbeCache
+            opts.probe_cache = ProbeCache(opts.probe_cache_ttl)
         metrics = None
         if args.metrics_listen:
             from .utils.prom import MetricsServer, parse_listen

@@ -357,14 +357,63 @@ def run_coroutine(coro: Any) -> Any:
     return box["value"]
 
 
+class ProbeCache:
+    """Fan-out results kept for ``ttl`` seconds, for the event watcher (``--watch-events``), which re-evaluates the
+    whole fleet on every batch of node events: the agents probe once a minute, so fetching every agent's report
+    on every event only loads them (1000 nodes heartbeating every 5 minutes are ~3 events a second).  A report is
+    reused per (node, URL) while younger than ``ttl``; a failed fetch is not kept (the next evaluation retries
+    it).  The agents' EndpointSlices are kept the same way (``endpoints``)."""
+
+    def __init__(self, ttl: float = 30.0):
+        self.ttl = ttl
+        self._reports: Dict[Any, Any] = {}
+        self.endpoints: Optional[Any] = None  # (monotonic time, (addresses, error))
+        self.fetched = 0
+        self.reused = 0
+
+    def get(self, target: Dict[str, str], now: float) -> Optional[Dict[str, Any]]:
+        hit = self._reports.get((target["name"], target["url"]))
+        if hit is not None and now - hit[0] < self.ttl:
+            self.reused += 1
+            return hit[1]
+        return None
+
+    def put(self, target: Dict[str, str], report: Any, now: float) -> None:
+        self.fetched += 1
+        if isinstance(report, dict) and not report.get("error"):
+            self._reports[(target["name"], target["url"])] = (now, report)
+
+    def fresh_endpoints(self, now: float) -> Optional[Any]:
+        e = self.endpoints
+        return e[1] if e is not None and now - e[0] < self.ttl and e[1][1] is None else None
+
+
 def fetch_probe_reports(scan: Any, template: str, concurrency: int = 64, timeout: float = 2.0,
                         ca_file: Optional[str] = None, client_cert: Optional[str] = None,
                         client_key: Optional[str] = None, pod_ips: Optional[Dict[str, str]] = None,
                         pod_ip_error: Optional[str] = None,
-                        server_name: Optional[str] = None) -> List[Optional[Dict[str, Any]]]:
-    """Fetch one probe report per GPU node (parallel to ``scan.gpu_nodes``)."""
+                        server_name: Optional[str] = None,
+                        cache: Optional[ProbeCache] = None) -> List[Optional[Dict[str, Any]]]:
+    """Fetch one probe report per GPU node (parallel to ``scan.gpu_nodes``); with a ``cache``, reports it holds
+    fresh are reused and only the rest are fetched."""
+    import time
     targets = build_targets(scan, template, pod_ips, pod_ip_error)
     if not targets:
         return []
-    return list(run_coroutine(fetch_all(targets, concurrency, timeout, ca_file=ca_file, client_cert=client_cert,
-                                        client_key=client_key, server_name=server_name)))
+    now = time.monotonic()
+    out: List[Optional[Dict[str, Any]]] = [None] * len(targets)
+    todo = []
+    for i, t in enumerate(targets):
+        hit = cache.get(t, now) if cache is not None and not t.get("error") else None
+        if hit is not None:
+            out[i] = hit
+        else:
+            todo.append(i)
+    if todo:
+        got = run_coroutine(fetch_all([targets[i] for i in todo], concurrency, timeout, ca_file=ca_file,
+                                      client_cert=client_cert, client_key=client_key, server_name=server_name))
+        for i, rep in zip(todo, got):
+            out[i] = rep
+            if cache is not None and not targets[i].get("error"):
+                cache.put(targets[i], rep, now)
+    return out

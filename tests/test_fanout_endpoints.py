@@ -182,3 +182,44 @@ def test_probe_service_flag_selects_another_service(pod_network, mock_cluster, r
                  "--probe-endpoint", f"http://{{pod_ip}}:{pod_network}/probe"])
     states = [n["health"]["state"] for n in json.loads(p.stdout)["mi355x"]["nodes"]]
     assert states == ["healthy", "unhealthy", "healthy", "unknown"]
+
+
+def test_watch_mode_reuses_fetched_reports_and_endpoints_within_the_ttl(pod_network, mock_cluster, monkeypatch):
+    """--watch-events re-evaluates the fleet on every batch of node events: with a ProbeCache the agents' reports
+    and the EndpointSlices are fetched once per TTL, a failed fetch is retried at once, and after the TTL
+    everything is fetched again."""
+    from k8s_gpu_node_checker_amd.checker import CheckOptions, apply_health, scan_cluster
+    from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+    from k8s_gpu_node_checker_amd.models import health as H
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    from k8s_gpu_node_checker_amd.utils.timing import NullTracer
+    ns, name, _ = _agent_service()
+    port = pod_network
+    srv = _cluster(mock_cluster, ns, name, port)
+    cluster = ClusterConnection(srv.url)
+    fetched = []
+    real = fanout.fetch_all
+
+    async def counting(targets, *a, **kw):
+        fetched.extend(t["name"] for t in targets if not t.get("error"))
+        return await real(targets, *a, **kw)
+    monkeypatch.setattr(fanout, "fetch_all", counting)
+    cache = fanout.ProbeCache(ttl=60.0)
+    opts = CheckOptions(probe_endpoint=f"http://{{pod_ip}}:{port}/probe", health_policy="require",
+                        probe_cache=cache)
+
+    def evaluate():
+        scan = scan_cluster(cluster, opts, NullTracer())
+        return {n["name"]: v.state for n, v in zip(scan.gpu_nodes, apply_health(scan, opts, NullTracer(), [], cluster))}
+    first = evaluate()
+    assert first == {"a": H.HEALTHY, "b": H.UNHEALTHY, "c": H.HEALTHY, "d": H.UNKNOWN}
+    assert sorted(fetched) == ["a", "b", "c"]  # d has no endpoint: nothing to fetch
+    slices = len([e for e in srv.log if "endpointslices" in e["path"]])
+    fetched.clear()
+    assert evaluate() == first
+    assert fetched == [] and cache.reused == 3  # all three from the cache
+    assert len([e for e in srv.log if "endpointslices" in e["path"]]) == slices  # no second EndpointSlice LIST
+    cache.ttl = 0.0  # expired: everything again
+    assert evaluate() == first and sorted(fetched) == ["a", "b", "c"]
+    from k8s_gpu_node_checker_amd import cli
+    assert cli.parse_args(["--probe-cache-ttl", "5"]).probe_cache_ttl == 5.0
