@@ -383,6 +383,13 @@ class ProbeCache:
         if isinstance(report, dict) and not report.get("error"):
             self._reports[(target["name"], target["url"])] = (now, report)
 
+    def prune(self, now: float) -> None:
+        """Forget reports well past the TTL: a rescheduled agent pod has a new address, so its old entry would
+        otherwise stay for the life of the watcher."""
+        old = [k for k, (t, _) in self._reports.items() if now - t >= 4 * self.ttl]
+        for k in old:
+            del self._reports[k]
+
     def fresh_endpoints(self, now: float) -> Optional[Any]:
         e = self.endpoints
         return e[1] if e is not None and now - e[0] < self.ttl and e[1][1] is None else None
@@ -401,6 +408,8 @@ def fetch_probe_reports(scan: Any, template: str, concurrency: int = 64, timeout
     if not targets:
         return []
     now = time.monotonic()
+    if cache is not None:
+        cache.prune(now)
     out: List[Optional[Dict[str, Any]]] = [None] * len(targets)
     todo = []
     for i, t in enumerate(targets):

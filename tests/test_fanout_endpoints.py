@@ -223,3 +223,17 @@ def test_watch_mode_reuses_fetched_reports_and_endpoints_within_the_ttl(pod_netw
     assert evaluate() == first and sorted(fetched) == ["a", "b", "c"]
     from k8s_gpu_node_checker_amd import cli
     assert cli.parse_args(["--probe-cache-ttl", "5"]).probe_cache_ttl == 5.0
+
+
+def test_probe_cache_forgets_entries_well_past_the_ttl():
+    from k8s_gpu_node_checker_amd.parallel.fanout import ProbeCache
+    c = ProbeCache(ttl=10.0)
+    t = {"name": "a", "url": "http://10.0.0.1:9464/probe"}
+    c.put(t, {"node": "a"}, now=0.0)
+    c.put({"name": "b", "url": "u"}, {"error": "x"}, now=0.0)  # a failed fetch is not kept
+    assert c.get(t, now=5.0) == {"node": "a"} and c.get({"name": "b", "url": "u"}, now=5.0) is None
+    assert c.get(t, now=10.0) is None  # expired, still held
+    c.prune(now=39.0)
+    assert len(c._reports) == 1
+    c.prune(now=40.0)
+    assert c._reports == {}
