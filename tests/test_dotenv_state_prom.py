@@ -224,3 +224,16 @@ def test_state_file_with_wrong_types_is_tolerated(tmp_path):
     assert statefile.should_notify(doc, res, only_on_error=True, on_node_change=True) is True
     p.write_text("[" * 100000)
     assert statefile.load(str(p)) is None
+
+
+def test_env_template_copied_as_is_changes_nothing(run_cli, mock_cluster, tmp_path):
+    """The shipped .env-template, copied to .env unedited (the reference's setup step), leaves the webhook
+    unset: the check runs, no Slack line is printed, the output is the plain report."""
+    import shutil
+    from k8s_gpu_node_checker_amd.testing import fixtures
+    from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+    shutil.copy(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), ".env-template"),
+                tmp_path / ".env")
+    kc = write_kubeconfig(str(tmp_path / "kc"), mock_cluster(fixtures.golden("readme")).url)
+    p = run_cli(["--kubeconfig", kc])
+    assert p.returncode == 0 and "슬랙" not in p.stdout + p.stderr, p.stdout + p.stderr
