@@ -429,6 +429,27 @@ def test_agent_with_diagnostics_is_healthy(dev):
     assert v.ok, v.to_dict()
 
 
+def test_agent_self_baseline_forms_on_the_gpu_without_drift(dev, tmp_path):
+    """models/baseline.py on real hardware: back-to-back level-1 cycles form the GPU's baseline from its first
+    clean runs (2 here), persist it, and the next cycles sit within the drift line of it (run-to-run spread of a
+    healthy MI355X: profiles/baseline_soak_l1_mi355x.json)."""
+    from k8s_gpu_node_checker_amd.agent.agent import Agent
+    from k8s_gpu_node_checker_amd.models import baseline as B
+    path = tmp_path / "baseline.json"
+    ag = Agent("gpu-node", source="native", diag_level=1, devices=[0], diag_when="always", diag_interval=0.0,
+               baseline_file=str(path))
+    ag.baselines.runs = 2
+    for _ in range(4):
+        rep = ag.probe_once()
+    g = rep["gpus"][0]
+    rated = {t: r for t, r in g["diag"].items() if isinstance(r, dict) and r.get("rates")}
+    assert rated and all(r.get("baseline") for r in rated.values()), g["diag"]
+    assert not any(r.get("drift") for r in rated.values()), {t: r.get("drift") for t, r in rated.items()}
+    assert min(v for r in rated.values() for v in r["baseline"]["ratio"].values()) > B.DRIFT_RATIO
+    doc = json.loads(path.read_text())
+    assert doc["schema"] == B.SCHEMA and len(doc["gpus"]) == 1
+
+
 def test_smoke(dev):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import __graft_entry__
