@@ -1015,7 +1015,10 @@ def render_text(out: Dict[str, Any]) -> str:
                 lines.append(f"  {test:<10} {'SKIPPED':<9} {r['skipped']}")
                 continue
             state = "FAIL" if not r.get("pass") else ("DEGRADED" if r.get("degraded") else "pass")
-            lines.append(f"  {test:<10} {state:<9} {_summary(test, r)}")
+            peers = r.get("peers") if isinstance(r.get("peers"), dict) else {}
+            ratios = [v for v in (peers.get("ratio") or {}).values() if isinstance(v, (int, float))]
+            vs = f"  (x{min(ratios):.2f} vs the other {peers.get('gpus', 0) - 1} GPUs)" if ratios else ""
+            lines.append(f"  {test:<10} {state:<9} {_summary(test, r)}{vs}")
             if state != "pass" and r.get("detail"):
                 lines.append(f"  {'':<10} {'':<9} {r['detail']}")
     for test, r in (out.get("fabric") or {}).items():

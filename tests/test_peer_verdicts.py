@@ -158,6 +158,7 @@ def test_mi355x_diag_cli_judges_devices_together(node, capsys):
     assert diag.main(["--level", "1", "--format", "text"]) == 1
     text = capsys.readouterr().out
     assert "of the node's other GPUs' median" in text and "result: FAIL" in text
+    assert "(x0.80 vs the other 3 GPUs)" in text and "(x1.00 vs the other 3 GPUs)" in text
 
 
 # --- self-baselines ----------------------------------------------------------------------------------------
