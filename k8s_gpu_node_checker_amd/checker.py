@@ -23,7 +23,7 @@ from . import report
 from .kube.client import KubeClient
 from .kube.config import ClusterConnection
 from .models import health as H
-from .models.node import ScanResult
+from .models.node import ScanResult, withdrawn_count
 from .models.node import HEALTH_ANNOTATION
 from .models.resources import GPU_RESOURCE_KEYS, PRIMARY_GPU_KEY
 from .utils.timing import NullTracer, Tracer
@@ -308,10 +308,14 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
             summary, fleet_views = F.judge_fleet([n["name"] for n in scan.gpu_nodes], current, fracs)
             if summary and fleet_out is not None:
                 fleet_out.update(summary=summary, views=fleet_views)
+        by_alloc = opts.gpu_source != "capacity"
         for i, (node, ex, rep) in enumerate(zip(scan.gpu_nodes, scan.extras, reports)):
             cap, alloc = ex.capacity.get(key), ex.allocatable.get(key)
-            is_amd = alloc is not None or key in node["gpu_breakdown"]
+            is_amd = alloc is not None or cap is not None or key in node["gpu_breakdown"]
             expected = max(cap or 0, alloc or 0)  # models.node.expected_gpu_count
+            # counting allocatable, a node whose device plugin withdrew every GPU is in the set (models.node
+            # classify_node) but has nothing to schedule on: never Ready, whatever its agent says
+            withdrawn = withdrawn_count(ex.capacity, ex.allocatable) if by_alloc else 0
             v: Optional[H.Verdict] = pre[i]
             rep = judged[i]
             if rep is None and fleet_views[i] is not None:
@@ -327,6 +331,19 @@ def apply_health(scan: ScanResult, opts: CheckOptions, tracer: Tracer,
                     unapplied.append(node["name"])
             elif rep is not None or policy == "require":
                 v = H.evaluate_report(rep, expected, exp, now, fleet_views[i])
+            if withdrawn:
+                plugin = (f"device plugin allocates {alloc or 0} of {cap} {key}" if cap
+                          else f"device plugin allocates 0 of {withdrawn} GPUs")
+                if v is None:
+                    v = H.Verdict(H.UNHEALTHY, [plugin])
+                else:
+                    v.reasons.insert(0, plugin)
+                    v.state = H.UNHEALTHY
+                verdicts.append(v)
+                if node["ready"]:  # classify_node already cleared it; kept false against any later gate
+                    node["ready"] = False
+                    changed = True
+                continue
             if v is None:
                 verdicts.append(None)
                 continue

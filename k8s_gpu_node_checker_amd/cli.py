@@ -310,8 +310,7 @@ def _watch_events(args: Any) -> int:
 
         def report(result) -> None:
             emit_report(result, opts)
-            memo["prev"] = {"fingerprint": statefile.fingerprint(result), "exit_code": result.exit_code,
-                            "slack_pending": result.slack_sent is False, "not_ready": statefile.not_ready(result)}
+            memo["prev"] = statefile.outcome(result)
             if args.state_file:
                 statefile.save(args.state_file, result, prev)
             if args.prometheus_textfile:
@@ -322,7 +321,7 @@ def _watch_events(args: Any) -> int:
             if elector is not None:
                 # the last-notified outcome rides on the Lease: a replica taking over starts from it (no repeated
                 # alert, no lost recovery notice across a failover)
-                elector.publish_state(memo["prev"])
+                elector.publish_state(statefile.compact(memo["prev"]))
             last["code"] = result.exit_code
 
         if not args.leader_elect:

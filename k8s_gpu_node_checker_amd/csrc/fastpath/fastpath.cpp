@@ -1174,7 +1174,17 @@ void emit_node(const NodeRec& r, const std::vector<PyObject*>& pykeys, bool use_
   if (!r.is_obj) return;
   long long total = 0;
   Ref bd(breakdown(pykeys, use_alloc ? r.alloc : r.cap, &total, scratch));
-  if (total <= 0) return;  // not a GPU node (reference :222)
+  bool ready = r.ready;
+  if (total <= 0) {
+    // not a GPU node (reference :222) -- unless, counting allocatable, the capacity still registers GPUs:
+    // the device plugin withdrew every one, and the node stays in the set as not Ready
+    // (models/node.py classify_node)
+    if (!use_alloc) return;
+    long long cap_total = 0;
+    Ref capbd(breakdown(pykeys, r.cap, &cap_total, scratch));
+    if (cap_total <= 0) return;
+    ready = false;
+  }
   PyObject* info = PyDict_New();
   if (!info) throw Fallback{"oom"};
   Ref hi(info);
@@ -1183,12 +1193,12 @@ void emit_node(const NodeRec& r, const std::vector<PyObject*>& pykeys, bool use_
   Ref taints(taints_list(r, cache, scratch));
   Ref gpus(PyLong_FromLongLong(total));
   if (!name.o || !gpus.o) throw Fallback{"oom"};
-  if (PyDict_SetItem(info, k_name, name.o) < 0 || PyDict_SetItem(info, k_ready, r.ready ? Py_True : Py_False) < 0 ||
+  if (PyDict_SetItem(info, k_name, name.o) < 0 || PyDict_SetItem(info, k_ready, ready ? Py_True : Py_False) < 0 ||
       PyDict_SetItem(info, k_gpus, gpus.o) < 0 || PyDict_SetItem(info, k_breakdown, bd.o) < 0 ||
       PyDict_SetItem(info, k_labels, labels.o) < 0 || PyDict_SetItem(info, k_taints, taints.o) < 0)
     throw Fallback{"dict"};
   if (PyList_Append(out.gpu_nodes.o, info) < 0) throw Fallback{"list"};
-  if (r.ready && PyList_Append(out.ready_nodes.o, info) < 0) throw Fallback{"list"};
+  if (ready && PyList_Append(out.ready_nodes.o, info) < 0) throw Fallback{"list"};
   if (!want_extras) return;
   Ref capd(breakdown(pykeys, r.cap, nullptr, scratch));
   Ref allocd(breakdown(pykeys, r.alloc, nullptr, scratch));

@@ -229,9 +229,13 @@ class LeaderElector:
         annotations must stay small -- and the previous one is dropped; False then."""
         text = json.dumps(state, sort_keys=True, separators=(",", ":"))
         fits = len(text) <= STATE_MAX_BYTES
+        if not fits:
+            text = "{}"
         with self._state_lock:
-            self._state = text if fits else "{}"
-        self._wake.set()
+            changed = text != self._state
+            self._state = text
+        if changed:  # an unchanged state rides on the periodic renewal: no extra Lease write per evaluation
+            self._wake.set()
         return fits
 
     def stop(self, timeout: float = 5.0) -> None:

@@ -31,7 +31,7 @@ import json
 import time
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
-from ..models.node import NodeExtras, ScanResult, node_extras, project_node
+from ..models.node import NodeExtras, ScanResult, classify_node, node_extras, project_node
 from ..models.resources import GPU_RESOURCE_KEYS
 from ..utils.backoff import Backoff
 from ..utils.http import HTTPError, LineStream
@@ -50,10 +50,10 @@ class NodeView:
         self.all_names: set = set()
 
     def upsert(self, node: Dict[str, Any]) -> None:
-        info = project_node(node, GPU_RESOURCE_KEYS, self.gpu_source)
-        name = info["name"]
+        info = classify_node(node, GPU_RESOURCE_KEYS, self.gpu_source)
+        name = info["name"] if info is not None else project_node(node, GPU_RESOURCE_KEYS, self.gpu_source)["name"]
         self.all_names.add(name)
-        if info["gpus"] > 0:
+        if info is not None:
             self.gpu[name] = (info, node_extras(node, GPU_RESOURCE_KEYS, self.annotation_mode))
         else:
             self.gpu.pop(name, None)

@@ -95,6 +95,37 @@ def project_node(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEY
     }
 
 
+def classify_node(node: Mapping[str, Any], keys: Sequence[str] = GPU_RESOURCE_KEYS,
+                  gpu_source: str = "capacity") -> Optional[Dict[str, Any]]:
+    """The report dict of a GPU node, ``None`` for any other node (reference ``:220-225``).
+
+    Membership is the reference's -- GPU keys summing above 0 in ``capacity`` (``:181-196``) -- or,
+    under ``--gpu-source allocatable``, above 0 in either map: counts come from allocatable, but a
+    node whose device plugin withdrew every GPU (allocatable 0, capacity 8: a crashed or wedged
+    plugin, the commonest GPU-node failure) stays in the set with ``"ready": false`` instead of
+    leaving the report, Slack and metrics.  A fleet entirely in that state exits 3, not 2
+    (``:289-293``).  The native scanner (``csrc/fastpath/fastpath.cpp`` ``emit_node``) applies the
+    same rule.
+    """
+    info = project_node(node, keys, gpu_source)
+    if info["gpus"] > 0:
+        return info
+    if gpu_source != "capacity" and withdrawn_count(gpu_breakdown(_get(_get(node, "status"), "capacity"), keys),
+                                                    info["gpu_breakdown"]):
+        info["ready"] = False
+        return info
+    return None
+
+
+def withdrawn_count(capacity: Mapping[str, int], allocatable: Mapping[str, int]) -> int:
+    """GPUs registered (capacity) on a node whose allocatable GPU keys sum to 0 or less: the device
+    plugin withdrew all of them.  0 for any node with an allocatable GPU or no registered one."""
+    cap = sum(capacity.values()) if capacity else 0
+    if cap <= 0 or (sum(allocatable.values()) if allocatable else 0) > 0:
+        return 0
+    return cap
+
+
 _UNPARSED = object()
 
 
@@ -216,9 +247,10 @@ class ScanResult:
         self.extras: List[NodeExtras] = []
         self.items_seen = 0
 
-    def add(self, info: Dict[str, Any], extras: Optional[NodeExtras] = None) -> None:
+    def add(self, info: Optional[Dict[str, Any]], extras: Optional[NodeExtras] = None) -> None:
+        """One scanned item: ``info`` is :func:`classify_node`'s (``None``: not a GPU node)."""
         self.items_seen += 1
-        if info["gpus"] > 0:
+        if info is not None:
             self.gpu_nodes.append(info)
             if extras is not None:
                 self.extras.append(extras)
@@ -243,8 +275,8 @@ def scan_items(items: Iterable[Mapping[str, Any]], result: Optional[ScanResult] 
     """Pure-Python scan of decoded ``NodeList.items`` (reference ``:217-225``)."""
     res = result if result is not None else ScanResult()
     for n in items or ():
-        info = project_node(n, keys, gpu_source)
-        res.add(info, node_extras(n, keys, annotation_mode) if want_extras else None)
+        info = classify_node(n, keys, gpu_source)
+        res.add(info, node_extras(n, keys, annotation_mode) if want_extras and info is not None else None)
     return res
 
 

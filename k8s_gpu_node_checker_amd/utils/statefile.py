@@ -10,7 +10,8 @@ checker remembers the previous outcome and only notifies when it changes:
 * with ``--slack-only-on-error --slack-on-node-change``: also send when the set of
   not-Ready GPU nodes changes while the exit code stays 0 (1 of 8 MI355X nodes turning
   unhealthy, and its recovery) -- the reference's "zero Ready nodes" rule
-  (``check-gpu-node.py:154-155``) alone never reports a single node;
+  (``check-gpu-node.py:154-155``) alone never reports a single node -- and when a node
+  leaves the GPU-node set altogether (:func:`left_gpu_set`);
 * a notification that was due but not delivered (the webhook failed on every
   attempt) stays due: the next run sends it, so an alert is not lost to a
   Slack outage.
@@ -47,12 +48,44 @@ def load(path: str) -> Optional[Dict[str, Any]]:
         return None
     if not isinstance(doc, dict):
         return None
-    if not isinstance(doc.get("not_ready", []), list) or not all(isinstance(n, str) for n in doc.get("not_ready", [])):
-        doc.pop("not_ready", None)
+    for k in ("not_ready", "gpu_nodes"):
+        if not isinstance(doc.get(k, []), list) or not all(isinstance(n, str) for n in doc.get(k, [])):
+            doc.pop(k, None)
     for k in ("exit_code", "runs"):
         if not isinstance(doc.get(k, 0), int) or isinstance(doc.get(k), bool):
             doc.pop(k, None)
     return doc
+
+
+def members(result: Any) -> list:
+    """Names of the GPU-node set, sorted."""
+    return sorted(n["name"] for n in result.gpu_nodes)
+
+
+def members_digest(names: list) -> str:
+    h = hashlib.sha256()
+    for n in names:
+        h.update(n.encode("utf-8", "surrogatepass") + b"\0")
+    return h.hexdigest()[:16]
+
+
+def outcome(result: Any) -> Dict[str, Any]:
+    """What the next evaluation's :func:`should_notify` compares against (state file, watcher memo)."""
+    names = members(result)
+    return {"fingerprint": fingerprint(result), "exit_code": result.exit_code,
+            "slack_pending": result.slack_sent is False, "not_ready": not_ready(result),
+            "gpu_nodes": names, "gpu_count": len(names), "members": members_digest(names)}
+
+
+#: a published outcome (the watcher's Lease) keeps the member names only up to this many; beyond, the digest and
+#: count stand in for them (:func:`left_gpu_set` then decides from those)
+COMPACT_MEMBERS = 1000
+
+
+def compact(state: Dict[str, Any]) -> Dict[str, Any]:
+    if len(state.get("gpu_nodes") or ()) <= COMPACT_MEMBERS:
+        return state
+    return {k: v for k, v in state.items() if k != "gpu_nodes"}
 
 
 def save(path: str, result: Any, prev: Optional[Dict[str, Any]] = None) -> None:
@@ -69,6 +102,7 @@ def save(path: str, result: Any, prev: Optional[Dict[str, Any]] = None) -> None:
         "slack_pending": result.slack_sent is False,
         "runs": (prev or {}).get("runs", 0) + 1,
     }
+    doc.update({k: v for k, v in outcome(result).items() if k in ("gpu_nodes", "gpu_count", "members")})
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
     fd, tmp = tempfile.mkstemp(prefix=".state-", dir=d)
@@ -96,7 +130,28 @@ def should_notify(prev: Optional[Dict[str, Any]], result: Any, only_on_error: bo
         return True  # recovery
     if on_node_change:
         before = sorted(prev.get("not_ready") or []) if prev is not None else []
-        return not_ready(result) != before  # a node went down (or came back) while others stay Ready
+        if not_ready(result) != before:
+            return True  # a node went down (or came back) while others stay Ready
+        return left_gpu_set(prev, result)
+    return False
+
+
+def left_gpu_set(prev: Optional[Dict[str, Any]], result: Any) -> bool:
+    """A node of the previous GPU-node set is gone from this one (deleted, relabelled, or -- counting
+    capacity -- its device plugin deregistered the GPUs): nothing of it is Not Ready any more, it is
+    simply absent, and only this comparison notices.  A state from before the member list was kept
+    (no ``gpu_nodes``/``members``) says nothing."""
+    if prev is None:
+        return False
+    names = prev.get("gpu_nodes")
+    if isinstance(names, list):
+        now = {n["name"] for n in result.gpu_nodes}
+        return any(n not in now for n in names)
+    digest, count = prev.get("members"), prev.get("gpu_count")
+    if isinstance(digest, str) and isinstance(count, int) and not isinstance(count, bool):
+        # names not kept (a large fleet's compacted Lease state): a different set that did not grow lost a node
+        cur = members(result)
+        return members_digest(cur) != digest and len(cur) <= count
     return False
 
 

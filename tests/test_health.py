@@ -133,10 +133,14 @@ def test_cli_require_policy_and_mi355x_preset(run_cli, mock_cluster, tmp_path):
     p = run_cli(["--kubeconfig", kc, "--json", "--health-policy", "require"])
     doc = json.loads(p.stdout)
     assert [n["ready"] for n in doc["nodes"]] == [True, False, True]
-    p = run_cli(["--kubeconfig", kc, "--json", "--mi355x"])  # allocatable-based + require
+    p = run_cli(["--kubeconfig", kc, "--json-extended", "--mi355x"])  # allocatable-based + require
     doc = json.loads(p.stdout)
-    assert [n["name"] for n in doc["nodes"]] == ["a", "b"]  # c has 0 allocatable GPUs
-    assert [n["ready"] for n in doc["nodes"]] == [True, False]
+    # c's device plugin withdrew all 8 GPUs (allocatable 0): it stays a GPU node, Not Ready, with the reason
+    assert [n["name"] for n in doc["nodes"]] == ["a", "b", "c"]
+    assert [n["ready"] for n in doc["nodes"]] == [True, False, False]
+    assert doc["nodes"][2]["gpus"] == 0 and doc["nodes"][2]["gpu_breakdown"] == {"amd.com/gpu": 0}
+    h = doc["mi355x"]["nodes"][2]["health"]
+    assert h["state"] == "unhealthy" and h["reasons"][0] == "device plugin allocates 0 of 8 amd.com/gpu"
 
 
 def test_cli_health_in_slack_and_extended_json(run_cli, mock_cluster, sink, tmp_path):

@@ -249,3 +249,18 @@ def test_an_oversized_leader_state_is_not_kept_on_the_lease(mock_cluster):
                      [L.STATE_ANNOTATION] == "{}")
     finally:
         a.stop()
+
+
+def test_publish_state_wakes_the_renewal_only_on_a_change():
+    """the watcher publishes after every evaluation; an unchanged state must not add a Lease write per
+    event batch (it rides on the periodic renewal)."""
+    e = LeaderElector(lambda: None, "ns", "n", "id", lease_duration=15.0, renew_deadline=10.0, retry_period=2.0)
+    assert e.publish_state({"exit_code": 0}) is True and e._wake.is_set()
+    e._wake.clear()
+    assert e.publish_state({"exit_code": 0}) is True and not e._wake.is_set()
+    assert e.publish_state({"exit_code": 3}) is True and e._wake.is_set()
+    e._wake.clear()
+    big = {"not_ready": ["x" * 100] * 1000}
+    assert e.publish_state(big) is False and e._wake.is_set()  # the old state is dropped: a change
+    e._wake.clear()
+    assert e.publish_state(big) is False and not e._wake.is_set()
