@@ -36,7 +36,7 @@ if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a
     from typing import Any, Callable, Optional, TextIO
 
 from ..utils.backoff import Backoff
-from ..utils.http import HTTPError, env_proxy, request
+from ..utils.http import HTTPError
 
 ICON = ":robot_face:"
 DEFAULT_USERNAME = "k8s-gpu-checker"
@@ -60,18 +60,6 @@ def slack_payload(message: str, username: str) -> bytes:
     return json.dumps({"text": message, "username": username, "icon_emoji": ICON}).encode("ascii")
 
 
-def _env_ssl_context():
-    """``REQUESTS_CA_BUNDLE`` / ``CURL_CA_BUNDLE`` (a file or an OpenSSL hashed directory), as requests
-    verifies with; None keeps the default trust store."""
-    bundle = os.environ.get("REQUESTS_CA_BUNDLE") or os.environ.get("CURL_CA_BUNDLE")
-    if not bundle:
-        return None
-    import ssl
-    if os.path.isdir(bundle):
-        return ssl.create_default_context(capath=bundle)
-    return ssl.create_default_context(cafile=bundle)
-
-
 def send_slack_message(webhook_url: Optional[str], message: str, username: str = DEFAULT_USERNAME,
                        max_retries: int = 3, retry_delay: float = 30, *, policy: str = "backoff",
                        timeout: float = 10.0, err: Optional[TextIO] = None,
@@ -82,20 +70,19 @@ def send_slack_message(webhook_url: Optional[str], message: str, username: str =
         return False
     err = err if err is not None else sys.stderr
     body = slack_payload(message, username)
-    headers = {"Content-Type": "application/json", "Accept": "*/*",
-               "User-Agent": "k8s-gpu-node-checker-amd/0.1"}
     bo = backoff or Backoff(base=1.0, cap=max(0.0, float(retry_delay)), jitter=0.5)
     attempts = max_retries + 1
-    # what requests.post does by default (trust_env): the environment's proxy and CA bundle
-    proxy = env_proxy(webhook_url)
-    if ssl_context is None and webhook_url.startswith("https"):
-        ssl_context = _env_ssl_context()
+    from . import webhook
     for attempt in range(attempts):
+        # requests.post semantics (notify/webhook.py): URL preparation, .netrc / URL credentials, redirects,
+        # the environment's proxy and CA bundle -- every failure of any of it inside this attempt's try, as
+        # the reference's requests.post call is (check-gpu-node.py:72-109)
         try:
-            resp = request(webhook_url, "POST", headers, body, timeout=timeout, ssl_context=ssl_context,
-                           proxy_url=proxy)
+            resp = webhook.post(webhook_url, body, timeout=timeout, ssl_context=ssl_context)
         except HTTPError as e:
-            if e.retryable_reset:
+            # requests' ConnectionError / Timeout: retried only when the text names a reset or an aborted
+            # connection (the reference's test, :88)
+            if e.kind != "invalid_url" and ("Connection reset by peer" in str(e) or "Connection aborted" in str(e)):
                 if attempt < max_retries:
                     print(f"슬랙 메시지 전송 실패 ({attempt + 1}/{attempts}회 시도): {e}", file=err)
                     print(f"⏳ {retry_delay}초 후 재시도합니다...", file=err)
@@ -112,7 +99,7 @@ def send_slack_message(webhook_url: Optional[str], message: str, username: str =
             if attempt > 0:
                 print(f"✅ 슬랙 메시지를 {attempt + 1}번째 시도에서 성공적으로 전송했습니다.", file=err)
             return True
-        print(f"슬랙 메시지 전송 실패 (HTTP {resp.status}): {resp.text}", file=err)
+        print(f"슬랙 메시지 전송 실패 (HTTP {resp.status}): {webhook.response_text(resp)}", file=err)
         if policy == "backoff" and attempt < max_retries:
             if resp.status in _BACKOFF_STATUS:
                 sleep(bo.delay(attempt, resp.header("Retry-After")))

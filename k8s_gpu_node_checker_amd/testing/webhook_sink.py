@@ -15,6 +15,11 @@ The URL path selects the behaviour, so one sink serves every test:
 ``/close``      close without a response ("Remote end closed connection")
 ``/seq/ID/A,B``  scripted: the n-th POST to this exact path gets step n (the last step repeats); a step is
                  ``200``, ``204``, ``404``, ``429``, ``500``, ``reset`` or ``close``; ``ID`` keeps runs apart
+``/301`` ...    ``301``, ``302``, ``303``, ``307``, ``308`` redirecting (relative ``Location``) to ``/postonly``
+``/postonly``   ``200`` to a POST, ``405 method_not_allowed`` to anything else
+``/loop``       ``302`` to itself, forever
+``/to/H/MODE``  ``307`` to ``http://H:<this port>/MODE`` (another host name for the same sink)
+``/cookie``     ``302`` to ``/200`` setting ``sid=abc`` (path ``/``)
 ==============  =============================================================
 
 Every request is logged (path, headers, body) for assertions.
@@ -84,6 +89,26 @@ class _SinkHandler(socketserver.BaseRequestHandler):
             return
         if path == "/slow":
             time.sleep(srv.slow_s)
+        if path in ("/301", "/302", "/303", "/307", "/308"):
+            self._respond(int(path[1:]), "Redirect", b"", "Location: /postonly\r\n")
+            return
+        if path == "/postonly":
+            if req["method"] == "POST":
+                self._respond(200, "OK", b"ok")
+            else:
+                self._respond(405, "Method Not Allowed", b"method_not_allowed")
+            return
+        if path == "/loop":
+            self._respond(302, "Found", b"", "Location: /loop\r\n")
+            return
+        if path.startswith("/to/"):
+            _, _, host, mode = path.split("/", 3)
+            port = srv.server_address[1]
+            self._respond(307, "Temporary Redirect", b"", f"Location: http://{host}:{port}/{mode}\r\n")
+            return
+        if path == "/cookie":
+            self._respond(302, "Found", b"", "Set-Cookie: sid=abc; Path=/\r\nLocation: /200\r\n")
+            return
         if path.startswith("/flaky"):
             n = int(path[6:] or 2)
             if count <= n:

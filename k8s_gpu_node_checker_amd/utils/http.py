@@ -128,8 +128,14 @@ class Connection:
             msg = (f"{pool}: Max retries exceeded with url: {url} (Caused by ConnectTimeoutError("
                    f"'Connection to {self.host} timed out. (connect timeout={self.timeout:g})'))")
         elif kind in ("refused", "dns"):
-            msg = (f"{pool}: Max retries exceeded with url: {url} (Caused by NewConnectionError("
-                   f"'Failed to establish a new connection: {e}'))")
+            # urllib3 2.6's text (the reference's requests stack as installed): the connection renders as
+            # HTTP[S]Connection(host=..., port=...); a failed lookup is a NameResolutionError
+            conn = f"{'HTTPSConnection' if self.scheme == 'https' else 'HTTPConnection'}(host={self.host!r}, port={self.port!r})"
+            if kind == "dns":
+                inner = f"NameResolutionError({conn + ': ' + f'Failed to resolve {self.host!r} ({e})'!r})"
+            else:
+                inner = f"NewConnectionError({conn + ': Failed to establish a new connection: ' + str(e)!r})"
+            msg = f"{pool}: Max retries exceeded with url: {url} (Caused by {inner})"
         elif kind == "tls":
             msg = f"{pool}: Max retries exceeded with url: {url} (Caused by SSLError({e!r}))"
         else:
@@ -249,9 +255,11 @@ class Connection:
         lines = [f"{method} {req_target} HTTP/1.1", f"Host: {self.host_header}"]
         if self.proxy and self.scheme == "http" and self.proxy.username is not None:
             lines.append(self._proxy_auth().rstrip("\r\n"))
+        given_length = False
         for k, v in (headers or {}).items():
             lines.append(f"{k}: {v}")
-        if body is not None:
+            given_length = given_length or k.lower() == "content-length"
+        if body is not None and not given_length:
             lines.append(f"Content-Length: {len(body)}")
         raw = ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
         return raw + body if body else raw
@@ -414,9 +422,9 @@ class Connection:
                 chunks.append(c)
             body = b"".join(chunks)
             self.close()
-        if hmap.get("content-encoding", "").lower() == "gzip" and body:
-            import zlib
-            body = zlib.decompress(body, 16 + zlib.MAX_WBITS)
+        coding = hmap.get("content-encoding", "").lower()
+        if coding and body:
+            body = _decode_content(body, coding)
         if hmap.get("connection", "").lower() == "close":
             self.close()
         return Response(status, reason, headers, body)
@@ -447,6 +455,21 @@ class Connection:
                 if prefix:
                     peek(prefix)
                 peek = None
+
+
+def _decode_content(body: bytes, coding: str) -> bytes:
+    """Undo ``Content-Encoding`` as urllib3 does: ``gzip`` (and ``x-gzip``), ``deflate`` (zlib-wrapped, or raw
+    as some servers send it), several codings applied in order listed; an unknown coding is left alone."""
+    import zlib
+    for c in reversed([c.strip() for c in coding.split(",") if c.strip()]):
+        if c in ("gzip", "x-gzip"):
+            body = zlib.decompress(body, 16 + zlib.MAX_WBITS)
+        elif c == "deflate":
+            try:
+                body = zlib.decompress(body)
+            except zlib.error:
+                body = zlib.decompress(body, -zlib.MAX_WBITS)
+    return body
 
 
 class LineStream:

@@ -361,7 +361,8 @@ def test_agent_metrics_carry_the_verdict_state():
 def test_image_carries_every_third_party_runtime_import():
     """Every non-stdlib module the package imports is either installed in the image's runtime stage or is
     optional by design (torch: bench / torchrun collectives; amdsmi: the Python probe fallback, shipped by
-    ROCm itself; prometheus_client / requests: tests and tools only)."""
+    ROCm itself; charset_normalizer: the guess of an undeclared webhook-error encoding, as requests makes it,
+    with a UTF-8/latin-1 fallback; prometheus_client / requests: tests and tools only)."""
     import ast
     import sys
     pkg = os.path.join(REPO, "k8s_gpu_node_checker_amd")
@@ -383,7 +384,7 @@ def test_image_carries_every_third_party_runtime_import():
     pip = " ".join(ln for ln in lines if "/opt/venv/bin/pip install" in ln)
     assert "COPY --from=build /opt/venv /opt/venv" in lines
     installed = {"yaml": "PyYAML" in pip, "grpc": "grpcio" in pip}
-    optional = {"torch", "amdsmi"}
+    optional = {"torch", "amdsmi", "charset_normalizer"}
     assert third <= set(installed) | optional, third - set(installed) - optional
     assert all(installed[m] for m in third & set(installed)), installed
 

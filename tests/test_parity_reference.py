@@ -249,3 +249,61 @@ def test_random_webhook_behaviour_same_retry_state_machine(tmp_path_factory, sin
             assert x.split(":")[0] == y.split(":")[0], (x, y)
         else:
             assert x == y, (steps, retries, x, y)
+
+
+# --- the Slack transport: what requests.post does beyond a plain POST -------------------------
+
+def _seq(reqs):
+    return [(r["method"], r["path"], [(k, v) for k, v in r["headers"].items() if k not in ("User-Agent", "Host")],
+             r["body"]) for r in reqs]
+
+
+def _transport_case(cluster, sink, url, env=None, flags=()):
+    kc = cluster(fixtures.golden("readme"))
+    args = ["--kubeconfig", kc, "--slack-webhook", url, "--slack-retry-delay", "0"] + list(flags)
+    e = {"HOME": "/nonexistent-home"}
+    e.update(env or {})
+    n0 = len(sink.requests)
+    a = run_ref(args, env=e)
+    n1 = len(sink.requests)
+    b = run_new(args + ["--slack-retry-policy", "reference"], env=e)
+    n2 = len(sink.requests)
+    return a, b, _seq(sink.requests[n0:n1]), _seq(sink.requests[n1:n2])
+
+
+@pytest.mark.parametrize("mode", ["301", "302", "303", "307", "308", "loop", "cookie", "to/localhost/200"])
+@pytest.mark.parametrize("flags", [[], ["--json"]])
+def test_slack_redirects_identical(cluster, sink, mode, flags):
+    a, b, ra, rb = _transport_case(cluster, sink, sink.url(mode), flags=flags)
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert ra == rb and ra
+    if mode in ("307", "308"):
+        assert "✅ 슬랙 메시지를 성공적으로 전송했습니다." in a.stdout or flags
+
+
+def test_slack_url_credentials_identical(cluster, sink, tmp_path):
+    host, port = sink.server_address[:2]
+    for url in (f"http://user:pass@{host}:{port}/200", f"http://us%40er:p%3Ass@{host}:{port}/to/localhost/200"):
+        a, b, ra, rb = _transport_case(cluster, sink, url)
+        assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+        assert ra == rb
+        if "user:pass" in url:
+            assert ("Authorization", "Basic dXNlcjpwYXNz") in rb[0][2]
+        else:  # the cross-host hop drops the credentials
+            assert any(k == "Authorization" for k, _ in rb[0][2]) and all(k != "Authorization" for k, _ in rb[1][2])
+    rc = tmp_path / "netrc"
+    rc.write_text(f"machine {host} login nu password np\n")
+    a, b, ra, rb = _transport_case(cluster, sink, f"http://{host}:{port}/200", env={"NETRC": str(rc)})
+    assert (a.stdout, a.stderr) == (b.stdout, b.stderr) and ra == rb
+    assert ("Authorization", "Basic bnU6bnA=") in rb[0][2]
+
+
+@pytest.mark.parametrize("url,env", [("http://127.0.0.1:99999/x", None), ("http://[::1/x", None),
+                                     ("https://127.0.0.1:1/x", {"REQUESTS_CA_BUNDLE": "/missing"}),
+                                     ("http://127.0.0.1:1/x", None), ("ftp://x/y", None)])
+@pytest.mark.parametrize("flags", [[], ["--json"]])
+def test_slack_transport_errors_identical(cluster, sink, url, env, flags):
+    """A malformed URL, a refused connection or a bad CA bundle: one failure line, never a thread traceback."""
+    a, b, ra, rb = _transport_case(cluster, sink, url, env=env, flags=flags)
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert "Traceback" not in b.stderr and b.stderr.startswith("슬랙 메시지 전송 실패: ")
