@@ -106,3 +106,32 @@ def test_deflate_and_gzip_responses_decoded():
     assert _decode_content(c.compress(raw) + c.flush(), "deflate") == raw
     g = zlib.compressobj(wbits=16 + zlib.MAX_WBITS)
     assert _decode_content(g.compress(raw) + g.flush(), "gzip") == raw
+
+
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+_URL_PART = st.lists(st.sampled_from(list("aZ09-._~!$&'()*+,;=:/?@%# é[]") + ["..", "./", "%41", "%zz", "%7e"]),
+                     max_size=10).map("".join)
+
+
+@settings(max_examples=400, deadline=None)
+@given(scheme=st.sampled_from(["http://", "https://", "HTTP://", "ftp://", ""]),
+       host=st.sampled_from(["127.0.0.1", "Hooks.Slack.com", "localhost", ".x", "[::1]", "a_b", "", "h"]),
+       port=st.sampled_from(["", ":80", ":080", ":0", ":65535", ":65536", ":x"]), rest=_URL_PART)
+def test_prepare_url_matches_requests(scheme, host, port, rest):
+    """The no-regex fast path and the full path both equal requests' PreparedRequest.prepare_url."""
+    url = scheme + host + port + ("/" + rest if rest else "")
+    try:
+        p = requests.models.PreparedRequest()
+        p.prepare_url(url, None)
+        want = ("ok", p.url)
+    except Exception as e:
+        want = ("error", str(e))
+    try:
+        got = ("ok", webhook.prepare_url(url))
+    except webhook.RequestError as e:
+        got = ("error", str(e))
+    assert got == want, url
+    fast = webhook._simple(url)
+    if fast is not None:
+        assert ("ok", fast) == want, url
