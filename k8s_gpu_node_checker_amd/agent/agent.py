@@ -48,7 +48,7 @@ from ..models.health import (HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, XGMI_
                               condition_for, condition_reason, driver_release, encode_annotation, evaluate_report,
                               format_k8s_time,
                               throttle_window)
-from ..models.baseline import Baselines, gpu_key
+from ..models.baseline import Baselines, epoch_of, gpu_key
 from ..models.node import HEALTH_ANNOTATION
 from ..models.resources import PRIMARY_GPU_KEY, gpu_breakdown
 from .server import _metrics, serve, tls_context  # noqa: F401  (the agent's HTTP side; re-exported)
@@ -415,6 +415,8 @@ class Agent:
         self._diag_done = threading.Event()  # set by every diagnostic thread as it returns
         self._rechecked: Dict[int, str] = {}  # device -> result_signature of the not-clean result rechecked
         self._hip_count0: Optional[int] = None  # HIP device count the process saw first (runtime_lost)
+        self._hip_ok: set = set()  # devices whose diagnostics ran without a runtime error in this process
+        self._driver_version: Any = None  # amdgpu driver of the latest probe (the baselines' epoch)
         self.diag_timeout = diag_timeout
         self._diag_skipped: Dict[int, str] = {}
         # node-level findings of the last judgement (models/peers.judge_node): every GPU slow alike
@@ -585,18 +587,23 @@ class Agent:
         lost_devs = {d: runtime_lost(res) for d, res in finished.items()}
         lost_devs = {d: why for d, why in lost_devs.items() if why is not None}
         if lost_devs and self.hip_lost is None:
-            # the HIP runtime, not a GPU, is gone only when the device count changed under the process or every
-            # device that ran this cycle (two or more) failed that way together -- GPUs skipped because a pod
-            # holds them, or scheduled at another time by a recheck, did not run and say nothing either way; one
-            # device's "invalid device ordinal" is that GPU's (or its configuration's) failure and stays in its
-            # verdict -- restarting the agent for it would only loop, diagnosing the same broken GPU every start
+            # the HIP runtime, not a GPU, is gone only when
+            # * the device count changed under the process, or
+            # * a device that ran fine earlier in this process now fails that way (a driver reload under a running
+            #   agent: whatever else is busy or rescheduled, a GPU HIP served before is refused now), or
+            # * every device of the node (two or more) failed that way together.
+            # Devices that never ran fine here -- two broken GPUs rechecked on their own (DIAG_RECHECK_S) while the
+            # others passed, or the only idle ones of a busy node -- are those GPUs' failures and stay in their
+            # verdicts: restarting the agent for them would only loop, diagnosing the same GPUs after every start
             now_count = diag.device_count()
-            everyone = len(lost_devs) == len(finished) >= 2
-            if (self._hip_count0 is not None and now_count != self._hip_count0) or everyone:
+            whole_node = len(lost_devs) >= 2 and set(lost_devs) >= set(devices)
+            was_fine = any(d in self._hip_ok for d in lost_devs)
+            if (self._hip_count0 is not None and now_count != self._hip_count0) or whole_node or was_fine:
                 lost = next(iter(lost_devs.values()))
                 print(f"HIP runtime lost its devices ({lost}); diagnostics stop, /healthz fails so the "
                       "agent is restarted", file=sys.stderr, flush=True)
                 self.hip_lost = lost
+        self._hip_ok.update(d for d in finished if d not in lost_devs)
         fresh = []
         for d, res in finished.items():
             if self.hip_lost is not None and d in lost_devs:
@@ -667,7 +674,8 @@ class Agent:
         if self.baselines is not None and fresh:
             for d in fresh:
                 key = baseline_key(entries.get(d) or {}, self._bdf.get(d, ""), d)
-                self.baselines.observe(key, self._diag_cache[d], now)
+                # the software the rates were measured under: a driver or firmware change re-forms the baseline
+                self.baselines.observe(key, self._diag_cache[d], now, epoch_of(entries.get(d), self._driver_version))
             self.diag_findings = peers.judge_node(pool, label)
 
     def _start_diag(self, d: int, memory_partition: Any, power: Optional[float]) -> None:
@@ -768,6 +776,8 @@ class Agent:
                    "error": f"probe: {type(e).__name__}: {e}"[:300]}
         self._throttle_windows(rep)
         self._ce_rates(rep)
+        drv = rep.get("driver")
+        self._driver_version = drv.get("version") if isinstance(drv, dict) else None
         gpus = rep.get("gpus") or []
         diags = self._diagnostics(gpus)
         if diags or self._diag_skipped:
@@ -1010,6 +1020,11 @@ def build_parser() -> argparse.ArgumentParser:
                          "JSON file across restarts (default: in memory only)")
     ap.add_argument("--no-diag-baseline", dest="diag_baseline", action="store_false",
                     help="do not keep per-GPU self-baselines (no drift warnings)")
+    ap.add_argument("--diag-baseline-reset", default=None, metavar="GPUS",
+                    help="at start, forget the self-baselines of these GPUs (comma-separated amd-smi UUIDs or PCI "
+                         "addresses, or 'all'): they re-form from their next clean runs (after a planned change, "
+                         "e.g. a lower power cap; a driver or firmware change re-forms them by itself).  A running "
+                         "agent takes POST /baseline/reset[?gpu=...] from inside its pod (kubectl port-forward)")
     return ap
 
 
@@ -1027,6 +1042,10 @@ def main(argv: Optional[List[str]] = None) -> int:
                   gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)), label_node=args.label_node,
                   annotation_encoding=args.annotation_encoding, diag_parallel=args.diag_parallel,
                   diag_baseline=args.diag_baseline, baseline_file=args.diag_baseline_file)
+    if args.diag_baseline_reset and agent.baselines is not None:
+        spec = args.diag_baseline_reset.strip()
+        gone = agent.baselines.drop(None if spec.lower() == "all" else spec.split(","))
+        print(f"self-baselines reset: {', '.join(gone) if gone else 'none matched'}", file=sys.stderr, flush=True)
     client = None
     srv = None
     try:

@@ -214,6 +214,33 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
             self.end_headers()
             self.wfile.write(body)
 
+        def do_POST(self) -> None:  # noqa: N802
+            """``POST /baseline/reset[?gpu=KEY[,KEY]]``: drop self-baselines (``models/baseline.Baselines.drop``).
+            Only from the pod itself -- a loopback peer, which is what ``kubectl port-forward`` and ``kubectl exec``
+            arrive as -- so nothing on the pod network (the checker's fan-out, Prometheus) can reset a GPU's
+            memory of its own normal."""
+            from urllib.parse import parse_qs, urlsplit
+            parts = urlsplit(self.path)
+            n = int(self.headers.get("Content-Length") or 0)
+            if n:
+                self.rfile.read(min(n, 65536))
+            peer = self.client_address[0] if self.client_address else ""
+            if parts.path != "/baseline/reset":
+                code, doc = 404, {"error": "not found"}
+            elif not (peer.startswith("127.") or peer in ("::1", "::ffff:127.0.0.1")):
+                code, doc = 403, {"error": "baseline reset is only accepted from inside the pod (loopback)"}
+            elif agent.baselines is None:
+                code, doc = 409, {"error": "self-baselines are off (--no-diag-baseline)"}
+            else:
+                want = [g for v in parse_qs(parts.query).get("gpu", []) for g in v.split(",") if g.strip()]
+                code, doc = 200, {"dropped": agent.baselines.drop(want or None)}
+            body = (json.dumps(doc) + "\n").encode()
+            self.send_response(code)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
     class Srv(ThreadingHTTPServer):
         daemon_threads = True
         request_queue_size = 128  # the checker's fan-out connects in bursts

@@ -1,19 +1,31 @@
 """Per-GPU self-baselines for the active diagnostics' rates (the node agent keeps one per GPU).
 
-The first ``runs`` clean results of a GPU (passed, not degraded, on the same test shape) fix its baseline:
-the median of each rate as a fraction of its scaled reference.  From then on a result whose rate falls below
-``drift_ratio`` of that GPU's own baseline carries a ``drift`` note, which the judgements
-(``ops/diag.judge_absolute``, ``models/peers.judge_node``) turn into ``degraded``: the GPU got slower than it
-used to be, even when it is still above the fleet-wide references and in line with its node's other GPUs
-(a node whose GPUs all age alike).  Drift is a warning, never a failure: the absolute and peer floors decide
-failures.
+The first ``runs`` clean results of a GPU (same test shape) fix its baseline: the median of each rate as a
+fraction of its scaled reference.  From then on a result whose rate falls below ``drift_ratio`` of that GPU's
+own baseline carries a ``drift`` note, which the judgements (``ops/diag.judge_absolute``,
+``models/peers.judge_node``) turn into ``degraded``: the GPU got slower than it used to be, even when it is
+still above the fleet-wide references and in line with its node's other GPUs (a node whose GPUs all age
+alike).  Drift is a warning, never a failure: the absolute and peer floors decide failures.
+
+**Clean** is decided from the result's own numbers, not from the peer- or fleet-adjusted ``pass`` /
+``degraded`` flags: no numerics failure, no lagging XCD/CU, and every rate at or above the absolute failure
+line (``FAIL_FRACTION`` of the reference).  So a lone GPU that sits at 0.93 -- absolutely "degraded" --
+still forms a baseline and later sees its own decay as drift, while a GPU whose peers excused a shortfall
+never forms a baseline at a fault level.
+
+**Epochs.**  A baseline belongs to the software it was measured under: the amdgpu driver release, the VBIOS
+and the firmware image set amd-smi reports for that GPU.  When the epoch changes (a ROCm or firmware
+upgrade that moves a rate by more than the drift margin, either way) the GPU's baselines are re-formed from
+the next clean runs, with no drift warning in between; the old epoch is kept as ``previous``.  A file from
+before epochs (schema v1) is read and upgraded: its baselines adopt the first epoch observed.
 
 Keyed by the GPU's amd-smi UUID (its PCI address when there is none) so a replaced board starts a new
 baseline; the test's shape is part of the key (the level-1 4096^3 and level-2 8192^3 GEMMs differ).  With a
 ``path`` the baselines persist as JSON across agent restarts (written atomically; an unreadable file starts
-empty rather than failing the agent).  Reference analogue: none -- the reference re-derives its binary
-verdict from each LIST (``/root/reference/check-gpu-node.py:172-178``); this is the per-GPU memory that
-lets a verdict stay stable across boxes without re-tuning constants.
+empty rather than failing the agent).  :meth:`Baselines.drop` forgets chosen GPUs (agent
+``--diag-baseline-reset``, ``POST /baseline/reset`` from inside the pod).  Reference analogue: none -- the
+reference re-derives its binary verdict from each LIST (``/root/reference/check-gpu-node.py:172-178``); this
+is the per-GPU memory that lets a verdict stay stable across boxes without re-tuning constants.
 """
 
 from __future__ import annotations
@@ -23,11 +35,14 @@ import os
 import statistics
 import threading
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, Iterable, List, Optional
 
-SCHEMA = "mi355x-diag-baseline/v1"
+SCHEMA = "mi355x-diag-baseline/v2"
+SCHEMA_V1 = "mi355x-diag-baseline/v1"
 BASELINE_RUNS = 5
 DRIFT_RATIO = 0.90
+# the absolute failure line of ops/diag (and models/peers): a run under it is never part of a baseline
+FAIL_FRACTION = 0.85
 
 
 def _fractions(res: Dict[str, Any]) -> Dict[str, float]:
@@ -51,6 +66,29 @@ def gpu_key(entry: Dict[str, Any], fallback: str = "") -> str:
     return fallback
 
 
+def epoch_of(entry: Optional[Dict[str, Any]], driver_version: Any = None) -> Optional[str]:
+    """The software a GPU's rates are measured under, as one string: ``driver <release>; vbios <version>;
+    fw <image>=<version>,...`` (amd-smi's firmware list, sorted).  None when nothing is known."""
+    from .health import driver_release, fw_version_str
+    parts = []
+    if driver_version:
+        parts.append(f"driver {driver_release(driver_version)}")
+    e = entry if isinstance(entry, dict) else {}
+    vb = e.get("vbios_version")
+    if isinstance(vb, str) and vb.strip():
+        parts.append(f"vbios {vb.strip()}")
+    fw = e.get("fw")
+    if isinstance(fw, dict) and fw:
+        parts.append("fw " + ",".join(f"{k}={fw_version_str(k, fw[k])}" for k in sorted(fw, key=str)))
+    return "; ".join(parts) or None
+
+
+def clean_run(res: Dict[str, Any], fractions: Optional[Dict[str, float]] = None) -> bool:
+    """A result that may enter its GPU's baseline (module docstring): judged on its own numbers."""
+    fr = _fractions(res) if fractions is None else fractions
+    return bool(fr) and not res.get("numerics") and not res.get("lag") and min(fr.values()) >= FAIL_FRACTION
+
+
 class Baselines:
     def __init__(self, path: Optional[str] = None, runs: int = BASELINE_RUNS, drift_ratio: float = DRIFT_RATIO):
         if runs < 1:
@@ -59,6 +97,7 @@ class Baselines:
         self.runs = runs
         self.drift_ratio = drift_ratio
         self.lock = threading.Lock()
+        #: gpu key -> {"epoch": str | None, "tests": {shape key: entry}, ["previous": {...}]}
         self.data: Dict[str, Dict[str, Any]] = {}
         if path:
             self._load()
@@ -67,10 +106,19 @@ class Baselines:
         try:
             with open(self.path, encoding="utf-8") as f:  # type: ignore[arg-type]
                 doc = json.load(f)
-        except (OSError, ValueError):
+        except (OSError, ValueError, RecursionError):
             return
-        if isinstance(doc, dict) and doc.get("schema") == SCHEMA and isinstance(doc.get("gpus"), dict):
-            self.data = {k: v for k, v in doc["gpus"].items() if isinstance(v, dict)}
+        if not isinstance(doc, dict) or not isinstance(doc.get("gpus"), dict):
+            return
+        if doc.get("schema") == SCHEMA:
+            for k, v in doc["gpus"].items():
+                if isinstance(v, dict) and isinstance(v.get("tests"), dict):
+                    ep = v.get("epoch")
+                    self.data[k] = dict(v, epoch=ep if isinstance(ep, str) else None)
+        elif doc.get("schema") == SCHEMA_V1:
+            # before epochs: per GPU, the shape-keyed entries themselves; they adopt the first epoch observed
+            self.data = {k: {"epoch": None, "tests": {t: e for t, e in v.items() if isinstance(e, dict)}}
+                         for k, v in doc["gpus"].items() if isinstance(v, dict)}
 
     def _save(self) -> None:
         if not self.path:
@@ -86,20 +134,60 @@ class Baselines:
             except OSError:
                 pass
 
+    def _tests(self, gpu: str) -> Dict[str, Any]:
+        per = self.data.get(gpu)
+        return per["tests"] if isinstance(per, dict) and isinstance(per.get("tests"), dict) else {}
+
     def baseline(self, gpu: str, test: str, res: Dict[str, Any]) -> Optional[Dict[str, float]]:
-        entry = self.data.get(gpu, {}).get(_shape(test, res))
+        entry = self._tests(gpu).get(_shape(test, res))
         return dict(entry["baseline"]) if isinstance(entry, dict) and isinstance(entry.get("baseline"), dict) else None
 
-    def observe(self, gpu: str, results: Dict[str, Dict[str, Any]], now: Optional[float] = None) -> List[str]:
-        """Fold one fresh diagnostic result of GPU ``gpu`` (test -> result) in: set ``drift`` on each rate test
-        below ``drift_ratio`` of its baseline (``baseline`` records the ratios), or add the clean ones to the
-        baseline still forming.  Returns the drift notes.  Call once per fresh result: the judgement is
-        re-applied from the recorded fields, so cached results keep their notes without being observed again."""
+    def epoch(self, gpu: str) -> Optional[str]:
+        per = self.data.get(gpu)
+        return per.get("epoch") if isinstance(per, dict) else None
+
+    def drop(self, gpus: Optional[Iterable[str]] = None) -> List[str]:
+        """Forget the baselines of ``gpus`` (keys, or a GPU's UUID / PCI address / ``hip:N`` spelled without its
+        ``uuid:`` / ``bdf:`` prefix), or of every GPU when None.  Returns the keys dropped; each re-forms from its
+        next clean runs."""
+        with self.lock:
+            if gpus is None:
+                gone = sorted(self.data)
+            else:
+                want = {str(g).strip().lower() for g in gpus if str(g).strip()}
+                gone = sorted(k for k in self.data if k.lower() in want or k.split(":", 1)[-1].lower() in want)
+            for k in gone:
+                del self.data[k]
+            if gone:
+                self._save()
+        return gone
+
+    def observe(self, gpu: str, results: Dict[str, Dict[str, Any]], now: Optional[float] = None,
+                epoch: Optional[str] = None) -> List[str]:
+        """Fold one fresh diagnostic result of GPU ``gpu`` (test -> result), measured under ``epoch``, in: set
+        ``drift`` on each rate test below ``drift_ratio`` of its baseline (``baseline`` records the ratios), or
+        add the clean ones to the baseline still forming.  A new epoch first re-forms the GPU's baselines.
+        Returns the drift notes.  Call once per fresh result: the judgement is re-applied from the recorded
+        fields, so cached results keep their notes without being observed again."""
         notes: List[str] = []
         now = time.time() if now is None else now
         changed = False
         with self.lock:
-            per = self.data.setdefault(gpu, {})
+            per = self.data.get(gpu)
+            if not isinstance(per, dict) or not isinstance(per.get("tests"), dict):
+                per = self.data[gpu] = {"epoch": epoch, "tests": {}}
+                changed = True
+            elif epoch is not None and per.get("epoch") is None:
+                per["epoch"] = epoch  # an upgraded v1 file: its baselines were formed under this software
+                changed = True
+            elif epoch is not None and per.get("epoch") != epoch:
+                formed = {t: e["baseline"] for t, e in per["tests"].items()
+                          if isinstance(e, dict) and isinstance(e.get("baseline"), dict)}
+                per = self.data[gpu] = {"epoch": epoch, "tests": {},
+                                        "previous": {"epoch": per.get("epoch"), "until": round(now, 1),
+                                                     "baselines": formed}}
+                changed = True
+            tests = per["tests"]
             for test, res in results.items():
                 if not isinstance(res, dict):
                     continue
@@ -107,9 +195,9 @@ class Baselines:
                 if not fr:
                     continue
                 key = _shape(test, res)
-                entry = per.get(key)
+                entry = tests.get(key)
                 if not isinstance(entry, dict):
-                    entry = per[key] = {"samples": []}
+                    entry = tests[key] = {"samples": []}
                 base = entry.get("baseline")
                 if isinstance(base, dict):
                     ratios = {m: round(v / base[m], 3) for m, v in fr.items()
@@ -123,8 +211,8 @@ class Baselines:
                     else:
                         res.pop("drift", None)
                     continue
-                clean = res.get("pass") is True and not res.get("degraded") and not res.get("numerics")
-                if clean:
+                res.pop("drift", None)
+                if clean_run(res, fr):
                     samples = entry.get("samples")  # a hand-edited or truncated file: keep what is well-formed
                     entry["samples"] = [s for s in samples if isinstance(s, dict)] if isinstance(samples, list) else []
                     entry["samples"].append({m: round(v, 4) for m, v in fr.items()})

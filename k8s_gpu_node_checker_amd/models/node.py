@@ -159,7 +159,7 @@ class NodeExtras:
             r = _UNPARSED
         if r is _UNPARSED:
             from .health import parse_annotation
-            r = self._report = _slim(parse_annotation(self.health_annotation))
+            r = self._report = slim_report(parse_annotation(self.health_annotation))
         return r
 
     def fleet_fractions(self) -> Dict[Any, float]:
@@ -191,7 +191,8 @@ class NodeExtras:
 DIAG_AGENT_ONLY = ("map", "kinds", "wall_s")
 
 
-def _slim(report: Any) -> Any:
+def slim_report(report: Any) -> Any:
+    """``report`` without the agent-only fields of its diagnostic results (:data:`DIAG_AGENT_ONLY`), in place."""
     gpus = report.get("gpus") if isinstance(report, dict) else None
     for g in gpus if isinstance(gpus, list) else ():
         diag = g.get("diag") if isinstance(g, dict) else None

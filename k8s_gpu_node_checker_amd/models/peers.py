@@ -11,8 +11,10 @@ GPU is judged against the other GPUs of the same node, which share every one of 
 * **outlier** -- a GPU below ``PEER_FAIL_RATIO`` of the median of the *other* GPUs (leave-one-out, so with two
   GPUs the slower is judged against the faster) fails, and the failure names it;
 * **node-wide shortfall** -- when the remaining GPUs agree within ``NODE_UNIFORM_SPREAD`` and their median is
-  below the degraded line, the node gets one node-level ``degraded`` finding (never ``unhealthy``): every GPU
-  is slow alike, which is the node's condition, not a GPU's;
+  below the degraded line, the node gets one node-level ``degraded`` finding: every GPU is slow alike, which
+  is the node's condition, not a GPU's.  Only down to the absolute failure line: when the shared median is
+  under ``FAIL_FRACTION`` the finding is still recorded (``below_floor``) but each GPU is also judged against
+  the references, so a node whose GPUs all run at 30 % fails;
 * otherwise (the GPUs disagree without a clear outlier, e.g. half of them slow) each GPU falls back to the
   absolute references, as does a lone GPU (fewer than ``MIN_PEERS`` measured).
 
@@ -103,8 +105,12 @@ def judge_node(results: Dict[Hashable, Dict[str, Any]], label: Optional[Dict[Has
                     findings.append({"test": test, "metric": m, "median_fraction": round(med, 3),
                                      "min_fraction": round(min(span), 3), "max_fraction": round(max(span), 3),
                                      "gpus": len(alike), "below_floor": med < FAIL_FRACTION})
-                continue
-            for d in alike:  # GPUs that disagree without a clear outlier: each against the references
+                if med >= FAIL_FRACTION:
+                    continue
+                # alike but under the absolute failure floor: peers excuse a shortfall between the degraded and
+                # the failure lines only -- eight GPUs at 30 % of the reference are eight failed GPUs, not a
+                # node-level note (the floor stays, models/fleet.py)
+            for d in alike:  # GPUs that disagree without a clear outlier, or alike under the floor: the references
                 res = members[d]
                 v, e = res["rates"][m], res["expect"][m]
                 txt = f"{m} {v:.3g} {res.get('unit', '')} = {vals[d]:.0%} of {e:.3g}"

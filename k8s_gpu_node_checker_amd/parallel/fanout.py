@@ -222,7 +222,10 @@ async def _http_get_json(url: str, timeout: float, ca_file: Optional[str] = None
             proto.transport.close()
     if proto.status != 200:
         raise RuntimeError(f"HTTP {proto.status}")
-    return json.loads(body)
+    # the agent-only per-test fields (per-XCD/CU maps, burn-in rows, wall time) go before the report is judged or
+    # cached: a --watch-events checker keeps every node's report (ProbeCache), as it keeps parsed annotations
+    from ..models.node import slim_report
+    return slim_report(json.loads(body))
 
 
 async def fetch_all(targets: Sequence[Dict[str, str]], concurrency: int = 64, timeout: float = 2.0,

@@ -596,20 +596,49 @@ def test_single_gpu_failing_with_runtime_strings_is_not_a_restart_loop(monkeypat
     assert ag.hip_lost == "HIP device count changed from 1 to 0"
 
 
-def test_runtime_loss_is_judged_on_the_devices_that_ran(monkeypatch):
-    """after a driver reload on a busy node the idle GPUs fail with 'invalid device ordinal' while the
-    GPU a pod holds is skipped.  Every device that *ran* failed that way (two or more): the runtime is lost, so
+def test_runtime_loss_is_judged_on_devices_that_ran_fine_before(monkeypatch):
+    """after a driver reload under a running agent the idle GPUs fail with 'invalid device ordinal'
+    while the GPU a pod holds is skipped.  Those GPUs ran fine earlier in this process: the runtime is lost, so
     /healthz restarts the agent -- the idle GPUs are not published as broken hardware for ever."""
     w = World(monkeypatch, n=4)
     lost = "mi355x diag failed (-1): hipSetDevice(device): invalid device ordinal"
+    ag = A.Agent("n", source="fake", diag_level=1, diag_interval=0.0)
+    assert ag.probe_once()["state"] == "healthy" and ag.hip_lost is None
     monkeypatch.setattr(diag, "run", lambda level, d, memory_partition=None, **kw: (
         w.runs.append(d), {"gemm": {"pass": False, "detail": lost}})[1])
     w.gpus[2] = gpu(2, procs=[{"pid": 7, "vram_mb": 200000}])  # a training job holds gpu2
-    ag = A.Agent("n", source="fake", diag_level=1)
+    w.runs.clear()
     rep = ag.probe_once()
     assert sorted(w.runs) == [0, 1, 3]
     assert ag.hip_lost == lost
     assert all(g["diag_skipped"].startswith("HIP runtime lost its devices") for g in rep["gpus"])
+
+
+def test_broken_gpus_rechecked_alone_are_not_a_lost_runtime(monkeypatch):
+    """two genuinely broken GPUs of eight fail with 'invalid device ordinal'; the recheck runs
+    just those two, both fail again -- still their failure, not a lost runtime (no /healthz restart loop)."""
+    w = World(monkeypatch, n=8)
+    lost = "mi355x diag failed (-1): hipSetDevice(device): invalid device ordinal"
+
+    def run(level, d, memory_partition=None, **kw):
+        w.runs.append(d)
+        return {"gemm": {"pass": False, "detail": lost}} if d in (3, 6) else {"gemm": {"pass": True}}
+    monkeypatch.setattr(diag, "run", run)
+    ag = A.Agent("n", source="fake", diag_level=1)
+    rep = ag.probe_once()
+    assert ag.hip_lost is None and rep["state"] == "unhealthy"
+    w.runs.clear()
+    w.clock += A.DIAG_RECHECK_S
+    rep = ag.probe_once()
+    assert sorted(w.runs) == [3, 6]  # the recheck: only the two not-clean GPUs
+    assert ag.hip_lost is None and ag.hung_diagnostic() is None and rep["state"] == "unhealthy"
+    # the same two as the only idle GPUs of a busy node, on a fresh agent: also their own failure
+    for d in range(8):
+        if d not in (3, 6):
+            w.gpus[d] = gpu(d, procs=[{"pid": 7, "vram_mb": 200000}])
+    ag2 = A.Agent("n", source="fake", diag_level=1)
+    ag2.probe_once()
+    assert ag2.hip_lost is None
 
 
 def test_one_busy_one_failing_gpu_is_not_a_lost_runtime(monkeypatch):

@@ -237,3 +237,40 @@ def test_probe_cache_forgets_entries_well_past_the_ttl():
     assert len(c._reports) == 1
     c.prune(now=40.0)
     assert c._reports == {}
+
+
+def test_fetched_reports_are_slimmed_before_they_are_cached():
+    """a --watch-events checker keeps every agent's /probe report in its ProbeCache; the
+    agent-only per-test fields (per-XCD/CU maps, burn-in rows, wall time) are dropped as for annotations."""
+    import http.server
+    import threading
+    from k8s_gpu_node_checker_amd.models.node import DIAG_AGENT_ONLY
+    from k8s_gpu_node_checker_amd.parallel import fanout
+    rep = fixtures.mi355x_probe_report("a", gpus=2)
+    for g in rep["gpus"]:
+        g["diag"] = {"mfma": {"pass": True, "map": {"cus": 256}, "kinds": {"bf16": {}}, "wall_s": 1.0, "rates": {}}}
+    body = json.dumps(rep).encode()
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        target = {"name": "a", "url": f"http://127.0.0.1:{srv.server_address[1]}/probe"}
+        out = fanout.run_coroutine(fanout.fetch_all([target], 4, 5.0))
+    finally:
+        srv.shutdown()
+        srv.server_close()
+    got = out[0]
+    assert got["node"] == "a" and all(g["diag"]["mfma"]["pass"] for g in got["gpus"])
+    assert not any(k in g["diag"]["mfma"] for g in got["gpus"] for k in DIAG_AGENT_ONLY)
+    cache = fanout.ProbeCache(ttl=10.0)
+    cache.put(target, got, now=0.0)
+    assert "map" not in cache.get(target, now=1.0)["gpus"][0]["diag"]["mfma"]

@@ -57,13 +57,24 @@ def test_a_fleet_slow_alike_is_the_platforms_normal(reports):
 
 
 def test_one_node_behind_the_fleet_is_degraded_by_name(reports):
-    reps = reports({"n0": 1.0, "n1": 1.0, "n2": 1.0, "slow": 0.80})
+    """A fast fleet (1.10 of the references) and one node whose GPUs all run at 0.88: above the absolute floor,
+    so its own agent calls it at most degraded; 80 % of the other nodes' median names it."""
+    reps = reports({"n0": 1.10, "n1": 1.10, "n2": 1.10, "slow": 0.88})
     summary, verdicts = _judge(reps)
     assert all(verdicts[n].state == H.HEALTHY for n in ("n0", "n1", "n2"))
     v = verdicts["slow"]
-    assert v.state == H.DEGRADED and not v.reasons  # all of its GPUs alike: the node's condition, never unhealthy
+    assert v.state == H.DEGRADED and not v.reasons  # all of its GPUs alike, above the floor: the node's condition
     fleet_w = [w for w in v.warnings if w.startswith("fleet: ")]
-    assert any(w.startswith("fleet: diag gemm tflops at 80% of the other 3 nodes' median (80% vs 100%") for w in fleet_w)
+    assert any(w.startswith("fleet: diag gemm tflops at 80% of the other 3 nodes' median (88% vs 110%") for w in fleet_w)
+    assert {"node": "slow", "ratio": 0.8} in summary["gemm@[4096, 4096, 4096]/tflops"]["outliers"]
+
+
+def test_a_node_behind_the_fleet_under_the_floor_fails(reports):
+    """GPUs alike under the absolute failure line fail; the fleet names the node as well."""
+    reps = reports({"n0": 1.0, "n1": 1.0, "n2": 1.0, "slow": 0.80})
+    summary, verdicts = _judge(reps)
+    v = verdicts["slow"]
+    assert v.state == H.UNHEALTHY and {r.split(":")[0] for r in v.reasons} == {f"gpu{d}" for d in range(8)}
     assert {"node": "slow", "ratio": 0.8} in summary["gemm@[4096, 4096, 4096]/tflops"]["outliers"]
 
 
@@ -141,10 +152,11 @@ def test_checker_paths(reports, mock_cluster, tmp_path):
         vs = apply_health(scan, opts, NullTracer(), [], cluster, out)
         return {n["name"]: v.state for n, v in zip(scan.gpu_nodes, vs)}, out
     plain, out = states()
-    assert set(plain.values()) == {H.DEGRADED} and out == {}
+    # the 0.70 node is under the absolute floor on every GPU: its agent already calls it unhealthy
+    assert plain == {"n0": H.DEGRADED, "n1": H.DEGRADED, "n2": H.DEGRADED, "slow": H.UNHEALTHY} and out == {}
     for kw in ({"health_reeval": True}, {"json_extended": True}):
         st, out = states(**kw)
-        assert st == {"n0": H.HEALTHY, "n1": H.HEALTHY, "n2": H.HEALTHY, "slow": H.DEGRADED}, (kw, st)
+        assert st == {"n0": H.HEALTHY, "n1": H.HEALTHY, "n2": H.HEALTHY, "slow": H.UNHEALTHY}, (kw, st)
         assert out["summary"]["gemm@[4096, 4096, 4096]/tflops"]["outliers"][0]["node"] == "slow"
 
 
@@ -153,8 +165,8 @@ def test_cli_fleet_and_explain_show_the_fleet(run_cli, reports, mock_cluster, tm
     _srv, kc = _cluster(mock_cluster, tmp_path, reps)
     p = run_cli(["--kubeconfig", kc, "--fleet"])
     assert p.returncode == 0, p.stdout + p.stderr
-    assert "MI355X verdicts: 3 healthy, 1 degraded" in p.stdout
-    assert "  slow: degraded  " in p.stdout
+    assert "MI355X verdicts: 3 healthy, 1 unhealthy" in p.stdout
+    assert "  slow: unhealthy (not Ready)  " in p.stdout
     line = next(ln for ln in p.stdout.splitlines() if ln.startswith("  gemm@[4096, 4096, 4096]/tflops: "))
     assert "4 nodes, median 88% (70%-88%)" in line and "platform shortfall" in line and "slow x0.80" in line
     p = run_cli(["--kubeconfig", kc, "--explain", "n1"])

@@ -346,3 +346,42 @@ def test_a_gpu_stuck_in_its_host_link_turn_does_not_hang_the_others(node8):
     finally:
         diag._release_shared()
     assert diag.run(2, 1)["host_link"].get("skipped") is None  # the lock is free again
+
+
+def test_eight_gpu_baselines_re_form_on_a_driver_upgrade_and_the_floor_holds(node8, monkeypatch):
+    """Round-5 rules on a whole 8-GPU node (fake ABI): every GPU forms its self-baseline, a driver upgrade that
+    makes the whole node 12 % slower re-forms all eight without a drift warning, and all eight at half rate --
+    alike, so peers would excuse each other -- fail under the absolute floor."""
+    from k8s_gpu_node_checker_amd.models import baseline as B
+    lib, _fab = node8(rate=1.10)
+    ag = A.Agent("n8", source="fake", diag_level=1, expect_gpus=8, diag_timeout=60, diag_interval=0.0)
+    for _ in range(B.BASELINE_RUNS):
+        assert ag.probe_once()["state"] == H.HEALTHY
+    assert len(ag.baselines.data) == 8
+    epochs = {ag.baselines.epoch(k) for k in ag.baselines.data}
+    assert len(epochs) == 1 and next(iter(epochs)).startswith("driver 6.18.54;")
+    node8.state["overrides"] = {"driver": {"name": "amdgpu", "version": "6.19.2"}}
+    lib.rate = 0.97
+    for _ in range(B.BASELINE_RUNS):
+        rep = ag.probe_once()
+        assert rep["state"] == H.HEALTHY, ag.evaluate(rep).warnings
+    assert all(ag.baselines.epoch(k).startswith("driver 6.19.2;") for k in ag.baselines.data)
+    lib.rate = 0.5
+    rep = ag.probe_once()
+    v = ag.evaluate(rep)
+    assert v.state == H.UNHEALTHY and (v.gpus_ok, v.gpus_seen) == (0, 8)
+
+
+def test_eight_node_fleet_with_a_withdrawn_device_plugin(mock_cluster, tmp_path):
+    """The membership rule over eight 8-GPU agents' reports: one node's device plugin withdrew every GPU; the
+    --mi355x check keeps it as Not Ready with the reason, the other seven Ready."""
+    from k8s_gpu_node_checker_amd.checker import CheckOptions, run_check
+    from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+    nodes = fixtures.cluster(8, "amd", with_health=True)
+    nodes[5]["status"]["allocatable"]["amd.com/gpu"] = "0"
+    srv = mock_cluster(nodes)
+    res = run_check(ClusterConnection(srv.url), CheckOptions(gpu_source="allocatable", health_policy="require",
+                                                             require_schedulable=True))
+    assert res.exit_code == 0 and len(res.gpu_nodes) == 8 and len(res.ready_gpu_nodes) == 7
+    v = res.verdicts[5]
+    assert v.state == H.UNHEALTHY and v.reasons[0] == "device plugin allocates 0 of 8 amd.com/gpu"

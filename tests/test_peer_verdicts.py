@@ -53,12 +53,24 @@ def test_eight_gpus_alike_at_088_are_one_node_level_warning(node):
     assert {f["test"] for f in rep["diag_node"]["findings"]} >= {"gemm", "gemm_fp8", "hbm", "mfma", "l2"}
 
 
-def test_a_node_wide_shortfall_under_the_floor_is_never_unhealthy(node):
-    node(8, rate=0.70)
+@pytest.mark.parametrize("rate", [0.70, 0.5, 0.3])
+def test_a_node_wide_shortfall_under_the_floor_fails_every_gpu(node, rate):
+    """GPUs alike do not excuse each other below the absolute failure line -- a node whose 8
+    GPUs all run at half rate is unhealthy, not one node-level note."""
+    node(8, rate=rate)
     rep = _agent(8).probe_once()
     v = H.evaluate_report(rep, 8)
-    assert v.state == H.DEGRADED and not v.reasons
+    assert v.state == H.UNHEALTHY and (v.gpus_ok, v.gpus_seen) == (0, 8)
+    assert {r.split(":")[0] for r in v.reasons} == {f"gpu{d}" for d in range(8)}
+    assert any(r.startswith("gpu0: diag gemm failed (tflops") for r in v.reasons), v.reasons
     assert all(f["below_floor"] for f in rep["diag_node"]["findings"])
+    assert H.condition_for(v)["status"] == "False"
+
+
+def test_a_node_wide_shortfall_between_the_lines_stays_a_warning(node):
+    node(8, rate=0.86)
+    v = H.evaluate_report(_agent(8).probe_once(), 8)
+    assert v.state == H.DEGRADED and not v.reasons
     assert H.condition_for(v)["status"] == "True"  # degraded still counts as Ready
 
 
@@ -176,7 +188,8 @@ def test_baseline_forms_from_clean_runs_then_flags_drift(node, tmp_path):
     doc = json.loads(path.read_text())
     assert doc["schema"] == B.SCHEMA and len(doc["gpus"]) == 4
     entry = next(iter(doc["gpus"].values()))
-    assert entry["gemm@[4096,4096,4096]"]["baseline"]["tflops"] == pytest.approx(1.10, rel=1e-3)
+    assert entry["tests"]["gemm@[4096,4096,4096]"]["baseline"]["tflops"] == pytest.approx(1.10, rel=1e-3)
+    assert entry["epoch"].startswith("driver 6.18.54; vbios 00175784; fw ")
     lib.rate = 0.96
     rep = ag.probe_once()
     v = H.evaluate_report(rep, 4)
@@ -223,7 +236,7 @@ def test_malformed_baseline_entries_are_rebuilt_not_fatal(tmp_path):
     p = tmp_path / "b.json"
     res = lambda: {"pass": True, "rates": {"tflops": 1000.0}, "expect": {"tflops": 1000.0},  # noqa: E731
                    "shape": [1, 1, 1]}
-    p.write_text(json.dumps({"schema": B.SCHEMA, "gpus": {
+    p.write_text(json.dumps({"schema": B.SCHEMA_V1, "gpus": {
         "a": {"gemm@[1,1,1]": ["not", "a", "dict"]},
         "b": {"gemm@[1,1,1]": {"samples": "junk"}},
         "c": {"gemm@[1,1,1]": {"samples": [1, {"tflops": 1.0}]}},
@@ -327,3 +340,152 @@ def test_status_table_shows_each_gpus_lowest_ratio_to_its_own_baseline(node):
     row0 = next(ln for ln in text.splitlines() if ln.strip().startswith("0 "))
     assert head.index("vs peers") < head.index("vs own") < head.index("findings")
     assert "x0.87" in row0 and "own baseline" in row0
+
+
+# --- baseline epochs and clean runs -------------------------------------------------
+
+def _fw(node_fixture, **over):
+    """Swap amd-smi's report for one with other driver / firmware fields."""
+    def probe(nd, src, fx, _n=node_fixture):
+        rep = fixtures.mi355x_probe_report(nd, gpus=_n)
+        rep["driver"].update(over.get("driver", {}))
+        for g in rep["gpus"]:
+            g["fw"].update(over.get("fw", {}))
+        return rep
+    return probe
+
+
+def test_a_driver_change_re_forms_the_baseline_without_drift(node, monkeypatch, tmp_path):
+    lib = node(2, rate=1.10)
+    path = tmp_path / "b.json"
+    ag = _agent(2, diag_interval=0.0, baseline_file=str(path))
+    for _ in range(B.BASELINE_RUNS):
+        ag.probe_once()
+    # the upgrade makes every GPU 12 % slower: under the old baseline that would be drift on every GPU forever
+    monkeypatch.setattr(amdsmi_probe, "probe", _fw(2, driver={"version": "6.19.2"}))
+    lib.rate = 0.97
+    for _ in range(B.BASELINE_RUNS):
+        rep = ag.probe_once()
+        assert rep["state"] == H.HEALTHY, H.evaluate_report(rep, 2).warnings
+        assert not any("own baseline" in w for w in H.evaluate_report(rep, 2).warnings)
+    doc = json.loads(path.read_text())
+    per = next(iter(doc["gpus"].values()))
+    assert per["epoch"].startswith("driver 6.19.2;") and per["previous"]["epoch"].startswith("driver 6.18.54;")
+    assert per["previous"]["baselines"]["gemm@[4096,4096,4096]"]["tflops"] == pytest.approx(1.10, rel=1e-3)
+    assert per["tests"]["gemm@[4096,4096,4096]"]["baseline"]["tflops"] == pytest.approx(0.97, rel=1e-3)
+    # drift is judged against the new software's normal: 0.86 is 89 % of 0.97
+    lib.rate = 0.86
+    rep = ag.probe_once()
+    assert any("gemm slow (tflops at 89% of this GPU's own baseline" in w for w in H.evaluate_report(rep, 2).warnings)
+    # a firmware flash is a new epoch too
+    monkeypatch.setattr(amdsmi_probe, "probe", _fw(2, driver={"version": "6.19.2"}, fw={"pm": 72748907}))
+    rep = ag.probe_once()
+    assert not any("own baseline" in w for w in H.evaluate_report(rep, 2).warnings)
+    gpu = next(iter(doc["gpus"]))
+    assert "pm=04.86.15.107" in B.Baselines(str(path)).epoch(gpu)
+
+
+def test_a_lone_gpu_at_093_forms_a_baseline_and_sees_a_drop_to_080_as_drift(node):
+    lib = node(1, rate=0.93)
+    ag = _agent(1, diag_interval=0.0)
+    for _ in range(B.BASELINE_RUNS):
+        rep = ag.probe_once()
+        assert rep["state"] == H.DEGRADED  # absolutely degraded (0.93 < 0.95), yet its runs are clean
+    key = A.baseline_key(fixtures.mi355x_probe_report("n", gpus=1)["gpus"][0], "", 0)
+    assert ag.baselines.baseline(key, "gemm", {"shape": [4096, 4096, 4096]})["tflops"] == pytest.approx(0.93, rel=1e-3)
+    lib.rate = 0.80
+    rep = ag.probe_once()
+    gemm = rep["gpus"][0]["diag"]["gemm"]
+    assert gemm["drift"] == ["tflops at 86% of this GPU's own baseline (5 clean runs)"]
+    assert H.evaluate_report(rep, 1).state == H.UNHEALTHY  # and under the absolute floor: failed as well
+
+
+def test_peer_excused_runs_under_the_floor_never_form_a_baseline():
+    """clean is judged on the result's own numbers, whatever pass/degraded flags a peer or
+    fleet judgement left on it."""
+    b = B.Baselines(runs=2)
+    res = lambda f, **kw: dict({"pass": True, "degraded": False, "rates": {"tflops": 1000.0 * f},  # noqa: E731
+                                "expect": {"tflops": 1000.0}, "shape": [1, 1, 1]}, **kw)
+    for _ in range(3):
+        b.observe("g", {"gemm": res(0.6)})
+    assert b.baseline("g", "gemm", res(0.6)) is None
+    for _ in range(3):
+        b.observe("g", {"gemm": res(1.0, numerics="checksum mismatch")})
+        b.observe("g", {"gemm": res(1.0, lag=["xcd3 at 80%"])})
+    assert b.baseline("g", "gemm", res(1.0)) is None
+    b.observe("g", {"gemm": res(0.9, **{"pass": False, "degraded": True})})
+    b.observe("g", {"gemm": res(0.9)})
+    assert b.baseline("g", "gemm", res(0.9)) == {"tflops": 0.9}
+
+
+def test_a_v1_baseline_file_is_read_and_upgraded(tmp_path):
+    p = tmp_path / "b.json"
+    p.write_text(json.dumps({"schema": B.SCHEMA_V1, "gpus": {"uuid:x": {
+        "gemm@[1,1,1]": {"baseline": {"tflops": 1.0}, "runs": 5, "since": 1.0}}}}))
+    b = B.Baselines(str(p))
+    res = {"rates": {"tflops": 800.0}, "expect": {"tflops": 1000.0}, "shape": [1, 1, 1]}
+    notes = b.observe("uuid:x", {"gemm": res}, epoch="driver 6.18.54")
+    assert notes == ["gemm: tflops at 80% of this GPU's own baseline (5 clean runs)"]  # kept, not re-formed
+    doc = json.loads(p.read_text())
+    assert doc["schema"] == B.SCHEMA and doc["gpus"]["uuid:x"]["epoch"] == "driver 6.18.54"
+    assert doc["gpus"]["uuid:x"]["tests"]["gemm@[1,1,1]"]["baseline"] == {"tflops": 1.0}
+
+
+def test_baselines_can_be_dropped_by_flag_and_by_a_loopback_post(node, tmp_path, monkeypatch):
+    import urllib.error
+    import urllib.request
+    from k8s_gpu_node_checker_amd.agent.server import serve
+    lib = node(2, rate=1.0)
+    path = tmp_path / "b.json"
+    ag = _agent(2, diag_interval=0.0, baseline_file=str(path))
+    for _ in range(B.BASELINE_RUNS):
+        ag.probe_once()
+    keys = sorted(ag.baselines.data)
+    assert len(keys) == 2
+    srv = serve(ag, "127.0.0.1", 0)
+    try:
+        url = f"http://127.0.0.1:{srv.server_address[1]}/baseline/reset?gpu={keys[0].split(':', 1)[1]}"
+        with urllib.request.urlopen(urllib.request.Request(url, method="POST", data=b""), timeout=5) as r:
+            assert json.loads(r.read()) == {"dropped": [keys[0]]}
+        assert sorted(ag.baselines.data) == keys[1:]
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(urllib.request.Request(url.replace("/baseline/reset", "/nope"), method="POST",
+                                                          data=b""), timeout=5)
+        assert e.value.code == 404
+    finally:
+        srv.shutdown()
+        srv.server_close()
+    assert json.loads(path.read_text())["gpus"].keys() == set(keys[1:])
+    b = B.Baselines(str(path))
+    assert b.drop(["no-such-gpu"]) == [] and b.drop(None) == keys[1:]
+    assert json.loads(path.read_text())["gpus"] == {}
+    # the start-up flag (--once with the fixture source: no HIP, the file is read, reset and written back)
+    path.write_text(json.dumps({"schema": B.SCHEMA, "gpus": {k: {"epoch": None, "tests": {}} for k in keys}}))
+    fx = tmp_path / "fx.json"
+    fx.write_text(json.dumps(fixtures.mi355x_probe_report("n", gpus=2)))
+    assert A.main(["--node", "n", "--once", "--source", "fixture", "--fixture", str(fx), "--publish", "stdout",
+                   "--diag-level", "0", "--diag-baseline-file", str(path), "--diag-baseline-reset", keys[1]]) in (0, 3)
+    assert set(json.loads(path.read_text())["gpus"]) == {keys[0]}
+
+
+def test_baseline_reset_is_refused_from_off_the_pod(node):
+    """POST /baseline/reset answers only a loopback peer: the checker's fan-out or Prometheus cannot reset it."""
+    import socket
+    import urllib.error
+    import urllib.request
+    from k8s_gpu_node_checker_amd.agent.server import serve
+    node(1)
+    ag = _agent(1, diag_interval=0.0)
+    ip = next((a[4][0] for a in socket.getaddrinfo(socket.gethostname(), None, socket.AF_INET)
+               if not a[4][0].startswith("127.")), None)
+    if ip is None:
+        pytest.skip("no non-loopback address")
+    srv = serve(ag, "0.0.0.0", 0)
+    try:
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(urllib.request.Request(f"http://{ip}:{srv.server_address[1]}/baseline/reset",
+                                                          method="POST", data=b""), timeout=5)
+        assert e.value.code == 403
+    finally:
+        srv.shutdown()
+        srv.server_close()
