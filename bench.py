@@ -24,7 +24,9 @@ annotation inside each step.
 Untimed extras (coldstart runs, the agent's diagnostics, the RCCL fabric check and the multi-GPU node
 cycle) share one wall-clock budget (``--extras-budget``, 180 s from start): an extra that would not fit in
 what is left is recorded as ``{"skipped": "budget"}``, the node-cycle child is killed at the budget, and the
-timed loop never waits on any of them.  Every phase's wall time is in the line (``phases_s``).
+timed loop never waits on any of them.  Every phase's wall time is in the line (``phases_s``), and where a
+timed step's milliseconds go -- connect, first byte, body, scan, health gate, render -- as medians
+(``step_ms``).
 
 Prints ONE JSON line (rank 0): value = nodes/s over the whole job.
 """
@@ -182,6 +184,30 @@ def _pctl(xs, q):
     return xs[i]
 
 
+def _step_breakdown(spans: list, lat: list) -> "dict | None":
+    """Median per-step milliseconds of each part of a check (``utils/timing.Tracer`` spans of the timed steps):
+    ``connect`` (TCP to the apiserver), ``first_byte`` (LIST sent to response head: the server's time),
+    ``body`` (the rest of the response), ``scan`` (NodeList scan), ``client`` (the rest of the LIST call:
+    client setup, headers, close), ``health`` (MI355X gate), ``render`` (JSON), ``other`` (what the step spent
+    outside those: Slack join when on, GC switch, the output sink)."""
+    if not spans or len(spans) != len(lat):
+        return None
+    rows = []
+    for sp, total in zip(spans, lat):
+        g = sp.get
+        lst = g("list", 0.0)
+        rows.append({"connect": g("connect", 0.0), "first_byte": g("first_byte", 0.0), "body": g("body", 0.0),
+                     "scan": g("parse", 0.0),
+                     "client": lst - g("connect", 0.0) - g("first_byte", 0.0) - g("body", 0.0) - g("parse", 0.0),
+                     "health": g("health", 0.0), "render": g("render", 0.0),
+                     "other": total - lst - g("health", 0.0) - g("render", 0.0)})
+    out = {k: round(_pctl([r[k] for r in rows], 0.5) * 1e3, 4) for k in rows[0]}
+    if any("slack" in sp for sp in spans):
+        out["slack"] = round(_pctl([sp.get("slack", 0.0) for sp in spans], 0.5) * 1e3, 4)
+    out["step"] = round(_pctl(lat, 0.5) * 1e3, 4)
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -258,6 +284,7 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
     from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
     from k8s_gpu_node_checker_amd.ops import fastpath
     from k8s_gpu_node_checker_amd.testing import fixtures
+    from k8s_gpu_node_checker_amd.utils.timing import Tracer
 
     cuda = torch.cuda.is_available()
     if cuda:
@@ -368,15 +395,19 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
         if rank == 0:
             sink_out.seek(0)
             sink_out.truncate()
-            res = check_and_report(cluster, opts, out=sink_out, err=sink_err)
+            tr = Tracer()  # per-step spans (utils/timing): a few perf_counter calls, ~2 us of the step
+            res = check_and_report(cluster, opts, out=sink_out, err=sink_err, tracer=tr)
+            spans.append(tr.spans)
             return res
         return None
 
     last = None
+    spans: list = []
     with budget.phase("warmup"):
         for _ in range(args.warmup):
             last = step()
         barrier()
+    spans.clear()
     lat = []
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -424,6 +455,8 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
             "latency_ms": {"p50": round(_pctl(lat, 0.5) * 1e3, 4), "p90": round(_pctl(lat, 0.9) * 1e3, 4),
                            "p99": round(_pctl(lat, 0.99) * 1e3, 4) if len(lat) >= 100 else None,
                            "min": round(min(lat) * 1e3, 4), "samples": len(lat)},
+            # where a step's milliseconds go: medians over the timed steps of the check's own spans
+            "step_ms": _step_breakdown(spans, lat),
             "coldstart_ms": (ctrl.get("coldstart") or {}).get("ms"),
             "coldstart": ctrl.get("coldstart"),
             "baseline_ms": ref,

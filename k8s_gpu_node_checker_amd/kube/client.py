@@ -119,7 +119,8 @@ class KubeClient:
             ctx = self.cluster.ssl_context() if self.cluster.server.startswith("https") else None
             self._conn = Connection(self.cluster.server, timeout=self.timeout, ssl_context=ctx,
                                     server_hostname=self.cluster.tls_server_name,
-                                    proxy_url=self.cluster.proxy_url)
+                                    proxy_url=self.cluster.proxy_url,
+                                    tracer=self.tracer if getattr(self.tracer, "live", False) else None)
         return self._conn
 
     def close(self) -> None:

@@ -100,7 +100,10 @@ class Connection:
     """One persistent HTTP/1.1 connection to ``scheme://host:port``."""
 
     def __init__(self, url: str, timeout: float = 30.0, ssl_context=None, server_hostname: Optional[str] = None,
-                 proxy_url: Optional[str] = None):
+                 proxy_url: Optional[str] = None, tracer=None):
+        #: ``utils.timing.Tracer`` (or None): :meth:`request` adds ``connect`` (TCP + TLS), ``first_byte`` (request
+        #: sent to response head read) and ``body`` (the rest of the response read)
+        self.tracer = tracer
         parts = urlsplit(url)
         self.scheme = parts.scheme or "http"
         self.host = parts.hostname or "localhost"
@@ -299,6 +302,9 @@ class Connection:
         raw = self._encode(method, path, headers, body)
         reused = self.sock is not None
         try:
+            tr = self.tracer
+            if tr is not None:
+                return self._traced(tr, method, url, raw, peek)
             self.connect(url)
             assert self.sock is not None
             self.sock.sendall(raw)
@@ -326,6 +332,23 @@ class Connection:
             if e.__class__.__name__.startswith("SSL"):
                 raise self._fail("tls", url, e)
             raise self._fail("aborted", url, e)
+
+    def _traced(self, tr, method: str, url: str, raw: bytes, peek) -> Response:
+        """:meth:`request`'s send and read with its three spans recorded on ``tr``."""
+        from time import perf_counter
+        t0 = perf_counter()
+        self.connect(url)
+        t1 = perf_counter()
+        assert self.sock is not None
+        self.sock.sendall(raw)
+        status, reason, headers, hmap = self._read_head()
+        t2 = perf_counter()
+        resp = self._finish_body(method, status, reason, headers, hmap, peek)
+        t3 = perf_counter()
+        tr.add("connect", t1 - t0)
+        tr.add("first_byte", t2 - t1)
+        tr.add("body", t3 - t2)
+        return resp
 
     def _peek_prefix(self, want: int, gz: bool, peek) -> None:
         """Buffer up to ``want`` body bytes (Content-Length bodies) and hand them to ``peek``."""

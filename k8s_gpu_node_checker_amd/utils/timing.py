@@ -1,8 +1,9 @@
 """Per-phase wall-clock tracer (SURVEY §5 "Tracing / profiling": the reference has none).
 
-Phases used by the checker: ``config``, ``list`` (network + server), ``parse``
-(NodeList scan, a sub-span of ``list``), ``health``, ``slack``, ``render``,
-``total``.  Shown with ``--trace`` on stderr and, with ``--json-extended``,
+Phases used by the checker: ``config``, ``list`` (network + server), and within it
+``connect`` (TCP + TLS), ``first_byte`` (request sent to response head), ``body``
+(the rest of the response) and ``parse`` (NodeList scan); ``health``, ``slack``,
+``render``, ``total``.  Shown with ``--trace`` on stderr and, with ``--json-extended``,
 as ``timings_ms`` in the payload; the default JSON is never touched.
 """
 
@@ -16,6 +17,9 @@ if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a
 
 
 class Tracer:
+    #: records anything (the transport skips its per-request spans for a :class:`NullTracer`)
+    live = True
+
     def __init__(self) -> None:
         self.spans: Dict[str, float] = {}
         self.t0 = time.perf_counter()
@@ -53,5 +57,7 @@ class _Span:
 
 
 class NullTracer(Tracer):
+    live = False
+
     def add(self, name: str, seconds: float) -> None:
         pass
