@@ -170,8 +170,41 @@ def _fast_parse(argv: List[str]) -> Optional[Any]:
     return _Args(ns)
 
 
+#: the reference's long options in its parser's order (``check-gpu-node.py:298-311``)
+_REF_FLAGS = ("--help", "--kubeconfig", "--json", "--slack-webhook", "--slack-username", "--slack-only-on-error",
+              "--slack-retry-count", "--slack-retry-delay")
+
+
+def _reference_abbrevs(argv: List[str]) -> List[str]:
+    """argparse accepts any unique prefix of a long option (``--js``, ``--kube PATH``, ``--slack-o``, ``--he``).
+    The hidden extension flags (``--json-extended``, ``--kube-timeout``, ``--slack-on-change``, ``--health-*``)
+    would make such a prefix ambiguous here while it is unique in the reference: a prefix that names exactly
+    one reference flag is spelled out, and one that names several reference flags gets the reference's own
+    ``ambiguous option`` error (listing only its flags).  Anything else -- exact flags, prefixes of extension
+    flags only, everything after ``--`` -- is left to argparse."""
+    known = {flag for _, flag, _ in _FLAGS}
+    known.update(("--help", "-h"))
+    out: List[str] = []
+    for i, tok in enumerate(argv):
+        if tok == "--":
+            out.extend(argv[i:])
+            break
+        if tok.startswith("--") and tok not in known:
+            prefix, eq, rest = tok.partition("=")
+            if prefix not in known:
+                hits = [f for f in _REF_FLAGS if f.startswith(prefix)]
+                if len(hits) == 1:
+                    tok = hits[0] + eq + rest
+                elif hits:
+                    build_parser().error(f"ambiguous option: {tok} could match {', '.join(hits)}")
+        out.append(tok)
+    return out
+
+
 def parse_args(argv: Optional[List[str]] = None) -> Any:
     argv = sys.argv[1:] if argv is None else argv
+    if any(t.startswith("--") for t in argv):
+        argv = _reference_abbrevs(argv)
     if "--help-all" in argv:
         build_parser(show_all=True).print_help()
         sys.exit(0)

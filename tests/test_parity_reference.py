@@ -307,3 +307,19 @@ def test_slack_transport_errors_identical(cluster, sink, url, env, flags):
     a, b, ra, rb = _transport_case(cluster, sink, url, env=env, flags=flags)
     assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
     assert "Traceback" not in b.stderr and b.stderr.startswith("슬랙 메시지 전송 실패: ")
+
+
+# --- argparse prefix matching: hidden extension flags must not make a reference abbreviation ambiguous ----------
+
+@pytest.mark.parametrize("args", [
+    ["--js"], ["--jso"], ["--kube", "MISSING"], ["--kubec=MISSING", "--json"], ["--slack-o", "--json"], ["--he"],
+    ["--h"], ["--slack"], ["--slack-retry"], ["--slack-retry=3"], ["--slack-u", "x", "--js"], ["--json", "--js"],
+    ["--slack-username", "--js"], ["--sl", "--json"], ["--k"], ["--j"], ["--", "--js"], ["--slack-w"],
+    ["--slack-retry-c", "x"], ["--jsonx"], ["-j"], ["--json=1"]])
+def test_abbreviations_behave_as_in_the_reference(args, tmp_path):
+    args = [str(tmp_path / "missing") if a == "MISSING" else a for a in args]
+    a, b = run_ref(args, cwd=str(tmp_path)), run_new(args, cwd=str(tmp_path))
+    assert (a.returncode, a.stdout) == (b.returncode, b.stdout), (a.stderr, b.stderr)
+    # stderr: identical, except the traceback frames of the kubeconfig error (the code that raised differs)
+    ta, tb = a.stderr.split("Traceback")[0], b.stderr.split("Traceback")[0]
+    assert ta == tb
