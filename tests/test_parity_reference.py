@@ -93,7 +93,8 @@ def _slack_case(cluster, sink, mode, extra_flags, nodes):
     return a, b, sink.requests[before:mid], sink.requests[mid:after]
 
 
-@pytest.mark.parametrize("mode", ["200", "500", "204", "flaky2", "resetflaky", "reset"])
+@pytest.mark.parametrize("mode", ["200", "500", "204", "flaky2", "resetflaky", "reset", "close", "404", "429",
+                                  "seq/mix1/close,500,200", "seq/mix2/reset,404,close"])
 def test_slack_behaviour_matches(cluster, sink, mode):
     a, b, ra, rb = _slack_case(cluster, sink, mode, [], fixtures.golden("readme"))
     assert a.returncode == b.returncode
