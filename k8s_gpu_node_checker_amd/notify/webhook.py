@@ -258,9 +258,9 @@ def netrc_auth(url: str, environ: Optional[Dict[str, str]] = None) -> Optional[T
     from urllib.parse import urlparse
     host = urlparse(url).hostname
     try:
-        from netrc import NetrcParseError, netrc
+        from netrc import netrc
         entry = netrc(found).authenticators(host)
-    except (ImportError, OSError, Exception):  # NetrcParseError, permissions, anything netrc raises
+    except Exception:  # NetrcParseError, OSError (permissions): skipped, as requests does
         return None
     if entry and any(entry):
         return (entry[0] if entry[0] else entry[1], entry[2])
@@ -373,10 +373,10 @@ def _target(url: str) -> str:
 
 def post(url: str, body: bytes, content_type: str = "application/json", timeout: float = 10.0,
          user_agent: str = "k8s-gpu-node-checker-amd/0.1", environ: Optional[Dict[str, str]] = None,
-         ssl_context=None, log: Optional[List[Tuple[str, str, Dict[str, str]]]] = None) -> Response:
+         ssl_context=None) -> Response:
     """``requests.post(url, data=body, timeout=timeout, headers={"Content-Type": content_type})``: the final
     response after redirects.  Raises :class:`HTTPError` (connection errors / timeouts) or
-    :class:`RequestError`.  ``log`` (tests) receives ``(method, url, headers)`` per hop."""
+    :class:`RequestError`."""
     env = os.environ if environ is None else environ
     prepared = prepare_url(url)
     if not prepared.lower().startswith(("http://", "https://")):
@@ -398,8 +398,6 @@ def post(url: str, body: bytes, content_type: str = "application/json", timeout:
         if ctx is None and current.lower().startswith("https"):
             ctx = env_ssl_context(env)
         target = _target(current)
-        if log is not None:
-            log.append((method, target, dict(headers)))
         resp = request(target, method, headers, data, timeout=timeout, ssl_context=ctx,
                        proxy_url=env_proxy(target, env))
         location = redirect_target(resp)

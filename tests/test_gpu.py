@@ -448,6 +448,10 @@ def test_agent_self_baseline_forms_on_the_gpu_without_drift(dev, tmp_path):
     assert min(v for r in rated.values() for v in r["baseline"]["ratio"].values()) > B.DRIFT_RATIO
     doc = json.loads(path.read_text())
     assert doc["schema"] == B.SCHEMA and len(doc["gpus"]) == 1
+    # the epoch is read off the real amd-smi report: the driver release and this GPU's firmware images
+    epoch = next(iter(doc["gpus"].values()))["epoch"]
+    assert epoch and epoch.startswith("driver ") and "; fw " in epoch and "pm=" in epoch, epoch
+    assert epoch == B.epoch_of(g, rep["driver"]["version"])
 
 
 def test_smoke(dev):
@@ -464,6 +468,10 @@ def test_bench_contract_on_gpu(repo):
     d = json.loads(line)
     assert d["check_ok"] and d["n_gpus"] == 1 and d["value"] > 0
     assert d["probe"]["source"] == "native", d["probe"]
+    # the line says where a step's time goes (medians; the parts add up to about the step)
+    sm = d["step_ms"]
+    assert set(sm) >= {"connect", "first_byte", "body", "scan", "client", "health", "render", "other", "step"}
+    assert abs(sum(v for k, v in sm.items() if k != "step") - sm["step"]) < 0.5 * sm["step"]
 
 
 def test_rccl_collective_single_rank(repo):
