@@ -37,7 +37,7 @@ from __future__ import annotations
 import os
 TYPE_CHECKING = False
 if TYPE_CHECKING:  # annotations only (PEP 563)
-    from typing import Any, Dict, List, Optional, Tuple
+    from typing import Dict, List, Optional, Tuple
 
 from ..utils.http import HTTPError, Response, env_proxy, request
 
