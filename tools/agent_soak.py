@@ -30,6 +30,22 @@ from k8s_gpu_node_checker_amd.testing import fixtures  # noqa: E402
 from k8s_gpu_node_checker_amd.testing.mock_apiserver import MockApiServer, write_kubeconfig  # noqa: E402
 
 
+def _baseline_summary(path: str):
+    """The baseline file the agent wrote: per GPU its epoch, the tests with a formed baseline and their values."""
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return {"file": None}
+    gpus = {}
+    for k, v in (doc.get("gpus") or {}).items():
+        tests = v.get("tests") or {}
+        gpus[k] = {"epoch": v.get("epoch"),
+                   "formed": {t: e["baseline"] for t, e in tests.items() if isinstance(e, dict) and "baseline" in e},
+                   "forming": sorted(t for t, e in tests.items() if isinstance(e, dict) and "baseline" not in e)}
+    return {"schema": doc.get("schema"), "gpus": gpus}
+
+
 def _rss_mb(pid: int):
     try:
         with open(f"/proc/{pid}/status") as f:
@@ -65,6 +81,9 @@ def main() -> int:
     ap.add_argument("--sample", type=float, default=10.0)
     ap.add_argument("--port", type=int, default=19464)
     ap.add_argument("--out", default="gpurun_out/agent_soak.json")
+    ap.add_argument("--baseline", action="store_true",
+                    help="run the agent with --diag-baseline-file, report the baselines it formed (epoch, ratios) "
+                         "and drop them at the end through POST /baseline/reset")
     args = ap.parse_args()
 
     nodes = fixtures.cluster(1, "amd", gpus_per_node=1)
@@ -76,6 +95,10 @@ def main() -> int:
            "--diag-interval", str(args.diag_interval), "--publish", "annotation,http",
            "--listen", f"127.0.0.1:{args.port}", "--kubeconfig", kc, "--annotation-encoding", "gzip",
            "--label-node", "--xgmi-links", "0", "--ignore-pid", str(os.getpid())]
+    baseline_path = os.path.join(os.path.dirname(kc), "baseline.json")
+    if args.baseline:
+        cmd += ["--diag-baseline-file", baseline_path]
+    baseline = None
     env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
     err_path = os.path.join(os.path.dirname(os.path.abspath(args.out)), "agent_soak.stderr")
     os.makedirs(os.path.dirname(err_path), exist_ok=True)
@@ -107,6 +130,12 @@ def main() -> int:
                                 if k.startswith("amd.com/")}}
                 samples.append(s)
                 print(json.dumps(s), flush=True)
+            if args.baseline and agent.poll() is None:
+                baseline = _baseline_summary(baseline_path)
+                req = urllib.request.Request(f"http://127.0.0.1:{args.port}/baseline/reset", data=b"", method="POST")
+                with urllib.request.urlopen(req, timeout=10) as r:
+                    baseline["reset"] = json.loads(r.read())
+                baseline["after_reset"] = _baseline_summary(baseline_path)
         finally:
             alive = agent.poll() is None
             agent.terminate()
@@ -136,6 +165,7 @@ def main() -> int:
         "diag_failures": sum(1 for s in samples for v in s["diag_pass"].values() if v is False),
         "apiserver_writes": {p: sum(1 for e in writes if e["path"] == p) for p in sorted({e["path"] for e in writes})},
         "labels_last": samples[-1]["labels"] if samples else None,
+        "baseline": baseline,
         "checker": {"exit_code": checker.returncode, "output": verdict},
         "explain": {"exit_code": explain.returncode, "text": explain.stdout.splitlines()},
         "series": samples,
