@@ -7,8 +7,11 @@
 //   gemm_bf16   C[M,N] = A[M,K] . Bt[N,K]^T, bf16 in / fp32 out on MFMA
 //               (v_mfma_f32_16x16x32_bf16), XOR-swizzled LDS (conflict-free
 //               ds_read_b128 fragment loads), XCD-aware tile order.
-//               v3: 256x256x64 tiles, 8 waves in two barrier-staggered groups, LDS-DMA
-//                   restaged region by region (large GEMMs, default);
+//               v4: 256x256x64 tiles, 4 waves of 128x128 each, the loop's MFMA /
+//                   ds_read / LDS-DMA interleave written out in asm (large bf16
+//                   GEMMs, default);
+//               v3: the same tile, 8 waves in two barrier-staggered groups, LDS-DMA
+//                   restaged region by region (fp8 / fp4, and bf16 for A/B);
 //               v2: the same tile, one barrier per K-tile (kept for A/B);
 //               v1: 128x128x64 tiles, 4 waves, register-staged (small grids).
 //               Verified against an fp32 reference kernel on sampled outputs.
@@ -39,6 +42,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 namespace {
@@ -750,6 +754,237 @@ gemm_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// v4 (bf16): hipBLASLt's gfx950 structure -- 256 threads, a 256x256x64 tile, each wave 128x128 (256 accumulator
+// AGPRs), 2 LDS stages -- with the loop's instruction order written out.  Every MFMA, fragment ds_read and LDS-DMA
+// of the loop is an `asm volatile` statement, so hipcc keeps their interleave and allocates the accumulators to
+// AGPRs ("+a") and the fragments to VGPRs once; the lgkmcnt / vmcnt waits are explicit.  Compiler-ordered
+// four-wave versions (rounds 2-3) lost to v3 on accumulator shuffling between AGPRs and VGPRs; this one beats it
+// (tools/gemm_w4a_lab.hip sweeps the schedule knobs, profiles/gemm_w4a_lab_mi355x.jsonl).
+//
+// Per K-tile kt (stage s = kt & 1; F0 = k-step 0 fragments of tile kt, already in registers):
+//   half 1: 64 MFMA on F0; one ds_read of F1 (tile kt, k-step 1, stage s) after every RS-th of the first 16 * RS;
+//           after MFMA X_AT lgkmcnt(0) + s_barrier X (every wave is done with stage s); D1 LDS-DMA pieces of tile
+//           kt+2 into stage s spread over the rest
+//   half 2: 64 MFMA on F1; after MFMA Y_AT vmcnt(D1) (tile kt+1, issued one K-tile ago, landed) + s_barrier Y;
+//           ds_read F0' (tile kt+1, k-step 0, stage s^1) one per R2 MFMAs; the other 16 - D1 DMA pieces spread
+//           over the rest; lgkmcnt(0) at the end
+// Near the end the DMA re-fetches tile KT-1 into a stage nobody reads any more, and the last iteration's F0' reads
+// load harmless stale fragments (branch-free loop); everything is drained before the epilogue.
+// The wave's rows are m * 16 + fq * 4 + j (m = 0..7) and the K order is v3's, so C and the fused column sums are
+// bit-identical to v3's.
+constexpr int V4_THREADS = 256;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void v4_mfma(floatx4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+template <int OFF>
+__device__ __forceinline__ void v4_read(bf16x8& f, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(addr), "i"(OFF));
+}
+
+// one LDS-DMA wave instruction: 64 lanes x 16 B from rsrc + voff + soff into LDS at m0 + lane * 16 (m0 is set in
+// the same statement, so nothing the compiler schedules in between can see or change it)
+__device__ __forceinline__ void v4_dma(uint32_t m0, uint32_t voff, const i32x4& rsrc, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(m0), "v"(voff), "s"(rsrc), "s"(soff)
+               : "memory");
+}
+
+__device__ __forceinline__ i32x4 v4_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  i32x4 r;
+  r.x = static_cast<int>(b);
+  r.y = static_cast<int>(b >> 32);
+  r.z = static_cast<int>(bytes);
+  r.w = 0x00020000;  // raw buffer, 32-bit data format
+  return r;
+}
+
+struct V4Frags {
+  bf16x8 a[8], b[8];
+};
+
+// piece p (0-7: A m-block p, 8-15: B n-block p-8) of a k-step's fragments; m-block offsets (2048 B) are immediates
+template <int P>
+__device__ __forceinline__ void v4_piece(V4Frags& f, uint32_t a_addr, uint32_t b_addr) {
+  if constexpr (P < 8) v4_read<P * 2048>(f.a[P], a_addr);
+  else v4_read<(P - 8) * 2048>(f.b[P - 8], b_addr);
+}
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void v4_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    v4_for<I + 1, N>(f);
+  }
+}
+
+// Schedule knobs (the shipped values won tools/gemm_w4a_lab.hip's sweep at 4096^3 and 8192^3):
+//   RS    half 1 issues one F1 read after every RS-th MFMA (16 reads)
+//   X_AT  the MFMA of half 1 after which lgkmcnt(0) + barrier X are taken (>= 16 * RS - 1)
+//   D1    LDS-DMA pieces of tile kt+2 issued in half 1 after X; the other 16 - D1 go in half 2 after Y
+//   Y_AT  the MFMA of half 2 after which vmcnt(D1) + barrier Y are taken; F0' reads follow, one per R2 MFMAs
+//   GM    GROUP_M of the tile order
+template <int OUT = OUT_F32, int RS = 1, int X_AT = 20, int D1 = 8, int Y_AT = 8, int GM = 4, int R2 = 2>
+__global__ void __launch_bounds__(V4_THREADS, 1)
+gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv,
+               double* __restrict__ csum, int M, int N, int K) {
+  static_assert(X_AT >= 16 * RS - 1 && Y_AT + 16 * R2 < 64 && D1 >= 0 && D1 <= 16, "schedule out of range");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages x 64 KiB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the DMA's m0 is an SGPR
+  const int wr = wid >> 1, wc = wid & 1;
+  const int tiles_m = M / V2_BM, tiles_n = N / V2_BN, nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int group = bid / (GM * tiles_n);
+  const int first_m = group * GM;
+  const int gsize = min(tiles_m - first_m, GM);
+  const int tm = first_m + (bid % (GM * tiles_n)) % gsize;
+  const int tn = (bid % (GM * tiles_n)) / gsize;
+  const __bf16* Ab = A + static_cast<size_t>(tm) * V2_BM * K;
+  const __bf16* Bb = Bt + static_cast<size_t>(tn) * V2_BN * K;
+  const int KT = K / BK;
+
+  // LDS-DMA: wave instruction j (0-15) of a tile: operand j >> 3, rows wid * 64 + (j & 7) * 8 + 0..7 (lane: row +
+  // (lane >> 3), physical chunk lane & 7, source chunk XOR-swizzled by row; the swizzle depends on the row's bit
+  // 3, i.e. on (j & 1): two per-lane offsets), the rest scalar: soffset = kt * 128 + (j & 7) * 8 * K * 2
+  const i32x4 rs_a = v4_rsrc(Ab, static_cast<uint32_t>(V2_BM) * K * 2);
+  const i32x4 rs_b = v4_rsrc(Bb, static_cast<uint32_t>(V2_BN) * K * 2);
+  const int rsub = lane >> 3, phys = lane & 7;
+  const int row_e = wid * 64 + rsub;
+  const uint32_t voff_e = (row_e * K + (phys ^ swz_row_xor(row_e, false)) * 8) * 2;
+  const uint32_t voff_o = (row_e * K + (phys ^ swz_row_xor(row_e + 8, false)) * 8) * 2;
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
+  const uint32_t m0_wave = lds0 + wid * 64 * (BK * 2);
+  const uint32_t row8 = 8u * K * 2;
+  auto dma = [&](uint32_t stage_off, int kt, int j) {
+    const int op = j >> 3, r = j & 7;
+    v4_dma(m0_wave + stage_off + op * (V2_BM * BK * 2) + r * 8 * (BK * 2), (r & 1) ? voff_o : voff_e,
+           op ? rs_b : rs_a, static_cast<uint32_t>(kt) * (BK * 2) + r * row8);
+  };
+
+  // fragment reads: lane (frow, fq); k-step 1 is chunk ^ 4
+  const int frow = lane & 15, fq = lane >> 4, x = (frow >> 1) & 7;
+  uint32_t ra[2][2], rb[2][2];  // [stage][k-step]
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint32_t c = static_cast<uint32_t>(((fq + 4 * ks) ^ x) * 16);
+      ra[s][ks] = lds0 + s * V2_STAGE_BYTES + (wr * 128 + frow) * (BK * 2) + c;
+      rb[s][ks] = lds0 + s * V2_STAGE_BYTES + V2_BM * BK * 2 + (wc * 128 + frow) * (BK * 2) + c;
+    }
+
+  floatx4 acc[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: tiles 0 and 1 into stages 0 and 1, tile 0 waited for, F0 of tile 0 read
+  v4_for<0, 16>([&](auto j) { dma(0, 0, j); });
+  v4_for<0, 16>([&](auto j) { dma(V2_STAGE_BYTES, KT > 1 ? 1 : 0, j); });
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  STG_BARRIER();
+  V4Frags f0, f1;
+  v4_for<0, 16>([&](auto p) { v4_piece<p>(f0, ra[0][0], rb[0][0]); });
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  for (int kt = 0; kt < KT; ++kt) {
+    const int s = kt & 1;
+    const uint32_t stage_off = s ? V2_STAGE_BYTES : 0;
+    const uint32_t a1 = s ? ra[1][1] : ra[0][1], b1 = s ? rb[1][1] : rb[0][1];
+    const uint32_t a0n = s ? ra[0][0] : ra[1][0], b0n = s ? rb[0][0] : rb[1][0];
+    const int kd = min(kt + 2, KT - 1);
+    constexpr int SP1 = D1 > 0 ? (63 - X_AT) / D1 : 1;  // MFMAs per DMA piece after X
+    v4_for<0, 64>([&](auto i) {
+      v4_mfma(acc[i >> 3][i & 7], f0.a[i >> 3], f0.b[i & 7]);
+      if constexpr (i % RS == RS - 1 && i / RS < 16) v4_piece<i / RS>(f1, a1, b1);
+      if constexpr (i == X_AT) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (i > X_AT && (i - X_AT) % SP1 == 0 && (i - X_AT) / SP1 - 1 < D1)
+        dma(stage_off, kd, (i - X_AT) / SP1 - 1);
+    });
+    constexpr int D2 = 16 - D1;
+    constexpr int SP2 = D2 > 0 ? (63 - Y_AT) / D2 : 1;
+    v4_for<0, 64>([&](auto i) {
+      v4_mfma(acc[i >> 3][i & 7], f1.a[i >> 3], f1.b[i & 7]);
+      if constexpr (i == Y_AT) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(D1) : "memory");
+      if constexpr (i > Y_AT && (i - Y_AT - 1) % R2 == 0 && (i - Y_AT - 1) / R2 < 16)
+        v4_piece<(i - Y_AT - 1) / R2>(f0, a0n, b0n);
+      if constexpr (D2 > 0 && i > Y_AT && (i - Y_AT) % SP2 == 0 && (i - Y_AT) / SP2 - 1 < D2)
+        dma(stage_off, kd, D1 + (i - Y_AT) / SP2 - 1);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // epilogue through each wave's own LDS patch (16 rows x 128 columns of fp32), as v3's
+  const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 128;
+  constexpr int LD = 128 + 4;
+  float* patch = reinterpret_cast<float*>(smem) + wid * (16 * LD);
+  if constexpr (OUT == OUT_BF16_CK) {
+    // column sums over the wave's 128 rows in v3's order (m, then j, then the 4 lanes fq holding the column)
+    double cs[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      cs[n] = 0.0;
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cs[n] += static_cast<double>(acc[m][n][j]);
+      cs[n] += __shfl_xor(cs[n], 16);
+      cs[n] += __shfl_xor(cs[n], 32);
+    }
+    if (fq == 0) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) csum[static_cast<size_t>(row0 / 128) * N + col0 + n * 16 + frow] = cs[n];
+    }
+    __bf16* __restrict__ Cb = static_cast<__bf16*>(Cv);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) patch[(fq * 4 + j) * LD + n * 16 + frow] = acc[m][n][j];
+      // 8 bf16 (16 bytes) per lane: one store instruction covers 4 rows x 256 contiguous bytes
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = q * 4 + (lane >> 4), c8 = (lane & 15) * 8;
+        const floatx4 lo = *reinterpret_cast<const floatx4*>(patch + r * LD + c8);
+        const floatx4 hi = *reinterpret_cast<const floatx4*>(patch + r * LD + c8 + 4);
+        const floatx8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        *reinterpret_cast<bf16x8*>(Cb + static_cast<size_t>(row0 + m * 16 + r) * N + col0 + c8) =
+            __builtin_convertvector(v, bf16x8);
+      }
+    }
+  } else {
+    float* __restrict__ C = static_cast<float*>(Cv);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) patch[(fq * 4 + j) * LD + n * 16 + frow] = acc[m][n][j];
+      // one store instruction covers 2 rows x 512 contiguous bytes
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = q * 2 + (lane >> 5), c4 = (lane & 31) * 4;
+        const floatx4 v = *reinterpret_cast<const floatx4*>(patch + r * LD + c4);
+        *reinterpret_cast<floatx4*>(C + static_cast<size_t>(row0 + m * 16 + r) * N + col0 + c4) = v;
+      }
+    }
+  }
+}
+
 // fp32 reference for sampled outputs: one thread per (row, col) sample.
 __global__ void gemm_ref_kernel(const __bf16* A, const __bf16* Bt, const int* rows, const int* cols, float* out,
                                 int nsamp, int K) {
@@ -968,14 +1203,20 @@ __global__ void __launch_bounds__(256) mt_verify_kernel(const uint4* p, size_t n
 }
 
 int grid_for(int device, int blocks_per_cu) {
-  int cus = 256;
-  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) {
+    (void)hipGetLastError();
+    cus = 256;  // the MI355X's CU count (a grid size only: any value is correct, this one fills the chip)
+  }
   return cus * blocks_per_cu;
 }
 
 float elapsed_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0.f;
-  hipEventElapsedTime(&ms, a, b);
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1.f;  // no time: a negative rate, which every rate check fails, rather than an infinite one
+  }
   return ms;
 }
 
@@ -1325,8 +1566,22 @@ int launch_v3_ck_fp8(const void* A, const void* Bt, __bf16* C, double* csum, int
                              : launch_v3_ck<DT_FP8>(A, Bt, C, csum, M, N, Kcols, stream);
 }
 
+// v4 launch (bf16; M, N multiples of 256, K of 64): fp32 C, or bf16 C + fused column sums (OUT_BF16_CK)
+template <int OUT>
+int launch_v4(const void* A, const void* Bt, void* C, double* csum, int M, int N, int K, hipStream_t stream) {
+  static LdsAttrOnce attr;
+  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_v4_kernel<OUT>), 2 * V2_STAGE_BYTES, "gemm v4") !=
+      0)
+    return -1;
+  const int nwg = (M / V2_BM) * (N / V2_BN);
+  hipLaunchKernelGGL((gemm_v4_kernel<OUT>), dim3(nwg), dim3(V4_THREADS), 2 * V2_STAGE_BYTES, stream,
+                     static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, csum, M, N, K);
+  return 0;
+}
+
 // The diagnostic runs (diag_gemm_*_x) take the bf16-output kernel wherever the production v3 configuration
-// would run (LDS-staged epilogue, global_load_lds staging); other knob settings keep fp32 C.
+// would run (LDS-staged epilogue, global_load_lds staging); other knob settings keep fp32 C.  v4 has one
+// configuration, always LDS-staged: it always has the bf16 output.
 bool v3_ck_path() { return g_gemm_epilogue == 1 && !g_gemm_buffer_loads; }
 
 // v3 launch (M, N multiples of 256; Kcols = bf16 columns, K8 / 2 for fp8), epilogue per g_gemm_epilogue,
@@ -1343,12 +1598,24 @@ int launch_v3(const void* A, const void* Bt, float* C, int M, int N, int Kcols, 
                          : launch_v3_inst<DT, false, false, 1>(A, Bt, C, M, N, Kcols, stream);
 }
 
-// The bf16 kernel diag_gemm_bf16_launch runs for M x N: 1 = v1 (128^2 tiles), 2 = v2, 3 = v3 (256^2).  v2/v3
-// need 256-multiples and enough 256^2 tiles to occupy the 256 CUs (one block per CU); below that the 128^2
+// The bf16 kernel diag_gemm_bf16_launch runs for M x N: 1 = v1 (128^2 tiles), 2 = v2, 3 = v3, 4 = v4 (256^2).
+// v2-v4 need 256-multiples and enough 256^2 tiles to occupy the 256 CUs (one block per CU); below that the 128^2
 // kernel's 4x larger grid wins (measured: 2048^3 v1 543 vs v2 321 TFLOP/s).
 int bf16_variant(int M, int N) {
   const bool big_ok = M % V2_BM == 0 && N % V2_BN == 0 && (M / V2_BM) * (N / V2_BN) >= 256;
-  return g_gemm_variant == 0 ? (big_ok ? 3 : 1) : g_gemm_variant;
+  return g_gemm_variant == 0 ? (big_ok ? 4 : 1) : g_gemm_variant;
+}
+
+// the bf16 launch with bf16 C + fused column sums: v4 when the thread's variant resolves to it, else v3
+int launch_bf16_ck(const void* A, const void* Bt, __bf16* C, double* csum, int M, int N, int K, hipStream_t stream) {
+  return bf16_variant(M, N) == 4 ? launch_v4<OUT_BF16_CK>(A, Bt, C, csum, M, N, K, stream)
+                                 : launch_v3_ck<DT_BF16>(A, Bt, C, csum, M, N, K, stream);
+}
+
+// diag_gemm_bf16_x writes bf16 C with fused column sums (else fp32 C)
+bool bf16_fused(int M, int N) {
+  const int v = bf16_variant(M, N);
+  return v == 4 || (v == 3 && v3_ck_path());
 }
 
 // Output tiles of a launch and their blockIdx regrouping (the mapping at the top of every GEMM kernel).
@@ -1507,8 +1774,9 @@ extern "C" {
 
 const char* diag_last_error(void) { return g_err.c_str(); }
 
-// 0 = auto (v3 staggered 256x256 LDS-DMA tiles when M, N are multiples of 256 and the grid fills the
-// chip, else v1), 1 = force v1 (128x128 register-staged), 2 = force v2, 3 = force v3
+// 0 = auto (bf16: v4 four-wave 256x256 tiles when M, N are multiples of 256 and the grid fills the chip, else
+// v1), 1 = force v1 (128x128 register-staged), 2 = force v2, 3 = force v3 (8 waves, staggered), 4 = force v4.
+// fp8 / fp4 GEMMs run v3 whatever this says.
 void diag_set_gemm_variant(int v) { g_gemm_variant = v; }
 void diag_set_gemm_epilogue(int e) { g_gemm_epilogue = e; }
 void diag_set_gemm_buffer_loads(int b) { g_gemm_buffer_loads = b; }
@@ -1553,12 +1821,14 @@ int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N,
     return -2;
   }
   const int variant = bf16_variant(M, N);
-  if (variant == 2 || variant == 3) {
+  if (variant >= 2 && variant <= 4) {
     if (M % V2_BM || N % V2_BN) {
-      g_err = "gemm_bf16 v2/v3: M, N must be multiples of 256";
+      g_err = "gemm_bf16 v2-v4: M, N must be multiples of 256";
       return -2;
     }
-    if (variant == 2) {
+    if (variant == 4) {
+      if (launch_v4<OUT_F32>(A, Bt, C, nullptr, M, N, K, static_cast<hipStream_t>(stream)) != 0) return -1;
+    } else if (variant == 2) {
       static LdsAttrOnce attr;
       if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_bf16_v2_kernel), 2 * V2_STAGE_BYTES,
                              "gemm v2") != 0)
@@ -1621,7 +1891,7 @@ int diag_gemm_launch_ck(int dt, const void* A, const void* Bt, void* C, double* 
   }
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const int rc = dt == DT_FP8 ? launch_v3_ck_fp8(A, Bt, static_cast<__bf16*>(C), csum, M, N, K / 2, st)
-                              : launch_v3_ck<DT_BF16>(A, Bt, static_cast<__bf16*>(C), csum, M, N, K, st);
+                              : launch_bf16_ck(A, Bt, static_cast<__bf16*>(C), csum, M, N, K, st);
   if (rc != 0) return -1;
   DIAG_CHECK(hipGetLastError());
   return 0;
@@ -1630,7 +1900,7 @@ int diag_gemm_launch_ck(int dt, const void* A, const void* Bt, void* C, double* 
 // 1 when diag_gemm_bf16_x (dt 0) / diag_gemm_fp8_x (dt 1) at M x N would time the bf16-output kernel with fused
 // column sums under the calling thread's knobs, 0 when it would write fp32 C
 int diag_gemm_ck_path(int dt, int M, int N) {
-  return v3_ck_path() && (dt == DT_FP8 || bf16_variant(M, N) == 3) ? 1 : 0;
+  return (dt == DT_FP8 ? v3_ck_path() : bf16_fused(M, N)) ? 1 : 0;
 }
 
 // Self-contained MFMA burn-in: allocate, fill, run `iters` GEMMs, time them, verify `nsamp` sampled outputs
@@ -1648,8 +1918,8 @@ int diag_gemm_bf16_x(int device, int M, int N, int K, int warmup, int iters, int
     return -2;
   }
   DIAG_CHECK(hipSetDevice(device));
-  // the v3 kernel writes bf16 C and its own column sums (OUT_BF16_CK); the 128^2 v1 kernel fp32 C
-  const bool fused = bf16_variant(M, N) == 3 && v3_ck_path();
+  // the v4 / v3 kernels write bf16 C and their own column sums (OUT_BF16_CK); the 128^2 v1 kernel fp32 C
+  const bool fused = bf16_fused(M, N);
   DevBuf bA, bBt, bC, bref, brows, bcols, bgot, bcs;
   DIAG_CHECK(bA.alloc(device, sizeof(__bf16) * static_cast<size_t>(M) * K));
   DIAG_CHECK(bBt.alloc(device, sizeof(__bf16) * static_cast<size_t>(N) * K));
@@ -1657,7 +1927,7 @@ int diag_gemm_bf16_x(int device, int M, int N, int K, int warmup, int iters, int
   if (fused) DIAG_CHECK(bcs.alloc(device, sizeof(double) * static_cast<size_t>(M / 128) * N));
   double* cs = static_cast<double*>(bcs.ptr);
   auto run = [&]() -> int {
-    return fused ? launch_v3_ck<DT_BF16>(bA.ptr, bBt.ptr, static_cast<__bf16*>(bC.ptr), cs, M, N, K, nullptr)
+    return fused ? launch_bf16_ck(bA.ptr, bBt.ptr, static_cast<__bf16*>(bC.ptr), cs, M, N, K, nullptr)
                  : diag_gemm_bf16_launch(bA.ptr, bBt.ptr, static_cast<float*>(bC.ptr), M, N, K, nullptr);
   };
   DIAG_CHECK(bref.alloc(device, sizeof(float) * nsamp));

@@ -298,13 +298,14 @@ def device_info(device: int = 0) -> Dict[str, Any]:
     return {"arch": arch, "name": name, "cus": int(cus), "mem_bytes": int(mem), "bdf": bdf}
 
 
-GEMM_VARIANTS = {"auto": 0, "v1": 1, "v2": 2, "v3": 3}
+GEMM_VARIANTS = {"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v4": 4}
 
 
 def set_gemm_variant(variant: str = "auto") -> None:
-    """Select the GEMM kernel: ``auto`` (v3 for 256-multiples that fill the chip, else v1),
-    ``v1`` 128x128 register-staged, ``v2`` 256x256 LDS-DMA, ``v3`` 256x256 staggered LDS-DMA.
-    v2/v3 need M, N multiples of 256."""
+    """Select the bf16 GEMM kernel: ``auto`` (v4 for 256-multiples that fill the chip, else v1),
+    ``v1`` 128x128 register-staged, ``v2`` 256x256 LDS-DMA, ``v3`` 256x256 staggered LDS-DMA (8 waves),
+    ``v4`` 256x256 with 4 waves of 128x128 and the loop's instruction order written out (diag.hip
+    ``gemm_v4_kernel``).  v2-v4 need M, N multiples of 256.  fp8 / fp4 GEMMs always run v3."""
     lib().diag_set_gemm_variant(GEMM_VARIANTS[variant])
 
 

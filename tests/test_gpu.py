@@ -125,7 +125,7 @@ def test_mfma_gemm_matches_fp32_reference(dev, m, n, k):
     assert rel < 1e-4 * max(1, k / 512), rel
 
 
-@pytest.mark.parametrize("variant", ["v1", "v2", "v3", "v3-lds-epilogue"])
+@pytest.mark.parametrize("variant", ["v1", "v2", "v3", "v3-lds-epilogue", "v4"])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (768, 512, 256),
                                    (1024, 768, 4096)])
 def test_mfma_gemm_variants_match_fp32_reference(dev, variant, m, n, k):
@@ -285,9 +285,9 @@ def test_fp8_burn_in_kind_runs_the_unscaled_f8f6f4_path_exactly(dev):
     assert fp8["tflops"] > 1.5 * bf16["tflops"], r["kinds"]
 
 
-def test_mfma_gemm_large_auto_uses_v3_and_matches(dev):
-    """4096^3 in auto mode runs the staggered v3 kernel; compare every output with a bf16-input,
-    fp32-accumulate torch reference.  Runs with the production knobs (what the agent launches)."""
+def test_mfma_gemm_large_auto_uses_v4_and_matches(dev):
+    """4096^3 in auto mode runs the four-wave v4 kernel, bit-identical to v3; compare every output with a
+    bf16-input, fp32-accumulate torch reference.  Runs with the production knobs (what the agent launches)."""
     from k8s_gpu_node_checker_amd.ops import diag
     assert diag.get_gemm_config() == {"variant": "auto", "epilogue": True, "buffer_loads": False, "schedule": 1,
                                      "fp8_unscaled": True}
@@ -301,6 +301,53 @@ def test_mfma_gemm_large_auto_uses_v3_and_matches(dev):
     ref = a.float() @ bt.float().t()
     rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
     assert rel < 1e-4 * (k / 512), rel
+    with diag.gemm_config(variant="v3"):
+        c3 = torch.full_like(c, float("nan"))
+        diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c3.data_ptr(), m, n, k, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    assert torch.equal(c, c3)
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (768, 512, 320),
+                                   (1024, 768, 4096), (2048, 2048, 2048), (4096, 4096, 1024)])
+def test_v4_gemm_is_bit_identical_to_v3(dev, m, n, k):
+    """The four-wave v4 kernel (asm-ordered loop, 128x128 per wave) accumulates in v3's K order: fp32 C, bf16 C and
+    the fused column sums all equal v3's bit for bit, over 1-64 K-tiles (the prologue, the re-fetch of the last tile
+    and the stale final fragment reads) and non-square grids; and it matches torch."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + 3 * n + 17 * k)
+    st = torch.cuda.current_stream().cuda_stream
+    a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
+    bt = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
+    outs = {}
+    for variant in ("v3", "v4"):
+        with diag.gemm_config(variant=variant):
+            c32 = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+            diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c32.data_ptr(), m, n, k, st)
+            c16 = torch.full((m, n), float("nan"), device=dev, dtype=torch.bfloat16)
+            cs = torch.full((m // 128, n), float("nan"), device=dev, dtype=torch.float64)
+            diag.gemm_launch_ck("bf16", a.data_ptr(), bt.data_ptr(), c16.data_ptr(), cs.data_ptr(), m, n, k, st)
+            torch.cuda.synchronize()
+            outs[variant] = (c32, c16, cs)
+    for x, y in zip(outs["v3"], outs["v4"]):
+        assert torch.equal(x, y)
+    c32, c16, cs = outs["v4"]
+    assert torch.equal(c16, c32.to(torch.bfloat16))
+    ref = a.float() @ bt.float().t()
+    assert ((c32 - ref).abs() / ref.abs().clamp_min(1.0)).max().item() < 1e-4 * max(1, k / 512)
+
+
+def test_v4_gemm_diagnostic_reports_bf16_output(dev):
+    """The bf16 diagnostic at a size that fills the chip times v4 with bf16 C and fused sums, and passes."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    assert diag.lib().diag_gemm_ck_path(0, 4096, 4096) == 1
+    with diag.gemm_config(variant="v4", epilogue=False):  # v4 has one epilogue: the knob does not apply
+        assert diag.lib().diag_gemm_ck_path(0, 4096, 4096) == 1
+    with diag.gemm_config(variant="v3", epilogue=False):
+        assert diag.lib().diag_gemm_ck_path(0, 4096, 4096) == 0
+    r = diag.gemm(0, size=4096, warmup=1, iters=3, samples=512)
+    assert r["numerics"] == "" and r["checksum_bad_tiles"] == 0, r
+    assert r["output"] == "bf16+colsums" and r["tflops"] > 0, r
 
 
 def test_mfma_gemm_identity_asymmetric(dev):

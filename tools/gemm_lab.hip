@@ -249,7 +249,7 @@ lab_v3_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float
 // reads (lgkmcnt(0)) before the barrier that closed its load slot, and the other group's phase-p load
 // slot closes before this group's phase p+1 load slot opens.  Issue: phase 1 R0 R0 R1, phase 2 R1 R2 R2,
 // phase 3 R3 R3; retire tile t+1 at phase 3 of tile t with vmcnt(8) (tile t+2's 8 pieces may fly).
-__device__ __forceinline__ void v4_piece(unsigned char* lds_stage, const __bf16* __restrict__ A,
+__device__ __forceinline__ void lab_piece(unsigned char* lds_stage, const __bf16* __restrict__ A,
                                          const __bf16* __restrict__ Bt, int K, int kt, int region, int i, int wid,
                                          int lane) {
   const int rsub = lane >> 3, phys = lane & 7;
@@ -272,7 +272,7 @@ __device__ __forceinline__ void v4_piece(unsigned char* lds_stage, const __bf16*
 
 template <bool PRIO>
 __global__ void __launch_bounds__(V2_THREADS, 1)
-gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N, int K) {
+gemm_lab_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
@@ -330,9 +330,9 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     SLOT_BARRIER();
     // phase 1
     if (pre) {
-      v4_piece(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
-      v4_piece(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
-      v4_piece(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
     }
 #pragma unroll
     for (int n = 0; n < 2; ++n)
@@ -345,9 +345,9 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     SLOT_BARRIER();
     // phase 2
     if (pre) {
-      v4_piece(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
-      v4_piece(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
-      v4_piece(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -360,8 +360,8 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     SLOT_BARRIER();
     // phase 3
     if (pre) {
-      v4_piece(cur, Ab, Bb, K, kt + 2, 3, 0, wid, lane);
-      v4_piece(cur, Ab, Bb, K, kt + 2, 3, 1, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 3, 0, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 3, 1, wid, lane);
       __builtin_amdgcn_s_waitcnt(0x3f78);  // vmcnt(8): tile kt+1 landed
     } else {
       __builtin_amdgcn_s_waitcnt(0x3f70);
@@ -438,8 +438,8 @@ gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     const bool pre = kt + 2 < KT;
     // phase 0 (+ tile kt+1's R3 into the other buffer; tile 1 came whole with the prologue)
     if (!(ABL & 1) && kt >= 1 && kt + 1 < KT) {
-      v4_piece(nxt, Ab, Bb, K, kt + 1, 3, 0, wid, lane);
-      v4_piece(nxt, Ab, Bb, K, kt + 1, 3, 1, wid, lane);
+      lab_piece(nxt, Ab, Bb, K, kt + 1, 3, 0, wid, lane);
+      lab_piece(nxt, Ab, Bb, K, kt + 1, 3, 1, wid, lane);
     }
 #pragma unroll
     for (int n = 0; n < 2; ++n)
@@ -465,10 +465,10 @@ gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     if (!(ABL & 2)) SLOT_BARRIER();
     // phase 2: restage R0, R1 of this buffer with tile kt+2
     if (!(ABL & 1) && pre) {
-      v4_piece(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
-      v4_piece(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
-      v4_piece(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
-      v4_piece(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 0, 0, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 0, 1, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 1, 0, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 1, 1, wid, lane);
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -481,8 +481,8 @@ gemm_v5_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     if (!(ABL & 2)) SLOT_BARRIER();
     // phase 3: restage R2; retire tile kt+1
     if (!(ABL & 1) && pre) {
-      v4_piece(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
-      v4_piece(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 2, 0, wid, lane);
+      lab_piece(cur, Ab, Bb, K, kt + 2, 2, 1, wid, lane);
       if (!(ABL & 4)) __builtin_amdgcn_s_waitcnt(0x3f76);  // vmcnt(6)
     } else {
       if (!(ABL & 4)) __builtin_amdgcn_s_waitcnt(0x3f70);
@@ -545,10 +545,10 @@ gemm_v6_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
   v2_fill(smem, Ab, Bb, K, 0, wid, lane);
   if (KT > 1) {
     unsigned char* s1 = smem + V2_STAGE_BYTES;
-    v4_piece(s1, Ab, Bb, K, 1, 0, 0, wid, lane);
-    v4_piece(s1, Ab, Bb, K, 1, 0, 1, wid, lane);
-    v4_piece(s1, Ab, Bb, K, 1, 1, 0, wid, lane);
-    v4_piece(s1, Ab, Bb, K, 1, 1, 1, wid, lane);
+    lab_piece(s1, Ab, Bb, K, 1, 0, 0, wid, lane);
+    lab_piece(s1, Ab, Bb, K, 1, 0, 1, wid, lane);
+    lab_piece(s1, Ab, Bb, K, 1, 1, 0, wid, lane);
+    lab_piece(s1, Ab, Bb, K, 1, 1, 1, wid, lane);
     __builtin_amdgcn_s_waitcnt(0x3f74);  // vmcnt(4): tile 0 landed
   } else {
     __builtin_amdgcn_s_waitcnt(0x3f70);
@@ -559,8 +559,8 @@ gemm_v6_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
 #define V6_STAGE(buf, tile, region)                                  \
   do {                                                               \
     if ((tile) < KT) {                                               \
-      v4_piece((buf), Ab, Bb, K, (tile), (region), 0, wid, lane);    \
-      v4_piece((buf), Ab, Bb, K, (tile), (region), 1, wid, lane);    \
+      lab_piece((buf), Ab, Bb, K, (tile), (region), 0, wid, lane);    \
+      lab_piece((buf), Ab, Bb, K, (tile), (region), 1, wid, lane);    \
       __builtin_amdgcn_s_waitcnt(0x3f78); /* vmcnt(8) */             \
     } else {                                                         \
       __builtin_amdgcn_s_waitcnt(0x3f70); /* vmcnt(0) */             \
@@ -680,8 +680,8 @@ int main(int argc, char** argv) {
     CK(hipFuncSetAttribute((const void*)gemm_vp_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     CK(hipFuncSetAttribute((const void*)lab_v3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     CK(hipFuncSetAttribute((const void*)lab_v3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
-    CK(hipFuncSetAttribute((const void*)gemm_v4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
-    CK(hipFuncSetAttribute((const void*)gemm_v4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    CK(hipFuncSetAttribute((const void*)gemm_lab_v4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    CK(hipFuncSetAttribute((const void*)gemm_lab_v4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     CK(hipFuncSetAttribute((const void*)gemm_v5_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     CK(hipFuncSetAttribute((const void*)gemm_v5_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     auto check = [&](const char* name, double ms) {
@@ -706,9 +706,9 @@ int main(int argc, char** argv) {
     check("v3", ms);
     ms = time_ms([&] { hipLaunchKernelGGL(lab_v3_kernel<true>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("v3+prio", ms);
-    ms = time_ms([&] { hipLaunchKernelGGL(gemm_v4_kernel<false>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
+    ms = time_ms([&] { hipLaunchKernelGGL(gemm_lab_v4_kernel<false>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("v4", ms);
-    ms = time_ms([&] { hipLaunchKernelGGL(gemm_v4_kernel<true>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
+    ms = time_ms([&] { hipLaunchKernelGGL(gemm_lab_v4_kernel<true>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("v4+prio", ms);
     ms = time_ms([&] { hipLaunchKernelGGL(gemm_v5_kernel<false>, dim3(nwg2), dim3(V2_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C1, M, N, K); }, it);
     check("v5", ms);

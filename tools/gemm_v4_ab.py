@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""A/B of the bf16 GEMM kernels in one process: the four-wave v4 kernel (diag.hip ``gemm_v4_kernel``, the default
+since round 5) against the 8-wave v3 kernel it replaced and torch.matmul (hipBLASLt), on the same random operands,
+interleaved rounds (the clock drifts with temperature: a kernel timed in one block would carry the drift).
+
+Both outputs the diagnostics use are timed: fp32 C (``gemm_launch``) and bf16 C with fused 128-row column sums
+(``gemm_launch_ck``, what the ``gemm`` diagnostic times; hipBLASLt writes bf16 C too).  Before timing, v4's fp32 C,
+bf16 C and column sums are compared with v3's bit for bit.  One JSON line per size.
+
+    python tools/gemm_v4_ab.py --rounds 7 --sizes 4096,8192,16384
+    python tools/gemm_v4_ab.py --sizes 4096x4096x32768,8192x8192x1024   # M x N x K
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from k8s_gpu_node_checker_amd.ops import diag  # noqa: E402
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--sizes", default="4096,8192")
+    args = ap.parse_args()
+    st = torch.cuda.current_stream().cuda_stream
+    for spec in args.sizes.split(","):
+        m, n, k = (int(x) for x in spec.split("x")) if "x" in spec else (int(spec),) * 3
+        flop = 2.0 * m * n * k
+        iters = max(3, min(40, int(40 * 4096 ** 3 / (m * n * k))))
+        g = torch.Generator(device="cuda").manual_seed(n)
+        a = (torch.rand(m, k, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand(n, k, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+        b = bt.t()
+        c32 = torch.empty(m, n, device="cuda")
+        c16 = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+        cs = torch.empty(m // 128, n, device="cuda", dtype=torch.float64)
+
+        def fp32(variant):
+            def go():
+                with diag.gemm_config(variant=variant):
+                    diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c32.data_ptr(), m, n, k, st)
+            return go
+
+        def ck(variant):
+            def go():
+                with diag.gemm_config(variant=variant):
+                    diag.gemm_launch_ck("bf16", a.data_ptr(), bt.data_ptr(), c16.data_ptr(), cs.data_ptr(), m, n, k,
+                                        st)
+            return go
+
+        outs = {}
+        for v in ("v3", "v4"):
+            fp32(v)()
+            ck(v)()
+            torch.cuda.synchronize()
+            outs[v] = (c32.clone(), c16.clone(), cs.clone())
+        same = {name: torch.equal(x, y) for name, x, y in zip(("fp32_c", "bf16_c", "colsums"), outs["v3"],
+                                                                outs["v4"])}
+        ref_err = ((outs["v4"][0] - a.float() @ b.float()).abs().max() / k).item() if m * n <= 8192 ** 2 else None
+        del outs
+        # the knob is switched outside the timed loop: gemm_config per launch would time ctypes calls too
+        runs = {}
+        for v in ("v3", "v4"):
+            runs[f"{v}_fp32_out"] = (v, lambda: diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c32.data_ptr(), m, n,
+                                                                 k, st))
+            runs[f"{v}_bf16_out_fused_ck"] = (v, lambda: diag.gemm_launch_ck("bf16", a.data_ptr(), bt.data_ptr(),
+                                                                             c16.data_ptr(), cs.data_ptr(), m, n, k,
+                                                                             st))
+        runs["hipblaslt_bf16_out"] = (None, lambda: torch.matmul(a, b))
+        tf = {k: [] for k in runs}
+        for _ in range(args.rounds):
+            for key, (v, fn) in runs.items():
+                if v is None:
+                    ms = timed(fn, iters)
+                else:
+                    with diag.gemm_config(variant=v):
+                        ms = timed(fn, iters)
+                tf[key].append(flop / ms / 1e9)
+        med = {k: round(statistics.median(x), 1) for k, x in tf.items()}
+        lib = med["hipblaslt_bf16_out"]
+        print(json.dumps({"dtype": "bf16", "size": n if m == n == k else [m, n, k], "rounds": args.rounds, "median_tflops": med,
+                          "best_tflops": {k: round(max(x), 1) for k, x in tf.items()},
+                          "fraction_of_hipblaslt": {k: round(med[k] / lib, 3) for k in med if k != "hipblaslt_bf16_out"},
+                          "v4_over_v3": {o: round(med[f"v4_{o}"] / med[f"v3_{o}"], 3)
+                                         for o in ("fp32_out", "bf16_out_fused_ck")},
+                          "v4_bit_identical_to_v3": same, "v4_max_abs_err_over_k": ref_err}), flush=True)
+        del a, bt, b, c32, c16, cs
+        torch.cuda.empty_cache()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

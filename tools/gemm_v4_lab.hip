@@ -24,29 +24,29 @@
 
 namespace {
 
-constexpr int V4_REGION = V2_BM * 64;       // one operand's k-half of a stage: 256 rows x 64 B = 16 KiB
-constexpr int V4_STAGE = 4 * V4_REGION;     // [half][A | B] = 64 KiB
-static_assert(2 * V4_STAGE <= 160 * 1024, "two stages fit the CU's LDS");
+constexpr int KS_REGION = V2_BM * 64;       // one operand's k-half of a stage: 256 rows x 64 B = 16 KiB
+constexpr int KS_STAGE = 4 * KS_REGION;     // [half][A | B] = 64 KiB
+static_assert(2 * KS_STAGE <= 160 * 1024, "two stages fit the CU's LDS");
 
-__device__ __forceinline__ int v4_swz(int row) { return (row >> 2) & 2; }
+__device__ __forceinline__ int ks_swz(int row) { return (row >> 2) & 2; }
 
 // One 16 KiB region (rows 0..255 of one operand, columns kt*64 + h*32 .. +32) as 16 wave-instructions of 16 rows x
 // 64 B; wave wid issues instructions 2*wid and 2*wid+1.  Lane: row (lane >> 2), physical chunk (lane & 3), which
-// holds logical chunk (lane & 3) ^ v4_swz(row).
-__device__ __forceinline__ void v4_dma(unsigned char* region, const __bf16* __restrict__ src, int K, int kt, int h,
+// holds logical chunk (lane & 3) ^ ks_swz(row).
+__device__ __forceinline__ void ks_dma(unsigned char* region, const __bf16* __restrict__ src, int K, int kt, int h,
                                        int wid, int lane) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int j = wid * 2 + i;
     const int row = j * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ v4_swz(row);
+    const int c = (lane & 3) ^ ks_swz(row);
     const __bf16* g = src + static_cast<size_t>(row) * K + kt * 64 + h * 32 + c * 8;
     __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(region + j * 1024), 16, 0, 0);
   }
 }
 
-__device__ __forceinline__ bf16x8 v4_frag(const unsigned char* region, int row, int fq) {
-  return *reinterpret_cast<const bf16x8*>(region + row * 64 + ((fq ^ v4_swz(row)) << 4));
+__device__ __forceinline__ bf16x8 ks_frag(const unsigned char* region, int row, int fq) {
+  return *reinterpret_cast<const bf16x8*>(region + row * 64 + ((fq ^ ks_swz(row)) << 4));
 }
 
 // LATE: group 0 waits for the LDS-DMA at the end of its MFMA slot instead of its load slot -- one slot more for
@@ -54,7 +54,7 @@ __device__ __forceinline__ bf16x8 v4_frag(const unsigned char* region, int row, 
 // slot's end).
 template <bool PRIO, bool LATE = false>
 __global__ void __launch_bounds__(V2_THREADS, 1)
-gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
+gemm_ks_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, float* __restrict__ C, int M, int N,
                int K) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -73,7 +73,7 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
   const int tn = (bid % (GROUP_M * tiles_n)) / gsize;
   const __bf16* Ab = A + static_cast<size_t>(tm) * V2_BM * K;
   const __bf16* Bb = Bt + static_cast<size_t>(tn) * V2_BN * K;
-  auto region = [&](int stage, int h, int op) { return smem + stage * V4_STAGE + (h * 2 + op) * V4_REGION; };
+  auto region = [&](int stage, int h, int op) { return smem + stage * KS_STAGE + (h * 2 + op) * KS_REGION; };
 
   floatx4 acc[8][4];
 #pragma unroll
@@ -85,8 +85,8 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
 
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    v4_dma(region(0, h, 0), Ab, K, 0, h, wid, lane);
-    v4_dma(region(0, h, 1), Bb, K, 0, h, wid, lane);
+    ks_dma(region(0, h, 0), Ab, K, 0, h, wid, lane);
+    ks_dma(region(0, h, 1), Bb, K, 0, h, wid, lane);
   }
   __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0)
   STG_BARRIER();
@@ -103,15 +103,15 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, floa
     for (int h = 0; h < 2; ++h) {
       // load slot
       if (more) {
-        v4_dma(region(nxt, h, 0), Ab, K, kt + 1, h, wid, lane);
-        v4_dma(region(nxt, h, 1), Bb, K, kt + 1, h, wid, lane);
+        ks_dma(region(nxt, h, 0), Ab, K, kt + 1, h, wid, lane);
+        ks_dma(region(nxt, h, 1), Bb, K, kt + 1, h, wid, lane);
       }
       const unsigned char* ra = region(cur, h, 0);
       const unsigned char* rb = region(cur, h, 1);
 #pragma unroll
-      for (int n = 0; n < 4; ++n) fb[n] = v4_frag(rb, wc * 64 + n * 16 + frow, fq);
+      for (int n = 0; n < 4; ++n) fb[n] = ks_frag(rb, wc * 64 + n * 16 + frow, fq);
 #pragma unroll
-      for (int m = 0; m < 8; ++m) fa[m] = v4_frag(ra, wr * 128 + m * 16 + frow, fq);
+      for (int m = 0; m < 8; ++m) fa[m] = ks_frag(ra, wr * 128 + m * 16 + frow, fq);
       if (!LATE || wr == 1) {
         if (more) {
           __builtin_amdgcn_s_waitcnt(0x3f74);  // vmcnt(4): the previous load slot's pieces landed
@@ -181,7 +181,7 @@ double time_ms(L launch, int iters) {
 
 template <bool PRIO, bool LATE = false>
 void launch_v4(const __bf16* A, const __bf16* Bt, float* C, int M, int N, int K) {
-  hipLaunchKernelGGL((gemm_v4_kernel<PRIO, LATE>), dim3((M / V2_BM) * (N / V2_BN)), dim3(V2_THREADS), 2 * V4_STAGE,
+  hipLaunchKernelGGL((gemm_ks_kernel<PRIO, LATE>), dim3((M / V2_BM) * (N / V2_BN)), dim3(V2_THREADS), 2 * KS_STAGE,
                      nullptr, A, Bt, C, M, N, K);
 }
 
@@ -191,14 +191,14 @@ int main(int argc, char** argv) {
   std::vector<int> sizes = {4096, 8192};
   if (argc > 1 && atoi(argv[1]) > 0) sizes = {atoi(argv[1])};
   const int reps = argc > 2 ? atoi(argv[2]) : 5;  // timed rounds per kernel, interleaved (DVFS drift)
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<false>),
-                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<true>),
-                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<false, true>),
-                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<true, true>),
-                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V4_STAGE));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_ks_kernel<false>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * KS_STAGE));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_ks_kernel<true>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * KS_STAGE));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_ks_kernel<false, true>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * KS_STAGE));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_ks_kernel<true, true>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * KS_STAGE));
   for (int size : sizes) {
     if (size % 256 || size < 512) {
       printf("size must be a multiple of 256, >= 512\n");

@@ -1,0 +1,30 @@
+"""Same operands, three bf16 GEMMs with bf16 C (default 8192^3): diag v3 (8 waves) and v4 (4 waves, asm-ordered
+loop), both with fused column sums, and torch (hipBLASLt).  Run under ``rocprofv3 --kernel-trace --pmc ...``
+(tools/gpu_pmc_v4.sh) to compare MFMA busy, LDS conflicts, waits and HBM bytes of the three kernels."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from k8s_gpu_node_checker_amd.ops import diag  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(7)
+a = (torch.rand(n, n, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+b = (torch.rand(n, n, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+st = torch.cuda.current_stream().cuda_stream
+c16 = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
+cs = torch.empty(n // 128, n, device=dev, dtype=torch.float64)
+# interleaved rounds (the first launches of each kernel run slow: take the median per kernel)
+for _ in range(5):
+    for variant in ("v3", "v4"):
+        with diag.gemm_config(variant=variant):
+            for _ in range(2):
+                diag.gemm_launch_ck("bf16", a.data_ptr(), b.data_ptr(), c16.data_ptr(), cs.data_ptr(), n, n, n, st)
+        torch.cuda.synchronize()
+    for _ in range(2):
+        torch.matmul(a, b.t())
+    torch.cuda.synchronize()
+print("done")
