@@ -779,18 +779,25 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void v4_mfma(floatx4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
+// the first MFMA into an accumulator: C = 0 as an inline constant, so the accumulators need no zeroing.  (Zeroing
+// them in C++ let hipcc copy a zero AGPR into the others with v_accvgpr_mov right before the first asm MFMA, a
+// sequence that left every accumulator wrong on the MI355X -- the K = 64 path, where no loop separated the two.)
+__device__ __forceinline__ void v4_mfma_first(floatx4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+}
 
 template <int OFF>
 __device__ __forceinline__ void v4_read(bf16x8& f, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(addr), "i"(OFF));
 }
 
-// one LDS-DMA wave instruction: 64 lanes x 16 B from rsrc + voff + soff into LDS at m0 + lane * 16 (m0 is set in
-// the same statement, so nothing the compiler schedules in between can see or change it)
-__device__ __forceinline__ void v4_dma(uint32_t m0, uint32_t voff, const i32x4& rsrc, uint32_t soff) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+// one LDS-DMA wave instruction: 64 lanes x 16 B from rsrc + voff + soff into LDS at m0 + lane * 16, with
+// m0 = base + IMM set in the same statement (nothing the compiler schedules in between can see or change it)
+template <uint32_t IMM>
+__device__ __forceinline__ void v4_dma_imm(uint32_t m0_base, uint32_t voff, const i32x4& rsrc, uint32_t soff) {
+  asm volatile("s_add_u32 m0, %0, %1\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds"
                :
-               : "s"(m0), "v"(voff), "s"(rsrc), "s"(soff)
+               : "s"(m0_base), "i"(IMM), "v"(voff), "s"(rsrc), "s"(soff)
                : "memory");
 }
 
@@ -823,17 +830,274 @@ __device__ __forceinline__ void v4_for(F&& f) {
   }
 }
 
-// Schedule knobs (the shipped values won tools/gemm_w4a_lab.hip's sweep at 4096^3 and 8192^3):
-//   RS    half 1 issues one F1 read after every RS-th MFMA (16 reads)
-//   X_AT  the MFMA of half 1 after which lgkmcnt(0) + barrier X are taken (>= 16 * RS - 1)
-//   D1    LDS-DMA pieces of tile kt+2 issued in half 1 after X; the other 16 - D1 go in half 2 after Y
-//   Y_AT  the MFMA of half 2 after which vmcnt(D1) + barrier Y are taken; F0' reads follow, one per R2 MFMAs
-//   GM    GROUP_M of the tile order
-template <int OUT = OUT_F32, int RS = 1, int X_AT = 20, int D1 = 8, int Y_AT = 8, int GM = 4, int R2 = 2>
+// In-kernel stamps of the v4 loop (a lab build only: -DDIAG_V4_STAMPS, tools/gemm_w4a_lab.hip --stamps).  Every
+// wave records s_memtime deltas into a buffer nothing else reads: [0] prologue, [1] K loop, [2] epilogue up to its
+// stores' completion, [3] the middle K-tile's iteration, and the time that iteration spent in [4] X (lgkmcnt +
+// barrier), [5] Y (vmcnt + barrier), [6] the closing lgkmcnt.  Each stamp pair waits for its own s_memtime, so
+// the stamped build runs a little slower than the production one, which compiles all of this out.
+#ifdef DIAG_V4_STAMPS
+constexpr bool kV4Stamps = true;
+__device__ unsigned long long g_v4_stamps[4096][4][8];
+#else
+constexpr bool kV4Stamps = false;
+#endif
+
+// One recursive-halving step of a 16-lane sum: this lane keeps half `bit` of s[0, 2 * H) (the upper half when bit
+// is 1) and adds the partner lane's copy of that half; the partner is the DPP permutation CTRL's image, a lane of
+// the other `bit`.  Afterwards s[0, H) holds the kept half.
+template <int H, int CTRL>
+__device__ __forceinline__ void v4_halve(double (&s)[32], int bit) {
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const double keep = bit ? s[i + H] : s[i];
+    const double send = bit ? s[i] : s[i + H];
+    const uint64_t u = __builtin_bit_cast(uint64_t, send);
+    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(u), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(u >> 32), CTRL, 0xf, 0xf, false);
+    s[i] = keep + __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) |
+                                                 static_cast<uint32_t>(lo));
+  }
+}
+
+// The K-tile's schedule as a plan over its 128 MFMA slots (slot i < 64: MFMA i on F0, the rest on F1).  After
+// slot i's MFMA come, in this order: fragment read read(i) (0-15: F1 piece, from this tile's stage; 16-31: F0'
+// piece of tile kt+1, from the other stage), wait(i) (1: lgkmcnt(0) + s_barrier, 2: vmcnt(vm(i)) + s_barrier) and
+// LDS-DMA dma(i) (piece j of tile kt+2 into this tile's stage).  v4_plan_ok checks a plan at compile time: every
+// F1 read retired (lgkmcnt barrier) before slot 64 and before any DMA into its operand's region, every F0' read
+// after the vmcnt barrier that retires the previous K-tile's DMAs, vm = the DMAs issued since, 16 DMAs in all.
+struct V4Slot {
+  int read = -1, wait = 0, vm = 0, dma = -1;
+};
+
+// Plan A (knobs; the shipped values won tools/gemm_w4a_lab.hip's sweeps at 4096^3 and 8192^3):
+//   RS    half 1 issues one F1 read after every RS-th MFMA (16 reads: the A pieces, then the B pieces)
+//   X_AT  the slot after which lgkmcnt(0) + barrier X are taken (>= 16 * RS - 1)
+//   D1    DMA pieces issued in half 1 after X, evenly; the other 16 - D1 in half 2 after Y
+//   Y_AT  the slot of half 2 after which vmcnt(D1) + barrier Y are taken; F0' reads follow, one per R2 MFMAs
+template <int RS, int X_AT, int D1, int Y_AT, int R2>
+struct V4PlanA {
+  static constexpr V4Slot at(int i) {
+    V4Slot o;
+    constexpr int SP1 = D1 > 0 ? (63 - X_AT) / D1 : 1, D2 = 16 - D1, SP2 = D2 > 0 ? (63 - Y_AT) / D2 : 1;
+    if (i < 64) {
+      if (i % RS == RS - 1 && i / RS < 16) o.read = i / RS;
+      if (i == X_AT) o.wait = 1;
+      if (i > X_AT && (i - X_AT) % SP1 == 0 && (i - X_AT) / SP1 - 1 < D1) o.dma = (i - X_AT) / SP1 - 1;
+    } else {
+      const int h = i - 64;
+      if (h == Y_AT) {
+        o.wait = 2;
+        o.vm = D1;
+      }
+      if (h > Y_AT && (h - Y_AT - 1) % R2 == 0 && (h - Y_AT - 1) / R2 < 16) o.read = 16 + (h - Y_AT - 1) / R2;
+      if (D2 > 0 && h > Y_AT && (h - Y_AT) % SP2 == 0 && (h - Y_AT) / SP2 - 1 < D2) o.dma = D1 + (h - Y_AT) / SP2 - 1;
+    }
+    return o;
+  }
+};
+
+// Plan S (hipBLASLt's order, read from its gfx950 MT256x256x64 kernel): the A pieces of F1 one per 2 MFMAs, barrier
+// X1 (XA), then the B pieces of F1 one per 2 MFMAs with the A-operand DMAs between them, barrier X2 (XB), the
+// B-operand DMAs one per BSP MFMAs, barrier Y (slot 64 + Y_AT) retiring the previous K-tile, F0' one per 2 MFMAs.
+template <int XA, int XB, int BSP, int Y_AT>
+struct V4PlanS {
+  static constexpr V4Slot at(int i) {
+    V4Slot o;
+    if (i < 16 && i % 2 == 0) o.read = i / 2;                                       // A pieces 0-7
+    if (i == XA) o.wait = 1;                                                         // X1
+    if (i > XA && i <= XA + 16 && (i - XA) % 2 == 1) o.read = 8 + (i - XA) / 2;     // B pieces 8-15
+    if (i > XA && i <= XA + 16 && (i - XA) % 2 == 0) o.dma = (i - XA) / 2 - 1;       // A DMAs 0-7
+    if (i == XB) o.wait = 1;                                                         // X2
+    if (i > XB && (i - XB) % BSP == 0 && (i - XB) / BSP <= 8) o.dma = 7 + (i - XB) / BSP;  // B DMAs 8-15
+    const int y = 64 + Y_AT;
+    if (i == y) {
+      o.wait = 2;
+      int n = 0;
+      for (int k = 0; k < y; ++k)
+        if (at_dma(k) >= 0) ++n;
+      o.vm = n;
+    }
+    if (i > y && (i - y - 1) % 2 == 0 && (i - y - 1) / 2 < 16) o.read = 16 + (i - y - 1) / 2;
+    return o;
+  }
+  static constexpr int at_dma(int i) {
+    if (i > XA && i <= XA + 16 && (i - XA) % 2 == 0) return (i - XA) / 2 - 1;
+    if (i > XB && (i - XB) % BSP == 0 && (i - XB) / BSP <= 8) return 7 + (i - XB) / BSP;
+    return -1;
+  }
+};
+
+template <class P>
+constexpr bool v4_plan_ok() {
+  int read_at[32] = {}, dma_at[16] = {}, lgk_barriers[128] = {}, vm_at = -1, vm = -1, nb = 0;
+  for (int k = 0; k < 32; ++k) read_at[k] = -1;
+  for (int k = 0; k < 16; ++k) dma_at[k] = -1;
+  for (int i = 0; i < 128; ++i) {
+    const V4Slot o = P::at(i);
+    if (o.read >= 0) {
+      if (o.read > 31 || read_at[o.read] >= 0) return false;
+      read_at[o.read] = i;
+    }
+    if (o.wait == 1) lgk_barriers[nb++] = i;
+    if (o.wait == 2) {
+      if (vm_at >= 0) return false;
+      vm_at = i;
+      vm = o.vm;
+    }
+    if (o.dma >= 0) {
+      if (o.dma > 15 || dma_at[o.dma] >= 0) return false;
+      dma_at[o.dma] = i;
+    }
+  }
+  if (vm_at < 0) return false;
+  int issued = 0;
+  for (int k = 0; k < 16; ++k) {
+    if (dma_at[k] < 0) return false;
+    if (dma_at[k] < vm_at) ++issued;
+  }
+  if (issued != vm) return false;
+  // the first lgkmcnt barrier after slot t (or -1)
+  auto barrier_after = [&](int t) {
+    for (int b = 0; b < nb; ++b)
+      if (lgk_barriers[b] >= t) return lgk_barriers[b];
+    return -1;
+  };
+  for (int k = 0; k < 16; ++k) {
+    const int b = barrier_after(read_at[k]);  // F1 piece k retired here (same slot: read, then the wait)
+    if (read_at[k] < 0 || b < 0 || b >= 64) return false;
+    // DMAs into the piece's operand region (A: pieces / DMAs 0-7, B: 8-15) only after that barrier
+    for (int j = (k < 8 ? 0 : 8); j < (k < 8 ? 8 : 16); ++j)
+      if (dma_at[j] <= b) return false;
+  }
+  for (int k = 16; k < 32; ++k)
+    if (read_at[k] <= vm_at) return false;
+  return true;
+}
+
+// ---- fp8 (E4M3) form of the v4 kernel: the same tile, waves, staging (a K-tile is 128 bytes, the fp8 swizzle)
+// and epilogue; one v_mfma_f32_16x16x128_f8f6f4 (hipBLASLt's fp8 instruction, unscaled) per output block and
+// K-tile, so C is v3's fp8 C bit for bit.  A fragment is a lane's 32 contiguous bytes of a row (two 16-byte
+// chunks, 8 VGPRs); the 16 fragments of a K-tile take 128 VGPRs, too many to double-buffer beside 256
+// accumulators, so -- as hipBLASLt's MT256x256x128 fp8 kernel does -- the K-tile's 64 MFMAs run by quadrant
+// (A0-3 x B0-3, A4-7 x B0-3, A0-3 x B4-7, A4-7 x B4-7) and each fragment is reloaded once its quadrants are done:
+// this tile's A4-7 / B4-7 at the start of the K-tile, the next tile's B0-3 / A0-3 at its end.
+struct V4F8Frags {
+  u32x4 alo[8], ahi[8], blo[8], bhi[8];
+};
+
+__device__ __forceinline__ void v4_mfma8(floatx4& acc, const u32x4& alo, const u32x4& ahi, const u32x4& blo,
+                                         const u32x4& bhi) {
+  const i32x8 a = __builtin_bit_cast(i32x8, __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7));
+  const i32x8 b = __builtin_bit_cast(i32x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
+  asm volatile("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void v4_mfma8_first(floatx4& acc, const u32x4& alo, const u32x4& ahi, const u32x4& blo,
+                                               const u32x4& bhi) {
+  const i32x8 a = __builtin_bit_cast(i32x8, __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7));
+  const i32x8 b = __builtin_bit_cast(i32x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
+  asm volatile("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+}
+template <int OFF>
+__device__ __forceinline__ void v4_read4(u32x4& f, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(addr), "i"(OFF));
+}
+// fp8 read id r: 0-7 this tile's A blocks 4-7 (block 4 + r / 2, chunk half r % 2), 8-15 its B blocks 4-7, 16-23 the
+// next tile's A blocks 0-3, 24-31 its B blocks 0-3.  ha / hb: the per-lane addresses of [half] in the stage read.
+template <int R>
+__device__ __forceinline__ void v4_piece8(V4F8Frags& g, const uint32_t (&ha)[2], const uint32_t (&hb)[2]) {
+  constexpr int q = R & 15, blk = (R < 16 ? 4 : 0) + (q & 7) / 2, h = q & 1;
+  constexpr bool is_b = q >= 8;
+  if constexpr (!is_b) v4_read4<blk * 2048>(h ? g.ahi[blk] : g.alo[blk], ha[h]);
+  else v4_read4<blk * 2048>(h ? g.bhi[blk] : g.blo[blk], hb[h]);
+}
+// fp8 slot i (0-63) -> output block: quadrant q = i / 16 in the order (A0-3, B0-3), (A4-7, B0-3), (A0-3, B4-7),
+// (A4-7, B4-7)
+constexpr int v4f8_m(int i) { return ((i >> 4) & 1) * 4 + ((i & 15) >> 2); }
+constexpr int v4f8_n(int i) { return ((i >> 4) >> 1) * 4 + (i & 3); }
+
+// fp8 plan: this tile's A4-7 reads in slots 0-7, barrier X1 at X1, its B4-7 reads in X1+1 .. X1+8 with the A-operand
+// DMAs every second slot from DA, barrier X2 at X2, the B-operand DMAs every second slot from DB, barrier Y at Y
+// (vmcnt: the previous K-tile's DMAs), then the next tile's B0-3 and (from slot 48, after their last use) A0-3
+template <int X1, int DA, int X2, int DB, int Y>
+struct V4PlanF8 {
+  static constexpr int at_dma(int i) {
+    if (i >= DA && i < DA + 16 && (i - DA) % 2 == 0) return (i - DA) / 2;
+    if (i >= DB && i < DB + 16 && (i - DB) % 2 == 0) return 8 + (i - DB) / 2;
+    return -1;
+  }
+  static constexpr V4Slot at(int i) {
+    V4Slot o;
+    if (i < 8) o.read = i;                                 // this tile's A4-7
+    if (i > X1 && i <= X1 + 8) o.read = 8 + (i - X1 - 1);  // this tile's B4-7
+    if (i > Y && i <= Y + 8) o.read = 24 + (i - Y - 1);    // next tile's B0-3
+    const int a0 = (Y + 9 > 48 ? Y + 9 : 48);
+    if (i >= a0 && i < a0 + 8) o.read = 16 + (i - a0);     // next tile's A0-3
+    if (i == X1 || i == X2) o.wait = 1;
+    if (i == Y) {
+      o.wait = 2;
+      for (int k = 0; k < Y; ++k)
+        if (at_dma(k) >= 0) ++o.vm;
+    }
+    o.dma = at_dma(i);
+    return o;
+  }
+};
+
+// the fp8 plan rules (slot i: MFMA, read, wait, DMA): this tile's A4-7 / B4-7 reads retired by an lgkmcnt barrier
+// before their first MFMA (slot 16 / 32) and before any DMA into their operand's region; the next tile's reads
+// after the vmcnt barrier and no earlier than the last MFMA of the fragment they replace (B0-3: 31, A0-3: 47)
+template <class P>
+constexpr bool v4f8_plan_ok() {
+  int read_at[32] = {}, dma_at[16] = {}, lgk[64] = {}, nb = 0, vm_at = -1, vm = -1;
+  for (int k = 0; k < 32; ++k) read_at[k] = -1;
+  for (int k = 0; k < 16; ++k) dma_at[k] = -1;
+  for (int i = 0; i < 64; ++i) {
+    const V4Slot o = P::at(i);
+    if (o.read >= 0) {
+      if (o.read > 31 || read_at[o.read] >= 0) return false;
+      read_at[o.read] = i;
+    }
+    if (o.wait == 1) lgk[nb++] = i;
+    if (o.wait == 2) {
+      if (vm_at >= 0) return false;
+      vm_at = i;
+      vm = o.vm;
+    }
+    if (o.dma >= 0) {
+      if (o.dma > 15 || dma_at[o.dma] >= 0) return false;
+      dma_at[o.dma] = i;
+    }
+  }
+  if (vm_at < 0) return false;
+  int issued = 0;
+  for (int k = 0; k < 16; ++k) {
+    if (dma_at[k] < 0) return false;
+    issued += dma_at[k] < vm_at;
+  }
+  if (issued != vm) return false;
+  for (int op = 0; op < 2; ++op) {
+    int last = -1;
+    for (int k = op * 8; k < op * 8 + 8; ++k) last = read_at[k] > last ? read_at[k] : last;
+    int b = -1;
+    for (int x = 0; x < nb && b < 0; ++x)
+      if (lgk[x] >= last) b = lgk[x];
+    if (last < 0 || b < 0 || b >= (op ? 32 : 16)) return false;
+    for (int j = op * 8; j < op * 8 + 8; ++j)
+      if (dma_at[j] <= b) return false;
+  }
+  for (int k = 16; k < 32; ++k)
+    if (read_at[k] <= vm_at || read_at[k] < (k < 24 ? 47 : 31)) return false;
+  return true;
+}
+
+template <int OUT = OUT_F32, class PLAN = V4PlanA<1, 20, 8, 8, 2>, int GM = 4, bool TR = false, int DT = DT_BF16>
 __global__ void __launch_bounds__(V4_THREADS, 1)
 gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv,
                double* __restrict__ csum, int M, int N, int K) {
-  static_assert(X_AT >= 16 * RS - 1 && Y_AT + 16 * R2 < 64 && D1 >= 0 && D1 <= 16, "schedule out of range");
+  constexpr bool FP8 = DT == DT_FP8U;
+  static_assert(DT == DT_BF16 || DT == DT_FP8U, "v4: bf16 or fp8 (unscaled MFMA)");
+  if constexpr (FP8) static_assert(v4f8_plan_ok<PLAN>(), "v4 fp8 plan breaks a read / DMA / barrier ordering rule");
+  else static_assert(v4_plan_ok<PLAN>(), "v4 schedule plan breaks a read / DMA / barrier ordering rule");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages x 64 KiB
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the DMA's m0 is an SGPR
@@ -853,22 +1117,30 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
   const __bf16* Bb = Bt + static_cast<size_t>(tn) * V2_BN * K;
   const int KT = K / BK;
 
-  // LDS-DMA: wave instruction j (0-15) of a tile: operand j >> 3, rows wid * 64 + (j & 7) * 8 + 0..7 (lane: row +
-  // (lane >> 3), physical chunk lane & 7, source chunk XOR-swizzled by row; the swizzle depends on the row's bit
-  // 3, i.e. on (j & 1): two per-lane offsets), the rest scalar: soffset = kt * 128 + (j & 7) * 8 * K * 2
+  // LDS-DMA: wave instruction j (0-15) of a tile: operand j >> 3, rows wid * 64 + 8r + 0..7 with r = j & 7 (lane:
+  // row + (lane >> 3), physical chunk lane & 7, source chunk XOR-swizzled by row: one VGPR offset per r), LDS
+  // address m0 = the wave's base + an immediate per (stage, j), and the tile's column offset kt * 128 as soffset:
+  // two instructions per DMA (s_add_u32 m0 + the load), as hipBLASLt issues them.  The K loop is unrolled by two so
+  // the stage's addresses are immediates; that and the lean DMA issue were worth +2.5 % at 4096^3 and +4.7 % at
+  // 8192^3 over a loop that selected them per K-tile (profiles/gemm_w4a_lab_mi355x.jsonl): with one wave per SIMD
+  // every instruction between MFMAs costs issue cycles.
   const i32x4 rs_a = v4_rsrc(Ab, static_cast<uint32_t>(V2_BM) * K * 2);
   const i32x4 rs_b = v4_rsrc(Bb, static_cast<uint32_t>(V2_BN) * K * 2);
-  const int rsub = lane >> 3, phys = lane & 7;
-  const int row_e = wid * 64 + rsub;
-  const uint32_t voff_e = (row_e * K + (phys ^ swz_row_xor(row_e, false)) * 8) * 2;
-  const uint32_t voff_o = (row_e * K + (phys ^ swz_row_xor(row_e + 8, false)) * 8) * 2;
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
   const uint32_t m0_wave = lds0 + wid * 64 * (BK * 2);
-  const uint32_t row8 = 8u * K * 2;
-  auto dma = [&](uint32_t stage_off, int kt, int j) {
-    const int op = j >> 3, r = j & 7;
-    v4_dma(m0_wave + stage_off + op * (V2_BM * BK * 2) + r * 8 * (BK * 2), (r & 1) ? voff_o : voff_e,
-           op ? rs_b : rs_a, static_cast<uint32_t>(kt) * (BK * 2) + r * row8);
+  uint32_t voff_r[8];
+  {
+    const int rsub = lane >> 3, phys = lane & 7;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int row = wid * 64 + 8 * r + rsub;
+      voff_r[r] = static_cast<uint32_t>((row * K + (phys ^ swz_row_xor(row, FP8)) * 8) * 2);
+    }
+  }
+  auto dma = [&](auto S, auto J, uint32_t soff) {
+    constexpr int s = decltype(S)::value, j = decltype(J)::value, op = j >> 3, r = j & 7;
+    v4_dma_imm<s * V2_STAGE_BYTES + op * (V2_BM * BK * 2) + r * 8 * (BK * 2)>(m0_wave, voff_r[r], op ? rs_b : rs_a,
+                                                                                soff);
   };
 
   // fragment reads: lane (frow, fq); k-step 1 is chunk ^ 4
@@ -883,52 +1155,201 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
       rb[s][ks] = lds0 + s * V2_STAGE_BYTES + V2_BM * BK * 2 + (wc * 128 + frow) * (BK * 2) + c;
     }
 
-  floatx4 acc[8][8];
+  // fp8: per-lane address of chunk half h (chunk 2 fq + h, swizzled by the row's bits 1 and 3) in each stage
+  uint32_t ra8[2][2], rb8[2][2];
+  if constexpr (FP8) {
+    const int x8 = swz_row_xor(frow, true);
 #pragma unroll
-  for (int m = 0; m < 8; ++m)
+    for (int st = 0; st < 2; ++st)
 #pragma unroll
-    for (int n = 0; n < 8; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t c = static_cast<uint32_t>(((2 * fq + h) ^ x8) * 16);
+        ra8[st][h] = lds0 + st * V2_STAGE_BYTES + (wr * 128 + frow) * (BK * 2) + c;
+        rb8[st][h] = lds0 + st * V2_STAGE_BYTES + V2_BM * BK * 2 + (wc * 128 + frow) * (BK * 2) + c;
+      }
+  }
 
+  floatx4 acc[8][8];  // written first by the first K-tile's first MFMAs (v4_mfma_first / v4_mfma8_first)
+
+  [[maybe_unused]] uint64_t st_k0 = 0, st_l0 = 0, st_l1 = 0, st_i0 = 0, st_i1 = 0, st_x = 0, st_y = 0, st_e = 0;
+  if constexpr (kV4Stamps) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_k0)::"memory");
   // prologue: tiles 0 and 1 into stages 0 and 1, tile 0 waited for, F0 of tile 0 read
-  v4_for<0, 16>([&](auto j) { dma(0, 0, j); });
-  v4_for<0, 16>([&](auto j) { dma(V2_STAGE_BYTES, KT > 1 ? 1 : 0, j); });
+  v4_for<0, 16>([&](auto j) { dma(std::integral_constant<int, 0>{}, j, 0u); });
+  v4_for<0, 16>([&](auto j) { dma(std::integral_constant<int, 1>{}, j, KT > 1 ? BK * 2u : 0u); });
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   STG_BARRIER();
-  V4Frags f0, f1;
-  v4_for<0, 16>([&](auto p) { v4_piece<p>(f0, ra[0][0], rb[0][0]); });
+  [[maybe_unused]] V4Frags f0, f1;
+  [[maybe_unused]] V4F8Frags g;
+  if constexpr (FP8) v4_for<16, 32>([&](auto r) { v4_piece8<r>(g, ra8[0], rb8[0]); });  // tile 0's A0-3, B0-3
+  else v4_for<0, 16>([&](auto p) { v4_piece<p>(f0, ra[0][0], rb[0][0]); });
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (kV4Stamps) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_l0)::"memory");
 
-  for (int kt = 0; kt < KT; ++kt) {
-    const int s = kt & 1;
-    const uint32_t stage_off = s ? V2_STAGE_BYTES : 0;
-    const uint32_t a1 = s ? ra[1][1] : ra[0][1], b1 = s ? rb[1][1] : rb[0][1];
-    const uint32_t a0n = s ? ra[0][0] : ra[1][0], b0n = s ? rb[0][0] : rb[1][0];
-    const int kd = min(kt + 2, KT - 1);
-    constexpr int SP1 = D1 > 0 ? (63 - X_AT) / D1 : 1;  // MFMAs per DMA piece after X
-    v4_for<0, 64>([&](auto i) {
-      v4_mfma(acc[i >> 3][i & 7], f0.a[i >> 3], f0.b[i & 7]);
-      if constexpr (i % RS == RS - 1 && i / RS < 16) v4_piece<i / RS>(f1, a1, b1);
-      if constexpr (i == X_AT) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if constexpr (i > X_AT && (i - X_AT) % SP1 == 0 && (i - X_AT) / SP1 - 1 < D1)
-        dma(stage_off, kd, (i - X_AT) / SP1 - 1);
+  // one K-tile kt in stage S (= kt & 1)
+  auto iter = [&](auto S, auto FIRST, int kt) {
+    constexpr int s = decltype(S)::value;
+    constexpr bool first = decltype(FIRST)::value;  // K-tile 0: its k-step-0 MFMAs start the accumulators
+    [[maybe_unused]] const uint32_t a1 = ra[s][1], b1 = rb[s][1], a0n = ra[s ^ 1][0], b0n = rb[s ^ 1][0];
+    const uint32_t soff = static_cast<uint32_t>(min(kt + 2, KT - 1)) * (BK * 2);  // the tile the DMAs fetch
+    [[maybe_unused]] const bool stamp = kV4Stamps && kt == KT / 2;
+    if constexpr (kV4Stamps) {
+      if (kt == KT / 2) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_i0)::"memory");
+      if (kt == KT / 2 + 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_i1)::"memory");
+    }
+    v4_for<0, FP8 ? 64 : 128>([&](auto i) {
+      constexpr V4Slot o = PLAN::at(i);
+      if constexpr (FP8) {
+        constexpr int m = v4f8_m(i), n = v4f8_n(i);
+        floatx4& c = acc[m][n];
+        if constexpr (first) {
+          if constexpr (TR) v4_mfma8_first(c, g.blo[n], g.bhi[n], g.alo[m], g.ahi[m]);
+          else v4_mfma8_first(c, g.alo[m], g.ahi[m], g.blo[n], g.bhi[n]);
+        } else {
+          if constexpr (TR) v4_mfma8(c, g.blo[n], g.bhi[n], g.alo[m], g.ahi[m]);
+          else v4_mfma8(c, g.alo[m], g.ahi[m], g.blo[n], g.bhi[n]);
+        }
+        if constexpr (o.read >= 0 && o.read < 16) v4_piece8<o.read>(g, ra8[s], rb8[s]);
+        if constexpr (o.read >= 16) v4_piece8<o.read>(g, ra8[s ^ 1], rb8[s ^ 1]);
+      } else {
+        const V4Frags& f = i < 64 ? f0 : f1;
+        floatx4& c = acc[(i & 63) >> 3][i & 7];
+        const bf16x8& fa = f.a[(i & 63) >> 3];
+        const bf16x8& fb = f.b[i & 7];
+        if constexpr (first && i < 64) {
+          if constexpr (TR) v4_mfma_first(c, fb, fa);
+          else v4_mfma_first(c, fa, fb);
+        } else {
+          if constexpr (TR) v4_mfma(c, fb, fa);
+          else v4_mfma(c, fa, fb);
+        }
+        if constexpr (o.read >= 0 && o.read < 16) v4_piece<o.read>(f1, a1, b1);
+        if constexpr (o.read >= 16) v4_piece<o.read - 16>(f0, a0n, b0n);
+      }
+      if constexpr (o.wait == 1) {
+        if (stamp) {
+          uint64_t t0, t1;
+          asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)"
+                       : "=s"(t0), "=s"(t1)::"memory");
+          st_x += t1 - t0;
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+      }
+      if constexpr (o.wait == 2) {
+        if (stamp) {
+          uint64_t t0, t1;
+          asm volatile("s_memtime %0\n\ts_waitcnt vmcnt(%2)\n\ts_barrier\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)"
+                       : "=s"(t0), "=s"(t1)
+                       : "i"(o.vm)
+                       : "memory");
+          st_y = t1 - t0;
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(o.vm) : "memory");
+        }
+      }
+      if constexpr (o.dma >= 0) dma(S, std::integral_constant<int, o.dma>{}, soff);
     });
-    constexpr int D2 = 16 - D1;
-    constexpr int SP2 = D2 > 0 ? (63 - Y_AT) / D2 : 1;
-    v4_for<0, 64>([&](auto i) {
-      v4_mfma(acc[i >> 3][i & 7], f1.a[i >> 3], f1.b[i & 7]);
-      if constexpr (i == Y_AT) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(D1) : "memory");
-      if constexpr (i > Y_AT && (i - Y_AT - 1) % R2 == 0 && (i - Y_AT - 1) / R2 < 16)
-        v4_piece<(i - Y_AT - 1) / R2>(f0, a0n, b0n);
-      if constexpr (D2 > 0 && i > Y_AT && (i - Y_AT) % SP2 == 0 && (i - Y_AT) / SP2 - 1 < D2)
-        dma(stage_off, kd, D1 + (i - Y_AT) / SP2 - 1);
-    });
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (stamp) {
+      uint64_t t0, t1;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)"
+                   : "=s"(t0), "=s"(t1)::"memory");
+      st_e = t1 - t0;
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  iter(I0{}, std::true_type{}, 0);
+  int kt = 1;
+  for (; kt + 1 < KT; kt += 2) {
+    iter(I1{}, std::false_type{}, kt);
+    iter(I0{}, std::false_type{}, kt + 1);
   }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (kt < KT) iter(I1{}, std::false_type{}, kt);
+  // drain; the s_nops are the wait states between the last MFMA's result and the epilogue's v_accvgpr_read, which
+  // hipcc's hazard recognizer cannot insert for an MFMA written in asm
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  if constexpr (kV4Stamps) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_l1)::"memory");
+#ifdef DIAG_V4_STAMPS
+  // after the epilogue's stores (below) the last stamp; written here by a lambda run at the end
+  auto write_stamps = [&] {
+    uint64_t t;
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    if (lane == 0 && blockIdx.x < 4096) {
+      unsigned long long* o = g_v4_stamps[blockIdx.x][wid];
+      o[0] = st_l0 - st_k0;
+      o[1] = st_l1 - st_l0;
+      o[2] = t - st_l1;
+      o[3] = st_i1 - st_i0;
+      o[4] = st_x;
+      o[5] = st_y;
+      o[6] = st_e;
+      o[7] = KT;
+    }
+  };
+#endif
 
-  // epilogue through each wave's own LDS patch (16 rows x 128 columns of fp32), as v3's
   const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 128;
+  if constexpr (TR) {
+    // Transposed blocks (the B fragment is the MFMA's first operand): lane (frow, fq) of block (m, n) holds row
+    // m * 16 + frow, columns n * 16 + 4 * fq + 0..3 -- row pieces, stored straight from registers, no LDS.
+    if constexpr (OUT == OUT_BF16_CK) {
+      // column sums over the wave's 128 rows: 32 per lane (its 4 columns of 8 blocks) summed over m, then over
+      // the 16 lanes holding the same columns by recursive halving (each step keeps half the columns and adds the
+      // partner lane's half: 16 + 8 + 4 + 2 exchanged sums); lane frow ends with columns 2 * frow, 2 * frow + 1
+      // of its 32 (index c = n * 4 + j)
+      double s[32];
+#pragma unroll
+      for (int c = 0; c < 32; ++c) {
+        s[c] = 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) s[c] += static_cast<double>(acc[m][c >> 2][c & 3]);
+      }
+      v4_halve<16, 0x140>(s, (frow >> 3) & 1);  // row_mirror: lane i <-> 15 - i (differs in bit 3)
+      v4_halve<8, 0x141>(s, (frow >> 2) & 1);   // row_half_mirror: i <-> 7 - i within 8 (bit 2)
+      v4_halve<4, 0x4E>(s, (frow >> 1) & 1);    // quad_perm [2,3,0,1]: xor 2
+      v4_halve<2, 0xB1>(s, frow & 1);           // quad_perm [1,0,3,2]: xor 1
+      const int c0 = 2 * frow;  // columns n * 16 + 4 * fq + j for c = c0, c0 + 1: adjacent
+      double2 v;
+      v.x = s[0];
+      v.y = s[1];
+      *reinterpret_cast<double2*>(csum + static_cast<size_t>(row0 / 128) * N + col0 + (c0 >> 2) * 16 + 4 * fq +
+                                  (c0 & 3)) = v;
+      // bf16 C: block pair (2p, 2p+1) packed to 2 dwords each, then v_permlane16_swap between the 16-lane rows
+      // fq even / odd: even rows end with columns 32p + 4fq + 0..7, odd rows with 32p + 16 + 4(fq - 1) + 0..7
+      __bf16* __restrict__ Cb = static_cast<__bf16*>(Cv);
+      const int cofs = (fq & 1) * 16 + (fq >> 1) * 8;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+          u32x2 lo = __builtin_bit_cast(u32x2, __builtin_convertvector(acc[m][2 * p], bf16x4));
+          u32x2 hi = __builtin_bit_cast(u32x2, __builtin_convertvector(acc[m][2 * p + 1], bf16x4));
+          const auto x = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
+          const auto y = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
+          const u32x4 out = {x[0], y[0], x[1], y[1]};
+          *reinterpret_cast<u32x4*>(Cb + static_cast<size_t>(row0 + m * 16 + frow) * N + col0 + p * 32 + cofs) = out;
+        }
+      }
+    } else {
+      float* __restrict__ C = static_cast<float*>(Cv);
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 8; ++n)
+          *reinterpret_cast<floatx4*>(C + static_cast<size_t>(row0 + m * 16 + frow) * N + col0 + n * 16 + 4 * fq) =
+              acc[m][n];
+    }
+#ifdef DIAG_V4_STAMPS
+    write_stamps();
+#endif
+    return;
+  }
+  // epilogue through each wave's own LDS patch (16 rows x 128 columns of fp32), as v3's
   constexpr int LD = 128 + 4;
   float* patch = reinterpret_cast<float*>(smem) + wid * (16 * LD);
   if constexpr (OUT == OUT_BF16_CK) {
@@ -983,6 +1404,9 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
       }
     }
   }
+#ifdef DIAG_V4_STAMPS
+  write_stamps();
+#endif
 }
 
 // fp32 reference for sampled outputs: one thread per (row, col) sample.
@@ -1567,16 +1991,38 @@ int launch_v3_ck_fp8(const void* A, const void* Bt, __bf16* C, double* csum, int
 }
 
 // v4 launch (bf16; M, N multiples of 256, K of 64): fp32 C, or bf16 C + fused column sums (OUT_BF16_CK)
-template <int OUT>
-int launch_v4(const void* A, const void* Bt, void* C, double* csum, int M, int N, int K, hipStream_t stream) {
+template <int OUT, bool TR, int DT>
+int launch_v4_inst(const void* A, const void* Bt, void* C, double* csum, int M, int N, int K, hipStream_t stream) {
+  using Plan = std::conditional_t<DT == DT_FP8U, V4PlanF8<8, 10, 26, 27, 42>, V4PlanA<1, 20, 8, 8, 2>>;
+  constexpr auto kern = gemm_v4_kernel<OUT, Plan, 4, TR, DT>;
   static LdsAttrOnce attr;
-  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_v4_kernel<OUT>), 2 * V2_STAGE_BYTES, "gemm v4") !=
-      0)
-    return -1;
+  if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(kern), 2 * V2_STAGE_BYTES, "gemm v4") != 0) return -1;
   const int nwg = (M / V2_BM) * (N / V2_BN);
-  hipLaunchKernelGGL((gemm_v4_kernel<OUT>), dim3(nwg), dim3(V4_THREADS), 2 * V2_STAGE_BYTES, stream,
-                     static_cast<const __bf16*>(A), static_cast<const __bf16*>(Bt), C, csum, M, N, K);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(V4_THREADS), 2 * V2_STAGE_BYTES, stream, static_cast<const __bf16*>(A),
+                     static_cast<const __bf16*>(Bt), C, csum, M, N, K);
   return 0;
+}
+// v4 with the LDS-patch epilogue (variant 4) or the transposed, register-direct one (variant 5); K in bf16 columns
+// (fp8: row bytes / 2)
+template <int OUT, int DT = DT_BF16>
+int launch_v4(int variant, const void* A, const void* Bt, void* C, double* csum, int M, int N, int K,
+              hipStream_t stream) {
+  return variant == 5 ? launch_v4_inst<OUT, true, DT>(A, Bt, C, csum, M, N, K, stream)
+                      : launch_v4_inst<OUT, false, DT>(A, Bt, C, csum, M, N, K, stream);
+}
+
+// The fp8 kernel the calling thread's knobs select: v4 (4 or 5) for auto / v4 / v4t with the unscaled MFMA, else v3
+int fp8_variant() {
+  const int v = g_gemm_variant == 0 ? 4 : g_gemm_variant;
+  return v >= 4 && g_gemm_fp8_unscaled ? v : 3;
+}
+
+// fp8 bf16 C + fused column sums on the selected kernel (Kcols = row bytes / 2)
+int launch_fp8_ck(const void* A, const void* Bt, __bf16* C, double* csum, int M, int N, int Kcols,
+                  hipStream_t stream) {
+  const int v = fp8_variant();
+  return v >= 4 ? launch_v4<OUT_BF16_CK, DT_FP8U>(v, A, Bt, C, csum, M, N, Kcols, stream)
+                : launch_v3_ck_fp8(A, Bt, C, csum, M, N, Kcols, stream);
 }
 
 // The diagnostic runs (diag_gemm_*_x) take the bf16-output kernel wherever the production v3 configuration
@@ -1608,14 +2054,15 @@ int bf16_variant(int M, int N) {
 
 // the bf16 launch with bf16 C + fused column sums: v4 when the thread's variant resolves to it, else v3
 int launch_bf16_ck(const void* A, const void* Bt, __bf16* C, double* csum, int M, int N, int K, hipStream_t stream) {
-  return bf16_variant(M, N) == 4 ? launch_v4<OUT_BF16_CK>(A, Bt, C, csum, M, N, K, stream)
-                                 : launch_v3_ck<DT_BF16>(A, Bt, C, csum, M, N, K, stream);
+  const int v = bf16_variant(M, N);
+  return v >= 4 ? launch_v4<OUT_BF16_CK>(v, A, Bt, C, csum, M, N, K, stream)
+                : launch_v3_ck<DT_BF16>(A, Bt, C, csum, M, N, K, stream);
 }
 
 // diag_gemm_bf16_x writes bf16 C with fused column sums (else fp32 C)
 bool bf16_fused(int M, int N) {
   const int v = bf16_variant(M, N);
-  return v == 4 || (v == 3 && v3_ck_path());
+  return v >= 4 || (v == 3 && v3_ck_path());
 }
 
 // Output tiles of a launch and their blockIdx regrouping (the mapping at the top of every GEMM kernel).
@@ -1775,8 +2222,9 @@ extern "C" {
 const char* diag_last_error(void) { return g_err.c_str(); }
 
 // 0 = auto (bf16: v4 four-wave 256x256 tiles when M, N are multiples of 256 and the grid fills the chip, else
-// v1), 1 = force v1 (128x128 register-staged), 2 = force v2, 3 = force v3 (8 waves, staggered), 4 = force v4.
-// fp8 / fp4 GEMMs run v3 whatever this says.
+// v1), 1 = force v1 (128x128 register-staged), 2 = force v2, 3 = force v3 (8 waves, staggered), 4 = force v4,
+// 5 = v4 with the transposed register-direct epilogue.  fp8: auto / 4 / 5 run v4 on the unscaled MFMA (the MX form,
+// fp8_unscaled = 0, and 1-3 run v3); fp4 always runs v3.
 void diag_set_gemm_variant(int v) { g_gemm_variant = v; }
 void diag_set_gemm_epilogue(int e) { g_gemm_epilogue = e; }
 void diag_set_gemm_buffer_loads(int b) { g_gemm_buffer_loads = b; }
@@ -1821,13 +2269,13 @@ int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N,
     return -2;
   }
   const int variant = bf16_variant(M, N);
-  if (variant >= 2 && variant <= 4) {
+  if (variant >= 2 && variant <= 5) {
     if (M % V2_BM || N % V2_BN) {
-      g_err = "gemm_bf16 v2-v4: M, N must be multiples of 256";
+      g_err = "gemm_bf16 v2-v5: M, N must be multiples of 256";
       return -2;
     }
-    if (variant == 4) {
-      if (launch_v4<OUT_F32>(A, Bt, C, nullptr, M, N, K, static_cast<hipStream_t>(stream)) != 0) return -1;
+    if (variant >= 4) {
+      if (launch_v4<OUT_F32>(variant, A, Bt, C, nullptr, M, N, K, static_cast<hipStream_t>(stream)) != 0) return -1;
     } else if (variant == 2) {
       static LdsAttrOnce attr;
       if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_bf16_v2_kernel), 2 * V2_STAGE_BYTES,
@@ -1856,8 +2304,11 @@ int diag_gemm_fp8_launch(const void* A, const void* Bt, float* C, int M, int N, 
     g_err = "gemm_fp8: M, N must be multiples of 256 and K a multiple of 128";
     return -2;
   }
-  if ((g_gemm_fp8_unscaled ? launch_v3<DT_FP8U>(A, Bt, C, M, N, K / 2, static_cast<hipStream_t>(stream))
-                           : launch_v3<DT_FP8>(A, Bt, C, M, N, K / 2, static_cast<hipStream_t>(stream))) != 0)
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  const int v = fp8_variant();
+  if ((v >= 4 ? launch_v4<OUT_F32, DT_FP8U>(v, A, Bt, C, nullptr, M, N, K / 2, st)
+       : g_gemm_fp8_unscaled ? launch_v3<DT_FP8U>(A, Bt, C, M, N, K / 2, st)
+                             : launch_v3<DT_FP8>(A, Bt, C, M, N, K / 2, st)) != 0)
     return -1;
   DIAG_CHECK(hipGetLastError());
   return 0;
@@ -1890,7 +2341,7 @@ int diag_gemm_launch_ck(int dt, const void* A, const void* Bt, void* C, double* 
     return -2;
   }
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  const int rc = dt == DT_FP8 ? launch_v3_ck_fp8(A, Bt, static_cast<__bf16*>(C), csum, M, N, K / 2, st)
+  const int rc = dt == DT_FP8 ? launch_fp8_ck(A, Bt, static_cast<__bf16*>(C), csum, M, N, K / 2, st)
                               : launch_bf16_ck(A, Bt, static_cast<__bf16*>(C), csum, M, N, K, st);
   if (rc != 0) return -1;
   DIAG_CHECK(hipGetLastError());
@@ -1900,7 +2351,7 @@ int diag_gemm_launch_ck(int dt, const void* A, const void* Bt, void* C, double* 
 // 1 when diag_gemm_bf16_x (dt 0) / diag_gemm_fp8_x (dt 1) at M x N would time the bf16-output kernel with fused
 // column sums under the calling thread's knobs, 0 when it would write fp32 C
 int diag_gemm_ck_path(int dt, int M, int N) {
-  return (dt == DT_FP8 ? v3_ck_path() : bf16_fused(M, N)) ? 1 : 0;
+  return (dt == DT_FP8 ? fp8_variant() >= 4 || v3_ck_path() : bf16_fused(M, N)) ? 1 : 0;
 }
 
 // Self-contained MFMA burn-in: allocate, fill, run `iters` GEMMs, time them, verify `nsamp` sampled outputs
@@ -2018,7 +2469,7 @@ int diag_gemm_fp8_x(int device, int M, int N, int K, int warmup, int iters, int 
     return -2;
   }
   DIAG_CHECK(hipSetDevice(device));
-  const bool fused = v3_ck_path();  // bf16 C + the kernel's own column sums (OUT_BF16_CK)
+  const bool fused = fp8_variant() >= 4 || v3_ck_path();  // bf16 C + the kernel's own column sums (OUT_BF16_CK)
   DevBuf A, Bt, C, ref, mag, rows, cols, got, bcs;
   DIAG_CHECK(A.alloc(device, static_cast<size_t>(M) * K));
   DIAG_CHECK(Bt.alloc(device, static_cast<size_t>(N) * K));
@@ -2026,7 +2477,7 @@ int diag_gemm_fp8_x(int device, int M, int N, int K, int warmup, int iters, int 
   if (fused) DIAG_CHECK(bcs.alloc(device, sizeof(double) * static_cast<size_t>(M / 128) * N));
   double* cs = static_cast<double*>(bcs.ptr);
   auto run = [&]() -> int {
-    return fused ? launch_v3_ck_fp8(A.ptr, Bt.ptr, static_cast<__bf16*>(C.ptr), cs, M, N, K / 2, nullptr)
+    return fused ? launch_fp8_ck(A.ptr, Bt.ptr, static_cast<__bf16*>(C.ptr), cs, M, N, K / 2, nullptr)
                  : diag_gemm_fp8_launch(A.ptr, Bt.ptr, static_cast<float*>(C.ptr), M, N, K, nullptr);
   };
   DIAG_CHECK(ref.alloc(device, sizeof(double) * nsamp));

@@ -305,7 +305,7 @@ def device_info(device: int = 0) -> Dict[str, Any]:
     return {"arch": arch, "name": name, "cus": int(cus), "mem_bytes": int(mem), "bdf": bdf}
 
 
-GEMM_VARIANTS = {"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v4": 4}
+GEMM_VARIANTS = {"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v4": 4, "v4t": 5}
 
 
 def set_gemm_variant(variant: str = "auto") -> None:

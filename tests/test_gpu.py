@@ -125,7 +125,7 @@ def test_mfma_gemm_matches_fp32_reference(dev, m, n, k):
     assert rel < 1e-4 * max(1, k / 512), rel
 
 
-@pytest.mark.parametrize("variant", ["v1", "v2", "v3", "v3-lds-epilogue", "v4"])
+@pytest.mark.parametrize("variant", ["v1", "v2", "v3", "v3-lds-epilogue", "v4", "v4t"])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (768, 512, 256),
                                    (1024, 768, 4096)])
 def test_mfma_gemm_variants_match_fp32_reference(dev, variant, m, n, k):
@@ -311,16 +311,17 @@ def test_mfma_gemm_large_auto_uses_v4_and_matches(dev):
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (768, 512, 320),
                                    (1024, 768, 4096), (2048, 2048, 2048), (4096, 4096, 1024)])
 def test_v4_gemm_is_bit_identical_to_v3(dev, m, n, k):
-    """The four-wave v4 kernel (asm-ordered loop, 128x128 per wave) accumulates in v3's K order: fp32 C, bf16 C and
-    the fused column sums all equal v3's bit for bit, over 1-64 K-tiles (the prologue, the re-fetch of the last tile
-    and the stale final fragment reads) and non-square grids; and it matches torch."""
+    """The four-wave v4 kernels (asm-ordered loop, 128x128 per wave; ``v4t`` with the MFMA operands swapped so the
+    accumulators hold row pieces, stored without LDS) accumulate in v3's K order: fp32 C and bf16 C equal v3's bit
+    for bit, over 1-64 K-tiles (the prologue, the re-fetch of the last tile and the stale final fragment reads) and
+    non-square grids; the fused column sums are v3's (v4: bitwise; v4t sums in another order: to fp64 rounding)."""
     from k8s_gpu_node_checker_amd.ops import diag
     g = torch.Generator(device=dev).manual_seed(m + 3 * n + 17 * k)
     st = torch.cuda.current_stream().cuda_stream
     a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
     bt = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
     outs = {}
-    for variant in ("v3", "v4"):
+    for variant in ("v3", "v4", "v4t"):
         with diag.gemm_config(variant=variant):
             c32 = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
             diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c32.data_ptr(), m, n, k, st)
@@ -329,12 +330,48 @@ def test_v4_gemm_is_bit_identical_to_v3(dev, m, n, k):
             diag.gemm_launch_ck("bf16", a.data_ptr(), bt.data_ptr(), c16.data_ptr(), cs.data_ptr(), m, n, k, st)
             torch.cuda.synchronize()
             outs[variant] = (c32, c16, cs)
-    for x, y in zip(outs["v3"], outs["v4"]):
-        assert torch.equal(x, y)
-    c32, c16, cs = outs["v4"]
+    mag = outs["v3"][0].double().abs().view(m // 128, 128, n).sum(dim=1)
+    for variant in ("v4", "v4t"):
+        assert torch.equal(outs["v3"][0], outs[variant][0]), variant
+        assert torch.equal(outs["v3"][1], outs[variant][1]), variant
+        assert ((outs["v3"][2] - outs[variant][2]).abs() / mag).max().item() < 1e-14, variant
+    assert torch.equal(outs["v3"][2], outs["v4"][2])
+    c32, c16, cs = outs["v4t"]
     assert torch.equal(c16, c32.to(torch.bfloat16))
     ref = a.float() @ bt.float().t()
     assert ((c32 - ref).abs() / ref.abs().clamp_min(1.0)).max().item() < 1e-4 * max(1, k / 512)
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (256, 512, 256), (512, 256, 384), (768, 512, 640),
+                                   (1024, 768, 4096), (2048, 2048, 2048)])
+def test_v4_fp8_gemm_is_bit_identical_to_v3(dev, m, n, k):
+    """The four-wave fp8 kernel (quadrant-ordered 16x16x128 MFMAs, half the fragments reloaded per K-tile) issues the
+    same MFMA per output block and K-tile as v3's unscaled fp8 path: fp32 C, bf16 C and the fused column sums equal
+    v3's bit for bit over 1-32 K-tiles and non-square grids, within the fp8 error bound of an fp64 reference."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + 11 * n + 3 * k)
+    st = torch.cuda.current_stream().cuda_stream
+    x = torch.randn(m, k, device=dev, generator=g).to(torch.float8_e4m3fn)
+    y = torch.randn(n, k, device=dev, generator=g).to(torch.float8_e4m3fn)
+    outs = {}
+    for variant in ("v3", "v4", "v4t"):
+        with diag.gemm_config(variant=variant):
+            assert diag.lib().diag_gemm_ck_path(1, m, n) == 1
+            c32 = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+            diag.gemm_fp8_launch(x.data_ptr(), y.data_ptr(), c32.data_ptr(), m, n, k, st)
+            c16 = torch.full((m, n), float("nan"), device=dev, dtype=torch.bfloat16)
+            cs = torch.full((m // 128, n), float("nan"), device=dev, dtype=torch.float64)
+            diag.gemm_launch_ck("fp8", x.data_ptr(), y.data_ptr(), c16.data_ptr(), cs.data_ptr(), m, n, k, st)
+            torch.cuda.synchronize()
+            outs[variant] = (c32, c16, cs)
+    mag = outs["v3"][0].double().abs().view(m // 128, 128, n).sum(dim=1)
+    for variant in ("v4", "v4t"):
+        assert torch.equal(outs["v3"][0], outs[variant][0]), variant
+        assert torch.equal(outs["v3"][1], outs[variant][1]), variant
+        assert ((outs["v3"][2] - outs[variant][2]).abs() / mag).max().item() < 1e-14, variant
+    ref = x.double() @ y.double().t()
+    err = ((outs["v4"][0].double() - ref).abs() / (x.double().abs() @ y.double().abs().t()).clamp_min(1e-30)).max()
+    assert err.item() < diag.GEMM_FP8_MAX_ERR
 
 
 def test_v4_gemm_diagnostic_reports_bf16_output(dev):

@@ -45,21 +45,70 @@ double time_ms(L launch, int iters) {
   return ms / iters;
 }
 
-template <int RS, int X_AT, int D1, int Y_AT, int GM, int R2 = 2>
-void launch_w4a(const __bf16* A, const __bf16* Bt, float* C, int M, int N, int K) {
+template <class PLAN, int GM = 4, bool TR = false>
+void launch_plan(const __bf16* A, const __bf16* Bt, float* C, int M, int N, int K) {
   static bool once = [] {
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<OUT_F32, RS, X_AT, D1, Y_AT, GM, R2>),
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<OUT_F32, PLAN, GM, TR>),
                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     return true;
   }();
   (void)once;
-  hipLaunchKernelGGL((gemm_v4_kernel<OUT_F32, RS, X_AT, D1, Y_AT, GM, R2>), dim3((M / V2_BM) * (N / V2_BN)),
-                     dim3(V4_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C, nullptr, M, N, K);
+  hipLaunchKernelGGL((gemm_v4_kernel<OUT_F32, PLAN, GM, TR>), dim3((M / V2_BM) * (N / V2_BN)), dim3(V4_THREADS),
+                     2 * V2_STAGE_BYTES, nullptr, A, Bt, C, nullptr, M, N, K);
+}
+
+template <int RS, int X_AT, int D1, int Y_AT, int GM, int R2 = 2, bool TR = false>
+void launch_w4a(const __bf16* A, const __bf16* Bt, float* C, int M, int N, int K) {
+  launch_plan<V4PlanA<RS, X_AT, D1, Y_AT, R2>, GM, TR>(A, Bt, C, M, N, K);
 }
 
 }  // namespace
 
+#ifdef DIAG_V4_STAMPS
+// stamps mode (build with -DDIAG_V4_STAMPS -o tools/gemm_w4a_lab_stamps.bin): run the production v4 schedule at
+// M = N = size, K = k a few times and print, per stamp, the median / p10 / p90 over all waves of the last launch
+template <bool TR>
+int run_stamps(int size, int K) {
+  const int M = size, N = size;
+  __bf16 *A, *Bt;
+  float* C;
+  CK(hipMalloc(&A, sizeof(__bf16) * M * K));
+  CK(hipMalloc(&Bt, sizeof(__bf16) * N * K));
+  CK(hipMalloc(&C, sizeof(float) * M * N));
+  hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, A, (size_t)M * K, 7ULL);
+  hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, Bt, (size_t)N * K, 11ULL);
+  const double ms = time_ms([&] { launch_w4a<1, 20, 8, 8, 4, 2, TR>(A, Bt, C, M, N, K); }, 10);
+  CK(hipDeviceSynchronize());
+  const int nwg = (M / V2_BM) * (N / V2_BN);
+  std::vector<unsigned long long> h(static_cast<size_t>(4096) * 4 * 8);
+  CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_v4_stamps), h.size() * sizeof(unsigned long long)));
+  const char* names[7] = {"prologue", "k_loop", "epilogue", "mid_iter", "x_wait", "y_wait", "end_wait"};
+  printf("{\"mode\": \"stamps\", \"tr\": %d, \"M\": %d, \"N\": %d, \"K\": %d, \"ms\": %.4f, \"tflops\": %.1f",
+         TR ? 1 : 0, M, N, K, ms, 2.0 * M * N * (double)K / (ms * 1e-3) / 1e12);
+  for (int q = 0; q < 7; ++q) {
+    std::vector<double> v;
+    for (int b = 0; b < std::min(nwg, 4096); ++b)
+      for (int w = 0; w < 4; ++w) v.push_back(static_cast<double>(h[(static_cast<size_t>(b) * 4 + w) * 8 + q]));
+    std::sort(v.begin(), v.end());
+    printf(", \"%s\": [%.0f, %.0f, %.0f]", names[q], v[v.size() / 10], v[v.size() / 2], v[v.size() * 9 / 10]);
+  }
+  printf("}\n");
+  fflush(stdout);
+  CK(hipFree(A));
+  CK(hipFree(Bt));
+  CK(hipFree(C));
+  return 0;
+}
+#endif
+
 int main(int argc, char** argv) {
+#ifdef DIAG_V4_STAMPS
+  // stamps SIZE K: the production v4 schedule and its transposed-epilogue form
+  const int ssize = argc > 1 ? atoi(argv[1]) : 8192, sk = argc > 2 ? atoi(argv[2]) : 8192;
+  run_stamps<false>(ssize, sk);
+  run_stamps<true>(ssize, sk);
+  return 0;
+#endif
   std::vector<int> sizes = {4096, 8192};
   if (argc > 1) {
     sizes.clear();
@@ -95,16 +144,15 @@ int main(int argc, char** argv) {
     };
     std::vector<Row> rows;
     rows.push_back({"v3(diag,lds-epi)", [&] { launch_v3<DT_BF16>(A, Bt, C1, M, N, K, nullptr); }});
-    rows.push_back({"w4a rs1 x16 d8 y8", [&] { launch_w4a<1, 16, 8, 8, 4>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"w4a rs1 x16 d4 y8", [&] { launch_w4a<1, 16, 4, 8, 4>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"w4a rs1 x16 d12 y8", [&] { launch_w4a<1, 16, 12, 8, 4>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"w4a rs1 x16 d8 y4", [&] { launch_w4a<1, 16, 8, 4, 4>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"w4a rs1 x16 d8 y12", [&] { launch_w4a<1, 16, 8, 12, 4>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"w4a rs1 x16 d6 y6", [&] { launch_w4a<1, 16, 6, 6, 4>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"w4a rs1 x16 d8 y8 r1", [&] { launch_w4a<1, 16, 8, 8, 4, 1>(A, Bt, C1, M, N, K); }});
     rows.push_back({"w4a rs1 x20 d8 y8", [&] { launch_w4a<1, 20, 8, 8, 4>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"w4a rs1 x16 d10 y8", [&] { launch_w4a<1, 16, 10, 8, 4>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"w4a rs2 x32 d8 y8", [&] { launch_w4a<2, 32, 8, 8, 4>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"w4a rs1 x20 d8 y8 TR", [&] { launch_w4a<1, 20, 8, 8, 4, 2, true>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"w4a rs1 x24 d8 y8", [&] { launch_w4a<1, 24, 8, 8, 4>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"w4a rs1 x20 d8 y4", [&] { launch_w4a<1, 20, 8, 4, 4>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"S xa16 xb34 b3 y8", [&] { launch_plan<V4PlanS<16, 34, 3, 8>>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"S xa16 xb34 b4 y12", [&] { launch_plan<V4PlanS<16, 34, 4, 12>>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"S xa18 xb38 b3 y8", [&] { launch_plan<V4PlanS<18, 38, 3, 8>>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"S xa16 xb36 b5 y12", [&] { launch_plan<V4PlanS<16, 36, 5, 12>>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"S xa20 xb40 b3 y8", [&] { launch_plan<V4PlanS<20, 40, 3, 8>>(A, Bt, C1, M, N, K); }});
     for (int r = 0; r < reps; ++r) {
       for (Row& row : rows) {
         CK(hipMemset(C1, 0xff, sizeof(float) * M * N));
