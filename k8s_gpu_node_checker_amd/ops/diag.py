@@ -82,17 +82,20 @@ DEGRADED_FRACTION = 0.95
 FULL_CUS = 256
 FULL_MEM_BYTES = 288 << 30
 REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
-    # bf16 MFMA GEMM, TFLOP/s.  The v3 kernel's references (4096: 1280, 8192: 1228, above) times the v4/v3 ratio of
-    # cold diagnostic runs on one box, alternated run by run since v4 became the default (round 5): 1.059 at
-    # level 1 (medians 1411 / 1332), 1.058 at level 2 (1315 / 1242), profiles/diag_cold_v3v4_mi355x.jsonl -- the
-    # same relative margin for every box as before.  That box's v4 soaks sit at 1.00-1.02 (level 2, 323 rounds:
-    # min 1301, median 1319) and 1.04-1.09 (level 1, 641 rounds: 1408-1478), profiles/soak_l{1,2}_v4_mi355x.json
-    "gemm": {4096: 1355.0, 8192: 1300.0},
+    # bf16 MFMA GEMM, TFLOP/s.  The diagnostics run the four-wave v4 kernel since round 5; its references are the
+    # v3 kernel's (4096: 1280, 8192: 1228, above) times the v4/v3 ratio of cold diagnostic runs on one box,
+    # alternated run by run (profiles/diag_cold_v3v4_mi355x.jsonl, second block): medians 1310 / 1217 = 1.076 at
+    # level 1 and 1308 / 1203 = 1.087 at level 2, rounded down -- the same relative margin for every box as before.
+    # That box is a slow one (v3 at 0.95 of its old reference); its v4 soaks: level 2, 322 rounds, 1300-1326, level 1,
+    # 669 rounds, 1309-1332 (profiles/soak_l{1,2}_v4_mi355x.json)
+    "gemm": {4096: 1370.0, 8192: 1330.0},
     # MX-fp8 GEMM, TFLOP/s.  8192^3 with the bf16-output kernel: 2,294-2,450 over a 6-minute level-2 burn-in
     # (median 2,402, profiles/diag_burn_in_level2_6min_bf16out_mi355x.json), 2,199 as the best of three on the
     # slowest box's cold node cycle (profiles/node_cycle_1gpu_mi355x.json) -> 2,300 puts that healthy run at
     # 0.956, above the degraded line (the fp32-output 2,380 left a slow healthy box degraded in most rounds)
-    "gemm_fp8": {4096: 2210.0, 8192: 2300.0},
+    # v3's 2,210 / 2,300 times the same box's fp8 v4/v3 cold ratio, 2,377 / 2,269 = 1.047 (level 1) and 2,386 / 2,277
+    # = 1.048 (level 2), rounded down; its v4 soaks 2,373-2,438
+    "gemm_fp8": {4096: 2300.0, 8192: 2400.0},
     "hbm": {"copy_tbs": 6.49, "read_tbs": 6.96},   # 16-byte copy (read + write bytes counted) / read, TB/s
     # register-resident burn-in.  fp8 is the unscaled f8f6f4 instruction since round 4 (it was the gfx94x
     # v_mfma_f32_16x16x32_fp8_fp8, 1,940): 40 runs median 4,872 vs MX-fp8's 4,844 in the same runs, first (cold)
