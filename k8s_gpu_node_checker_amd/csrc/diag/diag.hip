@@ -896,6 +896,23 @@ struct V4PlanA {
   }
 };
 
+// Plan A2: plan A with the half-2 DMA pieces issued from slot H2S of half 2 on (after the F0' reads, say), so an
+// MFMA gap carries a read or a DMA, not both (an LDS-DMA's issue costs ~60-185 cycles depending on what else its
+// gap issues: MI355X_MICROARCH.md)
+template <int RS, int X_AT, int D1, int Y_AT, int R2, int H2S>
+struct V4PlanA2 {
+  static constexpr V4Slot at(int i) {
+    V4Slot o = V4PlanA<RS, X_AT, D1, Y_AT, R2>::at(i);
+    if (i >= 64) {
+      const int h = i - 64;
+      constexpr int D2 = 16 - D1, SP = D2 > 0 ? (63 - H2S) / D2 + ((63 - H2S) / D2 == 0) : 1;
+      o.dma = -1;
+      if (D2 > 0 && h >= H2S && (h - H2S) % SP == 0 && (h - H2S) / SP < D2) o.dma = D1 + (h - H2S) / SP;
+    }
+    return o;
+  }
+};
+
 // Plan S (hipBLASLt's order, read from its gfx950 MT256x256x64 kernel): the A pieces of F1 one per 2 MFMAs, barrier
 // X1 (XA), then the B pieces of F1 one per 2 MFMAs with the A-operand DMAs between them, barrier X2 (XB), the
 // B-operand DMAs one per BSP MFMAs, barrier Y (slot 64 + Y_AT) retiring the previous K-tile, F0' one per 2 MFMAs.

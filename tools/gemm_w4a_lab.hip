@@ -57,6 +57,20 @@ void launch_plan(const __bf16* A, const __bf16* Bt, float* C, int M, int N, int 
                      2 * V2_STAGE_BYTES, nullptr, A, Bt, C, nullptr, M, N, K);
 }
 
+// fp8 (K in bytes; the kernels take bf16 columns = bytes / 2)
+template <class PLAN>
+void launch_plan8(const void* A, const void* Bt, float* C, int M, int N, int K) {
+  static bool once = [] {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<OUT_F32, PLAN, 4, false, DT_FP8U>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
+    return true;
+  }();
+  (void)once;
+  hipLaunchKernelGGL((gemm_v4_kernel<OUT_F32, PLAN, 4, false, DT_FP8U>), dim3((M / V2_BM) * (N / V2_BN)),
+                     dim3(V4_THREADS), 2 * V2_STAGE_BYTES, nullptr, static_cast<const __bf16*>(A),
+                     static_cast<const __bf16*>(Bt), C, nullptr, M, N, K / 2);
+}
+
 template <int RS, int X_AT, int D1, int Y_AT, int GM, int R2 = 2, bool TR = false>
 void launch_w4a(const __bf16* A, const __bf16* Bt, float* C, int M, int N, int K) {
   launch_plan<V4PlanA<RS, X_AT, D1, Y_AT, R2>, GM, TR>(A, Bt, C, M, N, K);
@@ -109,6 +123,7 @@ int main(int argc, char** argv) {
   run_stamps<true>(ssize, sk);
   return 0;
 #endif
+  const bool fp8 = argc > 3 && strcmp(argv[3], "fp8") == 0;  // SIZES REPS fp8: the fp8 plan sweep against v3's fp8
   std::vector<int> sizes = {4096, 8192};
   if (argc > 1) {
     sizes.clear();
@@ -127,11 +142,17 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&Bt, sizeof(__bf16) * N * K));
     CK(hipMalloc(&C0, sizeof(float) * M * N));
     CK(hipMalloc(&C1, sizeof(float) * M * N));
-    hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, A, (size_t)M * K, 7ULL);
-    hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, Bt, (size_t)N * K, 11ULL);
-    const int nwg1 = (M / BM) * (N / BN);
-    hipLaunchKernelGGL(gemm_bf16_kernel, dim3(nwg1), dim3(THREADS), 0, nullptr, (const u32x4*)A, (const u32x4*)Bt, C0,
-                       M, N, K);
+    if (fp8) {
+      hipLaunchKernelGGL(fill_fp8_kernel, dim3(2048), dim3(256), 0, nullptr, (uint8_t*)A, (size_t)M * K, 7ULL);
+      hipLaunchKernelGGL(fill_fp8_kernel, dim3(2048), dim3(256), 0, nullptr, (uint8_t*)Bt, (size_t)N * K, 11ULL);
+      CK(launch_v3<DT_FP8U>(A, Bt, C0, M, N, K / 2, nullptr) == 0 ? hipSuccess : hipErrorUnknown);
+    } else {
+      hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, A, (size_t)M * K, 7ULL);
+      hipLaunchKernelGGL(fill_bf16_kernel, dim3(2048), dim3(256), 0, nullptr, Bt, (size_t)N * K, 11ULL);
+      const int nwg1 = (M / BM) * (N / BN);
+      hipLaunchKernelGGL(gemm_bf16_kernel, dim3(nwg1), dim3(THREADS), 0, nullptr, (const u32x4*)A, (const u32x4*)Bt,
+                         C0, M, N, K);
+    }
     CK(hipDeviceSynchronize());
     std::vector<float> h0((size_t)M * N), h1((size_t)M * N);
     CK(hipMemcpy(h0.data(), C0, sizeof(float) * M * N, hipMemcpyDeviceToHost));
@@ -143,16 +164,28 @@ int main(int argc, char** argv) {
       std::vector<double> all;
     };
     std::vector<Row> rows;
+    if (fp8) {
+      rows.push_back({"fp8 warmup (v3)", [&] { (void)launch_v3<DT_FP8U>(A, Bt, C1, M, N, K / 2, nullptr); }});
+      rows.push_back({"fp8 v3", [&] { (void)launch_v3<DT_FP8U>(A, Bt, C1, M, N, K / 2, nullptr); }});
+      rows.push_back({"fp8 x8 da12 x30 db31 y46", [&] { launch_plan8<V4PlanF8<8, 12, 30, 31, 46>>(A, Bt, C1, M, N, K); }});
+      rows.push_back({"fp8 x8 da10 x26 db27 y42", [&] { launch_plan8<V4PlanF8<8, 10, 26, 27, 42>>(A, Bt, C1, M, N, K); }});
+      rows.push_back({"fp8 x10 da12 x30 db31 y46", [&] { launch_plan8<V4PlanF8<10, 12, 30, 31, 46>>(A, Bt, C1, M, N, K); }});
+      rows.push_back({"fp8 x10 da12 x28 db29 y44", [&] { launch_plan8<V4PlanF8<10, 12, 28, 29, 44>>(A, Bt, C1, M, N, K); }});
+      rows.push_back({"fp8 x8 da12 x30 db31 y46 #2", [&] { launch_plan8<V4PlanF8<8, 12, 30, 31, 46>>(A, Bt, C1, M, N, K); }});
+    } else {
     rows.push_back({"v3(diag,lds-epi)", [&] { launch_v3<DT_BF16>(A, Bt, C1, M, N, K, nullptr); }});
     rows.push_back({"w4a rs1 x20 d8 y8", [&] { launch_w4a<1, 20, 8, 8, 4>(A, Bt, C1, M, N, K); }});
     rows.push_back({"w4a rs1 x20 d8 y8 TR", [&] { launch_w4a<1, 20, 8, 8, 4, 2, true>(A, Bt, C1, M, N, K); }});
     rows.push_back({"w4a rs1 x24 d8 y8", [&] { launch_w4a<1, 24, 8, 8, 4>(A, Bt, C1, M, N, K); }});
     rows.push_back({"w4a rs1 x20 d8 y4", [&] { launch_w4a<1, 20, 8, 4, 4>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"A2 x20 d8 y8 h40", [&] { launch_plan<V4PlanA2<1, 20, 8, 8, 2, 40>>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"A2 x20 d8 y8 h33", [&] { launch_plan<V4PlanA2<1, 20, 8, 8, 2, 33>>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"A2 x20 d10 y8 h40", [&] { launch_plan<V4PlanA2<1, 20, 10, 8, 2, 40>>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"A2 x20 d12 y4 h38", [&] { launch_plan<V4PlanA2<1, 20, 12, 4, 2, 38>>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"A2 x20 d8 y4 r1 h24", [&] { launch_plan<V4PlanA2<1, 20, 8, 4, 1, 24>>(A, Bt, C1, M, N, K); }});
     rows.push_back({"S xa16 xb34 b3 y8", [&] { launch_plan<V4PlanS<16, 34, 3, 8>>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"S xa16 xb34 b4 y12", [&] { launch_plan<V4PlanS<16, 34, 4, 12>>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"S xa18 xb38 b3 y8", [&] { launch_plan<V4PlanS<18, 38, 3, 8>>(A, Bt, C1, M, N, K); }});
     rows.push_back({"S xa16 xb36 b5 y12", [&] { launch_plan<V4PlanS<16, 36, 5, 12>>(A, Bt, C1, M, N, K); }});
-    rows.push_back({"S xa20 xb40 b3 y8", [&] { launch_plan<V4PlanS<20, 40, 3, 8>>(A, Bt, C1, M, N, K); }});
+    }
     for (int r = 0; r < reps; ++r) {
       for (Row& row : rows) {
         CK(hipMemset(C1, 0xff, sizeof(float) * M * N));
