@@ -70,6 +70,7 @@ def _targets() -> Dict[str, Dict[str, object]]:
         },
         "diag": {
             "sources": [os.path.join(CSRC, "diag", "diag.hip")],
+            "headers": [os.path.join(CSRC, "diag", "v4_plan.h")],
             "out": os.path.join(OUT, "libmi355x_diag.so"),
             "cmd": [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
                     "-Wall", "-Wno-unused-result"],
