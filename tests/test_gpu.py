@@ -914,6 +914,9 @@ def test_gemm_knobs_are_thread_local_and_concurrent_threads_agree(dev):
                 seen.append(diag.get_gemm_config())
                 s = torch.cuda.Stream(device=dev)
                 c = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+                # the NaN fill ran on this thread's current stream: order it before the GEMM on s (torch's
+                # streams do not synchronize with it by themselves; a fill finishing late overwrote C with NaN)
+                s.wait_stream(torch.cuda.current_stream(dev))
                 with torch.cuda.stream(s):
                     diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, s.cuda_stream)
                 s.synchronize()
