@@ -1802,6 +1802,11 @@ template <int OUT, bool TR, int DT>
 int launch_v4_inst(const void* A, const void* Bt, void* C, double* csum, int M, int N, int K, hipStream_t stream) {
   using Plan = std::conditional_t<DT == DT_FP8U, V4PlanF8<8, 10, 26, 27, 42>, V4PlanA<1, 20, 8, 8, 2>>;
   constexpr auto kern = gemm_v4_kernel<OUT, Plan, 4, TR, DT>;
+  if (static_cast<uint64_t>(V2_BM) * static_cast<uint64_t>(K) * 2 >= (1ull << 32)) {
+    // the buffer resources cover a 256-row panel with 32-bit byte offsets
+    g_err = "gemm v4: a 256-row operand panel must stay under 4 GiB (K < 8,388,608 bf16 columns)";
+    return -2;
+  }
   static LdsAttrOnce attr;
   if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(kern), 2 * V2_STAGE_BYTES, "gemm v4") != 0) return -1;
   const int nwg = (M / V2_BM) * (N / V2_BN);
