@@ -1,6 +1,7 @@
 import json, sys, torch
 sys.path.insert(0, ".")
 from k8s_gpu_node_checker_amd.ops import diag
+diag.set_gemm_variant("v3")  # a v3 tool: the default (auto) runs the four-wave v4 kernel since round 5
 st = torch.cuda.current_stream().cuda_stream
 for (m, n, k) in [(256, 256, 128), (512, 256, 384), (1024, 768, 8192)]:
     g = torch.Generator(device="cuda").manual_seed(1)

@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from k8s_gpu_node_checker_amd.ops import diag  # noqa: E402
+diag.set_gemm_variant("v3")  # a v3 tool: the default (auto) runs the four-wave v4 kernel since round 5
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 dt = sys.argv[2] if len(sys.argv) > 2 else "bf16"
