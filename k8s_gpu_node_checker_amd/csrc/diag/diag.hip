@@ -8,10 +8,12 @@
 //               (v_mfma_f32_16x16x32_bf16), XOR-swizzled LDS (conflict-free
 //               ds_read_b128 fragment loads), XCD-aware tile order.
 //               v4: 256x256x64 tiles, 4 waves of 128x128 each, the loop's MFMA /
-//                   ds_read / LDS-DMA interleave written out in asm (large bf16
-//                   GEMMs, default);
+//                   ds_read / LDS-DMA interleave written out in asm on a checked
+//                   plan (v4_plan.h); bf16 and fp8 (16x16x128, by quadrant), the
+//                   default for large GEMMs;
 //               v3: the same tile, 8 waves in two barrier-staggered groups, LDS-DMA
-//                   restaged region by region (fp8 / fp4, and bf16 for A/B);
+//                   restaged region by region (MX-fp4, the scaled MX-fp8 form, and
+//                   bf16 / fp8 for A/B);
 //               v2: the same tile, one barrier per K-tile (kept for A/B);
 //               v1: 128x128x64 tiles, 4 waves, register-staged (small grids).
 //               Verified against an fp32 reference kernel on sampled outputs.
