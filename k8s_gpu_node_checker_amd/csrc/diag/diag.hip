@@ -1452,6 +1452,11 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b) {
   }
   return ms;
 }
+// The time between two completed events, for DIAG_CHECK: a failure is reported as the error it is
+hipError_t event_ms(hipEvent_t a, hipEvent_t b, float* ms) {
+  *ms = 0.f;
+  return hipEventElapsedTime(ms, a, b);
+}
 
 // ---------------------------------------------------------------------------
 // Matrix-core datapath burn-in, one kernel per precision the MI355X computes in (operand lane layouts
@@ -2229,7 +2234,9 @@ int diag_gemm_bf16_x(int device, int M, int N, int K, int warmup, int iters, int
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   DIAG_CHECK(hipGetLastError());
-  const double ms = elapsed_ms(e0, e1) / std::max(iters, 1);
+  float t_ms = 0.f;
+  DIAG_CHECK(event_ms(e0, e1, &t_ms));
+  const double ms = t_ms / std::max(iters, 1);
   if (fused) DIAG_CHECK(inject_output_ck(static_cast<__bf16*>(bC.ptr), cs, inject_elem, M, N));
   else DIAG_CHECK(inject_output(C, inject_elem, static_cast<long long>(M) * N));
   hipLaunchKernelGGL(gemm_ref_kernel, dim3((nsamp + 255) / 256), dim3(256), 0, nullptr, A, Bt, rows, cols, ref,
@@ -2326,7 +2333,9 @@ int diag_gemm_fp8_x(int device, int M, int N, int K, int warmup, int iters, int 
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   DIAG_CHECK(hipGetLastError());
-  const double ms = elapsed_ms(e0, e1) / std::max(iters, 1);
+  float t_ms = 0.f;
+  DIAG_CHECK(event_ms(e0, e1, &t_ms));
+  const double ms = t_ms / std::max(iters, 1);
   if (fused) DIAG_CHECK(inject_output_ck(static_cast<__bf16*>(C.ptr), cs, inject_elem, M, N));
   else DIAG_CHECK(inject_output(c, inject_elem, static_cast<long long>(M) * N));
   const int* r = static_cast<const int*>(rows.ptr);
@@ -2385,27 +2394,31 @@ int diag_hbm_bandwidth(int device, size_t bytes, int iters, double* copy_tbs, do
   DIAG_CHECK(tm.create());
   hipEvent_t e0 = tm.e0, e1 = tm.e1;
   const size_t nb = n * sizeof(f32x4);
+  float t_ms = 0.f;
   // copy
   hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, nullptr, a, b, n);
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, nullptr, a, b, n);
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
-  *copy_tbs = 2.0 * nb * iters / (elapsed_ms(e0, e1) * 1e-3) / 1e12;
+  DIAG_CHECK(event_ms(e0, e1, &t_ms));
+  *copy_tbs = 2.0 * nb * iters / (t_ms * 1e-3) / 1e12;
   // read
   hipLaunchKernelGGL(read_kernel, dim3(grid), dim3(256), 0, nullptr, a, n, sink);
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(read_kernel, dim3(grid), dim3(256), 0, nullptr, a, n, sink);
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
-  *read_tbs = 1.0 * nb * iters / (elapsed_ms(e0, e1) * 1e-3) / 1e12;
+  DIAG_CHECK(event_ms(e0, e1, &t_ms));
+  *read_tbs = 1.0 * nb * iters / (t_ms * 1e-3) / 1e12;
   // write
   hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, b, n, 3.0f);
   DIAG_CHECK(hipEventRecord(e0, nullptr));
   for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, nullptr, b, n, 3.0f);
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
-  *write_tbs = 1.0 * nb * iters / (elapsed_ms(e0, e1) * 1e-3) / 1e12;
+  DIAG_CHECK(event_ms(e0, e1, &t_ms));
+  *write_tbs = 1.0 * nb * iters / (t_ms * 1e-3) / 1e12;
   DIAG_CHECK(hipGetLastError());
   return 0;
 }
@@ -2449,7 +2462,9 @@ int diag_memtest_x(int device, size_t bytes, uint64_t seed, int passes, long lon
   DIAG_CHECK(hipMemcpy(h, dev, sizeof h, hipMemcpyDeviceToHost));
   *errors = h[0];
   *first_bad_byte = h[0] ? h[1] * sizeof(uint4) : ~0ULL;
-  *gbps = 4.0 * passes * static_cast<double>(n * sizeof(uint4)) / (elapsed_ms(e0, e1) * 1e-3) / 1e9;
+  float t_ms = 0.f;
+  DIAG_CHECK(event_ms(e0, e1, &t_ms));
+  *gbps = 4.0 * passes * static_cast<double>(n * sizeof(uint4)) / (t_ms * 1e-3) / 1e9;
   return 0;
 }
 
@@ -2532,7 +2547,8 @@ int diag_p2p_copy_t(int src, int dst, size_t bytes, int iters, double timeout_ms
   hipError_t w = wait_event_polled(e1, dl);
   if (w == hipErrorNotReady) return hung("copies");
   DIAG_CHECK(w);
-  const float ms = elapsed_ms(e0, e1);
+  float ms = 0.f;
+  DIAG_CHECK(event_ms(e0, e1, &ms));
   *gbps = ms > 0.f ? static_cast<double>(iters) * static_cast<double>(nbytes) / (ms * 1e-3) / 1e9 : 0.0;
   // verify what arrived
   DIAG_CHECK(hipSetDevice(dst));
@@ -2704,7 +2720,8 @@ int diag_mfma_burn_map(int device, int kind, int iters, int reps, double* tflops
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   DIAG_CHECK(hipGetLastError());
-  const float ms = elapsed_ms(e0, e1);
+  float ms = 0.f;
+  DIAG_CHECK(event_ms(e0, e1, &ms));
   DIAG_CHECK(hipMemcpy(errors, dcnt.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   if (cu_map != nullptr) DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   const double flop = static_cast<double>(blocks) * 4 /*waves*/ * iters * 16 /*MFMA per iter*/ * 2.0 * 16 * 16 * K;
@@ -2747,7 +2764,9 @@ int diag_lds_test(int device, int rounds, uint32_t seed, int inject_block, unsig
   DIAG_CHECK(hipGetLastError());
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
-  *ms = elapsed_ms(e0, e1);
+  float t_ms = 0.f;
+  DIAG_CHECK(event_ms(e0, e1, &t_ms));
+  *ms = t_ms;
   DIAG_CHECK(hipMemcpy(errors, derr.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   *lds_bytes = static_cast<int>(dyn);
@@ -2793,7 +2812,8 @@ int diag_l2_bandwidth(int device, size_t slice_bytes, int passes, int blocks_per
   DIAG_CHECK(hipEventRecord(e1, nullptr));
   DIAG_CHECK(hipEventSynchronize(e1));
   DIAG_CHECK(hipGetLastError());
-  const float ms = elapsed_ms(e0, e1);
+  float ms = 0.f;
+  DIAG_CHECK(event_ms(e0, e1, &ms));
   DIAG_CHECK(hipMemcpy(errors, derr.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   DIAG_CHECK(hipMemcpy(cu_map, dmap.ptr, map_bytes, hipMemcpyDeviceToHost));
   const double bytes = static_cast<double>(blocks) * passes * static_cast<double>(slice_bytes);
@@ -2913,7 +2933,8 @@ int diag_host_link(int device, size_t bytes, int iters, double* h2d_gbps, double
     for (int i = 0; i < iters; ++i) DIAG_CHECK(copy());
     DIAG_CHECK(hipEventRecord(e1, st));
     DIAG_CHECK(hipEventSynchronize(e1));
-    const float ms = elapsed_ms(e0, e1);
+    float ms = 0.f;
+    DIAG_CHECK(event_ms(e0, e1, &ms));
     const double gbps = ms > 0.f ? static_cast<double>(iters) * static_cast<double>(bytes) / (ms * 1e-3) / 1e9 : 0.0;
     *(dir == 0 ? h2d_gbps : d2h_gbps) = gbps;
   }
