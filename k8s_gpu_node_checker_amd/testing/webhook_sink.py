@@ -20,6 +20,8 @@ The URL path selects the behaviour, so one sink serves every test:
 ``/loop``       ``302`` to itself, forever
 ``/to/H/MODE``  ``307`` to ``http://H:<this port>/MODE`` (another host name for the same sink)
 ``/cookie``     ``302`` to ``/200`` setting ``sid=abc`` (path ``/``)
+``/loc/S/L``    status ``S`` with ``Location: L`` (percent-decoded; ``{port}`` becomes this sink's port; no header
+                when ``L`` is empty): relative, scheme-relative, query, fragment and foreign-scheme targets
 ==============  =============================================================
 
 Every request is logged (path, headers, body) for assertions.
@@ -33,6 +35,7 @@ import socketserver
 import struct
 import threading
 import time
+import urllib.parse
 from typing import Any, Dict, List, Optional
 
 
@@ -77,6 +80,11 @@ class _SinkHandler(socketserver.BaseRequestHandler):
             count = srv.counts.get(req["path"], 0) + 1
             srv.counts[req["path"]] = count
         path = req["path"].split("?", 1)[0]
+        if path.startswith("/loc/"):
+            _, _, status, loc = req["path"].split("/", 3)
+            loc = urllib.parse.unquote(loc).replace("{port}", str(srv.server_address[1]))
+            self._respond(int(status), "Redirect", b"moved", f"Location: {loc}\r\n" if loc else "")
+            return
         if path.startswith("/seq/"):
             steps = path.rsplit("/", 1)[-1].split(",")
             path = "/" + steps[min(count, len(steps)) - 1]

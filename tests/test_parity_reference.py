@@ -282,6 +282,26 @@ def test_slack_redirects_identical(cluster, sink, mode, flags):
         assert "✅ 슬랙 메시지를 성공적으로 전송했습니다." in a.stdout or flags
 
 
+@pytest.mark.parametrize("mode", [
+    "loc/302/",                                  # a redirect status without a Location: the 3xx is the answer
+    "loc/307/postonly%3Fa%3D1%26b",              # relative, with a query
+    "loc/308/%2F%2F127.0.0.1%3A{port}%2F200",    # scheme-relative
+    "loc/307/..%2F..%2F200",                     # dot segments above the root
+    "loc/301/%2F200%23frag",                     # a fragment (not sent)
+    "loc/307/%2F200%3Fq%3D%25E2%259C%2585",      # a percent-encoded query kept as is
+    "loc/307/%2Fp%C3%A4th",                      # a raw non-ASCII path (requests re-quotes it)
+    "loc/302/ftp%3A%2F%2Fexample.invalid%2Fx",   # a scheme requests has no adapter for
+    "loc/307/http%3A%2F%2F127.0.0.1%3A1%2F200",  # a refused connection after the hop
+    "loc/303/%2F307",                            # 303 -> GET, then 307 keeps the GET
+    "loc/200/%2F500",                            # a Location on a success is not followed
+])
+def test_slack_redirect_targets_identical(cluster, sink, mode):
+    port = sink.server_address[1]
+    a, b, ra, rb = _transport_case(cluster, sink, sink.url(mode.replace("{port}", str(port))))
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert ra == rb and ra
+
+
 def test_slack_url_credentials_identical(cluster, sink, tmp_path):
     host, port = sink.server_address[:2]
     for url in (f"http://user:pass@{host}:{port}/200", f"http://us%40er:p%3Ass@{host}:{port}/to/localhost/200"):
