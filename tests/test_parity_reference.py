@@ -302,6 +302,23 @@ def test_slack_redirect_targets_identical(cluster, sink, mode):
     assert ra == rb and ra
 
 
+@pytest.mark.parametrize("url,env", [
+    ("http://example.invalid/200", {"HTTP_PROXY": "SINK"}),
+    ("http://example.invalid/200", {"http_proxy": "SINK"}),
+    ("http://user:pw@example.invalid/200", {"HTTP_PROXY": "SINK"}),   # origin credentials travel to the proxy
+    ("http://example.invalid/200", {"ALL_PROXY": "SINK"}),
+    ("http://example.invalid:8080/200", {"HTTP_PROXY": "SINK", "NO_PROXY": "example.invalid"}),  # bypassed
+])
+def test_slack_env_proxies_identical(cluster, sink, url, env):
+    """requests' env proxies: the sink is the proxy (it logs the absolute-form target); 127.0.0.1 (the mock
+    apiserver, which the reference's stand-in client also reaches through requests) is always in NO_PROXY."""
+    e = {k: sink.base_url if v == "SINK" else v for k, v in env.items()}
+    e["NO_PROXY"] = ",".join(["127.0.0.1"] + ([e["NO_PROXY"]] if "NO_PROXY" in e else []))
+    a, b, ra, rb = _transport_case(cluster, sink, url, env=e)
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert ra == rb
+
+
 def test_slack_url_credentials_identical(cluster, sink, tmp_path):
     host, port = sink.server_address[:2]
     for url in (f"http://user:pass@{host}:{port}/200", f"http://us%40er:p%3Ass@{host}:{port}/to/localhost/200"):
