@@ -50,5 +50,10 @@ class TransportError(Exception):
     def __init__(self, scheme: str, host: str, port: int, url: str, cause: BaseException):
         self.cause = cause
         pool = "HTTPSConnectionPool" if scheme == "https" else "HTTPConnectionPool"
+        text = str(cause)
+        if text.startswith(f"{pool}(host=") and ": Max retries exceeded with url: " in text:
+            # the transport already rendered the urllib3 message (utils/http.py: refused, DNS, connect timeout, TLS)
+            super().__init__(text)
+            return
         super().__init__(f"{pool}(host='{host}', port={port}): Max retries exceeded with url: {url} "
-                         f"(Caused by {type(cause).__name__}({str(cause)!r}))")
+                         f"(Caused by {type(cause).__name__}({text!r}))")

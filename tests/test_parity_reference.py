@@ -6,6 +6,7 @@ Skipped when /root/reference is not mounted (e.g. on the GPU box).
 """
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -300,6 +301,38 @@ def test_slack_redirect_targets_identical(cluster, sink, mode):
     a, b, ra, rb = _transport_case(cluster, sink, sink.url(mode.replace("{port}", str(port))))
     assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
     assert ra == rb and ra
+
+
+def _undate(text):
+    return re.sub(r"'Date': '[^']*'", "'Date': D", text)
+
+
+@pytest.mark.parametrize("status", [403, 404, 500])
+@pytest.mark.parametrize("flags", [[], ["--json"]])
+def test_apiserver_error_status_identical(tmp_path, mock_cluster, status, flags):
+    """A LIST answered 403 / 404 / 500: the reference prints the client's ApiException (status, reason, headers,
+    body) after `에러: ` (or as the JSON `error`) and exits 1; so does the CLI.  Only the Date header may differ."""
+    srv = mock_cluster(fixtures.golden("readme"), status=status)
+    kc = write_kubeconfig(str(tmp_path / "kc.yaml"), srv.url)
+    a, b = run_ref(["--kubeconfig", kc] + flags), run_new(["--kubeconfig", kc] + flags)
+    assert (a.returncode, _undate(a.stdout)) == (b.returncode, _undate(b.stdout)) and a.returncode == 1
+    # stderr: identical up to the traceback the text mode prints (its frames name each program's own code)
+    ta, tb = a.stderr.split("Traceback"), b.stderr.split("Traceback")
+    assert _undate(ta[0]) == _undate(tb[0]) and len(ta) == len(tb)
+    if len(ta) > 1:  # the exception's own line: same text after the type name
+        assert ta[-1].strip().splitlines()[-1].split(":", 1)[1] == tb[-1].strip().splitlines()[-1].split(":", 1)[1]
+
+
+def test_apiserver_refused_same_message(tmp_path):
+    """No apiserver: both end in an uncaught connection error (exit 1) whose message is urllib3's MaxRetryError
+    text; the CLI's URL carries its page size (`?limit=500`, PARITY.md: paging)."""
+    kc = write_kubeconfig(str(tmp_path / "kc.yaml"), "http://127.0.0.1:1")
+    a, b = run_ref(["--kubeconfig", kc]), run_new(["--kubeconfig", kc])
+    assert (a.returncode, a.stdout) == (b.returncode, b.stdout) == (1, "")
+    ma = a.stderr.strip().splitlines()[-1].split(": ", 1)[1]
+    mb = b.stderr.strip().splitlines()[-1].split(": ", 1)[1]
+    assert mb == ma.replace("/api/v1/nodes ", "/api/v1/nodes?limit=500 ")
+    assert "Caused by NewConnectionError(" in mb and mb.count("Max retries exceeded") == 1
 
 
 @pytest.mark.parametrize("url,env", [
