@@ -7,6 +7,7 @@ Skipped when /root/reference is not mounted (e.g. on the GPU box).
 import json
 import os
 import re
+import ssl
 import subprocess
 import sys
 
@@ -14,6 +15,7 @@ import pytest
 
 from k8s_gpu_node_checker_amd.testing import fixtures
 from k8s_gpu_node_checker_amd.testing.mock_apiserver import write_kubeconfig
+from k8s_gpu_node_checker_amd.testing.webhook_sink import WebhookSink
 
 REF = os.environ.get("K8SGPU_REFERENCE", "/root/reference/check-gpu-node.py")
 STUBS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "refstub")
@@ -350,6 +352,46 @@ def test_slack_env_proxies_identical(cluster, sink, url, env):
     a, b, ra, rb = _transport_case(cluster, sink, url, env=e)
     assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
     assert ra == rb
+
+
+class _TLSSink(WebhookSink):
+    """The webhook sink behind TLS with the session's self-signed certificate (127.0.0.1 / localhost)."""
+
+    def __init__(self, crt, key):
+        super().__init__()
+        self.ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        self.ctx.load_cert_chain(crt, key)
+
+    def get_request(self):
+        s, addr = super().get_request()
+        try:
+            return self.ctx.wrap_socket(s, server_side=True), addr
+        except (OSError, ssl.SSLError):
+            s.close()
+            raise
+
+
+@pytest.fixture
+def tls_sink(certs):
+    s = _TLSSink(*certs).start()
+    yield s
+    s.stop()
+
+
+@pytest.mark.parametrize("host,env", [("127.0.0.1", "REQUESTS_CA_BUNDLE"), ("localhost", "REQUESTS_CA_BUNDLE"),
+                                      ("127.0.0.1", None), ("127.0.0.1", "CURL_CA_BUNDLE"),
+                                      ("127.0.0.1", "SSL_CERT_FILE")])
+def test_slack_https_verification_identical(cluster, tls_sink, certs, host, env):
+    """An https webhook: verified against the bundle requests would use (its env variables, else certifi), the
+    same success or the same `CERTIFICATE_VERIFY_FAILED` line."""
+    url = f"https://{host}:{tls_sink.server_address[1]}/200"
+    a, b, ra, rb = _transport_case(cluster, tls_sink, url, env={env: certs[0]} if env else None)
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert ra == rb
+    if env == "REQUESTS_CA_BUNDLE":
+        assert ra and "✅ 슬랙 메시지를 성공적으로 전송했습니다." in b.stdout
+    elif env is None:
+        assert not ra and "CERTIFICATE_VERIFY_FAILED" in b.stderr
 
 
 def test_slack_url_credentials_identical(cluster, sink, tmp_path):
