@@ -354,6 +354,15 @@ def test_slack_env_proxies_identical(cluster, sink, url, env):
     assert ra == rb
 
 
+def test_slack_read_timeout_identical(cluster):
+    """A webhook slower than requests' 10 s timeout: the same `Read timed out. (read timeout=10)` line (one
+    attempt each: about 20 s)."""
+    with WebhookSink(slow_s=10.6) as slow:
+        a, b, ra, rb = _transport_case(cluster, slow, slow.url("slow"), flags=["--slack-retry-count", "0"])
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert ra == rb and len(ra) == 1 and "Read timed out. (read timeout=10)" in b.stderr
+
+
 class _TLSSink(WebhookSink):
     """The webhook sink behind TLS with the session's self-signed certificate (127.0.0.1 / localhost)."""
 
