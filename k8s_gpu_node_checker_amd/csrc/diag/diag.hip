@@ -2094,7 +2094,8 @@ int diag_gemm_bf16_launch(const void* A, const void* Bt, float* C, int M, int N,
       return -2;
     }
     if (variant >= 4) {
-      if (launch_v4<OUT_F32>(variant, A, Bt, C, nullptr, M, N, K, static_cast<hipStream_t>(stream)) != 0) return -1;
+      const int rc = launch_v4<OUT_F32>(variant, A, Bt, C, nullptr, M, N, K, static_cast<hipStream_t>(stream));
+      if (rc != 0) return rc;
     } else if (variant == 2) {
       static LdsAttrOnce attr;
       if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(gemm_bf16_v2_kernel), 2 * V2_STAGE_BYTES,
@@ -2125,10 +2126,10 @@ int diag_gemm_fp8_launch(const void* A, const void* Bt, float* C, int M, int N, 
   }
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const int v = fp8_variant();
-  if ((v >= 4 ? launch_v4<OUT_F32, DT_FP8U>(v, A, Bt, C, nullptr, M, N, K / 2, st)
-       : g_gemm_fp8_unscaled ? launch_v3<DT_FP8U>(A, Bt, C, M, N, K / 2, st)
-                             : launch_v3<DT_FP8>(A, Bt, C, M, N, K / 2, st)) != 0)
-    return -1;
+  const int rc = v >= 4 ? launch_v4<OUT_F32, DT_FP8U>(v, A, Bt, C, nullptr, M, N, K / 2, st)
+                 : g_gemm_fp8_unscaled ? launch_v3<DT_FP8U>(A, Bt, C, M, N, K / 2, st)
+                                       : launch_v3<DT_FP8>(A, Bt, C, M, N, K / 2, st);
+  if (rc != 0) return rc;
   DIAG_CHECK(hipGetLastError());
   return 0;
 }
@@ -2162,7 +2163,7 @@ int diag_gemm_launch_ck(int dt, const void* A, const void* Bt, void* C, double* 
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const int rc = dt == DT_FP8 ? launch_fp8_ck(A, Bt, static_cast<__bf16*>(C), csum, M, N, K / 2, st)
                               : launch_bf16_ck(A, Bt, static_cast<__bf16*>(C), csum, M, N, K, st);
-  if (rc != 0) return -1;
+  if (rc != 0) return rc;
   DIAG_CHECK(hipGetLastError());
   return 0;
 }

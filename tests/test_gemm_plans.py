@@ -122,3 +122,32 @@ def test_shipped_plans_pass_their_checks(verdicts):
                                     "fp8_b_dma_before_x2"])
 def test_broken_plans_are_rejected(verdicts, broken):
     assert verdicts[broken] == 0, broken
+
+
+@pytest.fixture
+def diag_on_cpu():
+    """The in-tree diag library, on a host without a GPU: only argument checks that return before any HIP call are
+    exercised (on a GPU host these calls would launch, so the test is skipped there)."""
+    torch = pytest.importorskip("torch")
+    if torch.cuda.device_count() > 0:
+        pytest.skip("GPU present: the guard is exercised by the GPU suite's shapes instead")
+    from k8s_gpu_node_checker_amd.ops import diag
+    try:
+        diag.lib()
+    except OSError as e:
+        pytest.skip(f"diag library not loadable: {e}")
+    return diag
+
+
+@pytest.mark.parametrize("dtype,k", [("bf16", 1 << 23), ("fp8", 1 << 24)])
+def test_v4_rejects_panels_past_32_bit_offsets(diag_on_cpu, dtype, k):
+    """v4's buffer resources address a 256-row operand panel with 32-bit byte offsets: K >= 2^23 bf16 columns
+    (2^24 fp8) is refused as an invalid argument (-2) before anything is launched."""
+    diag = diag_on_cpu
+    with diag.gemm_config(variant="v4"), pytest.raises(RuntimeError, match=r"\(-2\).*4 GiB"):
+        if dtype == "bf16":
+            diag.gemm_launch(1, 1, 1, 256, 256, k, 0)
+        else:
+            diag.gemm_fp8_launch(1, 1, 1, 256, 256, k, 0)
+    with diag.gemm_config(variant="v4"), pytest.raises(RuntimeError, match=r"\(-2\).*4 GiB"):
+        diag.gemm_launch_ck(dtype, 1, 1, 1, 1, 256, 256, k, 0)
