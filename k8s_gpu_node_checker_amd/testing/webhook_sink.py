@@ -22,6 +22,7 @@ The URL path selects the behaviour, so one sink serves every test:
 ``/cookie``     ``302`` to ``/200`` setting ``sid=abc`` (path ``/``)
 ``/loc/S/L``    status ``S`` with ``Location: L`` (percent-decoded; ``{port}`` becomes this sink's port; no header
                 when ``L`` is empty): relative, scheme-relative, query, fragment and foreign-scheme targets
+``/locb/S/L``   the same with ``L``'s percent-decoded bytes sent raw (a Location that is not UTF-8)
 ==============  =============================================================
 
 Every request is logged (path, headers, body) for assertions.
@@ -80,6 +81,12 @@ class _SinkHandler(socketserver.BaseRequestHandler):
             count = srv.counts.get(req["path"], 0) + 1
             srv.counts[req["path"]] = count
         path = req["path"].split("?", 1)[0]
+        if path.startswith("/locb/"):  # the Location's bytes as given (percent-decoded, not re-encoded)
+            _, _, status, loc = req["path"].split("/", 3)
+            raw = urllib.parse.unquote_to_bytes(loc)
+            self.request.sendall(f"HTTP/1.1 {int(status)} Redirect\r\nContent-Length: 5\r\n".encode() + b"Location: " +
+                                 raw + b"\r\nConnection: close\r\n\r\nmoved")
+            return
         if path.startswith("/loc/"):
             _, _, status, loc = req["path"].split("/", 3)
             loc = urllib.parse.unquote(loc).replace("{port}", str(srv.server_address[1]))

@@ -297,6 +297,9 @@ def test_slack_redirects_identical(cluster, sink, mode, flags):
     "loc/307/http%3A%2F%2F127.0.0.1%3A1%2F200",  # a refused connection after the hop
     "loc/303/%2F307",                            # 303 -> GET, then 307 keeps the GET
     "loc/200/%2F500",                            # a Location on a success is not followed
+    "locb/307/%2Fp%E4th",                        # a Location that is not UTF-8 (requests' decode error)
+    "locb/302/%2F200%FF",
+    "locb/307/%2Fp%C3%A4th",                     # raw UTF-8 bytes
 ])
 def test_slack_redirect_targets_identical(cluster, sink, mode):
     port = sink.server_address[1]
