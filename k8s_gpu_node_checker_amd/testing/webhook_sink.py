@@ -22,6 +22,8 @@ The URL path selects the behaviour, so one sink serves every test:
 ``/cookie``     ``302`` to ``/200`` setting ``sid=abc`` (path ``/``)
 ``/loc/S/L``    status ``S`` with ``Location: L`` (percent-decoded; ``{port}`` becomes this sink's port; no header
                 when ``L`` is empty): relative, scheme-relative, query, fragment and foreign-scheme targets
+``/body/KIND``   ``500`` with a UTF-8 body sent ``gzip`` / ``deflate`` / ``chunked``, as ``euckr`` or ``latin``
+                (no charset), with no length (``nolength``) or as ``octet`` (guessed)
 ``/locb/S/L``   the same with ``L``'s percent-decoded bytes sent raw (a Location that is not UTF-8)
 ==============  =============================================================
 
@@ -71,6 +73,33 @@ class _SinkHandler(socketserver.BaseRequestHandler):
                f"{extra}Connection: close\r\n\r\n").encode() + body
         self.request.sendall(msg)
 
+    def _send_body(self, kind: str) -> None:
+        text = "서버 오류: rate limited ✗".encode("utf-8")
+        head = "HTTP/1.1 500 Internal Server Error\r\nConnection: close\r\n"
+        if kind == "gzip":
+            import gzip
+            body, head = gzip.compress(text), head + "Content-Type: text/plain; charset=utf-8\r\nContent-Encoding: gzip\r\n"
+        elif kind == "deflate":
+            import zlib
+            body, head = zlib.compress(text), head + "Content-Type: text/plain; charset=utf-8\r\nContent-Encoding: deflate\r\n"
+        elif kind == "chunked":
+            body = b"".join(b"%x\r\n%s\r\n" % (len(text[i:i + 7]), text[i:i + 7]) for i in range(0, len(text), 7))
+            body += b"0\r\n\r\n"
+            head += "Content-Type: application/json\r\nTransfer-Encoding: chunked\r\n"
+        elif kind == "euckr":
+            body, head = "서버 오류".encode("euc-kr"), head + "Content-Type: text/plain; charset=euc-kr\r\n"
+        elif kind == "latin":  # UTF-8 bytes labelled text/plain without a charset: ISO-8859-1 by requests' rule
+            body, head = text, head + "Content-Type: text/plain\r\n"
+        elif kind == "nolength":  # no Content-Length: the body runs to the close
+            body, head = text, head + "Content-Type: application/json\r\n"
+            self.request.sendall(head.encode() + b"\r\n" + body)
+            return
+        else:  # octet-stream: the encoding is guessed
+            body, head = text, head + "Content-Type: application/octet-stream\r\n"
+        if kind != "chunked":
+            head += f"Content-Length: {len(body)}\r\n"
+        self.request.sendall(head.encode() + b"\r\n" + body)
+
     def handle(self) -> None:
         req = self._read_request()
         if req is None:
@@ -81,6 +110,9 @@ class _SinkHandler(socketserver.BaseRequestHandler):
             count = srv.counts.get(req["path"], 0) + 1
             srv.counts[req["path"]] = count
         path = req["path"].split("?", 1)[0]
+        if path.startswith("/body/"):  # a 500 whose body is encoded some way: /body/gzip, deflate, chunked, ...
+            self._send_body(path[6:])
+            return
         if path.startswith("/locb/"):  # the Location's bytes as given (percent-decoded, not re-encoded)
             _, _, status, loc = req["path"].split("/", 3)
             raw = urllib.parse.unquote_to_bytes(loc)
