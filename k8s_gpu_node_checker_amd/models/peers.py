@@ -9,7 +9,11 @@ this module gives the MI355X gate the same stability.  On a node whose GPUs were
 GPU is judged against the other GPUs of the same node, which share every one of those conditions:
 
 * **outlier** -- a GPU below ``PEER_FAIL_RATIO`` of the median of the *other* GPUs (leave-one-out, so with two
-  GPUs the slower is judged against the faster) fails, and the failure names it;
+  GPUs the slower is judged against the faster) fails, and the failure names it -- unless the GPU itself is at
+  or above the absolute degraded line: then its peers are fast, not it slow, and it is ``degraded`` with the
+  ratio in the detail.  Healthy MI355X devices differ by up to ~14 % on MFMA-bound tests under the same code
+  (two devices of one pool, profiles/diag_box_spread_r05_mi355x.jsonl: GEMM 1,280 vs 1,484 TFLOP/s, MX-fp4
+  7,028 vs 8,171), so a slow-but-healthy GPU next to fast ones sits near 0.85 of them;
 * **node-wide shortfall** -- when the remaining GPUs agree within ``NODE_UNIFORM_SPREAD`` and their median is
   below the degraded line, the node gets one node-level ``degraded`` finding: every GPU is slow alike, which
   is the node's condition, not a GPU's.  Only down to the absolute failure line: when the shared median is
@@ -94,8 +98,11 @@ def judge_node(results: Dict[Hashable, Dict[str, Any]], label: Optional[Dict[Has
                     unit = res.get("unit", "")
                     rate = res["rates"][m]
                     peers = statistics.median([members[j]["rates"][m] for j in members if j != d])
-                    problems[d].append(f"{m} {rate:.3g} {unit} = {ratio:.0%} of the node's other GPUs' median "
-                                       f"{peers:.3g}")
+                    txt = f"{m} {rate:.3g} {unit} = {ratio:.0%} of the node's other GPUs' median {peers:.3g}"
+                    if v >= DEGRADED_FRACTION:  # at the MI355X reference itself: its peers are the fast ones
+                        slow[d].append(f"{txt} (itself at {v:.0%} of the MI355X reference)")
+                    else:
+                        problems[d].append(txt)
             alike = [d for d in vals if d not in peer_fail]
             span = [vals[d] for d in alike]
             uniform = len(alike) >= MIN_PEERS and max(span) <= NODE_UNIFORM_SPREAD * min(span)

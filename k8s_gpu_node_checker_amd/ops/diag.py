@@ -36,7 +36,12 @@ from .native import NativeUnavailable, load_cdll
 #       profiles/soak_level1_sched1_mi355x.json (963 rounds, 3 min) gemm 1343 warm but 1275-1294 in single
 #       cold runs, gemm_fp8 2300 warm / 2208-2242 cold (order 0 measured 1207-1226 / 2098-2108 cold)
 #   bf16 GEMM since the four-wave v4 kernel (round 5): the v3 references scaled by the measured v4/v3 ratio
-#       (REFERENCE_RATES["gemm"] below)
+#       (REFERENCE_RATES["gemm"] below), then lowered so the slowest healthy device measured sits at >= 0.97
+#   Devices differ: two MI355X of the round-5 pool, same tree, cold level-1 runs (profiles/
+#       diag_box_spread_r05_mi355x.jsonl): 0000:8e:00.0 gemm 1,278-1,280 / gemm_fp8 2,318-2,332 / MX-fp4 burn
+#       6,977-7,035 against 0000:d9:00.0's 1,457-1,487 / 2,585-2,635 / 8,004-8,252 (0.86-0.89 of it, with HBM,
+#       L2 and the bf16 burn-in alike).  A reference set on a fast device flags slow healthy ones "degraded"
+#       for life, so every compute reference is at most the slowest healthy device / 0.97
 # A result below FAIL_FRACTION of its reference fails (a GPU at 55 % clock or power is unhealthy); one
 # between FAIL_FRACTION and DEGRADED_FRACTION passes as *degraded* (a warning on the node, still Ready).
 # The 85 % floor sits under every soak minimum (worst: gemm_fp8 8192^3 at 90 % of its median) and under
@@ -87,20 +92,28 @@ REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
     # alternated run by run (profiles/diag_cold_v3v4_mi355x.jsonl, second block): medians 1310 / 1217 = 1.076 at
     # level 1 and 1308 / 1203 = 1.087 at level 2, rounded down -- the same relative margin for every box as before.
     # That box is a slow one (v3 at 0.95 of its old reference); its v4 soaks: level 2, 322 rounds, 1300-1326, level 1,
-    # 669 rounds, 1309-1332 (profiles/soak_l{1,2}_v4_mi355x.json)
-    "gemm": {4096: 1370.0, 8192: 1330.0},
+    # 669 rounds, 1309-1332 (profiles/soak_l{1,2}_v4_mi355x.json).  Lowered from 1,370 / 1,330 after a slower
+    # healthy device (8e:00.0 above) measured 1,278-1,280 cold at 4096^3 (0.93: degraded): 1,280 / 0.97 -> 1,310.
+    # Its 8192^3 rate was not measured (the pool did not hand it out again); level 2 / level 1 is 0.94-0.99 on
+    # the two devices that were (d9: 1,355-1,405 / 1,457-1,487; the calibration box above), so 1,203-1,267
+    # expected -> 1,240 puts even the low end at 0.97.  d9 sits at 1.12-1.13 of both.
+    "gemm": {4096: 1310.0, 8192: 1240.0},
     # MX-fp8 GEMM, TFLOP/s.  8192^3 with the bf16-output kernel: 2,294-2,450 over a 6-minute level-2 burn-in
     # (median 2,402, profiles/diag_burn_in_level2_6min_bf16out_mi355x.json), 2,199 as the best of three on the
     # slowest box's cold node cycle (profiles/node_cycle_1gpu_mi355x.json) -> 2,300 puts that healthy run at
     # 0.956, above the degraded line (the fp32-output 2,380 left a slow healthy box degraded in most rounds)
     # v3's 2,210 / 2,300 times the same box's fp8 v4/v3 cold ratio, 2,377 / 2,269 = 1.047 (level 1) and 2,386 / 2,277
-    # = 1.048 (level 2), rounded down; its v4 soaks 2,373-2,438
-    "gemm_fp8": {4096: 2300.0, 8192: 2400.0},
+    # = 1.048 (level 2), rounded down; its v4 soaks 2,373-2,438.  8192^3 lowered from 2,400: the slow device 8e:00.0
+    # (2,318-2,332 at 4096^3, level 2 not measured) at the level-2 / level-1 ratio of the measured devices
+    # (0.99-1.0) would sit at 0.96-0.97 of 2,400 -> 2,350
+    "gemm_fp8": {4096: 2300.0, 8192: 2350.0},
     "hbm": {"copy_tbs": 6.49, "read_tbs": 6.96},   # 16-byte copy (read + write bytes counted) / read, TB/s
     # register-resident burn-in.  fp8 is the unscaled f8f6f4 instruction since round 4 (it was the gfx94x
     # v_mfma_f32_16x16x32_fp8_fp8, 1,940): 40 runs median 4,872 vs MX-fp8's 4,844 in the same runs, first (cold)
-    # run 4,058 (profiles/mfma_kinds_mi355x.json) -> MX-fp8's reference x 4,872 / 4,844
-    "mfma": {"bf16": 1901.0, "fp8": 4350.0, "mxfp8": 4326.0, "mxfp4": 7610.0},
+    # run 4,058 (profiles/mfma_kinds_mi355x.json) -> MX-fp8's reference x 4,872 / 4,844.  MX-fp4 lowered from 7,610:
+    # the slow device 8e:00.0 burns 6,977-7,035 (0.92, degraded) while its other kinds sit at 0.98-1.02 ->
+    # 6,977 / 0.97 -> 7,190 (d9:00.0: 7,982-8,259)
+    "mfma": {"bf16": 1901.0, "fp8": 4350.0, "mxfp8": 4326.0, "mxfp4": 7190.0},
     "host_link": {"h2d_gbps": 57.0, "d2h_gbps": 56.8},  # pinned copies over PCIe Gen5 x16
     # per-XCD HBM reads, 8 x 256 MiB slices (read 4x since profiles/hbm_xcd_passes_mi355x.json: lone-XCD
     # spread 0.994 at 4 passes vs 0.987 at 2, +5 ms); at 2 passes all XCDs together 5.83-6.27 TB/s (a cold level-2

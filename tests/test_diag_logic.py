@@ -81,7 +81,7 @@ def test_gpu_at_55_percent_is_unhealthy(fake):
     out = diag.run(1, 0)
     for t in ("gemm", "gemm_fp8", "hbm", "mfma"):
         assert out[t]["pass"] is False and out[t]["retried"] and 0.54 < out[t]["fraction"] < 0.56, out[t]
-    assert "tflops 754 TFLOP/s = 55% of 1.37e+03" in out["gemm"]["detail"]
+    assert "tflops 720 TFLOP/s = 55% of 1.31e+03" in out["gemm"]["detail"]
     v = _verdict(out)
     assert v.state == "unhealthy" and any("diag gemm failed" in r for r in v.reasons)
 

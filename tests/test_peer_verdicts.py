@@ -86,6 +86,19 @@ def test_one_gpu_at_080_of_its_peers_is_unhealthy_by_name(node):
     assert all(g["diag"]["gemm"]["pass"] for g in rep["gpus"] if g["index"] != 3)
 
 
+def test_a_gpu_at_the_reference_next_to_fast_peers_is_degraded_not_failed(node):
+    """Seven GPUs at 1.15 of the references and gpu2 at 0.96: gpu2 is at 83 % of its peers but at the MI355X
+    reference itself -- healthy devices differ this much (profiles/diag_box_spread_r05_mi355x.jsonl) -- so it is
+    degraded with the ratio in the detail, never unhealthy."""
+    node(8, rate=1.15, gpu_rate={2: 0.96})
+    rep = _agent(8).probe_once()
+    v = H.evaluate_report(rep, 8)
+    assert v.state == H.DEGRADED and not v.reasons and (v.gpus_ok, v.gpus_seen) == (8, 8)
+    g2 = next(g for g in rep["gpus"] if g["index"] == 2)["diag"]["gemm"]
+    assert g2["pass"] and g2["degraded"] and "itself at 96% of the MI355X reference" in g2["detail"], g2
+    assert g2["peers"]["ratio"]["tflops"] == pytest.approx(0.96 / 1.15, abs=0.01)
+
+
 def test_one_gpu_behind_peers_on_a_slow_platform_still_fails(node):
     """Peers at 0.90 of the references, gpu5 at 0.72: gpu5 fails (80 % of its peers) while the other seven
     share one node-level warning -- the slow platform excuses the node, not the outlier."""
@@ -261,7 +274,7 @@ _fracs = st.floats(min_value=0.05, max_value=1.6, allow_nan=False)
 def test_peer_judgement_properties(fracs, numerics_bad):
     """For any node: judging twice changes nothing; a GPU failing numerics always fails; a lone GPU gets the
     absolute verdict; a node-wide finding is reported only when no GPU of that metric was failed by the floor;
-    a GPU at or above its peers' median is never failed on rate."""
+    a GPU at or above its peers' median, or at or above the absolute degraded line, is never failed on rate."""
     def res(f, bad=False):
         return diag._rated({}, {"tflops": 1228.0 * f}, {"tflops": 1228.0}, "TFLOP/s", not bad, "wrong" if bad else "")
     pool = {d: {"gemm": res(f, numerics_bad and d == 0)} for d, f in enumerate(fracs)}
@@ -282,6 +295,8 @@ def test_peer_judgement_properties(fracs, numerics_bad):
         r = pool[d]["gemm"]
         if f >= others and not (numerics_bad and d == 0):
             assert r["pass"] or f < P.FAIL_FRACTION, (fracs, d, r)
+        if f >= P.DEGRADED_FRACTION and not (numerics_bad and d == 0):
+            assert r["pass"], (fracs, d, r)  # at the reference: never failed on rate, whatever the peers
     for f in f1:
         assert f["test"] == "gemm" and f["median_fraction"] < P.DEGRADED_FRACTION
         assert f["max_fraction"] <= P.NODE_UNIFORM_SPREAD * f["min_fraction"] + 1e-9
