@@ -280,6 +280,9 @@ def fleet(cluster: ClusterConnection, opts: CheckOptions, out: TextIO) -> int:
                          if row["platform_shortfall"] else "")
                       + ("  outliers: " + ", ".join(f"{o['node']} x{o['ratio']:.2f}" for o in row["outliers"])
                          if row["outliers"] else "")
+                      + ("  behind at the reference: " + ", ".join(f"{o['node']} x{o['ratio']:.2f}"
+                                                                   for o in row["behind_at_reference"])
+                         if row.get("behind_at_reference") else "")
                       + ("  slowest: " + ", ".join(f"{x['node']} {fmt(x['fraction'])}" for x in row.get("slowest", []))
                          if not row["outliers"] else "") + "\n")
     return res.exit_code

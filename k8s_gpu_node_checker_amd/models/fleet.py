@@ -14,7 +14,8 @@ checker has it -- one LIST carries every node's report:
 * **node outlier** -- a node whose median GPU is below ``FLEET_FAIL_RATIO`` of the median of the *other* nodes
   gets a ``degraded`` finding naming the fleet median: all of its GPUs are slow alike (else the agent would
   have singled one out), which is the node's condition -- cooling, power delivery, a BIOS setting -- and a
-  warning, never a failure.
+  warning, never a failure.  A node at or above the degraded line of the references gets no finding and is no
+  outlier (the rest of the fleet is fast, not it slow); the summary lists it under ``behind_at_reference``.
 
 It needs at least ``FLEET_MIN_NODES`` nodes with results for the same test, shape and metric, and it needs the
 reports themselves (``--health-reeval``, ``--probe-endpoint``, or nodes that publish no condition): on the
@@ -179,13 +180,18 @@ def judge_fleet(names: List[str], reports: List[Optional[Dict[str, Any]]],
             others = loo[i]
             ratio = v / others if others > 0 else 1.0
             if ratio < FLEET_FAIL_RATIO:
+                if not raw and v >= DEGRADED_FRACTION:
+                    # at the MI355X reference itself: the rest of the fleet is fast, this node is not slow
+                    # (healthy devices differ by up to ~14 %, profiles/diag_box_spread_r05_mi355x.jsonl)
+                    row.setdefault("behind_at_reference", []).append({"node": names[i], "ratio": round(ratio, 3)})
+                    continue
+                row["outliers"].append({"node": names[i], "ratio": round(ratio, 3)})
                 f = {"test": key[0], "metric": key[2], "ratio": round(ratio, 3), "nodes": len(vals) - 1}
                 if raw:
                     f.update(node_value=round(v, 1), fleet_value=round(others, 1))
                 else:
                     f.update(node_fraction=round(v, 3), fleet_fraction=round(others, 3))
                 view(i)["findings"].append(f)
-                row["outliers"].append({"node": names[i], "ratio": round(ratio, 3)})
             elif platform_short and max(v, med) <= FLEET_UNIFORM_SPREAD * min(v, med):
                 view(i)["explained"][key] = {"fleet_fraction": round(med, 3), "nodes": len(vals)}
         summary[summary_key(key)] = row

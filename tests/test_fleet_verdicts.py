@@ -69,6 +69,17 @@ def test_one_node_behind_the_fleet_is_degraded_by_name(reports):
     assert {"node": "slow", "ratio": 0.8} in summary["gemm@[4096, 4096, 4096]/tflops"]["outliers"]
 
 
+def test_a_node_at_the_reference_behind_a_fast_fleet_is_listed_not_degraded(reports):
+    """A fleet at 1.15 of the references and one node at 0.96: 83 % of the others, but at the MI355X reference
+    itself (healthy devices differ this much, profiles/diag_box_spread_r05_mi355x.jsonl) -- no degraded finding,
+    no outlier (the MI355XNodeBehindFleet alert counts outliers); the summary lists it as behind at the reference."""
+    reps = reports({"n0": 1.15, "n1": 1.15, "n2": 1.15, "ok": 0.96})
+    summary, verdicts = _judge(reps)
+    assert verdicts["ok"].state == H.HEALTHY and not [w for w in verdicts["ok"].warnings if w.startswith("fleet: ")]
+    row = summary["gemm@[4096, 4096, 4096]/tflops"]
+    assert row["outliers"] == [] and [o["node"] for o in row["behind_at_reference"]] == ["ok"]
+
+
 def test_a_node_behind_the_fleet_under_the_floor_fails(reports):
     """GPUs alike under the absolute failure line fail; the fleet names the node as well."""
     reps = reports({"n0": 1.0, "n1": 1.0, "n2": 1.0, "slow": 0.80})
