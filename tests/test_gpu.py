@@ -876,6 +876,13 @@ def test_lds_test_every_cu_and_injected_fault(dev):
 def test_hbm_per_xcd_together_and_alone(dev):
     from k8s_gpu_node_checker_amd.ops import diag
     r = diag.hbm_xcd(0)
+    # as the production run does (ops/diag.run): a slow-only result is measured again, the best kept -- one box
+    # showed a single XCD at 0.41x of the others once, and 1.33 TB/s like the rest in the next three runs
+    for _ in range(diag.REMEASURE):
+        if not diag._slow_only(r):
+            break
+        again = diag.hbm_xcd(0)
+        r = again if diag._goodness(again) > diag._goodness(r) else r
     print(json.dumps(r))
     assert r["pass"] and r["errors"] == 0, r
     info = diag.device_info(0)
