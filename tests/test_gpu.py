@@ -759,7 +759,7 @@ def test_p2p_diag_on_this_box(dev):
 def test_mfma_burn_every_precision(dev):
     """bf16 / fp8 / MX-fp8 / MX-fp4 matrix cores: exact results on every wave, rates above the floors."""
     from k8s_gpu_node_checker_amd.ops import diag
-    r = diag.mfma_burn(0)
+    r = _as_production(lambda: diag.mfma_burn(0))
     assert r["pass"], r
     k = r["kinds"]
     assert all(v["errors"] == 0 for v in k.values())
@@ -819,7 +819,7 @@ def test_mxfp8_gemm_identity_asymmetric(dev):
 
 def test_diag_gemm_fp8_burn_in(dev):
     from k8s_gpu_node_checker_amd.ops import diag
-    r = diag.gemm_fp8(0, size=4096, warmup=2, iters=5, samples=512)
+    r = _as_production(lambda: diag.gemm_fp8(0, size=4096, warmup=2, iters=5, samples=512))
     assert r["pass"], r
     assert r["max_err_over_mag"] < 4e-5 and r["tflops"] > 1200
 
@@ -873,16 +873,24 @@ def test_lds_test_every_cu_and_injected_fault(dev):
     assert bad["bad_cus"][0].endswith("(1 words)") and bad["bad_cus"][0].startswith("xcd"), bad
 
 
-def test_hbm_per_xcd_together_and_alone(dev):
+def _as_production(measure):
+    """A rate diagnostic as ``ops/diag.run`` takes it: a slow-only result (rate or one lagging XCD, numerics fine)
+    is measured again, up to REMEASURE times, the best kept.  One box showed a single XCD reading HBM at 0.41x
+    of the others once and 1.33 TB/s like the rest in the next three runs
+    (profiles/pytest_gpu_r05_hbm_xcd_transient.log)."""
     from k8s_gpu_node_checker_amd.ops import diag
-    r = diag.hbm_xcd(0)
-    # as the production run does (ops/diag.run): a slow-only result is measured again, the best kept -- one box
-    # showed a single XCD at 0.41x of the others once, and 1.33 TB/s like the rest in the next three runs
+    r = measure()
     for _ in range(diag.REMEASURE):
         if not diag._slow_only(r):
             break
-        again = diag.hbm_xcd(0)
+        again = measure()
         r = again if diag._goodness(again) > diag._goodness(r) else r
+    return r
+
+
+def test_hbm_per_xcd_together_and_alone(dev):
+    from k8s_gpu_node_checker_amd.ops import diag
+    r = _as_production(lambda: diag.hbm_xcd(0))
     print(json.dumps(r))
     assert r["pass"] and r["errors"] == 0, r
     info = diag.device_info(0)
@@ -895,7 +903,7 @@ def test_l2_bandwidth_per_xcd(dev):
     """Each XCD reads its own L2-resident slice: aggregate rate above the floor, every CU and XCD seen,
     no XCD lagging, every word intact."""
     from k8s_gpu_node_checker_amd.ops import diag
-    r = diag.l2_bandwidth(0)
+    r = _as_production(lambda: diag.l2_bandwidth(0))
     info = diag.device_info(0)
     assert r["pass"] and r["errors"] == 0 and r["map"]["cus"] == info["cus"], r
     if info["cus"] == 256:
