@@ -221,11 +221,18 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
             memory of its own normal."""
             from urllib.parse import parse_qs, urlsplit
             parts = urlsplit(self.path)
-            n = int(self.headers.get("Content-Length") or 0)
-            if n:
+            try:
+                n = int(self.headers.get("Content-Length") or 0)
+            except ValueError:
+                n = -1
+            if n > 0:
                 self.rfile.read(min(n, 65536))
+            if n < 0 or n > 65536:  # a malformed or oversized body: answer, then drop the connection
+                self.close_connection = True
             peer = self.client_address[0] if self.client_address else ""
-            if parts.path != "/baseline/reset":
+            if n < 0:
+                code, doc = 400, {"error": "bad Content-Length"}
+            elif parts.path != "/baseline/reset":
                 code, doc = 404, {"error": "not found"}
             elif not (peer.startswith("127.") or peer in ("::1", "::ffff:127.0.0.1")):
                 code, doc = 403, {"error": "baseline reset is only accepted from inside the pod (loopback)"}

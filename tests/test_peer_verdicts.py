@@ -467,6 +467,12 @@ def test_baselines_can_be_dropped_by_flag_and_by_a_loopback_post(node, tmp_path,
             urllib.request.urlopen(urllib.request.Request(url.replace("/baseline/reset", "/nope"), method="POST",
                                                           data=b""), timeout=5)
         assert e.value.code == 404
+        # a malformed Content-Length is a 400, not a crashed handler
+        import socket
+        with socket.create_connection(("127.0.0.1", srv.server_address[1]), timeout=5) as c:
+            c.sendall(b"POST /baseline/reset HTTP/1.1\r\nHost: x\r\nContent-Length: nope\r\n\r\n")
+            assert c.recv(4096).startswith(b"HTTP/1.1 400 ")
+        assert sorted(ag.baselines.data) == keys[1:]
     finally:
         srv.shutdown()
         srv.server_close()
