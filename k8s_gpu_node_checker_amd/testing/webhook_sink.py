@@ -23,7 +23,8 @@ The URL path selects the behaviour, so one sink serves every test:
 ``/loc/S/L``    status ``S`` with ``Location: L`` (percent-decoded; ``{port}`` becomes this sink's port; no header
                 when ``L`` is empty): relative, scheme-relative, query, fragment and foreign-scheme targets
 ``/body/KIND``   ``500`` with a UTF-8 body sent ``gzip`` / ``deflate`` / ``chunked``, as ``euckr`` or ``latin``
-                (no charset), with no length (``nolength``) or as ``octet`` (guessed)
+                (no charset), with no length (``nolength``), as ``octet`` (guessed), or labelled compressed but
+                sent plain (``badgzip`` / ``baddeflate``)
 ``/locb/S/L``   the same with ``L``'s percent-decoded bytes sent raw (a Location that is not UTF-8)
 ==============  =============================================================
 
@@ -90,6 +91,9 @@ class _SinkHandler(socketserver.BaseRequestHandler):
             body, head = "서버 오류".encode("euc-kr"), head + "Content-Type: text/plain; charset=euc-kr\r\n"
         elif kind == "latin":  # UTF-8 bytes labelled text/plain without a charset: ISO-8859-1 by requests' rule
             body, head = text, head + "Content-Type: text/plain\r\n"
+        elif kind in ("badgzip", "baddeflate"):  # labelled compressed, sent plain: the client cannot decode it
+            body = text
+            head += f"Content-Type: text/plain; charset=utf-8\r\nContent-Encoding: {kind[3:]}\r\n"
         elif kind == "nolength":  # no Content-Length: the body runs to the close
             body, head = text, head + "Content-Type: application/json\r\n"
             self.request.sendall(head.encode() + b"\r\n" + body)

@@ -485,13 +485,18 @@ def _decode_content(body: bytes, coding: str) -> bytes:
     as some servers send it), several codings applied in order listed; an unknown coding is left alone."""
     import zlib
     for c in reversed([c.strip() for c in coding.split(",") if c.strip()]):
-        if c in ("gzip", "x-gzip"):
-            body = zlib.decompress(body, 16 + zlib.MAX_WBITS)
-        elif c == "deflate":
-            try:
-                body = zlib.decompress(body)
-            except zlib.error:
-                body = zlib.decompress(body, -zlib.MAX_WBITS)
+        try:
+            if c in ("gzip", "x-gzip"):
+                body = zlib.decompress(body, 16 + zlib.MAX_WBITS)
+            elif c == "deflate":
+                try:
+                    body = zlib.decompress(body)
+                except zlib.error:
+                    body = zlib.decompress(body, -zlib.MAX_WBITS)
+        except zlib.error as e:
+            # urllib3's DecodeError (requests' ContentDecodingError) and its text; not a connection error
+            raise HTTPError("decode", str((f"Received response with content-encoding: {c}, but failed to decode it.",
+                                           e)), e)
     return body
 
 
