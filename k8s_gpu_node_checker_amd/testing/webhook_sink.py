@@ -25,6 +25,10 @@ The URL path selects the behaviour, so one sink serves every test:
 ``/body/KIND``   ``500`` with a UTF-8 body sent ``gzip`` / ``deflate`` / ``chunked``, as ``euckr`` or ``latin``
                 (no charset), with no length (``nolength``), as ``octet`` (guessed), or labelled compressed but
                 sent plain (``badgzip`` / ``baddeflate``)
+``/raw/NAME``   a malformed or unusual response: ``badstatus``, ``notahttp``, ``truncated`` (body shorter than its
+                length), ``badchunk``, ``truncatedchunk``, ``continue`` (100 then 200), ``http10``, ``longheader``,
+                ``twolengths``, ``empty200``, ``manyheaders``, ``justenoughheaders``, ``longstatus``,
+                ``prematurechunk``, ``badcl``, ``samecl``, ``status99``, ``chunkext``
 ``/locb/S/L``   the same with ``L``'s percent-decoded bytes sent raw (a Location that is not UTF-8)
 ==============  =============================================================
 
@@ -41,6 +45,31 @@ import threading
 import time
 import urllib.parse
 from typing import Any, Dict, List, Optional
+
+
+# /raw/NAME: responses that break HTTP in one way each (what a proxy or a broken endpoint may send)
+_RAW = {
+    "badstatus": b"HTTP/1.1 abc Whatever\r\nContent-Length: 2\r\n\r\nok",
+    "notahttp": b"hello there\r\n\r\n",
+    "truncated": b"HTTP/1.1 500 Internal Server Error\r\nContent-Length: 100\r\nConnection: close\r\n\r\nonly ten b",
+    "badchunk": b"HTTP/1.1 500 Internal Server Error\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\nzz\r\nabc\r\n0\r\n\r\n",
+    "truncatedchunk": b"HTTP/1.1 500 Internal Server Error\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n10\r\nabc",
+    "continue": b"HTTP/1.1 100 Continue\r\n\r\nHTTP/1.1 200 OK\r\nContent-Length: 2\r\nConnection: close\r\n\r\nok",
+    "http10": b"HTTP/1.0 200 OK\r\nContent-Type: text/plain\r\n\r\nok",
+    "longheader": b"HTTP/1.1 500 Internal Server Error\r\nX-Long: " + b"a" * 70000 + b"\r\nContent-Length: 2\r\n\r\nno",
+    "twolengths": b"HTTP/1.1 500 Internal Server Error\r\nContent-Length: 2\r\nContent-Length: 3\r\nConnection: close\r\n\r\nabc",
+    "empty200": b"HTTP/1.1 200 OK\r\nConnection: close\r\n\r\n",
+    "manyheaders": b"HTTP/1.1 500 Internal Server Error\r\n" + b"".join(b"X-%d: v\r\n" % i for i in range(100))
+                   + b"Content-Length: 2\r\n\r\nno",
+    "justenoughheaders": b"HTTP/1.1 500 Internal Server Error\r\n" + b"".join(b"X-%d: v\r\n" % i for i in range(98))
+                         + b"Content-Length: 2\r\n\r\nno",
+    "longstatus": b"HTTP/1.1 500 " + b"x" * 70000 + b"\r\nContent-Length: 2\r\n\r\nno",
+    "prematurechunk": b"HTTP/1.1 500 Internal Server Error\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n3\r\nabc\r\n",
+    "badcl": b"HTTP/1.1 500 Internal Server Error\r\nContent-Length: abc\r\nConnection: close\r\n\r\nbody",
+    "samecl": b"HTTP/1.1 500 Internal Server Error\r\nContent-Length: 3\r\nContent-Length: 3\r\nConnection: close\r\n\r\nabc",
+    "status99": b"HTTP/1.1 099 Odd\r\nContent-Length: 2\r\n\r\nno",
+    "chunkext": b"HTTP/1.1 500 Internal Server Error\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n3;x=y\r\nabc\r\n0\r\n\r\n",
+}
 
 
 class _SinkHandler(socketserver.BaseRequestHandler):
@@ -116,6 +145,11 @@ class _SinkHandler(socketserver.BaseRequestHandler):
         path = req["path"].split("?", 1)[0]
         if path.startswith("/body/"):  # a 500 whose body is encoded some way: /body/gzip, deflate, chunked, ...
             self._send_body(path[6:])
+            return
+        if path.startswith("/raw/"):  # a malformed or unusual response (see _RAW)
+            self.request.sendall(_RAW[path[5:]])
+            if path[5:] in ("truncated", "truncatedchunk"):
+                time.sleep(0.05)
             return
         if path.startswith("/locb/"):  # the Location's bytes as given (percent-decoded, not re-encoded)
             _, _, status, loc = req["path"].split("/", 3)

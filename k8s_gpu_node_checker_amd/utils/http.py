@@ -67,6 +67,33 @@ class Response:
         return self.body.decode("utf-8", "replace")
 
 
+class _Shown:
+    """An object whose repr is the given text (an exception as urllib3 nests it inside a tuple's str)."""
+    __slots__ = ("text",)
+
+    def __init__(self, text: str):
+        self.text = text
+
+    def __repr__(self) -> str:
+        return self.text
+
+
+def _broken(inner: str) -> str:
+    """urllib3's ``ProtocolError(f"Connection broken: {e!r}", e)`` as requests prints it (a body cut short or
+    malformed after the head arrived: not a connection error, never retried by the reference)."""
+    return str((f"Connection broken: {inner}", _Shown(inner)))
+
+
+def _aborted(inner: str) -> HTTPError:
+    """urllib3's ``ProtocolError('Connection aborted.', e)`` for a head http.client refused."""
+    return HTTPError("aborted", f"('Connection aborted.', {inner})")
+
+
+_MAXLINE = 65536   # http.client's limits on a status / header line (bytes, CRLF included) and on header lines
+_MAXHEADERS = 100
+_CRLF = b"\r\n"
+
+
 def _pool_name(scheme: str, host: str, port: int) -> str:
     pool = "HTTPSConnectionPool" if scheme == "https" else "HTTPConnectionPool"
     return f"{pool}(host='{host}', port={port})"
@@ -235,8 +262,7 @@ class Connection:
         while have < n:
             got = sock.recv_into(view[have:], n - have)
             if not got:
-                raise HTTPError("aborted", "('Connection aborted.', RemoteDisconnected("
-                                           "'Remote end closed connection without response'))")
+                raise HTTPError("incomplete", _broken(f"IncompleteRead({have} bytes read, {n - have} more expected)"))
             have += got
         return out  # bytearray: json.loads and the native scanner take it without a copy
 
@@ -378,18 +404,38 @@ class Connection:
             lines = bytes(buf[:end]).split(b"\r\n")
             del buf[:end + 4]
             status_line = lines[0]
+            # http.client's checks, with its exceptions' text (urllib3 reports them as 'Connection aborted.')
+            if len(status_line) + 2 > _MAXLINE:
+                raise _aborted("LineTooLong('got more than 65536 bytes when reading status line')")
             parts = status_line.split(None, 2)
-            if len(parts) < 2 or not parts[0].startswith(b"HTTP/") or not parts[1].isdigit():
-                raise HTTPError("protocol", f"bad status line {status_line[:80]!r}")
-            status = int(parts[1])
+            status = 0
+            if len(parts) >= 2 and parts[0].startswith(b"HTTP/"):
+                try:
+                    status = int(parts[1])
+                except ValueError:
+                    status = 0
+            if not 100 <= status <= 999:
+                shown = (status_line + _CRLF).decode("latin-1")
+                raise _aborted(f"BadStatusLine({shown!r})")
             reason = parts[2].decode("latin-1") if len(parts) > 2 else ""
+            if len(lines) > _MAXHEADERS:  # header lines + the blank one ending the head > 100 (lines[0]: status)
+                raise _aborted(f"HTTPException('got more than {_MAXHEADERS} headers')")
             headers: List[Tuple[str, str]] = []
+            hmap: Dict[str, str] = {}
             for line in lines[1:]:
+                if len(line) + 2 > _MAXLINE:
+                    raise _aborted("LineTooLong('got more than 65536 bytes when reading header line')")
                 k, _, v = line.partition(b":")
-                headers.append((k.decode("latin-1").strip(), v.decode("latin-1").strip()))
+                k, v = k.decode("latin-1").strip(), v.decode("latin-1").strip()
+                headers.append((k, v))
+                kl = k.lower()
+                if kl == "content-length" and kl in hmap:
+                    hmap[kl] += ", " + v  # urllib3's HTTPHeaderDict joins repeats; unmatching ones are refused
+                else:
+                    hmap[kl] = v
             if 100 <= status < 200 and status != 101:
                 continue  # 100-continue / 103 early hints: read the real response
-            return status, reason, headers, {k.lower(): v for k, v in headers}
+            return status, reason, headers, hmap
 
     def open_stream(self, method: str, path: str, headers: Optional[Dict[str, str]] = None,
                     read_timeout: Optional[float] = None) -> "Response | LineStream":
@@ -429,8 +475,8 @@ class Connection:
         elif "chunked" in hmap.get("transfer-encoding", "").lower():
             body = self._read_chunked(peek if 200 <= status < 300 else None,
                                       hmap.get("content-encoding", "").lower() == "gzip")
-        elif "content-length" in hmap:
-            n = int(hmap["content-length"])
+        elif "content-length" in hmap and _content_length(hmap["content-length"]) is not None:
+            n = _content_length(hmap["content-length"])
             if peek is not None and 200 <= status < 300 and n > 0:
                 self._peek_prefix(min(n, 4096), hmap.get("content-encoding", "").lower() == "gzip", peek)
             body = self._read_exact(n)
@@ -456,8 +502,17 @@ class Connection:
         out = []
         have = 0
         while True:
-            size_line = self._read_line()
-            size = int(size_line.split(b";", 1)[0].strip() or b"0", 16)
+            try:
+                size_line = self._read_line()
+            except HTTPError as e:
+                if e.kind == "aborted":  # urllib3: the body ended where a chunk size was due
+                    raise HTTPError("incomplete", "Response ended prematurely")
+                raise
+            try:
+                size = int(size_line.split(b";", 1)[0].strip() or b"0", 16)
+            except ValueError:
+                got = (size_line + b"\r\n").split(b";", 1)[0]
+                raise HTTPError("incomplete", _broken(f"InvalidChunkLength(got length {got!r}, {have} bytes read)"))
             if size == 0:
                 while self._read_line():  # trailers
                     pass
@@ -478,6 +533,25 @@ class Connection:
                 if prefix:
                     peek(prefix)
                 peek = None
+
+
+def _content_length(value: str) -> Optional[int]:
+    """urllib3's reading of Content-Length: repeats must agree (else ``InvalidHeader``), a value that is not a
+    non-negative integer means none (the body runs to the close)."""
+    if "," not in value:
+        try:
+            n = int(value)
+        except ValueError:
+            return None
+        return n if n >= 0 else None
+    try:
+        lengths = {int(v) for v in value.split(",")}
+    except ValueError:
+        return None
+    if len(lengths) > 1:
+        raise HTTPError("protocol", f"Content-Length contained multiple unmatching values ({value})")
+    n = lengths.pop()
+    return n if n >= 0 else None
 
 
 def _decode_content(body: bytes, coding: str) -> bytes:

@@ -372,6 +372,18 @@ def test_slack_error_body_decoding_identical(cluster, sink, kind):
         assert ra == rb and "(HTTP 500): " in b.stderr
 
 
+@pytest.mark.parametrize("kind", ["badstatus", "notahttp", "status99", "longstatus", "longheader", "manyheaders",
+                                  "justenoughheaders", "truncated", "badchunk", "truncatedchunk", "prematurechunk",
+                                  "chunkext", "twolengths", "samecl", "badcl", "continue", "http10", "empty200"])
+def test_slack_malformed_responses_identical(cluster, sink, kind):
+    """Responses that break HTTP one way each: the head http.client refuses ('Connection aborted.', retried), a
+    body cut short or badly chunked ('Connection broken: …', not retried), unmatching or invalid lengths, and
+    the unusual-but-valid ones (100 Continue, HTTP/1.0, an empty 200)."""
+    a, b, ra, rb = _transport_case(cluster, sink, sink.url("raw/" + kind), flags=["--slack-retry-count", "1"])
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert ra == rb
+
+
 def test_slack_read_timeout_identical(cluster):
     """A webhook slower than requests' 10 s timeout: the same `Read timed out. (read timeout=10)` line (one
     attempt each: about 20 s)."""
