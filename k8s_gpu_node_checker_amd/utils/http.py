@@ -188,6 +188,7 @@ class Connection:
             raise self._fail("refused" if e.errno in (errno.ECONNREFUSED, errno.EHOSTUNREACH,
                                                       errno.ENETUNREACH) else "aborted", url, e)
         sock.setsockopt(_socket.IPPROTO_TCP, _socket.TCP_NODELAY, 1)
+        handshake = False
         try:
             if self.proxy and self.scheme == "https":
                 self._tunnel(sock)
@@ -196,10 +197,16 @@ class Connection:
                 if ctx is None:
                     import ssl
                     ctx = ssl.create_default_context()
+                handshake = True
                 sock = ctx.wrap_socket(sock, server_hostname=self.server_hostname)
         except HTTPError:
             sock.close()
             raise
+        except _socket.timeout as e:
+            sock.close()
+            # a peer that never answers the handshake (a plain-HTTP port, a black hole): urllib3 reports the
+            # handshake's socket timeout as a read timeout
+            raise self._fail("timeout" if handshake else "tls", url, e)
         except OSError as e:
             sock.close()
             raise self._fail("tls", url, e)

@@ -393,6 +393,30 @@ def test_slack_read_timeout_identical(cluster):
     assert ra == rb and len(ra) == 1 and "Read timed out. (read timeout=10)" in b.stderr
 
 
+@pytest.mark.parametrize("tmpl", [
+    "{b}/200 ", "{b}/2 00", "{b}/200\n", "{b}/200\t", "HTTP://{hp}/200", "{b}", "{b}?x=1", "{b}/200#frag",
+    "http://user@{hp}/200", "http://:pw@{hp}/200", "{b}/%zz", "{b}/ä", "  {b}/200", "http://{hp}:/200",
+    "http://{hp}/../200", "http:/{hp}/200", "http:{hp}/200", "//{hp}/200", "{hp}/200", "http://{hp}/200?a=%",
+    "http://{hp}/a b?c d"])
+def test_slack_odd_webhook_urls_identical(cluster, sink, tmpl):
+    """Webhook URLs with blanks, control characters, case, missing parts, bad escapes and non-ASCII: requests'
+    URL preparation decides where the POST goes (or which error it is), and the CLI decides the same."""
+    host, port = sink.server_address[:2]
+    url = tmpl.format(b=f"http://{host}:{port}", hp=f"{host}:{port}")
+    a, b, ra, rb = _transport_case(cluster, sink, url, flags=["--slack-retry-count", "0"])
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert ra == rb
+
+
+def test_slack_https_to_a_plain_http_port_identical(cluster, sink):
+    """https to a port that speaks plain HTTP: the handshake never completes; requests reports the 10 s socket
+    timeout as `Read timed out.` (one attempt each: about 20 s)."""
+    host, port = sink.server_address[:2]
+    a, b, ra, rb = _transport_case(cluster, sink, f"hTTps://{host}:{port}/200", flags=["--slack-retry-count", "0"])
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert "Read timed out. (read timeout=10)" in b.stderr
+
+
 class _TLSSink(WebhookSink):
     """The webhook sink behind TLS with the session's self-signed certificate (127.0.0.1 / localhost)."""
 
