@@ -482,8 +482,7 @@ class Connection:
         elif "chunked" in hmap.get("transfer-encoding", "").lower():
             body = self._read_chunked(peek if 200 <= status < 300 else None,
                                       hmap.get("content-encoding", "").lower() == "gzip")
-        elif "content-length" in hmap and _content_length(hmap["content-length"]) is not None:
-            n = _content_length(hmap["content-length"])
+        elif "content-length" in hmap and (n := _content_length(hmap["content-length"])) is not None:
             if peek is not None and 200 <= status < 300 and n > 0:
                 self._peek_prefix(min(n, 4096), hmap.get("content-encoding", "").lower() == "gzip", peek)
             body = self._read_exact(n)
