@@ -803,6 +803,25 @@ __device__ __forceinline__ void v4_dma_imm(uint32_t m0_base, uint32_t voff, cons
                : "memory");
 }
 
+// The grouped form (lab: gemm_v4_kernel<..., M0G = true>): the buffer instruction's immediate offset is added to
+// the global address and to the LDS destination, so four DMAs 1 KiB apart in LDS share one m0 -- the group's first
+// sets it (SET), the other three carry OFF = 1, 2, 3 KiB (the 12-bit field's reach) and per-row VGPR offsets
+// reduced by OFF.  The later ones rely on m0 surviving the MFMA / ds_read statements in between.
+template <uint32_t IMM, uint32_t OFF, bool SET>
+__device__ __forceinline__ void v4_dma_grouped(uint32_t m0_base, uint32_t voff, const i32x4& rsrc, uint32_t soff) {
+  if constexpr (SET) {
+    asm volatile("s_add_u32 m0, %0, %1\n\tbuffer_load_dwordx4 %2, %3, %4 offen offset:%5 lds"
+                 :
+                 : "s"(m0_base), "i"(IMM), "v"(voff), "s"(rsrc), "s"(soff), "i"(OFF)
+                 : "memory");
+  } else {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds"
+                 :
+                 : "v"(voff), "s"(rsrc), "s"(soff), "i"(OFF)
+                 : "memory");
+  }
+}
+
 __device__ __forceinline__ i32x4 v4_rsrc(const void* base, uint32_t bytes) {
   const uint64_t b = reinterpret_cast<uint64_t>(base);
   i32x4 r;
@@ -899,7 +918,8 @@ __device__ __forceinline__ void v4_piece8(V4F8Frags& g, const uint32_t (&ha)[2],
   if constexpr (!is_b) v4_read4<blk * 2048>(h ? g.ahi[blk] : g.alo[blk], ha[h]);
   else v4_read4<blk * 2048>(h ? g.bhi[blk] : g.blo[blk], hb[h]);
 }
-template <int OUT = OUT_F32, class PLAN = V4PlanA<1, 20, 8, 8, 2>, int GM = 4, bool TR = false, int DT = DT_BF16>
+template <int OUT = OUT_F32, class PLAN = V4PlanA<1, 20, 8, 8, 2>, int GM = 4, bool TR = false, int DT = DT_BF16,
+          bool M0G = false>
 __global__ void __launch_bounds__(V4_THREADS, 1)
 gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv,
                double* __restrict__ csum, int M, int N, int K) {
@@ -907,6 +927,7 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
   static_assert(DT == DT_BF16 || DT == DT_FP8U, "v4: bf16 or fp8 (unscaled MFMA)");
   if constexpr (FP8) static_assert(v4f8_plan_ok<PLAN>(), "v4 fp8 plan breaks a read / DMA / barrier ordering rule");
   else static_assert(v4_plan_ok<PLAN>(), "v4 schedule plan breaks a read / DMA / barrier ordering rule");
+  static_assert(!M0G || v4_m0_groups_ok<PLAN>(), "grouped m0: each group of 4 DMAs must be issued in order, back to back");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages x 64 KiB
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the DMA's m0 is an SGPR
@@ -943,13 +964,18 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int row = wid * 64 + 8 * r + rsub;
-      voff_r[r] = static_cast<uint32_t>((row * K + (phys ^ swz_row_xor(row, FP8)) * 8) * 2);
+      voff_r[r] = static_cast<uint32_t>((row * K + (phys ^ swz_row_xor(row, FP8)) * 8) * 2) -
+                  (M0G ? static_cast<uint32_t>((r & 3) * 8 * (BK * 2)) : 0u);
     }
   }
   auto dma = [&](auto S, auto J, uint32_t soff) {
     constexpr int s = decltype(S)::value, j = decltype(J)::value, op = j >> 3, r = j & 7;
-    v4_dma_imm<s * V2_STAGE_BYTES + op * (V2_BM * BK * 2) + r * 8 * (BK * 2)>(m0_wave, voff_r[r], op ? rs_b : rs_a,
-                                                                                soff);
+    if constexpr (M0G)
+      v4_dma_grouped<s * V2_STAGE_BYTES + op * (V2_BM * BK * 2) + (r >> 2) * 4 * 8 * (BK * 2), (r & 3) * 8 * (BK * 2),
+                     (r & 3) == 0>(m0_wave, voff_r[r], op ? rs_b : rs_a, soff);
+    else
+      v4_dma_imm<s * V2_STAGE_BYTES + op * (V2_BM * BK * 2) + r * 8 * (BK * 2)>(m0_wave, voff_r[r],
+                                                                                  op ? rs_b : rs_a, soff);
   };
 
   // fragment reads: lane (frow, fq); k-step 1 is chunk ^ 4

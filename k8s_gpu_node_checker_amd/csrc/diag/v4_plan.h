@@ -216,4 +216,18 @@ constexpr bool v4f8_plan_ok() {
   return true;
 }
 
+// Grouped m0 (gemm_v4_kernel<..., M0G>): DMA pieces 4g .. 4g+3 share one m0, set by piece 4g, so within a
+// K-tile every piece 4g+t (t > 0) must be the next DMA issued after piece 4g+t-1 (slot order, 128 slots).
+template <class P>
+constexpr bool v4_m0_groups_ok() {
+  int prev = -1;
+  for (int i = 0; i < 128; ++i) {
+    const int d = P::at(i).dma;
+    if (d < 0) continue;
+    if ((d & 3) != 0 && prev != d - 1) return false;
+    prev = d;
+  }
+  return true;
+}
+
 #endif  // K8S_GPU_NODE_CHECKER_AMD_V4_PLAN_H_

@@ -66,6 +66,16 @@ struct MoveDmaP {
     return o;
   }
 };
+// exchange the DMA pieces of slots A and B
+template <class P, int A, int B>
+struct SwapDma {
+  static constexpr V4Slot at(int i) {
+    V4Slot o = P::at(i);
+    if (i == A) o.dma = P::at(B).dma;
+    if (i == B) o.dma = P::at(A).dma;
+    return o;
+  }
+};
 using F8 = V4PlanF8<8, 10, 26, 27, 42>;
 }  // namespace
 
@@ -91,7 +101,10 @@ int main() {
   // the next tile's A0-3 read moved to slot 45, before quadrant 2's last MFMA on A0-3 (slot 47)
   std::printf("\"fp8_next_a_early\": %d,", v4f8_plan_ok<MoveRead<F8, 51, 45>>());
   // a B DMA (slot 27) moved before barrier X2 (slot 26) retires this tile's B4-7 reads
-  std::printf("\"fp8_b_dma_before_x2\": %d", v4f8_plan_ok<MoveDmaP<F8, 27, 17>>());
+  std::printf("\"fp8_b_dma_before_x2\": %d,", v4f8_plan_ok<MoveDmaP<F8, 27, 17>>());
+  // grouped m0 (lab): plan A issues its DMA pieces in order; swapping two pieces of a group breaks it
+  std::printf("\"m0_groups_shipped\": %d,", v4_m0_groups_ok<Good>());
+  std::printf("\"m0_groups_swapped\": %d", v4_m0_groups_ok<SwapDma<Good, 25, 30>>());
   std::printf("}\n");
   return 0;
 }
@@ -115,11 +128,12 @@ def verdicts(tmp_path_factory):
 def test_shipped_plans_pass_their_checks(verdicts):
     assert verdicts["shipped_bf16"] == 1 and verdicts["shipped_fp8"] == 1
     assert verdicts["a2"] == 1 and verdicts["hipblaslt_order"] == 1
+    assert verdicts["m0_groups_shipped"] == 1
 
 
 @pytest.mark.parametrize("broken", ["dma_before_x", "next_read_before_y", "f1_read_after_x", "wrong_vmcnt",
                                     "missing_dma", "missing_read", "fp8_late_y", "fp8_next_a_early",
-                                    "fp8_b_dma_before_x2"])
+                                    "fp8_b_dma_before_x2", "m0_groups_swapped"])
 def test_broken_plans_are_rejected(verdicts, broken):
     assert verdicts[broken] == 0, broken
 

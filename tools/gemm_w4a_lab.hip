@@ -45,16 +45,16 @@ double time_ms(L launch, int iters) {
   return ms / iters;
 }
 
-template <class PLAN, int GM = 4, bool TR = false>
+template <class PLAN, int GM = 4, bool TR = false, bool M0G = false>
 void launch_plan(const __bf16* A, const __bf16* Bt, float* C, int M, int N, int K) {
   static bool once = [] {
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<OUT_F32, PLAN, GM, TR>),
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_v4_kernel<OUT_F32, PLAN, GM, TR, DT_BF16, M0G>),
                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE_BYTES));
     return true;
   }();
   (void)once;
-  hipLaunchKernelGGL((gemm_v4_kernel<OUT_F32, PLAN, GM, TR>), dim3((M / V2_BM) * (N / V2_BN)), dim3(V4_THREADS),
-                     2 * V2_STAGE_BYTES, nullptr, A, Bt, C, nullptr, M, N, K);
+  hipLaunchKernelGGL((gemm_v4_kernel<OUT_F32, PLAN, GM, TR, DT_BF16, M0G>), dim3((M / V2_BM) * (N / V2_BN)),
+                     dim3(V4_THREADS), 2 * V2_STAGE_BYTES, nullptr, A, Bt, C, nullptr, M, N, K);
 }
 
 // fp8 (K in bytes; the kernels take bf16 columns = bytes / 2)
@@ -175,6 +175,11 @@ int main(int argc, char** argv) {
     } else {
     rows.push_back({"v3(diag,lds-epi)", [&] { launch_v3<DT_BF16>(A, Bt, C1, M, N, K, nullptr); }});
     rows.push_back({"w4a rs1 x20 d8 y8", [&] { launch_w4a<1, 20, 8, 8, 4>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"w4a rs1 x20 d8 y8 m0-grouped", [&] {
+                      launch_plan<V4PlanA<1, 20, 8, 8, 2>, 4, false, true>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"w4a rs1 x20 d8 y8 #2", [&] { launch_w4a<1, 20, 8, 8, 4>(A, Bt, C1, M, N, K); }});
+    rows.push_back({"w4a rs1 x20 d8 y8 m0-grouped #2", [&] {
+                      launch_plan<V4PlanA<1, 20, 8, 8, 2>, 4, false, true>(A, Bt, C1, M, N, K); }});
     rows.push_back({"w4a rs1 x20 d8 y8 TR", [&] { launch_w4a<1, 20, 8, 8, 4, 2, true>(A, Bt, C1, M, N, K); }});
     rows.push_back({"w4a rs1 x24 d8 y8", [&] { launch_w4a<1, 24, 8, 8, 4>(A, Bt, C1, M, N, K); }});
     rows.push_back({"w4a rs1 x20 d8 y4", [&] { launch_w4a<1, 20, 8, 4, 4>(A, Bt, C1, M, N, K); }});
