@@ -70,6 +70,17 @@ def test_same_output_same_exit_code(cluster, name, flags):
     assert a.stderr == b.stderr == ""
 
 
+@pytest.mark.parametrize("flags", [[], ["--json"]])
+def test_large_paged_cluster_identical(cluster, flags):
+    """2,500 mixed nodes (every 7th NotReady): the CLI pages the LIST (limit 500, five pages) and scans it natively,
+    the reference takes one unpaginated LIST; stdout and exit code are byte-identical."""
+    nodes = fixtures.cluster(2500, "mixed", not_ready=list(range(0, 2500, 7)))
+    kc = cluster(nodes)
+    a, b = run_ref(["--kubeconfig", kc] + flags), run_new(["--kubeconfig", kc] + flags)
+    assert (a.returncode, a.stderr) == (b.returncode, b.stderr) == (0, "")
+    assert a.stdout == b.stdout and len(a.stdout) > 100_000
+
+
 def test_help_and_usage_error_identical():
     a, b = run_ref(["--help"]), run_new(["--help"])
     assert (a.returncode, a.stdout) == (b.returncode, b.stdout)
