@@ -94,9 +94,9 @@ REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
     # That box is a slow one (v3 at 0.95 of its old reference); its v4 soaks: level 2, 322 rounds, 1300-1326, level 1,
     # 669 rounds, 1309-1332 (profiles/soak_l{1,2}_v4_mi355x.json).  Lowered from 1,370 / 1,330 after a slower
     # healthy device (8e:00.0 above) measured 1,278-1,280 cold at 4096^3 (0.93: degraded): 1,280 / 0.97 -> 1,310.
-    # Its 8192^3 rate was not measured (the pool did not hand it out again); level 2 / level 1 is 0.94-0.99 on
-    # the two devices that were (d9: 1,355-1,405 / 1,457-1,487; the calibration box above), so 1,203-1,267
-    # expected -> 1,240 puts even the low end at 0.97.  d9 sits at 1.12-1.13 of both.
+    # Its 8192^3 rate was not measured (the pool did not hand it out again); level 2 / level 1 is 0.93-0.99 on
+    # the devices that were (d9, 26, 5d: 1,355-1,405 at level 2 against 1,419-1,487 at level 1; the calibration
+    # box above), so 1,190-1,267 expected -> 1,240 puts even the low end at 0.96.  The others sit at 1.08-1.13.
     "gemm": {4096: 1310.0, 8192: 1240.0},
     # MX-fp8 GEMM, TFLOP/s.  8192^3 with the bf16-output kernel: 2,294-2,450 over a 6-minute level-2 burn-in
     # (median 2,402, profiles/diag_burn_in_level2_6min_bf16out_mi355x.json), 2,199 as the best of three on the
