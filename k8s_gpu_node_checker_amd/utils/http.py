@@ -179,19 +179,19 @@ class Connection:
         try:
             sock = _connect(target, self.timeout, plain=self.scheme != "https")
         except _socket.timeout as e:
-            raise self._fail("connect_timeout", url, e)
+            raise self._fail("connect_timeout", url, e) if not self.proxy else self._proxy_down("connect_timeout", url, e)
         except _socket.gaierror as e:
-            raise self._fail("dns", url, e)
+            raise self._fail("dns", url, e) if not self.proxy else self._proxy_down("dns", url, e)
         except ConnectionRefusedError as e:
-            raise self._fail("refused", url, e)
+            raise self._fail("refused", url, e) if not self.proxy else self._proxy_down("refused", url, e)
         except OSError as e:
-            raise self._fail("refused" if e.errno in (errno.ECONNREFUSED, errno.EHOSTUNREACH,
-                                                      errno.ENETUNREACH) else "aborted", url, e)
+            kind = "refused" if e.errno in (errno.ECONNREFUSED, errno.EHOSTUNREACH, errno.ENETUNREACH) else "aborted"
+            raise self._fail(kind, url, e) if not self.proxy or kind == "aborted" else self._proxy_down(kind, url, e)
         sock.setsockopt(_socket.IPPROTO_TCP, _socket.TCP_NODELAY, 1)
         handshake = False
         try:
             if self.proxy and self.scheme == "https":
-                self._tunnel(sock)
+                self._tunnel(sock, url)
             if self.scheme == "https":
                 ctx = self.ssl_context
                 if ctx is None:
@@ -221,7 +221,33 @@ class Connection:
         cred = f"{self.proxy.username}:{self.proxy.password or ''}".encode("latin-1")
         return f"Proxy-Authorization: Basic {base64.b64encode(cred).decode('ascii')}\r\n"
 
-    def _tunnel(self, sock: "socket.socket") -> None:
+    def _proxy_error(self, url: str, inner: str) -> HTTPError:
+        """urllib3's MaxRetryError(ProxyError('Unable to connect to proxy', e)) text, as requests prints it."""
+        pool = _pool_name(self.scheme, self.host, self.port)
+        return HTTPError("proxy", f"{pool}: Max retries exceeded with url: {url} (Caused by ProxyError('Unable to "
+                                  f"connect to proxy', {inner}))")
+
+    def _proxy_down(self, kind: str, url: str, e: BaseException) -> HTTPError:
+        """The proxy itself unreachable, as urllib3 words it: ``ProxyError('Unable to connect to proxy', <the
+        connection error naming the proxy>)``, under the target's pool for a tunnel (https) and under the proxy's
+        own pool, with the absolute URL, for a forwarded http request."""
+        assert self.proxy is not None
+        phost, pport = self.proxy.hostname or "", self.proxy.port or 80
+        conn = f"{'HTTPSConnection' if self.scheme == 'https' else 'HTTPConnection'}(host={phost!r}, port={pport!r})"
+        if kind == "dns":
+            inner = f"NameResolutionError({conn + ': ' + f'Failed to resolve {phost!r} ({e})'!r})"
+        elif kind == "connect_timeout":
+            inner = (f"ConnectTimeoutError({conn!r}, 'Connection to {phost} timed out. (connect timeout="
+                     f"{self.timeout:g})')")
+        else:
+            inner = f"NewConnectionError({conn + ': Failed to establish a new connection: ' + str(e)!r})"
+        if self.scheme == "https":
+            return self._proxy_error(url, inner)
+        pool = _pool_name("http", phost, pport)
+        return HTTPError("proxy", f"{pool}: Max retries exceeded with url: http://{self.host_header}{self.base_path}"
+                                  f"{url} (Caused by ProxyError('Unable to connect to proxy', {inner}))")
+
+    def _tunnel(self, sock: "socket.socket", url: str = "/") -> None:
         req = (f"CONNECT {self.host}:{self.port} HTTP/1.1\r\nHost: {self.host}:{self.port}\r\n"
                f"{self._proxy_auth()}\r\n").encode("latin-1")
         sock.sendall(req)
@@ -229,12 +255,15 @@ class Connection:
         while b"\r\n\r\n" not in data:
             chunk = sock.recv(4096)
             if not chunk:
-                raise HTTPError("protocol", "proxy closed the CONNECT tunnel")
+                raise self._proxy_error(url, "RemoteDisconnected('Remote end closed connection without response')")
             data += chunk
         first = data.split(b"\r\n", 1)[0]
-        status = first.split()
-        if len(status) < 2 or status[1] != b"200":
-            raise HTTPError("protocol", "proxy CONNECT failed: " + first.decode(errors="replace"))
+        status = first.split(None, 2)
+        code = int(status[1]) if len(status) >= 2 and status[1].isdigit() else 0
+        if code != 200:
+            # http.client's _tunnel: OSError("Tunnel connection failed: <code> <reason>")
+            reason = status[2].decode("latin-1").strip() if len(status) > 2 else ""
+            raise self._proxy_error(url, repr(OSError(f"Tunnel connection failed: {code} {reason}")))
 
     def close(self) -> None:
         if self.sock is not None:

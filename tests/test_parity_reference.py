@@ -468,6 +468,24 @@ def test_slack_https_verification_identical(cluster, tls_sink, certs, host, env)
         assert not ra and "CERTIFICATE_VERIFY_FAILED" in b.stderr
 
 
+@pytest.mark.parametrize("proxy,url", [
+    ("HTTPS_PROXY=SINK", "https://example.invalid/200"),               # CONNECT refused by the proxy (404)
+    ("https_proxy=SINK", "https://example.invalid/200"),
+    ("HTTPS_PROXY=http://127.0.0.1:1", "https://example.invalid/200"),  # the proxy itself refuses
+    ("HTTP_PROXY=http://127.0.0.1:1", "http://example.invalid:8080/a/b?c=d"),
+    ("HTTPS_PROXY=http://no-such-proxy.invalid:3128", "https://example.invalid/200"),  # the proxy does not resolve
+    ("HTTP_PROXY=http://no-such-proxy.invalid:3128", "http://example.invalid/200"),
+])
+def test_slack_proxy_failures_identical(cluster, sink, proxy, url):
+    """A proxy that refuses the tunnel, refuses the connection or does not resolve: urllib3's ProxyError text,
+    under the target's pool for a tunnel and the proxy's own pool (absolute URL) for a forwarded request."""
+    k, v = proxy.split("=", 1)
+    e = {k: sink.base_url if v == "SINK" else v, "NO_PROXY": "127.0.0.1"}
+    a, b, ra, rb = _transport_case(cluster, sink, url, env=e, flags=["--slack-retry-count", "0"])
+    assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+    assert ra == rb and "ProxyError('Unable to connect to proxy', " in b.stderr
+
+
 def test_slack_url_credentials_identical(cluster, sink, tmp_path):
     host, port = sink.server_address[:2]
     for url in (f"http://user:pass@{host}:{port}/200", f"http://us%40er:p%3Ass@{host}:{port}/to/localhost/200"):
