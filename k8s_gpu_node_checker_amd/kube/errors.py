@@ -51,8 +51,10 @@ class TransportError(Exception):
         self.cause = cause
         pool = "HTTPSConnectionPool" if scheme == "https" else "HTTPConnectionPool"
         text = str(cause)
-        if text.startswith(f"{pool}(host=") and ": Max retries exceeded with url: " in text:
-            # the transport already rendered the urllib3 message (utils/http.py: refused, DNS, connect timeout, TLS)
+        if text.startswith(("HTTPConnectionPool(host=", "HTTPSConnectionPool(host=")) and \
+                ": Max retries exceeded with url: " in text:
+            # the transport already rendered the urllib3 message (utils/http.py: refused, DNS, connect timeout, TLS,
+            # a proxy's failure -- whose pool may be the proxy's)
             super().__init__(text)
             return
         super().__init__(f"{pool}(host='{host}', port={port}): Max retries exceeded with url: {url} "
