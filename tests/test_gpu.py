@@ -408,7 +408,7 @@ def test_gemm_rejects_bad_shapes():
 
 def test_diag_gemm_burn_in(dev):
     from k8s_gpu_node_checker_amd.ops import diag
-    r = diag.gemm(0, size=4096, warmup=2, iters=10, samples=512)
+    r = _as_production(lambda: diag.gemm(0, size=4096, warmup=2, iters=10, samples=512))
     print(json.dumps(r))
     assert r["max_rel_err"] < diag.GEMM_MAX_REL_ERR
     assert r["pass"], r
@@ -416,7 +416,7 @@ def test_diag_gemm_burn_in(dev):
 
 def test_diag_hbm_bandwidth(dev):
     from k8s_gpu_node_checker_amd.ops import diag
-    r = diag.hbm(0, gib=2.0, iters=5)
+    r = _as_production(lambda: diag.hbm(0, gib=2.0, iters=5))
     print(json.dumps(r))
     assert r["pass"], r
     assert r["copy_tbs"] < 8.5  # cannot beat the 8 TB/s HBM3E spec (sanity of the timing)
@@ -498,7 +498,7 @@ def test_diag_failed_allocation_leaks_nothing(dev):
         assert L.diag_gemm_bf16(0, m, m, 1024, 0, 1, 16, *(ctypes.byref(x) for x in d)) == -1
     free1, _ = torch.cuda.mem_get_info(0)
     assert free0 - free1 < (256 << 20), (free0, free1)
-    r = diag.hbm(0, gib=0.5, iters=2)  # and the next call runs clean
+    r = _as_production(lambda: diag.hbm(0, gib=0.5, iters=2))  # and the next call runs clean
     assert r["pass"], r
 
 
