@@ -28,7 +28,15 @@ timed loop never waits on any of them.  Every phase's wall time is in the line (
 timed step's milliseconds go -- connect, first byte, body, scan, health gate, render -- as medians
 (``step_ms``).
 
-Prints ONE JSON line (rank 0): value = nodes/s over the whole job.
+Node-count curve (``curve``; rank 0, after the headline, others at the closing barrier): the same check, same
+``--steps`` / ``--warmup``, against one mock cluster per node count of ``--curve`` (1/2/4/8/16/1000; each server
+started with the headline's, before any GPU work, its nodes carrying the recorded MI355X probe annotation).  Every
+row -- the headline's own is one -- has ms per check, nodes/s, the survey proxy's ms at that count
+(``baseline_basis``: a different machine), ``vs_baseline``, and ``checker_ms``: the checker's own part of a check
+(scan + client + health + render + other), apart from ``transport_ms`` (connect + first byte + body: the socket
+and the mock's time).
+
+Prints ONE JSON line (rank 0): value = nodes/s over the whole job (headline node count = GPUs).
 """
 
 from __future__ import annotations
@@ -49,14 +57,39 @@ REF_MS = {1: 2.17, 2: 1.68, 4: 1.74, 8: 2.30, 16: 2.23, 1000: 92.7}
 REF_MS_SLACK = {1: 4.43, 2: 4.02, 4: 3.08, 8: 3.08, 16: 3.57, 1000: 86.1}
 
 
-def _spawn(module: str, *args: str) -> "tuple[subprocess.Popen, dict]":
+def _start(module: str, *args: str) -> subprocess.Popen:
     env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
-    proc = subprocess.Popen([sys.executable, "-m", module, *args], stdout=subprocess.PIPE, env=env, text=True)
+    return subprocess.Popen([sys.executable, "-m", module, *args], stdout=subprocess.PIPE, env=env, text=True)
+
+
+def _ready(proc: subprocess.Popen, module: str) -> dict:
+    """The first stdout line of a started control-plane process (its URL), once it is serving."""
     assert proc.stdout is not None
     line = proc.stdout.readline()
     if not line:
         raise RuntimeError(f"{module} failed to start")
-    return proc, json.loads(line)
+    return json.loads(line)
+
+
+def _spawn(module: str, *args: str) -> "tuple[subprocess.Popen, dict]":
+    proc = _start(module, *args)
+    return proc, _ready(proc, module)
+
+
+MOCK = "k8s_gpu_node_checker_amd.testing.mock_apiserver"
+# the BASELINE metric's node counts (1/2/4/8) plus the survey's 16 and 1000-node proxy points (SURVEY §6)
+CURVE_NODES = "1,2,4,8,16,1000"
+BASELINE_BASIS = ("SURVEY §6 proxy: the unmodified reference (check-gpu-node.py:215-293) with a stub kubernetes "
+                  "client, in-process one_shot median, 8-vCPU Xeon VM -- a different machine from this run")
+
+
+def _curve_servers(sizes: "list[int]") -> "tuple[list, dict]":
+    """One mock apiserver per curve point, all started at once (before any GPU work): ``n`` realistic MI355X
+    nodes (``amd.com/gpu: 1``) carrying the recorded probe annotation and condition the DaemonSet writes
+    (gzip-encoded), so every node goes through the same health gate as the headline's live ones."""
+    started = [(n, _start(MOCK, "--nodes", str(n), "--kind", "amd", "--gpus-per-node", "1",
+                          "--annotation-encoding", "gzip", "--with-health")) for n in sizes]
+    return [p for _, p in started], {n: _ready(p, MOCK)["url"] for n, p in started}
 
 
 def _own_gpu(gpus, local_rank, cuda):
@@ -189,23 +222,70 @@ def _step_breakdown(spans: list, lat: list) -> "dict | None":
     ``connect`` (TCP to the apiserver), ``first_byte`` (LIST sent to response head: the server's time),
     ``body`` (the rest of the response), ``scan`` (NodeList scan), ``client`` (the rest of the LIST call:
     client setup, headers, close), ``health`` (MI355X gate), ``render`` (JSON), ``other`` (what the step spent
-    outside those: Slack join when on, GC switch, the output sink)."""
+    outside those: Slack join when on, GC switch, the output sink).
+
+    ``checker`` is the checker's own cost -- scan + client + health + render + other, summed per step -- and
+    ``transport`` the rest (connect + first_byte + body: the socket and the mock apiserver's time), so a
+    comparison across boxes or rounds can tell the code's milliseconds from the mock's."""
     if not spans or len(spans) != len(lat):
         return None
     rows = []
     for sp, total in zip(spans, lat):
         g = sp.get
         lst = g("list", 0.0)
-        rows.append({"connect": g("connect", 0.0), "first_byte": g("first_byte", 0.0), "body": g("body", 0.0),
-                     "scan": g("parse", 0.0),
-                     "client": lst - g("connect", 0.0) - g("first_byte", 0.0) - g("body", 0.0) - g("parse", 0.0),
-                     "health": g("health", 0.0), "render": g("render", 0.0),
-                     "other": total - lst - g("health", 0.0) - g("render", 0.0)})
+        r = {"connect": g("connect", 0.0), "first_byte": g("first_byte", 0.0), "body": g("body", 0.0),
+             "scan": g("parse", 0.0),
+             "client": lst - g("connect", 0.0) - g("first_byte", 0.0) - g("body", 0.0) - g("parse", 0.0),
+             "health": g("health", 0.0), "render": g("render", 0.0),
+             "other": total - lst - g("health", 0.0) - g("render", 0.0)}
+        r["transport"] = r["connect"] + r["first_byte"] + r["body"]
+        r["checker"] = total - r["transport"]
+        rows.append(r)
     out = {k: round(_pctl([r[k] for r in rows], 0.5) * 1e3, 4) for k in rows[0]}
     if any("slack" in sp for sp in spans):
         out["slack"] = round(_pctl([sp.get("slack", 0.0) for sp in spans], 0.5) * 1e3, 4)
     out["step"] = round(_pctl(lat, 0.5) * 1e3, 4)
     return out
+
+
+def _timed_checks(cluster, opts, steps: int, warmup: int) -> "tuple[float, list, list, object]":
+    """``warmup`` untimed then ``steps`` timed ``check_and_report`` calls against ``cluster`` (the bench step):
+    (elapsed s, per-step latencies, per-step tracer spans, the last result)."""
+    from k8s_gpu_node_checker_amd.checker import check_and_report
+    from k8s_gpu_node_checker_amd.utils.timing import Tracer
+    sink_out, sink_err = io.StringIO(), io.StringIO()
+    last = None
+    for _ in range(warmup):
+        sink_out.seek(0)
+        sink_out.truncate()
+        last = check_and_report(cluster, opts, out=sink_out, err=sink_err)
+    lat, spans = [], []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sink_out.seek(0)
+        sink_out.truncate()
+        s = time.perf_counter()
+        tr = Tracer()
+        last = check_and_report(cluster, opts, out=sink_out, err=sink_err, tracer=tr)
+        lat.append(time.perf_counter() - s)
+        spans.append(tr.spans)
+    return time.perf_counter() - t0, lat, spans, last
+
+
+def curve_row(nodes: int, elapsed: float, steps: int, lat: list, spans: list, last, slack: bool,
+              annotations: str) -> dict:
+    """One point of the node-count curve: the same numbers as the headline (ms per check, nodes/s, the
+    survey proxy's ms at that node count and the ratio) plus where a check's milliseconds go."""
+    ms = elapsed / max(steps, 1) * 1e3
+    ref = (REF_MS_SLACK if slack else REF_MS).get(nodes)
+    bd = _step_breakdown(spans, lat)
+    return {"nodes": nodes, "ms_per_step": round(ms, 4), "p50_ms": round(_pctl(lat, 0.5) * 1e3, 4),
+            "nodes_per_s": round(nodes / (ms / 1e3), 2) if ms > 0 else None,
+            "checker_ms": bd["checker"] if bd else None, "transport_ms": bd["transport"] if bd else None,
+            "baseline_ms": ref, "vs_baseline": round(ref / ms, 3) if ref and ms > 0 else None,
+            "check_ok": last is not None and last.exit_code == 0 and len(last.ready_gpu_nodes) == nodes,
+            "exit_code": last.exit_code if last is not None else None, "annotations": annotations,
+            "step_ms": bd}
 
 
 def main() -> int:
@@ -218,6 +298,10 @@ def main() -> int:
     ap.add_argument("--diag-level", type=int, default=1, choices=(0, 1, 2))
     ap.add_argument("--slack", action="store_true", help="also POST the Slack report to a local sink each step")
     ap.add_argument("--page-size", type=int, default=500)
+    ap.add_argument("--curve", default=CURVE_NODES, metavar="N,N,...",
+                    help="also time the same check (same --steps / --warmup, rank 0, after the headline) against one "
+                         f"mock cluster per node count (default {CURVE_NODES}; '' to skip); the headline's own node "
+                         "count is its row")
     ap.add_argument("--coldstart-runs", type=int, default=11,
                     help="child-process runs of check-gpu-node --json for coldstart_ms (rank 0, before GPU work; 0: skip)")
     ap.add_argument("--no-fabric-check", dest="fabric_check", action="store_false",
@@ -255,6 +339,10 @@ def main() -> int:
             p, sinfo = _spawn("k8s_gpu_node_checker_amd.testing.webhook_sink")
             procs.append(p)
             ctrl["slack"] = sinfo["url"] + "/200"
+        sizes = sorted({int(x) for x in args.curve.split(",") if x.strip()} - {n_nodes})
+        if sizes:
+            started, ctrl["curve_api"] = _curve_servers(sizes)
+            procs.extend(started)
     budget.mark("control_plane", t_control)
     if rank == 0 and args.coldstart_runs > 0:
         if budget.fits(COLDSTART_MIN_S):
@@ -424,6 +512,19 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)  # the slowest rank's clock (gloo, CPU tensor)
         elapsed = float(t.item())
 
+    curve = None
+    if rank == 0:
+        # the BASELINE metric's node-count axis (the reference's one LIST + per-node loop,
+        # check-gpu-node.py:215-226): the headline's row, then one mock cluster per other node count, each timed
+        # like the headline; the other ranks wait at the closing gloo barrier meanwhile
+        curve = [curve_row(n_nodes, elapsed, args.steps, lat, spans, last, bool(args.slack),
+                           "live" if probe_source != "fixture" else "fixture")]
+        with budget.phase("curve"):
+            for n, url in sorted((ctrl.get("curve_api") or {}).items()):
+                el, lt, sp, ls = _timed_checks(ClusterConnection(url), opts, args.steps, args.warmup)
+                curve.append(curve_row(n, el, args.steps, lt, sp, ls, bool(args.slack), "recorded"))
+        curve.sort(key=lambda r: r["nodes"])
+
     if rank == 0:
         ok = last is not None and last.exit_code == 0 and len(last.ready_gpu_nodes) == n_nodes
         verdicts = [v.state for v in (last.verdicts or []) if v is not None] if last else []
@@ -457,6 +558,12 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
                            "min": round(min(lat) * 1e3, 4), "samples": len(lat)},
             # where a step's milliseconds go: medians over the timed steps of the check's own spans
             "step_ms": _step_breakdown(spans, lat),
+            # the checker's own milliseconds per check (scan + client + health + render + other), without the
+            # socket and the mock apiserver's time: what says something about the code across boxes and rounds
+            "checker_ms": (_step_breakdown(spans, lat) or {}).get("checker"),
+            "baseline_basis": BASELINE_BASIS,
+            # ms per check, nodes/s, checker_ms and vs_baseline at every node count (headline row included)
+            "curve": curve,
             "coldstart_ms": (ctrl.get("coldstart") or {}).get("ms"),
             "coldstart": ctrl.get("coldstart"),
             "baseline_ms": ref,

@@ -44,6 +44,21 @@ def test_bench_single_process_contract():
     assert d["value"] == pytest.approx(1 * 30 / (d["ms_per_step"] * 30 / 1e3), rel=0.01)
     assert d["vs_baseline"] == pytest.approx(d["value"] / (1 / 2.17e-3), rel=0.01)
     assert d["config"]["global_batch"] == 1 and d["backend"] == "native"
+    # the BASELINE metric's node-count curve, each row timed like the headline
+    curve = d["curve"]
+    assert [r["nodes"] for r in curve] == [1, 2, 4, 8, 16, 1000]
+    assert all(r["check_ok"] and r["exit_code"] == 0 for r in curve)
+    head = curve[0]
+    assert head["ms_per_step"] == d["ms_per_step"] and head["annotations"] in ("live", "fixture")
+    assert all(r["annotations"] == "recorded" for r in curve[1:])
+    for r in curve:
+        assert r["vs_baseline"] == pytest.approx(r["baseline_ms"] / r["ms_per_step"], rel=0.01)
+        assert r["nodes_per_s"] == pytest.approx(r["nodes"] / (r["ms_per_step"] / 1e3), rel=0.01)
+        bd = r["step_ms"]
+        # checker_ms is the step minus the socket and the mock's time, per step (medians of sums)
+        assert 0 < r["checker_ms"] < bd["step"] and r["transport_ms"] > 0
+        assert r["checker_ms"] == bd["checker"] and r["transport_ms"] == bd["transport"]
+    assert d["checker_ms"] == head["checker_ms"] and "different machine" in d["baseline_basis"]
 
 
 def test_bench_torchrun_two_ranks_gloo():
@@ -55,6 +70,8 @@ def test_bench_torchrun_two_ranks_gloo():
     d = last_json(p.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["check_ok"] and d["health"] == {"healthy": 2}
+    assert [r["nodes"] for r in d["curve"]] == [1, 2, 4, 8, 16, 1000] and all(r["check_ok"] for r in d["curve"])
+    assert next(r for r in d["curve"] if r["nodes"] == 2)["annotations"] == "fixture"  # the ranks' own: headline
     fab = d["fabric"]  # untimed all-reduce check over the job's process group (gloo here, RCCL on GPUs)
     assert fab["pass"] and fab["world"] == 2 and fab["backend"] == "gloo"
     assert all(r["correct"] for r in fab["rows"]) and len({r["op"] for r in fab["rows"]}) == 4
