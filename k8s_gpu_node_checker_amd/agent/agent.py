@@ -51,6 +51,7 @@ from ..models.health import (HEALTHY, UNHEALTHY, UNHEALTHY_TAINT, UNKNOWN, XGMI_
 from ..models.baseline import Baselines, epoch_of, gpu_key
 from ..models.node import HEALTH_ANNOTATION
 from ..models.resources import PRIMARY_GPU_KEY, gpu_breakdown
+from .isolation import ISOLATION, Job, Workers
 from .server import _metrics, serve, tls_context  # noqa: F401  (the agent's HTTP side; re-exported)
 
 
@@ -58,7 +59,8 @@ from .server import _metrics, serve, tls_context  # noqa: F401  (the agent's HTT
 # whether the annotation must be rewritten.
 _VOLATILE = frozenset(("ts", "probe_ms", "probe_us", "hotspot_c", "wall_s", "ms_per_gemm", "setup_ms",
                        "power_w", "hbm_temp_c", "gfxclk_mhz", "vram_used_mb", "processes", "throttle_acc",
-                       "throttle", "procs", "gfx_activity", "diag_skipped", "xgmi_kb", "ecc_ce_per_h"))
+                       "throttle", "procs", "gfx_activity", "diag_skipped", "xgmi_kb", "ecc_ce_per_h",
+                       "diag_proc"))
 
 # correctable-ECC trend: the rate is taken over the probes of the last hour, once they span 10 minutes
 CE_WINDOW_S = 3600.0
@@ -73,7 +75,7 @@ def baseline_key(entry: Dict[str, Any], bdf: str, device: int) -> str:
     """Whose self-baseline a device's result feeds: amd-smi UUID, else PCI address, else the HIP ordinal."""
     return gpu_key(entry) or (f"bdf:{bdf}" if bdf else f"hip:{device}")
 # per-GPU fields kept out of the node annotation (Agent.annotation)
-_ANNOTATION_DROP = frozenset(("xgmi_kb", "throttle_acc", "procs", "probe_us"))
+_ANNOTATION_DROP = frozenset(("xgmi_kb", "throttle_acc", "procs", "probe_us", "diag_proc"))
 # a JSON report annotation above this goes out gzip-encoded (the apiserver caps a node's annotations at 256 KiB)
 ANNOTATION_JSON_MAX = 128 << 10
 
@@ -166,11 +168,15 @@ def memory_budget_mib(devices: int, level: int, rccl: bool = False) -> int:
 
 
 class _DiagRun:
-    """One device's diagnostic thread: wall-clock start (reported), monotonic start (watchdog), result box."""
-    __slots__ = ("thread", "started", "mono", "box")
+    """One device's (or the node-level suite's) diagnostic job (``isolation.Job``: a child process or a thread):
+    wall-clock start (reported), monotonic start (watchdog), result box."""
+    __slots__ = ("job", "started", "mono", "box")
 
-    def __init__(self, thread: threading.Thread, started: float, mono: float, box: Dict[str, Any]):
-        self.thread, self.started, self.mono, self.box = thread, started, mono, box
+    def __init__(self, job: Job, started: float, mono: float):
+        self.job, self.started, self.mono, self.box = job, started, mono, job.box
+
+    def is_alive(self) -> bool:
+        return self.job.is_alive()
 
 
 def result_signature(res: Dict[str, Any]) -> str:
@@ -357,7 +363,27 @@ def _annotation_gpu(g: Dict[str, Any]) -> Dict[str, Any]:
     return out
 
 
+def _fabric_suite(devices: List[int], timeout_s: Optional[float] = None) -> Dict[str, Any]:
+    """The node-level tests (``ops/diag.fabric_tests``): the xGMI pair matrix and the RCCL collectives in this
+    process, both under the watchdog's deadline -- the matrix within ``P2P_SHARE`` of it, the collectives
+    within what is left up to 90 % -- so a hung copy or collective is given up, and named in the report,
+    rather than left holding the fabric thread."""
+    from ..ops import diag
+    try:
+        res = diag.fabric_tests(devices, timeout_s=timeout_s or None)
+    except Exception as e:  # the diag library itself is missing
+        return {"p2p": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
+    m, r = res.get("p2p") or {}, res.get("rccl") or {}
+    out: Dict[str, Any] = {"p2p": {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s",
+                                                     "stopped") if k in m}}
+    out["rccl"] = {k: r.get(k) for k in ("pass", "best_busbw_gbps", "best_busbw_by_op", "detail", "wall_s",
+                                         "rccl", "aborted") if k in r or k not in ("aborted",)}
+    return out
+
+
 class Agent:
+    _fabric_suite = staticmethod(_fabric_suite)
+
     def __init__(self, node: str, source: str = "auto", fixture: Optional[str] = None, diag_level: int = 0,
                  diag_interval: float = 3600.0, devices: Optional[List[int]] = None,
                  annotation_refresh: float = 900.0, heartbeat_interval: float = 300.0,
@@ -367,8 +393,20 @@ class Agent:
                  expect_gpus: Optional[int] = None, expectations: Optional[HealthExpectations] = None,
                  pod_resources_socket: Optional[str] = None, gpu_resources: Sequence[str] = (PRIMARY_GPU_KEY,),
                  label_node: bool = False, annotation_encoding: str = "json", diag_parallel: int = DIAG_PARALLEL,
-                 diag_baseline: bool = True, baseline_file: Optional[str] = None):
+                 diag_baseline: bool = True, baseline_file: Optional[str] = None, isolation: str = "thread",
+                 diag_setup: Optional[tuple] = None):
         self.node = node
+        if isolation not in ISOLATION:
+            raise ValueError(f"isolation must be one of {ISOLATION}")
+        # where the HIP work runs (agent/isolation.py): "process" -- disposable children of a forkserver started
+        # here, before this process calls amd-smi or HIP, so the agent itself never initialises HIP (the
+        # DaemonSet); "thread" -- threads of this process (library use: the benchmark, tests scripting ops.diag)
+        self.workers = Workers(isolation if diag_level > 0 else "thread", diag_setup)
+        self.isolation = self.workers.mode
+        # process isolation: HIP's device count and PCI addresses from the last enumeration child
+        self._hip_view: Optional[Dict[str, Any]] = None
+        # the last diagnostic child of each device (and "fabric"): pid, peak RSS, wall time (isolation._meta)
+        self.diag_procs: Dict[Any, Dict[str, Any]] = {}
         if diag_parallel < 1:
             raise ValueError("diag_parallel must be >= 1")
         # at most this many per-device diagnostic threads at once (hung ones count: they still hold their GPU)
@@ -486,25 +524,59 @@ class Agent:
         out: Dict[int, Dict[str, Any]] = {}
         for d in devices:
             if d not in self._bdf:
-                try:
-                    self._bdf[d] = normalize_bdf(diag.device_info(d)["bdf"])
-                except Exception:
-                    self._bdf[d] = ""
+                if self.workers.isolated:  # never a HIP call in this process: the enumeration child's answer
+                    self._bdf[d] = normalize_bdf(((self._hip_view or {}).get("bdf") or {}).get(d, ""))
+                else:
+                    try:
+                        self._bdf[d] = normalize_bdf(diag.device_info(d)["bdf"])
+                    except Exception:
+                        self._bdf[d] = ""
             g = by_bdf.get(self._bdf[d]) if self._bdf[d] else (gpus[d] if 0 <= d < len(gpus) else None)
             if g is not None:
                 out[d] = g
         return out
+
+    def _hip_devices(self, gpus: List[Dict[str, Any]], refresh: bool) -> Optional[int]:
+        """HIP's device count: from ``ops.diag`` in this process (thread isolation), else from an enumeration child
+        (re-run when ``refresh``, i.e. when a diagnostic may start) -- None with ``_diag_skipped`` filled when that
+        child failed."""
+        from ..ops import diag
+        if not self.workers.isolated:
+            return diag.device_count()
+        if refresh or self._hip_view is None:
+            view = self.workers.enumerate(min(60.0, max(5.0, self.diag_timeout)))
+            if "count" in view:
+                if self._hip_view is None or view.get("bdf") != self._hip_view.get("bdf"):
+                    self._bdf = {}  # ordinals -> PCI addresses changed (or first seen): map them again
+                self._hip_view = view
+            else:
+                for i in range(len(gpus)):
+                    self._diag_skipped[i] = f"HIP device enumeration failed: {view.get('error')}"[:200]
+                return None
+        return int(self._hip_view["count"])
 
     def _diagnostics(self, gpus: List[Dict[str, Any]]) -> Dict[int, Dict[str, Any]]:
         self._diag_skipped = {}
         if self.diag_level <= 0:
             return {}
         from ..ops import diag
-        visible = diag.device_count() if self.devices is None else len(self.devices)
+        isolated = self.workers.isolated
+        now = time.time()
+        # an enumeration child is worth its HIP start-up only when something may run this cycle
+        candidates = self.devices if self.devices is not None else list(range(len(gpus)))
+        maybe_due = any(now - self._diag_at.get(d, float("-inf")) >= self.diag_interval for d in candidates) or (
+            self.diag_level >= 2 and now - self._fabric_at >= self.diag_interval)
+        visible = self._hip_devices(gpus, refresh=maybe_due)
+        if visible is None:
+            return {d: self._diag_cache[d] for d in candidates if d in self._diag_cache}
+        if self.devices is not None:
+            visible = len(self.devices)
         if self._hip_count0 is None:
-            self._hip_count0 = diag.device_count() if self.devices is not None else visible
-        elif self.hip_lost is None and self.devices is None and visible != self._hip_count0:
+            self._hip_count0 = (diag.device_count() if not isolated else int(self._hip_view["count"])) \
+                if self.devices is not None else visible
+        elif not isolated and self.hip_lost is None and self.devices is None and visible != self._hip_count0:
             # HIP enumerates once per process: a count that moved is a driver reload or reset under the agent
+            # (process isolation: every child enumerates afresh, so there is no stale runtime to lose)
             self.hip_lost = f"HIP device count changed from {self._hip_count0} to {visible}"
             print(f"{self.hip_lost}; diagnostics stop, /healthz fails so the agent is restarted", file=sys.stderr,
                   flush=True)
@@ -519,14 +591,13 @@ class Agent:
             # a configured ordinal HIP does not have is a configuration error of that device, said as such: run
             # on it, every call would fail with "invalid device ordinal", which is neither the GPU's fault nor a
             # lost runtime
-            count = self._hip_count0 if self._hip_count0 is not None else diag.device_count()
+            count = self._hip_count0 if not isolated else int(self._hip_view["count"])
             for d in [d for d in devices if not 0 <= d < count]:
                 self._diag_skipped[d] = f"device {d} is not a HIP device of the agent ({count} visible): check --devices"
             devices = [d for d in devices if 0 <= d < count]
         entries = self._entries_by_device(gpus, devices)
-        now = time.time()
         due = [d for d in devices if now - self._diag_at.get(d, float("-inf")) >= self.diag_interval]
-        fabric_busy = self._fabric_thread is not None and self._fabric_thread.thread.is_alive()
+        fabric_busy = self._fabric_thread is not None and self._fabric_thread.is_alive()
         if fabric_busy and due:
             # a node-level suite that outlived its watchdog still holds every GPU (a collective's kernels stay
             # queued): per-GPU tests would contend with it or queue behind it and muddy their own verdict
@@ -549,42 +620,57 @@ class Agent:
                 self._diag_skipped[d] = why
             else:
                 run.append(d)
-        # one host thread per GPU, at most `diag_parallel` at once: each diagnostic is a ctypes call that
-        # releases the GIL and drives its own device, so an 8-GPU node is checked in the time of one GPU and a
-        # 64-partition CPX node in 8 waves instead of 64 threads contending for the host.  A GPU whose
-        # diagnostic never returns (a hung queue) is reported as failed after `diag_timeout` s instead of
-        # freezing the agent into a stale report; nothing new is started on it while that thread lives, and
-        # /healthz fails once it has outlived HUNG_RESTART_FACTOR x diag_timeout (hung_diagnostic).
+        # one job per GPU, at most `diag_parallel` at once: a child process each (process isolation) or a thread
+        # each whose ctypes calls release the GIL -- either way every device is driven at once, so an 8-GPU node is
+        # checked in the time of one GPU and a 64-partition CPX node in 8 waves.  A GPU whose diagnostic outlives
+        # `diag_timeout` s is reported failed instead of freezing the agent into a stale report: its child is
+        # SIGKILLed (freeing its slot and its GPU); a thread cannot be, so nothing new starts on that GPU while it
+        # lives, and /healthz fails once it has outlived HUNG_RESTART_FACTOR x diag_timeout (hung_diagnostic).
         queue = [d for d in run if d not in self._diag_threads] if self.hip_lost is None else []
         memory_partition = {d: (entries.get(d) or {}).get("memory_partition") for d in queue}
         power = {d: power_fraction(entries.get(d) or {}) for d in queue}
+        host = self.workers.host_lock() if queue else (None, None)
         while True:
             self._diag_done.clear()
-            while queue and sum(r.thread.is_alive() for r in self._diag_threads.values()) < self.diag_parallel:
+            while queue and sum(r.is_alive() for r in self._diag_threads.values()) < self.diag_parallel:
                 d = queue.pop(0)
-                self._start_diag(d, memory_partition.get(d), power.get(d))
+                self._start_diag(d, memory_partition.get(d), power.get(d), host)
+            if isolated:
+                for r in self._diag_threads.values():
+                    if not r.job.killed and r.is_alive() and time.monotonic() >= r.mono + self.diag_timeout:
+                        r.job.kill()  # its slot frees (unless the child is stuck in the driver)
             waiting = [r for r in self._diag_threads.values()
-                       if r.thread.is_alive() and time.monotonic() < r.mono + self.diag_timeout]
-            if not waiting:
+                       if r.is_alive() and time.monotonic() < r.mono + self.diag_timeout]
+            if not waiting and not (queue and isolated and
+                                    sum(r.is_alive() for r in self._diag_threads.values()) < self.diag_parallel):
                 break
-            self._diag_done.wait(max(0.0, min(min(r.mono for r in waiting) + self.diag_timeout - time.monotonic(),
-                                              1.0)))
+            if waiting:
+                self._diag_done.wait(max(0.0, min(min(r.mono for r in waiting) + self.diag_timeout - time.monotonic(),
+                                                  1.0)))
         for d in queue:  # every slot is held by a diagnostic that outlived its watchdog
             self._diag_skipped[d] = (f"waiting for a diagnostic slot: {self.diag_parallel} of {self.diag_parallel} "
                                      "held by hung diagnostics")
         finished: Dict[int, Dict[str, Any]] = {}
         for d, r in list(self._diag_threads.items()):
-            if not r.thread.is_alive():
+            if "meta" in r.box:
+                self.diag_procs[d] = r.box["meta"]
+            if not r.is_alive():
                 del self._diag_threads[d]
-                if "res" in r.box:
+                if r.job.killed:
+                    finished[d] = {"watchdog": {
+                        "pass": False, "detail": f"diagnostics did not finish within {self.diag_timeout:g} s (GPU "
+                                                 f"hang?): diagnostic process {r.job.pid} killed"}}
+                elif "res" in r.box:
                     finished[d] = r.box["res"]
                 self._diag_at[d] = r.started
             else:
+                stuck = f": diagnostic process {r.job.pid} did not exit after SIGKILL" if r.job.killed else ""
                 self._diag_cache[d] = {"watchdog": {
-                    "pass": False, "detail": f"diagnostics did not finish within {self.diag_timeout:g} s (GPU hang?)"}}
+                    "pass": False,
+                    "detail": f"diagnostics did not finish within {self.diag_timeout:g} s (GPU hang?){stuck}"}}
                 self._diag_ran[d] = r.started
                 self._diag_at[d] = r.started
-        lost_devs = {d: runtime_lost(res) for d, res in finished.items()}
+        lost_devs = {d: runtime_lost(res) for d, res in finished.items()} if not isolated else {}
         lost_devs = {d: why for d, why in lost_devs.items() if why is not None}
         if lost_devs and self.hip_lost is None:
             # the HIP runtime, not a GPU, is gone only when
@@ -594,7 +680,8 @@ class Agent:
             # * every device of the node (two or more) failed that way together.
             # Devices that never ran fine here -- two broken GPUs rechecked on their own (DIAG_RECHECK_S) while the
             # others passed, or the only idle ones of a busy node -- are those GPUs' failures and stay in their
-            # verdicts: restarting the agent for them would only loop, diagnosing the same GPUs after every start
+            # verdicts: restarting the agent for them would only loop, diagnosing the same GPUs after every start.
+            # (Process isolation: each child's runtime is fresh, so such an error there is the device's own.)
             now_count = diag.device_count()
             whole_node = len(lost_devs) >= 2 and set(lost_devs) >= set(devices)
             was_fine = any(d in self._hip_ok for d in lost_devs)
@@ -631,23 +718,35 @@ class Agent:
                 and not self._diag_threads and self._fabric_thread is None and self.fabric_abandoned is None
                 and now - self._fabric_at >= self.diag_interval):
             # node-level: every ordered GPU pair over xGMI (after the per-GPU tests, so no contention) and the
-            # RCCL collectives; it touches every GPU, so it waits until none is busy.  On its own thread under
-            # the same watchdog as the per-GPU tests: a collective that never completes (a link that stopped
-            # passing traffic) is a failed fabric, not a frozen agent.
-            box: Dict[str, Any] = {}
-            t = threading.Thread(target=lambda: box.update(res=self._fabric_suite(devices, self.diag_timeout)),
-                                 name="diag-fabric", daemon=True)
-            self._fabric_thread = _DiagRun(t, now, time.monotonic(), box)
-            t.start()
+            # RCCL collectives; it touches every GPU, so it waits until none is busy.  Under the same watchdog as
+            # the per-GPU tests: a collective that never completes (a link that stopped passing traffic) is a
+            # failed fabric, not a frozen agent.
+            done = threading.Event()
+            job = self.workers.fabric(_fabric_suite, devices, self.diag_timeout, done)
+            self._fabric_thread = _DiagRun(job, now, time.monotonic())
         if self._fabric_thread is not None:
             r = self._fabric_thread
-            r.thread.join(max(0.0, r.mono + self.diag_timeout - time.monotonic()))
+            deadline = r.mono + self.diag_timeout
+            while r.is_alive() and time.monotonic() < deadline:
+                time.sleep(min(0.05, max(0.0, deadline - time.monotonic())))
+            if isolated and r.is_alive() and not r.job.killed:
+                r.job.kill()
             self._fabric_at = r.started
-            if not r.thread.is_alive():
+            if "meta" in r.box:
+                self.diag_procs["fabric"] = r.box["meta"]
+            if not r.is_alive():
                 self._fabric_thread = None
-                self._fabric = r.box.get("res")
-                why = fabric_abandoned(self._fabric)
+                if r.job.killed:
+                    self._fabric = {"watchdog": {
+                        "pass": False, "detail": f"node-level xGMI/RCCL tests did not finish within "
+                                                 f"{self.diag_timeout:g} s (fabric hang?): diagnostic process "
+                                                 f"{r.job.pid} killed"}}
+                else:
+                    self._fabric = r.box.get("res")
+                why = fabric_abandoned(self._fabric) if not isolated else None
                 if why:
+                    # an abandoned test's queued copies and aborted communicators stay with this process (thread
+                    # isolation); in a child they ended with it, so the suite simply runs again next interval
                     self.fabric_abandoned = why
                     for res in self._fabric.values():
                         if isinstance(res, dict) and res.get("pass") is False:
@@ -655,9 +754,11 @@ class Agent:
                     print(f"{why}; the node-level tests are not re-run until the agent restarts", file=sys.stderr,
                           flush=True)
             else:
+                stuck = f": diagnostic process {r.job.pid} did not exit after SIGKILL" if r.job.killed else ""
                 self._fabric = {"watchdog": {
                     "pass": False,
-                    "detail": f"node-level xGMI/RCCL tests did not finish within {self.diag_timeout:g} s (fabric hang?)"}}
+                    "detail": f"node-level xGMI/RCCL tests did not finish within {self.diag_timeout:g} s (fabric "
+                              f"hang?){stuck}"}}
         return {d: self._diag_cache[d] for d in devices if d in self._diag_cache}
 
     def _judge_diagnostics(self, devices: List[int], entries: Dict[int, Dict[str, Any]], fresh: List[int]) -> None:
@@ -678,29 +779,17 @@ class Agent:
                 self.baselines.observe(key, self._diag_cache[d], now, epoch_of(entries.get(d), self._driver_version))
             self.diag_findings = peers.judge_node(pool, label)
 
-    def _start_diag(self, d: int, memory_partition: Any, power: Optional[float]) -> None:
-        """Start device ``d``'s diagnostics on its own thread (the partition's memory share comes from amd-smi's
-        NPS mode, CUs and VRAM from HIP; a lowered power cap scales the compute references)."""
-        from ..ops import diag
-        box: Dict[str, Any] = {}
+    def _start_diag(self, d: int, memory_partition: Any, power: Optional[float], host: tuple = (None, None)) -> None:
+        """Start device ``d``'s diagnostics as its own job (the partition's memory share comes from amd-smi's NPS
+        mode, CUs and VRAM from HIP; a lowered power cap scales the compute references)."""
         kw: Dict[str, Any] = {"memory_partition": memory_partition}
         if power is not None and power < 1.0:
             kw["power_fraction"] = power
-
         # the host-link turn is waited for only within this device's watchdog (a GPU stuck in its turn is that
-        # GPU's hang, not every GPU's)
+        # GPU's hang, not every GPU's); CLOCK_MONOTONIC is one clock for the agent and its children
         kw["deadline"] = time.monotonic() + 0.9 * self.diag_timeout
-
-        def work() -> None:
-            try:
-                box["res"] = diag.run(self.diag_level, d, **kw)
-            except Exception as e:  # a broken library or device: a failed test, not a dead agent
-                box["res"] = {"run": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
-            finally:
-                self._diag_done.set()
-        t = threading.Thread(target=work, name=f"diag-gpu{d}", daemon=True)
-        self._diag_threads[d] = _DiagRun(t, time.time(), time.monotonic(), box)
-        t.start()
+        job = self.workers.device(self.diag_level, d, kw, self._diag_done, host)
+        self._diag_threads[d] = _DiagRun(job, time.time(), time.monotonic())
 
     def _unmatched_allocations(self, allocated: Dict[str, str], entries: Dict[int, Dict[str, Any]],
                                devices: List[int]) -> Optional[str]:
@@ -720,6 +809,10 @@ class Agent:
     def hung_diagnostic(self, now: Optional[float] = None) -> Optional[str]:
         """Why /healthz must fail: a diagnostic thread alive for HUNG_RESTART_FACTOR x diag_timeout (its watchdog
         verdict was published at 1x); None when nothing is hung that long."""
+        if self.workers.isolated:
+            # a child past its watchdog was SIGKILLed and its GPU reported failed; one the kernel cannot end (stuck
+            # in the driver) would survive a restart of the agent as well, so it is reported, not restarted for
+            return None
         now = time.monotonic() if now is None else now
         limit = HUNG_RESTART_FACTOR * self.diag_timeout
         runs = [(f"gpu{d} diagnostics", r) for d, r in list(self._diag_threads.items())]
@@ -728,27 +821,9 @@ class Agent:
             runs.append(("node-level xGMI/RCCL tests", fab))
         for what, r in runs:
             age = now - r.mono
-            if r.thread.is_alive() and age >= limit:
+            if r.is_alive() and age >= limit:
                 return f"{what} running for {age:.0f} s (> {HUNG_RESTART_FACTOR:g} x --diag-timeout): restart to free the GPU"
         return None
-
-    @staticmethod
-    def _fabric_suite(devices: List[int], timeout_s: Optional[float] = None) -> Dict[str, Any]:
-        """The node-level tests (``ops/diag.fabric_tests``): the xGMI pair matrix and the RCCL collectives in this
-        process, both under the watchdog's deadline -- the matrix within ``P2P_SHARE`` of it, the collectives
-        within what is left up to 90 % -- so a hung copy or collective is given up, and named in the report,
-        rather than left holding the fabric thread."""
-        from ..ops import diag
-        try:
-            res = diag.fabric_tests(devices, timeout_s=timeout_s or None)
-        except Exception as e:  # the diag library itself is missing
-            return {"p2p": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
-        m, r = res.get("p2p") or {}, res.get("rccl") or {}
-        out: Dict[str, Any] = {"p2p": {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s",
-                                                         "stopped") if k in m}}
-        out["rccl"] = {k: r.get(k) for k in ("pass", "best_busbw_gbps", "best_busbw_by_op", "detail", "wall_s",
-                                             "rccl", "aborted") if k in r or k not in ("aborted",)}
-        return out
 
     def _allocated(self) -> Optional[Dict[str, str]]:
         """Devices the kubelet allocated to pods (normalised BDF -> "ns/pod"), or None when unknown."""
@@ -786,6 +861,8 @@ class Agent:
                 if diags.get(d):
                     g["diag"] = diags[d]
                     g["diag_at"] = round(self._diag_ran.get(d, 0.0), 1)  # when it ran (a busy GPU's result ages)
+                    if d in self.diag_procs:  # process isolation: the child that measured it (pid, peak RSS)
+                        g["diag_proc"] = self.diag_procs[d]
                 if d in self._diag_skipped:
                     g["diag_skipped"] = self._diag_skipped[d]
             if self._fabric:
@@ -981,6 +1058,11 @@ def build_parser() -> argparse.ArgumentParser:
                     help="a process other than the agent holding this much VRAM makes its GPU busy (default 2048)")
     ap.add_argument("--diag-timeout", type=float, default=300.0,
                     help="a GPU whose diagnostics run longer than this (s) is reported failed (hung); default 300")
+    ap.add_argument("--diag-isolation", choices=ISOLATION, default="process",
+                    help="process (default): each cycle's HIP diagnostics run in disposable child processes, so the "
+                         "agent never initialises HIP, a hung one is SIGKILLed at --diag-timeout and a GPU fault "
+                         "ends only its child; thread: in the agent process (a hung HIP call then needs a restart, "
+                         "/healthz)")
     ap.add_argument("--diag-parallel", type=int, default=DIAG_PARALLEL, metavar="N",
                     help=f"per-device diagnostic threads at once (default {DIAG_PARALLEL}: an SPX node's GPUs together, "
                          "a CPX node's 64 partitions in waves); tests on shared host resources (the PCIe host link) "
@@ -1041,7 +1123,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                   pod_resources_socket=args.pod_resources_socket,
                   gpu_resources=tuple(args.gpu_resource or (PRIMARY_GPU_KEY,)), label_node=args.label_node,
                   annotation_encoding=args.annotation_encoding, diag_parallel=args.diag_parallel,
-                  diag_baseline=args.diag_baseline, baseline_file=args.diag_baseline_file)
+                  diag_baseline=args.diag_baseline, baseline_file=args.diag_baseline_file,
+                  isolation=args.diag_isolation)
     if args.diag_baseline_reset and agent.baselines is not None:
         spec = args.diag_baseline_reset.strip()
         gone = agent.baselines.drop(None if spec.lower() == "all" else spec.split(","))

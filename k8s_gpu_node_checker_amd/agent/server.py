@@ -86,6 +86,9 @@ def _metrics(rep: Optional[Dict[str, Any]]) -> str:
             put("mi355x_gpu_firmware_info", f'{lbl},image="{_esc(image)}",version="{_esc(fw_version_str(image, ver))}"', 1)
         if g.get("diag") is not None or g.get("diag_skipped"):
             put("mi355x_gpu_diag_skipped", lbl, 1 if g.get("diag_skipped") else 0)
+        proc = g.get("diag_proc")  # process isolation: the diagnostic child's peak host memory (the pod's limit)
+        if isinstance(proc, dict) and isinstance(proc.get("peak_rss_mib"), (int, float)):
+            put("mi355x_agent_diag_child_peak_rss_bytes", lbl, int(proc["peak_rss_mib"] * 1048576))
         for test, res in (g.get("diag") or {}).items():
             if not isinstance(res, dict):
                 continue
@@ -148,10 +151,11 @@ IDLE_TIMEOUT_S = 30.0
 def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = None, tls: Any = None,
           require_client_cert: bool = False) -> ThreadingHTTPServer:
     """/probe, /metrics, /status (text) and /healthz; /healthz answers 503 once no probe has completed for
-    ``stale_after`` s (a wedged amd-smi call or driver), once a diagnostic thread has outlived
-    HUNG_RESTART_FACTOR x ``diag_timeout`` (a hung HIP queue the process cannot cancel) or after the HIP runtime
-    lost its devices, so a livenessProbe restarts the agent as a fresh process (the kubelet starts a new
-    container; nothing is re-executed in place)."""
+    ``stale_after`` s (a wedged amd-smi call or driver) and, with thread isolation only, once a diagnostic thread
+    has outlived HUNG_RESTART_FACTOR x ``diag_timeout`` (a hung HIP queue the process cannot cancel) or after the
+    HIP runtime lost its devices, so a livenessProbe restarts the agent as a fresh process (the kubelet starts a
+    new container; nothing is re-executed in place).  With process isolation (the DaemonSet's) neither applies:
+    a hung diagnostic child is SIGKILLed at its watchdog and every child starts a fresh HIP runtime."""
     started = time.monotonic()
 
     class H(BaseHTTPRequestHandler):

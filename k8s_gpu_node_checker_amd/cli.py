@@ -354,7 +354,9 @@ def _watch_events(args: Any) -> int:
             if elector is not None:
                 # the last-notified outcome rides on the Lease: a replica taking over starts from it (no repeated
                 # alert, no lost recovery notice across a failover)
-                elector.publish_state(statefile.compact(memo["prev"]))
+                if not elector.publish_state(statefile.compact(memo["prev"])):
+                    print("leader state does not fit the Lease even compacted: a replica taking over starts "
+                          "without it", file=sys.stderr, flush=True)
             last["code"] = result.exit_code
 
         if not args.leader_elect:

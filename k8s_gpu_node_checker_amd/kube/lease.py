@@ -41,7 +41,8 @@ RENEW_DEADLINE_S = 10.0
 RETRY_PERIOD_S = 2.0
 STATE_ANNOTATION = "gpu-health.amd.com/leader-state"
 # the apiserver caps an object's annotations at 256 KiB: a state larger than this is not kept on the Lease
-STATE_MAX_BYTES = 64 << 10
+# (utils/statefile.compact shrinks an outcome to it first)
+from ..utils.statefile import STATE_MAX_BYTES  # noqa: E402
 
 
 def _micro_time(epoch: float) -> str:

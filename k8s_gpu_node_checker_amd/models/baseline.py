@@ -16,8 +16,15 @@ never forms a baseline at a fault level.
 **Epochs.**  A baseline belongs to the software it was measured under: the amdgpu driver release, the VBIOS
 and the firmware image set amd-smi reports for that GPU.  When the epoch changes (a ROCm or firmware
 upgrade that moves a rate by more than the drift margin, either way) the GPU's baselines are re-formed from
-the next clean runs, with no drift warning in between; the old epoch is kept as ``previous``.  A file from
-before epochs (schema v1) is read and upgraded: its baselines adopt the first epoch observed.
+the next clean runs, with no drift warning in between; the old epoch is kept as ``previous``.  Epochs are compared
+component by component (driver, VBIOS, each firmware image), and only a component both sides know and that differs
+is a change: one probe where amd-smi could not read the VBIOS or the driver is not a new epoch (the missing part is
+kept from before), and a component seen for the first time is filled in without re-forming anything.
+
+**Revisions.**  A baseline is a fraction of the diagnostics' reference rates, so it also belongs to those and to
+the kernel that measured them (``ops/diag.rate_revision``): each test's entry records the revision it formed
+under, and a test whose kernel or references changed re-forms alone.  Entries from before revisions (schema v1
+and v2 files) were formed under references that can no longer be told, so they are dropped on load and re-form.
 
 Keyed by the GPU's amd-smi UUID (its PCI address when there is none) so a replaced board starts a new
 baseline; the test's shape is part of the key (the level-1 4096^3 and level-2 8192^3 GEMMs differ).  With a
@@ -35,9 +42,10 @@ import os
 import statistics
 import threading
 import time
-from typing import Any, Dict, Iterable, List, Optional
+from typing import Any, Callable, Dict, Iterable, List, Optional
 
-SCHEMA = "mi355x-diag-baseline/v2"
+SCHEMA = "mi355x-diag-baseline/v3"
+SCHEMA_V2 = "mi355x-diag-baseline/v2"
 SCHEMA_V1 = "mi355x-diag-baseline/v1"
 BASELINE_RUNS = 5
 DRIFT_RATIO = 0.90
@@ -70,17 +78,55 @@ def epoch_of(entry: Optional[Dict[str, Any]], driver_version: Any = None) -> Opt
     """The software a GPU's rates are measured under, as one string: ``driver <release>; vbios <version>;
     fw <image>=<version>,...`` (amd-smi's firmware list, sorted).  None when nothing is known."""
     from .health import driver_release, fw_version_str
-    parts = []
+    parts: Dict[str, str] = {}
     if driver_version:
-        parts.append(f"driver {driver_release(driver_version)}")
+        parts["driver"] = str(driver_release(driver_version))
     e = entry if isinstance(entry, dict) else {}
     vb = e.get("vbios_version")
     if isinstance(vb, str) and vb.strip():
-        parts.append(f"vbios {vb.strip()}")
+        parts["vbios"] = vb.strip()
     fw = e.get("fw")
-    if isinstance(fw, dict) and fw:
-        parts.append("fw " + ",".join(f"{k}={fw_version_str(k, fw[k])}" for k in sorted(fw, key=str)))
-    return "; ".join(parts) or None
+    if isinstance(fw, dict):
+        for k in fw:
+            parts[f"fw:{k}"] = fw_version_str(k, fw[k])
+    return epoch_str(parts)
+
+
+def epoch_str(parts: Dict[str, str]) -> Optional[str]:
+    """:func:`epoch_of`'s string of an epoch's components (``driver``, ``vbios``, ``fw:<image>``)."""
+    out = [f"{k} {parts[k]}" for k in ("driver", "vbios") if parts.get(k)]
+    fw = sorted((k[3:], v) for k, v in parts.items() if k.startswith("fw:"))
+    if fw:
+        out.append("fw " + ",".join(f"{k}={v}" for k, v in fw))
+    return "; ".join(out) or None
+
+
+def epoch_parts(epoch: Optional[str]) -> Dict[str, str]:
+    """The components of an :func:`epoch_of` string (the inverse of :func:`epoch_str`)."""
+    parts: Dict[str, str] = {}
+    for piece in (epoch or "").split("; "):
+        kind, _, rest = piece.partition(" ")
+        if kind in ("driver", "vbios") and rest:
+            parts[kind] = rest
+        elif kind == "fw" and rest:
+            for image in rest.split(","):
+                k, eq, v = image.partition("=")
+                if eq:
+                    parts[f"fw:{k}"] = v
+    return parts
+
+
+def epoch_change(old: Optional[str], new: Optional[str]) -> tuple:
+    """(changed, merged epoch) of a GPU's stored epoch ``old`` against this probe's ``new``: changed only when a
+    component both know differs; merged keeps what ``new`` lacks from ``old`` (a transient amd-smi miss) and
+    takes the rest from ``new``."""
+    if not new:
+        return False, old
+    if not old:
+        return False, new
+    op, np = epoch_parts(old), epoch_parts(new)
+    changed = any(op[k] != np[k] for k in op.keys() & np.keys())
+    return changed, epoch_str(dict(op, **np)) if not changed else new
 
 
 def clean_run(res: Dict[str, Any], fractions: Optional[Dict[str, float]] = None) -> bool:
@@ -110,15 +156,14 @@ class Baselines:
             return
         if not isinstance(doc, dict) or not isinstance(doc.get("gpus"), dict):
             return
-        if doc.get("schema") == SCHEMA:
+        if doc.get("schema") in (SCHEMA, SCHEMA_V2):
             for k, v in doc["gpus"].items():
                 if isinstance(v, dict) and isinstance(v.get("tests"), dict):
                     ep = v.get("epoch")
-                    self.data[k] = dict(v, epoch=ep if isinstance(ep, str) else None)
-        elif doc.get("schema") == SCHEMA_V1:
-            # before epochs: per GPU, the shape-keyed entries themselves; they adopt the first epoch observed
-            self.data = {k: {"epoch": None, "tests": {t: e for t, e in v.items() if isinstance(e, dict)}}
-                         for k, v in doc["gpus"].items() if isinstance(v, dict)}
+                    # an entry without the revision it formed under (v2) cannot be trusted: it re-forms
+                    tests = {t: e for t, e in v["tests"].items() if isinstance(e, dict) and isinstance(e.get("rev"), str)}
+                    self.data[k] = dict(v, epoch=ep if isinstance(ep, str) else None, tests=tests)
+        # a v1 file (before epochs and revisions) is dropped as a whole: its baselines re-form from the next runs
 
     def _save(self) -> None:
         if not self.path:
@@ -163,12 +208,15 @@ class Baselines:
         return gone
 
     def observe(self, gpu: str, results: Dict[str, Dict[str, Any]], now: Optional[float] = None,
-                epoch: Optional[str] = None) -> List[str]:
+                epoch: Optional[str] = None, revision: Optional[Callable[[str], str]] = None) -> List[str]:
         """Fold one fresh diagnostic result of GPU ``gpu`` (test -> result), measured under ``epoch``, in: set
         ``drift`` on each rate test below ``drift_ratio`` of its baseline (``baseline`` records the ratios), or
-        add the clean ones to the baseline still forming.  A new epoch first re-forms the GPU's baselines.
-        Returns the drift notes.  Call once per fresh result: the judgement is re-applied from the recorded
-        fields, so cached results keep their notes without being observed again."""
+        add the clean ones to the baseline still forming.  A new epoch first re-forms the GPU's baselines, a test
+        whose ``revision`` (default ``ops/diag.rate_revision``) changed re-forms its own.  Returns the drift notes.
+        Call once per fresh result: the judgement is re-applied from the recorded fields, so cached results keep
+        their notes without being observed again."""
+        if revision is None:
+            from ..ops.diag import rate_revision as revision  # ctypes-free at import
         notes: List[str] = []
         now = time.time() if now is None else now
         changed = False
@@ -177,16 +225,18 @@ class Baselines:
             if not isinstance(per, dict) or not isinstance(per.get("tests"), dict):
                 per = self.data[gpu] = {"epoch": epoch, "tests": {}}
                 changed = True
-            elif epoch is not None and per.get("epoch") is None:
-                per["epoch"] = epoch  # an upgraded v1 file: its baselines were formed under this software
-                changed = True
-            elif epoch is not None and per.get("epoch") != epoch:
-                formed = {t: e["baseline"] for t, e in per["tests"].items()
-                          if isinstance(e, dict) and isinstance(e.get("baseline"), dict)}
-                per = self.data[gpu] = {"epoch": epoch, "tests": {},
-                                        "previous": {"epoch": per.get("epoch"), "until": round(now, 1),
-                                                     "baselines": formed}}
-                changed = True
+            else:
+                moved, merged = epoch_change(per.get("epoch"), epoch)
+                if moved:
+                    formed = {t: e["baseline"] for t, e in per["tests"].items()
+                              if isinstance(e, dict) and isinstance(e.get("baseline"), dict)}
+                    per = self.data[gpu] = {"epoch": epoch, "tests": {},
+                                            "previous": {"epoch": per.get("epoch"), "until": round(now, 1),
+                                                         "baselines": formed}}
+                    changed = True
+                elif merged != per.get("epoch"):
+                    per["epoch"] = merged  # a component seen for the first time: filled in, nothing re-forms
+                    changed = True
             tests = per["tests"]
             for test, res in results.items():
                 if not isinstance(res, dict):
@@ -195,9 +245,15 @@ class Baselines:
                 if not fr:
                     continue
                 key = _shape(test, res)
+                rev = revision(test)
                 entry = tests.get(key)
+                if isinstance(entry, dict) and entry.get("rev") != rev:
+                    # the kernel or the references this test's fractions are relative to changed: its baseline says
+                    # nothing about today's fractions, so it re-forms (no drift in between)
+                    entry = None
                 if not isinstance(entry, dict):
-                    entry = tests[key] = {"samples": []}
+                    entry = tests[key] = {"samples": [], "rev": rev}
+                    changed = True
                 base = entry.get("baseline")
                 if isinstance(base, dict):
                     ratios = {m: round(v / base[m], 3) for m, v in fr.items()

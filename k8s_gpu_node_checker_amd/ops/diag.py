@@ -73,8 +73,11 @@ from .native import NativeUnavailable, load_cdll
 # whichever box ran last: a slower healthy platform shows as a node-level note, not as failed GPUs.
 FAIL_FRACTION = 0.85
 SHARED_TESTS = frozenset(("host_link",))
-_HOST_SHARED = threading.Lock()  # held by the one device measuring a SHARED_TESTS test
+_HOST_SHARED: Any = threading.Lock()  # held by the one device measuring a SHARED_TESTS test
 _HOST_HOLDER: Dict[str, Any] = {}  # who holds it: {"device": d, "since": monotonic time}
+# per-device diagnostic *processes* (agent/isolation.py) share a multiprocessing lock instead, and say who holds it
+# in a shared (device, since) cell: CLOCK_MONOTONIC is one clock for every process of the host
+_HOST_CELL: Any = None
 # how long a device waits for the host-resource lock when run() is given no deadline (s): a healthy 8-GPU turn
 # at the host link is ~8 x 0.1 s, so this only ever expires behind a device stuck inside its host-link test
 SHARED_WAIT_S = 120.0
@@ -123,6 +126,28 @@ REFERENCE_RATES: Dict[str, Dict[Any, float]] = {
     "l2": {"read_tbs": 30.5},                      # per-XCD L2 reads, 2 MiB slices, 8 WG/CU: 31.6-31.9 measured
                                                    # (profiles/l2_explore_mi355x.json; 34.5 TB/s is the L2's own figure)
 }
+# What produced each test's rates besides the references above: the kernel (and shape policy) that runs it.  Bump a
+# test's entry when a kernel change moves its rates; a self-baseline (models/baseline.py) formed under another
+# revision -- or under other REFERENCE_RATES for the test, since a baseline is a fraction of them -- re-forms.
+KERNEL_REVISION: Dict[str, str] = {
+    "gemm": "bf16-v4",           # four-wave v4 MFMA GEMM since round 5 (v3 before)
+    "gemm_fp8": "mxfp8-v4",
+    "hbm": "copy16-r1", "hbm_xcd": "xcd-slices-4pass", "l2": "xcd-l2-2mib",
+    "mfma": "burn-f8f6f4-r4",    # fp8 as the unscaled f8f6f4 instruction since round 4
+    "host_link": "pinned-r1",
+}
+
+
+def rate_revision(test: str) -> str:
+    """A short stamp of what a test's rate fractions are relative to: its kernel revision and its reference rates."""
+    import hashlib
+    import json as _json
+    ref = REFERENCE_RATES.get(test)
+    doc = {"kernel": KERNEL_REVISION.get(test, ""),
+           "ref": {str(k): v for k, v in ref.items()} if isinstance(ref, dict) else None}
+    return hashlib.sha256(_json.dumps(doc, sort_keys=True).encode()).hexdigest()[:12]
+
+
 # Sampled errors.  The v4 / v3 kernels the diagnostics time write bf16 C (diag.hip OUT_BF16_CK): there the error is
 # what lies beyond the output's own rounding (half a bf16 ulp), so the limits below hold for both outputs.
 GEMM_MAX_REL_ERR = 2e-3       # vs fp32 reference; bf16 inputs are exact in fp32, so ~1e-5 is typical
@@ -926,15 +951,29 @@ def _acquire_shared(device: int, deadline: Optional[float]) -> Optional[str]:
     wait = SHARED_WAIT_S if deadline is None else max(0.0, deadline - time.monotonic())
     if _HOST_SHARED.acquire(timeout=wait):
         _HOST_HOLDER.update(device=device, since=time.monotonic())
+        if _HOST_CELL is not None:
+            _HOST_CELL[0], _HOST_CELL[1] = float(device), time.monotonic()
         return None
     holder = dict(_HOST_HOLDER)
+    if _HOST_CELL is not None and _HOST_CELL[0] >= 0:
+        holder = {"device": int(_HOST_CELL[0]), "since": _HOST_CELL[1]}
     age = time.monotonic() - holder.get("since", time.monotonic())
     return f"host link held by gpu{holder.get('device', '?')} for {age:.0f} s"
 
 
 def _release_shared() -> None:
     _HOST_HOLDER.clear()
+    if _HOST_CELL is not None:
+        _HOST_CELL[0] = -1.0
     _HOST_SHARED.release()
+
+
+def use_host_lock(lock: Any, cell: Any) -> None:
+    """Take turns at the SHARED_TESTS with other *processes*: ``lock`` a ``multiprocessing`` lock and ``cell`` a
+    shared ``array('d', 2)`` of (holding device, since) that every per-device diagnostic process of one agent cycle
+    was given (agent/isolation.py)."""
+    global _HOST_SHARED, _HOST_CELL
+    _HOST_SHARED, _HOST_CELL = lock, cell
 
 
 def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,

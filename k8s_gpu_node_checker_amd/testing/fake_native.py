@@ -47,8 +47,13 @@ class FakeDiagLib:
                  hbm_xcd_slow: Optional[Dict[int, float]] = None, hbm_bad: Optional[Dict[Tuple[int, int], int]] = None,
                  compute_rate: Optional[Dict[int, float]] = None,
                  hung_pairs: Tuple[Tuple[int, int], ...] = (), p2p_wall_s: float = 0.0,
-                 gemm_bad_tiles: Optional[Dict[Tuple[int, str], Dict[int, int]]] = None):
+                 gemm_bad_tiles: Optional[Dict[Tuple[int, str], Dict[int, int]]] = None,
+                 hang_devices: Tuple[int, ...] = (), abort_devices: Tuple[int, ...] = ()):
         from ..ops import diag
+        # hang_devices: a GEMM call on that device never returns (a hung queue: no deadline ends it);
+        # abort_devices: it ends the process with SIGABRT, as the HIP runtime does on a GPU memory fault
+        self.hang_devices = set(hang_devices)
+        self.abort_devices = set(abort_devices)
         self.ref = diag.REFERENCE_RATES
         self.kinds = diag.MFMA_KINDS
         self.n = n
@@ -133,6 +138,14 @@ class FakeDiagLib:
 
     def _gemm(self, test, device, size, tflops, err, ms):
         self._log(device, test)
+        if device in self.abort_devices:
+            import os
+            import resource
+            resource.setrlimit(resource.RLIMIT_CORE, (0, 0))  # no core file from a scripted abort
+            os.abort()
+        if device in self.hang_devices:
+            while True:
+                time.sleep(3600)
         self._enter("gemm")
         if self.delay_s:
             time.sleep(self.delay_s)
@@ -337,8 +350,10 @@ class FakeFabricLib:
     """``libmi355x_fabric.so`` (in-process RCCL communicator over the node's GPUs)."""
 
     def __init__(self, busbw: float = 320.0, errors: int = 0, fail_open: bool = False, version: int = 22707,
-                 hang_op: Optional[int] = None, async_error_op: Optional[int] = None):
+                 hang_op: Optional[int] = None, async_error_op: Optional[int] = None, ignore_deadline: bool = False):
         self.busbw, self.errors, self.fail_open, self.version = busbw, errors, fail_open, version
+        # ignore_deadline: the hang_op collective never returns, deadline or not (a wait stuck in the driver)
+        self.ignore_deadline = ignore_deadline
         # hang_op: that collective never completes -- the call waits out its deadline (or forever without
         # one, until `release` is set) and then "aborts" the communicators like fabric.hip's abort_all
         self.hang_op = hang_op
@@ -361,7 +376,7 @@ class FakeFabricLib:
     def fabric_run(self, ctx, op, nbytes, iters, warmup, out, timeout_ms=0.0):
         self.timeouts_ms.append(timeout_ms)
         if op == self.hang_op:
-            self.release.wait(timeout_ms / 1e3 if timeout_ms > 0 else None)
+            self.release.wait(timeout_ms / 1e3 if timeout_ms > 0 and not self.ignore_deadline else None)
             if not self.release.is_set():
                 self.aborts += 1  # ncclCommAbort on every communicator
                 self.err = (f"timed collectives: not complete within {timeout_ms:.0f} ms: communicators aborted "
@@ -385,3 +400,15 @@ class FakeFabricLib:
 
     def fabric_rccl_version(self):
         return self.version
+
+
+def install(n: int = 1, fabric: Optional[Dict] = None, **diag_kw) -> None:
+    """Make this process's ``ops.diag`` and ``ops.fabric`` use the fakes: ``FakeDiagLib(n, **diag_kw)`` and
+    ``FakeFabricLib(**fabric)``.  The node agent's diagnostic children run it first when the agent is given
+    ``diag_setup=("k8s_gpu_node_checker_amd.testing.fake_native", "install", {...})`` (agent/isolation.py), so the
+    child code path runs unchanged on CPU with scripted GPUs."""
+    from ..ops import diag
+    from ..ops import fabric as fabric_mod
+    lib = FakeDiagLib(n=n, **diag_kw)
+    diag.lib = lambda: lib
+    fabric_mod._lib = FakeFabricLib(**(fabric or {}))

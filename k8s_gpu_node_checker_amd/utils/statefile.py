@@ -54,6 +54,10 @@ def load(path: str) -> Optional[Dict[str, Any]]:
     for k in ("exit_code", "runs"):
         if not isinstance(doc.get(k, 0), int) or isinstance(doc.get(k), bool):
             doc.pop(k, None)
+    if "gpu_sketch" in doc and sketch_members(doc["gpu_sketch"]) is None:
+        doc.pop("gpu_sketch")
+    if not isinstance(doc.get("not_ready_digest", ""), str):
+        doc.pop("not_ready_digest")
     return doc
 
 
@@ -77,15 +81,68 @@ def outcome(result: Any) -> Dict[str, Any]:
             "gpu_nodes": names, "gpu_count": len(names), "members": members_digest(names)}
 
 
-#: a published outcome (the watcher's Lease) keeps the member names only up to this many; beyond, the digest and
-#: count stand in for them (:func:`left_gpu_set` then decides from those)
-COMPACT_MEMBERS = 1000
+#: what a published outcome (the watcher's Lease annotation, ``kube/lease.STATE_MAX_BYTES``) may take as JSON
+STATE_MAX_BYTES = 64 << 10
 
 
-def compact(state: Dict[str, Any]) -> Dict[str, Any]:
-    if len(state.get("gpu_nodes") or ()) <= COMPACT_MEMBERS:
+def name_hash(name: str, width: int) -> bytes:
+    """The first ``width`` bytes of a node name's SHA-256 (a member of the compacted set's sketch)."""
+    return hashlib.sha256(name.encode("utf-8", "surrogatepass")).digest()[:width]
+
+
+def sketch(names: list, width: int) -> str:
+    """The member set as sorted ``width``-byte name hashes, base64: ``width`` x 4/3 bytes a member instead of the
+    name, and still able to tell that a previous member is gone when the set also grew (:func:`left_gpu_set`)."""
+    import base64
+    return f"{width}:" + base64.b64encode(b"".join(sorted({name_hash(n, width) for n in names}))).decode()
+
+
+def sketch_members(value: Any) -> Optional[tuple]:
+    """(width, set of hashes) of a :func:`sketch`, None when it is not one."""
+    import base64
+    import binascii
+    if not isinstance(value, str) or ":" not in value:
+        return None
+    w, _, b64 = value.partition(":")
+    try:
+        width, raw = int(w), base64.b64decode(b64, validate=True)
+    except (ValueError, binascii.Error):
+        return None
+    if width not in (4, 8) or len(raw) % width:
+        return None
+    return width, {raw[i:i + width] for i in range(0, len(raw), width)}
+
+
+def _size(state: Dict[str, Any]) -> int:
+    return len(json.dumps(state, sort_keys=True, separators=(",", ":")))
+
+
+def compact(state: Dict[str, Any], max_bytes: int = STATE_MAX_BYTES) -> Dict[str, Any]:
+    """The outcome shrunk until it fits ``max_bytes`` of JSON (the Lease), losing as little as it can:
+
+    1. as it is;
+    2. the member names replaced by an 8-byte hash each (:func:`sketch`; ~6,000 members), then a 4-byte one
+       (~12,000) -- a departure is still seen when the set also grew (one node leaves while two join);
+    3. no member list (digest and count: a departure hidden by growth is missed);
+    4. the not-Ready names replaced by their digest and count (a change of that set is still seen).
+
+    Sized by serialized bytes, not by count: 1,000 real node names (40-70 characters) alone exceed 64 KiB."""
+    if _size(state) <= max_bytes:
         return state
-    return {k: v for k, v in state.items() if k != "gpu_nodes"}
+    base = {k: v for k, v in state.items() if k != "gpu_nodes"}
+    names = state.get("gpu_nodes") if isinstance(state.get("gpu_nodes"), list) else None
+    if names is not None:
+        for width in (8, 4):
+            s = dict(base, gpu_sketch=sketch(names, width))
+            if _size(s) <= max_bytes:
+                return s
+    if _size(base) <= max_bytes:
+        return base
+    nr = base.get("not_ready")
+    if isinstance(nr, list):
+        base = {k: v for k, v in base.items() if k != "not_ready"}
+        base.update(not_ready_digest=members_digest(sorted(nr)), not_ready_count=len(nr))
+    return base
 
 
 def save(path: str, result: Any, prev: Optional[Dict[str, Any]] = None) -> None:
@@ -129,8 +186,11 @@ def should_notify(prev: Optional[Dict[str, Any]], result: Any, only_on_error: bo
     if prev is not None and prev.get("exit_code", 0) != 0:
         return True  # recovery
     if on_node_change:
-        before = sorted(prev.get("not_ready") or []) if prev is not None else []
-        if not_ready(result) != before:
+        now = not_ready(result)
+        if prev is not None and isinstance(prev.get("not_ready_digest"), str) and "not_ready" not in prev:
+            if members_digest(now) != prev["not_ready_digest"]:  # compacted: the names are gone, the digest is not
+                return True
+        elif now != (sorted(prev.get("not_ready") or []) if prev is not None else []):
             return True  # a node went down (or came back) while others stay Ready
         return left_gpu_set(prev, result)
     return False
@@ -147,6 +207,12 @@ def left_gpu_set(prev: Optional[Dict[str, Any]], result: Any) -> bool:
     if isinstance(names, list):
         now = {n["name"] for n in result.gpu_nodes}
         return any(n not in now for n in names)
+    sk = sketch_members(prev.get("gpu_sketch"))
+    if sk is not None:
+        # compacted to name hashes: a previous member whose hash no current name has is gone (a departed node whose
+        # hash collides with a current node's is missed: 1 in 2^64 / 2^32 per name)
+        width, before = sk
+        return bool(before - {name_hash(n["name"], width) for n in result.gpu_nodes})
     digest, count = prev.get("members"), prev.get("gpu_count")
     if isinstance(digest, str) and isinstance(count, int) and not isinstance(count, bool):
         # names not kept (a large fleet's compacted Lease state): a different set that did not grow lost a node

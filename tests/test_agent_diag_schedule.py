@@ -167,7 +167,7 @@ def test_hung_diagnostic_is_reported_not_waited_for(monkeypatch):
     assert rep["gpus"][1]["diag"]["watchdog"]["pass"] is False
     # the hang clears: its real result replaces the watchdog failure
     release.set()
-    ag._diag_threads[1].thread.join(5)
+    ag._diag_threads[1].job.thread.join(5)
     rep = ag.probe_once()
     assert rep["gpus"][1]["diag"] == {"gemm": {"pass": True}} and rep["state"] == HEALTHY
 
@@ -381,7 +381,7 @@ def test_healthz_fails_once_a_diagnostic_outlives_twice_its_watchdog(monkeypatch
         assert body.startswith("gpu0 diagnostics running for") and "2 x --diag-timeout" in body
         assert w.gpus
         release.set()
-        ag._diag_threads[0].thread.join(5)
+        ag._diag_threads[0].job.thread.join(5)
         assert urllib.request.urlopen(url, timeout=5).status == 200
     finally:
         release.set()
@@ -431,7 +431,7 @@ def test_per_gpu_diagnostics_wait_while_a_fabric_suite_is_hung(monkeypatch):
         assert all(g["diag"] for g in rep["gpus"])  # the last results are kept
     finally:
         release.set()
-    ag._fabric_thread.thread.join(5)
+    ag._fabric_thread.job.thread.join(5)
     w.clock += 1
     ag.probe_once()
     assert sorted(w.runs) == [0, 0, 1, 1]

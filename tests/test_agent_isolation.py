@@ -1,0 +1,180 @@
+"""Process isolation of the agent's HIP diagnostics (agent/isolation.py): each cycle's suites
+run in disposable children of a forkserver started before the agent touches amd-smi or HIP.  The children run the
+real ``ops/diag`` code against the fake C ABIs (``testing/fake_native.install``), so a hung or aborting GPU is
+scripted on CPU; the agent process itself never loads a diagnostics library."""
+import os
+import time
+import urllib.request
+
+import pytest
+
+from k8s_gpu_node_checker_amd.agent import agent as A
+from k8s_gpu_node_checker_amd.agent import isolation
+from k8s_gpu_node_checker_amd.models import health as H
+from k8s_gpu_node_checker_amd.ops import amdsmi_probe, diag
+from k8s_gpu_node_checker_amd.testing import fixtures
+
+FAKE = "k8s_gpu_node_checker_amd.testing.fake_native"
+
+
+@pytest.fixture
+def node(monkeypatch):
+    """An n-GPU MI355X node: the amd-smi report in this process, the diagnostics only in children (a call to the
+    diag library here fails the test)."""
+    def make(n=2, **overrides):
+        monkeypatch.setattr(amdsmi_probe, "probe", lambda nd, src, fx: fixtures.mi355x_probe_report(
+            nd, gpus=n, **overrides))
+
+        def no_hip_here():
+            raise AssertionError("the agent process called the HIP diagnostics library")
+        monkeypatch.setattr(diag, "lib", no_hip_here)
+    return make
+
+
+def agent(n=2, level=1, timeout=30.0, **fake):
+    return A.Agent("n", source="fake", diag_level=level, diag_interval=0.0, diag_timeout=timeout, expect_gpus=n,
+                   diag_when="always", isolation="process", diag_setup=(FAKE, "install", dict(n=n, **fake)))
+
+
+def gone(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return True
+    try:  # a zombie not yet reaped by its parent counts as gone
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split(")")[-1].split()[0] == "Z"
+    except OSError:
+        return True
+
+
+def test_diagnostics_run_in_children_and_the_agent_never_loads_hip(node):
+    node(2)
+    ag = agent(2)
+    rep = ag.probe_once()
+    assert rep["state"] == H.HEALTHY
+    for g in rep["gpus"]:
+        assert g["diag"]["gemm"]["pass"] and g["diag"]["hbm"]["pass"]
+        proc = g["diag_proc"]
+        assert proc["pid"] != os.getpid() and proc["peak_rss_mib"] > 0 and gone(proc["pid"])
+    kinds = [c["what"] for c in ag.workers.started]
+    assert kinds == ["hip-enumerate", "diag-gpu0", "diag-gpu1"]
+    assert ag._bdf == {0: "0000:05:00.0", 1: "0000:15:00.0"}  # PCI addresses from the enumeration child
+    # the child's metadata is not part of the annotation nor of the change digest
+    assert "diag_proc" not in ag.annotation(rep)[A.HEALTH_ANNOTATION]
+    m = A._metrics(rep)
+    assert 'mi355x_agent_diag_child_peak_rss_bytes{gpu="0"' in m
+    # the next cycle starts fresh children (new pids): nothing of the last one is kept
+    rep2 = ag.probe_once()
+    assert {g["diag_proc"]["pid"] for g in rep2["gpus"]}.isdisjoint({g["diag_proc"]["pid"] for g in rep["gpus"]})
+
+
+def test_a_hung_gpu_child_is_killed_at_the_watchdog_and_published_failed(node, mock_cluster):
+    """The done-when of VERDICT r5 #2: the agent publishes a failed verdict within --diag-timeout, /healthz stays
+    200, the hung child is gone, and the next cycle diagnoses the GPU again in a new child."""
+    from k8s_gpu_node_checker_amd.kube.client import KubeClient
+    from k8s_gpu_node_checker_amd.kube.config import ClusterConnection
+    node(2)
+    srv = mock_cluster([fixtures.realistic_node("n", gpu_count=2)])
+    ag = agent(2, timeout=2.0, hang_devices=(1,))
+    http = A.serve(ag, "127.0.0.1", 0, stale_after=60)
+    url = f"http://127.0.0.1:{http.server_address[1]}/healthz"
+    try:
+        t0 = time.monotonic()
+        rep = ag.probe_once()
+        wall = time.monotonic() - t0
+        with KubeClient(ClusterConnection(srv.url)) as kc:
+            ag.publish(kc, rep)
+            cond = [c for c in kc.get_node("n")["status"]["conditions"] if c["type"] == H.HEALTH_CONDITION][0]
+        assert wall < 2.0 + isolation.KILL_GRACE_S + 3, wall
+        g0, g1 = rep["gpus"]
+        assert g0["diag"]["gemm"]["pass"]
+        wd = g1["diag"]["watchdog"]
+        assert wd["pass"] is False and "within 2 s (GPU hang?): diagnostic process" in wd["detail"]
+        assert wd["detail"].endswith("killed")
+        assert rep["state"] == H.UNHEALTHY and cond["status"] == "False" and "watchdog" in cond["message"]
+        hung = [c["pid"] for c in ag.workers.started if c["what"] == "diag-gpu1"]
+        assert len(hung) == 1 and gone(hung[0])
+        assert ag._diag_threads == {} and ag.hung_diagnostic() is None and ag.hip_lost is None
+        assert urllib.request.urlopen(url, timeout=5).status == 200
+        # the next cycle: GPU 1 gets a new child (and is reported hung again), GPU 0 keeps passing
+        rep = ag.probe_once()
+        assert len([c for c in ag.workers.started if c["what"] == "diag-gpu1"]) == 2
+        assert "watchdog" in rep["gpus"][1]["diag"] and rep["gpus"][0]["diag"]["gemm"]["pass"]
+        assert urllib.request.urlopen(url, timeout=5).status == 200
+    finally:
+        http.shutdown()
+        http.server_close()
+
+
+def test_a_gpu_fault_that_aborts_the_runtime_costs_its_child_not_the_agent(node):
+    node(2)
+    ag = agent(2, abort_devices=(0,))
+    rep = ag.probe_once()
+    run = rep["gpus"][0]["diag"]["run"]
+    assert run["pass"] is False and "ended before reporting (signal SIGABRT)" in run["detail"]
+    assert rep["gpus"][1]["diag"]["gemm"]["pass"] and rep["state"] == H.UNHEALTHY
+    assert ag.hung_diagnostic() is None and ag.hip_lost is None
+
+
+def test_no_hip_device_in_the_enumeration_child(node):
+    node(2)
+    ag = agent(0)
+    rep = ag.probe_once()
+    assert [g.get("diag_skipped") for g in rep["gpus"]] == \
+        ["no HIP device visible to the agent (/dev/kfd and /dev/dri mounted?)"] * 2
+    assert [c["what"] for c in ag.workers.started] == ["hip-enumerate"]
+
+
+def test_level2_fabric_suite_runs_in_its_own_child(node):
+    node(2)
+    ag = agent(2, level=2)
+    rep = ag.probe_once()
+    assert rep["fabric"]["p2p"]["pass"] and rep["fabric"]["rccl"]["pass"] and rep["state"] == H.HEALTHY
+    assert [c["what"] for c in ag.workers.started] == ["hip-enumerate", "diag-gpu0", "diag-gpu1", "diag-fabric"]
+    assert "fabric" in ag.diag_procs and ag.diag_procs["fabric"]["pid"] != os.getpid()
+
+
+def test_a_hung_fabric_child_is_killed_and_the_suite_runs_again(node):
+    """An RCCL wait that ignores its deadline (stuck in the driver): the fabric child is SIGKILLed at the watchdog;
+    what it left queued ended with it, so the suite is not barred from running again (thread isolation must bar it,
+    fabric_abandoned)."""
+    node(2)
+    ag = agent(2, level=2, timeout=2.0, fabric={"hang_op": 0, "ignore_deadline": True})
+    t0 = time.monotonic()
+    rep = ag.probe_once()
+    assert time.monotonic() - t0 < 2 * 2.0 + isolation.KILL_GRACE_S + 3
+    wd = rep["fabric"]["watchdog"]
+    assert wd["pass"] is False and "fabric hang?): diagnostic process" in wd["detail"] and rep["state"] == H.UNHEALTHY
+    assert ag.fabric_abandoned is None and ag._fabric_thread is None
+    rep = ag.probe_once()
+    assert len([c for c in ag.workers.started if c["what"] == "diag-fabric"]) == 2
+
+
+def test_host_link_turns_are_shared_across_children(node):
+    """The suites of one cycle take turns at the PCIe host link through a multiprocessing lock: with a child that
+    hangs inside its host-link test, another child reports that test skipped, naming the holder, within its own
+    deadline."""
+    lock, cell = isolation.Workers("process").host_lock()
+    diag.use_host_lock(lock, cell)
+    try:
+        assert diag._acquire_shared(3, None) is None
+        assert cell[0] == 3.0
+        why = diag._acquire_shared(5, time.monotonic() + 0.2)
+        assert why.startswith("host link held by gpu3 for ")
+        diag._release_shared()
+        assert cell[0] == -1.0 and diag._acquire_shared(5, time.monotonic() + 0.2) is None
+        diag._release_shared()
+    finally:
+        import threading
+        diag.use_host_lock(threading.Lock(), None)
+
+
+def test_isolation_flag_and_thread_mode_default():
+    assert A.build_parser().parse_args([]).diag_isolation == "process"
+    assert A.build_parser().parse_args(["--diag-isolation", "thread"]).diag_isolation == "thread"
+    assert A.Agent("n", diag_level=1).isolation == "thread"  # the library default (benchmark, in-process tests)
+    assert A.Agent("n", diag_level=0, isolation="process").isolation == "thread"  # no diagnostics: no forkserver
+    with pytest.raises(ValueError):
+        A.Agent("n", isolation="container")
+    assert isolation.describe_exit(-9) == "signal SIGKILL" and isolation.describe_exit(3) == "exit code 3"

@@ -705,6 +705,43 @@ def test_agent_cli_once_runs_idle_diagnostics(repo):
     assert rep["state"] in ("healthy", "degraded"), rep["state"]
 
 
+_ISOLATED_AGENT = r"""
+import json, os, sys
+from k8s_gpu_node_checker_amd.agent.agent import Agent
+ag = Agent("gpu-node", source="native", diag_level=1, devices=[0], diag_when="always", diag_interval=0.0,
+           isolation="process")
+reps = [ag.probe_once() for _ in range(2)]
+maps = open("/proc/self/maps").read()
+with open(f"/proc/{os.getpid()}/status") as f:
+    rss = next(int(l.split()[1]) // 1024 for l in f if l.startswith("VmRSS:"))
+print(json.dumps({"pid": os.getpid(), "rss_mib": rss, "reps": reps, "started": ag.workers.started,
+                  "hip_in_agent": "libamdhip64" in maps, "diag_in_agent": "libmi355x_diag" in maps}))
+"""
+
+
+def test_agent_process_isolation_keeps_hip_out_of_the_agent(repo):
+    """VERDICT r5 #2 on the GPU: the agent's level-1 diagnostics run in forkserver children; the agent process
+    itself never maps the HIP runtime or the diagnostics library, stays small, and each cycle's child is new."""
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip("no GPU")
+    _wait_until_idle()
+    p = subprocess.run([sys.executable, "-c", _ISOLATED_AGENT], capture_output=True, text=True, timeout=300, cwd=repo,
+                       env=dict(os.environ, PYTHONPATH=repo))
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    print(json.dumps({k: d[k] for k in ("rss_mib", "started", "hip_in_agent", "diag_in_agent")}))
+    assert not d["hip_in_agent"] and not d["diag_in_agent"], d
+    procs = [r["gpus"][0]["diag_proc"] for r in d["reps"]]
+    print(json.dumps(procs))
+    for r in d["reps"]:
+        g = r["gpus"][0]
+        assert g["diag"]["gemm"]["pass"] and g["diag"]["hbm"]["pass"], g["diag"]
+    assert procs[0]["pid"] != procs[1]["pid"] and d["pid"] not in (procs[0]["pid"], procs[1]["pid"])
+    assert procs[0]["peak_rss_mib"] > d["rss_mib"]  # the HIP work's memory was the child's, not the agent's
+    assert d["rss_mib"] < 100, d["rss_mib"]
+
+
 def test_agent_diagnostics_threads_per_device(dev):
     from k8s_gpu_node_checker_amd.agent.agent import Agent
     from k8s_gpu_node_checker_amd.ops import diag

@@ -221,7 +221,7 @@ def test_hung_slots_leave_the_rest_waiting_not_running(monkeypatch):
     assert sorted(started) == [0, 1] and rep["gpus"][3]["diag_skipped"].startswith("waiting for a diagnostic slot")
     release.set()
     for r in list(ag._diag_threads.values()):
-        r.thread.join(5)
+        r.job.thread.join(5)
     rep = ag.probe_once()
     assert sorted(started) == [0, 1, 2, 3]
 

@@ -249,11 +249,13 @@ def test_malformed_baseline_entries_are_rebuilt_not_fatal(tmp_path):
     p = tmp_path / "b.json"
     res = lambda: {"pass": True, "rates": {"tflops": 1000.0}, "expect": {"tflops": 1000.0},  # noqa: E731
                    "shape": [1, 1, 1]}
-    p.write_text(json.dumps({"schema": B.SCHEMA_V1, "gpus": {
-        "a": {"gemm@[1,1,1]": ["not", "a", "dict"]},
-        "b": {"gemm@[1,1,1]": {"samples": "junk"}},
-        "c": {"gemm@[1,1,1]": {"samples": [1, {"tflops": 1.0}]}},
-        "d": {"gemm@[1,1,1]": {"baseline": {"tflops": 0}, "runs": 5}}}}))
+    from k8s_gpu_node_checker_amd.ops.diag import rate_revision
+    rev = rate_revision("gemm")
+    p.write_text(json.dumps({"schema": B.SCHEMA, "gpus": {
+        "a": {"epoch": None, "tests": {"gemm@[1,1,1]": ["not", "a", "dict"]}},
+        "b": {"epoch": None, "tests": {"gemm@[1,1,1]": {"samples": "junk", "rev": rev}}},
+        "c": {"epoch": None, "tests": {"gemm@[1,1,1]": {"samples": [1, {"tflops": 1.0}], "rev": rev}}},
+        "d": {"epoch": None, "tests": {"gemm@[1,1,1]": {"baseline": {"tflops": 0}, "runs": 5, "rev": rev}}}}}))
     b = B.Baselines(str(p), runs=2)
     for gpu in "abcd":
         assert b.observe(gpu, {"gemm": res()}) == []
@@ -433,17 +435,76 @@ def test_peer_excused_runs_under_the_floor_never_form_a_baseline():
     assert b.baseline("g", "gemm", res(0.9)) == {"tflops": 0.9}
 
 
-def test_a_v1_baseline_file_is_read_and_upgraded(tmp_path):
+def test_baselines_from_before_revisions_are_dropped_not_adopted(tmp_path):
+    """a baseline is a fraction of the references of its day; v1 (no epoch) and v2 (no revision)
+    entries were formed under references that may since have moved, so they re-form instead of silently shifting the
+    drift line."""
+    res = {"rates": {"tflops": 900.0}, "expect": {"tflops": 1000.0}, "shape": [1, 1, 1]}
     p = tmp_path / "b.json"
     p.write_text(json.dumps({"schema": B.SCHEMA_V1, "gpus": {"uuid:x": {
         "gemm@[1,1,1]": {"baseline": {"tflops": 1.0}, "runs": 5, "since": 1.0}}}}))
+    assert B.Baselines(str(p)).data == {}
+    p.write_text(json.dumps({"schema": B.SCHEMA_V2, "gpus": {"uuid:x": {"epoch": "driver 6.18.54", "tests": {
+        "gemm@[1,1,1]": {"baseline": {"tflops": 1.0}, "runs": 5, "since": 1.0}}}}}))
     b = B.Baselines(str(p))
-    res = {"rates": {"tflops": 800.0}, "expect": {"tflops": 1000.0}, "shape": [1, 1, 1]}
-    notes = b.observe("uuid:x", {"gemm": res}, epoch="driver 6.18.54")
-    assert notes == ["gemm: tflops at 80% of this GPU's own baseline (5 clean runs)"]  # kept, not re-formed
+    assert b.data["uuid:x"]["tests"] == {} and b.epoch("uuid:x") == "driver 6.18.54"
+    assert b.observe("uuid:x", {"gemm": dict(res)}, epoch="driver 6.18.54") == []  # forming again: no drift
     doc = json.loads(p.read_text())
-    assert doc["schema"] == B.SCHEMA and doc["gpus"]["uuid:x"]["epoch"] == "driver 6.18.54"
-    assert doc["gpus"]["uuid:x"]["tests"]["gemm@[1,1,1]"]["baseline"] == {"tflops": 1.0}
+    assert doc["schema"] == B.SCHEMA and doc["gpus"]["uuid:x"]["tests"]["gemm@[1,1,1]"]["samples"] == [{"tflops": 0.9}]
+
+
+def test_a_reference_or_kernel_change_re_forms_that_test_only(tmp_path):
+    """new REFERENCE_RATES (or a new kernel) for one test move its fractions; that test's
+    baseline re-forms, the others keep theirs."""
+    b = B.Baselines(runs=2)
+    gemm = lambda f: {"rates": {"tflops": 1000.0 * f}, "expect": {"tflops": 1000.0}, "shape": [1, 1, 1]}  # noqa: E731
+    hbm = lambda f: {"rates": {"read_tbs": 7.0 * f}, "expect": {"read_tbs": 7.0}, "gib": 2.0}  # noqa: E731
+    revs = {"gemm": "r1", "hbm": "h1"}
+    for _ in range(2):
+        b.observe("g", {"gemm": gemm(1.0), "hbm": hbm(1.0)}, revision=revs.get)
+    assert b.baseline("g", "gemm", gemm(1.0)) == {"tflops": 1.0}
+    # the gemm references were raised 7.6 %: the same GPU now measures 0.93 of them -- not drift, a new yardstick
+    revs["gemm"] = "r2"
+    assert b.observe("g", {"gemm": gemm(0.85), "hbm": hbm(0.85)}, revision=revs.get) == [
+        "hbm: read_tbs at 85% of this GPU's own baseline (2 clean runs)"]
+    assert b.baseline("g", "gemm", gemm(1.0)) is None and b.baseline("g", "hbm", hbm(1.0)) == {"read_tbs": 1.0}
+    b.observe("g", {"gemm": gemm(0.93)}, revision=revs.get)
+    assert b.baseline("g", "gemm", gemm(1.0)) == {"tflops": 0.89}  # re-formed on the new references
+    # the stamp the agent uses moves with REFERENCE_RATES and KERNEL_REVISION
+    from k8s_gpu_node_checker_amd.ops import diag
+    before = diag.rate_revision("gemm")
+    old = dict(diag.REFERENCE_RATES["gemm"])
+    try:
+        diag.REFERENCE_RATES["gemm"][4096] += 1
+        assert diag.rate_revision("gemm") != before and diag.rate_revision("hbm") == diag.rate_revision("hbm")
+    finally:
+        diag.REFERENCE_RATES["gemm"].clear()
+        diag.REFERENCE_RATES["gemm"].update(old)
+    assert diag.rate_revision("gemm") == before and set(diag.KERNEL_REVISION) >= {"gemm", "gemm_fp8", "hbm", "mfma"}
+
+
+def test_a_transient_amd_smi_miss_is_not_a_new_epoch():
+    """one probe without the VBIOS (or the driver) must neither wipe the baselines nor, when the
+    field comes back, re-form them a second time; a component that does differ still re-forms."""
+    b = B.Baselines(runs=1)
+    res = lambda f: {"rates": {"tflops": 1000.0 * f}, "expect": {"tflops": 1000.0}, "shape": [1, 1, 1]}  # noqa: E731
+    full = "driver 6.18.54; vbios 00175784; fw pm=1,sos=2"
+    b.observe("g", {"gemm": res(1.0)}, epoch=full)
+    for partial in ("driver 6.18.54; fw pm=1,sos=2", "vbios 00175784; fw pm=1,sos=2", "driver 6.18.54; vbios 00175784",
+                    None, full):
+        assert b.observe("g", {"gemm": res(0.8)}, epoch=partial) == [
+            "gemm: tflops at 80% of this GPU's own baseline (1 clean runs)"], partial
+        assert b.epoch("g") == full and "previous" not in b.data["g"]
+    # a component first seen later is filled in, nothing re-forms
+    b2 = B.Baselines(runs=1)
+    b2.observe("g", {"gemm": res(1.0)}, epoch="fw pm=1")
+    assert b2.observe("g", {"gemm": res(0.8)}, epoch="driver 6.18.54; fw pm=1")
+    assert b2.epoch("g") == "driver 6.18.54; fw pm=1"
+    # a real change of a known component re-forms
+    b.observe("g", {"gemm": res(0.9)}, epoch="driver 6.19.2; fw pm=1,sos=2")
+    assert b.data["g"]["previous"]["epoch"] == full and b.epoch("g") == "driver 6.19.2; fw pm=1,sos=2"
+    assert B.epoch_parts(full) == {"driver": "6.18.54", "vbios": "00175784", "fw:pm": "1", "fw:sos": "2"}
+    assert B.epoch_str(B.epoch_parts(full)) == full
 
 
 def test_baselines_can_be_dropped_by_flag_and_by_a_loopback_post(node, tmp_path, monkeypatch):

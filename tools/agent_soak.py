@@ -57,6 +57,27 @@ def _rss_mb(pid: int):
     return None
 
 
+def _descendants(pid: int):
+    """RSS (MiB) of every live descendant of ``pid`` (process isolation: the forkserver, and a diagnostic child if
+    one is running at the sample), by pid."""
+    kids = {}
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat") as f:
+                ppid = int(f.read().rsplit(")", 1)[1].split()[1])
+        except (OSError, ValueError, IndexError):
+            continue
+        kids.setdefault(ppid, []).append(int(d))
+    out, todo = {}, list(kids.get(pid, []))
+    while todo:
+        c = todo.pop()
+        out[c] = _rss_mb(c)
+        todo.extend(kids.get(c, []))
+    return {k: v for k, v in out.items() if v is not None}
+
+
 def _get(url: str, timeout: float = 5.0):
     try:
         with urllib.request.urlopen(url, timeout=timeout) as r:
@@ -81,6 +102,8 @@ def main() -> int:
     ap.add_argument("--sample", type=float, default=10.0)
     ap.add_argument("--port", type=int, default=19464)
     ap.add_argument("--out", default="gpurun_out/agent_soak.json")
+    ap.add_argument("--diag-isolation", choices=("process", "thread"), default="process",
+                    help="agent --diag-isolation (default process, as deployed)")
     ap.add_argument("--baseline", action="store_true",
                     help="run the agent with --diag-baseline-file, report the baselines it formed (epoch, ratios) "
                          "and drop them at the end through POST /baseline/reset")
@@ -94,7 +117,8 @@ def main() -> int:
            "--interval", str(args.interval), "--diag-level", str(args.diag_level),
            "--diag-interval", str(args.diag_interval), "--publish", "annotation,http",
            "--listen", f"127.0.0.1:{args.port}", "--kubeconfig", kc, "--annotation-encoding", "gzip",
-           "--label-node", "--xgmi-links", "0", "--ignore-pid", str(os.getpid())]
+           "--label-node", "--xgmi-links", "0", "--ignore-pid", str(os.getpid()),
+           "--diag-isolation", args.diag_isolation]
     baseline_path = os.path.join(os.path.dirname(kc), "baseline.json")
     if args.baseline:
         cmd += ["--diag-baseline-file", baseline_path]
@@ -124,6 +148,11 @@ def main() -> int:
                      "reason": cond and cond.get("reason"),
                      "heartbeat_age_s": round(time.time() - hb, 1) if hb else None, "healthz": hz,
                      "state": rep.get("state"), "agent_rss_mb": _rss_mb(agent.pid),
+                     # process isolation: the forkserver (and a child caught mid-diagnostic), and the peak RSS of the
+                     # child that produced the last result (its own getrusage, reported over the pipe)
+                     "children_rss_mb": _descendants(agent.pid),
+                     "diag_child_peak_mb": (g.get("diag_proc") or {}).get("peak_rss_mib"),
+                     "diag_child_pid": (g.get("diag_proc") or {}).get("pid"),
                      "vram_used_mb": g.get("vram_used_mb"), "diag_pass": {k: v.get("pass") for k, v in diag.items()
                                                                           if isinstance(v, dict)},
                      "labels": {k: v for k, v in (node["metadata"].get("labels") or {}).items()
@@ -161,6 +190,13 @@ def main() -> int:
         "healthz_seen": sorted({str(s["healthz"]) for s in samples}),
         "heartbeat_age_s": _spread([s["heartbeat_age_s"] for s in samples]),
         "agent_rss_mb": _spread(rss), "agent_rss_first_last": [rss[0], rss[-1]] if rss else None,
+        "diag_isolation": args.diag_isolation,
+        # the smallest descendant total seen: the forkserver alone, between diagnostic children
+        "children_rss_mb_min_total": min((sum(s["children_rss_mb"].values()) for s in samples), default=None),
+        "resident_total_mb": _spread([s["agent_rss_mb"] + min(s["children_rss_mb"].values() or [0])
+                                      for s in samples if s["agent_rss_mb"]]),
+        "diag_child_peak_mb": _spread([s["diag_child_peak_mb"] for s in samples]),
+        "diag_children_seen": len({s["diag_child_pid"] for s in samples if s["diag_child_pid"]}),
         "vram_used_mb": _spread([s["vram_used_mb"] for s in samples]),
         "diag_failures": sum(1 for s in samples for v in s["diag_pass"].values() if v is False),
         "apiserver_writes": {p: sum(1 for e in writes if e["path"] == p) for p in sorted({e["path"] for e in writes})},
