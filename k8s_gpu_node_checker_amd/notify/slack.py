@@ -81,8 +81,10 @@ def send_slack_message(webhook_url: Optional[str], message: str, username: str =
             resp = webhook.post(webhook_url, body, timeout=timeout, ssl_context=ssl_context)
         except HTTPError as e:
             # requests' ConnectionError / Timeout: retried only when the text names a reset or an aborted
-            # connection (the reference's test, :88)
-            if e.kind != "invalid_url" and ("Connection reset by peer" in str(e) or "Connection aborted" in str(e)):
+            # connection (the reference's test, :88).  A body cut short after the head ("incomplete": requests'
+            # ChunkedEncodingError, a RequestException) is not one of those, whatever its text names (:101-104)
+            if e.kind not in ("invalid_url", "incomplete") and (
+                    "Connection reset by peer" in str(e) or "Connection aborted" in str(e)):
                 if attempt < max_retries:
                     print(f"슬랙 메시지 전송 실패 ({attempt + 1}/{attempts}회 시도): {e}", file=err)
                     print(f"⏳ {retry_delay}초 후 재시도합니다...", file=err)

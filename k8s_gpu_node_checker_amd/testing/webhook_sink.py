@@ -28,7 +28,8 @@ The URL path selects the behaviour, so one sink serves every test:
 ``/raw/NAME``   a malformed or unusual response: ``badstatus``, ``notahttp``, ``truncated`` (body shorter than its
                 length), ``badchunk``, ``truncatedchunk``, ``continue`` (100 then 200), ``http10``, ``longheader``,
                 ``twolengths``, ``empty200``, ``manyheaders``, ``justenoughheaders``, ``longstatus``,
-                ``prematurechunk``, ``badcl``, ``samecl``, ``status99``, ``chunkext``
+                ``prematurechunk``, ``badcl``, ``samecl``, ``status99``, ``chunkext``, ``resetbody`` (a 200 head and
+                part of its body, then TCP RST: the connection dies mid-body after the server took the POST)
 ``/locb/S/L``   the same with ``L``'s percent-decoded bytes sent raw (a Location that is not UTF-8)
 ==============  =============================================================
 
@@ -145,6 +146,12 @@ class _SinkHandler(socketserver.BaseRequestHandler):
         path = req["path"].split("?", 1)[0]
         if path.startswith("/body/"):  # a 500 whose body is encoded some way: /body/gzip, deflate, chunked, ...
             self._send_body(path[6:])
+            return
+        if path == "/raw/resetbody":  # the head and 10 of 100 bytes, then RST once the client is reading the body
+            self.request.sendall(b"HTTP/1.1 200 OK\r\nContent-Length: 100\r\n\r\nonly ten b")
+            time.sleep(0.2)
+            self.request.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+            self.request.close()
             return
         if path.startswith("/raw/"):  # a malformed or unusual response (see _RAW)
             self.request.sendall(_RAW[path[5:]])

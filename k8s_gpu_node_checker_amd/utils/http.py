@@ -506,6 +506,19 @@ class Connection:
 
     def _finish_body(self, method: str, status: int, reason: str, headers: List[Tuple[str, str]],
                      hmap: Dict[str, str], peek) -> Response:
+        try:
+            return self._body_of(method, status, reason, headers, hmap, peek)
+        except _socket.timeout:
+            raise
+        except OSError as e:
+            # the head arrived, the body did not (a reset or abort mid-body): urllib3's ProtocolError("Connection
+            # broken: ...") that requests raises as ChunkedEncodingError -- a RequestException, not a ConnectionError,
+            # so the reference does not retry it (a server that processed the POST is not sent it twice)
+            self.close()
+            raise HTTPError("incomplete", _broken(repr(e)))
+
+    def _body_of(self, method: str, status: int, reason: str, headers: List[Tuple[str, str]],
+                 hmap: Dict[str, str], peek) -> Response:
         if method == "HEAD" or status in (204, 304):
             body = b""
         elif "chunked" in hmap.get("transfer-encoding", "").lower():

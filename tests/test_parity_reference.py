@@ -385,7 +385,8 @@ def test_slack_error_body_decoding_identical(cluster, sink, kind):
 
 @pytest.mark.parametrize("kind", ["badstatus", "notahttp", "status99", "longstatus", "longheader", "manyheaders",
                                   "justenoughheaders", "truncated", "badchunk", "truncatedchunk", "prematurechunk",
-                                  "chunkext", "twolengths", "samecl", "badcl", "continue", "http10", "empty200"])
+                                  "chunkext", "twolengths", "samecl", "badcl", "continue", "http10", "empty200",
+                                  "resetbody"])
 def test_slack_malformed_responses_identical(cluster, sink, kind):
     """Responses that break HTTP one way each: the head http.client refuses ('Connection aborted.', retried), a
     body cut short or badly chunked ('Connection broken: …', not retried), unmatching or invalid lengths, and
