@@ -35,6 +35,7 @@ process (:func:`fabric_abandoned`).
 from __future__ import annotations
 
 import argparse
+import functools
 import json
 import os
 import socket
@@ -363,19 +364,22 @@ def _annotation_gpu(g: Dict[str, Any]) -> Dict[str, Any]:
     return out
 
 
-def _fabric_suite(devices: List[int], timeout_s: Optional[float] = None) -> Dict[str, Any]:
-    """The node-level tests (``ops/diag.fabric_tests``): the xGMI pair matrix and the RCCL collectives in this
-    process, both under the watchdog's deadline -- the matrix within ``P2P_SHARE`` of it, the collectives
+def _fabric_suite(devices: List[int], timeout_s: Optional[float] = None, link: Optional[float] = None) -> Dict[str, Any]:
+    """The node-level tests (``ops/diag.fabric_tests``): the xGMI pair matrix (pairs, then every source's fan to all
+    its peers; ``link`` = one link's GB/s from amd-smi's training, the absolute floor's anchor) and the RCCL
+    collectives, both under the watchdog's deadline -- the matrix within ``P2P_SHARE`` of it, the collectives
     within what is left up to 90 % -- so a hung copy or collective is given up, and named in the report,
-    rather than left holding the fabric thread."""
+    rather than left holding the fabric job."""
     from ..ops import diag
     try:
-        res = diag.fabric_tests(devices, timeout_s=timeout_s or None)
+        res = diag.fabric_tests(devices, timeout_s=timeout_s or None, link=link)
     except Exception as e:  # the diag library itself is missing
         return {"p2p": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
     m, r = res.get("p2p") or {}, res.get("rccl") or {}
-    out: Dict[str, Any] = {"p2p": {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "detail", "wall_s",
-                                                     "stopped") if k in m}}
+    out: Dict[str, Any] = {"p2p": {k: m[k] for k in ("pass", "median_gbps", "min_gbps", "floor_gbps", "link_gbps",
+                                                     "detail", "wall_s", "stopped") if k in m}}
+    if isinstance(m.get("fan"), dict):  # the fan's summary (its per-destination rows stay with mi355x-diag)
+        out["p2p"]["fan"] = {k: v for k, v in m["fan"].items() if k != "to"}
     out["rccl"] = {k: r.get(k) for k in ("pass", "best_busbw_gbps", "best_busbw_by_op", "detail", "wall_s",
                                          "rccl", "aborted") if k in r or k not in ("aborted",)}
     return out
@@ -722,7 +726,12 @@ class Agent:
             # the per-GPU tests: a collective that never completes (a link that stopped passing traffic) is a
             # failed fabric, not a frozen agent.
             done = threading.Event()
-            job = self.workers.fabric(_fabric_suite, devices, self.diag_timeout, done)
+            # the absolute floor's link rate: the median GPU's trained xGMI link (amd-smi), so one GPU whose links
+            # trained down is judged against its hive's links, not the other way round
+            links = sorted(diag.link_gbs(g.get("xgmi_width"), g.get("xgmi_speed_gbps"))
+                           for g in (entries.get(d) or {} for d in devices))
+            suite = functools.partial(_fabric_suite, link=links[len(links) // 2] if links else None)
+            job = self.workers.fabric(suite, devices, self.diag_timeout, done)
             self._fabric_thread = _DiagRun(job, now, time.monotonic())
         if self._fabric_thread is not None:
             r = self._fabric_thread

@@ -2636,6 +2636,141 @@ int diag_p2p_copy(int src, int dst, size_t bytes, int iters, double* gbps, unsig
   return diag_p2p_copy_t(src, dst, bytes, iters, 0.0, gbps, errors, peer);
 }
 
+// The "fan" pass of the xGMI check: `src` copies to all `ndst` peers at once, so every one of its links carries
+// traffic together (the pair pass loads one link at a time; a link that holds up alone but not under load -- a
+// marginal lane retraining, an engine shared with another link -- only shows here).  One source buffer with the
+// address-hash pattern, one destination buffer per peer, one non-blocking stream per peer on `src`; every stream
+// waits on a common start event, runs `iters` hipMemcpyPeerAsync of `bytes` and records its own end, so
+// gbps[i] = the rate peer i saw while all were running and *total_gbps = all bytes over the slowest stream's end.
+// Each destination is then verified against the pattern (errors[i]); peer[i] = direct peer access both ways.
+// `timeout_ms` > 0 bounds copies and verification as in diag_p2p_copy_t (-4 "hung", resources leaked on purpose).
+int diag_p2p_fan_t(int src, const int* dsts, int ndst, size_t bytes, int iters, double timeout_ms, double* gbps,
+                   unsigned long long* errors, int* peer, double* total_gbps) {
+  constexpr int kMaxFan = 64;  // a CPX hive: 63 peers
+  int n = 0;
+  DIAG_CHECK(hipGetDeviceCount(&n));
+  if (src < 0 || src >= n || ndst < 1 || ndst > kMaxFan || iters < 1 || bytes < 16) {
+    g_err = "p2p fan: need a valid source, 1..64 peers, iters >= 1, bytes >= 16";
+    return -2;
+  }
+  for (int i = 0; i < ndst; ++i) {
+    if (dsts[i] < 0 || dsts[i] >= n || dsts[i] == src) {
+      g_err = "p2p fan: every peer must be a device other than the source";
+      return -2;
+    }
+    for (int j = 0; j < i; ++j)
+      if (dsts[j] == dsts[i]) {
+        g_err = "p2p fan: a peer is listed twice";
+        return -2;
+      }
+  }
+  int cur = 0;
+  DIAG_CHECK(hipGetDevice(&cur));
+  for (int i = 0; i < ndst; ++i) {
+    int sd = 0, ds = 0;
+    DIAG_CHECK(hipDeviceCanAccessPeer(&sd, src, dsts[i]));
+    DIAG_CHECK(hipDeviceCanAccessPeer(&ds, dsts[i], src));
+    peer[i] = sd && ds;
+    if (peer[i]) {
+      DIAG_CHECK(enable_peer(src, dsts[i]));
+      DIAG_CHECK(enable_peer(dsts[i], src));
+    }
+    errors[i] = 0;
+    gbps[i] = 0.0;
+  }
+  *total_gbps = 0.0;
+  const size_t nvec = bytes / sizeof(uint4);
+  const size_t nbytes = nvec * sizeof(uint4);
+  const uint64_t seed = 0xFA17ULL + static_cast<uint64_t>(src) * 131;
+  DevBuf a;
+  DevBuf b[kMaxFan], cnt[kMaxFan];
+  DIAG_CHECK(a.alloc(src, nbytes));
+  DIAG_CHECK(hipSetDevice(src));
+  hipLaunchKernelGGL(mt_write_kernel, dim3(grid_for(src, 4)), dim3(256), 0, nullptr, static_cast<uint4*>(a.ptr), nvec,
+                     seed, 0);
+  DIAG_CHECK(hipGetLastError());
+  DIAG_CHECK(hipDeviceSynchronize());
+  const unsigned long long init[2] = {0ULL, ~0ULL};
+  for (int i = 0; i < ndst; ++i) {
+    DIAG_CHECK(b[i].alloc(dsts[i], nbytes));
+    DIAG_CHECK(cnt[i].alloc(dsts[i], sizeof init));
+    DIAG_CHECK(hipMemset(b[i].ptr, 0xA5, nbytes));
+    DIAG_CHECK(hipMemcpy(cnt[i].ptr, init, sizeof init, hipMemcpyHostToDevice));
+    DIAG_CHECK(hipDeviceSynchronize());
+  }
+  // streams and events on the source device: a head stream records the common start, each peer's stream waits
+  // on it, then copies (after one untimed warm-up copy per peer, mapping the pages and waking the engines)
+  DIAG_CHECK(hipSetDevice(src));
+  Timer head;
+  DIAG_CHECK(head.create(true));
+  Timer per[kMaxFan];
+  for (int i = 0; i < ndst; ++i) {
+    DIAG_CHECK(per[i].create(true));
+    DIAG_CHECK(hipMemcpyPeerAsync(b[i].ptr, dsts[i], a.ptr, src, nbytes, per[i].stream));
+    DIAG_CHECK(hipEventRecord(per[i].e0, per[i].stream));
+  }
+  for (int i = 0; i < ndst; ++i) DIAG_CHECK(hipStreamWaitEvent(head.stream, per[i].e0, 0));  // warm-ups done
+  DIAG_CHECK(hipEventRecord(head.e0, head.stream));
+  for (int i = 0; i < ndst; ++i) {
+    DIAG_CHECK(hipStreamWaitEvent(per[i].stream, head.e0, 0));
+    for (int it = 0; it < iters; ++it) DIAG_CHECK(hipMemcpyPeerAsync(b[i].ptr, dsts[i], a.ptr, src, nbytes, per[i].stream));
+    DIAG_CHECK(hipEventRecord(per[i].e1, per[i].stream));
+  }
+  const PollDeadline dl(timeout_ms);
+  Timer verify[kMaxFan];
+  auto hung = [&](int i, const char* stage) {
+    // in-flight copies may still target these buffers: leak everything rather than free under them
+    a.ptr = nullptr;
+    for (int j = 0; j < ndst; ++j) {
+      b[j].ptr = cnt[j].ptr = nullptr;
+      per[j].e0 = per[j].e1 = nullptr;
+      per[j].stream = nullptr;
+      verify[j].e0 = verify[j].e1 = nullptr;
+    }
+    head.e0 = head.e1 = nullptr;
+    head.stream = nullptr;
+    (void)hipSetDevice(cur);
+    char msg[192];
+    std::snprintf(msg, sizeof msg, "p2p fan %d->%d: %s did not complete within %.0f ms (xGMI link or engine hung)",
+                  src, dsts[i], stage, timeout_ms);
+    g_err = msg;
+    return -4;
+  };
+  float slowest = 0.f;
+  for (int i = 0; i < ndst; ++i) {
+    hipError_t w = wait_event_polled(per[i].e1, dl);
+    if (w == hipErrorNotReady) return hung(i, "copies");
+    DIAG_CHECK(w);
+    float ms = 0.f;
+    DIAG_CHECK(event_ms(head.e0, per[i].e1, &ms));
+    gbps[i] = ms > 0.f ? static_cast<double>(iters) * static_cast<double>(nbytes) / (ms * 1e-3) / 1e9 : 0.0;
+    slowest = std::max(slowest, ms);
+  }
+  *total_gbps = slowest > 0.f
+                    ? static_cast<double>(ndst) * iters * static_cast<double>(nbytes) / (slowest * 1e-3) / 1e9
+                    : 0.0;
+  for (int i = 0; i < ndst; ++i) {
+    DIAG_CHECK(hipSetDevice(dsts[i]));
+    DIAG_CHECK(verify[i].create(false));
+    unsigned long long* c = static_cast<unsigned long long*>(cnt[i].ptr);
+    hipLaunchKernelGGL(mt_verify_kernel, dim3(grid_for(dsts[i], 4)), dim3(256), 0, nullptr,
+                       static_cast<const uint4*>(b[i].ptr), nvec, seed, 0, c, c + 1);
+    DIAG_CHECK(hipGetLastError());
+    DIAG_CHECK(hipEventRecord(verify[i].e0, nullptr));
+  }
+  for (int i = 0; i < ndst; ++i) {
+    hipError_t w = wait_event_polled(verify[i].e0, dl);
+    if (w == hipErrorNotReady) return hung(i, "verification");
+    DIAG_CHECK(w);
+    unsigned long long h[2];
+    DIAG_CHECK(hipSetDevice(dsts[i]));
+    DIAG_CHECK(hipMemcpy(h, cnt[i].ptr, sizeof h, hipMemcpyDeviceToHost));
+    errors[i] = h[0];
+  }
+  DIAG_CHECK(hipSetDevice(cur));
+  return 0;
+}
+
 // Matrix-core burn-in of one precision (`kind` as mfma_burn_kernel): `reps` launches of `iters`
 // iterations on every CU; *tflops = dense rate, *errors = wave-lanes whose exact result differed.
 int diag_mfma_burn_map(int device, int kind, int iters, int reps, double* tflops, unsigned long long* errors,

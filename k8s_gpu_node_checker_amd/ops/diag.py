@@ -161,6 +161,14 @@ GEMM_FP8_CK_TOL = 1e-5
 MEMTEST_MAX_ERRORS = 0
 MFMA_KINDS = ("bf16", "fp8", "mxfp8", "mxfp4")
 P2P_MIN_FRACTION_OF_MEDIAN = 0.5  # a GPU pair slower than half the node's median pair: suspect link
+# The absolute anchor of the xGMI pair matrix: one direction of one link carries lanes x Gb/s / 8 GB/s -- x16 at
+# 38 Gb/s on MI355X (amd-smi's xgmi_link_width / xgmi_link_speed, profiles/amdsmi_xgmi_link_metrics_mi355x.json), 76
+# GB/s -- and a pair copying under half of that fails whatever its node's median is, so a hive whose links are all
+# degraded alike fails too.  The fan pass (every peer of a source at once) is judged against half of the fan's median
+# destination and a quarter of the link: under load the copy engines, not only the links, set the pace.  Both floors
+# are set from the link's signalling rate, not from a measurement: no 8-GPU node was available to this project.
+P2P_MIN_FRACTION_OF_LINK = 0.5
+P2P_FAN_MIN_FRACTION_OF_LINK = 0.25
 # burn-in waves of one XCD taking this much longer than the median XCD's: that XCD's clock domain (or a
 # CU in it) lags -- degraded, not failed (the rate floors above judge the chip as a whole).  A healthy
 # MI355X spreads 1.003-1.024 (20 burn-ins, profiles/mfma_xcd_map_mi355x.json), so 1.15 is ~6x its noise.
@@ -326,6 +334,10 @@ def lib() -> ctypes.CDLL:
         L.diag_p2p_copy_t.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong),
                                       ctypes.POINTER(ctypes.c_int)]
+        L.diag_p2p_fan_t.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_size_t,
+                                     ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_int),
+                                     ctypes.POINTER(ctypes.c_double)]
         _lib = L
     return _lib
 
@@ -839,31 +851,67 @@ def p2p_copy(src: int, dst: int, mib: int = 256, iters: int = 5, timeout_s: Opti
     return {"src": src, "dst": dst, "gbps": round(gbps.value, 1), "errors": errs.value, "peer": bool(peer.value)}
 
 
+def link_gbs(width: Any = None, speed_gbps: Any = None) -> float:
+    """One direction of one xGMI link in GB/s from its trained lanes and per-lane rate (amd-smi), the MI355X's x16 at
+    38 Gb/s for whichever is unknown."""
+    from ..models.health import XGMI_LINK_GBPS, XGMI_LINK_WIDTH
+    w = width if isinstance(width, int) and not isinstance(width, bool) and width > 0 else XGMI_LINK_WIDTH
+    sp = speed_gbps if isinstance(speed_gbps, (int, float)) and not isinstance(speed_gbps, bool) and speed_gbps > 0 \
+        else XGMI_LINK_GBPS
+    return w * sp / 8.0
+
+
+def p2p_fan(src: int, dsts: List[int], mib: int = 256, iters: int = 5,
+            timeout_s: Optional[float] = None) -> Dict[str, Any]:
+    """``src`` copying to every one of ``dsts`` at once (all its links loaded together): per destination the GB/s it
+    saw, pattern errors and peer access, and the source's total.  ``{"hung": True, ...}`` at the deadline."""
+    n = len(dsts)
+    arr = (ctypes.c_int * n)(*dsts)
+    gbps, errs, peer = (ctypes.c_double * n)(), (ctypes.c_ulonglong * n)(), (ctypes.c_int * n)()
+    total = ctypes.c_double()
+    ms = 0.0 if not timeout_s else max(1.0, 1000.0 * timeout_s)
+    rc = lib().diag_p2p_fan_t(src, arr, n, mib << 20, iters, ms, gbps, errs, peer, ctypes.byref(total))
+    if rc == P2P_HUNG:
+        return {"src": src, "hung": True, "detail": lib().diag_last_error().decode(errors="replace"), "to": []}
+    _check(rc)
+    return {"src": src, "total_gbps": round(total.value, 1),
+            "to": [{"dst": d, "gbps": round(gbps[i], 1), "errors": errs[i], "peer": bool(peer[i])}
+                   for i, d in enumerate(dsts)]}
+
+
 def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5,
-               timeout_s: Optional[float] = None) -> Dict[str, Any]:
-    """Every ordered pair of ``devices`` (default: all): the node's xGMI fabric, link by link.
+               timeout_s: Optional[float] = None, link: Optional[float] = None, fan: bool = True) -> Dict[str, Any]:
+    """Every ordered pair of ``devices`` (default: all): the node's xGMI fabric, link by link, then (``fan``) every
+    source to all its peers at once.
 
     Pass: every pair has direct peer access, delivers its bytes intact, and runs at no less than
-    ``P2P_MIN_FRACTION_OF_MEDIAN`` of the median pair (relative, so it holds for any hive size,
-    partition mode or firmware; an absolute floor would need per-platform numbers).
+    ``P2P_MIN_FRACTION_OF_MEDIAN`` of the median pair (relative: one slow link among good ones) and no less than
+    ``P2P_MIN_FRACTION_OF_LINK`` of ``link`` GB/s (absolute: a hive whose links are all slow alike; ``link`` from the
+    training amd-smi reports, :func:`link_gbs`); under the fan every destination delivers intact at no less than
+    ``P2P_MIN_FRACTION_OF_MEDIAN`` of the fan's median destination and ``P2P_FAN_MIN_FRACTION_OF_LINK`` of ``link``.
 
-    ``timeout_s`` bounds the whole matrix: each pair gets what is left of it, and the first pair that hangs
-    ends the matrix (its devices are in an unknown state, with copies possibly still queued behind it), as
-    does a deadline that passes between pairs; both fail the test and name the pair.
+    ``timeout_s`` bounds the whole matrix, both passes: each copy gets what is left of it, and the first that hangs
+    ends the matrix (its devices are in an unknown state, with copies possibly still queued behind it), as does a
+    deadline that passes between copies; both fail the test and name the pair or the source.
     """
     devs = list(range(device_count())) if devices is None else list(devices)
     t0 = time.perf_counter()
     if len(devs) < 2:
         return {"pass": True, "skipped": f"{len(devs)} GPU(s): no pairs", "pairs": [], "detail": ""}
+    link = float(link) if link else link_gbs()
+    floor = P2P_MIN_FRACTION_OF_LINK * link
     order = [(a, b) for a in devs for b in devs if a != b]
     pairs: List[Dict[str, Any]] = []
     stopped = ""
+
+    def left() -> Optional[float]:
+        return None if not timeout_s else timeout_s - (time.perf_counter() - t0)
     for a, b in order:
-        left = None if not timeout_s else timeout_s - (time.perf_counter() - t0)
-        if left is not None and left <= 0:
+        rest = left()
+        if rest is not None and rest <= 0:
             stopped = f"deadline of {timeout_s:g} s passed after {len(pairs)}/{len(order)} pairs"
             break
-        p = p2p_copy(a, b, mib, iters) if left is None else p2p_copy(a, b, mib, iters, timeout_s=left)
+        p = p2p_copy(a, b, mib, iters) if rest is None else p2p_copy(a, b, mib, iters, timeout_s=rest)
         if p.get("hung"):
             stopped = f"{a}->{b} hung: {p['detail']}"
             break
@@ -871,14 +919,44 @@ def p2p_matrix(devices: Optional[list] = None, mib: int = 256, iters: int = 5,
     rates = sorted(p["gbps"] for p in pairs) or [0.0]
     median = rates[len(rates) // 2]
     slow = [p for p in pairs if p["gbps"] < P2P_MIN_FRACTION_OF_MEDIAN * median]
+    under = [p for p in pairs if p["gbps"] < floor and p not in slow]
     bad = [p for p in pairs if p["errors"]]
     nopeer = [p for p in pairs if not p["peer"]]
     problems = (([stopped] if stopped else [])
                 + [f"{p['src']}->{p['dst']} {p['gbps']} GB/s" for p in slow]
+                + [f"{p['src']}->{p['dst']} {p['gbps']} GB/s under {floor:.0f} GB/s "
+                   f"({P2P_MIN_FRACTION_OF_LINK:.0%} of a {link:.0f} GB/s link)" for p in under]
                 + [f"{p['src']}->{p['dst']} {p['errors']} bad words" for p in bad]
                 + [f"{p['src']}->{p['dst']} no peer access" for p in nopeer])
-    out = {"pass": not problems, "pairs": pairs, "median_gbps": median, "min_gbps": rates[0],
-           "wall_s": round(time.perf_counter() - t0, 3), "detail": "; ".join(problems[:8])}
+    out: Dict[str, Any] = {"pairs": pairs, "median_gbps": median, "min_gbps": rates[0], "link_gbps": round(link, 1),
+                           "floor_gbps": round(floor, 1)}
+    if fan and not stopped:
+        fans: List[Dict[str, Any]] = []
+        for a in devs:
+            rest = left()
+            if rest is not None and rest <= 0:
+                stopped = f"deadline of {timeout_s:g} s passed after {len(fans)}/{len(devs)} fan sources"
+                break
+            peers = [b for b in devs if b != a]
+            f = p2p_fan(a, peers, mib, iters) if rest is None else p2p_fan(a, peers, mib, iters, timeout_s=rest)
+            if f.get("hung"):
+                stopped = f"fan from {a} hung: {f['detail']}"
+                break
+            fans.append(f)
+        dests = [dict(t, src=f["src"]) for f in fans for t in f["to"]]
+        frates = sorted(t["gbps"] for t in dests) or [0.0]
+        fmed = frates[len(frates) // 2]
+        ffloor = P2P_FAN_MIN_FRACTION_OF_LINK * link
+        fslow = [t for t in dests if t["gbps"] < P2P_MIN_FRACTION_OF_MEDIAN * fmed or t["gbps"] < ffloor]
+        fbad = [t for t in dests if t["errors"]]
+        if stopped:
+            problems.insert(0, stopped)
+        problems += ([f"fan {t['src']}->{t['dst']} {t['gbps']} GB/s with every link of {t['src']} busy" for t in fslow]
+                     + [f"fan {t['src']}->{t['dst']} {t['errors']} bad words" for t in fbad])
+        out["fan"] = {"sources": len(fans), "median_gbps": fmed, "min_gbps": frates[0],
+                      "floor_gbps": round(ffloor, 1),
+                      "total_gbps": {str(f["src"]): f["total_gbps"] for f in fans}, "to": dests}
+    out.update({"pass": not problems, "wall_s": round(time.perf_counter() - t0, 3), "detail": "; ".join(problems[:8])})
     if stopped:
         out["stopped"] = stopped
     return out
@@ -1053,7 +1131,11 @@ def _summary(test: str, r: Dict[str, Any]) -> str:
     if test == "p2p":
         if r.get("skipped"):
             return f"skipped ({r['skipped']})"
-        return f"median {r.get('median_gbps', 0)} / min {r.get('min_gbps', 0)} GB/s over {len(r.get('pairs') or [])} pairs"
+        fan = r.get("fan") if isinstance(r.get("fan"), dict) else {}
+        tail = (f"; fan median {fan.get('median_gbps', 0)} / min {fan.get('min_gbps', 0)} GB/s over {fan.get('sources', 0)}"
+                " sources" if fan else "")
+        return (f"median {r.get('median_gbps', 0)} / min {r.get('min_gbps', 0)} GB/s over {len(r.get('pairs') or [])} "
+                f"pairs (floor {r.get('floor_gbps', '?')}){tail}")
     if test == "rccl":
         rows = r.get("rows") or []
         ops = len({x.get("op") for x in rows})
@@ -1125,12 +1207,13 @@ def run_devices(level: int, devices: List[int], parallel: int = 8) -> Dict[int, 
 
 
 # share of a node-level deadline the xGMI pair matrix may use before the RCCL suite (an 8-GPU matrix is 56 pairs of
-# 6 x 256 MiB copies plus a verify pass each: seconds at xGMI rates, far inside 0.45 x the agent's 300 s default)
+# 6 x 256 MiB copies plus a verify pass each, then 8 fans of 7 such copies at once: seconds at xGMI rates, far inside
+# 0.45 x the agent's 300 s default)
 P2P_SHARE = 0.45
 
 
 def fabric_tests(devices: List[int], p2p: bool = True, rccl: bool = True,
-                 timeout_s: Optional[float] = None) -> Dict[str, Any]:
+                 timeout_s: Optional[float] = None, link: Optional[float] = None) -> Dict[str, Any]:
     """The node-level tests of level 2: the xGMI pair matrix (within ``P2P_SHARE`` of ``timeout_s``) and the RCCL
     collectives (within what is left up to 90 %, aborted at that deadline); without a timeout both wait as long
     as they take.  A test that raises is reported as failed; only a missing diag library propagates."""
@@ -1139,7 +1222,7 @@ def fabric_tests(devices: List[int], p2p: bool = True, rccl: bool = True,
     t0 = _time.monotonic()
     if p2p:
         try:
-            out["p2p"] = p2p_matrix(devices, timeout_s=P2P_SHARE * timeout_s if timeout_s else None)
+            out["p2p"] = p2p_matrix(devices, timeout_s=P2P_SHARE * timeout_s if timeout_s else None, link=link)
         except NativeUnavailable:
             raise
         except Exception as e:  # a pair that errors out is a failed fabric, not a lost report

@@ -48,8 +48,14 @@ class FakeDiagLib:
                  compute_rate: Optional[Dict[int, float]] = None,
                  hung_pairs: Tuple[Tuple[int, int], ...] = (), p2p_wall_s: float = 0.0,
                  gemm_bad_tiles: Optional[Dict[Tuple[int, str], Dict[int, int]]] = None,
-                 hang_devices: Tuple[int, ...] = (), abort_devices: Tuple[int, ...] = ()):
+                 hang_devices: Tuple[int, ...] = (), abort_devices: Tuple[int, ...] = (),
+                 fan_slow: Optional[Dict[Tuple[int, int], float]] = None,
+                 fan_errors: Optional[Dict[Tuple[int, int], int]] = None):
         from ..ops import diag
+        # the fan pass (diag_p2p_fan_t): fan_slow[(src, dst)] = that pair's rate while every link of src is busy,
+        # fan_errors[(src, dst)] = bad words it delivers then
+        self.fan_slow = dict(fan_slow or {})
+        self.fan_errors = dict(fan_errors or {})
         # hang_devices: a GEMM call on that device never returns (a hung queue: no deadline ends it);
         # abort_devices: it ends the process with SIGABRT, as the HIP runtime does on a GPU memory fault
         self.hang_devices = set(hang_devices)
@@ -343,6 +349,28 @@ class FakeDiagLib:
         _put(gbps, ctypes.c_double, self.slow_pairs.get((src, dst), self.p2p_gbps))
         _put(errors, ctypes.c_ulonglong, 0)
         _put(peer, ctypes.c_int, 0 if (src, dst) in self.nopeer else 1)
+        return 0
+
+    def diag_p2p_fan_t(self, src, dsts, ndst, nbytes, iters, timeout_ms, gbps, errors, peer, total):
+        """Every peer of ``src`` at once: a pair's rate is ``fan_slow[(src, dst)]`` when given (a link that holds up
+        alone but not under load), else its pair rate (``slow_pairs`` / ``p2p_gbps``)."""
+        with self.lock:
+            self.calls.append(f"fan{src}")
+            self.p2p_timeouts_ms.append(float(timeout_ms))
+        peers = [dsts[i] for i in range(ndst)]
+        if not 0 <= src < self.n or not peers or any(not 0 <= d < self.n or d == src for d in peers):
+            self.err = b"p2p fan: every peer must be a device other than the source"
+            return -2
+        for d in peers:
+            if (src, d) in self.hung_pairs and timeout_ms > 0 and not self.release.wait(timeout_ms / 1000.0):
+                self.err = b"p2p fan %d->%d: copies did not complete within %d ms (xGMI link or engine hung)" % (
+                    src, d, int(timeout_ms))
+                return -4
+        for i, d in enumerate(peers):
+            gbps[i] = self.fan_slow.get((src, d), self.slow_pairs.get((src, d), self.p2p_gbps))
+            errors[i] = self.fan_errors.get((src, d), 0)
+            peer[i] = 0 if (src, d) in self.nopeer else 1
+        _put(total, ctypes.c_double, float(sum(gbps[i] for i in range(ndst))))
         return 0
 
 

@@ -284,9 +284,15 @@ def test_p2p_matrix_flags_slow_corrupting_and_non_peer_pairs(monkeypatch):
         g, e, p = fake[(a, b)]
         return {"src": a, "dst": b, "gbps": g, "errors": e, "peer": p}
     monkeypatch.setattr(diag, "p2p_copy", p2p_copy)
+
+    def p2p_fan(src, dsts, mib=256, iters=5):  # every link of src at once: the pair rates again
+        return {"src": src, "total_gbps": sum(fake[(src, d)][0] for d in dsts),
+                "to": [{"dst": d, "gbps": fake[(src, d)][0], "errors": 0, "peer": True} for d in dsts]}
+    monkeypatch.setattr(diag, "p2p_fan", p2p_fan)
     m = diag.p2p_matrix([0, 1, 2])
     assert not m["pass"] and len(m["pairs"]) == 6 and m["median_gbps"] == 50.0 and m["min_gbps"] == 12.0
     assert "2->0 12.0 GB/s" in m["detail"] and "1->2 7 bad words" in m["detail"] and "2->1 no peer access" in m["detail"]
+    assert "fan 2->0 12.0 GB/s with every link of 2 busy" in m["detail"] and m["fan"]["sources"] == 3
     for k in list(fake):
         fake[k] = (50.0, 0, True)
     assert diag.p2p_matrix([0, 1, 2])["pass"]

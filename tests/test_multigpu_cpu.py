@@ -247,6 +247,64 @@ def test_capped_power_scales_the_compute_references(node8):
     assert A.power_fraction({}) is None
 
 
+def test_a_uniformly_slow_hive_fails_the_absolute_floor(node8):
+    """every xGMI pair at 20 GB/s is "normal" against its own median, so the relative rule alone
+    passes it; the absolute anchor (half a 76 GB/s x16 link at 38 Gb/s, from amd-smi's training) fails it."""
+    lib, fab = node8(p2p_gbps=20.0)
+    ag = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8)
+    rep = ag.probe_once()
+    p2p = rep["fabric"]["p2p"]
+    assert p2p["pass"] is False and p2p["median_gbps"] == 20.0
+    assert p2p["link_gbps"] == 76.0 and p2p["floor_gbps"] == 38.0
+    assert "0->1 20.0 GB/s under 38 GB/s (50% of a 76 GB/s link)" in p2p["detail"]
+    assert rep["state"] == H.UNHEALTHY and any(r.startswith("xGMI p2p failed") for r in ag.evaluate(rep).reasons)
+    # a healthy hive at 48 GB/s a pair passes both rules, and both passes ran: 56 pairs, 8 fans of 7
+    lib2, _ = node8()
+    rep = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8).probe_once()
+    p2p = rep["fabric"]["p2p"]
+    assert p2p["pass"] and p2p["fan"]["sources"] == 8 and p2p["fan"]["median_gbps"] == 48.0
+    assert sum(1 for c in lib2.calls if c.startswith("fan")) == 8 and p2p["fan"]["total_gbps"]["0"] == 7 * 48.0
+
+
+def test_the_floor_follows_the_trained_link_of_the_median_gpu(node8):
+    """Links trained x16 at 25 Gb/s on every GPU (amd-smi): the floor is half of 50 GB/s, so 30 GB/s pairs pass;
+    one GPU whose links trained down does not lower the hive's floor."""
+    node8.state["overrides"] = {f"gpu{i}": {"xgmi_speed_gbps": 25} for i in range(8)}
+    node8(p2p_gbps=30.0)
+    rep = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8).probe_once()
+    assert rep["fabric"]["p2p"]["floor_gbps"] == 25.0 and rep["fabric"]["p2p"]["pass"]
+    node8.state["overrides"] = {"gpu4": {"xgmi_width": 4}}
+    node8(p2p_gbps=48.0)
+    rep = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8).probe_once()
+    assert rep["fabric"]["p2p"]["floor_gbps"] == 38.0
+
+
+def test_one_link_slow_only_under_load_fails_the_fan_pass(node8):
+    """gpu2's link to gpu6 copies at full rate alone (the pair pass) but at 9 GB/s while every link of
+    gpu2 is busy (the fan): the fan names it; bad data under load fails too."""
+    lib, fab = node8(fan_slow={(2, 6): 9.0})
+    ag = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8)
+    rep = ag.probe_once()
+    p2p = rep["fabric"]["p2p"]
+    assert p2p["min_gbps"] == 48.0  # the pair pass saw nothing
+    assert p2p["pass"] is False and "fan 2->6 9.0 GB/s with every link of 2 busy" in p2p["detail"]
+    assert p2p["fan"]["min_gbps"] == 9.0 and rep["state"] == H.UNHEALTHY
+    node8(fan_errors={(5, 1): 3})
+    rep = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8).probe_once()
+    assert "fan 5->1 3 bad words" in rep["fabric"]["p2p"]["detail"]
+
+
+def test_fan_pass_arguments_and_a_hung_fan(node8):
+    from k8s_gpu_node_checker_amd.ops import diag as D
+    lib, _ = node8(hung_pairs=((4, 0),))
+    # the pair pass hangs first at 4->0 with a deadline; without the pair pass in the way, the fan hangs at it
+    f = D.p2p_fan(4, [0, 1, 2], mib=1, iters=1, timeout_s=0.05)
+    assert f["hung"] and "p2p fan 4->0" in f["detail"]
+    with pytest.raises(RuntimeError, match="every peer must be a device other than the source"):
+        D.p2p_fan(1, [1, 2])
+    assert D.link_gbs(16, 38) == 76.0 and D.link_gbs(None, None) == 76.0 and D.link_gbs(8, 32) == 32.0
+
+
 def test_hung_collective_is_aborted_and_reported_as_a_failed_rccl_row(node8):
     """A collective that never completes: the fabric suite's own deadline (0.9 x the watchdog) aborts the
     communicators (ncclCommAbort in fabric.hip) and the report names the hung collective."""
