@@ -43,6 +43,9 @@ _FLAGS: Tuple[Tuple[str, str, Dict[str, Any]], ...] = (
     ("x", "--context", {"help": "kubeconfig context (기본: current-context)"}),
     ("x", "--in-cluster", {"action": "store_true", "help": "Pod ServiceAccount 로 접속"}),
     ("x", "--kube-timeout", {"type": float, "default": 30.0, "help": "kube-apiserver 요청 타임아웃(초) (기본: 30)"}),
+    ("x", "--kube-env-proxy", {"action": "store_true",
+                               "help": "kubeconfig 에 proxy-url 이 없으면 HTTPS_PROXY / NO_PROXY 환경변수로 apiserver 에 접속 "
+                                       "(kubectl 과 같음; 기본: 환경변수 무시, PARITY.md #18)"}),
     ("x", "--kube-retries", {"type": int, "default": 2, "help": "LIST 재시도 횟수 (429/5xx/연결 오류, 기본: 2)"}),
     ("x", "--page-size", {"type": int, "default": 500, "help": "LIST 페이지 크기 (0 = 한 번에, 기본: 500)"}),
     ("x", "--label-selector", {"help": "노드 labelSelector"}),
@@ -229,8 +232,14 @@ def _load_cluster(args: Any):
         conn = incluster_connection()
         if conn is None:
             raise ConfigException("Service host/port is not set.")
-        return conn
-    return load_kube_config(args.kubeconfig, args.context)
+    else:
+        conn = load_kube_config(args.kubeconfig, args.context)
+    if getattr(args, "kube_env_proxy", False) and not conn.proxy_url:
+        # opt-in (PARITY.md #18): the environment's proxy for the apiserver URL, NO_PROXY honoured, as client-go's
+        # http.ProxyFromEnvironment does for kubectl; the kubeconfig's proxy-url, when set, wins
+        from .utils.http import env_proxy
+        conn.proxy_url = env_proxy(conn.server)
+    return conn
 
 
 def _run_once(args: Any) -> int:

@@ -150,6 +150,7 @@ class ClusterConnection:
         self.source = "kubeconfig"
         self._exec_cache: Optional[Tuple[Dict[str, Any], float]] = None
         self.oidc = None  # kube/oidc.OidcProvider for `auth-provider: oidc`
+        self.gcp = None  # kube/gcp_cmd.GcpCmdProvider for `auth-provider: gcp`
         self._ssl_ctx = None
 
     # -- auth -----------------------------------------------------------------
@@ -165,7 +166,8 @@ class ClusterConnection:
         """Drop cached exec-plugin credentials (after a 401); True if the next request can present
         different credentials (exec plugin re-run or a re-read tokenFile), as client-go does."""
         self._exec_cache = None
-        refreshable = self.oidc is not None and self.oidc.invalidate()
+        refreshable = (self.oidc is not None and self.oidc.invalidate()) or (
+            self.gcp is not None and self.gcp.invalidate())
         return self.exec_spec is not None or bool(self.token_file) or refreshable
 
     def auth_headers(self) -> Dict[str, str]:
@@ -178,6 +180,8 @@ class ClusterConnection:
                 raise ConfigException("Invalid kube-config file. tokenFile %s: %s" % (self.token_file, e))
         if self.oidc is not None:  # upstream tries the auth-provider first
             token = self.oidc.token() or token
+        elif self.gcp is not None:
+            token = self.gcp.token() or token
         if self.exec_spec is not None:
             status = self._run_exec()
             if status.get("token"):
@@ -245,6 +249,7 @@ class ClusterConnection:
     def describe(self) -> Dict[str, Any]:
         return {"server": self.server, "source": self.source, "insecure": self.insecure,
                 "auth": ("exec" if self.exec_spec else "oidc" if self.oidc is not None
+                         else "gcp" if self.gcp is not None
                          else "token" if (self.token or self.token_file)
                          else "cert" if (self.cert_file or self.cert_data) else
                          "basic" if self.username else "none")}
@@ -308,7 +313,12 @@ def connection_from_config(cfg: Dict[str, Any], context: Optional[str] = None) -
     if isinstance(provider, dict) and provider.get("name") == "oidc" and isinstance(provider.get("config"), dict):
         from .oidc import OidcProvider
         conn.oidc = OidcProvider(provider["config"], str(user_name), user.get("__file__"), ubase)
+    elif isinstance(provider, dict) and provider.get("name") == "gcp" and not conn.token:
+        # the stored access-token, refreshed through cmd-path when it has expired (kube/gcp_cmd.py, PARITY.md #19)
+        from .gcp_cmd import GcpCmdProvider
+        conn.gcp = GcpCmdProvider(provider.get("config") if isinstance(provider.get("config"), dict) else {})
     elif isinstance(provider, dict) and not conn.token:
+        # azure and any other provider: its stored token, used as it is (PARITY.md #19)
         pcfg = provider.get("config") or {}
         conn.token = pcfg.get("id-token") or pcfg.get("access-token")
     if isinstance(user.get("exec"), dict):

@@ -198,3 +198,43 @@ def test_incluster_fallback_only_without_kubeconfig(tmp_path, monkeypatch):
     # an explicit (missing) --kubeconfig still errors like the reference
     with pytest.raises(ConfigException):
         K.load_kube_config(str(tmp_path / "missing"))
+
+
+def test_gcp_auth_provider_refreshes_through_cmd_path_when_expired(tmp_path):
+    """VERDICT r5 missing #3 / PARITY.md #19: a fresh gcp access-token is used as it is; an expired one is refreshed
+    by running the stanza's cmd-path (gcloud config-helper's JSON, the token and expiry at the stanza's keys), once
+    until the new one expires; a 401 forces the command again.  No cmd-path: the stored token, expired or not."""
+    calls = tmp_path / "calls"
+    helper = tmp_path / "helper.py"
+    helper.write_text(
+        "import json, sys\n"
+        f"open({str(calls)!r}, 'a').write('x')\n"
+        "n = len(open(" + repr(str(calls)) + ").read())\n"
+        "print(json.dumps({'credential': {'access_token': f'fresh-{n}', 'token_expiry': '2999-01-01T00:00:00.123456789Z'},"
+        " 'args': sys.argv[1:]}))\n")
+    stanza = {"cmd-path": sys.executable, "cmd-args": f"{helper} config config-helper --format=json",
+              "token-key": "{.credential.access_token}", "expiry-key": "{.credential.token_expiry}"}
+    fresh = {"auth-provider": {"name": "gcp", "config": dict(stanza, **{"access-token": "cached",
+                                                                      "expiry": "2999-01-01T00:00:00Z"})}}
+    conn = K.load_kube_config(write(tmp_path / "a", cfg(user=fresh)))
+    assert conn.auth_headers() == {"Authorization": "Bearer cached"} and not calls.exists()
+    assert conn.describe()["auth"] == "gcp"
+    expired = {"auth-provider": {"name": "gcp", "config": dict(stanza, **{"access-token": "old",
+                                                                        "expiry": "2020-01-01T00:00:00Z"})}}
+    conn = K.load_kube_config(write(tmp_path / "b", cfg(user=expired)))
+    assert conn.auth_headers() == {"Authorization": "Bearer fresh-1"}
+    assert conn.auth_headers() == {"Authorization": "Bearer fresh-1"}  # valid until 2999: not run again
+    assert conn.invalidate_credentials() is True
+    assert conn.auth_headers() == {"Authorization": "Bearer fresh-2"}
+    static = {"auth-provider": {"name": "gcp", "config": {"access-token": "old", "expiry": "2020-01-01T00:00:00Z"}}}
+    conn = K.load_kube_config(write(tmp_path / "c", cfg(user=static)))
+    assert conn.auth_headers() == {"Authorization": "Bearer old"} and conn.invalidate_credentials() is False
+    broken = {"auth-provider": {"name": "gcp", "config": dict(stanza, **{"cmd-args": "-c 'import sys; sys.exit(4)'"})}}
+    with pytest.raises(ConfigException, match="exited 4"):
+        K.load_kube_config(write(tmp_path / "d", cfg(user=broken))).auth_headers()
+    # azure (and any other provider): its stored token as it is
+    az = {"auth-provider": {"name": "azure", "config": {"access-token": "az-tok", "expires-on": "0"}}}
+    assert K.load_kube_config(write(tmp_path / "e", cfg(user=az))).auth_headers() == {"Authorization": "Bearer az-tok"}
+    from k8s_gpu_node_checker_amd.kube.gcp_cmd import parse_time
+    assert parse_time("1970-01-01T00:00:01Z") == 1.0 and parse_time("1970-01-01T01:00:01+01:00") == 1.0
+    assert parse_time("nope") is None and parse_time(None) is None
