@@ -217,6 +217,16 @@ def fabric_abandoned(fab: Optional[Dict[str, Any]]) -> Optional[str]:
     return None
 
 
+def misdirected(expected_bdf: str, meta: Any) -> Optional[str]:
+    """Why a narrowed diagnostic child's result is not the expected GPU's (it reports the PCI address it ran on,
+    agent/isolation.device_main), else None: a HIP visibility mapping that disagrees with the enumeration must not
+    put one GPU's numbers under another's name."""
+    got = normalize_bdf((meta or {}).get("bdf")) if isinstance(meta, dict) else ""
+    if expected_bdf and got and got != normalize_bdf(expected_bdf):
+        return f"diagnostic process ran on {got}, not {normalize_bdf(expected_bdf)}: HIP device visibility mismatch"
+    return None
+
+
 def normalize_bdf(bdf: Any) -> str:
     """PCI address in amd-smi's form (``0000:05:00.0``, lower case); a domain-less ``05:00.0`` gets 0000."""
     b = str(bdf or "").strip().lower()
@@ -660,10 +670,13 @@ class Agent:
                 self.diag_procs[d] = r.box["meta"]
             if not r.is_alive():
                 del self._diag_threads[d]
+                wrong = misdirected(self._bdf.get(d, ""), r.box.get("meta"))
                 if r.job.killed:
                     finished[d] = {"watchdog": {
                         "pass": False, "detail": f"diagnostics did not finish within {self.diag_timeout:g} s (GPU "
                                                  f"hang?): diagnostic process {r.job.pid} killed"}}
+                elif wrong:
+                    finished[d] = {"run": {"pass": False, "detail": wrong}}
                 elif "res" in r.box:
                     finished[d] = r.box["res"]
                 self._diag_at[d] = r.started

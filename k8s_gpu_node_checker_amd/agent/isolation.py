@@ -96,20 +96,48 @@ def enumerate_main(conn: Any, setup: Setup = None) -> None:
     _reply(conn, res, t0)
 
 
+def narrow_to(device: int, environ: Optional[Dict[str, str]] = None) -> Optional[str]:
+    """Make HIP ordinal ``device`` of this process's environment the only device a HIP runtime started afterwards
+    sees (its ordinal 0): ``HIP_VISIBLE_DEVICES`` set to the entry ``device`` selects -- of an existing
+    ``HIP_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES`` list when one narrows this process already, else ``device``
+    itself.  Returns the selector, or None when the list has no such entry (nothing changed)."""
+    env = os.environ if environ is None else environ
+    sel = str(device)
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        cur = env.get(var)
+        if cur is not None and cur.strip():
+            items = [x.strip() for x in cur.split(",") if x.strip()]
+            if not 0 <= device < len(items):
+                return None
+            sel = items[device]
+            break
+    env["HIP_VISIBLE_DEVICES"] = sel
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    return sel
+
+
 def device_main(conn: Any, setup: Setup, level: int, device: int, kw: Dict[str, Any],
                 host_lock: Any = None, host_cell: Any = None) -> None:
-    """Child: ``ops/diag.run(level, device, **kw)``; a run that raises is a failed ``run`` test."""
+    """Child: ``ops/diag.run(level, device, **kw)`` with this child's HIP runtime narrowed to that one GPU
+    (:func:`narrow_to`: the process is then what was measured on a one-GPU box, whatever the node's GPU count, and
+    touches no other GPU); a run that raises is a failed ``run`` test.  The meta says which PCI address it ran on."""
     t0 = time.monotonic()
     _quiet_signals()
+    ordinal = device if narrow_to(device) is None else 0
     _setup(setup)
     from ..ops import diag
     if host_lock is not None:
-        diag.use_host_lock(host_lock, host_cell)
+        diag.use_host_lock(host_lock, host_cell, label=device)
+    bdf = ""
     try:
-        res = diag.run(level, device, **kw)
+        bdf = str(diag.device_info(ordinal).get("bdf") or "")
+        res = diag.run(level, ordinal, **kw)
     except Exception as e:  # a broken library or device: a failed test, not a lost report
         res = {"run": {"pass": False, "detail": f"{type(e).__name__}: {e}"[:200]}}
-    _reply(conn, res, t0)
+    try:
+        conn.send((res, dict(_meta(t0), bdf=bdf)))
+    finally:
+        conn.close()
 
 
 def fabric_main(conn: Any, setup: Setup, suite: Callable[..., Dict[str, Any]], devices: List[int],

@@ -78,6 +78,7 @@ _HOST_HOLDER: Dict[str, Any] = {}  # who holds it: {"device": d, "since": monoto
 # per-device diagnostic *processes* (agent/isolation.py) share a multiprocessing lock instead, and say who holds it
 # in a shared (device, since) cell: CLOCK_MONOTONIC is one clock for every process of the host
 _HOST_CELL: Any = None
+_HOST_LABEL: Optional[int] = None  # the device a narrowed child (one visible GPU, ordinal 0) stands for
 # how long a device waits for the host-resource lock when run() is given no deadline (s): a healthy 8-GPU turn
 # at the host link is ~8 x 0.1 s, so this only ever expires behind a device stuck inside its host-link test
 SHARED_WAIT_S = 120.0
@@ -1030,7 +1031,7 @@ def _acquire_shared(device: int, deadline: Optional[float]) -> Optional[str]:
     if _HOST_SHARED.acquire(timeout=wait):
         _HOST_HOLDER.update(device=device, since=time.monotonic())
         if _HOST_CELL is not None:
-            _HOST_CELL[0], _HOST_CELL[1] = float(device), time.monotonic()
+            _HOST_CELL[0], _HOST_CELL[1] = float(device if _HOST_LABEL is None else _HOST_LABEL), time.monotonic()
         return None
     holder = dict(_HOST_HOLDER)
     if _HOST_CELL is not None and _HOST_CELL[0] >= 0:
@@ -1046,12 +1047,12 @@ def _release_shared() -> None:
     _HOST_SHARED.release()
 
 
-def use_host_lock(lock: Any, cell: Any) -> None:
+def use_host_lock(lock: Any, cell: Any, label: Optional[int] = None) -> None:
     """Take turns at the SHARED_TESTS with other *processes*: ``lock`` a ``multiprocessing`` lock and ``cell`` a
     shared ``array('d', 2)`` of (holding device, since) that every per-device diagnostic process of one agent cycle
-    was given (agent/isolation.py)."""
-    global _HOST_SHARED, _HOST_CELL
-    _HOST_SHARED, _HOST_CELL = lock, cell
+    was given (agent/isolation.py); ``label`` = the node's ordinal of this process's one visible GPU."""
+    global _HOST_SHARED, _HOST_CELL, _HOST_LABEL
+    _HOST_SHARED, _HOST_CELL, _HOST_LABEL = lock, cell, label
 
 
 def run(level: int = 1, device: int = 0, scale: Optional[Scale] = None,

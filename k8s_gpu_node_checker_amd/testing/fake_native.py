@@ -430,13 +430,46 @@ class FakeFabricLib:
         return self.version
 
 
+class NarrowedDiagLib:
+    """A :class:`FakeDiagLib` as a process sees it with ``HIP_VISIBLE_DEVICES=k``: one device, ordinal 0 = GPU k
+    (what a per-device diagnostic child of the agent sees, agent/isolation.narrow_to)."""
+
+    _PER_DEVICE = frozenset(("diag_device_arch", "diag_gemm_bf16", "diag_gemm_bf16_x", "diag_gemm_fp8_x",
+                             "diag_gemm_fp8", "diag_hbm_bandwidth", "diag_memtest", "diag_memtest_x", "diag_mfma_burn",
+                             "diag_mfma_burn_map", "diag_l2_bandwidth", "diag_hbm_xcd", "diag_lds_test",
+                             "diag_host_link", "diag_poll_selftest"))
+
+    def __init__(self, lib: FakeDiagLib, physical: int):
+        self.lib, self.physical = lib, physical
+
+    def diag_device_count(self) -> int:
+        return 1
+
+    def __getattr__(self, name: str):
+        fn = getattr(self.lib, name)
+        if name not in self._PER_DEVICE:
+            return fn
+
+        def on_physical(device, *a):
+            if device != 0:
+                self.lib.err = b"hipSetDevice: invalid device ordinal"
+                return -1
+            return fn(self.physical, *a)
+        return on_physical
+
+
 def install(n: int = 1, fabric: Optional[Dict] = None, **diag_kw) -> None:
     """Make this process's ``ops.diag`` and ``ops.fabric`` use the fakes: ``FakeDiagLib(n, **diag_kw)`` and
     ``FakeFabricLib(**fabric)``.  The node agent's diagnostic children run it first when the agent is given
     ``diag_setup=("k8s_gpu_node_checker_amd.testing.fake_native", "install", {...})`` (agent/isolation.py), so the
-    child code path runs unchanged on CPU with scripted GPUs."""
+    child code path runs unchanged on CPU with scripted GPUs; a child narrowed to one GPU (``HIP_VISIBLE_DEVICES``)
+    sees only that one, as under HIP."""
+    import os
     from ..ops import diag
     from ..ops import fabric as fabric_mod
-    lib = FakeDiagLib(n=n, **diag_kw)
+    lib: object = FakeDiagLib(n=n, **diag_kw)
+    vis = os.environ.get("HIP_VISIBLE_DEVICES", "").strip()
+    if vis.isdigit() and int(vis) < n:
+        lib = NarrowedDiagLib(lib, int(vis))  # type: ignore[arg-type]
     diag.lib = lambda: lib
     fabric_mod._lib = FakeFabricLib(**(fabric or {}))

@@ -178,3 +178,21 @@ def test_isolation_flag_and_thread_mode_default():
     with pytest.raises(ValueError):
         A.Agent("n", isolation="container")
     assert isolation.describe_exit(-9) == "signal SIGKILL" and isolation.describe_exit(3) == "exit code 3"
+
+
+def test_narrowing_and_a_misdirected_child():
+    """Each device child sees only its GPU (HIP_VISIBLE_DEVICES), picked from a list the agent itself was narrowed
+    to; a child that reports another PCI address than the enumeration gave its ordinal is not that GPU's result."""
+    env = {}
+    assert isolation.narrow_to(3, env) == "3" and env == {"HIP_VISIBLE_DEVICES": "3"}
+    env = {"HIP_VISIBLE_DEVICES": "4,6,7"}
+    assert isolation.narrow_to(1, env) == "6" and env["HIP_VISIBLE_DEVICES"] == "6"
+    env = {"CUDA_VISIBLE_DEVICES": "GPU-aa,GPU-bb"}
+    assert isolation.narrow_to(1, env) == "GPU-bb" and env == {"HIP_VISIBLE_DEVICES": "GPU-bb"}
+    env = {"HIP_VISIBLE_DEVICES": "2"}
+    assert isolation.narrow_to(1, env) is None and env == {"HIP_VISIBLE_DEVICES": "2"}
+    assert A.misdirected("0000:05:00.0", {"bdf": "0000:05:00.0"}) is None
+    assert A.misdirected("", {"bdf": "0000:05:00.0"}) is None and A.misdirected("0000:05:00.0", None) is None
+    assert A.misdirected("0000:05:00.0", {"bdf": "15:00.0"}) == (
+        "diagnostic process ran on 0000:15:00.0, not 0000:05:00.0: HIP device visibility mismatch")
+

@@ -555,7 +555,10 @@ def test_bench_contract_on_gpu(repo):
     # the line says where a step's time goes (medians; the parts add up to about the step)
     sm = d["step_ms"]
     assert set(sm) >= {"connect", "first_byte", "body", "scan", "client", "health", "render", "other", "step"}
-    assert abs(sum(v for k, v in sm.items() if k != "step") - sm["step"]) < 0.5 * sm["step"]
+    parts = [v for k, v in sm.items() if k not in ("step", "checker", "transport")]  # the last two are sums of parts
+    assert abs(sum(parts) - sm["step"]) < 0.5 * sm["step"]
+    assert abs(sm["checker"] + sm["transport"] - sm["step"]) < 0.5 * sm["step"] and d["checker_ms"] == sm["checker"]
+    assert [r["nodes"] for r in d["curve"]] == [1, 2, 4, 8, 16, 1000] and all(r["check_ok"] for r in d["curve"])
 
 
 def test_rccl_collective_single_rank(repo):

@@ -183,6 +183,7 @@ def main() -> int:
                               "--explain", name], capture_output=True, text=True, env=env, timeout=60)
     writes = [e for e in srv.log if e["method"] in ("PATCH", "POST")]
     rss = [s["agent_rss_mb"] for s in samples if s["agent_rss_mb"]]
+    resident = set.intersection(*(set(int(k) for k in s["children_rss_mb"]) for s in samples)) if samples else set()
     out = {
         "minutes": args.minutes, "agent_cmd": cmd[2:], "agent_alive_at_end": alive, "samples": len(samples),
         "conditions_seen": sorted({str(s["condition"]) for s in samples}),
@@ -191,9 +192,11 @@ def main() -> int:
         "heartbeat_age_s": _spread([s["heartbeat_age_s"] for s in samples]),
         "agent_rss_mb": _spread(rss), "agent_rss_first_last": [rss[0], rss[-1]] if rss else None,
         "diag_isolation": args.diag_isolation,
-        # the smallest descendant total seen: the forkserver alone, between diagnostic children
-        "children_rss_mb_min_total": min((sum(s["children_rss_mb"].values()) for s in samples), default=None),
-        "resident_total_mb": _spread([s["agent_rss_mb"] + min(s["children_rss_mb"].values() or [0])
+        # what stays resident: the agent plus the descendants present at every sample (process isolation: the
+        # forkserver and multiprocessing's resource tracker; a diagnostic child lives for seconds, between samples)
+        "resident_children": sorted(resident),
+        "resident_total_mb": _spread([s["agent_rss_mb"] + sum(v for k, v in s["children_rss_mb"].items()
+                                                              if int(k) in resident)
                                       for s in samples if s["agent_rss_mb"]]),
         "diag_child_peak_mb": _spread([s["diag_child_peak_mb"] for s in samples]),
         "diag_children_seen": len({s["diag_child_pid"] for s in samples if s["diag_child_pid"]}),
