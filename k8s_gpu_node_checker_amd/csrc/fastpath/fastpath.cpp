@@ -35,6 +35,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <new>
@@ -1408,131 +1409,247 @@ PyObject* scan_prescanned(PyObject*, PyObject* args) {
 }
 
 // ---------------------------------------------------------------- emitting --
-void emit_string(std::string& out, PyObject* s) {
-  Py_ssize_t n;
-  const char* u = PyUnicode_AsUTF8AndSize(s, &n);
-  if (!u) {
-    PyErr_Clear();
-    throw Fallback{"unencodable string"};
+// The report is mostly ASCII keys, names and label values, ~40 short strings a node.  The output goes to a raw
+// growable buffer with one capacity check per string (worst case 6 bytes a byte, all \u00XX) instead of a
+// std::string append per piece; strings are copied 16 bytes at a time until a byte that needs an escape (< 0x20,
+// '"', '\\'); ints below 2^63 are formatted without a Python object; an all-ASCII document becomes a str by one
+// memcpy (no UTF-8 decode pass).
+struct Emitter {
+  char* base = nullptr;
+  char* p = nullptr;
+  char* end = nullptr;
+  bool ascii = true;  // every byte so far < 0x80: the result is built as a 1-byte-kind str
+  Emitter() = default;
+  Emitter(const Emitter&) = delete;
+  Emitter& operator=(const Emitter&) = delete;
+  ~Emitter() { std::free(base); }
+  void reserve(size_t extra) {
+    if (static_cast<size_t>(end - p) >= extra) return;
+    const size_t used = static_cast<size_t>(p - base);
+    size_t cap = static_cast<size_t>(end - base);
+    cap = cap ? cap : 4096;
+    while (cap - used < extra) cap *= 2;
+    char* nb = static_cast<char*>(std::realloc(base, cap));
+    if (!nb) throw std::bad_alloc();
+    base = nb;
+    p = nb + used;
+    end = nb + cap;
   }
-  out.push_back('"');
+  void put(const char* s, size_t n) {  // after reserve()
+    std::memcpy(p, s, n);
+    p += n;
+  }
+  void append(const char* s, size_t n) {
+    reserve(n);
+    put(s, n);
+  }
+  size_t size() const { return static_cast<size_t>(p - base); }
+};
+
+// First byte at or after p that a JSON string must escape, e if none; *high |= any byte >= 0x80 before it.
+inline const char* find_escape(const char* p, const char* e, bool* high) {
+  const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), lim = _mm_set1_epi8(0x1F);
+  __m128i hi = _mm_setzero_si128();
+  while (e - p >= 16) {
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+    const __m128i ctl = _mm_cmpeq_epi8(_mm_min_epu8(v, lim), v);  // unsigned v <= 0x1F
+    const unsigned m = static_cast<unsigned>(
+        _mm_movemask_epi8(_mm_or_si128(ctl, _mm_or_si128(_mm_cmpeq_epi8(v, q), _mm_cmpeq_epi8(v, bs)))));
+    if (m) {
+      const int k = __builtin_ctz(m);
+      // the bytes before the escape: high bit set on any of them?
+      if ((static_cast<unsigned>(_mm_movemask_epi8(v)) & ((1u << k) - 1u)) || _mm_movemask_epi8(hi)) *high = true;
+      return p + k;
+    }
+    hi = _mm_or_si128(hi, v);
+    p += 16;
+  }
+  if (_mm_movemask_epi8(hi)) *high = true;
+  for (; p < e; ++p) {
+    const unsigned char ch = static_cast<unsigned char>(*p);
+    if (ch < 0x20 || ch == '"' || ch == '\\') return p;
+    if (ch >= 0x80) *high = true;
+  }
+  return e;
+}
+
+constexpr int kIndentMax = 64;  // levels served from the run below; deeper ones write spaces
+const char kIndentRun[] =
+    "\n                                                                                                    "
+    "                            ";
+
+// Reserves `extra` more bytes than the indent itself needs.
+inline void emit_indent(Emitter& em, int level, size_t extra = 0) {
+  const size_t n = 1 + 2 * static_cast<size_t>(level);
+  em.reserve(n + extra);
+  if (level <= kIndentMax) {
+    em.put(kIndentRun, n);
+  } else {
+    *em.p++ = '\n';
+    std::memset(em.p, ' ', n - 1);
+    em.p += n - 1;
+  }
+}
+
+void emit_string(Emitter& em, PyObject* s) {
+  Py_ssize_t n;
+  const char* u;
+  if (PyUnicode_IS_COMPACT_ASCII(s)) {  // the common case: the str's own bytes are its UTF-8
+    u = static_cast<const char*>(PyUnicode_DATA(s));
+    n = PyUnicode_GET_LENGTH(s);
+  } else {
+    u = PyUnicode_AsUTF8AndSize(s, &n);
+    if (!u) {
+      PyErr_Clear();
+      throw Fallback{"unencodable string"};
+    }
+  }
+  em.reserve(6 * static_cast<size_t>(n) + 4);  // every byte escaped as \u00XX, the quotes, ": "
+  *em.p++ = '"';
   const char* p = u;
   const char* e = u + n;
-  const char* run = p;
   static const char hex[] = "0123456789abcdef";
-  for (; p < e; ++p) {
-    unsigned char ch = static_cast<unsigned char>(*p);
-    if (ch >= 0x20 && ch != '"' && ch != '\\') continue;
-    out.append(run, p - run);
+  for (;;) {
+    bool high = false;
+    const char* q = find_escape(p, e, &high);
+    if (high) em.ascii = false;
+    em.put(p, static_cast<size_t>(q - p));
+    if (q == e) break;
+    const unsigned char ch = static_cast<unsigned char>(*q);
+    char* o = em.p;
     switch (ch) {
-      case '"': out.append("\\\""); break;
-      case '\\': out.append("\\\\"); break;
-      case '\n': out.append("\\n"); break;
-      case '\r': out.append("\\r"); break;
-      case '\t': out.append("\\t"); break;
-      case '\b': out.append("\\b"); break;
-      case '\f': out.append("\\f"); break;
+      case '"': o[0] = '\\'; o[1] = '"'; em.p += 2; break;
+      case '\\': o[0] = '\\'; o[1] = '\\'; em.p += 2; break;
+      case '\n': o[0] = '\\'; o[1] = 'n'; em.p += 2; break;
+      case '\r': o[0] = '\\'; o[1] = 'r'; em.p += 2; break;
+      case '\t': o[0] = '\\'; o[1] = 't'; em.p += 2; break;
+      case '\b': o[0] = '\\'; o[1] = 'b'; em.p += 2; break;
+      case '\f': o[0] = '\\'; o[1] = 'f'; em.p += 2; break;
       default: {
-        char buf[7] = {'\\', 'u', '0', '0', hex[ch >> 4], hex[ch & 15], 0};
-        out.append(buf, 6);
+        const char buf[6] = {'\\', 'u', '0', '0', hex[ch >> 4], hex[ch & 15]};
+        em.put(buf, 6);
       }
     }
-    run = p + 1;
+    p = q + 1;
   }
-  out.append(run, e - run);
-  out.push_back('"');
+  *em.p++ = '"';
 }
 
-void emit_indent(std::string& out, int level) {
-  out.push_back('\n');
-  out.append(static_cast<size_t>(level) * 2, ' ');
-}
-
-void emit_float(std::string& out, PyObject* o) {
+void emit_float(Emitter& em, PyObject* o) {
   double d = PyFloat_AS_DOUBLE(o);
   if (std::isnan(d)) {
-    out.append("NaN");
+    em.append("NaN", 3);
   } else if (std::isinf(d)) {
-    out.append(d > 0 ? "Infinity" : "-Infinity");
+    if (d > 0)
+      em.append("Infinity", 8);
+    else
+      em.append("-Infinity", 9);
   } else {
     PyObject* r = PyObject_Repr(o);
     if (!r) throw Fallback{"repr"};
     Py_ssize_t n;
     const char* u = PyUnicode_AsUTF8AndSize(r, &n);
-    out.append(u, static_cast<size_t>(n));
+    em.append(u, static_cast<size_t>(n));
     Py_DECREF(r);
   }
 }
 
-void emit_value(std::string& out, PyObject* o, int level) {
+void emit_int(Emitter& em, PyObject* o) {
+  int overflow = 0;
+  const long long v = PyLong_AsLongLongAndOverflow(o, &overflow);
+  if (!overflow && !(v == -1 && PyErr_Occurred())) {
+    char buf[24];
+    char* q = buf + sizeof buf;
+    unsigned long long m = v < 0 ? 0ULL - static_cast<unsigned long long>(v) : static_cast<unsigned long long>(v);
+    do {
+      *--q = static_cast<char>('0' + m % 10);
+      m /= 10;
+    } while (m);
+    if (v < 0) *--q = '-';
+    em.append(q, static_cast<size_t>(buf + sizeof buf - q));
+    return;
+  }
+  PyErr_Clear();
+  PyObject* r = PyObject_Str(o);  // beyond 64 bits: int.__str__ (CPython's own digit limit applies)
+  if (!r) throw Fallback{"str"};
+  Py_ssize_t n;
+  const char* u = PyUnicode_AsUTF8AndSize(r, &n);
+  em.append(u, static_cast<size_t>(n));
+  Py_DECREF(r);
+}
+
+void emit_value(Emitter& em, PyObject* o, int level) {
   if (level > 200) throw Fallback{"too deep"};
   if (o == Py_None) {
-    out.append("null");
+    em.append("null", 4);
   } else if (o == Py_True) {
-    out.append("true");
+    em.append("true", 4);
   } else if (o == Py_False) {
-    out.append("false");
+    em.append("false", 5);
   } else if (PyUnicode_CheckExact(o)) {
-    emit_string(out, o);
+    emit_string(em, o);
   } else if (PyLong_CheckExact(o)) {
-    PyObject* r = PyObject_Str(o);
-    if (!r) throw Fallback{"str"};
-    Py_ssize_t n;
-    const char* u = PyUnicode_AsUTF8AndSize(r, &n);
-    out.append(u, static_cast<size_t>(n));
-    Py_DECREF(r);
+    emit_int(em, o);
   } else if (PyFloat_CheckExact(o)) {
-    emit_float(out, o);
+    emit_float(em, o);
   } else if (PyDict_CheckExact(o)) {
     if (PyDict_GET_SIZE(o) == 0) {
-      out.append("{}");
+      em.append("{}", 2);
       return;
     }
-    out.push_back('{');
+    em.append("{", 1);
     Py_ssize_t pos = 0;
     PyObject *k, *v;
     bool first = true;
     while (PyDict_Next(o, &pos, &k, &v)) {
       if (!PyUnicode_CheckExact(k)) throw Fallback{"non-str key"};
-      if (!first) out.push_back(',');
+      if (!first) em.append(",", 1);
       first = false;
-      emit_indent(out, level + 1);
-      emit_string(out, k);
-      out.append(": ");
-      emit_value(out, v, level + 1);
+      emit_indent(em, level + 1);
+      emit_string(em, k);  // reserved room for the ": " after it
+      em.put(": ", 2);
+      emit_value(em, v, level + 1);
     }
-    emit_indent(out, level);
-    out.push_back('}');
+    emit_indent(em, level, 1);
+    *em.p++ = '}';
   } else if (PyList_CheckExact(o) || PyTuple_CheckExact(o)) {
     PyObject* seq = o;
     Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
     if (n == 0) {
-      out.append("[]");
+      em.append("[]", 2);
       return;
     }
-    out.push_back('[');
+    em.append("[", 1);
     for (Py_ssize_t i = 0; i < n; ++i) {
-      if (i) out.push_back(',');
-      emit_indent(out, level + 1);
-      emit_value(out, PySequence_Fast_GET_ITEM(seq, i), level + 1);
+      if (i) em.append(",", 1);
+      emit_indent(em, level + 1);
+      emit_value(em, PySequence_Fast_GET_ITEM(seq, i), level + 1);
     }
-    emit_indent(out, level);
-    out.push_back(']');
+    emit_indent(em, level, 1);
+    *em.p++ = ']';
   } else {
     throw Fallback{"unsupported type"};
   }
 }
 
 PyObject* dumps_indent2(PyObject*, PyObject* obj) {
-  std::string out;
-  out.reserve(4096);
+  Emitter em;
   try {
-    emit_value(out, obj, 0);
+    em.reserve(1 << 16);
+    emit_value(em, obj, 0);
   } catch (const Fallback& f) {
     if (!PyErr_Occurred()) PyErr_SetString(g_fallback, f.why);
     return nullptr;
+  } catch (const std::bad_alloc&) {
+    return PyErr_NoMemory();
   }
-  return PyUnicode_DecodeUTF8(out.data(), static_cast<Py_ssize_t>(out.size()), "surrogatepass");
+  const Py_ssize_t n = static_cast<Py_ssize_t>(em.size());
+  if (em.ascii) {
+    PyObject* s = PyUnicode_New(n, 127);
+    if (s) std::memcpy(PyUnicode_1BYTE_DATA(s), em.base, static_cast<size_t>(n));
+    return s;
+  }
+  return PyUnicode_DecodeUTF8(em.base, n, "surrogatepass");
 }
 
 // ------------------------------------------------------------------ loads --

@@ -167,6 +167,26 @@ def test_dumps_control_chars_and_unicode():
 
 
 @settings(max_examples=300, suppress_health_check=[HealthCheck.too_slow])
+@given(st.text(alphabet=st.sampled_from('ab"\\\n\x01é😀\x7fz'), max_size=80), st.integers(0, 40))
+def test_dumps_long_strings_escapes_at_every_offset(tail, pad):
+    """The emitter copies 16 bytes at a time: escapes and non-ASCII bytes before, inside and after a 16-byte run."""
+    obj = {"k" * pad: ["x" * pad + tail, tail + "y" * pad, -(2 ** 63), 2 ** 63 - 1, 2 ** 63, -7, 0]}
+    assert ext.dumps_indent2(obj) == json.dumps(obj, ensure_ascii=False, indent=2)
+
+
+def test_dumps_deep_indent_and_large_output():
+    deep = []
+    cur = deep
+    for _ in range(120):  # beyond the preallocated indent run (64 levels)
+        nxt = [1]
+        cur.append(nxt)
+        cur = nxt
+    assert ext.dumps_indent2(deep) == json.dumps(deep, ensure_ascii=False, indent=2)
+    big = {"nodes": [{"name": f"n{i}", "labels": {f"l{j}": "v" * 40 for j in range(20)}} for i in range(2000)]}
+    assert ext.dumps_indent2(big) == json.dumps(big, ensure_ascii=False, indent=2)
+
+
+@settings(max_examples=300, suppress_health_check=[HealthCheck.too_slow])
 @given(json_tree, st.integers(0, 70), st.booleans())
 def test_skipped_subtrees_with_escapes(junk, pad, ascii_only):
     """Arbitrary JSON (quotes, backslash runs, brackets inside strings) in skipped fields, at every
