@@ -24,12 +24,18 @@ RBAC: ``nodes: get, patch``, ``nodes/status: patch`` and ``events: create`` (``d
 the agent's own node and to the fields it owns by ``deploy/agent-policy.yaml`` (a ValidatingAdmissionPolicy on the
 node-name claim of its pod-bound token) and by :class:`_OwnNodeClient` here.
 
-Multi-device nodes (8 GPUs, or 64 CPX partitions): per-device diagnostic threads, at most ``--diag-parallel`` at
-once, tests of shared host resources serialized (``ops/diag.SHARED_TESTS``); a diagnostic that outlives
-``--diag-timeout`` is a failed GPU and one that outlives twice that fails ``/healthz`` (fresh process); the RCCL
-suite aborts its own communicators at its deadline (``csrc/fabric/fabric.hip``) and the xGMI pair copies are
-polled against theirs (``diag_p2p_copy_t``); a node-level test given up that way is not run again in the same
-process (:func:`fabric_abandoned`).
+Where the HIP work runs (``--diag-isolation``, ``agent/isolation.py``): by default in disposable child processes of
+a forkserver started before the agent touches amd-smi or HIP -- one per GPU, narrowed to that GPU, then one for the
+node-level tests -- so the agent itself never initialises HIP (65 MiB resident between cycles on MI355X), a
+diagnostic that outlives ``--diag-timeout`` is SIGKILLed and its GPU published as failed while the agent keeps
+probing, and a GPU fault that aborts the HIP runtime costs one child.  ``thread`` keeps the work in the agent.
+
+Multi-device nodes (8 GPUs, or 64 CPX partitions): per-device diagnostic jobs, at most ``--diag-parallel`` at
+once, tests of shared host resources serialized across them (``ops/diag.SHARED_TESTS``); the RCCL suite aborts its
+own communicators at its deadline (``csrc/fabric/fabric.hip``) and the xGMI copies are polled against theirs
+(``diag_p2p_copy_t``, ``diag_p2p_fan_t``).  With thread isolation a hung diagnostic cannot be ended: one that
+outlives twice its watchdog fails ``/healthz`` (fresh process), and a node-level test given up at its deadline is not
+run again in the same process (:func:`fabric_abandoned`).
 """
 
 from __future__ import annotations
@@ -135,36 +141,36 @@ HUNG_RESTART_FACTOR = 2.0
 from ..ops.diag import P2P_SHARE  # noqa: E402  (share of --diag-timeout the xGMI pair matrix may use)
 
 
-# Host memory of the agent process (MiB), measured on one MI355X (profiles/agent_rss_*_mi355x.json,
-# tools/agent_rss.py, tools/rccl_rss.py): Python + amd-smi probe + HIP runtime up, before any kernel
-MEM_BASE_MIB = 60
-# the first launch of the level-1 kernels (HIP queues, kernel-argument pools, comgr's code-object loading;
-# RSS 54 -> 695 MiB, flat afterwards at any problem size).  How much of it recurs per additional device could
-# not be measured on one GPU: the budget counts all of it per device, an upper bound
-MEM_PER_DEVICE_MIB = 640
-# level 2 on top (memtest, 8192^3 GEMMs; 695 -> 1,059 MiB) plus the host-link test's pinned 256 MiB buffer --
-# one at a time, ops/diag.SHARED_TESTS -- (peak 1,326 MiB)
-MEM_LEVEL2_MIB = 640
-# the in-process RCCL suite (level 2, >= 2 GPUs) with a warm comgr cache: peak 2,712 MiB on one GPU
-MEM_RCCL_WARM_MIB = 1400
-# ... and with a cold one: comgr decompresses RCCL's compressed code objects on the first load, peak 11,786 MiB
-# (profiles/rccl_rss_comgr_cache_mi355x.json); the level-2 overlay keeps the cache on the node
+# Host memory (MiB), measured on one MI355X with process isolation, the DaemonSet's mode (tools/agent_soak.py):
+# resident between cycles, the agent (31) + the forkserver (17) + multiprocessing's resource tracker (16) --
+# profiles/agent_soak_isolated_l{1,2}_r06_mi355x.json, flat over 48 / 36 cycles.  This is the pod's request.
+MEM_RESIDENT_MIB = 65
+# one diagnostic child's peak, its own getrusage (HIP runtime, comgr's code objects, the level's buffers; the child
+# sees one GPU, isolation.narrow_to, so it is the same process on a one-GPU box and on an 8-GPU node): level 1
+# 632 MiB over 48 children, level 2 1,273 MiB over 36 (the host link's pinned buffer and the 8192^3 GEMMs included)
+MEM_CHILD_PEAK_MIB = {1: 632, 2: 1273}
+# the node-level child (xGMI matrix, in-process RCCL suite; level 2, >= 2 GPUs) with a warm comgr cache: 2,712 MiB
+# for the suite on one GPU (profiles/rccl_rss_comgr_cache_mi355x.json).  Each further GPU is counted at a level-1
+# child's peak -- an upper bound, unmeasured: no multi-GPU box was available to this project
+MEM_FABRIC_ONE_GPU_MIB = 2712
+# ... and with a cold comgr cache: comgr decompresses RCCL's compressed code objects on the first load, peak 11,786
+# MiB (profiles/rccl_rss_comgr_cache_mi355x.json); the level-2 overlay keeps the cache on the node
 # (AMD_COMGR_CACHE_DIR on a hostPath) and fills it from an init container with its own limit
 MEM_RCCL_COLD_PEAK_MIB = 11786
 
 
-def memory_budget_mib(devices: int, level: int, rccl: bool = False) -> int:
-    """Upper bound of the agent's host memory for ``devices`` HIP devices at diagnostics ``level`` (the
-    DaemonSet's memory limit; tests/test_deploy.py holds the manifests to it).  Measured on one MI355X; beyond one
-    device the per-device part is an extrapolation (MEM_PER_DEVICE_MIB), unmeasured: no multi-GPU box was
-    available to this project."""
-    mib = MEM_BASE_MIB
+def memory_budget_mib(devices: int, level: int, rccl: bool = False, parallel: int = DIAG_PARALLEL) -> int:
+    """Upper bound of the agent pod's host memory for ``devices`` GPUs at diagnostics ``level`` (the DaemonSet's
+    limit; tests/test_deploy.py holds the manifests to it): what stays resident, plus the larger of the device
+    children running together (at most ``parallel``, each a measured one-GPU process) and the node-level child,
+    which runs alone after them.  :data:`MEM_RESIDENT_MIB` alone is the request."""
+    mib = MEM_RESIDENT_MIB
     if level >= 1:
-        mib += max(1, devices) * MEM_PER_DEVICE_MIB
-    if level >= 2:
-        mib += MEM_LEVEL2_MIB
-        if rccl and devices >= 2:
-            mib += MEM_RCCL_WARM_MIB
+        children = min(max(1, devices), max(1, parallel)) * MEM_CHILD_PEAK_MIB[min(level, 2)]
+        fabric = 0
+        if level >= 2 and rccl and devices >= 2:
+            fabric = MEM_FABRIC_ONE_GPU_MIB + (devices - 1) * MEM_CHILD_PEAK_MIB[1]
+        mib += max(children, fabric)
     return mib
 
 
@@ -731,9 +737,12 @@ class Agent:
         if self.hip_lost is not None:
             for d in devices:
                 self._diag_skipped[d] = f"HIP runtime lost its devices ({self.hip_lost[:120]}): agent restart pending"
+        # a GPU whose last diagnostic hung (its child killed, or its thread still stuck) would take the node-level
+        # suite down with it: that waits for a cycle in which every GPU came back
+        hung_gpu = any("watchdog" in (self._diag_cache.get(d) or {}) for d in devices)
         if (self.diag_level >= 2 and self.devices is None and len(devices) >= 2 and not self._diag_skipped
-                and not self._diag_threads and self._fabric_thread is None and self.fabric_abandoned is None
-                and now - self._fabric_at >= self.diag_interval):
+                and not self._diag_threads and not hung_gpu and self._fabric_thread is None
+                and self.fabric_abandoned is None and now - self._fabric_at >= self.diag_interval):
             # node-level: every ordered GPU pair over xGMI (after the per-GPU tests, so no contention) and the
             # RCCL collectives; it touches every GPU, so it waits until none is busy.  Under the same watchdog as
             # the per-GPU tests: a collective that never completes (a link that stopped passing traffic) is a

@@ -694,8 +694,15 @@ def test_daemonset_memory_limit_covers_the_budget_of_an_eight_gpu_node():
     c = _agent_container(ds)
     level = int(c["command"][c["command"].index("--diag-level") + 1])
     assert level == 1
-    assert _mib(c["resources"]["limits"]["memory"]) >= agent.memory_budget_mib(8, level)
-    assert agent.memory_budget_mib(1, 1) >= 695  # the measured one-GPU level-1 RSS (profiles/agent_rss_mi355x.json)
+    args = agent.build_parser().parse_args(c["command"][1:])
+    assert args.diag_isolation == "process"  # the budget below is the process-isolation one
+    assert _mib(c["resources"]["limits"]["memory"]) >= agent.memory_budget_mib(8, level, parallel=args.diag_parallel)
+    # the request is what stays resident (measured), not a first-launch cost
+    req = _mib(c["resources"]["requests"]["memory"])
+    assert agent.MEM_RESIDENT_MIB <= req <= 2 * agent.MEM_RESIDENT_MIB
+    # the measured one-GPU figures (profiles/agent_soak_isolated_l{1,2}_r06_mi355x.json)
+    assert agent.memory_budget_mib(1, 1) == 65 + 632 and agent.memory_budget_mib(1, 2) == 65 + 1273
+    assert agent.memory_budget_mib(8, 1, parallel=2) == 65 + 2 * 632  # children at once, not devices, count
     assert agent.memory_budget_mib(1, 2, rccl=True) >= agent.memory_budget_mib(1, 2)
 
 
@@ -707,7 +714,10 @@ def test_level2_overlay_keeps_the_comgr_cache_and_sizes_both_containers():
     c = _agent_container(patch)
     agent.build_parser().parse_args(c["command"][1:])
     assert c["command"][c["command"].index("--diag-level") + 1] == "2"
-    assert _mib(c["resources"]["limits"]["memory"]) >= agent.memory_budget_mib(8, 2, rccl=True)
+    args = agent.build_parser().parse_args(c["command"][1:])
+    assert _mib(c["resources"]["limits"]["memory"]) >= agent.memory_budget_mib(8, 2, rccl=True,
+                                                                               parallel=args.diag_parallel)
+    assert agent.MEM_RESIDENT_MIB <= _mib(c["resources"]["requests"]["memory"]) <= 2 * agent.MEM_RESIDENT_MIB
     init = patch["spec"]["template"]["spec"]["initContainers"][0]
     assert init["command"][0] == "mi355x-fabric"
     from k8s_gpu_node_checker_amd.ops import fabric

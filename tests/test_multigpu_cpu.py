@@ -443,3 +443,42 @@ def test_eight_node_fleet_with_a_withdrawn_device_plugin(mock_cluster, tmp_path)
     assert res.exit_code == 0 and len(res.gpu_nodes) == 8 and len(res.ready_gpu_nodes) == 7
     v = res.verdicts[5]
     assert v.state == H.UNHEALTHY and v.reasons[0] == "device plugin allocates 0 of 8 amd.com/gpu"
+
+
+def test_eight_gpu_level2_cycle_with_process_isolation(monkeypatch):
+    """the DaemonSet's configuration on a whole 8-GPU node, on CPU -- every GPU's suite in its own
+    child narrowed to that GPU, at most --diag-parallel at once, then the xGMI matrix (pairs and fans) and the RCCL
+    suite in one node-level child; one GPU hangs and is SIGKILLed at the watchdog, another's link is slow only under
+    the fan.  The agent process never loads the diagnostics library."""
+    from k8s_gpu_node_checker_amd.agent import isolation
+    monkeypatch.setattr(amdsmi_probe, "probe", lambda node, src, fx: fixtures.mi355x_probe_report(node, gpus=8))
+
+    def no_hip_here():
+        raise AssertionError("the agent process called the HIP diagnostics library")
+    monkeypatch.setattr(diag, "lib", no_hip_here)
+    fake = {"n": 8, "hang_devices": (5,), "fan_slow": {(3, 6): 9.0}}
+    ag = A.Agent("n8", source="fake", diag_level=2, expect_gpus=8, diag_timeout=4.0, diag_parallel=4, diag_interval=0.0,
+                 diag_when="always", isolation="process",
+                 diag_setup=("k8s_gpu_node_checker_amd.testing.fake_native", "install", fake))
+    t0 = time.monotonic()
+    rep = ag.probe_once()
+    assert time.monotonic() - t0 < 2 * 4.0 + isolation.KILL_GRACE_S + 5
+    started = [c["what"] for c in ag.workers.started]
+    assert started[0] == "hip-enumerate" and sorted(started[1:9]) == sorted(f"diag-gpu{d}" for d in range(8))
+    for d, g in enumerate(rep["gpus"]):
+        if d == 5:
+            assert g["diag"]["watchdog"]["pass"] is False and "killed" in g["diag"]["watchdog"]["detail"]
+            continue
+        assert all(r["pass"] for r in g["diag"].values()), (d, g["diag"])
+        assert g["diag_proc"]["bdf"] == g["bdf"]  # each child measured its own GPU (narrowed, then checked)
+    # the node-level suite waits for an all-clean cycle of per-GPU jobs: not this one (gpu5 hung)
+    assert "diag-fabric" not in started
+    v = ag.evaluate(rep)
+    assert v.state == H.UNHEALTHY and (v.gpus_ok, v.gpus_seen) == (7, 8)
+    # a later cycle without the hang runs the fabric child, whose fan pass names the slow link
+    ag.workers.setup = ("k8s_gpu_node_checker_amd.testing.fake_native", "install", dict(fake, hang_devices=()))
+    rep = ag.probe_once()
+    assert [c["what"] for c in ag.workers.started].count("diag-fabric") == 1
+    p2p = rep["fabric"]["p2p"]
+    assert p2p["pass"] is False and "fan 3->6 9.0 GB/s with every link of 3 busy" in p2p["detail"]
+    assert p2p["fan"]["sources"] == 8 and rep["fabric"]["rccl"]["pass"]
