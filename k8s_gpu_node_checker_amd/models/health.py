@@ -700,6 +700,26 @@ def verdict_from_condition(cond: Tuple[Optional[str], Optional[str], Optional[st
                                  else "AMDGPUHealthy condition has no heartbeat"], age_s=age)
     if age < -max_age_s:  # as for reports: a heartbeat from the future would count as fresh indefinitely
         return Verdict(UNKNOWN, [f"AMDGPUHealthy heartbeat is {-age:.0f} s in the future (clock skew?)"], age_s=age)
+    # a fresh condition's verdict depends only on (status, reason, message, expected): across a fleet a handful of
+    # distinct ones ("8/8 MI355X GPUs healthy" on every healthy node), so each is worked out once and copied (new
+    # lists per node: callers add reasons and warnings to one node's verdict)
+    key = (status, reason, message, expected_gpus)
+    t = _FRESH.get(key)
+    if t is None:
+        v = _fresh_condition_verdict(status, reason, message, expected_gpus)
+        if len(_FRESH) >= 4096:
+            _FRESH.clear()
+        t = _FRESH[key] = (v.state, tuple(v.reasons), tuple(v.warnings), v.gpus_ok, v.gpus_seen)
+    return Verdict(t[0], list(t[1]), list(t[2]), t[3], t[4], age)
+
+
+_FRESH: Dict[tuple, tuple] = {}
+
+
+def _fresh_condition_verdict(status: Optional[str], reason: Optional[str], message: Optional[str],
+                             expected_gpus: int) -> Verdict:
+    """:func:`verdict_from_condition` of a condition whose heartbeat is fresh (its age filled in by the caller)."""
+    age = None
     counts, detail = _message_parts(message)
     ok, seen = counts if counts else (0, 0)
     msg = [detail] if detail else []
