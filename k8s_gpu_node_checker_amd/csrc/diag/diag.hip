@@ -59,6 +59,8 @@ thread_local int g_gemm_buffer_loads = 0;  // v3 operand staging: 0 = global_loa
 // scaled form at 4096^3 and 8192^3 with bit-identical C, profiles/gemm_fp8_mfma_ab_mi355x.jsonl), 0 = the
 // v_mfma_scale_..._f8f6f4 MX path with unit E8M0 scales (kept for A/B)
 thread_local int g_gemm_fp8_unscaled = 1;
+// v4 bf16: a short last wave of 256^2 tiles runs as 128^2 quadrants (gemm_v4_tail_kernel; 0 = off, for A/B)
+thread_local int g_gemm_tail = 1;
 thread_local int g_gemm_epilogue = 1;  // 0 = direct 4-byte stores, 1 = LDS-staged 16-byte row pieces (v3
                                        // kernels; measured +2..12 %, profiles/gemm_fp8_mi355x.jsonl)
 
@@ -1244,6 +1246,150 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// v4's tail wave.  A grid of 256x256 tiles that is not a whole number of 256-CU waves leaves most of the chip idle in
+// its last wave: 6144^3 is 576 tiles, 2.25 waves, so the third wave runs 64 tiles on 64 CUs while 192 wait (6144^3
+// bf16 at 0.917 of hipBLASLt against 0.97 at 4096^3 and 8192^3, profiles/gemm_v4_sizes_ab_mi355x.jsonl).  The v4
+// launch then covers only the whole waves -- V4_TAIL_MAIN(nwg) workgroups; v4's XCD remap leaves each XCD's last
+// chunk of tile indices uncomputed -- and this kernel computes those tiles as four 128x128 quadrants each, 4x the
+// workgroups for the same work, with v1's K loop (the same v_mfma_f32_16x16x32_bf16 per 32-wide K chunk, in the same
+// order as v3 / v4: every C element and every fp64 column sum bit-identical to theirs).  Each 128x128 quadrant's
+// column sums continue, in wave wr = 1, the partial sums wave wr = 0 left in LDS, so they follow v4's own order over
+// the 128-row band (m, then j, then the xor-16 / xor-32 lane exchange).
+__host__ __device__ constexpr int v4_tail_main(int nwg) { return nwg / 256 * 256; }
+// only a short tail is worth it: a quarter wave of 256^2 tiles is one 2-per-CU wave of 128^2 quadrants
+__host__ __device__ constexpr bool v4_tail_applies(int nwg) { return nwg > 256 && nwg % 256 != 0 && nwg % 256 <= 64; }
+
+template <int OUT, int GM = 4>
+__global__ void __launch_bounds__(THREADS, 2)
+gemm_v4_tail_kernel(const u32x4* __restrict__ A, const u32x4* __restrict__ Bt, void* __restrict__ Cv,
+                    double* __restrict__ csum, int M, int N, int K) {
+  __shared__ u32x4 lds[2][2][TILE_CHUNKS];  // [buffer][A|B][chunk] = 64 KiB
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  // which 256^2 tile (v4's numbering) and which quadrant of it
+  const int tiles_m = M / V2_BM, tiles_n = N / V2_BN, nwg = tiles_m * tiles_n;
+  const int q = nwg / 8, r = nwg % 8, qmain = v4_tail_main(nwg) / 8;
+  int t = static_cast<int>(blockIdx.x) >> 2;
+  int idx = -1;
+  for (int x = 0; x < 8; ++x) {  // XCD x's tiles are [base, base + cnt); v4 computed the first qmain of them
+    const int cnt = q + (x < r ? 1 : 0), base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    if (t < cnt - qmain) {
+      idx = base + qmain + t;
+      break;
+    }
+    t -= cnt - qmain;
+  }
+  if (idx < 0) return;  // the launch covers exactly the tail (host side); no workgroup reaches this
+  const int group = idx / (GM * tiles_n), first_m = group * GM, gsize = min(tiles_m - first_m, GM);
+  const int tm = first_m + (idx % (GM * tiles_n)) % gsize, tn = (idx % (GM * tiles_n)) / gsize;
+  const int quad = static_cast<int>(blockIdx.x) & 3;
+  const int rm = 2 * tm + (quad >> 1), rn = 2 * tn + (quad & 1);  // the 128x128 tile
+
+  const int kchunks = K / 8;
+  const u32x4* Ablk = A + static_cast<size_t>(rm) * BM * kchunks;
+  const u32x4* Bblk = Bt + static_cast<size_t>(rn) * BN * kchunks;
+  u32x4 ra[LOADS_PER_THREAD], rb[LOADS_PER_THREAD];
+  int g_off[LOADS_PER_THREAD], l_off[LOADS_PER_THREAD];
+#pragma unroll
+  for (int i = 0; i < LOADS_PER_THREAD; ++i) {
+    const int ch = tid + i * THREADS;
+    const int rr = ch / CHUNKS_PER_ROW, c = ch % CHUNKS_PER_ROW;
+    g_off[i] = rr * kchunks + c;
+    l_off[i] = swz(rr, c);
+  }
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int KT = K / BK;
+  const int frow = lane & 15, fq = lane >> 4;
+  gemm_gload(ra, rb, Ablk, Bblk, g_off, 0);
+  gemm_lstore(lds[0], ra, rb, l_off);
+  __syncthreads();
+  for (int kt = 0; kt < KT; kt += 2) {
+    const bool more1 = kt + 1 < KT;
+    if (more1) gemm_gload(ra, rb, Ablk, Bblk, g_off, kt + 1);
+    gemm_compute(acc, lds[0], wr, wc, frow, fq);
+    if (more1) gemm_lstore(lds[1], ra, rb, l_off);
+    __syncthreads();
+    if (!more1) break;
+    const bool more2 = kt + 2 < KT;
+    if (more2) gemm_gload(ra, rb, Ablk, Bblk, g_off, kt + 2);
+    gemm_compute(acc, lds[1], wr, wc, frow, fq);
+    if (more2) gemm_lstore(lds[0], ra, rb, l_off);
+    __syncthreads();
+  }
+  // every wave is past its last LDS read (the loop ends on a barrier): the operand buffers are free for the epilogue
+  const int row0 = rm * BM + wr * 64, col0 = rn * BN + wc * 64;
+  unsigned char* scratch = reinterpret_cast<unsigned char*>(&lds[0][0][0]);
+  if constexpr (OUT == OUT_BF16_CK) {
+    // column sums of the 128-row band rm: wave wr = 0 sums its rows (m, then j) and hands the partials over, wave
+    // wr = 1 continues them over its own rows -- v4's wave order over the band's 128 rows -- then the lane exchange
+    double* part = reinterpret_cast<double*>(scratch) + wc * (4 * 64);  // [wc][n][lane]
+    double cs[4] = {0.0, 0.0, 0.0, 0.0};
+    if (wr == 0) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) cs[n] += static_cast<double>(acc[m][n][j]);
+        part[n * 64 + lane] = cs[n];
+      }
+    }
+    __syncthreads();
+    if (wr == 1) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        cs[n] = part[n * 64 + lane];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) cs[n] += static_cast<double>(acc[m][n][j]);
+        cs[n] += __shfl_xor(cs[n], 16);
+        cs[n] += __shfl_xor(cs[n], 32);
+      }
+      if (fq == 0) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) csum[static_cast<size_t>(rm) * N + rn * BN + wc * 64 + n * 16 + frow] = cs[n];
+      }
+    }
+    __syncthreads();  // the partials are read: the scratch becomes the waves' store patches
+    // bf16 C through each wave's own patch (16 rows x 64 fp32 columns): 16-byte row pieces per lane
+    constexpr int LD = 64 + 4;
+    float* patch = reinterpret_cast<float*>(scratch) + wid * (16 * LD);
+    __bf16* __restrict__ Cb = static_cast<__bf16*>(Cv);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) patch[(fq * 4 + j) * LD + n * 16 + frow] = acc[m][n][j];
+      // a wave's writes to its own patch are visible to its own later reads (one wave, in order: s_waitcnt)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rr = h * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+        const floatx4 lo = *reinterpret_cast<const floatx4*>(patch + rr * LD + c8);
+        const floatx4 hi = *reinterpret_cast<const floatx4*>(patch + rr * LD + c8 + 4);
+        const floatx8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        *reinterpret_cast<bf16x8*>(Cb + static_cast<size_t>(row0 + m * 16 + rr) * N + col0 + c8) =
+            __builtin_convertvector(v, bf16x8);
+      }
+    }
+  } else {
+    float* __restrict__ C = static_cast<float*>(Cv);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          C[static_cast<size_t>(row0 + m * 16 + fq * 4 + j) * N + col0 + n * 16 + frow] = acc[m][n][j];
+  }
+}
+
 // fp32 reference for sampled outputs: one thread per (row, col) sample.
 __global__ void gemm_ref_kernel(const __bf16* A, const __bf16* Bt, const int* rows, const int* cols, float* out,
                                 int nsamp, int K) {
@@ -1843,8 +1989,14 @@ int launch_v4_inst(const void* A, const void* Bt, void* C, double* csum, int M, 
   static LdsAttrOnce attr;
   if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(kern), 2 * V2_STAGE_BYTES, "gemm v4") != 0) return -1;
   const int nwg = (M / V2_BM) * (N / V2_BN);
-  hipLaunchKernelGGL(kern, dim3(nwg), dim3(V4_THREADS), 2 * V2_STAGE_BYTES, stream, static_cast<const __bf16*>(A),
+  // bf16 with a short last wave: v4 on the whole waves, the rest as 128^2 quadrants (gemm_v4_tail_kernel)
+  const bool tail = DT == DT_BF16 && g_gemm_tail && v4_tail_applies(nwg);
+  const int main_wg = tail ? v4_tail_main(nwg) : nwg;
+  hipLaunchKernelGGL(kern, dim3(main_wg), dim3(V4_THREADS), 2 * V2_STAGE_BYTES, stream, static_cast<const __bf16*>(A),
                      static_cast<const __bf16*>(Bt), C, csum, M, N, K);
+  if (tail)
+    hipLaunchKernelGGL((gemm_v4_tail_kernel<OUT, 4>), dim3(4 * (nwg - main_wg)), dim3(THREADS), 0, stream,
+                       static_cast<const u32x4*>(A), static_cast<const u32x4*>(Bt), C, csum, M, N, K);
   return 0;
 }
 // v4 with the LDS-patch epilogue (variant 4) or the transposed, register-direct one (variant 5); K in bf16 columns
@@ -2072,6 +2224,8 @@ const char* diag_last_error(void) { return g_err.c_str(); }
 // fp8_unscaled = 0, and 1-3 run v3); fp4 always runs v3.
 void diag_set_gemm_variant(int v) { g_gemm_variant = v; }
 void diag_set_gemm_epilogue(int e) { g_gemm_epilogue = e; }
+void diag_set_gemm_tail(int t) { g_gemm_tail = t ? 1 : 0; }
+int diag_get_gemm_tail(void) { return g_gemm_tail; }
 void diag_set_gemm_buffer_loads(int b) { g_gemm_buffer_loads = b; }
 void diag_set_gemm_schedule(int s) { g_gemm_schedule = s; }
 int diag_get_gemm_schedule(void) { return g_gemm_schedule; }

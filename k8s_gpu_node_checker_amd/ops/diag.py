@@ -284,6 +284,8 @@ def lib() -> ctypes.CDLL:
         L.diag_set_gemm_buffer_loads.argtypes = [ctypes.c_int]
         L.diag_set_gemm_schedule.argtypes = [ctypes.c_int]
         L.diag_set_gemm_fp8_unscaled.argtypes = [ctypes.c_int]
+        L.diag_set_gemm_tail.argtypes = [ctypes.c_int]
+        L.diag_get_gemm_tail.restype = ctypes.c_int
         for getter in ("diag_get_gemm_variant", "diag_get_gemm_epilogue", "diag_get_gemm_buffer_loads",
                        "diag_get_gemm_schedule", "diag_get_gemm_fp8_unscaled"):
             getattr(L, getter).restype = ctypes.c_int
@@ -404,6 +406,18 @@ def get_gemm_fp8_unscaled() -> bool:
     return bool(f()) if f is not None else True
 
 
+def set_gemm_tail(tail: bool) -> None:
+    """v4 bf16: run a short last wave of 256x256 tiles (at most a quarter of the chip's 256 CUs, e.g. 6144^3's 576
+    tiles) as 128x128 quadrants with v1's K loop (True, the default) or leave it to v4 (False, kept for A/B).  C and
+    the fused column sums are bit-identical either way.  Per calling thread."""
+    lib().diag_set_gemm_tail(1 if tail else 0)
+
+
+def get_gemm_tail() -> bool:
+    f = getattr(lib(), "diag_get_gemm_tail", None)  # (absent from the test doubles of the library)
+    return bool(f()) if f is not None else True
+
+
 def get_gemm_config() -> Dict[str, Any]:
     """The calling thread's GEMM knobs (they are thread-local in the library: every agent thread
     starts from the production defaults ``auto`` / LDS-staged epilogue / ``global_load_lds`` / schedule 1)."""
@@ -413,7 +427,7 @@ def get_gemm_config() -> Dict[str, Any]:
             "epilogue": bool(L.diag_get_gemm_epilogue()),
             "buffer_loads": bool(L.diag_get_gemm_buffer_loads()),
             "schedule": int(L.diag_get_gemm_schedule()),
-            "fp8_unscaled": get_gemm_fp8_unscaled()}
+            "fp8_unscaled": get_gemm_fp8_unscaled(), "tail": get_gemm_tail()}
 
 
 def get_gemm_epilogue() -> bool:
@@ -426,9 +440,9 @@ class gemm_config:
 
     def __init__(self, variant: Optional[str] = None, epilogue: Optional[bool] = None,
                  buffer_loads: Optional[bool] = None, schedule: Optional[int] = None,
-                 fp8_unscaled: Optional[bool] = None):
+                 fp8_unscaled: Optional[bool] = None, tail: Optional[bool] = None):
         self.want = {"variant": variant, "epilogue": epilogue, "buffer_loads": buffer_loads, "schedule": schedule,
-                     "fp8_unscaled": fp8_unscaled}
+                     "fp8_unscaled": fp8_unscaled, "tail": tail}
         self.saved: Dict[str, Any] = {}
 
     @staticmethod
@@ -443,6 +457,8 @@ class gemm_config:
             set_gemm_schedule(cfg["schedule"])
         if cfg.get("fp8_unscaled") is not None:
             set_gemm_fp8_unscaled(cfg["fp8_unscaled"])
+        if cfg.get("tail") is not None and getattr(lib(), "diag_set_gemm_tail", None) is not None:
+            set_gemm_tail(cfg["tail"])
 
     def __enter__(self) -> "gemm_config":
         self.saved = get_gemm_config()

@@ -290,7 +290,7 @@ def test_mfma_gemm_large_auto_uses_v4_and_matches(dev):
     bf16-input, fp32-accumulate torch reference.  Runs with the production knobs (what the agent launches)."""
     from k8s_gpu_node_checker_amd.ops import diag
     assert diag.get_gemm_config() == {"variant": "auto", "epilogue": True, "buffer_loads": False, "schedule": 1,
-                                     "fp8_unscaled": True}
+                                     "fp8_unscaled": True, "tail": True}
     m = n = k = 4096
     g = torch.Generator(device=dev).manual_seed(4096)
     a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
@@ -340,6 +340,37 @@ def test_v4_gemm_is_bit_identical_to_v3(dev, m, n, k):
     assert torch.equal(c16, c32.to(torch.bfloat16))
     ref = a.float() @ bt.float().t()
     assert ((c32 - ref).abs() / ref.abs().clamp_min(1.0)).max().item() < 1e-4 * max(1, k / 512)
+
+
+@pytest.mark.parametrize("m,n,k", [(6144, 6144, 256), (2304, 7424, 192), (4352, 4096, 64)])
+def test_v4_tail_wave_is_bit_identical(dev, m, n, k):
+    """a grid whose last wave is short (576 tiles = 2.25 waves; 261 tiles, an uneven 5-per-XCD
+    remainder; 272) runs its whole waves on v4 and the rest as 128x128 quadrants (gemm_v4_tail_kernel): fp32 C, bf16
+    C and the fused column sums equal v3's and tail-off v4's bit for bit (v4t: C bitwise, sums to fp64 rounding)."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + 5 * n + 11 * k)
+    st = torch.cuda.current_stream().cuda_stream
+    a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
+    bt = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
+    outs = {}
+    for name, variant, tail in (("v3", "v3", True), ("v4", "v4", True), ("v4-notail", "v4", False),
+                                ("v4t", "v4t", True)):
+        with diag.gemm_config(variant=variant, tail=tail):
+            c32 = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+            diag.gemm_launch(a.data_ptr(), bt.data_ptr(), c32.data_ptr(), m, n, k, st)
+            c16 = torch.full((m, n), float("nan"), device=dev, dtype=torch.bfloat16)
+            cs = torch.full((m // 128, n), float("nan"), device=dev, dtype=torch.float64)
+            diag.gemm_launch_ck("bf16", a.data_ptr(), bt.data_ptr(), c16.data_ptr(), cs.data_ptr(), m, n, k, st)
+            torch.cuda.synchronize()
+            outs[name] = (c32, c16, cs)
+    assert diag.get_gemm_config()["tail"] is True  # restored
+    for name in ("v4", "v4-notail", "v4t"):
+        assert not torch.isnan(outs[name][0]).any() and not torch.isnan(outs[name][2]).any(), name  # every tile
+        assert torch.equal(outs["v3"][0], outs[name][0]), name
+        assert torch.equal(outs["v3"][1], outs[name][1]), name
+    assert torch.equal(outs["v3"][2], outs["v4"][2]) and torch.equal(outs["v3"][2], outs["v4-notail"][2])
+    mag = outs["v3"][0].double().abs().view(m // 128, 128, n).sum(dim=1)
+    assert ((outs["v3"][2] - outs["v4t"][2]).abs() / mag).max().item() < 1e-14
 
 
 @pytest.mark.parametrize("m,n,k", [(256, 256, 128), (256, 512, 256), (512, 256, 384), (768, 512, 640),
@@ -991,3 +1022,16 @@ def test_gemm_knobs_are_thread_local_and_concurrent_threads_agree(dev):
         rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
         assert rel < 1e-4 * (k / 512), rel
         assert torch.equal(c, outs[0])
+
+
+def test_xgmi_fan_entry_point_on_one_gpu(dev):
+    """diag_p2p_fan_t loads and validates on real HIP (a one-GPU box has no peers to fan to): a fan to the source
+    itself is refused before anything is allocated; the matrix skips a lone GPU."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    with pytest.raises(RuntimeError, match="every peer must be a device other than the source"):
+        diag.p2p_fan(0, [0], mib=1, iters=1)
+    with pytest.raises(RuntimeError, match="1..64 peers"):
+        diag.p2p_fan(0, [], mib=1, iters=1)
+    if diag.device_count() == 1:
+        m = diag.p2p_matrix([0])
+        assert m["pass"] and m["skipped"]
