@@ -1260,10 +1260,28 @@ __host__ __device__ constexpr int v4_tail_main(int nwg) { return nwg / 256 * 256
 // only a short tail is worth it: a quarter wave of 256^2 tiles is one 2-per-CU wave of 128^2 quadrants
 __host__ __device__ constexpr bool v4_tail_applies(int nwg) { return nwg > 256 && nwg % 256 != 0 && nwg % 256 <= 64; }
 
-template <int OUT, int GM = 4>
+// fp8 (E4M3) form of v1's K-tile for the tail: a K-tile is 128 bytes, one v_mfma_f32_16x16x128_f8f6f4 per block on
+// the lane's 32 contiguous bytes (chunks 2fq, 2fq + 1, the fp8 swizzle) -- v3 / v4's fp8 fragments and instruction
+__device__ __forceinline__ void tail_compute_fp8(floatx4 (&acc)[4][4], const u32x4 (&buf)[2][TILE_CHUNKS], int wr,
+                                                 int wc, int frow, int fq) {
+  i32x8 af[4], bfr[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) stg_load(af[m], buf[0], wr * 64 + m * 16 + frow, fq);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) stg_load(bfr[n], buf[1], wc * 64 + n * 16 + frow, fq);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      acc[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[n], acc[m][n], 0, 0, 0, 0, 0, 0);
+}
+
+template <int OUT, int GM = 4, int DT = DT_BF16>
 __global__ void __launch_bounds__(THREADS, 2)
 gemm_v4_tail_kernel(const u32x4* __restrict__ A, const u32x4* __restrict__ Bt, void* __restrict__ Cv,
                     double* __restrict__ csum, int M, int N, int K) {
+  static_assert(DT == DT_BF16 || DT == DT_FP8U, "the tail runs v4's dtypes");
+  constexpr bool FP8 = DT == DT_FP8U;
   __shared__ u32x4 lds[2][2][TILE_CHUNKS];  // [buffer][A|B][chunk] = 64 KiB
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
@@ -1296,28 +1314,32 @@ gemm_v4_tail_kernel(const u32x4* __restrict__ A, const u32x4* __restrict__ Bt, v
     const int ch = tid + i * THREADS;
     const int rr = ch / CHUNKS_PER_ROW, c = ch % CHUNKS_PER_ROW;
     g_off[i] = rr * kchunks + c;
-    l_off[i] = swz(rr, c);
+    l_off[i] = FP8 ? swz8(rr, c) : swz(rr, c);
   }
   floatx4 acc[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int KT = K / BK;
+  const int KT = K / BK;  // K-tiles of 64 bf16 columns = 128 fp8 bytes
   const int frow = lane & 15, fq = lane >> 4;
+  auto compute = [&](const u32x4(&buf)[2][TILE_CHUNKS]) {
+    if constexpr (FP8) tail_compute_fp8(acc, buf, wr, wc, frow, fq);
+    else gemm_compute(acc, buf, wr, wc, frow, fq);
+  };
   gemm_gload(ra, rb, Ablk, Bblk, g_off, 0);
   gemm_lstore(lds[0], ra, rb, l_off);
   __syncthreads();
   for (int kt = 0; kt < KT; kt += 2) {
     const bool more1 = kt + 1 < KT;
     if (more1) gemm_gload(ra, rb, Ablk, Bblk, g_off, kt + 1);
-    gemm_compute(acc, lds[0], wr, wc, frow, fq);
+    compute(lds[0]);
     if (more1) gemm_lstore(lds[1], ra, rb, l_off);
     __syncthreads();
     if (!more1) break;
     const bool more2 = kt + 2 < KT;
     if (more2) gemm_gload(ra, rb, Ablk, Bblk, g_off, kt + 2);
-    gemm_compute(acc, lds[1], wr, wc, frow, fq);
+    compute(lds[1]);
     if (more2) gemm_lstore(lds[0], ra, rb, l_off);
     __syncthreads();
   }
@@ -1989,13 +2011,13 @@ int launch_v4_inst(const void* A, const void* Bt, void* C, double* csum, int M, 
   static LdsAttrOnce attr;
   if (ensure_dynamic_lds(attr, reinterpret_cast<const void*>(kern), 2 * V2_STAGE_BYTES, "gemm v4") != 0) return -1;
   const int nwg = (M / V2_BM) * (N / V2_BN);
-  // bf16 with a short last wave: v4 on the whole waves, the rest as 128^2 quadrants (gemm_v4_tail_kernel)
-  const bool tail = DT == DT_BF16 && g_gemm_tail && v4_tail_applies(nwg);
+  // a short last wave: v4 on the whole waves, the rest as 128^2 quadrants (gemm_v4_tail_kernel)
+  const bool tail = g_gemm_tail && v4_tail_applies(nwg);
   const int main_wg = tail ? v4_tail_main(nwg) : nwg;
   hipLaunchKernelGGL(kern, dim3(main_wg), dim3(V4_THREADS), 2 * V2_STAGE_BYTES, stream, static_cast<const __bf16*>(A),
                      static_cast<const __bf16*>(Bt), C, csum, M, N, K);
   if (tail)
-    hipLaunchKernelGGL((gemm_v4_tail_kernel<OUT, 4>), dim3(4 * (nwg - main_wg)), dim3(THREADS), 0, stream,
+    hipLaunchKernelGGL((gemm_v4_tail_kernel<OUT, 4, DT>), dim3(4 * (nwg - main_wg)), dim3(THREADS), 0, stream,
                        static_cast<const u32x4*>(A), static_cast<const u32x4*>(Bt), C, csum, M, N, K);
   return 0;
 }

@@ -407,9 +407,9 @@ def get_gemm_fp8_unscaled() -> bool:
 
 
 def set_gemm_tail(tail: bool) -> None:
-    """v4 bf16: run a short last wave of 256x256 tiles (at most a quarter of the chip's 256 CUs, e.g. 6144^3's 576
-    tiles) as 128x128 quadrants with v1's K loop (True, the default) or leave it to v4 (False, kept for A/B).  C and
-    the fused column sums are bit-identical either way.  Per calling thread."""
+    """v4 (bf16 and fp8): run a short last wave of 256x256 tiles (at most a quarter of the chip's 256 CUs, e.g.
+    6144^3's 576 tiles) as 128x128 quadrants with v1's K loop (True, the default) or leave it to v4 (False, kept for
+    A/B).  C and the fused column sums are bit-identical either way.  Per calling thread."""
     lib().diag_set_gemm_tail(1 if tail else 0)
 
 

@@ -405,6 +405,30 @@ def test_v4_fp8_gemm_is_bit_identical_to_v3(dev, m, n, k):
     assert err.item() < diag.GEMM_FP8_MAX_ERR
 
 
+@pytest.mark.parametrize("m,n,k", [(6144, 6144, 512), (2304, 7424, 256)])
+def test_v4_fp8_tail_wave_is_bit_identical(dev, m, n, k):
+    """The fp8 tail (128x128 quadrants on the unscaled 16x16x128 MFMA, v3 / v4's fp8 fragments): fp32 C, bf16 C and
+    the column sums equal v3's and tail-off v4's bit for bit."""
+    from k8s_gpu_node_checker_amd.ops import diag
+    g = torch.Generator(device=dev).manual_seed(m + 7 * n + 13 * k)
+    st = torch.cuda.current_stream().cuda_stream
+    x = torch.randn(m, k, device=dev, generator=g).to(torch.float8_e4m3fn)
+    y = torch.randn(n, k, device=dev, generator=g).to(torch.float8_e4m3fn)
+    outs = {}
+    for name, variant, tail in (("v3", "v3", True), ("v4", "v4", True), ("v4-notail", "v4", False)):
+        with diag.gemm_config(variant=variant, tail=tail):
+            c32 = torch.full((m, n), float("nan"), device=dev, dtype=torch.float32)
+            diag.gemm_fp8_launch(x.data_ptr(), y.data_ptr(), c32.data_ptr(), m, n, k, st)
+            c16 = torch.full((m, n), float("nan"), device=dev, dtype=torch.bfloat16)
+            cs = torch.full((m // 128, n), float("nan"), device=dev, dtype=torch.float64)
+            diag.gemm_launch_ck("fp8", x.data_ptr(), y.data_ptr(), c16.data_ptr(), cs.data_ptr(), m, n, k, st)
+            torch.cuda.synchronize()
+            outs[name] = (c32, c16, cs)
+    for name in ("v4", "v4-notail"):
+        for i in range(3):
+            assert torch.equal(outs["v3"][i], outs[name][i]), (name, i)
+
+
 def test_v4_gemm_diagnostic_reports_bf16_output(dev):
     """The bf16 diagnostic at a size that fills the chip times v4 with bf16 C and fused sums, and passes."""
     from k8s_gpu_node_checker_amd.ops import diag
