@@ -196,3 +196,17 @@ def test_narrowing_and_a_misdirected_child():
     assert A.misdirected("0000:05:00.0", {"bdf": "15:00.0"}) == (
         "diagnostic process ran on 0000:15:00.0, not 0000:05:00.0: HIP device visibility mismatch")
 
+
+
+def test_agent_cli_default_isolation_on_a_box_without_a_gpu(tmp_path, capsys):
+    """The DaemonSet's entry point with its default (process isolation) where HIP sees no GPU: the enumeration
+    child says so, every GPU carries the reason, and the agent itself exits normally."""
+    import json
+    fx = tmp_path / "fx.json"
+    fx.write_text(json.dumps(fixtures.mi355x_probe_report("n", gpus=2)))
+    rc = A.main(["--node", "n", "--once", "--source", "fixture", "--fixture", str(fx), "--publish", "stdout",
+                 "--diag-level", "1", "--diag-timeout", "60"])
+    rep = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
+    assert rc == 0
+    reasons = [g.get("diag_skipped") or "" for g in rep["gpus"]]
+    assert all(r.startswith(("no HIP device visible", "HIP device enumeration failed")) for r in reasons), reasons
