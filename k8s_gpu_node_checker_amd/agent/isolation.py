@@ -233,7 +233,14 @@ class Workers:
         box: Dict[str, Any] = {}
         parent, child = self.ctx.Pipe(duplex=False)
         proc = self.ctx.Process(target=target, args=(child, *args), name=f"mi355x-{what}", daemon=True)
-        proc.start()
+        try:
+            proc.start()
+        except Exception as e:  # the forkserver is gone, no memory for a child, ...: that job failed, not the agent
+            parent.close()
+            child.close()
+            box["res"] = died(f"could not start the diagnostic process: {type(e).__name__}: {e}")
+            done.set()
+            return Job(box=box)
         child.close()  # the child's end lives in the child only: its exit closes the pipe (EOF)
         self.started.append({"pid": proc.pid, "what": what})
 

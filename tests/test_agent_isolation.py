@@ -210,3 +210,21 @@ def test_agent_cli_default_isolation_on_a_box_without_a_gpu(tmp_path, capsys):
     assert rc == 0
     reasons = [g.get("diag_skipped") or "" for g in rep["gpus"]]
     assert all(r.startswith(("no HIP device visible", "HIP device enumeration failed")) for r in reasons), reasons
+
+
+def test_a_child_that_cannot_start_is_that_gpus_failure(node, monkeypatch):
+    node(2)
+    ag = agent(2)
+
+    class Broken:
+        def __init__(self, *a, **kw):
+            pass
+
+        def start(self):
+            raise OSError(12, "Cannot allocate memory")
+    monkeypatch.setattr(ag.workers.ctx, "Process", Broken)
+    rep = ag.probe_once()  # the enumeration could not start either: said per GPU, the agent goes on
+    assert all(g["diag_skipped"].startswith("HIP device enumeration failed: could not start the diagnostic process")
+               for g in rep["gpus"])
+    job = ag.workers.device(1, 0, {}, __import__("threading").Event())
+    assert not job.is_alive() and job.box["res"]["run"]["detail"].startswith("could not start the diagnostic process")
