@@ -1041,7 +1041,7 @@ def test_gemm_knobs_are_thread_local_and_concurrent_threads_agree(dev):
         assert diag.get_gemm_config()["variant"] == "v1"  # this thread's own setting survives
     assert not errs, errs
     assert seen == [{"variant": "auto", "epilogue": True, "buffer_loads": False, "schedule": 1,
-                     "fp8_unscaled": True}] * 4
+                     "fp8_unscaled": True, "tail": True}] * 4
     for c in outs:
         rel = ((c - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
         assert rel < 1e-4 * (k / 512), rel
