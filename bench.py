@@ -83,13 +83,18 @@ BASELINE_BASIS = ("SURVEY §6 proxy: the unmodified reference (check-gpu-node.py
                   "client, in-process one_shot median, 8-vCPU Xeon VM -- a different machine from this run")
 
 
-def _curve_servers(sizes: "list[int]") -> "tuple[list, dict]":
+def _curve_servers(sizes: "list[int]", procs: list) -> dict:
     """One mock apiserver per curve point, all started at once (before any GPU work): ``n`` realistic MI355X
     nodes (``amd.com/gpu: 1``) carrying the recorded probe annotation and condition the DaemonSet writes
-    (gzip-encoded), so every node goes through the same health gate as the headline's live ones."""
-    started = [(n, _start(MOCK, "--nodes", str(n), "--kind", "amd", "--gpus-per-node", "1",
-                          "--annotation-encoding", "gzip", "--with-health")) for n in sizes]
-    return [p for _, p in started], {n: _ready(p, MOCK)["url"] for n, p in started}
+    (gzip-encoded), so every node goes through the same health gate as the headline's live ones.  Each process
+    goes into ``procs`` as soon as it starts (the caller ends them, whatever fails after)."""
+    started = []
+    for n in sizes:
+        p = _start(MOCK, "--nodes", str(n), "--kind", "amd", "--gpus-per-node", "1", "--annotation-encoding", "gzip",
+                   "--with-health")
+        procs.append(p)
+        started.append((n, p))
+    return {n: _ready(p, MOCK)["url"] for n, p in started}
 
 
 def _own_gpu(gpus, local_rank, cuda):
@@ -341,8 +346,10 @@ def main() -> int:
             ctrl["slack"] = sinfo["url"] + "/200"
         sizes = sorted({int(x) for x in args.curve.split(",") if x.strip()} - {n_nodes})
         if sizes:
-            started, ctrl["curve_api"] = _curve_servers(sizes)
-            procs.extend(started)
+            try:
+                ctrl["curve_api"] = _curve_servers(sizes, procs)
+            except Exception as e:  # the curve is an extra: its servers failing must not cost the headline
+                ctrl["curve_error"] = f"{type(e).__name__}: {e}"[:300]
     budget.mark("control_plane", t_control)
     if rank == 0 and args.coldstart_runs > 0:
         if budget.fits(COLDSTART_MIN_S):
@@ -521,9 +528,14 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
                            "live" if probe_source != "fixture" else "fixture")]
         with budget.phase("curve"):
             for n, url in sorted((ctrl.get("curve_api") or {}).items()):
-                el, lt, sp, ls = _timed_checks(ClusterConnection(url), opts, args.steps, args.warmup)
-                curve.append(curve_row(n, el, args.steps, lt, sp, ls, bool(args.slack), "recorded"))
-        curve.sort(key=lambda r: r["nodes"])
+                try:
+                    el, lt, sp, ls = _timed_checks(ClusterConnection(url), opts, args.steps, args.warmup)
+                    curve.append(curve_row(n, el, args.steps, lt, sp, ls, bool(args.slack), "recorded"))
+                except Exception as e:  # a row that fails is reported as such; the line still prints
+                    curve.append({"nodes": n, "check_ok": False, "error": f"{type(e).__name__}: {e}"[:300]})
+            if ctrl.get("curve_error"):
+                curve.append({"nodes": None, "check_ok": False, "error": ctrl["curve_error"]})
+        curve.sort(key=lambda r: (r["nodes"] is None, r["nodes"] or 0))
 
     if rank == 0:
         ok = last is not None and last.exit_code == 0 and len(last.ready_gpu_nodes) == n_nodes
