@@ -57,6 +57,50 @@ def _rss_mb(pid: int):
     return None
 
 
+def _proc_counts(pid: int):
+    """Open file descriptors and threads of ``pid`` (what a leak per diagnostic child would grow: pipe ends, reader
+    threads)."""
+    try:
+        fds = len(os.listdir(f"/proc/{pid}/fd"))
+        with open(f"/proc/{pid}/status") as f:
+            threads = next(int(line.split()[1]) for line in f if line.startswith("Threads:"))
+        return fds, threads
+    except (OSError, StopIteration, ValueError):
+        return None, None
+
+
+def _zombies(pids):
+    """How many of ``pids`` are zombies (ended, never reaped)."""
+    n = 0
+    for p in pids:
+        try:
+            with open(f"/proc/{p}/stat") as f:
+                n += f.read().rsplit(")", 1)[1].split()[0] == "Z"
+        except (OSError, IndexError):
+            pass
+    return n
+
+
+def _descendant_pids(pid: int):
+    """Every descendant of ``pid``, zombies included."""
+    kids = {}
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat") as f:
+                ppid = int(f.read().rsplit(")", 1)[1].split()[1])
+        except (OSError, ValueError, IndexError):
+            continue
+        kids.setdefault(ppid, []).append(int(d))
+    out, todo = [], list(kids.get(pid, []))
+    while todo:
+        c = todo.pop()
+        out.append(c)
+        todo.extend(kids.get(c, []))
+    return out
+
+
 def _descendants(pid: int):
     """RSS (MiB) of every live descendant of ``pid`` (process isolation: the forkserver, and a diagnostic child if
     one is running at the sample), by pid."""
@@ -140,6 +184,8 @@ def main() -> int:
                              if c.get("type") == H.HEALTH_CONDITION), None)
                 hb = H.parse_k8s_time(cond.get("lastHeartbeatTime")) if cond else None
                 hz, _ = _get(f"http://127.0.0.1:{args.port}/healthz")
+                kids = _descendants(agent.pid)
+                fds, threads = _proc_counts(agent.pid)
                 pc, body = _get(f"http://127.0.0.1:{args.port}/probe")
                 rep = json.loads(body) if pc == 200 else {}
                 g = (rep.get("gpus") or [{}])[0]
@@ -150,7 +196,9 @@ def main() -> int:
                      "state": rep.get("state"), "agent_rss_mb": _rss_mb(agent.pid),
                      # process isolation: the forkserver (and a child caught mid-diagnostic), and the peak RSS of the
                      # child that produced the last result (its own getrusage, reported over the pipe)
-                     "children_rss_mb": _descendants(agent.pid),
+                     "children_rss_mb": kids,
+                     "zombies": _zombies(_descendant_pids(agent.pid)),
+                     "agent_fds": fds, "agent_threads": threads,
                      "diag_child_peak_mb": (g.get("diag_proc") or {}).get("peak_rss_mib"),
                      "diag_child_pid": (g.get("diag_proc") or {}).get("pid"),
                      "vram_used_mb": g.get("vram_used_mb"), "diag_pass": {k: v.get("pass") for k, v in diag.items()
@@ -201,6 +249,11 @@ def main() -> int:
         "diag_child_peak_mb": _spread([s["diag_child_peak_mb"] for s in samples]),
         "diag_children_seen": len({s["diag_child_pid"] for s in samples if s["diag_child_pid"]}),
         "vram_used_mb": _spread([s["vram_used_mb"] for s in samples]),
+        # leak watch over the run's diagnostic children: the agent's fds and threads, unreaped children
+        "agent_fds": _spread([s["agent_fds"] for s in samples]),
+        "agent_fds_first_last": [samples[0]["agent_fds"], samples[-1]["agent_fds"]] if samples else None,
+        "agent_threads": _spread([s["agent_threads"] for s in samples]),
+        "zombies_max": max((s["zombies"] for s in samples), default=0),
         "diag_failures": sum(1 for s in samples for v in s["diag_pass"].values() if v is False),
         "apiserver_writes": {p: sum(1 for e in writes if e["path"] == p) for p in sorted({e["path"] for e in writes})},
         "labels_last": samples[-1]["labels"] if samples else None,
