@@ -147,11 +147,15 @@ from ..ops.diag import P2P_SHARE  # noqa: E402  (share of --diag-timeout the xGM
 MEM_RESIDENT_MIB = 65
 # one diagnostic child's peak, its own getrusage (HIP runtime, comgr's code objects, the level's buffers; the child
 # sees one GPU, isolation.narrow_to, so it is the same process on a one-GPU box and on an 8-GPU node): level 1
-# 632 MiB over 48 children, level 2 1,273 MiB over 36 (the host link's pinned buffer and the 8192^3 GEMMs included)
-MEM_CHILD_PEAK_MIB = {1: 632, 2: 1273}
+# 443 MiB (its runtime starts without the SDMA engines, ops/diag.DMA_TESTS), level 2 1,082 MiB (the host link's
+# pinned buffer and the 8192^3 GEMMs included) -- profiles/agent_soak_isolated_l{1,2}_r06b_mi355x.json
+MEM_CHILD_PEAK_MIB = {1: 443, 2: 1082}
+# a one-GPU HIP process with its SDMA queues (the fabric child copies between GPUs over them): a level-1 suite with
+# the engines on peaks at 628-682 MiB (profiles/child_peak_rss_sdma_r06_mi355x.jsonl)
+MEM_GPU_WITH_SDMA_MIB = 682
 # the node-level child (xGMI matrix, in-process RCCL suite; level 2, >= 2 GPUs) with a warm comgr cache: 2,712 MiB
-# for the suite on one GPU (profiles/rccl_rss_comgr_cache_mi355x.json).  Each further GPU is counted at a level-1
-# child's peak -- an upper bound, unmeasured: no multi-GPU box was available to this project
+# for the suite on one GPU (profiles/rccl_rss_comgr_cache_mi355x.json).  Each further GPU is counted at
+# MEM_GPU_WITH_SDMA_MIB -- an upper bound, unmeasured: no multi-GPU box was available to this project
 MEM_FABRIC_ONE_GPU_MIB = 2712
 # ... and with a cold comgr cache: comgr decompresses RCCL's compressed code objects on the first load, peak 11,786
 # MiB (profiles/rccl_rss_comgr_cache_mi355x.json); the level-2 overlay keeps the cache on the node
@@ -169,7 +173,7 @@ def memory_budget_mib(devices: int, level: int, rccl: bool = False, parallel: in
         children = min(max(1, devices), max(1, parallel)) * MEM_CHILD_PEAK_MIB[min(level, 2)]
         fabric = 0
         if level >= 2 and rccl and devices >= 2:
-            fabric = MEM_FABRIC_ONE_GPU_MIB + (devices - 1) * MEM_CHILD_PEAK_MIB[1]
+            fabric = MEM_FABRIC_ONE_GPU_MIB + (devices - 1) * MEM_GPU_WITH_SDMA_MIB
         mib += max(children, fabric)
     return mib
 

@@ -124,6 +124,11 @@ def device_main(conn: Any, setup: Setup, level: int, device: int, kw: Dict[str, 
     t0 = time.monotonic()
     _quiet_signals()
     ordinal = device if narrow_to(device) is None else 0
+    from ..ops.diag import uses_dma
+    if not uses_dma(level):
+        # a suite that times no DMA-engine copy keeps the runtime off the SDMA engines: ~180 MiB less host memory
+        # (ops/diag.DMA_TESTS); set before this process starts its HIP runtime
+        os.environ.setdefault("HSA_ENABLE_SDMA", "0")
     _setup(setup)
     from ..ops import diag
     if host_lock is not None:

@@ -1128,6 +1128,12 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
   };
 #endif
 
+  // The epilogue takes lane / frow / fq afresh from the lane id (v_mbcnt) instead of the values computed for the
+  // prologue: those would be live across the K loop, where the 256 accumulators leave no VGPR for them, and the
+  // bf16 + column-sum kernels spilled three (fp8: five) to scratch -- the kernel's only scratch use.
+  {
+  const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int frow = lane & 15, fq = lane >> 4;
   const int row0 = tm * V2_BM + wr * 128, col0 = tn * V2_BN + wc * 128;
   if constexpr (TR) {
     // Transposed blocks (the B fragment is the MFMA's first operand): lane (frow, fq) of block (m, n) holds row
@@ -1241,6 +1247,7 @@ gemm_v4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void
       }
     }
   }
+  }  // the epilogue's scope
 #ifdef DIAG_V4_STAMPS
   write_stamps();
 #endif
@@ -3257,10 +3264,12 @@ int diag_host_link(int device, size_t bytes, int iters, double* h2d_gbps, double
   memset(host, 0x5A, bytes);
   DevBuf dev;
   DIAG_CHECK(dev.alloc(device, bytes));
+  // on the null stream, as every single-device test: a stream of its own would be one more hardware queue, and each
+  // queue the runtime creates holds ~170 MiB of host memory for the rest of the process (tools/hip_rss_probe.hip)
   Timer tm;
-  DIAG_CHECK(tm.create(true));
+  DIAG_CHECK(tm.create());
   hipEvent_t e0 = tm.e0, e1 = tm.e1;
-  hipStream_t st = tm.stream;
+  hipStream_t st = nullptr;
   for (int dir = 0; dir < 2; ++dir) {
     auto copy = [&]() {
       return dir == 0 ? hipMemcpyAsync(dev.ptr, host, bytes, hipMemcpyHostToDevice, st)

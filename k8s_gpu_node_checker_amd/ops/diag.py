@@ -73,6 +73,16 @@ from .native import NativeUnavailable, load_cdll
 # whichever box ran last: a slower healthy platform shows as a node-level note, not as failed GPUs.
 FAIL_FRACTION = 0.85
 SHARED_TESTS = frozenset(("host_link",))
+# tests that time the DMA (SDMA) engines: every other test keeps its copies to a few KiB or on the device.  A process
+# that runs none of them can start its HIP runtime with HSA_ENABLE_SDMA=0 -- copies then run as blit kernels, and the
+# runtime never sets up its SDMA queues, which hold ~180 MiB of host memory from the first copy of 32 KiB or more on
+# (tools/hip_rss_probe.hip, tools/copy_threshold.sh).  The agent's isolated children do (agent/isolation.py).
+DMA_TESTS = frozenset(("host_link",))
+
+
+def uses_dma(level: int) -> bool:
+    """Whether the suite of ``level`` times a DMA-engine copy (:data:`DMA_TESTS`)."""
+    return any(t.replace("_quick", "") in DMA_TESTS for t in LEVELS.get(level, ()))
 _HOST_SHARED: Any = threading.Lock()  # held by the one device measuring a SHARED_TESTS test
 _HOST_HOLDER: Dict[str, Any] = {}  # who holds it: {"device": d, "since": monotonic time}
 # per-device diagnostic *processes* (agent/isolation.py) share a multiprocessing lock instead, and say who holds it

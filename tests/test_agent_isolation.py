@@ -228,3 +228,27 @@ def test_a_child_that_cannot_start_is_that_gpus_failure(node, monkeypatch):
                for g in rep["gpus"])
     job = ag.workers.device(1, 0, {}, __import__("threading").Event())
     assert not job.is_alive() and job.box["res"]["run"]["detail"].startswith("could not start the diagnostic process")
+
+
+def _record_env():
+    """Child setup: the fake C ABI, and a suite that reports the environment the child's HIP runtime would start with."""
+    from k8s_gpu_node_checker_amd.testing import fake_native
+    fake_native.install(n=1)
+    diag.run = lambda level, device, **kw: {"env": {"pass": True, "sdma": os.environ.get("HSA_ENABLE_SDMA"),
+                                                    "visible": os.environ.get("HIP_VISIBLE_DEVICES")}}
+
+
+def test_a_child_whose_suite_times_no_dma_copy_starts_hip_without_sdma(monkeypatch):
+    """Level 1 times no DMA-engine copy: its child starts HIP with HSA_ENABLE_SDMA=0 (the SDMA queues' ~180 MiB of
+    host memory never allocated); level 2's host-link test times SDMA, so its child keeps the engines."""
+    import threading
+    monkeypatch.delenv("HSA_ENABLE_SDMA", raising=False)
+    assert not diag.uses_dma(1) and diag.uses_dma(2) and not diag.uses_dma(0)
+    w = isolation.Workers("process", setup=(__name__, "_record_env", {}), method="fork")
+    for level, want in ((1, "0"), (2, None)):
+        done = threading.Event()
+        job = w.device(level, 0, {}, done)
+        assert done.wait(30)
+        env = job.box["res"]["env"]
+        assert env["sdma"] == want and env["visible"] == "0", (level, env)
+    assert os.environ.get("HSA_ENABLE_SDMA") is None  # the agent's own environment is untouched

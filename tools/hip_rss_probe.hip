@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 static void step(const char* name) {
@@ -39,6 +40,15 @@ __global__ void lds_user(float* p) {
   s[threadIdx.x] = static_cast<float>(threadIdx.x);
   __syncthreads();
   p[blockIdx.x * blockDim.x + threadIdx.x] = s[(threadIdx.x * 7) & 255];
+}
+
+// a private array indexed at run time lives in scratch (private_segment_fixed_size > 0): the runtime sets up scratch
+// for the queue at this kernel's first dispatch
+__global__ void scratch_user(float* p, int k) {
+  float a[256];
+#pragma unroll 1
+  for (int i = 0; i < 256; ++i) a[i] = p[(i * 7 + threadIdx.x) & 4095];
+  p[blockIdx.x * blockDim.x + threadIdx.x] = a[(threadIdx.x * 13 + k) & 255];
 }
 
 #define CHECK(x)                                                             \
@@ -85,6 +95,40 @@ int main(int argc, char** argv) {
   CHECK(hipEventRecord(b, st));
   CHECK(hipEventSynchronize(b));
   step("events");
+  hipLaunchKernelGGL(scratch_user, dim3(1024), dim3(256), 0, nullptr, p, 3);
+  CHECK(hipGetLastError());
+  CHECK(hipDeviceSynchronize());
+  step("first kernel with scratch");
+  // `probe LIB KIB [pinned]`: one device-to-host copy of KIB KiB (into pinned memory with "pinned") and nothing else
+  if (argc > 2) {
+    const size_t s = static_cast<size_t>(std::atol(argv[2])) << 10;
+    const bool pinned = argc > 3 && std::strcmp(argv[3], "pinned") == 0;
+    void* dst = nullptr;
+    if (pinned) CHECK(hipHostMalloc(&dst, s, hipHostMallocDefault));
+    else dst = std::malloc(s);
+    step(pinned ? "hipHostMalloc" : "malloc");
+    CHECK(hipMemcpy(dst, p, s, hipMemcpyDeviceToHost));
+    char label[64];
+    std::snprintf(label, sizeof label, "%s D2H %zu KiB", pinned ? "pinned" : "pageable", s >> 10);
+    step(label);
+    return 0;
+  }
+  // pageable (malloc'd) copies of growing size each way: does the runtime stage them through a buffer of its own?
+  {
+    static char host[64 << 20];
+    const size_t sizes[] = {size_t(4) << 10, size_t(64) << 10, size_t(1) << 20, size_t(16) << 20, size_t(64) << 20};
+    char label[64];
+    for (size_t s : sizes) {
+      CHECK(hipMemcpy(host, p, s, hipMemcpyDeviceToHost));
+      std::snprintf(label, sizeof label, "pageable D2H %zu KiB", s >> 10);
+      step(label);
+    }
+    for (size_t s : sizes) {
+      CHECK(hipMemcpy(p, host, s, hipMemcpyHostToDevice));
+      std::snprintf(label, sizeof label, "pageable H2D %zu KiB", s >> 10);
+      step(label);
+    }
+  }
   if (argc > 1) {
     void* h = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
     if (!h) {
