@@ -57,6 +57,53 @@ REF_MS = {1: 2.17, 2: 1.68, 4: 1.74, 8: 2.30, 16: 2.23, 1000: 92.7}
 REF_MS_SLACK = {1: 4.43, 2: 4.02, 4: 3.08, 8: 3.08, 16: 3.57, 1000: 86.1}
 
 
+def _cpu_list(text: str) -> set:
+    """``0-3,8,10-11`` -> {0, 1, 2, 3, 8, 10, 11} (sysfs CPU lists)."""
+    out = set()
+    for part in text.strip().split(","):
+        if part:
+            lo, _, hi = part.partition("-")
+            out.update(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def cpu_pair() -> "dict | None":
+    """CPUs of one L3 domain this process may run on: one for the mock apiserver, the others (on another physical
+    core first) for the checking thread.  A request is a wake-up of the server and a wake-up back; across
+    dies that costs more than the server's own work, so where the scheduler happens to put the two is the box, not the
+    code.  None when no two allowed CPUs share an L3 or the topology is unreadable (then nothing is pinned)."""
+    try:
+        allowed = os.sched_getaffinity(0)
+    except (AttributeError, OSError):
+        return None
+    sysfs = "/sys/devices/system/cpu/cpu{}/{}"
+    seen: set = set()
+    try:  # the domain of the CPU this process runs on first (the scheduler put it where there was room)
+        with open("/proc/self/stat") as f:
+            here = int(f.read().rsplit(")", 1)[1].split()[36])
+    except (OSError, ValueError, IndexError):
+        here = -1
+    try:
+        for c in sorted(allowed, key=lambda x: (x != here, x)):
+            if c in seen:
+                continue
+            with open(sysfs.format(c, "cache/index3/shared_cpu_list")) as f:
+                group = _cpu_list(f.read())
+            seen |= group
+            usable = sorted(group & allowed)
+            if len(usable) < 2:
+                continue
+            client = usable[0]
+            with open(sysfs.format(client, "topology/thread_siblings_list")) as f:
+                siblings = _cpu_list(f.read())
+            server = next((x for x in usable if x not in siblings), usable[1])
+            # the checker's own threads (the paged LIST's prefetch, the Slack sender) get the rest of the domain
+            return {"client_cpus": sorted(set(usable) - {server}), "server_cpu": server, "l3_cpus": len(group)}
+    except (OSError, ValueError):
+        return None
+    return None
+
+
 def _start(module: str, *args: str) -> subprocess.Popen:
     env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
     return subprocess.Popen([sys.executable, "-m", module, *args], stdout=subprocess.PIPE, env=env, text=True)
@@ -83,7 +130,7 @@ BASELINE_BASIS = ("SURVEY §6 proxy: the unmodified reference (check-gpu-node.py
                   "client, in-process one_shot median, 8-vCPU Xeon VM -- a different machine from this run")
 
 
-def _curve_servers(sizes: "list[int]", procs: list) -> dict:
+def _curve_servers(sizes: "list[int]", procs: list, pin: "list | None" = None) -> dict:
     """One mock apiserver per curve point, all started at once (before any GPU work): ``n`` realistic MI355X
     nodes (``amd.com/gpu: 1``) carrying the recorded probe annotation and condition the DaemonSet writes
     (gzip-encoded), so every node goes through the same health gate as the headline's live ones.  Each process
@@ -91,7 +138,7 @@ def _curve_servers(sizes: "list[int]", procs: list) -> dict:
     started = []
     for n in sizes:
         p = _start(MOCK, "--nodes", str(n), "--kind", "amd", "--gpus-per-node", "1", "--annotation-encoding", "gzip",
-                   "--with-health")
+                   "--with-health", *(pin or []))
         procs.append(p)
         started.append((n, p))
     return {n: _ready(p, MOCK)["url"] for n, p in started}
@@ -307,6 +354,9 @@ def main() -> int:
                     help="also time the same check (same --steps / --warmup, rank 0, after the headline) against one "
                          f"mock cluster per node count (default {CURVE_NODES}; '' to skip); the headline's own node "
                          "count is its row")
+    ap.add_argument("--no-pin", dest="pin", action="store_false",
+                    help="leave the checking thread and the mock apiservers where the scheduler puts them (default: two "
+                         "CPUs of one L3 domain, cpu_pair())")
     ap.add_argument("--coldstart-runs", type=int, default=11,
                     help="child-process runs of check-gpu-node --json for coldstart_ms (rank 0, before GPU work; 0: skip)")
     ap.add_argument("--no-fabric-check", dest="fabric_check", action="store_false",
@@ -333,11 +383,14 @@ def main() -> int:
     ctrl = {}
     t_control = time.monotonic()
     if rank == 0:
+        pair = cpu_pair() if args.pin else None
+        ctrl["pinning"] = pair or {"skipped": "--no-pin" if not args.pin else "no two allowed CPUs share an L3"}
+        pin = ["--cpu", str(pair["server_cpu"])] if pair else []
         # nodes beyond the GPU count start with a recorded MI355X probe (condition + annotation, gzip-encoded
         # as the DaemonSet writes it); the ranks' own nodes get their live probe PATCHed below
         p, info = _spawn("k8s_gpu_node_checker_amd.testing.mock_apiserver", "--nodes", str(n_nodes), "--kind", "amd",
                          "--gpus-per-node", "1", "--annotation-encoding", "gzip",
-                         *(["--with-health"] if n_nodes > n_gpus else []))
+                         *(["--with-health"] if n_nodes > n_gpus else []), *pin)
         procs.append(p)
         ctrl["api"] = info["url"]
         if args.slack:
@@ -347,7 +400,7 @@ def main() -> int:
         sizes = sorted({int(x) for x in args.curve.split(",") if x.strip()} - {n_nodes})
         if sizes:
             try:
-                ctrl["curve_api"] = _curve_servers(sizes, procs)
+                ctrl["curve_api"] = _curve_servers(sizes, procs, pin)
             except Exception as e:  # the curve is an extra: its servers failing must not cost the headline
                 ctrl["curve_error"] = f"{type(e).__name__}: {e}"[:300]
     budget.mark("control_plane", t_control)
@@ -498,6 +551,15 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
 
     last = None
     spans: list = []
+    # rank 0 checks from the CPU beside the mock apiserver's (cpu_pair); this thread only, put back after the curve
+    pinned = ctrl.get("pinning") if rank == 0 and "client_cpus" in (ctrl.get("pinning") or {}) else None
+    mask = None
+    if pinned:
+        try:
+            mask = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, set(pinned["client_cpus"]))
+        except OSError:
+            mask = None
     with budget.phase("warmup"):
         for _ in range(args.warmup):
             last = step()
@@ -536,6 +598,8 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
             if ctrl.get("curve_error"):
                 curve.append({"nodes": None, "check_ok": False, "error": ctrl["curve_error"]})
         curve.sort(key=lambda r: (r["nodes"] is None, r["nodes"] or 0))
+    if mask is not None:
+        os.sched_setaffinity(0, mask)
 
     if rank == 0:
         ok = last is not None and last.exit_code == 0 and len(last.ready_gpu_nodes) == n_nodes
@@ -574,6 +638,8 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
             # socket and the mock apiserver's time: what says something about the code across boxes and rounds
             "checker_ms": (_step_breakdown(spans, lat) or {}).get("checker"),
             "baseline_basis": BASELINE_BASIS,
+            # where the checking thread and the mock apiservers ran (cpu_pair), or why they were not pinned
+            "pinning": ctrl.get("pinning"),
             # ms per check, nodes/s, checker_ms and vs_baseline at every node count (headline row included)
             "curve": curve,
             "coldstart_ms": (ctrl.get("coldstart") or {}).get("ms"),

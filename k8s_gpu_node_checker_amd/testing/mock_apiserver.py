@@ -31,6 +31,7 @@ from __future__ import annotations
 import argparse
 import copy
 import json
+import os
 import socket
 import struct
 import sys
@@ -646,7 +647,13 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--token")
     ap.add_argument("--golden", help="serve a golden fixture instead of a generated cluster")
+    ap.add_argument("--cpu", type=int, help="run on this CPU only (bench.py: the server beside the checking process)")
     args = ap.parse_args(argv)
+    if args.cpu is not None:
+        try:
+            os.sched_setaffinity(0, {args.cpu})  # before any thread: the request threads inherit it
+        except (OSError, AttributeError):
+            pass
     nodes = fixtures.golden(args.golden) if args.golden else build_nodes(
         args.nodes, args.kind, args.not_ready, args.with_health, args.gpus_per_node, args.annotation_encoding)
     srv = MockApiServer(nodes, args.host, args.port, MockConfig(token=args.token))

@@ -59,6 +59,19 @@ def test_bench_single_process_contract():
         assert 0 < r["checker_ms"] < bd["step"] and r["transport_ms"] > 0
         assert r["checker_ms"] == bd["checker"] and r["transport_ms"] == bd["transport"]
     assert d["checker_ms"] == head["checker_ms"] and "different machine" in d["baseline_basis"]
+    # the checking thread and the mock apiservers on one L3 domain, or the reason they are not
+    pin = d["pinning"]
+    assert ("skipped" in pin) or (pin["server_cpu"] not in pin["client_cpus"] and pin["client_cpus"])
+
+
+def test_cpu_pair_and_cpu_lists():
+    import bench
+    assert bench._cpu_list("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11} and bench._cpu_list("5") == {5}
+    pair = bench.cpu_pair()
+    if pair is not None:  # this machine's topology: all CPUs allowed, the server apart from the client's
+        allowed = os.sched_getaffinity(0)
+        assert pair["server_cpu"] in allowed and set(pair["client_cpus"]) <= allowed
+        assert pair["server_cpu"] not in pair["client_cpus"] and pair["l3_cpus"] >= 2
 
 
 def test_bench_torchrun_two_ranks_gloo():
