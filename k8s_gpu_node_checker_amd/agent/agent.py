@@ -495,6 +495,7 @@ class Agent:
         # again in this process, so what the abandoned test left queued and allocated is left once, not once per
         # --diag-interval; its failed result stays in the report until the agent is restarted
         self.fabric_abandoned: Optional[str] = None
+        self.fabric_skipped: Optional[str] = None  # why the last node-level child left no result (killed from outside)
         self._bdf: Dict[int, str] = {}  # HIP ordinal -> PCI address (amd-smi and HIP enumerate independently)
         self.last: Optional[Dict[str, Any]] = None
         self.last_probe_done: Optional[float] = None  # monotonic time of the last completed probe (/healthz)
@@ -680,6 +681,12 @@ class Agent:
                 self.diag_procs[d] = r.box["meta"]
             if not r.is_alive():
                 del self._diag_threads[d]
+                if r.box.get("external_kill"):
+                    # SIGKILLed from outside the agent (the pod's memory limit?): not this GPU's finding -- its last
+                    # results stand, the report says why there is no new one, and the next cycle diagnoses it again
+                    self._diag_skipped[d] = r.box["external_kill"][:200]
+                    self._diag_at[d] = float("-inf")
+                    continue
                 wrong = misdirected(self._bdf.get(d, ""), r.box.get("meta"))
                 if r.job.killed:
                     finished[d] = {"watchdog": {
@@ -769,8 +776,14 @@ class Agent:
             self._fabric_at = r.started
             if "meta" in r.box:
                 self.diag_procs["fabric"] = r.box["meta"]
-            if not r.is_alive():
+            if not r.is_alive() and r.box.get("external_kill"):
+                # as for a GPU's child: not the fabric's finding; the last result stands, retried next cycle
                 self._fabric_thread = None
+                self._fabric_at = float("-inf")
+                self.fabric_skipped = r.box["external_kill"][:200]
+            elif not r.is_alive():
+                self._fabric_thread = None
+                self.fabric_skipped = None
                 if r.job.killed:
                     self._fabric = {"watchdog": {
                         "pass": False, "detail": f"node-level xGMI/RCCL tests did not finish within "
@@ -904,6 +917,8 @@ class Agent:
                 rep["fabric"] = self._fabric
             if self.diag_findings:
                 rep["diag_node"] = {"findings": self.diag_findings}
+        if self.fabric_skipped:  # the node-level child was killed from outside the agent: no new result, and why
+            rep["fabric_skipped"] = self.fabric_skipped
         if self.pod_resources_state is not None:
             rep["pod_resources"] = self.pod_resources_state
         verdict = self.evaluate(rep)

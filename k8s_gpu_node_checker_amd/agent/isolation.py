@@ -170,7 +170,8 @@ class Job:
     """One diagnostic run -- a device's suite, the fabric suite or the enumeration -- on a child process or a thread.
 
     ``box["res"]`` holds the result once it is in (``died`` supplies one for a child that ended without sending),
-    ``box["meta"]`` the child's pid / peak RSS / wall time; ``done`` (shared by a cycle's jobs) is set when it ends.
+    ``box["meta"]`` the child's pid / peak RSS / wall time, ``box["external_kill"]`` the reason when a SIGKILL the
+    agent did not send ended the child; ``done`` (shared by a cycle's jobs) is set when it ends.
     """
 
     def __init__(self, proc: Any = None, thread: Optional[threading.Thread] = None,
@@ -248,6 +249,7 @@ class Workers:
             return Job(box=box)
         child.close()  # the child's end lives in the child only: its exit closes the pipe (EOF)
         self.started.append({"pid": proc.pid, "what": what})
+        holder: List[Job] = []
 
         def read() -> None:
             try:
@@ -258,11 +260,17 @@ class Workers:
                 parent.close()
                 proc.join()
                 if "res" not in box:
-                    box["res"] = died(f"diagnostic process {proc.pid} ended before reporting "
-                                      f"({describe_exit(proc.exitcode)})")
+                    why = f"diagnostic process {proc.pid} ended before reporting ({describe_exit(proc.exitcode)})"
+                    if proc.exitcode == -signal.SIGKILL and not (holder and holder[0].killed):
+                        # not the agent's watchdog: the kernel's OOM killer at the pod's memory limit, or an operator
+                        # -- not the GPU's finding (box["external_kill"]: the caller skips the result)
+                        why += "; not killed by the agent: the pod's memory limit (OOM)?"
+                        box["external_kill"] = why
+                    box["res"] = died(why)
                 done.set()
         reader = threading.Thread(target=read, name=f"{what}-reader", daemon=True)
         job = Job(proc=proc, reader=reader, box=box)
+        holder.append(job)
         reader.start()
         return job
 

@@ -252,3 +252,54 @@ def test_a_child_whose_suite_times_no_dma_copy_starts_hip_without_sdma(monkeypat
         env = job.box["res"]["env"]
         assert env["sdma"] == want and env["visible"] == "0", (level, env)
     assert os.environ.get("HSA_ENABLE_SDMA") is None  # the agent's own environment is untouched
+
+
+def _sigkill_self():
+    """Child setup: the child is SIGKILLed from outside the agent (as the kernel's OOM killer would) before reporting."""
+    import signal
+    os.kill(os.getpid(), signal.SIGKILL)
+
+
+def test_a_child_killed_from_outside_the_agent_says_so():
+    """A SIGKILL the agent did not send (the pod's memory limit) is told apart from the watchdog's."""
+    import threading
+    w = isolation.Workers("process", setup=(__name__, "_sigkill_self", {}), method="fork")
+    done = threading.Event()
+    job = w.device(1, 0, {}, done)
+    assert done.wait(30)
+    detail = job.box["res"]["run"]["detail"]
+    assert "signal SIGKILL" in detail and "not killed by the agent" in detail and "memory limit" in detail
+    assert not job.killed
+
+
+def test_an_oom_killed_child_is_not_the_gpus_failure(node, monkeypatch):
+    """A device child the pod's memory limit kills (a SIGKILL the agent did not send) leaves that GPU's last result
+    standing, says why in ``diag_skipped``, and the GPU is diagnosed again next cycle; the same for the node-level
+    child, in ``fabric_skipped``."""
+    node(2)
+    ag = agent(2, level=2)
+    rep = ag.probe_once()
+    assert rep["state"] == H.HEALTHY and all(g["diag"]["gemm"]["pass"] for g in rep["gpus"]) and rep["fabric"]
+    first = {g["index"]: g["diag_proc"]["pid"] for g in rep["gpus"]}
+    real_spawn = ag.workers._spawn
+
+    def oom(victims):
+        def spawn(what, target, args, done, died):
+            if what in victims:
+                args = ((__name__, "_sigkill_self", {}),) + tuple(args[1:])
+            return real_spawn(what, target, args, done, died)
+        monkeypatch.setattr(ag.workers, "_spawn", spawn)
+    oom({"diag-gpu1"})
+    rep = ag.probe_once()
+    g0, g1 = rep["gpus"]
+    assert rep["state"] == H.HEALTHY, rep.get("reasons")  # not the GPU's finding
+    assert g0["diag_proc"]["pid"] != first[0] and g0["diag"]["gemm"]["pass"]
+    assert "not killed by the agent" in g1["diag_skipped"] and g1["diag"]["gemm"]["pass"]  # last result stands
+    assert ag._diag_at[1] == float("-inf")  # due again next cycle
+    oom({"diag-fabric"})  # every GPU fine this time, so the node-level child runs -- and is killed
+    rep = ag.probe_once()
+    assert rep["state"] == H.HEALTHY and "diag_skipped" not in rep["gpus"][1]
+    assert "not killed by the agent" in rep["fabric_skipped"] and rep["fabric"]  # the last fabric result stands
+    monkeypatch.setattr(ag.workers, "_spawn", real_spawn)
+    rep = ag.probe_once()
+    assert "fabric_skipped" not in rep and rep["fabric"] and rep["state"] == H.HEALTHY
