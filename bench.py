@@ -97,8 +97,12 @@ def cpu_pair() -> "dict | None":
             with open(sysfs.format(client, "topology/thread_siblings_list")) as f:
                 siblings = _cpu_list(f.read())
             server = next((x for x in usable if x not in siblings), usable[1])
-            # the checker's own threads (the paged LIST's prefetch, the Slack sender) get the rest of the domain
-            return {"client_cpus": sorted(set(usable) - {server}), "server_cpu": server, "l3_cpus": len(group)}
+            with open(sysfs.format(server, "topology/thread_siblings_list")) as f:
+                core = _cpu_list(f.read()) | {server}
+            # the checker's own threads (the paged LIST's prefetch, the Slack sender) get the rest of the domain, off
+            # the server's physical core where that leaves any
+            client_cpus = sorted(set(usable) - core) or sorted(set(usable) - {server})
+            return {"client_cpus": client_cpus, "server_cpu": server, "l3_cpus": len(group)}
     except (OSError, ValueError):
         return None
     return None
