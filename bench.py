@@ -36,6 +36,9 @@ row -- the headline's own is one -- has ms per check, nodes/s, the survey proxy'
 (scan + client + health + render + other), apart from ``transport_ms`` (connect + first byte + body: the socket
 and the mock's time).
 
+Placement (``cpu_pair``; ``--no-pin``): the mock apiservers run on one CPU and rank 0's checking thread on the
+other CPUs of that CPU's L3 domain, for the timed steps and the curve; the line's ``pinning`` says which.
+
 Prints ONE JSON line (rank 0): value = nodes/s over the whole job (headline node count = GPUs).
 """
 
