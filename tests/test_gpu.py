@@ -798,6 +798,10 @@ def test_agent_process_isolation_keeps_hip_out_of_the_agent(repo):
     assert procs[0]["pid"] != procs[1]["pid"] and d["pid"] not in (procs[0]["pid"], procs[1]["pid"])
     assert procs[0]["peak_rss_mib"] > d["rss_mib"]  # the HIP work's memory was the child's, not the agent's
     assert d["rss_mib"] < 100, d["rss_mib"]
+    # a level-1 child starts HIP without the SDMA engines (no level-1 test times a DMA copy): ~445 MiB, against
+    # ~630 with them -- the DaemonSet's limit is sized on it (agent.MEM_CHILD_PEAK_MIB)
+    from k8s_gpu_node_checker_amd.agent import agent as A
+    assert all(p["peak_rss_mib"] <= A.MEM_CHILD_PEAK_MIB[1] * 1.1 for p in procs), procs
 
 
 def test_agent_diagnostics_threads_per_device(dev):
