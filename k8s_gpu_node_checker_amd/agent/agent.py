@@ -146,10 +146,12 @@ from ..ops.diag import P2P_SHARE  # noqa: E402  (share of --diag-timeout the xGM
 # profiles/agent_soak_isolated_l{1,2}_r06_mi355x.json, flat over 48 / 36 cycles.  This is the pod's request.
 MEM_RESIDENT_MIB = 65
 # one diagnostic child's peak, its own getrusage (HIP runtime, comgr's code objects, the level's buffers; the child
-# sees one GPU, isolation.narrow_to, so it is the same process on a one-GPU box and on an 8-GPU node): level 1
-# 443 MiB (its runtime starts without the SDMA engines, ops/diag.DMA_TESTS), level 2 1,082 MiB (the host link's
-# pinned buffer and the 8192^3 GEMMs included) -- profiles/agent_soak_isolated_l{1,2}_r06b_mi355x.json
-MEM_CHILD_PEAK_MIB = {1: 443, 2: 1082}
+# sees one GPU, isolation.narrow_to, so it is the same process on a one-GPU box and on an 8-GPU node), the first one
+# on a fresh box, which is the largest: level 1 493 MiB (its runtime starts without the SDMA engines,
+# ops/diag.DMA_TESTS; later children 437-445), level 2 1,128 MiB (the host link's pinned buffer and the 8192^3 GEMMs
+# included; later children 1,074-1,082) -- profiles/first_child_rss_r06_mi355x.jsonl,
+# profiles/agent_soak_isolated_l{1,2}_r06b_mi355x.json
+MEM_CHILD_PEAK_MIB = {1: 493, 2: 1128}
 # a one-GPU HIP process with its SDMA queues (the fabric child copies between GPUs over them): a level-1 suite with
 # the engines on peaks at 628-682 MiB (profiles/child_peak_rss_sdma_r06_mi355x.jsonl)
 MEM_GPU_WITH_SDMA_MIB = 682

@@ -701,8 +701,8 @@ def test_daemonset_memory_limit_covers_the_budget_of_an_eight_gpu_node():
     req = _mib(c["resources"]["requests"]["memory"])
     assert agent.MEM_RESIDENT_MIB <= req <= 2 * agent.MEM_RESIDENT_MIB
     # the measured one-GPU figures (profiles/agent_soak_isolated_l{1,2}_r06_mi355x.json)
-    assert agent.memory_budget_mib(1, 1) == 65 + 443 and agent.memory_budget_mib(1, 2) == 65 + 1082
-    assert agent.memory_budget_mib(8, 1, parallel=2) == 65 + 2 * 443  # children at once, not devices, count
+    assert agent.memory_budget_mib(1, 1) == 65 + 493 and agent.memory_budget_mib(1, 2) == 65 + 1128
+    assert agent.memory_budget_mib(8, 1, parallel=2) == 65 + 2 * 493  # children at once, not devices, count
     assert agent.memory_budget_mib(8, 2, rccl=True, parallel=4) == 65 + 2712 + 7 * 682  # the fabric child bounds it
     assert agent.memory_budget_mib(1, 2, rccl=True) >= agent.memory_budget_mib(1, 2)
 
