@@ -1,3 +1,5 @@
+"""fp8 (E4M3) GEMM numerics on the v3 kernel: three shapes against an fp64 reference of the same operands (error over
+the |A||B| magnitude, exact fraction), beside torch's fp32 matmul and _scaled_mm (profiles/fp8_numerics_mi355x.jsonl)."""
 import json, sys, torch
 sys.path.insert(0, ".")
 from k8s_gpu_node_checker_amd.ops import diag

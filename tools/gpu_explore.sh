@@ -1,4 +1,5 @@
 #!/bin/bash
+# GEMM / HBM exploration on one box: the GEMM tests, tools/gemm_explore.py, the HBM lab binary and a rocprofv3 pass.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out

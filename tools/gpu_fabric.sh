@@ -1,3 +1,4 @@
+# RCCL / fabric GPU tests, then the mi355x-fabric CLI over 1M-1G messages.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out

@@ -1,4 +1,5 @@
 #!/bin/bash
+# PMC passes over the 8192^3 GEMM (wave / wait, MFMA busy, LDS counters), one rocprofv3 run per counter set.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out

@@ -1,3 +1,5 @@
+"""Dump what the amd-smi Python binding reports about xGMI links, RAS and ECC on GPU 0 (exploration behind the native
+probe's link fields, profiles/amdsmi_xgmi_link_metrics_mi355x.json)."""
 import json, amdsmi as A
 A.amdsmi_init()
 h = A.amdsmi_get_processor_handles()[0]
