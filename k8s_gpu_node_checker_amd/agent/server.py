@@ -13,6 +13,7 @@ import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import TYPE_CHECKING, Any, Dict, List, Optional
 
+from ..utils.http import nodelay
 from ..models.health import DEGRADED, HEALTHY, UNHEALTHY, UNKNOWN, driver_release, fw_version_str
 
 if TYPE_CHECKING:
@@ -164,6 +165,10 @@ def serve(agent: Agent, host: str, port: int, stale_after: Optional[float] = Non
 
         def log_message(self, *a: Any) -> None:
             pass
+
+        def setup(self) -> None:
+            super().setup()
+            nodelay(self.connection)
 
         def do_GET(self) -> None:  # noqa: N802
             if require_client_cert and not self.path.startswith("/healthz"):

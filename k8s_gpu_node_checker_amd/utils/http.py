@@ -24,7 +24,7 @@ import errno
 import os
 TYPE_CHECKING = False
 if TYPE_CHECKING:  # annotations only (PEP 563): importing typing is ~10 ms of a cold start
-    from typing import Dict, List, Optional, Tuple
+    from typing import Any, Dict, List, Optional, Tuple
 
 from .urls import split as urlsplit
 
@@ -76,6 +76,17 @@ class _Shown:
 
     def __repr__(self) -> str:
         return self.text
+
+
+def nodelay(sock: Any) -> None:
+    """``TCP_NODELAY`` on a connection one of our HTTP servers accepted (``setup()`` of the agent's and the watcher's
+    handlers).  ``BaseHTTPRequestHandler`` writes a response's head and body separately; with Nagle on, the body
+    waits for the client's ACK of the head, and a keep-alive client past its first exchanges (a Prometheus scraper)
+    delays that ACK by up to 40 ms."""
+    try:
+        sock.setsockopt(_socket.IPPROTO_TCP, _socket.TCP_NODELAY, 1)
+    except (OSError, AttributeError):  # not a TCP socket (a test's socketpair)
+        pass
 
 
 def _broken(inner: str) -> str:

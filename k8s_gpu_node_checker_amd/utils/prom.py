@@ -19,6 +19,8 @@ import tempfile
 import time
 from typing import Any, List
 
+from .http import nodelay
+
 
 def _esc(v: Any) -> str:
     return str(v).replace("\\", "\\\\").replace("\n", "\\n").replace('"', '\\"')
@@ -128,6 +130,10 @@ class MetricsServer:
 
             def log_message(self, *a: Any) -> None:
                 pass
+
+            def setup(self) -> None:
+                super().setup()
+                nodelay(self.connection)
 
             def do_GET(self) -> None:  # noqa: N802
                 if self.path.split("?")[0] == "/metrics":

@@ -827,3 +827,39 @@ def test_probe_tls_server_name_verifies_agents_reached_by_pod_ip(tmp_path, fixtu
         srv.server_close()
     from k8s_gpu_node_checker_amd import cli
     assert cli.parse_args(["--probe-tls-server-name", name]).probe_tls_server_name == name
+
+
+def _keepalive_gets_ms(port, path, n=6):
+    """Median ms of ``n`` GETs on one keep-alive connection (a Prometheus scraper's pattern), after the first."""
+    import http.client
+    import statistics
+    import time
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+    ts = []
+    try:
+        for _ in range(n + 1):
+            t = time.perf_counter()
+            c.request("GET", path)
+            r = c.getresponse()
+            assert r.status == 200 and r.read()
+            ts.append((time.perf_counter() - t) * 1e3)
+    finally:
+        c.close()
+    return statistics.median(ts[1:])
+
+
+def test_keepalive_scrapes_are_not_held_by_a_delayed_ack(fixture_report):
+    """The agent's and the watcher's HTTP servers answer a keep-alive client (Prometheus) at once: with Nagle on, a
+    response's body waited for the ACK of its head, which such a client delays by up to 40 ms."""
+    from k8s_gpu_node_checker_amd.utils.prom import MetricsServer
+    ag = A.Agent("n", source="fixture", fixture=fixture_report)
+    ag.probe_once()
+    srv = A.serve(ag, "127.0.0.1", 0)
+    ms = MetricsServer("127.0.0.1", 0).start()
+    try:
+        assert _keepalive_gets_ms(srv.server_address[1], "/metrics") < 20.0
+        assert _keepalive_gets_ms(ms.port, "/metrics") < 20.0
+    finally:
+        srv.shutdown()
+        srv.server_close()
+        ms.stop()
