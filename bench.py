@@ -37,7 +37,8 @@ row -- the headline's own is one -- has ms per check, nodes/s, the survey proxy'
 and the mock's time).
 
 Placement (``cpu_pair``; ``--no-pin``): the mock apiservers run on one CPU and rank 0's checking thread on the
-other CPUs of that CPU's L3 domain, for the timed steps and the curve; the line's ``pinning`` says which.
+other CPUs of that CPU's L3 domain, for the timed steps and the curve; the line's ``pinning`` says which, and
+``unpinned`` is the headline's check timed once more at the end with neither side pinned.
 
 Prints ONE JSON line (rank 0): value = nodes/s over the whole job (headline node count = GPUs).
 """
@@ -400,6 +401,7 @@ def main() -> int:
                          *(["--with-health"] if n_nodes > n_gpus else []), *pin)
         procs.append(p)
         ctrl["api"] = info["url"]
+        ctrl["api_pid"] = p.pid
         if args.slack:
             p, sinfo = _spawn("k8s_gpu_node_checker_amd.testing.webhook_sink")
             procs.append(p)
@@ -605,8 +607,18 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
             if ctrl.get("curve_error"):
                 curve.append({"nodes": None, "check_ok": False, "error": ctrl["curve_error"]})
         curve.sort(key=lambda r: (r["nodes"] is None, r["nodes"] or 0))
+    unpinned = None
     if mask is not None:
         os.sched_setaffinity(0, mask)
+        # the headline once more with neither side pinned (the server's new request threads inherit its main
+        # thread's mask): how much of the number is placement, measured in every run rather than asserted
+        try:
+            os.sched_setaffinity(ctrl["api_pid"], mask)
+            el, lt, _, _ = _timed_checks(ClusterConnection(ctrl["api"]), opts, args.steps, args.warmup)
+            unpinned = {"ms_per_step": round(el / max(args.steps, 1) * 1e3, 4),
+                        "p50_ms": round(_pctl(lt, 0.5) * 1e3, 4), "steps": args.steps}
+        except Exception as e:  # an extra: never costs the line
+            unpinned = {"error": f"{type(e).__name__}: {e}"[:200]}
 
     if rank == 0:
         ok = last is not None and last.exit_code == 0 and len(last.ready_gpu_nodes) == n_nodes
@@ -645,8 +657,10 @@ def _run(args, world, rank, local_rank, n_gpus, n_nodes, ctrl, budget) -> int:
             # socket and the mock apiserver's time: what says something about the code across boxes and rounds
             "checker_ms": (_step_breakdown(spans, lat) or {}).get("checker"),
             "baseline_basis": BASELINE_BASIS,
-            # where the checking thread and the mock apiservers ran (cpu_pair), or why they were not pinned
+            # where the checking thread and the mock apiservers ran (cpu_pair), or why they were not pinned, and the
+            # headline's check timed again afterwards with neither side pinned
             "pinning": ctrl.get("pinning"),
+            "unpinned": unpinned,
             # ms per check, nodes/s, checker_ms and vs_baseline at every node count (headline row included)
             "curve": curve,
             "coldstart_ms": (ctrl.get("coldstart") or {}).get("ms"),

@@ -62,6 +62,8 @@ def test_bench_single_process_contract():
     # the checking thread and the mock apiservers on one L3 domain, or the reason they are not
     pin = d["pinning"]
     assert ("skipped" in pin) or (pin["server_cpu"] not in pin["client_cpus"] and pin["client_cpus"])
+    # pinned runs also time the headline's check with neither side pinned
+    assert d["unpinned"] is None if "skipped" in pin else d["unpinned"]["ms_per_step"] > 0
 
 
 def test_cpu_pair_and_cpu_lists():
