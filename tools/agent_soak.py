@@ -203,6 +203,13 @@ def main() -> int:
                      "diag_child_pid": (g.get("diag_proc") or {}).get("pid"),
                      "vram_used_mb": g.get("vram_used_mb"), "diag_pass": {k: v.get("pass") for k, v in diag.items()
                                                                           if isinstance(v, dict)},
+                     # what a not-healthy sample was about: each failed or degraded test's fraction, rates, detail
+                     "diag_notes": {k: {"pass": v.get("pass"), "degraded": v.get("degraded"),
+                                        "fraction": v.get("fraction"), "rates": v.get("rates"),
+                                        "detail": (v.get("detail") or "")[:160]}
+                                    for k, v in diag.items() if isinstance(v, dict)
+                                    and (v.get("pass") is False or v.get("degraded"))},
+                     "reasons": (rep.get("reasons") or [])[:4], "warnings": (rep.get("warnings") or [])[:4],
                      "labels": {k: v for k, v in (node["metadata"].get("labels") or {}).items()
                                 if k.startswith("amd.com/")}}
                 samples.append(s)
