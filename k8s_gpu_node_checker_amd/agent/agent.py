@@ -203,6 +203,24 @@ def not_clean(res: Dict[str, Any]) -> bool:
     return any(isinstance(r, dict) and (r.get("pass") is False or r.get("degraded")) for r in res.values())
 
 
+HELD_NOTE = "below its failure line once on a shared PCIe path: measured again before it fails the GPU"
+
+
+def _rate_only_failure(r: Dict[str, Any]) -> bool:
+    """A rate test that failed on its rates alone: correct data, measured (not skipped)."""
+    return r.get("pass") is False and not r.get("numerics") and "skipped" not in r and bool(r.get("rates"))
+
+
+def apply_holds(res: Dict[str, Any]) -> None:
+    """Publish a ``held`` test (``Agent._hold_unconfirmed``) that failed on rate alone as degraded, in place; run
+    after every judgement of the result, which re-derives ``pass`` from the raw rates."""
+    for r in res.values():
+        if isinstance(r, dict) and r.get("held") and _rate_only_failure(r):
+            r["pass"], r["degraded"] = True, True
+            if HELD_NOTE not in (r.get("detail") or ""):
+                r["detail"] = f"{r.get('detail') or ''}; {HELD_NOTE}".lstrip("; ")
+
+
 def runtime_lost(res: Dict[str, Any]) -> Optional[str]:
     """The first detail when every test of one GPU's diagnostic result failed because the HIP runtime lost
     its devices, else None."""
@@ -478,6 +496,9 @@ class Agent:
         self._diag_threads: Dict[int, _DiagRun] = {}  # device -> its diagnostic thread until it returns
         self._diag_done = threading.Event()  # set by every diagnostic thread as it returns
         self._rechecked: Dict[int, str] = {}  # device -> result_signature of the not-clean result rechecked
+        # device -> {shared-resource test: "held" (its last run failed on rate alone, published degraded) or
+        # "confirmed" (failed again: failures stand until it passes)}
+        self._held: Dict[int, Dict[str, str]] = {}
         self._hip_count0: Optional[int] = None  # HIP device count the process saw first (runtime_lost)
         self._hip_ok: set = set()  # devices whose diagnostics ran without a runtime error in this process
         self._driver_version: Any = None  # amdgpu driver of the latest probe (the baselines' epoch)
@@ -731,6 +752,7 @@ class Agent:
         for d, res in finished.items():
             if self.hip_lost is not None and d in lost_devs:
                 continue
+            self._hold_unconfirmed(d, res)
             self._diag_cache[d] = res
             self._diag_ran[d] = self._diag_at[d]
             fresh.append(d)
@@ -811,6 +833,27 @@ class Agent:
                               f"hang?){stuck}"}}
         return {d: self._diag_cache[d] for d in devices if d in self._diag_cache}
 
+    def _hold_unconfirmed(self, d: int, res: Dict[str, Any]) -> None:
+        """A test of a resource the GPU shares with the host's other GPUs and processes (``ops/diag.SHARED_TESTS``:
+        the PCIe host link, through the CPU's root complex) that fails on its rate alone is contention as often as a
+        fault.  Its first such failure is marked ``held`` -- published as *degraded* (:func:`apply_holds`, after
+        every judgement) and measured again after ``DIAG_RECHECK_S`` (the not-clean recheck); a second one in a row
+        fails the GPU, and so does every one after it until the test passes.  A link that trained down is the probe's
+        finding at once (amd-smi's PCIe width and speed)."""
+        from ..ops import diag
+        state = self._held.setdefault(d, {})
+        for t in diag.SHARED_TESTS:
+            r = res.get(t)
+            if not isinstance(r, dict):
+                continue
+            if not _rate_only_failure(r):
+                state.pop(t, None)  # passed (or failed on its data): the next rate-only failure is held again
+            elif t not in state:
+                state[t] = "held"
+                r["held"] = HELD_NOTE
+            else:
+                state[t] = "confirmed"  # the second in a row and every one after it until a pass: failures
+
     def _judge_diagnostics(self, devices: List[int], entries: Dict[int, Dict[str, Any]], fresh: List[int]) -> None:
         """Judge the GPUs' latest diagnostic results together (``models/peers.judge_node``): each rate against the
         node's other GPUs measured within ``PEER_MAX_AGE_S`` (a lone GPU against the references), a shortfall
@@ -828,6 +871,8 @@ class Agent:
                 # the software the rates were measured under: a driver or firmware change re-forms the baseline
                 self.baselines.observe(key, self._diag_cache[d], now, epoch_of(entries.get(d), self._driver_version))
             self.diag_findings = peers.judge_node(pool, label)
+        for res in pool.values():  # after the last judgement, which re-derives pass from the rates
+            apply_holds(res)
 
     def _start_diag(self, d: int, memory_partition: Any, power: Optional[float], host: tuple = (None, None)) -> None:
         """Start device ``d``'s diagnostics as its own job (the partition's memory share comes from amd-smi's NPS

@@ -651,3 +651,4 @@ def test_one_busy_one_failing_gpu_is_not_a_lost_runtime(monkeypatch):
     ag = A.Agent("n", source="fake", diag_level=1)
     rep = ag.probe_once()
     assert w.runs == [0] and ag.hip_lost is None and rep["state"] == "unhealthy"
+

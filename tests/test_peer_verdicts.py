@@ -571,3 +571,29 @@ def test_baseline_reset_is_refused_from_off_the_pod(node):
     finally:
         srv.shutdown()
         srv.server_close()
+
+
+def test_a_shared_host_link_failure_is_held_once_before_it_fails_the_gpu(node):
+    """The host-link test shares the PCIe path with the host's other GPUs and processes: its first rate-only
+    failure is published degraded (and re-measured), the second in a row fails the GPU, failures stand until the
+    test passes again, and a pass resets it.  Re-judging a cached result (every cycle) keeps the hold."""
+    lib = node(1, link=(20.0, 20.0))  # a third of the Gen5 x16 reference both ways
+    ag = _agent(1, level=2, diag_interval=0.0, diag_when="always")
+    states = []
+    for _ in range(3):
+        rep = ag.probe_once()
+        hl = rep["gpus"][0]["diag"]["host_link"]
+        states.append((rep["state"], hl["pass"], bool(hl.get("degraded"))))
+        if len(states) == 1:
+            assert A.HELD_NOTE in hl["detail"] and "h2d_gbps" in hl["detail"], hl["detail"]
+    assert states == [(H.DEGRADED, True, True), (H.UNHEALTHY, False, False), (H.UNHEALTHY, False, False)], states
+    lib.link = None  # back at its reference
+    rep = ag.probe_once()
+    assert rep["state"] == H.HEALTHY and rep["gpus"][0]["diag"]["host_link"]["pass"]
+    lib.link = (20.0, 20.0)  # a new dip: held again first
+    rep = ag.probe_once()
+    assert rep["state"] == H.DEGRADED and A.HELD_NOTE in rep["gpus"][0]["diag"]["host_link"]["detail"]
+    # a held result re-judged later (diagnostics not due) is still published degraded
+    ag.diag_interval = 3600.0
+    rep = ag.probe_once()
+    assert rep["state"] == H.DEGRADED and rep["gpus"][0]["diag"]["host_link"]["pass"]
