@@ -41,17 +41,32 @@ from .errors import ApiException
 
 
 class NodeView:
-    """GPU-node projection of the cluster keyed by node name (API order = name order)."""
+    """GPU-node projection of the cluster keyed by node name (API order = name order).
+
+    A LIST is scanned natively (``ops/fastpath``, as the one-shot check scans it): that yields the GPU nodes and
+    the number of items, not the other nodes' names -- ``unnamed`` counts those, and a watch event about a node
+    the view has no name for is one of them (MODIFIED, DELETED) or a new node (ADDED)."""
 
     def __init__(self, gpu_source: str = "capacity", annotation_mode: int = 1):
         self.gpu_source = gpu_source
         self.annotation_mode = annotation_mode
         self.gpu: Dict[str, Tuple[Dict[str, Any], NodeExtras]] = {}
         self.all_names: set = set()
+        self.unnamed = 0  # non-GPU nodes of the last LIST that no event has named yet
 
-    def upsert(self, node: Dict[str, Any]) -> None:
+    def load(self, scan: ScanResult, items: int) -> None:
+        """The view of one (natively scanned) LIST: its GPU nodes, and ``items`` nodes in all."""
+        self.reset()
+        for info, ex in zip(scan.gpu_nodes, scan.extras):
+            self.gpu[info["name"]] = (info, ex)
+        self.all_names.update(self.gpu)
+        self.unnamed = max(0, items - len(self.gpu))
+
+    def upsert(self, node: Dict[str, Any], kind: str = "MODIFIED") -> None:
         info = classify_node(node, GPU_RESOURCE_KEYS, self.gpu_source)
         name = info["name"] if info is not None else project_node(node, GPU_RESOURCE_KEYS, self.gpu_source)["name"]
+        if name not in self.all_names and kind != "ADDED" and self.unnamed > 0:
+            self.unnamed -= 1  # a node of the LIST we only counted, named now
         self.all_names.add(name)
         if info is not None:
             self.gpu[name] = (info, node_extras(node, GPU_RESOURCE_KEYS, self.annotation_mode))
@@ -60,12 +75,16 @@ class NodeView:
 
     def delete(self, node: Dict[str, Any]) -> None:
         name = project_node(node, GPU_RESOURCE_KEYS, self.gpu_source)["name"]
-        self.all_names.discard(name)
+        if name in self.all_names:
+            self.all_names.discard(name)
+        elif self.unnamed > 0:
+            self.unnamed -= 1  # a counted, unnamed node of the LIST
         self.gpu.pop(name, None)
 
     def reset(self) -> None:
         self.gpu.clear()
         self.all_names.clear()
+        self.unnamed = 0
 
     def scan_result(self) -> ScanResult:
         """A fresh :class:`ScanResult` (copies: the health gate rewrites ``ready`` in place)."""
@@ -75,8 +94,28 @@ class NodeView:
             res.gpu_nodes.append(dict(info))
             res.extras.append(ex)
         res.recompute_ready()
-        res.items_seen = len(self.all_names)
+        res.items_seen = len(self.all_names) + self.unnamed
         return res
+
+
+def list_resource_version(body: bytes) -> Optional[str]:
+    """``metadata.resourceVersion`` of a NodeList: from the ``metadata`` object apiservers put before ``items``
+    (decoded alone), else from the whole body."""
+    head = body[:4096]
+    i = head.find(b'"metadata"')
+    items = head.find(b'"items"')
+    if i >= 0 and (items < 0 or i < items):
+        j = head.find(b"{", i)
+        k = head.find(b"}", j)
+        if 0 <= j < k:
+            try:
+                meta = json.loads(head[j:k + 1])
+                return str(meta.get("resourceVersion") or "") or None
+            except ValueError:
+                pass
+    doc = json.loads(body)
+    meta = (doc.get("metadata") if isinstance(doc, dict) else None) or {}
+    return str(meta.get("resourceVersion") or "") or None
 
 
 def outcome_signature(result: Any) -> Tuple[Any, ...]:
@@ -111,9 +150,13 @@ class NodeWatcher:
 
     # -- state ------------------------------------------------------------------
     def relist(self, client: KubeClient) -> None:
-        """Paginated LIST into a fresh view; remembers the list's resourceVersion."""
+        """Paginated LIST into a fresh view, each page scanned natively (the one-shot check's scanner: 5,000 nodes
+        in milliseconds, not the ~1.5 s of decoding and classifying every object in Python); remembers the list's
+        resourceVersion, read off each page's leading ``metadata``."""
         from urllib.parse import quote
-        self.view.reset()
+        from ..ops import fastpath
+        scan = ScanResult()
+        items = 0
         cont: Optional[str] = None
         while True:
             path = "/api/v1/nodes"
@@ -124,15 +167,14 @@ class NodeWatcher:
                 q.append("continue=" + quote(cont, safe=""))
             if self.opts.label_selector:
                 q.append("labelSelector=" + quote(self.opts.label_selector, safe=""))
-            doc = json.loads(client.request("GET", path + ("?" + "&".join(q) if q else "")).body)
-            for item in doc.get("items") or []:
-                if isinstance(item, dict):
-                    self.view.upsert(item)
-            meta = doc.get("metadata") or {}
-            cont = meta.get("continue") or None
+            body = client.request("GET", path + ("?" + "&".join(q) if q else "")).body
+            cont, n = fastpath.scan_page(body, scan, GPU_RESOURCE_KEYS, self.view.gpu_source, True,
+                                         self.view.annotation_mode)
+            items += n
             if not cont or self.page_size <= 0:
-                self.rv = str(meta.get("resourceVersion") or "") or None
+                self.rv = list_resource_version(body)
                 break
+        self.view.load(scan, items)
         self.relists += 1
 
     def apply(self, ev: Dict[str, Any]) -> bool:
@@ -151,7 +193,7 @@ class NodeWatcher:
             return True
         self.events += 1
         if kind in ("ADDED", "MODIFIED"):
-            self.view.upsert(obj)
+            self.view.upsert(obj, kind)
         elif kind == "DELETED":
             self.view.delete(obj)
         if rv:

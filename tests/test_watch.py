@@ -138,6 +138,38 @@ def test_node_view_and_apply_semantics():
     assert w.view.scan_result().gpu_nodes[0]["ready"] is True
 
 
+def test_native_relist_view_matches_the_event_path_and_counts_unnamed_nodes(mock_cluster):
+    """The relist scans pages natively (the one-shot check's scanner) and so learns the GPU nodes and the item
+    count, not the CPU nodes' names: the view equals the one built node by node through upserts, and the count
+    stays right as unnamed CPU nodes are modified (no double count), deleted, and new ones added."""
+    from k8s_gpu_node_checker_amd.kube.client import KubeClient
+    from k8s_gpu_node_checker_amd.kube.watch import NodeView, list_resource_version
+    nodes = fixtures.cluster(7, "mixed", not_ready=range(2), with_health=True, gpus_per_node=8)
+    nodes += [fixtures.realistic_node(f"cpu-{i}", gpu_key=None, index=100 + i) for i in range(3)]
+    srv = mock_cluster(nodes)
+    opts = CheckOptions(json=True)
+    w = NodeWatcher(ClusterConnection(srv.url), opts, page_size=4)
+    with KubeClient(ClusterConnection(srv.url)) as kc:
+        w.relist(kc)
+    assert w.rv is not None and w.rv == str(srv.state.rv)
+    ref = NodeView(opts.gpu_source, 1)
+    for n in nodes:
+        ref.upsert(n)
+    a, b = w.view.scan_result(), ref.scan_result()
+    assert a.gpu_nodes == b.gpu_nodes and a.ready_gpu_nodes == b.ready_gpu_nodes
+    assert [ex.health_condition for ex in a.extras] == [ex.health_condition for ex in b.extras]
+    assert a.items_seen == b.items_seen == len(nodes) and w.view.unnamed == 3 + (len(nodes) - 3 - len(a.gpu_nodes))
+    w.apply({"type": "MODIFIED", "object": fixtures.realistic_node("cpu-0", gpu_key=None, index=100)})
+    assert w.view.scan_result().items_seen == len(nodes)  # named now, not counted twice
+    w.apply({"type": "DELETED", "object": fixtures.realistic_node("cpu-1", gpu_key=None, index=101)})
+    w.apply({"type": "DELETED", "object": fixtures.realistic_node("cpu-0", gpu_key=None, index=100)})
+    w.apply({"type": "ADDED", "object": fixtures.realistic_node("cpu-9", gpu_key=None, index=109)})
+    assert w.view.scan_result().items_seen == len(nodes) - 1
+    # the list's resourceVersion, with metadata before items or (a proxy's re-encoding) after them
+    assert list_resource_version(b'{"kind":"NodeList","metadata":{"resourceVersion":"42","continue":"x"},"items":[]}') == "42"
+    assert list_resource_version(b'{"items":[{"metadata":{"resourceVersion":"1"}}],"metadata":{"resourceVersion":"43"}}') == "43"
+
+
 def _set_ready(srv, name, ready):
     node = srv.state.find(name)
     conds = [dict(c) for c in node["status"]["conditions"]]
@@ -217,7 +249,8 @@ def test_node_watcher_notices_a_heartbeat_going_stale_without_events(mock_cluste
     from k8s_gpu_node_checker_amd.models import health as H
     rep = fixtures.mi355x_probe_report("n", gpus=8)
     cond = fixtures.health_condition(rep, 8)
-    cond["lastHeartbeatTime"] = H.format_k8s_time(time.time() - 1.0)  # fresh for 1 more second (max age 2 s)
+    # fresh for 1-2 more seconds (max age 2 s; the timestamp has whole seconds), stale within the 6 s run
+    cond["lastHeartbeatTime"] = H.format_k8s_time(time.time())
     srv = mock_cluster([fixtures.realistic_node("n", extra_conditions=[cond])])
     opts = CheckOptions(json=True)
     opts.health_policy, opts.probe_max_age, opts.probe_unknown = "require", 2.0, "deny"
